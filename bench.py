@@ -1,0 +1,261 @@
+"""Benchmark: full Neal-8 Gibbs iterations per second on the MI355X engine.
+
+One step = one pass of the reference loop body code/launcher.cpp:94-132 with neal8=TRUE,
+split_merge=FALSE: N sequential reassignments (sample_allocation) + update_phi +
+compute_loglikelihood, on synthetic data already resident in HBM.  The default workload
+is BASELINE config C5 (N = 1,000,000, D = 128, m_j = 4, K_true = 20, m = 3 latent
+clusters), initialised at the generator's ground truth (L = 0 path, la:32-39).
+
+Multi-GPU: one process per GPU (torch.distributed.run); every rank runs an independent
+chain with its own seed (replicas, "scaling": "weak"); the only collective is the
+barrier/max of the timing.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c5] [--n N]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def prepass_bytes_per_point(d: int, m: int, k: int) -> int:
+    """Algorithmic bytes k_prepass moves per point ('Roofline'): the point's
+    codes (D), m latent gathers of a u8 center row plus one f64 per attribute (9D each,
+    SURVEY.md 8(d)), its L row (8(K+m)), margin (8) and label (4)."""
+    return d * (1 + 9 * m) + 8 * (k + m) + 12
+
+
+def survey_sweep_bytes(n: int, d: int, m: int) -> int:
+    """B_sweep = N (D (2 + 9m) + 8)."""
+    return n * (d * (2 + 9 * m) + 8)
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+class Dist:
+    """Barrier and max-over-ranks for the timing (RCCL when >1 rank, else no-op)."""
+
+    def __init__(self, ws, rank, local, backend=None):
+        self.ws, self.rank, self.local = ws, rank, local
+        self.dist = None
+        if ws > 1:
+            import torch
+            import torch.distributed as dist
+            backend = backend or ("nccl" if torch.cuda.is_available() else "gloo")
+            if backend == "nccl":
+                torch.cuda.set_device(local)
+            dist.init_process_group(backend=backend)
+            self.dist, self.torch, self.backend = dist, torch, backend
+
+    def _dev(self):
+        return f"cuda:{self.local}" if self.backend == "nccl" else "cpu"
+
+    def barrier(self):
+        if self.dist is not None:
+            t = self.torch.zeros(1, device=self._dev())
+            self.dist.all_reduce(t)
+            if self.backend == "nccl":
+                self.torch.cuda.synchronize()
+
+    def max(self, x: float) -> float:
+        if self.dist is None:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self._dev())
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.dist is not None:
+            self.dist.destroy_process_group()
+
+
+def cuda_sync():
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+    except Exception:
+        pass
+
+
+def cpu_baseline(ds, eng, m: int, budget_s: float):
+    """Reference-faithful CPU restatement (oracle/, O(N) bookkeeping per point as in
+    code/neal8.cpp) timed on a bounded sample of consecutive sample_allocation calls
+    from the middle of a sweep on the current chain state, extrapolated to one sweep."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi as O  # cpu_baseline leg only
+    c, cen, sig = eng.get_state()
+    P = 30_000                      # per-point cost is independent of the pool size
+    st = O.seed_state(99)
+    pc, ps, _ = O.pool_generate(ds.attrisize, ds.v, ds.w, P, st)
+    data_cm = O.colmajor(ds.codes)
+    att = np.ascontiguousarray(ds.attrisize, np.int32)
+
+    def run(first, count):
+        ost = O.OracleState(c, cen.shape[0], cen, sig)
+        import ctypes as C
+        K = C.c_int(ost.K)
+        t0 = time.perf_counter()
+        r = O.lib().orc_ffi_neal8_sweep(data_cm, ds.n, ds.d, att, ds.gamma, np.ascontiguousarray(ds.v),
+                                        np.ascontiguousarray(ds.w), ost.c_i, C.byref(K), ost.centers.reshape(-1),
+                                        ost.sigma.reshape(-1), ost.cap, m, pc.reshape(-1), ps.reshape(-1), P, st,
+                                        0, first, count)
+        return time.perf_counter() - t0, r
+
+    mid = ds.n // 2
+    t_probe, _ = run(mid, 4)
+    per = max(t_probe / 4, 1e-7)
+    count = int(min(max(budget_s / per, 8), ds.n - mid))
+    t, r = run(mid, count)
+    per_point = t / count
+    return {
+        "value": 1.0 / (per_point * ds.n),
+        "unit": "sweeps/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": (f"{count} consecutive sample_allocation calls (points {mid}..{mid + count - 1}) of one sweep, "
+                   f"reference-faithful O(N) bookkeeping, {t:.1f} s, extrapolated x{ds.n / count:.0f} to a full "
+                   f"sweep (update_phi excluded); latent pool {P} prior draws"),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c5")
+    ap.add_argument("--n", type=int, default=None)
+    ap.add_argument("--m", type=int, default=3)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-csv", default=None,
+                    help="rocprofv3 --pmc counter CSV (FETCH_SIZE, WRITE_SIZE) for the roofline traffic field")
+    args = ap.parse_args()
+
+    ws, rank, local = dist_env()
+    D = Dist(ws, rank, local)
+    import split_and_merge_gibbs_sampling_amd as hd
+    from split_and_merge_gibbs_sampling_amd.data import CONFIGS, config
+
+    t_setup = time.perf_counter()
+    ds = config(args.config, n=args.n)
+    eng = hd.Engine(local)
+    eng.set_data(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w)
+    eng.set_seed(1 + rank)
+    params = eng.chain_params(m=args.m, iterations=args.steps + args.warmup, L=0, burnin=0, neal8=True,
+                              split_merge=False)
+    eng.init_chain(params, c_i=ds.truth)         # la:27-77, L = 0 (ground truth) path
+    setup_s = time.perf_counter() - t_setup
+    it = 1                                       # iteration 0 regenerates the pool (la:123); start at 1
+    for _ in range(args.warmup):
+        eng.iteration(it)
+        it += 1
+    eng.synchronize()
+    eng.reset_stats()
+    D.barrier()
+    cuda_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.iteration(it)
+        it += 1
+    eng.synchronize()
+    cuda_sync()
+    D.barrier()
+    elapsed = D.max(time.perf_counter() - t0)
+    st = eng.stats()
+    c, cen, _ = eng.get_state()
+    K = int(cen.shape[0])
+
+    value = ws * args.steps / elapsed
+    bpp = prepass_bytes_per_point(ds.d, args.m, K)
+    pre_ms = st["t_prepass_ms"]
+    achieved = (bpp * st["prepass_points"] / 1e9) / (pre_ms / 1e3) if pre_ms > 0 else None
+    launches = max(st["rounds"], 1)
+    traffic = None
+    if args.traffic_csv and os.path.exists(args.traffic_csv):
+        traffic = traffic_from_csv(args.traffic_csv)
+    out = {
+        "metric": "full Gibbs sweeps/sec (N-point reassign) at N=1M D=128; achieved HBM GB/s",
+        "value": round(value, 4),
+        "unit": "sweeps/s",
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (data_generation.R model, numpy draws); R-compatible MT19937 chain stream",
+        "config": {
+            "workload": (f"{args.config}: {CONFIGS.get(args.config, {}).get('name', args.config)}, N={ds.n} D={ds.d} "
+                         f"m={args.m}; one step = Neal-8 sweep + update_phi + compute_loglikelihood "
+                         f"(code/launcher.cpp:94-132), ground-truth init"),
+            "n": ds.n, "d": ds.d, "m": args.m, "K_final": K, "parallelism": f"replicas{ws}",
+            "sweep_effective_GBps": round(survey_sweep_bytes(ds.n, ds.d, args.m) * args.steps / elapsed / 1e9, 2),
+            "setup_s": round(setup_s, 1),
+            "breakdown_ms_per_step": {k: round(st[k] / args.steps, 4) for k in
+                                      ("t_prepass_ms", "t_resolve_ms", "t_stats_ms", "t_host_phi_ms", "t_rng_ms",
+                                       "t_loglik_ms")},
+            "exact_points_per_step": st["exact_points"] / args.steps,
+            "rounds_per_step": st["rounds"] / args.steps,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_prepass",
+            "achieved": None if achieved is None else round(achieved, 1),
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": None if achieved is None else round(achieved / HBM_PEAK_GBPS, 4),
+            "traffic": traffic,
+            "bytes_per_point": bpp,
+            "avg_launch_ms": round(pre_ms / launches, 4),
+        },
+        "cpu_baseline": None,
+    }
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(ds, eng, args.m, args.cpu_baseline_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+    D.close()
+
+
+def traffic_from_csv(path):
+    """Per-launch HBM bytes of k_prepass from a rocprofv3 --pmc counter_collection.csv:
+    (2 * FETCH_SIZE + WRITE_SIZE) KiB -> bytes (gfx950: FETCH_SIZE reports half the bytes
+    of a wide coalesced stream, MI355X_MICROARCH.md 'HBM')."""
+    import csv
+    fetch, write, nd = 0.0, 0.0, set()
+    for row in csv.DictReader(open(path)):
+        if "k_prepass" not in row.get("Kernel_Name", ""):
+            continue
+        nd.add(row.get("Dispatch_Id"))
+        name, val = row.get("Counter_Name"), float(row.get("Counter_Value", 0))
+        if name == "FETCH_SIZE":
+            fetch += val
+        elif name == "WRITE_SIZE":
+            write += val
+    if not nd:
+        return None
+    return round((2 * fetch + write) * 1024 / len(nd))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,130 @@
+/*
+ * hdpm.h -- C ABI of the MI355X-native Neal-8 / split-merge reassignment engine.
+ *
+ * Drop-in boundary for the hot path of Filippo-Galli/Split_and_merge_Gibbs_sampling.
+ * The reference exposes this path as in-process C++ calls behind one Rcpp export; each
+ * entry point below names the reference interface it replaces.  An Rcpp adapter that
+ * keeps the reference's R-facing signature is given in INTEGRATION.md.
+ *
+ * Conventions
+ *   - The caller owns every host buffer; the context owns device memory.
+ *   - Every call returns an int status (HDPM_OK = 0); hdpm_last_error() describes it.
+ *     No C++ exception crosses this boundary.
+ *   - One context per host thread per GPU.  The library never calls the R API.
+ *   - The R random stream (Mersenne-Twister, the 625 words of .Random.seed after the
+ *     kind word) lives in the context and is consumed in the reference's order; it can
+ *     be set and read back explicitly.
+ *   - Categorical data are codes 1..m_j (the reference's NumericMatrix values).
+ *     `codes` is row-major N x D uint8; `centers` are K x D doubles (integer-valued, as
+ *     the reference's NumericVector centers), `sigma` K x D doubles.
+ */
+#ifndef HDPM_H
+#define HDPM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HDPM_OK          0
+#define HDPM_E_VALIDATE  1  /* validate_state failed -> Rcpp::stop in the reference      */
+#define HDPM_E_GSL       2  /* norm_const2 threw (GSL 2F1 overflow)                         */
+#define HDPM_E_PROB      3  /* FixupProb stop(): no positive / non-finite probability      */
+#define HDPM_E_WALKER    4  /* >200 categories: Walker alias sampling not supported        */
+#define HDPM_E_ARG       5  /* invalid argument or capacity                                 */
+#define HDPM_E_DEVICE    6  /* HIP runtime error                                            */
+#define HDPM_E_NODEVICE  7  /* no usable gfx950 device                                      */
+
+typedef struct hdpm_ctx hdpm_ctx;
+
+/* Parameters of run_markov_chain (code/launcher.cpp:7-14), same names and meaning. */
+typedef struct {
+    int32_t verbose, m, iterations, L, burnin, t, r;
+    int32_t neal8, split_merge, n8_step_size, sam_step_size, thinning;
+} hdpm_chain_params;
+
+/* Per-context counters (cumulative since hdpm_ctx_create or hdpm_reset_stats). */
+typedef struct {
+    int64_t sweeps, rounds, restarts, exact_points, moves, checked_rounds, prepass_points;
+    double  t_prepass_ms, t_resolve_ms, t_stats_ms, t_host_phi_ms, t_rng_ms, t_loglik_ms;
+} hdpm_stats;
+
+int         hdpm_device_count(void);
+int         hdpm_ctx_create(int32_t device, hdpm_ctx** out);
+void        hdpm_ctx_destroy(hdpm_ctx* ctx);
+const char* hdpm_last_error(const hdpm_ctx* ctx);
+
+/* aux_data (code/common_functions.hpp:65-72): data, n, attrisize, gamma, v, w. */
+int hdpm_set_data(hdpm_ctx* ctx, const uint8_t* codes, int32_t n, int32_t d, const int32_t* attrisize,
+                  double gamma, const double* v, const double* w);
+
+/* R RNG: set.seed(seed) semantics, or the 625-word state (mti, mt[624]). */
+int hdpm_rng_set_seed(hdpm_ctx* ctx, uint32_t seed);
+int hdpm_rng_set_state(hdpm_ctx* ctx, const int32_t* state625);
+int hdpm_rng_get_state(const hdpm_ctx* ctx, int32_t* state625);
+
+/* internal_state (code/common_functions.hpp:32-63): c_i (labels 0..K-1), centers, sigma. */
+int hdpm_set_state(hdpm_ctx* ctx, const int32_t* c_i, int32_t K, const double* centers, const double* sigma);
+int hdpm_get_state(hdpm_ctx* ctx, int32_t* c_i, int32_t* K, double* centers, double* sigma, int32_t cap);
+
+/* Latent-parameter pool (code/launcher.cpp:67-77): P entries of (center, sigma). */
+int hdpm_set_pool(hdpm_ctx* ctx, const double* centers, const double* sigma, int64_t P);
+int hdpm_get_pool(hdpm_ctx* ctx, double* centers, double* sigma, int64_t P);
+/* Draw P prior entries from the context stream exactly as la:74-77 / la:124-128. */
+int hdpm_generate_pool(hdpm_ctx* ctx, int64_t P);
+
+/* One Neal-8 sweep: N calls of sample_allocation (code/neal8.hpp:4-5, neal8.cpp:10-160)
+ * in index order, i.e. the loop code/launcher.cpp:95-99.  Consumes m+1 uniforms/point. */
+int hdpm_neal8_sweep(hdpm_ctx* ctx, int32_t m);
+
+/* update_phi (code/common_functions.hpp:113, .cpp:511-591); idx == NULL -> all clusters. */
+int hdpm_update_phi(hdpm_ctx* ctx, const int32_t* cluster_indexes, int32_t n_idx);
+
+/* compute_loglikelihood (code/common_functions.hpp:105, .cpp:379-401). */
+int hdpm_compute_loglikelihood(hdpm_ctx* ctx, double* out);
+
+/* The N x K log-likelihood matrix and integer Hamming counts against the current
+ * clusters (code/neal8.cpp:40-50 inner loop), L[i*K+k], H[i*K+k]. */
+int hdpm_loglik_matrix(hdpm_ctx* ctx, double* L, int32_t* H);
+
+/* split_restricted_gibbs_sampler (code/split_merge.hpp:13, .cpp:163-225) on the state. */
+int hdpm_restricted_gibbs(hdpm_ctx* ctx, const int32_t* S, int32_t nS, int32_t i1, int32_t i2, int32_t t);
+
+/* logprobgs_c_i (code/split_merge.hpp:11, .cpp:96-161): gamma_star = context state,
+ * gamma = launch labels g_c_i. */
+int hdpm_logprobgs_c_i(hdpm_ctx* ctx, const int32_t* g_c_i, const int32_t* S, int32_t nS, int32_t i1,
+                       int32_t i2, double* out);
+
+/* split_and_merge (code/split_merge.hpp:217-219, .cpp:542-598). */
+int hdpm_split_and_merge(hdpm_ctx* ctx, int32_t t, int32_t r, int32_t idx_1_sm, int32_t* accepted);
+
+/* run_markov_chain (code/launcher.cpp:6-174).  c_i_init may be NULL (random init with L
+ * labels).  Output buffers (any may be NULL): out_total_cls[iterations],
+ * out_c_i[iterations * n], out_loglik[iterations], out_accepted[iterations], final_ass[n];
+ * out_time_s = wall seconds of the sampling loop (results$time). */
+int hdpm_run_markov_chain(hdpm_ctx* ctx, const hdpm_chain_params* p, const int32_t* c_i_init,
+                          int32_t* out_total_cls, int32_t* out_c_i, double* out_loglik,
+                          int32_t* out_accepted, int32_t* final_ass, double* out_time_s);
+
+/* The two halves of run_markov_chain, for callers that drive the loop themselves:
+ * hdpm_init_chain = la:27-77 (initial labels, centers, sigmas, update_phi, latent pool of
+ * n*m*thinning entries); hdpm_iteration = one pass of the loop body la:85-132 for
+ * iteration `iter` (Neal-8 sweep + update_phi, split-merge, pool regeneration when
+ * iter % 1000 == 0, compute_loglikelihood).  idx_1_sm is carried by the caller. */
+int hdpm_init_chain(hdpm_ctx* ctx, const hdpm_chain_params* p, const int32_t* c_i_init);
+int hdpm_iteration(hdpm_ctx* ctx, const hdpm_chain_params* p, int32_t iter, int32_t* idx_1_sm,
+                   int32_t* accepted, double* loglik);
+
+/* Diagnostics / testing. */
+int hdpm_get_stats(const hdpm_ctx* ctx, hdpm_stats* out);
+int hdpm_reset_stats(hdpm_ctx* ctx);
+/* mode bit 0: evaluate every point on the exact path (no certainty shortcut). */
+int hdpm_set_debug(hdpm_ctx* ctx, int32_t mode);
+/* Block until all device work of the context is done. */
+int hdpm_synchronize(hdpm_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HDPM_H */

@@ -1,0 +1,114 @@
+"""ctypes binding of libhdpm.so (include/hdpm.h).
+
+The shared library is built in-tree (split_and_merge_gibbs_sampling_amd/libhdpm.so) by
+``build()``.  There is no CPU fallback: loading fails loudly if the library is missing,
+and creating an engine fails loudly if no gfx950 device is visible.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libhdpm.so")
+CSRC = os.path.join(PKG_DIR, "csrc")
+
+EXPORTS = (
+    "hdpm_device_count", "hdpm_ctx_create", "hdpm_ctx_destroy", "hdpm_last_error", "hdpm_set_data",
+    "hdpm_rng_set_seed", "hdpm_rng_set_state", "hdpm_rng_get_state", "hdpm_set_state", "hdpm_get_state",
+    "hdpm_set_pool", "hdpm_get_pool", "hdpm_generate_pool", "hdpm_neal8_sweep", "hdpm_update_phi",
+    "hdpm_compute_loglikelihood", "hdpm_loglik_matrix", "hdpm_restricted_gibbs", "hdpm_logprobgs_c_i",
+    "hdpm_split_and_merge", "hdpm_run_markov_chain", "hdpm_get_stats", "hdpm_reset_stats",
+    "hdpm_set_debug", "hdpm_synchronize", "hdpm_init_chain", "hdpm_iteration",
+)
+
+STATUS = {0: "OK", 1: "E_VALIDATE", 2: "E_GSL", 3: "E_PROB", 4: "E_WALKER", 5: "E_ARG",
+          6: "E_DEVICE", 7: "E_NODEVICE"}
+
+
+class HdpmError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"hdpm {STATUS.get(status, status)}: {msg}")
+        self.status = status
+
+
+class ChainParams(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in (
+        "verbose", "m", "iterations", "L", "burnin", "t", "r", "neal8", "split_merge",
+        "n8_step_size", "sam_step_size", "thinning")]
+
+
+class Stats(C.Structure):
+    _fields_ = [(n, C.c_int64) for n in (
+        "sweeps", "rounds", "restarts", "exact_points", "moves", "checked_rounds", "prepass_points")] + \
+        [(n, C.c_double) for n in (
+            "t_prepass_ms", "t_resolve_ms", "t_stats_ms", "t_host_phi_ms", "t_rng_ms", "t_loglik_ms")]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+def build(force: bool = False) -> str:
+    """Compile the HIP kernels + host runtime for gfx950 into LIB_PATH (hipcc)."""
+    srcs = [os.path.join(CSRC, f) for f in os.listdir(CSRC)]
+    stale = force or not os.path.exists(LIB_PATH) or \
+        max(os.path.getmtime(s) for s in srcs) > os.path.getmtime(LIB_PATH)
+    if stale:
+        subprocess.run(["make", "-s", "-C", CSRC], check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libhdpm.so not built ({LIB_PATH}); run __graft_entry__.build()")
+    L = C.CDLL(LIB_PATH)
+    vp, i32, i64, f64 = C.c_void_p, C.c_int32, C.c_int64, C.c_double
+    P = C.POINTER
+    sig = {
+        "hdpm_device_count": ([], C.c_int),
+        "hdpm_ctx_create": ([i32, P(vp)], C.c_int),
+        "hdpm_ctx_destroy": ([vp], None),
+        "hdpm_last_error": ([vp], C.c_char_p),
+        "hdpm_set_data": ([vp, vp, i32, i32, vp, f64, vp, vp], C.c_int),
+        "hdpm_rng_set_seed": ([vp, C.c_uint32], C.c_int),
+        "hdpm_rng_set_state": ([vp, vp], C.c_int),
+        "hdpm_rng_get_state": ([vp, vp], C.c_int),
+        "hdpm_set_state": ([vp, vp, i32, vp, vp], C.c_int),
+        "hdpm_get_state": ([vp, vp, P(i32), vp, vp, i32], C.c_int),
+        "hdpm_set_pool": ([vp, vp, vp, i64], C.c_int),
+        "hdpm_get_pool": ([vp, vp, vp, i64], C.c_int),
+        "hdpm_generate_pool": ([vp, i64], C.c_int),
+        "hdpm_neal8_sweep": ([vp, i32], C.c_int),
+        "hdpm_update_phi": ([vp, vp, i32], C.c_int),
+        "hdpm_compute_loglikelihood": ([vp, P(f64)], C.c_int),
+        "hdpm_loglik_matrix": ([vp, vp, vp], C.c_int),
+        "hdpm_restricted_gibbs": ([vp, vp, i32, i32, i32, i32], C.c_int),
+        "hdpm_logprobgs_c_i": ([vp, vp, vp, i32, i32, i32, P(f64)], C.c_int),
+        "hdpm_split_and_merge": ([vp, i32, i32, i32, P(i32)], C.c_int),
+        "hdpm_run_markov_chain": ([vp, P(ChainParams), vp, vp, vp, vp, vp, vp, vp], C.c_int),
+        "hdpm_get_stats": ([vp, P(Stats)], C.c_int),
+        "hdpm_init_chain": ([vp, P(ChainParams), vp], C.c_int),
+        "hdpm_iteration": ([vp, P(ChainParams), i32, P(i32), P(i32), P(f64)], C.c_int),
+        "hdpm_reset_stats": ([vp], C.c_int),
+        "hdpm_set_debug": ([vp, i32], C.c_int),
+        "hdpm_synchronize": ([vp], C.c_int),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def ptr(a: np.ndarray | None):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)

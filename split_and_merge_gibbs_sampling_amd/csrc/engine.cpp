@@ -1,0 +1,984 @@
+// engine.cpp -- host runtime of the hdpm MI355X engine and its C ABI (include/hdpm.h).
+//
+// Owns the device-resident chain state and drives the gfx950 kernels in kernels.hip.
+// The host keeps the single R-compatible random stream and performs the draws that
+// consume a data-dependent number of uniforms (update_phi's center/sigma draws, pool
+// generation); the device consumes contiguous (m+1)-per-point slices for the sweep.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/hdpm.h"
+#include "kernels.hpp"
+#include "rmath.hpp"
+
+namespace hdpm {
+
+hipError_t launch_prepass(const PrepassArgs& a, int nblocks, hipStream_t s);
+hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s);
+size_t resolve_smem_bytes(int scap, int m);
+hipError_t launch_relabel(int* c, const int* los, int n, hipStream_t s);
+hipError_t launch_hist(const HistArgs& a, hipStream_t s);
+hipError_t launch_loglik(const LoglikArgs& a, hipStream_t s);
+hipError_t launch_lmatrix(const uint8_t* codes_t, int n, int d, int nq, ParamTables cl, int K, double* L,
+                          int* H, int64_t ldL, hipStream_t s);
+int sm_restricted_gibbs_device(struct Ctx* c, const int32_t* S, int32_t nS, int32_t i1, int32_t i2,
+                               int32_t t);
+
+struct HipError {
+  hipError_t e;
+  const char* what;
+};
+#define HIPCHK(x)                                      \
+  do {                                                 \
+    hipError_t _e = (x);                               \
+    if (_e != hipSuccess) throw HipError{_e, #x};     \
+  } while (0)
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  // Grow to at least `count` elements; keep_old copies the previous contents.
+  void ensure(size_t count, bool keep_old = false, hipStream_t s = nullptr) {
+    if (count <= n && p) return;
+    T* np = nullptr;
+    HIPCHK(hipMalloc(&np, std::max<size_t>(count, 1) * sizeof(T)));
+    if (keep_old && p && n) {
+      HIPCHK(hipMemcpyAsync(np, p, n * sizeof(T), hipMemcpyDeviceToDevice, s));
+      HIPCHK(hipStreamSynchronize(s));
+    }
+    release();
+    p = np;
+    n = count;
+  }
+};
+
+template <class T>
+struct PinBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  ~PinBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+  void ensure(size_t count) {
+    if (count <= n && p) return;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    HIPCHK(hipHostMalloc(&p, std::max<size_t>(count, 1) * sizeof(T), hipHostMallocDefault));
+    n = count;
+  }
+};
+
+static int host_threads() {
+  unsigned h = std::thread::hardware_concurrency();
+  if (h == 0) h = 4;
+  return (int)std::min<unsigned>(h, 16);
+}
+
+template <class F>
+static void parallel_for(int64_t n, F f) {
+  const int T = host_threads();
+  if (n < 4096 || T <= 1) {
+    f(0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  const int64_t chunk = (n + T - 1) / T;
+  for (int t = 0; t < T; ++t) {
+    int64_t a = t * chunk, b = std::min(n, a + chunk);
+    if (a >= b) break;
+    th.emplace_back([=] { f(a, b); });
+  }
+  for (auto& x : th) x.join();
+}
+
+// Device scratch of the split-merge move (split_merge.inl).
+struct SmWork {
+  DevBuf<int> d_S, d_side, d_side_ref, d_counts2;
+  DevBuf<double> d_ll, d_out;
+  DevBuf<uint8_t> d_two_codes;
+  DevBuf<double> d_two_tab;
+  DevBuf<uint32_t> d_raw;
+  std::vector<double> h_out;
+};
+
+struct Ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  hipEvent_t ev[8];
+
+  // aux_data
+  int n = 0, d = 0, nq = 0, dp = 0, mmax = 0;
+  double gamma = 0;
+  std::vector<int32_t> att;
+  std::vector<double> v, w;
+  std::vector<uint8_t> codes;  // row-major n x d
+  DevBuf<uint8_t> d_codes_t;
+  DevBuf<double> d_logn;
+  std::vector<double> h_logn;
+
+  Rng rng;
+
+  // internal_state.  Labels are device-authoritative after a sweep (host_c_valid).
+  int K = 0;
+  std::vector<int32_t> h_c;
+  bool host_c_valid = false;
+  std::vector<int32_t> h_counts;      // per label
+  std::vector<uint8_t> h_center;      // K x d codes
+  std::vector<double> h_sigma;        // K x d
+  bool have_state = false;
+  bool tables_dirty = true;
+
+  DevBuf<int> d_c, d_counts, d_sol, d_los, d_src;
+  DevBuf<uint8_t> d_slot_codes;
+  DevBuf<double> d_slot_tab;
+  int scap = 0;
+
+  // latent pool
+  int64_t P = 0;
+  std::vector<uint8_t> h_pool_c;      // P x d codes
+  std::vector<double> h_pool_s;       // P x d
+  DevBuf<uint8_t> d_pool_codes;
+  DevBuf<double> d_pool_tab;
+
+  // sweep scratch
+  PinBuf<uint32_t> h_raw;
+  DevBuf<uint32_t> d_raw;
+  DevBuf<double> d_L;
+  int Ecap = 0;
+  DevBuf<double> d_margin;
+  DevBuf<int> d_list, d_cnt;
+  DevBuf<ResolveCtl> d_ctl;
+  PinBuf<ResolveCtl> h_ctl;
+
+  // statistics buffers
+  DevBuf<unsigned> d_freq;
+  std::vector<unsigned> h_freq;
+  DevBuf<unsigned char> d_mask;
+  DevBuf<double> d_partial;
+  std::vector<double> h_partial;
+
+  hdpm_stats stats{};
+  int debug = 0;
+  std::unordered_map<uint64_t, bool> beta_cache;
+
+  SmWork sm;
+  // scratch for host sampling
+  std::vector<double> sp;
+  std::vector<int> sperm;
+
+  ~Ctx() {
+    if (stream) {
+      (void)hipStreamSynchronize(stream);
+      for (auto& e : ev) (void)hipEventDestroy(e);
+      (void)hipStreamDestroy(stream);
+    }
+  }
+
+  // ------------------------------------------------------------------ helpers
+  void tables_for(const uint8_t* cen, const double* sig, uint8_t* out_codes, double* out_tab) const {
+    std::memset(out_codes, 0, dp);
+    for (int j = 0; j < d; ++j) {
+      out_codes[j] = cen[j];
+      dhamming_pair(sig[j], att[j], &out_tab[2 * j], &out_tab[2 * j + 1]);
+    }
+  }
+
+  void ensure_slots(int need) {
+    if (need <= scap) return;
+    int nc = std::max(need, std::max(2 * scap, 64));
+    d_counts.ensure(nc, true, stream);
+    d_sol.ensure(nc, true, stream);
+    d_los.ensure(nc, true, stream);
+    d_src.ensure(nc, true, stream);
+    d_slot_codes.ensure((size_t)nc * dp, true, stream);
+    d_slot_tab.ensure((size_t)nc * 2 * d, true, stream);
+    scap = nc;
+  }
+
+  // Upload label tables, counts and identity slot maps for labels 0..K-1.
+  void upload_clusters() {
+    ensure_slots(K + 2);
+    std::vector<uint8_t> cc((size_t)K * dp);
+    std::vector<double> tt((size_t)K * 2 * d);
+    for (int k = 0; k < K; ++k)
+      tables_for(&h_center[(size_t)k * d], &h_sigma[(size_t)k * d], &cc[(size_t)k * dp], &tt[(size_t)k * 2 * d]);
+    std::vector<int> ident(K);
+    for (int k = 0; k < K; ++k) ident[k] = k;
+    std::vector<int> minus1(K, -1);
+    if (K) {
+      HIPCHK(hipMemcpyAsync(d_slot_codes.p, cc.data(), cc.size(), hipMemcpyHostToDevice, stream));
+      HIPCHK(hipMemcpyAsync(d_slot_tab.p, tt.data(), tt.size() * 8, hipMemcpyHostToDevice, stream));
+      HIPCHK(hipMemcpyAsync(d_sol.p, ident.data(), K * 4, hipMemcpyHostToDevice, stream));
+      HIPCHK(hipMemcpyAsync(d_los.p, ident.data(), K * 4, hipMemcpyHostToDevice, stream));
+      HIPCHK(hipMemcpyAsync(d_src.p, minus1.data(), K * 4, hipMemcpyHostToDevice, stream));
+      HIPCHK(hipMemcpyAsync(d_counts.p, h_counts.data(), K * 4, hipMemcpyHostToDevice, stream));
+    }
+    HIPCHK(hipStreamSynchronize(stream));
+    tables_dirty = false;
+  }
+
+  // Upload tables of the labels in `which` only (after update_phi on a subset).
+  void upload_some(const std::vector<int>& which) {
+    std::vector<uint8_t> cc(dp);
+    std::vector<double> tt(2 * d);
+    for (int k : which) {
+      tables_for(&h_center[(size_t)k * d], &h_sigma[(size_t)k * d], cc.data(), tt.data());
+      HIPCHK(hipMemcpyAsync(d_slot_codes.p + (size_t)k * dp, cc.data(), dp, hipMemcpyHostToDevice, stream));
+      HIPCHK(hipMemcpyAsync(d_slot_tab.p + (size_t)k * 2 * d, tt.data(), 16 * d, hipMemcpyHostToDevice, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+    }
+  }
+
+  void download_labels() {
+    if (host_c_valid) return;
+    h_c.resize(n);
+    HIPCHK(hipMemcpyAsync(h_c.data(), d_c.p, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    host_c_valid = true;
+  }
+
+  void upload_labels() {
+    d_c.ensure(n);
+    HIPCHK(hipMemcpyAsync(d_c.p, h_c.data(), (size_t)n * 4, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    host_c_valid = true;
+  }
+
+  void recount() {
+    h_counts.assign(K, 0);
+    for (int i = 0; i < n; ++i)
+      if (h_c[i] >= 0 && h_c[i] < K) h_counts[h_c[i]]++;
+  }
+
+  bool beta_path(double vv, double ww, double mj) {
+    uint64_t key;
+    {
+      uint64_t a, b, c;
+      std::memcpy(&a, &vv, 8);
+      std::memcpy(&b, &ww, 8);
+      std::memcpy(&c, &mj, 8);
+      key = a * 0x9E3779B97F4A7C15ull ^ (b + 0x632BE59BD9B4E019ull) * 0xC2B2AE3D27D4EB4Full ^ c;
+    }
+    auto it = beta_cache.find(key);
+    if (it != beta_cache.end()) return it->second;
+    bool r = rhig_beta_path(vv, ww, mj);
+    if (beta_cache.size() < (1u << 20)) beta_cache.emplace(key, r);
+    return r;
+  }
+
+  // sample_sigma_1_cluster (cf:218-235)
+  int sample_sigma(const double* vv, const double* ww, double* out) {
+    for (int j = 0; j < d; ++j) {
+      int e = kOk;
+      const double mj = (double)att[j];
+      out[j] = rhig1_decided(rng, vv[j], ww[j], mj, beta_path(vv[j], ww[j], mj), &e);
+      if (e) return e;
+    }
+    return kOk;
+  }
+  // sample_center_1_cluster without probabilities (cf:198-199)
+  void sample_center_uniform(uint8_t* out) {
+    for (int j = 0; j < d; ++j) out[j] = (uint8_t)(int)(att[j] * rng.unif() + 1);
+  }
+
+  // ------------------------------------------------------------------ data
+  int set_data(const uint8_t* x, int n_, int d_, const int32_t* attr, double g, const double* vv,
+               const double* ww) {
+    if (n_ <= 0 || d_ <= 0) { err = "n and d must be positive"; return kArg; }
+    for (int j = 0; j < d_; ++j)
+      if (attr[j] < 1 || attr[j] > 255) { err = "attrisize must be in 1..255"; return kArg; }
+    for (int64_t i = 0; i < (int64_t)n_ * d_; ++i) {
+      const int j = (int)(i % d_);
+      if (x[i] < 1 || x[i] > attr[j]) { err = "codes must lie in 1..attrisize[j]"; return kArg; }
+    }
+    n = n_; d = d_; nq = (d + 15) / 16; dp = nq * 16; gamma = g;
+    att.assign(attr, attr + d);
+    v.assign(vv, vv + d);
+    w.assign(ww, ww + d);
+    mmax = *std::max_element(att.begin(), att.end());
+    codes.assign(x, x + (size_t)n * d);
+    const int64_t n64 = ((int64_t)n + 63) / 64 * 64;
+    std::vector<uint8_t> t((size_t)n64 * dp, 0);
+    for (int64_t i = 0; i < n; ++i)
+      for (int j = 0; j < d; ++j) t[tiled_offset(i, j, nq)] = codes[(size_t)i * d + j];
+    d_codes_t.ensure(t.size());
+    HIPCHK(hipMemcpyAsync(d_codes_t.p, t.data(), t.size(), hipMemcpyHostToDevice, stream));
+    h_logn.resize((size_t)n + 2);
+    h_logn[0] = -INFINITY;
+    for (int k = 1; k < n + 2; ++k) h_logn[k] = std::log((double)k);
+    d_logn.ensure(h_logn.size());
+    HIPCHK(hipMemcpyAsync(d_logn.p, h_logn.data(), h_logn.size() * 8, hipMemcpyHostToDevice, stream));
+    d_c.ensure(n);
+    HIPCHK(hipStreamSynchronize(stream));
+    have_state = false;
+    P = 0;
+    return kOk;
+  }
+
+  int set_state(const int32_t* c_i, int K_, const double* cen, const double* sig) {
+    if (!n) { err = "set_data first"; return kArg; }
+    if (K_ < 0) { err = "K < 0"; return kArg; }
+    K = K_;
+    h_c.assign(c_i, c_i + n);
+    h_center.assign((size_t)K * d, 0);
+    h_sigma.assign(sig, sig + (size_t)K * d);
+    for (size_t q = 0; q < (size_t)K * d; ++q) h_center[q] = (uint8_t)(int)cen[q];
+    for (int i = 0; i < n; ++i)
+      if (h_c[i] < 0) { err = "negative label"; return kArg; }
+    recount();
+    upload_labels();
+    upload_clusters();
+    have_state = true;
+    return kOk;
+  }
+
+  int get_state(int32_t* c_i, int32_t* Kout, double* cen, double* sig, int cap) {
+    if (!have_state) { err = "no state"; return kArg; }
+    download_labels();
+    if (c_i) std::memcpy(c_i, h_c.data(), (size_t)n * 4);
+    if (Kout) *Kout = K;
+    if (K > cap && (cen || sig)) { err = "cap too small"; return kArg; }
+    for (size_t q = 0; q < (size_t)K * d; ++q) {
+      if (cen) cen[q] = (double)h_center[q];
+      if (sig) sig[q] = h_sigma[q];
+    }
+    return kOk;
+  }
+
+  // ------------------------------------------------------------------ pool
+  void upload_pool() {
+    std::vector<uint8_t> pc((size_t)P * dp, 0);
+    std::vector<double> pt((size_t)P * 2 * d);
+    parallel_for(P, [&](int64_t a, int64_t b) {
+      for (int64_t e = a; e < b; ++e)
+        tables_for(&h_pool_c[(size_t)e * d], &h_pool_s[(size_t)e * d], &pc[(size_t)e * dp], &pt[(size_t)e * 2 * d]);
+    });
+    d_pool_codes.ensure(pc.size());
+    d_pool_tab.ensure(pt.size());
+    HIPCHK(hipMemcpyAsync(d_pool_codes.p, pc.data(), pc.size(), hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(d_pool_tab.p, pt.data(), pt.size() * 8, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+  }
+
+  int set_pool(const double* cen, const double* sig, int64_t P_) {
+    if (!n) { err = "set_data first"; return kArg; }
+    if (P_ <= 0 || P_ > 0x7fffffff) { err = "pool size must be in 1..2^31-1"; return kArg; }
+    P = P_;
+    h_pool_c.resize((size_t)P * d);
+    h_pool_s.assign(sig, sig + (size_t)P * d);
+    for (size_t q = 0; q < (size_t)P * d; ++q) h_pool_c[q] = (uint8_t)(int)cen[q];
+    upload_pool();
+    return kOk;
+  }
+
+  // la:74-77 / la:124-128: per entry D centers then D sigmas, from the context stream.
+  int generate_pool(int64_t P_) {
+    if (!n) { err = "set_data first"; return kArg; }
+    if (P_ <= 0 || P_ > 0x7fffffff) { err = "pool size must be in 1..2^31-1"; return kArg; }
+    auto t0 = std::chrono::steady_clock::now();
+    P = P_;
+    h_pool_c.resize((size_t)P * d);
+    h_pool_s.resize((size_t)P * d);
+    for (int64_t e = 0; e < P; ++e) {
+      sample_center_uniform(&h_pool_c[(size_t)e * d]);
+      int st = sample_sigma(v.data(), w.data(), &h_pool_s[(size_t)e * d]);
+      if (st) { err = "rhig failed in pool generation"; return st; }
+    }
+    upload_pool();
+    stats.t_rng_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return kOk;
+  }
+
+  // ------------------------------------------------------------------ Neal-8 sweep
+  int neal8_sweep(int m) {
+    if (!have_state) { err = "no state"; return kArg; }
+    if (P <= 0) { err = "no latent pool"; return kArg; }
+    if (m <= 0) { err = "m must be positive"; return kArg; }
+    // validate_state before the first case (the reference stops at the first point)
+    {
+      if (!host_c_valid) { /* device labels are always consistent with K */ }
+      else {
+        std::vector<char> seen(K + 1, 0);
+        int u = 0;
+        for (int i = 0; i < n; ++i) {
+          const int c = h_c[i];
+          if (c >= K) { err = "State validation failed: inconsistent cluster count"; return kValidate; }
+          if (!seen[c]) { seen[c] = 1; u++; }
+        }
+        if (u != K) { err = "State validation failed: inconsistent cluster count"; return kValidate; }
+      }
+    }
+    if (tables_dirty) upload_clusters();
+    const int K0 = K;
+    std::vector<uint8_t> old_center = h_center;
+    std::vector<double> old_sigma = h_sigma;
+
+    // the sweep's slice of the R stream: m pick uniforms + 1 categorical per point
+    auto tr0 = std::chrono::steady_clock::now();
+    const size_t nraw = (size_t)n * (m + 1);
+    h_raw.ensure(nraw);
+    rng.raw_block(h_raw.p, (int64_t)nraw);
+    d_raw.ensure(nraw);
+    HIPCHK(hipMemcpyAsync(d_raw.p, h_raw.p, nraw * 4, hipMemcpyHostToDevice, stream));
+    stats.t_rng_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count();
+
+    const int nb_max = (n + kBlock - 1) / kBlock;
+    d_margin.ensure(n);
+    d_list.ensure((size_t)nb_max * kBlock);
+    d_cnt.ensure(nb_max);
+    d_ctl.ensure(1);
+    h_ctl.ensure(1);
+
+    int nslots = K;
+    int p = 0;
+    const double dmax = 0.25;
+    while (p < n) {
+      ensure_slots(nslots + 2);
+      const int S = nslots;
+      if (S + m > Ecap) {
+        Ecap = std::max(S + m, std::max(2 * Ecap, 32));
+        d_L.ensure((size_t)Ecap * n);
+      }
+      const int E = K + m;
+      const double T = 54.0 * M_LN2 + std::log((double)E) + 0.5;
+      PrepassArgs pa;
+      pa.codes_t = d_codes_t.p; pa.n = n; pa.d = d; pa.nq = nq;
+      pa.c = d_c.p; pa.counts = d_counts.p; pa.slot_of_label = d_sol.p; pa.K = K; pa.S = S;
+      pa.slots = ParamTables{d_slot_codes.p, d_slot_tab.p};
+      pa.pool = ParamTables{d_pool_codes.p, d_pool_tab.p};
+      pa.P = P; pa.raw = d_raw.p; pa.m = m; pa.logn = d_logn.p; pa.logfac = std::log(gamma / m);
+      pa.thresh = T + 2.0 * dmax;
+      pa.L = d_L.p; pa.ldL = n; pa.margin = d_margin.p; pa.list = d_list.p; pa.cnt = d_cnt.p; pa.p0 = p;
+      const int nblocks = (n - p + kBlock - 1) / kBlock;
+      HIPCHK(hipEventRecord(ev[0], stream));
+      HIPCHK(launch_prepass(pa, nblocks, stream));
+      stats.prepass_points += n - p;
+      HIPCHK(hipEventRecord(ev[1], stream));
+
+      ResolveArgs ra;
+      ra.n = n; ra.d = d; ra.dp = dp; ra.m = m; ra.P = P;
+      ra.c = d_c.p; ra.counts = d_counts.p; ra.slot_of_label = d_sol.p; ra.label_of_slot = d_los.p;
+      ra.slot_src = d_src.p; ra.slot_codes = d_slot_codes.p; ra.slot_tab = d_slot_tab.p;
+      ra.pool = pa.pool; ra.raw = d_raw.p; ra.logn = d_logn.p; ra.logfac = pa.logfac;
+      ra.L = d_L.p; ra.ldL = n; ra.S = S; ra.margin = d_margin.p; ra.list = d_list.p; ra.cnt = d_cnt.p;
+      ra.nblocks = nblocks; ra.p0 = p; ra.T = T; ra.dmax = dmax; ra.scap = scap; ra.K = K;
+      ra.nslots = nslots; ra.ctl = d_ctl.p; ra.force_exact = (debug & 1);
+      if (resolve_smem_bytes(scap, m) > 160 * 1024) { err = "too many clusters for the resolver (K > ~3000)"; return kArg; }
+      HIPCHK(launch_resolve(ra, stream));
+      HIPCHK(hipEventRecord(ev[2], stream));
+      HIPCHK(hipMemcpyAsync(h_ctl.p, d_ctl.p, sizeof(ResolveCtl), hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+      float t1 = 0, t2 = 0;
+      HIPCHK(hipEventElapsedTime(&t1, ev[0], ev[1]));
+      HIPCHK(hipEventElapsedTime(&t2, ev[1], ev[2]));
+      stats.t_prepass_ms += t1;
+      stats.t_resolve_ms += t2;
+      stats.rounds++;
+      const ResolveCtl c = *h_ctl.p;
+      stats.exact_points += c.exact;
+      stats.moves += c.moves;
+      stats.checked_rounds += c.checked;
+      if (c.status) {
+        err = c.status == kValidate ? "State validation failed: inconsistent cluster count from Neal8 case 2"
+              : c.status == kWalker ? "more than 200 categories: Walker alias sampling is not supported"
+              : c.status == kProb   ? "Too few positive probabilities"
+                                    : "resolver failure";
+        return c.status;
+      }
+      K = c.K;
+      nslots = c.nslots;
+      if (c.restart) stats.restarts++;
+      p = c.next;
+    }
+
+    // slots -> labels; rebuild per-label parameters and counts
+    auto ts0 = std::chrono::steady_clock::now();
+    std::vector<int> sol(K), cnt(nslots), src(nslots);
+    HIPCHK(hipMemcpyAsync(sol.data(), d_sol.p, (size_t)K * 4, hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipMemcpyAsync(cnt.data(), d_counts.p, (size_t)nslots * 4, hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipMemcpyAsync(src.data(), d_src.p, (size_t)nslots * 4, hipMemcpyDeviceToHost, stream));
+    HIPCHK(launch_relabel(d_c.p, d_los.p, n, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    h_center.assign((size_t)K * d, 0);
+    h_sigma.assign((size_t)K * d, 0.0);
+    h_counts.assign(K, 0);
+    for (int l = 0; l < K; ++l) {
+      const int s = sol[l];
+      h_counts[l] = cnt[s];
+      const uint8_t* cc;
+      const double* ss;
+      if (s < K0) {
+        cc = &old_center[(size_t)s * d];
+        ss = &old_sigma[(size_t)s * d];
+      } else {
+        cc = &h_pool_c[(size_t)src[s] * d];
+        ss = &h_pool_s[(size_t)src[s] * d];
+      }
+      std::memcpy(&h_center[(size_t)l * d], cc, d);
+      std::memcpy(&h_sigma[(size_t)l * d], ss, (size_t)d * 8);
+    }
+    host_c_valid = false;
+    tables_dirty = true;
+    // counts per label on the device (slot == label again after the relabel)
+    {
+      std::vector<int> ident(K);
+      for (int k = 0; k < K; ++k) ident[k] = k;
+      if (K) {
+        HIPCHK(hipMemcpyAsync(d_counts.p, h_counts.data(), (size_t)K * 4, hipMemcpyHostToDevice, stream));
+        HIPCHK(hipMemcpyAsync(d_sol.p, ident.data(), (size_t)K * 4, hipMemcpyHostToDevice, stream));
+        HIPCHK(hipMemcpyAsync(d_los.p, ident.data(), (size_t)K * 4, hipMemcpyHostToDevice, stream));
+      }
+      HIPCHK(hipStreamSynchronize(stream));
+    }
+    stats.t_stats_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
+    stats.sweeps++;
+    return kOk;
+  }
+
+  // ------------------------------------------------------------------ update_phi
+  // freq[k][j][l] for the labels in mask (device histogram), downloaded to h_freq.
+  void histogram(const std::vector<unsigned char>* mask) {
+    const size_t nent = (size_t)K * d * mmax;
+    d_freq.ensure(std::max<size_t>(nent, 1));
+    HIPCHK(hipMemsetAsync(d_freq.p, 0, nent * 4, stream));
+    HistArgs ha;
+    ha.codes_t = d_codes_t.p; ha.n = n; ha.d = d; ha.nq = nq; ha.label = d_c.p;
+    ha.mask = nullptr; ha.K = K; ha.mmax = mmax; ha.freq = d_freq.p;
+    if (mask) {
+      d_mask.ensure(std::max(K, 1));
+      HIPCHK(hipMemcpyAsync(d_mask.p, mask->data(), K, hipMemcpyHostToDevice, stream));
+      ha.mask = d_mask.p;
+    }
+    HIPCHK(launch_hist(ha, stream));
+    h_freq.resize(nent);
+    HIPCHK(hipMemcpyAsync(h_freq.data(), d_freq.p, nent * 4, hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+  }
+
+  // cf:511-591 with cluster sizes from h_counts and frequencies from the device.
+  int update_phi(const int32_t* idx, int nidx) {
+    if (!have_state) { err = "no state"; return kArg; }
+    if (tables_dirty) upload_clusters();
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<unsigned char> mask(K, nidx == 0 ? 1 : 0);
+    for (int q = 0; q < nidx; ++q)
+      if (idx[q] >= 0 && idx[q] < K) mask[idx[q]] = 1;
+    histogram(nidx == 0 ? nullptr : &mask);
+    auto t1 = std::chrono::steady_clock::now();
+    std::vector<double> prob(mmax), nv(d), nw(d);
+    std::vector<int> touched;
+    for (int i = 0; i < K; ++i) {
+      if (!mask[i]) continue;
+      const int nn = h_counts[i];
+      if (nn == 0) continue;
+      uint8_t* cen = &h_center[(size_t)i * d];
+      double* sig = &h_sigma[(size_t)i * d];
+      const unsigned* f = &h_freq[(size_t)i * d * mmax];
+      for (int j = 0; j < d; ++j) {          // compute_prob_centers + center draw
+        const int mj = att[j];
+        const unsigned* fj = f + (size_t)j * mmax;
+        for (int l = 0; l < mj; ++l) prob[l] = (-((double)nn - (double)fj[l])) / sig[j];
+        double mx = prob[0];
+        for (int l = 1; l < mj; ++l) if (prob[l] > mx) mx = prob[l];
+        for (int l = 0; l < mj; ++l) prob[l] = std::exp(prob[l] - mx);
+        double sum = 0.0;
+        for (int l = 0; l < mj; ++l) sum += prob[l];
+        for (int l = 0; l < mj; ++l) prob[l] = prob[l] / sum;
+        int pick = sample_prob1(rng, prob.data(), mj, sp, sperm);
+        if (pick < 0) { err = "center draw failed"; return -pick; }
+        cen[j] = (uint8_t)(pick + 1);
+      }
+      for (int j = 0; j < d; ++j) {
+        const double sumdelta = (double)f[(size_t)j * mmax + (cen[j] - 1)];
+        nw[j] = w[j] + nn - sumdelta;
+        nv[j] = v[j] + sumdelta;
+      }
+      int st = sample_sigma(nv.data(), nw.data(), sig);
+      if (st) { err = "norm_const2 - hypergeometric diverging with infinity"; return st; }
+      touched.push_back(i);
+    }
+    if ((int)touched.size() == K) upload_clusters();
+    else upload_some(touched);
+    auto t2 = std::chrono::steady_clock::now();
+    stats.t_stats_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
+    stats.t_host_phi_ms += std::chrono::duration<double, std::milli>(t2 - t1).count();
+    return kOk;
+  }
+
+  // ------------------------------------------------------------------ loglik
+  int compute_loglikelihood(double* out) {
+    if (!have_state) { err = "no state"; return kArg; }
+    if (tables_dirty) upload_clusters();
+    HIPCHK(hipEventRecord(ev[3], stream));
+    const int nb = (n + kBlock - 1) / kBlock;
+    d_partial.ensure((size_t)2 * nb);
+    LoglikArgs la;
+    la.codes_t = d_codes_t.p; la.n = n; la.d = d; la.nq = nq; la.label = d_c.p;
+    la.cl = ParamTables{d_slot_codes.p, d_slot_tab.p};
+    la.partial = d_partial.p;
+    HIPCHK(launch_loglik(la, stream));
+    h_partial.resize((size_t)2 * nb);
+    HIPCHK(hipMemcpyAsync(h_partial.data(), d_partial.p, h_partial.size() * 8, hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipEventRecord(ev[4], stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    float t = 0;
+    HIPCHK(hipEventElapsedTime(&t, ev[3], ev[4]));
+    stats.t_loglik_ms += t;
+    double hi = 0.0, lo = 0.0;
+    for (int b = 0; b < nb; ++b) {
+      const double a = h_partial[2 * b];
+      const double s = hi + a, bb = s - hi;
+      lo += (hi - (s - bb)) + (a - bb) + h_partial[2 * b + 1];
+      hi = s;
+    }
+    *out = hi + lo;
+    return kOk;
+  }
+
+  int loglik_matrix(double* L, int32_t* H) {
+    if (!have_state) { err = "no state"; return kArg; }
+    if (tables_dirty) upload_clusters();
+    DevBuf<double> dl;
+    DevBuf<int> dh;
+    dl.ensure((size_t)K * n);
+    dh.ensure((size_t)K * n);
+    HIPCHK(launch_lmatrix(d_codes_t.p, n, d, nq, ParamTables{d_slot_codes.p, d_slot_tab.p}, K, dl.p, dh.p, n,
+                          stream));
+    std::vector<double> tl((size_t)K * n);
+    std::vector<int> th((size_t)K * n);
+    HIPCHK(hipMemcpyAsync(tl.data(), dl.p, tl.size() * 8, hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipMemcpyAsync(th.data(), dh.p, th.size() * 4, hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    for (int i = 0; i < n; ++i)
+      for (int k = 0; k < K; ++k) {
+        if (L) L[(size_t)i * K + k] = tl[(size_t)k * n + i];
+        if (H) H[(size_t)i * K + k] = th[(size_t)k * n + i];
+      }
+    return kOk;
+  }
+
+  // ------------------------------------------------------------------ chain driver
+  int run_markov_chain(const hdpm_chain_params* p, const int32_t* c_init, int32_t* o_tot, int32_t* o_c,
+                       double* o_ll, int32_t* o_acc, int32_t* o_final, double* o_time);
+  int split_and_merge(int t, int r, int idx_1_sm, int* accepted);
+  int init_chain(const hdpm_chain_params* p, const int32_t* c_init);
+  int iteration(const hdpm_chain_params* p, int iter, int* idx_1_sm, int* accepted, double* ll);
+};
+
+}  // namespace hdpm
+
+#include "split_merge.inl"
+
+namespace hdpm {
+
+// la:27-77
+int Ctx::init_chain(const hdpm_chain_params* p, const int32_t* c_init) {
+  if (!n) { err = "set_data first"; return kArg; }
+  K = p->L;
+  h_c.resize(n);
+  if (c_init) {
+    int mn = c_init[0];
+    for (int i = 1; i < n; ++i) mn = std::min(mn, (int)c_init[i]);
+    for (int i = 0; i < n; ++i) h_c[i] = c_init[i] - mn;
+    int mx = *std::max_element(h_c.begin(), h_c.end());
+    std::vector<char> seen(mx + 1, 0);
+    int u = 0;
+    for (int i = 0; i < n; ++i) if (!seen[h_c[i]]) { seen[h_c[i]] = 1; u++; }
+    K = u;
+    if (mx >= K) { err = "initial labels must be contiguous after subtracting the minimum"; return kArg; }
+  } else {
+    if (p->L <= 0) { err = "L must be positive for a random initial assignment"; return kArg; }
+    for (int i = 0; i < n; ++i) h_c[i] = (int)(p->L * rng.unif() + 1) - 1;
+  }
+  // la:46-48: all centers, then all sigmas
+  h_center.assign((size_t)K * d, 0);
+  h_sigma.assign((size_t)K * d, 0.0);
+  for (int k = 0; k < K; ++k) sample_center_uniform(&h_center[(size_t)k * d]);
+  for (int k = 0; k < K; ++k) {
+    int st = sample_sigma(v.data(), w.data(), &h_sigma[(size_t)k * d]);
+    if (st) { err = "rhig failed"; return st; }
+  }
+  recount();
+  upload_labels();
+  upload_clusters();
+  have_state = true;
+  int st = update_phi(nullptr, 0);  // la:51
+  if (st) return st;
+  return generate_pool((int64_t)n * p->m * p->thinning);  // la:67-77
+}
+
+// la:85-132, one iteration
+int Ctx::iteration(const hdpm_chain_params* p, int iter, int* idx_1_sm, int* accepted, double* ll) {
+  int st;
+  *accepted = 0;
+  if (p->neal8 && iter % p->n8_step_size == 0) {       // la:94-103
+    st = neal8_sweep(p->m);
+    if (st) return st;
+    st = update_phi(nullptr, 0);
+    if (st) return st;
+  }
+  if (p->split_merge && iter % p->sam_step_size == 0) {  // la:111-115
+    st = split_and_merge(p->t, p->r, *idx_1_sm, accepted);
+    if (st) return st;
+    *idx_1_sm = (*idx_1_sm + 1) % n;
+  }
+  if (iter % 1000 == 0) {                                // la:123-129
+    st = generate_pool((int64_t)n * p->m * p->thinning);
+    if (st) return st;
+  }
+  return compute_loglikelihood(ll);                      // la:132
+}
+
+// la:6-174
+int Ctx::run_markov_chain(const hdpm_chain_params* p, const int32_t* c_init, int32_t* o_tot, int32_t* o_c,
+                          double* o_ll, int32_t* o_acc, int32_t* o_final, double* o_time) {
+  int st = init_chain(p, c_init);
+  if (st) return st;
+  auto t0 = std::chrono::steady_clock::now();
+  int idx_1_sm = 0;
+  const int total = (p->iterations + p->burnin) * p->thinning;
+  for (int iter = 0; iter < total; ++iter) {
+    int accepted = 0;
+    double ll = 0.0;
+    st = iteration(p, iter, &idx_1_sm, &accepted, &ll);
+    if (st) return st;
+    if (iter >= p->thinning * p->burnin && iter % p->thinning == 0) {   // la:140-153
+      const int at = iter / p->thinning - p->burnin;
+      if (o_tot) o_tot[at] = K;
+      if (o_c) {
+        download_labels();
+        std::memcpy(o_c + (size_t)at * n, h_c.data(), (size_t)n * 4);
+      }
+      if (o_ll) o_ll[at] = ll;
+      if (o_acc) o_acc[at] = accepted;
+    }
+  }
+  if (o_final) {
+    download_labels();
+    std::memcpy(o_final, h_c.data(), (size_t)n * 4);
+  }
+  if (o_time) o_time[0] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return kOk;
+}
+
+}  // namespace hdpm
+
+// ====================================================================== C ABI
+using hdpm::Ctx;
+
+#define GUARD(body)                                                            \
+  try {                                                                        \
+    body                                                                       \
+  } catch (const hdpm::HipError& he) {                                         \
+    ctx->err = std::string("HIP error: ") + hipGetErrorString(he.e) + " at " + he.what; \
+    return HDPM_E_DEVICE;                                                      \
+  } catch (const std::bad_alloc&) {                                            \
+    ctx->err = "host allocation failed";                                       \
+    return HDPM_E_ARG;                                                         \
+  } catch (...) {                                                              \
+    ctx->err = "unknown exception";                                            \
+    return HDPM_E_ARG;                                                         \
+  }
+
+extern "C" {
+
+int hdpm_device_count(void) {
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) return 0;
+  return c;
+}
+
+int hdpm_ctx_create(int32_t device, hdpm_ctx** out) {
+  if (!out) return HDPM_E_ARG;
+  *out = nullptr;
+  int cnt = 0;
+  if (hipGetDeviceCount(&cnt) != hipSuccess || cnt <= device || device < 0) return HDPM_E_NODEVICE;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return HDPM_E_NODEVICE;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return HDPM_E_NODEVICE;
+  auto* c = new (std::nothrow) Ctx();
+  if (!c) return HDPM_E_ARG;
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return HDPM_E_DEVICE;
+  }
+  for (auto& e : c->ev) (void)hipEventCreate(&e);
+  c->rng.set_seed(0);
+  *out = reinterpret_cast<hdpm_ctx*>(c);
+  return HDPM_OK;
+}
+
+void hdpm_ctx_destroy(hdpm_ctx* h) {
+  auto* c = reinterpret_cast<Ctx*>(h);
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  delete c;
+}
+
+const char* hdpm_last_error(const hdpm_ctx* h) {
+  auto* c = reinterpret_cast<const Ctx*>(h);
+  return c ? c->err.c_str() : "null context";
+}
+
+#define CTX()                                   \
+  auto* ctx = reinterpret_cast<Ctx*>(h);        \
+  if (!ctx) return HDPM_E_ARG;                  \
+  (void)hipSetDevice(ctx->device);              \
+  ctx->err.clear();
+
+int hdpm_set_data(hdpm_ctx* h, const uint8_t* codes, int32_t n, int32_t d, const int32_t* attrisize, double gamma,
+                  const double* v, const double* w) {
+  CTX();
+  if (!codes || !attrisize || !v || !w) return HDPM_E_ARG;
+  GUARD(return ctx->set_data(codes, n, d, attrisize, gamma, v, w);)
+}
+
+int hdpm_rng_set_seed(hdpm_ctx* h, uint32_t seed) {
+  CTX();
+  ctx->rng.set_seed(seed);
+  return HDPM_OK;
+}
+int hdpm_rng_set_state(hdpm_ctx* h, const int32_t* s) {
+  CTX();
+  if (!s) return HDPM_E_ARG;
+  ctx->rng.import625(s);
+  return HDPM_OK;
+}
+int hdpm_rng_get_state(const hdpm_ctx* h, int32_t* s) {
+  auto* ctx = reinterpret_cast<const Ctx*>(h);
+  if (!ctx || !s) return HDPM_E_ARG;
+  ctx->rng.export625(s);
+  return HDPM_OK;
+}
+
+int hdpm_set_state(hdpm_ctx* h, const int32_t* c_i, int32_t K, const double* centers, const double* sigma) {
+  CTX();
+  if (!c_i || (K > 0 && (!centers || !sigma))) return HDPM_E_ARG;
+  GUARD(return ctx->set_state(c_i, K, centers, sigma);)
+}
+int hdpm_get_state(hdpm_ctx* h, int32_t* c_i, int32_t* K, double* centers, double* sigma, int32_t cap) {
+  CTX();
+  GUARD(return ctx->get_state(c_i, K, centers, sigma, cap);)
+}
+int hdpm_set_pool(hdpm_ctx* h, const double* centers, const double* sigma, int64_t P) {
+  CTX();
+  if (!centers || !sigma) return HDPM_E_ARG;
+  GUARD(return ctx->set_pool(centers, sigma, P);)
+}
+int hdpm_get_pool(hdpm_ctx* h, double* centers, double* sigma, int64_t P) {
+  CTX();
+  if (P != ctx->P) { ctx->err = "pool size mismatch"; return HDPM_E_ARG; }
+  for (size_t q = 0; q < (size_t)P * ctx->d; ++q) {
+    if (centers) centers[q] = ctx->h_pool_c[q];
+    if (sigma) sigma[q] = ctx->h_pool_s[q];
+  }
+  return HDPM_OK;
+}
+int hdpm_generate_pool(hdpm_ctx* h, int64_t P) {
+  CTX();
+  GUARD(return ctx->generate_pool(P);)
+}
+int hdpm_neal8_sweep(hdpm_ctx* h, int32_t m) {
+  CTX();
+  GUARD(return ctx->neal8_sweep(m);)
+}
+int hdpm_update_phi(hdpm_ctx* h, const int32_t* idx, int32_t n_idx) {
+  CTX();
+  if (n_idx > 0 && !idx) return HDPM_E_ARG;
+  GUARD(return ctx->update_phi(idx, n_idx);)
+}
+int hdpm_compute_loglikelihood(hdpm_ctx* h, double* out) {
+  CTX();
+  if (!out) return HDPM_E_ARG;
+  GUARD(return ctx->compute_loglikelihood(out);)
+}
+int hdpm_loglik_matrix(hdpm_ctx* h, double* L, int32_t* H) {
+  CTX();
+  GUARD(return ctx->loglik_matrix(L, H);)
+}
+int hdpm_restricted_gibbs(hdpm_ctx* h, const int32_t* S, int32_t nS, int32_t i1, int32_t i2, int32_t t) {
+  CTX();
+  GUARD(return hdpm::sm_restricted_gibbs_device(ctx, S, nS, i1, i2, t);)
+}
+int hdpm_logprobgs_c_i(hdpm_ctx* h, const int32_t* g_c_i, const int32_t* S, int32_t nS, int32_t i1, int32_t i2,
+                       double* out) {
+  CTX();
+  GUARD(return hdpm::sm_logprobgs_c_i_api(ctx, g_c_i, S, nS, i1, i2, out);)
+}
+int hdpm_split_and_merge(hdpm_ctx* h, int32_t t, int32_t r, int32_t idx_1_sm, int32_t* accepted) {
+  CTX();
+  int acc = 0;
+  int st;
+  GUARD(st = ctx->split_and_merge(t, r, idx_1_sm, &acc);)
+  if (accepted) *accepted = acc;
+  return st;
+}
+int hdpm_run_markov_chain(hdpm_ctx* h, const hdpm_chain_params* p, const int32_t* c_i_init, int32_t* out_total_cls,
+                          int32_t* out_c_i, double* out_loglik, int32_t* out_accepted, int32_t* final_ass,
+                          double* out_time_s) {
+  CTX();
+  if (!p) return HDPM_E_ARG;
+  GUARD(return ctx->run_markov_chain(p, c_i_init, out_total_cls, out_c_i, out_loglik, out_accepted, final_ass,
+                                     out_time_s);)
+}
+int hdpm_init_chain(hdpm_ctx* h, const hdpm_chain_params* p, const int32_t* c_i_init) {
+  CTX();
+  if (!p) return HDPM_E_ARG;
+  GUARD(return ctx->init_chain(p, c_i_init);)
+}
+int hdpm_iteration(hdpm_ctx* h, const hdpm_chain_params* p, int32_t iter, int32_t* idx_1_sm, int32_t* accepted,
+                   double* loglik) {
+  CTX();
+  if (!p || !idx_1_sm) return HDPM_E_ARG;
+  int acc = 0;
+  double ll = 0.0;
+  int st;
+  GUARD(st = ctx->iteration(p, iter, idx_1_sm, &acc, &ll);)
+  if (accepted) *accepted = acc;
+  if (loglik) *loglik = ll;
+  return st;
+}
+int hdpm_get_stats(const hdpm_ctx* h, hdpm_stats* out) {
+  auto* ctx = reinterpret_cast<const Ctx*>(h);
+  if (!ctx || !out) return HDPM_E_ARG;
+  *out = ctx->stats;
+  return HDPM_OK;
+}
+int hdpm_reset_stats(hdpm_ctx* h) {
+  CTX();
+  ctx->stats = hdpm_stats{};
+  return HDPM_OK;
+}
+int hdpm_set_debug(hdpm_ctx* h, int32_t mode) {
+  CTX();
+  ctx->debug = mode;
+  return HDPM_OK;
+}
+int hdpm_synchronize(hdpm_ctx* h) {
+  CTX();
+  return hipStreamSynchronize(ctx->stream) == hipSuccess ? HDPM_OK : HDPM_E_DEVICE;
+}
+
+}  // extern "C"

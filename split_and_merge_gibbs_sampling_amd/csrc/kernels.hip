@@ -1,0 +1,806 @@
+// kernels.hip -- gfx950 kernels of the hdpm Neal-8 sweep.
+//
+// Hot path (BASELINE north_star):
+//   k_prepass   N x (K+m) Hamming log-likelihood matrix (exact, reference summation
+//               order, code/neal8.cpp:40-92) + per-point certainty classification.
+//   k_resolve   the sequential reassignment (n8:95-159) for the points whose draw is
+//               not already decided, in index order, with exact R/Rcpp draw semantics.
+//   k_relabel / k_hist / k_loglik   sufficient statistics for update_phi
+//               (cf:535-590) and compute_loglikelihood (cf:379-401).
+//
+// Bit-exactness: every per-attribute dhamming value comes from host tables computed
+// with glibc in the reference expression; the device only selects and adds them in
+// j order (built with -ffp-contract=off), so each log-likelihood is bit-identical to
+// the reference's.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+
+#include "kernels.hpp"
+
+namespace hdpm {
+
+__device__ __forceinline__ double raw_to_unif(uint32_t y) {
+  const double i2_32m1 = 2.328306437080797e-10;
+  double x = (double)y * 2.3283064365386963e-10;
+  if (x <= 0.0) return 0.5 * i2_32m1;
+  if ((1.0 - x) <= 0.0) return 1.0 - 0.5 * i2_32m1;
+  return x;
+}
+
+// sample(P, 1, FALSE)[0] - 1 with one uniform (Rcpp EmpiricalSample, n8:66).
+__device__ __forceinline__ int64_t pick_entry(uint32_t y, int64_t P) {
+  return (int64_t)((int)((double)(int)P * raw_to_unif(y) + 1)) - 1;
+}
+
+__device__ __forceinline__ bool byte_differs(const uint4& dx, int b) {
+  const uint32_t w = b < 4 ? dx.x : b < 8 ? dx.y : b < 12 ? dx.z : dx.w;
+  return ((w >> ((b & 3) * 8)) & 0xffu) != 0u;
+}
+
+// Register-staged codes of one point (NQR chunks of 16 bytes); NQR == 0 -> reload.
+template <int NQR>
+struct PointCodes {
+  uint4 r[NQR > 0 ? NQR : 1];
+  const uint8_t* base;
+  int64_t i;
+  int nq;
+  __device__ __forceinline__ void load(const uint8_t* codes_t, int64_t i_, int nq_) {
+    base = codes_t; i = i_; nq = nq_;
+    if constexpr (NQR > 0) {
+#pragma unroll
+      for (int q = 0; q < NQR; ++q) r[q] = *(const uint4*)(codes_t + tiled_offset(i, q * 16, nq));
+    }
+  }
+  __device__ __forceinline__ uint4 chunk(int q) const {
+    if constexpr (NQR > 0) return r[q];
+    else return *(const uint4*)(base + tiled_offset(i, q * 16, nq));
+  }
+};
+
+// Exact log-likelihood of the point against a wave-uniform table (existing cluster).
+template <int NQR>
+__device__ __forceinline__ double ll_uniform(const PointCodes<NQR>& x, int d, const uint8_t* __restrict__ cc,
+                                             const double* __restrict__ tab) {
+  double ll = 0.0;
+  auto body = [&](int q) {
+    const uint4 xq = x.chunk(q);
+    const uint4 cq = *(const uint4*)(cc + q * 16);
+    const uint4 dx = make_uint4(xq.x ^ cq.x, xq.y ^ cq.y, xq.z ^ cq.z, xq.w ^ cq.w);
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      const int j = q * 16 + b;
+      if (j < d) {
+        const double ta = tab[2 * j], tb = tab[2 * j + 1];
+        ll += byte_differs(dx, b) ? tb : ta;
+      }
+    }
+  };
+  if constexpr (NQR > 0) {
+#pragma unroll
+    for (int q = 0; q < NQR; ++q) body(q);
+  } else {
+    for (int q = 0; q < x.nq; ++q) body(q);
+  }
+  return ll;
+}
+
+// Exact log-likelihood against a per-lane table (latent pool entry): only the selected
+// half of each (match, mismatch) pair is fetched.
+template <int NQR>
+__device__ __forceinline__ double ll_lane(const PointCodes<NQR>& x, int d, const uint8_t* cc,
+                                          const double* tab, int* hamming) {
+  double ll = 0.0;
+  int h = 0;
+  auto body = [&](int q) {
+    const uint4 xq = x.chunk(q);
+    const uint4 cq = *(const uint4*)(cc + q * 16);
+    const uint4 dx = make_uint4(xq.x ^ cq.x, xq.y ^ cq.y, xq.z ^ cq.z, xq.w ^ cq.w);
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      const int j = q * 16 + b;
+      if (j < d) {
+        const int mis = byte_differs(dx, b) ? 1 : 0;
+        h += mis;
+        ll += tab[2 * j + mis];
+      }
+    }
+  };
+  if constexpr (NQR > 0) {
+#pragma unroll
+    for (int q = 0; q < NQR; ++q) body(q);
+  } else {
+    for (int q = 0; q < x.nq; ++q) body(q);
+  }
+  if (hamming) *hamming = h;
+  return ll;
+}
+
+// ------------------------------------------------------------------ prepass
+template <int NQR>
+__global__ __launch_bounds__(kBlock) void k_prepass(PrepassArgs a) {
+  const int tid = threadIdx.x;
+  const int64_t i = (int64_t)a.p0 + (int64_t)blockIdx.x * kBlock + tid;
+  const bool active = i < a.n;
+  const int64_t ii = active ? i : (int64_t)a.n - 1;
+  const int dp = a.nq * 16;
+  PointCodes<NQR> x;
+  x.load(a.codes_t, ii, a.nq);
+  const int own = a.c[ii];
+  const int own_cnt = a.counts[own];
+  double max1 = -INFINITY, max2 = -INFINITY;
+  int dom = -1;
+  for (int l = 0; l < a.K; ++l) {
+    const int s = a.slot_of_label[l];
+    const double ll = ll_uniform<NQR>(x, a.d, a.slots.codes + (int64_t)s * dp,
+                                      a.slots.tab + (int64_t)s * 2 * a.d);
+    if (active) a.L[(int64_t)s * a.ldL + i] = ll;
+    const int nz = a.counts[s] - (s == own ? 1 : 0);
+    const double v = nz != 0 ? a.logn[nz] + ll : -INFINITY;
+    if (v > max1) { max2 = max1; max1 = v; dom = s; }
+    else if (v > max2) { max2 = v; }
+  }
+  const uint32_t* raw = a.raw + ii * (a.m + 1);
+  for (int l = 0; l < a.m; ++l) {
+    const int64_t e = pick_entry(raw[l], a.P);
+    const double ll = ll_lane<NQR>(x, a.d, a.pool.codes + e * dp, a.pool.tab + e * 2 * a.d, nullptr);
+    if (active) a.L[(int64_t)(a.S + l) * a.ldL + i] = ll;
+    const double v = a.logfac + ll;
+    if (v > max1) { max2 = max1; max1 = v; dom = -2 - l; }
+    else if (v > max2) { max2 = v; }
+  }
+  const bool domown = own_cnt >= 2 && dom == own;
+  const double mg = domown ? max1 - max2 : -INFINITY;
+  const bool uncertain = active && !(domown && mg > a.thresh);
+  if (active) a.margin[i] = mg;
+
+  __shared__ int s_wcnt[kBlock / kWave];
+  const int lane = tid & 63, wv = tid >> 6;
+  const unsigned long long bal = __ballot(uncertain);
+  const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+  if (lane == 0) s_wcnt[wv] = __popcll(bal);
+  __syncthreads();
+  int off = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kBlock / kWave; ++w) {
+    off += w < wv ? s_wcnt[w] : 0;
+    tot += s_wcnt[w];
+  }
+  if (uncertain) a.list[(int64_t)blockIdx.x * kBlock + off + pre] = (int)i;
+  if (tid == 0) a.cnt[blockIdx.x] = tot;
+}
+
+// ------------------------------------------------------------------ resolver
+// One wave walks the sweep in index order.  State (counts, label<->slot maps) lives in
+// LDS; L rows, margins and the uncertain lists come from the prepass.
+struct RShared {
+  int K, nslots, status, next, restart, moves, exact, checked, pick, src, pad0, pad1;
+  double dnow, sum;
+};
+
+struct RState {
+  RShared* sh;
+  int* cnt;     // [scap]
+  int* snap;    // [scap]
+  int* sol;     // [scap] slot_of_label
+  int* los;     // [scap] label_of_slot
+  double* val;  // [emax]
+  double* p;    // [emax]
+  int* perm;    // [emax]
+};
+
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+  return v;
+}
+
+__device__ __forceinline__ double slot_drift(const RState& st, const double* logn, int s) {
+  const int a = st.snap[s], b = st.cnt[s];
+  if (a >= 2) {
+    if (b < 2) return INFINITY;
+    return fabs(logn[b - 1] - logn[a - 1]);
+  }
+  if (a == 1) return b == 0 ? 0.0 : logn[b];
+  return INFINITY;
+}
+
+// Serial revsort (R sort.c) on lane 0.
+__device__ void dev_revsort(double* a0, int* ib0, int n) {
+  if (n <= 1) return;
+  double* a = a0 - 1;
+  int* ib = ib0 - 1;
+  int l = (n >> 1) + 1, ir = n, i, j, ii;
+  double ra;
+  for (;;) {
+    if (l > 1) {
+      l = l - 1;
+      ra = a[l];
+      ii = ib[l];
+    } else {
+      ra = a[ir];
+      ii = ib[ir];
+      a[ir] = a[1];
+      ib[ir] = ib[1];
+      if (--ir == 1) {
+        a[1] = ra;
+        ib[1] = ii;
+        return;
+      }
+    }
+    i = l;
+    j = l << 1;
+    while (j <= ir) {
+      if (j < ir && a[j] > a[j + 1]) ++j;
+      if (ra > a[j]) {
+        a[i] = a[j];
+        ib[i] = ib[j];
+        j += (i = j);
+      } else {
+        j = ir + 1;
+      }
+    }
+    a[i] = ra;
+    ib[i] = ii;
+  }
+}
+
+// Exact n8:40-102 decision for point i.  Returns the drawn index in [0, K+m) or -status.
+__device__ int exact_decision(const ResolveArgs& a, const RState& st, int K, int64_t i, int own) {
+  const int lane = threadIdx.x;
+  const int E = K + a.m;
+  const bool singleton = st.cnt[own] == 1;
+  for (int e = lane; e < E; e += kWave) {
+    double v;
+    if (e < K) {
+      const int s = st.sol[e];
+      const int nz = st.cnt[s] - (s == own ? 1 : 0);
+      v = nz != 0 ? a.logn[nz] + a.L[(int64_t)s * a.ldL + i] : -INFINITY;
+    } else {
+      const int l = e - K;
+      const double ll = (l == 0 && singleton) ? a.L[(int64_t)own * a.ldL + i]
+                                              : a.L[(int64_t)(a.S + l) * a.ldL + i];
+      v = a.logfac + ll;
+    }
+    st.val[e] = v;
+  }
+  __syncthreads();
+  double mx = -INFINITY;
+  for (int e = lane; e < E; e += kWave) mx = fmax(mx, st.val[e]);
+  mx = wave_max(mx);
+  for (int e = lane; e < E; e += kWave) st.p[e] = exp(st.val[e] - mx);   // n8:95
+  __syncthreads();
+  if (lane == 0) {
+    double sum = 0.0;
+    for (int e = 0; e < E; ++e) sum += st.p[e];
+    st.sh->sum = sum;
+  }
+  __syncthreads();
+  const double sum = st.sh->sum;
+  for (int e = lane; e < E; e += kWave) st.p[e] = st.p[e] / sum;          // n8:96
+  __syncthreads();
+  // Rcpp FixupProb: sum of the positive entries (the same sequential sum), divide.
+  if (lane == 0) {
+    double s2 = 0.0;
+    for (int e = 0; e < E; ++e) if (st.p[e] > 0) s2 += st.p[e];
+    st.sh->sum = s2;
+  }
+  __syncthreads();
+  const double s2 = st.sh->sum;
+  if (!(s2 > 0)) return -3;  // kProb: no positive probability
+  int nc = 0;
+  double pmax = -1.0;
+  int amax = 0x7fffffff;
+  for (int e = lane; e < E; e += kWave) {
+    const double q = st.p[e] / s2;
+    st.p[e] = q;
+    nc += ((double)E * q > 0.1) ? 1 : 0;
+    if (q > pmax) { pmax = q; amax = e; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    nc += __shfl_xor(nc, o);
+    const double om = __shfl_xor(pmax, o);
+    const int oa = __shfl_xor(amax, o);
+    if (om > pmax || (om == pmax && oa < amax)) { pmax = om; amax = oa; }
+  }
+  if (nc > 200) return -4;  // kWalker
+  int ties = 0;
+  for (int e = lane; e < E; e += kWave) ties += (st.p[e] == pmax) ? 1 : 0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ties += __shfl_xor(ties, o);
+  __syncthreads();
+  const double rU = raw_to_unif(a.raw[i * (a.m + 1) + a.m]);
+  // Unique maximum drawn: revsort puts it first, cumsum[0] = pmax.
+  if (ties == 1 && rU <= pmax) return amax;
+  if (lane == 0) {
+    for (int e = 0; e < E; ++e) st.perm[e] = e + 1;
+    dev_revsort(st.p, st.perm, E);
+    for (int e = 1; e < E; ++e) st.p[e] += st.p[e - 1];
+    int j;
+    for (j = 0; j < E - 1; j++)
+      if (rU <= st.p[j]) break;
+    st.sh->pick = st.perm[j] - 1;
+  }
+  __syncthreads();
+  return st.sh->pick;
+}
+
+__device__ void copy_pool_params(const ResolveArgs& a, int64_t e, int s) {
+  const int lane = threadIdx.x;
+  const int dp = a.dp;
+  for (int b = lane; b < dp; b += kWave) a.slot_codes[(int64_t)s * dp + b] = a.pool.codes[e * dp + b];
+  for (int b = lane; b < 2 * a.d; b += kWave) a.slot_tab[(int64_t)s * 2 * a.d + b] = a.pool.tab[e * 2 * a.d + b];
+}
+
+__global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = threadIdx.x;
+  const int scap = a.scap;
+  const int emax = scap + a.m;
+  RState st;
+  st.sh = (RShared*)smem;
+  st.val = (double*)(smem + 64);
+  st.p = st.val + emax;
+  st.cnt = (int*)(st.p + emax);
+  st.snap = st.cnt + scap;
+  st.sol = st.snap + scap;
+  st.los = st.sol + scap;
+  st.perm = st.los + scap;
+  RShared& S = *st.sh;
+  for (int s = lane; s < scap; s += kWave) {
+    const int v = s < a.nslots ? a.counts[s] : 0;
+    st.cnt[s] = v;
+    st.snap[s] = v;
+    st.los[s] = s < a.nslots ? a.label_of_slot[s] : -1;
+    st.sol[s] = s < a.K ? a.slot_of_label[s] : -1;
+  }
+  if (lane == 0) {
+    S.K = a.K; S.nslots = a.nslots; S.status = 0; S.next = a.n; S.restart = 0;
+    S.moves = 0; S.exact = 0; S.checked = 0; S.dnow = 0.0;
+  }
+  __syncthreads();
+
+  // Decide point i exactly and apply n8:107-159.  Returns false to stop the sweep here.
+  auto process = [&](int64_t i) -> bool {
+    const int own = a.c[i];
+    const int K = S.K;
+    const int pick = exact_decision(a, st, K, i, own);
+    if (lane == 0) {
+      S.exact++;
+      if (pick < 0) { S.status = -pick; S.next = (int)i; }
+      else {
+        const int ownlab = st.los[own];
+        if (pick < K) {
+          const int ns = st.sol[pick];
+          if (st.cnt[own] != 1) {                                   // case 1
+            if (ns != own) {
+              a.c[i] = ns; st.cnt[own]--; st.cnt[ns]++; S.moves++;
+              S.dnow = fmax(S.dnow, fmax(slot_drift(st, a.logn, own), slot_drift(st, a.logn, ns)));
+            }
+          } else {                                                  // case 2
+            int target = ns;
+            if (pick == ownlab) {           // the own (-inf) cluster was drawn
+              if (ownlab == K - 1) { S.status = 1; S.next = (int)i; }
+              target = st.sol[K - 1];
+            }
+            if (S.status == 0) {
+              a.c[i] = target; st.cnt[own]--; st.cnt[target]++; S.moves++;
+              const int last = st.sol[K - 1];
+              st.los[own] = -1;
+              if (ownlab != K - 1) { st.sol[ownlab] = last; st.los[last] = ownlab; }
+              st.sol[K - 1] = -1;
+              S.K = K - 1;
+              S.dnow = fmax(S.dnow, fmax(slot_drift(st, a.logn, own), slot_drift(st, a.logn, target)));
+            }
+          }
+        } else {
+          const int l = pick - K;
+          const bool single = st.cnt[own] == 1;
+          if (!single || l != 0) {                                  // case 3 / case 4 (new params)
+            if (S.nslots >= scap) { S.status = 5; S.next = (int)i; }
+            else {
+              const int ns = S.nslots;
+              S.nslots = ns + 1;
+              if (!single) {                                        // case 3
+                st.sol[K] = ns; st.los[ns] = K; S.K = K + 1;
+                st.cnt[own]--;
+              } else {                                              // case 4
+                st.sol[ownlab] = ns; st.los[ns] = ownlab; st.los[own] = -1;
+                st.cnt[own] = 0;
+              }
+              st.cnt[ns] = 1;
+              a.c[i] = ns;
+              S.src = (int)pick_entry(a.raw[i * (a.m + 1) + l], a.P);
+              a.slot_src[ns] = S.src;
+              S.moves++;
+              S.restart = 1;
+              S.next = (int)i + 1;
+            }
+          }
+          // case 4 with latent 0 (the singleton's own parameters): nothing changes.
+        }
+      }
+    }
+    __syncthreads();
+    if (S.restart && S.status == 0) {
+      const int ns = S.nslots - 1;
+      copy_pool_params(a, S.src, ns);
+    }
+    return S.status == 0 && !S.restart;
+  };
+
+  bool go = true;
+  int64_t start_checked = -1;
+  if (!a.force_exact) {
+    // LIST mode: only the prepass's uncertain points need work while drift <= dmax.
+    for (int b = 0; b < a.nblocks && go; ++b) {
+      const int nb = a.cnt[b];
+      for (int q = 0; q < nb && go; ++q) {
+        const int64_t i = a.list[(int64_t)b * kBlock + q];
+        go = process(i);
+        if (go && S.dnow > a.dmax) { start_checked = i + 1; go = false; }
+      }
+    }
+  } else {
+    start_checked = a.p0;
+  }
+  // CHECKED mode: every remaining point is re-tested against the current drift.
+  if (start_checked >= 0 && S.status == 0 && !S.restart) {
+    if (lane == 0) S.checked = 1;
+    for (int64_t base = start_checked; base < a.n; base += kWave) {
+      const int64_t i = base + lane;
+      bool unc = false;
+      if (i < a.n) {
+        const double mg = a.margin[i];
+        unc = a.force_exact || !(mg - 2.0 * S.dnow > a.T && st.cnt[a.c[i]] >= 2);
+      }
+      unsigned long long bal = __ballot(unc);
+      bool stop = false;
+      while (bal) {
+        const int q = __ffsll((long long)bal) - 1;
+        if (!process(base + q)) { stop = true; break; }
+        // drift may have grown: re-test the remaining lanes
+        bool u2 = false;
+        if (lane > q && i < a.n) {
+          const double mg = a.margin[i];
+          u2 = a.force_exact || !(mg - 2.0 * S.dnow > a.T && st.cnt[a.c[i]] >= 2);
+        }
+        bal = __ballot(u2);
+      }
+      if (stop) break;
+    }
+  }
+  __syncthreads();
+  // write back
+  for (int s = lane; s < scap; s += kWave) {
+    if (s < S.nslots) { a.counts[s] = st.cnt[s]; a.label_of_slot[s] = st.los[s]; }
+    if (s < S.K) a.slot_of_label[s] = st.sol[s];
+  }
+  if (lane == 0) {
+    ResolveCtl c;
+    c.next = S.next; c.status = S.status; c.restart = S.restart; c.K = S.K; c.nslots = S.nslots;
+    c.moves = S.moves; c.exact = S.exact; c.checked = S.checked;
+    *a.ctl = c;
+  }
+}
+
+// ------------------------------------------------------------------ end of sweep
+__global__ void k_relabel(int* c, const int* label_of_slot, int n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) c[i] = label_of_slot[c[i]];
+}
+
+// freq[k][j][level-1] = #{i : label_i = k, x_ij = level}.  Each thread owns attribute
+// columns, so the LDS counters need no atomics; one flush of atomics per block.
+template <typename CT>
+__global__ __launch_bounds__(kBlock) void k_hist_lds(HistArgs a, int points_per_block) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  CT* h = (CT*)smem;
+  const int tid = threadIdx.x;
+  const int nent = a.K * a.d * a.mmax;
+  for (int e = tid; e < nent; e += kBlock) h[e] = 0;
+  __syncthreads();
+  const int64_t i0 = (int64_t)blockIdx.x * points_per_block;
+  const int64_t i1 = min((int64_t)a.n, i0 + points_per_block);
+  for (int64_t i = i0; i < i1; ++i) {
+    const int k = a.label[i];
+    if (a.mask && !a.mask[k]) continue;
+    for (int j = tid; j < a.d; j += kBlock) {
+      const int x = a.codes_t[tiled_offset(i, j, a.nq)];
+      CT* slot = h + ((int64_t)k * a.d + j) * a.mmax + (x - 1);
+      *slot = (CT)(*slot + 1);
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < nent; e += kBlock)
+    if (h[e]) atomicAdd(a.freq + e, (unsigned int)h[e]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_hist_global(HistArgs a) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = t / a.nq;
+  const int q = (int)(t % a.nq);
+  if (i >= a.n) return;
+  const int k = a.label[i];
+  if (a.mask && !a.mask[k]) return;
+  for (int b = 0; b < 16; ++b) {
+    const int j = q * 16 + b;
+    if (j >= a.d) break;
+    const int x = a.codes_t[tiled_offset(i, j, a.nq)];
+    atomicAdd(a.freq + ((int64_t)k * a.d + j) * a.mmax + (x - 1), 1u);
+  }
+}
+
+// compute_loglikelihood: exact per-point own-cluster log-likelihood (j order), then a
+// compensated (two-sum) reduction; partial[2*block] = (hi, lo).
+__device__ __forceinline__ void two_sum(double a, double b, double& s, double& e) {
+  s = a + b;
+  const double bb = s - a;
+  e = (a - (s - bb)) + (b - bb);
+}
+
+__global__ __launch_bounds__(kBlock) void k_loglik(LoglikArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  double hi = 0.0, lo = 0.0;
+  if (i < a.n) {
+    const int k = a.label[i];
+    const int dp = a.nq * 16;
+    PointCodes<0> x;
+    x.load(a.codes_t, i, a.nq);
+    hi = ll_lane<0>(x, a.d, a.cl.codes + (int64_t)k * dp, a.cl.tab + (int64_t)k * 2 * a.d, nullptr);
+  }
+  // wave reduction with error terms
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double oh = __shfl_xor(hi, o), ol = __shfl_xor(lo, o);
+    double s, e;
+    two_sum(hi, oh, s, e);
+    hi = s;
+    lo = lo + ol + e;
+  }
+  __shared__ double sh[kBlock / kWave][2];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) { sh[wv][0] = hi; sh[wv][1] = lo; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double H = 0.0, Lo = 0.0;
+    for (int w = 0; w < kBlock / kWave; ++w) {
+      double s, e;
+      two_sum(H, sh[w][0], s, e);
+      H = s;
+      Lo += sh[w][1] + e;
+    }
+    a.partial[2 * blockIdx.x] = H;
+    a.partial[2 * blockIdx.x + 1] = Lo;
+  }
+}
+
+// Test/diagnostic kernel: L[k*ldL + i] and Hamming counts H[k*ldL + i] for K label tables.
+__global__ __launch_bounds__(kBlock) void k_lmatrix(const uint8_t* codes_t, int n, int d, int nq,
+                                                   ParamTables cl, int K, double* L, int* H, int64_t ldL) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const int dp = nq * 16;
+  PointCodes<0> x;
+  x.load(codes_t, i, nq);
+  for (int k = 0; k < K; ++k) {
+    int h;
+    const double ll = ll_lane<0>(x, d, cl.codes + (int64_t)k * dp, cl.tab + (int64_t)k * 2 * d, &h);
+    L[(int64_t)k * ldL + i] = ll;
+    H[(int64_t)k * ldL + i] = h;
+  }
+}
+
+// ------------------------------------------------------------------ launchers
+template <int NQR>
+static hipError_t launch_prepass_t(const PrepassArgs& a, int nblocks, hipStream_t s) {
+  hipLaunchKernelGGL(k_prepass<NQR>, dim3(nblocks), dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_prepass(const PrepassArgs& a, int nblocks, hipStream_t s) {
+  switch (a.nq) {
+    case 1: return launch_prepass_t<1>(a, nblocks, s);
+    case 2: return launch_prepass_t<2>(a, nblocks, s);
+    case 3: return launch_prepass_t<3>(a, nblocks, s);
+    case 4: return launch_prepass_t<4>(a, nblocks, s);
+    case 5: return launch_prepass_t<5>(a, nblocks, s);
+    case 6: return launch_prepass_t<6>(a, nblocks, s);
+    case 7: return launch_prepass_t<7>(a, nblocks, s);
+    case 8: return launch_prepass_t<8>(a, nblocks, s);
+    default: return launch_prepass_t<0>(a, nblocks, s);
+  }
+}
+
+size_t resolve_smem_bytes(int scap, int m) {
+  const size_t emax = (size_t)scap + (size_t)m;
+  return 64 + emax * 2 * sizeof(double) + (size_t)scap * 4 * sizeof(int) + emax * sizeof(int);
+}
+
+hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_resolve, dim3(1), dim3(kWave), resolve_smem_bytes(a.scap, a.m), s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_relabel(int* c, const int* los, int n, hipStream_t s) {
+  hipLaunchKernelGGL(k_relabel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, c, los, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_hist(const HistArgs& a, hipStream_t s) {
+  const int64_t nent = (int64_t)a.K * a.d * a.mmax;
+  const int ppb = 2048;
+  const int nb = (a.n + ppb - 1) / ppb;
+  if (nent * 4 <= 96 * 1024) {
+    hipLaunchKernelGGL(k_hist_lds<unsigned int>, dim3(nb), dim3(kBlock), nent * 4, s, a, ppb);
+  } else if (nent * 2 <= 150 * 1024) {
+    hipLaunchKernelGGL(k_hist_lds<unsigned short>, dim3(nb), dim3(kBlock), ((nent * 2 + 15) / 16) * 16, s, a, ppb);
+  } else {
+    const int64_t nt = (int64_t)a.n * a.nq;
+    hipLaunchKernelGGL(k_hist_global, dim3((nt + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_loglik(const LoglikArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_loglik, dim3((a.n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_lmatrix(const uint8_t* codes_t, int n, int d, int nq, ParamTables cl, int K, double* L,
+                          int* H, int64_t ldL, hipStream_t s) {
+  hipLaunchKernelGGL(k_lmatrix, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, codes_t, n, d, nq, cl,
+                     K, L, H, ldL);
+  return hipGetLastError();
+}
+
+}  // namespace hdpm
+
+namespace hdpm {
+
+// ------------------------------------------------------------------ split-merge
+__global__ __launch_bounds__(kBlock) void k_sm_ll(SmArgs a) {
+  const int q = blockIdx.x * kBlock + threadIdx.x;
+  if (q >= a.nS) return;
+  const int64_t i = a.S[q];
+  const int dp = a.nq * 16;
+  PointCodes<0> x;
+  x.load(a.codes_t, i, a.nq);
+  a.ll[q] = ll_uniform<0>(x, a.d, a.two.codes, a.two.tab);
+  a.ll[a.nS + q] = ll_uniform<0>(x, a.d, a.two.codes + dp, a.two.tab + 2 * a.d);
+}
+
+// Exact sm:204-215 two-way draw.  probs[k] = log(n_k) + H_k; normalise; FixupProb;
+// revsort of two entries (ties: second first); cumulative compare.
+__device__ __forceinline__ int two_way_draw(double v0, double v1, double rU) {
+  const double mx = fmax(v0, v1);
+  double p0 = exp(v0 - mx), p1 = exp(v1 - mx);
+  double sum = 0.0;
+  sum += p0;
+  sum += p1;
+  p0 = p0 / sum;
+  p1 = p1 / sum;
+  double s2 = 0.0;
+  if (p0 > 0) s2 += p0;
+  if (p1 > 0) s2 += p1;
+  p0 = p0 / s2;
+  p1 = p1 / s2;
+  // revsort(n = 2): descending, equal -> index 2 first
+  const bool first0 = p0 > p1;
+  const double a0 = first0 ? p0 : p1;
+  return (rU <= a0) ? (first0 ? 0 : 1) : (first0 ? 1 : 0);
+}
+
+// One wave walks S in order.  A point whose two log-weights differ by more than T + 2*ln2
+// is decided without the exact path (its smaller weight cannot change any rounding),
+// so each batch of 64 only serialises on its uncertain points.
+__global__ __launch_bounds__(kWave) void k_sm_scan(SmArgs a, double T) {
+  const int lane = threadIdx.x;
+  int n1 = a.n1, n2 = a.n2;
+  for (int base = 0; base < a.nS; base += kWave) {
+    const int q = base + lane;
+    const bool act = q < a.nS;
+    int cur = act ? a.side[q] : 0;
+    const double l0 = act ? a.ll[q] : 0.0, l1 = act ? a.ll[a.nS + q] : 0.0;
+    const double rU = act ? raw_to_unif(a.raw[q]) : 0.0;
+    // certainty at batch-start counts; <= 64 moves in a batch change log n by < ln 2
+    // as long as both clusters keep >= 128 points
+    bool certain = false;
+    int choice = cur;
+    if (act && n1 >= 130 && n2 >= 130) {
+      const double v0 = a.logn[n1 - (cur == 0)] + l0, v1 = a.logn[n2 - (cur == 1)] + l1;
+      if (fabs(v0 - v1) > T + 2.0 * M_LN2) { certain = true; choice = v0 > v1 ? 0 : 1; }
+    }
+    unsigned long long unc = __ballot(act && !certain);
+    unsigned long long mv01 = __ballot(act && certain && cur == 0 && choice == 1);
+    unsigned long long mv10 = __ballot(act && certain && cur == 1 && choice == 0);
+    // walk uncertain lanes in order; counts at lane q = batch start + moves of lanes < q
+    int d1 = 0, d2 = 0;   // count deltas from uncertain lanes processed so far
+    int done_mask_lo = 0;
+    while (unc) {
+      const int u = __ffsll((long long)unc) - 1;
+      const unsigned long long below = (u == 0) ? 0ull : ((1ull << u) - 1ull);
+      const int c01 = __popcll(mv01 & below), c10 = __popcll(mv10 & below);
+      const int cn1 = n1 + d1 - c01 + c10, cn2 = n2 + d2 + c01 - c10;
+      int pick = 0;
+      if (lane == u) {
+        const int nz1 = cn1 - (cur == 0), nz2 = cn2 - (cur == 1);
+        const double v0 = a.logn[nz1] + l0, v1 = a.logn[nz2] + l1;
+        pick = two_way_draw(v0, v1, rU);
+        choice = pick;
+      }
+      pick = __shfl(pick, u);
+      const int cu = __shfl(cur, u);
+      if (cu == 0 && pick == 1) { d1--; d2++; }
+      if (cu == 1 && pick == 0) { d1++; d2--; }
+      unc &= ~(1ull << u);
+      (void)done_mask_lo;
+    }
+    n1 += d1 - __popcll(mv01) + __popcll(mv10);
+    n2 += d2 + __popcll(mv01) - __popcll(mv10);
+    if (act) a.side[q] = choice;
+  }
+  if (lane == 0) { a.out_counts[0] = n1; a.out_counts[1] = n2; }
+}
+
+// logprobgs_c_i terms: log(probs[current side]) with fixed launch sizes; compensated
+// per-block sums (hi, lo).
+__global__ __launch_bounds__(kBlock) void k_sm_lpgs(SmArgs a) {
+  const int q = blockIdx.x * kBlock + threadIdx.x;
+  double hi = 0.0, lo = 0.0;
+  if (q < a.nS) {
+    const int g = a.side_ref[q];
+    const double v0 = a.logn[a.n1 - (g == 0)] + a.ll[q];
+    const double v1 = a.logn[a.n2 - (g == 1)] + a.ll[a.nS + q];
+    const double mx = fmax(v0, v1);
+    double p0 = exp(v0 - mx), p1 = exp(v1 - mx);
+    double sum = 0.0;
+    sum += p0;
+    sum += p1;
+    p0 = p0 / sum;
+    p1 = p1 / sum;
+    hi = log(a.side[q] == 0 ? p0 : p1);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double oh = __shfl_xor(hi, o), ol = __shfl_xor(lo, o);
+    double s, e;
+    two_sum(hi, oh, s, e);
+    hi = s;
+    lo = lo + ol + e;
+  }
+  __shared__ double sh[kBlock / kWave][2];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) { sh[wv][0] = hi; sh[wv][1] = lo; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double H = 0.0, Lo = 0.0;
+    for (int w = 0; w < kBlock / kWave; ++w) {
+      double s, e;
+      two_sum(H, sh[w][0], s, e);
+      H = s;
+      Lo += sh[w][1] + e;
+    }
+    a.out[2 * blockIdx.x] = H;
+    a.out[2 * blockIdx.x + 1] = Lo;
+  }
+}
+
+hipError_t launch_sm_ll(const SmArgs& a, hipStream_t s) {
+  if (a.nS == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sm_ll, dim3((a.nS + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_sm_scan(const SmArgs& a, double T, hipStream_t s) {
+  hipLaunchKernelGGL(k_sm_scan, dim3(1), dim3(kWave), 0, s, a, T);
+  return hipGetLastError();
+}
+hipError_t launch_sm_lpgs(const SmArgs& a, hipStream_t s) {
+  if (a.nS == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sm_lpgs, dim3((a.nS + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace hdpm

@@ -1,0 +1,129 @@
+// kernels.hpp -- argument blocks shared by the host runtime and the gfx950 kernels.
+#pragma once
+#include <cstdint>
+
+namespace hdpm {
+
+constexpr int kBlock = 256;        // prepass points per workgroup (4 waves)
+constexpr int kWave = 64;
+
+// Byte-packed categorical rows, tiled for coalesced 16-B-per-lane loads:
+//   byte (i, j) lives at ((i/64 * nq + j/16) * 64 + i%64) * 16 + j%16
+// so one wave reading chunk q of its 64 points touches 1 KiB contiguous.
+__host__ __device__ inline int64_t tiled_offset(int64_t i, int j, int nq) {
+  return (((i >> 6) * nq + (j >> 4)) * 64 + (i & 63)) * 16 + (j & 15);
+}
+
+// Per-entry parameter tables: codes[e][dp] (dp = 16*nq, zero padded) and
+// tab[e][d][2] = {dhamming on match, dhamming on mismatch} (host glibc values).
+struct ParamTables {
+  const uint8_t* codes;
+  const double* tab;
+};
+
+struct PrepassArgs {
+  const uint8_t* codes_t;
+  int n, d, nq;
+  const int* c;              // slot of each point
+  const int* counts;         // points per slot (current)
+  const int* slot_of_label;  // K entries
+  int K;
+  int S;                     // slots (columns) at this snapshot
+  ParamTables slots;
+  ParamTables pool;
+  int64_t P;
+  const uint32_t* raw;       // R MT raw outputs, (m+1) per point
+  int m;
+  const double* logn;        // logn[k] = log(k) (glibc), k = 0..n+1
+  double logfac;             // log(gamma / m)
+  double thresh;             // certainty threshold incl. 2 * drift budget
+  double* L;                 // column-major: L[e * ldL + i], e < S + m
+  int64_t ldL;
+  double* margin;            // per point: margin if dominated by own cluster, else -inf
+  int* list;                 // per block: ordered uncertain points
+  int* cnt;                  // per block: number of uncertain points
+  int p0;
+};
+
+// Control block written by the resolver.
+struct ResolveCtl {
+  int next;       // first point not yet decided (n when the sweep is complete)
+  int status;     // 0 ok, else hdpm::Status
+  int restart;    // 1 if stopped to recompute columns after a new slot
+  int K;
+  int nslots;
+  int moves;
+  int exact;      // exact (slow-path) decisions taken
+  int checked;    // 1 if the drift budget was exceeded (checked mode)
+};
+
+struct ResolveArgs {
+  int n, d, dp, m;
+  int64_t P;
+  int* c;
+  int* counts;
+  int* slot_of_label;
+  int* label_of_slot;
+  int* slot_src;             // pool entry a dynamic slot was created from (-1: original)
+  uint8_t* slot_codes;
+  double* slot_tab;
+  ParamTables pool;
+  const uint32_t* raw;
+  const double* logn;
+  double logfac;
+  const double* L;
+  int64_t ldL;
+  int S;                     // columns of L (slots at snapshot)
+  const double* margin;
+  const int* list;
+  const int* cnt;
+  int nblocks;
+  int p0;
+  double T;                  // certainty threshold without drift
+  double dmax;               // drift budget used by the prepass
+  int scap;                  // slot capacity
+  int K;
+  int nslots;
+  ResolveCtl* ctl;
+  int force_exact;           // testing: evaluate every point on the exact path
+};
+
+struct HistArgs {
+  const uint8_t* codes_t;
+  int n, d, nq;
+  const int* label;          // label per point
+  const unsigned char* mask; // per label: include (nullptr = all)
+  int K, mmax;
+  unsigned int* freq;        // [K][d][mmax]
+};
+
+struct LoglikArgs {
+  const uint8_t* codes_t;
+  int n, d, nq;
+  const int* label;
+  ParamTables cl;            // per label tables
+  double* partial;           // per block (hi, lo) pairs
+};
+
+}  // namespace hdpm
+
+namespace hdpm {
+
+// Restricted Gibbs scan over S (code/split_merge.cpp:163-225) and logprobgs_c_i (96-161).
+struct SmArgs {
+  const uint8_t* codes_t;
+  int n, d, nq;
+  const int* S;              // point indices, scan order
+  int nS;
+  ParamTables two;           // tables of the two clusters (entry 0 = c_i_1, entry 1 = c_i_2)
+  double* ll;                // [2][nS]
+  int* side;                 // in/out: 0 -> c_i_1, 1 -> c_i_2, per S position
+  const int* side_ref;       // launch-state side (logprobgs_c_i), per S position
+  const uint32_t* raw;       // nS raw draws (scan)
+  const double* logn;
+  int n1, n2;                // current (scan) or launch (logprobgs) cluster sizes
+  int* out_counts;           // [2] final sizes after the scan
+  double* out;               // logprobgs partial (hi, lo) per block
+};
+
+}  // namespace hdpm

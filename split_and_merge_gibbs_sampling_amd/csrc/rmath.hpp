@@ -1,0 +1,408 @@
+// rmath.hpp -- host-side R/Rcpp/GSL-compatible numerics used by the hdpm runtime.
+//
+// The reference sampler draws every random number from R's global Mersenne-Twister
+// through Rcpp sugar and R nmath, and evaluates the HIG normaliser with GSL.  The
+// runtime keeps ONE R-compatible stream on the host (the device receives contiguous
+// slices of it), so these restatements must consume draws exactly as R does:
+//   Rng            R src/main/RNG.c  (set.seed scrambling, MT_genrand, fixup)
+//   sample_prob1   Rcpp sugar sample(x, 1, TRUE, p): FixupProb + revsort + SampleReplace
+//   rbeta          R nmath rbeta.c (Cheng 1978, BB / BC)
+//   qbeta01_lt     hg:359 branch test R::qbeta(0.1, a, b) < x  (as pbeta(x) > 0.1)
+//   hyperg_2F1     GSL gsl_sf_hyperg_2F1_e, positive-series branch
+//   rhig1 / bisec  code/hyperg.cpp:221-287, 346-378
+#pragma once
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <unordered_map>
+#include <vector>
+
+namespace hdpm {
+
+enum Status : int {
+  kOk = 0,
+  kValidate = 1,   // validate_state -> Rcpp::stop (cf:146-172)
+  kGsl = 2,        // norm_const2 throws (hg:38-45)
+  kProb = 3,       // FixupProb stop()
+  kWalker = 4,     // Walker alias (>200 categories): not supported
+  kArg = 5,        // bad argument / capacity
+  kDevice = 6,     // HIP runtime failure
+  kNoDevice = 7,   // no HIP device / extension unusable
+};
+
+// ------------------------------------------------------------------ R MT19937
+struct Rng {
+  int32_t mti = 625;
+  uint32_t mt[624];
+
+  void set_seed(uint32_t seed) {  // RNG_Init(MERSENNE_TWISTER, seed) + FixupSeeds
+    for (int j = 0; j < 50; j++) seed = 69069u * seed + 1u;
+    seed = 69069u * seed + 1u;  // i_seed[0] (dummy[0]) is overwritten by FixupSeeds
+    for (int j = 0; j < 624; j++) { seed = 69069u * seed + 1u; mt[j] = seed; }
+    mti = 624;
+  }
+  void import625(const int32_t* s) {
+    mti = s[0];
+    for (int i = 0; i < 624; i++) mt[i] = (uint32_t)s[i + 1];
+  }
+  void export625(int32_t* s) const {
+    s[0] = mti;
+    for (int i = 0; i < 624; i++) s[i + 1] = (int32_t)mt[i];
+  }
+  void twist() {
+    static const uint32_t mag01[2] = {0u, 0x9908b0dfu};
+    int kk;
+    uint32_t y;
+    for (kk = 0; kk < 624 - 397; kk++) {
+      y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
+      mt[kk] = mt[kk + 397] ^ (y >> 1) ^ mag01[y & 1u];
+    }
+    for (; kk < 623; kk++) {
+      y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
+      mt[kk] = mt[kk - 227] ^ (y >> 1) ^ mag01[y & 1u];
+    }
+    y = (mt[623] & 0x80000000u) | (mt[0] & 0x7fffffffu);
+    mt[623] = mt[396] ^ (y >> 1) ^ mag01[y & 1u];
+    mti = 0;
+  }
+  // Raw tempered 32-bit output (MT_genrand before the 2^-32 scaling).
+  uint32_t raw() {
+    if (mti >= 624) {
+      if (mti == 625) {  // MT_sgenrand(4357): never seeded
+        uint32_t seed = 4357;
+        for (int i = 0; i < 624; i++) {
+          mt[i] = seed & 0xffff0000u;
+          seed = 69069u * seed + 1u;
+          mt[i] |= (seed & 0xffff0000u) >> 16;
+          seed = 69069u * seed + 1u;
+        }
+      }
+      twist();
+    }
+    uint32_t y = mt[mti++];
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+  }
+  // Fill n raw outputs (same stream as n calls of raw()).
+  void raw_block(uint32_t* out, int64_t n) {
+    for (int64_t i = 0; i < n; i++) out[i] = raw();
+  }
+  double unif() { return raw_to_unif(raw()); }
+  static inline double raw_to_unif(uint32_t y) {
+    const double i2_32m1 = 2.328306437080797e-10;
+    double x = (double)y * 2.3283064365386963e-10;
+    if (x <= 0.0) return 0.5 * i2_32m1;
+    if ((1.0 - x) <= 0.0) return 1.0 - 0.5 * i2_32m1;
+    return x;
+  }
+};
+
+// ------------------------------------------------------------------ Rcpp sample
+// R sort.c revsort: descending heapsort of a[0..n) carrying ib[].
+inline void revsort(double* a0, int* ib0, int n) {
+  if (n <= 1) return;
+  double* a = a0 - 1;
+  int* ib = ib0 - 1;
+  int l = (n >> 1) + 1, ir = n, i, j, ii;
+  double ra;
+  for (;;) {
+    if (l > 1) {
+      l = l - 1;
+      ra = a[l];
+      ii = ib[l];
+    } else {
+      ra = a[ir];
+      ii = ib[ir];
+      a[ir] = a[1];
+      ib[ir] = ib[1];
+      if (--ir == 1) {
+        a[1] = ra;
+        ib[1] = ii;
+        return;
+      }
+    }
+    i = l;
+    j = l << 1;
+    while (j <= ir) {
+      if (j < ir && a[j] > a[j + 1]) ++j;
+      if (ra > a[j]) {
+        a[i] = a[j];
+        ib[i] = ib[j];
+        j += (i = j);
+      } else {
+        j = ir + 1;
+      }
+    }
+    a[i] = ra;
+    ib[i] = ii;
+  }
+}
+
+// sample(x, 1, TRUE, probs) given the uniform rU it will consume.  Returns a 0-based
+// position or a negative Status.  `p` is scratch (n doubles), `perm` scratch (n ints).
+inline int sample_prob1_u(const double* probs, int n, double rU, double* p, int* perm) {
+  double sum = 0.0;
+  int npos = 0;
+  for (int i = 0; i < n; i++) {
+    double x = probs[i];
+    if (!std::isfinite(x) || x < 0) return -kProb;
+    if (x > 0) { npos++; sum += x; }
+  }
+  if (npos == 0) return -kProb;
+  for (int i = 0; i < n; i++) p[i] = probs[i] / sum;
+  int nc = 0;
+  for (int i = 0; i < n; i++) nc += (n * p[i] > 0.1);
+  if (nc > 200) return -kWalker;
+  for (int i = 0; i < n; i++) perm[i] = i + 1;
+  revsort(p, perm, n);
+  for (int i = 1; i < n; i++) p[i] += p[i - 1];
+  int j;
+  for (j = 0; j < n - 1; j++)
+    if (rU <= p[j]) break;
+  return perm[j] - 1;
+}
+
+inline int sample_prob1(Rng& rng, const double* probs, int n, std::vector<double>& p,
+                        std::vector<int>& perm) {
+  if ((int)p.size() < n) { p.resize(n); perm.resize(n); }
+  // Validation happens before the draw in Rcpp (FixupProb precedes unif_rand()).
+  double sum = 0.0;
+  int npos = 0;
+  for (int i = 0; i < n; i++) {
+    double x = probs[i];
+    if (!std::isfinite(x) || x < 0) return -kProb;
+    if (x > 0) { npos++; sum += x; }
+  }
+  if (npos == 0) return -kProb;
+  (void)sum;
+  return sample_prob1_u(probs, n, rng.unif(), p.data(), perm.data());
+}
+
+// ------------------------------------------------------------------ nmath rbeta
+inline double rbeta(Rng& rng, double aa, double bb) {
+  const double expmax = DBL_MAX_EXP * M_LN2;
+  if (std::isnan(aa) || std::isnan(bb) || aa < 0. || bb < 0.) return NAN;
+  if (!std::isfinite(aa) && !std::isfinite(bb)) return 0.5;
+  if (aa == 0. && bb == 0.) return (rng.unif() < 0.5) ? 0. : 1.;
+  if (!std::isfinite(aa) || bb == 0.) return 1.0;
+  if (!std::isfinite(bb) || aa == 0.) return 0.0;
+  const double a = std::fmin(aa, bb), b = std::fmax(aa, bb), alpha = a + b;
+  double r, s, t = 0, u1, u2, v = 0, w = 0, y, z;
+  auto vw = [&](double beta, double AA) {
+    v = beta * std::log(u1 / (1.0 - u1));
+    if (v <= expmax) {
+      w = AA * std::exp(v);
+      if (!std::isfinite(w)) w = DBL_MAX;
+    } else {
+      w = DBL_MAX;
+    }
+  };
+  if (a <= 1.0) {  // Algorithm BC
+    const double beta = 1.0 / a, delta = 1.0 + b - a;
+    const double k1 = delta * (0.0138889 + 0.0416667 * a) / (b * beta - 0.777778);
+    const double k2 = 0.25 + (0.5 + 0.25 / delta) * a;
+    for (;;) {
+      u1 = rng.unif();
+      u2 = rng.unif();
+      if (u1 < 0.5) {
+        y = u1 * u2;
+        z = u1 * y;
+        if (0.25 * u2 + z - y >= k1) continue;
+      } else {
+        z = u1 * u1 * u2;
+        if (z <= 0.25) {
+          vw(beta, b);
+          break;
+        }
+        if (z >= k2) continue;
+      }
+      vw(beta, b);
+      if (alpha * (std::log(alpha / (a + w)) + v) - 1.3862944 >= std::log(z)) break;
+    }
+    return (aa == a) ? a / (a + w) : w / (a + w);
+  }
+  // Algorithm BB
+  const double beta = std::sqrt((alpha - 2.0) / (2.0 * a * b - alpha));
+  const double gamma = a + 1.0 / beta;
+  do {
+    u1 = rng.unif();
+    u2 = rng.unif();
+    vw(beta, a);
+    z = u1 * u1 * u2;
+    r = gamma * v - 1.3862944;
+    s = a + r - w;
+    if (s + 2.609438 >= 5.0 * z) break;
+    t = std::log(z);
+    if (s > t) break;
+  } while (r + alpha * std::log(alpha / (b + w)) < t);
+  return (aa != a) ? b / (b + w) : w / (b + w);
+}
+
+// ------------------------------------------------------------------ qbeta branch test
+namespace detail {
+inline double betacf(double a, double b, double x) {
+  const double FPMIN = 1e-300, EPS = 1e-16;
+  double qab = a + b, qap = a + 1.0, qam = a - 1.0, c = 1.0, d = 1.0 - qab * x / qap;
+  if (std::fabs(d) < FPMIN) d = FPMIN;
+  d = 1.0 / d;
+  double h = d;
+  for (int m = 1; m <= 200000; m++) {
+    int m2 = 2 * m;
+    double aa = m * (b - m) * x / ((qam + m2) * (a + m2));
+    d = 1.0 + aa * d; if (std::fabs(d) < FPMIN) d = FPMIN;
+    c = 1.0 + aa / c; if (std::fabs(c) < FPMIN) c = FPMIN;
+    d = 1.0 / d; h *= d * c;
+    aa = -(a + m) * (qab + m) * x / ((a + m2) * (qap + m2));
+    d = 1.0 + aa * d; if (std::fabs(d) < FPMIN) d = FPMIN;
+    c = 1.0 + aa / c; if (std::fabs(c) < FPMIN) c = FPMIN;
+    d = 1.0 / d;
+    double del = d * c;
+    h *= del;
+    if (std::fabs(del - 1.0) < EPS) break;
+  }
+  return h;
+}
+}  // namespace detail
+
+inline double pbeta(double x, double a, double b) {
+  if (x <= 0.0) return 0.0;
+  if (x >= 1.0) return 1.0;
+  double lbt = std::lgamma(a + b) - std::lgamma(a) - std::lgamma(b) + a * std::log(x) +
+               b * std::log1p(-x);
+  if (x < (a + 1.0) / (a + b + 2.0)) return std::exp(lbt) * detail::betacf(a, b, x) / a;
+  return 1.0 - std::exp(lbt) * detail::betacf(b, a, 1.0 - x) / b;
+}
+
+// R::qbeta(0.1, a, b, 1, 0) < x   <=>   pbeta(x; a, b) > 0.1.
+// Cantelli's inequality settles most calls without the continued fraction: with mean mu
+// and variance s2 of Beta(a, b), P(X > x) <= s2 / (s2 + (x - mu)^2) for x > mu and
+// P(X <= x) <= s2 / (s2 + (mu - x)^2) for x < mu.
+inline bool qbeta01_lt(double a, double b, double x) {
+  if (std::isnan(a) || std::isnan(b) || a < 0 || b < 0) return false;
+  if (b == 0) return false;
+  if (a == 0) return x > 0;
+  const double mu = a / (a + b);
+  const double s2 = a * b / ((a + b) * (a + b) * (a + b + 1.0));
+  const double dlt = x - mu;
+  const double bound = s2 / (s2 + dlt * dlt);
+  if (dlt > 0 && bound < 0.85) return true;    // P(X <= x) >= 0.15 > 0.1
+  if (dlt < 0 && bound < 0.05) return false;   // P(X <= x) <= 0.05 < 0.1
+  return pbeta(x, a, b) > 0.1;
+}
+
+// ------------------------------------------------------------------ GSL 2F1
+enum { GSL_SUCCESS = 0, GSL_EDOM = 1, GSL_EMAXITER = 11, GSL_EUNIMPL = 24 };
+
+inline int hyperg_2F1(double a, double b, double c, double x, double* val) {
+  const double eps = 2.2204460492503131e-16, loc_eps = 1000.0 * eps;
+  *val = 0.0;
+  if (x < -1.0 || 1.0 <= x) return GSL_EDOM;
+  if (std::fabs(c - b) < loc_eps || std::fabs(c - a) < loc_eps) {
+    *val = std::exp((c - a - b) * std::log(1.0 - x));
+    return GSL_SUCCESS;
+  }
+  if (!(a >= 0.0 && b >= 0.0 && c >= 0.0 && x >= 0.0 && x < 0.995)) return GSL_EUNIMPL;
+  if (std::fabs(c) < eps) return GSL_EUNIMPL;
+  double sum_pos = 1.0, sum_neg = 0.0, del_pos = 1.0, del_neg = 0.0, del = 1.0, k = 0.0;
+  int i = 0;
+  do {
+    if (++i > 30000) { *val = sum_pos - sum_neg; return GSL_EMAXITER; }
+    del *= (a + k) * (b + k) * x / ((c + k) * (k + 1.0));
+    if (del > 0.0) {
+      del_pos = del;
+      sum_pos += del;
+    } else if (del == 0.0) {
+      del_pos = 0.0;
+      del_neg = 0.0;
+      break;
+    } else {
+      del_neg = -del;
+      sum_neg -= del;
+    }
+    k += 1.0;
+  } while (std::fabs((del_pos + del_neg) / (sum_pos - sum_neg)) > eps);
+  *val = sum_pos - sum_neg;
+  return GSL_SUCCESS;
+}
+
+// hg:11-48.  Sets *err = kGsl where the reference throws.
+inline double norm_const2(double d, double c, double m, int* err) {
+  double val;
+  int st = hyperg_2F1(d + c, 1, d + 2, (m - 1) / m, &val);
+  if (st != GSL_SUCCESS) {
+    if (st == GSL_EMAXITER) return -INFINITY;
+    *err = kGsl;
+    return NAN;
+  }
+  if (!std::isfinite(val) || val == 0) { *err = kGsl; return NAN; }
+  return std::log(d + 1) + (d + c) * std::log(m) - std::log(val);
+}
+
+inline double lF_conK2(double u, double d, double c, double m, double lK) {  // hg:183-217
+  if (u == 0) return -INFINITY;
+  if (u == 1) return 0;
+  double x = u * (m - 1) / (1 + u * (m - 1));
+  double app;
+  if (hyperg_2F1(1, d + c, d + 2, x, &app) != GSL_SUCCESS) app = NAN;
+  return lK - std::log(d + 1) + (d + 1) * std::log(u) - (d + c) * std::log(1 + u * (m - 1)) +
+         std::log(app);
+}
+
+inline double bisec_hyper2(double d, double c, double m, double Omega, int* err) {  // hg:221-287
+  double centro = 0.5;
+  double lK = norm_const2(d, c, m, err);
+  if (*err) return NAN;
+  double app = lF_conK2(centro, d, c, m, lK) - std::log(Omega);
+  double su, giu;
+  int counter = 1;
+  if (app < 0) { giu = 0.5; su = 1; } else { giu = 0; su = 0.5; }
+  while (((su - giu) > 0.000000001) & (counter < 150)) {
+    centro = (su + giu) / 2;
+    app = lF_conK2(centro, d, c, m, lK) - std::log(Omega);
+    if (app < 0) giu = centro; else su = centro;
+    counter = counter + 1;
+  }
+  return centro;
+}
+
+// rhig(1, v, w, m) (hg:346-378); `beta_path` is the cached hg:359 decision.
+inline double rhig1_decided(Rng& rng, double v, double w, double m, bool beta_path, int* err) {
+  double out;
+  if (beta_path) {
+    double x = rbeta(rng, w + 1, v - 1);
+    while (x > (m - 1) / m) x = rbeta(rng, w + 1, v - 1);
+    out = x / ((m - 1) * (1 - x));
+  } else {
+    double Omega = rng.unif();
+    out = bisec_hyper2(w, v, m, Omega, err);
+    if (*err) return NAN;
+  }
+  return -1 / std::log(out);
+}
+
+inline bool rhig_beta_path(double v, double w, double m) {
+  return qbeta01_lt(w + 1, v - 1, (m - 1) / m) && (m - 1) / m > 4 / 5;
+}
+
+inline double rhig1(Rng& rng, double v, double w, double m, int* err) {
+  return rhig1_decided(rng, v, w, m, rhig_beta_path(v, w, m), err);
+}
+
+// dhamming (cf:355-377) split into its two attribute-level values: the device adds
+// tab_match when x == c and tab_mismatch otherwise, which is bit-identical to calling
+// dhamming(x, c, s, m) because numerator - denominator is evaluated the same way.
+inline void dhamming_pair(double s, int attrisize, double* match, double* mismatch) {
+  double exp_term = std::exp(1.0 / s);
+  double attr_ratio = (attrisize - 1.0) / exp_term;
+  double denominator = std::log(1.0 + attr_ratio);
+  double num0 = -0 / s;          // diff = 0 -> (double)(-0) / s = +0.0
+  double num1 = -1 / s;          // diff = 1 -> (double)(-1) / s
+  *match = num0 - denominator;
+  *mismatch = num1 - denominator;
+}
+
+}  // namespace hdpm

@@ -1,0 +1,223 @@
+"""Host-side mirror of the reference sampler's interface on the MI355X engine.
+
+``run_markov_chain`` keeps the signature and result fields of the reference's Rcpp
+export (code/launcher.cpp:6-14, 57-63, 170-173); ``Engine`` exposes the C++ entry points
+of the hot path (sample_allocation sweep, update_phi, compute_loglikelihood,
+split_restricted_gibbs_sampler, logprobgs_c_i, split_and_merge) over the C ABI.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import HdpmError, ptr
+
+
+def _i32(a):
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+class Engine:
+    """One hdpm context (one GPU, one chain, one R random stream)."""
+
+    def __init__(self, device: int = 0):
+        L = _lib.lib()
+        h = C.c_void_p()
+        st = L.hdpm_ctx_create(device, C.byref(h))
+        if st != 0:
+            raise HdpmError(st, f"cannot create a context on device {device} (needs a gfx950 GPU)")
+        self._L, self._h = L, h
+        self.n = self.d = 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.hdpm_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, st):
+        if st != 0:
+            raise HdpmError(st, self._L.hdpm_last_error(self._h).decode())
+
+    # ---------------------------------------------------------------- data / rng / state
+    def set_data(self, codes, attrisize, gamma, v, w):
+        codes = np.ascontiguousarray(codes, dtype=np.uint8)
+        self.n, self.d = codes.shape
+        self._att = _i32(attrisize)
+        self._keep = (codes, self._att, _f64(v), _f64(w))
+        self._check(self._L.hdpm_set_data(self._h, ptr(codes), self.n, self.d, ptr(self._att), float(gamma),
+                                          ptr(self._keep[2]), ptr(self._keep[3])))
+
+    def set_seed(self, seed: int):
+        self._check(self._L.hdpm_rng_set_seed(self._h, seed & 0xFFFFFFFF))
+
+    @property
+    def rng_state(self) -> np.ndarray:
+        s = np.zeros(625, np.int32)
+        self._check(self._L.hdpm_rng_get_state(self._h, ptr(s)))
+        return s
+
+    @rng_state.setter
+    def rng_state(self, s):
+        s = _i32(s)
+        self._check(self._L.hdpm_rng_set_state(self._h, ptr(s)))
+
+    def set_state(self, c_i, centers, sigma):
+        c = _i32(c_i)
+        cen, sig = _f64(centers), _f64(sigma)
+        self._check(self._L.hdpm_set_state(self._h, ptr(c), cen.shape[0], ptr(cen), ptr(sig)))
+
+    def get_state(self):
+        c = np.zeros(self.n, np.int32)
+        K = C.c_int32(0)
+        self._check(self._L.hdpm_get_state(self._h, ptr(c), C.byref(K), None, None, 0))
+        cen = np.zeros((K.value, self.d))
+        sig = np.zeros((K.value, self.d))
+        self._check(self._L.hdpm_get_state(self._h, ptr(c), C.byref(K), ptr(cen), ptr(sig), K.value))
+        return c, cen, sig
+
+    def set_pool(self, centers, sigma):
+        cen, sig = _f64(centers), _f64(sigma)
+        self._check(self._L.hdpm_set_pool(self._h, ptr(cen), ptr(sig), cen.shape[0]))
+
+    def generate_pool(self, P: int):
+        self._check(self._L.hdpm_generate_pool(self._h, int(P)))
+
+    def get_pool(self, P: int):
+        cen = np.zeros((P, self.d))
+        sig = np.zeros((P, self.d))
+        self._check(self._L.hdpm_get_pool(self._h, ptr(cen), ptr(sig), int(P)))
+        return cen, sig
+
+    # ---------------------------------------------------------------- hot path
+    def neal8_sweep(self, m: int):
+        """N sample_allocation calls in index order (code/launcher.cpp:95-99)."""
+        self._check(self._L.hdpm_neal8_sweep(self._h, int(m)))
+
+    def update_phi(self, cluster_indexes=None):
+        if cluster_indexes is None:
+            self._check(self._L.hdpm_update_phi(self._h, None, 0))
+        else:
+            idx = _i32(cluster_indexes)
+            self._check(self._L.hdpm_update_phi(self._h, ptr(idx), len(idx)))
+
+    def compute_loglikelihood(self) -> float:
+        out = C.c_double(0.0)
+        self._check(self._L.hdpm_compute_loglikelihood(self._h, C.byref(out)))
+        return out.value
+
+    def loglik_matrix(self, K: int):
+        Lm = np.zeros((self.n, K))
+        H = np.zeros((self.n, K), np.int32)
+        self._check(self._L.hdpm_loglik_matrix(self._h, ptr(Lm), ptr(H)))
+        return Lm, H
+
+    def restricted_gibbs(self, S, i1, i2, t=1):
+        S = _i32(S)
+        self._check(self._L.hdpm_restricted_gibbs(self._h, ptr(S), len(S), int(i1), int(i2), int(t)))
+
+    def logprobgs_c_i(self, g_c_i, S, i1, i2) -> float:
+        g, S = _i32(g_c_i), _i32(S)
+        out = C.c_double(0.0)
+        self._check(self._L.hdpm_logprobgs_c_i(self._h, ptr(g), ptr(S), len(S), int(i1), int(i2), C.byref(out)))
+        return out.value
+
+    def split_and_merge(self, t, r, idx_1_sm=0) -> int:
+        acc = C.c_int32(0)
+        self._check(self._L.hdpm_split_and_merge(self._h, int(t), int(r), int(idx_1_sm), C.byref(acc)))
+        return acc.value
+
+    def stats(self) -> dict:
+        s = _lib.Stats()
+        self._check(self._L.hdpm_get_stats(self._h, C.byref(s)))
+        return s.as_dict()
+
+    def reset_stats(self):
+        self._check(self._L.hdpm_reset_stats(self._h))
+
+    def set_debug(self, mode: int):
+        self._check(self._L.hdpm_set_debug(self._h, int(mode)))
+
+    def synchronize(self):
+        self._check(self._L.hdpm_synchronize(self._h))
+
+    # ---------------------------------------------------------------- driver
+    @staticmethod
+    def chain_params(verbose=0, m=5, iterations=1000, L=1, burnin=5000, t=10, r=10, neal8=False,
+                     split_merge=True, n8_step_size=1, sam_step_size=1, thinning=1):
+        return _lib.ChainParams(verbose, m, iterations, L, burnin, t, r, int(bool(neal8)), int(bool(split_merge)),
+                                n8_step_size, sam_step_size, thinning)
+
+    def init_chain(self, params, c_i=None):
+        """code/launcher.cpp:27-77 (initial state, update_phi, latent pool)."""
+        self._params = params
+        self._idx_1_sm = C.c_int32(0)
+        ci = None if c_i is None else _i32(c_i)
+        self._check(self._L.hdpm_init_chain(self._h, C.byref(params), ptr(ci)))
+
+    def iteration(self, it: int):
+        """One pass of the loop body code/launcher.cpp:85-132; returns (accepted, loglik)."""
+        acc = C.c_int32(0)
+        ll = C.c_double(0.0)
+        self._check(self._L.hdpm_iteration(self._h, C.byref(self._params), int(it), C.byref(self._idx_1_sm),
+                                           C.byref(acc), C.byref(ll)))
+        return acc.value, ll.value
+
+    def run_markov_chain(self, *, verbose=0, m=5, iterations=1000, L=1, c_i=None, burnin=5000, t=10, r=10,
+                         neal8=False, split_merge=True, n8_step_size=1, sam_step_size=1, thinning=1):
+        p = _lib.ChainParams(verbose, m, iterations, L, burnin, t, r, int(bool(neal8)), int(bool(split_merge)),
+                             n8_step_size, sam_step_size, thinning)
+        tot = np.zeros(iterations, np.int32)
+        cis = np.zeros((iterations, self.n), np.int32)
+        ll = np.zeros(iterations, np.float64)
+        acc = np.zeros(iterations, np.int32)
+        fin = np.zeros(self.n, np.int32)
+        tm = np.zeros(1, np.float64)
+        ci = None if c_i is None else _i32(c_i)
+        self._check(self._L.hdpm_run_markov_chain(self._h, C.byref(p), ptr(ci), ptr(tot), ptr(cis), ptr(ll),
+                                                  ptr(acc), ptr(fin), ptr(tm)))
+        return {"total_cls": tot, "c_i": cis, "loglikelihood": ll, "final_ass": fin,
+                "time": float(tm[0]), "accepted": acc}
+
+
+def run_markov_chain(data, attrisize, gamma, v, w, verbose=0, m=5, iterations=1000, L=1, c_i=None,
+                     burnin=5000, t=10, r=10, neal8=False, split_merge=True, n8_step_size=1,
+                     sam_step_size=1, thinning=1, *, seed=None, rng_state=None, device=0):
+    """Drop-in for the reference's ``run_markov_chain`` (code/launcher.cpp:6-14).
+
+    ``data`` holds the categorical codes 1..m_j (an N x D matrix).  The R random stream
+    is ``set.seed(seed)`` or an explicit 625-word ``rng_state``; the returned dict has
+    the fields of the reference's result list (plus ``rng_state`` after the run).
+    """
+    eng = Engine(device)
+    try:
+        eng.set_data(np.asarray(data), attrisize, gamma, v, w)
+        if rng_state is not None:
+            eng.rng_state = rng_state
+        else:
+            eng.set_seed(0 if seed is None else seed)
+        res = eng.run_markov_chain(verbose=verbose, m=m, iterations=iterations, L=L, c_i=c_i, burnin=burnin,
+                                   t=t, r=r, neal8=neal8, split_merge=split_merge, n8_step_size=n8_step_size,
+                                   sam_step_size=sam_step_size, thinning=thinning)
+        res["rng_state"] = eng.rng_state
+        res["stats"] = eng.stats()
+        return res
+    finally:
+        eng.close()

@@ -1,0 +1,269 @@
+"""MI355X parity tests: the HIP path through the C ABI against the CPU oracle and the
+committed golden traces.  Integer results (labels, K, Hamming counts) and the per-point
+log-likelihood matrix must be bit-exact; reductions (compute_loglikelihood,
+logprobgs_c_i) are compared with a relative tolerance of 1e-10 (north_star)."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+G = os.path.join(os.path.dirname(__file__), "golden")
+RTOL = 1e-10
+
+
+@pytest.fixture(scope="module")
+def hd():
+    import split_and_merge_gibbs_sampling_amd as hd
+    hd.build()
+    return hd
+
+
+def make_engine(hd, ds):
+    e = hd.Engine(0)
+    e.set_data(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w)
+    return e
+
+
+def random_params(ds, K, seed):
+    rng = np.random.default_rng(seed)
+    cen = np.stack([rng.integers(1, ds.attrisize + 1) for _ in range(K)]).astype(np.float64)
+    sig = rng.uniform(0.15, 2.5, size=(K, ds.d))
+    return cen, sig
+
+
+def synth(n, d, k, levels, seed=1):
+    from split_and_merge_gibbs_sampling_amd.data import hamming_mixture
+    return hamming_mixture(n, d, k, levels, seed=seed)
+
+
+def oracle_state(oracle, c, cen, sig):
+    return oracle.OracleState(c, cen.shape[0], cen, sig)
+
+
+def assert_same_state(eng, ost):
+    c, cen, sig = eng.get_state()
+    assert cen.shape[0] == ost.K
+    assert np.array_equal(c, ost.c_i)
+    assert np.array_equal(cen, ost.centers[:ost.K])
+    assert np.array_equal(sig, ost.sigma[:ost.K])
+
+
+# ------------------------------------------------------------------ loglik matrix
+@pytest.mark.parametrize("which", ["zoo", "synth32", "synth200"])
+def test_loglik_matrix_bit_exact(hd, oracle, zoo, which):
+    ds = {"zoo": zoo, "synth32": synth(3000, 32, 7, 2), "synth200": synth(700, 200, 5, (2, 6))}[which]
+    K = 9
+    cen, sig = random_params(ds, K, 1)
+    c = np.arange(ds.n, dtype=np.int32) % K
+    eng = make_engine(hd, ds)
+    eng.set_state(c, cen, sig)
+    L, H = eng.loglik_matrix(K)
+    Lo, Ho = oracle.loglik_matrix(ds.codes, ds.attrisize, cen, sig)
+    assert np.array_equal(H, Ho)
+    assert np.array_equal(L, Lo)          # bit-exact: same tables, same j order
+    eng.close()
+
+
+# ------------------------------------------------------------------ single sweep
+def sweep_case(hd, oracle, ds, c, cen, sig, P, seed, m=3, debug=0, sweeps=1, phi=False):
+    st = oracle.seed_state(seed)
+    pc, ps, s0 = oracle.pool_generate(ds.attrisize, ds.v, ds.w, P, st)
+    assert s0 == 0
+    eng = make_engine(hd, ds)
+    eng.set_debug(debug)
+    eng.set_state(c, cen, sig)
+    eng.set_pool(pc, ps)
+    eng.rng_state = st
+    ost = oracle_state(oracle, c, cen, sig)
+    ost_rng = st.copy()
+    for it in range(sweeps):
+        eng.neal8_sweep(m)
+        r = oracle.neal8_sweep(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w, ost, m, pc, ps, ost_rng, fast=1)
+        assert r == 0
+        assert_same_state(eng, ost)
+        assert np.array_equal(eng.rng_state, ost_rng), f"rng diverged after sweep {it}"
+        if phi:
+            eng.update_phi()
+            assert oracle.update_phi(ds.codes, ds.attrisize, ds.v, ds.w, ost, ost_rng) == 0
+            assert_same_state(eng, ost)
+            assert np.array_equal(eng.rng_state, ost_rng)
+    stats = eng.stats()
+    eng.close()
+    return stats
+
+
+@pytest.mark.parametrize("debug", [0, 1])
+def test_zoo_single_sweeps_from_truth(hd, oracle, zoo, debug):
+    cen, sig = random_params(zoo, 7, 3)
+    stats = sweep_case(hd, oracle, zoo, zoo.truth, cen, sig, zoo.n * 3, seed=17, debug=debug, sweeps=3)
+    assert stats["sweeps"] == 3
+
+
+def test_zoo_sweeps_with_update_phi_all_singletons(hd, oracle, zoo):
+    # L = 101 (every point its own cluster): exercises cases 2 and 4 heavily
+    c = np.arange(zoo.n, dtype=np.int32)
+    cen, sig = random_params(zoo, zoo.n, 5)
+    sweep_case(hd, oracle, zoo, c, cen, sig, zoo.n * 3, seed=23, sweeps=4, phi=True)
+
+
+def test_zoo_sweeps_with_update_phi_one_cluster(hd, oracle, zoo):
+    # L = 1: the first sweeps create clusters (case 3 -> device restarts)
+    c = np.zeros(zoo.n, np.int32)
+    cen, sig = random_params(zoo, 1, 6)
+    stats = sweep_case(hd, oracle, zoo, c, cen, sig, zoo.n * 3, seed=29, sweeps=6, phi=True)
+    assert stats["restarts"] > 0
+
+
+@pytest.mark.parametrize("debug", [0, 1])
+def test_synthetic_sweeps_with_update_phi(hd, oracle, debug):
+    ds = synth(6000, 32, 8, 2, seed=3)
+    cen, sig = random_params(ds, 8, 7)
+    sweep_case(hd, oracle, ds, ds.truth, cen, sig, ds.n * 3, seed=31, sweeps=3, phi=True, debug=debug)
+
+
+def test_synthetic_large_d_sweep(hd, oracle):
+    ds = synth(1500, 300, 4, (2, 6), seed=4)
+    cen, sig = random_params(ds, 4, 8)
+    sweep_case(hd, oracle, ds, ds.truth, cen, sig, ds.n * 3, seed=37, sweeps=2, phi=True)
+
+
+# ------------------------------------------------------------------ loglikelihood
+def test_compute_loglikelihood_matches_sequential_sum(hd, oracle, zoo):
+    for ds in (zoo, synth(20000, 64, 10, (2, 6), seed=5)):
+        cen, sig = random_params(ds, 10, 9)
+        c = (np.arange(ds.n) % 10).astype(np.int32)
+        eng = make_engine(hd, ds)
+        eng.set_state(c, cen, sig)
+        got = eng.compute_loglikelihood()
+        ref = oracle.compute_loglikelihood(ds.codes, ds.attrisize, oracle_state(oracle, c, cen, sig))
+        assert abs(got - ref) <= RTOL * abs(ref)
+        eng.close()
+
+
+# ------------------------------------------------------------------ split-merge pieces
+def test_restricted_gibbs_matches_oracle(hd, oracle, zoo):
+    cen, sig = random_params(zoo, 7, 10)
+    c = zoo.truth.astype(np.int32).copy()
+    i1, i2 = 3, 50
+    S = [i for i in range(zoo.n) if i not in (i1, i2) and c[i] in (c[i1], c[i2])]
+    st = oracle.seed_state(41)
+    eng = make_engine(hd, zoo)
+    eng.set_state(c, cen, sig)
+    eng.rng_state = st
+    eng.restricted_gibbs(S, i1, i2, t=5)
+    ost = oracle_state(oracle, c, cen, sig)
+    assert oracle.restricted_gibbs(zoo.codes, zoo.attrisize, zoo.v, zoo.w, S, ost, i1, i2, 5, st) == 0
+    assert_same_state(eng, ost)
+    assert np.array_equal(eng.rng_state, st)
+    eng.close()
+
+
+def test_restricted_gibbs_large_clusters(hd, oracle):
+    ds = synth(8000, 32, 4, 2, seed=6)
+    cen, sig = random_params(ds, 4, 11)
+    c = ds.truth.astype(np.int32).copy()
+    i1 = int(np.where(c == 1)[0][0])
+    i2 = int(np.where(c == 2)[0][0])
+    S = [i for i in range(ds.n) if i not in (i1, i2) and c[i] in (c[i1], c[i2])]
+    st = oracle.seed_state(43)
+    eng = make_engine(hd, ds)
+    eng.set_state(c, cen, sig)
+    eng.rng_state = st
+    eng.restricted_gibbs(S, i1, i2, t=3)
+    ost = oracle_state(oracle, c, cen, sig)
+    assert oracle.restricted_gibbs(ds.codes, ds.attrisize, ds.v, ds.w, S, ost, i1, i2, 3, st) == 0
+    assert_same_state(eng, ost)
+    eng.close()
+
+
+def test_logprobgs_c_i_matches_oracle(hd, oracle, zoo):
+    cen, sig = random_params(zoo, 7, 12)
+    c = zoo.truth.astype(np.int32).copy()
+    i1, i2 = 0, 60
+    S = [i for i in range(zoo.n) if i not in (i1, i2) and c[i] in (c[i1], c[i2])]
+    g = c.copy()
+    rng = np.random.default_rng(1)
+    for s in S:
+        g[s] = c[i1] if rng.random() < 0.5 else c[i2]
+    eng = make_engine(hd, zoo)
+    eng.set_state(c, cen, sig)
+    got = eng.logprobgs_c_i(g, S, i1, i2)
+    ref = oracle.logprobgs_c_i(zoo.codes, zoo.attrisize, oracle_state(oracle, c, cen, sig), g, S, i1, i2)
+    assert abs(got - ref) <= RTOL * max(1.0, abs(ref))
+    eng.close()
+
+
+# ------------------------------------------------------------------ full chains vs golden
+def test_run_markov_chain_zoo_neal8_golden(hd, zoo):
+    g = np.load(os.path.join(G, "zoo_neal8_seed1.npz"))
+    res = hd.run_markov_chain(zoo.codes, zoo.attrisize, zoo.gamma, zoo.v, zoo.w, m=3, iterations=40, L=1,
+                              c_i=np.zeros(zoo.n, np.int32), burnin=0, neal8=True, split_merge=False, seed=1)
+    assert np.array_equal(res["c_i"], g["c_i"])
+    assert np.array_equal(res["total_cls"], g["total_cls"])
+    np.testing.assert_allclose(res["loglikelihood"], g["loglikelihood"], rtol=RTOL, atol=0)
+
+
+def test_run_markov_chain_zoo_split_merge_golden(hd, zoo):
+    g = np.load(os.path.join(G, "zoo_sm_seed7.npz"))
+    res = hd.run_markov_chain(zoo.codes, zoo.attrisize, zoo.gamma, zoo.v, zoo.w, m=3, iterations=30, L=1,
+                              c_i=np.zeros(zoo.n, np.int32), burnin=0, t=10, r=10, neal8=True, split_merge=True,
+                              seed=7)
+    assert np.array_equal(res["c_i"], g["c_i"])
+    assert np.array_equal(res["accepted"], g["accepted"])
+    np.testing.assert_allclose(res["loglikelihood"], g["loglikelihood"], rtol=RTOL, atol=0)
+
+
+def test_run_markov_chain_random_init_matches_oracle(hd, oracle, zoo):
+    # L = 20 random labels, a seed whose initial draw uses all 20 labels
+    seed = next(s for s in range(1, 100)
+                if len(np.unique((20 * oracle.runif(oracle.seed_state(s), zoo.n) + 1).astype(int))) == 20)
+    kw = dict(m=3, iterations=15, L=20, burnin=5, t=4, r=4, neal8=True, split_merge=True)
+    st, ref = oracle.run_markov_chain(zoo.codes, zoo.attrisize, zoo.gamma, zoo.v, zoo.w, seed=seed, fast=1, **kw)
+    assert st == 0
+    res = hd.run_markov_chain(zoo.codes, zoo.attrisize, zoo.gamma, zoo.v, zoo.w, seed=seed, **kw)
+    assert np.array_equal(res["c_i"], ref["c_i"])
+    assert np.array_equal(res["total_cls"], ref["total_cls"])
+
+
+def test_run_markov_chain_unused_label_is_an_error(hd, oracle, zoo):
+    seed = next(s for s in range(1, 100)
+                if len(np.unique((20 * oracle.runif(oracle.seed_state(s), zoo.n) + 1).astype(int))) < 20)
+    with pytest.raises(hd.HdpmError) as e:
+        hd.run_markov_chain(zoo.codes, zoo.attrisize, zoo.gamma, zoo.v, zoo.w, m=3, iterations=2, L=20,
+                            burnin=0, neal8=True, split_merge=False, seed=seed)
+    assert e.value.status == 1
+
+
+def test_synthetic_chain_matches_oracle(hd, oracle):
+    ds = synth(10000, 32, 20, 2, seed=10091995)
+    kw = dict(m=3, iterations=3, L=1, c_i=ds.truth, burnin=0, neal8=True, split_merge=False)
+    st, ref = oracle.run_markov_chain(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w, seed=2, fast=1, **kw)
+    assert st == 0
+    res = hd.run_markov_chain(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w, seed=2, **kw)
+    assert np.array_equal(res["c_i"], ref["c_i"])
+    np.testing.assert_allclose(res["loglikelihood"], ref["loglikelihood"], rtol=RTOL, atol=0)
+
+
+# ------------------------------------------------------------------ size-independent properties
+def test_large_sweep_invariants(hd):
+    from split_and_merge_gibbs_sampling_amd.data import config
+    ds = config("c5", n=200_000)
+    eng = make_engine(hd, ds)
+    eng.set_seed(5)
+    K = 20
+    cen, sig = random_params(ds, K, 13)
+    eng.set_state(ds.truth, cen, sig)
+    eng.update_phi()
+    eng.generate_pool(ds.n * 3)
+    for _ in range(2):
+        eng.neal8_sweep(3)
+        eng.update_phi()
+    c, cen, sig = eng.get_state()
+    K = cen.shape[0]
+    assert set(np.unique(c)) == set(range(K))          # labels contiguous, none empty
+    assert np.all(sig > 0) and np.all(cen >= 1) and np.all(cen <= ds.attrisize)
+    ll = eng.compute_loglikelihood()
+    assert np.isfinite(ll) and ll < 0
+    eng.close()

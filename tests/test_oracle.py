@@ -1,0 +1,146 @@
+"""CPU tests of the oracle: pinned against R's RNG outputs, cross-checked against the
+independent Python restatement (tests/pyref.py) and the committed golden traces."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import pyref as P
+
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_r_runif_known_answers(oracle):
+    kat = json.load(open(os.path.join(G, "r_runif_kat.json")))
+    for seed, vals in kat["seeds"].items():
+        got = oracle.runif(oracle.seed_state(int(seed)), 5)
+        np.testing.assert_allclose(got, vals, atol=5e-8)          # R prints 7 digits
+        r = P.RRng(int(seed))
+        assert np.array_equal(got, [r.unif() for _ in range(5)])
+
+
+def test_rng_state_roundtrip_matches_numpy_mt(oracle):
+    st = oracle.seed_state(2024)
+    a = oracle.runif(st, 3000)          # crosses several 624-word twists
+    r = P.RRng(2024)
+    b = np.array([r.unif() for _ in range(3000)])
+    assert np.array_equal(a, b)
+    assert np.array_equal(st, r.export())
+
+
+@pytest.mark.parametrize("a,b", [(2.5, 7.0), (1.25, 5.0), (0.5, 3.0), (0.7, 0.4), (40.0, 900.0)])
+def test_rbeta_matches_pyref(oracle, a, b):
+    st = oracle.seed_state(11)
+    got = oracle.rbeta(st, a, b, 400)
+    r = P.RRng(11)
+    exp = np.array([P.rbeta(r, a, b) for _ in range(400)])
+    assert np.array_equal(got, exp)
+    assert np.array_equal(st, r.export())
+    assert abs(got.mean() - a / (a + b)) < 0.05
+
+
+@pytest.mark.parametrize("v,w,m", [(6, 0.25, 2), (3, 0.5, 6), (6.0, 40.25, 2.0), (8.0, 30.25, 4.0),
+                                   (2.5, 60.0, 2.0), (106.0, 3.25, 2.0)])
+def test_rhig_both_branches_match_pyref(oracle, v, w, m):
+    st = oracle.seed_state(5)
+    got, err = oracle.rhig(st, v, w, m, 25)
+    assert err == 0
+    r = P.RRng(5)
+    exp = np.array([P.rhig1(r, v, w, m) for _ in range(25)])
+    assert np.array_equal(got, exp)
+    assert np.all(got > 0)
+
+
+def test_qbeta_branch_against_scipy(oracle):
+    from scipy.special import betaincinv
+    rng = np.random.default_rng(0)
+    for _ in range(300):
+        a, b = rng.uniform(1.01, 80), rng.uniform(1.01, 80)
+        x = rng.uniform(0.3, 0.99)
+        q = betaincinv(a, b, 0.1)
+        if abs(q - x) < 1e-9:
+            continue
+        assert oracle.lib().orc_ffi_qbeta01_lt(a, b, x) == int(q < x)
+
+
+def test_norm_const2_against_mpmath(oracle):
+    mp = pytest.importorskip("mpmath")
+    for d, c, m in [(0.25, 6.0, 2.0), (3.5, 40.0, 4.0), (10.25, 200.0, 6.0)]:
+        v, err = oracle.norm_const2(d, c, m)
+        assert err == 0
+        ref = float(mp.log(d + 1) + (d + c) * mp.log(m) - mp.log(mp.hyp2f1(d + c, 1, d + 2, (m - 1) / m)))
+        assert abs(v - ref) < 1e-9 * max(1, abs(ref))
+    # overflow of the series -> the reference throws (norm_const2 hg:43-45)
+    _, err = oracle.norm_const2(0.25, 3000.0, 2.0)
+    assert err == 2
+
+
+def test_revsort_ties_and_order():
+    a, ib = [0.2, 0.5, 0.5, 0.1], [1, 2, 3, 4]
+    P.revsort(a, ib)
+    assert a == sorted(a, reverse=True)
+    a2, ib2 = [0.5, 0.5], [1, 2]
+    P.revsort(a2, ib2)
+    assert ib2 == [2, 1]        # equal pair: second index first
+
+
+def test_sample_prob1_matches_pyref(oracle):
+    rng = np.random.default_rng(3)
+    st = oracle.seed_state(9)
+    r = P.RRng(9)
+    for n in (1, 2, 3, 7, 23, 64):
+        for _ in range(20):
+            p = rng.random(n) ** 3
+            p[rng.random(n) < 0.2] = 0.0
+            if p.sum() == 0:
+                p[0] = 1.0
+            p = p / p.sum()
+            got, s = oracle.sample_prob1(st, p)
+            assert s == 0 and got == P.sample_prob1(r, list(p))
+
+
+def test_dhamming_matches_pyref(oracle):
+    for x, c, s, m in [(1, 1, 0.5, 2), (1, 2, 0.5, 2), (3, 3, 1.7, 6), (2, 5, 0.05, 6)]:
+        assert oracle.lib().orc_ffi_dhamming(x, c, s, m) == P.dhamming(x, c, s, m)
+
+
+def test_zoo_neal8_trace_oracle_vs_pyref_vs_golden(oracle, zoo):
+    g = np.load(os.path.join(G, "zoo_neal8_seed1.npz"))
+    c0 = np.zeros(zoo.n, np.int32)
+    for fast in (0, 1):
+        st, res = oracle.run_markov_chain(zoo.codes, zoo.attrisize, zoo.gamma, zoo.v, zoo.w, m=3, iterations=40,
+                                          L=1, c_i=c0, burnin=0, neal8=True, split_merge=False, seed=1, fast=fast)
+        assert st == 0
+        assert np.array_equal(res["c_i"], g["c_i"])
+        assert np.array_equal(res["loglikelihood"], g["loglikelihood"])
+    tr, lls = P.Model(zoo.codes, zoo.attrisize, zoo.gamma, zoo.v, zoo.w).run_neal8(P.RRng(1), list(c0), 3, 10)
+    assert np.array_equal(np.array(tr), g["c_i"][:10])
+
+
+def test_zoo_split_merge_faithful_equals_fast_and_golden(oracle, zoo):
+    g = np.load(os.path.join(G, "zoo_sm_seed7.npz"))
+    c0 = np.zeros(zoo.n, np.int32)
+    for fast in (0, 1):
+        st, res = oracle.run_markov_chain(zoo.codes, zoo.attrisize, zoo.gamma, zoo.v, zoo.w, m=3, iterations=30,
+                                          L=1, c_i=c0, burnin=0, t=10, r=10, neal8=True, split_merge=True,
+                                          seed=7, fast=fast)
+        assert st == 0
+        for k in ("c_i", "total_cls", "loglikelihood", "accepted"):
+            assert np.array_equal(res[k], g[k]), k
+    assert g["accepted"].sum() > 0
+
+
+def test_random_init_with_unused_label_fails_validation(oracle, zoo):
+    # la:28 + cf:146-172: L labels drawn at random; an unused label stops the chain.
+    bad = None
+    for seed in range(1, 60):
+        st0 = oracle.seed_state(seed)
+        u = oracle.runif(st0, zoo.n)
+        if len(np.unique((20 * u + 1).astype(int) - 1)) < 20:
+            bad = seed
+            break
+    assert bad is not None
+    st, _ = oracle.run_markov_chain(zoo.codes, zoo.attrisize, zoo.gamma, zoo.v, zoo.w, m=3, iterations=2, L=20,
+                                    burnin=0, neal8=True, split_merge=False, seed=bad, fast=0)
+    assert st == 1
