@@ -117,6 +117,9 @@ int hdpm_iteration(hdpm_ctx* ctx, const hdpm_chain_params* p, int32_t iter, int3
                    int32_t* accepted, double* loglik);
 
 /* Diagnostics / testing. */
+/* Draw `count` raw 32-bit MT outputs (MT_genrand before scaling) on the device and advance
+ * the context stream past them (same values as `count` host draws). */
+int hdpm_rng_fill_device(hdpm_ctx* ctx, int64_t count, uint32_t* out);
 int hdpm_get_stats(const hdpm_ctx* ctx, hdpm_stats* out);
 int hdpm_reset_stats(hdpm_ctx* ctx);
 /* mode bit 0: evaluate every point on the exact path (no certainty shortcut). */

@@ -22,7 +22,7 @@ EXPORTS = (
     "hdpm_set_pool", "hdpm_get_pool", "hdpm_generate_pool", "hdpm_neal8_sweep", "hdpm_update_phi",
     "hdpm_compute_loglikelihood", "hdpm_loglik_matrix", "hdpm_restricted_gibbs", "hdpm_logprobgs_c_i",
     "hdpm_split_and_merge", "hdpm_run_markov_chain", "hdpm_get_stats", "hdpm_reset_stats",
-    "hdpm_set_debug", "hdpm_synchronize", "hdpm_init_chain", "hdpm_iteration",
+    "hdpm_set_debug", "hdpm_synchronize", "hdpm_init_chain", "hdpm_iteration", "hdpm_rng_fill_device",
 )
 
 STATUS = {0: "OK", 1: "E_VALIDATE", 2: "E_GSL", 3: "E_PROB", 4: "E_WALKER", 5: "E_ARG",
@@ -99,6 +99,7 @@ def lib():
         "hdpm_init_chain": ([vp, P(ChainParams), vp], C.c_int),
         "hdpm_iteration": ([vp, P(ChainParams), i32, P(i32), P(i32), P(f64)], C.c_int),
         "hdpm_reset_stats": ([vp], C.c_int),
+        "hdpm_rng_fill_device": ([vp, i64, vp], C.c_int),
         "hdpm_set_debug": ([vp, i32], C.c_int),
         "hdpm_synchronize": ([vp], C.c_int),
     }

@@ -29,6 +29,7 @@ size_t resolve_smem_bytes(int scap, int m);
 hipError_t launch_relabel(int* c, const int* los, int n, hipStream_t s);
 hipError_t launch_hist(const HistArgs& a, hipStream_t s);
 hipError_t launch_loglik(const LoglikArgs& a, hipStream_t s);
+hipError_t launch_mt_gen(const MtGenArgs& a, hipStream_t s);
 hipError_t launch_lmatrix(const uint8_t* codes_t, int n, int d, int nq, ParamTables cl, int K, double* L,
                           int* H, int64_t ldL, hipStream_t s);
 int sm_restricted_gibbs_device(struct Ctx* c, const int32_t* S, int32_t nS, int32_t i1, int32_t i2,
@@ -121,19 +122,39 @@ struct SmWork {
   std::vector<double> h_out;
 };
 
+// A window of the R random stream generated on the device (k_mt_gen), starting at the
+// host stream position start_pos.  Two windows alternate: while a sweep consumes one, the
+// next window is generated from the state where that sweep's draws end, so the device
+// generator runs concurrently with the sweep and the host-side update_phi draws.
+struct RngWindow {
+  DevBuf<uint32_t> raw, arrays, init;
+  PinBuf<uint32_t> h_init;
+  uint64_t start_pos = 0, epoch = ~0ull;
+  int64_t count = 0;
+  int mti0 = 624, nblocks = 0;
+  uint32_t x0[624];
+  hipEvent_t done = nullptr;
+  bool valid = false;
+};
+
 struct Ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t gstream = nullptr;   // random-stream generator
+  RngWindow win[2];
+  int64_t cmax = 1 << 16;          // draws expected between two sweeps (update_phi etc.)
   std::string err;
   hipEvent_t ev[8];
 
   // aux_data
   int n = 0, d = 0, nq = 0, dp = 0, mmax = 0;
+  int wb = 1, W = 1, bw = 0;          // packed bits per attribute, words per row, bound words
   double gamma = 0;
   std::vector<int32_t> att;
   std::vector<double> v, w;
   std::vector<uint8_t> codes;  // row-major n x d
   DevBuf<uint8_t> d_codes_t;
+  DevBuf<uint64_t> d_xpk;             // packed rows (tiled)
   DevBuf<double> d_logn;
   std::vector<double> h_logn;
 
@@ -152,6 +173,7 @@ struct Ctx {
   DevBuf<int> d_c, d_counts, d_sol, d_los, d_src;
   DevBuf<uint8_t> d_slot_codes;
   DevBuf<double> d_slot_tab;
+  DevBuf<uint64_t> d_slot_bnd;
   int scap = 0;
 
   // latent pool
@@ -160,6 +182,7 @@ struct Ctx {
   std::vector<double> h_pool_s;       // P x d
   DevBuf<uint8_t> d_pool_codes;
   DevBuf<double> d_pool_tab;
+  DevBuf<uint64_t> d_pool_bnd;
 
   // sweep scratch
   PinBuf<uint32_t> h_raw;
@@ -167,6 +190,7 @@ struct Ctx {
   DevBuf<double> d_L;
   int Ecap = 0;
   DevBuf<double> d_margin;
+  DevBuf<int> d_rowpos;
   DevBuf<int> d_list, d_cnt;
   DevBuf<ResolveCtl> d_ctl;
   PinBuf<ResolveCtl> h_ctl;
@@ -188,11 +212,91 @@ struct Ctx {
   std::vector<int> sperm;
 
   ~Ctx() {
+    if (gstream) {
+      (void)hipStreamSynchronize(gstream);
+      for (auto& w : win)
+        if (w.done) (void)hipEventDestroy(w.done);
+      (void)hipStreamDestroy(gstream);
+    }
     if (stream) {
       (void)hipStreamSynchronize(stream);
       for (auto& e : ev) (void)hipEventDestroy(e);
       (void)hipStreamDestroy(stream);
     }
+  }
+
+  // ------------------------------------------------------------------ device random stream
+  void launch_window(RngWindow& W, int64_t count) {
+    if (rng.mti == 625) {  // never seeded: R seeds with 4357 (MT_sgenrand) on the first draw
+      uint32_t seed = 4357;
+      for (int i = 0; i < 624; i++) {
+        rng.mt[i] = seed & 0xffff0000u;
+        seed = 69069u * seed + 1u;
+        rng.mt[i] |= (seed & 0xffff0000u) >> 16;
+        seed = 69069u * seed + 1u;
+      }
+      rng.mti = 624;
+    }
+    HIPCHK(hipStreamSynchronize(gstream));  // previous use of W's buffers is complete
+    W.mti0 = rng.mti;
+    std::memcpy(W.x0, rng.mt, sizeof(W.x0));
+    W.start_pos = rng.pos;
+    W.epoch = rng.epoch;
+    const int head = W.mti0 >= 624 ? 0 : 624 - W.mti0;
+    W.nblocks = count > head ? (int)((count - head + 623) / 624) : 0;
+    W.count = count;
+    W.raw.ensure(count);
+    W.arrays.ensure((size_t)std::max(W.nblocks, 1) * 624);
+    W.init.ensure(624);
+    W.h_init.ensure(624);
+    std::memcpy(W.h_init.p, W.x0, sizeof(W.x0));
+    if (!W.done) HIPCHK(hipEventCreateWithFlags(&W.done, hipEventDisableTiming));
+    HIPCHK(hipMemcpyAsync(W.init.p, W.h_init.p, 624 * 4, hipMemcpyHostToDevice, gstream));
+    MtGenArgs a{W.init.p, W.mti0, count, W.raw.p, W.arrays.p, W.nblocks};
+    HIPCHK(launch_mt_gen(a, gstream));
+    HIPCHK(hipEventRecord(W.done, gstream));
+    W.valid = true;
+  }
+
+  bool covers(const RngWindow& W, uint64_t p, int64_t n) const {
+    return W.valid && W.epoch == rng.epoch && W.start_pos <= p && p + n <= W.start_pos + (uint64_t)W.count;
+  }
+
+  // Make the host stream continue at position `target` inside window W.
+  void adopt_state_at(RngWindow& W, uint64_t target) {
+    HIPCHK(hipEventSynchronize(W.done));
+    const uint64_t r = target - W.start_pos;
+    const uint64_t head = W.mti0 >= 624 ? 0 : 624 - W.mti0;
+    if (r < head) {
+      std::memcpy(rng.mt, W.x0, sizeof(W.x0));
+      rng.mti = W.mti0 + (int)r;
+    } else {
+      const uint64_t b = 1 + (r - head) / 624, k = (r - head) % 624;
+      const uint64_t blk = k == 0 ? b - 1 : b;   // at a block edge R keeps mti = 624
+      if (blk == 0) std::memcpy(rng.mt, W.x0, sizeof(W.x0));
+      else HIPCHK(hipMemcpy(rng.mt, W.arrays.p + (blk - 1) * 624, 624 * 4, hipMemcpyDeviceToHost));
+      rng.mti = k == 0 ? 624 : (int)k;
+    }
+    rng.pos = target;
+  }
+
+  // Device pointer to the next n raw draws of the stream; advances the host stream past
+  // them and prefetches the following window.
+  const uint32_t* device_draws(int64_t n) {
+    RngWindow* W = nullptr;
+    for (auto& w : win)
+      if (covers(w, rng.pos, n)) W = &w;
+    if (!W) {
+      if (win[0].valid || win[1].valid) cmax = std::min<int64_t>(cmax * 2, 1 << 26);
+      W = &win[0];
+      launch_window(*W, n + cmax);
+    }
+    HIPCHK(hipStreamWaitEvent(stream, W->done, 0));
+    const uint32_t* p = W->raw.p + (rng.pos - W->start_pos);
+    adopt_state_at(*W, rng.pos + n);
+    RngWindow* other = (W == &win[0]) ? &win[1] : &win[0];
+    launch_window(*other, n + cmax);
+    return p;
   }
 
   // ------------------------------------------------------------------ helpers
@@ -204,6 +308,32 @@ struct Ctx {
     }
   }
 
+  // Bound data of one parameter entry (kernels.hpp, "Bound data per parameter entry").
+  void bounds_for(const uint8_t* cen, const double* tab, uint64_t* out) const {
+    std::memset(out, 0, (size_t)bw * 8);
+    const int F = 64 / wb;
+    long double A = 0.0L;
+    double dmax = 0.0;
+    for (int j = 0; j < d; ++j) {
+      out[j / F] |= (uint64_t)(cen[j] - 1) << ((j % F) * wb);
+      A += (long double)tab[2 * j];
+      dmax = std::max(dmax, tab[2 * j] - tab[2 * j + 1]);
+    }
+    const double delta = dmax > 0 ? dmax / ((1 << kQ) - 1) : 0.0;
+    for (int j = 0; j < d; ++j) {
+      const double dj = tab[2 * j] - tab[2 * j + 1];
+      int q = delta > 0 ? (int)std::floor(dj / delta) : 0;
+      q = std::min(std::max(q, 0), (1 << kQ) - 1);
+      while (q > 0 && delta * q > dj) --q;
+      while (q < (1 << kQ) - 1 && delta * (q + 1) <= dj) ++q;
+      for (int b = 0; b < kQ; ++b)
+        if ((q >> b) & 1) out[W + b * W + j / F] |= 1ull << ((j % F) * wb);
+    }
+    double* sc = reinterpret_cast<double*>(out + (1 + kQ) * W);
+    sc[0] = (double)A;
+    sc[1] = delta;
+  }
+
   void ensure_slots(int need) {
     if (need <= scap) return;
     int nc = std::max(need, std::max(2 * scap, 64));
@@ -213,6 +343,7 @@ struct Ctx {
     d_src.ensure(nc, true, stream);
     d_slot_codes.ensure((size_t)nc * dp, true, stream);
     d_slot_tab.ensure((size_t)nc * 2 * d, true, stream);
+    d_slot_bnd.ensure((size_t)nc * bw, true, stream);
     scap = nc;
   }
 
@@ -221,14 +352,18 @@ struct Ctx {
     ensure_slots(K + 2);
     std::vector<uint8_t> cc((size_t)K * dp);
     std::vector<double> tt((size_t)K * 2 * d);
-    for (int k = 0; k < K; ++k)
+    std::vector<uint64_t> bb((size_t)K * bw);
+    for (int k = 0; k < K; ++k) {
       tables_for(&h_center[(size_t)k * d], &h_sigma[(size_t)k * d], &cc[(size_t)k * dp], &tt[(size_t)k * 2 * d]);
+      bounds_for(&h_center[(size_t)k * d], &tt[(size_t)k * 2 * d], &bb[(size_t)k * bw]);
+    }
     std::vector<int> ident(K);
     for (int k = 0; k < K; ++k) ident[k] = k;
     std::vector<int> minus1(K, -1);
     if (K) {
       HIPCHK(hipMemcpyAsync(d_slot_codes.p, cc.data(), cc.size(), hipMemcpyHostToDevice, stream));
       HIPCHK(hipMemcpyAsync(d_slot_tab.p, tt.data(), tt.size() * 8, hipMemcpyHostToDevice, stream));
+      HIPCHK(hipMemcpyAsync(d_slot_bnd.p, bb.data(), bb.size() * 8, hipMemcpyHostToDevice, stream));
       HIPCHK(hipMemcpyAsync(d_sol.p, ident.data(), K * 4, hipMemcpyHostToDevice, stream));
       HIPCHK(hipMemcpyAsync(d_los.p, ident.data(), K * 4, hipMemcpyHostToDevice, stream));
       HIPCHK(hipMemcpyAsync(d_src.p, minus1.data(), K * 4, hipMemcpyHostToDevice, stream));
@@ -242,10 +377,13 @@ struct Ctx {
   void upload_some(const std::vector<int>& which) {
     std::vector<uint8_t> cc(dp);
     std::vector<double> tt(2 * d);
+    std::vector<uint64_t> bb(bw);
     for (int k : which) {
       tables_for(&h_center[(size_t)k * d], &h_sigma[(size_t)k * d], cc.data(), tt.data());
+      bounds_for(&h_center[(size_t)k * d], tt.data(), bb.data());
       HIPCHK(hipMemcpyAsync(d_slot_codes.p + (size_t)k * dp, cc.data(), dp, hipMemcpyHostToDevice, stream));
       HIPCHK(hipMemcpyAsync(d_slot_tab.p + (size_t)k * 2 * d, tt.data(), 16 * d, hipMemcpyHostToDevice, stream));
+      HIPCHK(hipMemcpyAsync(d_slot_bnd.p + (size_t)k * bw, bb.data(), (size_t)bw * 8, hipMemcpyHostToDevice, stream));
       HIPCHK(hipStreamSynchronize(stream));
     }
   }
@@ -324,6 +462,20 @@ struct Ctx {
       for (int j = 0; j < d; ++j) t[tiled_offset(i, j, nq)] = codes[(size_t)i * d + j];
     d_codes_t.ensure(t.size());
     HIPCHK(hipMemcpyAsync(d_codes_t.p, t.data(), t.size(), hipMemcpyHostToDevice, stream));
+    // packed rows: code-1 in wb bits (wb = smallest power of two with 2^wb >= mmax)
+    wb = mmax <= 2 ? 1 : mmax <= 4 ? 2 : mmax <= 16 ? 4 : 8;
+    const int F = 64 / wb;
+    W = (d + F - 1) / F;
+    bw = bound_words(W);
+    std::vector<uint64_t> xp((size_t)n64 * W, 0);
+    for (int64_t i = 0; i < n; ++i)
+      for (int j = 0; j < d; ++j)
+        xp[packed_offset(i, j / F, W)] |= (uint64_t)(codes[(size_t)i * d + j] - 1) << ((j % F) * wb);
+    d_xpk.ensure(xp.size());
+    HIPCHK(hipMemcpyAsync(d_xpk.p, xp.data(), xp.size() * 8, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    scap = 0;   // slot arrays are re-laid out for the new bound size on next use
+    d_slot_bnd.release();
     h_logn.resize((size_t)n + 2);
     h_logn[0] = -INFINITY;
     for (int k = 1; k < n + 2; ++k) h_logn[k] = std::log((double)k);
@@ -370,14 +522,19 @@ struct Ctx {
   void upload_pool() {
     std::vector<uint8_t> pc((size_t)P * dp, 0);
     std::vector<double> pt((size_t)P * 2 * d);
+    std::vector<uint64_t> pb((size_t)P * bw);
     parallel_for(P, [&](int64_t a, int64_t b) {
-      for (int64_t e = a; e < b; ++e)
+      for (int64_t e = a; e < b; ++e) {
         tables_for(&h_pool_c[(size_t)e * d], &h_pool_s[(size_t)e * d], &pc[(size_t)e * dp], &pt[(size_t)e * 2 * d]);
+        bounds_for(&h_pool_c[(size_t)e * d], &pt[(size_t)e * 2 * d], &pb[(size_t)e * bw]);
+      }
     });
     d_pool_codes.ensure(pc.size());
     d_pool_tab.ensure(pt.size());
+    d_pool_bnd.ensure(pb.size());
     HIPCHK(hipMemcpyAsync(d_pool_codes.p, pc.data(), pc.size(), hipMemcpyHostToDevice, stream));
     HIPCHK(hipMemcpyAsync(d_pool_tab.p, pt.data(), pt.size() * 8, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(d_pool_bnd.p, pb.data(), pb.size() * 8, hipMemcpyHostToDevice, stream));
     HIPCHK(hipStreamSynchronize(stream));
   }
 
@@ -434,17 +591,16 @@ struct Ctx {
     std::vector<uint8_t> old_center = h_center;
     std::vector<double> old_sigma = h_sigma;
 
-    // the sweep's slice of the R stream: m pick uniforms + 1 categorical per point
+    // the sweep's slice of the R stream (m pick uniforms + 1 categorical per point),
+    // generated on the device; the host stream continues after it
     auto tr0 = std::chrono::steady_clock::now();
     const size_t nraw = (size_t)n * (m + 1);
-    h_raw.ensure(nraw);
-    rng.raw_block(h_raw.p, (int64_t)nraw);
-    d_raw.ensure(nraw);
-    HIPCHK(hipMemcpyAsync(d_raw.p, h_raw.p, nraw * 4, hipMemcpyHostToDevice, stream));
+    const uint32_t* d_sweep_raw = device_draws((int64_t)nraw);
     stats.t_rng_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count();
 
     const int nb_max = (n + kBlock - 1) / kBlock;
     d_margin.ensure(n);
+    d_rowpos.ensure(n);
     d_list.ensure((size_t)nb_max * kBlock);
     d_cnt.ensure(nb_max);
     d_ctl.ensure(1);
@@ -467,9 +623,11 @@ struct Ctx {
       pa.c = d_c.p; pa.counts = d_counts.p; pa.slot_of_label = d_sol.p; pa.K = K; pa.S = S;
       pa.slots = ParamTables{d_slot_codes.p, d_slot_tab.p};
       pa.pool = ParamTables{d_pool_codes.p, d_pool_tab.p};
-      pa.P = P; pa.raw = d_raw.p; pa.m = m; pa.logn = d_logn.p; pa.logfac = std::log(gamma / m);
-      pa.thresh = T + 2.0 * dmax;
-      pa.L = d_L.p; pa.ldL = n; pa.margin = d_margin.p; pa.list = d_list.p; pa.cnt = d_cnt.p; pa.p0 = p;
+      pa.P = P; pa.raw = d_sweep_raw; pa.m = m; pa.logn = d_logn.p; pa.logfac = std::log(gamma / m);
+      pa.xpk = d_xpk.p; pa.W = W; pa.wb = wb; pa.slot_bnd = d_slot_bnd.p; pa.pool_bnd = d_pool_bnd.p; pa.bw = bw;
+      pa.thresh = (debug & 1) ? INFINITY : T + 2.0 * dmax;
+      pa.L = d_L.p; pa.rowpos = d_rowpos.p; pa.margin = d_margin.p; pa.list = d_list.p; pa.cnt = d_cnt.p;
+      pa.p0 = p;
       const int nblocks = (n - p + kBlock - 1) / kBlock;
       HIPCHK(hipEventRecord(ev[0], stream));
       HIPCHK(launch_prepass(pa, nblocks, stream));
@@ -480,8 +638,9 @@ struct Ctx {
       ra.n = n; ra.d = d; ra.dp = dp; ra.m = m; ra.P = P;
       ra.c = d_c.p; ra.counts = d_counts.p; ra.slot_of_label = d_sol.p; ra.label_of_slot = d_los.p;
       ra.slot_src = d_src.p; ra.slot_codes = d_slot_codes.p; ra.slot_tab = d_slot_tab.p;
-      ra.pool = pa.pool; ra.raw = d_raw.p; ra.logn = d_logn.p; ra.logfac = pa.logfac;
-      ra.L = d_L.p; ra.ldL = n; ra.S = S; ra.margin = d_margin.p; ra.list = d_list.p; ra.cnt = d_cnt.p;
+      ra.pool = pa.pool; ra.raw = d_sweep_raw; ra.logn = d_logn.p; ra.logfac = pa.logfac;
+      ra.L = d_L.p; ra.rowpos = d_rowpos.p; ra.slot_bnd = d_slot_bnd.p; ra.pool_bnd = d_pool_bnd.p; ra.bw = bw;
+      ra.S = S; ra.margin = d_margin.p; ra.list = d_list.p; ra.cnt = d_cnt.p;
       ra.nblocks = nblocks; ra.p0 = p; ra.T = T; ra.dmax = dmax; ra.scap = scap; ra.K = K;
       ra.nslots = nslots; ra.ctl = d_ctl.p; ra.force_exact = (debug & 1);
       if (resolve_smem_bytes(scap, m) > 160 * 1024) { err = "too many clusters for the resolver (K > ~3000)"; return kArg; }
@@ -786,6 +945,7 @@ int Ctx::run_markov_chain(const hdpm_chain_params* p, const int32_t* c_init, int
 
 // ====================================================================== C ABI
 using hdpm::Ctx;
+using hdpm::HipError;
 
 #define GUARD(body)                                                            \
   try {                                                                        \
@@ -825,6 +985,10 @@ int hdpm_ctx_create(int32_t device, hdpm_ctx** out) {
     return HDPM_E_DEVICE;
   }
   for (auto& e : c->ev) (void)hipEventCreate(&e);
+  if (hipStreamCreateWithFlags(&c->gstream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return HDPM_E_DEVICE;
+  }
   c->rng.set_seed(0);
   *out = reinterpret_cast<hdpm_ctx*>(c);
   return HDPM_OK;
@@ -959,6 +1123,16 @@ int hdpm_iteration(hdpm_ctx* h, const hdpm_chain_params* p, int32_t iter, int32_
   if (accepted) *accepted = acc;
   if (loglik) *loglik = ll;
   return st;
+}
+int hdpm_rng_fill_device(hdpm_ctx* h, int64_t count, uint32_t* out) {
+  CTX();
+  if (count <= 0 || !out) return HDPM_E_ARG;
+  GUARD({
+    const uint32_t* p = ctx->device_draws(count);
+    HIPCHK(hipMemcpyAsync(out, p, (size_t)count * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return HDPM_OK;
+  })
 }
 int hdpm_get_stats(const hdpm_ctx* h, hdpm_stats* out) {
   auto* ctx = reinterpret_cast<const Ctx*>(h);

@@ -118,43 +118,142 @@ __device__ __forceinline__ double ll_lane(const PointCodes<NQR>& x, int d, const
 }
 
 // ------------------------------------------------------------------ prepass
-template <int NQR>
+// Uniform (wave-invariant) load through the constant address space -> scalar loads.
+template <class T>
+__device__ __forceinline__ T ldu(const T* p) {
+  return *(const __attribute__((address_space(4))) T*)p;
+}
+
+template <int WB>
+__device__ __forceinline__ uint64_t mismatch_mask(uint64_t z) {
+  if constexpr (WB == 1) return z;
+  if constexpr (WB == 2) return (z | (z >> 1)) & 0x5555555555555555ull;
+  if constexpr (WB == 4) {
+    z |= z >> 1;
+    z |= z >> 2;
+    return z & 0x1111111111111111ull;
+  }
+  z |= z >> 1;
+  z |= z >> 2;
+  z |= z >> 4;
+  return z & 0x0101010101010101ull;
+}
+
+struct Bounds {
+  double lo, hi;
+};
+
+// ll bounds of a point (packed words x[0..W)) against one entry's bound data `bd`.
+// UNIFORM: bd is wave-invariant (cluster slot) -> scalar loads.
+template <int WB, int WMAX, bool UNIFORM>
+__device__ __forceinline__ Bounds entry_bounds(const uint64_t (&x)[WMAX > 0 ? WMAX : 1], const uint64_t* xg,
+                                               int W, const uint64_t* bd) {
+  int H = 0, Sq = 0;
+  auto word = [&](int q, uint64_t xq) {
+    const uint64_t cq = UNIFORM ? ldu(bd + q) : bd[q];
+    const uint64_t mk = mismatch_mask<WB>(xq ^ cq);
+    H += __popcll(mk);
+#pragma unroll
+    for (int b = 0; b < kQ; ++b) {
+      const uint64_t pl = UNIFORM ? ldu(bd + W + b * W + q) : bd[W + b * W + q];
+      Sq += __popcll(mk & pl) << b;
+    }
+  };
+  if constexpr (WMAX > 0) {
+#pragma unroll
+    for (int q = 0; q < WMAX; ++q)
+      if (q < W) word(q, x[q]);
+  } else {
+    for (int q = 0; q < W; ++q) word(q, xg[q]);
+  }
+  const double A = UNIFORM ? ldu((const double*)(bd + (1 + kQ) * W)) : ((const double*)(bd + (1 + kQ) * W))[0];
+  const double dl = UNIFORM ? ldu((const double*)(bd + (1 + kQ) * W + 1)) : ((const double*)(bd + (1 + kQ) * W))[1];
+  const double pmin = dl * (double)Sq, pmax = dl * (double)(Sq + H);
+  const double eps = kBoundEps * (1.0 + fabs(A) + pmax);
+  return Bounds{A - pmax - eps, A - pmin + eps};
+}
+
+// Bounds-first prepass: every point gets rigorous bounds on its K + m log-weights from
+// Hamming popcounts; only points whose draw is not provably "stay" get exact rows.
+template <int WB, int WMAX>
 __global__ __launch_bounds__(kBlock) void k_prepass(PrepassArgs a) {
   const int tid = threadIdx.x;
   const int64_t i = (int64_t)a.p0 + (int64_t)blockIdx.x * kBlock + tid;
   const bool active = i < a.n;
   const int64_t ii = active ? i : (int64_t)a.n - 1;
-  const int dp = a.nq * 16;
-  PointCodes<NQR> x;
-  x.load(a.codes_t, ii, a.nq);
+  const int W = a.W;
+  uint64_t x[WMAX > 0 ? WMAX : 1];
+  if constexpr (WMAX > 0) {
+#pragma unroll
+    for (int q = 0; q < WMAX; ++q) x[q] = q < W ? a.xpk[packed_offset(ii, q, W)] : 0ull;
+  }
   const int own = a.c[ii];
   const int own_cnt = a.counts[own];
-  double max1 = -INFINITY, max2 = -INFINITY;
+  // dom = argmax of the lower bounds; the margin needs the largest upper bound among the
+  // other entries (top-2 upper bounds with the id of the first)
+  double lb1 = -INFINITY;
   int dom = -1;
+  double ubA = -INFINITY, ubB = -INFINITY;
+  int idA = -1;
+  auto consider = [&](int id, double lo, double hi) {
+    if (lo > lb1) { lb1 = lo; dom = id; }
+    if (hi > ubA) { ubB = ubA; ubA = hi; idA = id; }
+    else if (hi > ubB) { ubB = hi; }
+  };
   for (int l = 0; l < a.K; ++l) {
-    const int s = a.slot_of_label[l];
-    const double ll = ll_uniform<NQR>(x, a.d, a.slots.codes + (int64_t)s * dp,
-                                      a.slots.tab + (int64_t)s * 2 * a.d);
-    if (active) a.L[(int64_t)s * a.ldL + i] = ll;
+    const int s = ldu(a.slot_of_label + l);
+    Bounds b;
+    if constexpr (WMAX > 0) {
+      b = entry_bounds<WB, WMAX, true>(x, nullptr, W, a.slot_bnd + (int64_t)s * a.bw);
+    } else {
+      int H = 0, Sq = 0;
+      const uint64_t* bd = a.slot_bnd + (int64_t)s * a.bw;
+      for (int q = 0; q < W; ++q) {
+        const uint64_t mk = mismatch_mask<WB>(a.xpk[packed_offset(ii, q, W)] ^ ldu(bd + q));
+        H += __popcll(mk);
+        for (int bb = 0; bb < kQ; ++bb) Sq += __popcll(mk & ldu(bd + W + bb * W + q)) << bb;
+      }
+      const double A = ldu((const double*)(bd + (1 + kQ) * W));
+      const double dl = ldu((const double*)(bd + (1 + kQ) * W + 1));
+      const double pmin = dl * (double)Sq, pmax = dl * (double)(Sq + H);
+      const double eps = kBoundEps * (1.0 + fabs(A) + pmax);
+      b = Bounds{A - pmax - eps, A - pmin + eps};
+    }
     const int nz = a.counts[s] - (s == own ? 1 : 0);
-    const double v = nz != 0 ? a.logn[nz] + ll : -INFINITY;
-    if (v > max1) { max2 = max1; max1 = v; dom = s; }
-    else if (v > max2) { max2 = v; }
+    if (nz != 0) {
+      const double lg = a.logn[nz];
+      consider(s, lg + b.lo, lg + b.hi);
+    }
   }
   const uint32_t* raw = a.raw + ii * (a.m + 1);
   for (int l = 0; l < a.m; ++l) {
     const int64_t e = pick_entry(raw[l], a.P);
-    const double ll = ll_lane<NQR>(x, a.d, a.pool.codes + e * dp, a.pool.tab + e * 2 * a.d, nullptr);
-    if (active) a.L[(int64_t)(a.S + l) * a.ldL + i] = ll;
-    const double v = a.logfac + ll;
-    if (v > max1) { max2 = max1; max1 = v; dom = -2 - l; }
-    else if (v > max2) { max2 = v; }
+    const uint64_t* bd = a.pool_bnd + e * a.bw;
+    Bounds b;
+    if constexpr (WMAX > 0) {
+      b = entry_bounds<WB, WMAX, false>(x, nullptr, W, bd);
+    } else {
+      int H = 0, Sq = 0;
+      for (int q = 0; q < W; ++q) {
+        const uint64_t mk = mismatch_mask<WB>(a.xpk[packed_offset(ii, q, W)] ^ bd[q]);
+        H += __popcll(mk);
+        for (int bb = 0; bb < kQ; ++bb) Sq += __popcll(mk & bd[W + bb * W + q]) << bb;
+      }
+      const double A = ((const double*)(bd + (1 + kQ) * W))[0];
+      const double dl = ((const double*)(bd + (1 + kQ) * W))[1];
+      const double pmin = dl * (double)Sq, pmax = dl * (double)(Sq + H);
+      const double eps = kBoundEps * (1.0 + fabs(A) + pmax);
+      b = Bounds{A - pmax - eps, A - pmin + eps};
+    }
+    consider(-2 - l, a.logfac + b.lo, a.logfac + b.hi);
   }
+  const double ub_other = (idA == dom) ? ubB : ubA;
   const bool domown = own_cnt >= 2 && dom == own;
-  const double mg = domown ? max1 - max2 : -INFINITY;
+  const double mg = domown ? lb1 - ub_other : -INFINITY;
   const bool uncertain = active && !(domown && mg > a.thresh);
   if (active) a.margin[i] = mg;
 
+  // ordered compaction of the uncertain points of this block
   __shared__ int s_wcnt[kBlock / kWave];
   const int lane = tid & 63, wv = tid >> 6;
   const unsigned long long bal = __ballot(uncertain);
@@ -167,8 +266,33 @@ __global__ __launch_bounds__(kBlock) void k_prepass(PrepassArgs a) {
     off += w < wv ? s_wcnt[w] : 0;
     tot += s_wcnt[w];
   }
-  if (uncertain) a.list[(int64_t)blockIdx.x * kBlock + off + pre] = (int)i;
+  const int row = blockIdx.x * kBlock + off + pre;
+  if (active) a.rowpos[i] = uncertain ? row : -1;
+  if (uncertain) a.list[row] = (int)i;
   if (tid == 0) a.cnt[blockIdx.x] = tot;
+
+  // exact rows for the uncertain points (reference j order, host tables)
+  if (bal) {
+    const int E = a.S + a.m;
+    const int dp = a.nq * 16;
+    PointCodes<0> xc;
+    xc.load(a.codes_t, ii, a.nq);
+    double* Lr = a.L + (int64_t)row * E;
+    for (int l = 0; l < a.K; ++l) {
+      const int s = ldu(a.slot_of_label + l);
+      if (uncertain) {
+        const double ll = ll_lane<0>(xc, a.d, a.slots.codes + (int64_t)s * dp, a.slots.tab + (int64_t)s * 2 * a.d,
+                                     nullptr);
+        Lr[s] = ll;
+      }
+    }
+    for (int l = 0; l < a.m; ++l) {
+      if (uncertain) {
+        const int64_t e = pick_entry(raw[l], a.P);
+        Lr[a.S + l] = ll_lane<0>(xc, a.d, a.pool.codes + e * dp, a.pool.tab + e * 2 * a.d, nullptr);
+      }
+    }
+  }
 }
 
 // ------------------------------------------------------------------ resolver
@@ -247,20 +371,20 @@ __device__ void dev_revsort(double* a0, int* ib0, int n) {
 }
 
 // Exact n8:40-102 decision for point i.  Returns the drawn index in [0, K+m) or -status.
-__device__ int exact_decision(const ResolveArgs& a, const RState& st, int K, int64_t i, int own) {
+__device__ int exact_decision(const ResolveArgs& a, const RState& st, int K, int64_t i, int own, int row) {
   const int lane = threadIdx.x;
   const int E = K + a.m;
   const bool singleton = st.cnt[own] == 1;
+  const double* Lr = a.L + (int64_t)row * (a.S + a.m);
   for (int e = lane; e < E; e += kWave) {
     double v;
     if (e < K) {
       const int s = st.sol[e];
       const int nz = st.cnt[s] - (s == own ? 1 : 0);
-      v = nz != 0 ? a.logn[nz] + a.L[(int64_t)s * a.ldL + i] : -INFINITY;
+      v = nz != 0 ? a.logn[nz] + Lr[s] : -INFINITY;
     } else {
       const int l = e - K;
-      const double ll = (l == 0 && singleton) ? a.L[(int64_t)own * a.ldL + i]
-                                              : a.L[(int64_t)(a.S + l) * a.ldL + i];
+      const double ll = (l == 0 && singleton) ? Lr[own] : Lr[a.S + l];
       v = a.logfac + ll;
     }
     st.val[e] = v;
@@ -332,6 +456,7 @@ __device__ void copy_pool_params(const ResolveArgs& a, int64_t e, int s) {
   const int dp = a.dp;
   for (int b = lane; b < dp; b += kWave) a.slot_codes[(int64_t)s * dp + b] = a.pool.codes[e * dp + b];
   for (int b = lane; b < 2 * a.d; b += kWave) a.slot_tab[(int64_t)s * 2 * a.d + b] = a.pool.tab[e * 2 * a.d + b];
+  for (int b = lane; b < a.bw; b += kWave) a.slot_bnd[(int64_t)s * a.bw + b] = a.pool_bnd[e * a.bw + b];
 }
 
 __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
@@ -363,10 +488,10 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
   __syncthreads();
 
   // Decide point i exactly and apply n8:107-159.  Returns false to stop the sweep here.
-  auto process = [&](int64_t i) -> bool {
+  auto process = [&](int64_t i, int row) -> bool {
     const int own = a.c[i];
     const int K = S.K;
-    const int pick = exact_decision(a, st, K, i, own);
+    const int pick = exact_decision(a, st, K, i, own, row);
     if (lane == 0) {
       S.exact++;
       if (pick < 0) { S.status = -pick; S.next = (int)i; }
@@ -435,12 +560,25 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
   int64_t start_checked = -1;
   if (!a.force_exact) {
     // LIST mode: only the prepass's uncertain points need work while drift <= dmax.
-    for (int b = 0; b < a.nblocks && go; ++b) {
-      const int nb = a.cnt[b];
-      for (int q = 0; q < nb && go; ++q) {
-        const int64_t i = a.list[(int64_t)b * kBlock + q];
-        go = process(i);
-        if (go && S.dnow > a.dmax) { start_checked = i + 1; go = false; }
+    // 64 block counts per step; only blocks with uncertain points are visited, and each
+    // block's list is fetched 64 entries at a time.
+    for (int b0 = 0; b0 < a.nblocks && go; b0 += kWave) {
+      const int cb = (b0 + lane < a.nblocks) ? a.cnt[b0 + lane] : 0;
+      unsigned long long nz = __ballot(cb > 0);
+      while (nz && go) {
+        const int bl = __ffsll((long long)nz) - 1;
+        nz &= ~(1ull << bl);
+        const int b = b0 + bl;
+        const int nb = __shfl(cb, bl);
+        for (int q0 = 0; q0 < nb && go; q0 += kWave) {
+          const int li = (q0 + lane < nb) ? a.list[(int64_t)b * kBlock + q0 + lane] : 0;
+          const int lim = min(kWave, nb - q0);
+          for (int q = 0; q < lim && go; ++q) {
+            const int64_t i = __shfl(li, q);
+            go = process(i, b * kBlock + q0 + q);
+            if (go && S.dnow > a.dmax) { start_checked = i + 1; go = false; }
+          }
+        }
       }
     }
   } else {
@@ -460,7 +598,16 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
       bool stop = false;
       while (bal) {
         const int q = __ffsll((long long)bal) - 1;
-        if (!process(base + q)) { stop = true; break; }
+        const int row = a.rowpos[base + q];
+        if (row < 0) {
+          // certain at the snapshot but not under the current drift, and no exact row:
+          // stop here and let the host recompute bounds from this point
+          if (lane == 0) { S.restart = 1; S.next = (int)(base + q); }
+          __syncthreads();
+          stop = true;
+          break;
+        }
+        if (!process(base + q, row)) { stop = true; break; }
         // drift may have grown: re-test the remaining lanes
         bool u2 = false;
         if (lane > q && i < a.n) {
@@ -594,23 +741,25 @@ __global__ __launch_bounds__(kBlock) void k_lmatrix(const uint8_t* codes_t, int 
 }
 
 // ------------------------------------------------------------------ launchers
-template <int NQR>
+template <int WB, int WMAX>
 static hipError_t launch_prepass_t(const PrepassArgs& a, int nblocks, hipStream_t s) {
-  hipLaunchKernelGGL(k_prepass<NQR>, dim3(nblocks), dim3(kBlock), 0, s, a);
+  hipLaunchKernelGGL((k_prepass<WB, WMAX>), dim3(nblocks), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 
+template <int WB>
+static hipError_t launch_prepass_w(const PrepassArgs& a, int nblocks, hipStream_t s) {
+  if (a.W <= 4) return launch_prepass_t<WB, 4>(a, nblocks, s);
+  if (a.W <= 16) return launch_prepass_t<WB, 16>(a, nblocks, s);
+  return launch_prepass_t<WB, 0>(a, nblocks, s);
+}
+
 hipError_t launch_prepass(const PrepassArgs& a, int nblocks, hipStream_t s) {
-  switch (a.nq) {
-    case 1: return launch_prepass_t<1>(a, nblocks, s);
-    case 2: return launch_prepass_t<2>(a, nblocks, s);
-    case 3: return launch_prepass_t<3>(a, nblocks, s);
-    case 4: return launch_prepass_t<4>(a, nblocks, s);
-    case 5: return launch_prepass_t<5>(a, nblocks, s);
-    case 6: return launch_prepass_t<6>(a, nblocks, s);
-    case 7: return launch_prepass_t<7>(a, nblocks, s);
-    case 8: return launch_prepass_t<8>(a, nblocks, s);
-    default: return launch_prepass_t<0>(a, nblocks, s);
+  switch (a.wb) {
+    case 1: return launch_prepass_w<1>(a, nblocks, s);
+    case 2: return launch_prepass_w<2>(a, nblocks, s);
+    case 4: return launch_prepass_w<4>(a, nblocks, s);
+    default: return launch_prepass_w<8>(a, nblocks, s);
   }
 }
 
@@ -800,6 +949,58 @@ hipError_t launch_sm_scan(const SmArgs& a, double T, hipStream_t s) {
 hipError_t launch_sm_lpgs(const SmArgs& a, hipStream_t s) {
   if (a.nS == 0) return hipSuccess;
   hipLaunchKernelGGL(k_sm_lpgs, dim3((a.nS + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace hdpm
+
+namespace hdpm {
+
+__device__ __forceinline__ uint32_t mt_f(uint32_t a, uint32_t b, uint32_t c) {
+  return c ^ (((a & 0x80000000u) | (b & 0x7fffffffu)) >> 1) ^ ((b & 1u) ? 0x9908b0dfu : 0u);
+}
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+  y ^= (y >> 11);
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= (y >> 18);
+  return y;
+}
+
+// New value of element k after one in-place twist (R MT_genrand), from the old array only.
+__device__ __forceinline__ uint32_t mt_twist_elem(const uint32_t* o, int k) {
+  auto g1 = [&](int i) { return mt_f(o[i], o[i + 1], o[i + 397]); };            // i < 227
+  auto g2 = [&](int i) { return mt_f(o[i], o[i + 1], g1(i - 227)); };           // 227 <= i < 454
+  if (k < 227) return g1(k);
+  if (k < 454) return g2(k);
+  if (k < 623) return mt_f(o[k], o[k + 1], g2(k - 227));
+  return mt_f(o[623], g1(0), g2(396));
+}
+
+__global__ __launch_bounds__(640) void k_mt_gen(MtGenArgs a) {
+  __shared__ uint32_t buf[2][624];
+  const int t = threadIdx.x;
+  if (t < 624) buf[0][t] = a.init[t];
+  __syncthreads();
+  const int head = a.mti0 >= 624 ? 0 : 624 - a.mti0;
+  for (int r = t; r < head && r < a.count; r += 640) a.out[r] = mt_temper(buf[0][a.mti0 + r]);
+  int cur = 0;
+  for (int b = 1; b <= a.nblocks; ++b) {
+    uint32_t nv = 0;
+    if (t < 624) nv = mt_twist_elem(buf[cur], t);
+    if (t < 624) buf[cur ^ 1][t] = nv;
+    __syncthreads();
+    if (t < 624) {
+      a.arrays[(int64_t)(b - 1) * 624 + t] = nv;
+      const int64_t r = head + (int64_t)(b - 1) * 624 + t;
+      if (r < a.count) a.out[r] = mt_temper(nv);
+    }
+    cur ^= 1;
+  }
+}
+
+hipError_t launch_mt_gen(const MtGenArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_mt_gen, dim3(1), dim3(640), 0, s, a);
   return hipGetLastError();
 }
 

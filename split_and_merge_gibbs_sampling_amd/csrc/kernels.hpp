@@ -21,6 +21,23 @@ struct ParamTables {
   const double* tab;
 };
 
+// Bound data per parameter entry (cluster slot or pool entry), `bw` u64 words:
+//   [0, W)            packed center codes (code - 1 in `wb` bits per attribute)
+//   [W, W + kQ*W)     kQ penalty bit-planes in the same field layout: bit b of
+//                     q_j = floor(|d_j| / delta), d_j = dhamming(mismatch) - dhamming(match)
+//   then A = sum_j dhamming(match) and delta, as doubles.
+// For a point with mismatch mask M:  H = popc(M), Sq = sum_b 2^b popc(M & plane_b), and
+//   A - delta (Sq + H) <= ll <= A - delta Sq   (up to rounding, covered by kBoundEps).
+constexpr int kQ = 4;
+constexpr double kBoundEps = 1e-9;
+
+__host__ __device__ inline int bound_words(int W) { return (((1 + kQ) * W + 2) + 1) & ~1; }
+
+// Packed rows, tiled: word q of point i at ((i/64) * W + q) * 64 + i%64.
+__host__ __device__ inline int64_t packed_offset(int64_t i, int q, int W) {
+  return ((i >> 6) * W + q) * 64 + (i & 63);
+}
+
 struct PrepassArgs {
   const uint8_t* codes_t;
   int n, d, nq;
@@ -31,15 +48,20 @@ struct PrepassArgs {
   int S;                     // slots (columns) at this snapshot
   ParamTables slots;
   ParamTables pool;
+  const uint64_t* xpk;       // packed rows (tiled)
+  int W, wb;                 // packed words per row, bits per attribute
+  const uint64_t* slot_bnd;  // [slot][bw]
+  const uint64_t* pool_bnd;  // [entry][bw]
+  int bw;
   int64_t P;
   const uint32_t* raw;       // R MT raw outputs, (m+1) per point
   int m;
   const double* logn;        // logn[k] = log(k) (glibc), k = 0..n+1
   double logfac;             // log(gamma / m)
   double thresh;             // certainty threshold incl. 2 * drift budget
-  double* L;                 // column-major: L[e * ldL + i], e < S + m
-  int64_t ldL;
-  double* margin;            // per point: margin if dominated by own cluster, else -inf
+  double* L;                 // exact rows of the uncertain points: L[rowpos * (S + m) + e]
+  int* rowpos;               // per point: its row in L, or -1 (certain at the snapshot)
+  double* margin;            // per point: lower bound on the own-cluster margin, or -inf
   int* list;                 // per block: ordered uncertain points
   int* cnt;                  // per block: number of uncertain points
   int p0;
@@ -71,9 +93,12 @@ struct ResolveArgs {
   const uint32_t* raw;
   const double* logn;
   double logfac;
-  const double* L;
-  int64_t ldL;
-  int S;                     // columns of L (slots at snapshot)
+  const double* L;           // rows of uncertain points, S + m entries each
+  const int* rowpos;
+  uint64_t* slot_bnd;
+  const uint64_t* pool_bnd;
+  int bw;
+  int S;                     // slots at the snapshot (L columns 0..S-1; latents at S + l)
   const double* margin;
   const int* list;
   const int* cnt;
@@ -124,6 +149,23 @@ struct SmArgs {
   int n1, n2;                // current (scan) or launch (logprobgs) cluster sizes
   int* out_counts;           // [2] final sizes after the scan
   double* out;               // logprobgs partial (hi, lo) per block
+};
+
+}  // namespace hdpm
+
+namespace hdpm {
+
+// R's Mersenne-Twister stream on the device (one workgroup, one twist per barrier).
+// Output r >= 0 continues the host state (X_0, mti0): the first 624 - mti0 outputs temper
+// X_0[mti0..623]; then block b >= 1 tempers X_b = twist^b(X_0).  Every X_b is exported so
+// the host can adopt the state at any later position.
+struct MtGenArgs {
+  const uint32_t* init;   // X_0 (624 words)
+  int mti0;
+  int64_t count;
+  uint32_t* out;          // count raw outputs
+  uint32_t* arrays;       // X_1..X_nblocks
+  int nblocks;
 };
 
 }  // namespace hdpm

@@ -35,16 +35,22 @@ enum Status : int {
 struct Rng {
   int32_t mti = 625;
   uint32_t mt[624];
+  uint64_t pos = 0;     // outputs drawn since the last (re)seed
+  uint64_t epoch = 0;   // bumped whenever the state is replaced from outside
 
   void set_seed(uint32_t seed) {  // RNG_Init(MERSENNE_TWISTER, seed) + FixupSeeds
     for (int j = 0; j < 50; j++) seed = 69069u * seed + 1u;
     seed = 69069u * seed + 1u;  // i_seed[0] (dummy[0]) is overwritten by FixupSeeds
     for (int j = 0; j < 624; j++) { seed = 69069u * seed + 1u; mt[j] = seed; }
     mti = 624;
+    pos = 0;
+    epoch++;
   }
   void import625(const int32_t* s) {
     mti = s[0];
     for (int i = 0; i < 624; i++) mt[i] = (uint32_t)s[i + 1];
+    pos = 0;
+    epoch++;
   }
   void export625(int32_t* s) const {
     s[0] = mti;
@@ -80,6 +86,7 @@ struct Rng {
       }
       twist();
     }
+    pos++;
     uint32_t y = mt[mti++];
     y ^= (y >> 11);
     y ^= (y << 7) & 0x9d2c5680u;

@@ -79,6 +79,12 @@ class Engine:
         s = _i32(s)
         self._check(self._L.hdpm_rng_set_state(self._h, ptr(s)))
 
+    def rng_fill_device(self, count: int) -> np.ndarray:
+        """`count` raw MT outputs generated on the device (advances the stream)."""
+        out = np.zeros(count, np.uint32)
+        self._check(self._L.hdpm_rng_fill_device(self._h, int(count), ptr(out)))
+        return out
+
     def set_state(self, c_i, centers, sigma):
         c = _i32(c_i)
         cen, sig = _f64(centers), _f64(sigma)

@@ -267,3 +267,19 @@ def test_large_sweep_invariants(hd):
     ll = eng.compute_loglikelihood()
     assert np.isfinite(ll) and ll < 0
     eng.close()
+
+
+# ------------------------------------------------------------------ device random stream
+@pytest.mark.parametrize("pre", [0, 1, 623, 624, 1000, 5000])
+def test_device_mt_stream_matches_r(hd, oracle, zoo, pre):
+    eng = make_engine(hd, zoo)
+    st = oracle.seed_state(77)
+    oracle.runif(st, pre)                      # start mid-block
+    eng.rng_state = st
+    for count in (1, 623, 624, 625, 20000):
+        got = eng.rng_fill_device(count)
+        ref = oracle.runif(st, count)
+        u = got.astype(np.float64) * 2.3283064365386963e-10
+        assert np.array_equal(u, ref)           # no 0 draws in these ranges: fixup inactive
+        assert np.array_equal(eng.rng_state, st)
+    eng.close()
