@@ -28,11 +28,20 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-def prepass_bytes_per_point(d: int, m: int, k: int) -> int:
-    """Algorithmic bytes k_prepass moves per point ('Roofline'): the point's
-    codes (D), m latent gathers of a u8 center row plus one f64 per attribute (9D each,
-    SURVEY.md 8(d)), its L row (8(K+m)), margin (8) and label (4)."""
-    return d * (1 + 9 * m) + 8 * (k + m) + 12
+def packed_layout(d: int, mmax: int):
+    """(bits per attribute, packed words per row, bound words per entry) as in csrc."""
+    wb = 1 if mmax <= 2 else 2 if mmax <= 4 else 4 if mmax <= 16 else 8
+    W = -(-d * wb // 64)
+    bw = ((1 + 4) * W + 2 + 1) & ~1
+    return wb, W, bw
+
+
+def prepass_bytes_per_point(d: int, mmax: int, m: int) -> int:
+    """Compulsory bytes k_prepass moves per point ('Roofline'): its packed row
+    (8W), its m+1 raw draws (4(m+1)), its label (4), the bound data of its m latent pool
+    picks (8*bw each), its margin (8) and row index (4)."""
+    _, W, bw = packed_layout(d, mmax)
+    return 8 * W + 4 * (m + 1) + 4 + m * 8 * bw + 12
 
 
 def survey_sweep_bytes(n: int, d: int, m: int) -> int:
@@ -183,7 +192,7 @@ def main():
     K = int(cen.shape[0])
 
     value = ws * args.steps / elapsed
-    bpp = prepass_bytes_per_point(ds.d, args.m, K)
+    bpp = prepass_bytes_per_point(ds.d, int(ds.attrisize.max()), args.m)
     pre_ms = st["t_prepass_ms"]
     achieved = (bpp * st["prepass_points"] / 1e9) / (pre_ms / 1e3) if pre_ms > 0 else None
     launches = max(st["rounds"], 1)
@@ -211,8 +220,8 @@ def main():
             "sweep_effective_GBps": round(survey_sweep_bytes(ds.n, ds.d, args.m) * args.steps / elapsed / 1e9, 2),
             "setup_s": round(setup_s, 1),
             "breakdown_ms_per_step": {k: round(st[k] / args.steps, 4) for k in
-                                      ("t_prepass_ms", "t_resolve_ms", "t_stats_ms", "t_host_phi_ms", "t_rng_ms",
-                                       "t_loglik_ms")},
+                                      ("t_prepass_ms", "t_exact_ms", "t_resolve_ms", "t_stats_ms", "t_host_phi_ms",
+                                       "t_rng_ms", "t_loglik_ms")},
             "exact_points_per_step": st["exact_points"] / args.steps,
             "rounds_per_step": st["rounds"] / args.steps,
         },

@@ -47,7 +47,7 @@ typedef struct {
 /* Per-context counters (cumulative since hdpm_ctx_create or hdpm_reset_stats). */
 typedef struct {
     int64_t sweeps, rounds, restarts, exact_points, moves, checked_rounds, prepass_points;
-    double  t_prepass_ms, t_resolve_ms, t_stats_ms, t_host_phi_ms, t_rng_ms, t_loglik_ms;
+    double  t_prepass_ms, t_resolve_ms, t_stats_ms, t_host_phi_ms, t_rng_ms, t_loglik_ms, t_exact_ms;
 } hdpm_stats;
 
 int         hdpm_device_count(void);

@@ -45,7 +45,8 @@ class Stats(C.Structure):
     _fields_ = [(n, C.c_int64) for n in (
         "sweeps", "rounds", "restarts", "exact_points", "moves", "checked_rounds", "prepass_points")] + \
         [(n, C.c_double) for n in (
-            "t_prepass_ms", "t_resolve_ms", "t_stats_ms", "t_host_phi_ms", "t_rng_ms", "t_loglik_ms")]
+            "t_prepass_ms", "t_resolve_ms", "t_stats_ms", "t_host_phi_ms", "t_rng_ms", "t_loglik_ms",
+            "t_exact_ms")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -25,6 +25,7 @@ namespace hdpm {
 
 hipError_t launch_prepass(const PrepassArgs& a, int nblocks, hipStream_t s);
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s);
+hipError_t launch_exact_rows(const PrepassArgs& a, int nblocks, hipStream_t s);
 size_t resolve_smem_bytes(int scap, int m);
 hipError_t launch_relabel(int* c, const int* los, int n, hipStream_t s);
 hipError_t launch_hist(const HistArgs& a, hipStream_t s);
@@ -131,7 +132,8 @@ struct RngWindow {
   PinBuf<uint32_t> h_init;
   uint64_t start_pos = 0, epoch = ~0ull;
   int64_t count = 0;
-  int mti0 = 624, nblocks = 0;
+  int mti0 = 624, nblocks = 0, export_from = 1;
+  int64_t export_after = 0;
   uint32_t x0[624];
   hipEvent_t done = nullptr;
   bool valid = false;
@@ -226,7 +228,7 @@ struct Ctx {
   }
 
   // ------------------------------------------------------------------ device random stream
-  void launch_window(RngWindow& W, int64_t count) {
+  void launch_window(RngWindow& W, int64_t count, int64_t export_after = 0) {
     if (rng.mti == 625) {  // never seeded: R seeds with 4357 (MT_sgenrand) on the first draw
       uint32_t seed = 4357;
       for (int i = 0; i < 624; i++) {
@@ -252,14 +254,18 @@ struct Ctx {
     std::memcpy(W.h_init.p, W.x0, sizeof(W.x0));
     if (!W.done) HIPCHK(hipEventCreateWithFlags(&W.done, hipEventDisableTiming));
     HIPCHK(hipMemcpyAsync(W.init.p, W.h_init.p, 624 * 4, hipMemcpyHostToDevice, gstream));
-    MtGenArgs a{W.init.p, W.mti0, count, W.raw.p, W.arrays.p, W.nblocks};
+    // the host adopts states only at or after `export_after` draws into the window
+    W.export_from = (int)std::max<int64_t>(1, (export_after - head) / 624 - 1);
+    W.export_after = export_after;
+    MtGenArgs a{W.init.p, W.mti0, count, W.raw.p, W.arrays.p, W.nblocks, W.export_from};
     HIPCHK(launch_mt_gen(a, gstream));
     HIPCHK(hipEventRecord(W.done, gstream));
     W.valid = true;
   }
 
   bool covers(const RngWindow& W, uint64_t p, int64_t n) const {
-    return W.valid && W.epoch == rng.epoch && W.start_pos <= p && p + n <= W.start_pos + (uint64_t)W.count;
+    return W.valid && W.epoch == rng.epoch && W.start_pos <= p && p + n <= W.start_pos + (uint64_t)W.count &&
+           p + n >= W.start_pos + (uint64_t)W.export_after;
   }
 
   // Make the host stream continue at position `target` inside window W.
@@ -273,6 +279,7 @@ struct Ctx {
     } else {
       const uint64_t b = 1 + (r - head) / 624, k = (r - head) % 624;
       const uint64_t blk = k == 0 ? b - 1 : b;   // at a block edge R keeps mti = 624
+      if (blk != 0 && (int64_t)blk < W.export_from) throw HipError{hipErrorInvalidValue, "rng window export"};
       if (blk == 0) std::memcpy(rng.mt, W.x0, sizeof(W.x0));
       else HIPCHK(hipMemcpy(rng.mt, W.arrays.p + (blk - 1) * 624, 624 * 4, hipMemcpyDeviceToHost));
       rng.mti = k == 0 ? 624 : (int)k;
@@ -289,13 +296,13 @@ struct Ctx {
     if (!W) {
       if (win[0].valid || win[1].valid) cmax = std::min<int64_t>(cmax * 2, 1 << 26);
       W = &win[0];
-      launch_window(*W, n + cmax);
+      launch_window(*W, n, n);
     }
     HIPCHK(hipStreamWaitEvent(stream, W->done, 0));
     const uint32_t* p = W->raw.p + (rng.pos - W->start_pos);
     adopt_state_at(*W, rng.pos + n);
     RngWindow* other = (W == &win[0]) ? &win[1] : &win[0];
-    launch_window(*other, n + cmax);
+    launch_window(*other, n + cmax, n);
     return p;
   }
 
@@ -633,6 +640,8 @@ struct Ctx {
       HIPCHK(launch_prepass(pa, nblocks, stream));
       stats.prepass_points += n - p;
       HIPCHK(hipEventRecord(ev[1], stream));
+      HIPCHK(launch_exact_rows(pa, nblocks, stream));
+      HIPCHK(hipEventRecord(ev[5], stream));
 
       ResolveArgs ra;
       ra.n = n; ra.d = d; ra.dp = dp; ra.m = m; ra.P = P;
@@ -648,10 +657,12 @@ struct Ctx {
       HIPCHK(hipEventRecord(ev[2], stream));
       HIPCHK(hipMemcpyAsync(h_ctl.p, d_ctl.p, sizeof(ResolveCtl), hipMemcpyDeviceToHost, stream));
       HIPCHK(hipStreamSynchronize(stream));
-      float t1 = 0, t2 = 0;
+      float t1 = 0, t2 = 0, t3 = 0;
       HIPCHK(hipEventElapsedTime(&t1, ev[0], ev[1]));
-      HIPCHK(hipEventElapsedTime(&t2, ev[1], ev[2]));
+      HIPCHK(hipEventElapsedTime(&t3, ev[1], ev[5]));
+      HIPCHK(hipEventElapsedTime(&t2, ev[5], ev[2]));
       stats.t_prepass_ms += t1;
+      stats.t_exact_ms += t3;
       stats.t_resolve_ms += t2;
       stats.rounds++;
       const ResolveCtl c = *h_ctl.p;

@@ -14,6 +14,7 @@
 // the reference's.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
 
@@ -271,25 +272,56 @@ __global__ __launch_bounds__(kBlock) void k_prepass(PrepassArgs a) {
   if (uncertain) a.list[row] = (int)i;
   if (tid == 0) a.cnt[blockIdx.x] = tot;
 
-  // exact rows for the uncertain points (reference j order, host tables)
-  if (bal) {
-    const int E = a.S + a.m;
-    const int dp = a.nq * 16;
-    PointCodes<0> xc;
-    xc.load(a.codes_t, ii, a.nq);
-    double* Lr = a.L + (int64_t)row * E;
-    for (int l = 0; l < a.K; ++l) {
-      const int s = ldu(a.slot_of_label + l);
-      if (uncertain) {
-        const double ll = ll_lane<0>(xc, a.d, a.slots.codes + (int64_t)s * dp, a.slots.tab + (int64_t)s * 2 * a.d,
-                                     nullptr);
-        Lr[s] = ll;
+}
+
+// Exact rows of the uncertain points of one prepass block: one wave per point, lanes over
+// attributes.  The per-attribute dhamming values of up to 64 entries are staged in LDS
+// (coalesced loads), then lane e adds entry e's values in attribute order -- the
+// reference's summation order (n8:47-49), so every row is bit-exact.
+__global__ __launch_bounds__(kWave) void k_exact_rows(PrepassArgs a) {
+  const int b = blockIdx.x;
+  const int nb = a.cnt[b];
+  if (nb == 0) return;
+  __shared__ double T[64 * 65];
+  const int lane = threadIdx.x;
+  const int E = a.K + a.m;
+  const int dp = a.nq * 16;
+  for (int q = 0; q < nb; ++q) {
+    const int row = b * kBlock + q;
+    const int64_t i = a.list[row];
+    const uint32_t* raw = a.raw + i * (a.m + 1);
+    double* Lr = a.L + (int64_t)row * (a.S + a.m);
+    for (int e0 = 0; e0 < E; e0 += 64) {
+      const int ne = min(64, E - e0);
+      double acc = 0.0;
+      for (int j0 = 0; j0 < a.d; j0 += 64) {
+        const int j = j0 + lane;
+        const int nj = min(64, a.d - j0);
+        const int x = j < a.d ? a.codes_t[tiled_offset(i, j, a.nq)] : 0;
+        for (int ee = 0; ee < ne; ++ee) {
+          const int e = e0 + ee;
+          const uint8_t* cc;
+          const double* tab;
+          if (e < a.K) {
+            const int s = a.slot_of_label[e];
+            cc = a.slots.codes + (int64_t)s * dp;
+            tab = a.slots.tab + (int64_t)s * 2 * a.d;
+          } else {
+            const int64_t pe = pick_entry(raw[e - a.K], a.P);
+            cc = a.pool.codes + pe * dp;
+            tab = a.pool.tab + pe * 2 * a.d;
+          }
+          if (j < a.d) T[ee * 65 + lane] = tab[2 * j + (x != cc[j] ? 1 : 0)];
+        }
+        __syncthreads();
+        if (lane < ne)
+          for (int jj = 0; jj < nj; ++jj) acc += T[lane * 65 + jj];
+        __syncthreads();
       }
-    }
-    for (int l = 0; l < a.m; ++l) {
-      if (uncertain) {
-        const int64_t e = pick_entry(raw[l], a.P);
-        Lr[a.S + l] = ll_lane<0>(xc, a.d, a.pool.codes + e * dp, a.pool.tab + e * 2 * a.d, nullptr);
+      if (lane < ne) {
+        const int e = e0 + lane;
+        const int col = e < a.K ? a.slot_of_label[e] : a.S + (e - a.K);
+        Lr[col] = acc;
       }
     }
   }
@@ -639,25 +671,44 @@ __global__ void k_relabel(int* c, const int* label_of_slot, int n) {
   if (i < n) c[i] = label_of_slot[c[i]];
 }
 
-// freq[k][j][level-1] = #{i : label_i = k, x_ij = level}.  Each thread owns attribute
-// columns, so the LDS counters need no atomics; one flush of atomics per block.
+// freq[k][j][level-1] = #{i : label_i = k, x_ij = level}.  A block walks its tiles of 64
+// points; each tile's codes and labels are staged in LDS with coalesced loads, then
+// thread t counts attribute column t, so the LDS counters need no atomics; one flush
+// of atomics per block.
 template <typename CT>
-__global__ __launch_bounds__(kBlock) void k_hist_lds(HistArgs a, int points_per_block) {
+__global__ __launch_bounds__(kBlock) void k_hist_lds(HistArgs a, int tiles_per_block) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  CT* h = (CT*)smem;
+  const int dp = a.nq * 16;
+  int* lab = (int*)smem;                                   // 64
+  uint8_t* tile = smem + 256;                              // 64 * dp
+  CT* h = (CT*)(smem + 256 + (((size_t)64 * dp + 15) / 16) * 16);
   const int tid = threadIdx.x;
   const int nent = a.K * a.d * a.mmax;
   for (int e = tid; e < nent; e += kBlock) h[e] = 0;
-  __syncthreads();
-  const int64_t i0 = (int64_t)blockIdx.x * points_per_block;
-  const int64_t i1 = min((int64_t)a.n, i0 + points_per_block);
-  for (int64_t i = i0; i < i1; ++i) {
-    const int k = a.label[i];
-    if (a.mask && !a.mask[k]) continue;
+  const int64_t ntiles = ((int64_t)a.n + 63) / 64;
+  const int64_t t0 = (int64_t)blockIdx.x * tiles_per_block;
+  const int64_t t1 = min(ntiles, t0 + tiles_per_block);
+  for (int64_t t = t0; t < t1; ++t) {
+    __syncthreads();
+    const uint4* src = (const uint4*)(a.codes_t + t * 64 * dp);
+    uint4* dst = (uint4*)tile;
+    for (int v = tid; v < 4 * dp; v += kBlock) dst[v] = src[v];
+    if (tid < 64) {
+      const int64_t i = t * 64 + tid;
+      int k = i < a.n ? a.label[i] : -1;
+      if (k >= 0 && a.mask && !a.mask[k]) k = -1;
+      lab[tid] = k;
+    }
+    __syncthreads();
     for (int j = tid; j < a.d; j += kBlock) {
-      const int x = a.codes_t[tiled_offset(i, j, a.nq)];
-      CT* slot = h + ((int64_t)k * a.d + j) * a.mmax + (x - 1);
-      *slot = (CT)(*slot + 1);
+      const int q = j >> 4, bb = j & 15;
+      for (int p = 0; p < 64; ++p) {
+        const int k = lab[p];
+        if (k < 0) continue;
+        const int x = tile[(q * 64 + p) * 16 + bb];
+        CT* c = h + ((int64_t)k * a.d + j) * a.mmax + (x - 1);
+        *c = (CT)(*c + 1);
+      }
     }
   }
   __syncthreads();
@@ -754,6 +805,11 @@ static hipError_t launch_prepass_w(const PrepassArgs& a, int nblocks, hipStream_
   return launch_prepass_t<WB, 0>(a, nblocks, s);
 }
 
+hipError_t launch_exact_rows(const PrepassArgs& a, int nblocks, hipStream_t s) {
+  hipLaunchKernelGGL(k_exact_rows, dim3(nblocks), dim3(kWave), 0, s, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_prepass(const PrepassArgs& a, int nblocks, hipStream_t s) {
   switch (a.wb) {
     case 1: return launch_prepass_w<1>(a, nblocks, s);
@@ -780,12 +836,16 @@ hipError_t launch_relabel(int* c, const int* los, int n, hipStream_t s) {
 
 hipError_t launch_hist(const HistArgs& a, hipStream_t s) {
   const int64_t nent = (int64_t)a.K * a.d * a.mmax;
-  const int ppb = 2048;
-  const int nb = (a.n + ppb - 1) / ppb;
-  if (nent * 4 <= 96 * 1024) {
-    hipLaunchKernelGGL(k_hist_lds<unsigned int>, dim3(nb), dim3(kBlock), nent * 4, s, a, ppb);
-  } else if (nent * 2 <= 150 * 1024) {
-    hipLaunchKernelGGL(k_hist_lds<unsigned short>, dim3(nb), dim3(kBlock), ((nent * 2 + 15) / 16) * 16, s, a, ppb);
+  const int64_t ntiles = ((int64_t)a.n + 63) / 64;
+  const size_t stage = 256 + (((size_t)64 * a.nq * 16 + 15) / 16) * 16;
+  // enough blocks to fill the chip, and at most 1024 tiles (65536 points: u16 counters)
+  const int tpb = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (ntiles + 1023) / 1024));
+  const int nb = (int)((ntiles + tpb - 1) / tpb);
+  if (stage + nent * 4 <= 96 * 1024) {
+    hipLaunchKernelGGL(k_hist_lds<unsigned int>, dim3(nb), dim3(kBlock), stage + nent * 4, s, a, tpb);
+  } else if (stage + nent * 2 <= 150 * 1024) {
+    hipLaunchKernelGGL(k_hist_lds<unsigned short>, dim3(nb), dim3(kBlock), stage + ((nent * 2 + 15) / 16) * 16, s, a,
+                       tpb);
   } else {
     const int64_t nt = (int64_t)a.n * a.nq;
     hipLaunchKernelGGL(k_hist_global, dim3((nt + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
@@ -987,11 +1047,14 @@ __global__ __launch_bounds__(640) void k_mt_gen(MtGenArgs a) {
   int cur = 0;
   for (int b = 1; b <= a.nblocks; ++b) {
     uint32_t nv = 0;
-    if (t < 624) nv = mt_twist_elem(buf[cur], t);
-    if (t < 624) buf[cur ^ 1][t] = nv;
-    __syncthreads();
     if (t < 624) {
-      a.arrays[(int64_t)(b - 1) * 624 + t] = nv;
+      nv = mt_twist_elem(buf[cur], t);
+      buf[cur ^ 1][t] = nv;
+    }
+    // LDS-only barrier: the global stores of earlier blocks stay in flight
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (t < 624) {
+      if (b >= a.export_from) a.arrays[(int64_t)(b - 1) * 624 + t] = nv;
       const int64_t r = head + (int64_t)(b - 1) * 624 + t;
       if (r < a.count) a.out[r] = mt_temper(nv);
     }

@@ -164,8 +164,9 @@ struct MtGenArgs {
   int mti0;
   int64_t count;
   uint32_t* out;          // count raw outputs
-  uint32_t* arrays;       // X_1..X_nblocks
+  uint32_t* arrays;       // X_b for b >= export_from (index b - 1); earlier blocks not stored
   int nblocks;
+  int export_from;
 };
 
 }  // namespace hdpm
