@@ -19,6 +19,7 @@
 
 #include "../../include/hdpm.h"
 #include "kernels.hpp"
+#include "mtjump.hpp"
 #include "rmath.hpp"
 
 namespace hdpm {
@@ -144,6 +145,9 @@ struct Ctx {
   hipStream_t stream = nullptr;
   hipStream_t gstream = nullptr;   // random-stream generator
   RngWindow win[2];
+  // MT jump-ahead for multi-workgroup windows (mtjump.hpp)
+  int mt_G = 0, mt_bpg = 0;
+  DevBuf<uint64_t> d_jpoly;
   int64_t cmax = 1 << 16;          // draws expected between two sweeps (update_phi etc.)
   std::string err;
   hipEvent_t ev[8];
@@ -257,10 +261,47 @@ struct Ctx {
     // the host adopts states only at or after `export_after` draws into the window
     W.export_from = (int)std::max<int64_t>(1, (export_after - head) / 624 - 1);
     W.export_after = export_after;
-    MtGenArgs a{W.init.p, W.mti0, count, W.raw.p, W.arrays.p, W.nblocks, W.export_from};
+    ensure_jump(count);
+    const bool multi = mt_G > 1 && count >= (int64_t)mt_G * 624 * 8;
+    MtGenArgs a{W.init.p, W.mti0, count, W.raw.p, W.arrays.p, W.nblocks, W.export_from,
+                multi ? d_jpoly.p : nullptr, mt_bpg, multi ? mt_G : 1};
     HIPCHK(launch_mt_gen(a, gstream));
     HIPCHK(hipEventRecord(W.done, gstream));
     W.valid = true;
+  }
+
+  // Jump polynomials z^(624 * bpg * g) mod phi for g < G, built once per window size class
+  // and checked on the host against direct twisting.
+  void ensure_jump(int64_t count) {
+    const int G = 64;
+    if (count < (int64_t)G * 624 * 8) return;
+    if (mt_G == G && count <= (int64_t)624 * G * mt_bpg) return;
+    // headroom so later, slightly larger windows (sweep + draws between sweeps) reuse it
+    const int bpg = (int)((count * 5 / 4 + 624 * G - 1) / (624 * G));
+    static const Poly phi = mt_charpoly();
+    if (phi.empty()) return;
+    const Poly pj = poly_xpow((uint64_t)624 * bpg, phi);
+    std::vector<uint64_t> all((size_t)G * 312, 0);
+    Poly p(kPolyWords, 0);
+    p[0] = 1;
+    for (int g = 0; g < G; ++g) {
+      std::memcpy(&all[(size_t)g * 312], p.data(), 312 * 8);
+      if (g + 1 < G) p = poly_mulmod(p, pj, phi);
+    }
+    {  // self-check: jump by one segment == bpg twists
+      Rng r;
+      r.set_seed(20241015u);
+      (void)r.raw();
+      uint32_t jumped[624];
+      Poly p1(all.begin() + 312, all.begin() + 624);
+      mt_jump_host(r.mt, p1, jumped);
+      for (int b = 0; b < bpg; ++b) r.twist();
+      if (std::memcmp(jumped, r.mt, sizeof(jumped)) != 0) return;
+    }
+    d_jpoly.ensure(all.size());
+    HIPCHK(hipMemcpy(d_jpoly.p, all.data(), all.size() * 8, hipMemcpyHostToDevice));
+    mt_G = G;
+    mt_bpg = bpg;
   }
 
   bool covers(const RngWindow& W, uint64_t p, int64_t n) const {

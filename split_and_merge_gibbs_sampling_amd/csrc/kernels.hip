@@ -1062,8 +1062,75 @@ __global__ __launch_bounds__(640) void k_mt_gen(MtGenArgs a) {
   }
 }
 
+// G workgroups; workgroup g jumps 624 * bpg * g words ahead of X_0 with one GF(2)
+// correlation of the next 33 blocks of the stream (mtjump.hpp), then twists its own
+// segment of blocks [g * bpg, (g + 1) * bpg) (the last active one runs to the end).
+__global__ __launch_bounds__(640) void k_mt_gen_multi(MtGenArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  uint32_t* seq = lds;                    // 33 * 624 words (jumping workgroups)
+  uint32_t* buf0 = lds + 33 * 624;        // 2 * 624 words
+  uint32_t* buf1 = buf0 + 624;
+  const int t = threadIdx.x;
+  const int g = blockIdx.x;
+  const int64_t b_last = (a.count - 1 + a.mti0) / 624;      // last block with an output
+  const int64_t b_first = (int64_t)g * a.bpg;
+  if (b_first > b_last) return;
+  const bool last = (g == a.G - 1) || ((int64_t)(g + 1) * a.bpg > b_last);
+  const int64_t b_end = last ? b_last + 1 : (int64_t)(g + 1) * a.bpg;
+  if (g == 0) {
+    if (t < 624) buf0[t] = a.init[t];
+  } else {
+    if (t < 624) seq[t] = t == 0 ? (a.init[0] & 0x80000000u) : a.init[t];
+    for (int blk = 1; blk < 33; ++blk) {
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (t < 624) seq[blk * 624 + t] = mt_twist_elem(seq + (blk - 1) * 624, t);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    uint32_t acc = 0;
+    if (t < 624) {
+      const uint64_t* p = a.jpoly + (int64_t)g * 312;
+      for (int w = 0; w < 312; ++w) {
+        const uint64_t bits = ldu(p + w);
+        const uint32_t* s0 = seq + 64 * w + t;
+#pragma unroll
+        for (int b = 0; b < 64; ++b)
+          if ((bits >> b) & 1u) acc ^= s0[b];
+      }
+      buf0[t] = acc;
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  uint32_t* cur = buf0;
+  uint32_t* nxt = buf1;
+  for (int64_t b = b_first; b < b_end; ++b) {
+    uint32_t nv = 0;
+    if (b > b_first) {
+      if (t < 624) {
+        nv = mt_twist_elem(cur, t);
+        nxt[t] = nv;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      uint32_t* tmp = cur;
+      cur = nxt;
+      nxt = tmp;
+    } else if (t < 624) {
+      nv = cur[t];
+    }
+    if (t < 624) {
+      if (b >= 1 && b >= a.export_from) a.arrays[(b - 1) * 624 + t] = nv;
+      const int64_t r = b * 624 + t - a.mti0;
+      if (r >= 0 && r < a.count) a.out[r] = mt_temper(nv);
+    }
+  }
+}
+
 hipError_t launch_mt_gen(const MtGenArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_mt_gen, dim3(1), dim3(640), 0, s, a);
+  if (a.G > 1 && a.jpoly) {
+    const size_t lds = (size_t)(33 + 2) * 624 * 4;
+    hipLaunchKernelGGL(k_mt_gen_multi, dim3(a.G), dim3(640), lds, s, a);
+  } else {
+    hipLaunchKernelGGL(k_mt_gen, dim3(1), dim3(640), 0, s, a);
+  }
   return hipGetLastError();
 }
 

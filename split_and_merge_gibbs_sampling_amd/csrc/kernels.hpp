@@ -167,6 +167,11 @@ struct MtGenArgs {
   uint32_t* arrays;       // X_b for b >= export_from (index b - 1); earlier blocks not stored
   int nblocks;
   int export_from;
+  // multi-workgroup generation (k_mt_gen_multi): workgroup g starts at block g * bpg from
+  // the jump polynomial jpoly[g] (z^(624 * bpg * g) mod phi, 312 words each)
+  const uint64_t* jpoly;
+  int bpg;
+  int G;
 };
 
 }  // namespace hdpm

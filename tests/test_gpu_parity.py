@@ -283,3 +283,18 @@ def test_device_mt_stream_matches_r(hd, oracle, zoo, pre):
         assert np.array_equal(u, ref)           # no 0 draws in these ranges: fixup inactive
         assert np.array_equal(eng.rng_state, st)
     eng.close()
+
+
+@pytest.mark.parametrize("pre", [0, 311, 624])
+def test_device_mt_stream_jump_ahead_matches_r(hd, oracle, zoo, pre):
+    # windows above 64 * 624 * 8 draws use 64 workgroups started by jump polynomials
+    eng = make_engine(hd, zoo)
+    st = oracle.seed_state(2718)
+    oracle.runif(st, pre)
+    eng.rng_state = st
+    for count in (400_000, 1_234_567):
+        got = eng.rng_fill_device(count)
+        ref = oracle.runif(st, count)
+        assert np.array_equal(got.astype(np.float64) * 2.3283064365386963e-10, ref)
+        assert np.array_equal(eng.rng_state, st)
+    eng.close()
