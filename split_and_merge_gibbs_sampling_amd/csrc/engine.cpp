@@ -282,22 +282,26 @@ struct Ctx {
     if (phi.empty()) return;
     const Poly pj = poly_xpow((uint64_t)624 * bpg, phi);
     std::vector<uint64_t> all((size_t)G * 312, 0);
-    Poly p(kPolyWords, 0);
-    p[0] = 1;
-    for (int g = 0; g < G; ++g) {
+    Poly p = poly_xpow((uint64_t)624 * bpg - 1, phi);   // z^(gJ - 1), g = 1..G-1
+    for (int g = 1; g < G; ++g) {
       std::memcpy(&all[(size_t)g * 312], p.data(), 312 * 8);
       if (g + 1 < G) p = poly_mulmod(p, pj, phi);
     }
-    {  // self-check: jump by one segment == bpg twists
+    {  // self-check on the host: jumps by 1, G/2 and G-1 segments == direct twisting
       Rng r;
       r.set_seed(20241015u);
       (void)r.raw();
-      uint32_t jumped[624];
-      Poly p1(all.begin() + 312, all.begin() + 624);
-      mt_jump_host(r.mt, p1, jumped);
-      for (int b = 0; b < bpg; ++b) r.twist();
-      if (std::memcmp(jumped, r.mt, sizeof(jumped)) != 0) return;
+      Rng q = r;
+      int done = 0;
+      for (int g : {1, G / 2, G - 1}) {
+        uint32_t jumped[624];
+        Poly pg(all.begin() + (size_t)g * 312, all.begin() + (size_t)(g + 1) * 312);
+        mt_jump_host(r.mt, pg, jumped);
+        for (; done < g * bpg; ++done) q.twist();
+        if (std::memcmp(jumped, q.mt, sizeof(jumped)) != 0) return;
+      }
     }
+    HIPCHK(hipStreamSynchronize(gstream));   // no generator may still read d_jpoly
     d_jpoly.ensure(all.size());
     HIPCHK(hipMemcpy(d_jpoly.p, all.data(), all.size() * 8, hipMemcpyHostToDevice));
     mt_G = G;

@@ -1063,7 +1063,8 @@ __global__ __launch_bounds__(640) void k_mt_gen(MtGenArgs a) {
 }
 
 // G workgroups; workgroup g jumps 624 * bpg * g words ahead of X_0 with one GF(2)
-// correlation of the next 33 blocks of the stream (mtjump.hpp), then twists its own
+// correlation (jpoly[g] = z^(624 bpg g - 1) mod phi, offset +1) of the next 33 blocks of
+// the stream (mtjump.hpp), then twists its own
 // segment of blocks [g * bpg, (g + 1) * bpg) (the last active one runs to the end).
 __global__ __launch_bounds__(640) void k_mt_gen_multi(MtGenArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -1091,7 +1092,7 @@ __global__ __launch_bounds__(640) void k_mt_gen_multi(MtGenArgs a) {
       const uint64_t* p = a.jpoly + (int64_t)g * 312;
       for (int w = 0; w < 312; ++w) {
         const uint64_t bits = ldu(p + w);
-        const uint32_t* s0 = seq + 64 * w + t;
+        const uint32_t* s0 = seq + 64 * w + t + 1;
 #pragma unroll
         for (int b = 0; b < 64; ++b)
           if ((bits >> b) & 1u) acc ^= s0[b];

@@ -168,7 +168,7 @@ struct MtGenArgs {
   int nblocks;
   int export_from;
   // multi-workgroup generation (k_mt_gen_multi): workgroup g starts at block g * bpg from
-  // the jump polynomial jpoly[g] (z^(624 * bpg * g) mod phi, 312 words each)
+  // the jump polynomial jpoly[g] (z^(624 * bpg * g - 1) mod phi, 312 words each)
   const uint64_t* jpoly;
   int bpg;
   int G;

@@ -2,9 +2,11 @@
 //
 // R's Mersenne-Twister word sequence obeys x_{t+624} = x_{t+397} ^ f(x_t, x_{t+1}); on the
 // 19937 bits that matter its transition A has the primitive characteristic polynomial
-// phi(z) (degree 19937).  For p(z) = z^J mod phi(z) and any window w_t = (x_t..x_{t+623})
-// whose x_t has its 31 unused low bits cleared,
-//     x_{t+J+k} = XOR_{i : p_i = 1} x_{t+i+k}      (k = 0..623),
+// phi(z) (degree 19937), acting on windows w_t = (x_t..x_{t+623}) modulo the 31 unused low
+// bits of x_t.  With z^J = q(z) phi(z) + p(z), every word of A^J w_t equals the same word of
+// p(A) w_t except the low bits of the first word (error q_0 * garbage), hence, using the
+// polynomial of J - 1 and reading one word further,
+//     x_{t+J+k} = XOR_{i : p_i = 1} x_{t+i+k+1},   p = z^(J-1) mod phi,  k = 0..623,
 // so a generator can start J words ahead of a known state with one GF(2) correlation of
 // the next ~20.6k words (k_mt_gen_multi).  phi is recovered here with Berlekamp-Massey
 // from bit 31 of x_t (bit 0 of x_0 is one of the 31 unused bits); J-step polynomials by
@@ -145,7 +147,8 @@ inline Poly poly_xpow(uint64_t J, const Poly& phi) {
   return r;
 }
 
-// Host reference of the device jump: the window J words ahead of X (a block array).
+// Host reference of the device jump: the window J words ahead of X (a block array),
+// p = z^(J-1) mod phi.
 inline void mt_jump_host(const uint32_t* X, const Poly& p, uint32_t* out) {
   std::vector<uint32_t> seq(33 * 624);
   std::memcpy(seq.data(), X, 624 * 4);
@@ -157,7 +160,7 @@ inline void mt_jump_host(const uint32_t* X, const Poly& p, uint32_t* out) {
   for (int k = 0; k < 624; ++k) {
     uint32_t acc = 0;
     for (int i = 0; i < kMtDeg; ++i)
-      if (poly_bit(p, i)) acc ^= seq[i + k];
+      if (poly_bit(p, i)) acc ^= seq[i + k + 1];
     out[k] = acc;
   }
 }
