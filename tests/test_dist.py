@@ -1,0 +1,91 @@
+"""Multi-process timing harness of bench.py (replicas) on CPU/gloo.
+
+bench.py runs one independent chain per rank; the only collectives are the timing barrier
+and the max over ranks.  These tests run that harness with world_size 2 over gloo.
+"""
+import os
+import socket
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, ws, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(ws), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    import bench
+    ws_, rank_, local_ = bench.dist_env()
+    D = bench.Dist(ws_, rank_, local_, backend="gloo")
+    D.barrier()
+    mx = D.max(float(10 * (rank + 1)))
+    D.barrier()
+    q.put((rank, mx, ws_))
+    D.close()
+
+
+def test_dist_env_defaults(monkeypatch):
+    import bench
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    assert bench.dist_env() == (1, 0, 0)
+    D = bench.Dist(1, 0, 0)
+    D.barrier()
+    assert D.max(3.5) == 3.5
+    D.close()
+
+
+def test_gloo_world2_barrier_and_max():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert codes == [0, 0], codes
+    res = sorted(q.get(timeout=5) for _ in range(2))
+    assert [r[0] for r in res] == [0, 1]
+    assert all(r[1] == 20.0 for r in res)       # max over ranks reaches every rank
+    assert all(r[2] == 2 for r in res)
+
+
+def test_bench_helpers():
+    import bench
+    wb, W, bw = bench.packed_layout(128, 4)
+    assert (wb, W) == (2, 4)
+    assert bw == ((5 * W + 2) + 1) & ~1
+    assert bench.prepass_bytes_per_point(128, 4, 3) == 8 * W + 16 + 4 + 3 * 8 * bw + 12
+    assert bench.survey_sweep_bytes(10, 4, 1) == 10 * (4 * 11 + 8)
+
+
+@pytest.mark.parametrize("rows", [[("k_prepass<2,4>", 1, "FETCH_SIZE", 100.0), ("k_prepass<2,4>", 1, "WRITE_SIZE", 10.0),
+                                   ("k_prepass<2,4>", 2, "FETCH_SIZE", 300.0), ("k_prepass<2,4>", 2, "WRITE_SIZE", 30.0),
+                                   ("k_resolve", 3, "FETCH_SIZE", 5.0)]])
+def test_traffic_from_csv(tmp_path, rows):
+    import bench
+    p = tmp_path / "c.csv"
+    import csv
+    with open(p, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"])
+        for k, d, n, v in rows:
+            w.writerow([d, k, n, v])
+    # (2 * 400 + 40) KiB over 2 dispatches
+    assert bench.traffic_from_csv(str(p)) == round((2 * 400 + 40) * 1024 / 2)
