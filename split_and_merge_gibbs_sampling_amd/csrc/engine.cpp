@@ -7,7 +7,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <cstdlib>
+#include <functional>
+#include <mutex>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -29,7 +34,12 @@ hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s);
 hipError_t launch_exact_rows(const PrepassArgs& a, int nblocks, hipStream_t s);
 size_t resolve_smem_bytes(int scap, int m);
 hipError_t launch_relabel(int* c, const int* los, int n, hipStream_t s);
+hipError_t launch_finish_sweep(int* counts, int* sol, int* los, int* src, int K, int nslots, hipStream_t s);
+hipError_t launch_scatter_clusters(const uint8_t* stage, int nent, int dp, int d, int bw, int full, uint8_t* codes,
+                                   double* tab, uint64_t* bnd, int* counts, int* sol, int* los, int* src,
+                                   hipStream_t s);
 hipError_t launch_hist(const HistArgs& a, hipStream_t s);
+size_t hist_partial_words(const HistArgs& a, int* nbx, int* kc, int* tpb);
 hipError_t launch_loglik(const LoglikArgs& a, hipStream_t s);
 hipError_t launch_mt_gen(const MtGenArgs& a, hipStream_t s);
 hipError_t launch_lmatrix(const uint8_t* codes_t, int n, int d, int nq, ParamTables cl, int K, double* L,
@@ -112,6 +122,116 @@ static void parallel_for(int64_t n, F f) {
     th.emplace_back([=] { f(a, b); });
   }
   for (auto& x : th) x.join();
+}
+
+// Persistent host worker pool for the per-iteration host phases (parameter draws'
+// deterministic parts, table builds).  Workers spin for a short while after a job and
+// then sleep, so back-to-back iterations dispatch in about a microsecond.
+// HDPM_HOST_THREADS sets the number of threads (default min(8, hardware threads)).
+class HostPool {
+ public:
+  static HostPool& get() {
+    static HostPool p;
+    return p;
+  }
+  int threads() const { return (int)th_.size() + 1; }
+  // f(lo, hi) over [0, n) in chunks of `grain`; returns when all chunks are done.
+  template <class F>
+  void run(int64_t n, int64_t grain, F&& f) {
+    if (n <= 0) return;
+    if (th_.empty() || n <= grain) {
+      f((int64_t)0, n);
+      return;
+    }
+    std::lock_guard<std::mutex> serial(run_mu_);
+    while (active_.load(std::memory_order_acquire) != 0) spin_pause();
+    job_ = [&f](int64_t a, int64_t b) { f(a, b); };
+    total_ = n;
+    grain_ = grain;
+    next_.store(0, std::memory_order_relaxed);
+    done_.store(0, std::memory_order_relaxed);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      gen_.fetch_add(1, std::memory_order_release);
+    }
+    cv_.notify_all();
+    work();
+    while (done_.load(std::memory_order_acquire) < total_) spin_pause();
+  }
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+
+ private:
+  HostPool() {
+    int T = 0;
+    if (const char* e = std::getenv("HDPM_HOST_THREADS")) T = std::atoi(e);
+    if (T <= 0) {
+      unsigned h = std::thread::hardware_concurrency();
+      T = (int)std::min<unsigned>(h ? h : 4, 8);
+    }
+    for (int t = 1; t < T; ++t) th_.emplace_back([this] { loop(); });
+  }
+  static void spin_pause() { __builtin_ia32_pause(); }
+  void work() {
+    for (;;) {
+      const int64_t a = next_.fetch_add(grain_, std::memory_order_relaxed);
+      if (a >= total_) break;
+      const int64_t b = std::min(total_, a + grain_);
+      job_(a, b);
+      done_.fetch_add(b - a, std::memory_order_release);
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      auto t0 = std::chrono::steady_clock::now();
+      int polls = 0;
+      for (;;) {
+        active_.fetch_add(1, std::memory_order_acq_rel);
+        const uint64_t g = gen_.load(std::memory_order_acquire);
+        if (g != seen) {
+          seen = g;
+          work();
+          active_.fetch_sub(1, std::memory_order_acq_rel);
+          break;
+        }
+        active_.fetch_sub(1, std::memory_order_acq_rel);
+        if (stop_) return;
+        spin_pause();
+        if (++polls % 256 == 0 &&
+            std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(300)) {
+          std::unique_lock<std::mutex> lk(mu_);
+          cv_.wait(lk, [&] { return stop_ || gen_.load(std::memory_order_acquire) != seen; });
+          if (stop_) return;
+          t0 = std::chrono::steady_clock::now();
+        }
+      }
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex mu_, run_mu_;
+  std::condition_variable cv_;
+  std::atomic<uint64_t> gen_{0};
+  std::atomic<int> active_{0};
+  std::atomic<int64_t> next_{0}, done_{0};
+  int64_t total_ = 0, grain_ = 1;
+  std::function<void(int64_t, int64_t)> job_;
+  std::atomic<bool> stop_{false};
+};
+
+template <class F>
+static void pool_for(int64_t n, F f, int64_t grain = 0) {
+  HostPool& P = HostPool::get();
+  if (grain <= 0) grain = std::max<int64_t>(1, n / (4 * P.threads()));
+  P.run(n, grain, [&](int64_t a, int64_t b) {
+    for (int64_t i = a; i < b; ++i) f((int)i);
+  });
 }
 
 // Device scratch of the split-merge move (split_merge.inl).
@@ -197,16 +317,22 @@ struct Ctx {
   int Ecap = 0;
   DevBuf<double> d_margin;
   DevBuf<int> d_rowpos;
-  DevBuf<int> d_list, d_cnt;
-  DevBuf<ResolveCtl> d_ctl;
-  PinBuf<ResolveCtl> h_ctl;
+  DevBuf<int> d_list, d_cnt, d_dense, d_dense_total;
+  DevBuf<unsigned> d_hist_part;
+  DevBuf<int> d_ctl;                  // ResolveCtl + summary (kernels.hpp)
+  DevBuf<long long> d_rprof;          // resolver phase times (debug mode bit 1)
+  PinBuf<int> h_ctl;
+  // cluster parameter upload staging (UploadLayout)
+  PinBuf<uint8_t> h_stage;
+  DevBuf<uint8_t> d_stage;
+  hipEvent_t ev_stage = nullptr;
 
   // statistics buffers
   DevBuf<unsigned> d_freq;
-  std::vector<unsigned> h_freq;
+  PinBuf<unsigned> h_freq;
   DevBuf<unsigned char> d_mask;
   DevBuf<double> d_partial;
-  std::vector<double> h_partial;
+  PinBuf<double> h_partial;
 
   hdpm_stats stats{};
   int debug = 0;
@@ -227,6 +353,7 @@ struct Ctx {
     if (stream) {
       (void)hipStreamSynchronize(stream);
       for (auto& e : ev) (void)hipEventDestroy(e);
+      if (ev_stage) (void)hipEventDestroy(ev_stage);
       (void)hipStreamDestroy(stream);
     }
   }
@@ -364,12 +491,15 @@ struct Ctx {
   void bounds_for(const uint8_t* cen, const double* tab, uint64_t* out) const {
     std::memset(out, 0, (size_t)bw * 8);
     const int F = 64 / wb;
-    long double A = 0.0L;
-    double dmax = 0.0;
+    long double A = 0.0L, sc = 0.0L;
+    double dmax = 0.0, dmin = INFINITY;
     for (int j = 0; j < d; ++j) {
       out[j / F] |= (uint64_t)(cen[j] - 1) << ((j % F) * wb);
       A += (long double)tab[2 * j];
-      dmax = std::max(dmax, tab[2 * j] - tab[2 * j + 1]);
+      sc += (long double)std::max(std::fabs(tab[2 * j]), std::fabs(tab[2 * j + 1]));
+      const double dj = tab[2 * j] - tab[2 * j + 1];
+      dmax = std::max(dmax, dj);
+      dmin = std::min(dmin, dj);
     }
     const double delta = dmax > 0 ? dmax / ((1 << kQ) - 1) : 0.0;
     for (int j = 0; j < d; ++j) {
@@ -381,9 +511,11 @@ struct Ctx {
       for (int b = 0; b < kQ; ++b)
         if ((q >> b) & 1) out[W + b * W + j / F] |= 1ull << ((j % F) * wb);
     }
-    double* sc = reinterpret_cast<double*>(out + (1 + kQ) * W);
-    sc[0] = (double)A;
-    sc[1] = delta;
+    double* s = reinterpret_cast<double*>(out + (1 + kQ) * W);
+    s[0] = (double)A;
+    s[1] = delta;
+    s[2] = dmin > 0 ? dmin : 0.0;
+    s[3] = (double)sc;
   }
 
   void ensure_slots(int need) {
@@ -399,46 +531,41 @@ struct Ctx {
     scap = nc;
   }
 
+  // Cluster parameters of `which` (nullptr: labels 0..K-1 with counts and identity slot
+  // maps) through the pinned staging buffer: one copy + one scatter kernel, no host wait.
+  void stage_upload(const std::vector<int>* which) {
+    const int nent = which ? (int)which->size() : K;
+    if (nent == 0) return;
+    const UploadLayout L = upload_layout(nent, dp, d, bw);
+    if (!ev_stage) HIPCHK(hipEventCreateWithFlags(&ev_stage, hipEventDisableTiming));
+    HIPCHK(hipEventSynchronize(ev_stage));          // the previous upload has left h_stage
+    h_stage.ensure(L.bytes);
+    d_stage.ensure(L.bytes);
+    uint8_t* st = h_stage.p;
+    auto one = [&](int r) {
+      const int k = which ? (*which)[r] : r;
+      double* tt = (double*)(st + L.off_tab) + (size_t)r * 2 * d;
+      tables_for(&h_center[(size_t)k * d], &h_sigma[(size_t)k * d], st + L.off_codes + (size_t)r * dp, tt);
+      bounds_for(&h_center[(size_t)k * d], tt, (uint64_t*)(st + L.off_bnd) + (size_t)r * bw);
+      ((int*)(st + L.off_counts))[r] = h_counts[k];
+      ((int*)(st + L.off_slot))[r] = k;
+    };
+    pool_for(nent, one);
+    HIPCHK(hipMemcpyAsync(d_stage.p, st, L.bytes, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipEventRecord(ev_stage, stream));
+    HIPCHK(launch_scatter_clusters(d_stage.p, nent, dp, d, bw, which ? 0 : 1, d_slot_codes.p, d_slot_tab.p,
+                                   d_slot_bnd.p, d_counts.p, d_sol.p, d_los.p, d_src.p, stream));
+  }
+
   // Upload label tables, counts and identity slot maps for labels 0..K-1.
   void upload_clusters() {
     ensure_slots(K + 2);
-    std::vector<uint8_t> cc((size_t)K * dp);
-    std::vector<double> tt((size_t)K * 2 * d);
-    std::vector<uint64_t> bb((size_t)K * bw);
-    for (int k = 0; k < K; ++k) {
-      tables_for(&h_center[(size_t)k * d], &h_sigma[(size_t)k * d], &cc[(size_t)k * dp], &tt[(size_t)k * 2 * d]);
-      bounds_for(&h_center[(size_t)k * d], &tt[(size_t)k * 2 * d], &bb[(size_t)k * bw]);
-    }
-    std::vector<int> ident(K);
-    for (int k = 0; k < K; ++k) ident[k] = k;
-    std::vector<int> minus1(K, -1);
-    if (K) {
-      HIPCHK(hipMemcpyAsync(d_slot_codes.p, cc.data(), cc.size(), hipMemcpyHostToDevice, stream));
-      HIPCHK(hipMemcpyAsync(d_slot_tab.p, tt.data(), tt.size() * 8, hipMemcpyHostToDevice, stream));
-      HIPCHK(hipMemcpyAsync(d_slot_bnd.p, bb.data(), bb.size() * 8, hipMemcpyHostToDevice, stream));
-      HIPCHK(hipMemcpyAsync(d_sol.p, ident.data(), K * 4, hipMemcpyHostToDevice, stream));
-      HIPCHK(hipMemcpyAsync(d_los.p, ident.data(), K * 4, hipMemcpyHostToDevice, stream));
-      HIPCHK(hipMemcpyAsync(d_src.p, minus1.data(), K * 4, hipMemcpyHostToDevice, stream));
-      HIPCHK(hipMemcpyAsync(d_counts.p, h_counts.data(), K * 4, hipMemcpyHostToDevice, stream));
-    }
-    HIPCHK(hipStreamSynchronize(stream));
+    stage_upload(nullptr);
     tables_dirty = false;
   }
 
   // Upload tables of the labels in `which` only (after update_phi on a subset).
-  void upload_some(const std::vector<int>& which) {
-    std::vector<uint8_t> cc(dp);
-    std::vector<double> tt(2 * d);
-    std::vector<uint64_t> bb(bw);
-    for (int k : which) {
-      tables_for(&h_center[(size_t)k * d], &h_sigma[(size_t)k * d], cc.data(), tt.data());
-      bounds_for(&h_center[(size_t)k * d], tt.data(), bb.data());
-      HIPCHK(hipMemcpyAsync(d_slot_codes.p + (size_t)k * dp, cc.data(), dp, hipMemcpyHostToDevice, stream));
-      HIPCHK(hipMemcpyAsync(d_slot_tab.p + (size_t)k * 2 * d, tt.data(), 16 * d, hipMemcpyHostToDevice, stream));
-      HIPCHK(hipMemcpyAsync(d_slot_bnd.p + (size_t)k * bw, bb.data(), (size_t)bw * 8, hipMemcpyHostToDevice, stream));
-      HIPCHK(hipStreamSynchronize(stream));
-    }
-  }
+  void upload_some(const std::vector<int>& which) { stage_upload(&which); }
 
   void download_labels() {
     if (host_c_valid) return;
@@ -581,6 +708,7 @@ struct Ctx {
         bounds_for(&h_pool_c[(size_t)e * d], &pt[(size_t)e * 2 * d], &pb[(size_t)e * bw]);
       }
     });
+
     d_pool_codes.ensure(pc.size());
     d_pool_tab.ensure(pt.size());
     d_pool_bnd.ensure(pb.size());
@@ -655,14 +783,16 @@ struct Ctx {
     d_rowpos.ensure(n);
     d_list.ensure((size_t)nb_max * kBlock);
     d_cnt.ensure(nb_max);
-    d_ctl.ensure(1);
-    h_ctl.ensure(1);
+    d_dense.ensure((size_t)nb_max * kBlock);
+    d_dense_total.ensure(1);
 
     int nslots = K;
     int p = 0;
     const double dmax = 0.25;
     while (p < n) {
       ensure_slots(nslots + 2);
+      d_ctl.ensure(8 + 3 * (size_t)scap);
+      h_ctl.ensure(8 + 3 * (size_t)scap);
       const int S = nslots;
       if (S + m > Ecap) {
         Ecap = std::max(S + m, std::max(2 * Ecap, 32));
@@ -677,8 +807,10 @@ struct Ctx {
       pa.pool = ParamTables{d_pool_codes.p, d_pool_tab.p};
       pa.P = P; pa.raw = d_sweep_raw; pa.m = m; pa.logn = d_logn.p; pa.logfac = std::log(gamma / m);
       pa.xpk = d_xpk.p; pa.W = W; pa.wb = wb; pa.slot_bnd = d_slot_bnd.p; pa.pool_bnd = d_pool_bnd.p; pa.bw = bw;
+
       pa.thresh = (debug & 1) ? INFINITY : T + 2.0 * dmax;
       pa.L = d_L.p; pa.rowpos = d_rowpos.p; pa.margin = d_margin.p; pa.list = d_list.p; pa.cnt = d_cnt.p;
+      pa.dense = d_dense.p; pa.dense_total = d_dense_total.p;
       pa.p0 = p;
       const int nblocks = (n - p + kBlock - 1) / kBlock;
       HIPCHK(hipEventRecord(ev[0], stream));
@@ -694,13 +826,19 @@ struct Ctx {
       ra.slot_src = d_src.p; ra.slot_codes = d_slot_codes.p; ra.slot_tab = d_slot_tab.p;
       ra.pool = pa.pool; ra.raw = d_sweep_raw; ra.logn = d_logn.p; ra.logfac = pa.logfac;
       ra.L = d_L.p; ra.rowpos = d_rowpos.p; ra.slot_bnd = d_slot_bnd.p; ra.pool_bnd = d_pool_bnd.p; ra.bw = bw;
-      ra.S = S; ra.margin = d_margin.p; ra.list = d_list.p; ra.cnt = d_cnt.p;
+      ra.S = S; ra.margin = d_margin.p; ra.list = d_list.p; ra.dense = d_dense.p; ra.dense_total = d_dense_total.p;
       ra.nblocks = nblocks; ra.p0 = p; ra.T = T; ra.dmax = dmax; ra.scap = scap; ra.K = K;
-      ra.nslots = nslots; ra.ctl = d_ctl.p; ra.force_exact = (debug & 1);
-      if (resolve_smem_bytes(scap, m) > 160 * 1024) { err = "too many clusters for the resolver (K > ~3000)"; return kArg; }
+      ra.lcap = std::min(scap, nslots + 2);
+      ra.nslots = nslots; ra.ctl = (ResolveCtl*)d_ctl.p; ra.summary = d_ctl.p + 8; ra.force_exact = (debug & 1);
+      ra.prof = nullptr;
+      if (debug & 2) {
+        d_rprof.ensure(16);
+        ra.prof = d_rprof.p;
+      }
+      if (resolve_smem_bytes(ra.lcap, m) > 160 * 1024) { err = "too many clusters for the resolver (K > ~2300)"; return kArg; }
       HIPCHK(launch_resolve(ra, stream));
       HIPCHK(hipEventRecord(ev[2], stream));
-      HIPCHK(hipMemcpyAsync(h_ctl.p, d_ctl.p, sizeof(ResolveCtl), hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipMemcpyAsync(h_ctl.p, d_ctl.p, (8 + 3 * (size_t)scap) * 4, hipMemcpyDeviceToHost, stream));
       HIPCHK(hipStreamSynchronize(stream));
       float t1 = 0, t2 = 0, t3 = 0;
       HIPCHK(hipEventElapsedTime(&t1, ev[0], ev[1]));
@@ -710,7 +848,18 @@ struct Ctx {
       stats.t_exact_ms += t3;
       stats.t_resolve_ms += t2;
       stats.rounds++;
-      const ResolveCtl c = *h_ctl.p;
+      const ResolveCtl c = *(const ResolveCtl*)h_ctl.p;
+      if (debug & 2) {
+        long long tp[16];
+        HIPCHK(hipMemcpy(tp, d_rprof.p, sizeof(tp), hipMemcpyDeviceToHost));
+        std::fprintf(stderr,
+                     "[resolve] init %.2f us, dense %.2f us, row0 %.2f us, batches %.2f us, process %.2f us, "
+                     "land %.2f us, points %lld, total %.2f us\n",
+                     (tp[1] - tp[0]) / 100.0, (tp[2] - tp[1]) / 100.0, 0.0, tp[3] / 100.0, tp[4] / 100.0,
+                     tp[5] / 100.0, tp[6], (tp[7] - tp[0]) / 100.0);
+        std::fprintf(stderr, "[resolve] decision %.2f us: values %.2f, exp %.2f, sums %.2f, reductions %.2f us\n",
+                     tp[12] / 100.0, tp[8] / 100.0, tp[9] / 100.0, tp[10] / 100.0, tp[11] / 100.0);
+      }
       stats.exact_points += c.exact;
       stats.moves += c.moves;
       stats.checked_rounds += c.checked;
@@ -727,14 +876,13 @@ struct Ctx {
       p = c.next;
     }
 
-    // slots -> labels; rebuild per-label parameters and counts
+    // slots -> labels; rebuild per-label parameters and counts from the resolver summary
     auto ts0 = std::chrono::steady_clock::now();
-    std::vector<int> sol(K), cnt(nslots), src(nslots);
-    HIPCHK(hipMemcpyAsync(sol.data(), d_sol.p, (size_t)K * 4, hipMemcpyDeviceToHost, stream));
-    HIPCHK(hipMemcpyAsync(cnt.data(), d_counts.p, (size_t)nslots * 4, hipMemcpyDeviceToHost, stream));
-    HIPCHK(hipMemcpyAsync(src.data(), d_src.p, (size_t)nslots * 4, hipMemcpyDeviceToHost, stream));
+    const int* sol = h_ctl.p + 8;
+    const int* cnt = sol + scap;
+    const int* src = cnt + scap;
     HIPCHK(launch_relabel(d_c.p, d_los.p, n, stream));
-    HIPCHK(hipStreamSynchronize(stream));
+    HIPCHK(launch_finish_sweep(d_counts.p, d_sol.p, d_los.p, d_src.p, K, nslots, stream));
     h_center.assign((size_t)K * d, 0);
     h_sigma.assign((size_t)K * d, 0.0);
     h_counts.assign(K, 0);
@@ -755,17 +903,6 @@ struct Ctx {
     }
     host_c_valid = false;
     tables_dirty = true;
-    // counts per label on the device (slot == label again after the relabel)
-    {
-      std::vector<int> ident(K);
-      for (int k = 0; k < K; ++k) ident[k] = k;
-      if (K) {
-        HIPCHK(hipMemcpyAsync(d_counts.p, h_counts.data(), (size_t)K * 4, hipMemcpyHostToDevice, stream));
-        HIPCHK(hipMemcpyAsync(d_sol.p, ident.data(), (size_t)K * 4, hipMemcpyHostToDevice, stream));
-        HIPCHK(hipMemcpyAsync(d_los.p, ident.data(), (size_t)K * 4, hipMemcpyHostToDevice, stream));
-      }
-      HIPCHK(hipStreamSynchronize(stream));
-    }
     stats.t_stats_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
     stats.sweeps++;
     return kOk;
@@ -776,25 +913,30 @@ struct Ctx {
   void histogram(const std::vector<unsigned char>* mask) {
     const size_t nent = (size_t)K * d * mmax;
     d_freq.ensure(std::max<size_t>(nent, 1));
-    HIPCHK(hipMemsetAsync(d_freq.p, 0, nent * 4, stream));
     HistArgs ha;
     ha.codes_t = d_codes_t.p; ha.n = n; ha.d = d; ha.nq = nq; ha.label = d_c.p;
     ha.mask = nullptr; ha.K = K; ha.mmax = mmax; ha.freq = d_freq.p;
+    ha.xpk = d_xpk.p; ha.W = W; ha.wb = wb;
+    {
+      int nbx, kc, tpb;
+      const size_t pw = hist_partial_words(ha, &nbx, &kc, &tpb);
+      d_hist_part.ensure(std::max<size_t>(pw, 1));
+      ha.partial = pw ? d_hist_part.p : nullptr;
+    }
     if (mask) {
       d_mask.ensure(std::max(K, 1));
       HIPCHK(hipMemcpyAsync(d_mask.p, mask->data(), K, hipMemcpyHostToDevice, stream));
       ha.mask = d_mask.p;
     }
     HIPCHK(launch_hist(ha, stream));
-    h_freq.resize(nent);
-    HIPCHK(hipMemcpyAsync(h_freq.data(), d_freq.p, nent * 4, hipMemcpyDeviceToHost, stream));
+    h_freq.ensure(std::max<size_t>(nent, 1));
+    HIPCHK(hipMemcpyAsync(h_freq.p, d_freq.p, nent * 4, hipMemcpyDeviceToHost, stream));
     HIPCHK(hipStreamSynchronize(stream));
   }
 
   // cf:511-591 with cluster sizes from h_counts and frequencies from the device.
   int update_phi(const int32_t* idx, int nidx) {
     if (!have_state) { err = "no state"; return kArg; }
-    if (tables_dirty) upload_clusters();
     auto t0 = std::chrono::steady_clock::now();
     std::vector<unsigned char> mask(K, nidx == 0 ? 1 : 0);
     for (int q = 0; q < nidx; ++q)
@@ -809,7 +951,7 @@ struct Ctx {
       if (nn == 0) continue;
       uint8_t* cen = &h_center[(size_t)i * d];
       double* sig = &h_sigma[(size_t)i * d];
-      const unsigned* f = &h_freq[(size_t)i * d * mmax];
+      const unsigned* f = &h_freq.p[(size_t)i * d * mmax];
       for (int j = 0; j < d; ++j) {          // compute_prob_centers + center draw
         const int mj = att[j];
         const unsigned* fj = f + (size_t)j * mmax;
@@ -833,7 +975,7 @@ struct Ctx {
       if (st) { err = "norm_const2 - hypergeometric diverging with infinity"; return st; }
       touched.push_back(i);
     }
-    if ((int)touched.size() == K) upload_clusters();
+    if (tables_dirty || (int)touched.size() == K) upload_clusters();
     else upload_some(touched);
     auto t2 = std::chrono::steady_clock::now();
     stats.t_stats_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
@@ -853,8 +995,8 @@ struct Ctx {
     la.cl = ParamTables{d_slot_codes.p, d_slot_tab.p};
     la.partial = d_partial.p;
     HIPCHK(launch_loglik(la, stream));
-    h_partial.resize((size_t)2 * nb);
-    HIPCHK(hipMemcpyAsync(h_partial.data(), d_partial.p, h_partial.size() * 8, hipMemcpyDeviceToHost, stream));
+    h_partial.ensure((size_t)2 * nb);
+    HIPCHK(hipMemcpyAsync(h_partial.p, d_partial.p, (size_t)2 * nb * 8, hipMemcpyDeviceToHost, stream));
     HIPCHK(hipEventRecord(ev[4], stream));
     HIPCHK(hipStreamSynchronize(stream));
     float t = 0;
@@ -862,9 +1004,9 @@ struct Ctx {
     stats.t_loglik_ms += t;
     double hi = 0.0, lo = 0.0;
     for (int b = 0; b < nb; ++b) {
-      const double a = h_partial[2 * b];
+      const double a = h_partial.p[2 * b];
       const double s = hi + a, bb = s - hi;
-      lo += (hi - (s - bb)) + (a - bb) + h_partial[2 * b + 1];
+      lo += (hi - (s - bb)) + (a - bb) + h_partial.p[2 * b + 1];
       hi = s;
     }
     *out = hi + lo;

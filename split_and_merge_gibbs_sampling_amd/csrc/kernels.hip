@@ -176,82 +176,69 @@ __device__ __forceinline__ Bounds entry_bounds(const uint64_t (&x)[WMAX > 0 ? WM
 
 // Bounds-first prepass: every point gets rigorous bounds on its K + m log-weights from
 // Hamming popcounts; only points whose draw is not provably "stay" get exact rows.
+//   own cluster (count >= 2): precise lower bound lo (penalty planes, per-lane record);
+//   other clusters: crude upper bound A - dmin H from the codes alone (scalar loads),
+//     refined with the planes only in waves where some lane's crude bound could still
+//     stop the point from being certain (ub > lo - thresh);
+//   latent entries: precise upper bound from their pool record.
+// margin = lo - max(ub) is a lower bound on how far the own cluster leads every other
+// entry; the point is certain when it exceeds `thresh`.
 template <int WB, int WMAX>
 __global__ __launch_bounds__(kBlock) void k_prepass(PrepassArgs a) {
+  static_assert(WMAX > 0, "register rows");
   const int tid = threadIdx.x;
   const int64_t i = (int64_t)a.p0 + (int64_t)blockIdx.x * kBlock + tid;
   const bool active = i < a.n;
   const int64_t ii = active ? i : (int64_t)a.n - 1;
   const int W = a.W;
-  uint64_t x[WMAX > 0 ? WMAX : 1];
-  if constexpr (WMAX > 0) {
+  uint64_t x[WMAX];
 #pragma unroll
-    for (int q = 0; q < WMAX; ++q) x[q] = q < W ? a.xpk[packed_offset(ii, q, W)] : 0ull;
-  }
+  for (int q = 0; q < WMAX; ++q) x[q] = q < W ? a.xpk[packed_offset(ii, q, W)] : 0ull;
   const int own = a.c[ii];
   const int own_cnt = a.counts[own];
-  // dom = argmax of the lower bounds; the margin needs the largest upper bound among the
-  // other entries (top-2 upper bounds with the id of the first)
-  double lb1 = -INFINITY;
-  int dom = -1;
-  double ubA = -INFINITY, ubB = -INFINITY;
-  int idA = -1;
-  auto consider = [&](int id, double lo, double hi) {
-    if (lo > lb1) { lb1 = lo; dom = id; }
-    if (hi > ubA) { ubB = ubA; ubA = hi; idA = id; }
-    else if (hi > ubB) { ubB = hi; }
-  };
-  for (int l = 0; l < a.K; ++l) {
-    const int s = ldu(a.slot_of_label + l);
-    Bounds b;
-    if constexpr (WMAX > 0) {
-      b = entry_bounds<WB, WMAX, true>(x, nullptr, W, a.slot_bnd + (int64_t)s * a.bw);
-    } else {
-      int H = 0, Sq = 0;
-      const uint64_t* bd = a.slot_bnd + (int64_t)s * a.bw;
-      for (int q = 0; q < W; ++q) {
-        const uint64_t mk = mismatch_mask<WB>(a.xpk[packed_offset(ii, q, W)] ^ ldu(bd + q));
-        H += __popcll(mk);
-        for (int bb = 0; bb < kQ; ++bb) Sq += __popcll(mk & ldu(bd + W + bb * W + q)) << bb;
-      }
-      const double A = ldu((const double*)(bd + (1 + kQ) * W));
-      const double dl = ldu((const double*)(bd + (1 + kQ) * W + 1));
-      const double pmin = dl * (double)Sq, pmax = dl * (double)(Sq + H);
-      const double eps = kBoundEps * (1.0 + fabs(A) + pmax);
-      b = Bounds{A - pmax - eps, A - pmin + eps};
-    }
-    const int nz = a.counts[s] - (s == own ? 1 : 0);
-    if (nz != 0) {
-      const double lg = a.logn[nz];
-      consider(s, lg + b.lo, lg + b.hi);
-    }
-  }
   const uint32_t* raw = a.raw + ii * (a.m + 1);
-  for (int l = 0; l < a.m; ++l) {
-    const int64_t e = pick_entry(raw[l], a.P);
-    const uint64_t* bd = a.pool_bnd + e * a.bw;
-    Bounds b;
-    if constexpr (WMAX > 0) {
-      b = entry_bounds<WB, WMAX, false>(x, nullptr, W, bd);
-    } else {
-      int H = 0, Sq = 0;
-      for (int q = 0; q < W; ++q) {
-        const uint64_t mk = mismatch_mask<WB>(a.xpk[packed_offset(ii, q, W)] ^ bd[q]);
-        H += __popcll(mk);
-        for (int bb = 0; bb < kQ; ++bb) Sq += __popcll(mk & bd[W + bb * W + q]) << bb;
+  const int sc_off = (1 + kQ) * W;   // doubles A, delta, dmin, scale after the planes
+  double mg = -INFINITY;
+  if (own_cnt >= 2) {
+    const double lo = a.logn[own_cnt - 1] + entry_bounds<WB, WMAX, false>(x, nullptr, W, a.slot_bnd + (int64_t)own * a.bw).lo;
+    const double cut = lo - a.thresh;        // an entry whose ub stays below this cannot matter
+    double ubmax = -INFINITY;
+    for (int l = 0; l < a.K; ++l) {
+      const int s = ldu(a.slot_of_label + l);
+      const uint64_t* bd = a.slot_bnd + (int64_t)s * a.bw;
+      uint64_t mk[WMAX];
+      int H = 0;
+#pragma unroll
+      for (int q = 0; q < WMAX; ++q) {
+        mk[q] = q < W ? mismatch_mask<WB>(x[q] ^ ldu(bd + q)) : 0ull;
+        H += __popcll(mk[q]);
       }
-      const double A = ((const double*)(bd + (1 + kQ) * W))[0];
-      const double dl = ((const double*)(bd + (1 + kQ) * W))[1];
-      const double pmin = dl * (double)Sq, pmax = dl * (double)(Sq + H);
-      const double eps = kBoundEps * (1.0 + fabs(A) + pmax);
-      b = Bounds{A - pmax - eps, A - pmin + eps};
+      const double A = ldu((const double*)(bd + sc_off)), dmin = ldu((const double*)(bd + sc_off + 2));
+      const double scale = ldu((const double*)(bd + sc_off + 3));
+      const double lg = a.logn[ldu(a.counts + s)];
+      double ub = lg + (A - dmin * (double)H + kBoundEps * (1.0 + scale));
+      const bool need = s != own && ub > cut;
+      if (__ballot(need)) {
+        int Sq = 0;
+#pragma unroll
+        for (int q = 0; q < WMAX; ++q)
+          if (q < W) {
+#pragma unroll
+            for (int b = 0; b < kQ; ++b) Sq += __popcll(mk[q] & ldu(bd + W + b * W + q)) << b;
+          }
+        const double dl = ldu((const double*)(bd + sc_off + 1));
+        const double pmin = dl * (double)Sq, pmax = dl * (double)(Sq + H);
+        ub = fmin(ub, lg + (A - pmin + kBoundEps * (1.0 + fabs(A) + pmax)));
+      }
+      if (s != own) ubmax = fmax(ubmax, ub);
     }
-    consider(-2 - l, a.logfac + b.lo, a.logfac + b.hi);
+    for (int l = 0; l < a.m; ++l) {
+      const int64_t e = pick_entry(raw[l], a.P);
+      ubmax = fmax(ubmax, a.logfac + entry_bounds<WB, WMAX, false>(x, nullptr, W, a.pool_bnd + e * a.bw).hi);
+    }
+    mg = lo - ubmax;
   }
-  const double ub_other = (idA == dom) ? ubB : ubA;
-  const bool domown = own_cnt >= 2 && dom == own;
-  const double mg = domown ? lb1 - ub_other : -INFINITY;
-  const bool uncertain = active && !(domown && mg > a.thresh);
+  const bool uncertain = active && !(own_cnt >= 2 && mg > a.thresh);
   if (active) a.margin[i] = mg;
 
   // ordered compaction of the uncertain points of this block
@@ -274,20 +261,56 @@ __global__ __launch_bounds__(kBlock) void k_prepass(PrepassArgs a) {
 
 }
 
-// Exact rows of the uncertain points of one prepass block: one wave per point, lanes over
-// attributes.  The per-attribute dhamming values of up to 64 entries are staged in LDS
-// (coalesced loads), then lane e adds entry e's values in attribute order -- the
-// reference's summation order (n8:47-49), so every row is bit-exact.
+// Block offsets of the prepass lists and the dense, index-ordered list of uncertain rows
+// (row = prepass block * kBlock + position), so the serial resolver reads it 64 at a time
+// instead of walking every block count.  One workgroup of 1024 threads.
+constexpr int kScanThreads = 1024;
+__global__ __launch_bounds__(kScanThreads) void k_list_scan(const int* __restrict__ cnt, int nblocks,
+                                                           int* __restrict__ dense, int* __restrict__ total) {
+  __shared__ int s_sum[kScanThreads / kWave];
+  const int tid = threadIdx.x;
+  const int chunk = (nblocks + kScanThreads - 1) / kScanThreads;
+  const int b0 = min(nblocks, tid * chunk), b1 = min(nblocks, b0 + chunk);
+  int mine = 0;
+  for (int b = b0; b < b1; ++b) mine += cnt[b];
+  // block-wide exclusive scan of `mine`
+  const int lane = tid & 63, wv = tid >> 6;
+  int inc = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(inc, o);
+    if (lane >= o) inc += t;
+  }
+  if (lane == 63) s_sum[wv] = inc;
+  __syncthreads();
+  int base = 0, all = 0;
+#pragma unroll
+  for (int w = 0; w < kScanThreads / kWave; ++w) {
+    base += w < wv ? s_sum[w] : 0;
+    all += s_sum[w];
+  }
+  int off = base + inc - mine;
+  for (int b = b0; b < b1; ++b) {
+    const int c = cnt[b];
+    for (int q = 0; q < c; ++q) dense[off + q] = b * kBlock + q;
+    off += c;
+  }
+  if (tid == 0) *total = all;
+}
+
+// Exact rows of the uncertain points: one wave per point (grid-stride over the dense
+// list), lanes over attributes.  The per-attribute dhamming values of up to 64 entries
+// are staged in LDS (coalesced loads), then lane e adds entry e's values in attribute
+// order -- the reference's summation order (n8:47-49), so every row is bit-exact.
 __global__ __launch_bounds__(kWave) void k_exact_rows(PrepassArgs a) {
-  const int b = blockIdx.x;
-  const int nb = a.cnt[b];
-  if (nb == 0) return;
+  const int total = *a.dense_total;
+  if ((int)blockIdx.x >= total) return;
   __shared__ double T[64 * 65];
   const int lane = threadIdx.x;
   const int E = a.K + a.m;
   const int dp = a.nq * 16;
-  for (int q = 0; q < nb; ++q) {
-    const int row = b * kBlock + q;
+  for (int q = blockIdx.x; q < total; q += gridDim.x) {
+    const int row = a.dense[q];
     const int64_t i = a.list[row];
     const uint32_t* raw = a.raw + i * (a.m + 1);
     double* Lr = a.L + (int64_t)row * (a.S + a.m);
@@ -328,23 +351,41 @@ __global__ __launch_bounds__(kWave) void k_exact_rows(PrepassArgs a) {
 }
 
 // ------------------------------------------------------------------ resolver
-// One wave walks the sweep in index order.  State (counts, label<->slot maps) lives in
-// LDS; L rows, margins and the uncertain lists come from the prepass.
+// One wave walks the sweep in index order.  State (counts, label<->slot maps, the log
+// counts logn[cnt] and logn[cnt - 1] per slot) lives in LDS, so a decision touches global
+// memory only for its exact row, which is prefetched one point ahead into an LDS double
+// buffer, and its label / categorical draw, which are loaded 64 points at a time.
+// The resolver is a single wave: LDS ops of one wave complete in order, so a
+// compiler-ordering point plus an LDS wait replaces the workgroup barrier (and, unlike
+// __syncthreads, leaves prefetched global loads in flight).
+__device__ __forceinline__ void wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
 struct RShared {
   int K, nslots, status, next, restart, moves, exact, checked, pick, src, pad0, pad1;
   double dnow, sum;
+  long long tsub[8];   // diagnostics (resolver profiling)
 };
 
 struct RState {
   RShared* sh;
-  int* cnt;     // [scap]
-  int* snap;    // [scap]
-  int* sol;     // [scap] slot_of_label
-  int* los;     // [scap] label_of_slot
+  int lcap, emax;
+  int* cnt;     // [lcap]
+  int* snap;    // [lcap]
+  int* sol;     // [lcap] slot_of_label
+  int* los;     // [lcap] label_of_slot
+  double* l1;   // [lcap] logn[cnt]
+  double* l0;   // [lcap] logn[cnt - 1]
   double* val;  // [emax]
   double* p;    // [emax]
+  double* row;  // [2][emax] exact rows (double buffer)
   int* perm;    // [emax]
 };
+
+__host__ __device__ inline size_t resolve_lds_bytes(int lcap, int m) {
+  const size_t emax = (size_t)lcap + (size_t)m;
+  return 128 + emax * 4 * sizeof(double) + (size_t)lcap * 2 * sizeof(double) + (size_t)lcap * 4 * sizeof(int) +
+         emax * sizeof(int);
+}
 
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
@@ -360,6 +401,13 @@ __device__ __forceinline__ double slot_drift(const RState& st, const double* log
   }
   if (a == 1) return b == 0 ? 0.0 : logn[b];
   return INFINITY;
+}
+
+// lane 0: slot s's count changed -> refresh its log-count cache
+__device__ __forceinline__ void set_count(const RState& st, const double* logn, int s, int c) {
+  st.cnt[s] = c;
+  st.l1[s] = logn[c];
+  st.l0[s] = c > 0 ? logn[c - 1] : -INFINITY;
 }
 
 // Serial revsort (R sort.c) on lane 0.
@@ -402,74 +450,97 @@ __device__ void dev_revsort(double* a0, int* ib0, int n) {
   }
 }
 
-// Exact n8:40-102 decision for point i.  Returns the drawn index in [0, K+m) or -status.
-__device__ int exact_decision(const ResolveArgs& a, const RState& st, int K, int64_t i, int own, int row) {
+__device__ __forceinline__ double readlane_f64(double x, int l) {
+  const uint64_t u = __double_as_longlong(x);
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, l), hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), l);
+  return __longlong_as_double(((uint64_t)hi << 32) | lo);
+}
+
+// Exact n8:40-102 decision for a point whose exact row is Lr (LDS), own slot `own`,
+// categorical uniform rU.  Returns the drawn index in [0, K+m) or -status.
+//
+// Register path (E <= 64 RE): entry e lives in lane e % 64 of register e / 64.  The
+// reference's left-to-right reductions -- the max, sum(probs) (n8:96) and Rcpp
+// FixupProb's sum of the positive entries -- run in index order over readlane'd values,
+// so they round exactly as on the CPU.  The loops run over E rounded up to 8 with padding
+// entries -inf / 0.0, which leave a max or a non-negative running sum unchanged.  Counts,
+// the maximum's position and ties come from ballots.
+template <int RE>
+__device__ int exact_decision_reg(const ResolveArgs& a, const RState& st, int K, const double* Lr, int own, double rU) {
   const int lane = threadIdx.x;
+  K = __builtin_amdgcn_readfirstlane(K);
+  own = __builtin_amdgcn_readfirstlane(own);
   const int E = K + a.m;
+  const int E8 = (E + 7) & ~7;
   const bool singleton = st.cnt[own] == 1;
-  const double* Lr = a.L + (int64_t)row * (a.S + a.m);
-  for (int e = lane; e < E; e += kWave) {
-    double v;
+  const bool prof = a.prof != nullptr;
+  long long ts0 = prof ? wall_clock64() : 0;
+  double pv[RE];
+#pragma unroll
+  for (int r = 0; r < RE; ++r) {
+    const int e = r * kWave + lane;
+    double v = -INFINITY;
     if (e < K) {
       const int s = st.sol[e];
-      const int nz = st.cnt[s] - (s == own ? 1 : 0);
-      v = nz != 0 ? a.logn[nz] + Lr[s] : -INFINITY;
-    } else {
+      // logn[cnt - (s == own)] + ll; logn[0] = -inf covers the emptied singleton
+      v = (s == own ? st.l0[s] : st.l1[s]) + Lr[s];
+    } else if (e < E) {
       const int l = e - K;
-      const double ll = (l == 0 && singleton) ? Lr[own] : Lr[a.S + l];
-      v = a.logfac + ll;
+      v = a.logfac + ((l == 0 && singleton) ? Lr[own] : Lr[a.S + l]);
     }
-    st.val[e] = v;
+    pv[r] = v;
   }
-  __syncthreads();
-  double mx = -INFINITY;
-  for (int e = lane; e < E; e += kWave) mx = fmax(mx, st.val[e]);
-  mx = wave_max(mx);
-  for (int e = lane; e < E; e += kWave) st.p[e] = exp(st.val[e] - mx);   // n8:95
-  __syncthreads();
-  if (lane == 0) {
-    double sum = 0.0;
-    for (int e = 0; e < E; ++e) sum += st.p[e];
-    st.sh->sum = sum;
+  // sequential scans over the (padded) entries; f(acc, value) per entry
+  auto scan = [&](double acc, auto f) -> double {
+#pragma unroll
+    for (int r = 0; r < RE; ++r) {
+      const int lim = min(kWave, E8 - r * kWave);
+      for (int e0 = 0; e0 < lim; e0 += 8) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc = f(acc, readlane_f64(pv[r], e0 + k));
+      }
+    }
+    return acc;
+  };
+  const double mx = scan(-INFINITY, [](double m, double x) { return fmax(m, x); });
+  long long ts1 = prof ? wall_clock64() : 0;
+#pragma unroll
+  for (int r = 0; r < RE; ++r) pv[r] = (r * kWave + lane < E) ? exp(pv[r] - mx) : 0.0;      // n8:95
+  long long ts2 = prof ? wall_clock64() : 0;
+  const double sum = scan(0.0, [](double s, double x) { return s + x; });
+#pragma unroll
+  for (int r = 0; r < RE; ++r) pv[r] = pv[r] / sum;                                             // n8:96
+  const double s2 = scan(0.0, [](double s, double x) { return s + (x > 0 ? x : 0.0); });       // FixupProb
+  long long ts3 = prof ? wall_clock64() : 0;
+  if (prof && lane == 0) {
+    st.sh->tsub[0] += ts1 - ts0;
+    st.sh->tsub[1] += ts2 - ts1;
+    st.sh->tsub[2] += ts3 - ts2;
   }
-  __syncthreads();
-  const double sum = st.sh->sum;
-  for (int e = lane; e < E; e += kWave) st.p[e] = st.p[e] / sum;          // n8:96
-  __syncthreads();
-  // Rcpp FixupProb: sum of the positive entries (the same sequential sum), divide.
-  if (lane == 0) {
-    double s2 = 0.0;
-    for (int e = 0; e < E; ++e) if (st.p[e] > 0) s2 += st.p[e];
-    st.sh->sum = s2;
-  }
-  __syncthreads();
-  const double s2 = st.sh->sum;
   if (!(s2 > 0)) return -3;  // kProb: no positive probability
   int nc = 0;
-  double pmax = -1.0;
-  int amax = 0x7fffffff;
-  for (int e = lane; e < E; e += kWave) {
-    const double q = st.p[e] / s2;
-    st.p[e] = q;
-    nc += ((double)E * q > 0.1) ? 1 : 0;
-    if (q > pmax) { pmax = q; amax = e; }
-  }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    nc += __shfl_xor(nc, o);
-    const double om = __shfl_xor(pmax, o);
-    const int oa = __shfl_xor(amax, o);
-    if (om > pmax || (om == pmax && oa < amax)) { pmax = om; amax = oa; }
+  for (int r = 0; r < RE; ++r) {
+    const bool in = r * kWave + lane < E;
+    pv[r] = in ? pv[r] / s2 : 0.0;
+    nc += __popcll(__ballot(in && (double)E * pv[r] > 0.1));
   }
   if (nc > 200) return -4;  // kWalker
-  int ties = 0;
-  for (int e = lane; e < E; e += kWave) ties += (st.p[e] == pmax) ? 1 : 0;
+  const double pmax = scan(-1.0, [](double m, double x) { return fmax(m, x); });
+  int ties = 0, amax = -1;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) ties += __shfl_xor(ties, o);
-  __syncthreads();
-  const double rU = raw_to_unif(a.raw[i * (a.m + 1) + a.m]);
+  for (int r = 0; r < RE; ++r) {
+    const unsigned long long b = __ballot(r * kWave + lane < E && pv[r] == pmax);
+    ties += __popcll(b);
+    if (amax < 0 && b) amax = r * kWave + __ffsll((long long)b) - 1;
+  }
+  if (prof && lane == 0) st.sh->tsub[3] += wall_clock64() - ts3;
   // Unique maximum drawn: revsort puts it first, cumsum[0] = pmax.
   if (ties == 1 && rU <= pmax) return amax;
+#pragma unroll
+  for (int r = 0; r < RE; ++r)
+    if (r * kWave + lane < E) st.p[r * kWave + lane] = pv[r];
+  wave_sync();
   if (lane == 0) {
     for (int e = 0; e < E; ++e) st.perm[e] = e + 1;
     dev_revsort(st.p, st.perm, E);
@@ -479,8 +550,77 @@ __device__ int exact_decision(const ResolveArgs& a, const RState& st, int K, int
       if (rU <= st.p[j]) break;
     st.sh->pick = st.perm[j] - 1;
   }
-  __syncthreads();
+  wave_sync();
   return st.sh->pick;
+}
+
+// LDS path for more than 256 entries.
+__device__ int exact_decision_lds(const ResolveArgs& a, const RState& st, int K, const double* Lr, int own,
+                                  double rU) {
+  const int lane = threadIdx.x;
+  const int E = K + a.m;
+  const bool singleton = st.cnt[own] == 1;
+  double mx = -INFINITY;
+  for (int e = lane; e < E; e += kWave) {
+    double v;
+    if (e < K) {
+      const int s = st.sol[e];
+      v = (s == own ? st.l0[s] : st.l1[s]) + Lr[s];
+    } else {
+      const int l = e - K;
+      v = a.logfac + ((l == 0 && singleton) ? Lr[own] : Lr[a.S + l]);
+    }
+    st.val[e] = v;
+    mx = fmax(mx, v);
+  }
+  mx = wave_max(mx);
+  for (int e = lane; e < E; e += kWave) st.p[e] = exp(st.val[e] - mx);
+  wave_sync();
+  if (lane == 0) {
+    double sum = 0.0;
+    for (int e = 0; e < E; ++e) sum += st.p[e];
+    st.sh->sum = sum;
+  }
+  wave_sync();
+  const double sum = st.sh->sum;
+  for (int e = lane; e < E; e += kWave) st.p[e] = st.p[e] / sum;
+  wave_sync();
+  if (lane == 0) {
+    double s2 = 0.0;
+    for (int e = 0; e < E; ++e) if (st.p[e] > 0) s2 += st.p[e];
+    st.sh->sum = s2;
+  }
+  wave_sync();
+  const double s2 = st.sh->sum;
+  if (!(s2 > 0)) return -3;
+  int nc = 0;
+  for (int e = lane; e < E; e += kWave) {
+    const double q = st.p[e] / s2;
+    st.p[e] = q;
+    nc += ((double)E * q > 0.1) ? 1 : 0;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) nc += __shfl_xor(nc, o);
+  if (nc > 200) return -4;
+  wave_sync();
+  if (lane == 0) {
+    for (int e = 0; e < E; ++e) st.perm[e] = e + 1;
+    dev_revsort(st.p, st.perm, E);
+    for (int e = 1; e < E; ++e) st.p[e] += st.p[e - 1];
+    int j;
+    for (j = 0; j < E - 1; j++)
+      if (rU <= st.p[j]) break;
+    st.sh->pick = st.perm[j] - 1;
+  }
+  wave_sync();
+  return st.sh->pick;
+}
+
+__device__ int exact_decision(const ResolveArgs& a, const RState& st, int K, const double* Lr, int own, double rU) {
+  const int E = __builtin_amdgcn_readfirstlane(K) + a.m;
+  if (E <= kWave) return exact_decision_reg<1>(a, st, K, Lr, own, rU);
+  if (E <= 4 * kWave) return exact_decision_reg<4>(a, st, K, Lr, own, rU);
+  return exact_decision_lds(a, st, K, Lr, own, rU);
 }
 
 __device__ void copy_pool_params(const ResolveArgs& a, int64_t e, int s) {
@@ -491,39 +631,76 @@ __device__ void copy_pool_params(const ResolveArgs& a, int64_t e, int s) {
   for (int b = lane; b < a.bw; b += kWave) a.slot_bnd[(int64_t)s * a.bw + b] = a.pool_bnd[e * a.bw + b];
 }
 
+// Row prefetch: up to kRowRegs * 64 columns are held in registers while the previous point
+// is decided; wider rows load their tail on arrival.
+constexpr int kRowRegs = 4;
+struct RowPrefetch {
+  double r[kRowRegs];
+  __device__ __forceinline__ void issue(const double* src, int ncol) {
+    const int lane = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < kRowRegs; ++k) {
+      const int c = k * kWave + lane;
+      r[k] = c < ncol ? src[c] : 0.0;
+    }
+  }
+  __device__ __forceinline__ void land(const double* src, int ncol, double* dst) const {
+    const int lane = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < kRowRegs; ++k) {
+      const int c = k * kWave + lane;
+      if (c < ncol) dst[c] = r[k];
+    }
+    for (int c = kRowRegs * kWave + lane; c < ncol; c += kWave) dst[c] = src[c];
+  }
+};
+
 __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x;
   const int scap = a.scap;
-  const int emax = scap + a.m;
   RState st;
+  st.lcap = a.lcap;
+  st.emax = a.lcap + a.m;
   st.sh = (RShared*)smem;
-  st.val = (double*)(smem + 64);
-  st.p = st.val + emax;
-  st.cnt = (int*)(st.p + emax);
-  st.snap = st.cnt + scap;
-  st.sol = st.snap + scap;
-  st.los = st.sol + scap;
-  st.perm = st.los + scap;
+  st.val = (double*)(smem + 128);
+  st.p = st.val + st.emax;
+  st.row = st.p + st.emax;
+  st.l1 = st.row + 2 * st.emax;
+  st.l0 = st.l1 + st.lcap;
+  st.cnt = (int*)(st.l0 + st.lcap);
+  st.snap = st.cnt + st.lcap;
+  st.sol = st.snap + st.lcap;
+  st.los = st.sol + st.lcap;
+  st.perm = st.los + st.lcap;
   RShared& S = *st.sh;
-  for (int s = lane; s < scap; s += kWave) {
+  long long tp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const bool prof = a.prof != nullptr;
+  if (prof) tp[0] = wall_clock64();
+  for (int s = lane; s < st.lcap; s += kWave) {
     const int v = s < a.nslots ? a.counts[s] : 0;
     st.cnt[s] = v;
     st.snap[s] = v;
+    st.l1[s] = a.logn[v];
+    st.l0[s] = v > 0 ? a.logn[v - 1] : -INFINITY;
     st.los[s] = s < a.nslots ? a.label_of_slot[s] : -1;
     st.sol[s] = s < a.K ? a.slot_of_label[s] : -1;
   }
   if (lane == 0) {
     S.K = a.K; S.nslots = a.nslots; S.status = 0; S.next = a.n; S.restart = 0;
     S.moves = 0; S.exact = 0; S.checked = 0; S.dnow = 0.0;
+    for (int k = 0; k < 8; ++k) S.tsub[k] = 0;
   }
-  __syncthreads();
+  wave_sync();
+  const int ncol = a.S + a.m;
 
-  // Decide point i exactly and apply n8:107-159.  Returns false to stop the sweep here.
-  auto process = [&](int64_t i, int row) -> bool {
-    const int own = a.c[i];
+  // Decide point i (exact row in LDS at Lr) and apply n8:107-159.  Returns false to stop
+  // the sweep here.
+  auto process = [&](int64_t i, const double* Lr, int own, uint32_t rawU) -> bool {
     const int K = S.K;
-    const int pick = exact_decision(a, st, K, i, own, row);
+    const long long tq0 = prof ? wall_clock64() : 0;
+    const int pick = exact_decision(a, st, K, Lr, own, raw_to_unif(rawU));
+    if (prof && lane == 0) S.tsub[4] += wall_clock64() - tq0;
     if (lane == 0) {
       S.exact++;
       if (pick < 0) { S.status = -pick; S.next = (int)i; }
@@ -533,7 +710,8 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
           const int ns = st.sol[pick];
           if (st.cnt[own] != 1) {                                   // case 1
             if (ns != own) {
-              a.c[i] = ns; st.cnt[own]--; st.cnt[ns]++; S.moves++;
+              a.c[i] = ns; set_count(st, a.logn, own, st.cnt[own] - 1); set_count(st, a.logn, ns, st.cnt[ns] + 1);
+              S.moves++;
               S.dnow = fmax(S.dnow, fmax(slot_drift(st, a.logn, own), slot_drift(st, a.logn, ns)));
             }
           } else {                                                  // case 2
@@ -543,7 +721,9 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
               target = st.sol[K - 1];
             }
             if (S.status == 0) {
-              a.c[i] = target; st.cnt[own]--; st.cnt[target]++; S.moves++;
+              a.c[i] = target; set_count(st, a.logn, own, st.cnt[own] - 1);
+              set_count(st, a.logn, target, st.cnt[target] + 1);
+              S.moves++;
               const int last = st.sol[K - 1];
               st.los[own] = -1;
               if (ownlab != K - 1) { st.sol[ownlab] = last; st.los[last] = ownlab; }
@@ -556,18 +736,19 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
           const int l = pick - K;
           const bool single = st.cnt[own] == 1;
           if (!single || l != 0) {                                  // case 3 / case 4 (new params)
-            if (S.nslots >= scap) { S.status = 5; S.next = (int)i; }
+            if (S.nslots >= st.lcap || S.nslots >= scap) { S.status = 5; S.next = (int)i; }
             else {
               const int ns = S.nslots;
               S.nslots = ns + 1;
               if (!single) {                                        // case 3
                 st.sol[K] = ns; st.los[ns] = K; S.K = K + 1;
-                st.cnt[own]--;
+                set_count(st, a.logn, own, st.cnt[own] - 1);
               } else {                                              // case 4
                 st.sol[ownlab] = ns; st.los[ns] = ownlab; st.los[own] = -1;
-                st.cnt[own] = 0;
+                set_count(st, a.logn, own, 0);
               }
-              st.cnt[ns] = 1;
+              set_count(st, a.logn, ns, 1);
+              st.snap[ns] = 0;
               a.c[i] = ns;
               S.src = (int)pick_entry(a.raw[i * (a.m + 1) + l], a.P);
               a.slot_src[ns] = S.src;
@@ -580,7 +761,7 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
         }
       }
     }
-    __syncthreads();
+    wave_sync();
     if (S.restart && S.status == 0) {
       const int ns = S.nslots - 1;
       copy_pool_params(a, S.src, ns);
@@ -591,25 +772,50 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
   bool go = true;
   int64_t start_checked = -1;
   if (!a.force_exact) {
-    // LIST mode: only the prepass's uncertain points need work while drift <= dmax.
-    // 64 block counts per step; only blocks with uncertain points are visited, and each
-    // block's list is fetched 64 entries at a time.
-    for (int b0 = 0; b0 < a.nblocks && go; b0 += kWave) {
-      const int cb = (b0 + lane < a.nblocks) ? a.cnt[b0 + lane] : 0;
-      unsigned long long nz = __ballot(cb > 0);
-      while (nz && go) {
-        const int bl = __ffsll((long long)nz) - 1;
-        nz &= ~(1ull << bl);
-        const int b = b0 + bl;
-        const int nb = __shfl(cb, bl);
-        for (int q0 = 0; q0 < nb && go; q0 += kWave) {
-          const int li = (q0 + lane < nb) ? a.list[(int64_t)b * kBlock + q0 + lane] : 0;
-          const int lim = min(kWave, nb - q0);
-          for (int q = 0; q < lim && go; ++q) {
-            const int64_t i = __shfl(li, q);
-            go = process(i, b * kBlock + q0 + q);
-            if (go && S.dnow > a.dmax) { start_checked = i + 1; go = false; }
-          }
+    // LIST mode: only the prepass's uncertain points need work while drift <= dmax; the
+    // dense list, the points' labels and draws are read 64 at a time, and each exact row
+    // is prefetched while the previous point is decided.
+    const int total = *a.dense_total;
+    if (prof) tp[1] = wall_clock64();
+    int buf = 0;
+    RowPrefetch pf;
+    if (total > 0) {
+      const int r0 = a.dense[0];
+      pf.issue(a.L + (int64_t)r0 * ncol, ncol);
+      pf.land(a.L + (int64_t)r0 * ncol, ncol, st.row);
+    }
+    if (prof) tp[2] = wall_clock64();
+    for (int q0 = 0; q0 < total && go; q0 += kWave) {
+      long long tb = prof ? wall_clock64() : 0;
+      const int lim = min(kWave, total - q0);
+      const int rw = lane < lim ? a.dense[q0 + lane] : 0;
+      const int li = lane < lim ? a.list[rw] : 0;
+      const int ci = lane < lim ? a.c[li] : 0;
+      const uint32_t ru = lane < lim ? a.raw[(int64_t)li * (a.m + 1) + a.m] : 0u;
+      const int rnext = (q0 + kWave + lane < total && lane == 0) ? a.dense[q0 + kWave] : 0;
+      const int rn64 = __shfl(rnext, 0);
+      if (prof) { tp[3] += wall_clock64() - tb + 0 * (ci + (int)ru + rn64); }
+      for (int q = 0; q < lim && go; ++q) {
+        long long t0 = prof ? wall_clock64() : 0;
+        // next point's row -> registers (in flight while this point is decided)
+        int rn = -1;
+        if (q + 1 < lim) rn = __shfl(rw, q + 1);
+        else if (q0 + kWave < total) rn = rn64;
+        if (rn >= 0) pf.issue(a.L + (int64_t)rn * ncol, ncol);
+        const int64_t i = __shfl(li, q);
+        go = process(i, st.row + buf * st.emax, __shfl(ci, q), (uint32_t)__shfl((int)ru, q));
+        long long t1 = prof ? wall_clock64() : 0;
+        if (go && S.dnow > a.dmax) { start_checked = i + 1; go = false; }
+        if (go && rn >= 0) {
+          buf ^= 1;
+          pf.land(a.L + (int64_t)rn * ncol, ncol, st.row + buf * st.emax);
+        }
+        if (prof) {
+          wave_sync();
+          const long long t2 = wall_clock64();
+          tp[4] += t1 - t0;
+          tp[5] += t2 - t1;
+          tp[6] += 1;
         }
       }
     }
@@ -622,9 +828,11 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
     for (int64_t base = start_checked; base < a.n; base += kWave) {
       const int64_t i = base + lane;
       bool unc = false;
+      int ci = 0;
       if (i < a.n) {
+        ci = a.c[i];
         const double mg = a.margin[i];
-        unc = a.force_exact || !(mg - 2.0 * S.dnow > a.T && st.cnt[a.c[i]] >= 2);
+        unc = a.force_exact || !(mg - 2.0 * S.dnow > a.T && st.cnt[ci] >= 2);
       }
       unsigned long long bal = __ballot(unc);
       bool stop = false;
@@ -635,16 +843,19 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
           // certain at the snapshot but not under the current drift, and no exact row:
           // stop here and let the host recompute bounds from this point
           if (lane == 0) { S.restart = 1; S.next = (int)(base + q); }
-          __syncthreads();
+          wave_sync();
           stop = true;
           break;
         }
-        if (!process(base + q, row)) { stop = true; break; }
+        const double* src = a.L + (int64_t)row * ncol;
+        for (int c = lane; c < ncol; c += kWave) st.row[c] = src[c];
+        wave_sync();
+        if (!process(base + q, st.row, __shfl(ci, q), a.raw[(base + q) * (a.m + 1) + a.m])) { stop = true; break; }
         // drift may have grown: re-test the remaining lanes
         bool u2 = false;
         if (lane > q && i < a.n) {
           const double mg = a.margin[i];
-          u2 = a.force_exact || !(mg - 2.0 * S.dnow > a.T && st.cnt[a.c[i]] >= 2);
+          u2 = a.force_exact || !(mg - 2.0 * S.dnow > a.T && st.cnt[ci] >= 2);
         }
         bal = __ballot(u2);
       }
@@ -653,9 +864,19 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
   }
   __syncthreads();
   // write back
+  for (int s = lane; s < S.nslots; s += kWave) { a.counts[s] = st.cnt[s]; a.label_of_slot[s] = st.los[s]; }
+  for (int s = lane; s < S.K; s += kWave) a.slot_of_label[s] = st.sol[s];
+  // summary for the host (label -> slot, counts, pool sources), read with the control block
+  __syncthreads();
   for (int s = lane; s < scap; s += kWave) {
-    if (s < S.nslots) { a.counts[s] = st.cnt[s]; a.label_of_slot[s] = st.los[s]; }
-    if (s < S.K) a.slot_of_label[s] = st.sol[s];
+    a.summary[s] = s < S.K ? st.sol[s] : -1;
+    a.summary[scap + s] = s < S.nslots ? st.cnt[s] : 0;
+    a.summary[2 * scap + s] = s < S.nslots ? a.slot_src[s] : -1;
+  }
+  if (prof && lane == 0) {
+    tp[7] = wall_clock64();
+    for (int k = 0; k < 8; ++k) a.prof[k] = tp[k];
+    for (int k = 0; k < 8; ++k) a.prof[8 + k] = S.tsub[k];
   }
   if (lane == 0) {
     ResolveCtl c;
@@ -671,49 +892,50 @@ __global__ void k_relabel(int* c, const int* label_of_slot, int n) {
   if (i < n) c[i] = label_of_slot[c[i]];
 }
 
-// freq[k][j][level-1] = #{i : label_i = k, x_ij = level}.  A block walks its tiles of 64
-// points; each tile's codes and labels are staged in LDS with coalesced loads, then
-// thread t counts attribute column t, so the LDS counters need no atomics; one flush
-// of atomics per block.
-template <typename CT>
-__global__ __launch_bounds__(kBlock) void k_hist_lds(HistArgs a, int tiles_per_block) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int dp = a.nq * 16;
-  int* lab = (int*)smem;                                   // 64
-  uint8_t* tile = smem + 256;                              // 64 * dp
-  CT* h = (CT*)(smem + 256 + (((size_t)64 * dp + 15) / 16) * 16);
-  const int tid = threadIdx.x;
-  const int nent = a.K * a.d * a.mmax;
-  for (int e = tid; e < nent; e += kBlock) h[e] = 0;
-  const int64_t ntiles = ((int64_t)a.n + 63) / 64;
-  const int64_t t0 = (int64_t)blockIdx.x * tiles_per_block;
-  const int64_t t1 = min(ntiles, t0 + tiles_per_block);
-  for (int64_t t = t0; t < t1; ++t) {
-    __syncthreads();
-    const uint4* src = (const uint4*)(a.codes_t + t * 64 * dp);
-    uint4* dst = (uint4*)tile;
-    for (int v = tid; v < 4 * dp; v += kBlock) dst[v] = src[v];
-    if (tid < 64) {
-      const int64_t i = t * 64 + tid;
-      int k = i < a.n ? a.label[i] : -1;
-      if (k >= 0 && a.mask && !a.mask[k]) k = -1;
-      lab[tid] = k;
-    }
-    __syncthreads();
-    for (int j = tid; j < a.d; j += kBlock) {
-      const int q = j >> 4, bb = j & 15;
-      for (int p = 0; p < 64; ++p) {
-        const int k = lab[p];
-        if (k < 0) continue;
-        const int x = tile[(q * 64 + p) * 16 + bb];
-        CT* c = h + ((int64_t)k * a.d + j) * a.mmax + (x - 1);
-        *c = (CT)(*c + 1);
-      }
-    }
-  }
+// After k_relabel: counts per label, identity slot maps (slot == label again).  One block.
+__global__ __launch_bounds__(1024) void k_finish_sweep(int* counts, int* sol, int* los, int* src, int K,
+                                                      int nslots) {
+  extern __shared__ int fs[];
+  int* c = fs;            // [nslots]
+  int* m = fs + nslots;   // [K]
+  for (int s = threadIdx.x; s < nslots; s += blockDim.x) c[s] = counts[s];
+  for (int l = threadIdx.x; l < K; l += blockDim.x) m[l] = sol[l];
   __syncthreads();
-  for (int e = tid; e < nent; e += kBlock)
-    if (h[e]) atomicAdd(a.freq + e, (unsigned int)h[e]);
+  for (int l = threadIdx.x; l < K; l += blockDim.x) {
+    counts[l] = c[m[l]];
+    sol[l] = l;
+    los[l] = l;
+    src[l] = -1;
+  }
+}
+
+// Cluster parameter upload (UploadLayout) from the staging buffer.
+__global__ void k_scatter_clusters(const uint8_t* __restrict__ stage, int nent, int dp, int d, int bw, int full,
+                                   uint8_t* codes, double* tab, uint64_t* bnd, int* counts, int* sol, int* los,
+                                   int* src) {
+  const UploadLayout L = upload_layout(nent, dp, d, bw);
+  const int* slot = (const int*)(stage + L.off_slot);
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (int64_t)gridDim.x * blockDim.x;
+  const int tw = 2 * d;
+  for (int64_t q = tid; q < (int64_t)nent * tw; q += nth) {
+    const int r = (int)(q / tw), o = (int)(q - (int64_t)r * tw);
+    tab[(int64_t)slot[r] * tw + o] = ((const double*)(stage + L.off_tab))[q];
+  }
+  for (int64_t q = tid; q < (int64_t)nent * bw; q += nth) {
+    const int r = (int)(q / bw), o = (int)(q - (int64_t)r * bw);
+    bnd[(int64_t)slot[r] * bw + o] = ((const uint64_t*)(stage + L.off_bnd))[q];
+  }
+  for (int64_t q = tid; q < (int64_t)nent * dp; q += nth) {
+    const int r = (int)(q / dp), o = (int)(q - (int64_t)r * dp);
+    codes[(int64_t)slot[r] * dp + o] = stage[L.off_codes + q];
+  }
+  if (full)
+    for (int64_t r = tid; r < nent; r += nth) {
+      counts[r] = ((const int*)(stage + L.off_counts))[r];
+      sol[r] = (int)r;
+      los[r] = (int)r;
+      src[r] = -1;
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void k_hist_global(HistArgs a) {
@@ -729,6 +951,88 @@ __global__ __launch_bounds__(kBlock) void k_hist_global(HistArgs a) {
     const int x = a.codes_t[tiled_offset(i, j, a.nq)];
     atomicAdd(a.freq + ((int64_t)k * a.d + j) * a.mmax + (x - 1), 1u);
   }
+}
+
+// freq from the packed rows.  A workgroup (16 waves, one per CU) owns a contiguous range
+// of 64-point tiles and a slice of KC labels.  Per tile, lane p loads point p's packed row
+// (coalesced) into its wave's LDS stage; then the wave walks the points with lanes over
+// attributes: lane j reads field j of the point (broadcast read) and adds 1 to
+// h[(k - k0) * mmax + x][j] with a non-returning LDS atomic (consecutive banks: no
+// conflicts).  Points outside the slice count into a trash row, so the loop is
+// branch-free and unrolled over 8 points to keep reads in flight.  Each workgroup writes
+// its counters to `partial`; k_hist_reduce sums them into freq[k][j][x].
+constexpr int kHistBlock = 1024;
+constexpr int kHistUnroll = 8;
+__global__ __launch_bounds__(kHistBlock) void k_hist_packed(HistArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int row = a.mmax * a.d;
+  const int hsize = a.KC * row;
+  const int halloc = hsize + row;                           // + trash row
+  unsigned int* h = (unsigned int*)smem;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t* stg = (uint64_t*)(smem + (((size_t)halloc * 4 + 15) / 16) * 16) + (size_t)wv * a.W * 64;
+  for (int e = threadIdx.x; e < halloc; e += kHistBlock) h[e] = 0u;
+  __syncthreads();
+  const int k0 = blockIdx.y * a.KC;
+  const int64_t ntiles = ((int64_t)a.n + 63) / 64;
+  const int64_t t0 = (int64_t)blockIdx.x * a.tiles_per_block;
+  const int64_t t1 = min(ntiles, t0 + a.tiles_per_block);
+  const int W = a.W, wb = a.wb, d = a.d;
+  const uint64_t fmask = (1ull << wb) - 1ull;
+  for (int64_t t = t0 + wv; t < t1; t += kHistBlock / kWave) {
+    const int64_t i = t * 64 + lane;
+    int kk = a.KC;
+    if (i < a.n) {
+      const int k = a.label[i];
+      if ((!a.mask || a.mask[k]) && k >= k0 && k < k0 + a.KC) kk = k - k0;
+    }
+    const int kbase = kk * row;
+    for (int q = 0; q < W; ++q) stg[q * 64 + lane] = i < a.n ? a.xpk[packed_offset(i, q, W)] : 0ull;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (int jb = 0; jb < d; jb += 64) {
+      const int j = jb + lane;
+      const bool on = j < d;
+      const int bit = (on ? j : 0) * wb;
+      const uint64_t* sw = stg + (bit >> 6) * 64;
+      const int sh = bit & 63;
+      for (int p = 0; p < 64; p += kHistUnroll) {
+        uint64_t w[kHistUnroll];
+        int kb[kHistUnroll];
+#pragma unroll
+        for (int u = 0; u < kHistUnroll; ++u) {
+          w[u] = sw[p + u];
+          kb[u] = __builtin_amdgcn_readlane(kbase, p + u);
+        }
+#pragma unroll
+        for (int u = 0; u < kHistUnroll; ++u) {
+          const int x = (int)((w[u] >> sh) & fmask);
+          if (on) __hip_atomic_fetch_add(h + kb[u] + x * d + j, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  unsigned int* dst = a.partial + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * hsize;
+  for (int e = threadIdx.x; e < hsize; e += kHistBlock) dst[e] = h[e];
+}
+
+// freq[k][j][x] += sum of a group of workgroup partials (freq zeroed first).
+constexpr int kHistReduceSplit = 16;
+__global__ __launch_bounds__(256) void k_hist_reduce(HistArgs a, int nbx) {
+  const int hsize = a.KC * a.mmax * a.d;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= hsize) return;
+  const int per = (nbx + kHistReduceSplit - 1) / kHistReduceSplit;
+  const int b0 = blockIdx.z * per, b1 = min(nbx, b0 + per);
+  if (b0 >= b1) return;
+  const unsigned int* src = a.partial + (size_t)blockIdx.y * nbx * hsize + e;
+  unsigned int s = 0;
+  for (int b = b0; b < b1; ++b) s += src[(size_t)b * hsize];
+  const int kk = e / (a.mmax * a.d), rem = e - kk * a.mmax * a.d;
+  const int x = rem / a.d, j = rem - x * a.d;
+  const int k = blockIdx.y * a.KC + kk;
+  if (k < a.K && s) atomicAdd(a.freq + ((size_t)k * a.d + j) * a.mmax + x, s);
 }
 
 // compute_loglikelihood: exact per-point own-cluster log-likelihood (j order), then a
@@ -802,11 +1106,13 @@ template <int WB>
 static hipError_t launch_prepass_w(const PrepassArgs& a, int nblocks, hipStream_t s) {
   if (a.W <= 4) return launch_prepass_t<WB, 4>(a, nblocks, s);
   if (a.W <= 16) return launch_prepass_t<WB, 16>(a, nblocks, s);
-  return launch_prepass_t<WB, 0>(a, nblocks, s);
+  if (a.W <= 64) return launch_prepass_t<WB, 64>(a, nblocks, s);
+  return hipErrorInvalidValue;   // rows wider than 4096 bits (e.g. d > 512 at 8 bits)
 }
 
 hipError_t launch_exact_rows(const PrepassArgs& a, int nblocks, hipStream_t s) {
-  hipLaunchKernelGGL(k_exact_rows, dim3(nblocks), dim3(kWave), 0, s, a);
+  hipLaunchKernelGGL(k_list_scan, dim3(1), dim3(kScanThreads), 0, s, a.cnt, nblocks, a.dense, a.dense_total);
+  hipLaunchKernelGGL(k_exact_rows, dim3(std::min(nblocks * 4, 4096)), dim3(kWave), 0, s, a);
   return hipGetLastError();
 }
 
@@ -819,13 +1125,10 @@ hipError_t launch_prepass(const PrepassArgs& a, int nblocks, hipStream_t s) {
   }
 }
 
-size_t resolve_smem_bytes(int scap, int m) {
-  const size_t emax = (size_t)scap + (size_t)m;
-  return 64 + emax * 2 * sizeof(double) + (size_t)scap * 4 * sizeof(int) + emax * sizeof(int);
-}
+size_t resolve_smem_bytes(int lcap, int m) { return resolve_lds_bytes(lcap, m); }
 
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_resolve, dim3(1), dim3(kWave), resolve_smem_bytes(a.scap, a.m), s, a);
+  hipLaunchKernelGGL(k_resolve, dim3(1), dim3(kWave), resolve_lds_bytes(a.lcap, a.m), s, a);
   return hipGetLastError();
 }
 
@@ -834,18 +1137,52 @@ hipError_t launch_relabel(int* c, const int* los, int n, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_hist(const HistArgs& a, hipStream_t s) {
-  const int64_t nent = (int64_t)a.K * a.d * a.mmax;
+hipError_t launch_finish_sweep(int* counts, int* sol, int* los, int* src, int K, int nslots, hipStream_t s) {
+  hipLaunchKernelGGL(k_finish_sweep, dim3(1), dim3(1024), (size_t)(nslots + K) * 4, s, counts, sol, los, src, K,
+                     nslots);
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter_clusters(const uint8_t* stage, int nent, int dp, int d, int bw, int full, uint8_t* codes,
+                                   double* tab, uint64_t* bnd, int* counts, int* sol, int* los, int* src,
+                                   hipStream_t s) {
+  const int64_t work = (int64_t)nent * std::max(2 * d, std::max(dp, bw));
+  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (work + 255) / 256));
+  hipLaunchKernelGGL(k_scatter_clusters, dim3(nb), dim3(256), 0, s, stage, nent, dp, d, bw, full, codes, tab, bnd,
+                     counts, sol, los, src);
+  return hipGetLastError();
+}
+
+size_t hist_partial_words(const HistArgs& a, int* nbx_out, int* kc_out, int* tpb_out) {
+  const int64_t per_label = (int64_t)a.mmax * a.d * 4;
+  const int64_t budget = 96 * 1024 - (int64_t)(kHistBlock / kWave) * a.W * 64 * 8 - per_label;  // - trash row
+  const int kc = budget > 0 ? (int)std::min<int64_t>(a.K, budget / per_label) : 0;
   const int64_t ntiles = ((int64_t)a.n + 63) / 64;
-  const size_t stage = 256 + (((size_t)64 * a.nq * 16 + 15) / 16) * 16;
-  // enough blocks to fill the chip, and at most 1024 tiles (65536 points: u16 counters)
-  const int tpb = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (ntiles + 1023) / 1024));
-  const int nb = (int)((ntiles + tpb - 1) / tpb);
-  if (stage + nent * 4 <= 96 * 1024) {
-    hipLaunchKernelGGL(k_hist_lds<unsigned int>, dim3(nb), dim3(kBlock), stage + nent * 4, s, a, tpb);
-  } else if (stage + nent * 2 <= 150 * 1024) {
-    hipLaunchKernelGGL(k_hist_lds<unsigned short>, dim3(nb), dim3(kBlock), stage + ((nent * 2 + 15) / 16) * 16, s, a,
-                       tpb);
+  const int tpb = (int)std::max<int64_t>(16, (ntiles + 255) / 256);
+  const int nbx = (int)((ntiles + tpb - 1) / tpb);
+  *nbx_out = nbx;
+  *kc_out = kc;
+  *tpb_out = tpb;
+  if (kc <= 0 || a.W > 8) return 0;
+  const int ny = (a.K + kc - 1) / kc;
+  return (size_t)ny * nbx * kc * a.mmax * a.d;
+}
+
+hipError_t launch_hist(const HistArgs& a0, hipStream_t s) {
+  HistArgs a = a0;
+  int nbx, kc, tpb;
+  const size_t pw = hist_partial_words(a, &nbx, &kc, &tpb);
+  const hipError_t e = hipMemsetAsync(a.freq, 0, (size_t)a.K * a.d * a.mmax * 4, s);
+  if (e != hipSuccess) return e;
+  if (pw > 0 && a.partial && a.xpk) {
+    a.KC = kc;
+    a.tiles_per_block = tpb;
+    const int ny = (a.K + kc - 1) / kc;
+    const size_t hbytes = (((size_t)(kc + 1) * a.mmax * a.d * 4 + 15) / 16) * 16;
+    const size_t lds = hbytes + (size_t)(kHistBlock / kWave) * a.W * 64 * 8;
+    hipLaunchKernelGGL(k_hist_packed, dim3(nbx, ny), dim3(kHistBlock), lds, s, a);
+    const int hsize = kc * a.mmax * a.d;
+    hipLaunchKernelGGL(k_hist_reduce, dim3((hsize + 255) / 256, ny, kHistReduceSplit), dim3(256), 0, s, a, nbx);
   } else {
     const int64_t nt = (int64_t)a.n * a.nq;
     hipLaunchKernelGGL(k_hist_global, dim3((nt + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);

@@ -25,13 +25,17 @@ struct ParamTables {
 //   [0, W)            packed center codes (code - 1 in `wb` bits per attribute)
 //   [W, W + kQ*W)     kQ penalty bit-planes in the same field layout: bit b of
 //                     q_j = floor(|d_j| / delta), d_j = dhamming(mismatch) - dhamming(match)
-//   then A = sum_j dhamming(match) and delta, as doubles.
+//   then, as doubles: A = sum_j dhamming(match), delta, dmin = min_j |d_j|,
+//                     scale = sum_j max(|match_j|, |mismatch_j|).
 // For a point with mismatch mask M:  H = popc(M), Sq = sum_b 2^b popc(M & plane_b), and
-//   A - delta (Sq + H) <= ll <= A - delta Sq   (up to rounding, covered by kBoundEps).
+//   A - delta (Sq + H) <= ll <= A - delta Sq     (planes: precise)
+//   ll <= A - dmin H                              (codes only: crude)
+// up to rounding, covered by kBoundEps * (1 + scale) (a sum of d terms has error below
+// d 2^-53 scale).
 constexpr int kQ = 4;
 constexpr double kBoundEps = 1e-9;
 
-__host__ __device__ inline int bound_words(int W) { return (((1 + kQ) * W + 2) + 1) & ~1; }
+__host__ __device__ inline int bound_words(int W) { return (((1 + kQ) * W + 4) + 1) & ~1; }
 
 // Packed rows, tiled: word q of point i at ((i/64) * W + q) * 64 + i%64.
 __host__ __device__ inline int64_t packed_offset(int64_t i, int q, int W) {
@@ -64,6 +68,8 @@ struct PrepassArgs {
   double* margin;            // per point: lower bound on the own-cluster margin, or -inf
   int* list;                 // per block: ordered uncertain points
   int* cnt;                  // per block: number of uncertain points
+  int* dense;                // all uncertain rows in index order (k_list_scan)
+  int* dense_total;          // their number
   int p0;
 };
 
@@ -101,17 +107,40 @@ struct ResolveArgs {
   int S;                     // slots at the snapshot (L columns 0..S-1; latents at S + l)
   const double* margin;
   const int* list;
-  const int* cnt;
+  const int* dense;          // uncertain rows in index order
+  const int* dense_total;
   int nblocks;
   int p0;
   double T;                  // certainty threshold without drift
   double dmax;               // drift budget used by the prepass
-  int scap;                  // slot capacity
+  int scap;                  // slot capacity (device arrays, summary stride)
+  int lcap;                  // slot capacity of the resolver's LDS state (>= nslots + 2)
   int K;
   int nslots;
   ResolveCtl* ctl;
+  int* summary;              // at exit: [label -> slot: scap][count per slot: scap][pool source per slot: scap]
   int force_exact;           // testing: evaluate every point on the exact path
+  long long* prof;           // diagnostics: resolver phase times (s_memrealtime ticks) or nullptr
 };
+
+// Cluster parameter upload: one staging buffer, scattered on the device.
+//   [codes: nent * dp bytes][tab: nent * 2d doubles][bnd: nent * bw words][counts: nent ints][slot: nent ints]
+// (offsets rounded up to 16 B).  full == 1: entries are labels 0..nent-1, and the slot maps are
+// reset to the identity with the given counts; full == 0: entry r goes to slot[r] only.
+struct UploadLayout {
+  size_t off_codes, off_tab, off_bnd, off_counts, off_slot, bytes;
+};
+__host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+__host__ __device__ inline UploadLayout upload_layout(int nent, int dp, int d, int bw) {
+  UploadLayout L;
+  L.off_codes = 0;
+  L.off_tab = align16((size_t)nent * dp);
+  L.off_bnd = align16(L.off_tab + (size_t)nent * 2 * d * 8);
+  L.off_counts = align16(L.off_bnd + (size_t)nent * bw * 8);
+  L.off_slot = align16(L.off_counts + (size_t)nent * 4);
+  L.bytes = align16(L.off_slot + (size_t)nent * 4);
+  return L;
+}
 
 struct HistArgs {
   const uint8_t* codes_t;
@@ -120,6 +149,12 @@ struct HistArgs {
   const unsigned char* mask; // per label: include (nullptr = all)
   int K, mmax;
   unsigned int* freq;        // [K][d][mmax]
+  // packed path (k_hist_packed): rows in `wb`-bit fields, labels sliced KC per grid row
+  const uint64_t* xpk;
+  int W, wb;
+  int KC;                    // labels per slice (LDS counters KC * mmax * d)
+  int tiles_per_block;
+  unsigned int* partial;     // [slice][block][KC * mmax * d]
 };
 
 struct LoglikArgs {
