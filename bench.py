@@ -29,18 +29,18 @@ HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
 def packed_layout(d: int, mmax: int):
-    """(bits per attribute, packed words per row, bound words per entry) as in
-    csrc/kernels.hpp."""
+    """(bits per attribute, bit-sliced words per row, bound words per entry) as in
+    csrc/kernels.hpp (plane_words, bound_words)."""
     wb = 1 if mmax <= 2 else 2 if mmax <= 4 else 4 if mmax <= 16 else 8
-    W = -(-d * wb // 64)
-    bw = ((1 + 4) * W + 4 + 1) & ~1
-    return wb, W, bw
+    wd = -(-d // 64)
+    Ws = 2 if wd <= 2 else 4 if wd <= 4 else wd
+    return wb, wb * Ws, (wb + 4) * Ws + 4
 
 
 def prepass_bytes_per_point(d: int, mmax: int, m: int) -> int:
-    """Compulsory bytes k_prepass moves per point: its packed row
-    (8W), its m+1 raw draws (4(m+1)), its label (4), the bound records of its m latent pool
-    picks (8*bw each), its margin (8) and row index (4)."""
+    """Compulsory bytes k_prepass moves per point: its bit-sliced row
+    (8 W), its m+1 raw draws (4(m+1)), its label (4), the bound records of its m latent pool
+    picks (8 bw each), its margin (8) and row index (4)."""
     _, W, bw = packed_layout(d, mmax)
     return 8 * W + 4 * (m + 1) + 4 + m * 8 * bw + 12
 

@@ -169,6 +169,7 @@ class HostPool {
 
  private:
   HostPool() {
+    if (const char* e = std::getenv("HDPM_SPIN_US")) spin_us_ = std::max(0, std::atoi(e));
     int T = 0;
     if (const char* e = std::getenv("HDPM_HOST_THREADS")) T = std::atoi(e);
     if (T <= 0) {
@@ -204,8 +205,7 @@ class HostPool {
         active_.fetch_sub(1, std::memory_order_acq_rel);
         if (stop_) return;
         spin_pause();
-        if (++polls % 256 == 0 &&
-            std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(300)) {
+        if (++polls % 256 == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us_)) {
           std::unique_lock<std::mutex> lk(mu_);
           cv_.wait(lk, [&] { return stop_ || gen_.load(std::memory_order_acquire) != seen; });
           if (stop_) return;
@@ -223,6 +223,7 @@ class HostPool {
   int64_t total_ = 0, grain_ = 1;
   std::function<void(int64_t, int64_t)> job_;
   std::atomic<bool> stop_{false};
+  int spin_us_ = 3000;   // busy-wait this long after a job before sleeping (iterations ~1 ms apart)
 };
 
 template <class F>
@@ -268,19 +269,23 @@ struct Ctx {
   // MT jump-ahead for multi-workgroup windows (mtjump.hpp)
   int mt_G = 0, mt_bpg = 0;
   DevBuf<uint64_t> d_jpoly;
+  DevBuf<uint32_t> d_jidx;
+  DevBuf<int> d_joff;
   int64_t cmax = 1 << 16;          // draws expected between two sweeps (update_phi etc.)
   std::string err;
   hipEvent_t ev[8];
 
   // aux_data
   int n = 0, d = 0, nq = 0, dp = 0, mmax = 0;
-  int wb = 1, W = 1, bw = 0;          // packed bits per attribute, words per row, bound words
+  int wb = 1, W = 1, bw = 0;          // bits per attribute, field-packed words per row, bound words
+  int Ws = 2;                         // words per bit-plane of the bit-sliced rows
   double gamma = 0;
   std::vector<int32_t> att;
   std::vector<double> v, w;
   std::vector<uint8_t> codes;  // row-major n x d
   DevBuf<uint8_t> d_codes_t;
-  DevBuf<uint64_t> d_xpk;             // packed rows (tiled)
+  DevBuf<uint64_t> d_xpk;             // field-packed rows (tiled; histogram)
+  DevBuf<uint64_t> d_xbs;             // bit-sliced rows (tiled; prepass)
   DevBuf<double> d_logn;
   std::vector<double> h_logn;
 
@@ -295,6 +300,9 @@ struct Ctx {
   std::vector<double> h_sigma;        // K x d
   bool have_state = false;
   bool tables_dirty = true;
+  uint64_t labels_version = 1;        // bumped whenever device labels may change
+  uint64_t freq_version = 0;          // labels_version of the last full histogram (h_freq)
+  bool stage_full = false;            // h_stage holds the tables of every label (last upload was full)
 
   DevBuf<int> d_c, d_counts, d_sol, d_los, d_src;
   DevBuf<uint8_t> d_slot_codes;
@@ -391,7 +399,7 @@ struct Ctx {
     ensure_jump(count);
     const bool multi = mt_G > 1 && count >= (int64_t)mt_G * 624 * 8;
     MtGenArgs a{W.init.p, W.mti0, count, W.raw.p, W.arrays.p, W.nblocks, W.export_from,
-                multi ? d_jpoly.p : nullptr, mt_bpg, multi ? mt_G : 1};
+                multi ? d_jpoly.p : nullptr, d_jidx.p, d_joff.p, mt_bpg, multi ? mt_G : 1};
     HIPCHK(launch_mt_gen(a, gstream));
     HIPCHK(hipEventRecord(W.done, gstream));
     W.valid = true;
@@ -400,7 +408,11 @@ struct Ctx {
   // Jump polynomials z^(624 * bpg * g) mod phi for g < G, built once per window size class
   // and checked on the host against direct twisting.
   void ensure_jump(int64_t count) {
-    const int G = 64;
+    static const int G = [] {
+      const char* e = std::getenv("HDPM_MT_WORKGROUPS");
+      const int g = e ? std::atoi(e) : 0;
+      return g >= 2 && g <= 4096 ? g : 256;
+    }();
     if (count < (int64_t)G * 624 * 8) return;
     if (mt_G == G && count <= (int64_t)624 * G * mt_bpg) return;
     // headroom so later, slightly larger windows (sweep + draws between sweeps) reuse it
@@ -428,9 +440,23 @@ struct Ctx {
         if (std::memcmp(jumped, q.mt, sizeof(jumped)) != 0) return;
       }
     }
+    // set-bit lists of the polynomials (the generator's correlation walks these)
+    std::vector<int> off(G + 1, 0);
+    std::vector<uint32_t> idx;
+    for (int g = 0; g < G; ++g) {
+      off[g] = (int)idx.size();
+      if (g > 0)
+        for (int i = 0; i < kMtDeg; ++i)
+          if ((all[(size_t)g * 312 + (i >> 6)] >> (i & 63)) & 1u) idx.push_back((uint32_t)i);
+    }
+    off[G] = (int)idx.size();
     HIPCHK(hipStreamSynchronize(gstream));   // no generator may still read d_jpoly
     d_jpoly.ensure(all.size());
     HIPCHK(hipMemcpy(d_jpoly.p, all.data(), all.size() * 8, hipMemcpyHostToDevice));
+    d_jidx.ensure(std::max<size_t>(idx.size(), 1));
+    HIPCHK(hipMemcpy(d_jidx.p, idx.data(), idx.size() * 4, hipMemcpyHostToDevice));
+    d_joff.ensure(off.size());
+    HIPCHK(hipMemcpy(d_joff.p, off.data(), off.size() * 4, hipMemcpyHostToDevice));
     mt_G = G;
     mt_bpg = bpg;
   }
@@ -490,11 +516,12 @@ struct Ctx {
   // Bound data of one parameter entry (kernels.hpp, "Bound data per parameter entry").
   void bounds_for(const uint8_t* cen, const double* tab, uint64_t* out) const {
     std::memset(out, 0, (size_t)bw * 8);
-    const int F = 64 / wb;
     long double A = 0.0L, sc = 0.0L;
     double dmax = 0.0, dmin = INFINITY;
     for (int j = 0; j < d; ++j) {
-      out[j / F] |= (uint64_t)(cen[j] - 1) << ((j % F) * wb);
+      const unsigned code = cen[j] - 1u;
+      for (int b = 0; b < wb; ++b)
+        if ((code >> b) & 1u) out[b * Ws + (j >> 6)] |= 1ull << (j & 63);
       A += (long double)tab[2 * j];
       sc += (long double)std::max(std::fabs(tab[2 * j]), std::fabs(tab[2 * j + 1]));
       const double dj = tab[2 * j] - tab[2 * j + 1];
@@ -509,9 +536,9 @@ struct Ctx {
       while (q > 0 && delta * q > dj) --q;
       while (q < (1 << kQ) - 1 && delta * (q + 1) <= dj) ++q;
       for (int b = 0; b < kQ; ++b)
-        if ((q >> b) & 1) out[W + b * W + j / F] |= 1ull << ((j % F) * wb);
+        if ((q >> b) & 1) out[(wb + b) * Ws + (j >> 6)] |= 1ull << (j & 63);
     }
-    double* s = reinterpret_cast<double*>(out + (1 + kQ) * W);
+    double* s = reinterpret_cast<double*>(out + (wb + kQ) * Ws);
     s[0] = (double)A;
     s[1] = delta;
     s[2] = dmin > 0 ? dmin : 0.0;
@@ -553,6 +580,7 @@ struct Ctx {
     pool_for(nent, one);
     HIPCHK(hipMemcpyAsync(d_stage.p, st, L.bytes, hipMemcpyHostToDevice, stream));
     HIPCHK(hipEventRecord(ev_stage, stream));
+    stage_full = which == nullptr;
     HIPCHK(launch_scatter_clusters(d_stage.p, nent, dp, d, bw, which ? 0 : 1, d_slot_codes.p, d_slot_tab.p,
                                    d_slot_bnd.p, d_counts.p, d_sol.p, d_los.p, d_src.p, stream));
   }
@@ -578,6 +606,7 @@ struct Ctx {
   void upload_labels() {
     d_c.ensure(n);
     HIPCHK(hipMemcpyAsync(d_c.p, h_c.data(), (size_t)n * 4, hipMemcpyHostToDevice, stream));
+    labels_version++;
     HIPCHK(hipStreamSynchronize(stream));
     host_c_valid = true;
   }
@@ -645,13 +674,29 @@ struct Ctx {
     wb = mmax <= 2 ? 1 : mmax <= 4 ? 2 : mmax <= 16 ? 4 : 8;
     const int F = 64 / wb;
     W = (d + F - 1) / F;
-    bw = bound_words(W);
     std::vector<uint64_t> xp((size_t)n64 * W, 0);
     for (int64_t i = 0; i < n; ++i)
       for (int j = 0; j < d; ++j)
         xp[packed_offset(i, j / F, W)] |= (uint64_t)(codes[(size_t)i * d + j] - 1) << ((j % F) * wb);
     d_xpk.ensure(xp.size());
     HIPCHK(hipMemcpyAsync(d_xpk.p, xp.data(), xp.size() * 8, hipMemcpyHostToDevice, stream));
+    // bit-sliced rows (kernels.hpp)
+    Ws = plane_words(d);
+    bw = bound_words(wb, Ws);
+    {
+      const int Wr = wb * Ws;
+      std::vector<uint64_t> xs((size_t)n64 * Wr, 0);
+      parallel_for(n, [&](int64_t a0, int64_t a1) {
+        for (int64_t i = a0; i < a1; ++i)
+          for (int j = 0; j < d; ++j) {
+            const unsigned code = codes[(size_t)i * d + j] - 1u;
+            for (int b = 0; b < wb; ++b)
+              if ((code >> b) & 1u) xs[packed_offset(i, b * Ws + (j >> 6), Wr)] |= 1ull << (j & 63);
+          }
+      });
+      d_xbs.ensure(xs.size());
+      HIPCHK(hipMemcpyAsync(d_xbs.p, xs.data(), xs.size() * 8, hipMemcpyHostToDevice, stream));
+    }
     HIPCHK(hipStreamSynchronize(stream));
     scap = 0;   // slot arrays are re-laid out for the new bound size on next use
     d_slot_bnd.release();
@@ -767,6 +812,7 @@ struct Ctx {
       }
     }
     if (tables_dirty) upload_clusters();
+    labels_version++;
     const int K0 = K;
     std::vector<uint8_t> old_center = h_center;
     std::vector<double> old_sigma = h_sigma;
@@ -806,7 +852,7 @@ struct Ctx {
       pa.slots = ParamTables{d_slot_codes.p, d_slot_tab.p};
       pa.pool = ParamTables{d_pool_codes.p, d_pool_tab.p};
       pa.P = P; pa.raw = d_sweep_raw; pa.m = m; pa.logn = d_logn.p; pa.logfac = std::log(gamma / m);
-      pa.xpk = d_xpk.p; pa.W = W; pa.wb = wb; pa.slot_bnd = d_slot_bnd.p; pa.pool_bnd = d_pool_bnd.p; pa.bw = bw;
+      pa.xbs = d_xbs.p; pa.Ws = Ws; pa.wb = wb; pa.slot_bnd = d_slot_bnd.p; pa.pool_bnd = d_pool_bnd.p; pa.bw = bw;
 
       pa.thresh = (debug & 1) ? INFINITY : T + 2.0 * dmax;
       pa.L = d_L.p; pa.rowpos = d_rowpos.p; pa.margin = d_margin.p; pa.list = d_list.p; pa.cnt = d_cnt.p;
@@ -932,9 +978,32 @@ struct Ctx {
     h_freq.ensure(std::max<size_t>(nent, 1));
     HIPCHK(hipMemcpyAsync(h_freq.p, d_freq.p, nent * 4, hipMemcpyDeviceToHost, stream));
     HIPCHK(hipStreamSynchronize(stream));
+    freq_version = mask ? 0 : labels_version;
   }
 
-  // cf:511-591 with cluster sizes from h_counts and frequencies from the device.
+  // cf:511-591 with cluster sizes from h_counts and frequencies from the device, in three
+  // phases so that only the stream-consuming work is serial:
+  //   A (parallel)   per (cluster, attribute): center probabilities (cf:537-556),
+  //                  Rcpp sample's FixupProb / revsort / cumulative sums, and the rhig
+  //                  branch and rbeta setup for the most probable center;
+  //   B (serial)     the reference's draw order: per cluster, its d center uniforms, then
+  //                  its d sigma draws (rbeta rejection loops, or the bisection's Omega);
+  //   C (parallel)   sigma = -1/log(out) and the bisection solves, then the label tables.
+  // Every value is computed by the same expressions as the one-pass loop, so the chain is
+  // unchanged; on a norm_const2 failure the error is returned after phase B (the stream
+  // position then differs from the reference's, which stops at the failing draw).
+  struct PhiItem {
+    int err, lstar;
+    bool bp;                 // rhig beta path for lstar
+    RBeta rb;                // rbeta(w + 1, v - 1) setup for lstar
+    // phase B -> C
+    int path;                // 1 beta, 2 bisection
+    double x, nv, nw;        // beta draw x or Omega; sigma parameters of the drawn center
+  };
+  std::vector<PhiItem> phi_items;
+  std::vector<double> phi_cum;
+  std::vector<int> phi_perm, phi_off;
+
   int update_phi(const int32_t* idx, int nidx) {
     if (!have_state) { err = "no state"; return kArg; }
     auto t0 = std::chrono::steady_clock::now();
@@ -943,41 +1012,116 @@ struct Ctx {
       if (idx[q] >= 0 && idx[q] < K) mask[idx[q]] = 1;
     histogram(nidx == 0 ? nullptr : &mask);
     auto t1 = std::chrono::steady_clock::now();
-    std::vector<double> prob(mmax), nv(d), nw(d);
     std::vector<int> touched;
-    for (int i = 0; i < K; ++i) {
-      if (!mask[i]) continue;
-      const int nn = h_counts[i];
-      if (nn == 0) continue;
-      uint8_t* cen = &h_center[(size_t)i * d];
-      double* sig = &h_sigma[(size_t)i * d];
-      const unsigned* f = &h_freq.p[(size_t)i * d * mmax];
-      for (int j = 0; j < d; ++j) {          // compute_prob_centers + center draw
-        const int mj = att[j];
-        const unsigned* fj = f + (size_t)j * mmax;
-        for (int l = 0; l < mj; ++l) prob[l] = (-((double)nn - (double)fj[l])) / sig[j];
-        double mx = prob[0];
-        for (int l = 1; l < mj; ++l) if (prob[l] > mx) mx = prob[l];
-        for (int l = 0; l < mj; ++l) prob[l] = std::exp(prob[l] - mx);
-        double sum = 0.0;
-        for (int l = 0; l < mj; ++l) sum += prob[l];
-        for (int l = 0; l < mj; ++l) prob[l] = prob[l] / sum;
-        int pick = sample_prob1(rng, prob.data(), mj, sp, sperm);
-        if (pick < 0) { err = "center draw failed"; return -pick; }
-        cen[j] = (uint8_t)(pick + 1);
+    for (int i = 0; i < K; ++i)
+      if (mask[i] && h_counts[i] != 0) touched.push_back(i);
+    const int T = (int)touched.size();
+    phi_off.resize(d + 1);
+    phi_off[0] = 0;
+    for (int j = 0; j < d; ++j) phi_off[j + 1] = phi_off[j] + att[j];
+    const int sumatt = phi_off[d];
+    phi_items.resize((size_t)T * d);
+    phi_cum.resize((size_t)T * sumatt);
+    phi_perm.resize((size_t)T * sumatt);
+    // ---- phase A
+    pool_for((int64_t)T * d, [&](int it) {
+      const int t = it / d, j = it - t * d;
+      const int k = touched[t];
+      const int nn = h_counts[k];
+      const int mj = att[j];
+      const unsigned* fj = &h_freq.p[((size_t)k * d + j) * mmax];
+      const double sg = h_sigma[(size_t)k * d + j];
+      double prob[256];
+      for (int l = 0; l < mj; ++l) prob[l] = (-((double)nn - (double)fj[l])) / sg;
+      double mx = prob[0];
+      for (int l = 1; l < mj; ++l) if (prob[l] > mx) mx = prob[l];
+      for (int l = 0; l < mj; ++l) prob[l] = std::exp(prob[l] - mx);
+      double sum = 0.0;
+      for (int l = 0; l < mj; ++l) sum += prob[l];
+      for (int l = 0; l < mj; ++l) prob[l] = prob[l] / sum;
+      PhiItem& P = phi_items[it];
+      double* cum = &phi_cum[(size_t)t * sumatt + phi_off[j]];
+      int* perm = &phi_perm[(size_t)t * sumatt + phi_off[j]];
+      P.err = -sample_prob1_prep(prob, mj, cum, perm);
+      P.lstar = -1;
+      if (P.err) return;
+      const int l = perm[0] - 1;
+      const double sumdelta = (double)fj[l];
+      const double nw_ = w[j] + nn - sumdelta, nv_ = v[j] + sumdelta;
+      P.lstar = l;
+      P.bp = rhig_beta_path(nv_, nw_, (double)mj);
+      if (P.bp) P.rb = rbeta_setup(nw_ + 1, nv_ - 1);
+    });
+    auto tA = std::chrono::steady_clock::now();
+    // ---- phase B
+    for (int t = 0; t < T; ++t) {
+      const int k = touched[t];
+      const int nn = h_counts[k];
+      uint8_t* cen = &h_center[(size_t)k * d];
+      for (int j = 0; j < d; ++j) {
+        const PhiItem& P = phi_items[(size_t)t * d + j];
+        if (P.err) { err = "center draw failed"; return P.err; }
+        const size_t o = (size_t)t * sumatt + phi_off[j];
+        cen[j] = (uint8_t)(sample_prob1_pick(&phi_cum[o], &phi_perm[o], att[j], rng.unif()) + 1);
       }
       for (int j = 0; j < d; ++j) {
-        const double sumdelta = (double)f[(size_t)j * mmax + (cen[j] - 1)];
-        nw[j] = w[j] + nn - sumdelta;
-        nv[j] = v[j] + sumdelta;
+        PhiItem& P = phi_items[(size_t)t * d + j];
+        const int l = cen[j] - 1;
+        const double mj = (double)att[j];
+        const double sumdelta = (double)h_freq.p[((size_t)k * d + j) * mmax + l];
+        P.nw = w[j] + nn - sumdelta;
+        P.nv = v[j] + sumdelta;
+        bool bp;
+        RBeta rb;
+        if (l == P.lstar) {
+          bp = P.bp;
+          rb = P.rb;
+        } else {
+          bp = rhig_beta_path(P.nv, P.nw, mj);
+          if (bp) rb = rbeta_setup(P.nw + 1, P.nv - 1);
+        }
+        if (bp) {                                   // hg:359-363
+          double x = rbeta_draw(rng, rb);
+          while (x > (mj - 1) / mj) x = rbeta_draw(rng, rb);
+          P.path = 1;
+          P.x = x;
+        } else {                                    // hg:365-367
+          P.path = 2;
+          P.x = rng.unif();
+        }
       }
-      int st = sample_sigma(nv.data(), nw.data(), sig);
-      if (st) { err = "norm_const2 - hypergeometric diverging with infinity"; return st; }
-      touched.push_back(i);
     }
-    if (tables_dirty || (int)touched.size() == K) upload_clusters();
+    auto tB = std::chrono::steady_clock::now();
+    // ---- phase C
+    std::atomic<int> first_err{-1};
+    pool_for((int64_t)T * d, [&](int it) {
+      const int t = it / d, j = it - t * d;
+      PhiItem& P = phi_items[it];
+      const double mj = (double)att[j];
+      double out;
+      if (P.path == 1) {
+        out = P.x / ((mj - 1) * (1 - P.x));
+      } else {
+        int e = kOk;
+        out = bisec_hyper2(P.nw, P.nv, mj, P.x, &e);
+        if (e) {
+          int cur = first_err.load();
+          while ((cur < 0 || it < cur) && !first_err.compare_exchange_weak(cur, it)) {}
+          return;
+        }
+      }
+      h_sigma[(size_t)touched[t] * d + j] = -1 / std::log(out);
+    });
+    auto tC = std::chrono::steady_clock::now();
+    if (first_err.load() >= 0) { err = "norm_const2 - hypergeometric diverging with infinity"; return kGsl; }
+    if (tables_dirty || T == K) upload_clusters();
     else upload_some(touched);
     auto t2 = std::chrono::steady_clock::now();
+    if (debug & 2) {
+      auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+      std::fprintf(stderr, "[phi] hist %.1f us, A %.1f, B %.1f, C %.1f, upload %.1f us (%d x %d items, %d threads)\n",
+                   us(t0, t1), us(t1, tA), us(tA, tB), us(tB, tC), us(tC, t2), T, d, HostPool::get().threads());
+    }
     stats.t_stats_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
     stats.t_host_phi_ms += std::chrono::duration<double, std::milli>(t2 - t1).count();
     return kOk;
@@ -987,6 +1131,31 @@ struct Ctx {
   int compute_loglikelihood(double* out) {
     if (!have_state) { err = "no state"; return kArg; }
     if (tables_dirty) upload_clusters();
+    if (freq_version == labels_version && stage_full && !(debug & 4)) {
+      // the labels have not moved since the last full histogram: the sum over points
+      // regroups exactly into per-(cluster, attribute) match / mismatch counts times the
+      // dhamming table values (the tables of the last full upload, still in h_stage)
+      auto t0 = std::chrono::steady_clock::now();
+      const UploadLayout L = upload_layout(K, dp, d, bw);
+      const double* tab = (const double*)(h_stage.p + L.off_tab);
+      double hi = 0.0, lo = 0.0;
+      auto add = [&](double a) {
+        const double s = hi + a, bb = s - hi;
+        lo += (hi - (s - bb)) + (a - bb);
+        hi = s;
+      };
+      for (int k = 0; k < K; ++k) {
+        const double nk = (double)h_counts[k];
+        for (int j = 0; j < d; ++j) {
+          const double match = (double)h_freq.p[((size_t)k * d + j) * mmax + (h_center[(size_t)k * d + j] - 1)];
+          add(match * tab[((size_t)k * d + j) * 2]);
+          add((nk - match) * tab[((size_t)k * d + j) * 2 + 1]);
+        }
+      }
+      *out = hi + lo;
+      stats.t_loglik_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      return kOk;
+    }
     HIPCHK(hipEventRecord(ev[3], stream));
     const int nb = (n + kBlock - 1) / kBlock;
     d_partial.ensure((size_t)2 * nb);

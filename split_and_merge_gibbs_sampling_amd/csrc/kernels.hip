@@ -118,126 +118,10 @@ __device__ __forceinline__ double ll_lane(const PointCodes<NQR>& x, int d, const
   return ll;
 }
 
-// ------------------------------------------------------------------ prepass
-// Uniform (wave-invariant) load through the constant address space -> scalar loads.
-template <class T>
-__device__ __forceinline__ T ldu(const T* p) {
-  return *(const __attribute__((address_space(4))) T*)p;
-}
 
-template <int WB>
-__device__ __forceinline__ uint64_t mismatch_mask(uint64_t z) {
-  if constexpr (WB == 1) return z;
-  if constexpr (WB == 2) return (z | (z >> 1)) & 0x5555555555555555ull;
-  if constexpr (WB == 4) {
-    z |= z >> 1;
-    z |= z >> 2;
-    return z & 0x1111111111111111ull;
-  }
-  z |= z >> 1;
-  z |= z >> 2;
-  z |= z >> 4;
-  return z & 0x0101010101010101ull;
-}
-
-struct Bounds {
-  double lo, hi;
-};
-
-// ll bounds of a point (packed words x[0..W)) against one entry's bound data `bd`.
-// UNIFORM: bd is wave-invariant (cluster slot) -> scalar loads.
-template <int WB, int WMAX, bool UNIFORM>
-__device__ __forceinline__ Bounds entry_bounds(const uint64_t (&x)[WMAX > 0 ? WMAX : 1], const uint64_t* xg,
-                                               int W, const uint64_t* bd) {
-  int H = 0, Sq = 0;
-  auto word = [&](int q, uint64_t xq) {
-    const uint64_t cq = UNIFORM ? ldu(bd + q) : bd[q];
-    const uint64_t mk = mismatch_mask<WB>(xq ^ cq);
-    H += __popcll(mk);
-#pragma unroll
-    for (int b = 0; b < kQ; ++b) {
-      const uint64_t pl = UNIFORM ? ldu(bd + W + b * W + q) : bd[W + b * W + q];
-      Sq += __popcll(mk & pl) << b;
-    }
-  };
-  if constexpr (WMAX > 0) {
-#pragma unroll
-    for (int q = 0; q < WMAX; ++q)
-      if (q < W) word(q, x[q]);
-  } else {
-    for (int q = 0; q < W; ++q) word(q, xg[q]);
-  }
-  const double A = UNIFORM ? ldu((const double*)(bd + (1 + kQ) * W)) : ((const double*)(bd + (1 + kQ) * W))[0];
-  const double dl = UNIFORM ? ldu((const double*)(bd + (1 + kQ) * W + 1)) : ((const double*)(bd + (1 + kQ) * W))[1];
-  const double pmin = dl * (double)Sq, pmax = dl * (double)(Sq + H);
-  const double eps = kBoundEps * (1.0 + fabs(A) + pmax);
-  return Bounds{A - pmax - eps, A - pmin + eps};
-}
-
-// Bounds-first prepass: every point gets rigorous bounds on its K + m log-weights from
-// Hamming popcounts; only points whose draw is not provably "stay" get exact rows.
-//   own cluster (count >= 2): precise lower bound lo (penalty planes, per-lane record);
-//   other clusters: crude upper bound A - dmin H from the codes alone (scalar loads),
-//     refined with the planes only in waves where some lane's crude bound could still
-//     stop the point from being certain (ub > lo - thresh);
-//   latent entries: precise upper bound from their pool record.
-// margin = lo - max(ub) is a lower bound on how far the own cluster leads every other
-// entry; the point is certain when it exceeds `thresh`.
-template <int WB, int WMAX>
-__global__ __launch_bounds__(kBlock) void k_prepass(PrepassArgs a) {
-  static_assert(WMAX > 0, "register rows");
+// Margin, row position and the ordered compaction of the block's uncertain points.
+__device__ __forceinline__ void prepass_finish(const PrepassArgs& a, int64_t i, bool active, int own_cnt, double mg) {
   const int tid = threadIdx.x;
-  const int64_t i = (int64_t)a.p0 + (int64_t)blockIdx.x * kBlock + tid;
-  const bool active = i < a.n;
-  const int64_t ii = active ? i : (int64_t)a.n - 1;
-  const int W = a.W;
-  uint64_t x[WMAX];
-#pragma unroll
-  for (int q = 0; q < WMAX; ++q) x[q] = q < W ? a.xpk[packed_offset(ii, q, W)] : 0ull;
-  const int own = a.c[ii];
-  const int own_cnt = a.counts[own];
-  const uint32_t* raw = a.raw + ii * (a.m + 1);
-  const int sc_off = (1 + kQ) * W;   // doubles A, delta, dmin, scale after the planes
-  double mg = -INFINITY;
-  if (own_cnt >= 2) {
-    const double lo = a.logn[own_cnt - 1] + entry_bounds<WB, WMAX, false>(x, nullptr, W, a.slot_bnd + (int64_t)own * a.bw).lo;
-    const double cut = lo - a.thresh;        // an entry whose ub stays below this cannot matter
-    double ubmax = -INFINITY;
-    for (int l = 0; l < a.K; ++l) {
-      const int s = ldu(a.slot_of_label + l);
-      const uint64_t* bd = a.slot_bnd + (int64_t)s * a.bw;
-      uint64_t mk[WMAX];
-      int H = 0;
-#pragma unroll
-      for (int q = 0; q < WMAX; ++q) {
-        mk[q] = q < W ? mismatch_mask<WB>(x[q] ^ ldu(bd + q)) : 0ull;
-        H += __popcll(mk[q]);
-      }
-      const double A = ldu((const double*)(bd + sc_off)), dmin = ldu((const double*)(bd + sc_off + 2));
-      const double scale = ldu((const double*)(bd + sc_off + 3));
-      const double lg = a.logn[ldu(a.counts + s)];
-      double ub = lg + (A - dmin * (double)H + kBoundEps * (1.0 + scale));
-      const bool need = s != own && ub > cut;
-      if (__ballot(need)) {
-        int Sq = 0;
-#pragma unroll
-        for (int q = 0; q < WMAX; ++q)
-          if (q < W) {
-#pragma unroll
-            for (int b = 0; b < kQ; ++b) Sq += __popcll(mk[q] & ldu(bd + W + b * W + q)) << b;
-          }
-        const double dl = ldu((const double*)(bd + sc_off + 1));
-        const double pmin = dl * (double)Sq, pmax = dl * (double)(Sq + H);
-        ub = fmin(ub, lg + (A - pmin + kBoundEps * (1.0 + fabs(A) + pmax)));
-      }
-      if (s != own) ubmax = fmax(ubmax, ub);
-    }
-    for (int l = 0; l < a.m; ++l) {
-      const int64_t e = pick_entry(raw[l], a.P);
-      ubmax = fmax(ubmax, a.logfac + entry_bounds<WB, WMAX, false>(x, nullptr, W, a.pool_bnd + e * a.bw).hi);
-    }
-    mg = lo - ubmax;
-  }
   const bool uncertain = active && !(own_cnt >= 2 && mg > a.thresh);
   if (active) a.margin[i] = mg;
 
@@ -259,6 +143,210 @@ __global__ __launch_bounds__(kBlock) void k_prepass(PrepassArgs a) {
   if (uncertain) a.list[row] = (int)i;
   if (tid == 0) a.cnt[blockIdx.x] = tot;
 
+}
+
+// ------------------------------------------------------------------ prepass
+// Uniform (wave-invariant) load through the constant address space -> scalar loads.
+template <class T>
+__device__ __forceinline__ T ldu(const T* p) {
+  return *(const __attribute__((address_space(4))) T*)p;
+}
+
+template <bool U>
+__device__ __forceinline__ uint64_t ldw(const uint64_t* p) {
+  if constexpr (U) return ldu(p);
+  else return *p;
+}
+
+__device__ __forceinline__ double as_f64(uint64_t u) { return __longlong_as_double((long long)u); }
+
+// Mismatch mask M (one bit per attribute) of bit-sliced rows x and record codes, and H.
+template <int WB, int WS, bool U>
+__device__ __forceinline__ int mismatch_mask(const uint64_t (&x)[WB * WS], const uint64_t* rec, uint64_t (&M)[WS]) {
+  int H = 0;
+#pragma unroll
+  for (int w = 0; w < WS; ++w) {
+    uint64_t m = 0;
+#pragma unroll
+    for (int b = 0; b < WB; ++b) m |= x[b * WS + w] ^ ldw<U>(rec + b * WS + w);
+    M[w] = m;
+    H += __popcll(m);
+  }
+  return H;
+}
+
+// Sq = sum_b 2^b popc(M & plane_b)
+template <int WB, int WS, bool U>
+__device__ __forceinline__ int penalty_sum(const uint64_t (&M)[WS], const uint64_t* rec) {
+  int Sq = 0;
+#pragma unroll
+  for (int w = 0; w < WS; ++w)
+#pragma unroll
+    for (int b = 0; b < kQ; ++b) Sq += __popcll(M[w] & ldw<U>(rec + (WB + b) * WS + w)) << b;
+  return Sq;
+}
+
+// A whole record gathered with 16-B loads into registers.
+template <int RW>
+__device__ __forceinline__ void load_record(const uint64_t* rec, uint64_t (&R)[RW]) {
+  static_assert(RW % 2 == 0, "records are 16-B aligned");
+  const uint4* r4 = (const uint4*)rec;
+#pragma unroll
+  for (int k = 0; k < RW / 2; ++k) {
+    const uint4 v = r4[k];
+    R[2 * k] = ((uint64_t)v.y << 32) | v.x;
+    R[2 * k + 1] = ((uint64_t)v.w << 32) | v.z;
+  }
+}
+
+// Register-record versions (constant indices into R).
+template <int WB, int WS, int RW>
+__device__ __forceinline__ int mismatch_r(const uint64_t (&x)[WB * WS], const uint64_t (&R)[RW], uint64_t (&M)[WS]) {
+  int H = 0;
+#pragma unroll
+  for (int w = 0; w < WS; ++w) {
+    uint64_t m = 0;
+#pragma unroll
+    for (int b = 0; b < WB; ++b) m |= x[b * WS + w] ^ R[b * WS + w];
+    M[w] = m;
+    H += __popcll(m);
+  }
+  return H;
+}
+template <int WB, int WS, int RW>
+__device__ __forceinline__ int penalty_r(const uint64_t (&M)[WS], const uint64_t (&R)[RW]) {
+  int Sq = 0;
+#pragma unroll
+  for (int w = 0; w < WS; ++w)
+#pragma unroll
+    for (int b = 0; b < kQ; ++b) Sq += __popcll(M[w] & R[(WB + b) * WS + w]) << b;
+  return Sq;
+}
+
+// Bounds-first prepass: every point gets rigorous bounds on its K + m log-weights from
+// Hamming popcounts of bit-sliced rows; only points whose draw is not provably "stay" get
+// exact rows.
+//   own cluster (count >= 2): precise lower bound lo (penalty planes, record gathered);
+//   other clusters: crude upper bound A - dmin H from the codes alone (scalar loads),
+//     refined with the planes only in waves where some lane's crude bound could still
+//     stop the point from being certain (ub > lo - thresh);
+//   latent entries: precise upper bound from their pool record (16-B gathers, all m in
+//     flight together when the records are small).
+// margin = lo - max(ub) is a lower bound on how far the own cluster leads every other
+// entry; the point is certain when it exceeds `thresh`.
+template <int WB, int WS>
+__global__ __launch_bounds__(kBlock) void k_prepass(PrepassArgs a) {
+  constexpr int WR = WB * WS;                  // row words
+  constexpr int RW = (WB + kQ) * WS + 4;       // record words
+  constexpr int SC = (WB + kQ) * WS;           // record scalars: A, delta, dmin, scale
+  constexpr int NPF = RW <= 16 ? 4 : RW <= 32 ? 2 : 1;   // pool records in flight
+  const int tid = threadIdx.x;
+  const int64_t i = (int64_t)a.p0 + (int64_t)blockIdx.x * kBlock + tid;
+  const bool active = i < a.n;
+  const int64_t ii = active ? i : (int64_t)a.n - 1;
+  uint64_t x[WR];
+#pragma unroll
+  for (int q = 0; q < WR; ++q) x[q] = a.xbs[packed_offset(ii, q, WR)];
+  const int own = a.c[ii];
+  const int own_cnt = a.counts[own];
+  const uint32_t* raw = a.raw + ii * (a.m + 1);
+  double mg = -INFINITY;
+  if (own_cnt >= 2) {
+    uint64_t M[WS];
+    double lo;
+    {
+      uint64_t R[RW];
+      load_record<RW>(a.slot_bnd + (int64_t)own * a.bw, R);
+      const int H = mismatch_r<WB, WS, RW>(x, R, M);
+      const int Sq = penalty_r<WB, WS, RW>(M, R);
+      const double A = as_f64(R[SC]), dl = as_f64(R[SC + 1]);
+      const double pmax = dl * (double)(Sq + H);
+      lo = a.logn[own_cnt - 1] + (A - pmax - kBoundEps * (1.0 + fabs(A) + pmax));
+    }
+    const double cut = lo - a.thresh;        // an entry whose ub stays below this cannot matter
+    double ubmax = -INFINITY;
+    for (int l = 0; l < a.K; ++l) {
+      const int s = ldu(a.slot_of_label + l);
+      const uint64_t* bd = a.slot_bnd + (int64_t)s * a.bw;
+      const int H = mismatch_mask<WB, WS, true>(x, bd, M);
+      const double A = as_f64(ldu(bd + SC)), dmin = as_f64(ldu(bd + SC + 2)), scale = as_f64(ldu(bd + SC + 3));
+      const double lg = a.logn[ldu(a.counts + s)];
+      double ub = lg + (A - dmin * (double)H + kBoundEps * (1.0 + scale));
+      const bool need = s != own && ub > cut;
+      if (__ballot(need)) {
+        const int Sq = penalty_sum<WB, WS, true>(M, bd);
+        const double dl = as_f64(ldu(bd + SC + 1));
+        const double pmin = dl * (double)Sq, pmax = dl * (double)(Sq + H);
+        ub = fmin(ub, lg + (A - pmin + kBoundEps * (1.0 + fabs(A) + pmax)));
+      }
+      if (s != own) ubmax = fmax(ubmax, ub);
+    }
+    for (int l0 = 0; l0 < a.m; l0 += NPF) {
+      uint64_t R[NPF][RW];
+#pragma unroll
+      for (int u = 0; u < NPF; ++u)
+        if (l0 + u < a.m) load_record<RW>(a.pool_bnd + pick_entry(raw[l0 + u], a.P) * a.bw, R[u]);
+#pragma unroll
+      for (int u = 0; u < NPF; ++u) {
+        if (l0 + u < a.m) {
+          const int H = mismatch_r<WB, WS, RW>(x, R[u], M);
+          const int Sq = penalty_r<WB, WS, RW>(M, R[u]);
+          const double A = as_f64(R[u][SC]), dl = as_f64(R[u][SC + 1]);
+          const double pmin = dl * (double)Sq, pmax = dl * (double)(Sq + H);
+          ubmax = fmax(ubmax, a.logfac + (A - pmin + kBoundEps * (1.0 + fabs(A) + pmax)));
+        }
+      }
+    }
+    mg = lo - ubmax;
+  }
+  prepass_finish(a, i, active, own_cnt, mg);
+}
+
+// Generic width (planes wider than 4 words, or wide codes): rows and records read from
+// memory as needed.
+__global__ __launch_bounds__(kBlock) void k_prepass_generic(PrepassArgs a) {
+  const int tid = threadIdx.x;
+  const int64_t i = (int64_t)a.p0 + (int64_t)blockIdx.x * kBlock + tid;
+  const bool active = i < a.n;
+  const int64_t ii = active ? i : (int64_t)a.n - 1;
+  const int WB = a.wb, WS = a.Ws, WR = WB * WS, SC = (WB + kQ) * WS;
+  const int own = a.c[ii];
+  const int own_cnt = a.counts[own];
+  const uint32_t* raw = a.raw + ii * (a.m + 1);
+  auto bounds = [&](const uint64_t* rec, int& H, int& Sq) {
+    H = 0;
+    Sq = 0;
+    for (int w = 0; w < WS; ++w) {
+      uint64_t m = 0;
+      for (int b = 0; b < WB; ++b) m |= a.xbs[packed_offset(ii, b * WS + w, WR)] ^ rec[b * WS + w];
+      H += __popcll(m);
+      for (int b = 0; b < kQ; ++b) Sq += __popcll(m & rec[(WB + b) * WS + w]) << b;
+    }
+  };
+  double mg = -INFINITY;
+  if (own_cnt >= 2) {
+    int H, Sq;
+    const uint64_t* ro = a.slot_bnd + (int64_t)own * a.bw;
+    bounds(ro, H, Sq);
+    const double A = as_f64(ro[SC]), dl = as_f64(ro[SC + 1]);
+    const double pmax = dl * (double)(Sq + H);
+    const double lo = a.logn[own_cnt - 1] + (A - pmax - kBoundEps * (1.0 + fabs(A) + pmax));
+    double ubmax = -INFINITY;
+    auto upper = [&](const uint64_t* rec, double base) {
+      int h, sq;
+      bounds(rec, h, sq);
+      const double AA = as_f64(rec[SC]), d2 = as_f64(rec[SC + 1]);
+      const double pm = d2 * (double)(sq + h);
+      return base + (AA - d2 * (double)sq + kBoundEps * (1.0 + fabs(AA) + pm));
+    };
+    for (int l = 0; l < a.K; ++l) {
+      const int s = a.slot_of_label[l];
+      if (s != own) ubmax = fmax(ubmax, upper(a.slot_bnd + (int64_t)s * a.bw, a.logn[a.counts[s]]));
+    }
+    for (int l = 0; l < a.m; ++l) ubmax = fmax(ubmax, upper(a.pool_bnd + pick_entry(raw[l], a.P) * a.bw, a.logfac));
+    mg = lo - ubmax;
+  }
+  prepass_finish(a, i, active, own_cnt, mg);
 }
 
 // Block offsets of the prepass lists and the dense, index-ordered list of uncertain rows
@@ -1096,18 +1184,18 @@ __global__ __launch_bounds__(kBlock) void k_lmatrix(const uint8_t* codes_t, int 
 }
 
 // ------------------------------------------------------------------ launchers
-template <int WB, int WMAX>
+template <int WB, int WS>
 static hipError_t launch_prepass_t(const PrepassArgs& a, int nblocks, hipStream_t s) {
-  hipLaunchKernelGGL((k_prepass<WB, WMAX>), dim3(nblocks), dim3(kBlock), 0, s, a);
+  hipLaunchKernelGGL((k_prepass<WB, WS>), dim3(nblocks), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 
 template <int WB>
 static hipError_t launch_prepass_w(const PrepassArgs& a, int nblocks, hipStream_t s) {
-  if (a.W <= 4) return launch_prepass_t<WB, 4>(a, nblocks, s);
-  if (a.W <= 16) return launch_prepass_t<WB, 16>(a, nblocks, s);
-  if (a.W <= 64) return launch_prepass_t<WB, 64>(a, nblocks, s);
-  return hipErrorInvalidValue;   // rows wider than 4096 bits (e.g. d > 512 at 8 bits)
+  if (a.Ws == 2) return launch_prepass_t<WB, 2>(a, nblocks, s);
+  if (a.Ws == 4 && WB <= 4) return launch_prepass_t<WB, 4>(a, nblocks, s);
+  hipLaunchKernelGGL(k_prepass_generic, dim3(nblocks), dim3(kBlock), 0, s, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_exact_rows(const PrepassArgs& a, int nblocks, hipStream_t s) {
@@ -1424,16 +1512,22 @@ __global__ __launch_bounds__(640) void k_mt_gen_multi(MtGenArgs a) {
       if (t < 624) seq[blk * 624 + t] = mt_twist_elem(seq + (blk - 1) * 624, t);
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // out[t] = XOR over the set bits i of the jump polynomial of seq[i + t + 1]; the bit
+    // positions come as a list (scalar loads), so the LDS reads issue back to back
     uint32_t acc = 0;
     if (t < 624) {
-      const uint64_t* p = a.jpoly + (int64_t)g * 312;
-      for (int w = 0; w < 312; ++w) {
-        const uint64_t bits = ldu(p + w);
-        const uint32_t* s0 = seq + 64 * w + t + 1;
+      const uint32_t* L = a.jidx + ldu(a.joff + g);
+      const int cnt = ldu(a.joff + g + 1) - ldu(a.joff + g);
+      const uint32_t* s0 = seq + t + 1;
+      int q = 0;
+      for (; q + 16 <= cnt; q += 16) {
+        uint32_t v[16];
 #pragma unroll
-        for (int b = 0; b < 64; ++b)
-          if ((bits >> b) & 1u) acc ^= s0[b];
+        for (int u = 0; u < 16; ++u) v[u] = s0[ldu(L + q + u)];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) acc ^= v[u];
       }
+      for (; q < cnt; ++q) acc ^= s0[ldu(L + q)];
       buf0[t] = acc;
     }
   }

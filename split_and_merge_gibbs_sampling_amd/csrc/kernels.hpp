@@ -21,23 +21,33 @@ struct ParamTables {
   const double* tab;
 };
 
+// Bit-sliced codes.  A row's categorical codes (code - 1, `wb` bits) are stored as wb
+// bit-planes of Ws 64-bit words each (bit j % 64 of word j / 64 of plane b = bit b of
+// attribute j's code; Ws = words per plane, padded to 2 or 4 when d <= 256 so kernels can
+// keep a row in registers).  The mismatch mask of a point x and a center c is then
+// M = OR_b (x_b ^ c_b), one bit per attribute.
+__host__ __device__ inline int plane_words(int d) {
+  const int wd = (d + 63) / 64;
+  return wd <= 2 ? 2 : wd <= 4 ? 4 : wd;
+}
+
 // Bound data per parameter entry (cluster slot or pool entry), `bw` u64 words:
-//   [0, W)            packed center codes (code - 1 in `wb` bits per attribute)
-//   [W, W + kQ*W)     kQ penalty bit-planes in the same field layout: bit b of
-//                     q_j = floor(|d_j| / delta), d_j = dhamming(mismatch) - dhamming(match)
+//   [0, wb*Ws)              the center's bit-sliced codes
+//   [wb*Ws, (wb+kQ)*Ws)     kQ penalty bit-planes: bit b of q_j = floor(|d_j| / delta),
+//                           d_j = dhamming(match) - dhamming(mismatch)
 //   then, as doubles: A = sum_j dhamming(match), delta, dmin = min_j |d_j|,
 //                     scale = sum_j max(|match_j|, |mismatch_j|).
 // For a point with mismatch mask M:  H = popc(M), Sq = sum_b 2^b popc(M & plane_b), and
 //   A - delta (Sq + H) <= ll <= A - delta Sq     (planes: precise)
 //   ll <= A - dmin H                              (codes only: crude)
 // up to rounding, covered by kBoundEps * (1 + scale) (a sum of d terms has error below
-// d 2^-53 scale).
+// d 2^-53 scale).  bw is even, so records are 16-B aligned for vector loads.
 constexpr int kQ = 4;
 constexpr double kBoundEps = 1e-9;
 
-__host__ __device__ inline int bound_words(int W) { return (((1 + kQ) * W + 4) + 1) & ~1; }
+__host__ __device__ inline int bound_words(int wb, int Ws) { return (wb + kQ) * Ws + 4; }
 
-// Packed rows, tiled: word q of point i at ((i/64) * W + q) * 64 + i%64.
+// Rows, tiled: word q of point i at ((i/64) * W + q) * 64 + i%64 (W words per row).
 __host__ __device__ inline int64_t packed_offset(int64_t i, int q, int W) {
   return ((i >> 6) * W + q) * 64 + (i & 63);
 }
@@ -52,8 +62,8 @@ struct PrepassArgs {
   int S;                     // slots (columns) at this snapshot
   ParamTables slots;
   ParamTables pool;
-  const uint64_t* xpk;       // packed rows (tiled)
-  int W, wb;                 // packed words per row, bits per attribute
+  const uint64_t* xbs;       // bit-sliced rows (tiled), wb * Ws words per row
+  int Ws, wb;                // words per bit-plane, bits per attribute
   const uint64_t* slot_bnd;  // [slot][bw]
   const uint64_t* pool_bnd;  // [entry][bw]
   int bw;
@@ -205,6 +215,8 @@ struct MtGenArgs {
   // multi-workgroup generation (k_mt_gen_multi): workgroup g starts at block g * bpg from
   // the jump polynomial jpoly[g] (z^(624 * bpg * g - 1) mod phi, 312 words each)
   const uint64_t* jpoly;
+  const uint32_t* jidx;   // set-bit positions of jpoly[g]: jidx[joff[g] .. joff[g + 1])
+  const int* joff;
   int bpg;
   int G;
 };

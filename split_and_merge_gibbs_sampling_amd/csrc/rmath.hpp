@@ -149,9 +149,10 @@ inline void revsort(double* a0, int* ib0, int n) {
   }
 }
 
-// sample(x, 1, TRUE, probs) given the uniform rU it will consume.  Returns a 0-based
-// position or a negative Status.  `p` is scratch (n doubles), `perm` scratch (n ints).
-inline int sample_prob1_u(const double* probs, int n, double rU, double* p, int* perm) {
+// sample(x, 1, TRUE, probs) split into its parameter-only part -- FixupProb, the Walker
+// check, revsort and the cumulative sums, into p (n doubles) and perm (n ints) -- and the
+// pick for the uniform rU.  prep returns 0 or a negative Status.
+inline int sample_prob1_prep(const double* probs, int n, double* p, int* perm) {
   double sum = 0.0;
   int npos = 0;
   for (int i = 0; i < n; i++) {
@@ -167,10 +168,22 @@ inline int sample_prob1_u(const double* probs, int n, double rU, double* p, int*
   for (int i = 0; i < n; i++) perm[i] = i + 1;
   revsort(p, perm, n);
   for (int i = 1; i < n; i++) p[i] += p[i - 1];
+  return 0;
+}
+
+inline int sample_prob1_pick(const double* cum, const int* perm, int n, double rU) {
   int j;
   for (j = 0; j < n - 1; j++)
-    if (rU <= p[j]) break;
+    if (rU <= cum[j]) break;
   return perm[j] - 1;
+}
+
+// sample(x, 1, TRUE, probs) given the uniform rU it will consume.  Returns a 0-based
+// position or a negative Status.  `p` is scratch (n doubles), `perm` scratch (n ints).
+inline int sample_prob1_u(const double* probs, int n, double rU, double* p, int* perm) {
+  const int st = sample_prob1_prep(probs, n, p, perm);
+  if (st < 0) return st;
+  return sample_prob1_pick(p, perm, n, rU);
 }
 
 inline int sample_prob1(Rng& rng, const double* probs, int n, std::vector<double>& p,
@@ -190,16 +203,46 @@ inline int sample_prob1(Rng& rng, const double* probs, int n, std::vector<double
 }
 
 // ------------------------------------------------------------------ nmath rbeta
-inline double rbeta(Rng& rng, double aa, double bb) {
+// Split into the parameter-only setup (parallelisable) and the draw that consumes the
+// stream; rbeta(rng, aa, bb) == rbeta_draw(rng, rbeta_setup(aa, bb)) operation for operation.
+struct RBeta {
+  enum Kind { kConst, kCoin, kBC, kBB } kind;
+  double aa, a, b, alpha, beta, gamma, delta, k1, k2, cval;
+};
+
+__attribute__((always_inline)) inline RBeta rbeta_setup(double aa, double bb) {
+  RBeta r{};
+  r.aa = aa;
+  r.kind = RBeta::kConst;
+  if (std::isnan(aa) || std::isnan(bb) || aa < 0. || bb < 0.) { r.cval = NAN; return r; }
+  if (!std::isfinite(aa) && !std::isfinite(bb)) { r.cval = 0.5; return r; }
+  if (aa == 0. && bb == 0.) { r.kind = RBeta::kCoin; return r; }
+  if (!std::isfinite(aa) || bb == 0.) { r.cval = 1.0; return r; }
+  if (!std::isfinite(bb) || aa == 0.) { r.cval = 0.0; return r; }
+  r.a = std::fmin(aa, bb);
+  r.b = std::fmax(aa, bb);
+  r.alpha = r.a + r.b;
+  if (r.a <= 1.0) {  // Algorithm BC
+    r.kind = RBeta::kBC;
+    r.beta = 1.0 / r.a;
+    r.delta = 1.0 + r.b - r.a;
+    r.k1 = r.delta * (0.0138889 + 0.0416667 * r.a) / (r.b * r.beta - 0.777778);
+    r.k2 = 0.25 + (0.5 + 0.25 / r.delta) * r.a;
+  } else {           // Algorithm BB
+    r.kind = RBeta::kBB;
+    r.beta = std::sqrt((r.alpha - 2.0) / (2.0 * r.a * r.b - r.alpha));
+    r.gamma = r.a + 1.0 / r.beta;
+  }
+  return r;
+}
+
+__attribute__((always_inline)) inline double rbeta_draw(Rng& rng, const RBeta& p) {
   const double expmax = DBL_MAX_EXP * M_LN2;
-  if (std::isnan(aa) || std::isnan(bb) || aa < 0. || bb < 0.) return NAN;
-  if (!std::isfinite(aa) && !std::isfinite(bb)) return 0.5;
-  if (aa == 0. && bb == 0.) return (rng.unif() < 0.5) ? 0. : 1.;
-  if (!std::isfinite(aa) || bb == 0.) return 1.0;
-  if (!std::isfinite(bb) || aa == 0.) return 0.0;
-  const double a = std::fmin(aa, bb), b = std::fmax(aa, bb), alpha = a + b;
+  if (p.kind == RBeta::kConst) return p.cval;
+  if (p.kind == RBeta::kCoin) return (rng.unif() < 0.5) ? 0. : 1.;
+  const double a = p.a, b = p.b, alpha = p.alpha, beta = p.beta;
   double r, s, t = 0, u1, u2, v = 0, w = 0, y, z;
-  auto vw = [&](double beta, double AA) {
+  auto vw = [&](double AA) {
     v = beta * std::log(u1 / (1.0 - u1));
     if (v <= expmax) {
       w = AA * std::exp(v);
@@ -208,46 +251,42 @@ inline double rbeta(Rng& rng, double aa, double bb) {
       w = DBL_MAX;
     }
   };
-  if (a <= 1.0) {  // Algorithm BC
-    const double beta = 1.0 / a, delta = 1.0 + b - a;
-    const double k1 = delta * (0.0138889 + 0.0416667 * a) / (b * beta - 0.777778);
-    const double k2 = 0.25 + (0.5 + 0.25 / delta) * a;
+  if (p.kind == RBeta::kBC) {
     for (;;) {
       u1 = rng.unif();
       u2 = rng.unif();
       if (u1 < 0.5) {
         y = u1 * u2;
         z = u1 * y;
-        if (0.25 * u2 + z - y >= k1) continue;
+        if (0.25 * u2 + z - y >= p.k1) continue;
       } else {
         z = u1 * u1 * u2;
         if (z <= 0.25) {
-          vw(beta, b);
+          vw(b);
           break;
         }
-        if (z >= k2) continue;
+        if (z >= p.k2) continue;
       }
-      vw(beta, b);
+      vw(b);
       if (alpha * (std::log(alpha / (a + w)) + v) - 1.3862944 >= std::log(z)) break;
     }
-    return (aa == a) ? a / (a + w) : w / (a + w);
+    return (p.aa == a) ? a / (a + w) : w / (a + w);
   }
-  // Algorithm BB
-  const double beta = std::sqrt((alpha - 2.0) / (2.0 * a * b - alpha));
-  const double gamma = a + 1.0 / beta;
   do {
     u1 = rng.unif();
     u2 = rng.unif();
-    vw(beta, a);
+    vw(a);
     z = u1 * u1 * u2;
-    r = gamma * v - 1.3862944;
+    r = p.gamma * v - 1.3862944;
     s = a + r - w;
     if (s + 2.609438 >= 5.0 * z) break;
     t = std::log(z);
     if (s > t) break;
   } while (r + alpha * std::log(alpha / (b + w)) < t);
-  return (aa != a) ? b / (b + w) : w / (b + w);
+  return (p.aa != a) ? b / (b + w) : w / (b + w);
 }
+
+inline double rbeta(Rng& rng, double aa, double bb) { return rbeta_draw(rng, rbeta_setup(aa, bb)); }
 
 // ------------------------------------------------------------------ qbeta branch test
 namespace detail {

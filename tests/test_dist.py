@@ -69,7 +69,7 @@ def test_gloo_world2_barrier_and_max():
 def test_bench_helpers():
     import bench
     wb, W, bw = bench.packed_layout(128, 4)
-    assert (wb, W, bw) == (2, 4, 24)
+    assert (wb, W, bw) == (2, 4, 16)
     assert bench.prepass_bytes_per_point(128, 4, 3) == 8 * W + 16 + 4 + 3 * 8 * bw + 12
     assert bench.survey_sweep_bytes(10, 4, 1) == 10 * (4 * 11 + 8)
 

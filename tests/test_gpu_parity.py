@@ -142,6 +142,29 @@ def test_compute_loglikelihood_matches_sequential_sum(hd, oracle, zoo):
         eng.close()
 
 
+def test_compute_loglikelihood_from_counts_after_update_phi(hd, oracle):
+    # after a sweep + update_phi the engine regroups the sum into per-(cluster, attribute)
+    # match counts; it must agree with the per-point kernel (debug bit 2) and the oracle
+    ds = synth(30000, 96, 6, (2, 5), seed=8)
+    cen, sig = random_params(ds, 6, 11)
+    eng = make_engine(hd, ds)
+    eng.set_seed(5)
+    eng.set_state(ds.truth, cen, sig)
+    eng.generate_pool(ds.n * 2)
+    for _ in range(2):
+        eng.neal8_sweep(2)
+        eng.update_phi()
+        fast = eng.compute_loglikelihood()
+        eng.set_debug(4)
+        slow = eng.compute_loglikelihood()
+        eng.set_debug(0)
+        c, cen2, sig2 = eng.get_state()
+        ref = oracle.compute_loglikelihood(ds.codes, ds.attrisize, oracle_state(oracle, c, cen2, sig2))
+        assert abs(fast - slow) <= 1e-12 * abs(slow)
+        assert abs(fast - ref) <= RTOL * abs(ref)
+    eng.close()
+
+
 # ------------------------------------------------------------------ split-merge pieces
 def test_restricted_gibbs_matches_oracle(hd, oracle, zoo):
     cen, sig = random_params(zoo, 7, 10)
@@ -287,12 +310,12 @@ def test_device_mt_stream_matches_r(hd, oracle, zoo, pre):
 
 @pytest.mark.parametrize("pre", [0, 311, 624])
 def test_device_mt_stream_jump_ahead_matches_r(hd, oracle, zoo, pre):
-    # windows above 64 * 624 * 8 draws use 64 workgroups started by jump polynomials
+    # windows of at least 256 * 624 * 8 draws use 256 workgroups started by jump polynomials
     eng = make_engine(hd, zoo)
     st = oracle.seed_state(2718)
     oracle.runif(st, pre)
     eng.rng_state = st
-    for count in (400_000, 1_234_567):
+    for count in (400_000, 1_300_001, 2_500_000):
         got = eng.rng_fill_device(count)
         ref = oracle.runif(st, count)
         assert np.array_equal(got.astype(np.float64) * 2.3283064365386963e-10, ref)
