@@ -124,10 +124,12 @@ static void parallel_for(int64_t n, F f) {
   for (auto& x : th) x.join();
 }
 
-// Persistent host worker pool for the per-iteration host phases (parameter draws'
-// deterministic parts, table builds).  Workers spin for a short while after a job and
-// then sleep, so back-to-back iterations dispatch in about a microsecond.
-// HDPM_HOST_THREADS sets the number of threads (default min(8, hardware threads)).
+// Persistent host worker pool for the per-iteration host phases (the deterministic parts
+// of the parameter draws, table builds).  Workers spin for a short while after a job and
+// then sleep; prewake() gets sleeping workers spinning ahead of a job (e.g. while the
+// host waits for the device), so dispatch costs about a microsecond.
+// HDPM_HOST_THREADS sets the number of threads (default min(8, hardware threads)),
+// HDPM_SPIN_US the spin window.
 class HostPool {
  public:
   static HostPool& get() {
@@ -135,7 +137,9 @@ class HostPool {
     return p;
   }
   int threads() const { return (int)th_.size() + 1; }
-  // f(lo, hi) over [0, n) in chunks of `grain`; returns when all chunks are done.
+  int workers() const { return (int)th_.size(); }
+
+  // f(lo, hi) over [0, n) in chunks of `grain` on all threads; returns when done.
   template <class F>
   void run(int64_t n, int64_t grain, F&& f) {
     if (n <= 0) return;
@@ -144,20 +148,45 @@ class HostPool {
       return;
     }
     std::lock_guard<std::mutex> serial(run_mu_);
-    while (active_.load(std::memory_order_acquire) != 0) spin_pause();
-    job_ = [&f](int64_t a, int64_t b) { f(a, b); };
+    quiesce();
+    range_ = [&f](int64_t a, int64_t b) { f(a, b); };
+    bcast_ = nullptr;
     total_ = n;
     grain_ = grain;
     next_.store(0, std::memory_order_relaxed);
     done_.store(0, std::memory_order_relaxed);
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      gen_.fetch_add(1, std::memory_order_release);
-    }
-    cv_.notify_all();
+    publish();
     work();
     while (done_.load(std::memory_order_acquire) < total_) spin_pause();
   }
+
+  // Every worker calls f(worker_index) once; the caller continues (join() waits).
+  template <class F>
+  void launch(F&& f) {
+    run_mu_.lock();
+    quiesce();
+    bjob_ = std::forward<F>(f);
+    bcast_ = &bjob_;
+    range_ = nullptr;
+    bdone_.store(0, std::memory_order_relaxed);
+    widx_.store(0, std::memory_order_relaxed);
+    publish();
+  }
+  void join() {
+    while (bdone_.load(std::memory_order_acquire) < (int)th_.size()) spin_pause();
+    run_mu_.unlock();
+  }
+
+  void prewake() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      wake_seq_.fetch_add(1, std::memory_order_release);
+    }
+    cv_.notify_all();
+  }
+
+  static void spin_pause() { __builtin_ia32_pause(); }
+
   ~HostPool() {
     {
       std::lock_guard<std::mutex> lk(mu_);
@@ -178,18 +207,27 @@ class HostPool {
     }
     for (int t = 1; t < T; ++t) th_.emplace_back([this] { loop(); });
   }
-  static void spin_pause() { __builtin_ia32_pause(); }
+  void quiesce() {
+    while (active_.load(std::memory_order_acquire) != 0) spin_pause();
+  }
+  void publish() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      gen_.fetch_add(1, std::memory_order_release);
+    }
+    cv_.notify_all();
+  }
   void work() {
     for (;;) {
       const int64_t a = next_.fetch_add(grain_, std::memory_order_relaxed);
       if (a >= total_) break;
       const int64_t b = std::min(total_, a + grain_);
-      job_(a, b);
+      range_(a, b);
       done_.fetch_add(b - a, std::memory_order_release);
     }
   }
   void loop() {
-    uint64_t seen = 0;
+    uint64_t seen = 0, woke = 0;
     for (;;) {
       auto t0 = std::chrono::steady_clock::now();
       int polls = 0;
@@ -198,7 +236,12 @@ class HostPool {
         const uint64_t g = gen_.load(std::memory_order_acquire);
         if (g != seen) {
           seen = g;
-          work();
+          if (bcast_) {
+            (*bcast_)(widx_.fetch_add(1, std::memory_order_relaxed));
+            bdone_.fetch_add(1, std::memory_order_acq_rel);
+          } else {
+            work();
+          }
           active_.fetch_sub(1, std::memory_order_acq_rel);
           break;
         }
@@ -207,7 +250,11 @@ class HostPool {
         spin_pause();
         if (++polls % 256 == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us_)) {
           std::unique_lock<std::mutex> lk(mu_);
-          cv_.wait(lk, [&] { return stop_ || gen_.load(std::memory_order_acquire) != seen; });
+          cv_.wait(lk, [&] {
+            return stop_ || gen_.load(std::memory_order_acquire) != seen ||
+                   wake_seq_.load(std::memory_order_acquire) != woke;
+          });
+          woke = wake_seq_.load(std::memory_order_acquire);
           if (stop_) return;
           t0 = std::chrono::steady_clock::now();
         }
@@ -217,13 +264,15 @@ class HostPool {
   std::vector<std::thread> th_;
   std::mutex mu_, run_mu_;
   std::condition_variable cv_;
-  std::atomic<uint64_t> gen_{0};
-  std::atomic<int> active_{0};
+  std::atomic<uint64_t> gen_{0}, wake_seq_{0};
+  std::atomic<int> active_{0}, bdone_{0}, widx_{0};
   std::atomic<int64_t> next_{0}, done_{0};
   int64_t total_ = 0, grain_ = 1;
-  std::function<void(int64_t, int64_t)> job_;
+  std::function<void(int64_t, int64_t)> range_;
+  std::function<void(int)> bjob_;
+  std::function<void(int)>* bcast_ = nullptr;
   std::atomic<bool> stop_{false};
-  int spin_us_ = 3000;   // busy-wait this long after a job before sleeping (iterations ~1 ms apart)
+  int spin_us_ = 300;
 };
 
 template <class F>
@@ -256,7 +305,6 @@ struct RngWindow {
   int64_t count = 0;
   int mti0 = 624, nblocks = 0, export_from = 1;
   int64_t export_after = 0;
-  uint32_t x0[624];
   hipEvent_t done = nullptr;
   bool valid = false;
 };
@@ -272,6 +320,15 @@ struct Ctx {
   DevBuf<uint32_t> d_jidx;
   DevBuf<int> d_joff;
   int64_t cmax = 1 << 16;          // draws expected between two sweeps (update_phi etc.)
+  // Host-state adoption in flight: rng.pos is current, rng.mt / rng.mti arrive with `ev`
+  // (rng_sync() before any host use of the stream).
+  struct PendingAdopt {
+    bool active = false;
+    hipEvent_t ev = nullptr;
+    PinBuf<uint32_t> arr;
+    const uint32_t* host_src = nullptr;
+    int mti = 0;
+  } pend;
   std::string err;
   hipEvent_t ev[8];
 
@@ -339,6 +396,9 @@ struct Ctx {
   DevBuf<unsigned> d_freq;
   PinBuf<unsigned> h_freq;
   DevBuf<unsigned char> d_mask;
+  PinBuf<unsigned char> h_mask;
+  StreamAhead phi_stream;             // update_phi's slice of the R stream, generated ahead
+  int64_t phi_prefetch = 4096;
   DevBuf<double> d_partial;
   PinBuf<double> h_partial;
 
@@ -356,6 +416,7 @@ struct Ctx {
       (void)hipStreamSynchronize(gstream);
       for (auto& w : win)
         if (w.done) (void)hipEventDestroy(w.done);
+      if (pend.ev) (void)hipEventDestroy(pend.ev);
       (void)hipStreamDestroy(gstream);
     }
     if (stream) {
@@ -367,7 +428,41 @@ struct Ctx {
   }
 
   // ------------------------------------------------------------------ device random stream
+  void rng_sync() {
+    if (!pend.active) return;
+    HIPCHK(hipEventSynchronize(pend.ev));
+    std::memcpy(rng.mt, pend.host_src ? pend.host_src : pend.arr.p, sizeof(rng.mt));
+    rng.mti = pend.mti;
+    pend.active = false;
+  }
+  void rng_drop_pending() { pend.active = false; }
+
+  void size_window(RngWindow& W, int64_t count, int64_t export_after) {
+    const int head = W.mti0 >= 624 ? 0 : 624 - W.mti0;
+    W.nblocks = count > head ? (int)((count - head + 623) / 624) : 0;
+    W.count = count;
+    W.raw.ensure(count);
+    W.arrays.ensure((size_t)std::max(W.nblocks, 1) * 624);
+    W.init.ensure(624);
+    W.h_init.ensure(624);
+    if (!W.done) HIPCHK(hipEventCreateWithFlags(&W.done, hipEventDisableTiming));
+    // the host adopts states only at or after `export_after` draws into the window
+    W.export_from = (int)std::max<int64_t>(1, (export_after - head) / 624 - 1);
+    W.export_after = export_after;
+  }
+  void run_window(RngWindow& W) {
+    ensure_jump(W.count);
+    const bool multi = mt_G > 1 && W.count >= (int64_t)mt_G * 624 * 8;
+    MtGenArgs a{W.init.p, W.mti0, W.count, W.raw.p, W.arrays.p, W.nblocks, W.export_from,
+                multi ? d_jpoly.p : nullptr, d_jidx.p, d_joff.p, mt_bpg, multi ? mt_G : 1};
+    HIPCHK(launch_mt_gen(a, gstream));
+    HIPCHK(hipEventRecord(W.done, gstream));
+    W.valid = true;
+  }
+
+  // Window starting at the host stream's current state.
   void launch_window(RngWindow& W, int64_t count, int64_t export_after = 0) {
+    rng_sync();
     if (rng.mti == 625) {  // never seeded: R seeds with 4357 (MT_sgenrand) on the first draw
       uint32_t seed = 4357;
       for (int i = 0; i < 624; i++) {
@@ -380,29 +475,44 @@ struct Ctx {
     }
     HIPCHK(hipStreamSynchronize(gstream));  // previous use of W's buffers is complete
     W.mti0 = rng.mti;
-    std::memcpy(W.x0, rng.mt, sizeof(W.x0));
     W.start_pos = rng.pos;
     W.epoch = rng.epoch;
-    const int head = W.mti0 >= 624 ? 0 : 624 - W.mti0;
-    W.nblocks = count > head ? (int)((count - head + 623) / 624) : 0;
-    W.count = count;
-    W.raw.ensure(count);
-    W.arrays.ensure((size_t)std::max(W.nblocks, 1) * 624);
-    W.init.ensure(624);
-    W.h_init.ensure(624);
-    std::memcpy(W.h_init.p, W.x0, sizeof(W.x0));
-    if (!W.done) HIPCHK(hipEventCreateWithFlags(&W.done, hipEventDisableTiming));
+    size_window(W, count, export_after);
+    std::memcpy(W.h_init.p, rng.mt, sizeof(rng.mt));
     HIPCHK(hipMemcpyAsync(W.init.p, W.h_init.p, 624 * 4, hipMemcpyHostToDevice, gstream));
-    // the host adopts states only at or after `export_after` draws into the window
-    W.export_from = (int)std::max<int64_t>(1, (export_after - head) / 624 - 1);
-    W.export_after = export_after;
-    ensure_jump(count);
-    const bool multi = mt_G > 1 && count >= (int64_t)mt_G * 624 * 8;
-    MtGenArgs a{W.init.p, W.mti0, count, W.raw.p, W.arrays.p, W.nblocks, W.export_from,
-                multi ? d_jpoly.p : nullptr, d_jidx.p, d_joff.p, mt_bpg, multi ? mt_G : 1};
-    HIPCHK(launch_mt_gen(a, gstream));
-    HIPCHK(hipEventRecord(W.done, gstream));
-    W.valid = true;
+    run_window(W);
+  }
+
+  // Block and mti of the state after `target` draws, inside window W (R keeps mti = 624
+  // at a block edge).  blk 0 = W's initial array.
+  void locate(const RngWindow& W, uint64_t target, int64_t* blk, int* mti) const {
+    const uint64_t r = target - W.start_pos;
+    const uint64_t head = W.mti0 >= 624 ? 0 : 624 - W.mti0;
+    if (r < head) {
+      *blk = 0;
+      *mti = W.mti0 + (int)r;
+      return;
+    }
+    const uint64_t b = 1 + (r - head) / 624, k = (r - head) % 624;
+    *blk = (int64_t)(k == 0 ? b - 1 : b);
+    *mti = k == 0 ? 624 : (int)k;
+    if (*blk != 0 && *blk < W.export_from) throw HipError{hipErrorInvalidValue, "rng window export"};
+  }
+
+  // Window Wn starting at position `target` of window Ws, initialised on the device from
+  // Ws's exported arrays (no host round trip).
+  void launch_window_from(RngWindow& Wn, RngWindow& Ws, uint64_t target, int64_t count, int64_t export_after) {
+    int64_t blk;
+    int mti;
+    locate(Ws, target, &blk, &mti);
+    Wn.mti0 = mti;
+    Wn.start_pos = target;
+    Wn.epoch = rng.epoch;
+    size_window(Wn, count, export_after);
+    const uint32_t* src = blk == 0 ? Ws.init.p : Ws.arrays.p + (blk - 1) * 624;
+    HIPCHK(hipMemcpyAsync(Wn.init.p, src, 624 * 4, hipMemcpyDeviceToDevice, gstream));
+    HIPCHK(hipMemcpyAsync(Wn.h_init.p, Wn.init.p, 624 * 4, hipMemcpyDeviceToHost, gstream));
+    run_window(Wn);
   }
 
   // Jump polynomials z^(624 * bpg * g) mod phi for g < G, built once per window size class
@@ -466,27 +576,28 @@ struct Ctx {
            p + n >= W.start_pos + (uint64_t)W.export_after;
   }
 
-  // Make the host stream continue at position `target` inside window W.
+  // Make the host stream continue at position `target` inside window W: rng.pos now, the
+  // state array asynchronously (rng_sync()).
   void adopt_state_at(RngWindow& W, uint64_t target) {
-    HIPCHK(hipEventSynchronize(W.done));
-    const uint64_t r = target - W.start_pos;
-    const uint64_t head = W.mti0 >= 624 ? 0 : 624 - W.mti0;
-    if (r < head) {
-      std::memcpy(rng.mt, W.x0, sizeof(W.x0));
-      rng.mti = W.mti0 + (int)r;
+    int64_t blk;
+    int mti;
+    locate(W, target, &blk, &mti);
+    if (!pend.ev) HIPCHK(hipEventCreateWithFlags(&pend.ev, hipEventDisableTiming));
+    if (blk == 0) {
+      pend.host_src = W.h_init.p;     // valid once W's init has landed (W.done)
     } else {
-      const uint64_t b = 1 + (r - head) / 624, k = (r - head) % 624;
-      const uint64_t blk = k == 0 ? b - 1 : b;   // at a block edge R keeps mti = 624
-      if (blk != 0 && (int64_t)blk < W.export_from) throw HipError{hipErrorInvalidValue, "rng window export"};
-      if (blk == 0) std::memcpy(rng.mt, W.x0, sizeof(W.x0));
-      else HIPCHK(hipMemcpy(rng.mt, W.arrays.p + (blk - 1) * 624, 624 * 4, hipMemcpyDeviceToHost));
-      rng.mti = k == 0 ? 624 : (int)k;
+      pend.arr.ensure(624);
+      pend.host_src = nullptr;
+      HIPCHK(hipMemcpyAsync(pend.arr.p, W.arrays.p + (blk - 1) * 624, 624 * 4, hipMemcpyDeviceToHost, gstream));
     }
+    HIPCHK(hipEventRecord(pend.ev, gstream));
+    pend.mti = mti;
+    pend.active = true;
     rng.pos = target;
   }
 
   // Device pointer to the next n raw draws of the stream; advances the host stream past
-  // them and prefetches the following window.
+  // them and starts generating the following window from where they end.
   const uint32_t* device_draws(int64_t n) {
     RngWindow* W = nullptr;
     for (auto& w : win)
@@ -498,9 +609,10 @@ struct Ctx {
     }
     HIPCHK(hipStreamWaitEvent(stream, W->done, 0));
     const uint32_t* p = W->raw.p + (rng.pos - W->start_pos);
-    adopt_state_at(*W, rng.pos + n);
+    const uint64_t target = rng.pos + n;
+    adopt_state_at(*W, target);
     RngWindow* other = (W == &win[0]) ? &win[1] : &win[0];
-    launch_window(*other, n + cmax, n);
+    launch_window_from(*other, *W, target, n + cmax, n);
     return p;
   }
 
@@ -560,29 +672,39 @@ struct Ctx {
 
   // Cluster parameters of `which` (nullptr: labels 0..K-1 with counts and identity slot
   // maps) through the pinned staging buffer: one copy + one scatter kernel, no host wait.
-  void stage_upload(const std::vector<int>* which) {
-    const int nent = which ? (int)which->size() : K;
-    if (nent == 0) return;
+  // Three steps so that callers can fill entries concurrently: stage_begin (wait until
+  // the previous upload has left the buffer), stage_entry per entry r (label k),
+  // stage_commit (copy + scatter).
+  UploadLayout stage_begin(int nent) {
     const UploadLayout L = upload_layout(nent, dp, d, bw);
     if (!ev_stage) HIPCHK(hipEventCreateWithFlags(&ev_stage, hipEventDisableTiming));
     HIPCHK(hipEventSynchronize(ev_stage));          // the previous upload has left h_stage
     h_stage.ensure(L.bytes);
     d_stage.ensure(L.bytes);
+    return L;
+  }
+  void stage_entry(const UploadLayout& L, int r, int k) {
     uint8_t* st = h_stage.p;
-    auto one = [&](int r) {
-      const int k = which ? (*which)[r] : r;
-      double* tt = (double*)(st + L.off_tab) + (size_t)r * 2 * d;
-      tables_for(&h_center[(size_t)k * d], &h_sigma[(size_t)k * d], st + L.off_codes + (size_t)r * dp, tt);
-      bounds_for(&h_center[(size_t)k * d], tt, (uint64_t*)(st + L.off_bnd) + (size_t)r * bw);
-      ((int*)(st + L.off_counts))[r] = h_counts[k];
-      ((int*)(st + L.off_slot))[r] = k;
-    };
-    pool_for(nent, one);
-    HIPCHK(hipMemcpyAsync(d_stage.p, st, L.bytes, hipMemcpyHostToDevice, stream));
+    double* tt = (double*)(st + L.off_tab) + (size_t)r * 2 * d;
+    tables_for(&h_center[(size_t)k * d], &h_sigma[(size_t)k * d], st + L.off_codes + (size_t)r * dp, tt);
+    bounds_for(&h_center[(size_t)k * d], tt, (uint64_t*)(st + L.off_bnd) + (size_t)r * bw);
+    ((int*)(st + L.off_counts))[r] = h_counts[k];
+    ((int*)(st + L.off_slot))[r] = k;
+  }
+  void stage_commit(const UploadLayout& L, int nent, bool full) {
+    HIPCHK(hipMemcpyAsync(d_stage.p, h_stage.p, L.bytes, hipMemcpyHostToDevice, stream));
     HIPCHK(hipEventRecord(ev_stage, stream));
-    stage_full = which == nullptr;
-    HIPCHK(launch_scatter_clusters(d_stage.p, nent, dp, d, bw, which ? 0 : 1, d_slot_codes.p, d_slot_tab.p,
+    stage_full = full;
+    HIPCHK(launch_scatter_clusters(d_stage.p, nent, dp, d, bw, full ? 1 : 0, d_slot_codes.p, d_slot_tab.p,
                                    d_slot_bnd.p, d_counts.p, d_sol.p, d_los.p, d_src.p, stream));
+  }
+
+  void stage_upload(const std::vector<int>* which) {
+    const int nent = which ? (int)which->size() : K;
+    if (nent == 0) return;
+    const UploadLayout L = stage_begin(nent);
+    pool_for(nent, [&](int r) { stage_entry(L, r, which ? (*which)[r] : r); });
+    stage_commit(L, nent, which == nullptr);
   }
 
   // Upload label tables, counts and identity slot maps for labels 0..K-1.
@@ -635,6 +757,7 @@ struct Ctx {
 
   // sample_sigma_1_cluster (cf:218-235)
   int sample_sigma(const double* vv, const double* ww, double* out) {
+    rng_sync();
     for (int j = 0; j < d; ++j) {
       int e = kOk;
       const double mj = (double)att[j];
@@ -645,6 +768,7 @@ struct Ctx {
   }
   // sample_center_1_cluster without probabilities (cf:198-199)
   void sample_center_uniform(uint8_t* out) {
+    rng_sync();
     for (int j = 0; j < d; ++j) out[j] = (uint8_t)(int)(att[j] * rng.unif() + 1);
   }
 
@@ -957,6 +1081,10 @@ struct Ctx {
   // ------------------------------------------------------------------ update_phi
   // freq[k][j][l] for the labels in mask (device histogram), downloaded to h_freq.
   void histogram(const std::vector<unsigned char>* mask) {
+    histogram_launch(mask);
+    histogram_wait(mask);
+  }
+  void histogram_launch(const std::vector<unsigned char>* mask) {
     const size_t nent = (size_t)K * d * mmax;
     d_freq.ensure(std::max<size_t>(nent, 1));
     HistArgs ha;
@@ -971,12 +1099,16 @@ struct Ctx {
     }
     if (mask) {
       d_mask.ensure(std::max(K, 1));
-      HIPCHK(hipMemcpyAsync(d_mask.p, mask->data(), K, hipMemcpyHostToDevice, stream));
+      h_mask.ensure(std::max(K, 1));
+      std::memcpy(h_mask.p, mask->data(), K);
+      HIPCHK(hipMemcpyAsync(d_mask.p, h_mask.p, K, hipMemcpyHostToDevice, stream));
       ha.mask = d_mask.p;
     }
     HIPCHK(launch_hist(ha, stream));
     h_freq.ensure(std::max<size_t>(nent, 1));
     HIPCHK(hipMemcpyAsync(h_freq.p, d_freq.p, nent * 4, hipMemcpyDeviceToHost, stream));
+  }
+  void histogram_wait(const std::vector<unsigned char>* mask) {
     HIPCHK(hipStreamSynchronize(stream));
     freq_version = mask ? 0 : labels_version;
   }
@@ -1006,11 +1138,20 @@ struct Ctx {
 
   int update_phi(const int32_t* idx, int nidx) {
     if (!have_state) { err = "no state"; return kArg; }
+    HostPool& pool = HostPool::get();
+    pool.prewake();                                   // workers spin while the device counts
     auto t0 = std::chrono::steady_clock::now();
     std::vector<unsigned char> mask(K, nidx == 0 ? 1 : 0);
     for (int q = 0; q < nidx; ++q)
       if (idx[q] >= 0 && idx[q] < K) mask[idx[q]] = 1;
-    histogram(nidx == 0 ? nullptr : &mask);
+    histogram_launch(nidx == 0 ? nullptr : &mask);
+    // while the device counts: the next stretch of the stream and its logits
+    rng_sync();
+    StreamAhead& sa = phi_stream;
+    sa.live = &rng;
+    if (sa.fill(rng, phi_prefetch))
+      pool.run(sa.n, 1024, [&](int64_t a0, int64_t a1) { sa.logits(a0, a1); });
+    histogram_wait(nidx == 0 ? nullptr : &mask);
     auto t1 = std::chrono::steady_clock::now();
     std::vector<int> touched;
     for (int i = 0; i < K; ++i)
@@ -1023,46 +1164,68 @@ struct Ctx {
     phi_items.resize((size_t)T * d);
     phi_cum.resize((size_t)T * sumatt);
     phi_perm.resize((size_t)T * sumatt);
-    // ---- phase A
-    pool_for((int64_t)T * d, [&](int it) {
-      const int t = it / d, j = it - t * d;
+    // staging of the new tables: all labels when every label is updated (or the device
+    // tables are stale), else the touched ones
+    const bool full = tables_dirty || T == K;
+    if (full) ensure_slots(K + 2);
+    const int nent = full ? K : T;
+    const UploadLayout L = stage_begin(std::max(nent, 1));
+
+    // ---- phase A: one cluster at a time, in order
+    auto phaseA = [&](int t) {
       const int k = touched[t];
       const int nn = h_counts[k];
-      const int mj = att[j];
-      const unsigned* fj = &h_freq.p[((size_t)k * d + j) * mmax];
-      const double sg = h_sigma[(size_t)k * d + j];
-      double prob[256];
-      for (int l = 0; l < mj; ++l) prob[l] = (-((double)nn - (double)fj[l])) / sg;
-      double mx = prob[0];
-      for (int l = 1; l < mj; ++l) if (prob[l] > mx) mx = prob[l];
-      for (int l = 0; l < mj; ++l) prob[l] = std::exp(prob[l] - mx);
-      double sum = 0.0;
-      for (int l = 0; l < mj; ++l) sum += prob[l];
-      for (int l = 0; l < mj; ++l) prob[l] = prob[l] / sum;
-      PhiItem& P = phi_items[it];
-      double* cum = &phi_cum[(size_t)t * sumatt + phi_off[j]];
-      int* perm = &phi_perm[(size_t)t * sumatt + phi_off[j]];
-      P.err = -sample_prob1_prep(prob, mj, cum, perm);
-      P.lstar = -1;
-      if (P.err) return;
-      const int l = perm[0] - 1;
-      const double sumdelta = (double)fj[l];
-      const double nw_ = w[j] + nn - sumdelta, nv_ = v[j] + sumdelta;
-      P.lstar = l;
-      P.bp = rhig_beta_path(nv_, nw_, (double)mj);
-      if (P.bp) P.rb = rbeta_setup(nw_ + 1, nv_ - 1);
-    });
-    auto tA = std::chrono::steady_clock::now();
-    // ---- phase B
-    for (int t = 0; t < T; ++t) {
+      for (int j = 0; j < d; ++j) {
+        const int mj = att[j];
+        const unsigned* fj = &h_freq.p[((size_t)k * d + j) * mmax];
+        const double sg = h_sigma[(size_t)k * d + j];
+        double prob[256];
+        for (int l = 0; l < mj; ++l) prob[l] = (-((double)nn - (double)fj[l])) / sg;
+        double mx = prob[0];
+        for (int l = 1; l < mj; ++l) if (prob[l] > mx) mx = prob[l];
+        for (int l = 0; l < mj; ++l) prob[l] = std::exp(prob[l] - mx);
+        double sum = 0.0;
+        for (int l = 0; l < mj; ++l) sum += prob[l];
+        for (int l = 0; l < mj; ++l) prob[l] = prob[l] / sum;
+        PhiItem& P = phi_items[(size_t)t * d + j];
+        double* cum = &phi_cum[(size_t)t * sumatt + phi_off[j]];
+        int* perm = &phi_perm[(size_t)t * sumatt + phi_off[j]];
+        P.err = -sample_prob1_prep(prob, mj, cum, perm);
+        P.lstar = -1;
+        if (P.err) continue;
+        const int l = perm[0] - 1;
+        const double sumdelta = (double)fj[l];
+        const double nw_ = w[j] + nn - sumdelta, nv_ = v[j] + sumdelta;
+        P.lstar = l;
+        P.bp = rhig_beta_path(nv_, nw_, (double)mj);
+        if (P.bp) P.rb = rbeta_setup(nw_ + 1, nv_ - 1);
+      }
+    };
+    // ---- phase B: the stream-consuming draws of cluster t (reference order)
+    auto phaseB = [&](int t) -> int {
       const int k = touched[t];
       const int nn = h_counts[k];
       uint8_t* cen = &h_center[(size_t)k * d];
+      // the items were written by other cores: prefetch a few ahead (cross-core misses
+      // would otherwise serialise this loop)
+      constexpr int kAhead = 8;
+      for (int j = 0; j < std::min(d, kAhead); ++j) {
+        __builtin_prefetch(&phi_items[(size_t)t * d + j]);
+        __builtin_prefetch(&phi_cum[(size_t)t * sumatt + phi_off[j]]);
+      }
       for (int j = 0; j < d; ++j) {
+        if (j + kAhead < d) {
+          const size_t ja = (size_t)t * d + j + kAhead;
+          __builtin_prefetch(&phi_items[ja]);
+          __builtin_prefetch((const char*)&phi_items[ja] + 64);
+          __builtin_prefetch(&phi_cum[(size_t)t * sumatt + phi_off[j + kAhead]]);
+          __builtin_prefetch(&phi_perm[(size_t)t * sumatt + phi_off[j + kAhead]]);
+          __builtin_prefetch(&h_freq.p[((size_t)k * d + j + kAhead) * mmax]);
+        }
         const PhiItem& P = phi_items[(size_t)t * d + j];
-        if (P.err) { err = "center draw failed"; return P.err; }
+        if (P.err) return P.err;
         const size_t o = (size_t)t * sumatt + phi_off[j];
-        cen[j] = (uint8_t)(sample_prob1_pick(&phi_cum[o], &phi_perm[o], att[j], rng.unif()) + 1);
+        cen[j] = (uint8_t)(sample_prob1_pick(&phi_cum[o], &phi_perm[o], att[j], sa.next(nullptr)) + 1);
       }
       for (int j = 0; j < d; ++j) {
         PhiItem& P = phi_items[(size_t)t * d + j];
@@ -1081,46 +1244,112 @@ struct Ctx {
           if (bp) rb = rbeta_setup(P.nw + 1, P.nv - 1);
         }
         if (bp) {                                   // hg:359-363
-          double x = rbeta_draw(rng, rb);
-          while (x > (mj - 1) / mj) x = rbeta_draw(rng, rb);
+          double x = rbeta_draw_s(sa, rb);
+          while (x > (mj - 1) / mj) x = rbeta_draw_s(sa, rb);
           P.path = 1;
           P.x = x;
         } else {                                    // hg:365-367
           P.path = 2;
-          P.x = rng.unif();
+          P.x = sa.next(nullptr);
         }
       }
+      return 0;
+    };
+    // ---- phase C: sigma of cluster t, then its staged tables; returns false on a GSL error
+    auto phaseC = [&](int t) -> bool {
+      const int k = touched[t];
+      bool ok = true;
+      for (int j = 0; j < d; ++j) {
+        PhiItem& P = phi_items[(size_t)t * d + j];
+        const double mj = (double)att[j];
+        double out;
+        if (P.path == 1) {
+          out = P.x / ((mj - 1) * (1 - P.x));
+        } else {
+          int e = kOk;
+          out = bisec_hyper2(P.nw, P.nv, mj, P.x, &e);
+          if (e) { ok = false; continue; }
+        }
+        h_sigma[(size_t)k * d + j] = -1 / std::log(out);
+      }
+      if (ok) stage_entry(L, full ? k : t, k);
+      return ok;
+    };
+
+    // Pipeline: workers run A for clusters in order, then C for clusters whose B is done;
+    // this thread runs B in order as soon as A of the cluster is ready.
+    std::vector<std::atomic<int>> stA(T), stB(T);
+    for (int t = 0; t < T; ++t) { stA[t].store(0); stB[t].store(0); }
+    std::atomic<int> nextA{0}, nextC{0}, gsl_err{-1};
+    auto worker = [&](int) {
+      for (;;) {
+        const int t = nextA.fetch_add(1);
+        if (t >= T) break;
+        phaseA(t);
+        stA[t].store(1, std::memory_order_release);
+      }
+      for (;;) {
+        const int t = nextC.fetch_add(1);
+        if (t >= T) break;
+        int b;
+        while ((b = stB[t].load(std::memory_order_acquire)) == 0) HostPool::spin_pause();
+        if (b < 0) break;                           // B stopped on an error
+        if (!phaseC(t)) {
+          int cur = gsl_err.load();
+          while ((cur < 0 || t < cur) && !gsl_err.compare_exchange_weak(cur, t)) {}
+        }
+      }
+    };
+    const bool par = pool.workers() > 0 && T > 1;
+    if (par) pool.launch(worker);
+    else for (int t = 0; t < T; ++t) phaseA(t);
+    int berr = 0;
+    int tb = 0;
+    for (; tb < T; ++tb) {
+      while (stA[tb].load(std::memory_order_acquire) == 0 && par) HostPool::spin_pause();
+      berr = phaseB(tb);
+      if (berr) break;
+      stB[tb].store(1, std::memory_order_release);
     }
+    for (int t = tb; t < T; ++t) stB[t].store(-1, std::memory_order_release);
+    sa.finish();                                      // the host stream continues after B's draws
+    phi_prefetch = std::max<int64_t>(4096, sa.used + sa.used / 4 + 512);
     auto tB = std::chrono::steady_clock::now();
-    // ---- phase C
-    std::atomic<int> first_err{-1};
-    pool_for((int64_t)T * d, [&](int it) {
-      const int t = it / d, j = it - t * d;
-      PhiItem& P = phi_items[it];
-      const double mj = (double)att[j];
-      double out;
-      if (P.path == 1) {
-        out = P.x / ((mj - 1) * (1 - P.x));
-      } else {
-        int e = kOk;
-        out = bisec_hyper2(P.nw, P.nv, mj, P.x, &e);
-        if (e) {
-          int cur = first_err.load();
-          while ((cur < 0 || it < cur) && !first_err.compare_exchange_weak(cur, it)) {}
-          return;
+    if (par) {
+      // help with the remaining C work, then wait for the workers
+      for (;;) {
+        const int t = nextC.fetch_add(1);
+        if (t >= T) break;
+        if (stB[t].load(std::memory_order_acquire) < 0) break;
+        if (!phaseC(t)) {
+          int cur = gsl_err.load();
+          while ((cur < 0 || t < cur) && !gsl_err.compare_exchange_weak(cur, t)) {}
         }
       }
-      h_sigma[(size_t)touched[t] * d + j] = -1 / std::log(out);
-    });
+      pool.join();
+    } else if (!berr) {
+      for (int t = 0; t < T; ++t)
+        if (!phaseC(t) && gsl_err.load() < 0) gsl_err.store(t);
+    }
     auto tC = std::chrono::steady_clock::now();
-    if (first_err.load() >= 0) { err = "norm_const2 - hypergeometric diverging with infinity"; return kGsl; }
-    if (tables_dirty || T == K) upload_clusters();
-    else upload_some(touched);
+    if (berr) { err = "center draw failed"; return berr; }
+    if (gsl_err.load() >= 0) { err = "norm_const2 - hypergeometric diverging with infinity"; return kGsl; }
+    if (full) {
+      // labels that were not updated still need their (unchanged) tables staged
+      std::vector<char> done(K, 0);
+      for (int k : touched) done[k] = 1;
+      for (int k = 0; k < K; ++k)
+        if (!done[k]) stage_entry(L, k, k);
+      if (K) stage_commit(L, K, true);
+      tables_dirty = false;
+    } else if (T) {
+      stage_commit(L, T, false);
+    }
     auto t2 = std::chrono::steady_clock::now();
     if (debug & 2) {
       auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
-      std::fprintf(stderr, "[phi] hist %.1f us, A %.1f, B %.1f, C %.1f, upload %.1f us (%d x %d items, %d threads)\n",
-                   us(t0, t1), us(t1, tA), us(tA, tB), us(tB, tC), us(tC, t2), T, d, HostPool::get().threads());
+      std::fprintf(stderr, "[phi] hist %.1f us, A+B %.1f, C tail %.1f, commit %.1f us (%d x %d items, %d threads)\n",
+                   us(t0, t1), us(t1, tB), us(tB, tC), us(tC, t2), T, d, pool.threads());
     }
     stats.t_stats_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
     stats.t_host_phi_ms += std::chrono::duration<double, std::milli>(t2 - t1).count();
@@ -1221,6 +1450,7 @@ namespace hdpm {
 // la:27-77
 int Ctx::init_chain(const hdpm_chain_params* p, const int32_t* c_init) {
   if (!n) { err = "set_data first"; return kArg; }
+  rng_sync();
   K = p->L;
   h_c.resize(n);
   if (c_init) {
@@ -1388,20 +1618,26 @@ int hdpm_set_data(hdpm_ctx* h, const uint8_t* codes, int32_t n, int32_t d, const
 
 int hdpm_rng_set_seed(hdpm_ctx* h, uint32_t seed) {
   CTX();
+  ctx->rng_drop_pending();
   ctx->rng.set_seed(seed);
   return HDPM_OK;
 }
 int hdpm_rng_set_state(hdpm_ctx* h, const int32_t* s) {
   CTX();
   if (!s) return HDPM_E_ARG;
+  ctx->rng_drop_pending();
   ctx->rng.import625(s);
   return HDPM_OK;
 }
 int hdpm_rng_get_state(const hdpm_ctx* h, int32_t* s) {
-  auto* ctx = reinterpret_cast<const Ctx*>(h);
+  // the state is logically const; an adoption still in flight lands first
+  auto* ctx = const_cast<Ctx*>(reinterpret_cast<const Ctx*>(h));
   if (!ctx || !s) return HDPM_E_ARG;
-  ctx->rng.export625(s);
-  return HDPM_OK;
+  GUARD({
+    ctx->rng_sync();
+    ctx->rng.export625(s);
+    return HDPM_OK;
+  })
 }
 
 int hdpm_set_state(hdpm_ctx* h, const int32_t* c_i, int32_t K, const double* centers, const double* sigma) {

@@ -387,13 +387,14 @@ __global__ __launch_bounds__(kScanThreads) void k_list_scan(const int* __restric
 }
 
 // Exact rows of the uncertain points: one wave per point (grid-stride over the dense
-// list), lanes over attributes.  The per-attribute dhamming values of up to 64 entries
-// are staged in LDS (coalesced loads), then lane e adds entry e's values in attribute
-// order -- the reference's summation order (n8:47-49), so every row is bit-exact.
+// list), lane e computes entry e's log-likelihood, adding its per-attribute dhamming
+// values in attribute order -- the reference's summation order (n8:47-49), so every row
+// is bit-exact.  The point's codes are wave-uniform (scalar loads); each lane reads its
+// entry's codes 16 at a time and gathers the 32 table values of two chunks before adding
+// them, so the loads overlap.
 __global__ __launch_bounds__(kWave) void k_exact_rows(PrepassArgs a) {
   const int total = *a.dense_total;
   if ((int)blockIdx.x >= total) return;
-  __shared__ double T[64 * 65];
   const int lane = threadIdx.x;
   const int E = a.K + a.m;
   const int dp = a.nq * 16;
@@ -402,38 +403,47 @@ __global__ __launch_bounds__(kWave) void k_exact_rows(PrepassArgs a) {
     const int64_t i = a.list[row];
     const uint32_t* raw = a.raw + i * (a.m + 1);
     double* Lr = a.L + (int64_t)row * (a.S + a.m);
-    for (int e0 = 0; e0 < E; e0 += 64) {
-      const int ne = min(64, E - e0);
+    for (int e0 = 0; e0 < E; e0 += kWave) {
+      const int e = e0 + lane;
+      const bool on = e < E;
+      const uint8_t* cc;
+      const double* tab;
+      int col;
+      if (e < a.K) {
+        const int s = a.slot_of_label[e];
+        cc = a.slots.codes + (int64_t)s * dp;
+        tab = a.slots.tab + (int64_t)s * 2 * a.d;
+        col = s;
+      } else {
+        const int64_t pe = pick_entry(raw[on ? e - a.K : 0], a.P);
+        cc = a.pool.codes + pe * dp;
+        tab = a.pool.tab + pe * 2 * a.d;
+        col = a.S + (e - a.K);
+      }
       double acc = 0.0;
-      for (int j0 = 0; j0 < a.d; j0 += 64) {
-        const int j = j0 + lane;
-        const int nj = min(64, a.d - j0);
-        const int x = j < a.d ? a.codes_t[tiled_offset(i, j, a.nq)] : 0;
-        for (int ee = 0; ee < ne; ++ee) {
-          const int e = e0 + ee;
-          const uint8_t* cc;
-          const double* tab;
-          if (e < a.K) {
-            const int s = a.slot_of_label[e];
-            cc = a.slots.codes + (int64_t)s * dp;
-            tab = a.slots.tab + (int64_t)s * 2 * a.d;
-          } else {
-            const int64_t pe = pick_entry(raw[e - a.K], a.P);
-            cc = a.pool.codes + pe * dp;
-            tab = a.pool.tab + pe * 2 * a.d;
+      for (int c0 = 0; c0 < a.nq; c0 += 2) {
+        double t[32];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int c = c0 + h;
+          uint4 xc = make_uint4(0, 0, 0, 0);
+          if (c < a.nq) {
+            const uint32_t* xp = (const uint32_t*)(a.codes_t + tiled_offset(i, c * 16, a.nq));
+            xc = make_uint4(ldu(xp), ldu(xp + 1), ldu(xp + 2), ldu(xp + 3));
           }
-          if (j < a.d) T[ee * 65 + lane] = tab[2 * j + (x != cc[j] ? 1 : 0)];
+          const uint4 cq = (on && c < a.nq) ? *(const uint4*)(cc + c * 16) : make_uint4(0, 0, 0, 0);
+          const uint4 dx = make_uint4(xc.x ^ cq.x, xc.y ^ cq.y, xc.z ^ cq.z, xc.w ^ cq.w);
+#pragma unroll
+          for (int b = 0; b < 16; ++b) {
+            const int j = c * 16 + b;
+            t[h * 16 + b] = (on && j < a.d) ? tab[2 * j + (byte_differs(dx, b) ? 1 : 0)] : 0.0;
+          }
         }
-        __syncthreads();
-        if (lane < ne)
-          for (int jj = 0; jj < nj; ++jj) acc += T[lane * 65 + jj];
-        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 32; ++u)
+          if ((c0 * 16 + u) < a.d) acc += t[u];
       }
-      if (lane < ne) {
-        const int e = e0 + lane;
-        const int col = e < a.K ? a.slot_of_label[e] : a.S + (e - a.K);
-        Lr[col] = acc;
-      }
+      if (on) Lr[col] = acc;
     }
   }
 }

@@ -12,6 +12,7 @@
 //   rhig1 / bisec  code/hyperg.cpp:221-287, 346-378
 #pragma once
 #include <cfloat>
+#include <array>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -236,14 +237,26 @@ __attribute__((always_inline)) inline RBeta rbeta_setup(double aa, double bb) {
   return r;
 }
 
-__attribute__((always_inline)) inline double rbeta_draw(Rng& rng, const RBeta& p) {
+// A uniform source yields u and, on request, logit(u) = log(u / (1 - u)) -- the only
+// transcendental of an rbeta attempt that depends on the stream alone.
+struct RngSrc {
+  Rng& r;
+  double next(double* lg) {
+    const double u = r.unif();
+    if (lg) *lg = std::log(u / (1.0 - u));
+    return u;
+  }
+};
+
+template <class S>
+__attribute__((always_inline)) inline double rbeta_draw_s(S& src, const RBeta& p) {
   const double expmax = DBL_MAX_EXP * M_LN2;
   if (p.kind == RBeta::kConst) return p.cval;
-  if (p.kind == RBeta::kCoin) return (rng.unif() < 0.5) ? 0. : 1.;
+  if (p.kind == RBeta::kCoin) return (src.next(nullptr) < 0.5) ? 0. : 1.;
   const double a = p.a, b = p.b, alpha = p.alpha, beta = p.beta;
-  double r, s, t = 0, u1, u2, v = 0, w = 0, y, z;
+  double r, s, t = 0, u1, u2, v = 0, w = 0, y, z, lg1;
   auto vw = [&](double AA) {
-    v = beta * std::log(u1 / (1.0 - u1));
+    v = beta * lg1;                       // beta * log(u1 / (1 - u1))
     if (v <= expmax) {
       w = AA * std::exp(v);
       if (!std::isfinite(w)) w = DBL_MAX;
@@ -253,8 +266,8 @@ __attribute__((always_inline)) inline double rbeta_draw(Rng& rng, const RBeta& p
   };
   if (p.kind == RBeta::kBC) {
     for (;;) {
-      u1 = rng.unif();
-      u2 = rng.unif();
+      u1 = src.next(&lg1);
+      u2 = src.next(nullptr);
       if (u1 < 0.5) {
         y = u1 * u2;
         z = u1 * y;
@@ -273,8 +286,8 @@ __attribute__((always_inline)) inline double rbeta_draw(Rng& rng, const RBeta& p
     return (p.aa == a) ? a / (a + w) : w / (a + w);
   }
   do {
-    u1 = rng.unif();
-    u2 = rng.unif();
+    u1 = src.next(&lg1);
+    u2 = src.next(nullptr);
     vw(a);
     z = u1 * u1 * u2;
     r = p.gamma * v - 1.3862944;
@@ -285,6 +298,86 @@ __attribute__((always_inline)) inline double rbeta_draw(Rng& rng, const RBeta& p
   } while (r + alpha * std::log(alpha / (b + w)) < t);
   return (p.aa != a) ? b / (b + w) : w / (b + w);
 }
+
+__attribute__((always_inline)) inline double rbeta_draw(Rng& rng, const RBeta& p) {
+  RngSrc src{rng};
+  return rbeta_draw_s(src, p);
+}
+
+// A prefix of the stream generated ahead of its consumer: u[k] is the k-th uniform after
+// the state at fill() and lg[k] its logit (filled in parallel by the caller); restore()
+// leaves an Rng exactly as after c draws (same mt array and mti as drawing them one by
+// one, so .Random.seed matches).  Past the prefix, next() continues on the live Rng.
+struct StreamAhead {
+  Rng start;
+  std::vector<double> u, lg;
+  std::vector<int64_t> vfirst;                 // first word index served by each mt array
+  std::vector<std::array<uint32_t, 624>> arr;  // mt array versions (arr[0] = start.mt)
+  int64_t n = 0, used = 0;
+  Rng* live = nullptr;
+  bool spilled = false;
+
+  bool fill(const Rng& r, int64_t N) {
+    n = 0;
+    used = 0;
+    spilled = false;
+    if (r.mti > 624) return false;           // never seeded: let the live Rng handle it
+    start = r;
+    Rng g = r;
+    u.resize(N);
+    lg.resize(N);
+    vfirst.assign(1, 0);
+    arr.resize(1);
+    std::memcpy(arr[0].data(), g.mt, sizeof(g.mt));
+    for (int64_t k = 0; k < N; ++k) {
+      const bool tw = g.mti >= 624;
+      const uint32_t y = g.raw();
+      if (tw) {
+        vfirst.push_back(k);
+        arr.emplace_back();
+        std::memcpy(arr.back().data(), g.mt, sizeof(g.mt));
+      }
+      u[k] = Rng::raw_to_unif(y);
+    }
+    n = N;
+    return true;
+  }
+  void logits(int64_t a, int64_t b) {
+    for (int64_t k = a; k < b; ++k) lg[k] = std::log(u[k] / (1.0 - u[k]));
+  }
+  void restore(Rng& r, int64_t c) const {
+    const uint64_t ep = r.epoch;
+    if (c == 0) {
+      r = start;
+    } else {
+      const int64_t w = c - 1;
+      size_t v = 0;
+      while (v + 1 < vfirst.size() && vfirst[v + 1] <= w) ++v;
+      std::memcpy(r.mt, arr[v].data(), sizeof(r.mt));
+      r.mti = v == 0 ? (int32_t)(start.mti + c) : (int32_t)(w - vfirst[v] + 1);
+      r.pos = start.pos + (uint64_t)c;
+    }
+    r.epoch = ep;
+  }
+  double next(double* lgout) {
+    if (used < n) {
+      if (lgout) *lgout = lg[used];
+      return u[used++];
+    }
+    if (!spilled && n > 0) {
+      restore(*live, n);
+      spilled = true;
+    }
+    ++used;
+    const double x = live->unif();
+    if (lgout) *lgout = std::log(x / (1.0 - x));
+    return x;
+  }
+  // Leave the live Rng after everything drawn so far.
+  void finish() {
+    if (n > 0 && !spilled) restore(*live, used);
+  }
+};
 
 inline double rbeta(Rng& rng, double aa, double bb) { return rbeta_draw(rng, rbeta_setup(aa, bb)); }
 

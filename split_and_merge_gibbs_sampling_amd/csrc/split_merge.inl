@@ -333,6 +333,7 @@ static void push_cluster(Ctx* c, HState& s) {
 
 // sm:542-598
 int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
+  rng_sync();
   if (!have_state) { err = "no state"; return kArg; }
   (void)idx_1_sm;  // overwritten by select_observations_random (sm:278), as in the reference
   *accepted = 0;
@@ -460,6 +461,7 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
 
 // C-ABI helpers operating on the context state.
 int sm_restricted_gibbs_device(Ctx* c, const int32_t* S, int32_t nS, int32_t i1, int32_t i2, int32_t t) {
+  c->rng_sync();
   if (!c->have_state) { c->err = "no state"; return kArg; }
   HState s;
   ctx_to_hstate(c, s);
