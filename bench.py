@@ -154,8 +154,9 @@ def main():
     ap.add_argument("--m", type=int, default=3)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-csv", default=None,
-                    help="rocprofv3 --pmc counter CSV (FETCH_SIZE, WRITE_SIZE) for the roofline traffic field")
+    ap.add_argument("--traffic-csv", action="append", default=None,
+                    help="rocprofv3 --pmc counter_collection CSV(s) with FETCH_SIZE / WRITE_SIZE of this workload "
+                         "(separate passes); default: profiles/r01/pmc_{fetch,write}_<config>.csv when present")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
@@ -197,9 +198,14 @@ def main():
     pre_ms = st["t_prepass_ms"]
     achieved = (bpp * st["prepass_points"] / 1e9) / (pre_ms / 1e3) if pre_ms > 0 else None
     launches = max(st["rounds"], 1)
-    traffic = None
-    if args.traffic_csv and os.path.exists(args.traffic_csv):
-        traffic = traffic_from_csv(args.traffic_csv)
+    traffic, traffic_src = None, None
+    csvs = args.traffic_csv
+    if csvs is None:
+        csvs = [os.path.join(ROOT, "profiles", "r01", f"pmc_{c}_{args.config}.csv") for c in ("fetch", "write")]
+    csvs = [c for c in csvs if os.path.exists(c)]
+    if csvs and args.n is None:
+        traffic = traffic_from_csv(*csvs)
+        traffic_src = [os.path.relpath(c, ROOT) for c in csvs]
     out = {
         "metric": "full Gibbs sweeps/sec (N-point reassign) at N=1M D=128; achieved HBM GB/s",
         "value": round(value, 4),
@@ -234,6 +240,7 @@ def main():
             "unit": "GB/s",
             "frac": None if achieved is None else round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": traffic,
+            "traffic_source": traffic_src,
             "bytes_per_point": bpp,
             "avg_launch_ms": round(pre_ms / launches, 4),
         },
@@ -247,24 +254,25 @@ def main():
     D.close()
 
 
-def traffic_from_csv(path):
-    """Per-launch HBM bytes of k_prepass from a rocprofv3 --pmc counter_collection.csv:
-    (2 * FETCH_SIZE + WRITE_SIZE) KiB -> bytes (gfx950: FETCH_SIZE reports half the bytes
-    of a wide coalesced stream, MI355X_MICROARCH.md 'HBM')."""
+def traffic_from_csv(*paths):
+    """Per-launch HBM bytes of k_prepass from rocprofv3 --pmc counter_collection CSVs (one
+    pass per counter): 2 * FETCH_SIZE + WRITE_SIZE, KiB -> bytes.  gfx950's FETCH_SIZE
+    reports half the bytes of a wide streaming read (MI355X_MICROARCH.md 'HBM'); the
+    prepass reads 16-B lanes, the same width."""
     import csv
-    fetch, write, nd = 0.0, 0.0, set()
-    for row in csv.DictReader(open(path)):
-        if "k_prepass" not in row.get("Kernel_Name", ""):
-            continue
-        nd.add(row.get("Dispatch_Id"))
-        name, val = row.get("Counter_Name"), float(row.get("Counter_Value", 0))
-        if name == "FETCH_SIZE":
-            fetch += val
-        elif name == "WRITE_SIZE":
-            write += val
-    if not nd:
+    tot = {"FETCH_SIZE": [0.0, set()], "WRITE_SIZE": [0.0, set()]}
+    for path in paths:
+        for row in csv.DictReader(open(path)):
+            if "k_prepass" not in row.get("Kernel_Name", ""):
+                continue
+            name = row.get("Counter_Name")
+            if name in tot:
+                tot[name][0] += float(row.get("Counter_Value", 0))
+                tot[name][1].add((path, row.get("Dispatch_Id")))
+    per = {k: (v / len(ids) if ids else None) for k, (v, ids) in tot.items()}
+    if per["FETCH_SIZE"] is None:
         return None
-    return round((2 * fetch + write) * 1024 / len(nd))
+    return round((2 * per["FETCH_SIZE"] + (per["WRITE_SIZE"] or 0.0)) * 1024)
 
 
 if __name__ == "__main__":

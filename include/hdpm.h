@@ -122,7 +122,10 @@ int hdpm_iteration(hdpm_ctx* ctx, const hdpm_chain_params* p, int32_t iter, int3
 int hdpm_rng_fill_device(hdpm_ctx* ctx, int64_t count, uint32_t* out);
 int hdpm_get_stats(const hdpm_ctx* ctx, hdpm_stats* out);
 int hdpm_reset_stats(hdpm_ctx* ctx);
-/* mode bit 0: evaluate every point on the exact path (no certainty shortcut). */
+/* Testing / diagnostics.  mode bit 0: evaluate every point on the exact path (no
+ * certainty shortcut); bit 1: print per-phase timings to stderr; bit 2: compute the
+ * log-likelihood with the per-point kernel (no regrouping into match counts); bit 3: no
+ * snapshot speculation (the resolver decides every uncertain point itself). */
 int hdpm_set_debug(hdpm_ctx* ctx, int32_t mode);
 /* Block until all device work of the context is done. */
 int hdpm_synchronize(hdpm_ctx* ctx);

@@ -30,6 +30,7 @@
 namespace hdpm {
 
 hipError_t launch_prepass(const PrepassArgs& a, int nblocks, hipStream_t s);
+hipError_t launch_cluster_summary(const PrepassArgs& a, hipStream_t s);
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s);
 hipError_t launch_exact_rows(const PrepassArgs& a, int nblocks, hipStream_t s);
 size_t resolve_smem_bytes(int scap, int m);
@@ -382,7 +383,8 @@ struct Ctx {
   int Ecap = 0;
   DevBuf<double> d_margin;
   DevBuf<int> d_rowpos;
-  DevBuf<int> d_list, d_cnt, d_dense, d_dense_total;
+  DevBuf<int> d_list, d_cnt, d_dense, d_dense_total, d_spec;
+  DevBuf<uint64_t> d_csum;            // per-label cluster summary for the prepass
   DevBuf<unsigned> d_hist_part;
   DevBuf<int> d_ctl;                  // ResolveCtl + summary (kernels.hpp)
   DevBuf<long long> d_rprof;          // resolver phase times (debug mode bit 1)
@@ -955,6 +957,7 @@ struct Ctx {
     d_cnt.ensure(nb_max);
     d_dense.ensure((size_t)nb_max * kBlock);
     d_dense_total.ensure(1);
+    d_spec.ensure((size_t)nb_max * kBlock);
 
     int nslots = K;
     int p = 0;
@@ -977,12 +980,16 @@ struct Ctx {
       pa.pool = ParamTables{d_pool_codes.p, d_pool_tab.p};
       pa.P = P; pa.raw = d_sweep_raw; pa.m = m; pa.logn = d_logn.p; pa.logfac = std::log(gamma / m);
       pa.xbs = d_xbs.p; pa.Ws = Ws; pa.wb = wb; pa.slot_bnd = d_slot_bnd.p; pa.pool_bnd = d_pool_bnd.p; pa.bw = bw;
+      d_csum.ensure((size_t)std::max(K, 1) * (bw + 2));
+      pa.csum = d_csum.p;
 
       pa.thresh = (debug & 1) ? INFINITY : T + 2.0 * dmax;
       pa.L = d_L.p; pa.rowpos = d_rowpos.p; pa.margin = d_margin.p; pa.list = d_list.p; pa.cnt = d_cnt.p;
       pa.dense = d_dense.p; pa.dense_total = d_dense_total.p;
+      pa.spec = (debug & 8) ? nullptr : d_spec.p;
       pa.p0 = p;
       const int nblocks = (n - p + kBlock - 1) / kBlock;
+      HIPCHK(launch_cluster_summary(pa, stream));
       HIPCHK(hipEventRecord(ev[0], stream));
       HIPCHK(launch_prepass(pa, nblocks, stream));
       stats.prepass_points += n - p;
@@ -997,6 +1004,7 @@ struct Ctx {
       ra.pool = pa.pool; ra.raw = d_sweep_raw; ra.logn = d_logn.p; ra.logfac = pa.logfac;
       ra.L = d_L.p; ra.rowpos = d_rowpos.p; ra.slot_bnd = d_slot_bnd.p; ra.pool_bnd = d_pool_bnd.p; ra.bw = bw;
       ra.S = S; ra.margin = d_margin.p; ra.list = d_list.p; ra.dense = d_dense.p; ra.dense_total = d_dense_total.p;
+      ra.spec = pa.spec;
       ra.nblocks = nblocks; ra.p0 = p; ra.T = T; ra.dmax = dmax; ra.scap = scap; ra.K = K;
       ra.lcap = std::min(scap, nslots + 2);
       ra.nslots = nslots; ra.ctl = (ResolveCtl*)d_ctl.p; ra.summary = d_ctl.p + 8; ra.force_exact = (debug & 1);

@@ -223,6 +223,22 @@ __device__ __forceinline__ int penalty_r(const uint64_t (&M)[WS], const uint64_t
   return Sq;
 }
 
+// Per-label summary for the prepass's cluster loop (one level of independent scalar loads
+// per label instead of the label -> slot -> record / count -> logn chain):
+// csum[l] = [record of slot_of_label[l] (bw words), logn[count], slot].
+__global__ void k_cluster_summary(PrepassArgs a) {
+  const int sw = a.bw + 2;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < a.K * sw; e += gridDim.x * blockDim.x) {
+    const int l = e / sw, w = e - l * sw;
+    const int s = a.slot_of_label[l];
+    uint64_t v;
+    if (w < a.bw) v = a.slot_bnd[(int64_t)s * a.bw + w];
+    else if (w == a.bw) v = (uint64_t)__double_as_longlong(a.logn[a.counts[s]]);
+    else v = (uint64_t)s;
+    a.csum[e] = v;
+  }
+}
+
 // Bounds-first prepass: every point gets rigorous bounds on its K + m log-weights from
 // Hamming popcounts of bit-sliced rows; only points whose draw is not provably "stay" get
 // exact rows.
@@ -239,7 +255,7 @@ __global__ __launch_bounds__(kBlock) void k_prepass(PrepassArgs a) {
   constexpr int WR = WB * WS;                  // row words
   constexpr int RW = (WB + kQ) * WS + 4;       // record words
   constexpr int SC = (WB + kQ) * WS;           // record scalars: A, delta, dmin, scale
-  constexpr int NPF = RW <= 16 ? 4 : RW <= 32 ? 2 : 1;   // pool records in flight
+  constexpr int NPF = RW <= 16 ? 3 : RW <= 32 ? 2 : 1;   // pool records in flight
   const int tid = threadIdx.x;
   const int64_t i = (int64_t)a.p0 + (int64_t)blockIdx.x * kBlock + tid;
   const bool active = i < a.n;
@@ -252,6 +268,12 @@ __global__ __launch_bounds__(kBlock) void k_prepass(PrepassArgs a) {
   const uint32_t* raw = a.raw + ii * (a.m + 1);
   double mg = -INFINITY;
   if (own_cnt >= 2) {
+    // the first latent records' gathers go out first: their latency overlaps the
+    // own-cluster bound and the cluster loop
+    uint64_t Rp[NPF][RW];
+#pragma unroll
+    for (int u = 0; u < NPF; ++u)
+      if (u < a.m) load_record<RW>(a.pool_bnd + pick_entry(raw[u], a.P) * a.bw, Rp[u]);
     uint64_t M[WS];
     double lo;
     {
@@ -266,11 +288,11 @@ __global__ __launch_bounds__(kBlock) void k_prepass(PrepassArgs a) {
     const double cut = lo - a.thresh;        // an entry whose ub stays below this cannot matter
     double ubmax = -INFINITY;
     for (int l = 0; l < a.K; ++l) {
-      const int s = ldu(a.slot_of_label + l);
-      const uint64_t* bd = a.slot_bnd + (int64_t)s * a.bw;
+      const uint64_t* bd = a.csum + (int64_t)l * (RW + 2);
+      const int s = (int)ldu(bd + RW + 1);
       const int H = mismatch_mask<WB, WS, true>(x, bd, M);
       const double A = as_f64(ldu(bd + SC)), dmin = as_f64(ldu(bd + SC + 2)), scale = as_f64(ldu(bd + SC + 3));
-      const double lg = a.logn[ldu(a.counts + s)];
+      const double lg = as_f64(ldu(bd + RW));
       double ub = lg + (A - dmin * (double)H + kBoundEps * (1.0 + scale));
       const bool need = s != own && ub > cut;
       if (__ballot(need)) {
@@ -282,16 +304,17 @@ __global__ __launch_bounds__(kBlock) void k_prepass(PrepassArgs a) {
       if (s != own) ubmax = fmax(ubmax, ub);
     }
     for (int l0 = 0; l0 < a.m; l0 += NPF) {
-      uint64_t R[NPF][RW];
+      if (l0 > 0) {
 #pragma unroll
-      for (int u = 0; u < NPF; ++u)
-        if (l0 + u < a.m) load_record<RW>(a.pool_bnd + pick_entry(raw[l0 + u], a.P) * a.bw, R[u]);
+        for (int u = 0; u < NPF; ++u)
+          if (l0 + u < a.m) load_record<RW>(a.pool_bnd + pick_entry(raw[l0 + u], a.P) * a.bw, Rp[u]);
+      }
 #pragma unroll
       for (int u = 0; u < NPF; ++u) {
         if (l0 + u < a.m) {
-          const int H = mismatch_r<WB, WS, RW>(x, R[u], M);
-          const int Sq = penalty_r<WB, WS, RW>(M, R[u]);
-          const double A = as_f64(R[u][SC]), dl = as_f64(R[u][SC + 1]);
+          const int H = mismatch_r<WB, WS, RW>(x, Rp[u], M);
+          const int Sq = penalty_r<WB, WS, RW>(M, Rp[u]);
+          const double A = as_f64(Rp[u][SC]), dl = as_f64(Rp[u][SC + 1]);
           const double pmin = dl * (double)Sq, pmax = dl * (double)(Sq + H);
           ubmax = fmax(ubmax, a.logfac + (A - pmin + kBoundEps * (1.0 + fabs(A) + pmax)));
         }
@@ -384,68 +407,6 @@ __global__ __launch_bounds__(kScanThreads) void k_list_scan(const int* __restric
     off += c;
   }
   if (tid == 0) *total = all;
-}
-
-// Exact rows of the uncertain points: one wave per point (grid-stride over the dense
-// list), lane e computes entry e's log-likelihood, adding its per-attribute dhamming
-// values in attribute order -- the reference's summation order (n8:47-49), so every row
-// is bit-exact.  The point's codes are wave-uniform (scalar loads); each lane reads its
-// entry's codes 16 at a time and gathers the 32 table values of two chunks before adding
-// them, so the loads overlap.
-__global__ __launch_bounds__(kWave) void k_exact_rows(PrepassArgs a) {
-  const int total = *a.dense_total;
-  if ((int)blockIdx.x >= total) return;
-  const int lane = threadIdx.x;
-  const int E = a.K + a.m;
-  const int dp = a.nq * 16;
-  for (int q = blockIdx.x; q < total; q += gridDim.x) {
-    const int row = a.dense[q];
-    const int64_t i = a.list[row];
-    const uint32_t* raw = a.raw + i * (a.m + 1);
-    double* Lr = a.L + (int64_t)row * (a.S + a.m);
-    for (int e0 = 0; e0 < E; e0 += kWave) {
-      const int e = e0 + lane;
-      const bool on = e < E;
-      const uint8_t* cc;
-      const double* tab;
-      int col;
-      if (e < a.K) {
-        const int s = a.slot_of_label[e];
-        cc = a.slots.codes + (int64_t)s * dp;
-        tab = a.slots.tab + (int64_t)s * 2 * a.d;
-        col = s;
-      } else {
-        const int64_t pe = pick_entry(raw[on ? e - a.K : 0], a.P);
-        cc = a.pool.codes + pe * dp;
-        tab = a.pool.tab + pe * 2 * a.d;
-        col = a.S + (e - a.K);
-      }
-      double acc = 0.0;
-      for (int c0 = 0; c0 < a.nq; c0 += 2) {
-        double t[32];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int c = c0 + h;
-          uint4 xc = make_uint4(0, 0, 0, 0);
-          if (c < a.nq) {
-            const uint32_t* xp = (const uint32_t*)(a.codes_t + tiled_offset(i, c * 16, a.nq));
-            xc = make_uint4(ldu(xp), ldu(xp + 1), ldu(xp + 2), ldu(xp + 3));
-          }
-          const uint4 cq = (on && c < a.nq) ? *(const uint4*)(cc + c * 16) : make_uint4(0, 0, 0, 0);
-          const uint4 dx = make_uint4(xc.x ^ cq.x, xc.y ^ cq.y, xc.z ^ cq.z, xc.w ^ cq.w);
-#pragma unroll
-          for (int b = 0; b < 16; ++b) {
-            const int j = c * 16 + b;
-            t[h * 16 + b] = (on && j < a.d) ? tab[2 * j + (byte_differs(dx, b) ? 1 : 0)] : 0.0;
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < 32; ++u)
-          if ((c0 * 16 + u) < a.d) acc += t[u];
-      }
-      if (on) Lr[col] = acc;
-    }
-  }
 }
 
 // ------------------------------------------------------------------ resolver
@@ -554,41 +515,19 @@ __device__ __forceinline__ double readlane_f64(double x, int l) {
   return __longlong_as_double(((uint64_t)hi << 32) | lo);
 }
 
-// Exact n8:40-102 decision for a point whose exact row is Lr (LDS), own slot `own`,
-// categorical uniform rU.  Returns the drawn index in [0, K+m) or -status.
-//
-// Register path (E <= 64 RE): entry e lives in lane e % 64 of register e / 64.  The
-// reference's left-to-right reductions -- the max, sum(probs) (n8:96) and Rcpp
+// The n8:95-102 draw from the log-weights pv (entry e in lane e % 64 of register e / 64,
+// E entries), categorical uniform rU.  Returns the drawn index in [0, E) or -status.
+// The reference's left-to-right reductions -- the max, sum(probs) (n8:96) and Rcpp
 // FixupProb's sum of the positive entries -- run in index order over readlane'd values,
 // so they round exactly as on the CPU.  The loops run over E rounded up to 8 with padding
 // entries -inf / 0.0, which leave a max or a non-negative running sum unchanged.  Counts,
-// the maximum's position and ties come from ballots.
+// the maximum's position and ties come from ballots; ties or a draw past the maximum take
+// R's revsort on lane 0 (LDS scratch lp / lperm, result through *lpick).
 template <int RE>
-__device__ int exact_decision_reg(const ResolveArgs& a, const RState& st, int K, const double* Lr, int own, double rU) {
-  const int lane = threadIdx.x;
-  K = __builtin_amdgcn_readfirstlane(K);
-  own = __builtin_amdgcn_readfirstlane(own);
-  const int E = K + a.m;
+__device__ int decide_values(double (&pv)[RE], int E, double rU, double* lp, int* lperm, int* lpick) {
+  const int lane = threadIdx.x & 63;
+  E = __builtin_amdgcn_readfirstlane(E);
   const int E8 = (E + 7) & ~7;
-  const bool singleton = st.cnt[own] == 1;
-  const bool prof = a.prof != nullptr;
-  long long ts0 = prof ? wall_clock64() : 0;
-  double pv[RE];
-#pragma unroll
-  for (int r = 0; r < RE; ++r) {
-    const int e = r * kWave + lane;
-    double v = -INFINITY;
-    if (e < K) {
-      const int s = st.sol[e];
-      // logn[cnt - (s == own)] + ll; logn[0] = -inf covers the emptied singleton
-      v = (s == own ? st.l0[s] : st.l1[s]) + Lr[s];
-    } else if (e < E) {
-      const int l = e - K;
-      v = a.logfac + ((l == 0 && singleton) ? Lr[own] : Lr[a.S + l]);
-    }
-    pv[r] = v;
-  }
-  // sequential scans over the (padded) entries; f(acc, value) per entry
   auto scan = [&](double acc, auto f) -> double {
 #pragma unroll
     for (int r = 0; r < RE; ++r) {
@@ -600,21 +539,16 @@ __device__ int exact_decision_reg(const ResolveArgs& a, const RState& st, int K,
     }
     return acc;
   };
+#pragma unroll
+  for (int r = 0; r < RE; ++r)
+    if (r * kWave + lane >= E) pv[r] = -INFINITY;
   const double mx = scan(-INFINITY, [](double m, double x) { return fmax(m, x); });
-  long long ts1 = prof ? wall_clock64() : 0;
 #pragma unroll
   for (int r = 0; r < RE; ++r) pv[r] = (r * kWave + lane < E) ? exp(pv[r] - mx) : 0.0;      // n8:95
-  long long ts2 = prof ? wall_clock64() : 0;
   const double sum = scan(0.0, [](double s, double x) { return s + x; });
 #pragma unroll
   for (int r = 0; r < RE; ++r) pv[r] = pv[r] / sum;                                             // n8:96
   const double s2 = scan(0.0, [](double s, double x) { return s + (x > 0 ? x : 0.0); });       // FixupProb
-  long long ts3 = prof ? wall_clock64() : 0;
-  if (prof && lane == 0) {
-    st.sh->tsub[0] += ts1 - ts0;
-    st.sh->tsub[1] += ts2 - ts1;
-    st.sh->tsub[2] += ts3 - ts2;
-  }
   if (!(s2 > 0)) return -3;  // kProb: no positive probability
   int nc = 0;
 #pragma unroll
@@ -632,24 +566,50 @@ __device__ int exact_decision_reg(const ResolveArgs& a, const RState& st, int K,
     ties += __popcll(b);
     if (amax < 0 && b) amax = r * kWave + __ffsll((long long)b) - 1;
   }
-  if (prof && lane == 0) st.sh->tsub[3] += wall_clock64() - ts3;
   // Unique maximum drawn: revsort puts it first, cumsum[0] = pmax.
   if (ties == 1 && rU <= pmax) return amax;
 #pragma unroll
   for (int r = 0; r < RE; ++r)
-    if (r * kWave + lane < E) st.p[r * kWave + lane] = pv[r];
+    if (r * kWave + lane < E) lp[r * kWave + lane] = pv[r];
   wave_sync();
   if (lane == 0) {
-    for (int e = 0; e < E; ++e) st.perm[e] = e + 1;
-    dev_revsort(st.p, st.perm, E);
-    for (int e = 1; e < E; ++e) st.p[e] += st.p[e - 1];
+    for (int e = 0; e < E; ++e) lperm[e] = e + 1;
+    dev_revsort(lp, lperm, E);
+    for (int e = 1; e < E; ++e) lp[e] += lp[e - 1];
     int j;
     for (j = 0; j < E - 1; j++)
-      if (rU <= st.p[j]) break;
-    st.sh->pick = st.perm[j] - 1;
+      if (rU <= lp[j]) break;
+    *lpick = lperm[j] - 1;
   }
   wave_sync();
-  return st.sh->pick;
+  return *lpick;
+}
+
+// Exact n8:40-102 decision for a point whose exact row is Lr (LDS), own slot `own`, in the
+// resolver's current state.  Returns the drawn index in [0, K+m) or -status.
+template <int RE>
+__device__ int exact_decision_reg(const ResolveArgs& a, const RState& st, int K, const double* Lr, int own, double rU) {
+  const int lane = threadIdx.x;
+  K = __builtin_amdgcn_readfirstlane(K);
+  own = __builtin_amdgcn_readfirstlane(own);
+  const int E = K + a.m;
+  const bool singleton = st.cnt[own] == 1;
+  double pv[RE];
+#pragma unroll
+  for (int r = 0; r < RE; ++r) {
+    const int e = r * kWave + lane;
+    double v = -INFINITY;
+    if (e < K) {
+      const int s = st.sol[e];
+      // logn[cnt - (s == own)] + ll; logn[0] = -inf covers the emptied singleton
+      v = (s == own ? st.l0[s] : st.l1[s]) + Lr[s];
+    } else if (e < E) {
+      const int l = e - K;
+      v = a.logfac + ((l == 0 && singleton) ? Lr[own] : Lr[a.S + l]);
+    }
+    pv[r] = v;
+  }
+  return decide_values<RE>(pv, E, rU, st.p, st.perm, &st.sh->pick);
 }
 
 // LDS path for more than 256 entries.
@@ -753,6 +713,125 @@ struct RowPrefetch {
   }
 };
 
+// Exact rows of the uncertain points: one wave per point (grid-stride over the dense
+// list), lane e computes entry e's log-likelihood, adding its per-attribute dhamming
+// values in attribute order -- the reference's summation order (n8:47-49), so every row
+// is bit-exact.  The point's codes are wave-uniform (scalar loads); each lane reads its
+// entry's codes 16 at a time and gathers the 32 table values of two chunks before adding
+// them, so the loads overlap.
+//
+// Speculation: the same wave then draws the point in the snapshot state (the counts and
+// slots every row of this round was built against) with the resolver's exact decision.
+// While no earlier point of the round has moved, the resolver's state IS the snapshot,
+// so it takes these draws as they are; after the first move it decides on its own.
+template <int RE>
+__device__ void exact_rows_point(const PrepassArgs& a, int row, double* lp, int* lperm, int* lpick) {
+  const int lane = threadIdx.x;
+  const int E = a.K + a.m;
+  const int dp = a.nq * 16;
+  const int64_t i = a.list[row];
+  const uint32_t* raw = a.raw + i * (a.m + 1);
+  double* Lr = a.L + (int64_t)row * (a.S + a.m);
+  auto entry_ll = [&](int r) -> double {
+      const int e = r * kWave + lane;
+      const bool on = e < E;
+      const uint8_t* cc;
+      const double* tab;
+      int col;
+      if (e < a.K) {
+        const int s = a.slot_of_label[e];
+        cc = a.slots.codes + (int64_t)s * dp;
+        tab = a.slots.tab + (int64_t)s * 2 * a.d;
+        col = s;
+      } else {
+        const int64_t pe = pick_entry(raw[on ? e - a.K : 0], a.P);
+        cc = a.pool.codes + pe * dp;
+        tab = a.pool.tab + pe * 2 * a.d;
+        col = a.S + (e - a.K);
+      }
+      double acc = 0.0;
+      for (int c0 = 0; c0 < a.nq; c0 += 2) {
+        double t[32];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int c = c0 + h;
+          uint4 xc = make_uint4(0, 0, 0, 0);
+          if (c < a.nq) {
+            const uint32_t* xp = (const uint32_t*)(a.codes_t + tiled_offset(i, c * 16, a.nq));
+            xc = make_uint4(ldu(xp), ldu(xp + 1), ldu(xp + 2), ldu(xp + 3));
+          }
+          const uint4 cq = (on && c < a.nq) ? *(const uint4*)(cc + c * 16) : make_uint4(0, 0, 0, 0);
+          const uint4 dx = make_uint4(xc.x ^ cq.x, xc.y ^ cq.y, xc.z ^ cq.z, xc.w ^ cq.w);
+#pragma unroll
+          for (int b = 0; b < 16; ++b) {
+            const int j = c * 16 + b;
+            t[h * 16 + b] = (on && j < a.d) ? tab[2 * j + (byte_differs(dx, b) ? 1 : 0)] : 0.0;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 32; ++u)
+          if ((c0 * 16 + u) < a.d) acc += t[u];
+      }
+      if (on) Lr[col] = acc;
+      return acc;
+  };
+  double acc_r[RE > 0 ? RE : 1];
+  if constexpr (RE > 0) {
+#pragma unroll
+    for (int r = 0; r < RE; ++r) acc_r[r] = entry_ll(r);
+  } else {
+    for (int r = 0; r < (E + kWave - 1) / kWave; ++r) (void)entry_ll(r);
+  }
+  if constexpr (RE > 0) {
+    if (!a.spec) return;
+    // n8:40-94 in the snapshot state: logn[count - (slot == own)] + ll for the clusters,
+    // log(gamma / m) + ll for the latents (the singleton's first latent is its own cluster)
+    const int own = __builtin_amdgcn_readfirstlane(a.c[i]);
+    const int own_cnt = a.counts[own];
+    double ll_own = 0.0;
+    double pv[RE];
+#pragma unroll
+    for (int r = 0; r < RE; ++r) {
+      const int e = r * kWave + lane;
+      int s = -1;
+      if (e < a.K) s = a.slot_of_label[e];
+      const unsigned long long bo = __ballot(s == own);
+      if (bo) ll_own = readlane_f64(acc_r[r], __ffsll((long long)bo) - 1);
+      double v = -INFINITY;
+      if (e < a.K) v = a.logn[a.counts[s] - (s == own ? 1 : 0)] + acc_r[r];
+      pv[r] = v;
+    }
+#pragma unroll
+    for (int r = 0; r < RE; ++r) {
+      const int e = r * kWave + lane;
+      if (e >= a.K && e < E) {
+        const int l = e - a.K;
+        pv[r] = a.logfac + ((l == 0 && own_cnt == 1) ? ll_own : acc_r[r]);
+      }
+    }
+    const int pick = decide_values<RE>(pv, E, raw_to_unif(raw[a.m]), lp, lperm, lpick);
+    if (lane == 0) a.spec[row] = pick >= 0 ? pick : -1;
+  }
+}
+
+__global__ __launch_bounds__(kWave) void k_exact_rows(PrepassArgs a) {
+  const int total = *a.dense_total;
+  if ((int)blockIdx.x >= total) return;
+  __shared__ double lp[4 * kWave];
+  __shared__ int lperm[4 * kWave];
+  __shared__ int lpick;
+  const int E = a.K + a.m;
+  for (int q = blockIdx.x; q < total; q += gridDim.x) {
+    const int row = a.dense[q];
+    if (E <= kWave) exact_rows_point<1>(a, row, lp, lperm, &lpick);
+    else if (E <= 4 * kWave) exact_rows_point<4>(a, row, lp, lperm, &lpick);
+    else {
+      exact_rows_point<0>(a, row, lp, lperm, &lpick);
+      if (a.spec && threadIdx.x == 0) a.spec[row] = -1;
+    }
+  }
+}
+
 __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x;
@@ -794,10 +873,11 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
 
   // Decide point i (exact row in LDS at Lr) and apply n8:107-159.  Returns false to stop
   // the sweep here.
-  auto process = [&](int64_t i, const double* Lr, int own, uint32_t rawU) -> bool {
+  auto process = [&](int64_t i, const double* Lr, int own, uint32_t rawU, int spec) -> bool {
     const int K = S.K;
     const long long tq0 = prof ? wall_clock64() : 0;
-    const int pick = exact_decision(a, st, K, Lr, own, raw_to_unif(rawU));
+    // the snapshot draw holds while nothing has moved in this round
+    const int pick = (S.moves == 0 && spec >= 0) ? spec : exact_decision(a, st, K, Lr, own, raw_to_unif(rawU));
     if (prof && lane == 0) S.tsub[4] += wall_clock64() - tq0;
     if (lane == 0) {
       S.exact++;
@@ -890,6 +970,7 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
       const int li = lane < lim ? a.list[rw] : 0;
       const int ci = lane < lim ? a.c[li] : 0;
       const uint32_t ru = lane < lim ? a.raw[(int64_t)li * (a.m + 1) + a.m] : 0u;
+      const int sp = (lane < lim && a.spec) ? a.spec[rw] : -1;
       const int rnext = (q0 + kWave + lane < total && lane == 0) ? a.dense[q0 + kWave] : 0;
       const int rn64 = __shfl(rnext, 0);
       if (prof) { tp[3] += wall_clock64() - tb + 0 * (ci + (int)ru + rn64); }
@@ -901,7 +982,7 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
         else if (q0 + kWave < total) rn = rn64;
         if (rn >= 0) pf.issue(a.L + (int64_t)rn * ncol, ncol);
         const int64_t i = __shfl(li, q);
-        go = process(i, st.row + buf * st.emax, __shfl(ci, q), (uint32_t)__shfl((int)ru, q));
+        go = process(i, st.row + buf * st.emax, __shfl(ci, q), (uint32_t)__shfl((int)ru, q), __shfl(sp, q));
         long long t1 = prof ? wall_clock64() : 0;
         if (go && S.dnow > a.dmax) { start_checked = i + 1; go = false; }
         if (go && rn >= 0) {
@@ -948,7 +1029,7 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
         const double* src = a.L + (int64_t)row * ncol;
         for (int c = lane; c < ncol; c += kWave) st.row[c] = src[c];
         wave_sync();
-        if (!process(base + q, st.row, __shfl(ci, q), a.raw[(base + q) * (a.m + 1) + a.m])) { stop = true; break; }
+        if (!process(base + q, st.row, __shfl(ci, q), a.raw[(base + q) * (a.m + 1) + a.m], -1)) { stop = true; break; }
         // drift may have grown: re-test the remaining lanes
         bool u2 = false;
         if (lane > q && i < a.n) {
@@ -1211,6 +1292,14 @@ static hipError_t launch_prepass_w(const PrepassArgs& a, int nblocks, hipStream_
 hipError_t launch_exact_rows(const PrepassArgs& a, int nblocks, hipStream_t s) {
   hipLaunchKernelGGL(k_list_scan, dim3(1), dim3(kScanThreads), 0, s, a.cnt, nblocks, a.dense, a.dense_total);
   hipLaunchKernelGGL(k_exact_rows, dim3(std::min(nblocks * 4, 4096)), dim3(kWave), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_cluster_summary(const PrepassArgs& a, hipStream_t s) {
+  if (a.K > 0) {
+    const int work = a.K * (a.bw + 2);
+    hipLaunchKernelGGL(k_cluster_summary, dim3(std::min(64, (work + 255) / 256)), dim3(256), 0, s, a);
+  }
   return hipGetLastError();
 }
 

@@ -67,6 +67,7 @@ struct PrepassArgs {
   const uint64_t* slot_bnd;  // [slot][bw]
   const uint64_t* pool_bnd;  // [entry][bw]
   int bw;
+  uint64_t* csum;            // per label: its slot's record, logn[count], slot id (bw + 2 words)
   int64_t P;
   const uint32_t* raw;       // R MT raw outputs, (m+1) per point
   int m;
@@ -80,6 +81,7 @@ struct PrepassArgs {
   int* cnt;                  // per block: number of uncertain points
   int* dense;                // all uncertain rows in index order (k_list_scan)
   int* dense_total;          // their number
+  int* spec;                 // per row: the draw in the snapshot state (or -1), by k_exact_rows
   int p0;
 };
 
@@ -119,6 +121,7 @@ struct ResolveArgs {
   const int* list;
   const int* dense;          // uncertain rows in index order
   const int* dense_total;
+  const int* spec;           // per row: the draw in the snapshot state (k_exact_rows), or -1
   int nblocks;
   int p0;
   double T;                  // certainty threshold without drift

@@ -88,3 +88,13 @@ def test_traffic_from_csv(tmp_path, rows):
             w.writerow([d, k, n, v])
     # (2 * 400 + 40) KiB over 2 dispatches
     assert bench.traffic_from_csv(str(p)) == round((2 * 400 + 40) * 1024 / 2)
+    # one file per counter pass
+    pf, pw = tmp_path / "f.csv", tmp_path / "w.csv"
+    import csv
+    for path, name, vals in ((pf, "FETCH_SIZE", (100.0, 300.0)), (pw, "WRITE_SIZE", (10.0, 30.0))):
+        with open(path, "w", newline="") as f:
+            w = csv.writer(f)
+            w.writerow(["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"])
+            for d, v in enumerate(vals):
+                w.writerow([d, "k_prepass<2,2>", name, v])
+    assert bench.traffic_from_csv(str(pf), str(pw)) == round((2 * 200 + 20) * 1024)

@@ -94,7 +94,9 @@ def sweep_case(hd, oracle, ds, c, cen, sig, P, seed, m=3, debug=0, sweeps=1, phi
     return stats
 
 
-@pytest.mark.parametrize("debug", [0, 1])
+# debug 0: default (snapshot speculation in the exact-rows kernel), 1: every point on the
+# exact path in the resolver, 8: no speculation (the resolver decides every listed point)
+@pytest.mark.parametrize("debug", [0, 1, 8])
 def test_zoo_single_sweeps_from_truth(hd, oracle, zoo, debug):
     cen, sig = random_params(zoo, 7, 3)
     stats = sweep_case(hd, oracle, zoo, zoo.truth, cen, sig, zoo.n * 3, seed=17, debug=debug, sweeps=3)
@@ -108,15 +110,16 @@ def test_zoo_sweeps_with_update_phi_all_singletons(hd, oracle, zoo):
     sweep_case(hd, oracle, zoo, c, cen, sig, zoo.n * 3, seed=23, sweeps=4, phi=True)
 
 
-def test_zoo_sweeps_with_update_phi_one_cluster(hd, oracle, zoo):
+@pytest.mark.parametrize("debug", [0, 8])
+def test_zoo_sweeps_with_update_phi_one_cluster(hd, oracle, zoo, debug):
     # L = 1: the first sweeps create clusters (case 3 -> device restarts)
     c = np.zeros(zoo.n, np.int32)
     cen, sig = random_params(zoo, 1, 6)
-    stats = sweep_case(hd, oracle, zoo, c, cen, sig, zoo.n * 3, seed=29, sweeps=6, phi=True)
+    stats = sweep_case(hd, oracle, zoo, c, cen, sig, zoo.n * 3, seed=29, sweeps=6, phi=True, debug=debug)
     assert stats["restarts"] > 0
 
 
-@pytest.mark.parametrize("debug", [0, 1])
+@pytest.mark.parametrize("debug", [0, 1, 8])
 def test_synthetic_sweeps_with_update_phi(hd, oracle, debug):
     ds = synth(6000, 32, 8, 2, seed=3)
     cen, sig = random_params(ds, 8, 7)
