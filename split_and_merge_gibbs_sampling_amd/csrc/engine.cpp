@@ -406,6 +406,11 @@ struct Ctx {
 
   hdpm_stats stats{};
   int debug = 0;
+  // debug bit 1: per-iteration host timeline
+  std::vector<std::pair<const char*, std::chrono::steady_clock::time_point>> trace;
+  void mark(const char* what) {
+    if (debug & 2) trace.emplace_back(what, std::chrono::steady_clock::now());
+  }
   std::unordered_map<uint64_t, bool> beta_cache;
 
   SmWork sm;
@@ -948,6 +953,7 @@ struct Ctx {
     auto tr0 = std::chrono::steady_clock::now();
     const size_t nraw = (size_t)n * (m + 1);
     const uint32_t* d_sweep_raw = device_draws((int64_t)nraw);
+    mark("draws");
     stats.t_rng_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count();
 
     const int nb_max = (n + kBlock - 1) / kBlock;
@@ -962,6 +968,7 @@ struct Ctx {
     int nslots = K;
     int p = 0;
     const double dmax = 0.25;
+    const int64_t rounds0 = stats.rounds;
     while (p < n) {
       ensure_slots(nslots + 2);
       d_ctl.ensure(8 + 3 * (size_t)scap);
@@ -1017,7 +1024,11 @@ struct Ctx {
       HIPCHK(launch_resolve(ra, stream));
       HIPCHK(hipEventRecord(ev[2], stream));
       HIPCHK(hipMemcpyAsync(h_ctl.p, d_ctl.p, (8 + 3 * (size_t)scap) * 4, hipMemcpyDeviceToHost, stream));
+      mark("launched");
+      if (stats.rounds == rounds0) prefill_phi_stream();   // hidden behind the device work
+      mark("prefill");
       HIPCHK(hipStreamSynchronize(stream));
+      mark("resolved");
       float t1 = 0, t2 = 0, t3 = 0;
       HIPCHK(hipEventElapsedTime(&t1, ev[0], ev[1]));
       HIPCHK(hipEventElapsedTime(&t3, ev[1], ev[5]));
@@ -1081,6 +1092,7 @@ struct Ctx {
     }
     host_c_valid = false;
     tables_dirty = true;
+    mark("sweep_end");
     stats.t_stats_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
     stats.sweeps++;
     return kOk;
@@ -1144,6 +1156,18 @@ struct Ctx {
   std::vector<double> phi_cum;
   std::vector<int> phi_perm, phi_off;
 
+  // update_phi's slice of the host stream, generated ahead (also called while the device
+  // runs a sweep, which draws only from the device windows).
+  void prefill_phi_stream() {
+    rng_sync();
+    StreamAhead& sa = phi_stream;
+    if (sa.n > 0 && sa.used == 0 && sa.start.pos == rng.pos && sa.start.epoch == rng.epoch) return;
+    if (sa.fill(rng, phi_prefetch)) {
+      sa.used = 0;
+      HostPool::get().run(sa.n, 1024, [&](int64_t a0, int64_t a1) { sa.logits(a0, a1); });
+    }
+  }
+
   int update_phi(const int32_t* idx, int nidx) {
     if (!have_state) { err = "no state"; return kArg; }
     HostPool& pool = HostPool::get();
@@ -1153,13 +1177,15 @@ struct Ctx {
     for (int q = 0; q < nidx; ++q)
       if (idx[q] >= 0 && idx[q] < K) mask[idx[q]] = 1;
     histogram_launch(nidx == 0 ? nullptr : &mask);
-    // while the device counts: the next stretch of the stream and its logits
-    rng_sync();
+    mark("hist_launch");
+    // while the device counts: the next stretch of the stream and its logits (usually
+    // already generated during the sweep)
+    prefill_phi_stream();
     StreamAhead& sa = phi_stream;
     sa.live = &rng;
-    if (sa.fill(rng, phi_prefetch))
-      pool.run(sa.n, 1024, [&](int64_t a0, int64_t a1) { sa.logits(a0, a1); });
+    mark("prefill");
     histogram_wait(nidx == 0 ? nullptr : &mask);
+    mark("hist_wait");
     auto t1 = std::chrono::steady_clock::now();
     std::vector<int> touched;
     for (int i = 0; i < K; ++i)
@@ -1235,22 +1261,30 @@ struct Ctx {
         const size_t o = (size_t)t * sumatt + phi_off[j];
         cen[j] = (uint8_t)(sample_prob1_pick(&phi_cum[o], &phi_perm[o], att[j], sa.next(nullptr)) + 1);
       }
-      for (int j = 0; j < d; ++j) {
+      // sigma draws.  Items go in batches of up to kSpec whose first rbeta attempts are
+      // evaluated together at the stream positions they have if every earlier item of the
+      // batch is accepted on its first attempt (independent work the core overlaps);
+      // they are committed in order up to the first item that was not, which is then
+      // drawn sequentially from its true position.  Same arithmetic either way.
+      constexpr int kSpec = 4;
+      auto params = [&](int j, bool* bp, RBeta* rb) {
         PhiItem& P = phi_items[(size_t)t * d + j];
         const int l = cen[j] - 1;
         const double mj = (double)att[j];
         const double sumdelta = (double)h_freq.p[((size_t)k * d + j) * mmax + l];
         P.nw = w[j] + nn - sumdelta;
         P.nv = v[j] + sumdelta;
-        bool bp;
-        RBeta rb;
         if (l == P.lstar) {
-          bp = P.bp;
-          rb = P.rb;
+          *bp = P.bp;
+          if (*bp) *rb = P.rb;
         } else {
-          bp = rhig_beta_path(P.nv, P.nw, mj);
-          if (bp) rb = rbeta_setup(P.nw + 1, P.nv - 1);
+          *bp = rhig_beta_path(P.nv, P.nw, mj);
+          if (*bp) *rb = rbeta_setup(P.nw + 1, P.nv - 1);
         }
+      };
+      auto sequential = [&](int j, bool bp, const RBeta& rb) {
+        PhiItem& P = phi_items[(size_t)t * d + j];
+        const double mj = (double)att[j];
         if (bp) {                                   // hg:359-363
           double x = rbeta_draw_s(sa, rb);
           while (x > (mj - 1) / mj) x = rbeta_draw_s(sa, rb);
@@ -1260,6 +1294,55 @@ struct Ctx {
           P.path = 2;
           P.x = sa.next(nullptr);
         }
+      };
+      int j = 0;
+      while (j < d) {
+        bool bps[kSpec];
+        RBeta rbs[kSpec];
+        int cons[kSpec];
+        int nb = 0;
+        int64_t q = sa.used;
+        for (; nb < kSpec && j + nb < d; ++nb) {
+          params(j + nb, &bps[nb], &rbs[nb]);
+          cons[nb] = !bps[nb] ? 1 : rbs[nb].kind == RBeta::kBB ? 2 : 0;
+          if (cons[nb] == 0 || sa.spilled || q + cons[nb] > sa.n) break;
+          q += cons[nb];
+        }
+        const int nspec = nb;   // items with a speculative first attempt
+        double xs[kSpec];
+        bool ok[kSpec];
+        q = sa.used;
+        for (int b = 0; b < nspec; ++b) {
+          const double mj = (double)att[j + b];
+          if (bps[b]) {
+            double wv;
+            ok[b] = rbeta_bb_attempt(rbs[b], sa.u[q], sa.lg[q], sa.u[q + 1], sa.lz[q], &wv);
+            xs[b] = rbeta_bb_value(rbs[b], wv);
+            ok[b] = ok[b] && !(xs[b] > (mj - 1) / mj);
+          } else {
+            xs[b] = sa.u[q];
+            ok[b] = true;
+          }
+          q += cons[b];
+        }
+        int b = 0;
+        for (; b < nspec && ok[b]; ++b) {
+          PhiItem& P = phi_items[(size_t)t * d + j + b];
+          P.path = bps[b] ? 1 : 2;
+          P.x = xs[b];
+          sa.used += cons[b];
+        }
+        j += b;
+        if (j >= d) break;
+        if (b < nb) {                               // item j was prepared (speculated or not)
+          sequential(j, bps[b], rbs[b]);
+        } else {                                    // batch ended before item j was prepared
+          bool bp;
+          RBeta rb;
+          params(j, &bp, &rb);
+          sequential(j, bp, rb);
+        }
+        ++j;
       }
       return 0;
     };
@@ -1313,16 +1396,21 @@ struct Ctx {
     else for (int t = 0; t < T; ++t) phaseA(t);
     int berr = 0;
     int tb = 0;
+    double wait_us = 0;
     for (; tb < T; ++tb) {
+      auto w0 = std::chrono::steady_clock::now();
       while (stA[tb].load(std::memory_order_acquire) == 0 && par) HostPool::spin_pause();
+      if (debug & 2) wait_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - w0).count();
       berr = phaseB(tb);
       if (berr) break;
       stB[tb].store(1, std::memory_order_release);
     }
+    if (debug & 2) std::fprintf(stderr, "[phi] B waited %.1f us for A, %lld draws\n", wait_us, (long long)sa.used);
     for (int t = tb; t < T; ++t) stB[t].store(-1, std::memory_order_release);
+    mark("B");
     sa.finish();                                      // the host stream continues after B's draws
+    sa.n = 0;                                         // consumed
     phi_prefetch = std::max<int64_t>(4096, sa.used + sa.used / 4 + 512);
-    auto tB = std::chrono::steady_clock::now();
     if (par) {
       // help with the remaining C work, then wait for the workers
       for (;;) {
@@ -1339,7 +1427,7 @@ struct Ctx {
       for (int t = 0; t < T; ++t)
         if (!phaseC(t) && gsl_err.load() < 0) gsl_err.store(t);
     }
-    auto tC = std::chrono::steady_clock::now();
+    mark("C");
     if (berr) { err = "center draw failed"; return berr; }
     if (gsl_err.load() >= 0) { err = "norm_const2 - hypergeometric diverging with infinity"; return kGsl; }
     if (full) {
@@ -1354,11 +1442,7 @@ struct Ctx {
       stage_commit(L, T, false);
     }
     auto t2 = std::chrono::steady_clock::now();
-    if (debug & 2) {
-      auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
-      std::fprintf(stderr, "[phi] hist %.1f us, A+B %.1f, C tail %.1f, commit %.1f us (%d x %d items, %d threads)\n",
-                   us(t0, t1), us(t1, tB), us(tB, tC), us(tC, t2), T, d, pool.threads());
-    }
+    mark("commit");
     stats.t_stats_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
     stats.t_host_phi_ms += std::chrono::duration<double, std::milli>(t2 - t1).count();
     return kOk;
@@ -1496,6 +1580,8 @@ int Ctx::init_chain(const hdpm_chain_params* p, const int32_t* c_init) {
 int Ctx::iteration(const hdpm_chain_params* p, int iter, int* idx_1_sm, int* accepted, double* ll) {
   int st;
   *accepted = 0;
+  trace.clear();
+  mark("start");
   if (p->neal8 && iter % p->n8_step_size == 0) {       // la:94-103
     st = neal8_sweep(p->m);
     if (st) return st;
@@ -1511,7 +1597,19 @@ int Ctx::iteration(const hdpm_chain_params* p, int iter, int* idx_1_sm, int* acc
     st = generate_pool((int64_t)n * p->m * p->thinning);
     if (st) return st;
   }
-  return compute_loglikelihood(ll);                      // la:132
+  st = compute_loglikelihood(ll);                        // la:132
+  mark("loglik");
+  if ((debug & 2) && trace.size() > 1) {
+    std::string line = "[iter]";
+    for (size_t k = 1; k < trace.size(); ++k) {
+      char buf[96];
+      std::snprintf(buf, sizeof(buf), " %s %.1f", trace[k].first,
+                    std::chrono::duration<double, std::micro>(trace[k].second - trace[k - 1].second).count());
+      line += buf;
+    }
+    std::fprintf(stderr, "%s us\n", line.c_str());
+  }
+  return st;
 }
 
 // la:6-174

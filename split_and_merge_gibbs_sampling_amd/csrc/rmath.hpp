@@ -246,7 +246,44 @@ struct RngSrc {
     if (lg) *lg = std::log(u / (1.0 - u));
     return u;
   }
+  // an rbeta BB attempt's two uniforms; lz = log(u1 * u1 * u2) or NaN (not precomputed)
+  void pair(double* u1, double* lg1, double* u2, double* lz) {
+    *u1 = next(lg1);
+    *u2 = next(nullptr);
+    *lz = NAN;
+  }
 };
+
+// One attempt of Cheng's algorithm BB (nmath rbeta, a > 1) for uniforms u1, u2 with
+// lg1 = log(u1 / (1 - u1)): true when accepted, with w set; rbeta_bb_value(w) is the draw.
+// The draw loop and the speculative batches in update_phi share these, so both round
+// identically.
+// lz, when not NaN, is log(u1 * u1 * u2) computed ahead (same expression as below).
+__attribute__((always_inline)) inline bool rbeta_bb_attempt(const RBeta& p, double u1, double lg1, double u2,
+                                                             double lz, double* w_out) {
+  const double expmax = DBL_MAX_EXP * M_LN2;
+  const double a = p.a, b = p.b, alpha = p.alpha;
+  const double v = p.beta * lg1;
+  double w;
+  if (v <= expmax) {
+    w = a * std::exp(v);
+    if (!std::isfinite(w)) w = DBL_MAX;
+  } else {
+    w = DBL_MAX;
+  }
+  *w_out = w;
+  const double z = u1 * u1 * u2;
+  const double r = p.gamma * v - 1.3862944;
+  const double s = a + r - w;
+  if (s + 2.609438 >= 5.0 * z) return true;
+  const double t = lz == lz ? lz : std::log(z);
+  if (s > t) return true;
+  return !(r + alpha * std::log(alpha / (b + w)) < t);
+}
+
+__attribute__((always_inline)) inline double rbeta_bb_value(const RBeta& p, double w) {
+  return (p.aa != p.a) ? p.b / (p.b + w) : w / (p.b + w);
+}
 
 template <class S>
 __attribute__((always_inline)) inline double rbeta_draw_s(S& src, const RBeta& p) {
@@ -285,18 +322,13 @@ __attribute__((always_inline)) inline double rbeta_draw_s(S& src, const RBeta& p
     }
     return (p.aa == a) ? a / (a + w) : w / (a + w);
   }
-  do {
-    u1 = src.next(&lg1);
-    u2 = src.next(nullptr);
-    vw(a);
-    z = u1 * u1 * u2;
-    r = p.gamma * v - 1.3862944;
-    s = a + r - w;
-    if (s + 2.609438 >= 5.0 * z) break;
-    t = std::log(z);
-    if (s > t) break;
-  } while (r + alpha * std::log(alpha / (b + w)) < t);
-  return (p.aa != a) ? b / (b + w) : w / (b + w);
+  (void)r; (void)s; (void)t; (void)v; (void)z;
+  for (;;) {
+    double lz;
+    src.pair(&u1, &lg1, &u2, &lz);
+    if (rbeta_bb_attempt(p, u1, lg1, u2, lz, &w)) break;
+  }
+  return rbeta_bb_value(p, w);
 }
 
 __attribute__((always_inline)) inline double rbeta_draw(Rng& rng, const RBeta& p) {
@@ -310,7 +342,7 @@ __attribute__((always_inline)) inline double rbeta_draw(Rng& rng, const RBeta& p
 // one, so .Random.seed matches).  Past the prefix, next() continues on the live Rng.
 struct StreamAhead {
   Rng start;
-  std::vector<double> u, lg;
+  std::vector<double> u, lg, lz;   // lz[k] = log(u[k] * u[k] * u[k + 1])
   std::vector<int64_t> vfirst;                 // first word index served by each mt array
   std::vector<std::array<uint32_t, 624>> arr;  // mt array versions (arr[0] = start.mt)
   int64_t n = 0, used = 0;
@@ -326,6 +358,7 @@ struct StreamAhead {
     Rng g = r;
     u.resize(N);
     lg.resize(N);
+    lz.resize(N);
     vfirst.assign(1, 0);
     arr.resize(1);
     std::memcpy(arr[0].data(), g.mt, sizeof(g.mt));
@@ -343,7 +376,10 @@ struct StreamAhead {
     return true;
   }
   void logits(int64_t a, int64_t b) {
-    for (int64_t k = a; k < b; ++k) lg[k] = std::log(u[k] / (1.0 - u[k]));
+    for (int64_t k = a; k < b; ++k) {
+      lg[k] = std::log(u[k] / (1.0 - u[k]));
+      lz[k] = k + 1 < n ? std::log(u[k] * u[k] * u[k + 1]) : NAN;
+    }
   }
   void restore(Rng& r, int64_t c) const {
     const uint64_t ep = r.epoch;
@@ -372,6 +408,19 @@ struct StreamAhead {
     const double x = live->unif();
     if (lgout) *lgout = std::log(x / (1.0 - x));
     return x;
+  }
+  void pair(double* u1, double* lg1, double* u2, double* lzo) {
+    if (used + 1 < n) {
+      *u1 = u[used];
+      *lg1 = lg[used];
+      *u2 = u[used + 1];
+      *lzo = lz[used];
+      used += 2;
+      return;
+    }
+    *u1 = next(lg1);
+    *u2 = next(nullptr);
+    *lzo = NAN;
   }
   // Leave the live Rng after everything drawn so far.
   void finish() {

@@ -43,6 +43,7 @@ int main() {
         CHECK(sa.u[c] == one.unif());
         const double u = sa.u[c];
         CHECK(sa.lg[c] == std::log(u / (1.0 - u)));
+        if (c + 1 < 3000) CHECK(sa.lz[c] == std::log(u * u * sa.u[c + 1]));
       }
     }
     // spilling past the prefix continues the live stream
