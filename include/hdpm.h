@@ -125,7 +125,8 @@ int hdpm_reset_stats(hdpm_ctx* ctx);
 /* Testing / diagnostics.  mode bit 0: evaluate every point on the exact path (no
  * certainty shortcut); bit 1: print per-phase timings to stderr; bit 2: compute the
  * log-likelihood with the per-point kernel (no regrouping into match counts); bit 3: no
- * snapshot speculation (the resolver decides every uncertain point itself). */
+ * snapshot speculation (the resolver decides every uncertain point itself); bit 4: recount
+ * the frequency tables every update_phi (no incremental move log). */
 int hdpm_set_debug(hdpm_ctx* ctx, int32_t mode);
 /* Block until all device work of the context is done. */
 int hdpm_synchronize(hdpm_ctx* ctx);

@@ -36,6 +36,10 @@ hipError_t launch_exact_rows(const PrepassArgs& a, int nblocks, hipStream_t s);
 size_t resolve_smem_bytes(int scap, int m);
 hipError_t launch_relabel(int* c, const int* los, int n, hipStream_t s);
 hipError_t launch_finish_sweep(int* counts, int* sol, int* los, int* src, int K, int nslots, hipStream_t s);
+hipError_t launch_apply_moves(const int* mlog, const int* mcount, int nmoves, const uint8_t* codes_t, int d, int nq,
+                              int mmax, unsigned int* freq, hipStream_t s);
+hipError_t launch_freq_gather(const unsigned int* freq, const int* sol, int K, int fs, unsigned int* out,
+                              hipStream_t s);
 hipError_t launch_scatter_clusters(const uint8_t* stage, int nent, int dp, int d, int bw, int full, uint8_t* codes,
                                    double* tab, uint64_t* bnd, int* counts, int* sol, int* los, int* src,
                                    hipStream_t s);
@@ -394,8 +398,12 @@ struct Ctx {
   DevBuf<uint8_t> d_stage;
   hipEvent_t ev_stage = nullptr;
 
-  // statistics buffers
-  DevBuf<unsigned> d_freq;
+  // statistics buffers.  d_freq holds freq[slot][j][level] and, while freq_dev_valid,
+  // follows the labels through the sweeps incrementally (resolver move log); d_freq_m
+  // takes masked (subset) histograms.
+  DevBuf<unsigned> d_freq, d_freq2, d_freq_m;
+  bool freq_dev_valid = false;
+  DevBuf<int> d_mlog, d_mcount;
   PinBuf<unsigned> h_freq;
   DevBuf<unsigned char> d_mask;
   PinBuf<unsigned char> h_mask;
@@ -674,6 +682,8 @@ struct Ctx {
     d_slot_codes.ensure((size_t)nc * dp, true, stream);
     d_slot_tab.ensure((size_t)nc * 2 * d, true, stream);
     d_slot_bnd.ensure((size_t)nc * bw, true, stream);
+    d_freq.ensure((size_t)nc * d * mmax, true, stream);
+    d_freq2.ensure((size_t)nc * d * mmax);
     scap = nc;
   }
 
@@ -736,6 +746,7 @@ struct Ctx {
     d_c.ensure(n);
     HIPCHK(hipMemcpyAsync(d_c.p, h_c.data(), (size_t)n * 4, hipMemcpyHostToDevice, stream));
     labels_version++;
+    freq_dev_valid = false;
     HIPCHK(hipStreamSynchronize(stream));
     host_c_valid = true;
   }
@@ -830,6 +841,7 @@ struct Ctx {
     }
     HIPCHK(hipStreamSynchronize(stream));
     scap = 0;   // slot arrays are re-laid out for the new bound size on next use
+    freq_dev_valid = false;
     d_slot_bnd.release();
     h_logn.resize((size_t)n + 2);
     h_logn[0] = -INFINITY;
@@ -969,6 +981,13 @@ struct Ctx {
     int p = 0;
     const double dmax = 0.25;
     const int64_t rounds0 = stats.rounds;
+    const int64_t moves0 = stats.moves;
+    const bool track = freq_dev_valid;
+    if (track) {
+      d_mlog.ensure((size_t)3 * n);
+      d_mcount.ensure(1);
+      HIPCHK(hipMemsetAsync(d_mcount.p, 0, 4, stream));
+    }
     while (p < n) {
       ensure_slots(nslots + 2);
       d_ctl.ensure(8 + 3 * (size_t)scap);
@@ -1016,6 +1035,10 @@ struct Ctx {
       ra.lcap = std::min(scap, nslots + 2);
       ra.nslots = nslots; ra.ctl = (ResolveCtl*)d_ctl.p; ra.summary = d_ctl.p + 8; ra.force_exact = (debug & 1);
       ra.prof = nullptr;
+      ra.mlog = track ? d_mlog.p : nullptr;
+      ra.mcount = track ? d_mcount.p : nullptr;
+      ra.freq = track ? d_freq.p : nullptr;
+      ra.fstride = d * mmax;
       if (debug & 2) {
         d_rprof.ensure(16);
         ra.prof = d_rprof.p;
@@ -1071,6 +1094,13 @@ struct Ctx {
     const int* cnt = sol + scap;
     const int* src = cnt + scap;
     HIPCHK(launch_relabel(d_c.p, d_los.p, n, stream));
+    if (track) {   // carry the frequency tables: apply the moves, then re-index slots -> labels
+      HIPCHK(launch_apply_moves(d_mlog.p, d_mcount.p, (int)std::min<int64_t>(stats.moves - moves0, n), d_codes_t.p, d,
+                                nq, mmax, d_freq.p, stream));
+      HIPCHK(launch_freq_gather(d_freq.p, d_sol.p, K, d * mmax, d_freq2.p, stream));
+      std::swap(d_freq.p, d_freq2.p);
+      std::swap(d_freq.n, d_freq2.n);
+    }
     HIPCHK(launch_finish_sweep(d_counts.p, d_sol.p, d_los.p, d_src.p, K, nslots, stream));
     h_center.assign((size_t)K * d, 0);
     h_sigma.assign((size_t)K * d, 0.0);
@@ -1106,10 +1136,18 @@ struct Ctx {
   }
   void histogram_launch(const std::vector<unsigned char>* mask) {
     const size_t nent = (size_t)K * d * mmax;
-    d_freq.ensure(std::max<size_t>(nent, 1));
+    h_freq.ensure(std::max<size_t>(nent, 1));
+    if (!mask && freq_dev_valid && !(debug & 16)) {
+      // the per-label tables were carried through the sweep by the move log
+      HIPCHK(hipMemcpyAsync(h_freq.p, d_freq.p, nent * 4, hipMemcpyDeviceToHost, stream));
+      return;
+    }
+    DevBuf<unsigned>& dst = mask ? d_freq_m : d_freq;
+    if (mask) dst.ensure(std::max<size_t>(nent, 1));
+    else ensure_slots(K + 2);
     HistArgs ha;
     ha.codes_t = d_codes_t.p; ha.n = n; ha.d = d; ha.nq = nq; ha.label = d_c.p;
-    ha.mask = nullptr; ha.K = K; ha.mmax = mmax; ha.freq = d_freq.p;
+    ha.mask = nullptr; ha.K = K; ha.mmax = mmax; ha.freq = dst.p;
     ha.xpk = d_xpk.p; ha.W = W; ha.wb = wb;
     {
       int nbx, kc, tpb;
@@ -1125,8 +1163,8 @@ struct Ctx {
       ha.mask = d_mask.p;
     }
     HIPCHK(launch_hist(ha, stream));
-    h_freq.ensure(std::max<size_t>(nent, 1));
-    HIPCHK(hipMemcpyAsync(h_freq.p, d_freq.p, nent * 4, hipMemcpyDeviceToHost, stream));
+    if (!mask) freq_dev_valid = true;
+    HIPCHK(hipMemcpyAsync(h_freq.p, dst.p, nent * 4, hipMemcpyDeviceToHost, stream));
   }
   void histogram_wait(const std::vector<unsigned char>* mask) {
     HIPCHK(hipStreamSynchronize(stream));

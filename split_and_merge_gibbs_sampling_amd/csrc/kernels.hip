@@ -35,6 +35,10 @@ __device__ __forceinline__ int64_t pick_entry(uint32_t y, int64_t P) {
   return (int64_t)((int)((double)(int)P * raw_to_unif(y) + 1)) - 1;
 }
 
+__device__ __forceinline__ int a_code(const uint8_t* codes_t, int64_t i, int j, int nq) {
+  return codes_t[tiled_offset(i, j, nq)];
+}
+
 __device__ __forceinline__ bool byte_differs(const uint4& dx, int b) {
   const uint32_t w = b < 4 ? dx.x : b < 8 ? dx.y : b < 12 ? dx.z : dx.w;
   return ((w >> ((b & 3) * 8)) & 0xffu) != 0u;
@@ -462,6 +466,16 @@ __device__ __forceinline__ double slot_drift(const RState& st, const double* log
   return INFINITY;
 }
 
+// lane 0: record a reassignment for the incremental frequency tables
+__device__ __forceinline__ void log_move(const ResolveArgs& a, int& nlog, int64_t i, int from, int to) {
+  if (a.mlog) {
+    a.mlog[3 * nlog] = (int)i;
+    a.mlog[3 * nlog + 1] = from;
+    a.mlog[3 * nlog + 2] = to;
+    ++nlog;
+  }
+}
+
 // lane 0: slot s's count changed -> refresh its log-count cache
 __device__ __forceinline__ void set_count(const RState& st, const double* logn, int s, int c) {
   st.cnt[s] = c;
@@ -870,6 +884,7 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
   }
   wave_sync();
   const int ncol = a.S + a.m;
+  int nlog = a.mcount ? *a.mcount : 0;   // lane 0's running move-log length
 
   // Decide point i (exact row in LDS at Lr) and apply n8:107-159.  Returns false to stop
   // the sweep here.
@@ -890,6 +905,7 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
             if (ns != own) {
               a.c[i] = ns; set_count(st, a.logn, own, st.cnt[own] - 1); set_count(st, a.logn, ns, st.cnt[ns] + 1);
               S.moves++;
+              log_move(a, nlog, i, own, ns);
               S.dnow = fmax(S.dnow, fmax(slot_drift(st, a.logn, own), slot_drift(st, a.logn, ns)));
             }
           } else {                                                  // case 2
@@ -902,6 +918,7 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
               a.c[i] = target; set_count(st, a.logn, own, st.cnt[own] - 1);
               set_count(st, a.logn, target, st.cnt[target] + 1);
               S.moves++;
+              log_move(a, nlog, i, own, target);
               const int last = st.sol[K - 1];
               st.los[own] = -1;
               if (ownlab != K - 1) { st.sol[ownlab] = last; st.los[last] = ownlab; }
@@ -928,6 +945,7 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
               set_count(st, a.logn, ns, 1);
               st.snap[ns] = 0;
               a.c[i] = ns;
+              log_move(a, nlog, i, own, ns);
               S.src = (int)pick_entry(a.raw[i * (a.m + 1) + l], a.P);
               a.slot_src[ns] = S.src;
               S.moves++;
@@ -943,6 +961,8 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
     if (S.restart && S.status == 0) {
       const int ns = S.nslots - 1;
       copy_pool_params(a, S.src, ns);
+      if (a.freq)   // the new slot's frequency table starts empty (the logged move fills it)
+        for (int e = lane; e < a.fstride; e += kWave) a.freq[(int64_t)ns * a.fstride + e] = 0u;
     }
     return S.status == 0 && !S.restart;
   };
@@ -1057,6 +1077,7 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
     for (int k = 0; k < 8; ++k) a.prof[k] = tp[k];
     for (int k = 0; k < 8; ++k) a.prof[8 + k] = S.tsub[k];
   }
+  if (lane == 0 && a.mcount) *a.mcount = nlog;
   if (lane == 0) {
     ResolveCtl c;
     c.next = S.next; c.status = S.status; c.restart = S.restart; c.K = S.K; c.nslots = S.nslots;
@@ -1069,6 +1090,35 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
 __global__ void k_relabel(int* c, const int* label_of_slot, int n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) c[i] = label_of_slot[c[i]];
+}
+
+// Incremental sufficient statistics: every logged reassignment moves the point's codes
+// from one slot's frequency table to the other's (one wave per move, lanes over
+// attributes).  Equivalent to recounting, at the cost of the moves.
+__global__ __launch_bounds__(kWave) void k_apply_moves(const int* __restrict__ mlog, const int* __restrict__ mcount,
+                                                      const uint8_t* __restrict__ codes_t, int d, int nq, int mmax,
+                                                      unsigned int* freq) {
+  const int nm = *mcount;
+  const int fs = d * mmax;
+  for (int q = blockIdx.x; q < nm; q += gridDim.x) {
+    const int64_t i = mlog[3 * q];
+    const int from = mlog[3 * q + 1], to = mlog[3 * q + 2];
+    for (int j = threadIdx.x; j < d; j += kWave) {
+      const int x = a_code(codes_t, i, j, nq) - 1;
+      atomicSub(freq + (int64_t)from * fs + j * mmax + x, 1u);
+      atomicAdd(freq + (int64_t)to * fs + j * mmax + x, 1u);
+    }
+  }
+}
+
+// freq per label after the sweep: out[l] = freq[slot_of_label[l]].
+__global__ void k_freq_gather(const unsigned int* __restrict__ freq, const int* __restrict__ sol, int K, int fs,
+                              unsigned int* __restrict__ out) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < (int64_t)K * fs;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int l = (int)(e / fs);
+    out[e] = freq[(int64_t)sol[l] * fs + (e - (int64_t)l * fs)];
+  }
 }
 
 // After k_relabel: counts per label, identity slot maps (slot == label again).  One block.
@@ -1321,6 +1371,23 @@ hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s) {
 
 hipError_t launch_relabel(int* c, const int* los, int n, hipStream_t s) {
   hipLaunchKernelGGL(k_relabel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, c, los, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_apply_moves(const int* mlog, const int* mcount, int nmoves, const uint8_t* codes_t, int d, int nq,
+                              int mmax, unsigned int* freq, hipStream_t s) {
+  if (nmoves <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_apply_moves, dim3(std::min(nmoves, 4096)), dim3(kWave), 0, s, mlog, mcount, codes_t, d, nq, mmax,
+                     freq);
+  return hipGetLastError();
+}
+
+hipError_t launch_freq_gather(const unsigned int* freq, const int* sol, int K, int fs, unsigned int* out,
+                              hipStream_t s) {
+  const int64_t work = (int64_t)K * fs;
+  if (work <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_freq_gather, dim3((unsigned)std::min<int64_t>(1024, (work + 255) / 256)), dim3(256), 0, s, freq,
+                     sol, K, fs, out);
   return hipGetLastError();
 }
 

@@ -133,6 +133,12 @@ struct ResolveArgs {
   ResolveCtl* ctl;
   int* summary;              // at exit: [label -> slot: scap][count per slot: scap][pool source per slot: scap]
   int force_exact;           // testing: evaluate every point on the exact path
+  // move log for the incremental sufficient statistics (nullptr: not kept):
+  // mlog[3q .. 3q+2] = (point, from slot, to slot); *mcount entries so far this sweep
+  int* mlog;
+  int* mcount;
+  unsigned int* freq;        // per-slot freq [slot][d][mmax] (new slots are zeroed here)
+  int fstride;               // d * mmax
   long long* prof;           // diagnostics: resolver phase times (s_memrealtime ticks) or nullptr
 };
 

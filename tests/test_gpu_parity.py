@@ -119,7 +119,7 @@ def test_zoo_sweeps_with_update_phi_one_cluster(hd, oracle, zoo, debug):
     assert stats["restarts"] > 0
 
 
-@pytest.mark.parametrize("debug", [0, 1, 8])
+@pytest.mark.parametrize("debug", [0, 1, 8, 16])
 def test_synthetic_sweeps_with_update_phi(hd, oracle, debug):
     ds = synth(6000, 32, 8, 2, seed=3)
     cen, sig = random_params(ds, 8, 7)
