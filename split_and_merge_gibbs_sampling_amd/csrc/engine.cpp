@@ -13,6 +13,8 @@
 #include <cstdlib>
 #include <functional>
 #include <mutex>
+#include <pthread.h>
+#include <sched.h>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -101,7 +103,9 @@ struct PinBuf {
     if (count <= n && p) return;
     if (p) (void)hipHostFree(p);
     p = nullptr;
-    HIPCHK(hipHostMalloc(&p, std::max<size_t>(count, 1) * sizeof(T), hipHostMallocDefault));
+    // non-coherent (coarse-grained): CPU-cached, so the host reads these buffers at cache
+    // speed; every device write to them is followed by a stream or event wait before use
+    HIPCHK(hipHostMalloc(&p, std::max<size_t>(count, 1) * sizeof(T), hipHostMallocNonCoherent));
     n = count;
   }
 };
@@ -211,6 +215,59 @@ class HostPool {
       T = (int)std::min<unsigned>(h ? h : 4, 8);
     }
     for (int t = 1; t < T; ++t) th_.emplace_back([this] { loop(); });
+    pin_workers();
+  }
+  // Workers on distinct physical cores of the creating thread's L3 domain (the host
+  // phases hand data between cores every iteration); HDPM_PIN_THREADS=0 leaves placement
+  // to the OS.
+  void pin_workers() {
+    if (const char* e = std::getenv("HDPM_PIN_THREADS"))
+      if (std::atoi(e) == 0) return;
+    const int me = sched_getcpu();
+    if (me < 0) return;
+    cpu_set_t allowed;
+    if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return;
+    auto read_list = [](const std::string& path) {
+      std::vector<int> out;
+      FILE* f = std::fopen(path.c_str(), "r");
+      if (!f) return out;
+      char buf[4096];
+      if (!std::fgets(buf, sizeof(buf), f)) buf[0] = 0;
+      std::fclose(f);
+      for (char* p = buf; *p;) {
+        char* end;
+        long a = std::strtol(p, &end, 10);
+        if (end == p) { ++p; continue; }
+        long b = a;
+        if (*end == '-') b = std::strtol(end + 1, &end, 10);
+        for (long c = a; c <= b; ++c) out.push_back((int)c);
+        p = end;
+      }
+      return out;
+    };
+    const std::string base = "/sys/devices/system/cpu/cpu";
+    std::vector<int> dom = read_list(base + std::to_string(me) + "/cache/index3/shared_cpu_list");
+    if (dom.empty()) return;
+    std::vector<char> used_core(4096, 0);
+    auto core_of = [&](int c) {
+      const std::vector<int> sib = read_list(base + std::to_string(c) + "/topology/thread_siblings_list");
+      return sib.empty() ? c : sib.front();
+    };
+    used_core[core_of(me) & 4095] = 1;
+    std::vector<int> pick;
+    for (int c : dom) {
+      if (!CPU_ISSET(c, &allowed)) continue;
+      const int core = core_of(c) & 4095;
+      if (used_core[core]) continue;
+      used_core[core] = 1;
+      pick.push_back(c);
+    }
+    for (size_t t = 0; t < th_.size() && t < pick.size(); ++t) {
+      cpu_set_t cs;
+      CPU_ZERO(&cs);
+      CPU_SET(pick[t], &cs);
+      (void)pthread_setaffinity_np(th_[t].native_handle(), sizeof(cs), &cs);
+    }
   }
   void quiesce() {
     while (active_.load(std::memory_order_acquire) != 0) spin_pause();
@@ -277,7 +334,7 @@ class HostPool {
   std::function<void(int)> bjob_;
   std::function<void(int)>* bcast_ = nullptr;
   std::atomic<bool> stop_{false};
-  int spin_us_ = 300;
+  int spin_us_ = 2000;   // an iteration's host phases are ~1 ms apart: stay awake between them
 };
 
 template <class F>
@@ -982,6 +1039,7 @@ struct Ctx {
     const double dmax = 0.25;
     const int64_t rounds0 = stats.rounds;
     const int64_t moves0 = stats.moves;
+    HostPool::get().prewake();        // workers: stream logits now, update_phi's phases next
     const bool track = freq_dev_valid;
     if (track) {
       d_mlog.ensure((size_t)3 * n);
@@ -1244,10 +1302,10 @@ struct Ctx {
     const UploadLayout L = stage_begin(std::max(nent, 1));
 
     // ---- phase A: one cluster at a time, in order
-    auto phaseA = [&](int t) {
+    auto phaseA = [&](int t, int j0, int j1) {
       const int k = touched[t];
       const int nn = h_counts[k];
-      for (int j = 0; j < d; ++j) {
+      for (int j = j0; j < j1; ++j) {
         const int mj = att[j];
         const unsigned* fj = &h_freq.p[((size_t)k * d + j) * mmax];
         const double sg = h_sigma[(size_t)k * d + j];
@@ -1410,12 +1468,20 @@ struct Ctx {
     std::vector<std::atomic<int>> stA(T), stB(T);
     for (int t = 0; t < T; ++t) { stA[t].store(0); stB[t].store(0); }
     std::atomic<int> nextA{0}, nextC{0}, gsl_err{-1};
+    const auto tlaunch = std::chrono::steady_clock::now();
+    std::vector<double> a_beg(T, 0.0), a_end(T, 0.0);
+    // A in chunks of attributes so the first cluster is ready early
+    const int achunk = std::max(8, (d + 3) / 4);
+    const int nach = (d + achunk - 1) / achunk;
     auto worker = [&](int) {
       for (;;) {
-        const int t = nextA.fetch_add(1);
-        if (t >= T) break;
-        phaseA(t);
-        stA[t].store(1, std::memory_order_release);
+        const int task = nextA.fetch_add(1);
+        if (task >= T * nach) break;
+        const int t = task / nach, c = task - t * nach;
+        if ((debug & 2) && c == 0) a_beg[t] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tlaunch).count();
+        phaseA(t, c * achunk, std::min(d, (c + 1) * achunk));
+        if (stA[t].fetch_add(1, std::memory_order_acq_rel) + 1 == nach && (debug & 2))
+          a_end[t] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tlaunch).count();
       }
       for (;;) {
         const int t = nextC.fetch_add(1);
@@ -1431,19 +1497,27 @@ struct Ctx {
     };
     const bool par = pool.workers() > 0 && T > 1;
     if (par) pool.launch(worker);
-    else for (int t = 0; t < T; ++t) phaseA(t);
+    else for (int t = 0; t < T; ++t) phaseA(t, 0, d);
     int berr = 0;
     int tb = 0;
     double wait_us = 0;
     for (; tb < T; ++tb) {
       auto w0 = std::chrono::steady_clock::now();
-      while (stA[tb].load(std::memory_order_acquire) == 0 && par) HostPool::spin_pause();
+      while (par && stA[tb].load(std::memory_order_acquire) < nach) HostPool::spin_pause();
       if (debug & 2) wait_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - w0).count();
       berr = phaseB(tb);
       if (berr) break;
       stB[tb].store(1, std::memory_order_release);
     }
-    if (debug & 2) std::fprintf(stderr, "[phi] B waited %.1f us for A, %lld draws\n", wait_us, (long long)sa.used);
+    if (debug & 2) {
+      auto m0 = std::chrono::steady_clock::now();
+      if (T > 0) phaseA(0, 0, d);   // the same work again on this thread (diagnostic)
+      const double mainA = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - m0).count();
+      std::fprintf(stderr, "[phi] main-thread A(0) %.1f us (cpu %d); ", mainA, sched_getcpu());
+      std::fprintf(stderr, "[phi] B waited %.1f us for A, %lld draws; A(t) begin/end us:", wait_us, (long long)sa.used);
+      for (int t = 0; t < std::min(T, 10); ++t) std::fprintf(stderr, " %.0f/%.0f", a_beg[t], a_end[t]);
+      std::fprintf(stderr, "\n");
+    }
     for (int t = tb; t < T; ++t) stB[t].store(-1, std::memory_order_release);
     mark("B");
     sa.finish();                                      // the host stream continues after B's draws
