@@ -179,6 +179,8 @@ def main():
         it += 1
     eng.synchronize()
     eng.reset_stats()
+    if os.environ.get("HDPM_BENCH_TIMELINE"):
+        eng.set_debug(32)                        # host timeline of the timed iterations (stderr)
     D.barrier()
     cuda_sync()
     t0 = time.perf_counter()

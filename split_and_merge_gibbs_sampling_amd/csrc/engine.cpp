@@ -64,6 +64,8 @@ struct HipError {
     if (_e != hipSuccess) throw HipError{_e, #x};     \
   } while (0)
 
+static std::atomic<int64_t> g_dev_allocs{0};   // device allocations made (diagnostics)
+
 template <class T>
 struct DevBuf {
   T* p = nullptr;
@@ -81,6 +83,7 @@ struct DevBuf {
   void ensure(size_t count, bool keep_old = false, hipStream_t s = nullptr) {
     if (count <= n && p) return;
     T* np = nullptr;
+    g_dev_allocs.fetch_add(1, std::memory_order_relaxed);
     HIPCHK(hipMalloc(&np, std::max<size_t>(count, 1) * sizeof(T)));
     if (keep_old && p && n) {
       HIPCHK(hipMemcpyAsync(np, p, n * sizeof(T), hipMemcpyDeviceToDevice, s));
@@ -225,6 +228,7 @@ class HostPool {
       if (std::atoi(e) == 0) return;
     const int me = sched_getcpu();
     if (me < 0) return;
+    main_cpu_ = me;
     cpu_set_t allowed;
     if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return;
     auto read_list = [](const std::string& path) {
@@ -335,6 +339,29 @@ class HostPool {
   std::function<void(int)>* bcast_ = nullptr;
   std::atomic<bool> stop_{false};
   int spin_us_ = 2000;   // an iteration's host phases are ~1 ms apart: stay awake between them
+  int main_cpu_ = -1;    // the calling thread's core (kept free of workers)
+
+ public:
+  int main_cpu() const { return main_cpu_; }
+};
+
+// The calling thread on the core kept free of pool workers for the duration of an engine
+// call (the serial draws share data with the workers through the L3); the caller's
+// affinity is restored on exit.  HDPM_PIN_THREADS=0 disables it.
+struct ScopedPin {
+  cpu_set_t old;
+  bool active = false;
+  ScopedPin() {
+    const int c = HostPool::get().main_cpu();
+    if (c < 0 || sched_getaffinity(0, sizeof(old), &old) != 0 || !CPU_ISSET(c, &old)) return;
+    cpu_set_t cs;
+    CPU_ZERO(&cs);
+    CPU_SET(c, &cs);
+    active = sched_setaffinity(0, sizeof(cs), &cs) == 0;
+  }
+  ~ScopedPin() {
+    if (active) (void)sched_setaffinity(0, sizeof(old), &old);
+  }
 };
 
 template <class F>
@@ -362,6 +389,7 @@ struct SmWork {
 // generator runs concurrently with the sweep and the host-side update_phi draws.
 struct RngWindow {
   DevBuf<uint32_t> raw, arrays, init;
+  const uint32_t* init_src = nullptr;   // initial array on the device (init.p or a block of another window)
   PinBuf<uint32_t> h_init;
   uint64_t start_pos = 0, epoch = ~0ull;
   int64_t count = 0;
@@ -474,8 +502,12 @@ struct Ctx {
   // debug bit 1: per-iteration host timeline
   std::vector<std::pair<const char*, std::chrono::steady_clock::time_point>> trace;
   void mark(const char* what) {
-    if (debug & 2) trace.emplace_back(what, std::chrono::steady_clock::now());
+    if (debug & 34) trace.emplace_back(what, std::chrono::steady_clock::now());
   }
+  // debug bit 5: accumulate the per-iteration timeline (no extra synchronisation); printed
+  // by the context's destructor
+  std::vector<std::pair<std::string, double>> trace_sum;
+  int64_t trace_iters = 0, trace_alloc0 = -1;
   std::unordered_map<uint64_t, bool> beta_cache;
 
   SmWork sm;
@@ -484,6 +516,16 @@ struct Ctx {
   std::vector<int> sperm;
 
   ~Ctx() {
+    if (trace_iters > 0) {
+      std::string line = "[timeline] mean us/iteration:";
+      for (auto& kv : trace_sum) {
+        char buf[96];
+        std::snprintf(buf, sizeof(buf), " %s %.1f", kv.first.c_str(), kv.second / trace_iters);
+        line += buf;
+      }
+      std::fprintf(stderr, "%s (%lld iterations, %lld device allocations after the first)\n", line.c_str(),
+                   (long long)trace_iters, (long long)(g_dev_allocs.load() - trace_alloc0));
+    }
     if (gstream) {
       (void)hipStreamSynchronize(gstream);
       for (auto& w : win)
@@ -513,8 +555,10 @@ struct Ctx {
     const int head = W.mti0 >= 624 ? 0 : 624 - W.mti0;
     W.nblocks = count > head ? (int)((count - head + 623) / 624) : 0;
     W.count = count;
+    // sized for any start offset (the block count varies with it), so a window of a given
+    // length is never reallocated -- a free would synchronise the device
     W.raw.ensure(count);
-    W.arrays.ensure((size_t)std::max(W.nblocks, 1) * 624);
+    W.arrays.ensure((size_t)((count + 623) / 624 + 2) * 624);
     W.init.ensure(624);
     W.h_init.ensure(624);
     if (!W.done) HIPCHK(hipEventCreateWithFlags(&W.done, hipEventDisableTiming));
@@ -525,7 +569,7 @@ struct Ctx {
   void run_window(RngWindow& W) {
     ensure_jump(W.count);
     const bool multi = mt_G > 1 && W.count >= (int64_t)mt_G * 624 * 8;
-    MtGenArgs a{W.init.p, W.mti0, W.count, W.raw.p, W.arrays.p, W.nblocks, W.export_from,
+    MtGenArgs a{W.init_src ? W.init_src : W.init.p, W.mti0, W.count, W.raw.p, W.arrays.p, W.nblocks, W.export_from,
                 multi ? d_jpoly.p : nullptr, d_jidx.p, d_joff.p, mt_bpg, multi ? mt_G : 1};
     HIPCHK(launch_mt_gen(a, gstream));
     HIPCHK(hipEventRecord(W.done, gstream));
@@ -552,6 +596,7 @@ struct Ctx {
     size_window(W, count, export_after);
     std::memcpy(W.h_init.p, rng.mt, sizeof(rng.mt));
     HIPCHK(hipMemcpyAsync(W.init.p, W.h_init.p, 624 * 4, hipMemcpyHostToDevice, gstream));
+    W.init_src = W.init.p;
     run_window(W);
   }
 
@@ -581,9 +626,16 @@ struct Ctx {
     Wn.start_pos = target;
     Wn.epoch = rng.epoch;
     size_window(Wn, count, export_after);
-    const uint32_t* src = blk == 0 ? Ws.init.p : Ws.arrays.p + (blk - 1) * 624;
-    HIPCHK(hipMemcpyAsync(Wn.init.p, src, 624 * 4, hipMemcpyDeviceToDevice, gstream));
-    HIPCHK(hipMemcpyAsync(Wn.h_init.p, Wn.init.p, 624 * 4, hipMemcpyDeviceToHost, gstream));
+    if (blk == 0) {
+      // inside Ws's initial array, which may live in Wn's own exports: copy it out first
+      HIPCHK(hipMemcpyAsync(Wn.init.p, Ws.init_src ? Ws.init_src : Ws.init.p, 624 * 4, hipMemcpyDeviceToDevice,
+                            gstream));
+      Wn.init_src = Wn.init.p;
+    } else {
+      // read in place: Ws's exports are rewritten only by a later launch on this stream
+      Wn.init_src = Ws.arrays.p + (blk - 1) * 624;
+    }
+    HIPCHK(hipMemcpyAsync(Wn.h_init.p, Wn.init_src, 624 * 4, hipMemcpyDeviceToHost, gstream));
     run_window(Wn);
   }
 
@@ -1039,7 +1091,6 @@ struct Ctx {
     const double dmax = 0.25;
     const int64_t rounds0 = stats.rounds;
     const int64_t moves0 = stats.moves;
-    HostPool::get().prewake();        // workers: stream logits now, update_phi's phases next
     const bool track = freq_dev_valid;
     if (track) {
       d_mlog.ensure((size_t)3 * n);
@@ -1255,6 +1306,7 @@ struct Ctx {
   // update_phi's slice of the host stream, generated ahead (also called while the device
   // runs a sweep, which draws only from the device windows).
   void prefill_phi_stream() {
+    HostPool::get().prewake();        // for the logits below, then update_phi's phases
     rng_sync();
     StreamAhead& sa = phi_stream;
     if (sa.n > 0 && sa.used == 0 && sa.start.pos == rng.pos && sa.start.epoch == rng.epoch) return;
@@ -1711,6 +1763,17 @@ int Ctx::iteration(const hdpm_chain_params* p, int iter, int* idx_1_sm, int* acc
   }
   st = compute_loglikelihood(ll);                        // la:132
   mark("loglik");
+  if ((debug & 32) && trace.size() > 1) {
+    if (trace_alloc0 < 0) trace_alloc0 = g_dev_allocs.load();
+    for (size_t k = 1; k < trace.size(); ++k) {
+      const double us = std::chrono::duration<double, std::micro>(trace[k].second - trace[k - 1].second).count();
+      size_t q = 0;
+      while (q < trace_sum.size() && trace_sum[q].first != trace[k].first) ++q;
+      if (q == trace_sum.size()) trace_sum.emplace_back(trace[k].first, 0.0);
+      trace_sum[q].second += us;
+    }
+    trace_iters++;
+  }
   if ((debug & 2) && trace.size() > 1) {
     std::string line = "[iter]";
     for (size_t k = 1; k < trace.size(); ++k) {
@@ -1761,6 +1824,7 @@ int Ctx::run_markov_chain(const hdpm_chain_params* p, const int32_t* c_init, int
 // ====================================================================== C ABI
 using hdpm::Ctx;
 using hdpm::HipError;
+using hdpm::ScopedPin;
 
 #define GUARD(body)                                                            \
   try {                                                                        \
@@ -1887,10 +1951,12 @@ int hdpm_generate_pool(hdpm_ctx* h, int64_t P) {
 }
 int hdpm_neal8_sweep(hdpm_ctx* h, int32_t m) {
   CTX();
+  ScopedPin pin;
   GUARD(return ctx->neal8_sweep(m);)
 }
 int hdpm_update_phi(hdpm_ctx* h, const int32_t* idx, int32_t n_idx) {
   CTX();
+  ScopedPin pin;
   if (n_idx > 0 && !idx) return HDPM_E_ARG;
   GUARD(return ctx->update_phi(idx, n_idx);)
 }
@@ -1914,6 +1980,7 @@ int hdpm_logprobgs_c_i(hdpm_ctx* h, const int32_t* g_c_i, const int32_t* S, int3
 }
 int hdpm_split_and_merge(hdpm_ctx* h, int32_t t, int32_t r, int32_t idx_1_sm, int32_t* accepted) {
   CTX();
+  ScopedPin pin;
   int acc = 0;
   int st;
   GUARD(st = ctx->split_and_merge(t, r, idx_1_sm, &acc);)
@@ -1925,11 +1992,13 @@ int hdpm_run_markov_chain(hdpm_ctx* h, const hdpm_chain_params* p, const int32_t
                           double* out_time_s) {
   CTX();
   if (!p) return HDPM_E_ARG;
+  ScopedPin pin;
   GUARD(return ctx->run_markov_chain(p, c_i_init, out_total_cls, out_c_i, out_loglik, out_accepted, final_ass,
                                      out_time_s);)
 }
 int hdpm_init_chain(hdpm_ctx* h, const hdpm_chain_params* p, const int32_t* c_i_init) {
   CTX();
+  ScopedPin pin;
   if (!p) return HDPM_E_ARG;
   GUARD(return ctx->init_chain(p, c_i_init);)
 }
@@ -1937,6 +2006,7 @@ int hdpm_iteration(hdpm_ctx* h, const hdpm_chain_params* p, int32_t iter, int32_
                    double* loglik) {
   CTX();
   if (!p || !idx_1_sm) return HDPM_E_ARG;
+  ScopedPin pin;
   int acc = 0;
   double ll = 0.0;
   int st;
