@@ -36,12 +36,13 @@ hipError_t launch_cluster_summary(const PrepassArgs& a, hipStream_t s);
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s);
 hipError_t launch_exact_rows(const PrepassArgs& a, int nblocks, hipStream_t s);
 size_t resolve_smem_bytes(int scap, int m);
-hipError_t launch_relabel(int* c, const int* los, int n, hipStream_t s);
-hipError_t launch_finish_sweep(int* counts, int* sol, int* los, int* src, int K, int nslots, hipStream_t s);
-hipError_t launch_apply_moves(const int* mlog, const int* mcount, int nmoves, const uint8_t* codes_t, int d, int nq,
-                              int mmax, unsigned int* freq, hipStream_t s);
-hipError_t launch_freq_gather(const unsigned int* freq, const int* sol, int K, int fs, unsigned int* out,
-                              hipStream_t s);
+hipError_t launch_relabel(int* c, const int* los, int n, const ResolveCtl* ctl, hipStream_t s);
+hipError_t launch_finish_sweep(int* counts, int* sol, int* los, int* src, int cap, const ResolveCtl* ctl, int n,
+                               hipStream_t s);
+hipError_t launch_apply_moves(const int* mlog, const int* mcount, int grid, const uint8_t* codes_t, int d, int nq,
+                              int mmax, unsigned int* freq, const ResolveCtl* ctl, int n, hipStream_t s);
+hipError_t launch_freq_gather(const unsigned int* freq, const int* sol, int Kmax, int fs, unsigned int* out,
+                              const ResolveCtl* ctl, int n, hipStream_t s);
 hipError_t launch_scatter_clusters(const uint8_t* stage, int nent, int dp, int d, int bw, int full, uint8_t* codes,
                                    double* tab, uint64_t* bnd, int* counts, int* sol, int* los, int* src,
                                    hipStream_t s);
@@ -488,6 +489,7 @@ struct Ctx {
   // takes masked (subset) histograms.
   DevBuf<unsigned> d_freq, d_freq2, d_freq_m;
   bool freq_dev_valid = false;
+  uint64_t freq_d2h_version = 0;      // labels_version whose freq copy the sweep already started
   DevBuf<int> d_mlog, d_mcount;
   PinBuf<unsigned> h_freq;
   DevBuf<unsigned char> d_mask;
@@ -1090,7 +1092,6 @@ struct Ctx {
     int p = 0;
     const double dmax = 0.25;
     const int64_t rounds0 = stats.rounds;
-    const int64_t moves0 = stats.moves;
     const bool track = freq_dev_valid;
     if (track) {
       d_mlog.ensure((size_t)3 * n);
@@ -1156,10 +1157,25 @@ struct Ctx {
       HIPCHK(launch_resolve(ra, stream));
       HIPCHK(hipEventRecord(ev[2], stream));
       HIPCHK(hipMemcpyAsync(h_ctl.p, d_ctl.p, (8 + 3 * (size_t)scap) * 4, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipEventRecord(ev[6], stream));
+      {
+        // the sweep end, enqueued now: it runs only if this launch completes the sweep
+        const ResolveCtl* dctl = (const ResolveCtl*)d_ctl.p;
+        HIPCHK(launch_relabel(d_c.p, d_los.p, n, dctl, stream));
+        if (track) {   // carry the frequency tables: apply the moves, re-index slots -> labels
+          HIPCHK(launch_apply_moves(d_mlog.p, d_mcount.p, (int)std::min<int64_t>(n, 4096), d_codes_t.p, d, nq, mmax,
+                                    d_freq.p, dctl, n, stream));
+          HIPCHK(launch_freq_gather(d_freq.p, d_sol.p, std::min(scap, S + 2), d * mmax, d_freq2.p, dctl, n, stream));
+          const size_t fwords = (size_t)std::min(scap, S + 2) * d * mmax;
+          h_freq.ensure(fwords);
+          HIPCHK(hipMemcpyAsync(h_freq.p, d_freq2.p, fwords * 4, hipMemcpyDeviceToHost, stream));
+        }
+        HIPCHK(launch_finish_sweep(d_counts.p, d_sol.p, d_los.p, d_src.p, scap, dctl, n, stream));
+      }
       mark("launched");
       if (stats.rounds == rounds0) prefill_phi_stream();   // hidden behind the device work
       mark("prefill");
-      HIPCHK(hipStreamSynchronize(stream));
+      HIPCHK(hipEventSynchronize(ev[6]));
       mark("resolved");
       float t1 = 0, t2 = 0, t3 = 0;
       HIPCHK(hipEventElapsedTime(&t1, ev[0], ev[1]));
@@ -1202,15 +1218,11 @@ struct Ctx {
     const int* sol = h_ctl.p + 8;
     const int* cnt = sol + scap;
     const int* src = cnt + scap;
-    HIPCHK(launch_relabel(d_c.p, d_los.p, n, stream));
-    if (track) {   // carry the frequency tables: apply the moves, then re-index slots -> labels
-      HIPCHK(launch_apply_moves(d_mlog.p, d_mcount.p, (int)std::min<int64_t>(stats.moves - moves0, n), d_codes_t.p, d,
-                                nq, mmax, d_freq.p, stream));
-      HIPCHK(launch_freq_gather(d_freq.p, d_sol.p, K, d * mmax, d_freq2.p, stream));
+    if (track) {   // the gather of the final launch wrote freq2 (and its copy is on its way)
       std::swap(d_freq.p, d_freq2.p);
       std::swap(d_freq.n, d_freq2.n);
+      freq_d2h_version = labels_version;
     }
-    HIPCHK(launch_finish_sweep(d_counts.p, d_sol.p, d_los.p, d_src.p, K, nslots, stream));
     h_center.assign((size_t)K * d, 0);
     h_sigma.assign((size_t)K * d, 0.0);
     h_counts.assign(K, 0);
@@ -1247,8 +1259,10 @@ struct Ctx {
     const size_t nent = (size_t)K * d * mmax;
     h_freq.ensure(std::max<size_t>(nent, 1));
     if (!mask && freq_dev_valid && !(debug & 16)) {
-      // the per-label tables were carried through the sweep by the move log
-      HIPCHK(hipMemcpyAsync(h_freq.p, d_freq.p, nent * 4, hipMemcpyDeviceToHost, stream));
+      // the per-label tables were carried through the sweep by the move log (and usually
+      // copied out behind it already)
+      if (freq_d2h_version != labels_version)
+        HIPCHK(hipMemcpyAsync(h_freq.p, d_freq.p, nent * 4, hipMemcpyDeviceToHost, stream));
       return;
     }
     DevBuf<unsigned>& dst = mask ? d_freq_m : d_freq;

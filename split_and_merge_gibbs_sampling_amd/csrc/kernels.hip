@@ -1087,7 +1087,15 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
 }
 
 // ------------------------------------------------------------------ end of sweep
-__global__ void k_relabel(int* c, const int* label_of_slot, int n) {
+// The sweep-end kernels are enqueued behind every resolver launch and read its control
+// block: they act only when that launch finished the sweep (no restart pending), so the
+// host need not wait for the resolver before issuing them.
+__device__ __forceinline__ bool sweep_done(const ResolveCtl* ctl, int n) {
+  return ctl->status == 0 && ctl->restart == 0 && ctl->next >= n;
+}
+
+__global__ void k_relabel(int* c, const int* label_of_slot, int n, const ResolveCtl* ctl) {
+  if (!sweep_done(ctl, n)) return;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) c[i] = label_of_slot[c[i]];
 }
@@ -1097,7 +1105,8 @@ __global__ void k_relabel(int* c, const int* label_of_slot, int n) {
 // attributes).  Equivalent to recounting, at the cost of the moves.
 __global__ __launch_bounds__(kWave) void k_apply_moves(const int* __restrict__ mlog, const int* __restrict__ mcount,
                                                       const uint8_t* __restrict__ codes_t, int d, int nq, int mmax,
-                                                      unsigned int* freq) {
+                                                      unsigned int* freq, const ResolveCtl* ctl, int n) {
+  if (!sweep_done(ctl, n)) return;
   const int nm = *mcount;
   const int fs = d * mmax;
   for (int q = blockIdx.x; q < nm; q += gridDim.x) {
@@ -1112,8 +1121,10 @@ __global__ __launch_bounds__(kWave) void k_apply_moves(const int* __restrict__ m
 }
 
 // freq per label after the sweep: out[l] = freq[slot_of_label[l]].
-__global__ void k_freq_gather(const unsigned int* __restrict__ freq, const int* __restrict__ sol, int K, int fs,
-                              unsigned int* __restrict__ out) {
+__global__ void k_freq_gather(const unsigned int* __restrict__ freq, const int* __restrict__ sol, int fs,
+                              unsigned int* __restrict__ out, const ResolveCtl* ctl, int n) {
+  if (!sweep_done(ctl, n)) return;
+  const int K = ctl->K;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < (int64_t)K * fs;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int l = (int)(e / fs);
@@ -1122,8 +1133,10 @@ __global__ void k_freq_gather(const unsigned int* __restrict__ freq, const int* 
 }
 
 // After k_relabel: counts per label, identity slot maps (slot == label again).  One block.
-__global__ __launch_bounds__(1024) void k_finish_sweep(int* counts, int* sol, int* los, int* src, int K,
-                                                      int nslots) {
+__global__ __launch_bounds__(1024) void k_finish_sweep(int* counts, int* sol, int* los, int* src,
+                                                      const ResolveCtl* ctl, int n) {
+  if (!sweep_done(ctl, n)) return;
+  const int K = ctl->K, nslots = ctl->nslots;
   extern __shared__ int fs[];
   int* c = fs;            // [nslots]
   int* m = fs + nslots;   // [K]
@@ -1369,31 +1382,29 @@ hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_relabel(int* c, const int* los, int n, hipStream_t s) {
-  hipLaunchKernelGGL(k_relabel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, c, los, n);
+hipError_t launch_relabel(int* c, const int* los, int n, const ResolveCtl* ctl, hipStream_t s) {
+  hipLaunchKernelGGL(k_relabel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, c, los, n, ctl);
   return hipGetLastError();
 }
 
-hipError_t launch_apply_moves(const int* mlog, const int* mcount, int nmoves, const uint8_t* codes_t, int d, int nq,
-                              int mmax, unsigned int* freq, hipStream_t s) {
-  if (nmoves <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_apply_moves, dim3(std::min(nmoves, 4096)), dim3(kWave), 0, s, mlog, mcount, codes_t, d, nq, mmax,
-                     freq);
+hipError_t launch_apply_moves(const int* mlog, const int* mcount, int grid, const uint8_t* codes_t, int d, int nq,
+                              int mmax, unsigned int* freq, const ResolveCtl* ctl, int n, hipStream_t s) {
+  hipLaunchKernelGGL(k_apply_moves, dim3(std::max(1, std::min(grid, 4096))), dim3(kWave), 0, s, mlog, mcount, codes_t,
+                     d, nq, mmax, freq, ctl, n);
   return hipGetLastError();
 }
 
-hipError_t launch_freq_gather(const unsigned int* freq, const int* sol, int K, int fs, unsigned int* out,
-                              hipStream_t s) {
-  const int64_t work = (int64_t)K * fs;
-  if (work <= 0) return hipSuccess;
+hipError_t launch_freq_gather(const unsigned int* freq, const int* sol, int Kmax, int fs, unsigned int* out,
+                              const ResolveCtl* ctl, int n, hipStream_t s) {
+  const int64_t work = (int64_t)std::max(Kmax, 1) * fs;
   hipLaunchKernelGGL(k_freq_gather, dim3((unsigned)std::min<int64_t>(1024, (work + 255) / 256)), dim3(256), 0, s, freq,
-                     sol, K, fs, out);
+                     sol, fs, out, ctl, n);
   return hipGetLastError();
 }
 
-hipError_t launch_finish_sweep(int* counts, int* sol, int* los, int* src, int K, int nslots, hipStream_t s) {
-  hipLaunchKernelGGL(k_finish_sweep, dim3(1), dim3(1024), (size_t)(nslots + K) * 4, s, counts, sol, los, src, K,
-                     nslots);
+hipError_t launch_finish_sweep(int* counts, int* sol, int* los, int* src, int cap, const ResolveCtl* ctl, int n,
+                               hipStream_t s) {
+  hipLaunchKernelGGL(k_finish_sweep, dim3(1), dim3(1024), (size_t)(2 * cap) * 4, s, counts, sol, los, src, ctl, n);
   return hipGetLastError();
 }
 
