@@ -152,6 +152,8 @@ def main():
     ap.add_argument("--config", default="c5")
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--m", type=int, default=3)
+    ap.add_argument("--sm", action="store_true",
+                    help="include the split-merge move in every step (t = r = 10, la:111-115)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-csv", action="append", default=None,
@@ -170,7 +172,7 @@ def main():
     eng.set_data(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w)
     eng.set_seed(1 + rank)
     params = eng.chain_params(m=args.m, iterations=args.steps + args.warmup, L=0, burnin=0, neal8=True,
-                              split_merge=False)
+                              split_merge=args.sm, t=10, r=10)
     eng.init_chain(params, c_i=ds.truth)         # la:27-77, L = 0 (ground truth) path
     setup_s = time.perf_counter() - t_setup
     it = 1                                       # iteration 0 regenerates the pool (la:123); start at 1
@@ -223,7 +225,8 @@ def main():
         "data": "synthetic (data_generation.R model, numpy draws); R-compatible MT19937 chain stream",
         "config": {
             "workload": (f"{args.config}: {CONFIGS.get(args.config, {}).get('name', args.config)}, N={ds.n} D={ds.d} "
-                         f"m={args.m}; one step = Neal-8 sweep + update_phi + compute_loglikelihood "
+                         f"m={args.m}; one step = Neal-8 sweep + update_phi"
+                         f"{' + split-merge (t=r=10)' if args.sm else ''} + compute_loglikelihood "
                          f"(code/launcher.cpp:94-132), ground-truth init"),
             "n": ds.n, "d": ds.d, "m": args.m, "K_final": K, "parallelism": f"replicas{ws}",
             "sweep_effective_GBps": round(survey_sweep_bytes(ds.n, ds.d, args.m) * args.steps / elapsed / 1e9, 2),
@@ -232,6 +235,7 @@ def main():
                                       ("t_prepass_ms", "t_exact_ms", "t_resolve_ms", "t_stats_ms", "t_host_phi_ms",
                                        "t_rng_ms", "t_loglik_ms")},
             "exact_points_per_step": st["exact_points"] / args.steps,
+            "split_merge": bool(args.sm),
             "rounds_per_step": st["rounds"] / args.steps,
         },
         "roofline": {

@@ -19,3 +19,17 @@ def test_stream_ahead_and_split_rbeta(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert "host rng ok" in r.stdout
+
+
+def test_glibc_exp_log_replicas_match_libm(tmp_path):
+    """csrc/glibc_math.hpp (used by the device pool generator) equals the host libm's exp and
+    log bit for bit: special values, the generator's argument shapes, random bit patterns."""
+    exe = tmp_path / "glibc_math_test"
+    src = os.path.join(HERE, "cpp", "glibc_math_test.cpp")
+    r = subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-o", str(exe), src],
+                       capture_output=True, text=True)
+    if r.returncode != 0:
+        pytest.fail(r.stderr)
+    r = subprocess.run([str(exe), "1500000"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 exp mismatches, 0 log mismatches" in r.stdout
