@@ -154,6 +154,8 @@ def main():
     ap.add_argument("--m", type=int, default=3)
     ap.add_argument("--sm", action="store_true",
                     help="include the split-merge move in every step (t = r = 10, la:111-115)")
+    ap.add_argument("--start-iter", type=int, default=0,
+                    help="first iteration index (0: the warmup includes iteration 0's pool regeneration)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-csv", action="append", default=None,
@@ -171,18 +173,22 @@ def main():
     eng = hd.Engine(local)
     eng.set_data(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w)
     eng.set_seed(1 + rank)
+    if os.environ.get("HDPM_BENCH_HOST_POOL"):
+        eng.set_debug(64)                        # sequential host pool generator (A/B runs)
     params = eng.chain_params(m=args.m, iterations=args.steps + args.warmup, L=0, burnin=0, neal8=True,
                               split_merge=args.sm, t=10, r=10)
     eng.init_chain(params, c_i=ds.truth)         # la:27-77, L = 0 (ground truth) path
     setup_s = time.perf_counter() - t_setup
-    it = 1                                       # iteration 0 regenerates the pool (la:123); start at 1
+    st_init = eng.stats()
+    it = args.start_iter                         # iteration 0 regenerates the pool (la:123-129)
     for _ in range(args.warmup):
         eng.iteration(it)
         it += 1
     eng.synchronize()
+    st0 = eng.stats()                            # + iteration 0's regeneration
     eng.reset_stats()
     if os.environ.get("HDPM_BENCH_TIMELINE"):
-        eng.set_debug(32)                        # host timeline of the timed iterations (stderr)
+        eng.set_debug(32 | (64 if os.environ.get("HDPM_BENCH_HOST_POOL") else 0))                        # host timeline of the timed iterations (stderr)
     D.barrier()
     cuda_sync()
     t0 = time.perf_counter()
@@ -237,6 +243,8 @@ def main():
             "exact_points_per_step": st["exact_points"] / args.steps,
             "split_merge": bool(args.sm),
             "rounds_per_step": st["rounds"] / args.steps,
+            "pool_generation": {"init": pool_report(st_init, ds.n * args.m),
+                                "regeneration": pool_report(stats_diff(st0, st_init), ds.n * args.m)},
         },
         "roofline": {
             "bound": "hbm",
@@ -258,6 +266,26 @@ def main():
         print(json.dumps(out), flush=True)
     eng.close()
     D.close()
+
+
+def stats_diff(a, b):
+    return {k: a[k] - b[k] for k in a}
+
+
+def pool_report(st, P):
+    """Latent pool generation (la:74-77 in init_chain; regenerated at iteration 0 and every
+    1000 iterations, la:123-129) as timed by the engine: wall ms per call, its phases, and
+    the cost per iteration amortised over the 1000-iteration cadence."""
+    calls = int(st["pool_calls"])
+    if calls == 0:
+        return None
+    ms = st["t_pool_ms"] / calls
+    return {
+        "entries": P, "device": st["pool_device_calls"] == calls, "ms_per_call": round(ms, 2),
+        "phases_ms": {k[7:-3]: round(st[k] / calls, 2) for k in
+                      ("t_pool_mt_ms", "t_pool_accept_ms", "t_pool_parse_ms", "t_pool_values_ms")},
+        "amortised_ms_per_iteration": round(ms / 1000, 4),
+    }
 
 
 def traffic_from_csv(*paths):

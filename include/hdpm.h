@@ -48,6 +48,10 @@ typedef struct {
 typedef struct {
     int64_t sweeps, rounds, restarts, exact_points, moves, checked_rounds, prepass_points;
     double  t_prepass_ms, t_resolve_ms, t_stats_ms, t_host_phi_ms, t_rng_ms, t_loglik_ms, t_exact_ms;
+    /* latent pool generation (la:74-77, 124-128): calls, entries, wall time, and for the
+     * device generator its phases: stream slice, attempt tables, host walk, values */
+    int64_t pool_calls, pool_entries, pool_device_calls;
+    double  t_pool_ms, t_pool_mt_ms, t_pool_accept_ms, t_pool_parse_ms, t_pool_values_ms;
 } hdpm_stats;
 
 int         hdpm_device_count(void);
@@ -126,7 +130,9 @@ int hdpm_reset_stats(hdpm_ctx* ctx);
  * certainty shortcut); bit 1: print per-phase timings to stderr; bit 2: compute the
  * log-likelihood with the per-point kernel (no regrouping into match counts); bit 3: no
  * snapshot speculation (the resolver decides every uncertain point itself); bit 4: recount
- * the frequency tables every update_phi (no incremental move log). */
+ * the frequency tables every update_phi (no incremental move log); bit 5: accumulate a host
+ * timeline of hdpm_iteration (printed to stderr when the context is destroyed); bit 6:
+ * generate latent pools with the sequential host generator instead of the device one. */
 int hdpm_set_debug(hdpm_ctx* ctx, int32_t mode);
 /* Block until all device work of the context is done. */
 int hdpm_synchronize(hdpm_ctx* ctx);

@@ -46,7 +46,10 @@ class Stats(C.Structure):
         "sweeps", "rounds", "restarts", "exact_points", "moves", "checked_rounds", "prepass_points")] + \
         [(n, C.c_double) for n in (
             "t_prepass_ms", "t_resolve_ms", "t_stats_ms", "t_host_phi_ms", "t_rng_ms", "t_loglik_ms",
-            "t_exact_ms")]
+            "t_exact_ms")] + \
+        [(n, C.c_int64) for n in ("pool_calls", "pool_entries", "pool_device_calls")] + \
+        [(n, C.c_double) for n in (
+            "t_pool_ms", "t_pool_mt_ms", "t_pool_accept_ms", "t_pool_parse_ms", "t_pool_values_ms")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

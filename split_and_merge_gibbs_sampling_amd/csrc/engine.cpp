@@ -27,6 +27,7 @@
 #include "../../include/hdpm.h"
 #include "kernels.hpp"
 #include "mtjump.hpp"
+#include "pool_host.hpp"
 #include "rmath.hpp"
 
 namespace hdpm {
@@ -460,11 +461,35 @@ struct Ctx {
 
   // latent pool
   int64_t P = 0;
-  std::vector<uint8_t> h_pool_c;      // P x d codes
+  std::vector<uint8_t> h_pool_c;      // P x d codes (host-generated or user pools)
   std::vector<double> h_pool_s;       // P x d
+  bool pool_on_device = false;        // device-generated: the parameters live in d_pool_*
   DevBuf<uint8_t> d_pool_codes;
   DevBuf<double> d_pool_tab;
   DevBuf<uint64_t> d_pool_bnd;
+  DevBuf<double> d_pool_sig;          // P x d sigma (device generator)
+
+  // stream-exact device pool generator (pool_gen.hpp)
+  struct PoolGen {
+    PoolPlan plan;
+    bool planned = false;
+    int G = 0, bpg = 0;               // jump tables for the slice generator
+    DevBuf<uint64_t> jpoly;
+    DevBuf<uint32_t> jidx;
+    DevBuf<int> joff;
+    DevBuf<uint32_t> init, raw;
+    PinBuf<uint32_t> h_init, h_tail;
+    DevBuf<uint64_t> bm;
+    PinBuf<uint64_t> h_bm;
+    DevBuf<int64_t> starts;
+    PinBuf<int64_t> h_starts;
+    DevBuf<PoolClass> cls;
+    DevBuf<int> runs;
+    DevBuf<int32_t> att;
+    DevBuf<uint64_t> gtab;
+    DevBuf<int> err;
+    PinBuf<int> h_err;
+  } pg;
 
   // sweep scratch
   PinBuf<uint32_t> h_raw;
@@ -653,30 +678,54 @@ struct Ctx {
     if (mt_G == G && count <= (int64_t)624 * G * mt_bpg) return;
     // headroom so later, slightly larger windows (sweep + draws between sweeps) reuse it
     const int bpg = (int)((count * 5 / 4 + 624 * G - 1) / (624 * G));
+    HIPCHK(hipStreamSynchronize(gstream));   // no generator may still read the tables
+    if (!build_jump(d_jpoly, d_jidx, d_joff, G, bpg)) return;
+    mt_G = G;
+    mt_bpg = bpg;
+  }
+
+  // Tables of z^(624 bpg g - 1) mod phi, g = 1..G-1 (set-bit lists for the generator's
+  // correlation), the chain split over host threads (one exponentiation per thread, then
+  // multiplications by z^(624 bpg)); checked against direct twisting for segments 1 and 2
+  // (and G/2, G-1 when that is cheap).
+  bool build_jump(DevBuf<uint64_t>& jpoly, DevBuf<uint32_t>& jidx, DevBuf<int>& joff, int G, int bpg) {
     static const Poly phi = mt_charpoly();
-    if (phi.empty()) return;
-    const Poly pj = poly_xpow((uint64_t)624 * bpg, phi);
+    if (phi.empty()) return false;
+    const uint64_t J = (uint64_t)624 * bpg;
+    const Poly pj = poly_xpow(J, phi);
     std::vector<uint64_t> all((size_t)G * 312, 0);
-    Poly p = poly_xpow((uint64_t)624 * bpg - 1, phi);   // z^(gJ - 1), g = 1..G-1
-    for (int g = 1; g < G; ++g) {
-      std::memcpy(&all[(size_t)g * 312], p.data(), 312 * 8);
-      if (g + 1 < G) p = poly_mulmod(p, pj, phi);
+    const int T = std::max(1, std::min(host_threads(), (G - 1) / 8));
+    const int per = (G - 1 + T - 1) / T;
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t) {
+      const int g0 = 1 + t * per, g1 = std::min(G, g0 + per);
+      if (g0 >= g1) break;
+      th.emplace_back([&, g0, g1] {
+        Poly p = poly_xpow(J * g0 - 1, phi);
+        for (int g = g0; g < g1; ++g) {
+          std::memcpy(&all[(size_t)g * 312], p.data(), 312 * 8);
+          if (g + 1 < g1) p = poly_mulmod(p, pj, phi);
+        }
+      });
     }
-    {  // self-check on the host: jumps by 1, G/2 and G-1 segments == direct twisting
+    for (auto& x : th) x.join();
+    {
       Rng r;
       r.set_seed(20241015u);
       (void)r.raw();
       Rng q = r;
-      int done = 0;
-      for (int g : {1, G / 2, G - 1}) {
+      int64_t done = 0;
+      std::vector<int> segs{1, std::min(2, G - 1)};
+      if ((int64_t)(G - 1) * bpg <= 20000) segs.insert(segs.end(), {G / 2, G - 1});
+      std::sort(segs.begin(), segs.end());
+      for (int g : segs) {
         uint32_t jumped[624];
         Poly pg(all.begin() + (size_t)g * 312, all.begin() + (size_t)(g + 1) * 312);
         mt_jump_host(r.mt, pg, jumped);
-        for (; done < g * bpg; ++done) q.twist();
-        if (std::memcmp(jumped, q.mt, sizeof(jumped)) != 0) return;
+        for (; done < (int64_t)g * bpg; ++done) q.twist();
+        if (std::memcmp(jumped, q.mt, sizeof(jumped)) != 0) return false;
       }
     }
-    // set-bit lists of the polynomials (the generator's correlation walks these)
     std::vector<int> off(G + 1, 0);
     std::vector<uint32_t> idx;
     for (int g = 0; g < G; ++g) {
@@ -686,15 +735,13 @@ struct Ctx {
           if ((all[(size_t)g * 312 + (i >> 6)] >> (i & 63)) & 1u) idx.push_back((uint32_t)i);
     }
     off[G] = (int)idx.size();
-    HIPCHK(hipStreamSynchronize(gstream));   // no generator may still read d_jpoly
-    d_jpoly.ensure(all.size());
-    HIPCHK(hipMemcpy(d_jpoly.p, all.data(), all.size() * 8, hipMemcpyHostToDevice));
-    d_jidx.ensure(std::max<size_t>(idx.size(), 1));
-    HIPCHK(hipMemcpy(d_jidx.p, idx.data(), idx.size() * 4, hipMemcpyHostToDevice));
-    d_joff.ensure(off.size());
-    HIPCHK(hipMemcpy(d_joff.p, off.data(), off.size() * 4, hipMemcpyHostToDevice));
-    mt_G = G;
-    mt_bpg = bpg;
+    jpoly.ensure(all.size());
+    HIPCHK(hipMemcpy(jpoly.p, all.data(), all.size() * 8, hipMemcpyHostToDevice));
+    jidx.ensure(std::max<size_t>(idx.size(), 1));
+    HIPCHK(hipMemcpy(jidx.p, idx.data(), idx.size() * 4, hipMemcpyHostToDevice));
+    joff.ensure(off.size());
+    HIPCHK(hipMemcpy(joff.p, off.data(), off.size() * 4, hipMemcpyHostToDevice));
+    return true;
   }
 
   bool covers(const RngWindow& W, uint64_t p, int64_t n) const {
@@ -912,6 +959,7 @@ struct Ctx {
       if (x[i] < 1 || x[i] > attr[j]) { err = "codes must lie in 1..attrisize[j]"; return kArg; }
     }
     n = n_; d = d_; nq = (d + 15) / 16; dp = nq * 16; gamma = g;
+    pg.planned = false;
     att.assign(attr, attr + d);
     v.assign(vv, vv + d);
     w.assign(ww, ww + d);
@@ -1021,6 +1069,7 @@ struct Ctx {
     if (!n) { err = "set_data first"; return kArg; }
     if (P_ <= 0 || P_ > 0x7fffffff) { err = "pool size must be in 1..2^31-1"; return kArg; }
     P = P_;
+    pool_on_device = false;
     h_pool_c.resize((size_t)P * d);
     h_pool_s.assign(sig, sig + (size_t)P * d);
     for (size_t q = 0; q < (size_t)P * d; ++q) h_pool_c[q] = (uint8_t)(int)cen[q];
@@ -1029,11 +1078,25 @@ struct Ctx {
   }
 
   // la:74-77 / la:124-128: per entry D centers then D sigmas, from the context stream.
+  // The device generator (pool_gen.hpp) when the attributes qualify and the host libm is
+  // the one glibc_math.hpp reproduces; the sequential host generator otherwise (or with
+  // debug bit 6).  Both leave the same pool and the same stream position.
   int generate_pool(int64_t P_) {
     if (!n) { err = "set_data first"; return kArg; }
     if (P_ <= 0 || P_ > 0x7fffffff) { err = "pool size must be in 1..2^31-1"; return kArg; }
     auto t0 = std::chrono::steady_clock::now();
+    int st = -1;
+    if (!(debug & 64) && glibc_selfcheck()) st = generate_pool_device(P_);
+    if (st < 0) st = generate_pool_host(P_);
+    stats.pool_calls++;
+    stats.pool_entries += P_;
+    stats.t_pool_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return st;
+  }
+
+  int generate_pool_host(int64_t P_) {
     P = P_;
+    pool_on_device = false;
     h_pool_c.resize((size_t)P * d);
     h_pool_s.resize((size_t)P * d);
     for (int64_t e = 0; e < P; ++e) {
@@ -1042,8 +1105,196 @@ struct Ctx {
       if (st) { err = "rhig failed in pool generation"; return st; }
     }
     upload_pool();
-    stats.t_rng_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return kOk;
+  }
+
+  // The replicas of exp/log must equal this host's libm (they are the device's only way to
+  // round like the reference); checked once per process.
+  static bool glibc_selfcheck() {
+    static const bool ok = [] {
+      Rng r;
+      r.set_seed(424242u);
+      for (int k = 0; k < 200000; ++k) {
+        const double u = r.unif();
+        const double xs[4] = {u, u / (1.0 - u), 80.0 * u - 40.0, 0.9 + 0.2 * u};
+        for (double x : xs) {
+          const double a = std::exp(x), b = glibc::exp_h(x), c = std::log(x), e = glibc::log_h(x);
+          if (std::memcmp(&a, &b, 8) != 0 || std::memcmp(&c, &e, 8) != 0) return false;
+        }
+      }
+      return true;
+    }();
+    return ok;
+  }
+
+  // Returns -1 when the device generator does not apply (the caller falls back).
+  int generate_pool_device(int64_t P_) {
+    using clk = std::chrono::steady_clock;
+    auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    if (!pg.planned) {
+      pg.plan = pool_plan(d, att.data(), v.data(), w.data());
+      pg.planned = true;
+      if (pg.plan.ok) {
+        const auto& pl = pg.plan;
+        pg.cls.ensure(pl.cls.size());
+        HIPCHK(hipMemcpy(pg.cls.p, pl.cls.data(), pl.cls.size() * sizeof(PoolClass), hipMemcpyHostToDevice));
+        std::vector<int> runs(pl.run_cls);
+        runs.insert(runs.end(), pl.run_len.begin(), pl.run_len.end());
+        pg.runs.ensure(runs.size());
+        HIPCHK(hipMemcpy(pg.runs.p, runs.data(), runs.size() * 4, hipMemcpyHostToDevice));
+        pg.att.ensure(d);
+        HIPCHK(hipMemcpy(pg.att.p, att.data(), (size_t)d * 4, hipMemcpyHostToDevice));
+        pg.gtab.ensure(512);
+        HIPCHK(hipMemcpy(pg.gtab.p, glibc::kGlibcExpTab, 256 * 8, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(pg.gtab.p + 256, glibc::kGlibcLogTab, 256 * 8, hipMemcpyHostToDevice));
+        pg.err.ensure(1);
+        pg.h_err.ensure(1);
+      }
+    }
+    if (!pg.plan.ok) return -1;
+    const PoolPlan& pl = pg.plan;
+    const int nc = (int)pl.cls.size();
+
+    rng_sync();
+    if (rng.mti == 625) {   // never seeded: R's MT_sgenrand(4357) on the first draw
+      uint32_t seed = 4357;
+      for (int i = 0; i < 624; i++) {
+        rng.mt[i] = seed & 0xffff0000u;
+        seed = 69069u * seed + 1u;
+        rng.mt[i] |= (seed & 0xffff0000u) >> 16;
+        seed = 69069u * seed + 1u;
+      }
+      rng.mti = 624;
+    }
+    const int mti0 = rng.mti;
+    const int64_t head = mti0 >= 624 ? 0 : 624 - mti0;
+    pg.h_init.ensure(624);
+    pg.init.ensure(624);
+    std::memcpy(pg.h_init.p, rng.mt, sizeof(rng.mt));
+    // the pool's old arrays may still be read by queued kernels: all work is on `stream`
+    HIPCHK(hipMemcpyAsync(pg.init.p, pg.h_init.p, 624 * 4, hipMemcpyHostToDevice, stream));
+
+    for (int attempt = 0; attempt < 3; ++attempt) {
+      auto t0 = clk::now();
+      const int64_t count = pool_slice_len(pl, P_, 1.0 + 0.25 * attempt) + 624;
+      // slice generator: 256 workgroups with their own jump tables, or one for short slices
+      const int G = 256;
+      const bool multi = count >= (int64_t)G * 624 * 8;
+      if (multi && (pg.G != G || count + head > (int64_t)624 * G * pg.bpg)) {
+        const int bpg = (int)((count * 9 / 8 + 624 * G - 1) / (624 * G));
+        if (!build_jump(pg.jpoly, pg.jidx, pg.joff, G, bpg)) return -1;
+        pg.G = G;
+        pg.bpg = bpg;
+      }
+      pg.raw.ensure(count);
+      const int nblocks = count > head ? (int)((count - head + 623) / 624) : 0;
+      MtGenArgs ma{pg.init.p, mti0, count, pg.raw.p, nullptr, nblocks, 0x7fffffff,
+                   multi ? pg.jpoly.p : nullptr, pg.jidx.p, pg.joff.p, pg.bpg, multi ? G : 1};
+      HIPCHK(launch_mt_gen(ma, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+      auto tm = clk::now();
+
+      const int64_t nwords = (count + 127) / 128;
+      pg.bm.ensure((size_t)nc * 2 * nwords);
+      PoolAcceptArgs aa{pg.raw.p, count, nc, pg.cls.p, pg.bm.p, nwords, pg.gtab.p};
+      HIPCHK(launch_pool_accept(aa, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+      auto t1 = clk::now();
+      pg.h_bm.ensure((size_t)nc * 2 * nwords);
+      HIPCHK(hipMemcpyAsync(pg.h_bm.p, pg.bm.p, (size_t)nc * 2 * nwords * 8, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+
+      pg.h_starts.ensure(P_ + 1);
+      PoolRuns R{(int)pl.run_cls.size(), pl.run_cls.data(), pl.run_len.data()};
+      const int64_t end = pool_parse(pg.h_bm.p, nwords, d, R, 0, 0, P_, pg.h_starts.p);
+      auto t2 = clk::now();
+      stats.t_pool_mt_ms += ms(t0, tm);
+      stats.t_pool_accept_ms += ms(tm, t1);
+      stats.t_pool_parse_ms += ms(t1, t2);
+      if (end < 0 || end + 624 > count) continue;      // slice too short: a longer one
+      pg.h_starts.p[P_] = end;
+
+      P = P_;
+      d_pool_codes.ensure((size_t)P * dp);
+      d_pool_tab.ensure((size_t)P * 2 * d);
+      d_pool_bnd.ensure((size_t)P * bw);
+      d_pool_sig.ensure((size_t)P * d);
+      pg.starts.ensure(P + 1);
+      HIPCHK(hipMemcpyAsync(pg.starts.p, pg.h_starts.p, (size_t)(P + 1) * 8, hipMemcpyHostToDevice, stream));
+      HIPCHK(hipMemsetAsync(pg.err.p, 0, 4, stream));
+      PoolValueArgs va{pg.raw.p, count, pg.starts.p, P, d, dp, wb, Ws, bw, pg.att.p, (int)pl.run_cls.size(),
+                       pg.runs.p, pg.runs.p + pl.run_cls.size(), pg.cls.p, pg.bm.p, nwords, pg.gtab.p,
+                       d_pool_codes.p, d_pool_tab.p, d_pool_sig.p, d_pool_bnd.p, pg.err.p};
+      HIPCHK(launch_pool_values(va, stream));
+      HIPCHK(hipMemcpyAsync(pg.h_err.p, pg.err.p, 4, hipMemcpyDeviceToHost, stream));
+
+      // the stream continues after `end` draws: mti and the block array (untempered outputs)
+      int64_t blk;
+      int mti;
+      if (end < head) {
+        blk = 0;
+        mti = mti0 + (int)end;
+      } else {
+        const int64_t b = 1 + (end - head) / 624, k = (end - head) % 624;
+        blk = k == 0 ? b - 1 : b;
+        mti = k == 0 ? 624 : (int)k;
+      }
+      pg.h_tail.ensure(624);
+      if (blk > 0)
+        HIPCHK(hipMemcpyAsync(pg.h_tail.p, pg.raw.p + head + (blk - 1) * 624, 624 * 4, hipMemcpyDeviceToHost,
+                              stream));
+      HIPCHK(hipStreamSynchronize(stream));
+      stats.t_pool_values_ms += ms(t2, clk::now());
+      if (*pg.h_err.p) {
+        err = "device pool generator: inconsistent walk";
+        return kDevice;
+      }
+      if (blk > 0)
+        for (int t = 0; t < 624; ++t) rng.mt[t] = mt_untemper(pg.h_tail.p[t]);
+      rng.mti = mti;
+      rng.pos += (uint64_t)end;
+      pool_on_device = true;
+      h_pool_c.clear();
+      h_pool_c.shrink_to_fit();
+      h_pool_s.clear();
+      h_pool_s.shrink_to_fit();
+      stats.pool_device_calls++;
+      return kOk;
+    }
+    return -1;
+  }
+
+  void get_pool(double* centers, double* sigma) {
+    const size_t nn = (size_t)P * d;
+    if (!pool_on_device) {
+      for (size_t q = 0; q < nn; ++q) {
+        if (centers) centers[q] = h_pool_c[q];
+        if (sigma) sigma[q] = h_pool_s[q];
+      }
+      return;
+    }
+    if (centers) {
+      std::vector<uint8_t> c((size_t)P * dp);
+      HIPCHK(hipMemcpyAsync(c.data(), d_pool_codes.p, c.size(), hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+      for (int64_t e = 0; e < P; ++e)
+        for (int j = 0; j < d; ++j) centers[(size_t)e * d + j] = c[(size_t)e * dp + j];
+    }
+    if (sigma) {
+      HIPCHK(hipMemcpyAsync(sigma, d_pool_sig.p, nn * 8, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+    }
+  }
+
+  // Centers and sigmas of pool entry e (device pools are read back on demand).
+  void pool_entry(int64_t e, uint8_t* cen, double* sig) {
+    if (!pool_on_device) {
+      std::memcpy(cen, &h_pool_c[(size_t)e * d], d);
+      std::memcpy(sig, &h_pool_s[(size_t)e * d], (size_t)d * 8);
+      return;
+    }
+    HIPCHK(hipMemcpyAsync(cen, d_pool_codes.p + (size_t)e * dp, d, hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipMemcpyAsync(sig, d_pool_sig.p + (size_t)e * d, (size_t)d * 8, hipMemcpyDeviceToHost, stream));
   }
 
   // ------------------------------------------------------------------ Neal-8 sweep
@@ -1226,21 +1477,19 @@ struct Ctx {
     h_center.assign((size_t)K * d, 0);
     h_sigma.assign((size_t)K * d, 0.0);
     h_counts.assign(K, 0);
+    bool fetched = false;
     for (int l = 0; l < K; ++l) {
       const int s = sol[l];
       h_counts[l] = cnt[s];
-      const uint8_t* cc;
-      const double* ss;
       if (s < K0) {
-        cc = &old_center[(size_t)s * d];
-        ss = &old_sigma[(size_t)s * d];
+        std::memcpy(&h_center[(size_t)l * d], &old_center[(size_t)s * d], d);
+        std::memcpy(&h_sigma[(size_t)l * d], &old_sigma[(size_t)s * d], (size_t)d * 8);
       } else {
-        cc = &h_pool_c[(size_t)src[s] * d];
-        ss = &h_pool_s[(size_t)src[s] * d];
+        pool_entry(src[s], &h_center[(size_t)l * d], &h_sigma[(size_t)l * d]);
+        fetched = true;
       }
-      std::memcpy(&h_center[(size_t)l * d], cc, d);
-      std::memcpy(&h_sigma[(size_t)l * d], ss, (size_t)d * 8);
     }
+    if (fetched && pool_on_device) HIPCHK(hipStreamSynchronize(stream));
     host_c_valid = false;
     tables_dirty = true;
     mark("sweep_end");
@@ -1953,10 +2202,7 @@ int hdpm_set_pool(hdpm_ctx* h, const double* centers, const double* sigma, int64
 int hdpm_get_pool(hdpm_ctx* h, double* centers, double* sigma, int64_t P) {
   CTX();
   if (P != ctx->P) { ctx->err = "pool size mismatch"; return HDPM_E_ARG; }
-  for (size_t q = 0; q < (size_t)P * ctx->d; ++q) {
-    if (centers) centers[q] = ctx->h_pool_c[q];
-    if (sigma) sigma[q] = ctx->h_pool_s[q];
-  }
+  GUARD(ctx->get_pool(centers, sigma);)
   return HDPM_OK;
 }
 int hdpm_generate_pool(hdpm_ctx* h, int64_t P) {

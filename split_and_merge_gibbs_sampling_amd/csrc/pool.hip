@@ -1,0 +1,216 @@
+// pool.hip -- device side of the stream-exact latent-pool generator (pool_gen.hpp).
+//
+//   k_pool_accept  every possible rbeta attempt of the slice, per attribute class, packed
+//                  per position parity (one wave = 128 stream positions, ballots)
+//   k_pool_values  one wave per pool entry: centers, the entry's accepted attempts (wave
+//                  popcount scan + select over the packed words, run by run), sigma and
+//                  dhamming tables, bound record (kernels.hpp layout)
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "kernels.hpp"
+#include "pool_gen.hpp"
+
+namespace hdpm {
+
+namespace {
+
+__device__ __forceinline__ void load_tables(const uint64_t* g, uint64_t* lds) {
+  for (int i = threadIdx.x; i < 512; i += blockDim.x) lds[i] = g[i];
+  __syncthreads();
+}
+
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(v, o);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(256) void k_pool_accept(PoolAcceptArgs a) {
+  __shared__ uint64_t tabs[512];
+  load_tables(a.gtab, tabs);
+  const int lane = threadIdx.x & 63;
+  const int64_t wv = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wv >= a.nwords) return;
+  const int64_t p0 = wv * 128 + 2 * lane;
+  uint32_t y[3] = {0, 0, 0};
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+    if (p0 + k < a.count) y[k] = a.raw[p0 + k];
+  const bool v0 = p0 + 1 < a.count, v1 = p0 + 2 < a.count;
+  const double u0 = pool_unif(y[0]), u1 = pool_unif(y[1]), u2 = pool_unif(y[2]);
+  for (int c = 0; c < a.nclass; ++c) {
+    const PoolClass C = a.cls[c];
+    const bool acc0 = v0 && pool_accept(C, u0, u1, tabs, tabs + 256);
+    const bool acc1 = v1 && pool_accept(C, u1, u2, tabs, tabs + 256);
+    const uint64_t b0 = __ballot(acc0), b1 = __ballot(acc1);
+    if (lane == 0) {
+      a.bm[((int64_t)c * 2 + 0) * a.nwords + wv] = b0;
+      a.bm[((int64_t)c * 2 + 1) * a.nwords + wv] = b1;
+    }
+  }
+}
+
+// dynamic LDS: 512 table words, then per wave d doubles of sigma and 2d of tables
+__global__ __launch_bounds__(256) void k_pool_values(PoolValueArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+  load_tables(a.gtab, lds);
+  const uint64_t* texp = lds;
+  const uint64_t* tlog = lds + 256;
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blockIdx.x * 4 + wid;
+  if (e >= a.P) return;
+  const int d = a.d;
+  double* wsig = reinterpret_cast<double*>(lds + 512) + (size_t)wid * 3 * d;
+  double* wtab = wsig + d;
+  const int64_t s = a.starts[e];
+
+  // centers (common_functions.cpp:198-199): code = (int)(m_j * u + 1)
+  uint8_t* codes = a.codes + e * a.dp;
+  for (int j = lane; j < a.dp; j += 64)
+    codes[j] = j < d ? (uint8_t)(int)(a.att[j] * pool_unif(a.raw[s + j]) + 1) : (uint8_t)0;
+
+  // sigmas: run by run, the run's accepted attempts in stream order
+  int64_t pos = s + d;
+  int j0 = 0;
+  bool bad_attempt = false;
+  for (int r = 0; r < a.nruns; ++r) {
+    const int c = a.run_cls[r], len = a.run_len[r];
+    const PoolClass C = a.cls[c];
+    const int par = (int)(pos & 1);
+    const uint64_t* B = a.bm + ((int64_t)c * 2 + par) * a.nwords;
+    const int64_t slot = pos >> 1;
+    int64_t wbase = slot >> 6;
+    uint64_t fmask = ~0ull << (slot & 63);
+    int done = 0;
+    int64_t last = -1;
+    while (done < len) {
+      const int64_t wi = wbase + lane;
+      uint64_t word = wi < a.nwords ? B[wi] : 0ull;
+      if (lane == 0) word &= fmask;
+      const int cnt = __popcll(word);
+      const int incl = wave_incl_scan(cnt);
+      const int total = __shfl(incl, 63);
+      if (total == 0 && wbase + 64 >= a.nwords) {   // out of tables: the host parse disagrees
+        if (lane == 0) atomicOr(a.err, 1);
+        return;
+      }
+      const int nb = min(len - done, total);
+      for (int t0 = 0; t0 < nb; t0 += 64) {
+        const int t = t0 + lane;
+        const bool act = t < nb;
+        const int tt = act ? t : nb - 1;
+        int q = 0;
+#pragma unroll
+        for (int step = 32; step >= 1; step >>= 1)
+          if (__shfl(incl, q + step - 1) <= tt) q += step;
+        const uint64_t wq = __shfl(word, q);
+        const int prev = __shfl(incl, q) - __shfl(cnt, q);
+        const int bit = pool_select64(wq, tt - prev);
+        const int64_t p = 2 * ((wbase + q) * 64 + bit) + par;
+        if (act) {
+          const int j = j0 + done + t;
+          const double u1 = pool_unif(a.raw[p]), u2 = pool_unif(a.raw[p + 1]);
+          double x = 0.0;
+          if (!pool_attempt(C, u1, u2, texp, tlog, &x) || x > C.thr) bad_attempt = true;
+          double sg, m0, m1;
+          pool_sigma_tables(C, x, a.att[j], texp, tlog, &sg, &m0, &m1);
+          wsig[j] = sg;
+          wtab[2 * j] = m0;
+          wtab[2 * j + 1] = m1;
+        }
+        last = __shfl(p, (nb - 1 - t0) & 63);
+      }
+      done += nb;
+      wbase += 64;
+      fmask = ~0ull;
+    }
+    pos = last + 2;
+    j0 += len;
+  }
+  if (lane == 0 && pos != a.starts[e + 1]) atomicOr(a.err, 1);
+  if (__ballot(bad_attempt) && lane == 0) atomicOr(a.err, 2);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+  double* tab = a.tab + e * 2 * d;
+  double* sig = a.sig + e * d;
+  double A = 0.0, sc = 0.0, dmx = 0.0, dmn = __builtin_inf();
+  for (int j = lane; j < d; j += 64) {
+    const double m0 = wtab[2 * j], m1 = wtab[2 * j + 1];
+    tab[2 * j] = m0;
+    tab[2 * j + 1] = m1;
+    sig[j] = wsig[j];
+    A += m0;
+    sc += fmax(fabs(m0), fabs(m1));
+    const double dj = m0 - m1;
+    dmx = fmax(dmx, dj);
+    dmn = fmin(dmn, dj);
+  }
+  A = wave_sum(A);
+  sc = wave_sum(sc);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    dmx = fmax(dmx, __shfl_xor(dmx, o));
+    dmn = fmin(dmn, __shfl_xor(dmn, o));
+  }
+  // bound record (Ctx::bounds_for, kernels.hpp "Bound data per parameter entry")
+  const double delta = dmx > 0 ? dmx / ((1 << kQ) - 1) : 0.0;
+  uint64_t* rec = a.bnd + e * a.bw;
+  for (int k = 0; k < a.Ws; ++k) {
+    const int j = 64 * k + lane;
+    const bool valid = j < d;
+    const unsigned code = valid ? codes[j] - 1u : 0u;
+    int q = 0;
+    if (valid) {
+      const double dj = wtab[2 * j] - wtab[2 * j + 1];
+      q = delta > 0 ? (int)floor(dj / delta) : 0;
+      q = min(max(q, 0), (1 << kQ) - 1);
+      while (q > 0 && delta * q > dj) --q;
+      while (q < (1 << kQ) - 1 && delta * (q + 1) <= dj) ++q;
+    }
+    for (int b = 0; b < a.wb; ++b) {
+      const uint64_t bits = __ballot(valid && ((code >> b) & 1u));
+      if (lane == 0) rec[b * a.Ws + k] = bits;
+    }
+    for (int b = 0; b < kQ; ++b) {
+      const uint64_t bits = __ballot(valid && ((q >> b) & 1));
+      if (lane == 0) rec[(a.wb + b) * a.Ws + k] = bits;
+    }
+  }
+  if (lane == 0) {
+    double* sv = reinterpret_cast<double*>(rec + (a.wb + kQ) * a.Ws);
+    sv[0] = A;
+    sv[1] = delta;
+    sv[2] = dmn > 0 ? dmn : 0.0;
+    sv[3] = sc;
+  }
+}
+
+hipError_t launch_pool_accept(const PoolAcceptArgs& a, hipStream_t s) {
+  const int64_t blocks = (a.nwords + 3) / 4;
+  hipLaunchKernelGGL(k_pool_accept, dim3((unsigned)blocks), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_pool_values(const PoolValueArgs& a, hipStream_t s) {
+  const int64_t blocks = (a.P + 3) / 4;
+  const size_t lds = 512 * 8 + (size_t)4 * 3 * a.d * 8;
+  hipLaunchKernelGGL(k_pool_values, dim3((unsigned)blocks), dim3(256), lds, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace hdpm

@@ -324,3 +324,68 @@ def test_device_mt_stream_jump_ahead_matches_r(hd, oracle, zoo, pre):
         assert np.array_equal(got.astype(np.float64) * 2.3283064365386963e-10, ref)
         assert np.array_equal(eng.rng_state, st)
     eng.close()
+
+
+# ------------------------------------------------------------------ latent pool generator
+def _pool_case(hd, oracle, ds, v, w, P, pre, seed, debug=0):
+    eng = hd.Engine(0)
+    eng.set_data(ds.codes, ds.attrisize, ds.gamma, v, w)
+    eng.set_debug(debug)
+    st = oracle.seed_state(seed)
+    oracle.runif(st, pre)
+    eng.rng_state = st
+    eng.generate_pool(P)
+    pc, ps, _ = oracle.pool_generate(ds.attrisize, v, w, P, st)
+    gc, gs = eng.get_pool(P)
+    assert np.array_equal(gc, pc)
+    assert np.array_equal(gs, ps)                 # bit-exact sigmas
+    assert np.array_equal(eng.rng_state, st)      # same stream position after the pool
+    stats = eng.stats()
+    eng.close()
+    return stats
+
+
+@pytest.mark.parametrize("pre", [0, 1, 623, 624, 5000])
+def test_device_pool_matches_oracle_zoo(hd, oracle, zoo, pre):
+    st = _pool_case(hd, oracle, zoo, zoo.v, zoo.w, 303, pre, 31 + pre)
+    assert st["pool_device_calls"] == 1
+
+
+@pytest.mark.parametrize("case", ["mixed_levels", "odd_d_bc", "c5_like", "host_forced"])
+def test_device_pool_matches_oracle_synthetic(hd, oracle, case):
+    if case == "mixed_levels":
+        ds = synth(2000, 64, 5, (2, 6), seed=3)
+        v, w, P = np.full(64, 6.0), np.full(64, 0.25), 6000
+    elif case == "odd_d_bc":
+        ds = synth(1500, 7, 4, (2, 7), seed=4)
+        v = np.array([1.8, 1.8, 6.0, 6.0, 3.0, 1.5, 6.0])      # v - 1 < 1: rbeta algorithm BC
+        w = np.array([0.25, 0.25, 0.25, 0.4, 0.5, 0.3, 0.25])
+        P = 4500
+    else:
+        ds = synth(3000, 128, 6, 4, seed=5)
+        v, w, P = np.full(128, 6.0), np.full(128, 0.25), 30000   # ~14M draws: multi-workgroup slice
+    st = _pool_case(hd, oracle, ds, v, w, P, 77, 9, debug=64 if case == "host_forced" else 0)
+    assert st["pool_device_calls"] == (0 if case == "host_forced" else 1)
+
+
+def test_device_pool_then_sweeps_match_oracle(hd, oracle):
+    # the prepass / exact rows read the device-built pool records and tables
+    ds = synth(4000, 96, 6, (2, 5), seed=12)
+    cen, sig = random_params(ds, 6, 3)
+    eng = make_engine(hd, ds)
+    st = oracle.seed_state(5)
+    eng.rng_state = st
+    eng.set_state(ds.truth, cen, sig)
+    P = ds.n * 3
+    eng.generate_pool(P)
+    ost = oracle_state(oracle, ds.truth.astype(np.int32).copy(), cen.copy(), sig.copy())
+    pc, ps, _ = oracle.pool_generate(ds.attrisize, ds.v, ds.w, P, st)
+    for _ in range(3):
+        eng.neal8_sweep(3)
+        oracle.neal8_sweep(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w, ost, 3, pc, ps, st)
+        assert_same_state(eng, ost)
+        eng.update_phi()
+        oracle.update_phi(ds.codes, ds.attrisize, ds.v, ds.w, ost, st)
+        assert_same_state(eng, ost)
+    assert eng.stats()["pool_device_calls"] == 1
+    eng.close()

@@ -33,3 +33,19 @@ def test_glibc_exp_log_replicas_match_libm(tmp_path):
     r = subprocess.run([str(exe), "1500000"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 exp mismatches, 0 log mismatches" in r.stdout
+
+
+def test_pool_pipeline_model_matches_sequential_generator(tmp_path):
+    """The stream-exact pool pipeline (packed attempt tables -> host walk -> values; the
+    arithmetic the device kernels share) reproduces the sequential generator's pool and
+    stream position: Zoo hyperparameters at several stream offsets, odd D with an rbeta
+    BC class, C3-like mixed levels, a C4-like 784-attribute run."""
+    exe = tmp_path / "pool_gen_test"
+    src = os.path.join(HERE, "cpp", "pool_gen_test.cpp")
+    r = subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-o", str(exe), src],
+                       capture_output=True, text=True)
+    if r.returncode != 0:
+        pytest.fail(r.stderr)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "pool pipeline ok" in r.stdout
