@@ -174,7 +174,10 @@ class HostPool {
     while (done_.load(std::memory_order_acquire) < total_) spin_pause();
   }
 
-  // Every worker calls f(worker_index) once; the caller continues (join() waits).
+  // Workers that wake up while the job is open call f(worker_index) once; the caller
+  // continues.  join() closes the job and waits only for the workers that joined it, so a
+  // worker the OS has not run yet (a busy core) holds nobody up: f must hand out its work
+  // through shared counters that the caller drains too.
   template <class F>
   void launch(F&& f) {
     run_mu_.lock();
@@ -183,11 +186,12 @@ class HostPool {
     bcast_ = &bjob_;
     range_ = nullptr;
     bdone_.store(0, std::memory_order_relaxed);
-    widx_.store(0, std::memory_order_relaxed);
+    bclaim_.store(0, std::memory_order_relaxed);
     publish();
   }
   void join() {
-    while (bdone_.load(std::memory_order_acquire) < (int)th_.size()) spin_pause();
+    const int joined = bclaim_.fetch_or(kClosed, std::memory_order_acq_rel) & ~kClosed;
+    while (bdone_.load(std::memory_order_acquire) < joined) spin_pause();
     run_mu_.unlock();
   }
 
@@ -305,8 +309,11 @@ class HostPool {
         if (g != seen) {
           seen = g;
           if (bcast_) {
-            (*bcast_)(widx_.fetch_add(1, std::memory_order_relaxed));
-            bdone_.fetch_add(1, std::memory_order_acq_rel);
+            const int id = bclaim_.fetch_add(1, std::memory_order_acq_rel);
+            if (!(id & kClosed)) {
+              (*bcast_)(id);
+              bdone_.fetch_add(1, std::memory_order_acq_rel);
+            }
           } else {
             work();
           }
@@ -333,7 +340,8 @@ class HostPool {
   std::mutex mu_, run_mu_;
   std::condition_variable cv_;
   std::atomic<uint64_t> gen_{0}, wake_seq_{0};
-  std::atomic<int> active_{0}, bdone_{0}, widx_{0};
+  static constexpr int kClosed = 1 << 30;
+  std::atomic<int> active_{0}, bdone_{0}, bclaim_{0};
   std::atomic<int64_t> next_{0}, done_{0};
   int64_t total_ = 0, grain_ = 1;
   std::function<void(int64_t, int64_t)> range_;
@@ -1788,16 +1796,18 @@ struct Ctx {
     // A in chunks of attributes so the first cluster is ready early
     const int achunk = std::max(8, (d + 3) / 4);
     const int nach = (d + achunk - 1) / achunk;
+    auto take_a = [&]() -> bool {   // one A task from the shared queue; false when none left
+      const int task = nextA.fetch_add(1);
+      if (task >= T * nach) return false;
+      const int t = task / nach, c = task - t * nach;
+      if ((debug & 2) && c == 0) a_beg[t] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tlaunch).count();
+      phaseA(t, c * achunk, std::min(d, (c + 1) * achunk));
+      if (stA[t].fetch_add(1, std::memory_order_acq_rel) + 1 == nach && (debug & 2))
+        a_end[t] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tlaunch).count();
+      return true;
+    };
     auto worker = [&](int) {
-      for (;;) {
-        const int task = nextA.fetch_add(1);
-        if (task >= T * nach) break;
-        const int t = task / nach, c = task - t * nach;
-        if ((debug & 2) && c == 0) a_beg[t] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tlaunch).count();
-        phaseA(t, c * achunk, std::min(d, (c + 1) * achunk));
-        if (stA[t].fetch_add(1, std::memory_order_acq_rel) + 1 == nach && (debug & 2))
-          a_end[t] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tlaunch).count();
-      }
+      while (take_a()) {}
       for (;;) {
         const int t = nextC.fetch_add(1);
         if (t >= T) break;
@@ -1818,7 +1828,9 @@ struct Ctx {
     double wait_us = 0;
     for (; tb < T; ++tb) {
       auto w0 = std::chrono::steady_clock::now();
-      while (par && stA[tb].load(std::memory_order_acquire) < nach) HostPool::spin_pause();
+      // the caller takes queued A tasks itself rather than wait for a worker to wake up
+      while (par && stA[tb].load(std::memory_order_acquire) < nach)
+        if (!take_a()) HostPool::spin_pause();
       if (debug & 2) wait_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - w0).count();
       berr = phaseB(tb);
       if (berr) break;
