@@ -507,6 +507,7 @@ struct Ctx {
   DevBuf<double> d_margin;
   DevBuf<int> d_rowpos;
   DevBuf<int> d_list, d_cnt, d_dense, d_dense_total, d_spec;
+  DevBuf<double> d_spec_rad;
   DevBuf<uint64_t> d_csum;            // per-label cluster summary for the prepass
   DevBuf<unsigned> d_hist_part;
   DevBuf<int> d_ctl;                  // ResolveCtl + summary (kernels.hpp)
@@ -1346,6 +1347,7 @@ struct Ctx {
     d_dense.ensure((size_t)nb_max * kBlock);
     d_dense_total.ensure(1);
     d_spec.ensure((size_t)nb_max * kBlock);
+    d_spec_rad.ensure((size_t)nb_max * kBlock);
 
     int nslots = K;
     int p = 0;
@@ -1382,6 +1384,7 @@ struct Ctx {
       pa.L = d_L.p; pa.rowpos = d_rowpos.p; pa.margin = d_margin.p; pa.list = d_list.p; pa.cnt = d_cnt.p;
       pa.dense = d_dense.p; pa.dense_total = d_dense_total.p;
       pa.spec = (debug & 8) ? nullptr : d_spec.p;
+      pa.spec_rad = d_spec_rad.p;
       pa.p0 = p;
       const int nblocks = (n - p + kBlock - 1) / kBlock;
       HIPCHK(launch_cluster_summary(pa, stream));
@@ -1400,6 +1403,7 @@ struct Ctx {
       ra.L = d_L.p; ra.rowpos = d_rowpos.p; ra.slot_bnd = d_slot_bnd.p; ra.pool_bnd = d_pool_bnd.p; ra.bw = bw;
       ra.S = S; ra.margin = d_margin.p; ra.list = d_list.p; ra.dense = d_dense.p; ra.dense_total = d_dense_total.p;
       ra.spec = pa.spec;
+      ra.spec_rad = pa.spec_rad;
       ra.nblocks = nblocks; ra.p0 = p; ra.T = T; ra.dmax = dmax; ra.scap = scap; ra.K = K;
       ra.lcap = std::min(scap, nslots + 2);
       ra.nslots = nslots; ra.ctl = (ResolveCtl*)d_ctl.p; ra.summary = d_ctl.p + 8; ra.force_exact = (debug & 1);

@@ -424,10 +424,13 @@ __global__ __launch_bounds__(kScanThreads) void k_list_scan(const int* __restric
 __device__ __forceinline__ void wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 struct RShared {
-  int K, nslots, status, next, restart, moves, exact, checked, pick, src, pad0, pad1;
+  int K, nslots, status, next, restart, moves, exact, checked, pick, src, nstruct, spec_used;
   double dnow, sum;
+  double dvmax;        // max over slots of |logn[count] - logn[snapshot count]|
+  double pad;
   long long tsub[8];   // diagnostics (resolver profiling)
 };
+constexpr int kRSharedBytes = 192;
 
 struct RState {
   RShared* sh;
@@ -446,7 +449,7 @@ struct RState {
 
 __host__ __device__ inline size_t resolve_lds_bytes(int lcap, int m) {
   const size_t emax = (size_t)lcap + (size_t)m;
-  return 128 + emax * 4 * sizeof(double) + (size_t)lcap * 2 * sizeof(double) + (size_t)lcap * 4 * sizeof(int) +
+  return kRSharedBytes + emax * 4 * sizeof(double) + (size_t)lcap * 2 * sizeof(double) + (size_t)lcap * 4 * sizeof(int) +
          emax * sizeof(int);
 }
 
@@ -464,6 +467,14 @@ __device__ __forceinline__ double slot_drift(const RState& st, const double* log
   }
   if (a == 1) return b == 0 ? 0.0 : logn[b];
   return INFINITY;
+}
+
+// |logn[count] - logn[snapshot count]| of slot s (inf when either count is 0)
+__device__ __forceinline__ double count_drift(const RState& st, const double* logn, int s) {
+  const int a = st.snap[s], b = st.cnt[s];
+  if (a == b) return 0.0;
+  if (a < 1 || b < 1) return INFINITY;
+  return fabs(logn[b] - logn[a]);
 }
 
 // lane 0: record a reassignment for the incremental frequency tables
@@ -537,8 +548,16 @@ __device__ __forceinline__ double readlane_f64(double x, int l) {
 // entries -inf / 0.0, which leave a max or a non-negative running sum unchanged.  Counts,
 // the maximum's position and ties come from ballots; ties or a draw past the maximum take
 // R's revsort on lane 0 (LDS scratch lp / lperm, result through *lpick).
+//
+// With `rad` (the snapshot draws of k_exact_rows), *rad receives a radius: the draw is
+// unchanged when every log-weight moves by less than *rad (normalised probabilities then
+// move by factors within exp(+-2 rad)): the chosen entry keeps its place in revsort's order
+// (ratios to its neighbours) and the uniform stays inside its cumulative interval.  0 when
+// no such bound is kept (ties, the Walker threshold in reach).
 template <int RE>
-__device__ int decide_values(double (&pv)[RE], int E, double rU, double* lp, int* lperm, int* lpick) {
+__device__ int decide_values(double (&pv)[RE], int E, double rU, double* lp, int* lperm, int* lpick,
+                             double* rad = nullptr) {
+  if (rad) *rad = 0.0;
   const int lane = threadIdx.x & 63;
   E = __builtin_amdgcn_readfirstlane(E);
   const int E8 = (E + 7) & ~7;
@@ -556,7 +575,11 @@ __device__ int decide_values(double (&pv)[RE], int E, double rU, double* lp, int
 #pragma unroll
   for (int r = 0; r < RE; ++r)
     if (r * kWave + lane >= E) pv[r] = -INFINITY;
-  const double mx = scan(-INFINITY, [](double m, double x) { return fmax(m, x); });
+  // max is order-free: a butterfly instead of the sequential scan
+  double mx = pv[0];
+#pragma unroll
+  for (int r = 1; r < RE; ++r) mx = fmax(mx, pv[r]);
+  mx = wave_max(mx);
 #pragma unroll
   for (int r = 0; r < RE; ++r) pv[r] = (r * kWave + lane < E) ? exp(pv[r] - mx) : 0.0;      // n8:95
   const double sum = scan(0.0, [](double s, double x) { return s + x; });
@@ -572,7 +595,10 @@ __device__ int decide_values(double (&pv)[RE], int E, double rU, double* lp, int
     nc += __popcll(__ballot(in && (double)E * pv[r] > 0.1));
   }
   if (nc > 200) return -4;  // kWalker
-  const double pmax = scan(-1.0, [](double m, double x) { return fmax(m, x); });
+  double pmax = pv[0];
+#pragma unroll
+  for (int r = 1; r < RE; ++r) pmax = fmax(pmax, pv[r]);
+  pmax = wave_max(pmax);
   int ties = 0, amax = -1;
 #pragma unroll
   for (int r = 0; r < RE; ++r) {
@@ -581,7 +607,78 @@ __device__ int decide_values(double (&pv)[RE], int E, double rU, double* lp, int
     if (amax < 0 && b) amax = r * kWave + __ffsll((long long)b) - 1;
   }
   // Unique maximum drawn: revsort puts it first, cumsum[0] = pmax.
-  if (ties == 1 && rU <= pmax) return amax;
+  if (ties == 1 && rU <= pmax) {
+    if (rad && E <= 200) {
+      double p2 = -1.0;
+#pragma unroll
+      for (int r = 0; r < RE; ++r)
+        if (r * kWave + lane < E && r * kWave + lane != amax) p2 = fmax(p2, pv[r]);
+      p2 = wave_max(p2);
+      const double r1 = p2 > 0 ? 0.5 * log(pmax / p2) : INFINITY;
+      *rad = fmax(0.0, fmin(r1, 0.5 * log(pmax / rU)) - 1e-9);
+    }
+    return amax;
+  }
+  // Positive entries with distinct values: revsort (a heapsort) leaves them in plain
+  // descending order, so an entry's position is its rank, and the cumulative sums run
+  // over that order with the serial loop's additions.  Ties among positive entries, or a
+  // draw past the last positive entry (it would land among the zeros, whose order is
+  // heapsort's tie handling), take the serial revsort below.
+  if (ties == 1) {
+    int rank[RE];
+    bool tie = false;
+#pragma unroll
+    for (int r = 0; r < RE; ++r) rank[r] = 0;
+#pragma unroll
+    for (int r2 = 0; r2 < RE; ++r2) {
+      const int lim = min(kWave, E - r2 * kWave);
+      for (int l = 0; l < lim; ++l) {
+        const double x = readlane_f64(pv[r2], l);
+#pragma unroll
+        for (int r = 0; r < RE; ++r) {
+          rank[r] += x > pv[r] ? 1 : 0;
+          tie |= x == pv[r] && pv[r] > 0 && (r2 != r || l != lane);
+        }
+      }
+    }
+    int npos = 0;
+#pragma unroll
+    for (int r = 0; r < RE; ++r) npos += __popcll(__ballot(r * kWave + lane < E && pv[r] > 0));
+    if (!__ballot(tie)) {
+#pragma unroll
+      for (int r = 0; r < RE; ++r)
+        if (r * kWave + lane < E && pv[r] > 0) {
+          lp[rank[r]] = pv[r];
+          lperm[rank[r]] = r * kWave + lane;
+        }
+      wave_sync();
+      int pick = -1, jp = 0;
+      double c = 0.0, cprev = 0.0;
+      for (int j0 = 0; j0 < npos && pick < 0; j0 += 8) {
+        double v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = j0 + k < npos ? lp[j0 + k] : 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int j = j0 + k;
+          if (pick >= 0 || j >= npos) break;
+          cprev = c;
+          c += v[k];
+          if (j == E - 1 || rU <= c) { pick = lperm[j]; jp = j; }
+        }
+      }
+      if (rad && pick >= 0 && E <= 200) {
+        const double pj = lp[jp];
+        double r = INFINITY;
+        if (jp > 0) r = fmin(r, fmin(0.5 * log(lp[jp - 1] / pj), 0.5 * log(rU / cprev)));
+        if (jp + 1 < npos) r = fmin(r, 0.5 * log(pj / lp[jp + 1]));
+        if (jp != E - 1) r = fmin(r, 0.5 * log(c / rU));
+        *rad = fmax(0.0, r - 1e-9);
+      }
+      wave_sync();   // lp / lperm are reused by the next decision
+      if (pick >= 0) return pick;
+    }
+  }
 #pragma unroll
   for (int r = 0; r < RE; ++r)
     if (r * kWave + lane < E) lp[r * kWave + lane] = pv[r];
@@ -823,8 +920,12 @@ __device__ void exact_rows_point(const PrepassArgs& a, int row, double* lp, int*
         pv[r] = a.logfac + ((l == 0 && own_cnt == 1) ? ll_own : acc_r[r]);
       }
     }
-    const int pick = decide_values<RE>(pv, E, raw_to_unif(raw[a.m]), lp, lperm, lpick);
-    if (lane == 0) a.spec[row] = pick >= 0 ? pick : -1;
+    double rad = 0.0;
+    const int pick = decide_values<RE>(pv, E, raw_to_unif(raw[a.m]), lp, lperm, lpick, &rad);
+    if (lane == 0) {
+      a.spec[row] = pick >= 0 ? pick : -1;
+      a.spec_rad[row] = rad;
+    }
   }
 }
 
@@ -854,7 +955,7 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
   st.lcap = a.lcap;
   st.emax = a.lcap + a.m;
   st.sh = (RShared*)smem;
-  st.val = (double*)(smem + 128);
+  st.val = (double*)(smem + kRSharedBytes);
   st.p = st.val + st.emax;
   st.row = st.p + st.emax;
   st.l1 = st.row + 2 * st.emax;
@@ -879,7 +980,7 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
   }
   if (lane == 0) {
     S.K = a.K; S.nslots = a.nslots; S.status = 0; S.next = a.n; S.restart = 0;
-    S.moves = 0; S.exact = 0; S.checked = 0; S.dnow = 0.0;
+    S.moves = 0; S.exact = 0; S.checked = 0; S.dnow = 0.0; S.dvmax = 0.0; S.nstruct = 0; S.spec_used = 0;
     for (int k = 0; k < 8; ++k) S.tsub[k] = 0;
   }
   wave_sync();
@@ -888,11 +989,20 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
 
   // Decide point i (exact row in LDS at Lr) and apply n8:107-159.  Returns false to stop
   // the sweep here.
-  auto process = [&](int64_t i, const double* Lr, int own, uint32_t rawU, int spec) -> bool {
+  auto process = [&](int64_t i, const double* Lr, int own, uint32_t rawU, int spec, double srad) -> bool {
     const int K = S.K;
     const long long tq0 = prof ? wall_clock64() : 0;
-    // the snapshot draw holds while nothing has moved in this round
-    const int pick = (S.moves == 0 && spec >= 0) ? spec : exact_decision(a, st, K, Lr, own, raw_to_unif(rawU));
+    // The snapshot draw holds while nothing has moved in this launch, and after moves while
+    // the slots and labels are those of the snapshot and no log-weight of the point has
+    // moved by its radius: the others' by at most dvmax, its own slot's (count - 1) by du.
+    bool use_spec = spec >= 0 && S.moves == 0;
+    if (spec >= 0 && !use_spec && S.nstruct == 0) {
+      const int sa = st.snap[own], sb = st.cnt[own];
+      const double du = sa == sb ? 0.0 : (sa >= 2 && sb >= 2 ? fabs(a.logn[sb - 1] - a.logn[sa - 1]) : INFINITY);
+      use_spec = fmax(S.dvmax, du) < srad;
+    }
+    if (use_spec && S.moves != 0 && lane == 0) S.spec_used++;
+    const int pick = use_spec ? spec : exact_decision(a, st, K, Lr, own, raw_to_unif(rawU));
     if (prof && lane == 0) S.tsub[4] += wall_clock64() - tq0;
     if (lane == 0) {
       S.exact++;
@@ -907,6 +1017,7 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
               S.moves++;
               log_move(a, nlog, i, own, ns);
               S.dnow = fmax(S.dnow, fmax(slot_drift(st, a.logn, own), slot_drift(st, a.logn, ns)));
+              S.dvmax = fmax(S.dvmax, fmax(count_drift(st, a.logn, own), count_drift(st, a.logn, ns)));
             }
           } else {                                                  // case 2
             int target = ns;
@@ -924,6 +1035,7 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
               if (ownlab != K - 1) { st.sol[ownlab] = last; st.los[last] = ownlab; }
               st.sol[K - 1] = -1;
               S.K = K - 1;
+              S.nstruct++;
               S.dnow = fmax(S.dnow, fmax(slot_drift(st, a.logn, own), slot_drift(st, a.logn, target)));
             }
           }
@@ -969,6 +1081,26 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
 
   bool go = true;
   int64_t start_checked = -1;
+  // Once the drift exceeds dmax, the unlisted (certain at the snapshot) points between two
+  // listed ones are re-tested before the next listed point is decided: the n8 sequence is
+  // unchanged, and a point that is no longer certain stops the launch for the host to
+  // recompute bounds from there.  Returns false on such a point.
+  auto verify = [&](int64_t lo, int64_t hi) -> bool {
+    if (lane == 0) S.checked = 1;
+    const double dn = S.dnow;
+    for (int64_t base = lo; base < hi; base += kWave) {
+      const int64_t j = base + lane;
+      bool fail = false;
+      if (j < hi) fail = !(a.margin[j] - 2.0 * dn > a.T && st.cnt[a.c[j]] >= 2);
+      const unsigned long long bal = __ballot(fail);
+      if (bal) {
+        if (lane == 0) { S.restart = 1; S.next = (int)(base + __ffsll((long long)bal) - 1); }
+        wave_sync();
+        return false;
+      }
+    }
+    return true;
+  };
   if (!a.force_exact) {
     // LIST mode: only the prepass's uncertain points need work while drift <= dmax; the
     // dense list, the points' labels and draws are read 64 at a time, and each exact row
@@ -983,6 +1115,7 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
       pf.land(a.L + (int64_t)r0 * ncol, ncol, st.row);
     }
     if (prof) tp[2] = wall_clock64();
+    int64_t vfrom = a.p0;   // unlisted points [vfrom, next listed point) not yet re-tested
     for (int q0 = 0; q0 < total && go; q0 += kWave) {
       long long tb = prof ? wall_clock64() : 0;
       const int lim = min(kWave, total - q0);
@@ -991,6 +1124,7 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
       const int ci = lane < lim ? a.c[li] : 0;
       const uint32_t ru = lane < lim ? a.raw[(int64_t)li * (a.m + 1) + a.m] : 0u;
       const int sp = (lane < lim && a.spec) ? a.spec[rw] : -1;
+      const double sr = (lane < lim && a.spec) ? a.spec_rad[rw] : 0.0;
       const int rnext = (q0 + kWave + lane < total && lane == 0) ? a.dense[q0 + kWave] : 0;
       const int rn64 = __shfl(rnext, 0);
       if (prof) { tp[3] += wall_clock64() - tb + 0 * (ci + (int)ru + rn64); }
@@ -1002,9 +1136,11 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
         else if (q0 + kWave < total) rn = rn64;
         if (rn >= 0) pf.issue(a.L + (int64_t)rn * ncol, ncol);
         const int64_t i = __shfl(li, q);
-        go = process(i, st.row + buf * st.emax, __shfl(ci, q), (uint32_t)__shfl((int)ru, q), __shfl(sp, q));
+        if (S.dnow > a.dmax && !verify(vfrom, i)) { go = false; break; }
+        go = process(i, st.row + buf * st.emax, __shfl(ci, q), (uint32_t)__shfl((int)ru, q), __shfl(sp, q),
+                     __shfl(sr, q));
+        vfrom = i + 1;
         long long t1 = prof ? wall_clock64() : 0;
-        if (go && S.dnow > a.dmax) { start_checked = i + 1; go = false; }
         if (go && rn >= 0) {
           buf ^= 1;
           pf.land(a.L + (int64_t)rn * ncol, ncol, st.row + buf * st.emax);
@@ -1018,6 +1154,7 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
         }
       }
     }
+    if (go && S.status == 0 && !S.restart && S.dnow > a.dmax) (void)verify(vfrom, a.n);
   } else {
     start_checked = a.p0;
   }
@@ -1049,7 +1186,7 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
         const double* src = a.L + (int64_t)row * ncol;
         for (int c = lane; c < ncol; c += kWave) st.row[c] = src[c];
         wave_sync();
-        if (!process(base + q, st.row, __shfl(ci, q), a.raw[(base + q) * (a.m + 1) + a.m], -1)) { stop = true; break; }
+        if (!process(base + q, st.row, __shfl(ci, q), a.raw[(base + q) * (a.m + 1) + a.m], -1, 0.0)) { stop = true; break; }
         // drift may have grown: re-test the remaining lanes
         bool u2 = false;
         if (lane > q && i < a.n) {

@@ -82,6 +82,7 @@ struct PrepassArgs {
   int* dense;                // all uncertain rows in index order (k_list_scan)
   int* dense_total;          // their number
   int* spec;                 // per row: the draw in the snapshot state (or -1), by k_exact_rows
+  double* spec_rad;          // per row: log-weight drift under which that draw holds
   int p0;
 };
 
@@ -122,6 +123,7 @@ struct ResolveArgs {
   const int* dense;          // uncertain rows in index order
   const int* dense_total;
   const int* spec;           // per row: the draw in the snapshot state (k_exact_rows), or -1
+  const double* spec_rad;    // per row: its radius (decide_values)
   int nblocks;
   int p0;
   double T;                  // certainty threshold without drift
