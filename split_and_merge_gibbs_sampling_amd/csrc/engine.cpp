@@ -508,6 +508,7 @@ struct Ctx {
   DevBuf<int> d_rowpos;
   DevBuf<int> d_list, d_cnt, d_dense, d_dense_total, d_spec;
   DevBuf<double> d_spec_rad;
+  DevBuf<int4> d_rq;
   DevBuf<uint64_t> d_csum;            // per-label cluster summary for the prepass
   DevBuf<unsigned> d_hist_part;
   DevBuf<int> d_ctl;                  // ResolveCtl + summary (kernels.hpp)
@@ -1348,6 +1349,7 @@ struct Ctx {
     d_dense_total.ensure(1);
     d_spec.ensure((size_t)nb_max * kBlock);
     d_spec_rad.ensure((size_t)nb_max * kBlock);
+    d_rq.ensure((size_t)nb_max * kBlock);
 
     int nslots = K;
     int p = 0;
@@ -1385,6 +1387,7 @@ struct Ctx {
       pa.dense = d_dense.p; pa.dense_total = d_dense_total.p;
       pa.spec = (debug & 8) ? nullptr : d_spec.p;
       pa.spec_rad = d_spec_rad.p;
+      pa.rq = d_rq.p;
       pa.p0 = p;
       const int nblocks = (n - p + kBlock - 1) / kBlock;
       HIPCHK(launch_cluster_summary(pa, stream));
@@ -1404,6 +1407,7 @@ struct Ctx {
       ra.S = S; ra.margin = d_margin.p; ra.list = d_list.p; ra.dense = d_dense.p; ra.dense_total = d_dense_total.p;
       ra.spec = pa.spec;
       ra.spec_rad = pa.spec_rad;
+      ra.rq = pa.rq;
       ra.nblocks = nblocks; ra.p0 = p; ra.T = T; ra.dmax = dmax; ra.scap = scap; ra.K = K;
       ra.lcap = std::min(scap, nslots + 2);
       ra.nslots = nslots; ra.ctl = (ResolveCtl*)d_ctl.p; ra.summary = d_ctl.p + 8; ra.force_exact = (debug & 1);
@@ -1453,12 +1457,10 @@ struct Ctx {
         long long tp[16];
         HIPCHK(hipMemcpy(tp, d_rprof.p, sizeof(tp), hipMemcpyDeviceToHost));
         std::fprintf(stderr,
-                     "[resolve] init %.2f us, dense %.2f us, row0 %.2f us, batches %.2f us, process %.2f us, "
-                     "land %.2f us, points %lld, total %.2f us\n",
-                     (tp[1] - tp[0]) / 100.0, (tp[2] - tp[1]) / 100.0, 0.0, tp[3] / 100.0, tp[4] / 100.0,
-                     tp[5] / 100.0, tp[6], (tp[7] - tp[0]) / 100.0);
-        std::fprintf(stderr, "[resolve] decision %.2f us: values %.2f, exp %.2f, sums %.2f, reductions %.2f us\n",
-                     tp[12] / 100.0, tp[8] / 100.0, tp[9] / 100.0, tp[10] / 100.0, tp[11] / 100.0);
+                     "[resolve] init %.2f us, batches %.2f us, decided points %lld in %.2f us (exact decisions "
+                     "%.2f us), total %.2f us\n",
+                     (tp[1] - tp[0]) / 100.0, tp[3] / 100.0, tp[6], tp[4] / 100.0, tp[12] / 100.0,
+                     (tp[7] - tp[0]) / 100.0);
       }
       stats.exact_points += c.exact;
       stats.moves += c.moves;

@@ -424,7 +424,7 @@ __global__ __launch_bounds__(kScanThreads) void k_list_scan(const int* __restric
 __device__ __forceinline__ void wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 struct RShared {
-  int K, nslots, status, next, restart, moves, exact, checked, pick, src, nstruct, spec_used;
+  int K, nslots, status, next, restart, moves, exact, checked, pick, src, nstruct, pad0;
   double dnow, sum;
   double dvmax;        // max over slots of |logn[count] - logn[snapshot count]|
   double pad;
@@ -800,30 +800,6 @@ __device__ void copy_pool_params(const ResolveArgs& a, int64_t e, int s) {
   for (int b = lane; b < a.bw; b += kWave) a.slot_bnd[(int64_t)s * a.bw + b] = a.pool_bnd[e * a.bw + b];
 }
 
-// Row prefetch: up to kRowRegs * 64 columns are held in registers while the previous point
-// is decided; wider rows load their tail on arrival.
-constexpr int kRowRegs = 4;
-struct RowPrefetch {
-  double r[kRowRegs];
-  __device__ __forceinline__ void issue(const double* src, int ncol) {
-    const int lane = threadIdx.x;
-#pragma unroll
-    for (int k = 0; k < kRowRegs; ++k) {
-      const int c = k * kWave + lane;
-      r[k] = c < ncol ? src[c] : 0.0;
-    }
-  }
-  __device__ __forceinline__ void land(const double* src, int ncol, double* dst) const {
-    const int lane = threadIdx.x;
-#pragma unroll
-    for (int k = 0; k < kRowRegs; ++k) {
-      const int c = k * kWave + lane;
-      if (c < ncol) dst[c] = r[k];
-    }
-    for (int c = kRowRegs * kWave + lane; c < ncol; c += kWave) dst[c] = src[c];
-  }
-};
-
 // Exact rows of the uncertain points: one wave per point (grid-stride over the dense
 // list), lane e computes entry e's log-likelihood, adding its per-attribute dhamming
 // values in attribute order -- the reference's summation order (n8:47-49), so every row
@@ -836,7 +812,7 @@ struct RowPrefetch {
 // While no earlier point of the round has moved, the resolver's state IS the snapshot,
 // so it takes these draws as they are; after the first move it decides on its own.
 template <int RE>
-__device__ void exact_rows_point(const PrepassArgs& a, int row, double* lp, int* lperm, int* lpick) {
+__device__ void exact_rows_point(const PrepassArgs& a, int q, int row, double* lp, int* lperm, int* lpick) {
   const int lane = threadIdx.x;
   const int E = a.K + a.m;
   const int dp = a.nq * 16;
@@ -923,8 +899,8 @@ __device__ void exact_rows_point(const PrepassArgs& a, int row, double* lp, int*
     double rad = 0.0;
     const int pick = decide_values<RE>(pv, E, raw_to_unif(raw[a.m]), lp, lperm, lpick, &rad);
     if (lane == 0) {
-      a.spec[row] = pick >= 0 ? pick : -1;
-      a.spec_rad[row] = rad;
+      a.spec[q] = pick >= 0 ? pick : -1;
+      a.spec_rad[q] = rad;
     }
   }
 }
@@ -938,11 +914,15 @@ __global__ __launch_bounds__(kWave) void k_exact_rows(PrepassArgs a) {
   const int E = a.K + a.m;
   for (int q = blockIdx.x; q < total; q += gridDim.x) {
     const int row = a.dense[q];
-    if (E <= kWave) exact_rows_point<1>(a, row, lp, lperm, &lpick);
-    else if (E <= 4 * kWave) exact_rows_point<4>(a, row, lp, lperm, &lpick);
+    if (threadIdx.x == 0) {   // the resolver's per-point inputs, in list order
+      const int64_t i = a.list[row];
+      a.rq[q] = make_int4(row, (int)i, a.c[i], (int)a.raw[i * (a.m + 1) + a.m]);
+    }
+    if (E <= kWave) exact_rows_point<1>(a, q, row, lp, lperm, &lpick);
+    else if (E <= 4 * kWave) exact_rows_point<4>(a, q, row, lp, lperm, &lpick);
     else {
-      exact_rows_point<0>(a, row, lp, lperm, &lpick);
-      if (a.spec && threadIdx.x == 0) a.spec[row] = -1;
+      exact_rows_point<0>(a, q, row, lp, lperm, &lpick);
+      if (a.spec && threadIdx.x == 0) a.spec[q] = -1;
     }
   }
 }
@@ -980,7 +960,7 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
   }
   if (lane == 0) {
     S.K = a.K; S.nslots = a.nslots; S.status = 0; S.next = a.n; S.restart = 0;
-    S.moves = 0; S.exact = 0; S.checked = 0; S.dnow = 0.0; S.dvmax = 0.0; S.nstruct = 0; S.spec_used = 0;
+    S.moves = 0; S.exact = 0; S.checked = 0; S.dnow = 0.0; S.dvmax = 0.0; S.nstruct = 0;
     for (int k = 0; k < 8; ++k) S.tsub[k] = 0;
   }
   wave_sync();
@@ -989,7 +969,7 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
 
   // Decide point i (exact row in LDS at Lr) and apply n8:107-159.  Returns false to stop
   // the sweep here.
-  auto process = [&](int64_t i, const double* Lr, int own, uint32_t rawU, int spec, double srad) -> bool {
+  auto process = [&](int64_t i, int row, int own, uint32_t rawU, int spec, double srad) -> bool {
     const int K = S.K;
     const long long tq0 = prof ? wall_clock64() : 0;
     // The snapshot draw holds while nothing has moved in this launch, and after moves while
@@ -1001,11 +981,17 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
       const double du = sa == sb ? 0.0 : (sa >= 2 && sb >= 2 ? fabs(a.logn[sb - 1] - a.logn[sa - 1]) : INFINITY);
       use_spec = fmax(S.dvmax, du) < srad;
     }
-    if (use_spec && S.moves != 0 && lane == 0) S.spec_used++;
-    const int pick = use_spec ? spec : exact_decision(a, st, K, Lr, own, raw_to_unif(rawU));
+
+    int pick = spec;
+    if (!use_spec) {   // the point's exact row, on demand
+      const double* src = a.L + (int64_t)row * ncol;
+      for (int c = lane; c < ncol; c += kWave) st.row[c] = src[c];
+      wave_sync();
+      pick = exact_decision(a, st, K, st.row, own, raw_to_unif(rawU));
+    }
     if (prof && lane == 0) S.tsub[4] += wall_clock64() - tq0;
     if (lane == 0) {
-      S.exact++;
+      if (!use_spec) S.exact++;
       if (pick < 0) { S.status = -pick; S.next = (int)i; }
       else {
         const int ownlab = st.los[own];
@@ -1091,7 +1077,7 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
     for (int64_t base = lo; base < hi; base += kWave) {
       const int64_t j = base + lane;
       bool fail = false;
-      if (j < hi) fail = !(a.margin[j] - 2.0 * dn > a.T && st.cnt[a.c[j]] >= 2);
+      if (j < hi && a.rowpos[j] < 0) fail = !(a.margin[j] - 2.0 * dn > a.T && st.cnt[a.c[j]] >= 2);
       const unsigned long long bal = __ballot(fail);
       if (bal) {
         if (lane == 0) { S.restart = 1; S.next = (int)(base + __ffsll((long long)bal) - 1); }
@@ -1102,56 +1088,61 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
     return true;
   };
   if (!a.force_exact) {
-    // LIST mode: only the prepass's uncertain points need work while drift <= dmax; the
-    // dense list, the points' labels and draws are read 64 at a time, and each exact row
-    // is prefetched while the previous point is decided.
+    // LIST mode: only the prepass's uncertain points need work while drift <= dmax.  The
+    // dense list, the points' labels, draws and snapshot draws are read 64 at a time; the
+    // points whose snapshot draw still holds and keeps them in their cluster change
+    // nothing and are passed over with one ballot; the others are decided in order (exact
+    // rows loaded only for the points that need an exact decision).
     const int total = *a.dense_total;
     if (prof) tp[1] = wall_clock64();
-    int buf = 0;
-    RowPrefetch pf;
-    if (total > 0) {
-      const int r0 = a.dense[0];
-      pf.issue(a.L + (int64_t)r0 * ncol, ncol);
-      pf.land(a.L + (int64_t)r0 * ncol, ncol, st.row);
-    }
-    if (prof) tp[2] = wall_clock64();
     int64_t vfrom = a.p0;   // unlisted points [vfrom, next listed point) not yet re-tested
-    for (int q0 = 0; q0 < total && go; q0 += kWave) {
+    constexpr int kB = 4;   // chunks of 64 points whose inputs are loaded together
+    for (int qb = 0; qb < total && go; qb += kB * kWave) {
       long long tb = prof ? wall_clock64() : 0;
+      int4 rqv[kB];
+      int spv[kB];
+      double srv[kB];
+#pragma unroll
+      for (int b = 0; b < kB; ++b) {
+        const int qq = qb + b * kWave + lane;
+        const bool in = qq < total;
+        rqv[b] = in ? a.rq[qq] : make_int4(0, 0, 0, 0);
+        spv[b] = (in && a.spec) ? a.spec[qq] : -1;
+        srv[b] = (in && a.spec) ? a.spec_rad[qq] : 0.0;
+      }
+      if (prof) tp[3] += wall_clock64() - tb;
+#pragma unroll
+      for (int b = 0; b < kB; ++b) {
+      const int q0 = qb + b * kWave;
+      if (q0 >= total || !go) break;
       const int lim = min(kWave, total - q0);
-      const int rw = lane < lim ? a.dense[q0 + lane] : 0;
-      const int li = lane < lim ? a.list[rw] : 0;
-      const int ci = lane < lim ? a.c[li] : 0;
-      const uint32_t ru = lane < lim ? a.raw[(int64_t)li * (a.m + 1) + a.m] : 0u;
-      const int sp = (lane < lim && a.spec) ? a.spec[rw] : -1;
-      const double sr = (lane < lim && a.spec) ? a.spec_rad[rw] : 0.0;
-      const int rnext = (q0 + kWave + lane < total && lane == 0) ? a.dense[q0 + kWave] : 0;
-      const int rn64 = __shfl(rnext, 0);
-      if (prof) { tp[3] += wall_clock64() - tb + 0 * (ci + (int)ru + rn64); }
-      for (int q = 0; q < lim && go; ++q) {
+      const int rw = rqv[b].x, li = rqv[b].y, ci = rqv[b].z;
+      const uint32_t ru = (uint32_t)rqv[b].w;
+      const int sp = spv[b];
+      const double sr = srv[b];
+      int q = 0;
+      while (q < lim && go) {
         long long t0 = prof ? wall_clock64() : 0;
-        // next point's row -> registers (in flight while this point is decided)
-        int rn = -1;
-        if (q + 1 < lim) rn = __shfl(rw, q + 1);
-        else if (q0 + kWave < total) rn = rn64;
-        if (rn >= 0) pf.issue(a.L + (int64_t)rn * ncol, ncol);
+        bool stays = false;
+        if (lane >= q && lane < lim && sp >= 0 && sp < S.K && st.cnt[ci] != 1 && st.sol[sp] == ci) {
+          const int sa = st.snap[ci], sb = st.cnt[ci];
+          const double du =
+              sa == sb ? 0.0 : (sa >= 2 && sb >= 2 ? fabs(a.logn[sb - 1] - a.logn[sa - 1]) : INFINITY);
+          stays = S.moves == 0 || (S.nstruct == 0 && fmax(S.dvmax, du) < sr);
+        }
+        const unsigned long long todo = __ballot(lane >= q && lane < lim && !stays);
+        if (!todo) break;
+        q = __ffsll((long long)todo) - 1;
         const int64_t i = __shfl(li, q);
         if (S.dnow > a.dmax && !verify(vfrom, i)) { go = false; break; }
-        go = process(i, st.row + buf * st.emax, __shfl(ci, q), (uint32_t)__shfl((int)ru, q), __shfl(sp, q),
-                     __shfl(sr, q));
+        go = process(i, __shfl(rw, q), __shfl(ci, q), (uint32_t)__shfl((int)ru, q), __shfl(sp, q), __shfl(sr, q));
         vfrom = i + 1;
-        long long t1 = prof ? wall_clock64() : 0;
-        if (go && rn >= 0) {
-          buf ^= 1;
-          pf.land(a.L + (int64_t)rn * ncol, ncol, st.row + buf * st.emax);
-        }
+        ++q;
         if (prof) {
-          wave_sync();
-          const long long t2 = wall_clock64();
-          tp[4] += t1 - t0;
-          tp[5] += t2 - t1;
+          tp[4] += wall_clock64() - t0;
           tp[6] += 1;
         }
+      }
       }
     }
     if (go && S.status == 0 && !S.restart && S.dnow > a.dmax) (void)verify(vfrom, a.n);
@@ -1183,10 +1174,7 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
           stop = true;
           break;
         }
-        const double* src = a.L + (int64_t)row * ncol;
-        for (int c = lane; c < ncol; c += kWave) st.row[c] = src[c];
-        wave_sync();
-        if (!process(base + q, st.row, __shfl(ci, q), a.raw[(base + q) * (a.m + 1) + a.m], -1, 0.0)) { stop = true; break; }
+        if (!process(base + q, row, __shfl(ci, q), a.raw[(base + q) * (a.m + 1) + a.m], -1, 0.0)) { stop = true; break; }
         // drift may have grown: re-test the remaining lanes
         bool u2 = false;
         if (lane > q && i < a.n) {

@@ -1,5 +1,7 @@
 // kernels.hpp -- argument blocks shared by the host runtime and the gfx950 kernels.
 #pragma once
+#include <hip/hip_runtime.h>
+
 #include <cstdint>
 
 namespace hdpm {
@@ -81,8 +83,9 @@ struct PrepassArgs {
   int* cnt;                  // per block: number of uncertain points
   int* dense;                // all uncertain rows in index order (k_list_scan)
   int* dense_total;          // their number
-  int* spec;                 // per row: the draw in the snapshot state (or -1), by k_exact_rows
-  double* spec_rad;          // per row: log-weight drift under which that draw holds
+  int* spec;                 // per dense-list position: the draw in the snapshot state (or -1)
+  double* spec_rad;          // per dense-list position: log-weight drift under which it holds
+  int4* rq;                  // per dense-list position: {row, point, slot, categorical draw}
   int p0;
 };
 
@@ -94,7 +97,7 @@ struct ResolveCtl {
   int K;
   int nslots;
   int moves;
-  int exact;      // exact (slow-path) decisions taken
+  int exact;      // decisions computed in the resolver (not taken from the snapshot draws)
   int checked;    // 1 if the drift budget was exceeded (checked mode)
 };
 
@@ -122,8 +125,9 @@ struct ResolveArgs {
   const int* list;
   const int* dense;          // uncertain rows in index order
   const int* dense_total;
-  const int* spec;           // per row: the draw in the snapshot state (k_exact_rows), or -1
-  const double* spec_rad;    // per row: its radius (decide_values)
+  const int* spec;           // per dense-list position: the snapshot draw (k_exact_rows), or -1
+  const double* spec_rad;    // its radius (decide_values)
+  const int4* rq;            // per dense-list position: {row, point, slot, categorical draw}
   int nblocks;
   int p0;
   double T;                  // certainty threshold without drift
