@@ -181,9 +181,8 @@ def main():
     setup_s = time.perf_counter() - t_setup
     st_init = eng.stats()
     it = args.start_iter                         # iteration 0 regenerates the pool (la:123-129)
-    for _ in range(args.warmup):
-        eng.iteration(it)
-        it += 1
+    eng.iterations(it, args.warmup)             # hdpm_iterations: the la:85-154 loop in one call
+    it += args.warmup
     eng.synchronize()
     st0 = eng.stats()                            # + iteration 0's regeneration
     eng.reset_stats()
@@ -192,9 +191,8 @@ def main():
     D.barrier()
     cuda_sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        eng.iteration(it)
-        it += 1
+    eng.iterations(it, args.steps)
+    it += args.steps
     eng.synchronize()
     cuda_sync()
     D.barrier()

@@ -52,6 +52,9 @@ typedef struct {
      * device generator its phases: stream slice, attempt tables, host walk, values */
     int64_t pool_calls, pool_entries, pool_device_calls;
     double  t_pool_ms, t_pool_mt_ms, t_pool_accept_ms, t_pool_parse_ms, t_pool_values_ms;
+    /* update_phi speculated while the device sweeps: passes run, and clusters whose
+     * speculative draws were kept (the sweep left them untouched) */
+    int64_t phi_spec_runs, phi_spec_clusters;
 } hdpm_stats;
 
 int         hdpm_device_count(void);
@@ -119,6 +122,12 @@ int hdpm_run_markov_chain(hdpm_ctx* ctx, const hdpm_chain_params* p, const int32
 int hdpm_init_chain(hdpm_ctx* ctx, const hdpm_chain_params* p, const int32_t* c_i_init);
 int hdpm_iteration(hdpm_ctx* ctx, const hdpm_chain_params* p, int32_t iter, int32_t* idx_1_sm,
                    int32_t* accepted, double* loglik);
+/* `count` consecutive iterations iter0 .. iter0+count-1 (accepted / loglik: count entries
+ * each, may be NULL).  Same chain as calling hdpm_iteration for each; between two
+ * iterations of the batch the next sweep is launched on the device before this call's
+ * host work for the current one is done (the loop of la:85-154 without R in between). */
+int hdpm_iterations(hdpm_ctx* ctx, const hdpm_chain_params* p, int32_t iter0, int32_t count, int32_t* idx_1_sm,
+                    int32_t* accepted, double* loglik);
 
 /* Diagnostics / testing. */
 /* Draw `count` raw 32-bit MT outputs (MT_genrand before scaling) on the device and advance
@@ -132,7 +141,9 @@ int hdpm_reset_stats(hdpm_ctx* ctx);
  * snapshot speculation (the resolver decides every uncertain point itself); bit 4: recount
  * the frequency tables every update_phi (no incremental move log); bit 5: accumulate a host
  * timeline of hdpm_iteration (printed to stderr when the context is destroyed); bit 6:
- * generate latent pools with the sequential host generator instead of the device one. */
+ * generate latent pools with the sequential host generator instead of the device one; bit 7:
+ * no speculative update_phi during the sweep; bit 8: no next sweep prepared at the end of
+ * an iteration. */
 int hdpm_set_debug(hdpm_ctx* ctx, int32_t mode);
 /* Block until all device work of the context is done. */
 int hdpm_synchronize(hdpm_ctx* ctx);

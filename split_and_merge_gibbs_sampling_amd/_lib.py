@@ -22,7 +22,7 @@ EXPORTS = (
     "hdpm_set_pool", "hdpm_get_pool", "hdpm_generate_pool", "hdpm_neal8_sweep", "hdpm_update_phi",
     "hdpm_compute_loglikelihood", "hdpm_loglik_matrix", "hdpm_restricted_gibbs", "hdpm_logprobgs_c_i",
     "hdpm_split_and_merge", "hdpm_run_markov_chain", "hdpm_get_stats", "hdpm_reset_stats",
-    "hdpm_set_debug", "hdpm_synchronize", "hdpm_init_chain", "hdpm_iteration", "hdpm_rng_fill_device",
+    "hdpm_set_debug", "hdpm_synchronize", "hdpm_init_chain", "hdpm_iteration", "hdpm_iterations", "hdpm_rng_fill_device",
 )
 
 STATUS = {0: "OK", 1: "E_VALIDATE", 2: "E_GSL", 3: "E_PROB", 4: "E_WALKER", 5: "E_ARG",
@@ -49,7 +49,8 @@ class Stats(C.Structure):
             "t_exact_ms")] + \
         [(n, C.c_int64) for n in ("pool_calls", "pool_entries", "pool_device_calls")] + \
         [(n, C.c_double) for n in (
-            "t_pool_ms", "t_pool_mt_ms", "t_pool_accept_ms", "t_pool_parse_ms", "t_pool_values_ms")]
+            "t_pool_ms", "t_pool_mt_ms", "t_pool_accept_ms", "t_pool_parse_ms", "t_pool_values_ms")] + \
+        [(n, C.c_int64) for n in ("phi_spec_runs", "phi_spec_clusters")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -102,6 +103,7 @@ def lib():
         "hdpm_get_stats": ([vp, P(Stats)], C.c_int),
         "hdpm_init_chain": ([vp, P(ChainParams), vp], C.c_int),
         "hdpm_iteration": ([vp, P(ChainParams), i32, P(i32), P(i32), P(f64)], C.c_int),
+        "hdpm_iterations": ([vp, P(ChainParams), i32, i32, P(i32), vp, vp], C.c_int),
         "hdpm_reset_stats": ([vp], C.c_int),
         "hdpm_rng_fill_device": ([vp, i64, vp], C.c_int),
         "hdpm_set_debug": ([vp, i32], C.c_int),

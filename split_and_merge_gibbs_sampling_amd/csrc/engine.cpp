@@ -413,6 +413,16 @@ struct Ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t gstream = nullptr;   // random-stream generator
+  hipStream_t cstream = nullptr;   // copies of stream states to the host (never queued behind a generator launch)
+  // update_phi's slice of the stream copied from the window that holds it (StreamAhead::fill_raw)
+  struct PhiDev {
+    bool valid = false;
+    uint64_t pos = 0, epoch = 0;
+    int mti = 0;
+    int64_t N = 0;
+    hipEvent_t ev = nullptr;
+    PinBuf<uint32_t> raw, arrays;
+  } phidev;
   RngWindow win[2];
   // MT jump-ahead for multi-workgroup windows (mtjump.hpp)
   int mt_G = 0, mt_bpg = 0;
@@ -452,6 +462,7 @@ struct Ctx {
   int K = 0;
   std::vector<int32_t> h_c;
   bool host_c_valid = false;
+  bool host_c_device = false;         // h_c is a copy of the device labels (nothing to validate)
   std::vector<int32_t> h_counts;      // per label
   std::vector<uint8_t> h_center;      // K x d codes
   std::vector<double> h_sigma;        // K x d
@@ -515,9 +526,12 @@ struct Ctx {
   DevBuf<long long> d_rprof;          // resolver phase times (debug mode bit 1)
   PinBuf<int> h_ctl;
   // cluster parameter upload staging (UploadLayout)
-  PinBuf<uint8_t> h_stage;
+  // two pinned staging buffers: one can be filled (e.g. by the update_phi speculated for the
+  // next sweep) while the last commit's copy from the other is still in flight
+  PinBuf<uint8_t> h_stage_buf[2];
+  hipEvent_t ev_stage_buf[2] = {nullptr, nullptr};
+  int stage_fill = 0, stage_last = 1;   // buffer being filled / last committed
   DevBuf<uint8_t> d_stage;
-  hipEvent_t ev_stage = nullptr;
 
   // statistics buffers.  d_freq holds freq[slot][j][level] and, while freq_dev_valid,
   // follows the labels through the sweeps incrementally (resolver move log); d_freq_m
@@ -553,6 +567,10 @@ struct Ctx {
   std::vector<int> sperm;
 
   ~Ctx() {
+    try {
+      cancel_ahead();
+    } catch (...) {
+    }
     if (trace_iters > 0) {
       std::string line = "[timeline] mean us/iteration:";
       for (auto& kv : trace_sum) {
@@ -562,6 +580,11 @@ struct Ctx {
       }
       std::fprintf(stderr, "%s (%lld iterations, %lld device allocations after the first)\n", line.c_str(),
                    (long long)trace_iters, (long long)(g_dev_allocs.load() - trace_alloc0));
+    }
+    if (cstream) {
+      (void)hipStreamSynchronize(cstream);
+      if (phidev.ev) (void)hipEventDestroy(phidev.ev);
+      (void)hipStreamDestroy(cstream);
     }
     if (gstream) {
       (void)hipStreamSynchronize(gstream);
@@ -573,7 +596,8 @@ struct Ctx {
     if (stream) {
       (void)hipStreamSynchronize(stream);
       for (auto& e : ev) (void)hipEventDestroy(e);
-      if (ev_stage) (void)hipEventDestroy(ev_stage);
+      for (auto& e : ev_stage_buf)
+        if (e) (void)hipEventDestroy(e);
       (void)hipStreamDestroy(stream);
     }
   }
@@ -603,6 +627,11 @@ struct Ctx {
     W.export_from = (int)std::max<int64_t>(1, (export_after - head) / 624 - 1);
     W.export_after = export_after;
   }
+  // a generator launch may overwrite buffers the copy stream still reads
+  void gstream_after_copies() {
+    if (pend.ev) HIPCHK(hipStreamWaitEvent(gstream, pend.ev, 0));
+    if (phidev.ev) HIPCHK(hipStreamWaitEvent(gstream, phidev.ev, 0));
+  }
   void run_window(RngWindow& W) {
     ensure_jump(W.count);
     const bool multi = mt_G > 1 && W.count >= (int64_t)mt_G * 624 * 8;
@@ -627,6 +656,7 @@ struct Ctx {
       rng.mti = 624;
     }
     HIPCHK(hipStreamSynchronize(gstream));  // previous use of W's buffers is complete
+    if (cstream) HIPCHK(hipStreamSynchronize(cstream));
     W.mti0 = rng.mti;
     W.start_pos = rng.pos;
     W.epoch = rng.epoch;
@@ -662,6 +692,7 @@ struct Ctx {
     Wn.mti0 = mti;
     Wn.start_pos = target;
     Wn.epoch = rng.epoch;
+    gstream_after_copies();
     size_window(Wn, count, export_after);
     if (blk == 0) {
       // inside Ws's initial array, which may live in Wn's own exports: copy it out first
@@ -766,36 +797,79 @@ struct Ctx {
     int mti;
     locate(W, target, &blk, &mti);
     if (!pend.ev) HIPCHK(hipEventCreateWithFlags(&pend.ev, hipEventDisableTiming));
+    HIPCHK(hipStreamWaitEvent(cstream, W.done, 0));
     if (blk == 0) {
       pend.host_src = W.h_init.p;     // valid once W's init has landed (W.done)
     } else {
       pend.arr.ensure(624);
       pend.host_src = nullptr;
-      HIPCHK(hipMemcpyAsync(pend.arr.p, W.arrays.p + (blk - 1) * 624, 624 * 4, hipMemcpyDeviceToHost, gstream));
+      HIPCHK(hipMemcpyAsync(pend.arr.p, W.arrays.p + (blk - 1) * 624, 624 * 4, hipMemcpyDeviceToHost, cstream));
     }
-    HIPCHK(hipEventRecord(pend.ev, gstream));
+    HIPCHK(hipEventRecord(pend.ev, cstream));
     pend.mti = mti;
     pend.active = true;
     rng.pos = target;
   }
 
+  // update_phi's slice [target, target + N) with the state arrays of its twists, copied from
+  // window W when it holds them (else the host generates the slice itself).
+  void phi_device_prefetch(const RngWindow& W, uint64_t target, int64_t N) {
+    phidev.valid = false;
+    if (target + (uint64_t)N > W.start_pos + (uint64_t)W.count) return;
+    int64_t blk;
+    int mti;
+    locate(W, target, &blk, &mti);
+    if (blk == 0) return;
+    const int64_t first = mti >= 624 ? 0 : 624 - mti;
+    const int64_t nb = N > first ? (N - first + 623) / 624 : 0;   // twists inside the slice
+    if (blk + nb > W.nblocks) return;
+    // with headroom: a pinned reallocation (hipHostFree) would synchronise the device
+    if (phidev.raw.n < (size_t)N) phidev.raw.ensure(std::max<size_t>(2 * (size_t)N, 1 << 15));
+    if (phidev.arrays.n < (size_t)(nb + 1) * 624) phidev.arrays.ensure((size_t)(2 * nb + 64) * 624);
+    if (!phidev.ev) HIPCHK(hipEventCreateWithFlags(&phidev.ev, hipEventDisableTiming));
+    HIPCHK(hipMemcpyAsync(phidev.raw.p, W.raw.p + (target - W.start_pos), (size_t)N * 4, hipMemcpyDeviceToHost, cstream));
+    HIPCHK(hipMemcpyAsync(phidev.arrays.p, W.arrays.p + (blk - 1) * 624, (size_t)(nb + 1) * 624 * 4,
+                          hipMemcpyDeviceToHost, cstream));
+    HIPCHK(hipEventRecord(phidev.ev, cstream));
+    phidev.valid = true;
+    phidev.pos = target;
+    phidev.epoch = rng.epoch;
+    phidev.mti = mti;
+    phidev.N = N;
+  }
+
   // Device pointer to the next n raw draws of the stream; advances the host stream past
   // them and starts generating the following window from where they end.
+  //
+  // Windows span many sweeps (`window_span`): one jump-ahead + twist launch serves ~16
+  // sweeps and the draws between them, instead of one launch (dominated by the jump) per
+  // sweep.  The next window is launched from the end of the current sweep's draws when the
+  // current one has fewer than `kLead` sweeps' worth left, so it is ready well before use.
+  static constexpr int kLead = 3;
+  int64_t window_span(int64_t n) const {
+    const int64_t per = n + cmax;
+    const int64_t cap = (int64_t)1 << 27;      // 512 MB of draws (+ 512 MB of exported arrays)
+    return std::max(per, std::min<int64_t>(16 * per, cap));
+  }
   const uint32_t* device_draws(int64_t n) {
     RngWindow* W = nullptr;
     for (auto& w : win)
-      if (covers(w, rng.pos, n)) W = &w;
+      if (covers(w, rng.pos, n) && (!W || w.start_pos < W->start_pos)) W = &w;
     if (!W) {
       if (win[0].valid || win[1].valid) cmax = std::min<int64_t>(cmax * 2, 1 << 26);
       W = &win[0];
-      launch_window(*W, n, n);
+      launch_window(*W, window_span(n), n);
     }
     HIPCHK(hipStreamWaitEvent(stream, W->done, 0));
     const uint32_t* p = W->raw.p + (rng.pos - W->start_pos);
     const uint64_t target = rng.pos + n;
     adopt_state_at(*W, target);
+    phi_device_prefetch(*W, target, phi_prefetch);
     RngWindow* other = (W == &win[0]) ? &win[1] : &win[0];
-    launch_window_from(*other, *W, target, n + cmax, n);
+    const bool ahead = other->valid && other->epoch == rng.epoch && other->start_pos > W->start_pos;
+    const uint64_t wend = W->start_pos + (uint64_t)W->count;
+    if (!ahead && wend < target + (uint64_t)(kLead * (n + cmax)))
+      launch_window_from(*other, *W, target, window_span(n), n);
     return p;
   }
 
@@ -862,14 +936,18 @@ struct Ctx {
   // stage_commit (copy + scatter).
   UploadLayout stage_begin(int nent) {
     const UploadLayout L = upload_layout(nent, dp, d, bw);
-    if (!ev_stage) HIPCHK(hipEventCreateWithFlags(&ev_stage, hipEventDisableTiming));
-    HIPCHK(hipEventSynchronize(ev_stage));          // the previous upload has left h_stage
-    h_stage.ensure(L.bytes);
+    stage_fill = 1 - stage_last;
+    hipEvent_t& ev = ev_stage_buf[stage_fill];
+    if (!ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    HIPCHK(hipEventSynchronize(ev));                // the upload before last has left this buffer
+    PinBuf<uint8_t>& hb = h_stage_buf[stage_fill];
+    if (hb.n < L.bytes) hb.ensure(L.bytes + L.bytes / 2 + 4096);
     d_stage.ensure(L.bytes);
     return L;
   }
+  uint8_t* stage_ptr() { return h_stage_buf[stage_fill].p; }
   void stage_entry(const UploadLayout& L, int r, int k) {
-    uint8_t* st = h_stage.p;
+    uint8_t* st = stage_ptr();
     double* tt = (double*)(st + L.off_tab) + (size_t)r * 2 * d;
     tables_for(&h_center[(size_t)k * d], &h_sigma[(size_t)k * d], st + L.off_codes + (size_t)r * dp, tt);
     bounds_for(&h_center[(size_t)k * d], tt, (uint64_t*)(st + L.off_bnd) + (size_t)r * bw);
@@ -877,8 +955,9 @@ struct Ctx {
     ((int*)(st + L.off_slot))[r] = k;
   }
   void stage_commit(const UploadLayout& L, int nent, bool full) {
-    HIPCHK(hipMemcpyAsync(d_stage.p, h_stage.p, L.bytes, hipMemcpyHostToDevice, stream));
-    HIPCHK(hipEventRecord(ev_stage, stream));
+    HIPCHK(hipMemcpyAsync(d_stage.p, stage_ptr(), L.bytes, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipEventRecord(ev_stage_buf[stage_fill], stream));
+    stage_last = stage_fill;
     stage_full = full;
     HIPCHK(launch_scatter_clusters(d_stage.p, nent, dp, d, bw, full ? 1 : 0, d_slot_codes.p, d_slot_tab.p,
                                    d_slot_bnd.p, d_counts.p, d_sol.p, d_los.p, d_src.p, stream));
@@ -908,6 +987,7 @@ struct Ctx {
     HIPCHK(hipMemcpyAsync(h_c.data(), d_c.p, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
     HIPCHK(hipStreamSynchronize(stream));
     host_c_valid = true;
+    host_c_device = true;
   }
 
   void upload_labels() {
@@ -917,6 +997,7 @@ struct Ctx {
     freq_dev_valid = false;
     HIPCHK(hipStreamSynchronize(stream));
     host_c_valid = true;
+    host_c_device = false;
   }
 
   void recount() {
@@ -1308,38 +1389,8 @@ struct Ctx {
   }
 
   // ------------------------------------------------------------------ Neal-8 sweep
-  int neal8_sweep(int m) {
-    if (!have_state) { err = "no state"; return kArg; }
-    if (P <= 0) { err = "no latent pool"; return kArg; }
-    if (m <= 0) { err = "m must be positive"; return kArg; }
-    // validate_state before the first case (the reference stops at the first point)
-    {
-      if (!host_c_valid) { /* device labels are always consistent with K */ }
-      else {
-        std::vector<char> seen(K + 1, 0);
-        int u = 0;
-        for (int i = 0; i < n; ++i) {
-          const int c = h_c[i];
-          if (c >= K) { err = "State validation failed: inconsistent cluster count"; return kValidate; }
-          if (!seen[c]) { seen[c] = 1; u++; }
-        }
-        if (u != K) { err = "State validation failed: inconsistent cluster count"; return kValidate; }
-      }
-    }
-    if (tables_dirty) upload_clusters();
-    labels_version++;
-    const int K0 = K;
-    std::vector<uint8_t> old_center = h_center;
-    std::vector<double> old_sigma = h_sigma;
-
-    // the sweep's slice of the R stream (m pick uniforms + 1 categorical per point),
-    // generated on the device; the host stream continues after it
-    auto tr0 = std::chrono::steady_clock::now();
-    const size_t nraw = (size_t)n * (m + 1);
-    const uint32_t* d_sweep_raw = device_draws((int64_t)nraw);
-    mark("draws");
-    stats.t_rng_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count();
-
+  // Buffers of a sweep (sized for n).
+  void sweep_buffers(bool track) {
     const int nb_max = (n + kBlock - 1) / kBlock;
     d_margin.ensure(n);
     d_rowpos.ensure(n);
@@ -1350,97 +1401,223 @@ struct Ctx {
     d_spec.ensure((size_t)nb_max * kBlock);
     d_spec_rad.ensure((size_t)nb_max * kBlock);
     d_rq.ensure((size_t)nb_max * kBlock);
-
-    int nslots = K;
-    int p = 0;
-    const double dmax = 0.25;
-    const int64_t rounds0 = stats.rounds;
-    const bool track = freq_dev_valid;
     if (track) {
       d_mlog.ensure((size_t)3 * n);
       d_mcount.ensure(1);
       HIPCHK(hipMemsetAsync(d_mcount.p, 0, 4, stream));
     }
-    while (p < n) {
-      ensure_slots(nslots + 2);
-      d_ctl.ensure(8 + 3 * (size_t)scap);
-      h_ctl.ensure(8 + 3 * (size_t)scap);
-      const int S = nslots;
-      if (S + m > Ecap) {
-        Ecap = std::max(S + m, std::max(2 * Ecap, 32));
-        d_L.ensure((size_t)Ecap * n);
-      }
-      const int E = K + m;
-      const double T = 54.0 * M_LN2 + std::log((double)E) + 0.5;
-      PrepassArgs pa;
-      pa.codes_t = d_codes_t.p; pa.n = n; pa.d = d; pa.nq = nq;
-      pa.c = d_c.p; pa.counts = d_counts.p; pa.slot_of_label = d_sol.p; pa.K = K; pa.S = S;
-      pa.slots = ParamTables{d_slot_codes.p, d_slot_tab.p};
-      pa.pool = ParamTables{d_pool_codes.p, d_pool_tab.p};
-      pa.P = P; pa.raw = d_sweep_raw; pa.m = m; pa.logn = d_logn.p; pa.logfac = std::log(gamma / m);
-      pa.xbs = d_xbs.p; pa.Ws = Ws; pa.wb = wb; pa.slot_bnd = d_slot_bnd.p; pa.pool_bnd = d_pool_bnd.p; pa.bw = bw;
-      d_csum.ensure((size_t)std::max(K, 1) * (bw + 2));
-      pa.csum = d_csum.p;
+  }
 
-      pa.thresh = (debug & 1) ? INFINITY : T + 2.0 * dmax;
-      pa.L = d_L.p; pa.rowpos = d_rowpos.p; pa.margin = d_margin.p; pa.list = d_list.p; pa.cnt = d_cnt.p;
-      pa.dense = d_dense.p; pa.dense_total = d_dense_total.p;
-      pa.spec = (debug & 8) ? nullptr : d_spec.p;
-      pa.spec_rad = d_spec_rad.p;
-      pa.rq = d_rq.p;
-      pa.p0 = p;
-      const int nblocks = (n - p + kBlock - 1) / kBlock;
-      HIPCHK(launch_cluster_summary(pa, stream));
-      HIPCHK(hipEventRecord(ev[0], stream));
-      HIPCHK(launch_prepass(pa, nblocks, stream));
-      stats.prepass_points += n - p;
-      HIPCHK(hipEventRecord(ev[1], stream));
-      HIPCHK(launch_exact_rows(pa, nblocks, stream));
-      HIPCHK(hipEventRecord(ev[5], stream));
+  // One launch of the sweep from point p with nslots slots: cluster summary, prepass, exact
+  // rows, resolver, control copy, and the sweep-end kernels behind it (they act only if
+  // this launch completes the sweep).  kOk or kArg (resolver state too large for LDS).
+  int launch_round(int p, int nslots, int m, const uint32_t* d_sweep_raw, bool track) {
+    const double dmax = 0.25;
+    ensure_slots(nslots + 2);
+    d_ctl.ensure(8 + 3 * (size_t)scap);
+    h_ctl.ensure(8 + 3 * (size_t)scap);
+    const int S = nslots;
+    if (S + m > Ecap) {
+      Ecap = std::max(S + m, std::max(2 * Ecap, 32));
+      d_L.ensure((size_t)Ecap * n);
+    }
+    const int E = K + m;
+    const double T = 54.0 * M_LN2 + std::log((double)E) + 0.5;
+    PrepassArgs pa;
+    pa.codes_t = d_codes_t.p; pa.n = n; pa.d = d; pa.nq = nq;
+    pa.c = d_c.p; pa.counts = d_counts.p; pa.slot_of_label = d_sol.p; pa.K = K; pa.S = S;
+    pa.slots = ParamTables{d_slot_codes.p, d_slot_tab.p};
+    pa.pool = ParamTables{d_pool_codes.p, d_pool_tab.p};
+    pa.P = P; pa.raw = d_sweep_raw; pa.m = m; pa.logn = d_logn.p; pa.logfac = std::log(gamma / m);
+    pa.xbs = d_xbs.p; pa.Ws = Ws; pa.wb = wb; pa.slot_bnd = d_slot_bnd.p; pa.pool_bnd = d_pool_bnd.p; pa.bw = bw;
+    d_csum.ensure((size_t)std::max(K, 1) * (bw + 2));
+    pa.csum = d_csum.p;
 
-      ResolveArgs ra;
-      ra.n = n; ra.d = d; ra.dp = dp; ra.m = m; ra.P = P;
-      ra.c = d_c.p; ra.counts = d_counts.p; ra.slot_of_label = d_sol.p; ra.label_of_slot = d_los.p;
-      ra.slot_src = d_src.p; ra.slot_codes = d_slot_codes.p; ra.slot_tab = d_slot_tab.p;
-      ra.pool = pa.pool; ra.raw = d_sweep_raw; ra.logn = d_logn.p; ra.logfac = pa.logfac;
-      ra.L = d_L.p; ra.rowpos = d_rowpos.p; ra.slot_bnd = d_slot_bnd.p; ra.pool_bnd = d_pool_bnd.p; ra.bw = bw;
-      ra.S = S; ra.margin = d_margin.p; ra.list = d_list.p; ra.dense = d_dense.p; ra.dense_total = d_dense_total.p;
-      ra.spec = pa.spec;
-      ra.spec_rad = pa.spec_rad;
-      ra.rq = pa.rq;
-      ra.nblocks = nblocks; ra.p0 = p; ra.T = T; ra.dmax = dmax; ra.scap = scap; ra.K = K;
-      ra.lcap = std::min(scap, nslots + 2);
-      ra.nslots = nslots; ra.ctl = (ResolveCtl*)d_ctl.p; ra.summary = d_ctl.p + 8; ra.force_exact = (debug & 1);
-      ra.prof = nullptr;
-      ra.mlog = track ? d_mlog.p : nullptr;
-      ra.mcount = track ? d_mcount.p : nullptr;
-      ra.freq = track ? d_freq.p : nullptr;
-      ra.fstride = d * mmax;
-      if (debug & 2) {
-        d_rprof.ensure(16);
-        ra.prof = d_rprof.p;
+    pa.thresh = (debug & 1) ? INFINITY : T + 2.0 * dmax;
+    pa.L = d_L.p; pa.rowpos = d_rowpos.p; pa.margin = d_margin.p; pa.list = d_list.p; pa.cnt = d_cnt.p;
+    pa.dense = d_dense.p; pa.dense_total = d_dense_total.p;
+    pa.spec = (debug & 8) ? nullptr : d_spec.p;
+    pa.spec_rad = d_spec_rad.p;
+    pa.rq = d_rq.p;
+    pa.p0 = p;
+    const int nblocks = (n - p + kBlock - 1) / kBlock;
+    HIPCHK(launch_cluster_summary(pa, stream));
+    HIPCHK(hipEventRecord(ev[0], stream));
+    HIPCHK(launch_prepass(pa, nblocks, stream));
+    stats.prepass_points += n - p;
+    HIPCHK(hipEventRecord(ev[1], stream));
+    HIPCHK(launch_exact_rows(pa, nblocks, stream));
+    HIPCHK(hipEventRecord(ev[5], stream));
+
+    ResolveArgs ra;
+    ra.n = n; ra.d = d; ra.dp = dp; ra.m = m; ra.P = P;
+    ra.c = d_c.p; ra.counts = d_counts.p; ra.slot_of_label = d_sol.p; ra.label_of_slot = d_los.p;
+    ra.slot_src = d_src.p; ra.slot_codes = d_slot_codes.p; ra.slot_tab = d_slot_tab.p;
+    ra.pool = pa.pool; ra.raw = d_sweep_raw; ra.logn = d_logn.p; ra.logfac = pa.logfac;
+    ra.L = d_L.p; ra.rowpos = d_rowpos.p; ra.slot_bnd = d_slot_bnd.p; ra.pool_bnd = d_pool_bnd.p; ra.bw = bw;
+    ra.S = S; ra.margin = d_margin.p; ra.list = d_list.p; ra.dense = d_dense.p; ra.dense_total = d_dense_total.p;
+    ra.spec = pa.spec;
+    ra.spec_rad = pa.spec_rad;
+    ra.rq = pa.rq;
+    ra.nblocks = nblocks; ra.p0 = p; ra.T = T; ra.dmax = dmax; ra.scap = scap; ra.K = K;
+    ra.lcap = std::min(scap, nslots + 2);
+    ra.nslots = nslots; ra.ctl = (ResolveCtl*)d_ctl.p; ra.summary = d_ctl.p + 8; ra.force_exact = (debug & 1);
+    ra.prof = nullptr;
+    ra.mlog = track ? d_mlog.p : nullptr;
+    ra.mcount = track ? d_mcount.p : nullptr;
+    ra.freq = track ? d_freq.p : nullptr;
+    ra.fstride = d * mmax;
+    if (debug & 2) {
+      d_rprof.ensure(16);
+      ra.prof = d_rprof.p;
+    }
+    if (resolve_smem_bytes(ra.lcap, m) > 160 * 1024) { err = "too many clusters for the resolver (K > ~2300)"; return kArg; }
+    HIPCHK(launch_resolve(ra, stream));
+    HIPCHK(hipEventRecord(ev[2], stream));
+    HIPCHK(hipMemcpyAsync(h_ctl.p, d_ctl.p, (8 + 3 * (size_t)scap) * 4, hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipEventRecord(ev[6], stream));
+    {
+      // the sweep end, enqueued now: it runs only if this launch completes the sweep
+      const ResolveCtl* dctl = (const ResolveCtl*)d_ctl.p;
+      HIPCHK(launch_relabel(d_c.p, d_los.p, n, dctl, stream));
+      if (track) {   // carry the frequency tables: apply the moves, re-index slots -> labels
+        HIPCHK(launch_apply_moves(d_mlog.p, d_mcount.p, (int)std::min<int64_t>(n, 4096), d_codes_t.p, d, nq, mmax,
+                                  d_freq.p, dctl, n, stream));
+        HIPCHK(launch_freq_gather(d_freq.p, d_sol.p, std::min(scap, S + 2), d * mmax, d_freq2.p, dctl, n, stream));
+        const size_t fwords = (size_t)std::min(scap, S + 2) * d * mmax;
+        h_freq_next.ensure(fwords);
+        HIPCHK(hipMemcpyAsync(h_freq_next.p, d_freq2.p, fwords * 4, hipMemcpyDeviceToHost, stream));
       }
-      if (resolve_smem_bytes(ra.lcap, m) > 160 * 1024) { err = "too many clusters for the resolver (K > ~2300)"; return kArg; }
-      HIPCHK(launch_resolve(ra, stream));
-      HIPCHK(hipEventRecord(ev[2], stream));
-      HIPCHK(hipMemcpyAsync(h_ctl.p, d_ctl.p, (8 + 3 * (size_t)scap) * 4, hipMemcpyDeviceToHost, stream));
-      HIPCHK(hipEventRecord(ev[6], stream));
-      {
-        // the sweep end, enqueued now: it runs only if this launch completes the sweep
-        const ResolveCtl* dctl = (const ResolveCtl*)d_ctl.p;
-        HIPCHK(launch_relabel(d_c.p, d_los.p, n, dctl, stream));
-        if (track) {   // carry the frequency tables: apply the moves, re-index slots -> labels
-          HIPCHK(launch_apply_moves(d_mlog.p, d_mcount.p, (int)std::min<int64_t>(n, 4096), d_codes_t.p, d, nq, mmax,
-                                    d_freq.p, dctl, n, stream));
-          HIPCHK(launch_freq_gather(d_freq.p, d_sol.p, std::min(scap, S + 2), d * mmax, d_freq2.p, dctl, n, stream));
-          const size_t fwords = (size_t)std::min(scap, S + 2) * d * mmax;
-          h_freq.ensure(fwords);
-          HIPCHK(hipMemcpyAsync(h_freq.p, d_freq2.p, fwords * 4, hipMemcpyDeviceToHost, stream));
+      HIPCHK(launch_finish_sweep(d_counts.p, d_sol.p, d_los.p, d_src.p, scap, dctl, n, stream));
+    }
+    return kOk;
+  }
+
+  // The next sweep prepared at the end of an iteration (prepare_next_sweep): its draws
+  // reserved (their stream slice and update_phi's are copied out) and update_phi speculated
+  // on the pool, while the caller returns and comes back to launch the sweep.  Any other
+  // entry point cancels it (cancel_ahead): the job is joined and the stream rewound to
+  // where the sweep would have started.
+  struct Ahead {
+    bool active = false;
+    int m = 0;
+    uint64_t lv = 0;
+    Rng saved;
+    const uint32_t* raw = nullptr;
+    bool launched = false;             // round 0 of the sweep is already on the device
+    bool track = false;
+  } ahead;
+
+  // With `launch` (only when the caller runs the sweep next, no other call in between:
+  // a launched sweep cannot be cancelled), round 0 of the sweep is launched too, so the
+  // device goes on from this iteration's uploads without waiting for the host.
+  void prepare_next_sweep(int m, bool launch) {
+    if (ahead.active || !have_state || P <= 0 || m <= 0 || tables_dirty || (debug & (256 | 128 | 16))) return;
+    if (!(freq_dev_valid && freq_version == labels_version)) return;
+    rng_sync();
+    ahead.saved = rng;
+    ahead.raw = device_draws((int64_t)n * (m + 1));
+    ahead.m = m;
+    ahead.lv = labels_version;
+    ahead.launched = false;
+    ahead.active = true;
+    spec_launch();
+    if (launch && resolve_smem_bytes(std::min(scap, K + 2), m) <= 160 * 1024) {
+      ahead.track = freq_dev_valid;
+      sweep_buffers(ahead.track);
+      if (launch_round(0, K, m, ahead.raw, ahead.track) == kOk) ahead.launched = true;
+    }
+  }
+  void cancel_ahead() {
+    if (!ahead.active) return;
+    ahead.active = false;
+    if (ahead.launched) {
+      // a launched sweep cannot be taken back: the chain state is no longer defined
+      (void)hipStreamSynchronize(stream);
+      have_state = false;
+      err = "a prepared sweep was abandoned";
+    }
+    if (spec.ran) {
+      if (!spec.joined && pj_open) (void)pj_finish();
+      spec.ran = false;
+    }
+    phi_stream.n = 0;
+    pend.active = false;
+    rng = ahead.saved;
+  }
+
+  int neal8_sweep(int m) {
+    // the sweep prepared at the end of the last iteration (prepare_next_sweep), if nothing
+    // has changed since
+    const bool use_ahead = ahead.active && ahead.m == m && ahead.lv == labels_version && !tables_dirty;
+    if (!use_ahead) cancel_ahead();
+    if (!have_state) { err = "no state"; return kArg; }
+    if (P <= 0) { err = "no latent pool"; return kArg; }
+    if (m <= 0) { err = "m must be positive"; return kArg; }
+    // validate_state before the first case (the reference stops at the first point)
+    {
+      if (!host_c_valid || host_c_device) { /* device labels are always consistent with K */ }
+      else {
+        std::vector<char> seen(K + 1, 0);
+        int u = 0;
+        for (int i = 0; i < n; ++i) {
+          const int c = h_c[i];
+          if (c >= K) { cancel_ahead(); err = "State validation failed: inconsistent cluster count"; return kValidate; }
+          if (!seen[c]) { seen[c] = 1; u++; }
         }
-        HIPCHK(launch_finish_sweep(d_counts.p, d_sol.p, d_los.p, d_src.p, scap, dctl, n, stream));
+        if (u != K) { cancel_ahead(); err = "State validation failed: inconsistent cluster count"; return kValidate; }
+      }
+    }
+    if (tables_dirty) upload_clusters();
+    // update_phi can be speculated during the sweep when the host holds the pre-sweep
+    // frequency tables of every label and the sweep carries them (move log)
+    const bool spec_go = freq_dev_valid && freq_version == labels_version && !(debug & (128 | 16));
+    if (!use_ahead) spec.ran = false;
+    spec.lv = 0;
+    labels_version++;
+    const int K0 = K;
+    int sweep_moves = 0;
+    std::vector<uint8_t> old_center = h_center;
+    std::vector<double> old_sigma = h_sigma;
+
+    // the sweep's slice of the R stream (m pick uniforms + 1 categorical per point),
+    // generated on the device; the host stream continues after it
+    auto tr0 = std::chrono::steady_clock::now();
+    const size_t nraw = (size_t)n * (m + 1);
+    const uint32_t* d_sweep_raw = use_ahead ? ahead.raw : device_draws((int64_t)nraw);
+    const bool ahead_launched = use_ahead && ahead.launched;
+    ahead.active = false;
+    mark("draws");
+    // update_phi speculated on the pool while this thread launches the sweep
+    struct SpecGuard {
+      Ctx* c;
+      ~SpecGuard() {
+        if (c->spec.ran && !c->spec.joined && c->pj_open) {   // not joined (early exit)
+          (void)c->pj_finish();
+          c->spec.ran = false;
+        }
+      }
+    } spec_guard{this};
+    if (spec_go && !use_ahead) spec_launch();
+    stats.t_rng_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count();
+
+    int nslots = K;
+    int p = 0;
+    const int64_t rounds0 = stats.rounds;
+    // round 0 may already be on the device (prepare_next_sweep with launch)
+    const bool launched_ahead = ahead_launched;
+    const bool track = launched_ahead ? ahead.track : freq_dev_valid;
+    if (!launched_ahead) sweep_buffers(track);
+    while (p < n) {
+      if (!(launched_ahead && stats.rounds == rounds0)) {
+        const int lst = launch_round(p, nslots, m, d_sweep_raw, track);
+        if (lst) return lst;
       }
       mark("launched");
-      if (stats.rounds == rounds0) prefill_phi_stream();   // hidden behind the device work
+      if (stats.rounds == rounds0) {   // hidden behind the device work
+        if (spec.ran) spec_join();
+        else prefill_phi_stream();
+      }
       mark("prefill");
       HIPCHK(hipEventSynchronize(ev[6]));
       mark("resolved");
@@ -1464,6 +1641,7 @@ struct Ctx {
       }
       stats.exact_points += c.exact;
       stats.moves += c.moves;
+      sweep_moves += c.moves;
       stats.checked_rounds += c.checked;
       if (c.status) {
         err = c.status == kValidate ? "State validation failed: inconsistent cluster count from Neal8 case 2"
@@ -1487,6 +1665,7 @@ struct Ctx {
       std::swap(d_freq.p, d_freq2.p);
       std::swap(d_freq.n, d_freq2.n);
       freq_d2h_version = labels_version;
+      freq_next_pending = true;      // into h_freq_next; update_phi swaps it in
     }
     h_center.assign((size_t)K * d, 0);
     h_sigma.assign((size_t)K * d, 0.0);
@@ -1506,6 +1685,14 @@ struct Ctx {
     if (fetched && pool_on_device) HIPCHK(hipStreamSynchronize(stream));
     host_c_valid = false;
     tables_dirty = true;
+    if (spec.ran) {
+      // leading labels with the same slot (hence parameters) and count as at the speculation
+      spec.lv = labels_version;
+      spec.moves = sweep_moves;
+      int pfx = 0;
+      while (pfx < std::min(K, spec.K) && sol[pfx] == pfx && h_counts[pfx] == spec.counts[pfx]) ++pfx;
+      spec.pfx = pfx;
+    }
     mark("sweep_end");
     stats.t_stats_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
     stats.sweeps++;
@@ -1524,8 +1711,10 @@ struct Ctx {
     if (!mask && freq_dev_valid && !(debug & 16)) {
       // the per-label tables were carried through the sweep by the move log (and usually
       // copied out behind it already)
-      if (freq_d2h_version != labels_version)
+      if (freq_d2h_version != labels_version) {
         HIPCHK(hipMemcpyAsync(h_freq.p, d_freq.p, nent * 4, hipMemcpyDeviceToHost, stream));
+        freq_next_pending = false;
+      }
       return;
     }
     DevBuf<unsigned>& dst = mask ? d_freq_m : d_freq;
@@ -1549,7 +1738,10 @@ struct Ctx {
       ha.mask = d_mask.p;
     }
     HIPCHK(launch_hist(ha, stream));
-    if (!mask) freq_dev_valid = true;
+    if (!mask) {
+      freq_dev_valid = true;
+      freq_next_pending = false;
+    }
     HIPCHK(hipMemcpyAsync(h_freq.p, dst.p, nent * 4, hipMemcpyDeviceToHost, stream));
   }
   void histogram_wait(const std::vector<unsigned char>* mask) {
@@ -1557,17 +1749,6 @@ struct Ctx {
     freq_version = mask ? 0 : labels_version;
   }
 
-  // cf:511-591 with cluster sizes from h_counts and frequencies from the device, in three
-  // phases so that only the stream-consuming work is serial:
-  //   A (parallel)   per (cluster, attribute): center probabilities (cf:537-556),
-  //                  Rcpp sample's FixupProb / revsort / cumulative sums, and the rhig
-  //                  branch and rbeta setup for the most probable center;
-  //   B (serial)     the reference's draw order: per cluster, its d center uniforms, then
-  //                  its d sigma draws (rbeta rejection loops, or the bisection's Omega);
-  //   C (parallel)   sigma = -1/log(out) and the bisection solves, then the label tables.
-  // Every value is computed by the same expressions as the one-pass loop, so the chain is
-  // unchanged; on a norm_const2 failure the error is returned after phase B (the stream
-  // position then differs from the reference's, which stops at the failing draw).
   struct PhiItem {
     int err, lstar;
     bool bp;                 // rhig beta path for lstar
@@ -1580,6 +1761,51 @@ struct Ctx {
   std::vector<double> phi_cum;
   std::vector<int> phi_perm, phi_off;
 
+  // Speculative update_phi.  A Neal-8 sweep consumes exactly N (m + 1) uniforms whatever it
+  // decides, so the stream position of the update_phi that follows is known before the
+  // sweep runs, and update_phi of a cluster depends only on that cluster's size, frequency
+  // table and parameters.  While the device sweeps, the host runs update_phi on the
+  // pre-sweep state (spec_launch / spec_join); afterwards the results of the leading clusters the
+  // sweep left untouched (same slot, same count, same frequency table) are exactly
+  // update_phi's, and the draws resume from the stream offset where the first touched
+  // cluster's began.  A sweep without moves leaves every cluster untouched: update_phi is
+  // then done before the device finishes.
+  struct PhiSpec {
+    bool ran = false;
+    bool joined = false;               // spec_join collected the job
+    uint64_t lv = 0;                   // labels_version the results apply to (set at the sweep end)
+    uint64_t pos = 0, epoch = 0;       // stream position of the first draw
+    int K = 0;                         // labels at the speculation
+    int nvalid = 0;                    // clusters 0..nvalid-1 complete (no error, inside the prefetched stream)
+    int moves = -1;                    // reassignments of the sweep (set at its end)
+    int pfx = 0;                       // leading labels whose slot and count the sweep kept
+    std::vector<uint8_t> center;
+    std::vector<double> sigma;
+    std::vector<int> counts;
+    std::vector<int64_t> off;          // stream offset at the start of cluster t's draws
+  } spec;
+  Rng spec_live;                       // spill target of the speculative pass (never the chain's)
+  PinBuf<unsigned> h_freq_next;        // the sweep's frequency copy-out (h_freq keeps the pre-sweep one)
+  bool freq_next_pending = false;
+
+  // phi_stream from the chain's current state (after rng_sync): from the copy of the
+  // device window when it holds the slice, else generated here.  False if never seeded.
+  bool fill_phi_stream(int64_t N) {
+    StreamAhead& sa = phi_stream;
+    bool dev = phidev.valid && phidev.pos == rng.pos && phidev.epoch == rng.epoch && phidev.mti == rng.mti &&
+               phidev.N == N;
+    if (dev) {
+      HIPCHK(hipEventSynchronize(phidev.ev));
+      if (pj_open) pj.ns_f2.store(pj_ns());
+      dev = std::memcmp(phidev.arrays.p, rng.mt, sizeof(rng.mt)) == 0;
+    }
+    if (dev) {
+      sa.fill_raw(rng, phidev.raw.p, phidev.N, phidev.arrays.p + 624);
+      return true;
+    }
+    return sa.fill(rng, N);
+  }
+
   // update_phi's slice of the host stream, generated ahead (also called while the device
   // runs a sweep, which draws only from the device windows).
   void prefill_phi_stream() {
@@ -1587,294 +1813,530 @@ struct Ctx {
     rng_sync();
     StreamAhead& sa = phi_stream;
     if (sa.n > 0 && sa.used == 0 && sa.start.pos == rng.pos && sa.start.epoch == rng.epoch) return;
-    if (sa.fill(rng, phi_prefetch)) {
+    if (fill_phi_stream(phi_prefetch)) {
       sa.used = 0;
       HostPool::get().run(sa.n, 1024, [&](int64_t a0, int64_t a1) { sa.logits(a0, a1); });
     }
+  }
+
+  void stage_entry_from(const UploadLayout& L, int r, int k, const uint8_t* cen, const double* sig, int count) {
+    uint8_t* st = stage_ptr();
+    double* tt = (double*)(st + L.off_tab) + (size_t)r * 2 * d;
+    tables_for(cen, sig, st + L.off_codes + (size_t)r * dp, tt);
+    bounds_for(cen, tt, (uint64_t*)(st + L.off_bnd) + (size_t)r * bw);
+    ((int*)(st + L.off_counts))[r] = count;
+    ((int*)(st + L.off_slot))[r] = k;
+  }
+
+  // cf:511-591 as a pool job over the clusters touched[t0..T), with cluster sizes `counts`,
+  // frequencies `freq` (freq[k][j][level]) and current sigma from h_sigma, drawing from
+  // phi_stream.  The new centers / sigmas go to Cen / Sig (label-indexed), the label tables
+  // to the staging buffer L (entry k when `full`, else t).  Phases:
+  //   fill (one task)  the stream slice (phi_stream), when the job generates it;
+  //   logits           log(u / (1 - u)) and log(u u u') of the slice, in chunks;
+  //   A (parallel)     per (cluster, attribute): center probabilities (cf:537-556), Rcpp
+  //                    sample's FixupProb / revsort / cumulative sums, and the rhig branch and
+  //                    rbeta setup for the most probable center;
+  //   B (one thread)   the reference's draw order: per cluster, its d center uniforms, then
+  //                    its d sigma draws (rbeta rejection loops, or the bisection's Omega);
+  //   C (parallel)     sigma = -1/log(out) and the bisection solves, then the label tables.
+  // Every value is computed by the same expressions as the one-pass loop, so the chain is
+  // unchanged.  Tasks are handed out through shared counters; every thread (the caller
+  // too) takes what is ready, and a thread waiting on a dependency runs that dependency's
+  // tasks itself, so the job completes whichever threads the OS runs.
+  struct PhiJob {
+    std::vector<int> touched;
+    int t0 = 0, T = 0, nach = 1, achunk = 1, sumatt = 0;
+    const int* counts = nullptr;
+    const unsigned* freq = nullptr;
+    uint8_t* Cen = nullptr;
+    double* Sig = nullptr;
+    UploadLayout L{};
+    bool full = false;
+    int64_t* offs = nullptr;           // offs[t]: stream offset at the start of cluster t's draws
+    bool spec = false;                 // speculative: the slice is generated by the job from rng
+    int64_t fill_count = 0;
+    static constexpr int kLogitChunk = 1024;
+    std::atomic<int> fill{0};          // 0 open, 1 taken, 2 done
+    std::atomic<int> nextL{0}, doneL{0};
+    std::atomic<int> nL{0};
+    std::atomic<int> nextA{0};
+    std::unique_ptr<std::atomic<int>[]> stA, stB;
+    std::atomic<int> bclaim{0};
+    std::atomic<int> nextC{0}, gsl{-1};
+    int berr = 0, b_end = 0;
+    bool failed = false;
+    // diagnostics (debug bit 5): ns after launch
+    std::chrono::steady_clock::time_point t_launch;
+    std::atomic<int64_t> ns_fill{0}, ns_logits{0}, ns_b0{0}, ns_b1{0}, ns_f0{0}, ns_f1{0}, ns_f2{0};
+    std::atomic<int> b_thread{0};
+  } pj;
+  int64_t pj_ns() const {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - pj.t_launch).count();
+  }
+  void tsum(const char* name, double us) {
+    size_t q = 0;
+    while (q < trace_sum.size() && trace_sum[q].first != name) ++q;
+    if (q == trace_sum.size()) trace_sum.emplace_back(name, 0.0);
+    trace_sum[q].second += us;
+  }
+
+  void pj_phaseA(int t, int j0, int j1) {
+    const int k = pj.touched[t];
+    const int nn = pj.counts[k];
+    for (int j = j0; j < j1; ++j) {
+      const int mj = att[j];
+      const unsigned* fj = &pj.freq[((size_t)k * d + j) * mmax];
+      const double sg = h_sigma[(size_t)k * d + j];
+      double prob[256];
+      for (int l = 0; l < mj; ++l) prob[l] = (-((double)nn - (double)fj[l])) / sg;
+      double mx = prob[0];
+      for (int l = 1; l < mj; ++l) if (prob[l] > mx) mx = prob[l];
+      for (int l = 0; l < mj; ++l) prob[l] = std::exp(prob[l] - mx);
+      double sum = 0.0;
+      for (int l = 0; l < mj; ++l) sum += prob[l];
+      for (int l = 0; l < mj; ++l) prob[l] = prob[l] / sum;
+      PhiItem& P = phi_items[(size_t)t * d + j];
+      double* cum = &phi_cum[(size_t)t * pj.sumatt + phi_off[j]];
+      int* perm = &phi_perm[(size_t)t * pj.sumatt + phi_off[j]];
+      P.err = -sample_prob1_prep(prob, mj, cum, perm);
+      P.lstar = -1;
+      if (P.err) continue;
+      const int l = perm[0] - 1;
+      const double sumdelta = (double)fj[l];
+      const double nw_ = w[j] + nn - sumdelta, nv_ = v[j] + sumdelta;
+      P.lstar = l;
+      P.bp = rhig_beta_path(nv_, nw_, (double)mj);
+      if (P.bp) P.rb = rbeta_setup(nw_ + 1, nv_ - 1);
+    }
+  }
+
+  // the stream-consuming draws of cluster t (reference order)
+  int pj_phaseB(int t) {
+    StreamAhead& sa = phi_stream;
+    const int k = pj.touched[t];
+    const int nn = pj.counts[k];
+    const unsigned* freq = pj.freq;
+    const int sumatt = pj.sumatt;
+    uint8_t* cen = &pj.Cen[(size_t)k * d];
+    // the items were written by other cores: prefetch a few ahead (cross-core misses
+    // would otherwise serialise this loop)
+    constexpr int kAhead = 8;
+    for (int j = 0; j < std::min(d, kAhead); ++j) {
+      __builtin_prefetch(&phi_items[(size_t)t * d + j]);
+      __builtin_prefetch(&phi_cum[(size_t)t * sumatt + phi_off[j]]);
+    }
+    for (int j = 0; j < d; ++j) {
+      if (j + kAhead < d) {
+        const size_t ja = (size_t)t * d + j + kAhead;
+        __builtin_prefetch(&phi_items[ja]);
+        __builtin_prefetch((const char*)&phi_items[ja] + 64);
+        __builtin_prefetch(&phi_cum[(size_t)t * sumatt + phi_off[j + kAhead]]);
+        __builtin_prefetch(&phi_perm[(size_t)t * sumatt + phi_off[j + kAhead]]);
+        __builtin_prefetch(&freq[((size_t)k * d + j + kAhead) * mmax]);
+      }
+      const PhiItem& P = phi_items[(size_t)t * d + j];
+      if (P.err) return P.err;
+      const size_t o = (size_t)t * sumatt + phi_off[j];
+      cen[j] = (uint8_t)(sample_prob1_pick(&phi_cum[o], &phi_perm[o], att[j], sa.next(nullptr)) + 1);
+    }
+    // sigma draws.  Items go in batches of up to kSpec whose first rbeta attempts are
+    // evaluated together at the stream positions they have if every earlier item of the
+    // batch is accepted on its first attempt (independent work the core overlaps); they are
+    // committed in order up to the first item that was not, which is then drawn
+    // sequentially from its true position.  Same arithmetic either way.
+    constexpr int kSpec = 4;
+    auto params = [&](int j, bool* bp, RBeta* rb) {
+      PhiItem& P = phi_items[(size_t)t * d + j];
+      const int l = cen[j] - 1;
+      const double mj = (double)att[j];
+      const double sumdelta = (double)freq[((size_t)k * d + j) * mmax + l];
+      P.nw = w[j] + nn - sumdelta;
+      P.nv = v[j] + sumdelta;
+      if (l == P.lstar) {
+        *bp = P.bp;
+        if (*bp) *rb = P.rb;
+      } else {
+        *bp = rhig_beta_path(P.nv, P.nw, mj);
+        if (*bp) *rb = rbeta_setup(P.nw + 1, P.nv - 1);
+      }
+    };
+    auto sequential = [&](int j, bool bp, const RBeta& rb) {
+      PhiItem& P = phi_items[(size_t)t * d + j];
+      const double mj = (double)att[j];
+      if (bp) {                                   // hg:359-363
+        double x = rbeta_draw_s(sa, rb);
+        while (x > (mj - 1) / mj) x = rbeta_draw_s(sa, rb);
+        P.path = 1;
+        P.x = x;
+      } else {                                    // hg:365-367
+        P.path = 2;
+        P.x = sa.next(nullptr);
+      }
+    };
+    int j = 0;
+    while (j < d) {
+      bool bps[kSpec];
+      RBeta rbs[kSpec];
+      int cons[kSpec];
+      int nb = 0;
+      int64_t q = sa.used;
+      for (; nb < kSpec && j + nb < d; ++nb) {
+        params(j + nb, &bps[nb], &rbs[nb]);
+        cons[nb] = !bps[nb] ? 1 : rbs[nb].kind == RBeta::kBB ? 2 : 0;
+        if (cons[nb] == 0 || sa.spilled || q + cons[nb] > sa.n) break;
+        q += cons[nb];
+      }
+      const int nspec = nb;   // items with a speculative first attempt
+      double xs[kSpec];
+      bool ok[kSpec];
+      q = sa.used;
+      for (int b = 0; b < nspec; ++b) {
+        const double mj = (double)att[j + b];
+        if (bps[b]) {
+          double wv;
+          ok[b] = rbeta_bb_attempt(rbs[b], sa.u[q], sa.lg[q], sa.u[q + 1], sa.lz[q], &wv);
+          xs[b] = rbeta_bb_value(rbs[b], wv);
+          ok[b] = ok[b] && !(xs[b] > (mj - 1) / mj);
+        } else {
+          xs[b] = sa.u[q];
+          ok[b] = true;
+        }
+        q += cons[b];
+      }
+      int b = 0;
+      for (; b < nspec && ok[b]; ++b) {
+        PhiItem& P = phi_items[(size_t)t * d + j + b];
+        P.path = bps[b] ? 1 : 2;
+        P.x = xs[b];
+        sa.used += cons[b];
+      }
+      j += b;
+      if (j >= d) break;
+      if (b < nb) {                               // item j was prepared (speculated or not)
+        sequential(j, bps[b], rbs[b]);
+      } else {                                    // batch ended before item j was prepared
+        bool bp;
+        RBeta rb;
+        params(j, &bp, &rb);
+        sequential(j, bp, rb);
+      }
+      ++j;
+    }
+    return 0;
+  }
+
+  // sigma of cluster t, then its staged tables; false on a GSL error
+  bool pj_phaseC(int t) {
+    const int k = pj.touched[t];
+    bool ok = true;
+    for (int j = 0; j < d; ++j) {
+      PhiItem& P = phi_items[(size_t)t * d + j];
+      const double mj = (double)att[j];
+      double out;
+      if (P.path == 1) {
+        out = P.x / ((mj - 1) * (1 - P.x));
+      } else {
+        int e = kOk;
+        out = bisec_hyper2(P.nw, P.nv, mj, P.x, &e);
+        if (e) { ok = false; continue; }
+      }
+      pj.Sig[(size_t)k * d + j] = -1 / std::log(out);
+    }
+    if (ok) stage_entry_from(pj.L, pj.full ? k : t, k, &pj.Cen[(size_t)k * d], &pj.Sig[(size_t)k * d], pj.counts[k]);
+    return ok;
+  }
+
+  // Prepares pj for touched[t0..T).  With `spec`, the job itself generates the stream slice
+  // (waiting for the device state first) into phi_stream, with spec_live as spill target.
+  void pj_setup(std::vector<int> touched, int t0, const int* counts, const unsigned* freq, uint8_t* Cen, double* Sig,
+                const UploadLayout& L, bool full, int64_t* offs, bool spec) {
+    pj.touched = std::move(touched);
+    pj.T = (int)pj.touched.size();
+    pj.t0 = t0;
+    pj.counts = counts;
+    pj.freq = freq;
+    pj.Cen = Cen;
+    pj.Sig = Sig;
+    pj.L = L;
+    pj.full = full;
+    pj.offs = offs;
+    pj.spec = spec;
+    pj.fill_count = phi_prefetch;
+    phi_off.resize(d + 1);
+    phi_off[0] = 0;
+    for (int j = 0; j < d; ++j) phi_off[j + 1] = phi_off[j] + att[j];
+    pj.sumatt = phi_off[d];
+    phi_items.resize((size_t)pj.T * d);
+    phi_cum.resize((size_t)pj.T * pj.sumatt);
+    phi_perm.resize((size_t)pj.T * pj.sumatt);
+    // A in chunks of attributes so the first cluster is ready early
+    pj.achunk = std::max(8, (d + 3) / 4);
+    pj.nach = (d + pj.achunk - 1) / pj.achunk;
+    pj.stA.reset(new std::atomic<int>[std::max(pj.T, 1)]);
+    pj.stB.reset(new std::atomic<int>[std::max(pj.T, 1)]);
+    for (int t = 0; t < pj.T; ++t) { pj.stA[t].store(0); pj.stB[t].store(0); }
+    pj.fill.store(spec ? 0 : 2);
+    pj.nL.store(0);
+    pj.nextL.store(0);
+    pj.doneL.store(0);
+    pj.nextA.store(t0 * pj.nach);
+    pj.bclaim.store(t0 >= pj.T ? 1 : 0);
+    pj.nextC.store(t0);
+    pj.gsl.store(-1);
+    pj.berr = 0;
+    pj.b_end = t0;
+    pj.failed = false;
+    if (offs && t0 >= pj.T) offs[pj.T] = phi_stream.used;
+  }
+
+  bool pj_fill() {
+    int z = 0;
+    if (pj.fill.load(std::memory_order_acquire) != 0 || !pj.fill.compare_exchange_strong(z, 1)) return false;
+    StreamAhead& sa = phi_stream;
+    try {
+      pj.ns_f0.store(pj_ns());
+      rng_sync();                               // the device state at the sweep's end
+      pj.ns_f1.store(pj_ns());
+      spec_live = rng;
+      if (!fill_phi_stream(pj.fill_count)) sa.n = 0;
+    } catch (const HipError&) {                 // the caller meets the error again; no speculation
+      sa.n = 0;
+      pj.failed = true;
+    }
+    sa.used = 0;
+    sa.live = &spec_live;
+    pj.nL.store((int)((sa.n + PhiJob::kLogitChunk - 1) / PhiJob::kLogitChunk), std::memory_order_relaxed);
+    pj.ns_fill.store(pj_ns());
+    pj.fill.store(2, std::memory_order_release);
+    return true;
+  }
+  bool pj_logit() {
+    if (pj.fill.load(std::memory_order_acquire) != 2) return false;
+    const int c = pj.nextL.fetch_add(1);
+    if (c >= pj.nL.load(std::memory_order_relaxed)) return false;
+    StreamAhead& sa = phi_stream;
+    sa.logits((int64_t)c * PhiJob::kLogitChunk, std::min<int64_t>(sa.n, (int64_t)(c + 1) * PhiJob::kLogitChunk));
+    if (pj.doneL.fetch_add(1, std::memory_order_release) + 1 == pj.nL.load()) pj.ns_logits.store(pj_ns());
+    return true;
+  }
+  bool pj_take_a() {
+    const int task = pj.nextA.fetch_add(1);
+    if (task >= pj.T * pj.nach) return false;
+    const int t = task / pj.nach, c = task - t * pj.nach;
+    pj_phaseA(t, c * pj.achunk, std::min(d, (c + 1) * pj.achunk));
+    pj.stA[t].fetch_add(1, std::memory_order_acq_rel);
+    return true;
+  }
+  bool pj_stream_ready() const {
+    return pj.fill.load(std::memory_order_acquire) == 2 &&
+           pj.doneL.load(std::memory_order_acquire) >= pj.nL.load(std::memory_order_relaxed);
+  }
+  // B for every cluster, in order, on the thread that claims it once the stream is ready
+  bool pj_try_b() {
+    int z = 0;
+    if (pj.bclaim.load(std::memory_order_acquire) != 0 || !pj_stream_ready() || !pj.bclaim.compare_exchange_strong(z, 1))
+      return false;
+    StreamAhead& sa = phi_stream;
+    pj.ns_b0.store(pj_ns());
+    pj.b_thread.store(sched_getcpu() == HostPool::get().main_cpu() ? 1 : 0);
+    int tb = pj.t0;
+    for (; tb < pj.T; ++tb) {
+      while (pj.stA[tb].load(std::memory_order_acquire) < pj.nach)
+        if (!pj_take_a()) HostPool::spin_pause();
+      if (pj.offs) pj.offs[tb] = sa.used;
+      pj.berr = pj_phaseB(tb);
+      if (pj.berr) break;
+      pj.stB[tb].store(1, std::memory_order_release);
+    }
+    if (pj.offs && !pj.berr) pj.offs[pj.T] = sa.used;
+    pj.b_end = tb;
+    pj.ns_b1.store(pj_ns());
+    for (int t = tb; t < pj.T; ++t) pj.stB[t].store(-1, std::memory_order_release);
+    return true;
+  }
+  void pj_work() {
+    for (;;) {
+      if (pj_fill()) continue;                    // the stream slice first: B waits on it
+      if (pj_logit()) continue;
+      if (pj_try_b()) continue;
+      if (pj_take_a()) continue;
+      if (pj.bclaim.load(std::memory_order_acquire) != 0) break;
+      HostPool::spin_pause();                   // stream fill / logits in progress elsewhere
+    }
+    for (;;) {
+      const int t = pj.nextC.fetch_add(1);
+      if (t >= pj.T) break;
+      int b;
+      while ((b = pj.stB[t].load(std::memory_order_acquire)) == 0) HostPool::spin_pause();
+      if (b < 0) break;                           // B stopped on an error
+      if (!pj_phaseC(t)) {
+        int cur = pj.gsl.load();
+        while ((cur < 0 || t < cur) && !pj.gsl.compare_exchange_weak(cur, t)) {}
+      }
+    }
+  }
+  // Runs the prepared job on the pool and the calling thread; returns B's status.
+  bool pj_open = false;
+  void pj_launch() {
+    HostPool& pool = HostPool::get();
+    pj.t_launch = std::chrono::steady_clock::now();
+    pj_open = pool.workers() > 0;
+    if (pj_open) pool.launch([this](int) { pj_work(); });
+  }
+  int pj_finish() {
+    pj_work();
+    if (pj_open) HostPool::get().join();
+    pj_open = false;
+    return pj.berr;
+  }
+
+  // Started right after the sweep's draws are reserved, before its kernels are launched:
+  // update_phi of every label on the pre-sweep state, into spec.*, on the pool while the
+  // caller launches the sweep (spec_join collects it).  Its stream is phi_stream from the
+  // sweep's end position; the chain's own Rng is not touched.
+  void spec_launch() {
+    spec.ran = false;
+    spec.lv = 0;
+    if (K <= 0) return;
+    for (int k = 0; k < K; ++k)
+      if (h_counts[k] <= 0) return;
+    spec.K = K;
+    spec.pos = rng.pos;
+    spec.epoch = rng.epoch;
+    spec.center = h_center;
+    spec.sigma = h_sigma;
+    spec.counts = h_counts;
+    spec.off.assign((size_t)K + 1, 0);
+    std::vector<int> touched(K);
+    for (int k = 0; k < K; ++k) touched[k] = k;
+    const UploadLayout L = stage_begin(K);
+    pj_setup(std::move(touched), 0, spec.counts.data(), h_freq.p, spec.center.data(), spec.sigma.data(), L, true,
+             spec.off.data(), true);
+    spec.moves = -1;
+    spec.joined = false;
+    pj_launch();
+    spec.ran = true;
+  }
+  void spec_join() {
+    if (!spec.ran) return;
+    StreamAhead& sa = phi_stream;
+    const int berr = pj_finish();
+    int nv = berr ? pj.b_end : spec.K;
+    const int gsl_t = pj.gsl.load();
+    if (gsl_t >= 0) nv = std::min(nv, gsl_t);
+    if (pj.failed || sa.n == 0 || sa.start.pos != spec.pos) nv = 0;
+    if (sa.spilled)
+      for (int t = 0; t < nv; ++t)
+        if (spec.off[t + 1] > sa.n) { nv = t; break; }
+    spec.nvalid = nv;
+    if (debug & 32) {
+      tsum("spec.fill_start", pj.ns_f0.load() * 1e-3);
+      tsum("spec.state_at", pj.ns_f1.load() * 1e-3);
+      tsum("spec.slice_at", pj.ns_f2.load() * 1e-3);
+      tsum("spec.fill_at", pj.ns_fill.load() * 1e-3);
+      tsum("spec.logits_at", pj.ns_logits.load() * 1e-3);
+      tsum("spec.B_from", pj.ns_b0.load() * 1e-3);
+      tsum("spec.B_to", pj.ns_b1.load() * 1e-3);
+      tsum("spec.joined_at", pj_ns() * 1e-3);
+      tsum("spec.B_on_caller", pj.b_thread.load());
+    }
+    // rewind: update_phi continues from spec.off[t0] of the same prefetched stream
+    sa.used = 0;
+    sa.spilled = false;
+    sa.live = &rng;
+    spec.moves = -1;
+    spec.joined = true;
+    stats.phi_spec_runs++;
   }
 
   int update_phi(const int32_t* idx, int nidx) {
     if (!have_state) { err = "no state"; return kArg; }
     HostPool& pool = HostPool::get();
     pool.prewake();                                   // workers spin while the device counts
-    auto t0 = std::chrono::steady_clock::now();
+    auto t0c = std::chrono::steady_clock::now();
     std::vector<unsigned char> mask(K, nidx == 0 ? 1 : 0);
     for (int q = 0; q < nidx; ++q)
       if (idx[q] >= 0 && idx[q] < K) mask[idx[q]] = 1;
-    histogram_launch(nidx == 0 ? nullptr : &mask);
-    mark("hist_launch");
-    // while the device counts: the next stretch of the stream and its logits (usually
-    // already generated during the sweep)
-    prefill_phi_stream();
     StreamAhead& sa = phi_stream;
-    sa.live = &rng;
-    mark("prefill");
-    histogram_wait(nidx == 0 ? nullptr : &mask);
-    mark("hist_wait");
+    // speculation of the sweep just done (spec_launch), for the full update only
+    const bool use_spec = nidx == 0 && spec.ran && spec.lv == labels_version && spec.moves >= 0 &&
+                          spec.pos == rng.pos && spec.epoch == rng.epoch && sa.n > 0 && sa.start.pos == rng.pos &&
+                          !(debug & 128);
+    spec.ran = false;
+    int t0 = 0;
+    if (use_spec && spec.moves == 0 && K == spec.K) {
+      // nothing moved: the frequency tables are the pre-sweep ones (the sweep's copy-out,
+      // still in flight, has the same contents) -- no wait for the device
+      t0 = spec.nvalid;
+      freq_next_pending = false;
+      freq_version = labels_version;
+      rng_sync();
+      mark("hist_wait");
+    } else {
+      histogram_launch(nidx == 0 ? nullptr : &mask);
+      mark("hist_launch");
+      // while the device counts: the next stretch of the stream and its logits (usually
+      // already generated during the sweep)
+      if (!use_spec) prefill_phi_stream();
+      mark("prefill");
+      histogram_wait(nidx == 0 ? nullptr : &mask);
+      if (use_spec && freq_next_pending) {
+        // the leading labels the sweep left alone: same slot and count (spec.pfx), same table
+        const size_t row = (size_t)d * mmax;
+        int pfx = std::min(spec.pfx, spec.nvalid);
+        for (int l = 0; l < pfx; ++l)
+          if (std::memcmp(h_freq.p + l * row, h_freq_next.p + l * row, row * 4) != 0) { pfx = l; break; }
+        t0 = pfx;
+      }
+      if (freq_next_pending) {
+        std::swap(h_freq.p, h_freq_next.p);
+        std::swap(h_freq.n, h_freq_next.n);
+        freq_next_pending = false;
+      }
+      mark("hist_wait");
+    }
+    if (use_spec) {
+      sa.used = spec.off[t0];
+      sa.spilled = false;
+      sa.live = &rng;
+      for (int k = 0; k < t0; ++k) {
+        std::memcpy(&h_center[(size_t)k * d], &spec.center[(size_t)k * d], d);
+        std::memcpy(&h_sigma[(size_t)k * d], &spec.sigma[(size_t)k * d], (size_t)d * 8);
+      }
+      stats.phi_spec_clusters += t0;
+    } else {
+      sa.live = &rng;
+    }
     auto t1 = std::chrono::steady_clock::now();
     std::vector<int> touched;
     for (int i = 0; i < K; ++i)
       if (mask[i] && h_counts[i] != 0) touched.push_back(i);
     const int T = (int)touched.size();
-    phi_off.resize(d + 1);
-    phi_off[0] = 0;
-    for (int j = 0; j < d; ++j) phi_off[j + 1] = phi_off[j] + att[j];
-    const int sumatt = phi_off[d];
-    phi_items.resize((size_t)T * d);
-    phi_cum.resize((size_t)T * sumatt);
-    phi_perm.resize((size_t)T * sumatt);
+    if (t0 > T) t0 = T;
     // staging of the new tables: all labels when every label is updated (or the device
     // tables are stale), else the touched ones
     const bool full = tables_dirty || T == K;
     if (full) ensure_slots(K + 2);
     const int nent = full ? K : T;
     const UploadLayout L = stage_begin(std::max(nent, 1));
-
-    // ---- phase A: one cluster at a time, in order
-    auto phaseA = [&](int t, int j0, int j1) {
-      const int k = touched[t];
-      const int nn = h_counts[k];
-      for (int j = j0; j < j1; ++j) {
-        const int mj = att[j];
-        const unsigned* fj = &h_freq.p[((size_t)k * d + j) * mmax];
-        const double sg = h_sigma[(size_t)k * d + j];
-        double prob[256];
-        for (int l = 0; l < mj; ++l) prob[l] = (-((double)nn - (double)fj[l])) / sg;
-        double mx = prob[0];
-        for (int l = 1; l < mj; ++l) if (prob[l] > mx) mx = prob[l];
-        for (int l = 0; l < mj; ++l) prob[l] = std::exp(prob[l] - mx);
-        double sum = 0.0;
-        for (int l = 0; l < mj; ++l) sum += prob[l];
-        for (int l = 0; l < mj; ++l) prob[l] = prob[l] / sum;
-        PhiItem& P = phi_items[(size_t)t * d + j];
-        double* cum = &phi_cum[(size_t)t * sumatt + phi_off[j]];
-        int* perm = &phi_perm[(size_t)t * sumatt + phi_off[j]];
-        P.err = -sample_prob1_prep(prob, mj, cum, perm);
-        P.lstar = -1;
-        if (P.err) continue;
-        const int l = perm[0] - 1;
-        const double sumdelta = (double)fj[l];
-        const double nw_ = w[j] + nn - sumdelta, nv_ = v[j] + sumdelta;
-        P.lstar = l;
-        P.bp = rhig_beta_path(nv_, nw_, (double)mj);
-        if (P.bp) P.rb = rbeta_setup(nw_ + 1, nv_ - 1);
-      }
-    };
-    // ---- phase B: the stream-consuming draws of cluster t (reference order)
-    auto phaseB = [&](int t) -> int {
-      const int k = touched[t];
-      const int nn = h_counts[k];
-      uint8_t* cen = &h_center[(size_t)k * d];
-      // the items were written by other cores: prefetch a few ahead (cross-core misses
-      // would otherwise serialise this loop)
-      constexpr int kAhead = 8;
-      for (int j = 0; j < std::min(d, kAhead); ++j) {
-        __builtin_prefetch(&phi_items[(size_t)t * d + j]);
-        __builtin_prefetch(&phi_cum[(size_t)t * sumatt + phi_off[j]]);
-      }
-      for (int j = 0; j < d; ++j) {
-        if (j + kAhead < d) {
-          const size_t ja = (size_t)t * d + j + kAhead;
-          __builtin_prefetch(&phi_items[ja]);
-          __builtin_prefetch((const char*)&phi_items[ja] + 64);
-          __builtin_prefetch(&phi_cum[(size_t)t * sumatt + phi_off[j + kAhead]]);
-          __builtin_prefetch(&phi_perm[(size_t)t * sumatt + phi_off[j + kAhead]]);
-          __builtin_prefetch(&h_freq.p[((size_t)k * d + j + kAhead) * mmax]);
-        }
-        const PhiItem& P = phi_items[(size_t)t * d + j];
-        if (P.err) return P.err;
-        const size_t o = (size_t)t * sumatt + phi_off[j];
-        cen[j] = (uint8_t)(sample_prob1_pick(&phi_cum[o], &phi_perm[o], att[j], sa.next(nullptr)) + 1);
-      }
-      // sigma draws.  Items go in batches of up to kSpec whose first rbeta attempts are
-      // evaluated together at the stream positions they have if every earlier item of the
-      // batch is accepted on its first attempt (independent work the core overlaps);
-      // they are committed in order up to the first item that was not, which is then
-      // drawn sequentially from its true position.  Same arithmetic either way.
-      constexpr int kSpec = 4;
-      auto params = [&](int j, bool* bp, RBeta* rb) {
-        PhiItem& P = phi_items[(size_t)t * d + j];
-        const int l = cen[j] - 1;
-        const double mj = (double)att[j];
-        const double sumdelta = (double)h_freq.p[((size_t)k * d + j) * mmax + l];
-        P.nw = w[j] + nn - sumdelta;
-        P.nv = v[j] + sumdelta;
-        if (l == P.lstar) {
-          *bp = P.bp;
-          if (*bp) *rb = P.rb;
-        } else {
-          *bp = rhig_beta_path(P.nv, P.nw, mj);
-          if (*bp) *rb = rbeta_setup(P.nw + 1, P.nv - 1);
-        }
-      };
-      auto sequential = [&](int j, bool bp, const RBeta& rb) {
-        PhiItem& P = phi_items[(size_t)t * d + j];
-        const double mj = (double)att[j];
-        if (bp) {                                   // hg:359-363
-          double x = rbeta_draw_s(sa, rb);
-          while (x > (mj - 1) / mj) x = rbeta_draw_s(sa, rb);
-          P.path = 1;
-          P.x = x;
-        } else {                                    // hg:365-367
-          P.path = 2;
-          P.x = sa.next(nullptr);
-        }
-      };
-      int j = 0;
-      while (j < d) {
-        bool bps[kSpec];
-        RBeta rbs[kSpec];
-        int cons[kSpec];
-        int nb = 0;
-        int64_t q = sa.used;
-        for (; nb < kSpec && j + nb < d; ++nb) {
-          params(j + nb, &bps[nb], &rbs[nb]);
-          cons[nb] = !bps[nb] ? 1 : rbs[nb].kind == RBeta::kBB ? 2 : 0;
-          if (cons[nb] == 0 || sa.spilled || q + cons[nb] > sa.n) break;
-          q += cons[nb];
-        }
-        const int nspec = nb;   // items with a speculative first attempt
-        double xs[kSpec];
-        bool ok[kSpec];
-        q = sa.used;
-        for (int b = 0; b < nspec; ++b) {
-          const double mj = (double)att[j + b];
-          if (bps[b]) {
-            double wv;
-            ok[b] = rbeta_bb_attempt(rbs[b], sa.u[q], sa.lg[q], sa.u[q + 1], sa.lz[q], &wv);
-            xs[b] = rbeta_bb_value(rbs[b], wv);
-            ok[b] = ok[b] && !(xs[b] > (mj - 1) / mj);
-          } else {
-            xs[b] = sa.u[q];
-            ok[b] = true;
-          }
-          q += cons[b];
-        }
-        int b = 0;
-        for (; b < nspec && ok[b]; ++b) {
-          PhiItem& P = phi_items[(size_t)t * d + j + b];
-          P.path = bps[b] ? 1 : 2;
-          P.x = xs[b];
-          sa.used += cons[b];
-        }
-        j += b;
-        if (j >= d) break;
-        if (b < nb) {                               // item j was prepared (speculated or not)
-          sequential(j, bps[b], rbs[b]);
-        } else {                                    // batch ended before item j was prepared
-          bool bp;
-          RBeta rb;
-          params(j, &bp, &rb);
-          sequential(j, bp, rb);
-        }
-        ++j;
-      }
-      return 0;
-    };
-    // ---- phase C: sigma of cluster t, then its staged tables; returns false on a GSL error
-    auto phaseC = [&](int t) -> bool {
-      const int k = touched[t];
-      bool ok = true;
-      for (int j = 0; j < d; ++j) {
-        PhiItem& P = phi_items[(size_t)t * d + j];
-        const double mj = (double)att[j];
-        double out;
-        if (P.path == 1) {
-          out = P.x / ((mj - 1) * (1 - P.x));
-        } else {
-          int e = kOk;
-          out = bisec_hyper2(P.nw, P.nv, mj, P.x, &e);
-          if (e) { ok = false; continue; }
-        }
-        h_sigma[(size_t)k * d + j] = -1 / std::log(out);
-      }
-      if (ok) stage_entry(L, full ? k : t, k);
-      return ok;
-    };
-
-    // Pipeline: workers run A for clusters in order, then C for clusters whose B is done;
-    // this thread runs B in order as soon as A of the cluster is ready.
-    std::vector<std::atomic<int>> stA(T), stB(T);
-    for (int t = 0; t < T; ++t) { stA[t].store(0); stB[t].store(0); }
-    std::atomic<int> nextA{0}, nextC{0}, gsl_err{-1};
-    const auto tlaunch = std::chrono::steady_clock::now();
-    std::vector<double> a_beg(T, 0.0), a_end(T, 0.0);
-    // A in chunks of attributes so the first cluster is ready early
-    const int achunk = std::max(8, (d + 3) / 4);
-    const int nach = (d + achunk - 1) / achunk;
-    auto take_a = [&]() -> bool {   // one A task from the shared queue; false when none left
-      const int task = nextA.fetch_add(1);
-      if (task >= T * nach) return false;
-      const int t = task / nach, c = task - t * nach;
-      if ((debug & 2) && c == 0) a_beg[t] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tlaunch).count();
-      phaseA(t, c * achunk, std::min(d, (c + 1) * achunk));
-      if (stA[t].fetch_add(1, std::memory_order_acq_rel) + 1 == nach && (debug & 2))
-        a_end[t] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tlaunch).count();
-      return true;
-    };
-    auto worker = [&](int) {
-      while (take_a()) {}
-      for (;;) {
-        const int t = nextC.fetch_add(1);
-        if (t >= T) break;
-        int b;
-        while ((b = stB[t].load(std::memory_order_acquire)) == 0) HostPool::spin_pause();
-        if (b < 0) break;                           // B stopped on an error
-        if (!phaseC(t)) {
-          int cur = gsl_err.load();
-          while ((cur < 0 || t < cur) && !gsl_err.compare_exchange_weak(cur, t)) {}
-        }
-      }
-    };
-    const bool par = pool.workers() > 0 && T > 1;
-    if (par) pool.launch(worker);
-    else for (int t = 0; t < T; ++t) phaseA(t, 0, d);
-    int berr = 0;
-    int tb = 0;
-    double wait_us = 0;
-    for (; tb < T; ++tb) {
-      auto w0 = std::chrono::steady_clock::now();
-      // the caller takes queued A tasks itself rather than wait for a worker to wake up
-      while (par && stA[tb].load(std::memory_order_acquire) < nach)
-        if (!take_a()) HostPool::spin_pause();
-      if (debug & 2) wait_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - w0).count();
-      berr = phaseB(tb);
-      if (berr) break;
-      stB[tb].store(1, std::memory_order_release);
+    if (t0 > 0 && !(full && K == spec.K)) {
+      // the speculation staged its clusters for a different layout: stage them again
+      pool_for(t0, [&](int t) { stage_entry(L, full ? touched[t] : t, touched[t]); });
     }
-    if (debug & 2) {
-      auto m0 = std::chrono::steady_clock::now();
-      if (T > 0) phaseA(0, 0, d);   // the same work again on this thread (diagnostic)
-      const double mainA = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - m0).count();
-      std::fprintf(stderr, "[phi] main-thread A(0) %.1f us (cpu %d); ", mainA, sched_getcpu());
-      std::fprintf(stderr, "[phi] B waited %.1f us for A, %lld draws; A(t) begin/end us:", wait_us, (long long)sa.used);
-      for (int t = 0; t < std::min(T, 10); ++t) std::fprintf(stderr, " %.0f/%.0f", a_beg[t], a_end[t]);
-      std::fprintf(stderr, "\n");
+    int berr = 0, gsl_t = -1;
+    if (t0 < T) {
+      pj_setup(touched, t0, h_counts.data(), h_freq.p, h_center.data(), h_sigma.data(), L, full, nullptr, false);
+      pj_launch();
+      berr = pj_finish();
+      gsl_t = pj.gsl.load();
+      mark("B+C");
     }
-    for (int t = tb; t < T; ++t) stB[t].store(-1, std::memory_order_release);
-    mark("B");
-    sa.finish();                                      // the host stream continues after B's draws
-    sa.n = 0;                                         // consumed
+    sa.finish();                                      // the host stream continues after the draws
     phi_prefetch = std::max<int64_t>(4096, sa.used + sa.used / 4 + 512);
-    if (par) {
-      // help with the remaining C work, then wait for the workers
-      for (;;) {
-        const int t = nextC.fetch_add(1);
-        if (t >= T) break;
-        if (stB[t].load(std::memory_order_acquire) < 0) break;
-        if (!phaseC(t)) {
-          int cur = gsl_err.load();
-          while ((cur < 0 || t < cur) && !gsl_err.compare_exchange_weak(cur, t)) {}
-        }
-      }
-      pool.join();
-    } else if (!berr) {
-      for (int t = 0; t < T; ++t)
-        if (!phaseC(t) && gsl_err.load() < 0) gsl_err.store(t);
-    }
-    mark("C");
+    sa.n = 0;                                         // consumed
     if (berr) { err = "center draw failed"; return berr; }
-    if (gsl_err.load() >= 0) { err = "norm_const2 - hypergeometric diverging with infinity"; return kGsl; }
+    if (gsl_t >= 0) { err = "norm_const2 - hypergeometric diverging with infinity"; return kGsl; }
     if (full) {
       // labels that were not updated still need their (unchanged) tables staged
       std::vector<char> done(K, 0);
@@ -1888,7 +2350,7 @@ struct Ctx {
     }
     auto t2 = std::chrono::steady_clock::now();
     mark("commit");
-    stats.t_stats_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
+    stats.t_stats_ms += std::chrono::duration<double, std::milli>(t1 - t0c).count();
     stats.t_host_phi_ms += std::chrono::duration<double, std::milli>(t2 - t1).count();
     return kOk;
   }
@@ -1903,7 +2365,7 @@ struct Ctx {
       // dhamming table values (the tables of the last full upload, still in h_stage)
       auto t0 = std::chrono::steady_clock::now();
       const UploadLayout L = upload_layout(K, dp, d, bw);
-      const double* tab = (const double*)(h_stage.p + L.off_tab);
+      const double* tab = (const double*)(h_stage_buf[stage_last].p + L.off_tab);
       double hi = 0.0, lo = 0.0;
       auto add = [&](double a) {
         const double s = hi + a, bb = s - hi;
@@ -1975,7 +2437,8 @@ struct Ctx {
                        double* o_ll, int32_t* o_acc, int32_t* o_final, double* o_time);
   int split_and_merge(int t, int r, int idx_1_sm, int* accepted);
   int init_chain(const hdpm_chain_params* p, const int32_t* c_init);
-  int iteration(const hdpm_chain_params* p, int iter, int* idx_1_sm, int* accepted, double* ll);
+  int iteration(const hdpm_chain_params* p, int iter, int* idx_1_sm, int* accepted, double* ll,
+                bool launch_next = false, int32_t* labels_out = nullptr);
 };
 
 }  // namespace hdpm
@@ -2022,11 +2485,13 @@ int Ctx::init_chain(const hdpm_chain_params* p, const int32_t* c_init) {
 }
 
 // la:85-132, one iteration
-int Ctx::iteration(const hdpm_chain_params* p, int iter, int* idx_1_sm, int* accepted, double* ll) {
+int Ctx::iteration(const hdpm_chain_params* p, int iter, int* idx_1_sm, int* accepted, double* ll, bool launch_next,
+                   int32_t* labels_out) {
   int st;
   *accepted = 0;
   trace.clear();
   mark("start");
+  if (!(p->neal8 && iter % p->n8_step_size == 0)) cancel_ahead();
   if (p->neal8 && iter % p->n8_step_size == 0) {       // la:94-103
     st = neal8_sweep(p->m);
     if (st) return st;
@@ -2044,6 +2509,14 @@ int Ctx::iteration(const hdpm_chain_params* p, int iter, int* idx_1_sm, int* acc
   }
   st = compute_loglikelihood(ll);                        // la:132
   mark("loglik");
+  if (!st && labels_out) {                               // la:145 (before the next sweep is launched)
+    download_labels();
+    std::memcpy(labels_out, h_c.data(), (size_t)n * 4);
+  }
+  // the next iteration starts with a sweep: prepare it now (cancelled by any other call;
+  // launched on the device too when the caller runs that iteration next, launch_next)
+  if (!st && p->neal8 && (iter + 1) % p->n8_step_size == 0) prepare_next_sweep(p->m, launch_next);
+  mark("ahead");
   if ((debug & 32) && trace.size() > 1) {
     if (trace_alloc0 < 0) trace_alloc0 = g_dev_allocs.load();
     for (size_t k = 1; k < trace.size(); ++k) {
@@ -2079,15 +2552,12 @@ int Ctx::run_markov_chain(const hdpm_chain_params* p, const int32_t* c_init, int
   for (int iter = 0; iter < total; ++iter) {
     int accepted = 0;
     double ll = 0.0;
-    st = iteration(p, iter, &idx_1_sm, &accepted, &ll);
+    const bool rec = iter >= p->thinning * p->burnin && iter % p->thinning == 0;   // la:140-153
+    const int at = rec ? iter / p->thinning - p->burnin : 0;
+    st = iteration(p, iter, &idx_1_sm, &accepted, &ll, iter + 1 < total, (rec && o_c) ? o_c + (size_t)at * n : nullptr);
     if (st) return st;
-    if (iter >= p->thinning * p->burnin && iter % p->thinning == 0) {   // la:140-153
-      const int at = iter / p->thinning - p->burnin;
+    if (rec) {
       if (o_tot) o_tot[at] = K;
-      if (o_c) {
-        download_labels();
-        std::memcpy(o_c + (size_t)at * n, h_c.data(), (size_t)n * 4);
-      }
       if (o_ll) o_ll[at] = ll;
       if (o_acc) o_acc[at] = accepted;
     }
@@ -2149,6 +2619,10 @@ int hdpm_ctx_create(int32_t device, hdpm_ctx** out) {
     delete c;
     return HDPM_E_DEVICE;
   }
+  if (hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return HDPM_E_DEVICE;
+  }
   c->rng.set_seed(0);
   *out = reinterpret_cast<hdpm_ctx*>(c);
   return HDPM_OK;
@@ -2166,11 +2640,15 @@ const char* hdpm_last_error(const hdpm_ctx* h) {
   return c ? c->err.c_str() : "null context";
 }
 
-#define CTX()                                   \
+#define CTX_KEEP()                              \
   auto* ctx = reinterpret_cast<Ctx*>(h);        \
   if (!ctx) return HDPM_E_ARG;                  \
   (void)hipSetDevice(ctx->device);              \
   ctx->err.clear();
+// every entry point but the sweep and the iteration drops a prepared sweep first
+#define CTX()                                   \
+  CTX_KEEP();                                   \
+  GUARD(ctx->cancel_ahead();)
 
 int hdpm_set_data(hdpm_ctx* h, const uint8_t* codes, int32_t n, int32_t d, const int32_t* attrisize, double gamma,
                   const double* v, const double* w) {
@@ -2197,6 +2675,7 @@ int hdpm_rng_get_state(const hdpm_ctx* h, int32_t* s) {
   auto* ctx = const_cast<Ctx*>(reinterpret_cast<const Ctx*>(h));
   if (!ctx || !s) return HDPM_E_ARG;
   GUARD({
+    ctx->cancel_ahead();
     ctx->rng_sync();
     ctx->rng.export625(s);
     return HDPM_OK;
@@ -2228,7 +2707,7 @@ int hdpm_generate_pool(hdpm_ctx* h, int64_t P) {
   GUARD(return ctx->generate_pool(P);)
 }
 int hdpm_neal8_sweep(hdpm_ctx* h, int32_t m) {
-  CTX();
+  CTX_KEEP();
   ScopedPin pin;
   GUARD(return ctx->neal8_sweep(m);)
 }
@@ -2282,7 +2761,7 @@ int hdpm_init_chain(hdpm_ctx* h, const hdpm_chain_params* p, const int32_t* c_i_
 }
 int hdpm_iteration(hdpm_ctx* h, const hdpm_chain_params* p, int32_t iter, int32_t* idx_1_sm, int32_t* accepted,
                    double* loglik) {
-  CTX();
+  CTX_KEEP();
   if (!p || !idx_1_sm) return HDPM_E_ARG;
   ScopedPin pin;
   int acc = 0;
@@ -2291,6 +2770,23 @@ int hdpm_iteration(hdpm_ctx* h, const hdpm_chain_params* p, int32_t iter, int32_
   GUARD(st = ctx->iteration(p, iter, idx_1_sm, &acc, &ll);)
   if (accepted) *accepted = acc;
   if (loglik) *loglik = ll;
+  return st;
+}
+int hdpm_iterations(hdpm_ctx* h, const hdpm_chain_params* p, int32_t iter0, int32_t count, int32_t* idx_1_sm,
+                    int32_t* accepted, double* loglik) {
+  CTX_KEEP();
+  if (!p || !idx_1_sm || count < 0) return HDPM_E_ARG;
+  ScopedPin pin;
+  int st = HDPM_OK;
+  GUARD({
+    for (int k = 0; k < count && st == HDPM_OK; ++k) {
+      int acc = 0;
+      double ll = 0.0;
+      st = ctx->iteration(p, iter0 + k, idx_1_sm, &acc, &ll, k + 1 < count);
+      if (accepted) accepted[k] = acc;
+      if (loglik) loglik[k] = ll;
+    }
+  })
   return st;
 }
 int hdpm_rng_fill_device(hdpm_ctx* h, int64_t count, uint32_t* out) {

@@ -348,11 +348,13 @@ struct StreamAhead {
   int64_t n = 0, used = 0;
   Rng* live = nullptr;
   bool spilled = false;
+  const uint32_t* raw = nullptr;   // fill_raw: tempered words; u[] is filled by logits()
 
   bool fill(const Rng& r, int64_t N) {
     n = 0;
     used = 0;
     spilled = false;
+    raw = nullptr;
     if (r.mti > 624) return false;           // never seeded: let the live Rng handle it
     start = r;
     Rng g = r;
@@ -375,10 +377,37 @@ struct StreamAhead {
     n = N;
     return true;
   }
+  // The same prefix from words generated elsewhere (the device windows): r is the state
+  // before the first word (its mt array and mti), raw[0..N) the tempered outputs, and
+  // arrays[v] the mt array after the v-th twist past r (624 words each).  u[] is computed
+  // by logits(), so the caller only copies the state arrays here.
+  void fill_raw(const Rng& r, const uint32_t* raw_, int64_t N, const uint32_t* arrays) {
+    start = r;
+    n = 0;
+    used = 0;
+    spilled = false;
+    raw = raw_;
+    u.resize(N);
+    lg.resize(N);
+    lz.resize(N);
+    vfirst.assign(1, 0);
+    arr.resize(1);
+    std::memcpy(arr[0].data(), r.mt, sizeof(r.mt));
+    int64_t k = r.mti >= 624 ? 0 : 624 - r.mti;   // first word drawn after a twist
+    for (int v = 0; k < N; ++v, k += 624) {
+      vfirst.push_back(k);
+      arr.emplace_back();
+      std::memcpy(arr.back().data(), arrays + (size_t)v * 624, 624 * sizeof(uint32_t));
+    }
+    n = N;
+  }
   void logits(int64_t a, int64_t b) {
+    if (raw)
+      for (int64_t k = a; k < b; ++k) u[k] = Rng::raw_to_unif(raw[k]);
     for (int64_t k = a; k < b; ++k) {
       lg[k] = std::log(u[k] / (1.0 - u[k]));
-      lz[k] = k + 1 < n ? std::log(u[k] * u[k] * u[k + 1]) : NAN;
+      const double un = k + 1 < b || !raw ? u[k + 1 < n ? k + 1 : k] : Rng::raw_to_unif(raw[k + 1 < n ? k + 1 : k]);
+      lz[k] = k + 1 < n ? std::log(u[k] * u[k] * un) : NAN;
     }
   }
   void restore(Rng& r, int64_t c) const {

@@ -186,6 +186,15 @@ class Engine:
                                            C.byref(acc), C.byref(ll)))
         return acc.value, ll.value
 
+    def iterations(self, it0: int, count: int):
+        """Iterations it0 .. it0+count-1 in one call (the next sweep is launched while the
+        host finishes the current iteration); returns (accepted[count], loglik[count])."""
+        acc = np.zeros(count, np.int32)
+        ll = np.zeros(count, np.float64)
+        self._check(self._L.hdpm_iterations(self._h, C.byref(self._params), int(it0), int(count),
+                                            C.byref(self._idx_1_sm), ptr(acc), ptr(ll)))
+        return acc, ll
+
     def run_markov_chain(self, *, verbose=0, m=5, iterations=1000, L=1, c_i=None, burnin=5000, t=10, r=10,
                          neal8=False, split_merge=True, n8_step_size=1, sam_step_size=1, thinning=1):
         p = _lib.ChainParams(verbose, m, iterations, L, burnin, t, r, int(bool(neal8)), int(bool(split_merge)),

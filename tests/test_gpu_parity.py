@@ -119,11 +119,23 @@ def test_zoo_sweeps_with_update_phi_one_cluster(hd, oracle, zoo, debug):
     assert stats["restarts"] > 0
 
 
-@pytest.mark.parametrize("debug", [0, 1, 8, 16])
+# 16: recount the frequency tables every update_phi; 128: no speculative update_phi
+@pytest.mark.parametrize("debug", [0, 1, 8, 16, 128])
 def test_synthetic_sweeps_with_update_phi(hd, oracle, debug):
     ds = synth(6000, 32, 8, 2, seed=3)
     cen, sig = random_params(ds, 8, 7)
     sweep_case(hd, oracle, ds, ds.truth, cen, sig, ds.n * 3, seed=31, sweeps=3, phi=True, debug=debug)
+
+
+def test_speculative_update_phi(hd, oracle):
+    # Separated clusters from the truth: after the first update_phi the sweeps move few or no
+    # points, so update_phi comes (entirely, or for a prefix of labels) from the pass the host
+    # ran during the sweep; every step is compared with the oracle.
+    ds = synth(4000, 64, 6, 4, seed=9)
+    cen, sig = random_params(ds, 6, 11)
+    stats = sweep_case(hd, oracle, ds, ds.truth, cen, sig, ds.n * 3, seed=41, sweeps=8, phi=True)
+    assert stats["phi_spec_runs"] >= 6
+    assert stats["phi_spec_clusters"] > 0
 
 
 def test_synthetic_large_d_sweep(hd, oracle):
@@ -270,6 +282,45 @@ def test_synthetic_chain_matches_oracle(hd, oracle):
     res = hd.run_markov_chain(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w, seed=2, **kw)
     assert np.array_equal(res["c_i"], ref["c_i"])
     np.testing.assert_allclose(res["loglikelihood"], ref["loglikelihood"], rtol=RTOL, atol=0)
+
+
+def test_iteration_api_prepared_sweeps(hd, oracle):
+    # hdpm_iteration prepares the next sweep (draws reserved, update_phi speculated on the
+    # host pool); reading the stream state or the labels in between cancels it, which must
+    # leave no trace: labels and log-likelihoods follow the oracle's chain either way.
+    ds = synth(5000, 64, 8, 4, seed=12)
+    iters = 8
+    kw = dict(m=3, iterations=iters, L=1, c_i=ds.truth, burnin=0, neal8=True, split_merge=False)
+    st, ref = oracle.run_markov_chain(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w, seed=4, fast=1, **kw)
+    assert st == 0
+    eng = make_engine(hd, ds)
+    eng.set_seed(4)
+    params = eng.chain_params(m=3, iterations=iters, L=1, burnin=0, neal8=True, split_merge=False)
+    eng.init_chain(params, c_i=ds.truth)
+    for it in range(iters):
+        _, ll = eng.iteration(it)
+        assert abs(ll - ref["loglikelihood"][it]) <= RTOL * abs(ref["loglikelihood"][it])
+        if it % 3 == 1:
+            c, _, _ = eng.get_state()
+            assert np.array_equal(c, ref["c_i"][it])
+        if it % 3 == 2:
+            _ = eng.rng_state
+    c, _, _ = eng.get_state()
+    assert np.array_equal(c, ref["c_i"][iters - 1])
+    stats = eng.stats()
+    assert stats["phi_spec_clusters"] > 0
+    eng.close()
+    # the batch API launches each next sweep before the host has finished the iteration
+    eng = make_engine(hd, ds)
+    eng.set_seed(4)
+    eng.init_chain(params, c_i=ds.truth)
+    _, ll = eng.iterations(0, 5)
+    np.testing.assert_allclose(ll, ref["loglikelihood"][:5], rtol=RTOL, atol=0)
+    _, ll = eng.iterations(5, iters - 5)
+    np.testing.assert_allclose(ll, ref["loglikelihood"][5:], rtol=RTOL, atol=0)
+    c, _, _ = eng.get_state()
+    assert np.array_equal(c, ref["c_i"][iters - 1])
+    eng.close()
 
 
 # ------------------------------------------------------------------ size-independent properties
