@@ -55,6 +55,12 @@ typedef struct {
     /* update_phi speculated while the device sweeps: passes run, and clusters whose
      * speculative draws were kept (the sweep left them untouched) */
     int64_t phi_spec_runs, phi_spec_clusters;
+    /* prepass launches timed with HIP events (every 8th; t_prepass_ms covers these) and
+     * their points */
+    int64_t prepass_timed, prepass_timed_points;
+    /* device random-stream windows generated: all, and those started from the host state
+     * (a window that did not cover the next draws) */
+    int64_t rng_windows, rng_windows_fresh;
 } hdpm_stats;
 
 int         hdpm_device_count(void);
@@ -143,7 +149,7 @@ int hdpm_reset_stats(hdpm_ctx* ctx);
  * timeline of hdpm_iteration (printed to stderr when the context is destroyed); bit 6:
  * generate latent pools with the sequential host generator instead of the device one; bit 7:
  * no speculative update_phi during the sweep; bit 8: no next sweep prepared at the end of
- * an iteration. */
+ * an iteration; bit 9: HIP events around every kernel of every launch (per-kernel times). */
 int hdpm_set_debug(hdpm_ctx* ctx, int32_t mode);
 /* Block until all device work of the context is done. */
 int hdpm_synchronize(hdpm_ctx* ctx);

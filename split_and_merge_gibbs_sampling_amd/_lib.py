@@ -50,7 +50,8 @@ class Stats(C.Structure):
         [(n, C.c_int64) for n in ("pool_calls", "pool_entries", "pool_device_calls")] + \
         [(n, C.c_double) for n in (
             "t_pool_ms", "t_pool_mt_ms", "t_pool_accept_ms", "t_pool_parse_ms", "t_pool_values_ms")] + \
-        [(n, C.c_int64) for n in ("phi_spec_runs", "phi_spec_clusters")]
+        [(n, C.c_int64) for n in ("phi_spec_runs", "phi_spec_clusters", "prepass_timed", "prepass_timed_points",
+                                  "rng_windows", "rng_windows_fresh")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

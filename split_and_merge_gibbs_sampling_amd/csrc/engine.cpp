@@ -104,13 +104,14 @@ struct PinBuf {
   ~PinBuf() {
     if (p) (void)hipHostFree(p);
   }
-  void ensure(size_t count) {
+  // non-coherent (coarse-grained) by default: CPU-cached, so the host reads these buffers
+  // at cache speed; every device write to them is followed by a stream or event wait
+  // before use.  Buffers kernels read or write in place (no copy) are coherent.
+  void ensure(size_t count, unsigned flags = hipHostMallocNonCoherent) {
     if (count <= n && p) return;
     if (p) (void)hipHostFree(p);
     p = nullptr;
-    // non-coherent (coarse-grained): CPU-cached, so the host reads these buffers at cache
-    // speed; every device write to them is followed by a stream or event wait before use
-    HIPCHK(hipHostMalloc(&p, std::max<size_t>(count, 1) * sizeof(T), hipHostMallocNonCoherent));
+    HIPCHK(hipHostMalloc(&p, std::max<size_t>(count, 1) * sizeof(T), flags));
     n = count;
   }
 };
@@ -421,7 +422,7 @@ struct Ctx {
     int mti = 0;
     int64_t N = 0;
     hipEvent_t ev = nullptr;
-    PinBuf<uint32_t> raw, arrays;
+    PinBuf<uint32_t> raw;
   } phidev;
   RngWindow win[2];
   // MT jump-ahead for multi-workgroup windows (mtjump.hpp)
@@ -437,6 +438,7 @@ struct Ctx {
     hipEvent_t ev = nullptr;
     PinBuf<uint32_t> arr;
     const uint32_t* host_src = nullptr;
+    const uint32_t* from_raw = nullptr;   // tempered words of the state's block (phi_device_prefetch)
     int mti = 0;
   } pend;
   std::string err;
@@ -522,7 +524,6 @@ struct Ctx {
   DevBuf<int4> d_rq;
   DevBuf<uint64_t> d_csum;            // per-label cluster summary for the prepass
   DevBuf<unsigned> d_hist_part;
-  DevBuf<int> d_ctl;                  // ResolveCtl + summary (kernels.hpp)
   DevBuf<long long> d_rprof;          // resolver phase times (debug mode bit 1)
   PinBuf<int> h_ctl;
   // cluster parameter upload staging (UploadLayout)
@@ -549,6 +550,9 @@ struct Ctx {
   PinBuf<double> h_partial;
 
   hdpm_stats stats{};
+  int64_t launch_count = 0;           // resolver launches issued (prepass timing cadence)
+  bool round_timed = false, round_fine = false;
+  int64_t round_points = 0;
   int debug = 0;
   // debug bit 1: per-iteration host timeline
   std::vector<std::pair<const char*, std::chrono::steady_clock::time_point>> trace;
@@ -605,8 +609,13 @@ struct Ctx {
   // ------------------------------------------------------------------ device random stream
   void rng_sync() {
     if (!pend.active) return;
-    HIPCHK(hipEventSynchronize(pend.ev));
-    std::memcpy(rng.mt, pend.host_src ? pend.host_src : pend.arr.p, sizeof(rng.mt));
+    if (pend.from_raw) {
+      HIPCHK(hipEventSynchronize(phidev.ev));
+      for (int i = 0; i < 624; ++i) rng.mt[i] = mt_untemper(pend.from_raw[i]);
+    } else {
+      HIPCHK(hipEventSynchronize(pend.ev));
+      std::memcpy(rng.mt, pend.host_src ? pend.host_src : pend.arr.p, sizeof(rng.mt));
+    }
     rng.mti = pend.mti;
     pend.active = false;
   }
@@ -618,8 +627,10 @@ struct Ctx {
     W.count = count;
     // sized for any start offset (the block count varies with it), so a window of a given
     // length is never reallocated -- a free would synchronise the device
-    W.raw.ensure(count);
-    W.arrays.ensure((size_t)((count + 623) / 624 + 2) * 624);
+    // (with headroom: the span grows a little when the draws between sweeps do)
+    if (W.raw.n < (size_t)count) W.raw.ensure((size_t)count + (size_t)count / 4);
+    const size_t aw = (size_t)((count + 623) / 624 + 2) * 624;
+    if (W.arrays.n < aw) W.arrays.ensure(aw + aw / 4);
     W.init.ensure(624);
     W.h_init.ensure(624);
     if (!W.done) HIPCHK(hipEventCreateWithFlags(&W.done, hipEventDisableTiming));
@@ -639,6 +650,7 @@ struct Ctx {
                 multi ? d_jpoly.p : nullptr, d_jidx.p, d_joff.p, mt_bpg, multi ? mt_G : 1};
     HIPCHK(launch_mt_gen(a, gstream));
     HIPCHK(hipEventRecord(W.done, gstream));
+    stats.rng_windows++;
     W.valid = true;
   }
 
@@ -807,35 +819,43 @@ struct Ctx {
     }
     HIPCHK(hipEventRecord(pend.ev, cstream));
     pend.mti = mti;
+    pend.from_raw = nullptr;
     pend.active = true;
     rng.pos = target;
   }
 
   // update_phi's slice [target, target + N) with the state arrays of its twists, copied from
   // window W when it holds them (else the host generates the slice itself).
-  void phi_device_prefetch(const RngWindow& W, uint64_t target, int64_t N) {
+  // One copy serves both: the words of the state's block from its start (the state after
+  // `target` draws is that block untempered, rng_sync) through the block of the slice's
+  // last word.  False when window W does not hold them (then adopt_state_at).
+  bool phi_device_prefetch(const RngWindow& W, uint64_t target, int64_t N) {
     phidev.valid = false;
-    if (target + (uint64_t)N > W.start_pos + (uint64_t)W.count) return;
     int64_t blk;
     int mti;
     locate(W, target, &blk, &mti);
-    if (blk == 0) return;
-    const int64_t first = mti >= 624 ? 0 : 624 - mti;
-    const int64_t nb = N > first ? (N - first + 623) / 624 : 0;   // twists inside the slice
-    if (blk + nb > W.nblocks) return;
+    if (blk == 0 || mti < 1) return false;
+    const uint64_t s_blk = target - (uint64_t)mti;              // first word of the state's block
+    const int64_t words = 624 * ((mti + N - 1) / 624 + 1);       // through the block of word N - 1
+    if (s_blk < W.start_pos || s_blk + (uint64_t)words > W.start_pos + (uint64_t)W.count) return false;
     // with headroom: a pinned reallocation (hipHostFree) would synchronise the device
-    if (phidev.raw.n < (size_t)N) phidev.raw.ensure(std::max<size_t>(2 * (size_t)N, 1 << 15));
-    if (phidev.arrays.n < (size_t)(nb + 1) * 624) phidev.arrays.ensure((size_t)(2 * nb + 64) * 624);
+    if (phidev.raw.n < (size_t)words) phidev.raw.ensure(std::max<size_t>(2 * (size_t)words, 1 << 15));
     if (!phidev.ev) HIPCHK(hipEventCreateWithFlags(&phidev.ev, hipEventDisableTiming));
-    HIPCHK(hipMemcpyAsync(phidev.raw.p, W.raw.p + (target - W.start_pos), (size_t)N * 4, hipMemcpyDeviceToHost, cstream));
-    HIPCHK(hipMemcpyAsync(phidev.arrays.p, W.arrays.p + (blk - 1) * 624, (size_t)(nb + 1) * 624 * 4,
-                          hipMemcpyDeviceToHost, cstream));
+    HIPCHK(hipStreamWaitEvent(cstream, W.done, 0));
+    HIPCHK(hipMemcpyAsync(phidev.raw.p, W.raw.p + (s_blk - W.start_pos), (size_t)words * 4, hipMemcpyDeviceToHost,
+                          cstream));
     HIPCHK(hipEventRecord(phidev.ev, cstream));
     phidev.valid = true;
     phidev.pos = target;
     phidev.epoch = rng.epoch;
     phidev.mti = mti;
     phidev.N = N;
+    // the host stream continues at target: its state arrives with the copy
+    pend.active = true;
+    pend.from_raw = phidev.raw.p;
+    pend.mti = mti;
+    rng.pos = target;
+    return true;
   }
 
   // Device pointer to the next n raw draws of the stream; advances the host stream past
@@ -847,9 +867,10 @@ struct Ctx {
   // current one has fewer than `kLead` sweeps' worth left, so it is ready well before use.
   static constexpr int kLead = 3;
   int64_t window_span(int64_t n) const {
-    const int64_t per = n + cmax;
+    // independent of cmax unless the draws between sweeps outgrow its allowance, so the
+    // span (window buffers, jump tables) stays fixed
     const int64_t cap = (int64_t)1 << 27;      // 512 MB of draws (+ 512 MB of exported arrays)
-    return std::max(per, std::min<int64_t>(16 * per, cap));
+    return std::max(n + cmax, std::min<int64_t>(16 * (n + (1 << 18)), cap));
   }
   const uint32_t* device_draws(int64_t n) {
     RngWindow* W = nullptr;
@@ -859,12 +880,12 @@ struct Ctx {
       if (win[0].valid || win[1].valid) cmax = std::min<int64_t>(cmax * 2, 1 << 26);
       W = &win[0];
       launch_window(*W, window_span(n), n);
+      stats.rng_windows_fresh++;
     }
     HIPCHK(hipStreamWaitEvent(stream, W->done, 0));
     const uint32_t* p = W->raw.p + (rng.pos - W->start_pos);
     const uint64_t target = rng.pos + n;
-    adopt_state_at(*W, target);
-    phi_device_prefetch(*W, target, phi_prefetch);
+    if (!phi_device_prefetch(*W, target, phi_prefetch)) adopt_state_at(*W, target);
     RngWindow* other = (W == &win[0]) ? &win[1] : &win[0];
     const bool ahead = other->valid && other->epoch == rng.epoch && other->start_pos > W->start_pos;
     const uint64_t wend = W->start_pos + (uint64_t)W->count;
@@ -1414,8 +1435,12 @@ struct Ctx {
   int launch_round(int p, int nslots, int m, const uint32_t* d_sweep_raw, bool track) {
     const double dmax = 0.25;
     ensure_slots(nslots + 2);
-    d_ctl.ensure(8 + 3 * (size_t)scap);
-    h_ctl.ensure(8 + 3 * (size_t)scap);
+    // the resolver writes its control block and summary straight into host memory
+    if (h_ctl.n < 8 + 3 * (size_t)scap) h_ctl.ensure(8 + 3 * (size_t)scap, hipHostMallocCoherent);
+    // HIP events between kernels cost a dispatch gap each: the prepass is timed on every
+    // 8th launch (all launches, and the other kernels too, in the diagnostic modes)
+    round_fine = (debug & (2 | 32 | 512)) != 0;
+    round_timed = round_fine || (launch_count++ % 8 == 0);
     const int S = nslots;
     if (S + m > Ecap) {
       Ecap = std::max(S + m, std::max(2 * Ecap, 32));
@@ -1442,12 +1467,13 @@ struct Ctx {
     pa.p0 = p;
     const int nblocks = (n - p + kBlock - 1) / kBlock;
     HIPCHK(launch_cluster_summary(pa, stream));
-    HIPCHK(hipEventRecord(ev[0], stream));
+    if (round_timed) HIPCHK(hipEventRecord(ev[0], stream));
     HIPCHK(launch_prepass(pa, nblocks, stream));
     stats.prepass_points += n - p;
-    HIPCHK(hipEventRecord(ev[1], stream));
+    round_points = n - p;
+    if (round_timed) HIPCHK(hipEventRecord(ev[1], stream));
     HIPCHK(launch_exact_rows(pa, nblocks, stream));
-    HIPCHK(hipEventRecord(ev[5], stream));
+    if (round_fine) HIPCHK(hipEventRecord(ev[5], stream));
 
     ResolveArgs ra;
     ra.n = n; ra.d = d; ra.dp = dp; ra.m = m; ra.P = P;
@@ -1461,7 +1487,7 @@ struct Ctx {
     ra.rq = pa.rq;
     ra.nblocks = nblocks; ra.p0 = p; ra.T = T; ra.dmax = dmax; ra.scap = scap; ra.K = K;
     ra.lcap = std::min(scap, nslots + 2);
-    ra.nslots = nslots; ra.ctl = (ResolveCtl*)d_ctl.p; ra.summary = d_ctl.p + 8; ra.force_exact = (debug & 1);
+    ra.nslots = nslots; ra.ctl = (ResolveCtl*)h_ctl.p; ra.summary = h_ctl.p + 8; ra.force_exact = (debug & 1);
     ra.prof = nullptr;
     ra.mlog = track ? d_mlog.p : nullptr;
     ra.mcount = track ? d_mcount.p : nullptr;
@@ -1473,24 +1499,27 @@ struct Ctx {
     }
     if (resolve_smem_bytes(ra.lcap, m) > 160 * 1024) { err = "too many clusters for the resolver (K > ~2300)"; return kArg; }
     HIPCHK(launch_resolve(ra, stream));
-    HIPCHK(hipEventRecord(ev[2], stream));
-    HIPCHK(hipMemcpyAsync(h_ctl.p, d_ctl.p, (8 + 3 * (size_t)scap) * 4, hipMemcpyDeviceToHost, stream));
+    if (round_fine) HIPCHK(hipEventRecord(ev[2], stream));
     HIPCHK(hipEventRecord(ev[6], stream));
-    {
-      // the sweep end, enqueued now: it runs only if this launch completes the sweep
-      const ResolveCtl* dctl = (const ResolveCtl*)d_ctl.p;
-      HIPCHK(launch_relabel(d_c.p, d_los.p, n, dctl, stream));
-      if (track) {   // carry the frequency tables: apply the moves, re-index slots -> labels
-        HIPCHK(launch_apply_moves(d_mlog.p, d_mcount.p, (int)std::min<int64_t>(n, 4096), d_codes_t.p, d, nq, mmax,
-                                  d_freq.p, dctl, n, stream));
-        HIPCHK(launch_freq_gather(d_freq.p, d_sol.p, std::min(scap, S + 2), d * mmax, d_freq2.p, dctl, n, stream));
-        const size_t fwords = (size_t)std::min(scap, S + 2) * d * mmax;
-        h_freq_next.ensure(fwords);
-        HIPCHK(hipMemcpyAsync(h_freq_next.p, d_freq2.p, fwords * 4, hipMemcpyDeviceToHost, stream));
-      }
-      HIPCHK(launch_finish_sweep(d_counts.p, d_sol.p, d_los.p, d_src.p, scap, dctl, n, stream));
-    }
     return kOk;
+  }
+
+  // The sweep end after a completed sweep with moves (a sweep without moves leaves labels,
+  // counts, slot maps and frequency tables as they were): slot ids -> labels, the moves
+  // applied to the frequency tables and these re-indexed to labels (copied out behind),
+  // identity slot maps.  The kernels read the final launch's control block in host memory.
+  void launch_sweep_end(int nslots, bool track) {
+    const ResolveCtl* hctl = (const ResolveCtl*)h_ctl.p;
+    HIPCHK(launch_relabel(d_c.p, d_los.p, n, hctl, stream));
+    if (track) {
+      HIPCHK(launch_apply_moves(d_mlog.p, d_mcount.p, (int)std::min<int64_t>(n, 4096), d_codes_t.p, d, nq, mmax,
+                                d_freq.p, hctl, n, stream));
+      HIPCHK(launch_freq_gather(d_freq.p, d_sol.p, std::min(scap, nslots + 2), d * mmax, d_freq2.p, hctl, n, stream));
+      const size_t fwords = (size_t)std::min(scap, nslots + 2) * d * mmax;
+      h_freq_next.ensure(fwords);
+      HIPCHK(hipMemcpyAsync(h_freq_next.p, d_freq2.p, fwords * 4, hipMemcpyDeviceToHost, stream));
+    }
+    HIPCHK(launch_finish_sweep(d_counts.p, d_sol.p, d_los.p, d_src.p, scap, hctl, n, stream));
   }
 
   // The next sweep prepared at the end of an iteration (prepare_next_sweep): its draws
@@ -1572,6 +1601,7 @@ struct Ctx {
     // update_phi can be speculated during the sweep when the host holds the pre-sweep
     // frequency tables of every label and the sweep carries them (move log)
     const bool spec_go = freq_dev_valid && freq_version == labels_version && !(debug & (128 | 16));
+    const bool freq_before_ok = freq_version == labels_version && !(debug & 16);
     if (!use_ahead) spec.ran = false;
     spec.lv = 0;
     labels_version++;
@@ -1621,13 +1651,20 @@ struct Ctx {
       mark("prefill");
       HIPCHK(hipEventSynchronize(ev[6]));
       mark("resolved");
-      float t1 = 0, t2 = 0, t3 = 0;
-      HIPCHK(hipEventElapsedTime(&t1, ev[0], ev[1]));
-      HIPCHK(hipEventElapsedTime(&t3, ev[1], ev[5]));
-      HIPCHK(hipEventElapsedTime(&t2, ev[5], ev[2]));
-      stats.t_prepass_ms += t1;
-      stats.t_exact_ms += t3;
-      stats.t_resolve_ms += t2;
+      if (round_timed) {
+        float t1 = 0;
+        HIPCHK(hipEventElapsedTime(&t1, ev[0], ev[1]));
+        stats.t_prepass_ms += t1;
+        stats.prepass_timed++;
+        stats.prepass_timed_points += round_points;
+      }
+      if (round_fine) {
+        float t2 = 0, t3 = 0;
+        HIPCHK(hipEventElapsedTime(&t3, ev[1], ev[5]));
+        HIPCHK(hipEventElapsedTime(&t2, ev[5], ev[2]));
+        stats.t_exact_ms += t3;
+        stats.t_resolve_ms += t2;
+      }
       stats.rounds++;
       const ResolveCtl c = *(const ResolveCtl*)h_ctl.p;
       if (debug & 2) {
@@ -1661,11 +1698,19 @@ struct Ctx {
     const int* sol = h_ctl.p + 8;
     const int* cnt = sol + scap;
     const int* src = cnt + scap;
-    if (track) {   // the gather of the final launch wrote freq2 (and its copy is on its way)
-      std::swap(d_freq.p, d_freq2.p);
-      std::swap(d_freq.n, d_freq2.n);
+    if (sweep_moves > 0) {
+      launch_sweep_end(nslots, track);
+      if (track) {   // the gather wrote freq2 (and its copy is on its way)
+        std::swap(d_freq.p, d_freq2.p);
+        std::swap(d_freq.n, d_freq2.n);
+        freq_d2h_version = labels_version;
+        freq_next_pending = true;    // into h_freq_next; update_phi swaps it in
+      }
+    } else if (track && freq_before_ok) {
+      // nothing moved: the host's tables are still current
+      freq_version = labels_version;
       freq_d2h_version = labels_version;
-      freq_next_pending = true;      // into h_freq_next; update_phi swaps it in
+      freq_next_pending = false;
     }
     h_center.assign((size_t)K * d, 0);
     h_sigma.assign((size_t)K * d, 0.0);
@@ -1797,10 +1842,10 @@ struct Ctx {
     if (dev) {
       HIPCHK(hipEventSynchronize(phidev.ev));
       if (pj_open) pj.ns_f2.store(pj_ns());
-      dev = std::memcmp(phidev.arrays.p, rng.mt, sizeof(rng.mt)) == 0;
+      for (int i = 0; i < 624 && dev; ++i) dev = mt_untemper(phidev.raw.p[i]) == rng.mt[i];
     }
     if (dev) {
-      sa.fill_raw(rng, phidev.raw.p, phidev.N, phidev.arrays.p + 624);
+      sa.fill_raw(rng, phidev.raw.p, phidev.N);
       return true;
     }
     return sa.fill(rng, N);

@@ -1793,11 +1793,13 @@ __global__ __launch_bounds__(640) void k_mt_gen(MtGenArgs a) {
 // correlation (jpoly[g] = z^(624 bpg g - 1) mod phi, offset +1) of the next 33 blocks of
 // the stream (mtjump.hpp), then twists its own
 // segment of blocks [g * bpg, (g + 1) * bpg) (the last active one runs to the end).
+constexpr int kJumpChunk = 4096;
 __global__ __launch_bounds__(640) void k_mt_gen_multi(MtGenArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* seq = lds;                    // 33 * 624 words (jumping workgroups)
   uint32_t* buf0 = lds + 33 * 624;        // 2 * 624 words
   uint32_t* buf1 = buf0 + 624;
+  uint32_t* jl = buf1 + 624;              // kJumpChunk staged bit positions
   const int t = threadIdx.x;
   const int g = blockIdx.x;
   const int64_t b_last = (a.count - 1 + a.mti0) / 624;      // last block with an output
@@ -1814,24 +1816,31 @@ __global__ __launch_bounds__(640) void k_mt_gen_multi(MtGenArgs a) {
       if (t < 624) seq[blk * 624 + t] = mt_twist_elem(seq + (blk - 1) * 624, t);
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    // out[t] = XOR over the set bits i of the jump polynomial of seq[i + t + 1]; the bit
-    // positions come as a list (scalar loads), so the LDS reads issue back to back
+    // out[t] = XOR over the set bits i of the jump polynomial of seq[i + t + 1].  The bit
+    // positions are staged through LDS in chunks (coalesced loads; every lane then reads
+    // the same index, an LDS broadcast), so no lane waits on a global load per index.
     uint32_t acc = 0;
-    if (t < 624) {
-      const uint32_t* L = a.jidx + ldu(a.joff + g);
-      const int cnt = ldu(a.joff + g + 1) - ldu(a.joff + g);
-      const uint32_t* s0 = seq + t + 1;
-      int q = 0;
-      for (; q + 16 <= cnt; q += 16) {
-        uint32_t v[16];
+    const uint32_t* L = a.jidx + ldu(a.joff + g);
+    const int cnt = ldu(a.joff + g + 1) - ldu(a.joff + g);
+    const uint32_t* s0 = seq + t + 1;
+    for (int c0 = 0; c0 < cnt; c0 += kJumpChunk) {
+      const int cn = min(kJumpChunk, cnt - c0);
+      for (int q = t; q < cn; q += blockDim.x) jl[q] = L[c0 + q];
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (t < 624) {
+        int q = 0;
+        for (; q + 16 <= cn; q += 16) {
+          uint32_t v[16];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) v[u] = s0[ldu(L + q + u)];
+          for (int u = 0; u < 16; ++u) v[u] = s0[jl[q + u]];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) acc ^= v[u];
+          for (int u = 0; u < 16; ++u) acc ^= v[u];
+        }
+        for (; q < cn; ++q) acc ^= s0[jl[q]];
       }
-      for (; q < cnt; ++q) acc ^= s0[ldu(L + q)];
-      buf0[t] = acc;
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
+    if (t < 624) buf0[t] = acc;
   }
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   uint32_t* cur = buf0;
@@ -1860,7 +1869,7 @@ __global__ __launch_bounds__(640) void k_mt_gen_multi(MtGenArgs a) {
 
 hipError_t launch_mt_gen(const MtGenArgs& a, hipStream_t s) {
   if (a.G > 1 && a.jpoly) {
-    const size_t lds = (size_t)(33 + 2) * 624 * 4;
+    const size_t lds = ((size_t)(33 + 2) * 624 + kJumpChunk) * 4;
     hipLaunchKernelGGL(k_mt_gen_multi, dim3(a.G), dim3(640), lds, s, a);
   } else {
     hipLaunchKernelGGL(k_mt_gen, dim3(1), dim3(640), 0, s, a);

@@ -81,17 +81,7 @@ inline int64_t pool_slice_len(const PoolPlan& pl, int64_t P, double extra = 1.0)
   return (int64_t)((mu * 1.005 + 10.0 * sd) * extra) + 4096;
 }
 
-// MT19937 tempering inverse: the state word behind an output
-inline uint32_t mt_untemper(uint32_t y) {
-  y ^= y >> 18;
-  y ^= (y << 15) & 0xefc60000u;
-  uint32_t t = y;
-  for (int i = 0; i < 5; ++i) t = y ^ ((t << 7) & 0x9d2c5680u);
-  y = t;
-  t = y;
-  for (int i = 0; i < 3; ++i) t = y ^ (t >> 11);
-  return t;
-}
+// (mt_untemper: rmath.hpp)
 
 // Host model of the device pipeline on `raw` (the slice): packed accept tables, parse,
 // values.  Returns the position after the P-th entry, or -1 on overrun.

@@ -33,6 +33,17 @@ enum Status : int {
 };
 
 // ------------------------------------------------------------------ R MT19937
+// Inverse of MT19937's tempering: the mt word behind a raw output.
+inline uint32_t mt_untemper(uint32_t y) {
+  y ^= y >> 18;                                  // self-inverse
+  y ^= (y << 15) & 0xefc60000u;                  // self-inverse (the shifted bits leave the word)
+  uint32_t r = y;
+  for (int i = 0; i < 5; ++i) r = y ^ ((r << 7) & 0x9d2c5680u);
+  y = r;
+  for (int i = 0; i < 3; ++i) r = y ^ (r >> 11);
+  return r;
+}
+
 struct Rng {
   int32_t mti = 625;
   uint32_t mt[624];
@@ -349,12 +360,15 @@ struct StreamAhead {
   Rng* live = nullptr;
   bool spilled = false;
   const uint32_t* raw = nullptr;   // fill_raw: tempered words; u[] is filled by logits()
+  const uint32_t* rawblk = nullptr;  // fill_raw: the words from the start of the state's block
+  int mti0 = 0;
 
   bool fill(const Rng& r, int64_t N) {
     n = 0;
     used = 0;
     spilled = false;
     raw = nullptr;
+    rawblk = nullptr;
     if (r.mti > 624) return false;           // never seeded: let the live Rng handle it
     start = r;
     Rng g = r;
@@ -378,27 +392,22 @@ struct StreamAhead {
     return true;
   }
   // The same prefix from words generated elsewhere (the device windows): r is the state
-  // before the first word (its mt array and mti), raw[0..N) the tempered outputs, and
-  // arrays[v] the mt array after the v-th twist past r (624 words each).  u[] is computed
-  // by logits(), so the caller only copies the state arrays here.
-  void fill_raw(const Rng& r, const uint32_t* raw_, int64_t N, const uint32_t* arrays) {
+  // before the first word (mt array, mti); blk holds the tempered words of r's block from
+  // its start, then the following blocks (at least through the block of word N - 1), so
+  // word k is blk[r.mti + k] and every later state array is the untempered block.  u[] is
+  // computed by logits(), the arrays by restore() when needed.
+  void fill_raw(const Rng& r, const uint32_t* blk, int64_t N) {
     start = r;
-    n = 0;
     used = 0;
     spilled = false;
-    raw = raw_;
+    rawblk = blk;
+    mti0 = r.mti;
+    raw = blk + r.mti;
     u.resize(N);
     lg.resize(N);
     lz.resize(N);
     vfirst.assign(1, 0);
     arr.resize(1);
-    std::memcpy(arr[0].data(), r.mt, sizeof(r.mt));
-    int64_t k = r.mti >= 624 ? 0 : 624 - r.mti;   // first word drawn after a twist
-    for (int v = 0; k < N; ++v, k += 624) {
-      vfirst.push_back(k);
-      arr.emplace_back();
-      std::memcpy(arr.back().data(), arrays + (size_t)v * 624, 624 * sizeof(uint32_t));
-    }
     n = N;
   }
   void logits(int64_t a, int64_t b) {
@@ -414,6 +423,12 @@ struct StreamAhead {
     const uint64_t ep = r.epoch;
     if (c == 0) {
       r = start;
+    } else if (rawblk) {
+      const int64_t w = c - 1;
+      const int64_t v = (mti0 + w) / 624;
+      for (int i = 0; i < 624; ++i) r.mt[i] = mt_untemper(rawblk[624 * v + i]);
+      r.mti = (int32_t)(mti0 + w - 624 * v + 1);
+      r.pos = start.pos + (uint64_t)c;
     } else {
       const int64_t w = c - 1;
       size_t v = 0;

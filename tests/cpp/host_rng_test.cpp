@@ -4,6 +4,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "../../split_and_merge_gibbs_sampling_amd/csrc/rmath.hpp"
 
@@ -56,6 +57,37 @@ int main() {
     sa.finish();
     CHECK(same(live, seq));
     (void)ref;
+  }
+  // fill_raw: the same prefix from the tempered words of the state's block onwards (as
+  // copied from a device window); states come back by untempering
+  for (int pre : {1, 311, 623, 624, 1300}) {
+    Rng r;
+    r.set_seed(20240602u);
+    for (int k = 0; k < pre; ++k) (void)r.unif();
+    // the words of r's block from its start, then the next blocks (a replay from the block start)
+    Rng g;
+    g.set_seed(20240602u);
+    const int blk_start = pre - r.mti;
+    for (int k = 0; k < blk_start; ++k) (void)g.unif();
+    std::vector<uint32_t> words(624 * 8);
+    for (auto& w : words) w = g.raw();
+    for (int i = 0; i < 624; ++i) CHECK(mt_untemper(words[i]) == r.mt[i]);
+    StreamAhead sa;
+    sa.fill_raw(r, words.data(), 3000);
+    sa.logits(0, 1500);
+    sa.logits(1500, sa.n);
+    for (int c = 0; c <= 3000; c += (c < 1300 ? 1 : 97)) {
+      Rng got = r;
+      sa.restore(got, c);
+      Rng seq = r;
+      for (int k = 0; k < c; ++k) (void)seq.unif();
+      CHECK(same(got, seq));
+      if (c < 3000) {
+        Rng one = seq;
+        CHECK(sa.u[c] == one.unif());
+        if (c + 1 < 3000) CHECK(sa.lz[c] == std::log(sa.u[c] * sa.u[c] * sa.u[c + 1]));
+      }
+    }
   }
   // the split rbeta equals the one-call form, draw for draw
   const double ps[][2] = {{0.3, 0.7}, {0.5, 5.0}, {2.0, 3.0}, {14501.0, 35501.0}, {1.0, 1.0}, {0.0, 0.0}, {3.0, 0.0}};
