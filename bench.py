@@ -39,10 +39,19 @@ def packed_layout(d: int, mmax: int):
 
 def prepass_bytes_per_point(d: int, mmax: int, m: int) -> int:
     """Compulsory bytes k_prepass moves per point: its bit-sliced row
-    (8 W), its m+1 raw draws (4(m+1)), its label (4), the bound records of its m latent pool
-    picks (8 bw each), its margin (8) and row index (4)."""
-    _, W, bw = packed_layout(d, mmax)
-    return 8 * W + 4 * (m + 1) + 4 + m * 8 * bw + 12
+    (8 W), its m+1 raw draws (4(m+1)), its label (4), the first gather of each of its m
+    latent pool picks -- the pool-entry head (W + 2 words padded to a power of two: 64 B at
+    C5) when the layout has one, else the full bound record (8 bw) -- its margin (8) and
+    row index (4).  The full
+    records a head leaves uncertain (6e-5 of the picks at C5) are extra traffic, not
+    counted here."""
+    wb, W, bw = packed_layout(d, mmax)
+    Ws = W // wb
+    head = Ws == 2 or (Ws == 4 and wb <= 4)           # csrc/kernels.hpp head_fits
+    hs = 4
+    while hs < W + 2:
+        hs *= 2
+    return 8 * W + 4 * (m + 1) + 4 + m * 8 * (hs if head else bw) + 12
 
 
 def survey_sweep_bytes(n: int, d: int, m: int) -> int:
@@ -242,6 +251,7 @@ def main():
                 **{k: round(st[k] / args.steps, 4) for k in ("t_exact_ms", "t_resolve_ms") if st[k] > 0},
                 **{k: round(st[k] / args.steps, 4) for k in ("t_stats_ms", "t_host_phi_ms", "t_rng_ms", "t_loglik_ms")}),
             "exact_points_per_step": st["exact_points"] / args.steps,
+            "listed_points_per_step": st["listed_points"] / args.steps,
             "split_merge": bool(args.sm),
             "rounds_per_step": st["rounds"] / args.steps,
             "rng_windows": {"launched": st["rng_windows"], "fresh": st["rng_windows_fresh"]},

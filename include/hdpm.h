@@ -61,6 +61,8 @@ typedef struct {
     /* device random-stream windows generated: all, and those started from the host state
      * (a window that did not cover the next draws) */
     int64_t rng_windows, rng_windows_fresh;
+    /* points the prepass could not prove "stay" (exact rows built for them) */
+    int64_t listed_points;
 } hdpm_stats;
 
 int         hdpm_device_count(void);
@@ -149,8 +151,14 @@ int hdpm_reset_stats(hdpm_ctx* ctx);
  * timeline of hdpm_iteration (printed to stderr when the context is destroyed); bit 6:
  * generate latent pools with the sequential host generator instead of the device one; bit 7:
  * no speculative update_phi during the sweep; bit 8: no next sweep prepared at the end of
- * an iteration; bit 9: HIP events around every kernel of every launch (per-kernel times). */
+ * an iteration; bit 9: HIP events around every kernel of every launch (per-kernel times);
+ * bit 10: the prepass gathers full bound records for latent picks (no pool-entry heads);
+ * bit 11: exact rows one wave per point (no workgroup-per-point LDS staging). */
 int hdpm_set_debug(hdpm_ctx* ctx, int32_t mode);
+/* The prepass's pool-entry heads, P entries of wb*Ws + 2 words padded to a power of two
+ * (csrc/kernels.hpp "Pool-entry heads"); HDPM_E_ARG when the data's layout has none (d > 256, or d > 128 with
+ * m_j > 16). */
+int hdpm_get_pool_heads(hdpm_ctx* ctx, uint64_t* out, int64_t P);
 /* Block until all device work of the context is done. */
 int hdpm_synchronize(hdpm_ctx* ctx);
 

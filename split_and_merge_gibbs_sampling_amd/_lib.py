@@ -23,6 +23,7 @@ EXPORTS = (
     "hdpm_compute_loglikelihood", "hdpm_loglik_matrix", "hdpm_restricted_gibbs", "hdpm_logprobgs_c_i",
     "hdpm_split_and_merge", "hdpm_run_markov_chain", "hdpm_get_stats", "hdpm_reset_stats",
     "hdpm_set_debug", "hdpm_synchronize", "hdpm_init_chain", "hdpm_iteration", "hdpm_iterations", "hdpm_rng_fill_device",
+    "hdpm_get_pool_heads",
 )
 
 STATUS = {0: "OK", 1: "E_VALIDATE", 2: "E_GSL", 3: "E_PROB", 4: "E_WALKER", 5: "E_ARG",
@@ -51,7 +52,7 @@ class Stats(C.Structure):
         [(n, C.c_double) for n in (
             "t_pool_ms", "t_pool_mt_ms", "t_pool_accept_ms", "t_pool_parse_ms", "t_pool_values_ms")] + \
         [(n, C.c_int64) for n in ("phi_spec_runs", "phi_spec_clusters", "prepass_timed", "prepass_timed_points",
-                                  "rng_windows", "rng_windows_fresh")]
+                                  "rng_windows", "rng_windows_fresh", "listed_points")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -109,6 +110,7 @@ def lib():
         "hdpm_rng_fill_device": ([vp, i64, vp], C.c_int),
         "hdpm_set_debug": ([vp, i32], C.c_int),
         "hdpm_synchronize": ([vp], C.c_int),
+        "hdpm_get_pool_heads": ([vp, vp, i64], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

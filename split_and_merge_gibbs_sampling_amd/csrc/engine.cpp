@@ -47,6 +47,8 @@ hipError_t launch_freq_gather(const unsigned int* freq, const int* sol, int Kmax
 hipError_t launch_scatter_clusters(const uint8_t* stage, int nent, int dp, int d, int bw, int full, uint8_t* codes,
                                    double* tab, uint64_t* bnd, int* counts, int* sol, int* los, int* src,
                                    hipStream_t s);
+hipError_t launch_pool_heads(const double* tab, const uint64_t* bnd, int64_t P, int d, int wb, int Ws, int bw, int ha,
+                             int hb, uint64_t* head, hipStream_t s);
 hipError_t launch_hist(const HistArgs& a, hipStream_t s);
 size_t hist_partial_words(const HistArgs& a, int* nbx, int* kc, int* tpb);
 hipError_t launch_loglik(const LoglikArgs& a, hipStream_t s);
@@ -488,7 +490,16 @@ struct Ctx {
   DevBuf<uint8_t> d_pool_codes;
   DevBuf<double> d_pool_tab;
   DevBuf<uint64_t> d_pool_bnd;
+  DevBuf<uint64_t> d_pool_head;       // P x head_words (head_fits): the prepass's gather per latent pick
+  int head_ha = 0, head_hb = 0;       // kernels.hpp "Pool-entry heads": h_a, h_b of this data
   DevBuf<double> d_pool_sig;          // P x d sigma (device generator)
+
+  // pool-entry heads from the device tables and bound records (every pool install)
+  void build_pool_heads() {
+    if (!head_fits(wb, Ws) || P <= 0) return;
+    d_pool_head.ensure((size_t)P * head_stride(wb, Ws));
+    HIPCHK(launch_pool_heads(d_pool_tab.p, d_pool_bnd.p, P, d, wb, Ws, bw, head_ha, head_hb, d_pool_head.p, stream));
+  }
 
   // stream-exact device pool generator (pool_gen.hpp)
   struct PoolGen {
@@ -525,7 +536,9 @@ struct Ctx {
   DevBuf<uint64_t> d_csum;            // per-label cluster summary for the prepass
   DevBuf<unsigned> d_hist_part;
   DevBuf<long long> d_rprof;          // resolver phase times (debug mode bit 1)
-  PinBuf<int> h_ctl;
+  PinBuf<int> h_ctl;                  // [ResolveCtl | pad to kCtlInts][resolver summary: 3 scap]
+  static constexpr size_t kCtlInts = 16;
+  static_assert(sizeof(ResolveCtl) <= kCtlInts * sizeof(int), "control block");
   // cluster parameter upload staging (UploadLayout)
   // two pinned staging buffers: one can be filled (e.g. by the update_phi speculated for the
   // next sweep) while the last commit's copy from the other is still in flight
@@ -1097,6 +1110,17 @@ struct Ctx {
     Ws = plane_words(d);
     bw = bound_words(wb, Ws);
     {
+      // mismatches of a point with a uniform latent center: mean and sd over the attributes
+      double mu = 0.0, s2 = 0.0;
+      for (int j = 0; j < d; ++j) {
+        const double q = 1.0 / att[j];
+        mu += 1.0 - q;
+        s2 += (1.0 - q) * q;
+      }
+      head_ha = std::max(0, (int)std::floor(mu - 4.0 * std::sqrt(s2)));
+      head_hb = std::max(0, (int)std::floor(mu - 1.25 * std::sqrt(s2)));
+    }
+    {
       const int Wr = wb * Ws;
       std::vector<uint64_t> xs((size_t)n64 * Wr, 0);
       parallel_for(n, [&](int64_t a0, int64_t a1) {
@@ -1174,6 +1198,7 @@ struct Ctx {
     HIPCHK(hipMemcpyAsync(d_pool_codes.p, pc.data(), pc.size(), hipMemcpyHostToDevice, stream));
     HIPCHK(hipMemcpyAsync(d_pool_tab.p, pt.data(), pt.size() * 8, hipMemcpyHostToDevice, stream));
     HIPCHK(hipMemcpyAsync(d_pool_bnd.p, pb.data(), pb.size() * 8, hipMemcpyHostToDevice, stream));
+    build_pool_heads();
     HIPCHK(hipStreamSynchronize(stream));
   }
 
@@ -1338,6 +1363,7 @@ struct Ctx {
                        pg.runs.p, pg.runs.p + pl.run_cls.size(), pg.cls.p, pg.bm.p, nwords, pg.gtab.p,
                        d_pool_codes.p, d_pool_tab.p, d_pool_sig.p, d_pool_bnd.p, pg.err.p};
       HIPCHK(launch_pool_values(va, stream));
+      build_pool_heads();
       HIPCHK(hipMemcpyAsync(pg.h_err.p, pg.err.p, 4, hipMemcpyDeviceToHost, stream));
 
       // the stream continues after `end` draws: mti and the block array (untempered outputs)
@@ -1436,7 +1462,7 @@ struct Ctx {
     const double dmax = 0.25;
     ensure_slots(nslots + 2);
     // the resolver writes its control block and summary straight into host memory
-    if (h_ctl.n < 8 + 3 * (size_t)scap) h_ctl.ensure(8 + 3 * (size_t)scap, hipHostMallocCoherent);
+    if (h_ctl.n < kCtlInts + 3 * (size_t)scap) h_ctl.ensure(kCtlInts + 3 * (size_t)scap, hipHostMallocCoherent);
     // HIP events between kernels cost a dispatch gap each: the prepass is timed on every
     // 8th launch (all launches, and the other kernels too, in the diagnostic modes)
     round_fine = (debug & (2 | 32 | 512)) != 0;
@@ -1455,6 +1481,9 @@ struct Ctx {
     pa.pool = ParamTables{d_pool_codes.p, d_pool_tab.p};
     pa.P = P; pa.raw = d_sweep_raw; pa.m = m; pa.logn = d_logn.p; pa.logfac = std::log(gamma / m);
     pa.xbs = d_xbs.p; pa.Ws = Ws; pa.wb = wb; pa.slot_bnd = d_slot_bnd.p; pa.pool_bnd = d_pool_bnd.p; pa.bw = bw;
+    pa.pool_head = (head_fits(wb, Ws) && !(debug & 1024)) ? d_pool_head.p : nullptr;
+    pa.head_ha = head_ha;
+    pa.head_hb = head_hb;
     d_csum.ensure((size_t)std::max(K, 1) * (bw + 2));
     pa.csum = d_csum.p;
 
@@ -1465,6 +1494,7 @@ struct Ctx {
     pa.spec_rad = d_spec_rad.p;
     pa.rq = d_rq.p;
     pa.p0 = p;
+    pa.exact_wave = (debug & 2048) ? 1 : 0;
     const int nblocks = (n - p + kBlock - 1) / kBlock;
     HIPCHK(launch_cluster_summary(pa, stream));
     if (round_timed) HIPCHK(hipEventRecord(ev[0], stream));
@@ -1487,7 +1517,7 @@ struct Ctx {
     ra.rq = pa.rq;
     ra.nblocks = nblocks; ra.p0 = p; ra.T = T; ra.dmax = dmax; ra.scap = scap; ra.K = K;
     ra.lcap = std::min(scap, nslots + 2);
-    ra.nslots = nslots; ra.ctl = (ResolveCtl*)h_ctl.p; ra.summary = h_ctl.p + 8; ra.force_exact = (debug & 1);
+    ra.nslots = nslots; ra.ctl = (ResolveCtl*)h_ctl.p; ra.summary = h_ctl.p + kCtlInts; ra.force_exact = (debug & 1);
     ra.prof = nullptr;
     ra.mlog = track ? d_mlog.p : nullptr;
     ra.mcount = track ? d_mcount.p : nullptr;
@@ -1677,6 +1707,7 @@ struct Ctx {
                      (tp[7] - tp[0]) / 100.0);
       }
       stats.exact_points += c.exact;
+      stats.listed_points += c.listed;
       stats.moves += c.moves;
       sweep_moves += c.moves;
       stats.checked_rounds += c.checked;
@@ -1695,7 +1726,7 @@ struct Ctx {
 
     // slots -> labels; rebuild per-label parameters and counts from the resolver summary
     auto ts0 = std::chrono::steady_clock::now();
-    const int* sol = h_ctl.p + 8;
+    const int* sol = h_ctl.p + kCtlInts;
     const int* cnt = sol + scap;
     const int* src = cnt + scap;
     if (sweep_moves > 0) {
@@ -2859,6 +2890,17 @@ int hdpm_set_debug(hdpm_ctx* h, int32_t mode) {
   CTX();
   ctx->debug = mode;
   return HDPM_OK;
+}
+int hdpm_get_pool_heads(hdpm_ctx* h, uint64_t* out, int64_t P) {
+  CTX();
+  if (!out || P != ctx->P || P <= 0) { ctx->err = "pool size mismatch"; return HDPM_E_ARG; }
+  if (!hdpm::head_fits(ctx->wb, ctx->Ws)) { ctx->err = "no pool-entry heads for this layout"; return HDPM_E_ARG; }
+  GUARD({
+    HIPCHK(hipMemcpyAsync(out, ctx->d_pool_head.p, (size_t)P * hdpm::head_stride(ctx->wb, ctx->Ws) * 8, hipMemcpyDeviceToHost,
+                          ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return HDPM_OK;
+  })
 }
 int hdpm_synchronize(hdpm_ctx* h) {
   CTX();

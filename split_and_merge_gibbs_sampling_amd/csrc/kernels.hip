@@ -254,12 +254,41 @@ __global__ void k_cluster_summary(PrepassArgs a) {
 //     flight together when the records are small).
 // margin = lo - max(ub) is a lower bound on how far the own cluster leads every other
 // entry; the point is certain when it exceeds `thresh`.
+// Upper bound on a latent entry's log-weight from its head (kernels.hpp "Pool-entry
+// heads"); lanes whose head bound does not clear `cut` gather the full record and take
+// the precise bound as well.
 template <int WB, int WS>
+__device__ __forceinline__ double latent_ub_head(const PrepassArgs& a, const uint64_t (&x)[WB * WS],
+                                                 const uint64_t (&Hd)[WB * WS + 2], int64_t e, double cut) {
+  constexpr int RW = (WB + kQ) * WS + 4, SC = (WB + kQ) * WS, HW = WB * WS + 2;
+  uint64_t M[WS];
+  const int H = mismatch_r<WB, WS, HW>(x, Hd, M);
+  const uint64_t p0 = Hd[HW - 2], p1 = Hd[HW - 1];
+  const double A = (double)__uint_as_float((uint32_t)p0), dmn = (double)__uint_as_float((uint32_t)(p0 >> 32));
+  const double sa = (double)__uint_as_float((uint32_t)p1), sb = (double)__uint_as_float((uint32_t)(p1 >> 32));
+  double low = dmn * (double)H;
+  if (H >= a.head_ha) low = fmax(low, sa + dmn * (double)(H - a.head_ha));
+  if (H >= a.head_hb) low = fmax(low, sb + dmn * (double)(H - a.head_hb));
+  double ub = a.logfac + (A - low + kBoundEps * (1.0 + fabs(A) + low));
+  if (ub > cut) {
+    uint64_t R[RW];
+    load_record<RW>(a.pool_bnd + e * a.bw, R);
+    const int Sq = penalty_r<WB, WS, RW>(M, R);
+    const double Af = as_f64(R[SC]), dl = as_f64(R[SC + 1]);
+    const double pmin = dl * (double)Sq, pmax = dl * (double)(Sq + H);
+    ub = fmin(ub, a.logfac + (Af - pmin + kBoundEps * (1.0 + fabs(Af) + pmax)));
+  }
+  return ub;
+}
+
+template <int WB, int WS, bool HEAD>
 __global__ __launch_bounds__(kBlock) void k_prepass(PrepassArgs a) {
   constexpr int WR = WB * WS;                  // row words
   constexpr int RW = (WB + kQ) * WS + 4;       // record words
   constexpr int SC = (WB + kQ) * WS;           // record scalars: A, delta, dmin, scale
-  constexpr int NPF = RW <= 16 ? 3 : RW <= 32 ? 2 : 1;   // pool records in flight
+  constexpr int NPF = HEAD ? 3 : RW <= 16 ? 3 : RW <= 32 ? 2 : 1;   // pool records in flight
+  constexpr int LW = HEAD ? WR + 2 : RW;       // words gathered first per latent pick
+  constexpr int HS = head_stride(WB, WS);      // head stride (words)
   const int tid = threadIdx.x;
   const int64_t i = (int64_t)a.p0 + (int64_t)blockIdx.x * kBlock + tid;
   const bool active = i < a.n;
@@ -274,10 +303,16 @@ __global__ __launch_bounds__(kBlock) void k_prepass(PrepassArgs a) {
   if (own_cnt >= 2) {
     // the first latent records' gathers go out first: their latency overlaps the
     // own-cluster bound and the cluster loop
-    uint64_t Rp[NPF][RW];
+    uint64_t Rp[NPF][LW];
+    int64_t pe[NPF];
+    auto gather = [&](int u, int l) {
+      pe[u] = pick_entry(raw[l], a.P);
+      if constexpr (HEAD) load_record<LW>(a.pool_head + pe[u] * HS, Rp[u]);
+      else load_record<LW>(a.pool_bnd + pe[u] * a.bw, Rp[u]);
+    };
 #pragma unroll
     for (int u = 0; u < NPF; ++u)
-      if (u < a.m) load_record<RW>(a.pool_bnd + pick_entry(raw[u], a.P) * a.bw, Rp[u]);
+      if (u < a.m) gather(u, u);
     uint64_t M[WS];
     double lo;
     {
@@ -311,11 +346,13 @@ __global__ __launch_bounds__(kBlock) void k_prepass(PrepassArgs a) {
       if (l0 > 0) {
 #pragma unroll
         for (int u = 0; u < NPF; ++u)
-          if (l0 + u < a.m) load_record<RW>(a.pool_bnd + pick_entry(raw[l0 + u], a.P) * a.bw, Rp[u]);
+          if (l0 + u < a.m) gather(u, l0 + u);
       }
 #pragma unroll
       for (int u = 0; u < NPF; ++u) {
-        if (l0 + u < a.m) {
+        if constexpr (HEAD) {
+          if (l0 + u < a.m) ubmax = fmax(ubmax, latent_ub_head<WB, WS>(a, x, Rp[u], pe[u], cut));
+        } else if (l0 + u < a.m) {
           const int H = mismatch_r<WB, WS, RW>(x, Rp[u], M);
           const int Sq = penalty_r<WB, WS, RW>(M, Rp[u]);
           const double A = as_f64(Rp[u][SC]), dl = as_f64(Rp[u][SC + 1]);
@@ -800,6 +837,49 @@ __device__ void copy_pool_params(const ResolveArgs& a, int64_t e, int s) {
   for (int b = lane; b < a.bw; b += kWave) a.slot_bnd[(int64_t)s * a.bw + b] = a.pool_bnd[e * a.bw + b];
 }
 
+// The snapshot draw of an uncertain point from its row (acc_r: entry e in lane e % 64 of
+// register e / 64), with the resolver's exact decision (one wave).
+template <int RE>
+__device__ void exact_rows_decide(const PrepassArgs& a, int q, int64_t i, const uint32_t* raw, double (&acc_r)[RE],
+                                  double* lp, int* lperm, int* lpick) {
+  const int lane = threadIdx.x & 63;
+  const int E = a.K + a.m;
+  {
+    if (!a.spec) return;
+    // n8:40-94 in the snapshot state: logn[count - (slot == own)] + ll for the clusters,
+    // log(gamma / m) + ll for the latents (the singleton's first latent is its own cluster)
+    const int own = __builtin_amdgcn_readfirstlane(a.c[i]);
+    const int own_cnt = a.counts[own];
+    double ll_own = 0.0;
+    double pv[RE];
+#pragma unroll
+    for (int r = 0; r < RE; ++r) {
+      const int e = r * kWave + lane;
+      int s = -1;
+      if (e < a.K) s = a.slot_of_label[e];
+      const unsigned long long bo = __ballot(s == own);
+      if (bo) ll_own = readlane_f64(acc_r[r], __ffsll((long long)bo) - 1);
+      double v = -INFINITY;
+      if (e < a.K) v = a.logn[a.counts[s] - (s == own ? 1 : 0)] + acc_r[r];
+      pv[r] = v;
+    }
+#pragma unroll
+    for (int r = 0; r < RE; ++r) {
+      const int e = r * kWave + lane;
+      if (e >= a.K && e < E) {
+        const int l = e - a.K;
+        pv[r] = a.logfac + ((l == 0 && own_cnt == 1) ? ll_own : acc_r[r]);
+      }
+    }
+    double rad = 0.0;
+    const int pick = decide_values<RE>(pv, E, raw_to_unif(raw[a.m]), lp, lperm, lpick, &rad);
+    if (lane == 0) {
+      a.spec[q] = pick >= 0 ? pick : -1;
+      a.spec_rad[q] = rad;
+    }
+  }
+}
+
 // Exact rows of the uncertain points: one wave per point (grid-stride over the dense
 // list), lane e computes entry e's log-likelihood, adding its per-attribute dhamming
 // values in attribute order -- the reference's summation order (n8:47-49), so every row
@@ -813,7 +893,7 @@ __device__ void copy_pool_params(const ResolveArgs& a, int64_t e, int s) {
 // so it takes these draws as they are; after the first move it decides on its own.
 template <int RE>
 __device__ void exact_rows_point(const PrepassArgs& a, int q, int row, double* lp, int* lperm, int* lpick) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   const int E = a.K + a.m;
   const int dp = a.nq * 16;
   const int64_t i = a.list[row];
@@ -869,61 +949,116 @@ __device__ void exact_rows_point(const PrepassArgs& a, int q, int row, double* l
   } else {
     for (int r = 0; r < (E + kWave - 1) / kWave; ++r) (void)entry_ll(r);
   }
-  if constexpr (RE > 0) {
-    if (!a.spec) return;
-    // n8:40-94 in the snapshot state: logn[count - (slot == own)] + ll for the clusters,
-    // log(gamma / m) + ll for the latents (the singleton's first latent is its own cluster)
-    const int own = __builtin_amdgcn_readfirstlane(a.c[i]);
-    const int own_cnt = a.counts[own];
-    double ll_own = 0.0;
-    double pv[RE];
-#pragma unroll
-    for (int r = 0; r < RE; ++r) {
-      const int e = r * kWave + lane;
-      int s = -1;
-      if (e < a.K) s = a.slot_of_label[e];
-      const unsigned long long bo = __ballot(s == own);
-      if (bo) ll_own = readlane_f64(acc_r[r], __ffsll((long long)bo) - 1);
-      double v = -INFINITY;
-      if (e < a.K) v = a.logn[a.counts[s] - (s == own ? 1 : 0)] + acc_r[r];
-      pv[r] = v;
+  if constexpr (RE > 0) exact_rows_decide<RE>(a, q, i, raw, acc_r, lp, lperm, lpick);
+}
+
+// Independent waves per workgroup (no block-level barrier): a sweep whose points are all
+// certain costs one small grid of early exits, not one workgroup per prepass block.
+constexpr int kExactWaves = 4;
+__global__ __launch_bounds__(kWave * kExactWaves) void k_exact_rows(PrepassArgs a) {
+  const int total = *a.dense_total;
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int q0 = blockIdx.x * kExactWaves + wv;
+  if (q0 >= total) return;
+  __shared__ double lp_w[kExactWaves][4 * kWave];
+  __shared__ int lperm_w[kExactWaves][4 * kWave];
+  __shared__ int lpick_w[kExactWaves];
+  double* lp = lp_w[wv];
+  int* lperm = lperm_w[wv];
+  int* lpick = &lpick_w[wv];
+  const int E = a.K + a.m;
+  for (int q = q0; q < total; q += gridDim.x * kExactWaves) {
+    const int row = a.dense[q];
+    if (lane == 0) {   // the resolver's per-point inputs, in list order
+      const int64_t i = a.list[row];
+      a.rq[q] = make_int4(row, (int)i, a.c[i], (int)a.raw[i * (a.m + 1) + a.m]);
     }
-#pragma unroll
-    for (int r = 0; r < RE; ++r) {
-      const int e = r * kWave + lane;
-      if (e >= a.K && e < E) {
-        const int l = e - a.K;
-        pv[r] = a.logfac + ((l == 0 && own_cnt == 1) ? ll_own : acc_r[r]);
-      }
-    }
-    double rad = 0.0;
-    const int pick = decide_values<RE>(pv, E, raw_to_unif(raw[a.m]), lp, lperm, lpick, &rad);
-    if (lane == 0) {
-      a.spec[q] = pick >= 0 ? pick : -1;
-      a.spec_rad[q] = rad;
+    if (E <= kWave) exact_rows_point<1>(a, q, row, lp, lperm, lpick);
+    else if (E <= 4 * kWave) exact_rows_point<4>(a, q, row, lp, lperm, lpick);
+    else {
+      exact_rows_point<0>(a, q, row, lp, lperm, lpick);
+      if (a.spec && lane == 0) a.spec[q] = -1;
     }
   }
 }
 
-__global__ __launch_bounds__(kWave) void k_exact_rows(PrepassArgs a) {
+// Workgroup per point, when the point's E x D table values fit in LDS: the 256 threads
+// gather them all at once (codes 4 attributes at a time, then the selected table value),
+// so a row costs one round of gather latency instead of D / 32; wave 0 then adds each
+// entry's values in attribute order (the reference's summation order, bit-exact) and
+// draws the snapshot decision.  Dynamic LDS: exact_wg_lds_bytes.
+constexpr int kExactWgThreads = 256;
+constexpr size_t kExactWgLdsMax = 64 * 1024;
+__host__ __device__ inline size_t exact_wg_lds_bytes(int E, int d, int dp) {
+  return (size_t)E * (d + 1) * 8 + (size_t)E * 16 + (size_t)E * 4 + (size_t)dp + 16;
+}
+
+template <int RE>
+__global__ __launch_bounds__(kExactWgThreads) void k_exact_rows_wg(PrepassArgs a) {
   const int total = *a.dense_total;
   if ((int)blockIdx.x >= total) return;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ double lp[4 * kWave];
   __shared__ int lperm[4 * kWave];
   __shared__ int lpick;
-  const int E = a.K + a.m;
+  const int E = a.K + a.m, D = a.d, dp = a.nq * 16, RS = D + 1;   // odd row stride: no bank aliasing
+  double* vals = (double*)smem;                                    // [E][RS]
+  const uint8_t** ecode = (const uint8_t**)(vals + (size_t)E * RS);
+  const double** etab = (const double**)(ecode + E);
+  int* ecol = (int*)(etab + E);
+  uint8_t* xc = (uint8_t*)(ecol + E);
+  const int t = threadIdx.x, lane = t & 63;
+  const int nj4 = (D + 3) >> 2;
   for (int q = blockIdx.x; q < total; q += gridDim.x) {
     const int row = a.dense[q];
-    if (threadIdx.x == 0) {   // the resolver's per-point inputs, in list order
-      const int64_t i = a.list[row];
-      a.rq[q] = make_int4(row, (int)i, a.c[i], (int)a.raw[i * (a.m + 1) + a.m]);
+    const int64_t i = a.list[row];
+    const uint32_t* raw = a.raw + i * (a.m + 1);
+    if (t == 0) a.rq[q] = make_int4(row, (int)i, a.c[i], (int)raw[a.m]);   // the resolver's inputs
+    for (int e = t; e < E; e += kExactWgThreads) {
+      if (e < a.K) {
+        const int s = a.slot_of_label[e];
+        ecode[e] = a.slots.codes + (int64_t)s * dp;
+        etab[e] = a.slots.tab + (int64_t)s * 2 * D;
+        ecol[e] = s;
+      } else {
+        const int64_t pe = pick_entry(raw[e - a.K], a.P);
+        ecode[e] = a.pool.codes + pe * dp;
+        etab[e] = a.pool.tab + pe * 2 * D;
+        ecol[e] = a.S + (e - a.K);
+      }
     }
-    if (E <= kWave) exact_rows_point<1>(a, q, row, lp, lperm, &lpick);
-    else if (E <= 4 * kWave) exact_rows_point<4>(a, q, row, lp, lperm, &lpick);
-    else {
-      exact_rows_point<0>(a, q, row, lp, lperm, &lpick);
-      if (a.spec && threadIdx.x == 0) a.spec[q] = -1;
+    for (int j = t; j < dp; j += kExactWgThreads) xc[j] = a.codes_t[tiled_offset(i, j, a.nq)];
+    __syncthreads();
+    for (int f = t; f < E * nj4; f += kExactWgThreads) {
+      const int e = f / nj4, j0 = (f - e * nj4) * 4;
+      const uint32_t dx = *(const uint32_t*)(ecode[e] + j0) ^ *(const uint32_t*)(xc + j0);
+      const double* tb = etab[e];
+      double v[4];
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        v[b] = (j0 + b < D) ? tb[2 * (j0 + b) + (((dx >> (8 * b)) & 0xffu) ? 1 : 0)] : 0.0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        if (j0 + b < D) vals[e * RS + j0 + b] = v[b];
     }
+    __syncthreads();
+    if (t < kWave) {
+      double acc_r[RE];
+      double* Lr = a.L + (int64_t)row * (a.S + a.m);
+#pragma unroll
+      for (int r = 0; r < RE; ++r) {
+        const int e = r * kWave + lane;
+        double acc = 0.0;
+        if (e < E) {
+          const double* vr = vals + e * RS;
+          for (int j = 0; j < D; ++j) acc += vr[j];
+          Lr[ecol[e]] = acc;
+        }
+        acc_r[r] = acc;
+      }
+      exact_rows_decide<RE>(a, q, i, raw, acc_r, lp, lperm, &lpick);
+    }
+    __syncthreads();   // the LDS staging is reused by the next point
   }
 }
 
@@ -1207,6 +1342,7 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
     ResolveCtl c;
     c.next = S.next; c.status = S.status; c.restart = S.restart; c.K = S.K; c.nslots = S.nslots;
     c.moves = S.moves; c.exact = S.exact; c.checked = S.checked;
+    c.listed = *a.dense_total;
     *a.ctl = c;
   }
 }
@@ -1463,23 +1599,37 @@ __global__ __launch_bounds__(kBlock) void k_lmatrix(const uint8_t* codes_t, int 
 }
 
 // ------------------------------------------------------------------ launchers
-template <int WB, int WS>
+template <int WB, int WS, bool HEAD>
 static hipError_t launch_prepass_t(const PrepassArgs& a, int nblocks, hipStream_t s) {
-  hipLaunchKernelGGL((k_prepass<WB, WS>), dim3(nblocks), dim3(kBlock), 0, s, a);
+  hipLaunchKernelGGL((k_prepass<WB, WS, HEAD>), dim3(nblocks), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 
 template <int WB>
 static hipError_t launch_prepass_w(const PrepassArgs& a, int nblocks, hipStream_t s) {
-  if (a.Ws == 2) return launch_prepass_t<WB, 2>(a, nblocks, s);
-  if (a.Ws == 4 && WB <= 4) return launch_prepass_t<WB, 4>(a, nblocks, s);
+  if (a.Ws == 2) {
+    if (a.pool_head) return launch_prepass_t<WB, 2, true>(a, nblocks, s);
+    return launch_prepass_t<WB, 2, false>(a, nblocks, s);
+  }
+  if constexpr (WB <= 4) {
+    if (a.Ws == 4) {
+      if (a.pool_head) return launch_prepass_t<WB, 4, true>(a, nblocks, s);
+      return launch_prepass_t<WB, 4, false>(a, nblocks, s);
+    }
+  }
   hipLaunchKernelGGL(k_prepass_generic, dim3(nblocks), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_exact_rows(const PrepassArgs& a, int nblocks, hipStream_t s) {
   hipLaunchKernelGGL(k_list_scan, dim3(1), dim3(kScanThreads), 0, s, a.cnt, nblocks, a.dense, a.dense_total);
-  hipLaunchKernelGGL(k_exact_rows, dim3(std::min(nblocks * 4, 4096)), dim3(kWave), 0, s, a);
+  const int E = a.K + a.m;
+  const size_t lds = exact_wg_lds_bytes(E, a.d, a.nq * 16);
+  const dim3 g(std::min(nblocks * 4, 1024)), b(kExactWgThreads);
+  const bool wg = !a.exact_wave && lds <= kExactWgLdsMax;
+  if (wg && E <= kWave) hipLaunchKernelGGL(k_exact_rows_wg<1>, g, b, lds, s, a);
+  else if (wg && E <= 4 * kWave) hipLaunchKernelGGL(k_exact_rows_wg<4>, g, b, lds, s, a);
+  else hipLaunchKernelGGL(k_exact_rows, dim3(std::min(nblocks, 1024)), dim3(kWave * kExactWaves), 0, s, a);
   return hipGetLastError();
 }
 

@@ -49,6 +49,29 @@ constexpr double kBoundEps = 1e-9;
 
 __host__ __device__ inline int bound_words(int wb, int Ws) { return (wb + kQ) * Ws + 4; }
 
+// Pool-entry heads: what the prepass gathers for a latent pick, wb*Ws + 2 words padded to
+// a power of two (64 B at C5 instead of the 128-B bound record; a random gather costs
+// one memory request per aligned head, measured: 64-B heads 76 us, 48-B packed heads 85 us,
+// 128-B records 85 us per C5 prepass) --
+//   [0, wb*Ws)   the center's bit-sliced codes (as in the bound record)
+//   then four floats: A_up = A + kBoundEps (1 + scale) rounded up, and rounded down dmin,
+//   S_a = S(h_a), S_b = S(h_b), where S(h) is the sum of the h smallest d_j.
+// A mismatch set of H attributes costs at least S(H) >= S(h) + (H - h) dmin for H >= h
+// (the H smallest d_j include the h smallest, and every further one is >= dmin), so
+//   ll <= A_up - max(dmin H, S_a + (H - h_a) dmin [H >= h_a], S_b + (H - h_b) dmin [H >= h_b]).
+// A latent center is uniform over the levels, so H has mean mu = sum_j (1 - 1/m_j) and
+// variance s2 = sum_j (1 - 1/m_j) / m_j whatever the point; h_a = mu - 4 s, h_b = mu - 1.25 s
+// (tools/latent_bound_study.py: at C5 the bound leaves 6e-5 of the picks uncertain; those
+// lanes gather the full record).  Used for the templated prepass layouts (Ws == 2, or
+// Ws == 4 with wb <= 4).
+constexpr __host__ __device__ inline int head_words(int wb, int Ws) { return wb * Ws + 2; }
+constexpr __host__ __device__ inline int head_stride(int wb, int Ws) {
+  int s = 4;
+  while (s < head_words(wb, Ws)) s *= 2;
+  return s;
+}
+__host__ __device__ inline bool head_fits(int wb, int Ws) { return Ws == 2 || (Ws == 4 && wb <= 4); }
+
 // Rows, tiled: word q of point i at ((i/64) * W + q) * 64 + i%64 (W words per row).
 __host__ __device__ inline int64_t packed_offset(int64_t i, int q, int W) {
   return ((i >> 6) * W + q) * 64 + (i & 63);
@@ -68,8 +91,10 @@ struct PrepassArgs {
   int Ws, wb;                // words per bit-plane, bits per attribute
   const uint64_t* slot_bnd;  // [slot][bw]
   const uint64_t* pool_bnd;  // [entry][bw]
+  const uint64_t* pool_head; // [entry][head_words] (head_fits), or nullptr: full records only
+  int head_ha, head_hb;      // the heads' h_a, h_b
   int bw;
-  uint64_t* csum;            // per label: its slot's record, logn[count], slot id (bw + 2 words)
+  uint64_t* csum;           // per label: its slot's record, logn[count], slot id (bw + 2 words)
   int64_t P;
   const uint32_t* raw;       // R MT raw outputs, (m+1) per point
   int m;
@@ -87,6 +112,7 @@ struct PrepassArgs {
   double* spec_rad;          // per dense-list position: log-weight drift under which it holds
   int4* rq;                  // per dense-list position: {row, point, slot, categorical draw}
   int p0;
+  int exact_wave;            // 1: exact rows one wave per point (no workgroup staging)
 };
 
 // Control block written by the resolver.
@@ -99,6 +125,7 @@ struct ResolveCtl {
   int moves;
   int exact;      // decisions computed in the resolver (not taken from the snapshot draws)
   int checked;    // 1 if the drift budget was exceeded (checked mode)
+  int listed;     // points the prepass left uncertain (exact rows built) in this launch
 };
 
 struct ResolveArgs {

@@ -200,6 +200,93 @@ __global__ __launch_bounds__(256) void k_pool_values(PoolValueArgs a) {
   }
 }
 
+__device__ __forceinline__ float f32_down(double x) {
+  float f = (float)x;
+  if ((double)f > x) f = nextafterf(f, -__builtin_inff());
+  return f;
+}
+__device__ __forceinline__ float f32_up(double x) {
+  float f = (float)x;
+  if ((double)f < x) f = nextafterf(f, __builtin_inff());
+  return f;
+}
+
+// Pool-entry heads (kernels.hpp) from the dhamming tables and bound records: one wave per
+// entry, NV = Ws attributes per lane (d <= 64 Ws).  The rank of d_j among the entry's d
+// (ties by index) selects the h_a / h_b smallest for S_a / S_b.  Host and device pools alike.
+template <int NV>
+__global__ __launch_bounds__(256) void k_pool_heads(const double* __restrict__ tab, const uint64_t* __restrict__ bnd,
+                                                   int64_t P, int d, int wb, int bw, int ha, int hb,
+                                                   uint64_t* __restrict__ head) {
+  const int lane = threadIdx.x & 63;
+  const int64_t e = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (e >= P) return;
+  const double* t = tab + e * 2 * d;
+  double dv[NV];
+  double mn = __builtin_inf();
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int j = 64 * k + lane;
+    dv[k] = j < d ? t[2 * j] - t[2 * j + 1] : __builtin_inf();   // d_j as in Ctx::bounds_for
+    mn = fmin(mn, dv[k]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mn = fmin(mn, __shfl_xor(mn, o));
+  int rank[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) rank[k] = 0;
+  for (int k2 = 0; k2 < NV; ++k2)
+    for (int l = 0; l < 64; ++l) {
+      const double y = __shfl(dv[k2], l);
+      const int jy = 64 * k2 + l;
+#pragma unroll
+      for (int k = 0; k < NV; ++k) rank[k] += (y < dv[k] || (y == dv[k] && jy < 64 * k + lane)) ? 1 : 0;
+    }
+  double sa = 0.0, sb = 0.0;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    if (64 * k + lane < d && rank[k] < ha) sa += dv[k];
+    if (64 * k + lane < d && rank[k] < hb) sb += dv[k];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    sa += __shfl_xor(sa, o);
+    sb += __shfl_xor(sb, o);
+  }
+  const int HW = wb * NV + 2, HS = head_stride(wb, NV);
+  if (lane < HS) {
+    const uint64_t* r = bnd + e * bw;
+    uint64_t v = 0;
+    if (lane >= HW) {
+      // padding to the power-of-two stride
+    } else if (lane < HW - 2) {
+      v = r[lane];
+    } else if (lane == HW - 2) {
+      const int SC = (wb + kQ) * NV;
+      const double A_up = __longlong_as_double((long long)r[SC]) +
+                          kBoundEps * (1.0 + __longlong_as_double((long long)r[SC + 3]));
+      v = (uint64_t)__float_as_uint(f32_up(A_up)) | ((uint64_t)__float_as_uint(f32_down(mn > 0 ? mn : 0.0)) << 32);
+    } else {
+      // one float ulp below the rounded-down sums: the double sums' own rounding (<= d ulps)
+      // stays on the safe side
+      const float fa = nextafterf(f32_down(sa), -__builtin_inff()), fb = nextafterf(f32_down(sb), -__builtin_inff());
+      v = (uint64_t)__float_as_uint(ha > 0 ? fmaxf(fa, 0.0f) : 0.0f) |
+          ((uint64_t)__float_as_uint(hb > 0 ? fmaxf(fb, 0.0f) : 0.0f) << 32);
+    }
+    head[e * HS + lane] = v;
+  }
+}
+
+hipError_t launch_pool_heads(const double* tab, const uint64_t* bnd, int64_t P, int d, int wb, int Ws, int bw, int ha,
+                             int hb, uint64_t* head, hipStream_t s) {
+  if (P <= 0) return hipSuccess;
+  const dim3 g((unsigned)((P + 3) / 4)), b(256);
+  if (Ws == 2) hipLaunchKernelGGL(k_pool_heads<2>, g, b, 0, s, tab, bnd, P, d, wb, bw, ha, hb, head);
+  else if (Ws == 4) hipLaunchKernelGGL(k_pool_heads<4>, g, b, 0, s, tab, bnd, P, d, wb, bw, ha, hb, head);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
 hipError_t launch_pool_accept(const PoolAcceptArgs& a, hipStream_t s) {
   const int64_t blocks = (a.nwords + 3) / 4;
   hipLaunchKernelGGL(k_pool_accept, dim3((unsigned)blocks), dim3(256), 0, s, a);

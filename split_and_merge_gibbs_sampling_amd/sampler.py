@@ -112,6 +112,20 @@ class Engine:
         self._check(self._L.hdpm_get_pool(self._h, ptr(cen), ptr(sig), int(P)))
         return cen, sig
 
+    def get_pool_heads(self, P: int) -> np.ndarray:
+        """The prepass's pool-entry heads, P x stride uint64 words, wb Ws + 2 of them used
+        (diagnostics; csrc/kernels.hpp "Pool-entry heads")."""
+        mmax = int(self._att.max())
+        wb = 1 if mmax <= 2 else 2 if mmax <= 4 else 4 if mmax <= 16 else 8
+        wd = -(-self.d // 64)
+        Ws = 2 if wd <= 2 else 4 if wd <= 4 else wd
+        stride = 4
+        while stride < wb * Ws + 2:
+            stride *= 2
+        out = np.zeros((P, stride), np.uint64)
+        self._check(self._L.hdpm_get_pool_heads(self._h, ptr(out), int(P)))
+        return out
+
     # ---------------------------------------------------------------- hot path
     def neal8_sweep(self, m: int):
         """N sample_allocation calls in index order (code/launcher.cpp:95-99)."""

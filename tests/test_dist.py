@@ -70,7 +70,9 @@ def test_bench_helpers():
     import bench
     wb, W, bw = bench.packed_layout(128, 4)
     assert (wb, W, bw) == (2, 4, 16)
-    assert bench.prepass_bytes_per_point(128, 4, 3) == 8 * W + 16 + 4 + 3 * 8 * bw + 12
+    assert bench.prepass_bytes_per_point(128, 4, 3) == 8 * W + 16 + 4 + 3 * 64 + 12     # 64-B heads
+    wb, W, bw = bench.packed_layout(784, 6)                                          # generic: full records
+    assert bench.prepass_bytes_per_point(784, 6, 3) == 8 * W + 16 + 4 + 3 * 8 * bw + 12
     assert bench.survey_sweep_bytes(10, 4, 1) == 10 * (4 * 11 + 8)
 
 

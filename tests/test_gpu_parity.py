@@ -96,7 +96,7 @@ def sweep_case(hd, oracle, ds, c, cen, sig, P, seed, m=3, debug=0, sweeps=1, phi
 
 # debug 0: default (snapshot speculation in the exact-rows kernel), 1: every point on the
 # exact path in the resolver, 8: no speculation (the resolver decides every listed point)
-@pytest.mark.parametrize("debug", [0, 1, 8])
+@pytest.mark.parametrize("debug", [0, 1, 8, 2048])
 def test_zoo_single_sweeps_from_truth(hd, oracle, zoo, debug):
     cen, sig = random_params(zoo, 7, 3)
     stats = sweep_case(hd, oracle, zoo, zoo.truth, cen, sig, zoo.n * 3, seed=17, debug=debug, sweeps=3)
@@ -119,8 +119,9 @@ def test_zoo_sweeps_with_update_phi_one_cluster(hd, oracle, zoo, debug):
     assert stats["restarts"] > 0
 
 
-# 16: recount the frequency tables every update_phi; 128: no speculative update_phi
-@pytest.mark.parametrize("debug", [0, 1, 8, 16, 128])
+# 16: recount the frequency tables every update_phi; 128: no speculative update_phi;
+# 2048: exact rows one wave per point
+@pytest.mark.parametrize("debug", [0, 1, 8, 16, 128, 2048, 2048 | 1])
 def test_synthetic_sweeps_with_update_phi(hd, oracle, debug):
     ds = synth(6000, 32, 8, 2, seed=3)
     cen, sig = random_params(ds, 8, 7)
@@ -440,3 +441,103 @@ def test_device_pool_then_sweeps_match_oracle(hd, oracle):
         assert_same_state(eng, ost)
     assert eng.stats()["pool_device_calls"] == 1
     eng.close()
+
+
+# ------------------------------------------------------------------ pool-entry heads
+def _head_bound_check(oracle, ds, heads, pc, ps, npts=600, nent=400, seed=0):
+    """Every head bound (csrc/kernels.hpp 'Pool-entry heads') is >= the entry's exact row
+    value for sampled points: A_up - max(dmin H, S_a + (H - h_a) dmin, S_b + (H - h_b) dmin),
+    and the head's codes, dmin and partial sums are those of the entry."""
+    rng = np.random.default_rng(seed)
+    pts = rng.choice(ds.n, size=min(npts, ds.n), replace=False)
+    ents = rng.choice(pc.shape[0], size=min(nent, pc.shape[0]), replace=False)
+    L, _ = oracle.loglik_matrix(ds.codes[pts], ds.attrisize, pc[ents], ps[ents])     # exact rows
+    d = ds.d
+    mmax = int(ds.attrisize.max())
+    wb = 1 if mmax <= 2 else 2 if mmax <= 4 else 4
+    Ws = 2 if d <= 128 else 4
+    hw = wb * Ws + 2
+    assert heads.shape[1] >= hw and np.all(heads[:, hw:] == 0)
+    heads = heads[:, :hw]
+    q = 1.0 / ds.attrisize
+    mu, sd = (1 - q).sum(), np.sqrt(((1 - q) * q).sum())
+    ha, hb = max(0, int(np.floor(mu - 4 * sd))), max(0, int(np.floor(mu - 1.25 * sd)))
+    h = heads[ents]
+    bits = lambda wds: np.array([[(int(w[j >> 6]) >> (j & 63)) & 1 for j in range(d)] for w in wds])  # noqa: E731
+    code = sum(bits(h[:, b * Ws:(b + 1) * Ws]) << b for b in range(wb)) + 1
+    assert np.array_equal(code, pc[ents].astype(np.int64))
+    f32 = lambda w: (w & 0xffffffff).astype(np.uint32).view(np.float32).astype(np.float64)  # noqa: E731
+    A_up, dmin = f32(h[:, -2]), f32(h[:, -2] >> 32)
+    Sa, Sb = f32(h[:, -1]), f32(h[:, -1] >> 32)
+    e = np.exp(1.0 / ps[ents])
+    den = np.log(1.0 + (ds.attrisize - 1.0) / e)
+    dd = (-den) - (-1.0 / ps[ents] - den)
+    srt = np.sort(dd, 1)
+    assert np.all(dmin <= srt[:, 0]) and np.all(dmin >= srt[:, 0] * (1 - 1e-6))
+    for S, hh in ((Sa, ha), (Sb, hb)):
+        ref = srt[:, :hh].sum(1)
+        assert np.all(S <= ref) and np.all(S >= ref * (1 - 1e-6) - 1e-30)
+    M = ds.codes[pts][:, None, :] != pc[ents][None, :, :]      # npts x nent x d
+    H = M.sum(-1)
+    low = dmin[None] * H
+    low = np.maximum(low, np.where(H >= ha, Sa[None] + (H - ha) * dmin[None], 0))
+    low = np.maximum(low, np.where(H >= hb, Sb[None] + (H - hb) * dmin[None], 0))
+    ub = A_up[None] - low
+    assert np.all(ub >= L), float((L - ub).max())
+    return float(np.median(ub - L))
+
+
+@pytest.mark.parametrize("src", ["device", "host"])
+def test_pool_heads_bound_exact_rows(hd, oracle, src):
+    ds = synth(3000, 128, 6, 4, seed=21)
+    eng = make_engine(hd, ds)
+    st = oracle.seed_state(13)
+    eng.rng_state = st
+    P = 9000
+    if src == "device":
+        eng.generate_pool(P)
+        pc, ps = eng.get_pool(P)
+    else:
+        pc, ps, _ = oracle.pool_generate(ds.attrisize, ds.v, ds.w, P, st)
+        eng.set_pool(pc, ps)
+    heads = eng.get_pool_heads(P)
+    _head_bound_check(oracle, ds, heads, pc, ps)
+    eng.close()
+
+
+def test_pool_heads_binary_and_absent(hd, oracle):
+    ds = synth(2000, 32, 6, 2, seed=22)                # wb = 1: codes and scalars in 4 words
+    eng = make_engine(hd, ds)
+    st = oracle.seed_state(14)
+    pc, ps, _ = oracle.pool_generate(ds.attrisize, ds.v, ds.w, 6000, st)
+    eng.set_pool(pc, ps)
+    _head_bound_check(oracle, ds, eng.get_pool_heads(6000), pc, ps)
+    eng.close()
+    wide = synth(500, 200, 4, (2, 6), seed=23)         # d = 200, m_j <= 6: Ws = 4, wb = 4 (18 words)
+    eng = make_engine(hd, wide)
+    pc, ps, _ = oracle.pool_generate(wide.attrisize, wide.v, wide.w, 1500, st)
+    eng.set_pool(pc, ps)
+    _head_bound_check(oracle, wide, eng.get_pool_heads(1500), pc, ps, npts=300, nent=300)
+    eng.close()
+    wider = synth(300, 300, 4, 4, seed=26)             # d > 256: generic prepass, no heads
+    eng = make_engine(hd, wider)
+    pc, ps, _ = oracle.pool_generate(wider.attrisize, wider.v, wider.w, 900, st)
+    eng.set_pool(pc, ps)
+    with pytest.raises(hd.HdpmError):
+        eng.get_pool_heads(900)
+    eng.close()
+
+
+# 1024: full bound records for the latent picks (no heads) on a head-eligible layout
+@pytest.mark.parametrize("debug", [0, 1024])
+def test_c5_like_sweeps_heads_and_records(hd, oracle, debug):
+    ds = synth(5000, 128, 8, 4, seed=24)
+    cen, sig = random_params(ds, 8, 25)
+    sweep_case(hd, oracle, ds, ds.truth, cen, sig, ds.n * 3, seed=43, sweeps=3, phi=True, debug=debug)
+
+
+@pytest.mark.parametrize("debug", [0, 1024])
+def test_wide_mixed_levels_sweeps_heads_and_records(hd, oracle, debug):
+    ds = synth(3000, 200, 6, (2, 6), seed=27)          # Ws = 4, wb = 4 heads
+    cen, sig = random_params(ds, 6, 28)
+    sweep_case(hd, oracle, ds, ds.truth, cen, sig, ds.n * 3, seed=47, sweeps=3, phi=True, debug=debug)
