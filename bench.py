@@ -37,6 +37,27 @@ def packed_layout(d: int, mmax: int):
     return wb, wb * Ws, (wb + 4) * Ws + 4
 
 
+# FETCH_SIZE calibration on gfx950 (tools/fetch_calib.hip, profiles/r01/fetch_calib.log):
+# reported / true bytes and measured rates of the prepass's access shapes
+FETCH_FACTOR = {"stream16": 0.5, "gather64": 1.0, "gather128": 0.584}
+RATE_GBPS = {"stream16": 5650.0, "gather64": 3080.0, "gather128": 3830.0}
+
+
+def prepass_shape(d: int, mmax: int, m: int):
+    """(streamed bytes, gathered bytes, gather shape) per point of k_prepass: streamed are
+    the row, raw draws and label reads (margin / row index writes are WRITE_SIZE), gathered
+    the m latent picks (64-B heads, else full 8 bw-byte records)."""
+    wb, W, bw = packed_layout(d, mmax)
+    Ws = W // wb
+    head = Ws == 2 or (Ws == 4 and wb <= 4)
+    hs = 4
+    while hs < W + 2:
+        hs *= 2
+    g = m * 8 * (hs if head else bw)
+    shape = "gather64" if head and hs == 8 else "gather128"
+    return 8 * W + 4 * (m + 1) + 4, g, shape
+
+
 def prepass_bytes_per_point(d: int, mmax: int, m: int) -> int:
     """Compulsory bytes k_prepass moves per point: its bit-sliced row
     (8 W), its m+1 raw draws (4(m+1)), its label (4), the first gather of each of its m
@@ -220,9 +241,20 @@ def main():
     if csvs is None:
         csvs = [os.path.join(ROOT, "profiles", "r01", f"pmc_{c}_{args.config}.csv") for c in ("fetch", "write")]
     csvs = [c for c in csvs if os.path.exists(c)]
+    s_b, g_b, gshape = prepass_shape(ds.d, int(ds.attrisize.max()), args.m)
     if csvs and args.n is None:
-        traffic = traffic_from_csv(*csvs)
-        traffic_src = [os.path.relpath(c, ROOT) for c in csvs]
+        raw = traffic_from_csv(*csvs)
+        if raw is not None:
+            # calibrated: the streamed reads report half their bytes, the gathers FETCH_FACTOR
+            fetch, write = raw
+            stream = s_b * ds.n
+            traffic = round(stream + (fetch - FETCH_FACTOR["stream16"] * stream) / FETCH_FACTOR[gshape] + write)
+        traffic_src = [os.path.relpath(c, ROOT) for c in csvs] + ["profiles/r01/fetch_calib.log"]
+    # the measured ceiling of this access mix: its streamed and gathered bytes at the rates
+    # tools/fetch_calib.hip measured for those shapes on MI355X
+    wb_ = bpp - s_b - g_b
+    ceil_ns = s_b / RATE_GBPS["stream16"] + g_b / RATE_GBPS[gshape] + wb_ / RATE_GBPS["stream16"]
+    ceiling = bpp / ceil_ns
     out = {
         "metric": "full Gibbs sweeps/sec (N-point reassign) at N=1M D=128; achieved HBM GB/s",
         "value": round(value, 4),
@@ -267,6 +299,10 @@ def main():
             "frac": None if achieved is None else round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": traffic,
             "traffic_source": traffic_src,
+            "measured_ceiling": {"GBps": round(ceiling, 1),
+                                 "frac": None if achieved is None else round(achieved / ceiling, 4),
+                                 "what": f"{s_b} B/point streamed + {g_b} B/point in {gshape[6:]}-B random gathers "
+                                         f"at the rates tools/fetch_calib.hip measured (profiles/r01/fetch_calib.log)"},
             "bytes_per_point": bpp,
             "avg_launch_ms": round(pre_ms / launches, 4),
         },
@@ -301,10 +337,9 @@ def pool_report(st, P):
 
 
 def traffic_from_csv(*paths):
-    """Per-launch HBM bytes of k_prepass from rocprofv3 --pmc counter_collection CSVs (one
-    pass per counter): 2 * FETCH_SIZE + WRITE_SIZE, KiB -> bytes.  gfx950's FETCH_SIZE
-    reports half the bytes of a wide streaming read (MI355X_MICROARCH.md 'HBM'); the
-    prepass reads 16-B lanes, the same width."""
+    """Per-launch (FETCH_SIZE, WRITE_SIZE) bytes of k_prepass from rocprofv3 --pmc
+    counter_collection CSVs (one pass per counter), as reported (KiB -> bytes); the caller
+    applies the calibration (FETCH_FACTOR)."""
     import csv
     tot = {"FETCH_SIZE": [0.0, set()], "WRITE_SIZE": [0.0, set()]}
     for path in paths:
@@ -318,7 +353,7 @@ def traffic_from_csv(*paths):
     per = {k: (v / len(ids) if ids else None) for k, (v, ids) in tot.items()}
     if per["FETCH_SIZE"] is None:
         return None
-    return round((2 * per["FETCH_SIZE"] + (per["WRITE_SIZE"] or 0.0)) * 1024)
+    return per["FETCH_SIZE"] * 1024, (per["WRITE_SIZE"] or 0.0) * 1024
 
 
 if __name__ == "__main__":

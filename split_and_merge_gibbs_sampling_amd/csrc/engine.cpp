@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cctype>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -141,6 +142,26 @@ static void parallel_for(int64_t n, F f) {
   for (auto& x : th) x.join();
 }
 
+// CPU list files of sysfs ("0-7,16-23").
+static std::vector<int> read_cpu_list(const std::string& path) {
+  std::vector<int> out;
+  FILE* f = std::fopen(path.c_str(), "r");
+  if (!f) return out;
+  char buf[4096];
+  if (!std::fgets(buf, sizeof(buf), f)) buf[0] = 0;
+  std::fclose(f);
+  for (char* p = buf; *p;) {
+    char* end;
+    long a = std::strtol(p, &end, 10);
+    if (end == p) { ++p; continue; }
+    long b = a;
+    if (*end == '-') b = std::strtol(end + 1, &end, 10);
+    for (long c = a; c <= b; ++c) out.push_back((int)c);
+    p = end;
+  }
+  return out;
+}
+
 // Persistent host worker pool for the per-iteration host phases (the deterministic parts
 // of the parameter draws, table builds).  Workers spin for a short while after a job and
 // then sleep; prewake() gets sleeping workers spinning ahead of a job (e.g. while the
@@ -229,38 +250,23 @@ class HostPool {
     for (int t = 1; t < T; ++t) th_.emplace_back([this] { loop(); });
     pin_workers();
   }
-  // Workers on distinct physical cores of the creating thread's L3 domain (the host
-  // phases hand data between cores every iteration); HDPM_PIN_THREADS=0 leaves placement
-  // to the OS.
+  // Workers on distinct physical cores of one L3 domain (the host phases hand data between
+  // cores every iteration): the home domain set before the pool's creation (the GPU's,
+  // hdpm_ctx_create), else the creating thread's; HDPM_PIN_THREADS=0 leaves placement to
+  // the OS.
   void pin_workers() {
     if (const char* e = std::getenv("HDPM_PIN_THREADS"))
       if (std::atoi(e) == 0) return;
-    const int me = sched_getcpu();
-    if (me < 0) return;
-    main_cpu_ = me;
     cpu_set_t allowed;
     if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return;
-    auto read_list = [](const std::string& path) {
-      std::vector<int> out;
-      FILE* f = std::fopen(path.c_str(), "r");
-      if (!f) return out;
-      char buf[4096];
-      if (!std::fgets(buf, sizeof(buf), f)) buf[0] = 0;
-      std::fclose(f);
-      for (char* p = buf; *p;) {
-        char* end;
-        long a = std::strtol(p, &end, 10);
-        if (end == p) { ++p; continue; }
-        long b = a;
-        if (*end == '-') b = std::strtol(end + 1, &end, 10);
-        for (long c = a; c <= b; ++c) out.push_back((int)c);
-        p = end;
-      }
-      return out;
-    };
     const std::string base = "/sys/devices/system/cpu/cpu";
-    std::vector<int> dom = read_list(base + std::to_string(me) + "/cache/index3/shared_cpu_list");
+    std::vector<int> dom = home();
+    int me = dom.empty() ? sched_getcpu() : dom.front();
+    if (me < 0) return;
+    main_cpu_ = me;
+    if (dom.empty()) dom = read_cpu_list(base + std::to_string(me) + "/cache/index3/shared_cpu_list");
     if (dom.empty()) return;
+    auto read_list = [](const std::string& path) { return read_cpu_list(path); };
     std::vector<char> used_core(4096, 0);
     auto core_of = [&](int c) {
       const std::vector<int> sib = read_list(base + std::to_string(c) + "/topology/thread_siblings_list");
@@ -356,7 +362,59 @@ class HostPool {
 
  public:
   int main_cpu() const { return main_cpu_; }
+  // CPUs of the L3 domain the pool is to live on (set before the first get())
+  static std::vector<int>& home() {
+    static std::vector<int> h;
+    return h;
+  }
 };
+
+// The host pool's home for a process driving `device`: an L3 domain among the CPUs local to
+// the GPU (its PCI device's local_cpulist, within this process's affinity), a different
+// one for each GPU that shares those CPUs, so one process per GPU (bench.py --gpus N)
+// spreads its pinned workers instead of stacking them on whichever domain each process
+// started on.  Empty (creating thread's domain) when the topology is not readable.
+static std::vector<int> gpu_home_domain(int device) {
+  std::vector<int> none;
+  if (const char* e = std::getenv("HDPM_PIN_THREADS"))
+    if (std::atoi(e) == 0) return none;
+  int cnt = 0;
+  if (hipGetDeviceCount(&cnt) != hipSuccess || device < 0 || device >= cnt) return none;
+  auto local_list = [](int dev) {
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus), dev) != hipSuccess) return std::vector<int>{};
+    for (char* p = bus; *p; ++p) *p = (char)std::tolower((unsigned char)*p);
+    return read_cpu_list(std::string("/sys/bus/pci/devices/") + bus + "/local_cpulist");
+  };
+  const std::vector<int> mine = local_list(device);
+  if (mine.empty()) return none;
+  int slot = 0, share = 0;
+  for (int d2 = 0; d2 < cnt; ++d2)
+    if (local_list(d2) == mine) {
+      if (d2 < device) ++slot;
+      ++share;
+    }
+  cpu_set_t allowed;
+  if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return none;
+  std::vector<std::vector<int>> doms;
+  std::vector<int> keys;
+  for (int c : mine) {
+    if (c < 0 || c >= CPU_SETSIZE || !CPU_ISSET(c, &allowed)) continue;
+    const std::vector<int> l3 =
+        read_cpu_list("/sys/devices/system/cpu/cpu" + std::to_string(c) + "/cache/index3/shared_cpu_list");
+    const int key = l3.empty() ? c : l3.front();
+    size_t q = 0;
+    while (q < keys.size() && keys[q] != key) ++q;
+    if (q == keys.size()) {
+      keys.push_back(key);
+      doms.emplace_back();
+    }
+    doms[q].push_back(c);
+  }
+  if (doms.empty() || share <= 0) return none;
+  // spread over the domains, keeping off the first (CPU 0's: interrupts and daemons)
+  return doms[std::min(doms.size() - 1, (size_t)(slot + 1) * doms.size() / (size_t)(share + 1))];
+}
 
 // The calling thread on the core kept free of pool workers for the duration of an engine
 // call (the serial draws share data with the workers through the L3); the caller's
@@ -1574,16 +1632,22 @@ struct Ctx {
     if (ahead.active || !have_state || P <= 0 || m <= 0 || tables_dirty || (debug & (256 | 128 | 16))) return;
     if (!(freq_dev_valid && freq_version == labels_version)) return;
     rng_sync();
+    mark("ahead.sync");
     ahead.saved = rng;
     ahead.raw = device_draws((int64_t)n * (m + 1));
+    mark("ahead.draws");
     ahead.m = m;
     ahead.lv = labels_version;
     ahead.launched = false;
     ahead.active = true;
+    // the speculative update_phi first: its serial draws, not the device sweep, are the
+    // longer path (timeline: launching the sweep first cost ~8% of the iteration rate)
     spec_launch();
+    mark("ahead.spec");
     if (launch && resolve_smem_bytes(std::min(scap, K + 2), m) <= 160 * 1024) {
       ahead.track = freq_dev_valid;
       sweep_buffers(ahead.track);
+      mark("ahead.buf");
       if (launch_round(0, K, m, ahead.raw, ahead.track) == kOk) ahead.launched = true;
     }
   }
@@ -2683,6 +2747,11 @@ int hdpm_ctx_create(int32_t device, hdpm_ctx** out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) return HDPM_E_NODEVICE;
   if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return HDPM_E_NODEVICE;
+  {
+    // the host pool's home next to this GPU, before the pool exists (one process per GPU)
+    static std::once_flag once;
+    std::call_once(once, [device] { hdpm::HostPool::home() = hdpm::gpu_home_domain(device); });
+  }
   auto* c = new (std::nothrow) Ctx();
   if (!c) return HDPM_E_ARG;
   c->device = device;

@@ -88,8 +88,8 @@ def test_traffic_from_csv(tmp_path, rows):
         w.writerow(["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"])
         for k, d, n, v in rows:
             w.writerow([d, k, n, v])
-    # (2 * 400 + 40) KiB over 2 dispatches
-    assert bench.traffic_from_csv(str(p)) == round((2 * 400 + 40) * 1024 / 2)
+    # 400 KiB fetched and 40 KiB written over 2 dispatches (as reported)
+    assert bench.traffic_from_csv(str(p)) == (200 * 1024, 20 * 1024)
     # one file per counter pass
     pf, pw = tmp_path / "f.csv", tmp_path / "w.csv"
     import csv
@@ -99,4 +99,7 @@ def test_traffic_from_csv(tmp_path, rows):
             w.writerow(["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"])
             for d, v in enumerate(vals):
                 w.writerow([d, "k_prepass<2,2>", name, v])
-    assert bench.traffic_from_csv(str(pf), str(pw)) == round((2 * 200 + 20) * 1024)
+    assert bench.traffic_from_csv(str(pf), str(pw)) == (200 * 1024, 20 * 1024)
+    # the C5 prepass shape: 52 B/point streamed, 3 x 64-B head gathers
+    assert bench.prepass_shape(128, 4, 3) == (52, 192, "gather64")
+    assert bench.prepass_shape(784, 6, 3)[2] == "gather128"

@@ -1,0 +1,80 @@
+// fetch_calib.hip -- calibrates rocprofv3's FETCH_SIZE on gfx950 for the prepass's access
+// shapes (design tool, not part of the library): aligned random gathers of 64-B and
+// 128-B records and 16-B-per-lane streaming reads, each over a 1 GiB buffer (beyond the
+// Infinity Cache), with a known byte count per dispatch.
+//   hipcc --offload-arch=gfx950 -O3 -o fetch_calib tools/fetch_calib.hip
+//   rocprofv3 --pmc FETCH_SIZE --kernel-trace -d out -o run --output-format csv -- ./fetch_calib
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+
+__device__ __forceinline__ uint64_t mix(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  return x ^ (x >> 33);
+}
+
+// each thread gathers R records of W uint4 at random record indices
+template <int W>
+__global__ void k_gather(const uint4* __restrict__ buf, int64_t nrec, int R, uint64_t seed, uint4* out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  for (int r = 0; r < R; ++r) {
+    const int64_t e = (int64_t)(mix(seed + t * 131 + r) % (uint64_t)nrec);
+    const uint4* p = buf + e * W;
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+      const uint4 v = p[k];
+      acc.x ^= v.x; acc.y ^= v.y; acc.z ^= v.z; acc.w ^= v.w;
+    }
+  }
+  if ((acc.x & 0xfffff) == 0x12345) out[t & 1023] = acc;
+}
+
+__global__ void k_stream(const uint4* __restrict__ buf, int64_t n16, uint4* out) {
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint4 v = buf[i];
+    acc.x ^= v.x; acc.y ^= v.y; acc.z ^= v.z; acc.w ^= v.w;
+  }
+  if ((acc.x & 0xfffff) == 0x12345) out[threadIdx.x] = acc;
+}
+
+int main() {
+  const size_t bytes = (size_t)1 << 30;
+  uint4 *buf, *out;
+  if (hipMalloc(&buf, bytes) != hipSuccess || hipMalloc(&out, 1024 * sizeof(uint4)) != hipSuccess) return 1;
+  (void)hipMemset(buf, 1, bytes);
+  const int threads = 256, blocks = 4096, R = 3;
+  const double nthr = (double)threads * blocks;
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  for (int rep = 0; rep < 3; ++rep) {
+    float ms;
+    (void)hipEventRecord(a);
+    hipLaunchKernelGGL(k_gather<4>, dim3(blocks), dim3(threads), 0, 0, buf, (int64_t)(bytes / 64), R, 77 + rep, out);
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    (void)hipEventElapsedTime(&ms, a, b);
+    std::printf("gather64  %.0f records, %.1f MB, %.1f us\n", nthr * R, nthr * R * 64 / 1e6, ms * 1e3);
+    (void)hipEventRecord(a);
+    hipLaunchKernelGGL(k_gather<8>, dim3(blocks), dim3(threads), 0, 0, buf, (int64_t)(bytes / 128), R, 91 + rep, out);
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    (void)hipEventElapsedTime(&ms, a, b);
+    std::printf("gather128 %.0f records, %.1f MB, %.1f us\n", nthr * R, nthr * R * 128 / 1e6, ms * 1e3);
+    (void)hipEventRecord(a);
+    hipLaunchKernelGGL(k_stream, dim3(2048), dim3(256), 0, 0, buf, (int64_t)(bytes / 16 / 4), out);
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    (void)hipEventElapsedTime(&ms, a, b);
+    std::printf("stream16  %.1f MB, %.1f us\n", bytes / 4 / 1e6, ms * 1e3);
+  }
+  (void)hipFree(buf);
+  (void)hipFree(out);
+  return 0;
+}
