@@ -1956,6 +1956,7 @@ struct Ctx {
     if (fill_phi_stream(phi_prefetch)) {
       sa.used = 0;
       HostPool::get().run(sa.n, 1024, [&](int64_t a0, int64_t a1) { sa.logits(a0, a1); });
+      sa.avail = INT64_MAX;
     }
   }
 
@@ -2000,6 +2001,8 @@ struct Ctx {
     std::atomic<int> fill{0};          // 0 open, 1 taken, 2 done
     std::atomic<int> nextL{0}, doneL{0};
     std::atomic<int> nL{0};
+    std::unique_ptr<std::atomic<uint8_t>[]> ldone;   // per logit chunk: computed
+    int ldone_cap = 0;
     std::atomic<int> nextA{0};
     std::unique_ptr<std::atomic<int>[]> stA, stB;
     std::atomic<int> bclaim{0};
@@ -2131,6 +2134,7 @@ struct Ctx {
       double xs[kSpec];
       bool ok[kSpec];
       q = sa.used;
+      if (nspec > 0) sa.need(q + 2 * kSpec);
       for (int b = 0; b < nspec; ++b) {
         const double mj = (double)att[j + b];
         if (bps[b]) {
@@ -2217,6 +2221,7 @@ struct Ctx {
     pj.stB.reset(new std::atomic<int>[std::max(pj.T, 1)]);
     for (int t = 0; t < pj.T; ++t) { pj.stA[t].store(0); pj.stB[t].store(0); }
     pj.fill.store(spec ? 0 : 2);
+    if (!spec) phi_stream.avail = INT64_MAX;     // filled and logits computed beforehand
     pj.nL.store(0);
     pj.nextL.store(0);
     pj.doneL.store(0);
@@ -2246,7 +2251,16 @@ struct Ctx {
     }
     sa.used = 0;
     sa.live = &spec_live;
-    pj.nL.store((int)((sa.n + PhiJob::kLogitChunk - 1) / PhiJob::kLogitChunk), std::memory_order_relaxed);
+    const int nl = (int)((sa.n + PhiJob::kLogitChunk - 1) / PhiJob::kLogitChunk);
+    if (nl > pj.ldone_cap) {
+      pj.ldone.reset(new std::atomic<uint8_t>[nl]);
+      pj.ldone_cap = nl;
+    }
+    for (int c = 0; c < nl; ++c) pj.ldone[c].store(0, std::memory_order_relaxed);
+    // B may start on the first chunks: later positions wait for (or compute) their chunk
+    sa.avail = 0;
+    sa.wait_avail = [this](int64_t pos) { return pj_wait_chunk(pos); };
+    pj.nL.store(nl, std::memory_order_relaxed);
     pj.ns_fill.store(pj_ns());
     pj.fill.store(2, std::memory_order_release);
     return true;
@@ -2257,8 +2271,21 @@ struct Ctx {
     if (c >= pj.nL.load(std::memory_order_relaxed)) return false;
     StreamAhead& sa = phi_stream;
     sa.logits((int64_t)c * PhiJob::kLogitChunk, std::min<int64_t>(sa.n, (int64_t)(c + 1) * PhiJob::kLogitChunk));
+    pj.ldone[c].store(1, std::memory_order_release);
     if (pj.doneL.fetch_add(1, std::memory_order_release) + 1 == pj.nL.load()) pj.ns_logits.store(pj_ns());
     return true;
+  }
+  // B's reads at `pos`: wait for its logit chunk (computing chunks meanwhile); returns the
+  // end of the leading run of computed chunks
+  int64_t pj_wait_chunk(int64_t pos) {
+    const StreamAhead& sa = phi_stream;
+    const int nl = pj.nL.load(std::memory_order_relaxed);
+    int c = (int)(pos / PhiJob::kLogitChunk);
+    if (c >= nl) return INT64_MAX;
+    while (!pj.ldone[c].load(std::memory_order_acquire))
+      if (!pj_logit()) HostPool::spin_pause();
+    while (c + 1 < nl && pj.ldone[c + 1].load(std::memory_order_acquire)) ++c;
+    return c + 1 >= nl ? INT64_MAX : std::min<int64_t>(sa.n, (int64_t)(c + 1) * PhiJob::kLogitChunk);
   }
   bool pj_take_a() {
     const int task = pj.nextA.fetch_add(1);
@@ -2269,8 +2296,10 @@ struct Ctx {
     return true;
   }
   bool pj_stream_ready() const {
-    return pj.fill.load(std::memory_order_acquire) == 2 &&
-           pj.doneL.load(std::memory_order_acquire) >= pj.nL.load(std::memory_order_relaxed);
+    if (pj.fill.load(std::memory_order_acquire) != 2) return false;
+    const int nl = pj.nL.load(std::memory_order_relaxed);
+    if (debug & 4096) return pj.doneL.load(std::memory_order_acquire) >= nl;   // all logits first
+    return nl == 0 || pj.ldone[0].load(std::memory_order_acquire);
   }
   // B for every cluster, in order, on the thread that claims it once the stream is ready
   bool pj_try_b() {

@@ -16,6 +16,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <functional>
 #include <unordered_map>
 #include <vector>
 
@@ -439,8 +440,17 @@ struct StreamAhead {
     }
     r.epoch = ep;
   }
+  // Entries produced by other threads in chunks: positions at or past `avail` are read only
+  // after wait_avail(pos) (which returns the new limit); unset, the whole prefix is ready.
+  int64_t avail = INT64_MAX;
+  std::function<int64_t(int64_t)> wait_avail;
+  void need(int64_t pos) {
+    if (pos >= avail && pos < n) avail = wait_avail(pos);
+  }
+
   double next(double* lgout) {
     if (used < n) {
+      need(used);
       if (lgout) *lgout = lg[used];
       return u[used++];
     }
@@ -455,6 +465,7 @@ struct StreamAhead {
   }
   void pair(double* u1, double* lg1, double* u2, double* lzo) {
     if (used + 1 < n) {
+      need(used + 1);
       *u1 = u[used];
       *lg1 = lg[used];
       *u2 = u[used + 1];
