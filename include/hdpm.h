@@ -159,6 +159,15 @@ int hdpm_set_debug(hdpm_ctx* ctx, int32_t mode);
  * (csrc/kernels.hpp "Pool-entry heads"); HDPM_E_ARG when the data's layout has none (d > 256, or d > 128 with
  * m_j > 16). */
 int hdpm_get_pool_heads(hdpm_ctx* ctx, uint64_t* out, int64_t P);
+/* Options.  HDPM_OPT_HIG_LOGSPACE (value != 0): an extension beyond the reference -- the
+ * HIG normalising constant's 2F1 series (norm_const2, hg:11-48, and lF_conK2, hg:183-217)
+ * is summed with a rescaled partial sum, so clusters of thousands of members get a finite
+ * log-density where GSL's double series overflows and the reference throws
+ * (HDPM_E_GSL); 10^7 series terms instead of 30000.  Wherever the reference's series stays
+ * finite within 30000 terms the values are bit-identical.  Default 0 (reference
+ * semantics). */
+#define HDPM_OPT_HIG_LOGSPACE 1
+int hdpm_set_option(hdpm_ctx* ctx, int32_t option, double value);
 /* Block until all device work of the context is done. */
 int hdpm_synchronize(hdpm_ctx* ctx);
 

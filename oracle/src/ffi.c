@@ -49,6 +49,8 @@ double orc_ffi_norm_const2(double d, double c, double m, int* err) {
     return orc_norm_const2(d, c, m, err);
 }
 
+void orc_ffi_set_hig_logspace(int on) { orc_set_hig_logspace(on); }
+
 int orc_ffi_qbeta01_lt(double a, double b, double x) { return orc_qbeta01_lt(a, b, x); }
 double orc_ffi_pbeta(double x, double a, double b) { return orc_pbeta(x, a, b); }
 double orc_ffi_dhamming(int x, int c, double s, int m) { return orc_dhamming(x, c, s, m); }

@@ -9,9 +9,28 @@
 #define GSL_SUCCESS  0
 #define GSL_EMAXITER 11
 
+/* HDPM_OPT_HIG_LOGSPACE mirror (extension, not the reference): norm_const2 and lF_conK2
+ * take log 2F1 from orc_log_hyperg_2F1. */
+static int g_hig_logspace = 0;
+void orc_set_hig_logspace(int on) { g_hig_logspace = on != 0; }
+
 /* hg:11-48 norm_const2(d, c, m).  *err = ORC_E_GSL where the reference throws. */
 double orc_norm_const2(double d, double c, double m, int* err) {
     double z = (m - 1) / m;
+    if (g_hig_logspace) {
+        double lv;
+        int st = orc_log_hyperg_2F1(d + c, 1, d + 2, z, &lv);
+        if (st != GSL_SUCCESS) {
+            if (st == GSL_EMAXITER) return -INFINITY;
+            if (err) *err = ORC_E_GSL;
+            return NAN;
+        }
+        if (!isfinite(lv)) {
+            if (err) *err = ORC_E_GSL;
+            return NAN;
+        }
+        return log(d + 1) + (d + c) * log(m) - lv;
+    }
     double alpha = d + c;
     double beta = 1;
     double gamma = d + 2;
@@ -44,8 +63,13 @@ double orc_lF_conK2(double u, double d, double c, double m, double lK) {
     if (u == 0) return -INFINITY;
     if (u == 1) return 0;
     double x = u * (m - 1) / (1 + u * (m - 1));
-    double app = orc_hyperg2(1, d + c, d + 2, x);
-    double out = lK - log(d + 1) + (d + 1) * log(u) - (d + c) * log(1 + u * (m - 1)) + log(app);
+    double lapp;
+    if (g_hig_logspace) {
+        if (orc_log_hyperg_2F1(1, d + c, d + 2, x, &lapp) != GSL_SUCCESS) lapp = NAN;
+    } else {
+        lapp = log(orc_hyperg2(1, d + c, d + 2, x));
+    }
+    double out = lK - log(d + 1) + (d + 1) * log(u) - (d + c) * log(1 + u * (m - 1)) + lapp;
     return out;
 }
 

@@ -66,6 +66,9 @@ double orc_hyperg2(double a, double b, double c, double x);                /* hg
 double orc_lF_conK2(double u, double d, double c, double m, double lK);    /* hg:183-217 */
 double orc_bisec_hyper2(double d, double c, double m, double Omega, int* err); /* hg:221-287 */
 double orc_rhig1(orc_rng* r, double v, double w, double m, int* err);      /* hg:346-378, n=1 */
+/* extension mirrored from hdpm (HDPM_OPT_HIG_LOGSPACE), not the reference: */
+int    orc_log_hyperg_2F1(double a, double b, double c, double x, double* lval);
+void   orc_set_hig_logspace(int on);
 
 /* ---- model ---- */
 double orc_dhamming(int x, int c, double s, int attrisize);               /* cf:355-377 */

@@ -23,8 +23,10 @@ EXPORTS = (
     "hdpm_compute_loglikelihood", "hdpm_loglik_matrix", "hdpm_restricted_gibbs", "hdpm_logprobgs_c_i",
     "hdpm_split_and_merge", "hdpm_run_markov_chain", "hdpm_get_stats", "hdpm_reset_stats",
     "hdpm_set_debug", "hdpm_synchronize", "hdpm_init_chain", "hdpm_iteration", "hdpm_iterations", "hdpm_rng_fill_device",
-    "hdpm_get_pool_heads",
+    "hdpm_get_pool_heads", "hdpm_set_option",
 )
+
+OPT_HIG_LOGSPACE = 1
 
 STATUS = {0: "OK", 1: "E_VALIDATE", 2: "E_GSL", 3: "E_PROB", 4: "E_WALKER", 5: "E_ARG",
           6: "E_DEVICE", 7: "E_NODEVICE"}
@@ -111,6 +113,7 @@ def lib():
         "hdpm_set_debug": ([vp, i32], C.c_int),
         "hdpm_synchronize": ([vp], C.c_int),
         "hdpm_get_pool_heads": ([vp, vp, i64], C.c_int),
+        "hdpm_set_option": ([vp, i32, f64], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

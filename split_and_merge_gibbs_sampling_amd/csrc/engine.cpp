@@ -507,6 +507,7 @@ struct Ctx {
   // aux_data
   int n = 0, d = 0, nq = 0, dp = 0, mmax = 0;
   int wb = 1, W = 1, bw = 0;          // bits per attribute, field-packed words per row, bound words
+  bool hig_log = false;               // HDPM_OPT_HIG_LOGSPACE (rmath.hpp log_hyperg_2F1)
   int Ws = 2;                         // words per bit-plane of the bit-sliced rows
   double gamma = 0;
   std::vector<int32_t> att;
@@ -1120,7 +1121,7 @@ struct Ctx {
     for (int j = 0; j < d; ++j) {
       int e = kOk;
       const double mj = (double)att[j];
-      out[j] = rhig1_decided(rng, vv[j], ww[j], mj, beta_path(vv[j], ww[j], mj), &e);
+      out[j] = rhig1_decided(rng, vv[j], ww[j], mj, beta_path(vv[j], ww[j], mj), &e, hig_log);
       if (e) return e;
     }
     return kOk;
@@ -2182,7 +2183,7 @@ struct Ctx {
         out = P.x / ((mj - 1) * (1 - P.x));
       } else {
         int e = kOk;
-        out = bisec_hyper2(P.nw, P.nv, mj, P.x, &e);
+        out = bisec_hyper2(P.nw, P.nv, mj, P.x, &e, hig_log);
         if (e) { ok = false; continue; }
       }
       pj.Sig[(size_t)k * d + j] = -1 / std::log(out);
@@ -2999,6 +3000,17 @@ int hdpm_get_pool_heads(hdpm_ctx* h, uint64_t* out, int64_t P) {
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return HDPM_OK;
   })
+}
+int hdpm_set_option(hdpm_ctx* h, int32_t option, double value) {
+  CTX();
+  switch (option) {
+    case HDPM_OPT_HIG_LOGSPACE:
+      ctx->hig_log = value != 0.0;
+      return HDPM_OK;
+    default:
+      ctx->err = "unknown option";
+      return HDPM_E_ARG;
+  }
 }
 int hdpm_synchronize(hdpm_ctx* h) {
   CTX();

@@ -572,8 +572,57 @@ inline int hyperg_2F1(double a, double b, double c, double x, double* val) {
   return GSL_SUCCESS;
 }
 
-// hg:11-48.  Sets *err = kGsl where the reference throws.
-inline double norm_const2(double d, double c, double m, int* err) {
+// Extension (HDPM_OPT_HIG_LOGSPACE; not the reference): log 2F1.  The reference's series
+// runs first; when it ends finite its log is returned, so those values keep their bits.
+// When it overflows (clusters of ~1.4k+ members) or runs out of its 30000
+// terms, the same positive series is summed again with the partial sum rescaled by 2^-960
+// whenever it passes 2^960, for up to 10^7 terms.  Statuses as hyperg_2F1.
+inline int log_hyperg_2F1(double a, double b, double c, double x, double* lval) {
+  const double eps = 2.2204460492503131e-16, loc_eps = 1000.0 * eps;
+  double plain;
+  const int st = hyperg_2F1(a, b, c, x, &plain);
+  *lval = NAN;
+  if (st == GSL_SUCCESS && std::isfinite(plain)) {
+    *lval = std::log(plain);
+    return st;
+  }
+  if (st != GSL_SUCCESS && st != GSL_EMAXITER) return st;
+  if (std::fabs(c - b) < loc_eps || std::fabs(c - a) < loc_eps) {
+    *lval = (c - a - b) * std::log(1.0 - x);       // exp() overflowed in the plain path
+    return GSL_SUCCESS;
+  }
+  double sum = 1.0, del = 1.0, k = 0.0, scale = 0.0;
+  int i = 0;
+  do {
+    if (++i > 10000000) { *lval = std::log(sum) + scale * M_LN2; return GSL_EMAXITER; }
+    del *= (a + k) * (b + k) * x / ((c + k) * (k + 1.0));
+    if (del == 0.0) break;
+    sum += del;
+    if (sum > 0x1p960) {
+      sum *= 0x1p-960;
+      del *= 0x1p-960;
+      scale += 960.0;
+    }
+    k += 1.0;
+  } while (std::fabs(del / sum) > eps);
+  *lval = scale == 0.0 ? std::log(sum) : std::log(sum) + scale * M_LN2;
+  return GSL_SUCCESS;
+}
+
+// hg:11-48.  Sets *err = kGsl where the reference throws.  `logspace`: the extension above
+// (an overflowing series gives its finite log instead of the throw).
+inline double norm_const2(double d, double c, double m, int* err, bool logspace = false) {
+  if (logspace) {
+    double lv;
+    const int st = log_hyperg_2F1(d + c, 1, d + 2, (m - 1) / m, &lv);
+    if (st != GSL_SUCCESS) {
+      if (st == GSL_EMAXITER) return -INFINITY;
+      *err = kGsl;
+      return NAN;
+    }
+    if (!std::isfinite(lv)) { *err = kGsl; return NAN; }
+    return std::log(d + 1) + (d + c) * std::log(m) - lv;
+  }
   double val;
   int st = hyperg_2F1(d + c, 1, d + 2, (m - 1) / m, &val);
   if (st != GSL_SUCCESS) {
@@ -585,27 +634,33 @@ inline double norm_const2(double d, double c, double m, int* err) {
   return std::log(d + 1) + (d + c) * std::log(m) - std::log(val);
 }
 
-inline double lF_conK2(double u, double d, double c, double m, double lK) {  // hg:183-217
+inline double lF_conK2(double u, double d, double c, double m, double lK, bool logspace = false) {  // hg:183-217
   if (u == 0) return -INFINITY;
   if (u == 1) return 0;
   double x = u * (m - 1) / (1 + u * (m - 1));
-  double app;
-  if (hyperg_2F1(1, d + c, d + 2, x, &app) != GSL_SUCCESS) app = NAN;
-  return lK - std::log(d + 1) + (d + 1) * std::log(u) - (d + c) * std::log(1 + u * (m - 1)) +
-         std::log(app);
+  double lapp;
+  if (logspace) {
+    if (log_hyperg_2F1(1, d + c, d + 2, x, &lapp) != GSL_SUCCESS) lapp = NAN;
+  } else {
+    double app;
+    if (hyperg_2F1(1, d + c, d + 2, x, &app) != GSL_SUCCESS) app = NAN;
+    lapp = std::log(app);
+  }
+  return lK - std::log(d + 1) + (d + 1) * std::log(u) - (d + c) * std::log(1 + u * (m - 1)) + lapp;
 }
 
-inline double bisec_hyper2(double d, double c, double m, double Omega, int* err) {  // hg:221-287
+inline double bisec_hyper2(double d, double c, double m, double Omega, int* err,
+                           bool logspace = false) {  // hg:221-287
   double centro = 0.5;
-  double lK = norm_const2(d, c, m, err);
+  double lK = norm_const2(d, c, m, err, logspace);
   if (*err) return NAN;
-  double app = lF_conK2(centro, d, c, m, lK) - std::log(Omega);
+  double app = lF_conK2(centro, d, c, m, lK, logspace) - std::log(Omega);
   double su, giu;
   int counter = 1;
   if (app < 0) { giu = 0.5; su = 1; } else { giu = 0; su = 0.5; }
   while (((su - giu) > 0.000000001) & (counter < 150)) {
     centro = (su + giu) / 2;
-    app = lF_conK2(centro, d, c, m, lK) - std::log(Omega);
+    app = lF_conK2(centro, d, c, m, lK, logspace) - std::log(Omega);
     if (app < 0) giu = centro; else su = centro;
     counter = counter + 1;
   }
@@ -613,7 +668,8 @@ inline double bisec_hyper2(double d, double c, double m, double Omega, int* err)
 }
 
 // rhig(1, v, w, m) (hg:346-378); `beta_path` is the cached hg:359 decision.
-inline double rhig1_decided(Rng& rng, double v, double w, double m, bool beta_path, int* err) {
+inline double rhig1_decided(Rng& rng, double v, double w, double m, bool beta_path, int* err,
+                            bool logspace = false) {
   double out;
   if (beta_path) {
     double x = rbeta(rng, w + 1, v - 1);
@@ -621,7 +677,7 @@ inline double rhig1_decided(Rng& rng, double v, double w, double m, bool beta_pa
     out = x / ((m - 1) * (1 - x));
   } else {
     double Omega = rng.unif();
-    out = bisec_hyper2(w, v, m, Omega, err);
+    out = bisec_hyper2(w, v, m, Omega, err, logspace);
     if (*err) return NAN;
   }
   return -1 / std::log(out);
@@ -631,8 +687,8 @@ inline bool rhig_beta_path(double v, double w, double m) {
   return qbeta01_lt(w + 1, v - 1, (m - 1) / m) && (m - 1) / m > 4 / 5;
 }
 
-inline double rhig1(Rng& rng, double v, double w, double m, int* err) {
-  return rhig1_decided(rng, v, w, m, rhig_beta_path(v, w, m), err);
+inline double rhig1(Rng& rng, double v, double w, double m, int* err, bool logspace = false) {
+  return rhig1_decided(rng, v, w, m, rhig_beta_path(v, w, m), err, logspace);
 }
 
 // dhamming (cf:355-377) split into its two attribute-level values: the device adds

@@ -219,8 +219,8 @@ static double logprobgs_c_i(Ctx* c, const HState& gs, const HState& g, const std
 }
 
 // sm:6-18
-static double logdensity_hig(double sigmaj, double vv, double ww, double m, int* err) {
-  double K = norm_const2(ww, vv, m, err);
+static double logdensity_hig(double sigmaj, double vv, double ww, double m, int* err, bool logspace) {
+  double K = norm_const2(ww, vv, m, err, logspace);
   return K - (vv + ww) * std::log(1 + std::exp(-1 / sigmaj) * (m - 1)) - (ww + 1) / sigmaj - 2 * std::log(sigmaj);
 }
 
@@ -251,7 +251,7 @@ static double logprobgs_phi(Ctx* c, const HState& gs, const HState& g, int idx, 
     const double sumdelta = f[(size_t)j * c->mmax + (cstar[j] - 1)];
     const double new_v = c->v[j] + sumdelta;
     const double new_w = c->w[j] + nm - sumdelta;
-    log_sigma_prob += logdensity_hig(gss[j], new_v, new_w, c->att[j], err);
+    log_sigma_prob += logdensity_hig(gss[j], new_v, new_w, c->att[j], err, c->hig_log);
   }
   return log_center_prob + log_sigma_prob;
 }
@@ -276,7 +276,7 @@ static double priors(Ctx* c, const HState& s, int k, int* err) {
   double priorg = 0;
   for (int j = 0; j < c->d; ++j) {
     priorg -= std::log((double)c->att[j]);
-    priorg += logdensity_hig(sig[j], c->v[j], c->w[j], c->att[j], err);
+    priorg += logdensity_hig(sig[j], c->v[j], c->w[j], c->att[j], err, c->hig_log);
   }
   return priorg;
 }

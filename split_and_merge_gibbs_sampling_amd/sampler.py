@@ -178,6 +178,11 @@ class Engine:
     def synchronize(self):
         self._check(self._L.hdpm_synchronize(self._h))
 
+    def set_hig_logspace(self, on: bool = True):
+        """Extension beyond the reference (include/hdpm.h HDPM_OPT_HIG_LOGSPACE): finite HIG
+        log-densities for clusters whose 2F1 series overflows (the reference throws)."""
+        self._check(self._L.hdpm_set_option(self._h, _lib.OPT_HIG_LOGSPACE, 1.0 if on else 0.0))
+
     # ---------------------------------------------------------------- driver
     @staticmethod
     def chain_params(verbose=0, m=5, iterations=1000, L=1, burnin=5000, t=10, r=10, neal8=False,
@@ -228,16 +233,20 @@ class Engine:
 
 def run_markov_chain(data, attrisize, gamma, v, w, verbose=0, m=5, iterations=1000, L=1, c_i=None,
                      burnin=5000, t=10, r=10, neal8=False, split_merge=True, n8_step_size=1,
-                     sam_step_size=1, thinning=1, *, seed=None, rng_state=None, device=0):
+                     sam_step_size=1, thinning=1, *, seed=None, rng_state=None, device=0, hig_logspace=False):
     """Drop-in for the reference's ``run_markov_chain`` (code/launcher.cpp:6-14).
 
     ``data`` holds the categorical codes 1..m_j (an N x D matrix).  The R random stream
     is ``set.seed(seed)`` or an explicit 625-word ``rng_state``; the returned dict has
     the fields of the reference's result list (plus ``rng_state`` after the run).
+    ``hig_logspace=True`` turns on the log-space 2F1 extension (``Engine.set_hig_logspace``);
+    the default keeps the reference's semantics, including its throw on overflow.
     """
     eng = Engine(device)
     try:
         eng.set_data(np.asarray(data), attrisize, gamma, v, w)
+        if hig_logspace:
+            eng.set_hig_logspace(True)
         if rng_state is not None:
             eng.rng_state = rng_state
         else:

@@ -39,6 +39,8 @@ def lib():
         build()
         L = C.CDLL(LIB_PATH)
         L.orc_ffi_set_seed.argtypes = [C.c_uint32, _i32p]
+        L.orc_ffi_set_hig_logspace.argtypes = [C.c_int]
+        L.orc_ffi_set_hig_logspace.restype = None
         L.orc_ffi_runif.argtypes = [_i32p, C.c_int64, _f64p]
         L.orc_ffi_rbeta.argtypes = [_i32p, C.c_double, C.c_double, C.c_int, _f64p]
         L.orc_ffi_rhig.argtypes = [_i32p, C.c_double, C.c_double, C.c_double, C.c_int, _f64p]
@@ -114,6 +116,11 @@ def norm_const2(d, c, m):
     err = C.c_int(0)
     v = lib().orc_ffi_norm_const2(d, c, m, C.byref(err))
     return v, err.value
+
+
+def set_hig_logspace(on: bool):
+    """Mirror of hdpm's HDPM_OPT_HIG_LOGSPACE extension (process-wide in the oracle)."""
+    lib().orc_ffi_set_hig_logspace(1 if on else 0)
 
 
 # ----------------------------------------------------------------- model

@@ -541,3 +541,25 @@ def test_wide_mixed_levels_sweeps_heads_and_records(hd, oracle, debug):
     ds = synth(3000, 200, 6, (2, 6), seed=27)          # Ws = 4, wb = 4 heads
     cen, sig = random_params(ds, 6, 28)
     sweep_case(hd, oracle, ds, ds.truth, cen, sig, ds.n * 3, seed=47, sweeps=3, phi=True, debug=debug)
+
+
+def test_hig_logspace_chain_large_clusters(hd, oracle):
+    # Two clusters of ~1.5k members: the SM priors' 2F1 series (hg:11-48) overflows, so the
+    # reference throws (HDPM_E_GSL).  With the HDPM_OPT_HIG_LOGSPACE extension the chain
+    # runs and follows the oracle's mirror of the extension step for step.
+    ds = synth(3000, 16, 2, 2, seed=3)
+    kw = dict(m=3, iterations=10, L=1, c_i=ds.truth, burnin=0, t=3, r=3, neal8=True, split_merge=True)
+    with pytest.raises(hd.HdpmError) as e:
+        hd.run_markov_chain(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w, seed=5, **kw)
+    assert e.value.status == 2
+    try:
+        oracle.set_hig_logspace(True)
+        st, ref = oracle.run_markov_chain(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w, seed=5, fast=1, **kw)
+    finally:
+        oracle.set_hig_logspace(False)
+    assert st == 0
+    res = hd.run_markov_chain(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w, seed=5, hig_logspace=True, **kw)
+    assert np.array_equal(res["c_i"], ref["c_i"])
+    assert np.array_equal(res["total_cls"], ref["total_cls"])
+    assert np.array_equal(res["accepted"], ref["accepted"])
+    np.testing.assert_allclose(res["loglikelihood"], ref["loglikelihood"], rtol=RTOL, atol=0)

@@ -144,3 +144,37 @@ def test_random_init_with_unused_label_fails_validation(oracle, zoo):
     st, _ = oracle.run_markov_chain(zoo.codes, zoo.attrisize, zoo.gamma, zoo.v, zoo.w, m=3, iterations=2, L=20,
                                     burnin=0, neal8=True, split_merge=False, seed=bad, fast=0)
     assert st == 1
+
+
+def _bits(x):
+    return np.float64(x).view(np.uint64)
+
+
+def test_hig_logspace_extension(oracle):
+    """HDPM_OPT_HIG_LOGSPACE (an extension, not the reference): where the reference's 2F1
+    series (hg:11-48) is finite within 30000 terms the log-space value has the same bits;
+    where it overflows (the reference throws, hg:43-45) the value is finite and agrees with
+    mpmath at 50 digits within 1e-12 relative."""
+    mp = pytest.importorskip("mpmath")
+    try:
+        for d in (0.25, 0.5, 3.5, 40.25):
+            for c in (2.0, 3.0, 6.0, 57.0, 400.0, 900.0):
+                for m in (2.0, 4.0, 6.0):
+                    oracle.set_hig_logspace(False)
+                    a, ea = oracle.norm_const2(d, c, m)
+                    oracle.set_hig_logspace(True)
+                    b, eb = oracle.norm_const2(d, c, m)
+                    if ea == 0:
+                        assert eb == 0 and _bits(a) == _bits(b), (d, c, m, a, b)
+        mp.mp.dps = 50
+        for d, c, m in [(0.25, 3000.0, 2.0), (0.25, 20000.0, 2.0), (5.25, 8000.0, 4.0), (2.5, 2500.0, 6.0)]:
+            oracle.set_hig_logspace(False)
+            _, ea = oracle.norm_const2(d, c, m)
+            assert ea == 2                          # the reference throws here
+            oracle.set_hig_logspace(True)
+            b, eb = oracle.norm_const2(d, c, m)
+            assert eb == 0 and np.isfinite(b)
+            ref = float(mp.log(d + 1) + (d + c) * mp.log(m) - mp.log(mp.hyp2f1(d + c, 1, d + 2, mp.mpf(m - 1) / m, maxterms=10**6)))
+            assert abs(b - ref) <= 1e-12 * abs(ref), (d, c, m, b, ref)
+    finally:
+        oracle.set_hig_logspace(False)
