@@ -187,6 +187,9 @@ def main():
     ap.add_argument("--m", type=int, default=3)
     ap.add_argument("--sm", action="store_true",
                     help="include the split-merge move in every step (t = r = 10, la:111-115)")
+    ap.add_argument("--hig-logspace", choices=("auto", "on", "off"), default="auto",
+                    help="HDPM_OPT_HIG_LOGSPACE (log-space 2F1, an extension): auto = on with --sm, where "
+                         "clusters of thousands of members overflow the reference's series (it throws)")
     ap.add_argument("--start-iter", type=int, default=0,
                     help="first iteration index (0: the warmup includes iteration 0's pool regeneration)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
@@ -206,6 +209,9 @@ def main():
     eng = hd.Engine(local)
     eng.set_data(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w)
     eng.set_seed(1 + rank)
+    hig_log = args.hig_logspace == "on" or (args.hig_logspace == "auto" and args.sm)
+    if hig_log:
+        eng.set_hig_logspace(True)
     if os.environ.get("HDPM_BENCH_HOST_POOL"):
         eng.set_debug(64)                        # sequential host pool generator (A/B runs)
     params = eng.chain_params(m=args.m, iterations=args.steps + args.warmup, L=0, burnin=0, neal8=True,
@@ -290,6 +296,7 @@ def main():
             "exact_points_per_step": st["exact_points"] / args.steps,
             "listed_points_per_step": st["listed_points"] / args.steps,
             "split_merge": bool(args.sm),
+            "hig_logspace": hig_log,
             "rounds_per_step": st["rounds"] / args.steps,
             "rng_windows": {"launched": st["rng_windows"], "fresh": st["rng_windows_fresh"]},
             "pool_generation": {"init": pool_report(st_init, ds.n * args.m),

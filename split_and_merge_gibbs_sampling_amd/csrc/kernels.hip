@@ -1760,9 +1760,10 @@ __global__ __launch_bounds__(kBlock) void k_sm_ll(SmArgs a) {
 
 // Exact sm:204-215 two-way draw.  probs[k] = log(n_k) + H_k; normalise; FixupProb;
 // revsort of two entries (ties: second first); cumulative compare.
-__device__ __forceinline__ int two_way_draw(double v0, double v1, double rU) {
+__device__ __forceinline__ void two_way_probs(double v0, double v1, double& p0, double& p1) {
   const double mx = fmax(v0, v1);
-  double p0 = exp(v0 - mx), p1 = exp(v1 - mx);
+  p0 = exp(v0 - mx);
+  p1 = exp(v1 - mx);
   double sum = 0.0;
   sum += p0;
   sum += p1;
@@ -1773,38 +1774,61 @@ __device__ __forceinline__ int two_way_draw(double v0, double v1, double rU) {
   if (p1 > 0) s2 += p1;
   p0 = p0 / s2;
   p1 = p1 / s2;
+}
+__device__ __forceinline__ int two_way_pick(double p0, double p1, double rU) {
   // revsort(n = 2): descending, equal -> index 2 first
   const bool first0 = p0 > p1;
   const double a0 = first0 ? p0 : p1;
   return (rU <= a0) ? (first0 ? 0 : 1) : (first0 ? 1 : 0);
 }
+__device__ __forceinline__ int two_way_draw(double v0, double v1, double rU) {
+  double p0, p1;
+  two_way_probs(v0, v1, p0, p1);
+  return two_way_pick(p0, p1, rU);
+}
 
-// One wave walks S in order.  A point whose two log-weights differ by more than T + 2*ln2
-// is decided without the exact path (its smaller weight cannot change any rounding),
-// so each batch of 64 only serialises on its uncertain points.
+// One wave walks S in batches of 64 in order.  Within a batch the size n1 of c1 seen by
+// lane p lies in [n1 - p, n1 + p] (n1 + n2 is fixed: points only change sides).  p0 of the
+// draw is monotone in n1 in exact arithmetic, and the pick only changes where p0 crosses
+// 1/2 (the revsort order), rU or 1 - rU (sm:215 with revsort).  So a lane evaluates the
+// exact draw at both ends of its range; when no threshold lies within 1e-9 of [p0(lo),
+// p0(hi)] (rounding moves p0 by far less) its pick is the same for every count it can see
+// and it is settled in parallel.  The others are walked one by one with their exact counts.
 __global__ __launch_bounds__(kWave) void k_sm_scan(SmArgs a, double T) {
+  (void)T;
   const int lane = threadIdx.x;
   int n1 = a.n1, n2 = a.n2;
+  const int tot = n1 + n2;
+  const double margin = 1e-9;
   for (int base = 0; base < a.nS; base += kWave) {
     const int q = base + lane;
     const bool act = q < a.nS;
     int cur = act ? a.side[q] : 0;
     const double l0 = act ? a.ll[q] : 0.0, l1 = act ? a.ll[a.nS + q] : 0.0;
     const double rU = act ? raw_to_unif(a.raw[q]) : 0.0;
-    // certainty at batch-start counts; <= 64 moves in a batch change log n by < ln 2
-    // as long as both clusters keep >= 128 points
     bool certain = false;
     int choice = cur;
-    if (act && n1 >= 130 && n2 >= 130) {
-      const double v0 = a.logn[n1 - (cur == 0)] + l0, v1 = a.logn[n2 - (cur == 1)] + l1;
-      if (fabs(v0 - v1) > T + 2.0 * M_LN2) { certain = true; choice = v0 > v1 ? 0 : 1; }
+    if (act) {
+      // n1 as lane `lane` may see it, within the sizes the clusters can take
+      const int lo = max(n1 - lane, 1 + (cur == 0)), hi = min(n1 + lane, tot - 1 - (cur == 1));
+      double pa0, pa1, pb0, pb1;
+      two_way_probs(a.logn[lo - (cur == 0)] + l0, a.logn[tot - lo - (cur == 1)] + l1, pa0, pa1);
+      const int pick = two_way_pick(pa0, pa1, rU);
+      if (lo == hi) {
+        certain = true;
+      } else {
+        two_way_probs(a.logn[hi - (cur == 0)] + l0, a.logn[tot - hi - (cur == 1)] + l1, pb0, pb1);
+        const double pmin = fmin(pa0, pb0) - margin, pmax = fmax(pa0, pb0) + margin;
+        const double onem = 1.0 - rU;
+        certain = !(pmin <= 0.5 && 0.5 <= pmax) && !(pmin <= rU && rU <= pmax) && !(pmin <= onem && onem <= pmax);
+      }
+      if (certain) choice = pick;
     }
     unsigned long long unc = __ballot(act && !certain);
-    unsigned long long mv01 = __ballot(act && certain && cur == 0 && choice == 1);
-    unsigned long long mv10 = __ballot(act && certain && cur == 1 && choice == 0);
-    // walk uncertain lanes in order; counts at lane q = batch start + moves of lanes < q
+    const unsigned long long mv01 = __ballot(act && certain && cur == 0 && choice == 1);
+    const unsigned long long mv10 = __ballot(act && certain && cur == 1 && choice == 0);
+    // walk uncertain lanes in order; counts at lane u = batch start + moves of lanes < u
     int d1 = 0, d2 = 0;   // count deltas from uncertain lanes processed so far
-    int done_mask_lo = 0;
     while (unc) {
       const int u = __ffsll((long long)unc) - 1;
       const unsigned long long below = (u == 0) ? 0ull : ((1ull << u) - 1ull);
@@ -1822,7 +1846,6 @@ __global__ __launch_bounds__(kWave) void k_sm_scan(SmArgs a, double T) {
       if (cu == 0 && pick == 1) { d1--; d2++; }
       if (cu == 1 && pick == 0) { d1++; d2--; }
       unc &= ~(1ull << u);
-      (void)done_mask_lo;
     }
     n1 += d1 - __popcll(mv01) + __popcll(mv10);
     n2 += d2 + __popcll(mv01) - __popcll(mv10);

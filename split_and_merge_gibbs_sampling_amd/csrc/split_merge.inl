@@ -58,53 +58,81 @@ static void row_tables(const Ctx* c, const uint8_t* cen, const double* sig, std:
   (void)cen;
 }
 
-// freq of one cluster over its members (host): f[j][l]
-static void host_freq(const Ctx* c, const HState& s, int k, std::vector<double>& f, int& nn) {
-  f.assign((size_t)c->d * c->mmax, 0.0);
-  nn = 0;
-  for (int i = 0; i < c->n; ++i) {
-    if (s.c[i] != k) continue;
-    nn++;
-    const uint8_t* x = &c->codes[(size_t)i * c->d];
-    for (int j = 0; j < c->d; ++j) f[(size_t)j * c->mmax + (x[j] - 1)] += 1.0;
-  }
+// Frequency tables of one cluster (f[j * mmax + l] = members with code l + 1 at attribute j,
+// integer-valued doubles) and its size.  The split-merge move touches only the members M =
+// S + {i1, i2} of c(i1) and c(i2) (sm:263-301), so every table it needs is a subset of M's;
+// they are built once per move and updated by the points a restricted scan moves, instead of
+// the reference's O(N D) membership scan per update_phi / logprobgs_phi call.  Counts are
+// exact in doubles, so the tables equal the reference's freq bit for bit.
+struct Freq {
+  std::vector<double> f;
+  int nn = 0;
+};
+
+static void freq_add_row(const Ctx* c, Freq& F, int i, double sgn) {
+  const uint8_t* x = &c->codes[(size_t)i * c->d];
+  double* f = F.f.data();
+  for (int j = 0; j < c->d; ++j) f[(size_t)j * c->mmax + (x[j] - 1)] += sgn;
+  F.nn += sgn > 0 ? 1 : -1;
 }
 
-// update_phi (cf:511-591) on a host state for the clusters in idx (ascending order).
-static int hupdate_phi(Ctx* c, HState& s, std::vector<int> idx) {
-  std::vector<char> mask(s.K, 0);
-  for (int k : idx)
-    if (k >= 0 && k < s.K) mask[k] = 1;
-  std::vector<double> f, prob(c->mmax), nv(c->d), nw(c->d);
-  for (int i = 0; i < s.K; ++i) {
-    if (!mask[i]) continue;
-    int nn;
-    host_freq(c, s, i, f, nn);
-    if (nn == 0) continue;
-    uint8_t* cen = &s.center[(size_t)i * c->d];
-    double* sig = &s.sigma[(size_t)i * c->d];
-    for (int j = 0; j < c->d; ++j) {
-      const int mj = c->att[j];
-      for (int l = 0; l < mj; ++l) prob[l] = (-((double)nn - f[(size_t)j * c->mmax + l])) / sig[j];
-      double mx = prob[0];
-      for (int l = 1; l < mj; ++l) if (prob[l] > mx) mx = prob[l];
-      for (int l = 0; l < mj; ++l) prob[l] = std::exp(prob[l] - mx);
-      double sum = 0.0;
-      for (int l = 0; l < mj; ++l) sum += prob[l];
-      for (int l = 0; l < mj; ++l) prob[l] = prob[l] / sum;
-      int pick = sample_prob1(c->rng, prob.data(), mj, c->sp, c->sperm);
-      if (pick < 0) return -pick;
-      cen[j] = (uint8_t)(pick + 1);
+// Table of the members q of M with s.c[q] == k (k < 0: all of M); attribute ranges on the
+// host pool for wide rows.
+static void freq_over(const Ctx* c, const HState& s, const std::vector<int>& M, int k, Freq& F) {
+  F.f.assign((size_t)c->d * c->mmax, 0.0);
+  std::vector<int> mem;
+  mem.reserve(M.size());
+  for (int q : M)
+    if (k < 0 || s.c[q] == k) mem.push_back(q);
+  F.nn = (int)mem.size();
+  const int64_t work = (int64_t)mem.size() * c->d;
+  const int chunk = 32;
+  const int nchunk = (c->d + chunk - 1) / chunk;
+  auto run = [&](int ch) {
+    const int j0 = ch * chunk, j1 = std::min(c->d, j0 + chunk);
+    double* f = F.f.data();
+    for (int q : mem) {
+      const uint8_t* x = &c->codes[(size_t)q * c->d];
+      for (int j = j0; j < j1; ++j) f[(size_t)j * c->mmax + (x[j] - 1)] += 1.0;
     }
-    for (int j = 0; j < c->d; ++j) {
-      const double sumdelta = f[(size_t)j * c->mmax + (cen[j] - 1)];
-      nw[j] = c->w[j] + nn - sumdelta;
-      nv[j] = c->v[j] + sumdelta;
-    }
-    int st = c->sample_sigma(nv.data(), nw.data(), sig);
-    if (st) return st;
+  };
+  if (work >= (1 << 18) && nchunk > 1) pool_for(nchunk, run, 1);
+  else for (int ch = 0; ch < nchunk; ++ch) run(ch);
+}
+
+static void freq_minus(const Freq& A, const Freq& B, Freq& out) {
+  out.f.resize(A.f.size());
+  for (size_t i = 0; i < A.f.size(); ++i) out.f[i] = A.f[i] - B.f[i];
+  out.nn = A.nn - B.nn;
+}
+
+// update_phi (cf:511-591) of one cluster k of s whose table is F.
+static int hupdate_phi_one(Ctx* c, HState& s, int k, const Freq& F) {
+  if (F.nn == 0) return kOk;
+  std::vector<double> prob(c->mmax), nv(c->d), nw(c->d);
+  const double nn = (double)F.nn;
+  uint8_t* cen = &s.center[(size_t)k * c->d];
+  double* sig = &s.sigma[(size_t)k * c->d];
+  for (int j = 0; j < c->d; ++j) {
+    const int mj = c->att[j];
+    const double* f = &F.f[(size_t)j * c->mmax];
+    for (int l = 0; l < mj; ++l) prob[l] = (-(nn - f[l])) / sig[j];
+    double mx = prob[0];
+    for (int l = 1; l < mj; ++l) if (prob[l] > mx) mx = prob[l];
+    for (int l = 0; l < mj; ++l) prob[l] = std::exp(prob[l] - mx);
+    double sum = 0.0;
+    for (int l = 0; l < mj; ++l) sum += prob[l];
+    for (int l = 0; l < mj; ++l) prob[l] = prob[l] / sum;
+    int pick = sample_prob1(c->rng, prob.data(), mj, c->sp, c->sperm);
+    if (pick < 0) return -pick;
+    cen[j] = (uint8_t)(pick + 1);
   }
-  return kOk;
+  for (int j = 0; j < c->d; ++j) {
+    const double sumdelta = F.f[(size_t)j * c->mmax + (cen[j] - 1)];
+    nw[j] = c->w[j] + nn - sumdelta;
+    nv[j] = c->v[j] + sumdelta;
+  }
+  return c->sample_sigma(nv.data(), nw.data(), sig);
 }
 
 static void hrecount(const Ctx* c, HState& s) {
@@ -147,50 +175,61 @@ static void sm_upload_S(Ctx* c, SmWork& W, const std::vector<int>& S) {
   if (nS) HIPCHK(hipMemcpyAsync(W.d_S.p, S.data(), nS * 4, hipMemcpyHostToDevice, c->stream));
 }
 
-// sm:163-225 on host state s with the scan on the device.
-static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1, int i2, int t) {
+// sm:163-225 on host state s with the scan on the device.  F1 / F2: the tables of s.c[i1]
+// and s.c[i2] on entry, kept current (points the scan moves change sides).  The members of
+// both clusters are S + {i1, i2}, so their sizes come from the tables, neither can empty
+// (i1, i2 never move) and validate_state (sm:222) cannot fail.
+static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1, int i2, int t, Freq& F1,
+                            Freq& F2) {
   SmWork& W = smwork(c);
   const int c1 = s.c[i1], c2 = s.c[i2];
   const int nS = (int)S.size();
   sm_upload_S(c, W, S);
-  std::vector<int> side(nS);
+  std::vector<int> side(nS), prev(nS);
   std::vector<uint32_t> raw(nS);
   const double T = 54.0 * M_LN2 + std::log(2.0) + 0.5;
+  for (int q = 0; q < nS; ++q) side[q] = (s.c[S[q]] == c1) ? 0 : 1;
   for (int iter = 0; iter < t; ++iter) {
-    int n1 = 0, n2 = 0;
-    for (int i = 0; i < c->n; ++i) { n1 += (s.c[i] == c1); n2 += (s.c[i] == c2); }
-    for (int q = 0; q < nS; ++q) side[q] = (s.c[S[q]] == c1) ? 0 : 1;
     c->rng.raw_block(raw.data(), nS);
     if (nS) {
+      prev = side;
       sm_upload_two(c, W, s, c1, c2);
       HIPCHK(hipMemcpyAsync(W.d_side.p, side.data(), (size_t)nS * 4, hipMemcpyHostToDevice, c->stream));
       HIPCHK(hipMemcpyAsync(W.d_raw.p, raw.data(), (size_t)nS * 4, hipMemcpyHostToDevice, c->stream));
       SmArgs a = sm_args(c, W, nS);
-      a.n1 = n1; a.n2 = n2;
+      a.n1 = F1.nn; a.n2 = F2.nn;
       HIPCHK(launch_sm_ll(a, c->stream));
       HIPCHK(launch_sm_scan(a, T, c->stream));
       HIPCHK(hipMemcpyAsync(side.data(), W.d_side.p, (size_t)nS * 4, hipMemcpyDeviceToHost, c->stream));
       HIPCHK(hipStreamSynchronize(c->stream));
-      for (int q = 0; q < nS; ++q) s.c[S[q]] = side[q] == 0 ? c1 : c2;
+      for (int q = 0; q < nS; ++q) {
+        if (side[q] == prev[q] || c1 == c2) continue;
+        const int i = S[q];
+        s.c[i] = side[q] == 0 ? c1 : c2;
+        freq_add_row(c, side[q] == 0 ? F1 : F2, i, 1.0);
+        freq_add_row(c, side[q] == 0 ? F2 : F1, i, -1.0);
+      }
     }
-    hrecount(c, s);
-    int st = hupdate_phi(c, s, {c1, c2});   // sm:221 (mask -> ascending order)
+    s.counts[c1] = F1.nn;
+    s.counts[c2] = F2.nn;
+    // sm:221 update_phi({c1, c2}): the mask visits clusters in ascending index order, a
+    // repeated index once (c1 == c2 only through the restricted-Gibbs C ABI)
+    int st = c1 <= c2 ? hupdate_phi_one(c, s, c1, F1) : hupdate_phi_one(c, s, c2, F2);
     if (st) return st;
-    st = hvalidate(s);
+    if (c1 != c2) st = c1 < c2 ? hupdate_phi_one(c, s, c2, F2) : hupdate_phi_one(c, s, c1, F1);
     if (st) return st;
   }
   return kOk;
 }
 
 // sm:96-161, gamma_star = gs, gamma = g (launch).  Device terms, compensated sum.
+// n1, n2: sizes of g's clusters c(i1), c(i2).
 static double logprobgs_c_i(Ctx* c, const HState& gs, const HState& g, const std::vector<int>& S, int i1,
-                            int i2) {
+                            int i2, int n1, int n2) {
   SmWork& W = smwork(c);
   const int c1 = g.c[i1], c2 = g.c[i2];
   const int nS = (int)S.size();
   if (nS == 0) return 0.0;
-  int n1 = 0, n2 = 0;
-  for (int i = 0; i < c->n; ++i) { n1 += (g.c[i] == c1); n2 += (g.c[i] == c2); }
   sm_upload_S(c, W, S);
   std::vector<int> side(nS), sref(nS);
   for (int q = 0; q < nS; ++q) {
@@ -225,11 +264,11 @@ static double logdensity_hig(double sigmaj, double vv, double ww, double m, int*
 }
 
 // sm:20-94
-static double logprobgs_phi(Ctx* c, const HState& gs, const HState& g, int idx, int* err) {
+// F: the table of gs's cluster c(idx).
+static double logprobgs_phi(Ctx* c, const HState& gs, const HState& g, int idx, const Freq& F, int* err) {
   const int k = gs.c[idx];
-  std::vector<double> f;
-  int nm;
-  host_freq(c, gs, k, f, nm);
+  const std::vector<double>& f = F.f;
+  const int nm = F.nn;
   const double* gsig = &g.sigma[(size_t)g.c[idx] * c->d];
   const uint8_t* cstar = &gs.center[(size_t)k * c->d];
   double log_center_prob = 0;
@@ -256,18 +295,26 @@ static double logprobgs_phi(Ctx* c, const HState& gs, const HState& g, int idx, 
   return log_center_prob + log_sigma_prob;
 }
 
-// sm:393-417 (one running sum over members then attributes)
-static double loglikelihood_hamming(Ctx* c, const HState& s, int k) {
+// sm:393-417 from the cluster's table: per attribute f matches and nn - f mismatches of its
+// two dhamming values, summed with a compensated (Neumaier) sum.  The reference adds the N_k D
+// terms one by one; this regrouping agrees with it to its own rounding (~1e-13 relative at
+// 10^6 terms) and only enters the acceptance test log(u) < ratio (sm:591).
+static double loglikelihood_hamming(Ctx* c, const HState& s, int k, const Freq& F) {
   std::vector<double> tab;
   row_tables(c, &s.center[(size_t)k * c->d], &s.sigma[(size_t)k * c->d], tab);
   const uint8_t* cen = &s.center[(size_t)k * c->d];
-  double ll = 0.0;
-  for (int i = 0; i < c->n; ++i) {
-    if (s.c[i] != k) continue;
-    const uint8_t* x = &c->codes[(size_t)i * c->d];
-    for (int j = 0; j < c->d; ++j) ll += tab[2 * j + (x[j] != cen[j] ? 1 : 0)];
+  double hi = 0.0, lo = 0.0;
+  auto add = [&](double x) {
+    const double t = hi + x;
+    lo += std::fabs(hi) >= std::fabs(x) ? (hi - t) + x : (x - t) + hi;
+    hi = t;
+  };
+  for (int j = 0; j < c->d; ++j) {
+    const double fm = F.f[(size_t)j * c->mmax + (cen[j] - 1)];
+    add(fm * tab[2 * j]);
+    add(((double)F.nn - fm) * tab[2 * j + 1]);
   }
-  return ll;
+  return hi + lo;
 }
 
 // sm:419-436
@@ -279,12 +326,6 @@ static double priors(Ctx* c, const HState& s, int k, int* err) {
     priorg += logdensity_hig(sig[j], c->v[j], c->w[j], c->att[j], err, c->hig_log);
   }
   return priorg;
-}
-
-static int csize(const HState& s, int k) {
-  int x = 0;
-  for (int v : s.c) x += (v == k);
-  return x;
 }
 
 static double min0(double x) { return (x < 0.0) ? x : 0.0; }
@@ -349,11 +390,14 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
     const int j2 = (int)(nn * rng.unif());
     i2 = (j2 == j) ? n - 1 : j2;
   }
-  std::vector<int> S;
+  std::vector<int> S, M;               // M: S + {i1, i2}, ascending
   for (int i = 0; i < n; ++i) {
-    if (i == i1 || i == i2) continue;
-    if (st.c[i] == st.c[i1] || st.c[i] == st.c[i2]) S.push_back(i);
+    if (st.c[i] != st.c[i1] && st.c[i] != st.c[i2]) continue;
+    M.push_back(i);
+    if (i != i1 && i != i2) S.push_back(i);
   }
+  Freq FM;                             // every cluster below that holds i1 or i2 is within M
+  freq_over(this, st, M, -1, FM);
   int e;
   // sm:303-352 split_launch_state
   HState sl = st;
@@ -377,10 +421,14 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
     for (int q : S) sl.c[q] = ref[(int)(2 * rng.unif())];
   }
   hrecount(this, sl);
-  e = restricted_gibbs(this, S, sl, i1, i2, t);
+  Freq F1, F2;                         // tables of sl.c[i1], sl.c[i2]
+  freq_over(this, sl, M, sl.c[i1], F1);
+  freq_minus(FM, F1, F2);
+  e = restricted_gibbs(this, S, sl, i1, i2, t, F1, F2);
   if (e) { err = "split launch state failed"; return e; }
   e = hvalidate(sl);
   if (e) { err = "State validation failed: split_launch_state"; return e; }
+  const int n1_sl = F1.nn, n2_sl = F2.nn;
   // sm:354-391 merge_launch_state
   HState ml = st;
   if (ml.c[i1] != ml.c[i2]) {
@@ -393,7 +441,7 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
   e = clean_var(this, ml, ml);
   if (e) { err = "State validation failed: clean_var"; return e; }
   for (int iter = 0; iter < r; ++iter) {
-    e = hupdate_phi(this, ml, {ml.c[i2]});
+    e = hupdate_phi_one(this, ml, ml.c[i2], FM);
     if (e) { err = "update_phi failed"; return e; }
   }
   e = hvalidate(ml);
@@ -405,45 +453,48 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
   const double alpha = gamma;
   if (st.c[i1] == st.c[i2]) {
     ss = sl;
-    e = restricted_gibbs(this, S, ss, i1, i2, 1);
+    e = restricted_gibbs(this, S, ss, i1, i2, 1, F1, F2);    // F1, F2 now ss's tables
     if (e) { err = "restricted gibbs failed"; return e; }
-    // sm:438-487
+    // sm:438-487 (st.c[i1]'s members are all of M)
     double log_prior = 0.0, log_likelihood = 0.0, log_proposal = 0.0;
     log_prior += std::log(alpha);
-    log_prior += std::lgamma((double)csize(ss, ss.c[i1]));
-    log_prior += std::lgamma((double)csize(ss, ss.c[i2]));
+    log_prior += std::lgamma((double)F1.nn);
+    log_prior += std::lgamma((double)F2.nn);
     log_prior += priors(this, ss, ss.c[i1], &gerr);
     log_prior += priors(this, ss, ss.c[i2], &gerr);
-    log_prior -= std::lgamma((double)csize(st, st.c[i1]));
+    log_prior -= std::lgamma((double)FM.nn);
     log_prior -= priors(this, st, st.c[i1], &gerr);
-    log_likelihood += loglikelihood_hamming(this, ss, ss.c[i1]);
-    log_likelihood += loglikelihood_hamming(this, ss, ss.c[i2]);
-    log_likelihood -= loglikelihood_hamming(this, st, st.c[i1]);
-    log_proposal += logprobgs_phi(this, st, ml, i1, &gerr);
-    log_proposal -= logprobgs_phi(this, ss, sl, i1, &gerr);
-    log_proposal -= logprobgs_phi(this, ss, sl, i2, &gerr);
-    log_proposal -= logprobgs_c_i(this, ss, sl, S, i1, i2);
+    log_likelihood += loglikelihood_hamming(this, ss, ss.c[i1], F1);
+    log_likelihood += loglikelihood_hamming(this, ss, ss.c[i2], F2);
+    log_likelihood -= loglikelihood_hamming(this, st, st.c[i1], FM);
+    log_proposal += logprobgs_phi(this, st, ml, i1, FM, &gerr);
+    log_proposal -= logprobgs_phi(this, ss, sl, i1, F1, &gerr);
+    log_proposal -= logprobgs_phi(this, ss, sl, i2, F2, &gerr);
+    log_proposal -= logprobgs_c_i(this, ss, sl, S, i1, i2, n1_sl, n2_sl);
     acpt = min0(log_prior + log_likelihood + log_proposal);
   } else {
     ss = ml;
-    e = hupdate_phi(this, ss, {ss.c[i2]});
+    e = hupdate_phi_one(this, ss, ss.c[i2], FM);
     if (e) { err = "update_phi failed"; return e; }
-    // sm:489-540
+    // sm:489-540 (ss's merged cluster is M; st's two clusters split M)
+    Freq S1, S2;
+    freq_over(this, st, M, st.c[i1], S1);
+    freq_minus(FM, S1, S2);
     double log_prior = 0.0, log_likelihood = 0.0, log_proposal = 0.0;
-    log_prior += std::lgamma((double)csize(ss, ss.c[i1]));
+    log_prior += std::lgamma((double)FM.nn);
     log_prior += priors(this, ss, ss.c[i1], &gerr);
     log_prior -= std::log(alpha);
-    log_prior -= std::lgamma((double)csize(st, st.c[i1]));
-    log_prior -= std::lgamma((double)csize(st, st.c[i2]));
+    log_prior -= std::lgamma((double)S1.nn);
+    log_prior -= std::lgamma((double)S2.nn);
     log_prior -= priors(this, st, st.c[i1], &gerr);
     log_prior -= priors(this, st, st.c[i2], &gerr);
-    log_likelihood += loglikelihood_hamming(this, ss, ss.c[i2]);
-    log_likelihood -= loglikelihood_hamming(this, st, st.c[i1]);
-    log_likelihood -= loglikelihood_hamming(this, st, st.c[i2]);
-    log_proposal += logprobgs_phi(this, st, sl, i1, &gerr);
-    log_proposal += logprobgs_phi(this, st, sl, i2, &gerr);
-    log_proposal += logprobgs_c_i(this, st, sl, S, i1, i2);
-    log_proposal -= logprobgs_phi(this, ss, ml, i2, &gerr);
+    log_likelihood += loglikelihood_hamming(this, ss, ss.c[i2], FM);
+    log_likelihood -= loglikelihood_hamming(this, st, st.c[i1], S1);
+    log_likelihood -= loglikelihood_hamming(this, st, st.c[i2], S2);
+    log_proposal += logprobgs_phi(this, st, sl, i1, S1, &gerr);
+    log_proposal += logprobgs_phi(this, st, sl, i2, S2, &gerr);
+    log_proposal += logprobgs_c_i(this, st, sl, S, i1, i2, n1_sl, n2_sl);
+    log_proposal -= logprobgs_phi(this, ss, ml, i2, FM, &gerr);
     acpt = min0(log_prior + log_likelihood + log_proposal);
   }
   if (gerr) { err = "norm_const2 - hypergeometric diverging with infinity"; return gerr; }
@@ -465,9 +516,15 @@ int sm_restricted_gibbs_device(Ctx* c, const int32_t* S, int32_t nS, int32_t i1,
   if (!c->have_state) { c->err = "no state"; return kArg; }
   HState s;
   ctx_to_hstate(c, s);
-  std::vector<int> SS(S, S + nS);
-  int st = restricted_gibbs(c, SS, s, i1, i2, t);
+  std::vector<int> SS(S, S + nS), all(c->n);
+  for (int i = 0; i < c->n; ++i) all[i] = i;
+  Freq F1, F2;                         // the clusters may hold points outside S here
+  freq_over(c, s, all, s.c[i1], F1);
+  freq_over(c, s, all, s.c[i2], F2);
+  int st = restricted_gibbs(c, SS, s, i1, i2, t, F1, F2);
   if (st) { c->err = "restricted gibbs failed"; return st; }
+  st = hvalidate(s);
+  if (st) { c->err = "State validation failed: restricted gibbs"; return st; }
   hstate_to_ctx(c, s);
   return kOk;
 }
@@ -480,7 +537,9 @@ int sm_logprobgs_c_i_api(Ctx* c, const int32_t* g_c_i, const int32_t* S, int32_t
   g = gs;
   g.c.assign(g_c_i, g_c_i + c->n);
   std::vector<int> SS(S, S + nS);
-  *out = logprobgs_c_i(c, gs, g, SS, i1, i2);
+  int n1 = 0, n2 = 0;
+  for (int i = 0; i < c->n; ++i) { n1 += (g.c[i] == g.c[i1]); n2 += (g.c[i] == g.c[i2]); }
+  *out = logprobgs_c_i(c, gs, g, SS, i1, i2, n1, n2);
   return kOk;
 }
 

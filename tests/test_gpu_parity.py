@@ -563,3 +563,29 @@ def test_hig_logspace_chain_large_clusters(hd, oracle):
     assert np.array_equal(res["total_cls"], ref["total_cls"])
     assert np.array_equal(res["accepted"], ref["accepted"])
     np.testing.assert_allclose(res["loglikelihood"], ref["loglikelihood"], rtol=RTOL, atol=0)
+
+
+def test_restricted_gibbs_random_split_of_one_cluster(hd, oracle):
+    # The split proposal's launch state: one true cluster's members dealt at random to two
+    # labels with fresh parameters, so most scan draws are close calls whose pick depends
+    # on the running sizes (k_sm_scan's interval test and its serial walk both run).
+    ds = synth(9000, 24, 3, 2, seed=8)
+    c = ds.truth.astype(np.int32).copy()
+    K = 4
+    members = np.where(c == 0)[0]
+    rng = np.random.default_rng(5)
+    c[members[rng.random(len(members)) < 0.5]] = 3
+    i1 = int(members[c[members] == 0][0])
+    i2 = int(members[c[members] == 3][0])
+    cen, sig = random_params(ds, K, 13)
+    S = [i for i in range(ds.n) if i not in (i1, i2) and c[i] in (c[i1], c[i2])]
+    st = oracle.seed_state(47)
+    eng = make_engine(hd, ds)
+    eng.set_state(c, cen, sig)
+    eng.rng_state = st
+    eng.restricted_gibbs(S, i1, i2, t=6)
+    ost = oracle_state(oracle, c, cen, sig)
+    assert oracle.restricted_gibbs(ds.codes, ds.attrisize, ds.v, ds.w, S, ost, i1, i2, 6, st) == 0
+    assert_same_state(eng, ost)
+    assert np.array_equal(eng.rng_state, st)
+    eng.close()
