@@ -292,7 +292,9 @@ def main():
             "breakdown_ms_per_step": dict(
                 {"t_prepass_ms": round(pre_ms / launches * st["rounds"] / args.steps, 4)},
                 **{k: round(st[k] / args.steps, 4) for k in ("t_exact_ms", "t_resolve_ms") if st[k] > 0},
-                **{k: round(st[k] / args.steps, 4) for k in ("t_stats_ms", "t_host_phi_ms", "t_rng_ms", "t_loglik_ms")}),
+                **{k: round(st[k] / args.steps, 4) for k in ("t_stats_ms", "t_host_phi_ms", "t_rng_ms", "t_loglik_ms")},
+                **{k: round(st[k] / args.steps, 4) for k in ("t_sm_ms", "t_sm_scan_ms", "t_sm_phi_ms", "t_sm_terms_ms")
+                   if st["sm_moves"] > 0}),
             "exact_points_per_step": st["exact_points"] / args.steps,
             "listed_points_per_step": st["listed_points"] / args.steps,
             "split_merge": bool(args.sm),

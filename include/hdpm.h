@@ -63,6 +63,10 @@ typedef struct {
     int64_t rng_windows, rng_windows_fresh;
     /* points the prepass could not prove "stay" (exact rows built for them) */
     int64_t listed_points;
+    /* split-merge moves (sm:542-598): count, wall time, and its parts: restricted scans
+     * on the device (upload + kernels + wait), update_phi draws, acceptance terms */
+    int64_t sm_moves;
+    double  t_sm_ms, t_sm_scan_ms, t_sm_phi_ms, t_sm_terms_ms;
 } hdpm_stats;
 
 int         hdpm_device_count(void);

@@ -340,7 +340,23 @@ int orc_hyperg_2F1(double a, double b, double c, double x, double* val) {
 /* Extension (hdpm HDPM_OPT_HIG_LOGSPACE; not the reference): log 2F1.  The reference's
  * series first (a finite value keeps its bits through log); on overflow or maxiter the
  * positive series again with the partial sum rescaled by 2^-960 past 2^960, 10^7 terms. */
+static double log2f1_a1_upper(double A, double C, double x) {
+    /* 2F1(A, 1; C; x) = (C-1) x^(1-C) (1-x)^(C-A-1) B_x(C-1, A-C+1), upper-tail form */
+    double p = C - 1.0, q = A - C + 1.0;
+    double lbeta = lgamma(p) + lgamma(q) - lgamma(p + q);
+    double lt = q * log1p(-x) + p * log(x) - log(q) + log(betacf(q, p, 1.0 - x)) - lbeta;
+    return log(p) - p * log(x) - q * log1p(-x) + lbeta + log1p(-exp(lt));
+}
+
 int orc_log_hyperg_2F1(double a, double b, double c, double x, double* lval) {
+    double L = NAN;
+    if ((a == 1.0 || b == 1.0) && x > 0.0 && x < 1.0) {
+        double A = b == 1.0 ? a : b, p = c - 1.0, q = A - c + 1.0;
+        if (p > 0.0 && q > 0.0 && x >= (p + 1.0) / (p + q + 2.0)) {
+            L = log2f1_a1_upper(A, c, x);
+            if (L > 712.0) { *lval = L; return GSL_SUCCESS; }  /* the plain series overflows */
+        }
+    }
     double plain;
     int st = orc_hyperg_2F1(a, b, c, x, &plain);
     *lval = NAN;
@@ -349,6 +365,7 @@ int orc_log_hyperg_2F1(double a, double b, double c, double x, double* lval) {
         return st;
     }
     if (st != GSL_SUCCESS && st != GSL_EMAXITER) return st;
+    if (isfinite(L)) { *lval = L; return GSL_SUCCESS; }
     if (fabs(c - b) < LOC_EPS || fabs(c - a) < LOC_EPS) {
         *lval = (c - a - b) * log(1.0 - x);
         return GSL_SUCCESS;

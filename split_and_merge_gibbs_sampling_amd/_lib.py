@@ -54,7 +54,8 @@ class Stats(C.Structure):
         [(n, C.c_double) for n in (
             "t_pool_ms", "t_pool_mt_ms", "t_pool_accept_ms", "t_pool_parse_ms", "t_pool_values_ms")] + \
         [(n, C.c_int64) for n in ("phi_spec_runs", "phi_spec_clusters", "prepass_timed", "prepass_timed_points",
-                                  "rng_windows", "rng_windows_fresh", "listed_points")]
+                                  "rng_windows", "rng_windows_fresh", "listed_points", "sm_moves")] + \
+        [(n, C.c_double) for n in ("t_sm_ms", "t_sm_scan_ms", "t_sm_phi_ms", "t_sm_terms_ms")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

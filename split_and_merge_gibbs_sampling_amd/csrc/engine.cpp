@@ -2669,7 +2669,10 @@ int Ctx::iteration(const hdpm_chain_params* p, int iter, int* idx_1_sm, int* acc
     if (st) return st;
   }
   if (p->split_merge && iter % p->sam_step_size == 0) {  // la:111-115
+    const auto t0 = std::chrono::steady_clock::now();
     st = split_and_merge(p->t, p->r, *idx_1_sm, accepted);
+    stats.t_sm_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    stats.sm_moves++;
     if (st) return st;
     *idx_1_sm = (*idx_1_sm + 1) % n;
   }

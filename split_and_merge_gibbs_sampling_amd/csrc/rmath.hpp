@@ -577,8 +577,33 @@ inline int hyperg_2F1(double a, double b, double c, double x, double* val) {
 // When it overflows (clusters of ~1.4k+ members) or runs out of its 30000
 // terms, the same positive series is summed again with the partial sum rescaled by 2^-960
 // whenever it passes 2^960, for up to 10^7 terms.  Statuses as hyperg_2F1.
+//
+// The HIG constants only take 2F1(A, 1; C; x) = (C-1) x^(1-C) (1-x)^(C-A-1) B_x(C-1, A-C+1)
+// (DLMF 15.4 / 8.17), and in the upper tail of the incomplete beta its log has the closed
+// form log2f1_a1_upper below (lgamma and the continued fraction of pbeta, ~1e-15 relative).
+// Where that puts log 2F1 above 712 the plain series would overflow (log DBL_MAX = 709.78)
+// after summing up to ~5 A terms, so the closed form is returned without it.
+inline double log2f1_a1_upper(double A, double C, double x) {
+  const double p = C - 1.0, q = A - C + 1.0;
+  // log B_x(p, q) = lbeta(p, q) + log1p(-I_{1-x}(q, p))
+  const double lbeta = std::lgamma(p) + std::lgamma(q) - std::lgamma(p + q);
+  const double lt = q * std::log1p(-x) + p * std::log(x) - std::log(q) + std::log(detail::betacf(q, p, 1.0 - x)) - lbeta;
+  return std::log(p) - p * std::log(x) - q * std::log1p(-x) + lbeta + std::log1p(-std::exp(lt));
+}
+
 inline int log_hyperg_2F1(double a, double b, double c, double x, double* lval) {
   const double eps = 2.2204460492503131e-16, loc_eps = 1000.0 * eps;
+  double L = NAN;
+  if ((a == 1.0 || b == 1.0) && x > 0.0 && x < 1.0) {
+    const double A = b == 1.0 ? a : b, p = c - 1.0, q = A - c + 1.0;
+    if (p > 0.0 && q > 0.0 && x >= (p + 1.0) / (p + q + 2.0)) {
+      L = log2f1_a1_upper(A, c, x);
+      if (L > 712.0) {
+        *lval = L;
+        return GSL_SUCCESS;
+      }
+    }
+  }
   double plain;
   const int st = hyperg_2F1(a, b, c, x, &plain);
   *lval = NAN;
@@ -587,6 +612,10 @@ inline int log_hyperg_2F1(double a, double b, double c, double x, double* lval) 
     return st;
   }
   if (st != GSL_SUCCESS && st != GSL_EMAXITER) return st;
+  if (std::isfinite(L)) {
+    *lval = L;
+    return GSL_SUCCESS;
+  }
   if (std::fabs(c - b) < loc_eps || std::fabs(c - a) < loc_eps) {
     *lval = (c - a - b) * std::log(1.0 - x);       // exp() overflowed in the plain path
     return GSL_SUCCESS;

@@ -58,6 +58,14 @@ static void row_tables(const Ctx* c, const uint8_t* cen, const double* sig, std:
   (void)cen;
 }
 
+// Adds the wall time of its scope to a stats field.
+struct SmTimer {
+  double& acc;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  explicit SmTimer(double& a) : acc(a) {}
+  ~SmTimer() { acc += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
+};
+
 // Frequency tables of one cluster (f[j * mmax + l] = members with code l + 1 at attribute j,
 // integer-valued doubles) and its size.  The split-merge move touches only the members M =
 // S + {i1, i2} of c(i1) and c(i2) (sm:263-301), so every table it needs is a subset of M's;
@@ -109,6 +117,7 @@ static void freq_minus(const Freq& A, const Freq& B, Freq& out) {
 // update_phi (cf:511-591) of one cluster k of s whose table is F.
 static int hupdate_phi_one(Ctx* c, HState& s, int k, const Freq& F) {
   if (F.nn == 0) return kOk;
+  SmTimer tm(c->stats.t_sm_phi_ms);
   std::vector<double> prob(c->mmax), nv(c->d), nw(c->d);
   const double nn = (double)F.nn;
   uint8_t* cen = &s.center[(size_t)k * c->d];
@@ -192,6 +201,7 @@ static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1
   for (int iter = 0; iter < t; ++iter) {
     c->rng.raw_block(raw.data(), nS);
     if (nS) {
+      SmTimer tm(c->stats.t_sm_scan_ms);
       prev = side;
       sm_upload_two(c, W, s, c1, c2);
       HIPCHK(hipMemcpyAsync(W.d_side.p, side.data(), (size_t)nS * 4, hipMemcpyHostToDevice, c->stream));
@@ -456,6 +466,7 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
     e = restricted_gibbs(this, S, ss, i1, i2, 1, F1, F2);    // F1, F2 now ss's tables
     if (e) { err = "restricted gibbs failed"; return e; }
     // sm:438-487 (st.c[i1]'s members are all of M)
+    SmTimer tm(stats.t_sm_terms_ms);
     double log_prior = 0.0, log_likelihood = 0.0, log_proposal = 0.0;
     log_prior += std::log(alpha);
     log_prior += std::lgamma((double)F1.nn);
@@ -477,6 +488,7 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
     e = hupdate_phi_one(this, ss, ss.c[i2], FM);
     if (e) { err = "update_phi failed"; return e; }
     // sm:489-540 (ss's merged cluster is M; st's two clusters split M)
+    SmTimer tm(stats.t_sm_terms_ms);
     Freq S1, S2;
     freq_over(this, st, M, st.c[i1], S1);
     freq_minus(FM, S1, S2);
