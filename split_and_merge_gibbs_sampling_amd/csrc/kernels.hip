@@ -1758,6 +1758,42 @@ __global__ __launch_bounds__(kBlock) void k_sm_ll(SmArgs a) {
   a.ll[a.nS + q] = ll_uniform<0>(x, a.d, a.two.codes + dp, a.two.tab + 2 * a.d);
 }
 
+// k_sm_ll with both clusters' tables and codes staged in LDS and the two attribute-order
+// sums interleaved (two independent dependency chains per lane); 64-lane workgroups so a
+// scan of ~10^4 points spreads over the CUs.
+constexpr int kSmLLBlock = 64;
+__global__ __launch_bounds__(kSmLLBlock) void k_sm_ll_lds(SmArgs a) {
+  extern __shared__ double sm_lds[];
+  const int d = a.d, dp = a.nq * 16;
+  double* tab = sm_lds;                                    // [2][d][2]
+  uint8_t* cc = (uint8_t*)(sm_lds + 4 * d);                // [2][dp]
+  for (int t = threadIdx.x; t < 4 * d; t += kSmLLBlock) tab[t] = a.two.tab[t];
+  for (int t = threadIdx.x; t < 2 * dp / 16; t += kSmLLBlock) ((uint4*)cc)[t] = ((const uint4*)a.two.codes)[t];
+  __syncthreads();
+  const int q = blockIdx.x * kSmLLBlock + threadIdx.x;
+  if (q >= a.nS) return;
+  const int64_t i = a.S[q];
+  const double* t0 = tab;
+  const double* t1 = tab + 2 * d;
+  double l0 = 0.0, l1 = 0.0;
+  for (int qq = 0; qq < a.nq; ++qq) {
+    const uint4 xq = *(const uint4*)(a.codes_t + tiled_offset(i, qq * 16, a.nq));
+    const uint4 c0 = ((const uint4*)cc)[qq], c1 = ((const uint4*)(cc + dp))[qq];
+    const uint4 dx0 = make_uint4(xq.x ^ c0.x, xq.y ^ c0.y, xq.z ^ c0.z, xq.w ^ c0.w);
+    const uint4 dx1 = make_uint4(xq.x ^ c1.x, xq.y ^ c1.y, xq.z ^ c1.z, xq.w ^ c1.w);
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      const int j = qq * 16 + b;
+      if (j < d) {
+        l0 += t0[2 * j + (byte_differs(dx0, b) ? 1 : 0)];
+        l1 += t1[2 * j + (byte_differs(dx1, b) ? 1 : 0)];
+      }
+    }
+  }
+  a.ll[q] = l0;
+  a.ll[a.nS + q] = l1;
+}
+
 // Exact sm:204-215 two-way draw.  probs[k] = log(n_k) + H_k; normalise; FixupProb;
 // revsort of two entries (ties: second first); cumulative compare.
 __device__ __forceinline__ void two_way_probs(double v0, double v1, double& p0, double& p1) {
@@ -1794,30 +1830,47 @@ __device__ __forceinline__ int two_way_draw(double v0, double v1, double rU) {
 // exact draw at both ends of its range; when no threshold lies within 1e-9 of [p0(lo),
 // p0(hi)] (rounding moves p0 by far less) its pick is the same for every count it can see
 // and it is settled in parallel.  The others are walked one by one with their exact counts.
+// logn[0 .. n1 + n2] is staged in LDS when it fits (the walk's count-dependent lookups then
+// cost an LDS read instead of an L2 round trip), and each batch's inputs are loaded one
+// batch ahead.
+template <bool kLdsLogn>
 __global__ __launch_bounds__(kWave) void k_sm_scan(SmArgs a, double T) {
   (void)T;
+  extern __shared__ double scan_lds[];
   const int lane = threadIdx.x;
   int n1 = a.n1, n2 = a.n2;
   const int tot = n1 + n2;
+  const double* logn = a.logn;
+  if constexpr (kLdsLogn) {
+    for (int t = lane; t <= tot; t += kWave) scan_lds[t] = a.logn[t];
+    __syncthreads();
+    logn = scan_lds;
+  }
   const double margin = 1e-9;
+  int nx_cur = 0;
+  double nx_l0 = 0.0, nx_l1 = 0.0;
+  uint32_t nx_raw = 0;
+  if (lane < a.nS) { nx_cur = a.side[lane]; nx_l0 = a.ll[lane]; nx_l1 = a.ll[a.nS + lane]; nx_raw = a.raw[lane]; }
   for (int base = 0; base < a.nS; base += kWave) {
     const int q = base + lane;
     const bool act = q < a.nS;
-    int cur = act ? a.side[q] : 0;
-    const double l0 = act ? a.ll[q] : 0.0, l1 = act ? a.ll[a.nS + q] : 0.0;
-    const double rU = act ? raw_to_unif(a.raw[q]) : 0.0;
+    int cur = nx_cur;
+    const double l0 = nx_l0, l1 = nx_l1;
+    const double rU = act ? raw_to_unif(nx_raw) : 0.0;
+    const int qn = q + kWave;
+    if (qn < a.nS) { nx_cur = a.side[qn]; nx_l0 = a.ll[qn]; nx_l1 = a.ll[a.nS + qn]; nx_raw = a.raw[qn]; }
     bool certain = false;
     int choice = cur;
     if (act) {
       // n1 as lane `lane` may see it, within the sizes the clusters can take
       const int lo = max(n1 - lane, 1 + (cur == 0)), hi = min(n1 + lane, tot - 1 - (cur == 1));
       double pa0, pa1, pb0, pb1;
-      two_way_probs(a.logn[lo - (cur == 0)] + l0, a.logn[tot - lo - (cur == 1)] + l1, pa0, pa1);
+      two_way_probs(logn[lo - (cur == 0)] + l0, logn[tot - lo - (cur == 1)] + l1, pa0, pa1);
       const int pick = two_way_pick(pa0, pa1, rU);
       if (lo == hi) {
         certain = true;
       } else {
-        two_way_probs(a.logn[hi - (cur == 0)] + l0, a.logn[tot - hi - (cur == 1)] + l1, pb0, pb1);
+        two_way_probs(logn[hi - (cur == 0)] + l0, logn[tot - hi - (cur == 1)] + l1, pb0, pb1);
         const double pmin = fmin(pa0, pb0) - margin, pmax = fmax(pa0, pb0) + margin;
         const double onem = 1.0 - rU;
         certain = !(pmin <= 0.5 && 0.5 <= pmax) && !(pmin <= rU && rU <= pmax) && !(pmin <= onem && onem <= pmax);
@@ -1837,7 +1890,7 @@ __global__ __launch_bounds__(kWave) void k_sm_scan(SmArgs a, double T) {
       int pick = 0;
       if (lane == u) {
         const int nz1 = cn1 - (cur == 0), nz2 = cn2 - (cur == 1);
-        const double v0 = a.logn[nz1] + l0, v1 = a.logn[nz2] + l1;
+        const double v0 = logn[nz1] + l0, v1 = logn[nz2] + l1;
         pick = two_way_draw(v0, v1, rU);
         choice = pick;
       }
@@ -1899,11 +1952,20 @@ __global__ __launch_bounds__(kBlock) void k_sm_lpgs(SmArgs a) {
 
 hipError_t launch_sm_ll(const SmArgs& a, hipStream_t s) {
   if (a.nS == 0) return hipSuccess;
+  const size_t lds = (size_t)4 * a.d * 8 + (size_t)2 * a.nq * 16;
+  if (lds <= 64 * 1024) {
+    hipLaunchKernelGGL(k_sm_ll_lds, dim3((a.nS + kSmLLBlock - 1) / kSmLLBlock), dim3(kSmLLBlock), lds, s, a);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_sm_ll, dim3((a.nS + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_sm_scan(const SmArgs& a, double T, hipStream_t s) {
-  hipLaunchKernelGGL(k_sm_scan, dim3(1), dim3(kWave), 0, s, a, T);
+  const size_t lds = (size_t)(a.n1 + a.n2 + 1) * 8;
+  if (lds <= 160 * 1024)
+    hipLaunchKernelGGL(k_sm_scan<true>, dim3(1), dim3(kWave), lds, s, a, T);
+  else
+    hipLaunchKernelGGL(k_sm_scan<false>, dim3(1), dim3(kWave), 0, s, a, T);
   return hipGetLastError();
 }
 hipError_t launch_sm_lpgs(const SmArgs& a, hipStream_t s) {

@@ -77,13 +77,6 @@ struct Freq {
   int nn = 0;
 };
 
-static void freq_add_row(const Ctx* c, Freq& F, int i, double sgn) {
-  const uint8_t* x = &c->codes[(size_t)i * c->d];
-  double* f = F.f.data();
-  for (int j = 0; j < c->d; ++j) f[(size_t)j * c->mmax + (x[j] - 1)] += sgn;
-  F.nn += sgn > 0 ? 1 : -1;
-}
-
 // Table of the members q of M with s.c[q] == k (k < 0: all of M); attribute ranges on the
 // host pool for wide rows.
 static void freq_over(const Ctx* c, const HState& s, const std::vector<int>& M, int k, Freq& F) {
@@ -106,6 +99,39 @@ static void freq_over(const Ctx* c, const HState& s, const std::vector<int>& M, 
   };
   if (work >= (1 << 18) && nchunk > 1) pool_for(nchunk, run, 1);
   else for (int ch = 0; ch < nchunk; ++ch) run(ch);
+}
+
+// Rows `to1` move from F2 to F1 and rows `to2` from F1 to F2 (attribute ranges on the host
+// pool when there are many).
+static void freq_move(const Ctx* c, Freq& F1, Freq& F2, const std::vector<int>& to1, const std::vector<int>& to2) {
+  const int64_t work = (int64_t)(to1.size() + to2.size()) * c->d;
+  const int chunk = 32;
+  const int nchunk = (c->d + chunk - 1) / chunk;
+  auto run = [&](int ch) {
+    const int j0 = ch * chunk, j1 = std::min(c->d, j0 + chunk);
+    double* f1 = F1.f.data();
+    double* f2 = F2.f.data();
+    for (int i : to1) {
+      const uint8_t* x = &c->codes[(size_t)i * c->d];
+      for (int j = j0; j < j1; ++j) {
+        const size_t o = (size_t)j * c->mmax + (x[j] - 1);
+        f1[o] += 1.0;
+        f2[o] -= 1.0;
+      }
+    }
+    for (int i : to2) {
+      const uint8_t* x = &c->codes[(size_t)i * c->d];
+      for (int j = j0; j < j1; ++j) {
+        const size_t o = (size_t)j * c->mmax + (x[j] - 1);
+        f2[o] += 1.0;
+        f1[o] -= 1.0;
+      }
+    }
+  };
+  if (work >= (1 << 18) && nchunk > 1) pool_for(nchunk, run, 1);
+  else for (int ch = 0; ch < nchunk; ++ch) run(ch);
+  F1.nn += (int)to1.size() - (int)to2.size();
+  F2.nn += (int)to2.size() - (int)to1.size();
 }
 
 static void freq_minus(const Freq& A, const Freq& B, Freq& out) {
@@ -194,13 +220,15 @@ static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1
   const int c1 = s.c[i1], c2 = s.c[i2];
   const int nS = (int)S.size();
   sm_upload_S(c, W, S);
-  std::vector<int> side(nS), prev(nS);
+  std::vector<int> side(nS), prev(nS), to1, to2;
   std::vector<uint32_t> raw(nS);
   const double T = 54.0 * M_LN2 + std::log(2.0) + 0.5;
   for (int q = 0; q < nS; ++q) side[q] = (s.c[S[q]] == c1) ? 0 : 1;
   for (int iter = 0; iter < t; ++iter) {
     c->rng.raw_block(raw.data(), nS);
-    if (nS) {
+    // c1 == c2 (only through the C ABI): every draw picks the same label, so only the
+    // draws are consumed
+    if (nS && c1 != c2) {
       SmTimer tm(c->stats.t_sm_scan_ms);
       prev = side;
       sm_upload_two(c, W, s, c1, c2);
@@ -212,13 +240,15 @@ static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1
       HIPCHK(launch_sm_scan(a, T, c->stream));
       HIPCHK(hipMemcpyAsync(side.data(), W.d_side.p, (size_t)nS * 4, hipMemcpyDeviceToHost, c->stream));
       HIPCHK(hipStreamSynchronize(c->stream));
+      to1.clear();
+      to2.clear();
       for (int q = 0; q < nS; ++q) {
-        if (side[q] == prev[q] || c1 == c2) continue;
+        if (side[q] == prev[q]) continue;
         const int i = S[q];
         s.c[i] = side[q] == 0 ? c1 : c2;
-        freq_add_row(c, side[q] == 0 ? F1 : F2, i, 1.0);
-        freq_add_row(c, side[q] == 0 ? F2 : F1, i, -1.0);
+        (side[q] == 0 ? to1 : to2).push_back(i);
       }
+      freq_move(c, F1, F2, to1, to2);
     }
     s.counts[c1] = F1.nn;
     s.counts[c2] = F2.nn;
