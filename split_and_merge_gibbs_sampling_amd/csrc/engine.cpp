@@ -1126,6 +1126,36 @@ struct Ctx {
     }
     return kOk;
   }
+  // sample_sigma with the per-attribute branch tests (hg:359, the qbeta) and rbeta constants
+  // evaluated on the host pool first; the draws stay in attribute order on this thread, so
+  // the stream and the values are sample_sigma's.  For wide rows (split-merge at large D).
+  int sample_sigma_wide(const double* vv, const double* ww, double* out) {
+    if (d < 128) return sample_sigma(vv, ww, out);
+    rng_sync();
+    std::vector<char> bp(d);
+    std::vector<RBeta> setup(d);
+    pool_for(d, [&](int j) {
+      const double mj = (double)att[j];
+      bp[j] = rhig_beta_path(vv[j], ww[j], mj);
+      if (bp[j]) setup[j] = rbeta_setup(ww[j] + 1, vv[j] - 1);
+    }, 16);
+    for (int j = 0; j < d; ++j) {
+      const double m = (double)att[j];
+      double u;
+      if (bp[j]) {                                   // hg:359-366
+        double x = rbeta_draw(rng, setup[j]);
+        while (x > (m - 1) / m) x = rbeta_draw(rng, setup[j]);
+        u = x / ((m - 1) * (1 - x));
+      } else {                                       // hg:367-371
+        int e = kOk;
+        const double Omega = rng.unif();
+        u = bisec_hyper2(ww[j], vv[j], m, Omega, &e, hig_log);
+        if (e) return e;
+      }
+      out[j] = -1 / std::log(u);
+    }
+    return kOk;
+  }
   // sample_center_1_cluster without probabilities (cf:198-199)
   void sample_center_uniform(uint8_t* out) {
     rng_sync();

@@ -20,6 +20,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include <math.h>  // lgamma_r
+
 namespace hdpm {
 
 enum Status : int {
@@ -486,6 +488,12 @@ struct StreamAhead {
 inline double rbeta(Rng& rng, double aa, double bb) { return rbeta_draw(rng, rbeta_setup(aa, bb)); }
 
 // ------------------------------------------------------------------ qbeta branch test
+// lgamma without the global signgam write (the host pool evaluates these concurrently)
+inline double lgam(double x) {
+  int sg;
+  return ::lgamma_r(x, &sg);
+}
+
 namespace detail {
 inline double betacf(double a, double b, double x) {
   const double FPMIN = 1e-300, EPS = 1e-16;
@@ -514,7 +522,7 @@ inline double betacf(double a, double b, double x) {
 inline double pbeta(double x, double a, double b) {
   if (x <= 0.0) return 0.0;
   if (x >= 1.0) return 1.0;
-  double lbt = std::lgamma(a + b) - std::lgamma(a) - std::lgamma(b) + a * std::log(x) +
+  double lbt = lgam(a + b) - lgam(a) - lgam(b) + a * std::log(x) +
                b * std::log1p(-x);
   if (x < (a + 1.0) / (a + b + 2.0)) return std::exp(lbt) * detail::betacf(a, b, x) / a;
   return 1.0 - std::exp(lbt) * detail::betacf(b, a, 1.0 - x) / b;
@@ -586,7 +594,7 @@ inline int hyperg_2F1(double a, double b, double c, double x, double* val) {
 inline double log2f1_a1_upper(double A, double C, double x) {
   const double p = C - 1.0, q = A - C + 1.0;
   // log B_x(p, q) = lbeta(p, q) + log1p(-I_{1-x}(q, p))
-  const double lbeta = std::lgamma(p) + std::lgamma(q) - std::lgamma(p + q);
+  const double lbeta = lgam(p) + lgam(q) - lgam(p + q);
   const double lt = q * std::log1p(-x) + p * std::log(x) - std::log(q) + std::log(detail::betacf(q, p, 1.0 - x)) - lbeta;
   return std::log(p) - p * std::log(x) - q * std::log1p(-x) + lbeta + std::log1p(-std::exp(lt));
 }

@@ -141,25 +141,38 @@ static void freq_minus(const Freq& A, const Freq& B, Freq& out) {
 }
 
 // update_phi (cf:511-591) of one cluster k of s whose table is F.
+// The center probabilities of every attribute are computed first (on the host pool for wide
+// rows; each attribute's values come from the same expressions), then drawn in attribute
+// order, then the sigmas (Ctx::sample_sigma_wide).
 static int hupdate_phi_one(Ctx* c, HState& s, int k, const Freq& F) {
   if (F.nn == 0) return kOk;
   SmTimer tm(c->stats.t_sm_phi_ms);
-  std::vector<double> prob(c->mmax), nv(c->d), nw(c->d);
+  const int mm = c->mmax;
+  std::vector<double> prob((size_t)c->d * mm), cum((size_t)c->d * mm), nv(c->d), nw(c->d);
+  std::vector<int> perm((size_t)c->d * mm), pst(c->d);
   const double nn = (double)F.nn;
   uint8_t* cen = &s.center[(size_t)k * c->d];
   double* sig = &s.sigma[(size_t)k * c->d];
-  for (int j = 0; j < c->d; ++j) {
+  auto probs = [&](int j) {    // cf:496-503
     const int mj = c->att[j];
-    const double* f = &F.f[(size_t)j * c->mmax];
-    for (int l = 0; l < mj; ++l) prob[l] = (-(nn - f[l])) / sig[j];
-    double mx = prob[0];
-    for (int l = 1; l < mj; ++l) if (prob[l] > mx) mx = prob[l];
-    for (int l = 0; l < mj; ++l) prob[l] = std::exp(prob[l] - mx);
+    const double* f = &F.f[(size_t)j * mm];
+    double* pr = &prob[(size_t)j * mm];
+    for (int l = 0; l < mj; ++l) pr[l] = (-(nn - f[l])) / sig[j];
+    double mx = pr[0];
+    for (int l = 1; l < mj; ++l) if (pr[l] > mx) mx = pr[l];
+    for (int l = 0; l < mj; ++l) pr[l] = std::exp(pr[l] - mx);
     double sum = 0.0;
-    for (int l = 0; l < mj; ++l) sum += prob[l];
-    for (int l = 0; l < mj; ++l) prob[l] = prob[l] / sum;
-    int pick = sample_prob1(c->rng, prob.data(), mj, c->sp, c->sperm);
-    if (pick < 0) return -pick;
+    for (int l = 0; l < mj; ++l) sum += pr[l];
+    for (int l = 0; l < mj; ++l) pr[l] = pr[l] / sum;
+    // sample(1:m_j, 1, TRUE, prob) up to its uniform: FixupProb, revsort, cumulative sums
+    pst[j] = sample_prob1_prep(pr, mj, &cum[(size_t)j * mm], &perm[(size_t)j * mm]);
+  };
+  if (c->d >= 128) pool_for(c->d, probs, 16);
+  else for (int j = 0; j < c->d; ++j) probs(j);
+  c->rng_sync();
+  for (int j = 0; j < c->d; ++j) {
+    if (pst[j] < 0) return -pst[j];           // validation precedes the draw
+    const int pick = sample_prob1_pick(&cum[(size_t)j * mm], &perm[(size_t)j * mm], c->att[j], c->rng.unif());
     cen[j] = (uint8_t)(pick + 1);
   }
   for (int j = 0; j < c->d; ++j) {
@@ -167,7 +180,7 @@ static int hupdate_phi_one(Ctx* c, HState& s, int k, const Freq& F) {
     nw[j] = c->w[j] + nn - sumdelta;
     nv[j] = c->v[j] + sumdelta;
   }
-  return c->sample_sigma(nv.data(), nw.data(), sig);
+  return c->sample_sigma_wide(nv.data(), nw.data(), sig);
 }
 
 static void hrecount(const Ctx* c, HState& s) {
@@ -304,6 +317,13 @@ static double logdensity_hig(double sigmaj, double vv, double ww, double m, int*
 }
 
 // sm:20-94
+// Per-attribute terms on the host pool for wide rows; the sums keep attribute order.
+template <class F>
+static void per_attribute(const Ctx* c, F f) {
+  if (c->d >= 128) pool_for(c->d, f, 16);
+  else for (int j = 0; j < c->d; ++j) f(j);
+}
+
 // F: the table of gs's cluster c(idx).
 static double logprobgs_phi(Ctx* c, const HState& gs, const HState& g, int idx, const Freq& F, int* err) {
   const int k = gs.c[idx];
@@ -311,10 +331,12 @@ static double logprobgs_phi(Ctx* c, const HState& gs, const HState& g, int idx, 
   const int nm = F.nn;
   const double* gsig = &g.sigma[(size_t)g.c[idx] * c->d];
   const uint8_t* cstar = &gs.center[(size_t)k * c->d];
-  double log_center_prob = 0;
-  std::vector<double> z(c->mmax);
-  for (int j = 0; j < c->d; ++j) {
+  const double* gss = &gs.sigma[(size_t)k * c->d];
+  std::vector<double> lc(c->d), ls(c->d);
+  std::vector<int> er(c->d, 0);
+  per_attribute(c, [&](int j) {
     const int mj = c->att[j];
+    double z[256];
     for (int l = 0; l < mj; ++l) z[l] = (-((double)nm - f[(size_t)j * c->mmax + l])) / gsig[j];
     double mx = z[0];
     for (int l = 1; l < mj; ++l) if (z[l] > mx) mx = z[l];
@@ -322,15 +344,19 @@ static double logprobgs_phi(Ctx* c, const HState& gs, const HState& g, int idx, 
     double sum = 0.0;
     for (int l = 0; l < mj; ++l) sum += z[l];
     for (int l = 0; l < mj; ++l) z[l] = z[l] / sum;
-    log_center_prob += std::log(z[cstar[j] - 1]);
-  }
-  double log_sigma_prob = 0;
-  const double* gss = &gs.sigma[(size_t)k * c->d];
-  for (int j = 0; j < c->d; ++j) {
+    lc[j] = std::log(z[cstar[j] - 1]);
     const double sumdelta = f[(size_t)j * c->mmax + (cstar[j] - 1)];
     const double new_v = c->v[j] + sumdelta;
     const double new_w = c->w[j] + nm - sumdelta;
-    log_sigma_prob += logdensity_hig(gss[j], new_v, new_w, c->att[j], err, c->hig_log);
+    int e = 0;
+    ls[j] = logdensity_hig(gss[j], new_v, new_w, c->att[j], &e, c->hig_log);
+    er[j] = e;
+  });
+  double log_center_prob = 0, log_sigma_prob = 0;
+  for (int j = 0; j < c->d; ++j) log_center_prob += lc[j];
+  for (int j = 0; j < c->d; ++j) {
+    log_sigma_prob += ls[j];
+    if (er[j]) *err = er[j];
   }
   return log_center_prob + log_sigma_prob;
 }
@@ -360,10 +386,18 @@ static double loglikelihood_hamming(Ctx* c, const HState& s, int k, const Freq& 
 // sm:419-436
 static double priors(Ctx* c, const HState& s, int k, int* err) {
   const double* sig = &s.sigma[(size_t)k * c->d];
+  std::vector<double> ld(c->d);
+  std::vector<int> er(c->d, 0);
+  per_attribute(c, [&](int j) {
+    int e = 0;
+    ld[j] = logdensity_hig(sig[j], c->v[j], c->w[j], c->att[j], &e, c->hig_log);
+    er[j] = e;
+  });
   double priorg = 0;
   for (int j = 0; j < c->d; ++j) {
     priorg -= std::log((double)c->att[j]);
-    priorg += logdensity_hig(sig[j], c->v[j], c->w[j], c->att[j], err, c->hig_log);
+    priorg += ld[j];
+    if (er[j]) *err = er[j];
   }
   return priorg;
 }
