@@ -245,7 +245,8 @@ static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1
       SmTimer tm(c->stats.t_sm_scan_ms);
       prev = side;
       sm_upload_two(c, W, s, c1, c2);
-      HIPCHK(hipMemcpyAsync(W.d_side.p, side.data(), (size_t)nS * 4, hipMemcpyHostToDevice, c->stream));
+      // later scans start from the sides the previous scan left on the device
+      if (iter == 0) HIPCHK(hipMemcpyAsync(W.d_side.p, side.data(), (size_t)nS * 4, hipMemcpyHostToDevice, c->stream));
       HIPCHK(hipMemcpyAsync(W.d_raw.p, raw.data(), (size_t)nS * 4, hipMemcpyHostToDevice, c->stream));
       SmArgs a = sm_args(c, W, nS);
       a.n1 = F1.nn; a.n2 = F2.nn;
