@@ -1824,15 +1824,15 @@ __device__ __forceinline__ int two_way_draw(double v0, double v1, double rU) {
 }
 
 // One wave walks S in batches of 64 in order.  Within a batch the size n1 of c1 seen by
-// lane p lies in [n1 - p, n1 + p] (n1 + n2 is fixed: points only change sides).  p0 of the
-// draw is monotone in n1 in exact arithmetic, and the pick only changes where p0 crosses
-// 1/2 (the revsort order), rU or 1 - rU (sm:215 with revsort).  So a lane evaluates the
-// exact draw at both ends of its range; when no threshold lies within 1e-9 of [p0(lo),
-// p0(hi)] (rounding moves p0 by far less) its pick is the same for every count it can see
-// and it is settled in parallel.  The others are walked one by one with their exact counts.
-// logn[0 .. n1 + n2] is staged in LDS when it fits (the walk's count-dependent lookups then
-// cost an LDS read instead of an L2 round trip), and each batch's inputs are loaded one
-// batch ahead.
+// lane p lies in [n1 - p, n1 + p] (n1 + n2 is fixed: points only change sides).  The draw's
+// p0 is a function of D = v0 - v1 alone (one of the two exps is exp(0)), D is monotone in
+// n1 (logn is increasing, rounding is monotone), and in exact arithmetic the pick is
+// "0 iff (D > 0 and D >= lam) or (D <= 0 and D > -lam)" with lam = log(rU / (1 - rU)): it
+// only changes where D crosses 0 (the revsort order), lam or -lam.  A lane whose D range
+// stays 1e-4 away from all three (there p0 is >= 2e-15 from its threshold, far beyond the
+// few-ulp rounding of the exp and divisions) has one pick for every count it can see and is
+// settled in parallel without evaluating the draw; the others are drawn one by one with
+// their exact counts.
 template <bool kLdsLogn>
 __global__ __launch_bounds__(kWave) void k_sm_scan(SmArgs a, double T) {
   (void)T;
@@ -1846,7 +1846,7 @@ __global__ __launch_bounds__(kWave) void k_sm_scan(SmArgs a, double T) {
     __syncthreads();
     logn = scan_lds;
   }
-  const double margin = 1e-9;
+  const double margin = 1e-4;
   int nx_cur = 0;
   double nx_l0 = 0.0, nx_l1 = 0.0;
   uint32_t nx_raw = 0;
@@ -1864,18 +1864,12 @@ __global__ __launch_bounds__(kWave) void k_sm_scan(SmArgs a, double T) {
     if (act) {
       // n1 as lane `lane` may see it, within the sizes the clusters can take
       const int lo = max(n1 - lane, 1 + (cur == 0)), hi = min(n1 + lane, tot - 1 - (cur == 1));
-      double pa0, pa1, pb0, pb1;
-      two_way_probs(logn[lo - (cur == 0)] + l0, logn[tot - lo - (cur == 1)] + l1, pa0, pa1);
-      const int pick = two_way_pick(pa0, pa1, rU);
-      if (lo == hi) {
-        certain = true;
-      } else {
-        two_way_probs(logn[hi - (cur == 0)] + l0, logn[tot - hi - (cur == 1)] + l1, pb0, pb1);
-        const double pmin = fmin(pa0, pb0) - margin, pmax = fmax(pa0, pb0) + margin;
-        const double onem = 1.0 - rU;
-        certain = !(pmin <= 0.5 && 0.5 <= pmax) && !(pmin <= rU && rU <= pmax) && !(pmin <= onem && onem <= pmax);
-      }
-      if (certain) choice = pick;
+      const double dlo = (logn[lo - (cur == 0)] + l0) - (logn[tot - lo - (cur == 1)] + l1);
+      const double dhi = (logn[hi - (cur == 0)] + l0) - (logn[tot - hi - (cur == 1)] + l1);
+      const double lam = log(rU / (1.0 - rU));
+      const double a0 = fmin(dlo, dhi) - margin, a1 = fmax(dlo, dhi) + margin;
+      certain = !(a0 <= 0.0 && 0.0 <= a1) && !(a0 <= lam && lam <= a1) && !(a0 <= -lam && -lam <= a1);
+      if (certain) choice = ((dlo > 0.0 && dlo >= lam) || (dlo <= 0.0 && dlo > -lam)) ? 0 : 1;
     }
     unsigned long long unc = __ballot(act && !certain);
     const unsigned long long mv01 = __ballot(act && certain && cur == 0 && choice == 1);
