@@ -1776,17 +1776,36 @@ __global__ __launch_bounds__(kSmLLBlock) void k_sm_ll_lds(SmArgs a) {
   const double* t0 = tab;
   const double* t1 = tab + 2 * d;
   double l0 = 0.0, l1 = 0.0;
+  const int nfull = d / 16;
+  uint4 xn = *(const uint4*)(a.codes_t + tiled_offset(i, 0, a.nq));
   for (int qq = 0; qq < a.nq; ++qq) {
-    const uint4 xq = *(const uint4*)(a.codes_t + tiled_offset(i, qq * 16, a.nq));
+    const uint4 xq = xn;
+    if (qq + 1 < a.nq) xn = *(const uint4*)(a.codes_t + tiled_offset(i, (qq + 1) * 16, a.nq));
     const uint4 c0 = ((const uint4*)cc)[qq], c1 = ((const uint4*)(cc + dp))[qq];
     const uint4 dx0 = make_uint4(xq.x ^ c0.x, xq.y ^ c0.y, xq.z ^ c0.z, xq.w ^ c0.w);
     const uint4 dx1 = make_uint4(xq.x ^ c1.x, xq.y ^ c1.y, xq.z ^ c1.z, xq.w ^ c1.w);
+    if (qq < nfull) {
+      // all 16 terms of both chains read before the ordered adds (LDS reads in flight)
+      double v0[16], v1[16];
 #pragma unroll
-    for (int b = 0; b < 16; ++b) {
-      const int j = qq * 16 + b;
-      if (j < d) {
-        l0 += t0[2 * j + (byte_differs(dx0, b) ? 1 : 0)];
-        l1 += t1[2 * j + (byte_differs(dx1, b) ? 1 : 0)];
+      for (int b = 0; b < 16; ++b) {
+        const int j = qq * 16 + b;
+        v0[b] = t0[2 * j + (byte_differs(dx0, b) ? 1 : 0)];
+        v1[b] = t1[2 * j + (byte_differs(dx1, b) ? 1 : 0)];
+      }
+#pragma unroll
+      for (int b = 0; b < 16; ++b) {
+        l0 += v0[b];
+        l1 += v1[b];
+      }
+    } else {
+#pragma unroll
+      for (int b = 0; b < 16; ++b) {
+        const int j = qq * 16 + b;
+        if (j < d) {
+          l0 += t0[2 * j + (byte_differs(dx0, b) ? 1 : 0)];
+          l1 += t1[2 * j + (byte_differs(dx1, b) ? 1 : 0)];
+        }
       }
     }
   }
