@@ -1758,9 +1758,8 @@ __global__ __launch_bounds__(kBlock) void k_sm_ll(SmArgs a) {
   a.ll[a.nS + q] = ll_uniform<0>(x, a.d, a.two.codes + dp, a.two.tab + 2 * a.d);
 }
 
-// k_sm_ll with both clusters' tables and codes staged in LDS and the two attribute-order
-// sums interleaved (two independent dependency chains per lane); 64-lane workgroups so a
-// scan of ~10^4 points spreads over the CUs.
+// k_sm_ll with both clusters' tables and codes staged in LDS; one lane per (point, cluster)
+// attribute-order sum and 64-lane workgroups, so a scan of ~10^4 points spreads over the CUs.
 constexpr int kSmLLBlock = 64;
 __global__ __launch_bounds__(kSmLLBlock) void k_sm_ll_lds(SmArgs a) {
   extern __shared__ double sm_lds[];
@@ -1770,47 +1769,39 @@ __global__ __launch_bounds__(kSmLLBlock) void k_sm_ll_lds(SmArgs a) {
   for (int t = threadIdx.x; t < 4 * d; t += kSmLLBlock) tab[t] = a.two.tab[t];
   for (int t = threadIdx.x; t < 2 * dp / 16; t += kSmLLBlock) ((uint4*)cc)[t] = ((const uint4*)a.two.codes)[t];
   __syncthreads();
-  const int q = blockIdx.x * kSmLLBlock + threadIdx.x;
+  // lane pair (2p, 2p + 1): point p of the block against cluster 0 and cluster 1, so a scan
+  // of |S| points runs 2|S| lanes (the chains are sequential; more waves per SIMD is what
+  // hides their issue and LDS latency)
+  const int cl = threadIdx.x & 1;
+  const int q = blockIdx.x * (kSmLLBlock / 2) + (threadIdx.x >> 1);
   if (q >= a.nS) return;
   const int64_t i = a.S[q];
-  const double* t0 = tab;
-  const double* t1 = tab + 2 * d;
-  double l0 = 0.0, l1 = 0.0;
+  const double* t = tab + 2 * d * cl;
+  const uint4* cz = (const uint4*)(cc + dp * cl);
+  double l = 0.0;
   const int nfull = d / 16;
   uint4 xn = *(const uint4*)(a.codes_t + tiled_offset(i, 0, a.nq));
   for (int qq = 0; qq < a.nq; ++qq) {
     const uint4 xq = xn;
     if (qq + 1 < a.nq) xn = *(const uint4*)(a.codes_t + tiled_offset(i, (qq + 1) * 16, a.nq));
-    const uint4 c0 = ((const uint4*)cc)[qq], c1 = ((const uint4*)(cc + dp))[qq];
-    const uint4 dx0 = make_uint4(xq.x ^ c0.x, xq.y ^ c0.y, xq.z ^ c0.z, xq.w ^ c0.w);
-    const uint4 dx1 = make_uint4(xq.x ^ c1.x, xq.y ^ c1.y, xq.z ^ c1.z, xq.w ^ c1.w);
+    const uint4 c = cz[qq];
+    const uint4 dx = make_uint4(xq.x ^ c.x, xq.y ^ c.y, xq.z ^ c.z, xq.w ^ c.w);
     if (qq < nfull) {
-      // all 16 terms of both chains read before the ordered adds (LDS reads in flight)
-      double v0[16], v1[16];
+      // all 16 terms read before their ordered adds (LDS reads in flight)
+      double v[16];
 #pragma unroll
-      for (int b = 0; b < 16; ++b) {
-        const int j = qq * 16 + b;
-        v0[b] = t0[2 * j + (byte_differs(dx0, b) ? 1 : 0)];
-        v1[b] = t1[2 * j + (byte_differs(dx1, b) ? 1 : 0)];
-      }
+      for (int b = 0; b < 16; ++b) v[b] = t[2 * (qq * 16 + b) + (byte_differs(dx, b) ? 1 : 0)];
 #pragma unroll
-      for (int b = 0; b < 16; ++b) {
-        l0 += v0[b];
-        l1 += v1[b];
-      }
+      for (int b = 0; b < 16; ++b) l += v[b];
     } else {
 #pragma unroll
       for (int b = 0; b < 16; ++b) {
         const int j = qq * 16 + b;
-        if (j < d) {
-          l0 += t0[2 * j + (byte_differs(dx0, b) ? 1 : 0)];
-          l1 += t1[2 * j + (byte_differs(dx1, b) ? 1 : 0)];
-        }
+        if (j < d) l += t[2 * j + (byte_differs(dx, b) ? 1 : 0)];
       }
     }
   }
-  a.ll[q] = l0;
-  a.ll[a.nS + q] = l1;
+  a.ll[cl * a.nS + q] = l;
 }
 
 // Exact sm:204-215 two-way draw.  probs[k] = log(n_k) + H_k; normalise; FixupProb;
@@ -1967,7 +1958,8 @@ hipError_t launch_sm_ll(const SmArgs& a, hipStream_t s) {
   if (a.nS == 0) return hipSuccess;
   const size_t lds = (size_t)4 * a.d * 8 + (size_t)2 * a.nq * 16;
   if (lds <= 64 * 1024) {
-    hipLaunchKernelGGL(k_sm_ll_lds, dim3((a.nS + kSmLLBlock - 1) / kSmLLBlock), dim3(kSmLLBlock), lds, s, a);
+    const int per = kSmLLBlock / 2;     // points per workgroup (two lanes each)
+    hipLaunchKernelGGL(k_sm_ll_lds, dim3((a.nS + per - 1) / per), dim3(kSmLLBlock), lds, s, a);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_sm_ll, dim3((a.nS + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
