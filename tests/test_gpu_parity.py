@@ -589,3 +589,26 @@ def test_restricted_gibbs_random_split_of_one_cluster(hd, oracle):
     assert_same_state(eng, ost)
     assert np.array_equal(eng.rng_state, st)
     eng.close()
+
+
+def test_restricted_gibbs_sizes_beyond_lds_logn(hd, oracle):
+    # |c1| + |c2| > 20479: k_sm_scan reads log(n) from global memory instead of LDS
+    ds = synth(24000, 12, 2, 2, seed=9)
+    c = ds.truth.astype(np.int32).copy()
+    rng = np.random.default_rng(2)
+    c[rng.random(ds.n) < 0.5] = 0
+    c[c != 0] = 1
+    i1 = int(np.where(c == 0)[0][0])
+    i2 = int(np.where(c == 1)[0][0])
+    cen, sig = random_params(ds, 2, 17)
+    S = [i for i in range(ds.n) if i not in (i1, i2)]
+    st = oracle.seed_state(53)
+    eng = make_engine(hd, ds)
+    eng.set_state(c, cen, sig)
+    eng.rng_state = st
+    eng.restricted_gibbs(S, i1, i2, t=2)
+    ost = oracle_state(oracle, c, cen, sig)
+    assert oracle.restricted_gibbs(ds.codes, ds.attrisize, ds.v, ds.w, S, ost, i1, i2, 2, st) == 0
+    assert_same_state(eng, ost)
+    assert np.array_equal(eng.rng_state, st)
+    eng.close()
