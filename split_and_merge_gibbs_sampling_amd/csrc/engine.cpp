@@ -452,6 +452,11 @@ struct SmWork {
   DevBuf<double> d_two_tab;
   DevBuf<uint32_t> d_raw;
   std::vector<double> h_out;
+  // pinned staging of the restricted scans' per-iteration transfers (sides, draws, tables)
+  PinBuf<int> h_side;
+  PinBuf<uint32_t> h_raw;
+  PinBuf<uint8_t> h_two_codes;
+  PinBuf<double> h_two_tab;
 };
 
 // A window of the R random stream generated on the device (k_mt_gen), starting at the

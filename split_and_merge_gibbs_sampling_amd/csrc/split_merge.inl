@@ -190,15 +190,21 @@ static void hrecount(const Ctx* c, HState& s) {
 }
 
 // Device: exact lls of the S points against clusters (k1, k2) of state s.
+// The pinned staging buffers are reused by the next call only after a stream wait (every
+// caller synchronizes before it returns).
 static void sm_upload_two(Ctx* c, SmWork& W, const HState& s, int k1, int k2) {
-  std::vector<uint8_t> cc(2 * (size_t)c->dp, 0);
-  std::vector<double> tt(4 * (size_t)c->d);
-  c->tables_for(&s.center[(size_t)k1 * c->d], &s.sigma[(size_t)k1 * c->d], cc.data(), tt.data());
-  c->tables_for(&s.center[(size_t)k2 * c->d], &s.sigma[(size_t)k2 * c->d], cc.data() + c->dp, tt.data() + 2 * c->d);
-  W.d_two_codes.ensure(cc.size());
-  W.d_two_tab.ensure(tt.size());
-  HIPCHK(hipMemcpyAsync(W.d_two_codes.p, cc.data(), cc.size(), hipMemcpyHostToDevice, c->stream));
-  HIPCHK(hipMemcpyAsync(W.d_two_tab.p, tt.data(), tt.size() * 8, hipMemcpyHostToDevice, c->stream));
+  const size_t nc = 2 * (size_t)c->dp, nt = 4 * (size_t)c->d;
+  W.h_two_codes.ensure(nc);
+  W.h_two_tab.ensure(nt);
+  uint8_t* cc = W.h_two_codes.p;
+  double* tt = W.h_two_tab.p;
+  std::memset(cc, 0, nc);
+  c->tables_for(&s.center[(size_t)k1 * c->d], &s.sigma[(size_t)k1 * c->d], cc, tt);
+  c->tables_for(&s.center[(size_t)k2 * c->d], &s.sigma[(size_t)k2 * c->d], cc + c->dp, tt + 2 * c->d);
+  W.d_two_codes.ensure(nc);
+  W.d_two_tab.ensure(nt);
+  HIPCHK(hipMemcpyAsync(W.d_two_codes.p, cc, nc, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(W.d_two_tab.p, tt, nt * 8, hipMemcpyHostToDevice, c->stream));
 }
 
 static SmArgs sm_args(Ctx* c, SmWork& W, int nS) {
@@ -233,31 +239,38 @@ static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1
   const int c1 = s.c[i1], c2 = s.c[i2];
   const int nS = (int)S.size();
   sm_upload_S(c, W, S);
-  std::vector<int> side(nS), prev(nS), to1, to2;
-  std::vector<uint32_t> raw(nS);
+  std::vector<int> side(nS), to1, to2;   // sides before the current scan
+  // pinned staging: draws up, sides down (each iteration ends with a stream wait)
+  W.h_side.ensure(std::max(nS, 1));
+  W.h_raw.ensure(std::max(nS, 1));
+  int* hs = W.h_side.p;
+  uint32_t* raw = W.h_raw.p;
   const double T = 54.0 * M_LN2 + std::log(2.0) + 0.5;
   for (int q = 0; q < nS; ++q) side[q] = (s.c[S[q]] == c1) ? 0 : 1;
   for (int iter = 0; iter < t; ++iter) {
-    c->rng.raw_block(raw.data(), nS);
+    c->rng.raw_block(raw, nS);
     // c1 == c2 (only through the C ABI): every draw picks the same label, so only the
     // draws are consumed
     if (nS && c1 != c2) {
       SmTimer tm(c->stats.t_sm_scan_ms);
-      prev = side;
       sm_upload_two(c, W, s, c1, c2);
       // later scans start from the sides the previous scan left on the device
-      if (iter == 0) HIPCHK(hipMemcpyAsync(W.d_side.p, side.data(), (size_t)nS * 4, hipMemcpyHostToDevice, c->stream));
-      HIPCHK(hipMemcpyAsync(W.d_raw.p, raw.data(), (size_t)nS * 4, hipMemcpyHostToDevice, c->stream));
+      if (iter == 0) {
+        std::memcpy(hs, side.data(), (size_t)nS * 4);
+        HIPCHK(hipMemcpyAsync(W.d_side.p, hs, (size_t)nS * 4, hipMemcpyHostToDevice, c->stream));
+      }
+      HIPCHK(hipMemcpyAsync(W.d_raw.p, raw, (size_t)nS * 4, hipMemcpyHostToDevice, c->stream));
       SmArgs a = sm_args(c, W, nS);
       a.n1 = F1.nn; a.n2 = F2.nn;
       HIPCHK(launch_sm_ll(a, c->stream));
       HIPCHK(launch_sm_scan(a, T, c->stream));
-      HIPCHK(hipMemcpyAsync(side.data(), W.d_side.p, (size_t)nS * 4, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipMemcpyAsync(hs, W.d_side.p, (size_t)nS * 4, hipMemcpyDeviceToHost, c->stream));
       HIPCHK(hipStreamSynchronize(c->stream));
       to1.clear();
       to2.clear();
       for (int q = 0; q < nS; ++q) {
-        if (side[q] == prev[q]) continue;
+        if (hs[q] == side[q]) continue;
+        side[q] = hs[q];
         const int i = S[q];
         s.c[i] = side[q] == 0 ? c1 : c2;
         (side[q] == 0 ? to1 : to2).push_back(i);
@@ -480,16 +493,16 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
     sl.c[i1] = st.K;
     push_cluster(this, sl);
     sample_center_uniform(&sl.center[(size_t)sl.K * d]);
-    e = sample_sigma(v.data(), w.data(), &sl.sigma[(size_t)sl.K * d]);
+    e = sample_sigma_wide(v.data(), w.data(),&sl.sigma[(size_t)sl.K * d]);
     if (e) { err = "rhig failed"; return e; }
     sl.K++;
   } else {
     sample_center_uniform(&sl.center[(size_t)st.c[i1] * d]);
-    e = sample_sigma(v.data(), w.data(), &sl.sigma[(size_t)st.c[i1] * d]);
+    e = sample_sigma_wide(v.data(), w.data(),&sl.sigma[(size_t)st.c[i1] * d]);
     if (e) { err = "rhig failed"; return e; }
   }
   sample_center_uniform(&sl.center[(size_t)st.c[i2] * d]);
-  e = sample_sigma(v.data(), w.data(), &sl.sigma[(size_t)st.c[i2] * d]);
+  e = sample_sigma_wide(v.data(), w.data(),&sl.sigma[(size_t)st.c[i2] * d]);
   if (e) { err = "rhig failed"; return e; }
   {
     const int ref[2] = {sl.c[i1], sl.c[i2]};
@@ -511,7 +524,7 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
     for (int q : S) ml.c[q] = ml.c[i2];
   }
   sample_center_uniform(&ml.center[(size_t)ml.c[i2] * d]);
-  e = sample_sigma(v.data(), w.data(), &ml.sigma[(size_t)ml.c[i2] * d]);
+  e = sample_sigma_wide(v.data(), w.data(),&ml.sigma[(size_t)ml.c[i2] * d]);
   if (e) { err = "rhig failed"; return e; }
   e = clean_var(this, ml, ml);
   if (e) { err = "State validation failed: clean_var"; return e; }
