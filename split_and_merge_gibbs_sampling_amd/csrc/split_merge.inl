@@ -134,6 +134,35 @@ static void freq_move(const Ctx* c, Freq& F1, Freq& F2, const std::vector<int>& 
   F2.nn += (int)to2.size() - (int)to1.size();
 }
 
+// Tables of the two clusters that split M in s: rows labelled k1 into F1, the others into
+// F2, in one pass (attribute ranges on the host pool).
+static void freq_split(const Ctx* c, const HState& s, const std::vector<int>& M, int k1, Freq& F1, Freq& F2) {
+  F1.f.assign((size_t)c->d * c->mmax, 0.0);
+  F2.f.assign((size_t)c->d * c->mmax, 0.0);
+  int n1 = 0;
+  for (int q : M) n1 += s.c[q] == k1;
+  F1.nn = n1;
+  F2.nn = (int)M.size() - n1;
+  const int chunk = 32;
+  const int nchunk = (c->d + chunk - 1) / chunk;
+  auto run = [&](int ch) {
+    const int j0 = ch * chunk, j1 = std::min(c->d, j0 + chunk);
+    for (int q : M) {
+      double* f = (s.c[q] == k1 ? F1 : F2).f.data();
+      const uint8_t* x = &c->codes[(size_t)q * c->d];
+      for (int j = j0; j < j1; ++j) f[(size_t)j * c->mmax + (x[j] - 1)] += 1.0;
+    }
+  };
+  if ((int64_t)M.size() * c->d >= (1 << 18) && nchunk > 1) pool_for(nchunk, run, 1);
+  else for (int ch = 0; ch < nchunk; ++ch) run(ch);
+}
+
+static void freq_plus(const Freq& A, const Freq& B, Freq& out) {
+  out.f.resize(A.f.size());
+  for (size_t i = 0; i < A.f.size(); ++i) out.f[i] = A.f[i] + B.f[i];
+  out.nn = A.nn + B.nn;
+}
+
 static void freq_minus(const Freq& A, const Freq& B, Freq& out) {
   out.f.resize(A.f.size());
   for (size_t i = 0; i < A.f.size(); ++i) out.f[i] = A.f[i] - B.f[i];
@@ -485,7 +514,6 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
     if (i != i1 && i != i2) S.push_back(i);
   }
   Freq FM;                             // every cluster below that holds i1 or i2 is within M
-  freq_over(this, st, M, -1, FM);
   int e;
   // sm:303-352 split_launch_state
   HState sl = st;
@@ -509,9 +537,9 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
     for (int q : S) sl.c[q] = ref[(int)(2 * rng.unif())];
   }
   hrecount(this, sl);
-  Freq F1, F2;                         // tables of sl.c[i1], sl.c[i2]
-  freq_over(this, sl, M, sl.c[i1], F1);
-  freq_minus(FM, F1, F2);
+  Freq F1, F2;                         // tables of sl.c[i1], sl.c[i2] (they split M)
+  freq_split(this, sl, M, sl.c[i1], F1, F2);
+  freq_plus(F1, F2, FM);
   e = restricted_gibbs(this, S, sl, i1, i2, t, F1, F2);
   if (e) { err = "split launch state failed"; return e; }
   e = hvalidate(sl);
