@@ -262,8 +262,10 @@ static void sm_upload_S(Ctx* c, SmWork& W, const std::vector<int>& S) {
 // and s.c[i2] on entry, kept current (points the scan moves change sides).  The members of
 // both clusters are S + {i1, i2}, so their sizes come from the tables, neither can empty
 // (i1, i2 never move) and validate_state (sm:222) cannot fail.
+// members_are_S: the two clusters hold exactly S + {i1, i2} (the split-merge move; the C ABI
+// entry point takes any S).
 static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1, int i2, int t, Freq& F1,
-                            Freq& F2) {
+                            Freq& F2, bool members_are_S) {
   SmWork& W = smwork(c);
   const int c1 = s.c[i1], c2 = s.c[i2];
   const int nS = (int)S.size();
@@ -304,7 +306,21 @@ static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1
         s.c[i] = side[q] == 0 ? c1 : c2;
         (side[q] == 0 ? to1 : to2).push_back(i);
       }
-      freq_move(c, F1, F2, to1, to2);
+      if (members_are_S && 4 * (to1.size() + to2.size()) > (size_t)nS) {
+        // many moves (the first scan of a random split): rebuilding c1's table from its
+        // rows costs |c1| D, moving them 2 (moves) D
+        Freq tot;
+        freq_plus(F1, F2, tot);
+        std::vector<int> rows1;
+        rows1.reserve(F1.nn + to1.size());
+        rows1.push_back(i1);
+        for (int q = 0; q < nS; ++q)
+          if (side[q] == 0) rows1.push_back(S[q]);
+        freq_over(c, s, rows1, -1, F1);
+        freq_minus(tot, F1, F2);
+      } else {
+        freq_move(c, F1, F2, to1, to2);
+      }
     }
     s.counts[c1] = F1.nn;
     s.counts[c2] = F2.nn;
@@ -540,7 +556,7 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
   Freq F1, F2;                         // tables of sl.c[i1], sl.c[i2] (they split M)
   freq_split(this, sl, M, sl.c[i1], F1, F2);
   freq_plus(F1, F2, FM);
-  e = restricted_gibbs(this, S, sl, i1, i2, t, F1, F2);
+  e = restricted_gibbs(this, S, sl, i1, i2, t, F1, F2, true);
   if (e) { err = "split launch state failed"; return e; }
   e = hvalidate(sl);
   if (e) { err = "State validation failed: split_launch_state"; return e; }
@@ -569,7 +585,7 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
   const double alpha = gamma;
   if (st.c[i1] == st.c[i2]) {
     ss = sl;
-    e = restricted_gibbs(this, S, ss, i1, i2, 1, F1, F2);    // F1, F2 now ss's tables
+    e = restricted_gibbs(this, S, ss, i1, i2, 1, F1, F2, true);    // F1, F2 now ss's tables
     if (e) { err = "restricted gibbs failed"; return e; }
     // sm:438-487 (st.c[i1]'s members are all of M)
     SmTimer tm(stats.t_sm_terms_ms);
@@ -639,7 +655,7 @@ int sm_restricted_gibbs_device(Ctx* c, const int32_t* S, int32_t nS, int32_t i1,
   Freq F1, F2;                         // the clusters may hold points outside S here
   freq_over(c, s, all, s.c[i1], F1);
   freq_over(c, s, all, s.c[i2], F2);
-  int st = restricted_gibbs(c, SS, s, i1, i2, t, F1, F2);
+  int st = restricted_gibbs(c, SS, s, i1, i2, t, F1, F2, false);
   if (st) { c->err = "restricted gibbs failed"; return st; }
   st = hvalidate(s);
   if (st) { c->err = "State validation failed: restricted gibbs"; return st; }
