@@ -6,9 +6,11 @@ compute_loglikelihood, on synthetic data already resident in HBM.  The default w
 is BASELINE config C5 (N = 1,000,000, D = 128, m_j = 4, K_true = 20, m = 3 latent
 clusters), initialised at the generator's ground truth (L = 0 path, la:32-39).
 
-Multi-GPU: one process per GPU (torch.distributed.run); every rank runs an independent
-chain with its own seed (replicas, "scaling": "weak"); the only collective is the
-barrier/max of the timing.
+Multi-GPU: one process per GPU; every rank runs an independent chain with its own seed
+(replicas, "scaling": "weak"); the only collectives are the timing barrier / max and a
+gather of the per-rank setup.  Under torch.distributed.run (WORLD_SIZE set) this process is
+one rank; `--gpus N > 1` without it starts the N ranks under torch.distributed.run as a
+child process (before anything touches a GPU) and exits with its code.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c5] [--n N]
 """
@@ -87,6 +89,39 @@ def dist_env():
     return ws, rank, local
 
 
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n: int, argv) -> int:
+    """`--gpus N > 1` without a launcher: start N rank processes (one per GPU) under
+    torch.distributed.run as a CHILD of this process -- nothing here has touched a GPU, and
+    this process never re-executes itself -- and return its exit code."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + list(argv)
+    return subprocess.run(cmd, env=env).returncode
+
+
+def rank_setup(rank: int, local: int) -> dict:
+    """Per-rank chain setup (replicas): GPU `local`, chain seed 1 + rank (the
+    data seed is shared, so every rank samples the same posterior with its own stream); the
+    engine homes its host pool on an L3 domain local to that GPU (engine.cpp gpu_home_domain)."""
+    return {"rank": rank, "device": local, "seed": 1 + rank}
+
+
+def aggregate(ws: int, steps: int, elapsed_max: float) -> float:
+    """Whole-job throughput: the iterations all ranks ran over the slowest rank's time."""
+    return ws * steps / elapsed_max
+
+
 class Dist:
     """Barrier and max-over-ranks for the timing (RCCL when >1 rank, else no-op)."""
 
@@ -118,6 +153,13 @@ class Dist:
         t = self.torch.tensor([x], dtype=self.torch.float64, device=self._dev())
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
+
+    def gather(self, obj):
+        if self.dist is None:
+            return [obj]
+        out = [None] * self.ws
+        self.dist.all_gather_object(out, obj)
+        return out
 
     def close(self):
         if self.dist is not None:
@@ -197,18 +239,27 @@ def main():
     ap.add_argument("--traffic-csv", action="append", default=None,
                     help="rocprofv3 --pmc counter_collection CSV(s) with FETCH_SIZE / WRITE_SIZE of this workload "
                          "(separate passes); default: profiles/r01/pmc_{fetch,write}_<config>.csv when present")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="rank setup, barrier / max timing and the aggregate without the engine (CPU, gloo)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     ws, rank, local = dist_env()
+    if ws != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}")
+    if args.dry_run:
+        return dry_run(args, ws, rank, local)
     D = Dist(ws, rank, local)
     import split_and_merge_gibbs_sampling_amd as hd
     from split_and_merge_gibbs_sampling_amd.data import CONFIGS, config
 
+    setup = rank_setup(rank, local)
     t_setup = time.perf_counter()
     ds = config(args.config, n=args.n)
-    eng = hd.Engine(local)
+    eng = hd.Engine(setup["device"])
     eng.set_data(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w)
-    eng.set_seed(1 + rank)
+    eng.set_seed(setup["seed"])
     hig_log = args.hig_logspace == "on" or (args.hig_logspace == "auto" and args.sm)
     if hig_log:
         eng.set_hig_logspace(True)
@@ -237,12 +288,14 @@ def main():
     eng.synchronize()
     cuda_sync()
     D.barrier()
-    elapsed = D.max(time.perf_counter() - t0)
+    mine = time.perf_counter() - t0
+    elapsed = D.max(mine)
+    ranks = D.gather(dict(setup, ms_per_step=round(1e3 * mine / args.steps, 4)))
     st = eng.stats()
     c, cen, _ = eng.get_state()
     K = int(cen.shape[0])
 
-    value = ws * args.steps / elapsed
+    value = aggregate(ws, args.steps, elapsed)
     bpp = prepass_bytes_per_point(ds.d, int(ds.attrisize.max()), args.m)
     pre_ms = st["t_prepass_ms"]                  # HIP events around every 8th prepass launch
     achieved = (bpp * st["prepass_timed_points"] / 1e9) / (pre_ms / 1e3) if pre_ms > 0 else None
@@ -285,6 +338,7 @@ def main():
                          f"{' + split-merge (t=r=10)' if args.sm else ''} + compute_loglikelihood "
                          f"(code/launcher.cpp:94-132), ground-truth init"),
             "n": ds.n, "d": ds.d, "m": args.m, "K_final": K, "parallelism": f"replicas{ws}",
+            "ranks": ranks,
             "sweep_effective_GBps": round(survey_sweep_bytes(ds.n, ds.d, args.m) * args.steps / elapsed / 1e9, 2),
             "setup_s": round(setup_s, 1),
             # device: prepass from its HIP-event-timed launches (x launches per step); exact rows
@@ -327,6 +381,27 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()
+    D.close()
+
+
+def dry_run(args, ws, rank, local):
+    """The multi-rank harness without the engine: per-rank setup, barrier, a stand-in step
+    loop, max over ranks, gather and the aggregate line (tests/test_dist.py runs it on gloo)."""
+    D = Dist(ws, rank, local, backend="gloo")
+    setup = rank_setup(rank, local)
+    D.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.001 * (1 + rank))
+    D.barrier()
+    mine = time.perf_counter() - t0
+    elapsed = D.max(mine)
+    ranks = D.gather(dict(setup, ms_per_step=round(1e3 * mine / args.steps, 4)))
+    if rank == 0:
+        print(json.dumps({"metric": "dry run", "value": aggregate(ws, args.steps, elapsed), "unit": "steps/s",
+                          "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(1e3 * elapsed / args.steps, 4), "scaling": "weak",
+                          "config": {"parallelism": f"replicas{ws}", "ranks": ranks}}), flush=True)
     D.close()
 
 

@@ -172,6 +172,16 @@ int hdpm_get_pool_heads(hdpm_ctx* ctx, uint64_t* out, int64_t P);
  * semantics). */
 #define HDPM_OPT_HIG_LOGSPACE 1
 int hdpm_set_option(hdpm_ctx* ctx, int32_t option, double value);
+/* Testing: one draw on the device from log-weights logw[E] (E <= 256) and the uniform rU --
+ * the n8:95-102 categorical draw (two_way = 0; *pick = the 0-based index, or -status) or the
+ * sm:204-215 two-way draw (two_way = 1, E = 2) -- with the engine's exp, glibc's algorithm
+ * (ocml = 0), or the device libm's (ocml = 1: what the engine used before; shows the ulp
+ * differences the glibc replica removes). */
+int hdpm_debug_draw(hdpm_ctx* ctx, const double* logw, int32_t E, double rU, int32_t two_way, int32_t ocml,
+                    int32_t* pick);
+/* Testing: exp (fn = 0) or log (fn = 1) of x[n] on the device, glibc's algorithm (ocml = 0)
+ * or the device libm's (ocml = 1). */
+int hdpm_debug_math(hdpm_ctx* ctx, const double* x, int64_t n, int32_t fn, int32_t ocml, double* out);
 /* Block until all device work of the context is done. */
 int hdpm_synchronize(hdpm_ctx* ctx);
 

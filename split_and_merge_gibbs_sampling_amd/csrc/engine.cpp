@@ -54,6 +54,8 @@ hipError_t launch_hist(const HistArgs& a, hipStream_t s);
 size_t hist_partial_words(const HistArgs& a, int* nbx, int* kc, int* tpb);
 hipError_t launch_loglik(const LoglikArgs& a, hipStream_t s);
 hipError_t launch_mt_gen(const MtGenArgs& a, hipStream_t s);
+hipError_t launch_debug_draw(const double* logw, int E, double rU, int two_way, int ocml, int* out, hipStream_t s);
+hipError_t launch_debug_math(const double* x, int64_t n, int fn, int ocml, double* out, hipStream_t s);
 hipError_t launch_lmatrix(const uint8_t* codes_t, int n, int d, int nq, ParamTables cl, int K, double* L,
                           int* H, int64_t ldL, hipStream_t s);
 int sm_restricted_gibbs_device(struct Ctx* c, const int32_t* S, int32_t nS, int32_t i1, int32_t i2,
@@ -2784,6 +2786,7 @@ int Ctx::run_markov_chain(const hdpm_chain_params* p, const int32_t* c_init, int
 using hdpm::Ctx;
 using hdpm::HipError;
 using hdpm::ScopedPin;
+using hdpm::DevBuf;
 
 #define GUARD(body)                                                            \
   try {                                                                        \
@@ -3049,6 +3052,37 @@ int hdpm_set_option(hdpm_ctx* h, int32_t option, double value) {
       ctx->err = "unknown option";
       return HDPM_E_ARG;
   }
+}
+int hdpm_debug_draw(hdpm_ctx* h, const double* logw, int32_t E, double rU, int32_t two_way, int32_t ocml,
+                    int32_t* pick) {
+  CTX();
+  if (!logw || !pick || E < 1 || E > 256 || (two_way && E != 2)) return HDPM_E_ARG;
+  GUARD({
+    DevBuf<double> dw;
+    DevBuf<int> dp;
+    dw.ensure((size_t)E);
+    dp.ensure(1);
+    HIPCHK(hipMemcpyAsync(dw.p, logw, (size_t)E * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hdpm::launch_debug_draw(dw.p, E, rU, two_way, ocml, dp.p, ctx->stream));
+    HIPCHK(hipMemcpyAsync(pick, dp.p, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return HDPM_OK;
+  })
+}
+int hdpm_debug_math(hdpm_ctx* h, const double* x, int64_t n, int32_t fn, int32_t ocml, double* out) {
+  CTX();
+  if (!x || !out || n <= 0 || (fn != 0 && fn != 1)) return HDPM_E_ARG;
+  GUARD({
+    DevBuf<double> dx;
+    DevBuf<double> dy;
+    dx.ensure((size_t)n);
+    dy.ensure((size_t)n);
+    HIPCHK(hipMemcpyAsync(dx.p, x, (size_t)n * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hdpm::launch_debug_math(dx.p, n, fn, ocml, dy.p, ctx->stream));
+    HIPCHK(hipMemcpyAsync(out, dy.p, (size_t)n * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return HDPM_OK;
+  })
 }
 int hdpm_synchronize(hdpm_ctx* h) {
   CTX();

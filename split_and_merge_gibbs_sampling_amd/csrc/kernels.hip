@@ -18,9 +18,31 @@
 #include <cfloat>
 #include <cmath>
 
+#include "glibc_math.hpp"
 #include "kernels.hpp"
 
 namespace hdpm {
+
+// Device copies of glibc's exp / log tables: every exp and log whose result decides a draw
+// (n8:95, sm:209-210, sm:150-158) runs glibc's algorithm (glibc_math.hpp), so the device's
+// probabilities are the host libm's bit for bit and the reference's cumulative compare
+// `rU <= p[j]` cannot flip on an ulp (ocml's exp differs from glibc's in the last place).
+namespace devtab {
+#define HDPM_GLIBC_TABLE __constant__
+#include "glibc_tables.inc"
+#undef HDPM_GLIBC_TABLE
+}  // namespace devtab
+
+template <bool kOcml = false>
+__device__ __forceinline__ double dexp(double x) {
+  if constexpr (kOcml) return exp(x);   // testing only: the pre-glibc behaviour
+  else return glibc::exp_r(x, devtab::kGlibcExpTab);
+}
+template <bool kOcml = false>
+__device__ __forceinline__ double dlog(double x) {
+  if constexpr (kOcml) return log(x);
+  else return glibc::log_r(x, devtab::kGlibcLogTab);
+}
 
 __device__ __forceinline__ double raw_to_unif(uint32_t y) {
   const double i2_32m1 = 2.328306437080797e-10;
@@ -591,7 +613,7 @@ __device__ __forceinline__ double readlane_f64(double x, int l) {
 // move by factors within exp(+-2 rad)): the chosen entry keeps its place in revsort's order
 // (ratios to its neighbours) and the uniform stays inside its cumulative interval.  0 when
 // no such bound is kept (ties, the Walker threshold in reach).
-template <int RE>
+template <int RE, bool kOcml = false>
 __device__ int decide_values(double (&pv)[RE], int E, double rU, double* lp, int* lperm, int* lpick,
                              double* rad = nullptr) {
   if (rad) *rad = 0.0;
@@ -618,7 +640,7 @@ __device__ int decide_values(double (&pv)[RE], int E, double rU, double* lp, int
   for (int r = 1; r < RE; ++r) mx = fmax(mx, pv[r]);
   mx = wave_max(mx);
 #pragma unroll
-  for (int r = 0; r < RE; ++r) pv[r] = (r * kWave + lane < E) ? exp(pv[r] - mx) : 0.0;      // n8:95
+  for (int r = 0; r < RE; ++r) pv[r] = (r * kWave + lane < E) ? dexp<kOcml>(pv[r] - mx) : 0.0;  // n8:95
   const double sum = scan(0.0, [](double s, double x) { return s + x; });
 #pragma unroll
   for (int r = 0; r < RE; ++r) pv[r] = pv[r] / sum;                                             // n8:96
@@ -780,7 +802,7 @@ __device__ int exact_decision_lds(const ResolveArgs& a, const RState& st, int K,
     mx = fmax(mx, v);
   }
   mx = wave_max(mx);
-  for (int e = lane; e < E; e += kWave) st.p[e] = exp(st.val[e] - mx);
+  for (int e = lane; e < E; e += kWave) st.p[e] = dexp(st.val[e] - mx);
   wave_sync();
   if (lane == 0) {
     double sum = 0.0;
@@ -1806,10 +1828,11 @@ __global__ __launch_bounds__(kSmLLBlock) void k_sm_ll_lds(SmArgs a) {
 
 // Exact sm:204-215 two-way draw.  probs[k] = log(n_k) + H_k; normalise; FixupProb;
 // revsort of two entries (ties: second first); cumulative compare.
+template <bool kOcml = false>
 __device__ __forceinline__ void two_way_probs(double v0, double v1, double& p0, double& p1) {
   const double mx = fmax(v0, v1);
-  p0 = exp(v0 - mx);
-  p1 = exp(v1 - mx);
+  p0 = dexp<kOcml>(v0 - mx);
+  p1 = dexp<kOcml>(v1 - mx);
   double sum = 0.0;
   sum += p0;
   sum += p1;
@@ -1827,9 +1850,10 @@ __device__ __forceinline__ int two_way_pick(double p0, double p1, double rU) {
   const double a0 = first0 ? p0 : p1;
   return (rU <= a0) ? (first0 ? 0 : 1) : (first0 ? 1 : 0);
 }
+template <bool kOcml = false>
 __device__ __forceinline__ int two_way_draw(double v0, double v1, double rU) {
   double p0, p1;
-  two_way_probs(v0, v1, p0, p1);
+  two_way_probs<kOcml>(v0, v1, p0, p1);
   return two_way_pick(p0, p1, rU);
 }
 
@@ -1843,9 +1867,17 @@ __device__ __forceinline__ int two_way_draw(double v0, double v1, double rU) {
 // few-ulp rounding of the exp and divisions) has one pick for every count it can see and is
 // settled in parallel without evaluating the draw; the others are drawn one by one with
 // their exact counts.
+//
+// The margin.  Near a threshold D0 (0, lam or -lam) the computed p0 = 1 / (1 + exp(-D)) (or
+// its complement) moves by |p0'| |D - D0| >= p (1 - p) |D - D0|, and p (1 - p) >= 2e-11 for the
+// thresholds a uniform in (2.3e-10, 1 - 2.3e-10) can set, so a D range kept 1e-4 from the
+// threshold keeps p0 at least ~2e-15 away from the value that would flip the pick.  The
+// computed D carries the error of two logn entries and two log-likelihood sums (a few ulp of
+// their magnitudes, < 1e-9 for any |S| and D the engine accepts), and exp / the two
+// divisions add a few ulp of p0 (< 1e-15): both far inside the margin.
+constexpr double kSmScanMargin = 1e-4;
 template <bool kLdsLogn>
-__global__ __launch_bounds__(kWave) void k_sm_scan(SmArgs a, double T) {
-  (void)T;
+__global__ __launch_bounds__(kWave) void k_sm_scan(SmArgs a) {
   extern __shared__ double scan_lds[];
   const int lane = threadIdx.x;
   int n1 = a.n1, n2 = a.n2;
@@ -1856,7 +1888,7 @@ __global__ __launch_bounds__(kWave) void k_sm_scan(SmArgs a, double T) {
     __syncthreads();
     logn = scan_lds;
   }
-  const double margin = 1e-4;
+  const double margin = kSmScanMargin;
   int nx_cur = 0;
   double nx_l0 = 0.0, nx_l1 = 0.0;
   uint32_t nx_raw = 0;
@@ -1921,13 +1953,13 @@ __global__ __launch_bounds__(kBlock) void k_sm_lpgs(SmArgs a) {
     const double v0 = a.logn[a.n1 - (g == 0)] + a.ll[q];
     const double v1 = a.logn[a.n2 - (g == 1)] + a.ll[a.nS + q];
     const double mx = fmax(v0, v1);
-    double p0 = exp(v0 - mx), p1 = exp(v1 - mx);
+    double p0 = dexp(v0 - mx), p1 = dexp(v1 - mx);
     double sum = 0.0;
     sum += p0;
     sum += p1;
     p0 = p0 / sum;
     p1 = p1 / sum;
-    hi = log(a.side[q] == 0 ? p0 : p1);
+    hi = dlog(a.side[q] == 0 ? p0 : p1);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -1965,12 +1997,52 @@ hipError_t launch_sm_ll(const SmArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_sm_ll, dim3((a.nS + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
-hipError_t launch_sm_scan(const SmArgs& a, double T, hipStream_t s) {
+hipError_t launch_sm_scan(const SmArgs& a, hipStream_t s) {
   const size_t lds = (size_t)(a.n1 + a.n2 + 1) * 8;
   if (lds <= 160 * 1024)
-    hipLaunchKernelGGL(k_sm_scan<true>, dim3(1), dim3(kWave), lds, s, a, T);
+    hipLaunchKernelGGL(k_sm_scan<true>, dim3(1), dim3(kWave), lds, s, a);
   else
-    hipLaunchKernelGGL(k_sm_scan<false>, dim3(1), dim3(kWave), 0, s, a, T);
+    hipLaunchKernelGGL(k_sm_scan<false>, dim3(1), dim3(kWave), 0, s, a);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ testing
+// One draw from given log-weights and uniform on the device: the n8:95-102 categorical draw
+// (decide_values) or the sm:204-215 two-way draw, with the engine's glibc exp or, kOcml,
+// the device libm's (the behaviour before the glibc replica; the parity test shows the
+// difference).
+template <bool kOcml>
+__global__ __launch_bounds__(kWave) void k_debug_draw(const double* logw, int E, double rU, int two_way, int* out) {
+  __shared__ double lp[4 * kWave];
+  __shared__ int lperm[4 * kWave];
+  __shared__ int lpick;
+  const int lane = threadIdx.x;
+  if (two_way) {
+    if (lane == 0) out[0] = two_way_draw<kOcml>(logw[0], logw[1], rU);
+    return;
+  }
+  double pv[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) pv[r] = (r * kWave + lane < E) ? logw[r * kWave + lane] : -INFINITY;
+  const int pick = decide_values<4, kOcml>(pv, E, rU, lp, lperm, &lpick);
+  if (lane == 0) out[0] = pick;
+}
+template <bool kOcml>
+__global__ void k_debug_math(const double* x, int64_t n, int fn, double* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = fn == 0 ? dexp<kOcml>(x[i]) : dlog<kOcml>(x[i]);
+}
+hipError_t launch_debug_draw(const double* logw, int E, double rU, int two_way, int ocml, int* out, hipStream_t s) {
+  if (E < 1 || E > 4 * kWave || (two_way && E != 2)) return hipErrorInvalidValue;
+  if (ocml) hipLaunchKernelGGL(k_debug_draw<true>, dim3(1), dim3(kWave), 0, s, logw, E, rU, two_way, out);
+  else hipLaunchKernelGGL(k_debug_draw<false>, dim3(1), dim3(kWave), 0, s, logw, E, rU, two_way, out);
+  return hipGetLastError();
+}
+hipError_t launch_debug_math(const double* x, int64_t n, int fn, int ocml, double* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const dim3 g((unsigned)((n + kBlock - 1) / kBlock));
+  if (ocml) hipLaunchKernelGGL(k_debug_math<true>, g, dim3(kBlock), 0, s, x, n, fn, out);
+  else hipLaunchKernelGGL(k_debug_math<false>, g, dim3(kBlock), 0, s, x, n, fn, out);
   return hipGetLastError();
 }
 hipError_t launch_sm_lpgs(const SmArgs& a, hipStream_t s) {

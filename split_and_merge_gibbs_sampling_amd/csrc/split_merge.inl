@@ -7,7 +7,7 @@
 namespace hdpm {
 
 hipError_t launch_sm_ll(const SmArgs& a, hipStream_t s);
-hipError_t launch_sm_scan(const SmArgs& a, double T, hipStream_t s);
+hipError_t launch_sm_scan(const SmArgs& a, hipStream_t s);
 hipError_t launch_sm_lpgs(const SmArgs& a, hipStream_t s);
 
 // A host copy of internal_state (cfh:32-63): labels, parameters, sizes.
@@ -276,7 +276,6 @@ static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1
   W.h_raw.ensure(std::max(nS, 1));
   int* hs = W.h_side.p;
   uint32_t* raw = W.h_raw.p;
-  const double T = 54.0 * M_LN2 + std::log(2.0) + 0.5;
   for (int q = 0; q < nS; ++q) side[q] = (s.c[S[q]] == c1) ? 0 : 1;
   for (int iter = 0; iter < t; ++iter) {
     c->rng.raw_block(raw, nS);
@@ -294,7 +293,7 @@ static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1
       SmArgs a = sm_args(c, W, nS);
       a.n1 = F1.nn; a.n2 = F2.nn;
       HIPCHK(launch_sm_ll(a, c->stream));
-      HIPCHK(launch_sm_scan(a, T, c->stream));
+      HIPCHK(launch_sm_scan(a, c->stream));
       HIPCHK(hipMemcpyAsync(hs, W.d_side.p, (size_t)nS * 4, hipMemcpyDeviceToHost, c->stream));
       HIPCHK(hipStreamSynchronize(c->stream));
       to1.clear();

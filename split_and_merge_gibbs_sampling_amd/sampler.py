@@ -178,6 +178,23 @@ class Engine:
     def synchronize(self):
         self._check(self._L.hdpm_synchronize(self._h))
 
+    def debug_draw(self, logw, rU: float, two_way: bool = False, ocml: bool = False) -> int:
+        """Testing: one device draw from log-weights (n8:95-102, or the sm:204-215 two-way
+        draw) with the engine's glibc exp, or the device libm's (ocml)."""
+        w = _f64(logw)
+        pick = C.c_int32(0)
+        self._check(self._L.hdpm_debug_draw(self._h, _lib.ptr(w), int(w.size), float(rU), int(two_way), int(ocml),
+                                            C.byref(pick)))
+        return pick.value
+
+    def debug_math(self, x, fn: str = "exp", ocml: bool = False) -> np.ndarray:
+        """Testing: exp / log of x on the device (glibc's algorithm, or the device libm's)."""
+        xs = _f64(x).ravel()
+        out = np.empty_like(xs)
+        self._check(self._L.hdpm_debug_math(self._h, _lib.ptr(xs), int(xs.size), 0 if fn == "exp" else 1,
+                                            int(ocml), _lib.ptr(out)))
+        return out
+
     def set_hig_logspace(self, on: bool = True):
         """Extension beyond the reference (include/hdpm.h HDPM_OPT_HIG_LOGSPACE): finite HIG
         log-densities for clusters whose 2F1 series overflows (the reference throws)."""

@@ -27,10 +27,12 @@ def _worker(rank, ws, port, q):
     import bench
     ws_, rank_, local_ = bench.dist_env()
     D = bench.Dist(ws_, rank_, local_, backend="gloo")
+    setup = bench.rank_setup(rank_, local_)
     D.barrier()
     mx = D.max(float(10 * (rank + 1)))
+    ranks = D.gather(setup)
     D.barrier()
-    q.put((rank, mx, ws_))
+    q.put((rank, mx, ws_, [(r["rank"], r["device"], r["seed"]) for r in ranks], bench.aggregate(ws_, 7, mx)))
     D.close()
 
 
@@ -64,6 +66,44 @@ def test_gloo_world2_barrier_and_max():
     assert [r[0] for r in res] == [0, 1]
     assert all(r[1] == 20.0 for r in res)       # max over ranks reaches every rank
     assert all(r[2] == 2 for r in res)
+    # every rank sees every rank's setup: GPU = local rank, chain seed 1 + rank
+    assert all(r[3] == [(0, 0, 1), (1, 1, 2)] for r in res)
+    assert all(r[4] == 2 * 7 / 20.0 for r in res)
+
+
+def _clean_env():
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "LOCAL_WORLD_SIZE", "GROUP_RANK"):
+        env.pop(k, None)
+    return env
+
+
+def test_bench_gpus2_starts_two_ranks():
+    """`python bench.py --gpus 2` (no launcher) starts two rank processes and prints ONE
+    aggregate line with n_gpus 2 (the dry run: the same harness without the engine)."""
+    import json
+    import subprocess
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "0",
+                        "--dry-run"], capture_output=True, text=True, timeout=300, env=_clean_env())
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "replicas2"
+    ranks = sorted(out["config"]["ranks"], key=lambda x: x["rank"])
+    assert [(x["rank"], x["device"], x["seed"]) for x in ranks] == [(0, 0, 1), (1, 1, 2)]
+    # aggregate = all ranks' steps over the slowest rank's time
+    assert abs(out["value"] * out["ms_per_step"] / 1e3 - 2.0) < 1e-3
+    assert out["ms_per_step"] >= max(x["ms_per_step"] for x in ranks) - 1e-3
+
+
+def test_bench_rejects_gpus_world_size_mismatch():
+    import subprocess
+    env = _clean_env()
+    env.update(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "1"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
 
 
 def test_bench_helpers():
