@@ -12,7 +12,9 @@ int orc_run_markov_chain(const double* data, int n, int d, const int* attrisize,
                          const double* v, const double* w, const orc_chain_params* p,
                          const int* c_i_init, int32_t* rng_state, int* out_total_cls, int* out_c_i,
                          double* out_loglik, int* out_accepted, int* final_ass) {
-    orc_aux A = {n, d, data, attrisize, gamma, v, w};
+    orc_aux A = {n, d, data, attrisize, gamma, v, w, NULL};
+    uint8_t* codes = p->fast >= 2 ? orc_codes_rowmajor(&A) : NULL;   /* optimised oracle */
+    A.codes = codes;
     orc_rng rng;
     orc_rng_import(&rng, rng_state);
     orc_state s;
@@ -60,9 +62,14 @@ int orc_run_markov_chain(const double* data, int n, int d, const int* attrisize,
                 memset(counts, 0, sizeof(int) * ((size_t)n + 2));
                 for (int i = 0; i < n; i++) counts[s.c_i[i]]++;
             }
-            for (int i = 0; i < n; i++) {
-                st = orc_sample_allocation(i, &A, &s, p->m, &pool, &rng, counts);
+            if (p->fast >= 2) {
+                st = orc_neal8_sweep_opt(&A, &s, p->m, &pool, &rng, counts, 0, -1);
                 if (st) goto out;
+            } else {
+                for (int i = 0; i < n; i++) {
+                    st = orc_sample_allocation(i, &A, &s, p->m, &pool, &rng, counts);
+                    if (st) goto out;
+                }
             }
             st = orc_update_phi(&rng, &A, &s, NULL, 0);
             if (st) goto out;
@@ -78,7 +85,8 @@ int orc_run_markov_chain(const double* data, int n, int d, const int* attrisize,
         }
         const int rec = iter >= p->thinning * p->burnin && iter % p->thinning == 0;
         double ll = 0.0;
-        if (rec || !p->fast) ll = orc_compute_loglikelihood(&A, &s);   /* la:132 */
+        if (rec || !p->fast)                                    /* la:132 */
+            ll = p->fast >= 2 ? orc_compute_loglikelihood_opt(&A, &s) : orc_compute_loglikelihood(&A, &s);
         if (rec) {
             int at = iter / p->thinning - p->burnin;
             if (out_total_cls) out_total_cls[at] = s.total_cls;
@@ -90,7 +98,7 @@ int orc_run_markov_chain(const double* data, int n, int d, const int* attrisize,
     if (final_ass) memcpy(final_ass, s.c_i, sizeof(int) * (size_t)n);
 out:
     orc_rng_export(&rng, rng_state);
-    free(pool.center); free(pool.sigma); free(counts);
+    free(pool.center); free(pool.sigma); free(counts); free(codes);
     orc_state_free(&s);
     return st;
 }

@@ -100,7 +100,7 @@ int orc_ffi_neal8_sweep(const double* data, int n, int d, const int* attrisize, 
                         double* sigma, int cap, int m, const double* pool_center,
                         const double* pool_sigma, int64_t P, int32_t* state625, int fast,
                         int first, int count) {
-    orc_aux A = {n, d, data, attrisize, gamma, v, w};
+    orc_aux A = {n, d, data, attrisize, gamma, v, w, NULL};
     orc_state s;
     int st = load_state(&s, n, d, cap, c_i, *K, centers, sigma);
     if (st) return st;
@@ -108,15 +108,23 @@ int orc_ffi_neal8_sweep(const double* data, int n, int d, const int* attrisize, 
     orc_rng r;
     orc_rng_import(&r, state625);
     int* counts = NULL;
+    uint8_t* codes = NULL;
     if (fast) {
         counts = (int*)calloc((size_t)cap + 1, sizeof(int));
         for (int i = 0; i < n; i++) counts[s.c_i[i]]++;
     }
-    int last = count < 0 ? n : first + count;
-    for (int i = first; i < last && !st; i++) st = orc_sample_allocation(i, &A, &s, m, &pool, &r, counts);
+    if (fast >= 2) {
+        codes = orc_codes_rowmajor(&A);
+        A.codes = codes;
+        st = orc_neal8_sweep_opt(&A, &s, m, &pool, &r, counts, first, count);
+    } else {
+        int last = count < 0 ? n : first + count;
+        for (int i = first; i < last && !st; i++) st = orc_sample_allocation(i, &A, &s, m, &pool, &r, counts);
+    }
     orc_rng_export(&r, state625);
     store_state(&s, c_i, K, centers, sigma);
     free(counts);
+    free(codes);
     orc_state_free(&s);
     return st;
 }
@@ -140,13 +148,29 @@ int orc_ffi_update_phi(const double* data, int n, int d, const int* attrisize, c
 
 double orc_ffi_compute_loglikelihood(const double* data, int n, int d, const int* attrisize,
                                      const int* c_i, int K, const double* centers, const double* sigma) {
-    orc_aux A = {n, d, data, attrisize, 0.0, NULL, NULL};
+    orc_aux A = {n, d, data, attrisize, 0.0, NULL, NULL, NULL};
     orc_state s;
     if (load_state(&s, n, d, K > 0 ? K : 1, c_i, K, centers, sigma)) return 0.0;
     double ll = orc_compute_loglikelihood(&A, &s);
     orc_state_free(&s);
     return ll;
 }
+
+/* the same sum from the cluster tables (fast.c): bit-identical, without N D exp/log */
+double orc_ffi_compute_loglikelihood_opt(const double* data, int n, int d, const int* attrisize,
+                                         const int* c_i, int K, const double* centers, const double* sigma) {
+    orc_aux A = {n, d, data, attrisize, 0.0, NULL, NULL, NULL};
+    orc_state s;
+    if (load_state(&s, n, d, K > 0 ? K : 1, c_i, K, centers, sigma)) return 0.0;
+    uint8_t* codes = orc_codes_rowmajor(&A);
+    A.codes = codes;
+    double ll = orc_compute_loglikelihood_opt(&A, &s);
+    free(codes);
+    orc_state_free(&s);
+    return ll;
+}
+
+void orc_ffi_set_threads(int nthreads) { orc_set_threads(nthreads); }
 
 int orc_ffi_pool_generate(const int* attrisize, int d, const double* v, const double* w, int64_t P,
                           double* pool_center, double* pool_sigma, int32_t* state625) {
@@ -162,13 +186,16 @@ int orc_ffi_pool_generate(const int* attrisize, int d, const double* v, const do
 int orc_ffi_restricted_gibbs(const double* data, int n, int d, const int* attrisize, const double* v,
                              const double* w, const int* S, int nS, int* c_i, int K, double* centers,
                              double* sigma, int i1, int i2, int t, int32_t* state625, int fast) {
-    orc_aux A = {n, d, data, attrisize, 0.0, v, w};
+    orc_aux A = {n, d, data, attrisize, 0.0, v, w, NULL};
     orc_state s;
     int st = load_state(&s, n, d, K, c_i, K, centers, sigma);
     if (st) return st;
+    uint8_t* codes = fast >= 2 ? orc_codes_rowmajor(&A) : NULL;
+    A.codes = codes;
     orc_rng r;
     orc_rng_import(&r, state625);
     st = orc_restricted_gibbs(S, nS, &s, i1, i2, &A, t, &r, fast);
+    free(codes);
     orc_rng_export(&r, state625);
     int Kout;
     store_state(&s, c_i, &Kout, centers, sigma);
@@ -193,13 +220,16 @@ int orc_ffi_split_and_merge(const double* data, int n, int d, const int* attrisi
                             const double* v, const double* w, int* c_i, int* K, double* centers,
                             double* sigma, int cap, int t, int r, int idx_1_sm, int32_t* state625,
                             int fast, int* accepted) {
-    orc_aux A = {n, d, data, attrisize, gamma, v, w};
+    orc_aux A = {n, d, data, attrisize, gamma, v, w, NULL};
     orc_state s;
     int st = load_state(&s, n, d, cap, c_i, *K, centers, sigma);
     if (st) return st;
+    uint8_t* codes = fast >= 2 ? orc_codes_rowmajor(&A) : NULL;
+    A.codes = codes;
     orc_rng rng;
     orc_rng_import(&rng, state625);
     st = orc_split_and_merge(&s, &A, t, r, idx_1_sm, &rng, fast, accepted);
+    free(codes);
     orc_rng_export(&rng, state625);
     store_state(&s, c_i, K, centers, sigma);
     orc_state_free(&s);

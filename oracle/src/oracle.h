@@ -80,6 +80,8 @@ typedef struct {
     double gamma;
     const double* v;         /* d */
     const double* w;         /* d */
+    const uint8_t* codes;    /* optional: the same data as row-major n x d uint8 codes
+                                (the optimised paths of fast.c; NULL elsewhere)    */
 } orc_aux;
 
 typedef struct {
@@ -115,6 +117,16 @@ int    orc_clean_var(orc_state* upd, const orc_state* cur, const orc_aux* A);   
 int orc_sample_allocation(int idx, const orc_aux* A, orc_state* s, int m, const orc_pool* pool,
                           orc_rng* r, int* counts);
 int orc_pool_generate(orc_rng* r, const orc_aux* A, orc_pool* pool);   /* la:74-77 / la:124-128 */
+
+/* ---- optimised oracle (fast.c): same arithmetic and draws, bit-identical results ---- */
+void    orc_set_threads(int n);                       /* OpenMP threads (0: default)      */
+uint8_t* orc_codes_rowmajor(const orc_aux* A);       /* malloc'd n x d codes              */
+void    orc_cluster_table(const orc_aux* A, const double* sig, double* tab);   /* [d][2] */
+double  orc_row_ll_table(const uint8_t* x, const double* cen, const double* tab, int d);
+int     orc_neal8_sweep_opt(const orc_aux* A, orc_state* s, int m, const orc_pool* pool, orc_rng* r,
+                            int* counts, int first, int count);
+double  orc_compute_loglikelihood_opt(const orc_aux* A, const orc_state* s);
+int     orc_sample_prob1_u(const double* probs, int n, double rU, int* out_index); /* given uniform */
 
 /* split-merge (sm) */
 int orc_restricted_gibbs(const int* S, int nS, orc_state* s, int i1, int i2, const orc_aux* A,

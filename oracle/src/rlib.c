@@ -134,7 +134,19 @@ void orc_revsort(double* a, int* ib, int n) {
 
 /* sample(x, 1, TRUE, probs): FixupProb -> (Walker if >200) -> SampleReplace.
  * Returns the 0-based position into x.  probs is not modified (Rcpp clones it). */
+static int sample_prob1_impl(orc_rng* r, double rU_given, const double* probs, int n, int* out_index);
+
 int orc_sample_prob1(orc_rng* r, const double* probs, int n, int* out_index) {
+    return sample_prob1_impl(r, 0.0, probs, n, out_index);
+}
+
+/* The same draw with its uniform given (the optimised oracle draws a sweep's uniforms
+ * ahead; FixupProb's failures return before the uniform would be consumed). */
+int orc_sample_prob1_u(const double* probs, int n, double rU, int* out_index) {
+    return sample_prob1_impl(NULL, rU, probs, n, out_index);
+}
+
+static int sample_prob1_impl(orc_rng* r, double rU_given, const double* probs, int n, int* out_index) {
     double  pbuf[256];
     int     permbuf[256];
     double* p = n <= 256 ? pbuf : (double*)malloc(sizeof(double) * (size_t)n);
@@ -165,7 +177,7 @@ int orc_sample_prob1(orc_rng* r, const double* probs, int n, int* out_index) {
         for (int i = 0; i < n; i++) perm[i] = i + 1;
         orc_revsort(p, perm, n);
         for (int i = 1; i < n; i++) p[i] += p[i - 1];
-        double rU = orc_unif_rand(r);
+        double rU = r ? orc_unif_rand(r) : rU_given;
         for (j = 0; j < nm1; j++)
             if (rU <= p[j]) break;
         *out_index = perm[j] - 1;

@@ -21,6 +21,23 @@ static double row_ll(const orc_aux* A, int i, const double* cen, const double* s
     return h;
 }
 
+/* fast >= 2 with A->codes (the optimised oracle, fast.c): the same sums from the two
+ * clusters' dhamming tables (bit-identical terms in the same order) */
+static int g_tables = 0;
+typedef struct { double* t[2]; } two_tabs;
+static int tabs_on(const orc_aux* A) { return g_tables && A->codes; }
+static void two_tabs_make(two_tabs* T, const orc_aux* A, const double* s0, const double* s1) {
+    T->t[0] = (double*)malloc(sizeof(double) * 2 * (size_t)A->d);
+    T->t[1] = (double*)malloc(sizeof(double) * 2 * (size_t)A->d);
+    orc_cluster_table(A, s0, T->t[0]);
+    orc_cluster_table(A, s1, T->t[1]);
+}
+static void two_tabs_free(two_tabs* T) { free(T->t[0]); free(T->t[1]); }
+static double row_ll_k(const orc_aux* A, const two_tabs* T, int k, int i, const double* cen, const double* sig) {
+    if (T->t[0]) return orc_row_ll_table(A->codes + (size_t)i * A->d, cen, T->t[k], A->d);
+    return row_ll(A, i, cen, sig);
+}
+
 /* sm:6-18 logdensity_hig */
 static double logdensity_hig(double sigmaj, double v, double w, double m, int* err) {
     double K = orc_norm_const2(w, v, m, err);
@@ -75,12 +92,14 @@ double orc_logprobgs_c_i(const orc_state* gs, const orc_state* g, const orc_aux*
     double logpgs = 0;
     int c1 = g->c_i[i1], c2 = g->c_i[i2];
     int n1 = count_eq(g->c_i, A->n, c1), n2 = count_eq(g->c_i, A->n, c2);
+    two_tabs T = {{NULL, NULL}};
+    if (tabs_on(A)) two_tabs_make(&T, A, gs->sigma + (size_t)c1 * d, gs->sigma + (size_t)c2 * d);
     for (int q = 0; q < nS; q++) {
         int s = S[q];
         double probs[2];
         for (int k = 0; k < 2; k++) {
             int cls = k == 0 ? c1 : c2;
-            double H = row_ll(A, s, gs->center + (size_t)cls * d, gs->sigma + (size_t)cls * d);
+            double H = row_ll_k(A, &T, k, s, gs->center + (size_t)cls * d, gs->sigma + (size_t)cls * d);
             int n = (k == 0 ? n1 : n2) - (g->c_i[s] == cls);
             probs[k] = log((double)n) + H;
         }
@@ -95,6 +114,7 @@ double orc_logprobgs_c_i(const orc_state* gs, const orc_state* g, const orc_aux*
         int cur = gs->c_i[s] == c1 ? 0 : 1;
         logpgs += log(probs[cur]);
     }
+    two_tabs_free(&T);
     return logpgs;
 }
 
@@ -103,15 +123,18 @@ int orc_restricted_gibbs(const int* S, int nS, orc_state* s, int i1, int i2, con
                          int t, orc_rng* r, int fast) {
     const int d = A->d;
     int c1 = s->c_i[i1], c2 = s->c_i[i2];
+    g_tables = fast >= 2;
     for (int iter = 0; iter < t; ++iter) {
         int n1 = 0, n2 = 0;
         if (fast) { n1 = count_eq(s->c_i, A->n, c1); n2 = count_eq(s->c_i, A->n, c2); }
+        two_tabs T = {{NULL, NULL}};
+        if (fast >= 2 && A->codes) two_tabs_make(&T, A, s->sigma + (size_t)c1 * d, s->sigma + (size_t)c2 * d);
         for (int q = 0; q < nS; q++) {
             int sp = S[q];
             double probs[2];
             for (int k = 0; k < 2; k++) {
                 int cls = k == 0 ? c1 : c2;
-                double H = row_ll(A, sp, s->center + (size_t)cls * d, s->sigma + (size_t)cls * d);
+                double H = row_ll_k(A, &T, k, sp, s->center + (size_t)cls * d, s->sigma + (size_t)cls * d);
                 int n = fast ? (k == 0 ? n1 : n2) - (s->c_i[sp] == cls)
                              : count_eq(s->c_i, A->n, cls) - (s->c_i[sp] == cls);
                 probs[k] = log((double)n) + H;
@@ -126,13 +149,14 @@ int orc_restricted_gibbs(const int* S, int nS, orc_state* s, int i1, int i2, con
             probs[1] = probs[1] / sum;
             int pick;
             int st = orc_sample_prob1(r, probs, 2, &pick);
-            if (st) return st;
+            if (st) { two_tabs_free(&T); return st; }
             int newc = pick == 0 ? c1 : c2;
             if (fast && newc != s->c_i[sp]) {
                 if (s->c_i[sp] == c1) { n1--; n2++; } else { n2--; n1++; }
             }
             s->c_i[sp] = newc;
         }
+        two_tabs_free(&T);
         int idx[2] = {c1, c2};
         int st = orc_update_phi(r, A, s, idx, 2);
         if (st) return st;
@@ -147,6 +171,17 @@ static double loglikelihood_hamming(const orc_state* s, int c, const orc_aux* A)
     double ll = 0.0;
     const double* cen = s->center + (size_t)c * A->d;
     const double* sig = s->sigma + (size_t)c * A->d;
+    if (tabs_on(A)) {
+        double* t = (double*)malloc(sizeof(double) * 2 * (size_t)A->d);
+        orc_cluster_table(A, sig, t);
+        for (int i = 0; i < A->n; i++)
+            if (s->c_i[i] == c) {
+                const uint8_t* x = A->codes + (size_t)i * A->d;
+                for (int j = 0; j < A->d; j++) ll += t[2 * j + ((int)x[j] != (int)cen[j])];
+            }
+        free(t);
+        return ll;
+    }
     for (int i = 0; i < A->n; i++)
         if (s->c_i[i] == c)
             for (int j = 0; j < A->d; j++)
@@ -278,6 +313,7 @@ int orc_split_and_merge(orc_state* s, const orc_aux* A, int t, int rr, int idx_1
     int i1 = idx_1_sm, i2;
     (void)i1;
     *accepted = 0;
+    g_tables = fast >= 2;
     /* sample(seq(0, n-1), 2, FALSE): EmpiricalSample without replacement */
     {
         int nn = n;

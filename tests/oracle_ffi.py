@@ -62,6 +62,10 @@ def lib():
         L.orc_ffi_compute_loglikelihood.argtypes = [_f64p, C.c_int, C.c_int, _i32p, _i32p, C.c_int,
                                                     _f64p, _f64p]
         L.orc_ffi_compute_loglikelihood.restype = C.c_double
+        L.orc_ffi_compute_loglikelihood_opt.argtypes = L.orc_ffi_compute_loglikelihood.argtypes
+        L.orc_ffi_compute_loglikelihood_opt.restype = C.c_double
+        L.orc_ffi_set_threads.argtypes = [C.c_int]
+        L.orc_ffi_set_threads.restype = None
         L.orc_ffi_pool_generate.argtypes = [_i32p, C.c_int, _f64p, _f64p, C.c_int64, _f64p, _f64p,
                                             _i32p]
         L.orc_ffi_restricted_gibbs.argtypes = [_f64p, C.c_int, C.c_int, _i32p, _f64p, _f64p, _i32p,
@@ -124,9 +128,27 @@ def set_hig_logspace(on: bool):
 
 
 # ----------------------------------------------------------------- model
+_cm_cache = {}
+
+
 def colmajor(codes: np.ndarray) -> np.ndarray:
-    """N x D integer codes -> column-major float64 buffer (Rcpp::NumericMatrix layout)."""
-    return np.ascontiguousarray(np.asarray(codes, np.float64).T).reshape(-1)
+    """N x D integer codes -> column-major float64 buffer (Rcpp::NumericMatrix layout).
+    The last large conversion is memoised (the BASELINE-size cases reuse one matrix)."""
+    codes = np.asarray(codes)
+    if codes.size < 1_000_000:
+        return np.ascontiguousarray(np.asarray(codes, np.float64).T).reshape(-1)
+    key = (codes.__array_interface__["data"][0], codes.shape, codes.strides, codes.dtype.str)
+    hit = _cm_cache.get(key)
+    if hit is None or hit[0] is not codes:
+        _cm_cache.clear()
+        hit = (codes, np.ascontiguousarray(np.asarray(codes, np.float64).T).reshape(-1))
+        _cm_cache[key] = hit
+    return hit[1]
+
+
+def set_threads(n: int):
+    """OpenMP threads of the optimised oracle (fast=2); 0 = the runtime default."""
+    lib().orc_ffi_set_threads(int(n))
 
 
 def loglik_matrix(codes, attrisize, centers, sigma):
@@ -147,7 +169,7 @@ class OracleState:
     def __init__(self, c_i, K, centers, sigma, cap=None):
         n = len(c_i)
         d = centers.shape[1]
-        cap = cap or (n + 2)
+        cap = cap or (n + 2)          # BASELINE-size cases pass a smaller cap (clusters, not points)
         self.c_i = np.ascontiguousarray(c_i, np.int32).copy()
         self.K = int(K)
         self.centers = np.zeros((cap, d), np.float64)
@@ -195,10 +217,11 @@ def update_phi(codes, attrisize, v, w, state: OracleState, rng, idx=None):
     return st
 
 
-def compute_loglikelihood(codes, attrisize, state: OracleState):
+def compute_loglikelihood(codes, attrisize, state: OracleState, fast=1):
     codes = np.asarray(codes)
     n, d = codes.shape
-    return lib().orc_ffi_compute_loglikelihood(colmajor(codes), n, d,
+    f = lib().orc_ffi_compute_loglikelihood_opt if fast >= 2 else lib().orc_ffi_compute_loglikelihood
+    return f(colmajor(codes), n, d,
                                                np.ascontiguousarray(attrisize, np.int32), state.c_i,
                                                state.K, np.ascontiguousarray(state.centers[:state.K]).reshape(-1),
                                                np.ascontiguousarray(state.sigma[:state.K]).reshape(-1))
