@@ -175,45 +175,84 @@ def cuda_sync():
         pass
 
 
-def cpu_baseline(ds, eng, m: int, budget_s: float):
-    """Reference-faithful CPU restatement (oracle/, O(N) bookkeeping per point as in
-    code/neal8.cpp) timed on a bounded sample of consecutive sample_allocation calls
-    from the middle of a sweep on the current chain state, extrapolated to one sweep."""
+def host_cpu():
+    """CPU model and the cores this process may use (the GPU box shares a larger host)."""
+    model = "unknown"
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return model, len(os.sched_getaffinity(0)), os.cpu_count()
+
+
+def cpu_baseline(ds, eng, m: int, budget_s: float, opt_threads: int):
+    """The CPU baselines of SURVEY 8(d), timed on this host on the current chain state with
+    the engine's latent pool (oracle/ is the checker; these legs only time it):
+      1. reference-faithful restatement (O(N) bookkeeping per point as in code/neal8.cpp,
+         one core, as the single-threaded reference): a full sweep when it fits the budget
+         (C2), else consecutive sample_allocation calls from the middle of a sweep,
+         extrapolated to one sweep;
+      2. optimised oracle (oracle/src/fast.c: same trace; log-likelihoods in parallel on
+         `opt_threads` threads, serial scan on one): one full sweep + update_phi +
+         compute_loglikelihood, the step the GPU is timed on."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import ctypes as C
     import oracle_ffi as O  # cpu_baseline leg only
     c, cen, sig = eng.get_state()
-    P = 30_000                      # per-point cost is independent of the pool size
+    P = ds.n * m
+    pc, ps = eng.get_pool(P)
     st = O.seed_state(99)
-    pc, ps, _ = O.pool_generate(ds.attrisize, ds.v, ds.w, P, st)
     data_cm = O.colmajor(ds.codes)
     att = np.ascontiguousarray(ds.attrisize, np.int32)
+    model, cores, ncpu = host_cpu()
 
-    def run(first, count):
-        ost = O.OracleState(c, cen.shape[0], cen, sig)
-        import ctypes as C
+    def run(first, count, fast=0):
+        ost = O.OracleState(c, cen.shape[0], cen, sig, cap=max(4096, 2 * cen.shape[0]))
         K = C.c_int(ost.K)
         t0 = time.perf_counter()
         r = O.lib().orc_ffi_neal8_sweep(data_cm, ds.n, ds.d, att, ds.gamma, np.ascontiguousarray(ds.v),
                                         np.ascontiguousarray(ds.w), ost.c_i, C.byref(K), ost.centers.reshape(-1),
-                                        ost.sigma.reshape(-1), ost.cap, m, pc.reshape(-1), ps.reshape(-1), P, st,
-                                        0, first, count)
-        return time.perf_counter() - t0, r
+                                        ost.sigma.reshape(-1), ost.cap, m, pc.reshape(-1), ps.reshape(-1), P,
+                                        st.copy(), fast, first, count)
+        ost.K = K.value
+        return time.perf_counter() - t0, r, ost
 
-    mid = ds.n // 2
-    t_probe, _ = run(mid, 4)
+    t_probe, _, _ = run(ds.n // 2, 4)
     per = max(t_probe / 4, 1e-7)
-    count = int(min(max(budget_s / per, 8), ds.n - mid))
-    t, r = run(mid, count)
+    if per * ds.n <= budget_s:
+        first, count = 0, ds.n
+    else:
+        first = ds.n // 2
+        count = int(min(max(budget_s / per, 8), ds.n - first))
+    t, r, _ = run(first, count)
     per_point = t / count
-    return {
+    full = count == ds.n
+    faithful = {
         "value": 1.0 / (per_point * ds.n),
         "unit": "sweeps/s",
         "cores": 1,
         "kind": "port",
-        "sample": (f"{count} consecutive sample_allocation calls (points {mid}..{mid + count - 1}) of one sweep, "
-                   f"reference-faithful O(N) bookkeeping, {t:.1f} s, extrapolated x{ds.n / count:.0f} to a full "
-                   f"sweep (update_phi excluded); latent pool {P} prior draws"),
+        "sample": (f"{'one full sweep' if full else f'{count} consecutive sample_allocation calls (points {first}..{first + count - 1}) of one sweep'}"
+                   f", reference-faithful O(N) bookkeeping, {t:.1f} s"
+                   f"{'' if full else f', extrapolated x{ds.n / count:.0f} to a full sweep'} (update_phi excluded); "
+                   f"engine's latent pool ({P} entries); host {model}, {cores} of {ncpu} CPUs usable"),
     }
+    O.set_threads(opt_threads)
+    t, r, ost = run(0, -1, fast=2)
+    t0 = time.perf_counter()
+    O.update_phi(ds.codes, ds.attrisize, ds.v, ds.w, ost, st.copy())
+    O.compute_loglikelihood(ds.codes, ds.attrisize, ost, fast=2)
+    t_rest = time.perf_counter() - t0
+    faithful["optimised"] = {
+        "value": 1.0 / (t + t_rest), "unit": "sweeps/s", "cores": opt_threads, "kind": "port",
+        "sample": (f"one full step of the optimised oracle (oracle/src/fast.c, same trace): sweep {t:.2f} s "
+                   f"(log-likelihoods on {opt_threads} threads, serial scan) + update_phi + compute_loglikelihood "
+                   f"{t_rest:.2f} s; host {model}"),
+    }
+    return faithful
 
 
 def main():
@@ -232,9 +271,14 @@ def main():
     ap.add_argument("--hig-logspace", choices=("auto", "on", "off"), default="auto",
                     help="HDPM_OPT_HIG_LOGSPACE (log-space 2F1, an extension): auto = on with --sm, where "
                          "clusters of thousands of members overflow the reference's series (it throws)")
+    ap.add_argument("--init", choices=("truth", "one", "random20"), default="truth",
+                    help="initial labels: the generator's ground truth (la:32-39, L = 0), one cluster (L = 1), or a "
+                         "random assignment to 20 labels (la:31, the scripts' L = 20): the unconverged regime")
     ap.add_argument("--start-iter", type=int, default=0,
                     help="first iteration index (0: the warmup includes iteration 0's pool regeneration)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the optimised CPU baseline (0: the usable CPUs, at most 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-csv", action="append", default=None,
                     help="rocprofv3 --pmc counter_collection CSV(s) with FETCH_SIZE / WRITE_SIZE of this workload "
@@ -265,9 +309,10 @@ def main():
         eng.set_hig_logspace(True)
     if os.environ.get("HDPM_BENCH_HOST_POOL"):
         eng.set_debug(64)                        # sequential host pool generator (A/B runs)
-    params = eng.chain_params(m=args.m, iterations=args.steps + args.warmup, L=0, burnin=0, neal8=True,
+    L, ci = {"truth": (0, ds.truth), "one": (1, np.zeros(ds.n, np.int32)), "random20": (20, None)}[args.init]
+    params = eng.chain_params(m=args.m, iterations=args.steps + args.warmup, L=L, burnin=0, neal8=True,
                               split_merge=args.sm, t=10, r=10)
-    eng.init_chain(params, c_i=ds.truth)         # la:27-77, L = 0 (ground truth) path
+    eng.init_chain(params, c_i=ci)               # la:27-77
     setup_s = time.perf_counter() - t_setup
     st_init = eng.stats()
     it = args.start_iter                         # iteration 0 regenerates the pool (la:123-129)
@@ -336,7 +381,8 @@ def main():
             "workload": (f"{args.config}: {CONFIGS.get(args.config, {}).get('name', args.config)}, N={ds.n} D={ds.d} "
                          f"m={args.m}; one step = Neal-8 sweep + update_phi"
                          f"{' + split-merge (t=r=10)' if args.sm else ''} + compute_loglikelihood "
-                         f"(code/launcher.cpp:94-132), ground-truth init"),
+                         f"(code/launcher.cpp:94-132), "
+                         f"{ {'truth': 'ground-truth init', 'one': 'one-cluster init (L=1)', 'random20': 'random init, L=20'}[args.init]}"),
             "n": ds.n, "d": ds.d, "m": args.m, "K_final": K, "parallelism": f"replicas{ws}",
             "ranks": ranks,
             "sweep_effective_GBps": round(survey_sweep_bytes(ds.n, ds.d, args.m) * args.steps / elapsed / 1e9, 2),
@@ -376,8 +422,22 @@ def main():
         },
         "cpu_baseline": None,
     }
+    regen = out["config"]["pool_generation"]["regeneration"]
+    if regen:
+        # the la:85-154 loop rate: the timed step plus the pool regeneration of every 1000th
+        # iteration (la:123-129, outside the timed window) amortised over its cadence
+        out["config"]["full_loop"] = {
+            "value": round(ws * 1e3 / (1e3 * elapsed / args.steps + regen["amortised_ms_per_iteration"]), 2),
+            "unit": "sweeps/s", "what": "value with the latent pool regeneration (la:123-129) amortised per iteration"}
+    # byte models: what the certified sweep moves vs SURVEY 8(d)'s direct design
+    out["config"]["byte_model"] = {
+        "certified_prepass_bytes_per_sweep": bpp * ds.n,
+        "survey_8d_bytes_per_sweep": survey_sweep_bytes(ds.n, ds.d, args.m),
+        "note": "the sweep proves 'stay' from bounds for most points (DESIGN.md 4.3-4.4) and moves the prepass bytes; "
+                "SURVEY 8(d)'s N(D(2+9m)+8) is the direct design's traffic and is not the roofline of this path"}
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(ds, eng, args.m, args.cpu_baseline_seconds)
+        thr = args.cpu_threads or min(16, host_cpu()[1])
+        out["cpu_baseline"] = cpu_baseline(ds, eng, args.m, args.cpu_baseline_seconds, thr)
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()
