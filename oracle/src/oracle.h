@@ -35,7 +35,7 @@ extern "C" {
 #define ORC_E_VALIDATE    1   /* validate_state -> Rcpp::stop (cf:146-172)            */
 #define ORC_E_GSL         2   /* norm_const2 throw std::runtime_error (hg:38-45)        */
 #define ORC_E_PROB        3   /* FixupProb stop(): NA / negative / too few positive      */
-#define ORC_E_WALKER      4   /* Walker alias branch (>200 categories) not restated      */
+#define ORC_E_WALKER      4   /* (no longer returned: Walker alias sampling is restated)  */
 #define ORC_E_ARG         5   /* bad argument / allocation failure                       */
 
 /* ---- R MT19937 (R src/main/RNG.c: MT_genrand, RNG_Init, fixup) ---- */

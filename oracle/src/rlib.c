@@ -132,6 +132,34 @@ void orc_revsort(double* a, int* ib, int n) {
     }
 }
 
+/* Walker's alias draw (Rcpp sugar sample.h WalkerSample, restated from R src/main/random.c
+ * walker_ProbSampleReplace): the table over the FixupProb-normalised p, then one uniform:
+ * rU = unif_rand() * n, k = (int) rU, pick k if rU < q[k] + k else its alias a[k].
+ * HL holds the entries with q < 1 from the front and the others from the back.  R leaves
+ * a[] uninitialised for entries the loop never assigns (they keep q >= 1 in exact
+ * arithmetic); here they alias themselves. */
+static int walker_pick(const double* p, int n, double u, int* HL, double* q, int* a) {
+    int h = -1, l = n;
+    for (int i = 0; i < n; i++) {
+        q[i] = p[i] * n;
+        a[i] = i;
+        if (q[i] < 1.) HL[++h] = i; else HL[--l] = i;
+    }
+    if (h >= 0 && l < n) {
+        for (int k = 0; k < n - 1; k++) {
+            const int i = HL[k], j = HL[l];
+            a[i] = j;
+            q[j] += q[i] - 1;
+            if (q[j] < 1.) l++;
+            if (l >= n) break;
+        }
+    }
+    for (int i = 0; i < n; i++) q[i] += i;
+    const double rU = u * n;
+    const int k = (int)rU;
+    return rU < q[k] ? k : a[k];
+}
+
 /* sample(x, 1, TRUE, probs): FixupProb -> (Walker if >200) -> SampleReplace.
  * Returns the 0-based position into x.  probs is not modified (Rcpp clones it). */
 static int sample_prob1_impl(orc_rng* r, double rU_given, const double* probs, int n, int* out_index);
@@ -169,7 +197,15 @@ static int sample_prob1_impl(orc_rng* r, double rU_given, const double* probs, i
     {
         int nc = 0;
         for (int i = 0; i < n; i++) nc += (n * p[i] > 0.1);
-        if (nc > 200) { st = ORC_E_WALKER; goto done; }
+        if (nc > 200) {                                   /* Walker alias (> 200 categories) */
+            int* HL = (int*)malloc(sizeof(int) * (size_t)n);
+            int* a = (int*)malloc(sizeof(int) * (size_t)n);
+            double* q = (double*)malloc(sizeof(double) * (size_t)n);
+            if (!HL || !a || !q) st = ORC_E_ARG;
+            else *out_index = walker_pick(p, n, r ? orc_unif_rand(r) : rU_given, HL, q, a);
+            free(HL); free(a); free(q);
+            goto done;
+        }
     }
     /* SampleReplace, k = 1 */
     {

@@ -1815,7 +1815,7 @@ struct Ctx {
       stats.checked_rounds += c.checked;
       if (c.status) {
         err = c.status == kValidate ? "State validation failed: inconsistent cluster count from Neal8 case 2"
-              : c.status == kWalker ? "more than 200 categories: Walker alias sampling is not supported"
+              : c.status == kWalker ? "Walker alias table failure"
               : c.status == kProb   ? "Too few positive probabilities"
                                     : "resolver failure";
         return c.status;
@@ -1929,6 +1929,7 @@ struct Ctx {
 
   struct PhiItem {
     int err, lstar;
+    int mode;                // sample_prob1_prep: 0 cumulative, 1 Walker alias table
     bool bp;                 // rhig beta path for lstar
     RBeta rb;                // rbeta(w + 1, v - 1) setup for lstar
     // phase B -> C
@@ -2080,9 +2081,11 @@ struct Ctx {
       PhiItem& P = phi_items[(size_t)t * d + j];
       double* cum = &phi_cum[(size_t)t * pj.sumatt + phi_off[j]];
       int* perm = &phi_perm[(size_t)t * pj.sumatt + phi_off[j]];
-      P.err = -sample_prob1_prep(prob, mj, cum, perm);
+      const int mode = sample_prob1_prep(prob, mj, cum, perm);
+      P.err = mode < 0 ? -mode : 0;
+      P.mode = mode;
       P.lstar = -1;
-      if (P.err) continue;
+      if (P.err || mode == 1) continue;       // no likely center to speculate on (Walker)
       const int l = perm[0] - 1;
       const double sumdelta = (double)fj[l];
       const double nw_ = w[j] + nn - sumdelta, nv_ = v[j] + sumdelta;
@@ -2119,7 +2122,7 @@ struct Ctx {
       const PhiItem& P = phi_items[(size_t)t * d + j];
       if (P.err) return P.err;
       const size_t o = (size_t)t * sumatt + phi_off[j];
-      cen[j] = (uint8_t)(sample_prob1_pick(&phi_cum[o], &phi_perm[o], att[j], sa.next(nullptr)) + 1);
+      cen[j] = (uint8_t)(sample_prob1_pick(&phi_cum[o], &phi_perm[o], att[j], sa.next(nullptr), P.mode) + 1);
     }
     // sigma draws.  Items go in batches of up to kSpec whose first rbeta attempts are
     // evaluated together at the stream positions they have if every earlier item of the

@@ -593,6 +593,37 @@ __device__ void dev_revsort(double* a0, int* ib0, int n) {
   }
 }
 
+// Walker's alias draw (Rcpp sugar WalkerSample, R random.c walker_ProbSampleReplace) for
+// n > 200 effective categories, serial on one lane: q holds the FixupProb-normalised
+// probabilities (overwritten with the table), w is scratch packing the alias (low 16 bits)
+// and the small/large work list HL (high 16 bits) of each entry; n < 65536.  One uniform u:
+// rU = u n, k = (int) rU, k if rU < q[k] + k else alias[k].  Same operations as the host's
+// walker_table / sample_prob1_pick (rmath.hpp) and the oracle.
+__device__ int dev_walker(double* q, int* w, int n, double u) {
+  auto hl = [&](int pos) { return (int)((unsigned)w[pos] >> 16); };
+  auto set_hl = [&](int pos, int v) { w[pos] = (int)(((unsigned)w[pos] & 0xffffu) | ((unsigned)v << 16)); };
+  auto set_a = [&](int i, int v) { w[i] = (int)(((unsigned)w[i] & 0xffff0000u) | (unsigned)v); };
+  for (int i = 0; i < n; i++) w[i] = i;
+  int h = -1, l = n;
+  for (int i = 0; i < n; i++) {
+    q[i] = q[i] * n;
+    if (q[i] < 1.) set_hl(++h, i); else set_hl(--l, i);
+  }
+  if (h >= 0 && l < n) {
+    for (int k = 0; k < n - 1; k++) {
+      const int i = hl(k), j = hl(l);
+      set_a(i, j);
+      q[j] += q[i] - 1;
+      if (q[j] < 1.) l++;
+      if (l >= n) break;
+    }
+  }
+  for (int i = 0; i < n; i++) q[i] += i;
+  const double rU = u * n;
+  const int k = (int)rU;
+  return rU < q[k] ? k : (w[k] & 0xffff);
+}
+
 __device__ __forceinline__ double readlane_f64(double x, int l) {
   const uint64_t u = __double_as_longlong(x);
   const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, l), hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), l);
@@ -653,7 +684,15 @@ __device__ int decide_values(double (&pv)[RE], int E, double rU, double* lp, int
     pv[r] = in ? pv[r] / s2 : 0.0;
     nc += __popcll(__ballot(in && (double)E * pv[r] > 0.1));
   }
-  if (nc > 200) return -4;  // kWalker
+  if (nc > 200) {          // Walker's alias method (Rcpp sample() with > 200 categories)
+#pragma unroll
+    for (int r = 0; r < RE; ++r)
+      if (r * kWave + lane < E) lp[r * kWave + lane] = pv[r];
+    wave_sync();
+    if (lane == 0) *lpick = dev_walker(lp, lperm, E, rU);
+    wave_sync();
+    return *lpick;
+  }
   double pmax = pv[0];
 #pragma unroll
   for (int r = 1; r < RE; ++r) pmax = fmax(pmax, pv[r]);
@@ -829,8 +868,12 @@ __device__ int exact_decision_lds(const ResolveArgs& a, const RState& st, int K,
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) nc += __shfl_xor(nc, o);
-  if (nc > 200) return -4;
   wave_sync();
+  if (nc > 200) {          // Walker's alias method
+    if (lane == 0) st.sh->pick = dev_walker(st.p, st.perm, E, rU);
+    wave_sync();
+    return st.sh->pick;
+  }
   if (lane == 0) {
     for (int e = 0; e < E; ++e) st.perm[e] = e + 1;
     dev_revsort(st.p, st.perm, E);

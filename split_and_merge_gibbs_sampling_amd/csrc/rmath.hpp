@@ -29,7 +29,7 @@ enum Status : int {
   kValidate = 1,   // validate_state -> Rcpp::stop (cf:146-172)
   kGsl = 2,        // norm_const2 throws (hg:38-45)
   kProb = 3,       // FixupProb stop()
-  kWalker = 4,     // Walker alias (>200 categories): not supported
+  kWalker = 4,     // (no longer returned: Walker alias sampling is restated)
   kArg = 5,        // bad argument / capacity
   kDevice = 6,     // HIP runtime failure
   kNoDevice = 7,   // no HIP device / extension unusable
@@ -167,6 +167,34 @@ inline void revsort(double* a0, int* ib0, int n) {
 // sample(x, 1, TRUE, probs) split into its parameter-only part -- FixupProb, the Walker
 // check, revsort and the cumulative sums, into p (n doubles) and perm (n ints) -- and the
 // pick for the uniform rU.  prep returns 0 or a negative Status.
+// Walker's alias table (Rcpp sugar WalkerSample, R random.c walker_ProbSampleReplace) over
+// the FixupProb-normalised p: q[i] = p[i] n, entries with q < 1 listed from the front of HL
+// and the others from the back, each small entry aliased to the current large one; then
+// q[i] += i.  On return p holds q and a the aliases (entries the loop never assigns keep
+// q >= 1 in exact arithmetic; R leaves their alias uninitialised, here they alias themselves).
+inline void walker_table(double* p, int* a, int n) {
+  std::vector<int> HL((size_t)n);
+  int h = -1, l = n;
+  for (int i = 0; i < n; i++) {
+    p[i] = p[i] * n;
+    a[i] = i;
+    if (p[i] < 1.) HL[++h] = i; else HL[--l] = i;
+  }
+  if (h >= 0 && l < n) {
+    for (int k = 0; k < n - 1; k++) {
+      const int i = HL[k], j = HL[l];
+      a[i] = j;
+      p[j] += p[i] - 1;
+      if (p[j] < 1.) l++;
+      if (l >= n) break;
+    }
+  }
+  for (int i = 0; i < n; i++) p[i] += i;
+}
+
+// FixupProb, then either the cumulative sums in revsort order (returns 0; p = cumulative
+// probabilities, perm = 1-based indices) or, with more than 200 entries of n p > 0.1,
+// Walker's alias table (returns 1; p = q + i, perm = aliases).  Negative: a Status.
 inline int sample_prob1_prep(const double* probs, int n, double* p, int* perm) {
   double sum = 0.0;
   int npos = 0;
@@ -179,14 +207,23 @@ inline int sample_prob1_prep(const double* probs, int n, double* p, int* perm) {
   for (int i = 0; i < n; i++) p[i] = probs[i] / sum;
   int nc = 0;
   for (int i = 0; i < n; i++) nc += (n * p[i] > 0.1);
-  if (nc > 200) return -kWalker;
+  if (nc > 200) {
+    walker_table(p, perm, n);
+    return 1;
+  }
   for (int i = 0; i < n; i++) perm[i] = i + 1;
   revsort(p, perm, n);
   for (int i = 1; i < n; i++) p[i] += p[i - 1];
   return 0;
 }
 
-inline int sample_prob1_pick(const double* cum, const int* perm, int n, double rU) {
+// The draw with its uniform rU; mode = sample_prob1_prep's return (0 or 1).
+inline int sample_prob1_pick(const double* cum, const int* perm, int n, double rU, int mode = 0) {
+  if (mode == 1) {                       // Walker: rU n, k = (int) rU n, k or its alias
+    const double r = rU * n;
+    const int k = (int)r;
+    return r < cum[k] ? k : perm[k];
+  }
   int j;
   for (j = 0; j < n - 1; j++)
     if (rU <= cum[j]) break;
@@ -198,7 +235,7 @@ inline int sample_prob1_pick(const double* cum, const int* perm, int n, double r
 inline int sample_prob1_u(const double* probs, int n, double rU, double* p, int* perm) {
   const int st = sample_prob1_prep(probs, n, p, perm);
   if (st < 0) return st;
-  return sample_prob1_pick(p, perm, n, rU);
+  return sample_prob1_pick(p, perm, n, rU, st);
 }
 
 inline int sample_prob1(Rng& rng, const double* probs, int n, std::vector<double>& p,

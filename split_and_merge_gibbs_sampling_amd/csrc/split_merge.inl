@@ -201,7 +201,7 @@ static int hupdate_phi_one(Ctx* c, HState& s, int k, const Freq& F) {
   c->rng_sync();
   for (int j = 0; j < c->d; ++j) {
     if (pst[j] < 0) return -pst[j];           // validation precedes the draw
-    const int pick = sample_prob1_pick(&cum[(size_t)j * mm], &perm[(size_t)j * mm], c->att[j], c->rng.unif());
+    const int pick = sample_prob1_pick(&cum[(size_t)j * mm], &perm[(size_t)j * mm], c->att[j], c->rng.unif(), pst[j]);
     cen[j] = (uint8_t)(pick + 1);
   }
   for (int j = 0; j < c->d; ++j) {

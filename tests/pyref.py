@@ -102,7 +102,7 @@ def sample_prob1(rng: RRng, probs) -> int:
             tot += x
     p = [x / tot for x in p]
     if sum(1 for x in p if n * x > 0.1) > 200:
-        raise NotImplementedError("Walker")
+        return walker(p, rng.unif())
     perm = list(range(1, n + 1))
     revsort(p, perm)
     for i in range(1, n):
@@ -112,6 +112,30 @@ def sample_prob1(rng: RRng, probs) -> int:
     while j < n - 1 and not (rU <= p[j]):
         j += 1
     return perm[j] - 1
+
+
+def walker(p, u) -> int:
+    """R random.c walker_ProbSampleReplace (Rcpp WalkerSample), one draw, 0-based."""
+    n = len(p)
+    q = [x * n for x in p]
+    small = [i for i in range(n) if q[i] < 1.0]
+    large = [i for i in range(n) if not q[i] < 1.0]
+    HL = small + large[::-1]                 # smalls from the front, larges from the back
+    a = list(range(n))
+    lpos = len(small)                        # *L: first entry of the large region
+    if small and large:
+        for k in range(n - 1):
+            i, j = HL[k], HL[lpos]
+            a[i] = j
+            q[j] += q[i] - 1
+            if q[j] < 1.0:
+                lpos += 1
+            if lpos >= n:
+                break
+    q = [q[i] + i for i in range(n)]
+    rU = u * n
+    k = int(rU)
+    return k if rU < q[k] else a[k]
 
 
 def rbeta(rng: RRng, aa: float, bb: float) -> float:

@@ -149,3 +149,88 @@ def test_draw_on_every_cumulative_boundary(eng, E):
                 if not 0.0 < rU < 1.0:
                     continue
                 assert eng.debug_draw(logw, rU) == ref_draw(logw, rU), (E, trial, rU)
+
+
+# ------------------------------------------------------------------ Walker alias (> 200)
+@pytest.mark.parametrize("E", [230, 256])
+def test_walker_draws_match_reference(eng, E):
+    """More than 200 entries with n p > 0.1: Rcpp's sample() uses Walker's alias method
+    (R random.c walker_ProbSampleReplace); the device's n8 draw builds the same table."""
+    rng = np.random.default_rng(E)
+    for trial in range(10):
+        logw = list(rng.normal(0.0, 0.3, E))
+        if trial % 2:
+            logw[0] += 3.0                          # one heavy entry
+        p = np.exp(np.array(logw) - max(logw))
+        assert (E * p / p.sum() > 0.1).sum() > 200  # the Walker branch of Rcpp sample()
+        for rU in list(rng.random(20)) + [1e-9, 0.5, 1 - 1e-9]:
+            assert eng.debug_draw(logw, float(rU)) == ref_draw(logw, float(rU)), (E, trial, rU)
+
+
+def _walker_dataset():
+    from split_and_merge_gibbs_sampling_amd.data import Dataset
+    rng = np.random.default_rng(17)
+    att = np.array([250, 4, 2, 3], np.int32)
+    n = 480
+    codes = np.stack([rng.integers(1, a + 1, size=n) for a in att], axis=1).astype(np.uint8)
+    return Dataset(codes, att, np.full(4, 6.0), np.full(4, 0.25), 0.68, np.zeros(n, np.int32), "walker")
+
+
+def test_walker_update_phi_center_draws(hd_mod, oracle):
+    """update_phi's center draw over an attribute with m_j = 250 levels: a small cluster with
+    a large sigma has near-flat level probabilities, so sample(1:m_j, 1, TRUE, prob)
+    (cf:199) takes Walker's path on the host as in the reference."""
+    ds = _walker_dataset()
+    K = 160
+    c = (np.arange(ds.n) % K).astype(np.int32)
+    rng = np.random.default_rng(3)
+    cen = np.stack([rng.integers(1, ds.attrisize + 1) for _ in range(K)]).astype(np.float64)
+    sig = rng.uniform(2.0, 6.0, size=(K, ds.d))
+    st = oracle.seed_state(12)
+    e = hd_mod.Engine(0)
+    e.set_data(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w)
+    e.set_state(c, cen, sig)
+    e.rng_state = st
+    ost = oracle.OracleState(c, K, cen, sig)
+    for _ in range(3):
+        e.update_phi()
+        assert oracle.update_phi(ds.codes, ds.attrisize, ds.v, ds.w, ost, st) == 0
+        c2, cen2, sig2 = e.get_state()
+        assert np.array_equal(cen2, ost.centers[:K]) and np.array_equal(sig2, ost.sigma[:K])
+        assert np.array_equal(e.rng_state, st)
+    e.close()
+
+
+@pytest.mark.parametrize("K", [240, 480])
+def test_walker_neal8_sweeps(hd_mod, oracle, K):
+    """Neal-8 draws over K + m > 200 comparable entries (n8:99-102 -> Walker): K = 240
+    exercises the register path of the device draw, K = 480 (every point its own cluster)
+    the LDS path."""
+    ds = _walker_dataset()
+    c = (np.arange(ds.n) % K).astype(np.int32)
+    rng = np.random.default_rng(4)
+    cen = np.stack([rng.integers(1, ds.attrisize + 1) for _ in range(K)]).astype(np.float64)
+    sig = rng.uniform(3.0, 8.0, size=(K, ds.d))
+    st = oracle.seed_state(13)
+    pc, ps, _ = oracle.pool_generate(ds.attrisize, ds.v, ds.w, ds.n * 3, st)
+    e = hd_mod.Engine(0)
+    e.set_data(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w)
+    e.set_state(c, cen, sig)
+    e.set_pool(pc, ps)
+    e.rng_state = st
+    ost = oracle.OracleState(c, K, cen, sig)
+    for _ in range(2):
+        e.neal8_sweep(3)
+        assert oracle.neal8_sweep(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w, ost, 3, pc, ps, st, fast=1) == 0
+        c2, cen2, sig2 = e.get_state()
+        assert cen2.shape[0] == ost.K and np.array_equal(c2, ost.c_i)
+        assert np.array_equal(cen2, ost.centers[:ost.K]) and np.array_equal(sig2, ost.sigma[:ost.K])
+        assert np.array_equal(e.rng_state, st)
+    e.close()
+
+
+@pytest.fixture(scope="module")
+def hd_mod():
+    import split_and_merge_gibbs_sampling_amd as hd
+    hd.build()
+    return hd

@@ -100,6 +100,39 @@ def test_sample_prob1_matches_pyref(oracle):
             assert s == 0 and got == P.sample_prob1(r, list(p))
 
 
+def test_walker_alias_matches_pyref(oracle):
+    """> 200 entries with n p > 0.1 after FixupProb: Rcpp's sample() switches to Walker's
+    alias method (R random.c walker_ProbSampleReplace); C oracle vs the Python restatement,
+    and the draw frequencies against p (a loose statistical check of the alias table)."""
+    rng = np.random.default_rng(31)
+    st = oracle.seed_state(5)
+    r = P.RRng(5)
+    for n in (230, 300, 403, 1000):
+        for trial in range(15):
+            p = rng.random(n) + (0.3 if trial % 2 else 1.0)
+            if n >= 400:
+                p[rng.random(n) < 0.1] = 0.0        # zero-probability entries
+            if trial % 5 == 0:
+                p[:3] *= 20.0                       # a few heavy entries
+            assert (n * p / p.sum() > 0.1).sum() > 200
+            for _ in range(4):
+                got, s = oracle.sample_prob1(st, p)
+                assert s == 0 and got == P.sample_prob1(r, list(p)), (n, trial)
+    assert np.array_equal(st, r.export())
+    # frequencies: 20000 draws over n = 300 entries with 3 heavy ones
+    n = 300
+    p = np.ones(n)
+    p[:3] = 30.0
+    p /= p.sum()
+    st = oracle.seed_state(6)
+    cnt = np.zeros(n)
+    for _ in range(20000):
+        got, s = oracle.sample_prob1(st, p)
+        cnt[got] += 1
+    assert abs(cnt[:3].sum() / 20000 - p[:3].sum()) < 0.02
+    assert abs(cnt[3:].sum() / 20000 - p[3:].sum()) < 0.02
+
+
 def test_dhamming_matches_pyref(oracle):
     for x, c, s, m in [(1, 1, 0.5, 2), (1, 2, 0.5, 2), (3, 3, 1.7, 6), (2, 5, 0.05, 6)]:
         assert oracle.lib().orc_ffi_dhamming(x, c, s, m) == P.dhamming(x, c, s, m)
