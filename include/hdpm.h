@@ -157,7 +157,9 @@ int hdpm_reset_stats(hdpm_ctx* ctx);
  * no speculative update_phi during the sweep; bit 8: no next sweep prepared at the end of
  * an iteration; bit 9: HIP events around every kernel of every launch (per-kernel times);
  * bit 10: the prepass gathers full bound records for latent picks (no pool-entry heads);
- * bit 11: exact rows one wave per point (no workgroup-per-point LDS staging). */
+ * bit 11: exact rows one wave per point (no workgroup-per-point LDS staging); bit 12: no
+ * block mode in the resolver (uncertain points decided one by one); bit 13: block mode for
+ * every resolver launch (not only after a launch that listed kResolveBlkMin points). */
 int hdpm_set_debug(hdpm_ctx* ctx, int32_t mode);
 /* The prepass's pool-entry heads, P entries of wb*Ws + 2 words padded to a power of two
  * (csrc/kernels.hpp "Pool-entry heads"); HDPM_E_ARG when the data's layout has none (d > 256, or d > 128 with

@@ -37,7 +37,7 @@ hipError_t launch_prepass(const PrepassArgs& a, int nblocks, hipStream_t s);
 hipError_t launch_cluster_summary(const PrepassArgs& a, hipStream_t s);
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s);
 hipError_t launch_exact_rows(const PrepassArgs& a, int nblocks, hipStream_t s);
-size_t resolve_smem_bytes(int scap, int m);
+size_t resolve_smem_bytes(int scap, int m, int blocks);
 hipError_t launch_relabel(int* c, const int* los, int n, const ResolveCtl* ctl, hipStream_t s);
 hipError_t launch_finish_sweep(int* counts, int* sol, int* los, int* src, int cap, const ResolveCtl* ctl, int n,
                                hipStream_t s);
@@ -547,6 +547,7 @@ struct Ctx {
   DevBuf<double> d_slot_tab;
   DevBuf<uint64_t> d_slot_bnd;
   int scap = 0;
+  int last_listed = 0;        // uncertain points of the previous resolver launch (block-mode choice)
 
   // latent pool
   int64_t P = 0;
@@ -1623,7 +1624,13 @@ struct Ctx {
       d_rprof.ensure(16);
       ra.prof = d_rprof.p;
     }
-    if (resolve_smem_bytes(ra.lcap, m) > 160 * 1024) { err = "too many clusters for the resolver (K > ~2300)"; return kArg; }
+    // block mode when the previous launch listed many uncertain points (an unconverged chain)
+    ra.blocks = (K + m <= 64 && nslots <= 64 && !(debug & 4096) && !(debug & 1) &&
+                 ((debug & 8192) || last_listed >= kResolveBlkMin)) ? 1 : 0;
+    if (resolve_smem_bytes(ra.lcap, m, ra.blocks) > 160 * 1024) {
+      err = "too many clusters for the resolver (K > ~2300)";
+      return kArg;
+    }
     HIPCHK(launch_resolve(ra, stream));
     if (round_fine) HIPCHK(hipEventRecord(ev[2], stream));
     HIPCHK(hipEventRecord(ev[6], stream));
@@ -1682,7 +1689,7 @@ struct Ctx {
     // longer path (timeline: launching the sweep first cost ~8% of the iteration rate)
     spec_launch();
     mark("ahead.spec");
-    if (launch && resolve_smem_bytes(std::min(scap, K + 2), m) <= 160 * 1024) {
+    if (launch && resolve_smem_bytes(std::min(scap, K + 2), m, K + m <= 64 ? 1 : 0) <= 160 * 1024) {
       ahead.track = freq_dev_valid;
       sweep_buffers(ahead.track);
       mark("ahead.buf");
@@ -1804,12 +1811,13 @@ struct Ctx {
         HIPCHK(hipMemcpy(tp, d_rprof.p, sizeof(tp), hipMemcpyDeviceToHost));
         std::fprintf(stderr,
                      "[resolve] init %.2f us, batches %.2f us, decided points %lld in %.2f us (exact decisions "
-                     "%.2f us), total %.2f us\n",
-                     (tp[1] - tp[0]) / 100.0, tp[3] / 100.0, tp[6], tp[4] / 100.0, tp[12] / 100.0,
+                     "%.2f us; block mode: %lld blocks), total %.2f us\n",
+                     (tp[1] - tp[0]) / 100.0, tp[3] / 100.0, tp[6], tp[4] / 100.0, tp[12] / 100.0, tp[5],
                      (tp[7] - tp[0]) / 100.0);
       }
       stats.exact_points += c.exact;
       stats.listed_points += c.listed;
+      last_listed = c.listed;
       stats.moves += c.moves;
       sweep_moves += c.moves;
       stats.checked_rounds += c.checked;

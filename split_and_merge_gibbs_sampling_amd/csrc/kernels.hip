@@ -488,8 +488,21 @@ struct RShared {
   double dvmax;        // max over slots of |logn[count] - logn[snapshot count]|
   double pad;
   long long tsub[8];   // diagnostics (resolver profiling)
+  int bgo, bq;         // block mode: continue flag, next dense-list position
 };
 constexpr int kRSharedBytes = 192;
+static_assert(sizeof(RShared) <= kRSharedBytes, "RShared");
+
+// Block mode (k_resolve_blk, one wave, for a chain far from convergence: most points
+// uncertain): the next kBlk listed points are drawn together, one lane per point, in the
+// state at the block start (the reference's draw run literally per lane, revsort included);
+// then, still in parallel, each point's draw is kept while no log-weight of it has moved by
+// its radius -- a bound from the count changes of the points before it in the block -- and
+// the block commits its points up to the first draw that is not kept or the first
+// structural move (case 2 relabels, cases 3 / 4 take a new slot and end the launch, both
+// processed by the serial path).  A block's first draw is always kept.
+constexpr int kBlk = 64;
+constexpr int kRqWin = 512;
 
 struct RState {
   RShared* sh;
@@ -504,12 +517,26 @@ struct RState {
   double* p;    // [emax]
   double* row;  // [2][emax] exact rows (double buffer)
   int* perm;    // [emax]
+  uint64_t* ltab;   // glibc's log table (logn[c] = log(c) on the device, bit for bit)
+  // block mode only (nullptr otherwise):
+  double* sl1;  // [lcap] logn[snapshot count]
+  double* sl0;  // [lcap] logn[snapshot count - 1]
+  double* bp;   // [64 entries][64 lanes] per-lane draw scratch (probabilities)
+  int* bperm;   // [64][64] per-lane revsort indices
+  int* bcmin;   // [kWave] lower bounds on the slot counts during a block's walk
+  int4* brq;    // [kRqWin] window of the listed points' inputs {row, point, slot, draw}
 };
 
-__host__ __device__ inline size_t resolve_lds_bytes(int lcap, int m) {
+__host__ __device__ inline size_t resolve_lds_bytes(int lcap, int m, int blocks) {
   const size_t emax = (size_t)lcap + (size_t)m;
-  return kRSharedBytes + emax * 4 * sizeof(double) + (size_t)lcap * 2 * sizeof(double) + (size_t)lcap * 4 * sizeof(int) +
-         emax * sizeof(int);
+  size_t b = kRSharedBytes + emax * 4 * sizeof(double) + (size_t)lcap * 2 * sizeof(double) + (size_t)lcap * 4 * sizeof(int) +
+             emax * sizeof(int);
+  b = (b + 15) & ~(size_t)15;
+  b += 256 * sizeof(uint64_t);
+  if (blocks)
+    b += (size_t)lcap * 2 * sizeof(double) + 64 * kWave * (sizeof(double) + sizeof(int)) + kWave * sizeof(int) +
+         16 + kRqWin * sizeof(int4);
+  return b;
 }
 
 __device__ __forceinline__ double wave_max(double v) {
@@ -522,9 +549,9 @@ __device__ __forceinline__ double slot_drift(const RState& st, const double* log
   const int a = st.snap[s], b = st.cnt[s];
   if (a >= 2) {
     if (b < 2) return INFINITY;
-    return fabs(logn[b - 1] - logn[a - 1]);
+    return fabs(st.l0[s] - (st.sl0 ? st.sl0[s] : logn[a - 1]));   // logn[b - 1] - logn[a - 1]
   }
-  if (a == 1) return b == 0 ? 0.0 : logn[b];
+  if (a == 1) return b == 0 ? 0.0 : st.l1[s];
   return INFINITY;
 }
 
@@ -533,8 +560,10 @@ __device__ __forceinline__ double count_drift(const RState& st, const double* lo
   const int a = st.snap[s], b = st.cnt[s];
   if (a == b) return 0.0;
   if (a < 1 || b < 1) return INFINITY;
-  return fabs(logn[b] - logn[a]);
+  return fabs(st.l1[s] - (st.sl1 ? st.sl1[s] : logn[a]));
 }
+
+
 
 // lane 0: record a reassignment for the incremental frequency tables
 __device__ __forceinline__ void log_move(const ResolveArgs& a, int& nlog, int64_t i, int from, int to) {
@@ -546,11 +575,29 @@ __device__ __forceinline__ void log_move(const ResolveArgs& a, int& nlog, int64_
   }
 }
 
-// lane 0: slot s's count changed -> refresh its log-count cache
+// logn[c] = log((double) c) as the host's table holds it (glibc's algorithm, LDS table)
+__device__ __forceinline__ double logn_dev(const RState& st, int c) {
+  return c <= 0 ? -INFINITY : glibc::log_r((double)c, st.ltab);
+}
+
+// lane 0: slot s's count changed -> refresh its log-count cache.  A count moves by one per
+// reassignment, so one of the two values is the other's old one; the new one is computed
+// (no dependent global load on the resolver's serial path).
 __device__ __forceinline__ void set_count(const RState& st, const double* logn, int s, int c) {
+  (void)logn;
+  const int old = st.cnt[s];
   st.cnt[s] = c;
-  st.l1[s] = logn[c];
-  st.l0[s] = c > 0 ? logn[c - 1] : -INFINITY;
+  if (c == old) return;
+  if (c == old - 1) {
+    st.l1[s] = st.l0[s];
+    st.l0[s] = logn_dev(st, c - 1);
+  } else if (c == old + 1) {
+    st.l0[s] = st.l1[s];
+    st.l1[s] = logn_dev(st, c);
+  } else {
+    st.l1[s] = logn_dev(st, c);
+    st.l0[s] = logn_dev(st, c - 1);
+  }
 }
 
 // Serial revsort (R sort.c) on lane 0.
@@ -590,6 +637,47 @@ __device__ void dev_revsort(double* a0, int* ib0, int n) {
     }
     a[i] = ra;
     ib[i] = ii;
+  }
+}
+
+// R's revsort on one lane's column of a [n][kWave] LDS array (a0, ib0 point at the lane's
+// entry 0; entry e at e * kWave): the same operations as dev_revsort.
+__device__ void lane_revsort(double* a0, int* ib0, int n) {
+  if (n <= 1) return;
+  auto A = [&](int x) -> double& { return a0[(x - 1) * kWave]; };
+  auto B = [&](int x) -> int& { return ib0[(x - 1) * kWave]; };
+  int l = (n >> 1) + 1, ir = n, i, j, ii;
+  double ra;
+  for (;;) {
+    if (l > 1) {
+      l = l - 1;
+      ra = A(l);
+      ii = B(l);
+    } else {
+      ra = A(ir);
+      ii = B(ir);
+      A(ir) = A(1);
+      B(ir) = B(1);
+      if (--ir == 1) {
+        A(1) = ra;
+        B(1) = ii;
+        return;
+      }
+    }
+    i = l;
+    j = l << 1;
+    while (j <= ir) {
+      if (j < ir && A(j) > A(j + 1)) ++j;
+      if (ra > A(j)) {
+        A(i) = A(j);
+        B(i) = B(j);
+        j += (i = j);
+      } else {
+        j = ir + 1;
+      }
+    }
+    A(i) = ra;
+    B(i) = ii;
   }
 }
 
@@ -798,7 +886,7 @@ __device__ int decide_values(double (&pv)[RE], int E, double rU, double* lp, int
 // resolver's current state.  Returns the drawn index in [0, K+m) or -status.
 template <int RE>
 __device__ int exact_decision_reg(const ResolveArgs& a, const RState& st, int K, const double* Lr, int own, double rU) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   K = __builtin_amdgcn_readfirstlane(K);
   own = __builtin_amdgcn_readfirstlane(own);
   const int E = K + a.m;
@@ -824,7 +912,7 @@ __device__ int exact_decision_reg(const ResolveArgs& a, const RState& st, int K,
 // LDS path for more than 256 entries.
 __device__ int exact_decision_lds(const ResolveArgs& a, const RState& st, int K, const double* Lr, int own,
                                   double rU) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   const int E = K + a.m;
   const bool singleton = st.cnt[own] == 1;
   double mx = -INFINITY;
@@ -895,7 +983,7 @@ __device__ int exact_decision(const ResolveArgs& a, const RState& st, int K, con
 }
 
 __device__ void copy_pool_params(const ResolveArgs& a, int64_t e, int s) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   const int dp = a.dp;
   for (int b = lane; b < dp; b += kWave) a.slot_codes[(int64_t)s * dp + b] = a.pool.codes[e * dp + b];
   for (int b = lane; b < 2 * a.d; b += kWave) a.slot_tab[(int64_t)s * 2 * a.d + b] = a.pool.tab[e * 2 * a.d + b];
@@ -1127,11 +1215,143 @@ __global__ __launch_bounds__(kExactWgThreads) void k_exact_rows_wg(PrepassArgs a
   }
 }
 
-__global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int lane = threadIdx.x;
-  const int scap = a.scap;
-  RState st;
+// The resolver's per-launch context (shared by k_resolve and k_resolve_blk): the point
+// decisions and state updates run on one wave (lane 0 writes the shared state).
+struct RCtx {
+  const ResolveArgs& a;
+  const RState& st;
+  RShared& S;
+  int lane, ncol, scap;
+  int nlog;    // running move-log length (uniform across the wave)
+  bool prof;
+  __device__ bool process(int64_t i, int row, int own, uint32_t rawU, int spec, double srad, bool given = false);
+  __device__ bool verify(int64_t lo, int64_t hi, double dn_over = -1.0, const int* cmin = nullptr);
+};
+
+// Decide point i (exact row in LDS at Lr) and apply n8:107-159.  Returns false to stop
+// the sweep here.
+__device__ __forceinline__ bool RCtx::process(int64_t i, int row, int own, uint32_t rawU, int spec, double srad, bool given) {
+  const int K = S.K;
+  const long long tq0 = prof ? wall_clock64() : 0;
+  // The snapshot draw holds while nothing has moved in this launch, and after moves while
+  // the slots and labels are those of the snapshot and no log-weight of the point has
+  // moved by its radius: the others' by at most dvmax, its own slot's (count - 1) by du.
+  // `given`: block mode, the caller has checked the draw against its block start.
+  bool use_spec = given || (spec >= 0 && S.moves == 0);
+  if (spec >= 0 && !use_spec && S.nstruct == 0) {
+    const int sa = st.snap[own], sb = st.cnt[own];
+    const double du = sa == sb ? 0.0 : (sa >= 2 && sb >= 2 ? fabs(a.logn[sb - 1] - a.logn[sa - 1]) : INFINITY);
+    use_spec = fmax(S.dvmax, du) < srad;
+  }
+
+  int pick = spec;
+  if (!use_spec) {   // the point's exact row, on demand
+    const double* src = a.L + (int64_t)row * ncol;
+    for (int c = lane; c < ncol; c += kWave) st.row[c] = src[c];
+    wave_sync();
+    pick = exact_decision(a, st, K, st.row, own, raw_to_unif(rawU));
+  }
+  if (prof && lane == 0) S.tsub[4] += wall_clock64() - tq0;
+  if (lane == 0) {
+    if (!use_spec) S.exact++;
+    if (pick < 0) { S.status = -pick; S.next = (int)i; }
+    else {
+      const int ownlab = st.los[own];
+      if (pick < K) {
+        const int ns = st.sol[pick];
+        if (st.cnt[own] != 1) {                                   // case 1
+          if (ns != own) {
+            a.c[i] = ns; set_count(st, a.logn, own, st.cnt[own] - 1); set_count(st, a.logn, ns, st.cnt[ns] + 1);
+            S.moves++;
+            log_move(a, nlog, i, own, ns);
+            S.dnow = fmax(S.dnow, fmax(slot_drift(st, a.logn, own), slot_drift(st, a.logn, ns)));
+            S.dvmax = fmax(S.dvmax, fmax(count_drift(st, a.logn, own), count_drift(st, a.logn, ns)));
+          }
+        } else {                                                  // case 2
+          int target = ns;
+          if (pick == ownlab) {           // the own (-inf) cluster was drawn
+            if (ownlab == K - 1) { S.status = 1; S.next = (int)i; }
+            target = st.sol[K - 1];
+          }
+          if (S.status == 0) {
+            a.c[i] = target; set_count(st, a.logn, own, st.cnt[own] - 1);
+            set_count(st, a.logn, target, st.cnt[target] + 1);
+            S.moves++;
+            log_move(a, nlog, i, own, target);
+            const int last = st.sol[K - 1];
+            st.los[own] = -1;
+            if (ownlab != K - 1) { st.sol[ownlab] = last; st.los[last] = ownlab; }
+            st.sol[K - 1] = -1;
+            S.K = K - 1;
+            S.nstruct++;
+            S.dnow = fmax(S.dnow, fmax(slot_drift(st, a.logn, own), slot_drift(st, a.logn, target)));
+          }
+        }
+      } else {
+        const int l = pick - K;
+        const bool single = st.cnt[own] == 1;
+        if (!single || l != 0) {                                  // case 3 / case 4 (new params)
+          if (S.nslots >= st.lcap || S.nslots >= scap) { S.status = 5; S.next = (int)i; }
+          else {
+            const int ns = S.nslots;
+            S.nslots = ns + 1;
+            if (!single) {                                        // case 3
+              st.sol[K] = ns; st.los[ns] = K; S.K = K + 1;
+              set_count(st, a.logn, own, st.cnt[own] - 1);
+            } else {                                              // case 4
+              st.sol[ownlab] = ns; st.los[ns] = ownlab; st.los[own] = -1;
+              set_count(st, a.logn, own, 0);
+            }
+            set_count(st, a.logn, ns, 1);
+            st.snap[ns] = 0;
+            a.c[i] = ns;
+            log_move(a, nlog, i, own, ns);
+            S.src = (int)pick_entry(a.raw[i * (a.m + 1) + l], a.P);
+            a.slot_src[ns] = S.src;
+            S.moves++;
+            S.restart = 1;
+            S.next = (int)i + 1;
+          }
+        }
+        // case 4 with latent 0 (the singleton's own parameters): nothing changes.
+      }
+    }
+  }
+  wave_sync();
+  if (S.restart && S.status == 0) {
+    const int ns = S.nslots - 1;
+    copy_pool_params(a, S.src, ns);
+    if (a.freq)   // the new slot's frequency table starts empty (the logged move fills it)
+      for (int e = lane; e < a.fstride; e += kWave) a.freq[(int64_t)ns * a.fstride + e] = 0u;
+  }
+  return S.status == 0 && !S.restart;
+}
+
+// Once the drift exceeds dmax, the unlisted (certain at the snapshot) points between two
+// listed ones are re-tested before the next listed point is decided: the n8 sequence is
+// unchanged, and a point that is no longer certain stops the launch for the host to
+// recompute bounds from there.  Returns false on such a point.
+// (Block mode passes dn_over, a bound on the drift over a block's walk, and cmin, lower
+// bounds on the counts during it.)
+__device__ __forceinline__ bool RCtx::verify(int64_t lo, int64_t hi, double dn_over, const int* cmin) {
+  if (lane == 0) S.checked = 1;
+  const double dn = dn_over >= 0.0 ? dn_over : S.dnow;
+  const int* cn = cmin ? cmin : st.cnt;
+  for (int64_t base = lo; base < hi; base += kWave) {
+    const int64_t j = base + lane;
+    bool fail = false;
+    if (j < hi && a.rowpos[j] < 0) fail = !(a.margin[j] - 2.0 * dn > a.T && cn[a.c[j]] >= 2);
+    const unsigned long long bal = __ballot(fail);
+    if (bal) {
+      if (lane == 0) { S.restart = 1; S.next = (int)(base + __ffsll((long long)bal) - 1); }
+      wave_sync();
+      return false;
+    }
+  }
+  return true;
+}
+
+__device__ __forceinline__ void resolve_layout(const ResolveArgs& a, RState& st, unsigned char* smem, bool blocks) {
   st.lcap = a.lcap;
   st.emax = a.lcap + a.m;
   st.sh = (RShared*)smem;
@@ -1145,11 +1365,27 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
   st.sol = st.snap + st.lcap;
   st.los = st.sol + st.lcap;
   st.perm = st.los + st.lcap;
+  st.ltab = (uint64_t*)(((uintptr_t)(st.perm + st.emax) + 15) & ~(uintptr_t)15);
+  st.sl1 = st.sl0 = nullptr;
+  st.bp = nullptr;
+  st.bperm = nullptr;
+  st.bcmin = nullptr;
+  st.brq = nullptr;
+  if (blocks) {
+    st.sl1 = (double*)(st.ltab + 256);
+    st.sl0 = st.sl1 + st.lcap;
+    st.bp = st.sl0 + st.lcap;
+    st.bperm = (int*)(st.bp + 64 * kWave);
+    st.bcmin = st.bperm + 64 * kWave;
+    st.brq = (int4*)(((uintptr_t)(st.bcmin + kWave) + 15) & ~(uintptr_t)15);
+  }
+}
+
+// all threads: the launch's state in LDS
+__device__ __forceinline__ void resolve_init(const ResolveArgs& a, const RState& st) {
   RShared& S = *st.sh;
-  long long tp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const bool prof = a.prof != nullptr;
-  if (prof) tp[0] = wall_clock64();
-  for (int s = lane; s < st.lcap; s += kWave) {
+  for (int e = threadIdx.x; e < 256; e += blockDim.x) st.ltab[e] = devtab::kGlibcLogTab[e];
+  for (int s = threadIdx.x; s < st.lcap; s += blockDim.x) {
     const int v = s < a.nslots ? a.counts[s] : 0;
     st.cnt[s] = v;
     st.snap[s] = v;
@@ -1157,249 +1393,38 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
     st.l0[s] = v > 0 ? a.logn[v - 1] : -INFINITY;
     st.los[s] = s < a.nslots ? a.label_of_slot[s] : -1;
     st.sol[s] = s < a.K ? a.slot_of_label[s] : -1;
+    if (st.sl1) { st.sl1[s] = st.l1[s]; st.sl0[s] = st.l0[s]; }
   }
-  if (lane == 0) {
+  if (threadIdx.x == 0) {
     S.K = a.K; S.nslots = a.nslots; S.status = 0; S.next = a.n; S.restart = 0;
     S.moves = 0; S.exact = 0; S.checked = 0; S.dnow = 0.0; S.dvmax = 0.0; S.nstruct = 0;
+    S.bgo = 1; S.bq = 0;
     for (int k = 0; k < 8; ++k) S.tsub[k] = 0;
   }
-  wave_sync();
-  const int ncol = a.S + a.m;
-  int nlog = a.mcount ? *a.mcount : 0;   // lane 0's running move-log length
+  __syncthreads();
+}
 
-  // Decide point i (exact row in LDS at Lr) and apply n8:107-159.  Returns false to stop
-  // the sweep here.
-  auto process = [&](int64_t i, int row, int own, uint32_t rawU, int spec, double srad) -> bool {
-    const int K = S.K;
-    const long long tq0 = prof ? wall_clock64() : 0;
-    // The snapshot draw holds while nothing has moved in this launch, and after moves while
-    // the slots and labels are those of the snapshot and no log-weight of the point has
-    // moved by its radius: the others' by at most dvmax, its own slot's (count - 1) by du.
-    bool use_spec = spec >= 0 && S.moves == 0;
-    if (spec >= 0 && !use_spec && S.nstruct == 0) {
-      const int sa = st.snap[own], sb = st.cnt[own];
-      const double du = sa == sb ? 0.0 : (sa >= 2 && sb >= 2 ? fabs(a.logn[sb - 1] - a.logn[sa - 1]) : INFINITY);
-      use_spec = fmax(S.dvmax, du) < srad;
-    }
-
-    int pick = spec;
-    if (!use_spec) {   // the point's exact row, on demand
-      const double* src = a.L + (int64_t)row * ncol;
-      for (int c = lane; c < ncol; c += kWave) st.row[c] = src[c];
-      wave_sync();
-      pick = exact_decision(a, st, K, st.row, own, raw_to_unif(rawU));
-    }
-    if (prof && lane == 0) S.tsub[4] += wall_clock64() - tq0;
-    if (lane == 0) {
-      if (!use_spec) S.exact++;
-      if (pick < 0) { S.status = -pick; S.next = (int)i; }
-      else {
-        const int ownlab = st.los[own];
-        if (pick < K) {
-          const int ns = st.sol[pick];
-          if (st.cnt[own] != 1) {                                   // case 1
-            if (ns != own) {
-              a.c[i] = ns; set_count(st, a.logn, own, st.cnt[own] - 1); set_count(st, a.logn, ns, st.cnt[ns] + 1);
-              S.moves++;
-              log_move(a, nlog, i, own, ns);
-              S.dnow = fmax(S.dnow, fmax(slot_drift(st, a.logn, own), slot_drift(st, a.logn, ns)));
-              S.dvmax = fmax(S.dvmax, fmax(count_drift(st, a.logn, own), count_drift(st, a.logn, ns)));
-            }
-          } else {                                                  // case 2
-            int target = ns;
-            if (pick == ownlab) {           // the own (-inf) cluster was drawn
-              if (ownlab == K - 1) { S.status = 1; S.next = (int)i; }
-              target = st.sol[K - 1];
-            }
-            if (S.status == 0) {
-              a.c[i] = target; set_count(st, a.logn, own, st.cnt[own] - 1);
-              set_count(st, a.logn, target, st.cnt[target] + 1);
-              S.moves++;
-              log_move(a, nlog, i, own, target);
-              const int last = st.sol[K - 1];
-              st.los[own] = -1;
-              if (ownlab != K - 1) { st.sol[ownlab] = last; st.los[last] = ownlab; }
-              st.sol[K - 1] = -1;
-              S.K = K - 1;
-              S.nstruct++;
-              S.dnow = fmax(S.dnow, fmax(slot_drift(st, a.logn, own), slot_drift(st, a.logn, target)));
-            }
-          }
-        } else {
-          const int l = pick - K;
-          const bool single = st.cnt[own] == 1;
-          if (!single || l != 0) {                                  // case 3 / case 4 (new params)
-            if (S.nslots >= st.lcap || S.nslots >= scap) { S.status = 5; S.next = (int)i; }
-            else {
-              const int ns = S.nslots;
-              S.nslots = ns + 1;
-              if (!single) {                                        // case 3
-                st.sol[K] = ns; st.los[ns] = K; S.K = K + 1;
-                set_count(st, a.logn, own, st.cnt[own] - 1);
-              } else {                                              // case 4
-                st.sol[ownlab] = ns; st.los[ns] = ownlab; st.los[own] = -1;
-                set_count(st, a.logn, own, 0);
-              }
-              set_count(st, a.logn, ns, 1);
-              st.snap[ns] = 0;
-              a.c[i] = ns;
-              log_move(a, nlog, i, own, ns);
-              S.src = (int)pick_entry(a.raw[i * (a.m + 1) + l], a.P);
-              a.slot_src[ns] = S.src;
-              S.moves++;
-              S.restart = 1;
-              S.next = (int)i + 1;
-            }
-          }
-          // case 4 with latent 0 (the singleton's own parameters): nothing changes.
-        }
-      }
-    }
-    wave_sync();
-    if (S.restart && S.status == 0) {
-      const int ns = S.nslots - 1;
-      copy_pool_params(a, S.src, ns);
-      if (a.freq)   // the new slot's frequency table starts empty (the logged move fills it)
-        for (int e = lane; e < a.fstride; e += kWave) a.freq[(int64_t)ns * a.fstride + e] = 0u;
-    }
-    return S.status == 0 && !S.restart;
-  };
-
-  bool go = true;
-  int64_t start_checked = -1;
-  // Once the drift exceeds dmax, the unlisted (certain at the snapshot) points between two
-  // listed ones are re-tested before the next listed point is decided: the n8 sequence is
-  // unchanged, and a point that is no longer certain stops the launch for the host to
-  // recompute bounds from there.  Returns false on such a point.
-  auto verify = [&](int64_t lo, int64_t hi) -> bool {
-    if (lane == 0) S.checked = 1;
-    const double dn = S.dnow;
-    for (int64_t base = lo; base < hi; base += kWave) {
-      const int64_t j = base + lane;
-      bool fail = false;
-      if (j < hi && a.rowpos[j] < 0) fail = !(a.margin[j] - 2.0 * dn > a.T && st.cnt[a.c[j]] >= 2);
-      const unsigned long long bal = __ballot(fail);
-      if (bal) {
-        if (lane == 0) { S.restart = 1; S.next = (int)(base + __ffsll((long long)bal) - 1); }
-        wave_sync();
-        return false;
-      }
-    }
-    return true;
-  };
-  if (!a.force_exact) {
-    // LIST mode: only the prepass's uncertain points need work while drift <= dmax.  The
-    // dense list, the points' labels, draws and snapshot draws are read 64 at a time; the
-    // points whose snapshot draw still holds and keeps them in their cluster change
-    // nothing and are passed over with one ballot; the others are decided in order (exact
-    // rows loaded only for the points that need an exact decision).
-    const int total = *a.dense_total;
-    if (prof) tp[1] = wall_clock64();
-    int64_t vfrom = a.p0;   // unlisted points [vfrom, next listed point) not yet re-tested
-    constexpr int kB = 4;   // chunks of 64 points whose inputs are loaded together
-    for (int qb = 0; qb < total && go; qb += kB * kWave) {
-      long long tb = prof ? wall_clock64() : 0;
-      int4 rqv[kB];
-      int spv[kB];
-      double srv[kB];
-#pragma unroll
-      for (int b = 0; b < kB; ++b) {
-        const int qq = qb + b * kWave + lane;
-        const bool in = qq < total;
-        rqv[b] = in ? a.rq[qq] : make_int4(0, 0, 0, 0);
-        spv[b] = (in && a.spec) ? a.spec[qq] : -1;
-        srv[b] = (in && a.spec) ? a.spec_rad[qq] : 0.0;
-      }
-      if (prof) tp[3] += wall_clock64() - tb;
-#pragma unroll
-      for (int b = 0; b < kB; ++b) {
-      const int q0 = qb + b * kWave;
-      if (q0 >= total || !go) break;
-      const int lim = min(kWave, total - q0);
-      const int rw = rqv[b].x, li = rqv[b].y, ci = rqv[b].z;
-      const uint32_t ru = (uint32_t)rqv[b].w;
-      const int sp = spv[b];
-      const double sr = srv[b];
-      int q = 0;
-      while (q < lim && go) {
-        long long t0 = prof ? wall_clock64() : 0;
-        bool stays = false;
-        if (lane >= q && lane < lim && sp >= 0 && sp < S.K && st.cnt[ci] != 1 && st.sol[sp] == ci) {
-          const int sa = st.snap[ci], sb = st.cnt[ci];
-          const double du =
-              sa == sb ? 0.0 : (sa >= 2 && sb >= 2 ? fabs(a.logn[sb - 1] - a.logn[sa - 1]) : INFINITY);
-          stays = S.moves == 0 || (S.nstruct == 0 && fmax(S.dvmax, du) < sr);
-        }
-        const unsigned long long todo = __ballot(lane >= q && lane < lim && !stays);
-        if (!todo) break;
-        q = __ffsll((long long)todo) - 1;
-        const int64_t i = __shfl(li, q);
-        if (S.dnow > a.dmax && !verify(vfrom, i)) { go = false; break; }
-        go = process(i, __shfl(rw, q), __shfl(ci, q), (uint32_t)__shfl((int)ru, q), __shfl(sp, q), __shfl(sr, q));
-        vfrom = i + 1;
-        ++q;
-        if (prof) {
-          tp[4] += wall_clock64() - t0;
-          tp[6] += 1;
-        }
-      }
-      }
-    }
-    if (go && S.status == 0 && !S.restart && S.dnow > a.dmax) (void)verify(vfrom, a.n);
-  } else {
-    start_checked = a.p0;
-  }
-  // CHECKED mode: every remaining point is re-tested against the current drift.
-  if (start_checked >= 0 && S.status == 0 && !S.restart) {
-    if (lane == 0) S.checked = 1;
-    for (int64_t base = start_checked; base < a.n; base += kWave) {
-      const int64_t i = base + lane;
-      bool unc = false;
-      int ci = 0;
-      if (i < a.n) {
-        ci = a.c[i];
-        const double mg = a.margin[i];
-        unc = a.force_exact || !(mg - 2.0 * S.dnow > a.T && st.cnt[ci] >= 2);
-      }
-      unsigned long long bal = __ballot(unc);
-      bool stop = false;
-      while (bal) {
-        const int q = __ffsll((long long)bal) - 1;
-        const int row = a.rowpos[base + q];
-        if (row < 0) {
-          // certain at the snapshot but not under the current drift, and no exact row:
-          // stop here and let the host recompute bounds from this point
-          if (lane == 0) { S.restart = 1; S.next = (int)(base + q); }
-          wave_sync();
-          stop = true;
-          break;
-        }
-        if (!process(base + q, row, __shfl(ci, q), a.raw[(base + q) * (a.m + 1) + a.m], -1, 0.0)) { stop = true; break; }
-        // drift may have grown: re-test the remaining lanes
-        bool u2 = false;
-        if (lane > q && i < a.n) {
-          const double mg = a.margin[i];
-          u2 = a.force_exact || !(mg - 2.0 * S.dnow > a.T && st.cnt[ci] >= 2);
-        }
-        bal = __ballot(u2);
-      }
-      if (stop) break;
-    }
-  }
+// all threads: write the state back, the host summary and the control block
+__device__ __forceinline__ void resolve_finish(const ResolveArgs& a, const RState& st, int nlog, const long long* tp,
+                                               bool prof) {
+  RShared& S = *st.sh;
+  const int scap = a.scap;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   __syncthreads();
   // write back
-  for (int s = lane; s < S.nslots; s += kWave) { a.counts[s] = st.cnt[s]; a.label_of_slot[s] = st.los[s]; }
-  for (int s = lane; s < S.K; s += kWave) a.slot_of_label[s] = st.sol[s];
+  for (int s = threadIdx.x; s < S.nslots; s += blockDim.x) { a.counts[s] = st.cnt[s]; a.label_of_slot[s] = st.los[s]; }
+  for (int s = threadIdx.x; s < S.K; s += blockDim.x) a.slot_of_label[s] = st.sol[s];
   // summary for the host (label -> slot, counts, pool sources), read with the control block
   __syncthreads();
-  for (int s = lane; s < scap; s += kWave) {
+  for (int s = threadIdx.x; s < scap; s += blockDim.x) {
     a.summary[s] = s < S.K ? st.sol[s] : -1;
     a.summary[scap + s] = s < S.nslots ? st.cnt[s] : 0;
     a.summary[2 * scap + s] = s < S.nslots ? a.slot_src[s] : -1;
   }
+  if (wv != 0) return;
   if (prof && lane == 0) {
-    tp[7] = wall_clock64();
-    for (int k = 0; k < 8; ++k) a.prof[k] = tp[k];
+    for (int k = 0; k < 7; ++k) a.prof[k] = tp[k];
+    a.prof[7] = wall_clock64();
     for (int k = 0; k < 8; ++k) a.prof[8 + k] = S.tsub[k];
   }
   if (lane == 0 && a.mcount) *a.mcount = nlog;
@@ -1410,6 +1435,386 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
     c.listed = *a.dense_total;
     *a.ctl = c;
   }
+}
+
+__global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = threadIdx.x & 63;
+  RState st;
+  resolve_layout(a, st, smem, false);
+  RShared& S = *st.sh;
+  long long tp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const bool prof = a.prof != nullptr;
+  if (prof) tp[0] = wall_clock64();
+  resolve_init(a, st);
+  RCtx R{a, st, S, lane, a.S + a.m, a.scap, a.mcount ? *a.mcount : 0, prof};
+  const int ncol = R.ncol;
+  (void)ncol;
+  bool go = true;
+  int64_t start_checked = -1;
+if (!a.force_exact) {
+  // LIST mode: only the prepass's uncertain points need work while drift <= dmax.  The
+  // dense list, the points' labels, draws and snapshot draws are read 64 at a time; the
+  // points whose snapshot draw still holds and keeps them in their cluster change
+  // nothing and are passed over with one ballot; the others are decided in order (exact
+  // rows loaded only for the points that need an exact decision).
+  const int total = *a.dense_total;
+  if (prof) tp[1] = wall_clock64();
+  int64_t vfrom = a.p0;   // unlisted points [vfrom, next listed point) not yet re-tested
+  constexpr int kB = 4;   // chunks of 64 points whose inputs are loaded together
+  for (int qb = 0; qb < total && go; qb += kB * kWave) {
+    long long tb = prof ? wall_clock64() : 0;
+    int4 rqv[kB];
+    int spv[kB];
+    double srv[kB];
+#pragma unroll
+    for (int b = 0; b < kB; ++b) {
+      const int qq = qb + b * kWave + lane;
+      const bool in = qq < total;
+      rqv[b] = in ? a.rq[qq] : make_int4(0, 0, 0, 0);
+      spv[b] = (in && a.spec) ? a.spec[qq] : -1;
+      srv[b] = (in && a.spec) ? a.spec_rad[qq] : 0.0;
+    }
+    if (prof) tp[3] += wall_clock64() - tb;
+#pragma unroll
+    for (int b = 0; b < kB; ++b) {
+    const int q0 = qb + b * kWave;
+    if (q0 >= total || !go) break;
+    const int lim = min(kWave, total - q0);
+    const int rw = rqv[b].x, li = rqv[b].y, ci = rqv[b].z;
+    const uint32_t ru = (uint32_t)rqv[b].w;
+    const int sp = spv[b];
+    const double sr = srv[b];
+    int q = 0;
+    while (q < lim && go) {
+      long long t0 = prof ? wall_clock64() : 0;
+      bool stays = false;
+      if (lane >= q && lane < lim && sp >= 0 && sp < S.K && st.cnt[ci] != 1 && st.sol[sp] == ci) {
+        const int sa = st.snap[ci], sb = st.cnt[ci];
+        const double du =
+            sa == sb ? 0.0 : (sa >= 2 && sb >= 2 ? fabs(a.logn[sb - 1] - a.logn[sa - 1]) : INFINITY);
+        stays = S.moves == 0 || (S.nstruct == 0 && fmax(S.dvmax, du) < sr);
+      }
+      const unsigned long long todo = __ballot(lane >= q && lane < lim && !stays);
+      if (!todo) break;
+      q = __ffsll((long long)todo) - 1;
+      const int64_t i = __shfl(li, q);
+      if (S.dnow > a.dmax && !R.verify(vfrom, i)) { go = false; break; }
+      go = R.process(i, __shfl(rw, q), __shfl(ci, q), (uint32_t)__shfl((int)ru, q), __shfl(sp, q), __shfl(sr, q));
+      vfrom = i + 1;
+      ++q;
+      if (prof) {
+        tp[4] += wall_clock64() - t0;
+        tp[6] += 1;
+      }
+    }
+    }
+  }
+  if (go && S.status == 0 && !S.restart && S.dnow > a.dmax) (void)R.verify(vfrom, a.n);
+} else {
+  start_checked = a.p0;
+}
+// CHECKED mode: every remaining point is re-tested against the current drift.
+if (start_checked >= 0 && S.status == 0 && !S.restart) {
+  if (lane == 0) S.checked = 1;
+  for (int64_t base = start_checked; base < a.n; base += kWave) {
+    const int64_t i = base + lane;
+    bool unc = false;
+    int ci = 0;
+    if (i < a.n) {
+      ci = a.c[i];
+      const double mg = a.margin[i];
+      unc = a.force_exact || !(mg - 2.0 * S.dnow > a.T && st.cnt[ci] >= 2);
+    }
+    unsigned long long bal = __ballot(unc);
+    bool stop = false;
+    while (bal) {
+      const int q = __ffsll((long long)bal) - 1;
+      const int row = a.rowpos[base + q];
+      if (row < 0) {
+        // certain at the snapshot but not under the current drift, and no exact row:
+        // stop here and let the host recompute bounds from this point
+        if (lane == 0) { S.restart = 1; S.next = (int)(base + q); }
+        wave_sync();
+        stop = true;
+        break;
+      }
+      if (!R.process(base + q, row, __shfl(ci, q), a.raw[(base + q) * (a.m + 1) + a.m], -1, 0.0)) { stop = true; break; }
+      // drift may have grown: re-test the remaining lanes
+      bool u2 = false;
+      if (lane > q && i < a.n) {
+        const double mg = a.margin[i];
+        u2 = a.force_exact || !(mg - 2.0 * S.dnow > a.T && st.cnt[ci] >= 2);
+      }
+      bal = __ballot(u2);
+    }
+    if (stop) break;
+  }
+}
+  resolve_finish(a, st, R.nlog, tp, prof);
+}
+
+// The n8:95-102 draw of this lane's point from its E log-weights w (LDS column: entry e at
+// w[e * kWave]), run literally: max, exp, sum, normalise, FixupProb, revsort, cumulative
+// compare (n8:95-102 with Rcpp's sample()), the same operations as decide_values.  *rad: as
+// decide_values' radius (the draw holds while every log-weight moves by less), 0 when no
+// bound is kept (ties among the positive probabilities, a draw past them).  Returns the
+// index or -status.  The column is overwritten (p), perm is the lane's index column.
+__device__ int decide_lane(double* w, int* perm, int E, double rU, double* rad) {
+  *rad = 0.0;
+  double mx = w[0];
+  for (int e = 1; e < E; ++e) mx = fmax(mx, w[e * kWave]);
+  for (int e = 0; e < E; ++e) w[e * kWave] = dexp(w[e * kWave] - mx);                     // n8:95
+  double sum = 0.0;
+  for (int e = 0; e < E; ++e) sum += w[e * kWave];
+  for (int e = 0; e < E; ++e) w[e * kWave] = w[e * kWave] / sum;                          // n8:96
+  double s2 = 0.0;                                                                         // FixupProb
+  for (int e = 0; e < E; ++e) { const double x = w[e * kWave]; s2 += x > 0 ? x : 0.0; }
+  if (!(s2 > 0)) return -3;
+  double pmax = -1.0, p2 = -1.0;
+  int amax = -1, ties = 0, npos = 0;
+  for (int e = 0; e < E; ++e) {
+    const double x = w[e * kWave] / s2;
+    w[e * kWave] = x;
+    npos += x > 0 ? 1 : 0;
+    if (x > pmax) { p2 = pmax; pmax = x; amax = e; ties = 1; }
+    else if (x == pmax) ++ties;
+    else if (x > p2) p2 = x;
+  }
+  if (ties == 1 && rU <= pmax) {          // revsort puts the unique maximum first
+    const double r1 = p2 > 0 ? 0.5 * log(pmax / p2) : INFINITY;
+    *rad = fmax(0.0, fmin(r1, 0.5 * log(pmax / rU)) - 1e-9);
+    return amax;
+  }
+  for (int e = 0; e < E; ++e) perm[e * kWave] = e + 1;
+  lane_revsort(w, perm, E);
+  // the reference's cumulative sums in sorted order (in place there; the same additions
+  // in a register here, so w keeps the sorted probabilities for the radius)
+  double c = 0.0, cprev = 0.0;
+  int j;
+  for (j = 0; j < E - 1; ++j) {
+    cprev = c;
+    c += w[j * kWave];
+    if (rU <= c) break;
+  }
+  if (j == E - 1) { cprev = c; c += w[j * kWave]; }
+  const int pick = perm[j * kWave] - 1;
+  // radius: the pick keeps its place among the positive entries (strictly between its
+  // neighbours) and rU its interval (as decide_values)
+  if (j < npos) {
+    const double pj = w[j * kWave];
+    double r = INFINITY;
+    bool ok = true;
+    if (j > 0) {
+      const double pprev = w[(j - 1) * kWave];
+      ok &= pprev > pj;
+      r = fmin(r, fmin(0.5 * log(pprev / pj), 0.5 * log(rU / cprev)));
+    }
+    if (j + 1 < npos) {
+      const double pnext = w[(j + 1) * kWave];
+      ok &= pj > pnext;
+      r = fmin(r, 0.5 * log(pj / pnext));
+    }
+    if (j != E - 1) r = fmin(r, 0.5 * log(c / rU));
+    if (ok) *rad = fmax(0.0, r - 1e-9);
+  }
+  return pick;
+}
+
+// Block mode (see kBlk): one wave, launched when the previous launch listed at least
+// kResolveBlkMin uncertain points and K + m <= 64, nslots <= 64 (lane = block point, and
+// lane = slot in the walk).
+__global__ __launch_bounds__(kWave) void k_resolve_blk(ResolveArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = threadIdx.x & 63;
+  RState st;
+  resolve_layout(a, st, smem, true);
+  RShared& S = *st.sh;
+  long long tp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const bool prof = a.prof != nullptr;
+  if (prof) tp[0] = wall_clock64();
+  resolve_init(a, st);
+  RCtx R{a, st, S, lane, a.S + a.m, a.scap, a.mcount ? *a.mcount : 0, prof};
+  const int ncol = R.ncol;
+  const int total = *a.dense_total;
+  int64_t vfrom = a.p0;   // unlisted points [vfrom, next listed point) not yet re-tested
+  bool go = true;
+  if (prof) tp[1] = wall_clock64();
+  const unsigned long long below = (1ull << lane) - 1ull;
+  int rq_lo = 0, rq_hi = 0;
+  for (int qb = 0; qb < total && go;) {
+    const long long tb = prof ? wall_clock64() : 0;
+    const int nb = min(kBlk, total - qb);
+    const int K = S.K, E = K + a.m;
+    const bool inb = lane < nb;
+    // ---- the block's draws, lane k = point qb + k, in the state at the block start; the
+    // points' inputs come through an LDS window of kRqWin list positions
+    if (qb + nb > rq_hi) {
+      rq_lo = qb;
+      rq_hi = min(total, qb + kRqWin);
+      for (int q = lane; q < rq_hi - rq_lo; q += kWave) st.brq[q] = a.rq[rq_lo + q];
+      wave_sync();
+    }
+    const int4 r = inb ? st.brq[qb - rq_lo + lane] : make_int4(0, 0, 0, 0);
+    const int own = r.z;
+    const bool single = inb && st.cnt[own] == 1;
+    double* wcol = st.bp + lane;
+    int* pcol = st.bperm + lane;
+    if (inb) {
+      // the row entries 16 at a time (loads in flight together), then the log-weights
+      const double* Lr = a.L + (int64_t)r.x * ncol;
+      const double lo = Lr[own];
+      for (int e0 = 0; e0 < E; e0 += 16) {
+        double x[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+          const int e = e0 + t;
+          x[t] = e < E ? Lr[e < K ? st.sol[e] : a.S + e - K] : 0.0;
+        }
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+          const int e = e0 + t;
+          if (e < K) {
+            const int sl = st.sol[e];
+            wcol[e * kWave] = (sl == own ? st.l0[sl] : st.l1[sl]) + x[t];
+          } else if (e < E) {
+            wcol[e * kWave] = a.logfac + ((e == K && single) ? lo : x[t]);
+          }
+        }
+      }
+    }
+    double rad = 0.0;
+    int pick = -1;
+    if (inb) {
+      const double rU = raw_to_unif((uint32_t)r.w);
+      pick = decide_lane(wcol, pcol, E, rU, &rad);
+    }
+    if (prof) tp[3] += wall_clock64() - tb;
+    const long long tw = prof ? wall_clock64() : 0;
+    // ---- classification in the block-start state (a kept point has its own count unchanged,
+    // so its state at its turn is this one): stay, case-1 move own -> tgt, or structural
+    bool mover = false, structural = false;
+    int tgt = own;
+    if (inb) {
+      if (pick < 0) structural = true;
+      else if (pick < K) {
+        const int ns = st.sol[pick];
+        if (!single) { mover = ns != own; tgt = ns; }
+        else structural = true;                                             // case 2
+      } else {
+        structural = !(single && pick == K);                                // cases 3 / 4 (new params)
+      }
+    }
+    const unsigned long long smask = __ballot(structural);
+    const int ks0 = smask ? __ffsll((long long)smask) - 1 : nb;
+    const unsigned long long mvm = __ballot(mover) & (ks0 >= 64 ? ~0ull : ((1ull << ks0) - 1ull));
+    // slots the block's moves touch
+    unsigned long long touch = mover && lane < ks0 ? ((1ull << own) | (1ull << tgt)) : 0ull;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) touch |= __shfl_xor(touch, o);
+    const int cs = lane < S.nslots ? st.cnt[lane] : 0;     // block-start counts (lane = slot)
+    // ---- the walk in parallel: count changes before each point, from the moves before it;
+    // |log(c + d) - log(c)| <= |d| / min(c, c + d) bounds the drift of a count's log (fp32,
+    // integers below 2^24 exact, the factor covers the division's rounding)
+    auto bound = [](int d, int c) -> float {
+      if (d == 0) return 0.0f;
+      const int mn = min(c, c + d);
+      return mn <= 0 ? INFINITY : (float)abs(d) / (float)mn * 1.000001f;
+    };
+    float Dk = 0.0f, du = 0.0f;
+    for (unsigned long long t = touch; t; t &= t - 1) {
+      const int sl = __ffsll((long long)t) - 1;
+      const unsigned long long in = __ballot(mover && tgt == sl) & mvm, out = __ballot(mover && own == sl) & mvm;
+      const int d = __popcll(in & below) - __popcll(out & below);
+      const int c = __builtin_amdgcn_readlane(cs, sl);
+      Dk = fmaxf(Dk, bound(d, c));
+      if (own == sl) du = bound(d, c - 1);
+    }
+    const bool keep = lane == 0 || (double)fmaxf(Dk, du) < rad;
+    const unsigned long long bad = __ballot(inb && !keep);
+    const int kstop = bad ? __ffsll((long long)bad) - 1 : nb;
+    int kc = min(kstop, ks0);
+    bool serial_next = ks0 < kstop;
+    // unlisted points before the last kept one: re-tested with a bound on the drift and
+    // lower bounds on the counts over the walk (their turn comes during it)
+    if (kc > 0) {
+      const int64_t ilast = __shfl(r.y, kc - 1);
+      const unsigned long long ltk = kc >= 64 ? ~0ull : ((1ull << kc) - 1ull);
+      const float Dall = wave_max(lane < kc ? (double)Dk : 0.0);
+      if (S.dnow + (double)Dall > a.dmax) {
+        int co = 0;
+        for (unsigned long long t = touch; t; t &= t - 1) {
+          const int sl = __ffsll((long long)t) - 1;
+          const int nout = __popcll(__ballot(mover && own == sl) & mvm & ltk);
+          if (lane == sl) co = nout;
+        }
+        if (lane < S.nslots) st.bcmin[lane] = cs - co;
+        wave_sync();
+        if (!R.verify(vfrom, ilast, S.dnow + (double)Dall, st.bcmin)) {
+          const int64_t u = S.next;     // the launch stops at the first failing unlisted point
+          kc = __popcll(__ballot(lane < kc && (int64_t)r.y < u));
+          go = false;
+          serial_next = false;
+        }
+      }
+    }
+    // ---- commit the kept points together: labels, move log, counts, drifts
+    const unsigned long long ltk = kc >= 64 ? ~0ull : ((1ull << kc) - 1ull);
+    const bool cm = lane < kc && mover;
+    const unsigned long long mm = __ballot(cm);
+    if (cm) {
+      a.c[r.y] = tgt;
+      if (a.mlog) {
+        const int q = R.nlog + __popcll(mm & below);
+        a.mlog[3 * q] = r.y;
+        a.mlog[3 * q + 1] = own;
+        a.mlog[3 * q + 2] = tgt;
+      }
+    }
+    if (a.mlog) R.nlog += __popcll(mm);
+    int dl = 0;
+    for (unsigned long long t = touch; t; t &= t - 1) {
+      const int sl = __ffsll((long long)t) - 1;
+      const int d = __popcll(__ballot(mover && tgt == sl) & mvm & ltk) - __popcll(__ballot(mover && own == sl) & mvm & ltk);
+      if (lane == sl) dl = d;
+    }
+    double sd = 0.0, cd = 0.0;
+    if (lane < S.nslots && dl != 0) {
+      const int c = cs + dl;
+      st.cnt[lane] = c;
+      st.l1[lane] = logn_dev(st, c);
+      st.l0[lane] = logn_dev(st, c - 1);
+      sd = slot_drift(st, a.logn, lane);
+      cd = count_drift(st, a.logn, lane);
+    }
+    sd = wave_max(sd);
+    cd = wave_max(cd);
+    if (lane == 0) {
+      S.moves += __popcll(mm);
+      S.exact += kc;
+      S.dnow = fmax(S.dnow, sd);
+      S.dvmax = fmax(S.dvmax, cd);
+    }
+    if (kc > 0) vfrom = (int64_t)__shfl(r.y, kc - 1) + 1;
+    int done = kc;
+    wave_sync();
+    // ---- a structural point (case 2, 3 or 4) in turn: the serial path
+    if (serial_next && go) {
+      const int64_t i = __shfl(r.y, kc);
+      if (S.dnow > a.dmax && !R.verify(vfrom, i)) go = false;
+      else {
+        go = R.process(i, __shfl(r.x, kc), __shfl(own, kc), (uint32_t)__shfl(r.w, kc), __shfl(pick, kc), 0.0, true);
+        R.nlog = __builtin_amdgcn_readfirstlane(R.nlog);
+        vfrom = i + 1;
+        ++done;
+        if (lane == 0) S.exact++;
+      }
+    }
+    qb += done;
+    if (prof) { tp[4] += wall_clock64() - tw; tp[6] += done; tp[5] += 1; }
+  }
+  if (go && S.status == 0 && !S.restart && S.dnow > a.dmax) (void)R.verify(vfrom, a.n);
+  resolve_finish(a, st, R.nlog, tp, prof);
 }
 
 // ------------------------------------------------------------------ end of sweep
@@ -1715,10 +2120,13 @@ hipError_t launch_prepass(const PrepassArgs& a, int nblocks, hipStream_t s) {
   }
 }
 
-size_t resolve_smem_bytes(int lcap, int m) { return resolve_lds_bytes(lcap, m); }
+size_t resolve_smem_bytes(int lcap, int m, int blocks) { return resolve_lds_bytes(lcap, m, blocks); }
 
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_resolve, dim3(1), dim3(kWave), resolve_lds_bytes(a.lcap, a.m), s, a);
+  if (a.blocks)
+    hipLaunchKernelGGL(k_resolve_blk, dim3(1), dim3(kWave), resolve_lds_bytes(a.lcap, a.m, 1), s, a);
+  else
+    hipLaunchKernelGGL(k_resolve, dim3(1), dim3(kWave), resolve_lds_bytes(a.lcap, a.m, 0), s, a);
   return hipGetLastError();
 }
 

@@ -115,6 +115,10 @@ struct PrepassArgs {
   int exact_wave;            // 1: exact rows one wave per point (no workgroup staging)
 };
 
+// The resolver runs in block mode (csrc/kernels.hip, k_resolve_blk) when the previous launch
+// listed at least this many uncertain points.
+constexpr int kResolveBlkMin = 256;
+
 // Control block written by the resolver.
 struct ResolveCtl {
   int next;       // first point not yet decided (n when the sweep is complete)
@@ -173,6 +177,7 @@ struct ResolveArgs {
   unsigned int* freq;        // per-slot freq [slot][d][mmax] (new slots are zeroed here)
   int fstride;               // d * mmax
   long long* prof;           // diagnostics: resolver phase times (s_memrealtime ticks) or nullptr
+  int blocks;                // 1: block mode (k_resolve_blk; needs K + m <= 64, nslots <= 64)
 };
 
 // Cluster parameter upload: one staging buffer, scattered on the device.

@@ -232,9 +232,12 @@ class Engine:
         return acc, ll
 
     def run_markov_chain(self, *, verbose=0, m=5, iterations=1000, L=1, c_i=None, burnin=5000, t=10, r=10,
-                         neal8=False, split_merge=True, n8_step_size=1, sam_step_size=1, thinning=1):
+                         neal8=False, split_merge=True, n8_step_size=1, sam_step_size=1, thinning=1,
+                         keep_params=False):
         p = _lib.ChainParams(verbose, m, iterations, L, burnin, t, r, int(bool(neal8)), int(bool(split_merge)),
                              n8_step_size, sam_step_size, thinning)
+        if keep_params:
+            return self._run_recording(p, c_i)
         tot = np.zeros(iterations, np.int32)
         cis = np.zeros((iterations, self.n), np.int32)
         ll = np.zeros(iterations, np.float64)
@@ -247,10 +250,35 @@ class Engine:
         return {"total_cls": tot, "c_i": cis, "loglikelihood": ll, "final_ass": fin,
                 "time": float(tm[0]), "accepted": acc}
 
+    def _run_recording(self, p, c_i):
+        """The la:85-154 loop iteration by iteration (hdpm_init_chain + hdpm_iteration), also
+        recording the cluster parameters of every saved iteration as the reference does
+        (centers / sigmas, la:144-147: K x D arrays)."""
+        import time
+        iterations, burnin, thinning = p.iterations, p.burnin, p.thinning
+        tot = np.zeros(iterations, np.int32)
+        cis = np.zeros((iterations, self.n), np.int32)
+        ll = np.zeros(iterations, np.float64)
+        acc = np.zeros(iterations, np.int32)
+        cens, sigs = [None] * iterations, [None] * iterations
+        t0 = time.perf_counter()
+        self.init_chain(p, c_i)
+        for it in range((iterations + burnin) * thinning):
+            a, lik = self.iteration(it)
+            if it >= thinning * burnin and it % thinning == 0:
+                at = it // thinning - burnin
+                c, cen, sig = self.get_state()
+                tot[at], cis[at], ll[at], acc[at] = cen.shape[0], c, lik, a
+                cens[at], sigs[at] = cen, sig
+        fin = self.get_state()[0]
+        return {"total_cls": tot, "c_i": cis, "centers": cens, "sigmas": sigs, "loglikelihood": ll,
+                "final_ass": fin, "time": time.perf_counter() - t0, "accepted": acc}
+
 
 def run_markov_chain(data, attrisize, gamma, v, w, verbose=0, m=5, iterations=1000, L=1, c_i=None,
                      burnin=5000, t=10, r=10, neal8=False, split_merge=True, n8_step_size=1,
-                     sam_step_size=1, thinning=1, *, seed=None, rng_state=None, device=0, hig_logspace=False):
+                     sam_step_size=1, thinning=1, *, seed=None, rng_state=None, device=0, hig_logspace=False,
+                     keep_params=False):
     """Drop-in for the reference's ``run_markov_chain`` (code/launcher.cpp:6-14).
 
     ``data`` holds the categorical codes 1..m_j (an N x D matrix).  The R random stream
@@ -258,6 +286,8 @@ def run_markov_chain(data, attrisize, gamma, v, w, verbose=0, m=5, iterations=10
     the fields of the reference's result list (plus ``rng_state`` after the run).
     ``hig_logspace=True`` turns on the log-space 2F1 extension (``Engine.set_hig_logspace``);
     the default keeps the reference's semantics, including its throw on overflow.
+    ``keep_params=True`` also returns ``centers`` / ``sigmas`` of every saved iteration
+    (la:144-147), running the loop iteration by iteration.
     """
     eng = Engine(device)
     try:
@@ -270,7 +300,7 @@ def run_markov_chain(data, attrisize, gamma, v, w, verbose=0, m=5, iterations=10
             eng.set_seed(0 if seed is None else seed)
         res = eng.run_markov_chain(verbose=verbose, m=m, iterations=iterations, L=L, c_i=c_i, burnin=burnin,
                                    t=t, r=r, neal8=neal8, split_merge=split_merge, n8_step_size=n8_step_size,
-                                   sam_step_size=sam_step_size, thinning=thinning)
+                                   sam_step_size=sam_step_size, thinning=thinning, keep_params=keep_params)
         res["rng_state"] = eng.rng_state
         res["stats"] = eng.stats()
         return res

@@ -122,7 +122,8 @@ def test_c4_full_size_neal8_and_split_merge(hd, oracle):
 
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("L", [1, 20])
-def test_c2_full_size_unconverged_starts(hd, oracle, L):
+@pytest.mark.parametrize("debug", [0, 4096])     # 4096: the resolver without block mode
+def test_c2_full_size_unconverged_starts(hd, oracle, L, debug):
     """C2: N = 10,000, D = 32, binary, from one cluster (L = 1) or a random assignment to 20
     labels (la:31-43, the scripts' L = 20): far from the posterior, points move every sweep
     and clusters appear and vanish (cases 2-4, resolver restarts)."""
@@ -131,6 +132,7 @@ def test_c2_full_size_unconverged_starts(hd, oracle, L):
     eng = hd.Engine(0)
     eng.set_data(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w)
     eng.set_seed(4)
+    eng.set_debug(debug)
     params = eng.chain_params(m=3, iterations=1, L=L, burnin=0, neal8=True, split_merge=False)
     eng.init_chain(params, c_i=np.zeros(ds.n, np.int32) if L == 1 else None)
     c, cen, sig = eng.get_state()
@@ -141,4 +143,24 @@ def test_c2_full_size_unconverged_starts(hd, oracle, L):
     neal8_steps(eng, oracle, ds, ost, rng, pc, ps, sweeps=4)
     if L == 20:
         assert eng.stats()["moves"] > 0
+    eng.close()
+
+
+@pytest.mark.timeout(900)
+def test_c5_full_size_random20_start(hd, oracle):
+    """C5 from a random assignment to 20 labels (la:31, the scripts' L = 20): every point is
+    uncertain in the first sweeps, the resolver's block mode decides them."""
+    from split_and_merge_gibbs_sampling_amd.data import config
+    ds = config("c5")
+    eng = hd.Engine(0)
+    eng.set_data(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w)
+    eng.set_seed(6)
+    params = eng.chain_params(m=3, iterations=1, L=20, burnin=0, neal8=True, split_merge=False)
+    eng.init_chain(params, c_i=None)
+    c, cen, sig = eng.get_state()
+    pc, ps = eng.get_pool(ds.n * 3)
+    ost = oracle.OracleState(c, cen.shape[0], cen, sig, cap=4096)
+    rng = eng.rng_state.copy()
+    neal8_steps(eng, oracle, ds, ost, rng, pc, ps, sweeps=2)
+    assert eng.stats()["moves"] > 100_000
     eng.close()

@@ -96,7 +96,8 @@ def sweep_case(hd, oracle, ds, c, cen, sig, P, seed, m=3, debug=0, sweeps=1, phi
 
 # debug 0: default (snapshot speculation in the exact-rows kernel), 1: every point on the
 # exact path in the resolver, 8: no speculation (the resolver decides every listed point)
-@pytest.mark.parametrize("debug", [0, 1, 8, 2048])
+# 8192: the resolver's block mode for every launch (parallel decisions, serial walk)
+@pytest.mark.parametrize("debug", [0, 1, 8, 2048, 8192])
 def test_zoo_single_sweeps_from_truth(hd, oracle, zoo, debug):
     cen, sig = random_params(zoo, 7, 3)
     stats = sweep_case(hd, oracle, zoo, zoo.truth, cen, sig, zoo.n * 3, seed=17, debug=debug, sweeps=3)
@@ -110,7 +111,7 @@ def test_zoo_sweeps_with_update_phi_all_singletons(hd, oracle, zoo):
     sweep_case(hd, oracle, zoo, c, cen, sig, zoo.n * 3, seed=23, sweeps=4, phi=True)
 
 
-@pytest.mark.parametrize("debug", [0, 8])
+@pytest.mark.parametrize("debug", [0, 8, 8192])
 def test_zoo_sweeps_with_update_phi_one_cluster(hd, oracle, zoo, debug):
     # L = 1: the first sweeps create clusters (case 3 -> device restarts)
     c = np.zeros(zoo.n, np.int32)
@@ -120,8 +121,9 @@ def test_zoo_sweeps_with_update_phi_one_cluster(hd, oracle, zoo, debug):
 
 
 # 16: recount the frequency tables every update_phi; 128: no speculative update_phi;
-# 2048: exact rows one wave per point
-@pytest.mark.parametrize("debug", [0, 1, 8, 16, 128, 2048, 2048 | 1])
+# 2048: exact rows one wave per point; 4096: no block mode in the resolver; 8192: block mode
+# for every launch
+@pytest.mark.parametrize("debug", [0, 1, 8, 16, 128, 2048, 2048 | 1, 4096, 8192, 8192 | 8])
 def test_synthetic_sweeps_with_update_phi(hd, oracle, debug):
     ds = synth(6000, 32, 8, 2, seed=3)
     cen, sig = random_params(ds, 8, 7)
@@ -252,6 +254,29 @@ def test_run_markov_chain_zoo_split_merge_golden(hd, zoo):
     assert np.array_equal(res["c_i"], g["c_i"])
     assert np.array_equal(res["accepted"], g["accepted"])
     np.testing.assert_allclose(res["loglikelihood"], g["loglikelihood"], rtol=RTOL, atol=0)
+
+
+def test_run_markov_chain_keep_params_and_stream_handback(hd, oracle, zoo):
+    """The adapter's contract: centers / sigmas of every saved iteration
+    (la:144-147), and the random stream handed back so that a second chain started from it
+    continues the reference's stream (consecutive R calls without set.seed)."""
+    kw = dict(m=3, iterations=12, L=1, c_i=np.zeros(zoo.n, np.int32), burnin=3, t=10, r=10, neal8=True,
+              split_merge=True)
+    a = hd.run_markov_chain(zoo.codes, zoo.attrisize, zoo.gamma, zoo.v, zoo.w, seed=7, **kw)
+    b = hd.run_markov_chain(zoo.codes, zoo.attrisize, zoo.gamma, zoo.v, zoo.w, seed=7, keep_params=True, **kw)
+    for k in ("c_i", "total_cls", "accepted", "final_ass"):
+        assert np.array_equal(a[k], b[k]), k
+    np.testing.assert_allclose(a["loglikelihood"], b["loglikelihood"], rtol=RTOL, atol=0)
+    assert len(b["centers"]) == 12
+    for it in range(12):
+        assert b["centers"][it].shape == (b["total_cls"][it], zoo.d) == b["sigmas"][it].shape
+    st = oracle.seed_state(7)
+    ost, ref = oracle.run_markov_chain(zoo.codes, zoo.attrisize, zoo.gamma, zoo.v, zoo.w, rng=st, fast=1, **kw)
+    assert ost == 0 and np.array_equal(ref["c_i"], b["c_i"])
+    assert np.array_equal(b["rng_state"], st) and np.array_equal(a["rng_state"], st)
+    c = hd.run_markov_chain(zoo.codes, zoo.attrisize, zoo.gamma, zoo.v, zoo.w, rng_state=b["rng_state"], **kw)
+    ost, ref2 = oracle.run_markov_chain(zoo.codes, zoo.attrisize, zoo.gamma, zoo.v, zoo.w, rng=st, fast=1, **kw)
+    assert ost == 0 and np.array_equal(ref2["c_i"], c["c_i"]) and np.array_equal(c["rng_state"], st)
 
 
 def test_run_markov_chain_random_init_matches_oracle(hd, oracle, zoo):
@@ -529,7 +554,7 @@ def test_pool_heads_binary_and_absent(hd, oracle):
 
 
 # 1024: full bound records for the latent picks (no heads) on a head-eligible layout
-@pytest.mark.parametrize("debug", [0, 1024])
+@pytest.mark.parametrize("debug", [0, 1024, 8192])
 def test_c5_like_sweeps_heads_and_records(hd, oracle, debug):
     ds = synth(5000, 128, 8, 4, seed=24)
     cen, sig = random_params(ds, 8, 25)
