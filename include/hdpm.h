@@ -174,6 +174,16 @@ int hdpm_get_pool_heads(hdpm_ctx* ctx, uint64_t* out, int64_t P);
  * semantics). */
 #define HDPM_OPT_HIG_LOGSPACE 1
 int hdpm_set_option(hdpm_ctx* ctx, int32_t option, double value);
+/* Posterior analysis (realdata_analysis/zoo_simulator.R:193-236, 339-344; mcclust /
+ * mcclust.ext).  hdpm_psm_build: the posterior similarity matrix of M saved label vectors
+ * c_trace[M x N] (results$c_i, labels 0..254) -- comp.psm(C) -- kept on the device as
+ * co-clustering counts (psm = count / M).  hdpm_psm_rows: rows row0 .. row0+nrows-1 of psm
+ * (N doubles each).  hdpm_psm_vi_lb: VI.lb(cls, psm) of ncand candidate partitions
+ * cls[ncand x N] (the lower bound of the posterior expected variation of information that
+ * minVI minimises). */
+int hdpm_psm_build(hdpm_ctx* ctx, const int32_t* c_trace, int32_t M, int32_t N);
+int hdpm_psm_rows(hdpm_ctx* ctx, int32_t row0, int32_t nrows, double* out);
+int hdpm_psm_vi_lb(hdpm_ctx* ctx, const int32_t* cls, int32_t ncand, double* out);
 /* Testing: one draw on the device from log-weights logw[E] (E <= 256) and the uniform rU --
  * the n8:95-102 categorical draw (two_way = 0; *pick = the 0-based index, or -status) or the
  * sm:204-215 two-way draw (two_way = 1, E = 2) -- with the engine's exp, glibc's algorithm

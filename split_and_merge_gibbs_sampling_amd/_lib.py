@@ -24,6 +24,7 @@ EXPORTS = (
     "hdpm_split_and_merge", "hdpm_run_markov_chain", "hdpm_get_stats", "hdpm_reset_stats",
     "hdpm_set_debug", "hdpm_synchronize", "hdpm_init_chain", "hdpm_iteration", "hdpm_iterations", "hdpm_rng_fill_device",
     "hdpm_get_pool_heads", "hdpm_set_option", "hdpm_debug_draw", "hdpm_debug_math",
+    "hdpm_psm_build", "hdpm_psm_rows", "hdpm_psm_vi_lb",
 )
 
 OPT_HIG_LOGSPACE = 1
@@ -117,6 +118,9 @@ def lib():
         "hdpm_set_option": ([vp, i32, f64], C.c_int),
         "hdpm_debug_draw": ([vp, vp, i32, f64, i32, i32, P(i32)], C.c_int),
         "hdpm_debug_math": ([vp, vp, i64, i32, i32, vp], C.c_int),
+        "hdpm_psm_build": ([vp, vp, i32, i32], C.c_int),
+        "hdpm_psm_rows": ([vp, i32, i32, vp], C.c_int),
+        "hdpm_psm_vi_lb": ([vp, vp, i32, vp], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

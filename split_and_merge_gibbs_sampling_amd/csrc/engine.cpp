@@ -54,6 +54,9 @@ hipError_t launch_hist(const HistArgs& a, hipStream_t s);
 size_t hist_partial_words(const HistArgs& a, int* nbx, int* kc, int* tpb);
 hipError_t launch_loglik(const LoglikArgs& a, hipStream_t s);
 hipError_t launch_mt_gen(const MtGenArgs& a, hipStream_t s);
+hipError_t launch_psm(const int32_t* trace, int M, int N, uint8_t* lab, uint32_t* cnt, hipStream_t s);
+hipError_t launch_vi_terms(const uint32_t* cnt, int N, int M, const int32_t* cls, int ncand, double* all, double* same,
+                           hipStream_t s);
 hipError_t launch_debug_draw(const double* logw, int E, double rU, int two_way, int ocml, int* out, hipStream_t s);
 hipError_t launch_debug_math(const double* x, int64_t n, int fn, int ocml, double* out, hipStream_t s);
 hipError_t launch_lmatrix(const uint8_t* codes_t, int n, int d, int nq, ParamTables cl, int K, double* L,
@@ -525,6 +528,12 @@ struct Ctx {
   DevBuf<uint64_t> d_xbs;             // bit-sliced rows (tiled; prepass)
   DevBuf<double> d_logn;
   std::vector<double> h_logn;
+  // posterior analysis (hdpm_psm_*): label bytes, co-clustering counts, VI.lb sums
+  DevBuf<int32_t> d_psm_trace, d_psm_cls;
+  DevBuf<uint8_t> d_psm_lab;
+  DevBuf<uint32_t> d_psm_cnt;
+  DevBuf<double> d_psm_all, d_psm_same;
+  int psm_N = 0, psm_M = 0;
 
   Rng rng;
 
@@ -3063,6 +3072,73 @@ int hdpm_set_option(hdpm_ctx* h, int32_t option, double value) {
       ctx->err = "unknown option";
       return HDPM_E_ARG;
   }
+}
+int hdpm_psm_build(hdpm_ctx* h, const int32_t* c_trace, int32_t M, int32_t N) {
+  CTX();
+  if (!c_trace || M <= 0 || N <= 0) return HDPM_E_ARG;
+  for (int64_t q = 0; q < (int64_t)M * N; ++q)
+    if (c_trace[q] < 0 || c_trace[q] > 254) { ctx->err = "psm: labels must be in 0..254"; return HDPM_E_ARG; }
+  GUARD({
+    const int Mp = (M + 15) & ~15;
+    ctx->d_psm_trace.ensure((size_t)M * N);
+    ctx->d_psm_lab.ensure((size_t)N * Mp);
+    ctx->d_psm_cnt.ensure((size_t)N * N);
+    HIPCHK(hipMemcpyAsync(ctx->d_psm_trace.p, c_trace, (size_t)M * N * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hdpm::launch_psm(ctx->d_psm_trace.p, M, N, ctx->d_psm_lab.p, ctx->d_psm_cnt.p, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->psm_N = N;
+    ctx->psm_M = M;
+    return HDPM_OK;
+  })
+}
+int hdpm_psm_rows(hdpm_ctx* h, int32_t row0, int32_t nrows, double* out) {
+  CTX();
+  const int N = ctx->psm_N;
+  if (!out || N == 0 || row0 < 0 || nrows < 0 || row0 + nrows > N) return HDPM_E_ARG;
+  GUARD({
+    std::vector<uint32_t> c((size_t)nrows * N);
+    HIPCHK(hipMemcpyAsync(c.data(), ctx->d_psm_cnt.p + (size_t)row0 * N, c.size() * 4, hipMemcpyDeviceToHost,
+                          ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    const double M = (double)ctx->psm_M;
+    for (size_t q = 0; q < c.size(); ++q) out[q] = (double)c[q] / M;
+    return HDPM_OK;
+  })
+}
+int hdpm_psm_vi_lb(hdpm_ctx* h, const int32_t* cls, int32_t ncand, double* out) {
+  CTX();
+  const int N = ctx->psm_N;
+  if (!cls || !out || N == 0 || ncand <= 0) return HDPM_E_ARG;
+  GUARD({
+    ctx->d_psm_cls.ensure((size_t)ncand * N);
+    ctx->d_psm_all.ensure((size_t)N);
+    ctx->d_psm_same.ensure((size_t)ncand * N);
+    HIPCHK(hipMemcpyAsync(ctx->d_psm_cls.p, cls, (size_t)ncand * N * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hdpm::launch_vi_terms(ctx->d_psm_cnt.p, N, ctx->psm_M, ctx->d_psm_cls.p, ncand, ctx->d_psm_all.p,
+                                 ctx->d_psm_same.p, ctx->stream));
+    std::vector<double> all((size_t)N);
+    std::vector<double> same((size_t)ncand * N);
+    HIPCHK(hipMemcpyAsync(all.data(), ctx->d_psm_all.p, all.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(same.data(), ctx->d_psm_same.p, same.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    // mcclust.ext VI.lb: f = sum_i (log2 n_{c_i} + log2 sum_j psm_ij - 2 log2 sum_{j in c_i} psm_ij) / n
+    std::vector<int> sz;
+    for (int c = 0; c < ncand; ++c) {
+      const int32_t* cl = cls + (size_t)c * N;
+      int mx = 0;
+      for (int i = 0; i < N; ++i) mx = std::max(mx, cl[i]);
+      sz.assign((size_t)mx + 1, 0);
+      for (int i = 0; i < N; ++i) {
+        if (cl[i] < 0) { ctx->err = "psm: negative cluster label"; return HDPM_E_ARG; }
+        sz[cl[i]]++;
+      }
+      double f = 0.0;
+      for (int i = 0; i < N; ++i)
+        f = f + (std::log2((double)sz[cl[i]]) + std::log2(all[i]) - 2 * std::log2(same[(size_t)c * N + i])) / N;
+      out[c] = f;
+    }
+    return HDPM_OK;
+  })
 }
 int hdpm_debug_draw(hdpm_ctx* h, const double* logw, int32_t E, double rU, int32_t two_way, int32_t ocml,
                     int32_t* pick) {

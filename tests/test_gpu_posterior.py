@@ -1,0 +1,92 @@
+"""MI355X: the posterior similarity matrix and VI lower bounds on the device
+(csrc/posterior.hip) against numpy restatements of mcclust::comp.psm and
+mcclust.ext::VI.lb (zoo_simulator.R:193-236; the packages are absent, parity unpinned for
+their tie conventions, exact for the counts)."""
+import math
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def hd():
+    import split_and_merge_gibbs_sampling_amd as hd
+    hd.build()
+    return hd
+
+
+def psm_ref(tr):
+    M, N = tr.shape
+    cnt = np.zeros((N, N), np.int64)
+    for m in range(M):
+        cnt += tr[m][:, None] == tr[m][None, :]
+    return cnt / M
+
+
+def vi_lb_ref(cl, psm):
+    n = psm.shape[0]
+    f = 0.0
+    for i in range(n):
+        ind = cl == cl[i]
+        f += (math.log2(ind.sum()) + math.log2(psm[i].sum()) - 2 * math.log2((ind * psm[i]).sum())) / n
+    return f
+
+
+@pytest.mark.parametrize("N,M,K", [(1000, 37, 12), (300, 16, 3), (129, 1, 254)])
+def test_psm_exact(hd, N, M, K):
+    from split_and_merge_gibbs_sampling_amd.posterior import PSM
+    rng = np.random.default_rng(N + M)
+    tr = rng.integers(0, K + 1 if K < 254 else 255, size=(M, N)).astype(np.int32)
+    p = PSM(tr)
+    got = p.matrix()
+    assert np.array_equal(got, psm_ref(tr))
+    assert np.array_equal(p.rows(N // 3, 5), got[N // 3:N // 3 + 5])
+    p.close()
+
+
+def test_vi_lb_and_minvi(hd, zoo):
+    from split_and_merge_gibbs_sampling_amd import posterior as P
+    res = hd.run_markov_chain(zoo.codes, zoo.attrisize, zoo.gamma, zoo.v, zoo.w, m=3, iterations=200, L=1,
+                              c_i=np.zeros(zoo.n, np.int32), burnin=100, t=10, r=10, neal8=True, split_merge=True,
+                              seed=3)
+    tr = res["c_i"]
+    p = P.PSM(tr)
+    psm = p.matrix()
+    assert np.array_equal(psm, psm_ref(tr))
+    cand = np.stack([tr[0], tr[-1], zoo.truth, np.zeros(zoo.n, np.int32), np.arange(zoo.n)])
+    got = p.vi_lb(cand)
+    want = [vi_lb_ref(c, psm) for c in cand]
+    np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-12)
+    cl_d, v_d = P.minvi(p, cls_draw=tr, method="draws")
+    assert v_d == pytest.approx(min(vi_lb_ref(c, psm) for c in tr), rel=1e-12)
+    cl_a, v_a = P.minvi(p, method="avg")
+    assert v_a <= vi_lb_ref(np.zeros(zoo.n, np.int32), psm) + 1e-12
+    # the chain recovers Zoo's classes reasonably (the script's ARI check, zoo:339-344)
+    assert P.arandi(cl_a, zoo.truth) > 0.4
+    p.close()
+
+
+@pytest.mark.timeout(600)
+def test_psm_c4_size(hd):
+    """C4 size (N = 70,000): 4.9e9 pair counts on the device; diagonal, symmetry and
+    sampled rows exact."""
+    from split_and_merge_gibbs_sampling_amd.posterior import PSM
+    N, M = 70_000, 24
+    rng = np.random.default_rng(7)
+    truth = rng.integers(0, 10, N)
+    tr = np.where(rng.random((M, N)) < 0.9, truth[None, :], rng.integers(0, 12, (M, N))).astype(np.int32)
+    p = PSM(tr)
+    for i in (0, 1, 12345, 69_999):
+        row = p.rows(i, 1)[0]
+        want = (tr == tr[:, i][:, None]).sum(0) / M
+        assert np.array_equal(row, want), i
+        assert row[i] == 1.0
+    sub = p.rows(500, 3)
+    for k in range(3):
+        col = p.rows(0, 1)[0]  # symmetry spot check against row 0
+        assert sub[k][0] == col[500 + k]
+    v = p.vi_lb(np.stack([truth, tr[0]]))
+    assert np.all(np.isfinite(v)) and v[0] < v[1] + 1.0
+    p.close()
