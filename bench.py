@@ -397,6 +397,7 @@ def main():
                    if st["sm_moves"] > 0}),
             "exact_points_per_step": st["exact_points"] / args.steps,
             "listed_points_per_step": st["listed_points"] / args.steps,
+            "moves_per_step": st["moves"] / args.steps,
             "split_merge": bool(args.sm),
             "hig_logspace": hig_log,
             "rounds_per_step": st["rounds"] / args.steps,

@@ -556,7 +556,7 @@ struct Ctx {
   DevBuf<double> d_slot_tab;
   DevBuf<uint64_t> d_slot_bnd;
   int scap = 0;
-  int last_listed = 0;        // uncertain points of the previous resolver launch (block-mode choice)
+  int last_exact = 0;         // points the previous resolver launch decided one by one (block-mode choice)
 
   // latent pool
   int64_t P = 0;
@@ -1633,9 +1633,11 @@ struct Ctx {
       d_rprof.ensure(16);
       ra.prof = d_rprof.p;
     }
-    // block mode when the previous launch listed many uncertain points (an unconverged chain)
+    // block mode when in the previous launch many uncertain points had to be decided one by
+    // one (their snapshot draws no longer held: an unconverged chain, or clusters appearing
+    // and vanishing); LIST mode passes over the rest in one ballot per 64
     ra.blocks = (K + m <= 64 && nslots <= 64 && !(debug & 4096) && !(debug & 1) &&
-                 ((debug & 8192) || last_listed >= kResolveBlkMin)) ? 1 : 0;
+                 ((debug & 8192) || last_exact >= kResolveBlkMin)) ? 1 : 0;
     if (resolve_smem_bytes(ra.lcap, m, ra.blocks) > 160 * 1024) {
       err = "too many clusters for the resolver (K > ~2300)";
       return kArg;
@@ -1826,7 +1828,7 @@ struct Ctx {
       }
       stats.exact_points += c.exact;
       stats.listed_points += c.listed;
-      last_listed = c.listed;
+      last_exact = c.exact;
       stats.moves += c.moves;
       sweep_moves += c.moves;
       stats.checked_rounds += c.checked;

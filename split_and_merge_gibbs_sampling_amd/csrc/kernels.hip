@@ -1705,6 +1705,17 @@ __global__ __launch_bounds__(kWave) void k_resolve_blk(ResolveArgs a) {
         structural = !(single && pick == K);                                // cases 3 / 4 (new params)
       }
     }
+    // whether LIST mode would have had to decide the point itself (its snapshot draw from
+    // k_exact_rows no longer held): the host's choice between the two modes
+    bool list_exact = true;
+    if (inb && a.spec) {
+      const int sp = a.spec[qb + lane];
+      if (sp >= 0) {
+        const int sa = st.snap[own], sb = st.cnt[own];
+        const double du0 = sa == sb ? 0.0 : (sa >= 2 && sb >= 2 ? fabs(st.l0[own] - st.sl0[own]) : INFINITY);
+        list_exact = !(S.moves == 0 || (S.nstruct == 0 && fmax(S.dvmax, du0) < a.spec_rad[qb + lane]));
+      }
+    }
     const unsigned long long smask = __ballot(structural);
     const int ks0 = smask ? __ffsll((long long)smask) - 1 : nb;
     const unsigned long long mvm = __ballot(mover) & (ks0 >= 64 ? ~0ull : ((1ull << ks0) - 1ull));
@@ -1789,9 +1800,10 @@ __global__ __launch_bounds__(kWave) void k_resolve_blk(ResolveArgs a) {
     }
     sd = wave_max(sd);
     cd = wave_max(cd);
+    const int lex = __popcll(__ballot(lane < kc && list_exact));
     if (lane == 0) {
       S.moves += __popcll(mm);
-      S.exact += kc;
+      S.exact += lex;
       S.dnow = fmax(S.dnow, sd);
       S.dvmax = fmax(S.dvmax, cd);
     }
@@ -1807,7 +1819,7 @@ __global__ __launch_bounds__(kWave) void k_resolve_blk(ResolveArgs a) {
         R.nlog = __builtin_amdgcn_readfirstlane(R.nlog);
         vfrom = i + 1;
         ++done;
-        if (lane == 0) S.exact++;
+        if (lane == 0 && __shfl(list_exact ? 1 : 0, kc)) S.exact++;
       }
     }
     qb += done;

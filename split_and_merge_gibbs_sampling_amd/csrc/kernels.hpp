@@ -115,8 +115,9 @@ struct PrepassArgs {
   int exact_wave;            // 1: exact rows one wave per point (no workgroup staging)
 };
 
-// The resolver runs in block mode (csrc/kernels.hip, k_resolve_blk) when the previous launch
-// listed at least this many uncertain points.
+// The resolver runs in block mode (csrc/kernels.hip, k_resolve_blk) when in the previous
+// launch at least this many uncertain points needed a decision of their own (their
+// snapshot draws no longer held).
 constexpr int kResolveBlkMin = 256;
 
 // Control block written by the resolver.
