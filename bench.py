@@ -39,41 +39,56 @@ def packed_layout(d: int, mmax: int):
     return wb, wb * Ws, (wb + 4) * Ws + 4
 
 
-# FETCH_SIZE calibration on gfx950 (tools/fetch_calib.hip, profiles/r01/fetch_calib.log):
-# reported / true bytes and measured rates of the prepass's access shapes
-FETCH_FACTOR = {"stream16": 0.5, "gather64": 1.0, "gather128": 0.584}
-RATE_GBPS = {"stream16": 5650.0, "gather64": 3080.0, "gather128": 3830.0}
+# FETCH_SIZE calibration on gfx950 (tools/fetch_calib.hip, profiles/r01/fetch_calib.log;
+# gather448g -- 16-lane groups gathering 448-B wide heads -- profiles/r02/fetch_calib_wide.log,
+# its FETCH_SIZE factor not calibrated): reported / true bytes and measured rates of the
+# prepass's access shapes
+FETCH_FACTOR = {"stream16": 0.5, "gather64": 1.0, "gather128": 0.584, "gather448g": 1.0}
+RATE_GBPS = {"stream16": 5650.0, "gather64": 3080.0, "gather128": 3830.0, "gather448g": 5757.0}
+
+
+def head_layout(d: int, mmax: int):
+    """(has heads, head stride in words) as in csrc/kernels.hpp (templ_fits, wide_fits,
+    head_stride): templated layouts pad wb Ws + 2 words to a power of two, wide ones
+    (k_prepass_wide) to a multiple of 8 words."""
+    wb, W, bw = packed_layout(d, mmax)
+    Ws = W // wb
+    templ = Ws == 2 or (Ws == 4 and wb <= 4)
+    wide = not templ and Ws <= 32 and W <= 64
+    if templ:
+        hs = 4
+        while hs < W + 2:
+            hs *= 2
+    else:
+        hs = -(-(W + 2) // 8) * 8
+    return templ or wide, hs, templ
 
 
 def prepass_shape(d: int, mmax: int, m: int):
     """(streamed bytes, gathered bytes, gather shape) per point of k_prepass: streamed are
     the row, raw draws and label reads (margin / row index writes are WRITE_SIZE), gathered
-    the m latent picks (64-B heads, else full 8 bw-byte records)."""
+    the m latent picks (heads, else full 8 bw-byte records)."""
     wb, W, bw = packed_layout(d, mmax)
-    Ws = W // wb
-    head = Ws == 2 or (Ws == 4 and wb <= 4)
-    hs = 4
-    while hs < W + 2:
-        hs *= 2
+    head, hs, templ = head_layout(d, mmax)
     g = m * 8 * (hs if head else bw)
-    shape = "gather64" if head and hs == 8 else "gather128"
+    if head and templ:
+        shape = "gather64" if hs == 8 else "gather128"
+    elif head:
+        shape = "gather448g"
+    else:
+        shape = "gather128"
     return 8 * W + 4 * (m + 1) + 4, g, shape
 
 
 def prepass_bytes_per_point(d: int, mmax: int, m: int) -> int:
     """Compulsory bytes k_prepass moves per point: its bit-sliced row
     (8 W), its m+1 raw draws (4(m+1)), its label (4), the first gather of each of its m
-    latent pool picks -- the pool-entry head (W + 2 words padded to a power of two: 64 B at
-    C5) when the layout has one, else the full bound record (8 bw) -- its margin (8) and
-    row index (4).  The full
-    records a head leaves uncertain (6e-5 of the picks at C5) are extra traffic, not
-    counted here."""
+    latent pool picks -- the pool-entry head (W + 2 words padded: 64 B at C5, 448 B at C4)
+    when the layout has one, else the full bound record (8 bw) -- its margin (8) and row
+    index (4).  The full records a head leaves uncertain (6e-5 of the picks at C5) are extra
+    traffic, not counted here; cluster records are cache-resident (K of them per sweep)."""
     wb, W, bw = packed_layout(d, mmax)
-    Ws = W // wb
-    head = Ws == 2 or (Ws == 4 and wb <= 4)           # csrc/kernels.hpp head_fits
-    hs = 4
-    while hs < W + 2:
-        hs *= 2
+    head, hs, _ = head_layout(d, mmax)
     return 8 * W + 4 * (m + 1) + 4 + m * 8 * (hs if head else bw) + 12
 
 

@@ -159,11 +159,13 @@ int hdpm_reset_stats(hdpm_ctx* ctx);
  * bit 10: the prepass gathers full bound records for latent picks (no pool-entry heads);
  * bit 11: exact rows one wave per point (no workgroup-per-point LDS staging); bit 12: no
  * block mode in the resolver (uncertain points decided one by one); bit 13: block mode for
- * every resolver launch (not only after a launch that listed kResolveBlkMin points). */
+ * every resolver launch (not only after a launch that listed kResolveBlkMin points); bit 14:
+ * wide layouts take the generic prepass (one thread per point) instead of k_prepass_wide. */
 int hdpm_set_debug(hdpm_ctx* ctx, int32_t mode);
 /* The prepass's pool-entry heads, P entries of wb*Ws + 2 words padded to a power of two
- * (csrc/kernels.hpp "Pool-entry heads"); HDPM_E_ARG when the data's layout has none (d > 256, or d > 128 with
- * m_j > 16). */
+ * (Ws <= 4) or to a multiple of 8 words (wide layouts) (csrc/kernels.hpp "Pool-entry heads",
+ * head_stride); HDPM_E_ARG when the data's layout has none (Ws > 32, i.e. d > 2048, or rows
+ * of more than 64 words: wb * Ws > 64). */
 int hdpm_get_pool_heads(hdpm_ctx* ctx, uint64_t* out, int64_t P);
 /* Options.  HDPM_OPT_HIG_LOGSPACE (value != 0): an extension beyond the reference -- the
  * HIG normalising constant's 2F1 series (norm_const2, hg:11-48, and lF_conK2, hg:183-217)

@@ -1601,6 +1601,7 @@ struct Ctx {
     pa.rq = d_rq.p;
     pa.p0 = p;
     pa.exact_wave = (debug & 2048) ? 1 : 0;
+    pa.wide = (debug & 16384) ? 0 : 1;
     const int nblocks = (n - p + kBlock - 1) / kBlock;
     HIPCHK(launch_cluster_summary(pa, stream));
     if (round_timed) HIPCHK(hipEventRecord(ev[0], stream));

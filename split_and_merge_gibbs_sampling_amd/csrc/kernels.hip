@@ -145,14 +145,16 @@ __device__ __forceinline__ double ll_lane(const PointCodes<NQR>& x, int d, const
 }
 
 
-// Margin, row position and the ordered compaction of the block's uncertain points.
+// Margin, row position and the ordered compaction of the block's uncertain points (the
+// block's kBlock points are threads 0..kBlock-1 of its NT; the others pass active = false).
+template <int NT = kBlock>
 __device__ __forceinline__ void prepass_finish(const PrepassArgs& a, int64_t i, bool active, int own_cnt, double mg) {
   const int tid = threadIdx.x;
   const bool uncertain = active && !(own_cnt >= 2 && mg > a.thresh);
   if (active) a.margin[i] = mg;
 
   // ordered compaction of the uncertain points of this block
-  __shared__ int s_wcnt[kBlock / kWave];
+  __shared__ int s_wcnt[NT / kWave];
   const int lane = tid & 63, wv = tid >> 6;
   const unsigned long long bal = __ballot(uncertain);
   const int pre = __popcll(bal & ((1ull << lane) - 1ull));
@@ -160,7 +162,7 @@ __device__ __forceinline__ void prepass_finish(const PrepassArgs& a, int64_t i, 
   __syncthreads();
   int off = 0, tot = 0;
 #pragma unroll
-  for (int w = 0; w < kBlock / kWave; ++w) {
+  for (int w = 0; w < NT / kWave; ++w) {
     off += w < wv ? s_wcnt[w] : 0;
     tot += s_wcnt[w];
   }
@@ -433,6 +435,278 @@ __global__ __launch_bounds__(kBlock) void k_prepass_generic(PrepassArgs a) {
     mg = lo - ubmax;
   }
   prepass_finish(a, i, active, own_cnt, mg);
+}
+
+// Wide layouts (kernels.hpp wide_fits; C4: d = 784, wb = 4, Ws = 13 -- a 416-B row, 864-B
+// records): the same bounds as k_prepass, but a point is worked on by a 16-lane group, lane
+// w holding plane word w (and w + 16) of every bit-plane, so each record is read once per
+// point with coalesced 8-B loads (a 104-B run per plane) and H / Sq are summed across the
+// group with DPP row operations (one DPP row = one group).  The workgroup's kBlock points
+// go through in 64-point passes: the pass's rows are staged in LDS from the tiled row array
+// (coalesced), point-major with one word of padding.  Latent picks gather the entry's head
+// (codes + the four floats, 448 B at C4); a group whose head bound does not clear `cut`
+// reads the record's penalty planes too.
+constexpr int kWideThreads = 1024;          // 64 groups of 16: one 64-point pass at a time
+
+// Sum over the 16 lanes of a DPP row (every lane gets the total).
+__device__ __forceinline__ int row_sum16(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
+  v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
+  v += __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, false);   // row_ror:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false);   // row_ror:8
+  return v;
+}
+
+// Record arrays in HBM are read through buffer resources: one 32-bit lane offset per
+// record (entry * stride + 8 w) and the plane offsets in the scalar offset operand, so a
+// record costs one VGPR of addressing instead of a 64-bit address per plane word.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, int64_t bytes) {
+  const int nrec = (int)min(bytes, (int64_t)0x7fffffff);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, nrec, 0x00020000);
+}
+__device__ __forceinline__ uint64_t bload(__amdgpu_buffer_rsrc_t r, int vo, int so) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0);
+  return ((uint64_t)v[1] << 32) | v[0];
+}
+
+// A point's row in a 16-lane group: lane w holds word w (and w + 16) of each bit-plane.
+// `ld(k, q)` returns the lane's word w + 16 k of a record at the wave-uniform word offset q.
+template <int WB, int NW>
+struct WideRow {
+  uint64_t x[NW][WB];
+  int WS;
+  bool val[NW];                              // w + 16 k < WS
+  template <class LD>
+  __device__ __forceinline__ int mismatch(LD ld, uint64_t (&M)[NW]) const {
+    int h = 0;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+      uint64_t m = 0;
+#pragma unroll
+      for (int b = 0; b < WB; ++b) m |= x[k][b] ^ ld(k, b * WS);
+      m = val[k] ? m : 0ull;
+      M[k] = m;
+      h += __popcll(m);
+    }
+    return row_sum16(h);
+  }
+  // Sq = sum_b 2^b popc(M & plane_b), planes at word offsets (WB + b) WS
+  template <class LD>
+  __device__ __forceinline__ int penalty(LD ld, const uint64_t (&M)[NW]) const {
+    int s = 0;
+#pragma unroll
+    for (int k = 0; k < NW; ++k)
+#pragma unroll
+      for (int b = 0; b < kQ; ++b) s += __popcll(M[k] & ld(k, (WB + b) * WS)) << b;
+    return row_sum16(s);
+  }
+};
+
+// Dynamic LDS of k_prepass_wide: the pass's rows [64][wb Ws + 1], the block's raw draws
+// [kBlock][m + 1] (u32), and (CL) the cluster summaries [K][bw + 2].
+constexpr int kWidePf = kWideRowMax * 64 / kWideThreads;   // row words per thread prefetched for the next pass
+__host__ __device__ inline size_t wide_rows_words(int wb, int Ws) { return (size_t)64 * (wb * Ws + 1); }
+__host__ __device__ inline size_t wide_raw_words(int m) { return ((size_t)kBlock * (m + 1) + 1) / 2; }
+size_t prepass_wide_lds_bytes(int wb, int Ws, int m, int K, int bw, bool cl) {
+  return 8 * (wide_rows_words(wb, Ws) + wide_raw_words(m) + (cl ? (size_t)K * (bw + 2) : 0));
+}
+// byte offsets of the record arrays must fit the buffer instructions' 32-bit offsets
+bool prepass_wide_offsets_fit(const PrepassArgs& a) {
+  const int64_t hs = head_stride(a.wb, a.Ws);
+  return a.P * (int64_t)std::max<int64_t>(a.bw, hs) * 8 + 4096 < 0x7fffffff;
+}
+
+template <int WB, int NW, bool CL>
+__global__ __launch_bounds__(kWideThreads) void k_prepass_wide(PrepassArgs a) {
+  extern __shared__ uint64_t s_dyn[];
+  __shared__ double s_mg[kBlock];
+  __shared__ int s_oc[kBlock];
+  __shared__ int s_own[kBlock];
+  const int WS = a.Ws, WR = WB * WS, RS = WR + 1, SC = (WB + kQ) * WS, HS = head_stride(WB, WS);
+  const int bw = a.bw, cw = a.bw + 2;
+  uint64_t* s_rows = s_dyn;
+  uint32_t* s_raw = (uint32_t*)(s_dyn + wide_rows_words(WB, WS));
+  uint64_t* s_cs = s_dyn + wide_rows_words(WB, WS) + wide_raw_words(a.m);
+  const int tid = threadIdx.x, g = tid >> 4, w = tid & 15, m1 = a.m + 1;
+  const int w8 = 8 * w;
+  const int64_t b0 = (int64_t)a.p0 + (int64_t)blockIdx.x * kBlock;
+  const int npts = (int)min((int64_t)kBlock, (int64_t)a.n - b0);
+  const __amdgpu_buffer_rsrc_t r_slot = make_rsrc(a.slot_bnd, (int64_t)(a.S + 2) * bw * 8);
+  const __amdgpu_buffer_rsrc_t r_pool = make_rsrc(a.pool_bnd, a.P * bw * 8);
+  const __amdgpu_buffer_rsrc_t r_head = make_rsrc(a.pool_head, a.P * HS * 8);
+  const __amdgpu_buffer_rsrc_t r_csum = make_rsrc(a.csum, (int64_t)a.K * cw * 8);
+  // block prologue: labels and counts, raw draws, cluster summaries, the first pass's rows
+  if (tid < npts) {
+    const int o = a.c[b0 + tid];
+    s_own[tid] = o;
+    s_oc[tid] = a.counts[o];
+  }
+  for (int e = tid; e < npts * m1; e += kWideThreads) s_raw[e] = a.raw[b0 * m1 + e];
+  if constexpr (CL) {
+    for (int e = tid; e < a.K * cw; e += kWideThreads) s_cs[e] = a.csum[e];
+  }
+  uint64_t pf[kWidePf];
+  auto fetch = [&](int64_t t0) {
+#pragma unroll
+    for (int r = 0; r < kWidePf; ++r) {
+      const int e = tid + r * kWideThreads;
+      if (e < 64 * WR) {
+        const int64_t i = min(t0 + (e & 63), (int64_t)a.n - 1);
+        pf[r] = a.xbs[packed_offset(i, e >> 6, WR)];
+      }
+    }
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int r = 0; r < kWidePf; ++r) {
+      const int e = tid + r * kWideThreads;
+      if (e < 64 * WR) s_rows[(e & 63) * RS + (e >> 6)] = pf[r];
+    }
+  };
+  fetch(b0);
+  stage();
+  WideRow<WB, NW> xr;
+  xr.WS = WS;
+#pragma unroll
+  for (int k = 0; k < NW; ++k) xr.val[k] = w + 16 * k < WS;
+  const int npass = (npts + 63) / 64;
+#pragma unroll 1
+  for (int pass = 0; pass < npass; ++pass) {
+    __syncthreads();                          // rows of this pass staged (and the prologue)
+    if (pass + 1 < npass) fetch(b0 + 64 * (pass + 1));
+    const int pt = 64 * pass + g;             // point within the block
+    const bool act = pt < npts;
+    const int ptc = act ? pt : npts - 1;
+#pragma unroll
+    for (int k = 0; k < NW; ++k)
+#pragma unroll
+      for (int b = 0; b < WB; ++b) xr.x[k][b] = xr.val[k] ? s_rows[g * RS + b * WS + w + 16 * k] : 0ull;
+    const int own = s_own[ptc];
+    const int own_cnt = s_oc[ptc];
+    double mg = -INFINITY;
+    if (own_cnt >= 2) {                       // group-uniform
+      const uint32_t* raw = s_raw + ptc * m1;
+      // the first latent heads' gathers go out first (their latency overlaps the own-cluster
+      // bound and the cluster loop)
+      constexpr int LW = WB * NW;
+      constexpr int NPF = LW <= 4 ? 3 : LW <= 8 ? 2 : 1;   // heads in flight (register budget)
+      uint64_t Hd[NPF][LW + 2];
+      int pe[NPF];                            // byte offset of the pick's record / head
+      const bool heads = a.pool_head != nullptr;
+      auto gather = [&](int u, int l) {
+        const int e = (int)pick_entry(raw[l], a.P);
+        pe[u] = e;
+        if (heads) {
+          const int hb = e * HS * 8;
+#pragma unroll
+          for (int k = 0; k < NW; ++k)
+#pragma unroll
+            for (int b = 0; b < WB; ++b) Hd[u][k * WB + b] = bload(r_head, hb + w8 + 128 * k, 8 * b * WS);
+          Hd[u][LW] = bload(r_head, hb, 8 * WR);
+          Hd[u][LW + 1] = bload(r_head, hb, 8 * (WR + 1));
+        }
+      };
+#pragma unroll
+      for (int u = 0; u < NPF; ++u)
+        if (u < a.m) gather(u, u);
+      uint64_t M[NW];
+      double lo;
+      {
+        const int ob = own * bw * 8;
+        auto ld = [&](int k, int q) { return bload(r_slot, ob + w8 + 128 * k, 8 * q); };
+        const int H = xr.mismatch(ld, M);
+        const int Sq = xr.penalty(ld, M);
+        const double A = as_f64(bload(r_slot, ob, 8 * SC)), dl = as_f64(bload(r_slot, ob, 8 * (SC + 1)));
+        const double pmax = dl * (double)(Sq + H);
+        lo = a.logn[own_cnt - 1] + (A - pmax - kBoundEps * (1.0 + fabs(A) + pmax));
+      }
+      const double cut = lo - a.thresh;
+      double ubmax = -INFINITY;
+#pragma unroll 1
+      for (int l = 0; l < a.K; ++l) {
+        // wave-uniform record: LDS (CL) or the csum buffer
+        auto ldc = [&](int q) -> uint64_t {
+          if constexpr (CL) return s_cs[l * cw + q];
+          else return bload(r_csum, 0, 8 * (l * cw + q));
+        };
+        auto ld = [&](int k, int q) -> uint64_t {
+          if constexpr (CL) return s_cs[l * cw + q + w + 16 * k];
+          else return bload(r_csum, w8 + 128 * k, 8 * (l * cw + q));
+        };
+        const int s = (int)ldc(bw + 1);
+        if (s == own) continue;               // group-uniform
+        const int H = xr.mismatch(ld, M);
+        const double A = as_f64(ldc(SC)), dmin = as_f64(ldc(SC + 2)), scale = as_f64(ldc(SC + 3));
+        const double lg = as_f64(ldc(bw));
+        double ub = lg + (A - dmin * (double)H + kBoundEps * (1.0 + scale));
+        if (ub > cut) {
+          const int Sq = xr.penalty(ld, M);
+          const double dl = as_f64(ldc(SC + 1));
+          const double pmin = dl * (double)Sq, pmax = dl * (double)(Sq + H);
+          ub = fmin(ub, lg + (A - pmin + kBoundEps * (1.0 + fabs(A) + pmax)));
+        }
+        ubmax = fmax(ubmax, ub);
+      }
+#pragma unroll 1
+      for (int l0 = 0; l0 < a.m; l0 += NPF) {
+        if (l0 > 0) {
+#pragma unroll
+          for (int u = 0; u < NPF; ++u)
+            if (l0 + u < a.m) gather(u, l0 + u);
+        }
+#pragma unroll
+        for (int u = 0; u < NPF; ++u) {
+          if (l0 + u >= a.m) continue;
+          const int rb = pe[u] * bw * 8;
+          auto ldr = [&](int k, int q) { return bload(r_pool, rb + w8 + 128 * k, 8 * q); };
+          double ub;
+          if (heads) {
+            int h = 0;
+#pragma unroll
+            for (int k = 0; k < NW; ++k) {
+              uint64_t mm = 0;
+#pragma unroll
+              for (int b = 0; b < WB; ++b) mm |= xr.x[k][b] ^ Hd[u][k * WB + b];
+              mm = xr.val[k] ? mm : 0ull;
+              M[k] = mm;
+              h += __popcll(mm);
+            }
+            const int H = row_sum16(h);
+            const uint64_t p0 = Hd[u][LW], p1 = Hd[u][LW + 1];
+            const double A = (double)__uint_as_float((uint32_t)p0), dmn = (double)__uint_as_float((uint32_t)(p0 >> 32));
+            const double sa = (double)__uint_as_float((uint32_t)p1), sb = (double)__uint_as_float((uint32_t)(p1 >> 32));
+            double low = dmn * (double)H;
+            if (H >= a.head_ha) low = fmax(low, sa + dmn * (double)(H - a.head_ha));
+            if (H >= a.head_hb) low = fmax(low, sb + dmn * (double)(H - a.head_hb));
+            ub = a.logfac + (A - low + kBoundEps * (1.0 + fabs(A) + low));
+            if (ub > cut) {
+              const int Sq = xr.penalty(ldr, M);
+              const double Af = as_f64(bload(r_pool, rb, 8 * SC)), dl = as_f64(bload(r_pool, rb, 8 * (SC + 1)));
+              const double pmin = dl * (double)Sq, pmax = dl * (double)(Sq + H);
+              ub = fmin(ub, a.logfac + (Af - pmin + kBoundEps * (1.0 + fabs(Af) + pmax)));
+            }
+          } else {
+            const int H = xr.mismatch(ldr, M);
+            const int Sq = xr.penalty(ldr, M);
+            const double Af = as_f64(bload(r_pool, rb, 8 * SC)), dl = as_f64(bload(r_pool, rb, 8 * (SC + 1)));
+            const double pmin = dl * (double)Sq, pmax = dl * (double)(Sq + H);
+            ub = a.logfac + (Af - pmin + kBoundEps * (1.0 + fabs(Af) + pmax));
+          }
+          ubmax = fmax(ubmax, ub);
+        }
+      }
+      mg = lo - ubmax;
+    }
+    if (w == 0 && act) s_mg[pt] = mg;
+    if (pass + 1 < npass) {
+      __syncthreads();                        // every group has read this pass's rows
+      stage();
+    }
+  }
+  __syncthreads();
+  const int64_t i = b0 + tid;
+  const bool active = tid < npts;
+  prepass_finish<kWideThreads>(a, i, active, active ? s_oc[tid] : 0, active ? s_mg[tid] : -INFINITY);
 }
 
 // Block offsets of the prepass lists and the dense, index-ordered list of uncertain rows
@@ -2099,6 +2373,24 @@ static hipError_t launch_prepass_w(const PrepassArgs& a, int nblocks, hipStream_
       return launch_prepass_t<WB, 4, false>(a, nblocks, s);
     }
   }
+  if (a.wide && wide_fits(WB, a.Ws) && prepass_wide_offsets_fit(a)) {
+    // cluster summaries in LDS while they fit beside the rows (40 KB at C4 with K = 10), for
+    // the instances that keep it without spilling (wb Ws <= 64 leaves NW = 2 to wb <= 2)
+    constexpr bool kClOk = WB == 1 || WB == 4;
+    const bool cl = kClOk && prepass_wide_lds_bytes(WB, a.Ws, a.m, a.K, a.bw, true) <= 96 * 1024;
+    const size_t lds = prepass_wide_lds_bytes(WB, a.Ws, a.m, a.K, a.bw, cl);
+    const dim3 g(nblocks), b(kWideThreads);
+    if constexpr (WB <= 2) {
+      if (a.Ws > 16) {
+        if (cl) hipLaunchKernelGGL((k_prepass_wide<WB, 2, kClOk>), g, b, lds, s, a);
+        else hipLaunchKernelGGL((k_prepass_wide<WB, 2, false>), g, b, lds, s, a);
+        return hipGetLastError();
+      }
+    }
+    if (cl) hipLaunchKernelGGL((k_prepass_wide<WB, 1, kClOk>), g, b, lds, s, a);
+    else hipLaunchKernelGGL((k_prepass_wide<WB, 1, false>), g, b, lds, s, a);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_prepass_generic, dim3(nblocks), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
@@ -2128,7 +2420,8 @@ hipError_t launch_prepass(const PrepassArgs& a, int nblocks, hipStream_t s) {
     case 1: return launch_prepass_w<1>(a, nblocks, s);
     case 2: return launch_prepass_w<2>(a, nblocks, s);
     case 4: return launch_prepass_w<4>(a, nblocks, s);
-    default: return launch_prepass_w<8>(a, nblocks, s);
+    case 8: return launch_prepass_w<8>(a, nblocks, s);
+    default: return hipErrorInvalidValue;
   }
 }
 

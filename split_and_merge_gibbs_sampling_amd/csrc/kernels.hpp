@@ -63,14 +63,25 @@ __host__ __device__ inline int bound_words(int wb, int Ws) { return (wb + kQ) * 
 // variance s2 = sum_j (1 - 1/m_j) / m_j whatever the point; h_a = mu - 4 s, h_b = mu - 1.25 s
 // (tools/latent_bound_study.py: at C5 the bound leaves 6e-5 of the picks uncertain; those
 // lanes gather the full record).  Used for the templated prepass layouts (Ws == 2, or
-// Ws == 4 with wb <= 4).
+// Ws == 4 with wb <= 4: the head padded to a power of two words) and the wide prepass
+// (k_prepass_wide: padded to a multiple of 8 words, 64 B; 448 B at C4 instead of the
+// 864-B record).
 constexpr __host__ __device__ inline int head_words(int wb, int Ws) { return wb * Ws + 2; }
+constexpr __host__ __device__ inline bool templ_fits(int wb, int Ws) { return Ws == 2 || (Ws == 4 && wb <= 4); }
+// Wide layouts: one 16-lane group per point (a lane per plane word, Ws <= 32 so at most two
+// words per lane), the workgroup's 64-point row tile staged in LDS ((wb Ws + 1) words per
+// point) and the next tile prefetched in registers (wb Ws <= 64: 4 words per thread).
+constexpr int kWideRowMax = 64;
+constexpr __host__ __device__ inline bool wide_fits(int wb, int Ws) {
+  return !templ_fits(wb, Ws) && Ws <= 32 && wb * Ws <= kWideRowMax;
+}
 constexpr __host__ __device__ inline int head_stride(int wb, int Ws) {
+  if (!templ_fits(wb, Ws)) return (head_words(wb, Ws) + 7) / 8 * 8;
   int s = 4;
   while (s < head_words(wb, Ws)) s *= 2;
   return s;
 }
-__host__ __device__ inline bool head_fits(int wb, int Ws) { return Ws == 2 || (Ws == 4 && wb <= 4); }
+__host__ __device__ inline bool head_fits(int wb, int Ws) { return templ_fits(wb, Ws) || wide_fits(wb, Ws); }
 
 // Rows, tiled: word q of point i at ((i/64) * W + q) * 64 + i%64 (W words per row).
 __host__ __device__ inline int64_t packed_offset(int64_t i, int q, int W) {
@@ -113,6 +124,7 @@ struct PrepassArgs {
   int4* rq;                  // per dense-list position: {row, point, slot, categorical draw}
   int p0;
   int exact_wave;            // 1: exact rows one wave per point (no workgroup staging)
+  int wide;                  // 1: wide layouts take k_prepass_wide (0: the generic kernel)
 };
 
 // The resolver runs in block mode (csrc/kernels.hip, k_resolve_blk) when in the previous

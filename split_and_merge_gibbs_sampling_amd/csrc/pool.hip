@@ -211,58 +211,79 @@ __device__ __forceinline__ float f32_up(double x) {
   return f;
 }
 
+// Order-preserving key of a double (unsigned compare of keys = numeric compare).
+__device__ __forceinline__ uint64_t dkey(double x) {
+  const uint64_t u = (uint64_t)__double_as_longlong(x);
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+
+// Sum of the h smallest of the wave's values dv (NV per lane, +inf padding): bisection on
+// the key for the h-th smallest value t (64 steps, each a wave-wide count of keys < mid),
+// then sum(values < t) + (h - count(values < t)) t.
+template <int NV>
+__device__ __forceinline__ double sum_smallest(const double (&dv)[NV], const uint64_t (&key)[NV], int h) {
+  if (h <= 0) return 0.0;
+  uint64_t lo = 0, hi = ~0ull;        // invariant: count(key <= lo) < h <= count(key <= hi)
+  while (hi - lo > 1) {
+    const uint64_t mid = lo + (hi - lo) / 2;
+    int c = 0;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) c += __popcll(__ballot(key[k] <= mid));
+    if (c >= h) hi = mid;
+    else lo = mid;
+  }
+  // hi is the key of the h-th smallest value
+  double s = 0.0, t = -__builtin_inf();
+  int below = 0;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    if (key[k] < hi) s += dv[k];
+    if (key[k] == hi) t = dv[k];
+    below += __popcll(__ballot(key[k] < hi));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o);
+    t = fmax(t, __shfl_xor(t, o));     // every lane holding the key holds the same value
+  }
+  return s + (double)(h - below) * t;
+}
+
 // Pool-entry heads (kernels.hpp) from the dhamming tables and bound records: one wave per
-// entry, NV = Ws attributes per lane (d <= 64 Ws).  The rank of d_j among the entry's d
-// (ties by index) selects the h_a / h_b smallest for S_a / S_b.  Host and device pools alike.
+// entry, nv = Ws attributes per lane (d <= 64 nv, nv <= NV).  S_a / S_b are the sums of the
+// h_a / h_b smallest d_j (sum_smallest).  Host and device pools alike.
 template <int NV>
 __global__ __launch_bounds__(256) void k_pool_heads(const double* __restrict__ tab, const uint64_t* __restrict__ bnd,
-                                                   int64_t P, int d, int wb, int bw, int ha, int hb,
+                                                   int64_t P, int d, int wb, int nv, int bw, int ha, int hb,
                                                    uint64_t* __restrict__ head) {
   const int lane = threadIdx.x & 63;
   const int64_t e = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (e >= P) return;
   const double* t = tab + e * 2 * d;
   double dv[NV];
+  uint64_t key[NV];
   double mn = __builtin_inf();
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int j = 64 * k + lane;
     dv[k] = j < d ? t[2 * j] - t[2 * j + 1] : __builtin_inf();   // d_j as in Ctx::bounds_for
+    key[k] = dkey(dv[k]);
     mn = fmin(mn, dv[k]);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mn = fmin(mn, __shfl_xor(mn, o));
-  int rank[NV];
-#pragma unroll
-  for (int k = 0; k < NV; ++k) rank[k] = 0;
-  for (int k2 = 0; k2 < NV; ++k2)
-    for (int l = 0; l < 64; ++l) {
-      const double y = __shfl(dv[k2], l);
-      const int jy = 64 * k2 + l;
-#pragma unroll
-      for (int k = 0; k < NV; ++k) rank[k] += (y < dv[k] || (y == dv[k] && jy < 64 * k + lane)) ? 1 : 0;
-    }
-  double sa = 0.0, sb = 0.0;
-#pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    if (64 * k + lane < d && rank[k] < ha) sa += dv[k];
-    if (64 * k + lane < d && rank[k] < hb) sb += dv[k];
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    sa += __shfl_xor(sa, o);
-    sb += __shfl_xor(sb, o);
-  }
-  const int HW = wb * NV + 2, HS = head_stride(wb, NV);
-  if (lane < HS) {
-    const uint64_t* r = bnd + e * bw;
+  const double sa = sum_smallest<NV>(dv, key, ha < d ? ha : d);
+  const double sb = sum_smallest<NV>(dv, key, hb < d ? hb : d);
+  const int HW = wb * nv + 2, HS = head_stride(wb, nv);
+  const uint64_t* r = bnd + e * bw;
+  for (int q = lane; q < HS; q += 64) {
     uint64_t v = 0;
-    if (lane >= HW) {
-      // padding to the power-of-two stride
-    } else if (lane < HW - 2) {
-      v = r[lane];
-    } else if (lane == HW - 2) {
-      const int SC = (wb + kQ) * NV;
+    if (q >= HW) {
+      // padding to the head stride
+    } else if (q < HW - 2) {
+      v = r[q];
+    } else if (q == HW - 2) {
+      const int SC = (wb + kQ) * nv;
       const double A_up = __longlong_as_double((long long)r[SC]) +
                           kBoundEps * (1.0 + __longlong_as_double((long long)r[SC + 3]));
       v = (uint64_t)__float_as_uint(f32_up(A_up)) | ((uint64_t)__float_as_uint(f32_down(mn > 0 ? mn : 0.0)) << 32);
@@ -273,17 +294,20 @@ __global__ __launch_bounds__(256) void k_pool_heads(const double* __restrict__ t
       v = (uint64_t)__float_as_uint(ha > 0 ? fmaxf(fa, 0.0f) : 0.0f) |
           ((uint64_t)__float_as_uint(hb > 0 ? fmaxf(fb, 0.0f) : 0.0f) << 32);
     }
-    head[e * HS + lane] = v;
+    head[e * HS + q] = v;
   }
 }
 
 hipError_t launch_pool_heads(const double* tab, const uint64_t* bnd, int64_t P, int d, int wb, int Ws, int bw, int ha,
                              int hb, uint64_t* head, hipStream_t s) {
   if (P <= 0) return hipSuccess;
+  if (!head_fits(wb, Ws)) return hipErrorInvalidValue;
   const dim3 g((unsigned)((P + 3) / 4)), b(256);
-  if (Ws == 2) hipLaunchKernelGGL(k_pool_heads<2>, g, b, 0, s, tab, bnd, P, d, wb, bw, ha, hb, head);
-  else if (Ws == 4) hipLaunchKernelGGL(k_pool_heads<4>, g, b, 0, s, tab, bnd, P, d, wb, bw, ha, hb, head);
-  else return hipErrorInvalidValue;
+  if (Ws == 2) hipLaunchKernelGGL(k_pool_heads<2>, g, b, 0, s, tab, bnd, P, d, wb, Ws, bw, ha, hb, head);
+  else if (Ws == 4) hipLaunchKernelGGL(k_pool_heads<4>, g, b, 0, s, tab, bnd, P, d, wb, Ws, bw, ha, hb, head);
+  else if (Ws <= 8) hipLaunchKernelGGL(k_pool_heads<8>, g, b, 0, s, tab, bnd, P, d, wb, Ws, bw, ha, hb, head);
+  else if (Ws <= 16) hipLaunchKernelGGL(k_pool_heads<16>, g, b, 0, s, tab, bnd, P, d, wb, Ws, bw, ha, hb, head);
+  else hipLaunchKernelGGL(k_pool_heads<32>, g, b, 0, s, tab, bnd, P, d, wb, Ws, bw, ha, hb, head);
   return hipGetLastError();
 }
 

@@ -119,9 +119,13 @@ class Engine:
         wb = 1 if mmax <= 2 else 2 if mmax <= 4 else 4 if mmax <= 16 else 8
         wd = -(-self.d // 64)
         Ws = 2 if wd <= 2 else 4 if wd <= 4 else wd
-        stride = 4
-        while stride < wb * Ws + 2:
-            stride *= 2
+        hw = wb * Ws + 2
+        if Ws == 2 or (Ws == 4 and wb <= 4):      # kernels.hpp head_stride
+            stride = 4
+            while stride < hw:
+                stride *= 2
+        else:
+            stride = -(-hw // 8) * 8
         out = np.zeros((P, stride), np.uint64)
         self._check(self._L.hdpm_get_pool_heads(self._h, ptr(out), int(P)))
         return out

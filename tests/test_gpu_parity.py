@@ -479,8 +479,9 @@ def _head_bound_check(oracle, ds, heads, pc, ps, npts=600, nent=400, seed=0):
     L, _ = oracle.loglik_matrix(ds.codes[pts], ds.attrisize, pc[ents], ps[ents])     # exact rows
     d = ds.d
     mmax = int(ds.attrisize.max())
-    wb = 1 if mmax <= 2 else 2 if mmax <= 4 else 4
-    Ws = 2 if d <= 128 else 4
+    wb = 1 if mmax <= 2 else 2 if mmax <= 4 else 4 if mmax <= 16 else 8
+    wd = -(-d // 64)
+    Ws = 2 if wd <= 2 else 4 if wd <= 4 else wd           # kernels.hpp plane_words
     hw = wb * Ws + 2
     assert heads.shape[1] >= hw and np.all(heads[:, hw:] == 0)
     heads = heads[:, :hw]
@@ -544,12 +545,28 @@ def test_pool_heads_binary_and_absent(hd, oracle):
     eng.set_pool(pc, ps)
     _head_bound_check(oracle, wide, eng.get_pool_heads(1500), pc, ps, npts=300, nent=300)
     eng.close()
-    wider = synth(300, 300, 4, 4, seed=26)             # d > 256: generic prepass, no heads
+    wider = synth(300, 300, 4, 4, seed=26)             # d = 300: Ws = 5, wb = 2, wide prepass heads
     eng = make_engine(hd, wider)
     pc, ps, _ = oracle.pool_generate(wider.attrisize, wider.v, wider.w, 900, st)
     eng.set_pool(pc, ps)
+    heads = eng.get_pool_heads(900)
+    assert heads.shape[1] == 16                        # 12 words padded to a multiple of 8
+    _head_bound_check(oracle, wider, heads, pc, ps, npts=200, nent=200)
+    eng.close()
+    c4ish = synth(200, 784, 4, 6, seed=29)             # C4's layout: Ws = 13, wb = 4, 56-word heads
+    eng = make_engine(hd, c4ish)
+    pc, ps, _ = oracle.pool_generate(c4ish.attrisize, c4ish.v, c4ish.w, 600, st)
+    eng.set_pool(pc, ps)
+    heads = eng.get_pool_heads(600)
+    assert heads.shape[1] == 56
+    _head_bound_check(oracle, c4ish, heads, pc, ps, npts=100, nent=150)
+    eng.close()
+    widest = synth(100, 2100, 3, 2, seed=30)           # Ws = 33 > 32: generic prepass, no heads
+    eng = make_engine(hd, widest)
+    pc, ps, _ = oracle.pool_generate(widest.attrisize, widest.v, widest.w, 300, st)
+    eng.set_pool(pc, ps)
     with pytest.raises(hd.HdpmError):
-        eng.get_pool_heads(900)
+        eng.get_pool_heads(300)
     eng.close()
 
 
@@ -566,6 +583,49 @@ def test_wide_mixed_levels_sweeps_heads_and_records(hd, oracle, debug):
     ds = synth(3000, 200, 6, (2, 6), seed=27)          # Ws = 4, wb = 4 heads
     cen, sig = random_params(ds, 6, 28)
     sweep_case(hd, oracle, ds, ds.truth, cen, sig, ds.n * 3, seed=47, sweeps=3, phi=True, debug=debug)
+
+
+# k_prepass_wide (16-lane group per point) against the oracle on wide layouts, with heads,
+# with full records (1024) and with the generic one-thread-per-point prepass (16384).  The
+# chain starts from the ground truth with update_phi'd parameters (hdpm_init_chain), so
+# most points are certified by the bounds and the rest take exact rows.
+@pytest.mark.parametrize("debug", [0, 1024, 16384])
+@pytest.mark.parametrize("shape", ["c4", "c4_k80", "ws18_binary", "ws5_wb8", "ws5_wb2", "ws20_wb2"])
+def test_wide_prepass_sweeps(hd, oracle, debug, shape):
+    if shape == "c4":
+        ds = synth(4000, 784, 6, 6, seed=31)           # Ws = 13, wb = 4 (C4's layout)
+    elif shape == "c4_k80":
+        ds = synth(4000, 784, 80, 6, seed=36)          # cluster summaries beyond the LDS budget
+    elif shape == "ws18_binary":
+        ds = synth(3000, 1100, 5, 2, seed=32)          # Ws = 18: two plane words per lane
+    elif shape == "ws5_wb8":
+        ds = synth(2000, 300, 5, 20, seed=33)          # Ws = 5, wb = 8
+    elif shape == "ws5_wb2":
+        ds = synth(2000, 300, 5, 4, seed=37)           # Ws = 5, wb = 2
+    else:
+        ds = synth(2000, 1250, 5, 4, seed=38)          # Ws = 20, wb = 2: two words per lane
+    eng = make_engine(hd, ds)
+    eng.set_seed(35)
+    eng.set_debug(debug)
+    params = eng.chain_params(m=3, iterations=1, L=0, burnin=0, neal8=True, split_merge=False)
+    eng.init_chain(params, c_i=ds.truth)
+    c, cen, sig = eng.get_state()
+    pc, ps = eng.get_pool(ds.n * 3)
+    ost = oracle_state(oracle, c.copy(), cen.copy(), sig.copy())
+    st = eng.rng_state.copy()
+    for _ in range(3):
+        eng.neal8_sweep(3)
+        assert oracle.neal8_sweep(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w, ost, 3, pc, ps, st) == 0
+        assert_same_state(eng, ost)
+        assert np.array_equal(eng.rng_state, st)
+        eng.update_phi()
+        assert oracle.update_phi(ds.codes, ds.attrisize, ds.v, ds.w, ost, st) == 0
+        assert_same_state(eng, ost)
+        assert np.array_equal(eng.rng_state, st)
+    stats = eng.stats()
+    if debug == 0:
+        assert stats["listed_points"] < 3 * ds.n // 2, stats     # the bounds certify most points
+    eng.close()
 
 
 def test_hig_logspace_chain_large_clusters(hd, oracle):

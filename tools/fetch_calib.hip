@@ -34,6 +34,23 @@ __global__ void k_gather(const uint4* __restrict__ buf, int64_t nrec, int R, uin
   if ((acc.x & 0xfffff) == 0x12345) out[t & 1023] = acc;
 }
 
+// 16-lane groups each gather R records of W 8-B words at random record indices (a lane per
+// word, as k_prepass_wide reads a wide pool-entry head: 56 words = 448 B at C4)
+template <int W>
+__global__ void k_gather_group(const uint64_t* __restrict__ buf, int64_t nrec, int R, uint64_t seed, uint4* out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t g = t >> 4;
+  const int lane = (int)(t & 15);
+  uint64_t acc = 0;
+  for (int r = 0; r < R; ++r) {
+    const int64_t e = (int64_t)(mix(seed + g * 131 + r) % (uint64_t)nrec);
+    const uint64_t* p = buf + e * W;
+#pragma unroll
+    for (int k = lane; k < W; k += 16) acc ^= p[k];
+  }
+  if ((acc & 0xfffff) == 0x12345) out[t & 1023] = make_uint4((uint32_t)acc, 0, 0, 0);
+}
+
 __global__ void k_stream(const uint4* __restrict__ buf, int64_t n16, uint4* out) {
   uint4 acc = make_uint4(0, 0, 0, 0);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x) {
@@ -73,6 +90,14 @@ int main() {
     (void)hipEventSynchronize(b);
     (void)hipEventElapsedTime(&ms, a, b);
     std::printf("stream16  %.1f MB, %.1f us\n", bytes / 4 / 1e6, ms * 1e3);
+    (void)hipEventRecord(a);
+    hipLaunchKernelGGL(k_gather_group<56>, dim3(blocks * 4), dim3(threads), 0, 0, (const uint64_t*)buf,
+                       (int64_t)(bytes / 448), R, 55 + rep, out);
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    (void)hipEventElapsedTime(&ms, a, b);
+    std::printf("gather448g %.0f records, %.1f MB, %.1f us\n", nthr * 4 / 16 * R, nthr * 4 / 16 * R * 448 / 1e6,
+                ms * 1e3);
   }
   (void)hipFree(buf);
   (void)hipFree(out);
