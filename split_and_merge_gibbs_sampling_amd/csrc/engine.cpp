@@ -1548,7 +1548,7 @@ struct Ctx {
     d_margin.ensure(n);
     d_rowpos.ensure(n);
     d_list.ensure((size_t)nb_max * kBlock);
-    d_cnt.ensure(nb_max);
+    d_cnt.ensure((size_t)nb_max * (kBlock / 16));   // list blocks of 16 points (k_prepass_wide chunks)
     d_dense.ensure((size_t)nb_max * kBlock);
     d_dense_total.ensure(1);
     d_spec.ensure((size_t)nb_max * kBlock);

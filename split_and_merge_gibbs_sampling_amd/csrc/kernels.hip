@@ -441,12 +441,15 @@ __global__ __launch_bounds__(kBlock) void k_prepass_generic(PrepassArgs a) {
 // records): the same bounds as k_prepass, but a point is worked on by a 16-lane group, lane
 // w holding plane word w (and w + 16) of every bit-plane, so each record is read once per
 // point with coalesced 8-B loads (a 104-B run per plane) and H / Sq are summed across the
-// group with DPP row operations (one DPP row = one group).  The workgroup's kBlock points
-// go through in 64-point passes: the pass's rows are staged in LDS from the tiled row array
-// (coalesced), point-major with one word of padding.  Latent picks gather the entry's head
-// (codes + the four floats, 448 B at C4); a group whose head bound does not clear `cut`
-// reads the record's penalty planes too.
-constexpr int kWideThreads = 1024;          // 64 groups of 16: one 64-point pass at a time
+// group with DPP row operations (one DPP row = one group).  Persistent workgroups of 16
+// groups walk 16-point chunks (chunk c = blockIdx + k gridDim: no tail of a second wave of
+// workgroups), staging each chunk's rows, labels, counts and raw draws in LDS while the
+// previous chunk is computed (register prefetch); the cluster summaries are staged once per
+// workgroup.  Latent picks gather the entry's head (codes + the four floats, 448 B at C4); a
+// group whose head bound does not clear `cut` reads the record's penalty planes too.  Each
+// chunk is its own list block (kWideChunk points: cnt[c], list rows c * kWideChunk + q).
+constexpr int kWideThreads = 256;           // 16 groups of 16 lanes
+constexpr int kWideChunk = kWideThreads / 16;
 
 // Sum over the 16 lanes of a DPP row (every lane gets the total).
 __device__ __forceinline__ int row_sum16(int v) {
@@ -502,96 +505,117 @@ struct WideRow {
   }
 };
 
-// Dynamic LDS of k_prepass_wide: the pass's rows [64][wb Ws + 1], the block's raw draws
-// [kBlock][m + 1] (u32), and (CL) the cluster summaries [K][bw + 2].
-constexpr int kWidePf = kWideRowMax * 64 / kWideThreads;   // row words per thread prefetched for the next pass
-__host__ __device__ inline size_t wide_rows_words(int wb, int Ws) { return (size_t)64 * (wb * Ws + 1); }
-__host__ __device__ inline size_t wide_raw_words(int m) { return ((size_t)kBlock * (m + 1) + 1) / 2; }
+// Dynamic LDS of k_prepass_wide: the chunk's rows [16][wb Ws + 1], and (CL) the cluster
+// summaries [K][bw + 2].
+constexpr int kWidePf = kWideRowMax * kWideChunk / kWideThreads;   // row words per thread prefetched
+constexpr int kWideMaxM1 = 16;              // m + 1 <= 16: a chunk's raw draws fit one wave's lanes x 4
+__host__ __device__ inline size_t wide_rows_words(int wb, int Ws) { return (size_t)kWideChunk * (wb * Ws + 1); }
 size_t prepass_wide_lds_bytes(int wb, int Ws, int m, int K, int bw, bool cl) {
-  return 8 * (wide_rows_words(wb, Ws) + wide_raw_words(m) + (cl ? (size_t)K * (bw + 2) : 0));
+  (void)m;
+  return 8 * (wide_rows_words(wb, Ws) + (cl ? (size_t)K * (bw + 2) : 0));
 }
 // byte offsets of the record arrays must fit the buffer instructions' 32-bit offsets
 bool prepass_wide_offsets_fit(const PrepassArgs& a) {
   const int64_t hs = head_stride(a.wb, a.Ws);
-  return a.P * (int64_t)std::max<int64_t>(a.bw, hs) * 8 + 4096 < 0x7fffffff;
+  return a.m + 1 <= kWideMaxM1 && a.P * (int64_t)std::max<int64_t>(a.bw, hs) * 8 + 4096 < 0x7fffffff;
 }
 
 template <int WB, int NW, bool CL>
-__global__ __launch_bounds__(kWideThreads) void k_prepass_wide(PrepassArgs a) {
+__global__ __launch_bounds__(kWideThreads) void k_prepass_wide(PrepassArgs a, int nchunks) {
   extern __shared__ uint64_t s_dyn[];
-  __shared__ double s_mg[kBlock];
-  __shared__ int s_oc[kBlock];
-  __shared__ int s_own[kBlock];
+  __shared__ double s_mg[2][kWideChunk];
+  __shared__ int s_oc[2][kWideChunk];
+  __shared__ int s_own[2][kWideChunk];
+  __shared__ uint32_t s_raw[2][kWideChunk * kWideMaxM1];
   const int WS = a.Ws, WR = WB * WS, RS = WR + 1, SC = (WB + kQ) * WS, HS = head_stride(WB, WS);
   const int bw = a.bw, cw = a.bw + 2;
   uint64_t* s_rows = s_dyn;
-  uint32_t* s_raw = (uint32_t*)(s_dyn + wide_rows_words(WB, WS));
-  uint64_t* s_cs = s_dyn + wide_rows_words(WB, WS) + wide_raw_words(a.m);
+  uint64_t* s_cs = s_dyn + wide_rows_words(WB, WS);
   const int tid = threadIdx.x, g = tid >> 4, w = tid & 15, m1 = a.m + 1;
   const int w8 = 8 * w;
-  const int64_t b0 = (int64_t)a.p0 + (int64_t)blockIdx.x * kBlock;
-  const int npts = (int)min((int64_t)kBlock, (int64_t)a.n - b0);
   const __amdgpu_buffer_rsrc_t r_slot = make_rsrc(a.slot_bnd, (int64_t)(a.S + 2) * bw * 8);
   const __amdgpu_buffer_rsrc_t r_pool = make_rsrc(a.pool_bnd, a.P * bw * 8);
   const __amdgpu_buffer_rsrc_t r_head = make_rsrc(a.pool_head, a.P * HS * 8);
   const __amdgpu_buffer_rsrc_t r_csum = make_rsrc(a.csum, (int64_t)a.K * cw * 8);
-  // block prologue: labels and counts, raw draws, cluster summaries, the first pass's rows
-  if (tid < npts) {
-    const int o = a.c[b0 + tid];
-    s_own[tid] = o;
-    s_oc[tid] = a.counts[o];
-  }
-  for (int e = tid; e < npts * m1; e += kWideThreads) s_raw[e] = a.raw[b0 * m1 + e];
   if constexpr (CL) {
     for (int e = tid; e < a.K * cw; e += kWideThreads) s_cs[e] = a.csum[e];
   }
+  // the next chunk's rows, label / count and raw draws, in registers until staged
   uint64_t pf[kWidePf];
-  auto fetch = [&](int64_t t0) {
+  int pf_own = 0, pf_oc = 0;
+  uint32_t pf_raw[4];
+  auto fetch = [&](int c) {
+    const int64_t i0 = (int64_t)a.p0 + (int64_t)c * kWideChunk;
 #pragma unroll
     for (int r = 0; r < kWidePf; ++r) {
       const int e = tid + r * kWideThreads;
-      if (e < 64 * WR) {
-        const int64_t i = min(t0 + (e & 63), (int64_t)a.n - 1);
-        pf[r] = a.xbs[packed_offset(i, e >> 6, WR)];
+      if (e < kWideChunk * WR) {
+        const int64_t i = min(i0 + (e & (kWideChunk - 1)), (int64_t)a.n - 1);
+        pf[r] = a.xbs[packed_offset(i, e / kWideChunk, WR)];
+      }
+    }
+    if (tid < kWideChunk) {
+      pf_own = a.c[min(i0 + tid, (int64_t)a.n - 1)];
+      pf_oc = a.counts[pf_own];
+    }
+    if (tid < 64) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int e = tid + 64 * r;
+        const int64_t ie = i0 * m1 + e;
+        pf_raw[r] = (e < kWideChunk * m1 && ie < (int64_t)a.n * m1) ? a.raw[ie] : 0u;
       }
     }
   };
-  auto stage = [&]() {
+  auto stage = [&](int par) {
 #pragma unroll
     for (int r = 0; r < kWidePf; ++r) {
       const int e = tid + r * kWideThreads;
-      if (e < 64 * WR) s_rows[(e & 63) * RS + (e >> 6)] = pf[r];
+      if (e < kWideChunk * WR) s_rows[(e & (kWideChunk - 1)) * RS + e / kWideChunk] = pf[r];
+    }
+    if (tid < kWideChunk) {
+      s_own[par][tid] = pf_own;
+      s_oc[par][tid] = pf_oc;
+    }
+    if (tid < 64) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (tid + 64 * r < kWideChunk * m1) s_raw[par][tid + 64 * r] = pf_raw[r];
     }
   };
-  fetch(b0);
-  stage();
+  int c = blockIdx.x;
+  if (c < nchunks) {
+    fetch(c);
+    stage(0);
+  }
   WideRow<WB, NW> xr;
   xr.WS = WS;
 #pragma unroll
   for (int k = 0; k < NW; ++k) xr.val[k] = w + 16 * k < WS;
-  const int npass = (npts + 63) / 64;
+  int par = 0;
 #pragma unroll 1
-  for (int pass = 0; pass < npass; ++pass) {
-    __syncthreads();                          // rows of this pass staged (and the prologue)
-    if (pass + 1 < npass) fetch(b0 + 64 * (pass + 1));
-    const int pt = 64 * pass + g;             // point within the block
-    const bool act = pt < npts;
-    const int ptc = act ? pt : npts - 1;
+  for (; c < nchunks; c += gridDim.x, par ^= 1) {
+    __syncthreads();                          // the chunk is staged (and the cluster summaries)
+    const int cn = c + gridDim.x;
+    if (cn < nchunks) fetch(cn);
+    const int64_t i0 = (int64_t)a.p0 + (int64_t)c * kWideChunk;
+    const int npts = (int)min((int64_t)kWideChunk, (int64_t)a.n - i0);
+    const bool act = g < npts;
 #pragma unroll
     for (int k = 0; k < NW; ++k)
 #pragma unroll
       for (int b = 0; b < WB; ++b) xr.x[k][b] = xr.val[k] ? s_rows[g * RS + b * WS + w + 16 * k] : 0ull;
-    const int own = s_own[ptc];
-    const int own_cnt = s_oc[ptc];
+    const int own = s_own[par][g];
+    const int own_cnt = s_oc[par][g];
     double mg = -INFINITY;
-    if (own_cnt >= 2) {                       // group-uniform
-      const uint32_t* raw = s_raw + ptc * m1;
+    if (act && own_cnt >= 2) {                // group-uniform
+      const uint32_t* raw = s_raw[par] + g * m1;
       // the first latent heads' gathers go out first (their latency overlaps the own-cluster
       // bound and the cluster loop)
       constexpr int LW = WB * NW;
       constexpr int NPF = LW <= 4 ? 3 : LW <= 8 ? 2 : 1;   // heads in flight (register budget)
       uint64_t Hd[NPF][LW + 2];
-      int pe[NPF];                            // byte offset of the pick's record / head
+      int pe[NPF];                            // entry of the pick
       const bool heads = a.pool_head != nullptr;
       auto gather = [&](int u, int l) {
         const int e = (int)pick_entry(raw[l], a.P);
@@ -697,23 +721,49 @@ __global__ __launch_bounds__(kWideThreads) void k_prepass_wide(PrepassArgs a) {
       }
       mg = lo - ubmax;
     }
-    if (w == 0 && act) s_mg[pt] = mg;
-    if (pass + 1 < npass) {
-      __syncthreads();                        // every group has read this pass's rows
-      stage();
+    if (w == 0) s_mg[par][g] = mg;
+    __syncthreads();                          // margins written; every group has read the rows
+    if (tid < 64) {
+      // the chunk's margins, row positions and ordered compaction (one list block per chunk)
+      const bool on = tid < npts;
+      const double mgp = on ? s_mg[par][tid] : -INFINITY;
+      const int ocp = on ? s_oc[par][tid] : 0;
+      const bool uncertain = on && !(ocp >= 2 && mgp > a.thresh);
+      const int64_t i = i0 + tid;
+      if (on) a.margin[i] = mgp;
+      const unsigned long long bal = __ballot(uncertain);
+      const int row = c * kWideChunk + __popcll(bal & ((1ull << tid) - 1ull));
+      if (on) a.rowpos[i] = uncertain ? row : -1;
+      if (uncertain) a.list[row] = (int)i;
+      if (tid == 0) a.cnt[c] = __popcll(bal);
     }
+    if (cn < nchunks) stage(par ^ 1);
   }
-  __syncthreads();
-  const int64_t i = b0 + tid;
-  const bool active = tid < npts;
-  prepass_finish<kWideThreads>(a, i, active, active ? s_oc[tid] : 0, active ? s_mg[tid] : -INFINITY);
+}
+
+// Workgroups of k_prepass_wide in flight on the whole GPU (persistent grid).
+template <class F>
+static int wide_grid(F kern, size_t lds) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  int per = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, kWideThreads, lds) != hipSuccess || per <= 0) per = 1;
+  return cus * per;
+}
+
+int prepass_list_block(const PrepassArgs& a) {
+  return (a.wide && wide_fits(a.wb, a.Ws) && prepass_wide_offsets_fit(a)) ? kWideChunk : kBlock;
 }
 
 // Block offsets of the prepass lists and the dense, index-ordered list of uncertain rows
-// (row = prepass block * kBlock + position), so the serial resolver reads it 64 at a time
+// (row = list block * its points (kBlock, or kWideChunk) + position), so the serial resolver reads it 64 at a time
 // instead of walking every block count.  One workgroup of 1024 threads.
 constexpr int kScanThreads = 1024;
-__global__ __launch_bounds__(kScanThreads) void k_list_scan(const int* __restrict__ cnt, int nblocks,
+__global__ __launch_bounds__(kScanThreads) void k_list_scan(const int* __restrict__ cnt, int nblocks, int lblock,
                                                            int* __restrict__ dense, int* __restrict__ total) {
   __shared__ int s_sum[kScanThreads / kWave];
   const int tid = threadIdx.x;
@@ -740,7 +790,7 @@ __global__ __launch_bounds__(kScanThreads) void k_list_scan(const int* __restric
   int off = base + inc - mine;
   for (int b = b0; b < b1; ++b) {
     const int c = cnt[b];
-    for (int q = 0; q < c; ++q) dense[off + q] = b * kBlock + q;
+    for (int q = 0; q < c; ++q) dense[off + q] = b * lblock + q;
     off += c;
   }
   if (tid == 0) *total = all;
@@ -2374,29 +2424,30 @@ static hipError_t launch_prepass_w(const PrepassArgs& a, int nblocks, hipStream_
     }
   }
   if (a.wide && wide_fits(WB, a.Ws) && prepass_wide_offsets_fit(a)) {
-    // cluster summaries in LDS while they fit beside the rows (40 KB at C4 with K = 10), for
+    // cluster summaries in LDS while they fit beside the rows (9 KB at C4 with K = 10), for
     // the instances that keep it without spilling (wb Ws <= 64 leaves NW = 2 to wb <= 2)
     constexpr bool kClOk = WB == 1 || WB == 4;
-    const bool cl = kClOk && prepass_wide_lds_bytes(WB, a.Ws, a.m, a.K, a.bw, true) <= 96 * 1024;
+    const bool cl = kClOk && prepass_wide_lds_bytes(WB, a.Ws, a.m, a.K, a.bw, true) <= 40 * 1024;
     const size_t lds = prepass_wide_lds_bytes(WB, a.Ws, a.m, a.K, a.bw, cl);
-    const dim3 g(nblocks), b(kWideThreads);
+    const int nchunks = (a.n - a.p0 + kWideChunk - 1) / kWideChunk;
+    auto go = [&](auto kern) {
+      const int grid = std::min(nchunks, wide_grid(kern, lds));
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(kWideThreads), lds, s, a, nchunks);
+      return hipGetLastError();
+    };
     if constexpr (WB <= 2) {
-      if (a.Ws > 16) {
-        if (cl) hipLaunchKernelGGL((k_prepass_wide<WB, 2, kClOk>), g, b, lds, s, a);
-        else hipLaunchKernelGGL((k_prepass_wide<WB, 2, false>), g, b, lds, s, a);
-        return hipGetLastError();
-      }
+      if (a.Ws > 16) return cl ? go(k_prepass_wide<WB, 2, kClOk>) : go(k_prepass_wide<WB, 2, false>);
     }
-    if (cl) hipLaunchKernelGGL((k_prepass_wide<WB, 1, kClOk>), g, b, lds, s, a);
-    else hipLaunchKernelGGL((k_prepass_wide<WB, 1, false>), g, b, lds, s, a);
-    return hipGetLastError();
+    return cl ? go(k_prepass_wide<WB, 1, kClOk>) : go(k_prepass_wide<WB, 1, false>);
   }
   hipLaunchKernelGGL(k_prepass_generic, dim3(nblocks), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_exact_rows(const PrepassArgs& a, int nblocks, hipStream_t s) {
-  hipLaunchKernelGGL(k_list_scan, dim3(1), dim3(kScanThreads), 0, s, a.cnt, nblocks, a.dense, a.dense_total);
+  const int lb = prepass_list_block(a);
+  hipLaunchKernelGGL(k_list_scan, dim3(1), dim3(kScanThreads), 0, s, a.cnt, (a.n - a.p0 + lb - 1) / lb, lb, a.dense,
+                     a.dense_total);
   const int E = a.K + a.m;
   const size_t lds = exact_wg_lds_bytes(E, a.d, a.nq * 16);
   const dim3 g(std::min(nblocks * 4, 1024)), b(kExactWgThreads);
