@@ -451,7 +451,7 @@ static void pool_for(int64_t n, F f, int64_t grain = 0) {
 
 // Device scratch of the split-merge move (split_merge.inl).
 struct SmWork {
-  DevBuf<int> d_S, d_side, d_side_ref, d_counts2;
+  DevBuf<int> d_S, d_side, d_side_ref, d_counts2, d_cert;
   DevBuf<double> d_ll, d_out;
   DevBuf<uint8_t> d_two_codes;
   DevBuf<double> d_two_tab;

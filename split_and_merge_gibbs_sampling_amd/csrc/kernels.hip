@@ -2672,8 +2672,8 @@ __device__ __forceinline__ int two_way_draw(double v0, double v1, double rU) {
 // only changes where D crosses 0 (the revsort order), lam or -lam.  A lane whose D range
 // stays 1e-4 away from all three (there p0 is >= 2e-15 from its threshold, far beyond the
 // few-ulp rounding of the exp and divisions) has one pick for every count it can see and is
-// settled in parallel without evaluating the draw; the others are drawn one by one with
-// their exact counts.
+// settled in parallel without evaluating the draw; the others are drawn with their exact
+// counts, all at once, by the fixed-point iteration below.
 //
 // The margin.  Near a threshold D0 (0, lam or -lam) the computed p0 = 1 / (1 + exp(-D)) (or
 // its complement) moves by |p0'| |D - D0| >= p (1 - p) |D - D0|, and p (1 - p) >= 2e-11 for the
@@ -2683,71 +2683,152 @@ __device__ __forceinline__ int two_way_draw(double v0, double v1, double rU) {
 // their magnitudes, < 1e-9 for any |S| and D the engine accepts), and exp / the two
 // divisions add a few ulp of p0 (< 1e-15): both far inside the margin.
 constexpr double kSmScanMargin = 1e-4;
-template <bool kLdsLogn>
-__global__ __launch_bounds__(kWave) void k_sm_scan(SmArgs a) {
-  extern __shared__ double scan_lds[];
-  const int lane = threadIdx.x;
-  int n1 = a.n1, n2 = a.n2;
-  const int tot = n1 + n2;
-  const double* logn = a.logn;
-  if constexpr (kLdsLogn) {
-    for (int t = lane; t <= tot; t += kWave) scan_lds[t] = a.logn[t];
-    __syncthreads();
-    logn = scan_lds;
+
+// Certified count bands of every point of S, in parallel before the walk.  For point q with
+// current side s (s0 = [s == 0], s1 = [s == 1]) the scan's D at size n1 of c1 is
+//   D(n1) = (log(n1 - s0) + l0) - (log(tot - n1 - s1) + l1) = log(a / (L - a)) + l0 - l1
+// (a = n1 - s0, L = tot - s0 - s1) up to rounding (< 1e-9), increasing in n1.  For each
+// threshold D_t in {0, lam, -lam} the real n1 where D crosses D_t -/+ margin is
+// s0 + L sigmoid(D_t -/+ margin - (l0 - l1)); every integer n1 below the band
+// [floor(x-) - 1, ceil(x+) + 1] has D < D_t - margin + 1e-9, every one above it D > D_t +
+// margin - 1e-9.  The walk then certifies a lane by integer compares against 3 bands.
+__global__ __launch_bounds__(kBlock) void k_sm_cert(SmArgs a) {
+  const int q = blockIdx.x * kBlock + threadIdx.x;
+  if (q >= a.nS) return;
+  const int cur = a.side[q];
+  const double dl = a.ll[q] - a.ll[a.nS + q];
+  const double rU = raw_to_unif(a.raw[q]);
+  const int tot = a.n1 + a.n2;
+  const int s0 = cur == 0, s1 = cur == 1;
+  const double L = (double)(tot - s0 - s1);
+  const double lam = log(rU / (1.0 - rU));
+  const double th[3] = {0.0, lam, -lam};
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const double zm = (th[t] - kSmScanMargin) - dl, zp = (th[t] + kSmScanMargin) - dl;
+    const double xm = (double)s0 + L / (1.0 + exp(-zm)), xp = (double)s0 + L / (1.0 + exp(-zp));
+    a.cert[(2 * t) * a.nS + q] = (int)floor(xm) - 1;
+    a.cert[(2 * t + 1) * a.nS + q] = (int)ceil(xp) + 1;
   }
-  const double margin = kSmScanMargin;
-  int nx_cur = 0;
-  double nx_l0 = 0.0, nx_l1 = 0.0;
-  uint32_t nx_raw = 0;
-  if (lane < a.nS) { nx_cur = a.side[lane]; nx_l0 = a.ll[lane]; nx_l1 = a.ll[a.nS + lane]; nx_raw = a.raw[lane]; }
-  for (int base = 0; base < a.nS; base += kWave) {
-    const int q = base + lane;
-    const bool act = q < a.nS;
-    int cur = nx_cur;
-    const double l0 = nx_l0, l1 = nx_l1;
-    const double rU = act ? raw_to_unif(nx_raw) : 0.0;
-    const int qn = q + kWave;
-    if (qn < a.nS) { nx_cur = a.side[qn]; nx_l0 = a.ll[qn]; nx_l1 = a.ll[a.nS + qn]; nx_raw = a.raw[qn]; }
-    bool certain = false;
-    int choice = cur;
-    if (act) {
-      // n1 as lane `lane` may see it, within the sizes the clusters can take
-      const int lo = max(n1 - lane, 1 + (cur == 0)), hi = min(n1 + lane, tot - 1 - (cur == 1));
-      const double dlo = (logn[lo - (cur == 0)] + l0) - (logn[tot - lo - (cur == 1)] + l1);
-      const double dhi = (logn[hi - (cur == 0)] + l0) - (logn[tot - hi - (cur == 1)] + l1);
-      const double lam = log(rU / (1.0 - rU));
-      const double a0 = fmin(dlo, dhi) - margin, a1 = fmax(dlo, dhi) + margin;
-      certain = !(a0 <= 0.0 && 0.0 <= a1) && !(a0 <= lam && lam <= a1) && !(a0 <= -lam && -lam <= a1);
-      if (certain) choice = ((dlo > 0.0 && dlo >= lam) || (dlo <= 0.0 && dlo > -lam)) ? 0 : 1;
+}
+
+// The walk: wave 0 goes through S in batches of 64 in order; waves 1..15 stage the next chunk
+// of S's inputs (sides, certified bands, log-likelihoods, raw draws) into an LDS double
+// buffer meanwhile.  Within a batch the size n1 of c1 seen by lane p lies in [n1 - p,
+// n1 + p] (n1 + n2 is fixed: points only change sides); in exact arithmetic the pick is
+// "0 iff (D > 0 and D >= lam) or (D <= 0 and D > -lam)" with lam = log(rU / (1 - rU)), so it
+// only changes where D crosses 0 (the revsort order), lam or -lam.  A lane whose count range
+// misses all three bands keeps D 1e-4 away from every threshold (there p0 is >= 2e-15 from
+// its threshold, far beyond the few-ulp rounding of the exp and divisions): it has one pick
+// for every count it can see and is settled by compares; the others are drawn exactly, all
+// at once, by the fixed-point iteration below.
+//
+// The margin.  Near a threshold D0 (0, lam or -lam) the computed p0 = 1 / (1 + exp(-D)) (or
+// its complement) moves by |p0'| |D - D0| >= p (1 - p) |D - D0|, and p (1 - p) >= 2e-11 for the
+// thresholds a uniform in (2.3e-10, 1 - 2.3e-10) can set, so a D kept 1e-4 from the
+// threshold keeps p0 at least ~2e-15 away from the value that would flip the pick.  The
+// computed D carries the error of two logn entries and two log-likelihood sums (a few ulp of
+// their magnitudes, < 1e-9 for any |S| and D the engine accepts), and exp / the two
+// divisions add a few ulp of p0 (< 1e-15): both far inside the margin.
+constexpr int kSmScanThreads = 1024;          // wave 0 walks, 15 waves stage (one load round per chunk)
+constexpr int kSmChunk = 1024;              // points per staged chunk
+struct SmChunk {
+  double l0[kSmChunk], l1[kSmChunk];
+  uint32_t raw[kSmChunk];
+  int side[kSmChunk];
+  int band[6][kSmChunk];
+};
+__global__ __launch_bounds__(kSmScanThreads) void k_sm_scan(SmArgs a) {
+  extern __shared__ unsigned char sm_scan_lds[];
+  SmChunk* buf = (SmChunk*)sm_scan_lds;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  int n1 = a.n1;
+  const int tot = a.n1 + a.n2;
+  const int nch = (a.nS + kSmChunk - 1) / kSmChunk;
+  auto stage = [&](int c, int t0, int nt) {
+    SmChunk& B = buf[c & 1];
+    const int q0 = c * kSmChunk, nq = min(kSmChunk, a.nS - q0);
+    for (int e = t0; e < nq; e += nt) {
+      B.l0[e] = a.ll[q0 + e];
+      B.l1[e] = a.ll[a.nS + q0 + e];
+      B.raw[e] = a.raw[q0 + e];
+      B.side[e] = a.side[q0 + e];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) B.band[k][e] = a.cert[k * a.nS + q0 + e];
     }
-    unsigned long long unc = __ballot(act && !certain);
-    const unsigned long long mv01 = __ballot(act && certain && cur == 0 && choice == 1);
-    const unsigned long long mv10 = __ballot(act && certain && cur == 1 && choice == 0);
-    // walk uncertain lanes in order; counts at lane u = batch start + moves of lanes < u
-    int d1 = 0, d2 = 0;   // count deltas from uncertain lanes processed so far
-    while (unc) {
-      const int u = __ffsll((long long)unc) - 1;
-      const unsigned long long below = (u == 0) ? 0ull : ((1ull << u) - 1ull);
-      const int c01 = __popcll(mv01 & below), c10 = __popcll(mv10 & below);
-      const int cn1 = n1 + d1 - c01 + c10, cn2 = n2 + d2 + c01 - c10;
-      int pick = 0;
-      if (lane == u) {
-        const int nz1 = cn1 - (cur == 0), nz2 = cn2 - (cur == 1);
-        const double v0 = logn[nz1] + l0, v1 = logn[nz2] + l1;
-        pick = two_way_draw(v0, v1, rU);
-        choice = pick;
+  };
+  if (nch > 0) stage(0, tid, kSmScanThreads);
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    if (wv > 0) {
+      if (c + 1 < nch) stage(c + 1, tid - kWave, kSmScanThreads - kWave);
+    } else {
+      const SmChunk& B = buf[c & 1];
+      const int q0 = c * kSmChunk, nq = min(kSmChunk, a.nS - q0);
+      for (int base = 0; base < nq; base += kWave) {
+        const int e = base + lane;
+        const bool act = e < nq;
+        const int cur = act ? B.side[e] : 0;
+        bool certain = false;
+        int choice = cur;
+        if (act) {
+          // n1 as lane `lane` may see it, within the sizes the clusters can take
+          const int lo = max(n1 - lane, 1 + (cur == 0)), hi = min(n1 + lane, tot - 1 - (cur == 1));
+          bool above[3];
+          certain = true;
+#pragma unroll
+          for (int t = 0; t < 3; ++t) {
+            const int blo = B.band[2 * t][e], bhi = B.band[2 * t + 1][e];
+            certain = certain && (hi < blo || lo > bhi);
+            above[t] = lo > bhi;
+          }
+          if (certain) choice = ((above[0] && above[1]) || (!above[0] && above[2])) ? 0 : 1;
+        }
+        // The uncertain lanes are drawn together by a fixed-point iteration: every lane's
+        // count is the batch start plus the moves of the lanes before it (an exclusive prefix
+        // sum of the current choices); each uncertain lane draws exactly at that count, and
+        // the sweep repeats until no choice changes.  Lane k's count only depends on lanes
+        // < k, so after round r the first r uncertain lanes hold their true draws: the fixed
+        // point is the reference's sequential walk (reached in <= 64 rounds, usually 1-3).
+        // Counts a lane sees before the fixed point are clamped to the sizes the clusters can
+        // take.
+        const bool unc = act && !certain;
+        if (__ballot(unc)) {
+          const double l0 = unc ? B.l0[e] : 0.0, l1 = unc ? B.l1[e] : 0.0;
+          const double rU = unc ? raw_to_unif(B.raw[e]) : 0.5;
+          int gprev = -1;
+          for (;;) {
+            const int dl = act ? ((choice == 0) - (cur == 0)) : 0;   // this lane's move of n1
+            int inc = dl;
+#pragma unroll
+            for (int o = 1; o < kWave; o <<= 1) {
+              const int t = __shfl_up(inc, o);
+              if (lane >= o) inc += t;
+            }
+            bool changed = false;
+            if (unc) {
+              const int g = min(max(n1 + inc - dl, 1 + (cur == 0)), tot - 1 - (cur == 1));
+              if (g != gprev) {
+                gprev = g;
+                const int nz1 = g - (cur == 0), nz2 = tot - g - (cur == 1);
+                const int pk = two_way_draw(dlog((double)nz1) + l0, dlog((double)nz2) + l1, rU);
+                changed = pk != choice;
+                choice = pk;
+              }
+            }
+            if (!__ballot(changed)) break;
+          }
+        }
+        int dl = act ? ((choice == 0) - (cur == 0)) : 0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) dl += __shfl_xor(dl, o);
+        n1 += dl;
+        if (act) a.side[q0 + e] = choice;
       }
-      pick = __shfl(pick, u);
-      const int cu = __shfl(cur, u);
-      if (cu == 0 && pick == 1) { d1--; d2++; }
-      if (cu == 1 && pick == 0) { d1++; d2--; }
-      unc &= ~(1ull << u);
     }
-    n1 += d1 - __popcll(mv01) + __popcll(mv10);
-    n2 += d2 + __popcll(mv01) - __popcll(mv10);
-    if (act) a.side[q] = choice;
+    __syncthreads();
   }
-  if (lane == 0) { a.out_counts[0] = n1; a.out_counts[1] = n2; }
+  if (tid == 0) { a.out_counts[0] = n1; a.out_counts[1] = tot - n1; }
 }
 
 // logprobgs_c_i terms: log(probs[current side]) with fixed launch sizes; compensated
@@ -2805,11 +2886,8 @@ hipError_t launch_sm_ll(const SmArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 hipError_t launch_sm_scan(const SmArgs& a, hipStream_t s) {
-  const size_t lds = (size_t)(a.n1 + a.n2 + 1) * 8;
-  if (lds <= 160 * 1024)
-    hipLaunchKernelGGL(k_sm_scan<true>, dim3(1), dim3(kWave), lds, s, a);
-  else
-    hipLaunchKernelGGL(k_sm_scan<false>, dim3(1), dim3(kWave), 0, s, a);
+  if (a.nS > 0) hipLaunchKernelGGL(k_sm_cert, dim3((a.nS + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
+  hipLaunchKernelGGL(k_sm_scan, dim3(1), dim3(kSmScanThreads), 2 * sizeof(SmChunk), s, a);
   return hipGetLastError();
 }
 

@@ -254,6 +254,7 @@ struct SmArgs {
   int n1, n2;                // current (scan) or launch (logprobgs) cluster sizes
   int* out_counts;           // [2] final sizes after the scan
   double* out;               // logprobgs partial (hi, lo) per block
+  int* cert;                 // scan: per S position, [3][2] certified count bands (k_sm_cert)
 };
 
 }  // namespace hdpm

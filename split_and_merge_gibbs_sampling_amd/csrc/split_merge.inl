@@ -243,6 +243,7 @@ static SmArgs sm_args(Ctx* c, SmWork& W, int nS) {
   a.two = ParamTables{W.d_two_codes.p, W.d_two_tab.p};
   a.ll = W.d_ll.p; a.side = W.d_side.p; a.side_ref = W.d_side_ref.p; a.raw = W.d_raw.p;
   a.logn = c->d_logn.p; a.n1 = 0; a.n2 = 0; a.out_counts = W.d_counts2.p; a.out = W.d_out.p;
+  a.cert = W.d_cert.p;
   return a;
 }
 
@@ -253,6 +254,7 @@ static void sm_upload_S(Ctx* c, SmWork& W, const std::vector<int>& S) {
   W.d_side_ref.ensure(std::max<size_t>(nS, 1));
   W.d_ll.ensure(std::max<size_t>(2 * nS, 2));
   W.d_raw.ensure(std::max<size_t>(nS, 1));
+  W.d_cert.ensure(std::max<size_t>(6 * nS, 6));
   W.d_counts2.ensure(2);
   W.d_out.ensure(std::max<size_t>(2 * ((nS + kBlock - 1) / kBlock), 2));
   if (nS) HIPCHK(hipMemcpyAsync(W.d_S.p, S.data(), nS * 4, hipMemcpyHostToDevice, c->stream));
