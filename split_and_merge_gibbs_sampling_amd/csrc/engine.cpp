@@ -462,6 +462,7 @@ struct SmWork {
   PinBuf<uint32_t> h_raw;
   PinBuf<uint8_t> h_two_codes;
   PinBuf<double> h_two_tab;
+  int64_t phi_prefetch = 0;   // stream slice generated ahead for the move's update_phi jobs
 };
 
 // A window of the R random stream generated on the device (k_mt_gen), starting at the
@@ -2068,6 +2069,8 @@ struct Ctx {
     std::atomic<int> nextC{0}, gsl{-1};
     int berr = 0, b_end = 0;
     bool failed = false;
+    const double* sig_in = nullptr;    // current sigmas (phase A), indexed like Sig
+    bool stage = true;                 // phase C stages the label tables into L
     // diagnostics (debug bit 5): ns after launch
     std::chrono::steady_clock::time_point t_launch;
     std::atomic<int64_t> ns_fill{0}, ns_logits{0}, ns_b0{0}, ns_b1{0}, ns_f0{0}, ns_f1{0}, ns_f2{0};
@@ -2089,7 +2092,7 @@ struct Ctx {
     for (int j = j0; j < j1; ++j) {
       const int mj = att[j];
       const unsigned* fj = &pj.freq[((size_t)k * d + j) * mmax];
-      const double sg = h_sigma[(size_t)k * d + j];
+      const double sg = pj.sig_in[(size_t)k * d + j];
       double prob[256];
       for (int l = 0; l < mj; ++l) prob[l] = (-((double)nn - (double)fj[l])) / sg;
       double mx = prob[0];
@@ -2248,7 +2251,8 @@ struct Ctx {
       }
       pj.Sig[(size_t)k * d + j] = -1 / std::log(out);
     }
-    if (ok) stage_entry_from(pj.L, pj.full ? k : t, k, &pj.Cen[(size_t)k * d], &pj.Sig[(size_t)k * d], pj.counts[k]);
+    if (ok && pj.stage)
+      stage_entry_from(pj.L, pj.full ? k : t, k, &pj.Cen[(size_t)k * d], &pj.Sig[(size_t)k * d], pj.counts[k]);
     return ok;
   }
 
@@ -2267,6 +2271,8 @@ struct Ctx {
     pj.full = full;
     pj.offs = offs;
     pj.spec = spec;
+    pj.sig_in = h_sigma.data();
+    pj.stage = true;
     pj.fill_count = phi_prefetch;
     phi_off.resize(d + 1);
     phi_off[0] = 0;

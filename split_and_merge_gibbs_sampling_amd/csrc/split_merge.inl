@@ -212,6 +212,80 @@ static int hupdate_phi_one(Ctx* c, HState& s, int k, const Freq& F) {
   return c->sample_sigma_wide(nv.data(), nw.data(), sig);
 }
 
+// update_phi (cf:511-591) of clusters ks[0..nk) (ascending labels: the order of the
+// reference's cluster mask) for wide rows, through the engine's update_phi pipeline
+// (Ctx::pj_*, the Neal-8 path's): the stream slice is generated ahead with its logits on the
+// host pool, phase A (center probabilities, revsort, rhig branch and rbeta constants of the
+// likely center) runs per attribute on the pool, phase B draws in reference order with
+// speculative first rbeta attempts, phase C solves the bisections.  Same expressions and
+// draws as hupdate_phi_one; one pool job per call instead of two pool passes and serial
+// log / exp per rbeta attempt.
+static int hupdate_phi_job(Ctx* c, HState& s, const int* ks, const Freq* const* Fs, int nk) {
+  SmTimer tm(c->stats.t_sm_phi_ms);
+  const int d = c->d, mm = c->mmax;
+  std::vector<unsigned> fq((size_t)nk * d * mm);
+  std::vector<int> cnt(nk);
+  std::vector<uint8_t> cen((size_t)nk * d);
+  std::vector<double> sig((size_t)nk * d);
+  std::vector<int> touched;
+  for (int t = 0; t < nk; ++t) {
+    const Freq& F = *Fs[t];
+    cnt[t] = F.nn;
+    for (size_t e = 0; e < (size_t)d * mm; ++e) fq[(size_t)t * d * mm + e] = (unsigned)F.f[e];
+    std::memcpy(&cen[(size_t)t * d], &s.center[(size_t)ks[t] * d], d);
+    std::memcpy(&sig[(size_t)t * d], &s.sigma[(size_t)ks[t] * d], (size_t)d * 8);
+    if (F.nn > 0) touched.push_back(t);
+  }
+  if (touched.empty()) return kOk;
+  SmWork& W = smwork(c);
+  c->rng_sync();
+  StreamAhead& sa = c->phi_stream;
+  if (W.phi_prefetch <= 0) W.phi_prefetch = (int64_t)4 * nk * d + 1024;
+  if (!sa.fill(c->rng, W.phi_prefetch)) {
+    // an unseeded stream: the one-pass path
+    for (int t = 0; t < nk; ++t) {
+      const int st = hupdate_phi_one(c, s, ks[t], *Fs[t]);
+      if (st) return st;
+    }
+    return kOk;
+  }
+  sa.used = 0;
+  HostPool::get().run(sa.n, 1024, [&](int64_t a0, int64_t a1) { sa.logits(a0, a1); });
+  sa.avail = INT64_MAX;
+  sa.wait_avail = nullptr;
+  sa.live = &c->rng;
+  c->pj_setup(touched, 0, cnt.data(), fq.data(), cen.data(), sig.data(), UploadLayout{}, false, nullptr, false);
+  c->pj.sig_in = sig.data();
+  c->pj.stage = false;
+  c->pj_launch();
+  const int berr = c->pj_finish();
+  const int gsl_t = c->pj.gsl.load();
+  sa.finish();
+  W.phi_prefetch = std::max<int64_t>((int64_t)nk * d + 1024, sa.used + sa.used / 4 + 512);
+  sa.n = 0;
+  if (berr) return berr;
+  if (gsl_t >= 0) return kGsl;
+  for (int t : touched) {
+    std::memcpy(&s.center[(size_t)ks[t] * d], &cen[(size_t)t * d], d);
+    std::memcpy(&s.sigma[(size_t)ks[t] * d], &sig[(size_t)t * d], (size_t)d * 8);
+  }
+  return kOk;
+}
+
+// update_phi of {ka, kb} in the reference's order (ascending label; a repeated label once)
+static int hupdate_phi_pair(Ctx* c, HState& s, int ka, const Freq& Fa, int kb, const Freq& Fb) {
+  if (c->d < 128 || (c->debug & 128)) {
+    int st = ka <= kb ? hupdate_phi_one(c, s, ka, Fa) : hupdate_phi_one(c, s, kb, Fb);
+    if (st) return st;
+    if (ka != kb) st = ka < kb ? hupdate_phi_one(c, s, kb, Fb) : hupdate_phi_one(c, s, ka, Fa);
+    return st;
+  }
+  if (ka == kb) return hupdate_phi_job(c, s, &ka, std::array<const Freq*, 1>{&Fa}.data(), 1);
+  const int ks[2] = {std::min(ka, kb), std::max(ka, kb)};
+  const Freq* fs[2] = {ka < kb ? &Fa : &Fb, ka < kb ? &Fb : &Fa};
+  return hupdate_phi_job(c, s, ks, fs, 2);
+}
+
 static void hrecount(const Ctx* c, HState& s) {
   s.counts.assign(s.K, 0);
   for (int i = 0; i < c->n; ++i)
@@ -327,9 +401,7 @@ static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1
     s.counts[c2] = F2.nn;
     // sm:221 update_phi({c1, c2}): the mask visits clusters in ascending index order, a
     // repeated index once (c1 == c2 only through the restricted-Gibbs C ABI)
-    int st = c1 <= c2 ? hupdate_phi_one(c, s, c1, F1) : hupdate_phi_one(c, s, c2, F2);
-    if (st) return st;
-    if (c1 != c2) st = c1 < c2 ? hupdate_phi_one(c, s, c2, F2) : hupdate_phi_one(c, s, c1, F1);
+    const int st = hupdate_phi_pair(c, s, c1, F1, c2, F2);
     if (st) return st;
   }
   return kOk;
@@ -574,7 +646,7 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
   e = clean_var(this, ml, ml);
   if (e) { err = "State validation failed: clean_var"; return e; }
   for (int iter = 0; iter < r; ++iter) {
-    e = hupdate_phi_one(this, ml, ml.c[i2], FM);
+    e = hupdate_phi_pair(this, ml, ml.c[i2], FM, ml.c[i2], FM);
     if (e) { err = "update_phi failed"; return e; }
   }
   e = hvalidate(ml);
@@ -608,7 +680,7 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
     acpt = min0(log_prior + log_likelihood + log_proposal);
   } else {
     ss = ml;
-    e = hupdate_phi_one(this, ss, ss.c[i2], FM);
+    e = hupdate_phi_pair(this, ss, ss.c[i2], FM, ss.c[i2], FM);
     if (e) { err = "update_phi failed"; return e; }
     // sm:489-540 (ss's merged cluster is M; st's two clusters split M)
     SmTimer tm(stats.t_sm_terms_ms);

@@ -219,6 +219,39 @@ def test_restricted_gibbs_large_clusters(hd, oracle):
     eng.close()
 
 
+# d >= 128: the scans' update_phi goes through the engine's pipelined update_phi job
+# (split_merge.inl hupdate_phi_job); debug 128 keeps the one-pass path
+@pytest.mark.parametrize("debug", [0, 128])
+def test_restricted_gibbs_wide_update_phi(hd, oracle, debug):
+    ds = synth(3000, 200, 4, 6, seed=39)
+    cen, sig = random_params(ds, 4, 12)
+    c = ds.truth.astype(np.int32).copy()
+    i1 = int(np.where(c == 2)[0][0])
+    i2 = int(np.where(c == 1)[0][0])              # c1 > c2: update_phi in ascending label order
+    S = [i for i in range(ds.n) if i not in (i1, i2) and c[i] in (c[i1], c[i2])]
+    st = oracle.seed_state(44)
+    eng = make_engine(hd, ds)
+    eng.set_debug(debug)
+    eng.set_state(c, cen, sig)
+    eng.rng_state = st
+    eng.restricted_gibbs(S, i1, i2, t=4)
+    ost = oracle_state(oracle, c, cen, sig)
+    assert oracle.restricted_gibbs(ds.codes, ds.attrisize, ds.v, ds.w, S, ost, i1, i2, 4, st) == 0
+    assert_same_state(eng, ost)
+    assert np.array_equal(eng.rng_state, st)
+    eng.close()
+
+
+def test_run_markov_chain_wide_split_merge_matches_oracle(hd, oracle):
+    ds = synth(1200, 160, 4, 5, seed=40)
+    kw = dict(m=3, iterations=8, L=4, burnin=2, t=3, r=3, neal8=True, split_merge=True)
+    st, ref = oracle.run_markov_chain(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w, seed=17, fast=1, **kw)
+    assert st == 0
+    res = hd.run_markov_chain(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w, seed=17, **kw)
+    assert np.array_equal(res["c_i"], ref["c_i"])
+    assert np.array_equal(res["total_cls"], ref["total_cls"])
+
+
 def test_logprobgs_c_i_matches_oracle(hd, oracle, zoo):
     cen, sig = random_params(zoo, 7, 12)
     c = zoo.truth.astype(np.int32).copy()
