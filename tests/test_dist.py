@@ -111,8 +111,13 @@ def test_bench_helpers():
     wb, W, bw = bench.packed_layout(128, 4)
     assert (wb, W, bw) == (2, 4, 16)
     assert bench.prepass_bytes_per_point(128, 4, 3) == 8 * W + 16 + 4 + 3 * 64 + 12     # 64-B heads
-    wb, W, bw = bench.packed_layout(784, 6)                                          # generic: full records
-    assert bench.prepass_bytes_per_point(784, 6, 3) == 8 * W + 16 + 4 + 3 * 8 * bw + 12
+    wb, W, bw = bench.packed_layout(784, 6)                                          # wide: 448-B heads
+    assert (wb, W) == (4, 52)
+    assert bench.head_layout(784, 6) == (True, 56, False)
+    assert bench.prepass_bytes_per_point(784, 6, 3) == 8 * W + 16 + 4 + 3 * 448 + 12
+    wb, W, bw = bench.packed_layout(2100, 2)                                         # Ws = 33: generic, full records
+    assert bench.head_layout(2100, 2)[0] is False
+    assert bench.prepass_bytes_per_point(2100, 2, 3) == 8 * W + 16 + 4 + 3 * 8 * bw + 12
     assert bench.survey_sweep_bytes(10, 4, 1) == 10 * (4 * 11 + 8)
 
 
