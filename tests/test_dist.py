@@ -147,4 +147,5 @@ def test_traffic_from_csv(tmp_path, rows):
     assert bench.traffic_from_csv(str(pf), str(pw)) == (200 * 1024, 20 * 1024)
     # the C5 prepass shape: 52 B/point streamed, 3 x 64-B head gathers
     assert bench.prepass_shape(128, 4, 3) == (52, 192, "gather64")
-    assert bench.prepass_shape(784, 6, 3)[2] == "gather128"
+    assert bench.prepass_shape(784, 6, 3) == (436, 3 * 448, "gather448g")
+    assert bench.prepass_shape(2100, 2, 3)[2] == "gather128"
