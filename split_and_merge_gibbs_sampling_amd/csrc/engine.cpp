@@ -1699,14 +1699,22 @@ struct Ctx {
     ahead.launched = false;
     ahead.active = true;
     // the speculative update_phi first: its serial draws, not the device sweep, are the
-    // longer path (timeline: launching the sweep first cost ~8% of the iteration rate)
-    spec_launch();
-    mark("ahead.spec");
+    // longer path (timeline: launching the sweep first cost ~8% of the iteration rate);
+    // debug bit 15 launches the sweep first
+    const bool sweep_first = (debug & 32768) != 0;
+    if (!sweep_first) {
+      spec_launch();
+      mark("ahead.spec");
+    }
     if (launch && resolve_smem_bytes(std::min(scap, K + 2), m, K + m <= 64 ? 1 : 0) <= 160 * 1024) {
       ahead.track = freq_dev_valid;
       sweep_buffers(ahead.track);
       mark("ahead.buf");
       if (launch_round(0, K, m, ahead.raw, ahead.track) == kOk) ahead.launched = true;
+    }
+    if (sweep_first) {
+      spec_launch();
+      mark("ahead.spec");
     }
   }
   void cancel_ahead() {

@@ -2797,17 +2797,15 @@ __global__ __launch_bounds__(kSmScanThreads) void k_sm_scan(SmArgs a) {
           const double l0 = unc ? B.l0[e] : 0.0, l1 = unc ? B.l1[e] : 0.0;
           const double rU = unc ? raw_to_unif(B.raw[e]) : 0.5;
           int gprev = -1;
+          const unsigned long long below = (1ull << lane) - 1ull;
           for (;;) {
-            const int dl = act ? ((choice == 0) - (cur == 0)) : 0;   // this lane's move of n1
-            int inc = dl;
-#pragma unroll
-            for (int o = 1; o < kWave; o <<= 1) {
-              const int t = __shfl_up(inc, o);
-              if (lane >= o) inc += t;
-            }
+            // exclusive prefix of the lanes' moves of n1 (+1: to c1, -1: to c2) by ballots
+            const unsigned long long up = __ballot(act && choice == 0 && cur == 1);
+            const unsigned long long dn = __ballot(act && choice == 1 && cur == 0);
+            const int pre = __popcll(up & below) - __popcll(dn & below);
             bool changed = false;
             if (unc) {
-              const int g = min(max(n1 + inc - dl, 1 + (cur == 0)), tot - 1 - (cur == 1));
+              const int g = min(max(n1 + pre, 1 + (cur == 0)), tot - 1 - (cur == 1));
               if (g != gprev) {
                 gprev = g;
                 const int nz1 = g - (cur == 0), nz2 = tot - g - (cur == 1);
@@ -2819,10 +2817,7 @@ __global__ __launch_bounds__(kSmScanThreads) void k_sm_scan(SmArgs a) {
             if (!__ballot(changed)) break;
           }
         }
-        int dl = act ? ((choice == 0) - (cur == 0)) : 0;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) dl += __shfl_xor(dl, o);
-        n1 += dl;
+        n1 += __popcll(__ballot(act && choice == 0 && cur == 1)) - __popcll(__ballot(act && choice == 1 && cur == 0));
         if (act) a.side[q0 + e] = choice;
       }
     }
