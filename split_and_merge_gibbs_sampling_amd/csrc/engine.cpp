@@ -1543,6 +1543,7 @@ struct Ctx {
   }
 
   // ------------------------------------------------------------------ Neal-8 sweep
+  bool mcount_clear = false;
   // Buffers of a sweep (sized for n).
   void sweep_buffers(bool track) {
     const int nb_max = (n + kBlock - 1) / kBlock;
@@ -1558,7 +1559,7 @@ struct Ctx {
     if (track) {
       d_mlog.ensure((size_t)3 * n);
       d_mcount.ensure(1);
-      HIPCHK(hipMemsetAsync(d_mcount.p, 0, 4, stream));
+      mcount_clear = true;            // by the next launch's k_cluster_summary
     }
   }
 
@@ -1603,6 +1604,12 @@ struct Ctx {
     pa.p0 = p;
     pa.exact_wave = (debug & 2048) ? 1 : 0;
     pa.wide = (debug & 16384) ? 0 : 1;
+    pa.zero = nullptr;
+    if (mcount_clear) {
+      if (K > 0) pa.zero = d_mcount.p;
+      else HIPCHK(hipMemsetAsync(d_mcount.p, 0, 4, stream));
+      mcount_clear = false;
+    }
     const int nblocks = (n - p + kBlock - 1) / kBlock;
     HIPCHK(launch_cluster_summary(pa, stream));
     if (round_timed) HIPCHK(hipEventRecord(ev[0], stream));

@@ -255,6 +255,7 @@ __device__ __forceinline__ int penalty_r(const uint64_t (&M)[WS], const uint64_t
 // per label instead of the label -> slot -> record / count -> logn chain):
 // csum[l] = [record of slot_of_label[l] (bw words), logn[count], slot].
 __global__ void k_cluster_summary(PrepassArgs a) {
+  if (a.zero && blockIdx.x == 0 && threadIdx.x == 0) *a.zero = 0;   // a memset dispatch less per sweep
   const int sw = a.bw + 2;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < a.K * sw; e += gridDim.x * blockDim.x) {
     const int l = e / sw, w = e - l * sw;

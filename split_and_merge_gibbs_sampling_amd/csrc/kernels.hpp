@@ -125,6 +125,7 @@ struct PrepassArgs {
   int p0;
   int exact_wave;            // 1: exact rows one wave per point (no workgroup staging)
   int wide;                  // 1: wide layouts take k_prepass_wide (0: the generic kernel)
+  int* zero;                 // k_cluster_summary clears this word first (the sweep's move count), or nullptr
 };
 
 // The resolver runs in block mode (csrc/kernels.hip, k_resolve_blk) when in the previous
