@@ -2870,12 +2870,19 @@ int hdpm_ctx_create(int32_t device, hdpm_ctx** out) {
   auto* c = new (std::nothrow) Ctx();
   if (!c) return HDPM_E_ARG;
   c->device = device;
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  // the sweep's stream at the highest priority, the generator windows' side stream at the
+  // lowest: a window's generation (~1 ms per 16 sweeps of draws) then takes the CUs the
+  // sweep leaves (HDPM_STREAM_PRIO=0: default priorities)
+  int prio_lo = 0, prio_hi = 0;
+  const char* sp = std::getenv("HDPM_STREAM_PRIO");
+  if (!(sp && sp[0] == '0') && hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi) != hipSuccess) {
     delete c;
     return HDPM_E_DEVICE;
   }
   for (auto& e : c->ev) (void)hipEventCreate(&e);
-  if (hipStreamCreateWithFlags(&c->gstream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithPriority(&c->gstream, hipStreamNonBlocking, prio_lo) != hipSuccess) {
     delete c;
     return HDPM_E_DEVICE;
   }
@@ -3065,13 +3072,17 @@ int hdpm_get_stats(const hdpm_ctx* h, hdpm_stats* out) {
   *out = ctx->stats;
   return HDPM_OK;
 }
+// Counters and synchronisation leave a prepared sweep in place (they change no chain
+// state), so a caller that runs hdpm_iterations in batches keeps the pipeline warm across
+// them; changing the debug mode drops it (the prepared work followed the old mode).
 int hdpm_reset_stats(hdpm_ctx* h) {
-  CTX();
+  CTX_KEEP();
   ctx->stats = hdpm_stats{};
   return HDPM_OK;
 }
 int hdpm_set_debug(hdpm_ctx* h, int32_t mode) {
-  CTX();
+  CTX_KEEP();
+  if (mode != ctx->debug) GUARD(ctx->cancel_ahead();)
   ctx->debug = mode;
   return HDPM_OK;
 }
@@ -3196,7 +3207,7 @@ int hdpm_debug_math(hdpm_ctx* h, const double* x, int64_t n, int32_t fn, int32_t
   })
 }
 int hdpm_synchronize(hdpm_ctx* h) {
-  CTX();
+  CTX_KEEP();
   return hipStreamSynchronize(ctx->stream) == hipSuccess ? HDPM_OK : HDPM_E_DEVICE;
 }
 
