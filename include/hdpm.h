@@ -161,7 +161,9 @@ int hdpm_reset_stats(hdpm_ctx* ctx);
  * block mode in the resolver (uncertain points decided one by one); bit 13: block mode for
  * every resolver launch (not only after a launch that listed kResolveBlkMin points); bit 14:
  * wide layouts take the generic prepass (one thread per point) instead of k_prepass_wide; bit 15:
- * the prepared next sweep is launched before the speculative update_phi is started. */
+ * the prepared next sweep is launched before the speculative update_phi is started; bit 16:
+ * restricted scans of >= 4096 points draw their uniforms on the host (not from the device
+ * generator windows). */
 int hdpm_set_debug(hdpm_ctx* ctx, int32_t mode);
 /* The prepass's pool-entry heads, P entries of wb*Ws + 2 words padded to a power of two
  * (Ws <= 4) or to a multiple of 8 words (wide layouts) (csrc/kernels.hpp "Pool-entry heads",

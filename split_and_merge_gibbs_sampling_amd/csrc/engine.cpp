@@ -2021,6 +2021,24 @@ struct Ctx {
     return sa.fill(rng, N);
   }
 
+  // A slice of N uniforms for the split-merge update_phi jobs: the device window's words
+  // when the last device_draws prefetched at least N of them from this position (the
+  // scan's draws came from a window), else generated on the host.
+  bool fill_stream_from(int64_t N) {
+    StreamAhead& sa = phi_stream;
+    bool dev = phidev.valid && phidev.pos == rng.pos && phidev.epoch == rng.epoch && phidev.mti == rng.mti &&
+               phidev.N >= N;
+    if (dev) {
+      HIPCHK(hipEventSynchronize(phidev.ev));
+      for (int i = 0; i < 624 && dev; ++i) dev = mt_untemper(phidev.raw.p[i]) == rng.mt[i];
+    }
+    if (dev) {
+      sa.fill_raw(rng, phidev.raw.p, N);
+      return true;
+    }
+    return sa.fill(rng, N);
+  }
+
   // update_phi's slice of the host stream, generated ahead (also called while the device
   // runs a sweep, which draws only from the device windows).
   void prefill_phi_stream() {

@@ -241,7 +241,7 @@ static int hupdate_phi_job(Ctx* c, HState& s, const int* ks, const Freq* const* 
   c->rng_sync();
   StreamAhead& sa = c->phi_stream;
   if (W.phi_prefetch <= 0) W.phi_prefetch = (int64_t)4 * nk * d + 1024;
-  if (!sa.fill(c->rng, W.phi_prefetch)) {
+  if (!c->fill_stream_from(W.phi_prefetch)) {
     // an unseeded stream: the one-pass path
     for (int t = 0; t < nk; ++t) {
       const int st = hupdate_phi_one(c, s, ks[t], *Fs[t]);
@@ -302,8 +302,22 @@ static void sm_upload_two(Ctx* c, SmWork& W, const HState& s, int k1, int k2) {
   uint8_t* cc = W.h_two_codes.p;
   double* tt = W.h_two_tab.p;
   std::memset(cc, 0, nc);
-  c->tables_for(&s.center[(size_t)k1 * c->d], &s.sigma[(size_t)k1 * c->d], cc, tt);
-  c->tables_for(&s.center[(size_t)k2 * c->d], &s.sigma[(size_t)k2 * c->d], cc + c->dp, tt + 2 * c->d);
+  if (c->d >= 128) {
+    // wide rows: the two clusters' dhamming pairs (an exp and a log each) on the host pool
+    const int d = c->d;
+    const uint8_t* c1 = &s.center[(size_t)k1 * d];
+    const uint8_t* c2 = &s.center[(size_t)k2 * d];
+    const double* s1 = &s.sigma[(size_t)k1 * d];
+    const double* s2 = &s.sigma[(size_t)k2 * d];
+    pool_for(2 * d, [&](int q) {
+      const int e = q / d, j = q - e * d;
+      cc[e * c->dp + j] = (e ? c2 : c1)[j];
+      dhamming_pair((e ? s2 : s1)[j], c->att[j], &tt[2 * d * e + 2 * j], &tt[2 * d * e + 2 * j + 1]);
+    }, 64);
+  } else {
+    c->tables_for(&s.center[(size_t)k1 * c->d], &s.sigma[(size_t)k1 * c->d], cc, tt);
+    c->tables_for(&s.center[(size_t)k2 * c->d], &s.sigma[(size_t)k2 * c->d], cc + c->dp, tt + 2 * c->d);
+  }
   W.d_two_codes.ensure(nc);
   W.d_two_tab.ensure(nt);
   HIPCHK(hipMemcpyAsync(W.d_two_codes.p, cc, nc, hipMemcpyHostToDevice, c->stream));
@@ -353,8 +367,17 @@ static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1
   int* hs = W.h_side.p;
   uint32_t* raw = W.h_raw.p;
   for (int q = 0; q < nS; ++q) side[q] = (s.c[S[q]] == c1) ? 0 : 1;
+  // large scans take their |S| draws from the device windows (no host generation and copy;
+  // the host stream adopts the state after them); debug bit 16 draws them on the host
+  const bool dev_draws = nS >= 4096 && !(c->debug & 65536);
   for (int iter = 0; iter < t; ++iter) {
-    c->rng.raw_block(raw, nS);
+    const uint32_t* d_raw = nullptr;
+    if (dev_draws) {
+      c->rng_sync();
+      d_raw = c->device_draws(nS);
+    } else {
+      c->rng.raw_block(raw, nS);
+    }
     // c1 == c2 (only through the C ABI): every draw picks the same label, so only the
     // draws are consumed
     if (nS && c1 != c2) {
@@ -365,8 +388,9 @@ static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1
         std::memcpy(hs, side.data(), (size_t)nS * 4);
         HIPCHK(hipMemcpyAsync(W.d_side.p, hs, (size_t)nS * 4, hipMemcpyHostToDevice, c->stream));
       }
-      HIPCHK(hipMemcpyAsync(W.d_raw.p, raw, (size_t)nS * 4, hipMemcpyHostToDevice, c->stream));
+      if (!d_raw) HIPCHK(hipMemcpyAsync(W.d_raw.p, raw, (size_t)nS * 4, hipMemcpyHostToDevice, c->stream));
       SmArgs a = sm_args(c, W, nS);
+      if (d_raw) a.raw = d_raw;
       a.n1 = F1.nn; a.n2 = F2.nn;
       HIPCHK(launch_sm_ll(a, c->stream));
       HIPCHK(launch_sm_scan(a, c->stream));

@@ -709,8 +709,10 @@ def test_restricted_gibbs_random_split_of_one_cluster(hd, oracle):
     eng.close()
 
 
-def test_restricted_gibbs_sizes_beyond_lds_logn(hd, oracle):
-    # |c1| + |c2| > 20479: k_sm_scan reads log(n) from global memory instead of LDS
+# |S| = 24k: several staged chunks of the scan; the draws come from the device generator
+# windows (|S| >= 4096), or from the host stream (debug bit 16)
+@pytest.mark.parametrize("debug", [0, 65536])
+def test_restricted_gibbs_sizes_beyond_lds_logn(hd, oracle, debug):
     ds = synth(24000, 12, 2, 2, seed=9)
     c = ds.truth.astype(np.int32).copy()
     rng = np.random.default_rng(2)
@@ -722,11 +724,35 @@ def test_restricted_gibbs_sizes_beyond_lds_logn(hd, oracle):
     S = [i for i in range(ds.n) if i not in (i1, i2)]
     st = oracle.seed_state(53)
     eng = make_engine(hd, ds)
+    eng.set_debug(debug)
     eng.set_state(c, cen, sig)
     eng.rng_state = st
     eng.restricted_gibbs(S, i1, i2, t=2)
     ost = oracle_state(oracle, c, cen, sig)
     assert oracle.restricted_gibbs(ds.codes, ds.attrisize, ds.v, ds.w, S, ost, i1, i2, 2, st) == 0
+    assert_same_state(eng, ost)
+    assert np.array_equal(eng.rng_state, st)
+    eng.close()
+
+
+# wide rows and a large S: device-window draws for the scans, then the pipelined update_phi
+# job fed from the window's prefetched slice (Ctx::fill_stream_from)
+@pytest.mark.parametrize("debug", [0, 65536])
+def test_restricted_gibbs_wide_large_device_draws(hd, oracle, debug):
+    ds = synth(9000, 160, 2, 4, seed=41)
+    c = ds.truth.astype(np.int32).copy()
+    i1 = int(np.where(c == 0)[0][0])
+    i2 = int(np.where(c == 1)[0][0])
+    cen, sig = random_params(ds, 2, 18)
+    S = [i for i in range(ds.n) if i not in (i1, i2)]
+    st = oracle.seed_state(55)
+    eng = make_engine(hd, ds)
+    eng.set_debug(debug)
+    eng.set_state(c, cen, sig)
+    eng.rng_state = st
+    eng.restricted_gibbs(S, i1, i2, t=3)
+    ost = oracle_state(oracle, c, cen, sig)
+    assert oracle.restricted_gibbs(ds.codes, ds.attrisize, ds.v, ds.w, S, ost, i1, i2, 3, st) == 0
     assert_same_state(eng, ost)
     assert np.array_equal(eng.rng_state, st)
     eng.close()
