@@ -40,10 +40,10 @@ def packed_layout(d: int, mmax: int):
 
 
 # FETCH_SIZE calibration on gfx950 (tools/fetch_calib.hip, profiles/r01/fetch_calib.log;
-# gather448g -- 16-lane groups gathering 448-B wide heads -- profiles/r02/fetch_calib_wide.log,
-# its FETCH_SIZE factor not calibrated): reported / true bytes and measured rates of the
+# gather448g -- 16-lane groups gathering 448-B wide heads -- profiles/r02/fetch_calib_wide.log
+# and profiles/r02/pmc_fetch_calib.csv): reported / true bytes and measured rates of the
 # prepass's access shapes
-FETCH_FACTOR = {"stream16": 0.5, "gather64": 1.0, "gather128": 0.584, "gather448g": 1.0}
+FETCH_FACTOR = {"stream16": 0.5, "gather64": 1.0, "gather128": 0.584, "gather448g": 0.569}
 RATE_GBPS = {"stream16": 5650.0, "gather64": 3080.0, "gather128": 3830.0, "gather448g": 5757.0}
 
 
@@ -78,6 +78,12 @@ def prepass_shape(d: int, mmax: int, m: int):
     else:
         shape = "gather128"
     return 8 * W + 4 * (m + 1) + 4, g, shape
+
+
+def prepass_kernel_name(d: int, mmax: int) -> str:
+    """The prepass kernel the layout takes (csrc/kernels.hip launch_prepass)."""
+    head, _, templ = head_layout(d, mmax)
+    return "k_prepass" if templ else "k_prepass_wide" if head else "k_prepass_generic"
 
 
 def prepass_bytes_per_point(d: int, mmax: int, m: int) -> int:
@@ -363,7 +369,7 @@ def main():
     traffic, traffic_src = None, None
     csvs = args.traffic_csv
     if csvs is None:
-        csvs = [os.path.join(ROOT, "profiles", "r01", f"pmc_{c}_{args.config}.csv") for c in ("fetch", "write")]
+        csvs = [os.path.join(ROOT, "profiles", "r02", f"pmc_{c}_{args.config}.csv") for c in ("fetch", "write")]
     csvs = [c for c in csvs if os.path.exists(c)]
     s_b, g_b, gshape = prepass_shape(ds.d, int(ds.attrisize.max()), args.m)
     if csvs and args.n is None:
@@ -373,7 +379,8 @@ def main():
             fetch, write = raw
             stream = s_b * ds.n
             traffic = round(stream + (fetch - FETCH_FACTOR["stream16"] * stream) / FETCH_FACTOR[gshape] + write)
-        traffic_src = [os.path.relpath(c, ROOT) for c in csvs] + ["profiles/r01/fetch_calib.log"]
+        traffic_src = [os.path.relpath(c, ROOT) for c in csvs] + ["profiles/r01/fetch_calib.log",
+                                                                  "profiles/r02/pmc_fetch_calib.csv"]
     # the measured ceiling of this access mix: its streamed and gathered bytes at the rates
     # tools/fetch_calib.hip measured for those shapes on MI355X
     wb_ = bpp - s_b - g_b
@@ -422,7 +429,7 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_prepass",
+            "kernel": prepass_kernel_name(ds.d, int(ds.attrisize.max())),
             "achieved": None if achieved is None else round(achieved, 1),
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
