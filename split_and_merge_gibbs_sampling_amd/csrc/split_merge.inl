@@ -378,11 +378,13 @@ static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1
     } else {
       c->rng.raw_block(raw, nS);
     }
+    c->mark("sm.draws");
     // c1 == c2 (only through the C ABI): every draw picks the same label, so only the
     // draws are consumed
     if (nS && c1 != c2) {
       SmTimer tm(c->stats.t_sm_scan_ms);
       sm_upload_two(c, W, s, c1, c2);
+      c->mark("sm.upload");
       // later scans start from the sides the previous scan left on the device
       if (iter == 0) {
         std::memcpy(hs, side.data(), (size_t)nS * 4);
@@ -396,6 +398,7 @@ static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1
       HIPCHK(launch_sm_scan(a, c->stream));
       HIPCHK(hipMemcpyAsync(hs, W.d_side.p, (size_t)nS * 4, hipMemcpyDeviceToHost, c->stream));
       HIPCHK(hipStreamSynchronize(c->stream));
+      c->mark("sm.device");
       to1.clear();
       to2.clear();
       for (int q = 0; q < nS; ++q) {
@@ -405,6 +408,7 @@ static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1
         s.c[i] = side[q] == 0 ? c1 : c2;
         (side[q] == 0 ? to1 : to2).push_back(i);
       }
+      c->mark("sm.sides");
       if (members_are_S && 4 * (to1.size() + to2.size()) > (size_t)nS) {
         // many moves (the first scan of a random split): rebuilding c1's table from its
         // rows costs |c1| D, moving them 2 (moves) D
@@ -420,12 +424,14 @@ static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1
       } else {
         freq_move(c, F1, F2, to1, to2);
       }
+      c->mark("sm.freq");
     }
     s.counts[c1] = F1.nn;
     s.counts[c2] = F2.nn;
     // sm:221 update_phi({c1, c2}): the mask visits clusters in ascending index order, a
     // repeated index once (c1 == c2 only through the restricted-Gibbs C ABI)
     const int st = hupdate_phi_pair(c, s, c1, F1, c2, F2);
+    c->mark("sm.phi");
     if (st) return st;
   }
   return kOk;

@@ -683,6 +683,33 @@ def test_hig_logspace_chain_large_clusters(hd, oracle):
     np.testing.assert_allclose(res["loglikelihood"], ref["loglikelihood"], rtol=RTOL, atol=0)
 
 
+# Moves over |S| >= 4096 points: the scans draw from the device windows (debug bit 16 keeps
+# them on the host); wide rows (d = 160) also take the pipelined update_phi job.
+@pytest.mark.parametrize("debug", [0, 65536])
+def test_split_merge_chain_large_moves(hd, oracle, debug):
+    ds = synth(10000, 160, 2, 3, seed=42)
+    kw = dict(m=3, iterations=6, L=1, c_i=ds.truth, burnin=0, t=3, r=3, neal8=True, split_merge=True)
+    try:
+        oracle.set_hig_logspace(True)
+        st, ref = oracle.run_markov_chain(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w, seed=6, fast=2, **kw)
+    finally:
+        oracle.set_hig_logspace(False)
+    assert st == 0
+    eng = make_engine(hd, ds)
+    try:
+        eng.set_hig_logspace(True)
+        eng.set_seed(6)
+        eng.set_debug(debug)
+        res = eng.run_markov_chain(**kw)
+        assert eng.stats()["sm_moves"] == 6
+    finally:
+        eng.close()
+    assert np.array_equal(res["c_i"], ref["c_i"])
+    assert np.array_equal(res["total_cls"], ref["total_cls"])
+    assert np.array_equal(res["accepted"], ref["accepted"])
+    np.testing.assert_allclose(res["loglikelihood"], ref["loglikelihood"], rtol=RTOL, atol=0)
+
+
 def test_restricted_gibbs_random_split_of_one_cluster(hd, oracle):
     # The split proposal's launch state: one true cluster's members dealt at random to two
     # labels with fresh parameters, so most scan draws are close calls whose pick depends
