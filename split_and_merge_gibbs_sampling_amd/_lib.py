@@ -14,6 +14,9 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "libhdpm.so")
+# A/B builds of the same library (tools/ab_*.sh): HDPM_LIB_VARIANT=x loads libhdpm_x.so
+if os.environ.get("HDPM_LIB_VARIANT"):
+    LIB_PATH = os.path.join(PKG_DIR, f"libhdpm_{os.environ['HDPM_LIB_VARIANT']}.so")
 CSRC = os.path.join(PKG_DIR, "csrc")
 
 EXPORTS = (

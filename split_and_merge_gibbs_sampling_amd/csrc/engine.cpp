@@ -74,6 +74,9 @@ struct HipError {
     if (_e != hipSuccess) throw HipError{_e, #x};     \
   } while (0)
 
+#ifndef HDPM_PHI_SPEC
+#define HDPM_PHI_SPEC 4   // update_phi phase B: first rbeta attempts speculated per batch
+#endif
 static std::atomic<int64_t> g_dev_allocs{0};   // device allocations made (diagnostics)
 
 template <class T>
@@ -2185,7 +2188,7 @@ struct Ctx {
     // batch is accepted on its first attempt (independent work the core overlaps); they are
     // committed in order up to the first item that was not, which is then drawn
     // sequentially from its true position.  Same arithmetic either way.
-    constexpr int kSpec = 4;
+    constexpr int kSpec = HDPM_PHI_SPEC;
     auto params = [&](int j, bool* bp, RBeta* rb) {
       PhiItem& P = phi_items[(size_t)t * d + j];
       const int l = cen[j] - 1;
