@@ -561,6 +561,7 @@ struct Ctx {
   DevBuf<uint64_t> d_slot_bnd;
   int scap = 0;
   int last_exact = 0;         // points the previous resolver launch decided one by one (block-mode choice)
+  int last_listed = -1;       // points the previous launch's prepass listed (exact-rows grid), -1 unknown
 
   // latent pool
   int64_t P = 0;
@@ -1606,6 +1607,7 @@ struct Ctx {
     pa.rq = d_rq.p;
     pa.p0 = p;
     pa.exact_wave = (debug & 2048) ? 1 : 0;
+    pa.exact_grid = last_listed < 0 ? 0 : std::min(1024, std::max(64, 4 * last_listed + 64));
     pa.wide = (debug & 16384) ? 0 : 1;
     pa.zero = nullptr;
     if (mcount_clear) {
@@ -1849,6 +1851,7 @@ struct Ctx {
       stats.exact_points += c.exact;
       stats.listed_points += c.listed;
       last_exact = c.exact;
+      last_listed = c.listed;
       stats.moves += c.moves;
       sweep_moves += c.moves;
       stats.checked_rounds += c.checked;

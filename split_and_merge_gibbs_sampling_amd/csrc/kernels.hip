@@ -2451,7 +2451,10 @@ hipError_t launch_exact_rows(const PrepassArgs& a, int nblocks, hipStream_t s) {
                      a.dense_total);
   const int E = a.K + a.m;
   const size_t lds = exact_wg_lds_bytes(E, a.d, a.nq * 16);
-  const dim3 g(std::min(nblocks * 4, 1024)), b(kExactWgThreads);
+  // grid: the previous launch's list size sets a cap (a converged chain lists ~13 points per
+  // C5 sweep, so 1024 mostly idle workgroups were launched); a longer list is looped over
+  const int gx = std::min(nblocks * 4, 1024);
+  const dim3 g(a.exact_grid > 0 ? std::min(gx, a.exact_grid) : gx), b(kExactWgThreads);
   const bool wg = !a.exact_wave && lds <= kExactWgLdsMax;
   if (wg && E <= kWave) hipLaunchKernelGGL(k_exact_rows_wg<1>, g, b, lds, s, a);
   else if (wg && E <= 4 * kWave) hipLaunchKernelGGL(k_exact_rows_wg<4>, g, b, lds, s, a);

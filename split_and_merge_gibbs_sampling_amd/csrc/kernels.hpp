@@ -126,6 +126,7 @@ struct PrepassArgs {
   int exact_wave;            // 1: exact rows one wave per point (no workgroup staging)
   int wide;                  // 1: wide layouts take k_prepass_wide (0: the generic kernel)
   int* zero;                 // k_cluster_summary clears this word first (the sweep's move count), or nullptr
+  int exact_grid;            // cap on the exact-rows grid (0: none); workgroups loop over the list
 };
 
 // The resolver runs in block mode (csrc/kernels.hip, k_resolve_blk) when in the previous
