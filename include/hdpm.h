@@ -163,7 +163,8 @@ int hdpm_reset_stats(hdpm_ctx* ctx);
  * wide layouts take the generic prepass (one thread per point) instead of k_prepass_wide; bit 15:
  * the prepared next sweep is launched before the speculative update_phi is started; bit 16:
  * restricted scans of >= 4096 points draw their uniforms on the host (not from the device
- * generator windows). */
+ * generator windows); bit 17: a sweep prepared at the end of hdpm_iterations does not start
+ * its prepass on the device. */
 int hdpm_set_debug(hdpm_ctx* ctx, int32_t mode);
 /* The prepass's pool-entry heads, P entries of wb*Ws + 2 words padded to a power of two
  * (Ws <= 4) or to a multiple of 8 words (wide layouts) (csrc/kernels.hpp "Pool-entry heads",
@@ -199,7 +200,8 @@ int hdpm_debug_draw(hdpm_ctx* ctx, const double* logw, int32_t E, double rU, int
 /* Testing: exp (fn = 0) or log (fn = 1) of x[n] on the device, glibc's algorithm (ocml = 0)
  * or the device libm's (ocml = 1). */
 int hdpm_debug_math(hdpm_ctx* ctx, const double* x, int64_t n, int32_t fn, int32_t ocml, double* out);
-/* Block until all device work of the context is done. */
+/* Block until the chain's device work is done (a prepared next sweep's prefix -- scratch
+ * outputs only -- may still be running; hipDeviceSynchronize waits for it too). */
 int hdpm_synchronize(hdpm_ctx* ctx);
 
 #ifdef __cplusplus

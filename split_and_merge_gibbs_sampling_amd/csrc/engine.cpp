@@ -1570,15 +1570,21 @@ struct Ctx {
   // One launch of the sweep from point p with nslots slots: cluster summary, prepass, exact
   // rows, resolver, control copy, and the sweep-end kernels behind it (they act only if
   // this launch completes the sweep).  kOk or kArg (resolver state too large for LDS).
-  int launch_round(int p, int nslots, int m, const uint32_t* d_sweep_raw, bool track) {
+  // part: kRoundAll, kRoundPrefix (up to the exact rows: kernels that write scratch only, so
+  // a prepared sweep can start on the device and still be dropped), kRoundResolve (the rest,
+  // after a prefix launched with the same arguments and no state change in between).
+  enum { kRoundAll = 0, kRoundPrefix = 1, kRoundResolve = 2 };
+  int launch_round(int p, int nslots, int m, const uint32_t* d_sweep_raw, bool track, int part = kRoundAll) {
     const double dmax = 0.25;
     ensure_slots(nslots + 2);
     // the resolver writes its control block and summary straight into host memory
     if (h_ctl.n < kCtlInts + 3 * (size_t)scap) h_ctl.ensure(kCtlInts + 3 * (size_t)scap, hipHostMallocCoherent);
     // HIP events between kernels cost a dispatch gap each: the prepass is timed on every
     // 8th launch (all launches, and the other kernels too, in the diagnostic modes)
-    round_fine = (debug & (2 | 32 | 512)) != 0;
-    round_timed = round_fine || (launch_count++ % 8 == 0);
+    if (part != kRoundResolve) {
+      round_fine = (debug & (2 | 32 | 512)) != 0;
+      round_timed = round_fine || (launch_count++ % 8 == 0);
+    }
     const int S = nslots;
     if (S + m > Ecap) {
       Ecap = std::max(S + m, std::max(2 * Ecap, 32));
@@ -1610,20 +1616,22 @@ struct Ctx {
     pa.exact_grid = last_listed < 0 ? 0 : std::min(1024, std::max(64, 4 * last_listed + 64));
     pa.wide = (debug & 16384) ? 0 : 1;
     pa.zero = nullptr;
-    if (mcount_clear) {
+    if (mcount_clear && part != kRoundResolve) {
       if (K > 0) pa.zero = d_mcount.p;
       else HIPCHK(hipMemsetAsync(d_mcount.p, 0, 4, stream));
       mcount_clear = false;
     }
     const int nblocks = (n - p + kBlock - 1) / kBlock;
-    HIPCHK(launch_cluster_summary(pa, stream));
-    if (round_timed) HIPCHK(hipEventRecord(ev[0], stream));
-    HIPCHK(launch_prepass(pa, nblocks, stream));
-    stats.prepass_points += n - p;
-    round_points = n - p;
-    if (round_timed) HIPCHK(hipEventRecord(ev[1], stream));
-    HIPCHK(launch_exact_rows(pa, nblocks, stream));
-    if (round_fine) HIPCHK(hipEventRecord(ev[5], stream));
+    if (part != kRoundResolve) {
+      HIPCHK(launch_cluster_summary(pa, stream));
+      if (round_timed) HIPCHK(hipEventRecord(ev[0], stream));
+      HIPCHK(launch_prepass(pa, nblocks, stream));
+      stats.prepass_points += n - p;
+      round_points = n - p;
+      if (round_timed) HIPCHK(hipEventRecord(ev[1], stream));
+      HIPCHK(launch_exact_rows(pa, nblocks, stream));
+      if (round_fine) HIPCHK(hipEventRecord(ev[5], stream));
+    }
 
     ResolveArgs ra;
     ra.n = n; ra.d = d; ra.dp = dp; ra.m = m; ra.P = P;
@@ -1656,6 +1664,7 @@ struct Ctx {
       err = "too many clusters for the resolver (K > ~2300)";
       return kArg;
     }
+    if (part == kRoundPrefix) return kOk;
     HIPCHK(launch_resolve(ra, stream));
     if (round_fine) HIPCHK(hipEventRecord(ev[2], stream));
     HIPCHK(hipEventRecord(ev[6], stream));
@@ -1692,6 +1701,7 @@ struct Ctx {
     Rng saved;
     const uint32_t* raw = nullptr;
     bool launched = false;             // round 0 of the sweep is already on the device
+    bool prefix = false;               // round 0's prepass part is on the device (droppable)
     bool track = false;
   } ahead;
 
@@ -1709,6 +1719,7 @@ struct Ctx {
     ahead.m = m;
     ahead.lv = labels_version;
     ahead.launched = false;
+    ahead.prefix = false;
     ahead.active = true;
     // the speculative update_phi first: its serial draws, not the device sweep, are the
     // longer path (timeline: launching the sweep first cost ~8% of the iteration rate);
@@ -1718,11 +1729,19 @@ struct Ctx {
       spec_launch();
       mark("ahead.spec");
     }
-    if (launch && resolve_smem_bytes(std::min(scap, K + 2), m, K + m <= 64 ? 1 : 0) <= 160 * 1024) {
+    if (resolve_smem_bytes(std::min(scap, K + 2), m, K + m <= 64 ? 1 : 0) <= 160 * 1024) {
       ahead.track = freq_dev_valid;
       sweep_buffers(ahead.track);
       mark("ahead.buf");
-      if (launch_round(0, K, m, ahead.raw, ahead.track) == kOk) ahead.launched = true;
+      // the whole round 0 when the caller runs the sweep next; otherwise its prepass part
+      // only (scratch outputs: any other call can still drop the prepared sweep)
+      if (launch) {
+        if (launch_round(0, K, m, ahead.raw, ahead.track) == kOk) ahead.launched = true;
+      } else if (!(debug & 131072)) {
+        // hdpm_synchronize waits for the chain's work up to here, not for the prepared prefix
+        HIPCHK(hipEventRecord(ev[7], stream));
+        if (launch_round(0, K, m, ahead.raw, ahead.track, kRoundPrefix) == kOk) ahead.prefix = true;
+      }
     }
     if (sweep_first) {
       spec_launch();
@@ -1788,6 +1807,7 @@ struct Ctx {
     const size_t nraw = (size_t)n * (m + 1);
     const uint32_t* d_sweep_raw = use_ahead ? ahead.raw : device_draws((int64_t)nraw);
     const bool ahead_launched = use_ahead && ahead.launched;
+    const bool ahead_prefix = use_ahead && ahead.prefix && !ahead.launched;
     ahead.active = false;
     mark("draws");
     // update_phi speculated on the pool while this thread launches the sweep
@@ -1808,11 +1828,13 @@ struct Ctx {
     const int64_t rounds0 = stats.rounds;
     // round 0 may already be on the device (prepare_next_sweep with launch)
     const bool launched_ahead = ahead_launched;
-    const bool track = launched_ahead ? ahead.track : freq_dev_valid;
-    if (!launched_ahead) sweep_buffers(track);
+    const bool track = (launched_ahead || ahead_prefix) ? ahead.track : freq_dev_valid;
+    if (!launched_ahead && !ahead_prefix) sweep_buffers(track);
     while (p < n) {
       if (!(launched_ahead && stats.rounds == rounds0)) {
-        const int lst = launch_round(p, nslots, m, d_sweep_raw, track);
+        // round 0 after a prepared prefix: the resolver part only (same arguments)
+        const int part = (ahead_prefix && stats.rounds == rounds0) ? kRoundResolve : kRoundAll;
+        const int lst = launch_round(p, nslots, m, d_sweep_raw, track, part);
         if (lst) return lst;
       }
       mark("launched");
@@ -3232,6 +3254,9 @@ int hdpm_debug_math(hdpm_ctx* h, const double* x, int64_t n, int32_t fn, int32_t
 }
 int hdpm_synchronize(hdpm_ctx* h) {
   CTX_KEEP();
+  // the chain's committed work; a prepared sweep's prefix (scratch only) may still run
+  if (ctx->ahead.active && ctx->ahead.prefix && !ctx->ahead.launched)
+    return hipEventSynchronize(ctx->ev[7]) == hipSuccess ? HDPM_OK : HDPM_E_DEVICE;
   return hipStreamSynchronize(ctx->stream) == hipSuccess ? HDPM_OK : HDPM_E_DEVICE;
 }
 
