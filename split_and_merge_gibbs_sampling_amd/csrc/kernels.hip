@@ -1471,9 +1471,66 @@ __host__ __device__ inline size_t exact_wg_lds_bytes(int E, int d, int dp) {
   return (size_t)E * (d + 1) * 8 + (size_t)E * 16 + (size_t)E * 4 + (size_t)dp + 16;
 }
 
+// k_list_scan inside the exact-rows workgroups (one launch less per round): every workgroup
+// scans the list blocks' counts in kExactWgThreads chunks (exclusive offsets in s_off);
+// workgroup 0 also writes the dense list and its length, which the resolver reads.
+__device__ int exact_dense_scan(const PrepassArgs& a, int* s_off) {
+  __shared__ int s_w[kExactWgThreads / kWave];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int chunk = (a.nlb + kExactWgThreads - 1) / kExactWgThreads;
+  const int b0 = min(a.nlb, t * chunk), b1 = min(a.nlb, b0 + chunk);
+  int mine = 0;
+  for (int b = b0; b < b1; ++b) mine += a.cnt[b];
+  int inc = mine;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int u = __shfl_up(inc, o);
+    if (lane >= o) inc += u;
+  }
+  if (lane == kWave - 1) s_w[wv] = inc;
+  __syncthreads();
+  int base = 0, all = 0;
+#pragma unroll
+  for (int w = 0; w < kExactWgThreads / kWave; ++w) {
+    base += w < wv ? s_w[w] : 0;
+    all += s_w[w];
+  }
+  const int off0 = base + inc - mine;
+  s_off[t] = off0;
+  if (t == 0) s_off[kExactWgThreads] = all;
+  if (blockIdx.x == 0) {
+    int off = off0;
+    for (int b = b0; b < b1; ++b) {
+      const int c = a.cnt[b];
+      for (int q = 0; q < c; ++q) a.dense[off + q] = b * a.lblock + q;
+      off += c;
+    }
+    if (t == 0) *a.dense_total = all;
+  }
+  __syncthreads();
+  return all;
+}
+// row of dense position q: the thread chunk whose offsets hold q, then its blocks
+__device__ int exact_dense_row(const PrepassArgs& a, const int* s_off, int q) {
+  int lo = 0, hi = kExactWgThreads - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (s_off[mid + 1] > q) hi = mid;
+    else lo = mid + 1;
+  }
+  const int chunk = (a.nlb + kExactWgThreads - 1) / kExactWgThreads;
+  int b = lo * chunk, off = s_off[lo];
+  for (;; ++b) {
+    const int c = a.cnt[b];
+    if (q < off + c) return b * a.lblock + (q - off);
+    off += c;
+  }
+}
+
 template <int RE>
 __global__ __launch_bounds__(kExactWgThreads) void k_exact_rows_wg(PrepassArgs a) {
-  const int total = *a.dense_total;
+  __shared__ int s_off[kExactWgThreads + 1];
+  const int total = exact_dense_scan(a, s_off);
   if ((int)blockIdx.x >= total) return;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ double lp[4 * kWave];
@@ -1488,7 +1545,7 @@ __global__ __launch_bounds__(kExactWgThreads) void k_exact_rows_wg(PrepassArgs a
   const int t = threadIdx.x, lane = t & 63;
   const int nj4 = (D + 3) >> 2;
   for (int q = blockIdx.x; q < total; q += gridDim.x) {
-    const int row = a.dense[q];
+    const int row = exact_dense_row(a, s_off, q);
     const int64_t i = a.list[row];
     const uint32_t* raw = a.raw + i * (a.m + 1);
     if (t == 0) a.rq[q] = make_int4(row, (int)i, a.c[i], (int)raw[a.m]);   // the resolver's inputs
@@ -2445,12 +2502,16 @@ static hipError_t launch_prepass_w(const PrepassArgs& a, int nblocks, hipStream_
   return hipGetLastError();
 }
 
-hipError_t launch_exact_rows(const PrepassArgs& a, int nblocks, hipStream_t s) {
-  const int lb = prepass_list_block(a);
-  hipLaunchKernelGGL(k_list_scan, dim3(1), dim3(kScanThreads), 0, s, a.cnt, (a.n - a.p0 + lb - 1) / lb, lb, a.dense,
-                     a.dense_total);
+hipError_t launch_exact_rows(const PrepassArgs& a0, int nblocks, hipStream_t s) {
+  PrepassArgs a = a0;
+  a.lblock = prepass_list_block(a);
+  a.nlb = (a.n - a.p0 + a.lblock - 1) / a.lblock;
   const int E = a.K + a.m;
   const size_t lds = exact_wg_lds_bytes(E, a.d, a.nq * 16);
+  // the workgroup kernels scan the list themselves; the one-wave kernel needs k_list_scan
+  if (a.exact_wave || lds > kExactWgLdsMax || E > 4 * kWave)
+    hipLaunchKernelGGL(k_list_scan, dim3(1), dim3(kScanThreads), 0, s, a.cnt, a.nlb, a.lblock, a.dense,
+                       a.dense_total);
   // grid: the previous launch's list size sets a cap (a converged chain lists ~13 points per
   // C5 sweep, so 1024 mostly idle workgroups were launched); a longer list is looped over
   const int gx = std::min(nblocks * 4, 1024);
