@@ -506,14 +506,14 @@ struct WideRow {
   }
 };
 
-// Dynamic LDS of k_prepass_wide: the chunk's rows [16][wb Ws + 1], and (CL) the cluster
+// Dynamic LDS of k_prepass_wide: two chunks' rows [2][16][wb Ws + 1], and (CL) the cluster
 // summaries [K][bw + 2].
 constexpr int kWidePf = kWideRowMax * kWideChunk / kWideThreads;   // row words per thread prefetched
 constexpr int kWideMaxM1 = 16;              // m + 1 <= 16: a chunk's raw draws fit one wave's lanes x 4
 __host__ __device__ inline size_t wide_rows_words(int wb, int Ws) { return (size_t)kWideChunk * (wb * Ws + 1); }
 size_t prepass_wide_lds_bytes(int wb, int Ws, int m, int K, int bw, bool cl) {
   (void)m;
-  return 8 * (wide_rows_words(wb, Ws) + (cl ? (size_t)K * (bw + 2) : 0));
+  return 8 * (2 * wide_rows_words(wb, Ws) + (cl ? (size_t)K * (bw + 2) : 0));
 }
 // byte offsets of the record arrays must fit the buffer instructions' 32-bit offsets
 bool prepass_wide_offsets_fit(const PrepassArgs& a) {
@@ -530,8 +530,8 @@ __global__ __launch_bounds__(kWideThreads) void k_prepass_wide(PrepassArgs a, in
   __shared__ uint32_t s_raw[2][kWideChunk * kWideMaxM1];
   const int WS = a.Ws, WR = WB * WS, RS = WR + 1, SC = (WB + kQ) * WS, HS = head_stride(WB, WS);
   const int bw = a.bw, cw = a.bw + 2;
-  uint64_t* s_rows = s_dyn;
-  uint64_t* s_cs = s_dyn + wide_rows_words(WB, WS);
+  uint64_t* s_rows0 = s_dyn;                 // two row buffers: chunk c reads one while c + grid is staged
+  uint64_t* s_cs = s_dyn + 2 * wide_rows_words(WB, WS);
   const int tid = threadIdx.x, g = tid >> 4, w = tid & 15, m1 = a.m + 1;
   const int w8 = 8 * w;
   const __amdgpu_buffer_rsrc_t r_slot = make_rsrc(a.slot_bnd, (int64_t)(a.S + 2) * bw * 8);
@@ -572,7 +572,7 @@ __global__ __launch_bounds__(kWideThreads) void k_prepass_wide(PrepassArgs a, in
 #pragma unroll
     for (int r = 0; r < kWidePf; ++r) {
       const int e = tid + r * kWideThreads;
-      if (e < kWideChunk * WR) s_rows[(e & (kWideChunk - 1)) * RS + e / kWideChunk] = pf[r];
+      if (e < kWideChunk * WR) s_rows0[par * wide_rows_words(WB, WS) + (e & (kWideChunk - 1)) * RS + e / kWideChunk] = pf[r];
     }
     if (tid < kWideChunk) {
       s_own[par][tid] = pf_own;
@@ -594,9 +594,28 @@ __global__ __launch_bounds__(kWideThreads) void k_prepass_wide(PrepassArgs a, in
 #pragma unroll
   for (int k = 0; k < NW; ++k) xr.val[k] = w + 16 * k < WS;
   int par = 0;
+  // the chunk's margins, row positions and ordered compaction (one list block per chunk), by
+  // wave 0 at the top of the next iteration (one barrier per chunk)
+  auto finish = [&](int cf, int pf_) {
+    const int64_t f0 = (int64_t)a.p0 + (int64_t)cf * kWideChunk;
+    const int fn = (int)min((int64_t)kWideChunk, (int64_t)a.n - f0);
+    const bool on = tid < fn;
+    const double mgp = on ? s_mg[pf_][tid] : -INFINITY;
+    const int ocp = on ? s_oc[pf_][tid] : 0;
+    const bool uncertain = on && !(ocp >= 2 && mgp > a.thresh);
+    const int64_t i = f0 + tid;
+    if (on) a.margin[i] = mgp;
+    const unsigned long long bal = __ballot(uncertain);
+    const int row = cf * kWideChunk + __popcll(bal & ((1ull << tid) - 1ull));
+    if (on) a.rowpos[i] = uncertain ? row : -1;
+    if (uncertain) a.list[row] = (int)i;
+    if (tid == 0) a.cnt[cf] = __popcll(bal);
+  };
+  int cprev = -1;
 #pragma unroll 1
   for (; c < nchunks; c += gridDim.x, par ^= 1) {
-    __syncthreads();                          // the chunk is staged (and the cluster summaries)
+    __syncthreads();                          // the chunk is staged; the previous chunk's margins are in
+    if (cprev >= 0 && tid < 64) finish(cprev, par ^ 1);
     const int cn = c + gridDim.x;
     if (cn < nchunks) fetch(cn);
     const int64_t i0 = (int64_t)a.p0 + (int64_t)c * kWideChunk;
@@ -605,7 +624,8 @@ __global__ __launch_bounds__(kWideThreads) void k_prepass_wide(PrepassArgs a, in
 #pragma unroll
     for (int k = 0; k < NW; ++k)
 #pragma unroll
-      for (int b = 0; b < WB; ++b) xr.x[k][b] = xr.val[k] ? s_rows[g * RS + b * WS + w + 16 * k] : 0ull;
+      for (int b = 0; b < WB; ++b)
+        xr.x[k][b] = xr.val[k] ? s_rows0[par * wide_rows_words(WB, WS) + g * RS + b * WS + w + 16 * k] : 0ull;
     const int own = s_own[par][g];
     const int own_cnt = s_oc[par][g];
     double mg = -INFINITY;
@@ -723,23 +743,13 @@ __global__ __launch_bounds__(kWideThreads) void k_prepass_wide(PrepassArgs a, in
       mg = lo - ubmax;
     }
     if (w == 0) s_mg[par][g] = mg;
-    __syncthreads();                          // margins written; every group has read the rows
-    if (tid < 64) {
-      // the chunk's margins, row positions and ordered compaction (one list block per chunk)
-      const bool on = tid < npts;
-      const double mgp = on ? s_mg[par][tid] : -INFINITY;
-      const int ocp = on ? s_oc[par][tid] : 0;
-      const bool uncertain = on && !(ocp >= 2 && mgp > a.thresh);
-      const int64_t i = i0 + tid;
-      if (on) a.margin[i] = mgp;
-      const unsigned long long bal = __ballot(uncertain);
-      const int row = c * kWideChunk + __popcll(bal & ((1ull << tid) - 1ull));
-      if (on) a.rowpos[i] = uncertain ? row : -1;
-      if (uncertain) a.list[row] = (int)i;
-      if (tid == 0) a.cnt[c] = __popcll(bal);
-    }
+    // the next chunk into the other buffers (wave 0 stages its labels / draws only after it
+    // finished the previous chunk from them, above)
     if (cn < nchunks) stage(par ^ 1);
+    cprev = c;
   }
+  __syncthreads();
+  if (cprev >= 0 && tid < 64) finish(cprev, par ^ 1);
 }
 
 // Workgroups of k_prepass_wide in flight on the whole GPU (persistent grid).
