@@ -90,6 +90,15 @@ def test_device_exp_log_are_host_libm(eng):
     assert np.array_equal(dl.view(np.uint64), hl.view(np.uint64))
 
 
+def test_device_log_of_counts_is_host_libm(eng):
+    # log(n) of cluster sizes: the resolver and the restricted scan take it from the glibc
+    # replica on the device where the host reads its logn table (std::log)
+    y = np.concatenate([np.arange(1, 1 << 21, dtype=np.float64),
+                        np.random.default_rng(7).uniform(1.0, 1e12, 100_000)])
+    dl = eng.debug_math(y, "log")
+    assert np.array_equal(dl.view(np.uint64), np.array([math.log(v) for v in y]).view(np.uint64))
+
+
 def test_ulp_boundary_draws_follow_glibc(eng):
     x = grid()
     x = x[np.isfinite(x) & (x < -1e-6) & (x > -30.0)]
