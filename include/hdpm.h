@@ -164,7 +164,8 @@ int hdpm_reset_stats(hdpm_ctx* ctx);
  * the prepared next sweep is launched before the speculative update_phi is started; bit 16:
  * restricted scans of >= 4096 points draw their uniforms on the host (not from the device
  * generator windows); bit 17: a sweep prepared at the end of hdpm_iterations does not start
- * its prepass on the device. */
+ * its prepass on the device; bit 18: the prepass certifies "stay" by the margin only (not by
+ * the draw's uniform, kernels.hip stay_by_uniform). */
 int hdpm_set_debug(hdpm_ctx* ctx, int32_t mode);
 /* The prepass's pool-entry heads, P entries of wb*Ws + 2 words padded to a power of two
  * (Ws <= 4) or to a multiple of 8 words (wide layouts) (csrc/kernels.hpp "Pool-entry heads",

@@ -562,6 +562,7 @@ struct Ctx {
   int scap = 0;
   int last_exact = 0;         // points the previous resolver launch decided one by one (block-mode choice)
   int last_listed = -1;       // points the previous launch's prepass listed (exact-rows grid), -1 unknown
+  bool last_unsettled = false;  // the previous launch exceeded its drift budget or restarted
 
   // latent pool
   int64_t P = 0;
@@ -1606,6 +1607,10 @@ struct Ctx {
     pa.csum = d_csum.p;
 
     pa.thresh = (debug & 1) ? INFINITY : T + 2.0 * dmax;
+    // certification by the draw's uniform only while the chain is settled: after a launch
+    // that exceeded its drift budget, restarted or decided many points itself, uniform-
+    // certified points (no exact rows) would fail re-verification and restart the launch
+    pa.dmax2 = ((debug & (1 | 262144)) || last_unsettled || last_exact >= kResolveBlkMin) ? INFINITY : 2.0 * dmax;
     pa.L = d_L.p; pa.rowpos = d_rowpos.p; pa.margin = d_margin.p; pa.list = d_list.p; pa.cnt = d_cnt.p;
     pa.dense = d_dense.p; pa.dense_total = d_dense_total.p;
     pa.spec = (debug & 8) ? nullptr : d_spec.p;
@@ -1877,6 +1882,7 @@ struct Ctx {
       stats.moves += c.moves;
       sweep_moves += c.moves;
       stats.checked_rounds += c.checked;
+      last_unsettled = c.checked || c.restart;
       if (c.status) {
         err = c.status == kValidate ? "State validation failed: inconsistent cluster count from Neal8 case 2"
               : c.status == kWalker ? "Walker alias table failure"

@@ -145,12 +145,28 @@ __device__ __forceinline__ double ll_lane(const PointCodes<NQR>& x, int d, const
 }
 
 
+// Certainty by the draw's uniform (n8:95-102).  With the own cluster ahead of every other of
+// the E entries by at least mg in log-weight, the max is the own entry (exp(0) = 1), revsort
+// puts it first, and its computed probability after the sums and FixupProb is at least
+// 1 / (1 + (E - 1) e^-mg) up to ~(2E + 10) ulps of rounding; Rcpp's ProbSampleReplace picks
+// the first entry iff rU <= that probability.  So a point whose categorical uniform lies
+// below the bound (shrunk by 1e-12 relative, and mg by 1e-6) stays whatever the exact rows
+// -- no exact row is needed even though the margin is far below T.  E <= 200 keeps the
+// Walker alias out of reach (only the own entry has n p > 0.1).
+__device__ __forceinline__ bool stay_by_uniform(double mg, uint32_t raw_cat, int E) {
+  if (!(mg > 1e-6) || E > 200) return false;
+  const double pl = 1.0 / (1.0 + (double)(E - 1) * exp(-(mg - 1e-6)));
+  return raw_to_unif(raw_cat) <= pl * (1.0 - 1e-12);
+}
+
 // Margin, row position and the ordered compaction of the block's uncertain points (the
 // block's kBlock points are threads 0..kBlock-1 of its NT; the others pass active = false).
 template <int NT = kBlock>
 __device__ __forceinline__ void prepass_finish(const PrepassArgs& a, int64_t i, bool active, int own_cnt, double mg) {
   const int tid = threadIdx.x;
-  const bool uncertain = active && !(own_cnt >= 2 && mg > a.thresh);
+  const bool uncertain =
+      active && !(own_cnt >= 2 && (mg > a.thresh ||
+                                   stay_by_uniform(mg - a.dmax2, a.raw[i * (a.m + 1) + a.m], a.K + a.m)));
   if (active) a.margin[i] = mg;
 
   // ordered compaction of the uncertain points of this block
@@ -602,7 +618,9 @@ __global__ __launch_bounds__(kWideThreads) void k_prepass_wide(PrepassArgs a, in
     const bool on = tid < fn;
     const double mgp = on ? s_mg[pf_][tid] : -INFINITY;
     const int ocp = on ? s_oc[pf_][tid] : 0;
-    const bool uncertain = on && !(ocp >= 2 && mgp > a.thresh);
+    const bool uncertain =
+        on && !(ocp >= 2 && (mgp > a.thresh ||
+                             stay_by_uniform(mgp - a.dmax2, a.raw[(f0 + tid) * m1 + a.m], a.K + a.m)));
     const int64_t i = f0 + tid;
     if (on) a.margin[i] = mgp;
     const unsigned long long bal = __ballot(uncertain);
@@ -1732,7 +1750,10 @@ __device__ __forceinline__ bool RCtx::verify(int64_t lo, int64_t hi, double dn_o
   for (int64_t base = lo; base < hi; base += kWave) {
     const int64_t j = base + lane;
     bool fail = false;
-    if (j < hi && a.rowpos[j] < 0) fail = !(a.margin[j] - 2.0 * dn > a.T && cn[a.c[j]] >= 2);
+    if (j < hi && a.rowpos[j] < 0) {
+      const double mg = a.margin[j] - 2.0 * dn;
+      fail = !((mg > a.T || stay_by_uniform(mg, a.raw[j * (a.m + 1) + a.m], a.K + a.m)) && cn[a.c[j]] >= 2);
+    }
     const unsigned long long bal = __ballot(fail);
     if (bal) {
       if (lane == 0) { S.restart = 1; S.next = (int)(base + __ffsll((long long)bal) - 1); }
@@ -1915,8 +1936,9 @@ if (start_checked >= 0 && S.status == 0 && !S.restart) {
     int ci = 0;
     if (i < a.n) {
       ci = a.c[i];
-      const double mg = a.margin[i];
-      unc = a.force_exact || !(mg - 2.0 * S.dnow > a.T && st.cnt[ci] >= 2);
+      const double mg = a.margin[i] - 2.0 * S.dnow;
+      unc = a.force_exact ||
+            !((mg > a.T || stay_by_uniform(mg, a.raw[i * (a.m + 1) + a.m], a.K + a.m)) && st.cnt[ci] >= 2);
     }
     unsigned long long bal = __ballot(unc);
     bool stop = false;
@@ -1935,8 +1957,9 @@ if (start_checked >= 0 && S.status == 0 && !S.restart) {
       // drift may have grown: re-test the remaining lanes
       bool u2 = false;
       if (lane > q && i < a.n) {
-        const double mg = a.margin[i];
-        u2 = a.force_exact || !(mg - 2.0 * S.dnow > a.T && st.cnt[ci] >= 2);
+        const double mg = a.margin[i] - 2.0 * S.dnow;
+        u2 = a.force_exact ||
+             !((mg > a.T || stay_by_uniform(mg, a.raw[i * (a.m + 1) + a.m], a.K + a.m)) && st.cnt[ci] >= 2);
       }
       bal = __ballot(u2);
     }

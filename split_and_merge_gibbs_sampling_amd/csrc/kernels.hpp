@@ -112,6 +112,7 @@ struct PrepassArgs {
   const double* logn;        // logn[k] = log(k) (glibc), k = 0..n+1
   double logfac;             // log(gamma / m)
   double thresh;             // certainty threshold incl. 2 * drift budget
+  double dmax2;              // 2 * drift budget (stay_by_uniform), +inf: margins only
   double* L;                 // exact rows of the uncertain points: L[rowpos * (S + m) + e]
   int* rowpos;               // per point: its row in L, or -1 (certain at the snapshot)
   double* margin;            // per point: lower bound on the own-cluster margin, or -inf

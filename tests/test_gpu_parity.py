@@ -123,7 +123,7 @@ def test_zoo_sweeps_with_update_phi_one_cluster(hd, oracle, zoo, debug):
 # 16: recount the frequency tables every update_phi; 128: no speculative update_phi;
 # 2048: exact rows one wave per point; 4096: no block mode in the resolver; 8192: block mode
 # for every launch
-@pytest.mark.parametrize("debug", [0, 1, 8, 16, 128, 2048, 2048 | 1, 4096, 8192, 8192 | 8])
+@pytest.mark.parametrize("debug", [0, 1, 8, 16, 128, 2048, 2048 | 1, 4096, 8192, 8192 | 8, 262144])
 def test_synthetic_sweeps_with_update_phi(hd, oracle, debug):
     ds = synth(6000, 32, 8, 2, seed=3)
     cen, sig = random_params(ds, 8, 7)
