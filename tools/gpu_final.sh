@@ -14,4 +14,6 @@ timeout -k 10 200 python -u bench.py --config c2 --no-cpu-baseline --steps 100 -
 timeout -k 10 200 python -u bench.py --config c4 --sm --no-cpu-baseline --steps 30 --warmup 3 > $O/bench_c4_sm.jsonl 2> $O/bench_c4_sm.err &&
 timeout -k 10 200 python -u bench.py --config c3 --sm --no-cpu-baseline --steps 60 --warmup 5 > $O/bench_c3_sm.jsonl 2> $O/bench_c3_sm.err &&
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof_c4 -o run --output-format csv -- python3 bench.py --config c4 --no-cpu-baseline --steps 100 --warmup 5 > $O/prof_c4.log 2>&1 &&
-timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof_c4sm -o run --output-format csv -- python3 bench.py --config c4 --sm --no-cpu-baseline --steps 10 --warmup 3 > $O/prof_c4sm.log 2>&1
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof_c4sm -o run --output-format csv -- python3 bench.py --config c4 --sm --no-cpu-baseline --steps 10 --warmup 3 > $O/prof_c4sm.log 2>&1 &&
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof_c5 -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 100 --warmup 5 > $O/prof_c5.log 2>&1 &&
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof_c3 -o run --output-format csv -- python3 bench.py --config c3 --no-cpu-baseline --steps 100 --warmup 5 > $O/prof_c3.log 2>&1
