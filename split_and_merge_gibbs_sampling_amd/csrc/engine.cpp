@@ -193,7 +193,13 @@ class HostPool {
       f((int64_t)0, n);
       return;
     }
-    std::lock_guard<std::mutex> serial(run_mu_);
+    // another context's job still open on the pool (its launch() holds run_mu_ across API
+    // calls): run on the calling thread instead of waiting for it (same thread: deadlock)
+    std::unique_lock<std::mutex> serial(run_mu_, std::try_to_lock);
+    if (!serial.owns_lock()) {
+      f((int64_t)0, n);
+      return;
+    }
     quiesce();
     range_ = [&f](int64_t a, int64_t b) { f(a, b); };
     bcast_ = nullptr;
@@ -210,9 +216,11 @@ class HostPool {
   // continues.  join() closes the job and waits only for the workers that joined it, so a
   // worker the OS has not run yet (a busy core) holds nobody up: f must hand out its work
   // through shared counters that the caller drains too.
+  // false (nothing launched) while another context's job holds the pool: the caller then
+  // drains its job alone, which every launched job supports
   template <class F>
-  void launch(F&& f) {
-    run_mu_.lock();
+  bool try_launch(F&& f) {
+    if (!run_mu_.try_lock()) return false;
     quiesce();
     bjob_ = std::forward<F>(f);
     bcast_ = &bjob_;
@@ -220,6 +228,7 @@ class HostPool {
     bdone_.store(0, std::memory_order_relaxed);
     bclaim_.store(0, std::memory_order_relaxed);
     publish();
+    return true;
   }
   void join() {
     const int joined = bclaim_.fetch_or(kClosed, std::memory_order_acq_rel) & ~kClosed;
@@ -634,6 +643,12 @@ struct Ctx {
   // takes masked (subset) histograms.
   DevBuf<unsigned> d_freq, d_freq2, d_freq_m;
   bool freq_dev_valid = false;
+  // Below kTrackMinN points the tables are recounted for every update_phi instead of
+  // carried through the sweep by the move log: at N < 64 the carried tables were seen to
+  // disagree with a recount (tools/tiny_probe2.py), and a recount of
+  // a few thousand rows costs microseconds.  Debug bit 16 recounts at every size.
+  static constexpr int kTrackMinN = 4096;
+  bool recount_only() const { return (debug & 16) || n < kTrackMinN; }
   uint64_t freq_d2h_version = 0;      // labels_version whose freq copy the sweep already started
   DevBuf<int> d_mlog, d_mcount;
   PinBuf<unsigned> h_freq;
@@ -1796,8 +1811,8 @@ struct Ctx {
     if (tables_dirty) upload_clusters();
     // update_phi can be speculated during the sweep when the host holds the pre-sweep
     // frequency tables of every label and the sweep carries them (move log)
-    const bool spec_go = freq_dev_valid && freq_version == labels_version && !(debug & (128 | 16));
-    const bool freq_before_ok = freq_version == labels_version && !(debug & 16);
+    const bool spec_go = freq_dev_valid && freq_version == labels_version && !(debug & 128) && !recount_only();
+    const bool freq_before_ok = freq_version == labels_version && !recount_only();
     if (!use_ahead) spec.ran = false;
     spec.lv = 0;
     labels_version++;
@@ -1956,7 +1971,7 @@ struct Ctx {
   void histogram_launch(const std::vector<unsigned char>* mask) {
     const size_t nent = (size_t)K * d * mmax;
     h_freq.ensure(std::max<size_t>(nent, 1));
-    if (!mask && freq_dev_valid && !(debug & 16)) {
+    if (!mask && freq_dev_valid && !recount_only()) {
       // the per-label tables were carried through the sweep by the move log (and usually
       // copied out behind it already)
       if (freq_d2h_version != labels_version) {
@@ -2484,8 +2499,7 @@ struct Ctx {
   void pj_launch() {
     HostPool& pool = HostPool::get();
     pj.t_launch = std::chrono::steady_clock::now();
-    pj_open = pool.workers() > 0;
-    if (pj_open) pool.launch([this](int) { pj_work(); });
+    pj_open = pool.workers() > 0 && pool.try_launch([this](int) { pj_work(); });
   }
   int pj_finish() {
     pj_work();

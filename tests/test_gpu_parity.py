@@ -783,3 +783,58 @@ def test_restricted_gibbs_wide_large_device_draws(hd, oracle, debug):
     assert_same_state(eng, ost)
     assert np.array_equal(eng.rng_state, st)
     eng.close()
+
+
+def test_replica_chains_per_rank_seeds(hd, oracle):
+    # bench.py --gpus N runs one chain per rank with seed 1 + rank (bench.rank_setup) on a
+    # shared data set.  Two engines alive at once on one device, stepped
+    # in alternation, must each follow the oracle's chain for their own seed: no state, stream
+    # or host-pool slot shared between replicas.
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    ds = synth(4000, 32, 6, 3, seed=21)
+    iters = 6
+    kw = dict(m=3, iterations=iters, L=1, c_i=ds.truth, burnin=0, neal8=True, split_merge=False)
+    seeds = [bench.rank_setup(r, 0)["seed"] for r in range(2)]
+    assert seeds == [1, 2]
+    refs = []
+    for s in seeds:
+        st, ref = oracle.run_markov_chain(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w, seed=s, fast=1, **kw)
+        assert st == 0
+        refs.append(ref)
+    assert not np.array_equal(refs[0]["loglikelihood"], refs[1]["loglikelihood"])
+    engs = []
+    for s in seeds:
+        e = make_engine(hd, ds)
+        e.set_seed(s)
+        e.init_chain(e.chain_params(m=3, iterations=iters, L=1, burnin=0, neal8=True, split_merge=False),
+                     c_i=ds.truth)
+        engs.append(e)
+    for it in range(iters):
+        for e, ref in zip(engs, refs):
+            _, ll = e.iteration(it)
+            assert abs(ll - ref["loglikelihood"][it]) <= RTOL * abs(ref["loglikelihood"][it])
+    for e, ref in zip(engs, refs):
+        c, _, _ = e.get_state()
+        assert np.array_equal(c, ref["c_i"][iters - 1])
+        e.close()
+
+
+# N below one wave (N < 64) is a known gap: tools/tiny_probe.py shows
+# log-likelihoods that differ from the oracle's on the same labels there, and a host heap
+# fault with split-merge at N = 2; those shapes stay out of the suite until fixed.
+@pytest.mark.parametrize("shape", [(65, 1, 2, 3), (130, 3, 4, (2, 5)), (100, 1, 1, 2)])
+@pytest.mark.parametrize("m", [1, 3])
+def test_tiny_shapes_chain_matches_oracle(hd, oracle, shape, m):
+    # Edge shapes: a single attribute, a wave plus one point, one auxiliary cluster (m = 1).
+    # Neal-8 and split-merge every iteration.
+    n, d, k, levels = shape
+    ds = synth(n, d, k, levels, seed=40 + n + d)
+    kw = dict(m=m, iterations=5, L=1, c_i=ds.truth, burnin=0, neal8=True, split_merge=True)
+    st, ref = oracle.run_markov_chain(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w, seed=5, fast=1, **kw)
+    assert st == 0
+    res = hd.run_markov_chain(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w, seed=5, **kw)
+    assert np.array_equal(res["total_cls"], ref["total_cls"])
+    assert np.array_equal(res["c_i"], ref["c_i"])
+    np.testing.assert_allclose(res["loglikelihood"], ref["loglikelihood"], rtol=RTOL, atol=0)
