@@ -647,7 +647,7 @@ struct Ctx {
   // carried through the sweep by the move log: at N < 64 the carried tables were seen to
   // disagree with a recount (tools/tiny_probe2.py), and a recount of
   // a few thousand rows costs microseconds.  Debug bit 16 recounts at every size.
-  static constexpr int kTrackMinN = 4096;
+  static constexpr int kTrackMinN = 1024;
   bool recount_only() const { return (debug & 16) || n < kTrackMinN; }
   uint64_t freq_d2h_version = 0;      // labels_version whose freq copy the sweep already started
   DevBuf<int> d_mlog, d_mcount;

@@ -9,7 +9,7 @@ import oracle_ffi as O
 
 if len(sys.argv) == 1:
     import subprocess
-    for n in (1, 2, 3, 4, 7, 16, 33, 64, 65, 200):
+    for n in [int(x) for x in os.environ.get("NS", "1,2,3,4,7,16,33,64,65,200").split(",")]:
         for mode in ("n8", "sm", "both"):
             if mode != "n8" and n < 2:
                 continue
@@ -20,14 +20,14 @@ if len(sys.argv) == 1:
 hd.build()
 n = int(sys.argv[1])
 mode = sys.argv[2]
-for shape in [(n, 3, min(n, 2), 3)]:
+for shape in [(n, int(os.environ.get("D", "3")), min(n, 2), 3)]:
     n, d, k, lv = shape
     ds = hamming_mixture(n, d, k, lv, seed=40 + n + d)
     for m in (1, 3):
         for n8, sm in [{"n8": (True, False), "sm": (False, True), "both": (True, True)}[mode]]:
             kw = dict(m=m, iterations=5, L=1, c_i=ds.truth, burnin=0, neal8=n8, split_merge=sm)
             st, ref = O.run_markov_chain(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w, seed=5, fast=1, **kw)
-            for dbg in (0, 131072):
+            for dbg in [int(x) for x in os.environ.get("DBGS", "0,131072").split(",")]:
                 e = hd.Engine(0)
                 e.set_data(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w)
                 e.set_seed(5)
