@@ -31,7 +31,7 @@ extern "C" {
 #define HDPM_E_VALIDATE  1  /* validate_state failed -> Rcpp::stop in the reference      */
 #define HDPM_E_GSL       2  /* norm_const2 threw (GSL 2F1 overflow)                         */
 #define HDPM_E_PROB      3  /* FixupProb stop(): no positive / non-finite probability      */
-#define HDPM_E_WALKER    4  /* >200 categories: Walker alias sampling not supported        */
+#define HDPM_E_WALKER    4  /* Walker alias table (Rcpp sample, > 200 categories) failed  */
 #define HDPM_E_ARG       5  /* invalid argument or capacity                                 */
 #define HDPM_E_DEVICE    6  /* HIP runtime error                                            */
 #define HDPM_E_NODEVICE  7  /* no usable gfx950 device                                      */

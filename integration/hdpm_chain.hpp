@@ -1,0 +1,110 @@
+// hdpm_chain.hpp -- the body of the reference's Rcpp export run_markov_chain
+// (code/launcher.cpp:6-174) as a sequence of calls into the C ABI (include/hdpm.h), with no
+// R types: launcher_hip.cpp wraps it in the Rcpp signature, tests/cpp/adapter_replay.cpp
+// replays it against the CPU oracle.  Header-only, C++17.
+//
+// Call sequence (one call of the R function):
+//   hdpm_ctx_create -> hdpm_set_data (NumericMatrix -> codes) -> hdpm_rng_set_state
+//   (.Random.seed words 1..625, la: RNGScope entry) -> hdpm_init_chain (la:27-77) ->
+//   hdpm_iteration x (iterations + burnin) * thinning (la:85-154), hdpm_get_state at every
+//   saved iteration (la:140-153) -> hdpm_get_state (final_ass, la:170) -> hdpm_rng_get_state
+//   (the advanced stream back to R) -> hdpm_ctx_destroy.
+#pragma once
+
+#include <chrono>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../include/hdpm.h"
+
+namespace hdpm_adapter {
+
+// la:57-63 results, one entry per saved iteration; centers / sigmas as K x d rows
+struct ChainResult {
+  std::vector<int32_t> total_cls;
+  std::vector<std::vector<int32_t>> c_i;
+  std::vector<std::vector<double>> centers, sigmas;
+  std::vector<double> loglikelihood;
+  std::vector<int32_t> accepted;
+  std::vector<int32_t> final_ass;
+  double time_s = 0.0;
+};
+
+// Owns one context for the duration of a call (destroyed on every exit path).
+class Ctx {
+ public:
+  explicit Ctx(int device) { status_ = hdpm_ctx_create(device, &c_); }
+  ~Ctx() {
+    if (c_) hdpm_ctx_destroy(c_);
+  }
+  Ctx(const Ctx&) = delete;
+  Ctx& operator=(const Ctx&) = delete;
+  hdpm_ctx* get() const { return c_; }
+  int status() const { return status_; }
+
+ private:
+  hdpm_ctx* c_ = nullptr;
+  int status_ = HDPM_OK;
+};
+
+// run_markov_chain (la:6-174).  `data` is the N x D NumericMatrix (column-major doubles,
+// values 1..m_j), `c_i_init` may be null (random init with L labels, la:28-31).
+// `rng_state` holds the 625 words of .Random.seed after the kind word (mti, mt[624]): read
+// on entry, overwritten with the advanced stream on success.  Returns HDPM_OK or the
+// engine's status, with `err` set.
+inline int run_markov_chain(const double* data, int n, int d, const int32_t* attrisize, double gamma, const double* v,
+                            const double* w, const hdpm_chain_params& p, const int32_t* c_i_init,
+                            int32_t* rng_state, ChainResult* out, std::string* err, int device = 0) {
+  Ctx ctx(device);
+  auto fail = [&](int st) {
+    if (err) *err = ctx.get() ? hdpm_last_error(ctx.get()) : "no gfx950 device";
+    return st;
+  };
+  if (ctx.status() != HDPM_OK) return fail(ctx.status());
+  std::vector<uint8_t> codes((size_t)n * d);            // NumericMatrix -> row-major codes
+  for (int i = 0; i < n; i++)
+    for (int j = 0; j < d; j++) codes[(size_t)i * d + j] = (uint8_t)data[(size_t)j * n + i];
+  int st = hdpm_set_data(ctx.get(), codes.data(), n, d, attrisize, gamma, v, w);
+  if (st) return fail(st);
+  if ((st = hdpm_rng_set_state(ctx.get(), rng_state))) return fail(st);
+
+  const auto t0 = std::chrono::steady_clock::now();
+  if ((st = hdpm_init_chain(ctx.get(), &p, c_i_init))) return fail(st);   // la:27-77
+  const int saved = p.iterations;
+  out->total_cls.assign(saved, 0);
+  out->c_i.assign(saved, {});
+  out->centers.assign(saved, {});
+  out->sigmas.assign(saved, {});
+  out->loglikelihood.assign(saved, 0.0);
+  out->accepted.assign(saved, 0);
+  std::vector<int32_t> lab(n);
+  int32_t idx_1_sm = 0;
+  const int total = (p.iterations + p.burnin) * p.thinning;
+  for (int iter = 0; iter < total; ++iter) {                                  // la:85-154
+    int32_t a = 0;
+    double lik = 0.0;
+    if ((st = hdpm_iteration(ctx.get(), &p, iter, &idx_1_sm, &a, &lik))) return fail(st);
+    if (iter >= p.thinning * p.burnin && iter % p.thinning == 0) {          // la:140-153
+      const int at = iter / p.thinning - p.burnin;
+      int32_t K = 0;
+      if ((st = hdpm_get_state(ctx.get(), lab.data(), &K, nullptr, nullptr, 0))) return fail(st);
+      out->centers[at].resize((size_t)K * d);
+      out->sigmas[at].resize((size_t)K * d);
+      if ((st = hdpm_get_state(ctx.get(), lab.data(), &K, out->centers[at].data(), out->sigmas[at].data(), K)))
+        return fail(st);
+      out->total_cls[at] = K;
+      out->c_i[at] = lab;
+      out->loglikelihood[at] = lik;
+      out->accepted[at] = a;
+    }
+  }
+  out->time_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  int32_t K = 0;
+  if ((st = hdpm_get_state(ctx.get(), lab.data(), &K, nullptr, nullptr, 0))) return fail(st);
+  out->final_ass = lab;                                                      // la:170
+  if ((st = hdpm_rng_get_state(ctx.get(), rng_state))) return fail(st);     // the stream back to R
+  return HDPM_OK;
+}
+
+}  // namespace hdpm_adapter

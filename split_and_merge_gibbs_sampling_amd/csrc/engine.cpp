@@ -193,13 +193,16 @@ class HostPool {
       f((int64_t)0, n);
       return;
     }
-    // another context's job still open on the pool (its launch() holds run_mu_ across API
-    // calls): run on the calling thread instead of waiting for it (same thread: deadlock)
-    std::unique_lock<std::mutex> serial(run_mu_, std::try_to_lock);
-    if (!serial.owns_lock()) {
+    // another context's job still open on the pool (its try_launch() holds the pool across
+    // API calls, possibly on this same thread): run on the calling thread instead of waiting
+    if (!acquire()) {
       f((int64_t)0, n);
       return;
     }
+    struct Release {
+      HostPool* p;
+      ~Release() { p->busy_.store(false, std::memory_order_release); }
+    } rel{this};
     quiesce();
     range_ = [&f](int64_t a, int64_t b) { f(a, b); };
     bcast_ = nullptr;
@@ -220,7 +223,7 @@ class HostPool {
   // drains its job alone, which every launched job supports
   template <class F>
   bool try_launch(F&& f) {
-    if (!run_mu_.try_lock()) return false;
+    if (!acquire()) return false;
     quiesce();
     bjob_ = std::forward<F>(f);
     bcast_ = &bjob_;
@@ -233,7 +236,7 @@ class HostPool {
   void join() {
     const int joined = bclaim_.fetch_or(kClosed, std::memory_order_acq_rel) & ~kClosed;
     while (bdone_.load(std::memory_order_acquire) < joined) spin_pause();
-    run_mu_.unlock();
+    busy_.store(false, std::memory_order_release);
   }
 
   void prewake() {
@@ -308,6 +311,12 @@ class HostPool {
   void quiesce() {
     while (active_.load(std::memory_order_acquire) != 0) spin_pause();
   }
+  // The pool is owned by one job at a time: a flag taken by compare-and-swap (not a mutex --
+  // a launched job holds it across API calls and may be joined from another thread).
+  bool acquire() {
+    bool expect = false;
+    return busy_.compare_exchange_strong(expect, true, std::memory_order_acq_rel);
+  }
   void publish() {
     {
       std::lock_guard<std::mutex> lk(mu_);
@@ -363,7 +372,8 @@ class HostPool {
     }
   }
   std::vector<std::thread> th_;
-  std::mutex mu_, run_mu_;
+  std::mutex mu_;
+  std::atomic<bool> busy_{false};
   std::condition_variable cv_;
   std::atomic<uint64_t> gen_{0}, wake_seq_{0};
   static constexpr int kClosed = 1 << 30;
@@ -643,12 +653,11 @@ struct Ctx {
   // takes masked (subset) histograms.
   DevBuf<unsigned> d_freq, d_freq2, d_freq_m;
   bool freq_dev_valid = false;
-  // Below kTrackMinN points the tables are recounted for every update_phi instead of
-  // carried through the sweep by the move log: at N < 64 the carried tables were seen to
-  // disagree with a recount (tools/tiny_probe2.py), and a recount of
-  // a few thousand rows costs microseconds.  Debug bit 16 recounts at every size.
-  static constexpr int kTrackMinN = 1024;
-  bool recount_only() const { return (debug & 16) || n < kTrackMinN; }
+  // Debug bit 4 (value 16) recounts the tables for every update_phi instead of carrying them
+  // through the sweep by the move log (the move log then does not run).  The carried tables
+  // are used at every N: a sweep whose last point opened a cluster used to skip the sweep-end
+  // kernels (kernels.hip sweep_done), which left the tables, and the labels, un-updated.
+  bool recount_only() const { return (debug & 16) != 0; }
   uint64_t freq_d2h_version = 0;      // labels_version whose freq copy the sweep already started
   DevBuf<int> d_mlog, d_mcount;
   PinBuf<unsigned> h_freq;
@@ -1848,7 +1857,7 @@ struct Ctx {
     const int64_t rounds0 = stats.rounds;
     // round 0 may already be on the device (prepare_next_sweep with launch)
     const bool launched_ahead = ahead_launched;
-    const bool track = (launched_ahead || ahead_prefix) ? ahead.track : freq_dev_valid;
+    const bool track = (launched_ahead || ahead_prefix) ? ahead.track : (freq_dev_valid && !recount_only());
     if (!launched_ahead && !ahead_prefix) sweep_buffers(track);
     while (p < n) {
       if (!(launched_ahead && stats.rounds == rounds0)) {
@@ -1897,7 +1906,7 @@ struct Ctx {
       stats.moves += c.moves;
       sweep_moves += c.moves;
       stats.checked_rounds += c.checked;
-      last_unsettled = c.checked || c.restart;
+      last_unsettled = c.checked || (c.restart && c.next < n);
       if (c.status) {
         err = c.status == kValidate ? "State validation failed: inconsistent cluster count from Neal8 case 2"
               : c.status == kWalker ? "Walker alias table failure"
@@ -1923,6 +1932,8 @@ struct Ctx {
         std::swap(d_freq.n, d_freq2.n);
         freq_d2h_version = labels_version;
         freq_next_pending = true;    // into h_freq_next; update_phi swaps it in
+      } else {
+        freq_dev_valid = false;      // not carried: the next update_phi recounts
       }
     } else if (track && freq_before_ok) {
       // nothing moved: the host's tables are still current

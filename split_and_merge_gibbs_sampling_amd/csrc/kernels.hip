@@ -2246,10 +2246,12 @@ __global__ __launch_bounds__(kWave) void k_resolve_blk(ResolveArgs a) {
 
 // ------------------------------------------------------------------ end of sweep
 // The sweep-end kernels are enqueued behind every resolver launch and read its control
-// block: they act only when that launch finished the sweep (no restart pending), so the
-// host need not wait for the resolver before issuing them.
+// block: they act only when that launch finished the sweep, so the host need not wait for
+// the resolver before issuing them.  A launch whose last point opened a cluster (case 3 /
+// case 4 set `restart` with next = i + 1) has finished it too when i is the last point:
+// `next >= n` alone decides (every restart that leaves work sets next < n).
 __device__ __forceinline__ bool sweep_done(const ResolveCtl* ctl, int n) {
-  return ctl->status == 0 && ctl->restart == 0 && ctl->next >= n;
+  return ctl->status == 0 && ctl->next >= n;
 }
 
 __global__ void k_relabel(int* c, const int* label_of_slot, int n, const ResolveCtl* ctl) {

@@ -616,6 +616,11 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
   *accepted = 0;
   HState st;
   ctx_to_hstate(this, st);
+  // every host index below is a label < K (the state's arrays are K x d): refuse a state
+  // that breaks this rather than write outside them
+  for (int x : st.c)
+    if (x < 0 || x >= st.K) { err = "State validation failed: label outside 0..K-1"; return kValidate; }
+  if (n < 2) { err = "split_and_merge needs at least two observations"; return kArg; }
   // sm:263-301 select_observations_random: sample(0..n-1, 2, FALSE)
   int i1, i2;
   {

@@ -14,7 +14,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-ZOO_PATH = os.path.join(os.path.dirname(_HERE), "tests", "golden", "zoo.data")
+# the UCI Zoo data the reference ships (data/zoo.data), kept as package data
+ZOO_PATH = os.path.join(_HERE, "datasets", "zoo.data")
 
 
 @dataclasses.dataclass

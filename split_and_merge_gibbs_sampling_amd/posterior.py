@@ -27,7 +27,10 @@ from ._lib import ptr
 
 class PSM:
     """comp.psm(C) on the device: ``c_trace`` is the M x N matrix of saved labels
-    (results$c_i, 0-based, < 255).  Rows come back as doubles (count / M)."""
+    (results$c_i, any integers).  The PSM depends only on which points share a label within
+    an iteration, so each saved row is relabelled 0..K_m-1 first (the device packs one byte
+    per label: at most 255 clusters in one iteration, else ValueError).  Rows come back as
+    doubles (count / M)."""
 
     def __init__(self, c_trace, engine=None, device: int = 0):
         from .sampler import Engine
@@ -35,6 +38,12 @@ class PSM:
         if tr.ndim != 2:
             raise ValueError("c_trace must be M x N")
         self.M, self.N = tr.shape
+        dense = np.empty_like(tr)
+        for q in range(self.M):
+            u, dense[q] = np.unique(tr[q], return_inverse=True)
+            if u.size > 255:
+                raise ValueError(f"iteration {q} has {u.size} clusters; the device PSM packs at most 255")
+        tr = np.ascontiguousarray(dense, dtype=np.int32)
         self._own = engine is None
         self.eng = Engine(device) if engine is None else engine
         self.eng._check(self.eng._L.hdpm_psm_build(self.eng._h, ptr(tr), self.M, self.N))

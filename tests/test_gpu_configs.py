@@ -164,3 +164,49 @@ def test_c5_full_size_random20_start(hd, oracle):
     neal8_steps(eng, oracle, ds, ost, rng, pc, ps, sweeps=2)
     assert eng.stats()["moves"] > 100_000
     eng.close()
+
+
+@pytest.mark.timeout(1200)
+@pytest.mark.parametrize("name,warm,timed", [("c5", 5, 25), ("c3", 5, 25), ("c4", 3, 25)])
+def test_bench_path_iterations_api(hd, oracle, name, warm, timed):
+    """The path bench.py times (bench.py main: hdpm_iterations for the warmup, synchronize,
+    reset_stats, hdpm_iterations for the timed window) at the full BASELINE size, against
+    the oracle's chain (la:94-132: sweep, update_phi, compute_loglikelihood per iteration,
+    fast = 2).  Between two batches the next sweep stays prepared on the device (its prepass
+    started at the end of the first batch, kRoundPrefix), and every iteration but the last of
+    a batch launches the next sweep before its host work is done -- the pipelined code is
+    what is compared here, not the one-call-per-step API.  The chain starts at iteration 1
+    (iteration 0 regenerates the latent pool, la:123; the device pool generator has its own
+    bit-exact tests), so the oracle reads the engine's pool once.  Per-iteration
+    log-likelihoods, then labels, K, centers, sigmas and the 625-word stream after the timed
+    batch, and again after a short batch that follows a get_state (which drops the prepared
+    sweep) -- as launcher.cpp:85-132 would leave them."""
+    ds, eng, ost, rng, pc, ps = start(hd, oracle, name, seed=11)
+    params = eng.chain_params(m=3, iterations=warm + timed + 3, L=0, burnin=0, neal8=True, split_merge=False)
+    eng._params = params
+
+    def oracle_iters(it0, count):
+        out = []
+        for _ in range(count):
+            assert oracle.neal8_sweep(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w, ost, 3, pc, ps, rng, fast=2) == 0
+            assert oracle.update_phi(ds.codes, ds.attrisize, ds.v, ds.w, ost, rng) == 0
+            out.append(oracle.compute_loglikelihood(ds.codes, ds.attrisize, ost, fast=2))
+        return np.array(out)
+
+    it = 1
+    _, ll = eng.iterations(it, warm)
+    it += warm
+    eng.synchronize()
+    eng.reset_stats()
+    np.testing.assert_allclose(ll, oracle_iters(it - warm, warm), rtol=RTOL, atol=0)
+    _, ll = eng.iterations(it, timed)
+    it += timed
+    eng.synchronize()
+    st = eng.stats()
+    assert st["sweeps"] == timed
+    np.testing.assert_allclose(ll, oracle_iters(it - timed, timed), rtol=RTOL, atol=0)
+    same(eng, ost, rng, "after the timed batch")
+    _, ll = eng.iterations(it, 3)
+    np.testing.assert_allclose(ll, oracle_iters(it, 3), rtol=RTOL, atol=0)
+    same(eng, ost, rng, "after a batch that follows get_state")
+    eng.close()

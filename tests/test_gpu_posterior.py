@@ -90,3 +90,16 @@ def test_psm_c4_size(hd):
     v = p.vi_lb(np.stack([truth, tr[0]]))
     assert np.all(np.isfinite(v)) and v[0] < v[1] + 1.0
     p.close()
+
+
+def test_psm_any_label_values_and_too_many_clusters(hd):
+    # labels >= 255 (e.g. a trace relabelled by the caller) are compacted per iteration;
+    # an iteration with more than 255 clusters is refused loudly, never aliased
+    from split_and_merge_gibbs_sampling_amd.posterior import PSM
+    rng = np.random.default_rng(7)
+    tr = rng.integers(0, 9, size=(11, 400)).astype(np.int32)
+    p = PSM(tr * 1000 + 300)
+    assert np.array_equal(p.matrix(), psm_ref(tr))
+    p.close()
+    with pytest.raises(ValueError):
+        PSM(np.arange(300, dtype=np.int32)[None, :])
