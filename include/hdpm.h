@@ -67,6 +67,10 @@ typedef struct {
      * on the device (upload + kernels + wait), update_phi draws, acceptance terms */
     int64_t sm_moves;
     double  t_sm_ms, t_sm_scan_ms, t_sm_phi_ms, t_sm_terms_ms;
+    /* update_phi on the device (csrc/phi.hip): updates committed there, and updates it
+     * handed back to the host (a case it does not restate: Walker, rhig's bisection path, a
+     * drift outside its window, ...); the status of the last one (PhiStatus, 0 = ok) */
+    int64_t phi_device_calls, phi_device_fallbacks, phi_device_last_status;
 } hdpm_stats;
 
 int         hdpm_device_count(void);
@@ -165,7 +169,8 @@ int hdpm_reset_stats(hdpm_ctx* ctx);
  * restricted scans of >= 4096 points draw their uniforms on the host (not from the device
  * generator windows); bit 17: a sweep prepared at the end of hdpm_iterations does not start
  * its prepass on the device; bit 18: the prepass certifies "stay" by the margin only (not by
- * the draw's uniform, kernels.hip stay_by_uniform). */
+ * the draw's uniform, kernels.hip stay_by_uniform); bit 19: update_phi on the host (the job
+ * speculated during the sweep) instead of the device (csrc/phi.hip; also HDPM_PHI=host). */
 int hdpm_set_debug(hdpm_ctx* ctx, int32_t mode);
 /* The prepass's pool-entry heads, P entries of wb*Ws + 2 words padded to a power of two
  * (Ws <= 4) or to a multiple of 8 words (wide layouts) (csrc/kernels.hpp "Pool-entry heads",
@@ -180,6 +185,12 @@ int hdpm_get_pool_heads(hdpm_ctx* ctx, uint64_t* out, int64_t P);
  * finite within 30000 terms the values are bit-identical.  Default 0 (reference
  * semantics). */
 #define HDPM_OPT_HIG_LOGSPACE 1
+/* HDPM_OPT_PHI_DEVICE (value != 0): update_phi runs on the device (csrc/phi.hip: center
+ * draws, rhig's beta-path sigma draws resolved by speculative parallel walks over
+ * acceptance masks, tables and bound records) instead of the host job speculated during the
+ * sweep; cases the device does not restate fall back to the host.  Same chain either way.
+ * Default 0 (or HDPM_PHI=device in the environment). */
+#define HDPM_OPT_PHI_DEVICE 2
 int hdpm_set_option(hdpm_ctx* ctx, int32_t option, double value);
 /* Posterior analysis (realdata_analysis/zoo_simulator.R:193-236, 339-344; mcclust /
  * mcclust.ext).  hdpm_psm_build: the posterior similarity matrix of M saved label vectors

@@ -31,6 +31,7 @@ EXPORTS = (
 )
 
 OPT_HIG_LOGSPACE = 1
+OPT_PHI_DEVICE = 2
 
 STATUS = {0: "OK", 1: "E_VALIDATE", 2: "E_GSL", 3: "E_PROB", 4: "E_WALKER", 5: "E_ARG",
           6: "E_DEVICE", 7: "E_NODEVICE"}
@@ -59,7 +60,8 @@ class Stats(C.Structure):
             "t_pool_ms", "t_pool_mt_ms", "t_pool_accept_ms", "t_pool_parse_ms", "t_pool_values_ms")] + \
         [(n, C.c_int64) for n in ("phi_spec_runs", "phi_spec_clusters", "prepass_timed", "prepass_timed_points",
                                   "rng_windows", "rng_windows_fresh", "listed_points", "sm_moves")] + \
-        [(n, C.c_double) for n in ("t_sm_ms", "t_sm_scan_ms", "t_sm_phi_ms", "t_sm_terms_ms")]
+        [(n, C.c_double) for n in ("t_sm_ms", "t_sm_scan_ms", "t_sm_phi_ms", "t_sm_terms_ms")] + \
+        [(n, C.c_int64) for n in ("phi_device_calls", "phi_device_fallbacks", "phi_device_last_status")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -47,7 +47,9 @@ hipError_t launch_freq_gather(const unsigned int* freq, const int* sol, int Kmax
                               const ResolveCtl* ctl, int n, hipStream_t s);
 hipError_t launch_scatter_clusters(const uint8_t* stage, int nent, int dp, int d, int bw, int full, uint8_t* codes,
                                    double* tab, uint64_t* bnd, int* counts, int* sol, int* los, int* src,
-                                   hipStream_t s);
+                                   hipStream_t s, const int* gate = nullptr);
+hipError_t launch_phi_locate(const PipeArgs& a, hipStream_t s);
+hipError_t launch_pipe_check(const PipeArgs& a, hipStream_t s);
 hipError_t launch_pool_heads(const double* tab, const uint64_t* bnd, int64_t P, int d, int wb, int Ws, int bw, int ha,
                              int hb, uint64_t* head, hipStream_t s);
 hipError_t launch_hist(const HistArgs& a, hipStream_t s);
@@ -61,6 +63,9 @@ hipError_t launch_debug_draw(const double* logw, int E, double rU, int two_way, 
 hipError_t launch_debug_math(const double* x, int64_t n, int fn, int ocml, double* out, hipStream_t s);
 hipError_t launch_lmatrix(const uint8_t* codes_t, int n, int d, int nq, ParamTables cl, int K, double* L,
                           int* H, int64_t ldL, hipStream_t s);
+hipError_t launch_phi(const PhiArgs& a, hipStream_t s);
+size_t phi_cwalk_lds(int d, int nw, int wpb);
+size_t phi_values_lds(int d, int nw);
 int sm_restricted_gibbs_device(struct Ctx* c, const int32_t* S, int32_t nS, int32_t i1, int32_t i2,
                                int32_t t);
 
@@ -1221,6 +1226,8 @@ struct Ctx {
     }
     n = n_; d = d_; nq = (d + 15) / 16; dp = nq * 16; gamma = g;
     pg.planned = false;
+    phd.ready = false;
+    dev_ll_version = 0;
     att.assign(attr, attr + d);
     v.assign(vv, vv + d);
     w.assign(ww, ww + d);
@@ -1618,6 +1625,8 @@ struct Ctx {
     const int E = K + m;
     const double T = 54.0 * M_LN2 + std::log((double)E) + 0.5;
     PrepassArgs pa;
+    pa.gate = nullptr;
+    pa.raw_ptr = nullptr;
     pa.codes_t = d_codes_t.p; pa.n = n; pa.d = d; pa.nq = nq;
     pa.c = d_c.p; pa.counts = d_counts.p; pa.slot_of_label = d_sol.p; pa.K = K; pa.S = S;
     pa.slots = ParamTables{d_slot_codes.p, d_slot_tab.p};
@@ -1663,6 +1672,9 @@ struct Ctx {
     }
 
     ResolveArgs ra;
+    ra.gate = nullptr;
+    ra.raw_ptr = nullptr;
+    ra.dry = 0;
     ra.n = n; ra.d = d; ra.dp = dp; ra.m = m; ra.P = P;
     ra.c = d_c.p; ra.counts = d_counts.p; ra.slot_of_label = d_sol.p; ra.label_of_slot = d_los.p;
     ra.slot_src = d_src.p; ra.slot_codes = d_slot_codes.p; ra.slot_tab = d_slot_tab.p;
@@ -1754,7 +1766,7 @@ struct Ctx {
     // longer path (timeline: launching the sweep first cost ~8% of the iteration rate);
     // debug bit 15 launches the sweep first
     const bool sweep_first = (debug & 32768) != 0;
-    if (!sweep_first) {
+    if (!sweep_first && host_spec()) {
       spec_launch();
       mark("ahead.spec");
     }
@@ -1772,7 +1784,7 @@ struct Ctx {
         if (launch_round(0, K, m, ahead.raw, ahead.track, kRoundPrefix) == kOk) ahead.prefix = true;
       }
     }
-    if (sweep_first) {
+    if (sweep_first && host_spec()) {
       spec_launch();
       mark("ahead.spec");
     }
@@ -1820,7 +1832,8 @@ struct Ctx {
     if (tables_dirty) upload_clusters();
     // update_phi can be speculated during the sweep when the host holds the pre-sweep
     // frequency tables of every label and the sweep carries them (move log)
-    const bool spec_go = freq_dev_valid && freq_version == labels_version && !(debug & 128) && !recount_only();
+    const bool spec_go = freq_dev_valid && freq_version == labels_version && !(debug & 128) && !recount_only() &&
+                         host_spec();
     const bool freq_before_ok = freq_version == labels_version && !recount_only();
     if (!use_ahead) spec.ran = false;
     spec.lv = 0;
@@ -2578,6 +2591,253 @@ struct Ctx {
     stats.phi_spec_runs++;
   }
 
+  // ------------------------------------------------------------------ update_phi on the device
+  // csrc/phi.hip.  Static per-data arrays (m_j, their prefix sums, v, w, glibc tables), the
+  // cluster descriptors and current sigmas of the update, scratch, and the outputs copied
+  // back (status, centers, sigmas, log-likelihood terms).
+  struct PhiDevice {
+    bool ready = false;
+    int sumatt = 0;
+    DevBuf<int32_t> att, aoff;
+    DevBuf<double> v, w;
+    DevBuf<uint64_t> gtab;
+    DevBuf<int> lab_cnt;               // [T] labels then [T] counts
+    DevBuf<double> sig_in, sig_out, ll, cum;
+    DevBuf<uint8_t> perm, det, pick, stage;
+    DevBuf<PhiCand> cand;
+    DevBuf<int> act, status;
+    DevBuf<uint64_t> mask, maskd;
+    DevBuf<uint8_t> ikind;
+    DevBuf<int64_t> apos, dts;
+    DevBuf<double> lg, lzz;
+    DevBuf<int> F;
+    PinBuf<uint8_t> h_in, h_out;
+    double p_rej = 0.12;               // rbeta attempts rejected (window model), adapted per call
+    int64_t calls = 0, fallbacks = 0;
+    int last_status = 0;
+  } phd;
+  // update_phi placement: the host job speculated during the sweep (default), or the device
+  // (phi.hip, after the sweep): HDPM_OPT_PHI_DEVICE, or HDPM_PHI=device in the environment;
+  // debug bit 19 (value 524288) forces the host.
+  int phi_mode = [] {
+    const char* e = std::getenv("HDPM_PHI");
+    return e && std::strcmp(e, "device") == 0 ? 1 : 0;
+  }();
+  bool host_spec() const { return phi_mode == 0 || (debug & 524288); }
+  double dev_ll = 0.0;                 // compute_loglikelihood from the last full device update
+  uint64_t dev_ll_version = 0;         // labels_version it belongs to (0: none)
+
+  void phi_device_setup() {
+    if (phd.ready) return;
+    std::vector<int32_t> off(d + 1, 0);
+    for (int j = 0; j < d; ++j) off[j + 1] = off[j] + att[j];
+    phd.sumatt = off[d];
+    phd.att.ensure(d);
+    phd.aoff.ensure(d + 1);
+    phd.v.ensure(d);
+    phd.w.ensure(d);
+    phd.gtab.ensure(512);
+    HIPCHK(hipMemcpy(phd.att.p, att.data(), (size_t)d * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(phd.aoff.p, off.data(), (size_t)(d + 1) * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(phd.v.p, v.data(), (size_t)d * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(phd.w.p, w.data(), (size_t)d * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(phd.gtab.p, glibc::kGlibcExpTab, 256 * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(phd.gtab.p + 256, glibc::kGlibcLogTab, 256 * 8, hipMemcpyHostToDevice));
+    phd.ready = true;
+  }
+
+  // The window holding [pos, pos + n) and able to hand the host its state after it.
+  RngWindow* window_at(uint64_t pos, int64_t n) {
+    RngWindow* W = nullptr;
+    for (auto& w_ : win)
+      if (covers(w_, pos, n) && (!W || w_.start_pos < W->start_pos)) W = &w_;
+    return W;
+  }
+  bool can_adopt(const RngWindow& W, uint64_t target) const {
+    const uint64_t r = target - W.start_pos;
+    const uint64_t head = W.mti0 >= 624 ? 0 : 624 - W.mti0;
+    if (r < head) return true;
+    const uint64_t b = 1 + (r - head) / 624, k = (r - head) % 624;
+    const int64_t blk = (int64_t)(k == 0 ? b - 1 : b);
+    return blk == 0 || blk >= W.export_from;
+  }
+
+  // update_phi (cf:511-591) of the labels in mask on the device.  Returns kOk when committed
+  // (new centers / sigmas in h_center / h_sigma and in the device tables, the host stream
+  // past the update's draws), -1 when the device path does not apply or met a case it
+  // leaves to the host (nothing changed: same stream position, same tables).
+  // Sizes of a device update of T clusters (phi.hip): drift windows (kernels.hpp phi_lo /
+  // phi_hi, from the rate and spread of the extra uniforms per sigma draw), mask words per
+  // candidate, start drifts walked per cluster, stream words read, walk workgroup shape.
+  struct PhiPlan {
+    bool ok = false;
+    int T = 0, nw = 0, Wc = 0, wpb = 0, groups = 0;
+    int64_t items = 0, need = 0;
+    double rate = 0, sdev = 0;
+  };
+  PhiPlan phi_plan(int T) const {
+    PhiPlan pl;
+    if (T <= 0 || d > 2048) return pl;
+    pl.T = T;
+    const double p = phd.p_rej;
+    pl.rate = 2 * p / (1 - p);
+    pl.sdev = 2 * std::sqrt(p) / (1 - p);
+    pl.items = (int64_t)T * d;
+    const int64_t klast = pl.items - 1, tl = (int64_t)(T - 1) * d;
+    pl.nw = (int)((phi_hi(klast, pl.rate, pl.sdev) - phi_lo(klast, pl.rate, pl.sdev) + 63) / 64) + 3;
+    pl.Wc = (int)(phi_hi(tl, pl.rate, pl.sdev) - phi_lo(tl, pl.rate, pl.sdev)) + 2;
+    pl.need = 3 * pl.items + phi_hi(pl.items, pl.rate, pl.sdev) + 256;
+    // LDS of the walks: the cluster image (d nw mask words) with the per-wave pick rows;
+    // 16 waves per workgroup while that fits, fewer otherwise
+    int wpb = 16;
+    while (wpb > 1 && (phi_cwalk_lds(d, pl.nw, wpb) > 150 * 1024 || phi_values_lds(d, pl.nw) > 150 * 1024)) wpb /= 2;
+    if (phi_cwalk_lds(d, pl.nw, wpb) > 150 * 1024 || phi_values_lds(d, pl.nw) > 150 * 1024) return pl;
+    pl.wpb = wpb;
+    // workgroups per cluster: about two start drifts per wave, at least a workgroup per CU overall
+    pl.groups = std::max(1, std::min((pl.Wc + 2 * wpb - 1) / (2 * wpb), (256 + T - 1) / T * 2));
+    pl.ok = true;
+    return pl;
+  }
+  // scratch of a plan, and the arguments every call shares (the caller sets raw, labels /
+  // counts, freq, sigmas in and out, outputs)
+  PhiArgs phi_args(const PhiPlan& pl) {
+    phi_device_setup();
+    const int T = pl.T;
+    const int64_t items = pl.items, cap = (int64_t)T * phd.sumatt;
+    phd.cum.ensure((size_t)T * phd.sumatt);
+    phd.perm.ensure((size_t)T * phd.sumatt);
+    phd.cand.ensure((size_t)T * phd.sumatt);
+    phd.det.ensure(items);
+    phd.apos.ensure(items);
+    phd.act.ensure(1 + 2 * cap);
+    phd.mask.ensure((size_t)cap * pl.nw);
+    phd.maskd.ensure((size_t)items * pl.nw);
+    phd.ikind.ensure(items);
+    phd.lg.ensure(pl.need);
+    phd.lzz.ensure(pl.need);
+    phd.F.ensure((size_t)T * pl.Wc);
+    phd.dts.ensure(T);
+    PhiArgs a{};
+    a.T = T; a.d = d; a.dp = dp; a.mmax = mmax; a.sumatt = phd.sumatt; a.wb = wb; a.Ws = Ws; a.bw = bw;
+    a.att = phd.att.p; a.aoff = phd.aoff.p; a.v = phd.v.p; a.w = phd.w.p; a.gtab = phd.gtab.p;
+    a.cum = phd.cum.p; a.perm = phd.perm.p; a.det = phd.det.p; a.cand = phd.cand.p;
+    a.act = phd.act.p; a.nact_cap = cap; a.mask = phd.mask.p; a.nw = pl.nw; a.rate = pl.rate; a.sdev = pl.sdev;
+    a.apos = phd.apos.p;
+    a.lg = phd.lg.p; a.lzz = phd.lzz.p; a.span = pl.need - 1; a.F = phd.F.p; a.Wc = pl.Wc; a.dts = phd.dts.p;
+    a.maskd = phd.maskd.p; a.ikind = phd.ikind.p; a.wpb = pl.wpb; a.groups = pl.groups;
+    a.raw_ptr = nullptr; a.gate = nullptr; a.pos_in = nullptr; a.pos_out = nullptr; a.sweep_len = 0;
+    a.slot_of = nullptr;
+    return a;
+  }
+
+  int device_update_phi(const std::vector<unsigned char>& mask, int nidx) {
+    if (phi_mode == 0 || (debug & (524288 | 64))) return -1;   // bit 19: host update_phi; bit 6: host pools
+    if (!glibc_selfcheck() || d > 2048) return -1;
+    std::vector<int> touched;
+    for (int k = 0; k < K; ++k)
+      if (mask[k] && h_counts[k] != 0) touched.push_back(k);
+    const int T = (int)touched.size();
+    if (T == 0) return -1;
+    const bool full = tables_dirty || T == K;
+    if (full && T != K) return -1;                        // untouched labels need the host's tables
+    rng_sync();
+    const PhiPlan pl = phi_plan(T);
+    if (!pl.ok) return -1;
+    const int64_t items = pl.items, need = pl.need;
+    RngWindow* W = window_at(rng.pos, need);
+    if (!W) return -1;
+    PhiArgs a = phi_args(pl);
+    auto tp0 = std::chrono::steady_clock::now();
+    histogram_launch(nidx == 0 ? nullptr : &mask);
+    const unsigned* fsrc = nidx == 0 ? d_freq.p : d_freq_m.p;
+    // inputs: labels, counts, current sigmas
+    const size_t in_bytes = (size_t)2 * T * 4 + (size_t)items * 8;
+    phd.h_in.ensure(in_bytes + 64);
+    int* hl = (int*)phd.h_in.p;
+    double* hs = (double*)(phd.h_in.p + align16((size_t)2 * T * 4));
+    for (int t = 0; t < T; ++t) {
+      hl[t] = touched[t];
+      hl[T + t] = h_counts[touched[t]];
+      std::memcpy(hs + (size_t)t * d, &h_sigma[(size_t)touched[t] * d], (size_t)d * 8);
+    }
+    phd.lab_cnt.ensure(2 * T);
+    phd.sig_in.ensure(items);
+    phd.sig_out.ensure(items);
+    phd.ll.ensure(2 * T);
+    phd.pick.ensure(items);
+    phd.status.ensure(4);
+    const UploadLayout L = upload_layout(T, dp, d, bw);
+    phd.stage.ensure(L.bytes);
+    HIPCHK(hipMemcpyAsync(phd.lab_cnt.p, hl, (size_t)2 * T * 4, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(phd.sig_in.p, hs, (size_t)items * 8, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemsetAsync(phd.status.p, 0, 16, stream));
+    HIPCHK(hipMemsetAsync(phd.act.p, 0, 4, stream));
+    HIPCHK(hipStreamWaitEvent(stream, W->done, 0));
+    a.lab = phd.lab_cnt.p; a.cnt = phd.lab_cnt.p + T; a.freq = fsrc; a.sig_in = phd.sig_in.p;
+    a.raw = W->raw.p + (rng.pos - W->start_pos);
+    a.nraw = (int64_t)(W->start_pos + (uint64_t)W->count - rng.pos);
+    a.pick = phd.pick.p; a.status = phd.status.p;
+    a.stage = phd.stage.p; a.sig_out = phd.sig_out.p; a.ll = phd.ll.p;
+    HIPCHK(launch_phi(a, stream));
+    // results: status + consumption, picks, sigmas, log-likelihood terms
+    const size_t o_pick = 16, o_sig = align16(o_pick + (size_t)items), o_ll = o_sig + (size_t)items * 8;
+    phd.h_out.ensure(o_ll + (size_t)2 * T * 8);
+    HIPCHK(hipMemcpyAsync(phd.h_out.p, phd.status.p, 16, hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipMemcpyAsync(phd.h_out.p + o_pick, phd.pick.p, (size_t)items, hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipMemcpyAsync(phd.h_out.p + o_sig, phd.sig_out.p, (size_t)items * 8, hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipMemcpyAsync(phd.h_out.p + o_ll, phd.ll.p, (size_t)2 * T * 8, hipMemcpyDeviceToHost, stream));
+    histogram_wait(nidx == 0 ? nullptr : &mask);
+    if (freq_next_pending) {
+      std::swap(h_freq.p, h_freq_next.p);
+      std::swap(h_freq.n, h_freq_next.n);
+      freq_next_pending = false;
+    }
+    phd.calls++;
+    const int status = ((const int*)phd.h_out.p)[0];
+    stats.phi_device_last_status = status;
+    int64_t cons = 0;
+    std::memcpy(&cons, phd.h_out.p + 8, 8);
+    phd.last_status = status;
+    const uint64_t target = rng.pos + (uint64_t)cons;
+    if (status != kPhiOk || cons <= 0 || !can_adopt(*W, target)) {
+      phd.fallbacks++;
+      stats.phi_device_fallbacks++;
+      if (status == kPhiOk) stats.phi_device_last_status = -1;
+      return -1;
+    }
+    stats.phi_device_calls++;
+    // commit: tables on the device, parameters on the host, the stream past the draws
+    HIPCHK(launch_scatter_clusters(phd.stage.p, T, dp, d, bw, full ? 1 : 0, d_slot_codes.p, d_slot_tab.p, d_slot_bnd.p,
+                                   d_counts.p, d_sol.p, d_los.p, d_src.p, stream));
+    const uint8_t* pk = phd.h_out.p + o_pick;
+    const double* sg = (const double*)(phd.h_out.p + o_sig);
+    const double* ll = (const double*)(phd.h_out.p + o_ll);
+    double hi = 0.0, lo = 0.0;
+    for (int t = 0; t < T; ++t) {
+      const int k = touched[t];
+      for (int j = 0; j < d; ++j) h_center[(size_t)k * d + j] = (uint8_t)(pk[(size_t)t * d + j] + 1);
+      std::memcpy(&h_sigma[(size_t)k * d], sg + (size_t)t * d, (size_t)d * 8);
+      for (int q = 0; q < 2; ++q) {
+        const double x = ll[2 * t + q], s = hi + x;
+        lo += std::fabs(hi) >= std::fabs(x) ? (hi - s) + x : (x - s) + hi;
+        hi = s;
+      }
+    }
+    if (full) {
+      dev_ll = hi + lo;
+      dev_ll_version = labels_version;
+      tables_dirty = false;
+    }
+    stage_full = false;                // the host staging no longer mirrors the device tables
+    adopt_state_at(*W, target);
+    // the drift model follows the chain: extra uniforms per sigma draw seen here
+    const double drift = (double)(cons - 3 * items);
+    const double ph = drift / (drift + 2.0 * (double)items);
+    phd.p_rej = std::min(0.3, std::max(0.05, 0.7 * phd.p_rej + 0.3 * ph));
+    stats.t_host_phi_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp0).count();
+    return kOk;
+  }
+
   int update_phi(const int32_t* idx, int nidx) {
     if (!have_state) { err = "no state"; return kArg; }
     HostPool& pool = HostPool::get();
@@ -2592,6 +2852,11 @@ struct Ctx {
                           spec.pos == rng.pos && spec.epoch == rng.epoch && sa.n > 0 && sa.start.pos == rng.pos &&
                           !(debug & 128);
     spec.ran = false;
+    if (!use_spec) {
+      // the update on the device (csrc/phi.hip); -1: not applicable here, the host runs it
+      const int st = device_update_phi(mask, nidx);
+      if (st >= 0) return st;
+    }
     int t0 = 0;
     if (use_spec && spec.moves == 0 && K == spec.K) {
       // nothing moved: the frequency tables are the pre-sweep ones (the sweep's copy-out,
@@ -2686,6 +2951,11 @@ struct Ctx {
   // ------------------------------------------------------------------ loglik
   int compute_loglikelihood(double* out) {
     if (!have_state) { err = "no state"; return kArg; }
+    if (dev_ll_version == labels_version && !tables_dirty && !(debug & 4)) {
+      // the full device update_phi of these labels summed the regrouped terms (phi.hip)
+      *out = dev_ll;
+      return kOk;
+    }
     if (tables_dirty) upload_clusters();
     if (freq_version == labels_version && stage_full && !(debug & 4)) {
       // the labels have not moved since the last full histogram: the sum over points
@@ -3179,6 +3449,10 @@ int hdpm_set_option(hdpm_ctx* h, int32_t option, double value) {
   switch (option) {
     case HDPM_OPT_HIG_LOGSPACE:
       ctx->hig_log = value != 0.0;
+      return HDPM_OK;
+    case HDPM_OPT_PHI_DEVICE:
+      GUARD(ctx->cancel_ahead();)
+      ctx->phi_mode = value != 0.0 ? 1 : 0;
       return HDPM_OK;
     default:
       ctx->err = "unknown option";

@@ -271,6 +271,7 @@ __device__ __forceinline__ int penalty_r(const uint64_t (&M)[WS], const uint64_t
 // per label instead of the label -> slot -> record / count -> logn chain):
 // csum[l] = [record of slot_of_label[l] (bw words), logn[count], slot].
 __global__ void k_cluster_summary(PrepassArgs a) {
+  if (!pipe_gate(a)) return;
   if (a.zero && blockIdx.x == 0 && threadIdx.x == 0) *a.zero = 0;   // a memset dispatch less per sweep
   const int sw = a.bw + 2;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < a.K * sw; e += gridDim.x * blockDim.x) {
@@ -324,6 +325,7 @@ __device__ __forceinline__ double latent_ub_head(const PrepassArgs& a, const uin
 
 template <int WB, int WS, bool HEAD>
 __global__ __launch_bounds__(kBlock) void k_prepass(PrepassArgs a) {
+  if (!pipe_gate(a)) return;
   constexpr int WR = WB * WS;                  // row words
   constexpr int RW = (WB + kQ) * WS + 4;       // record words
   constexpr int SC = (WB + kQ) * WS;           // record scalars: A, delta, dmin, scale
@@ -410,6 +412,7 @@ __global__ __launch_bounds__(kBlock) void k_prepass(PrepassArgs a) {
 // Generic width (planes wider than 4 words, or wide codes): rows and records read from
 // memory as needed.
 __global__ __launch_bounds__(kBlock) void k_prepass_generic(PrepassArgs a) {
+  if (!pipe_gate(a)) return;
   const int tid = threadIdx.x;
   const int64_t i = (int64_t)a.p0 + (int64_t)blockIdx.x * kBlock + tid;
   const bool active = i < a.n;
@@ -539,6 +542,7 @@ bool prepass_wide_offsets_fit(const PrepassArgs& a) {
 
 template <int WB, int NW, bool CL>
 __global__ __launch_bounds__(kWideThreads) void k_prepass_wide(PrepassArgs a, int nchunks) {
+  if (!pipe_gate(a)) return;
   extern __shared__ uint64_t s_dyn[];
   __shared__ double s_mg[2][kWideChunk];
   __shared__ int s_oc[2][kWideChunk];
@@ -1462,6 +1466,7 @@ __device__ void exact_rows_point(const PrepassArgs& a, int q, int row, double* l
 // certain costs one small grid of early exits, not one workgroup per prepass block.
 constexpr int kExactWaves = 4;
 __global__ __launch_bounds__(kWave * kExactWaves) void k_exact_rows(PrepassArgs a) {
+  if (!pipe_gate(a)) return;
   const int total = *a.dense_total;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int q0 = blockIdx.x * kExactWaves + wv;
@@ -1557,6 +1562,7 @@ __device__ int exact_dense_row(const PrepassArgs& a, const int* s_off, int q) {
 
 template <int RE>
 __global__ __launch_bounds__(kExactWgThreads) void k_exact_rows_wg(PrepassArgs a) {
+  if (!pipe_gate(a)) return;
   __shared__ int s_off[kExactWgThreads + 1];
   const int total = exact_dense_scan(a, s_off);
   if ((int)blockIdx.x >= total) return;
@@ -1664,7 +1670,11 @@ __device__ __forceinline__ bool RCtx::process(int64_t i, int row, int own, uint3
   if (prof && lane == 0) S.tsub[4] += wall_clock64() - tq0;
   if (lane == 0) {
     if (!use_spec) S.exact++;
-    if (pick < 0) { S.status = -pick; S.next = (int)i; }
+    // a pipelined sweep stops before its first decision that is not "stay" (nothing changed)
+    const bool stay = pick >= 0 && ((pick < K && st.cnt[own] != 1 && st.sol[pick] == own) ||
+                                    (pick >= K && st.cnt[own] == 1 && pick == K));
+    if (a.dry && !stay) { S.status = kDryStop; S.next = (int)i; }
+    else if (pick < 0) { S.status = -pick; S.next = (int)i; }
     else {
       const int ownlab = st.los[own];
       if (pick < K) {
@@ -1851,6 +1861,7 @@ __device__ __forceinline__ void resolve_finish(const ResolveArgs& a, const RStat
 }
 
 __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
+  if (!pipe_gate(a)) return;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63;
   RState st;
@@ -2040,6 +2051,7 @@ __device__ int decide_lane(double* w, int* perm, int E, double rU, double* rad) 
 // kResolveBlkMin uncertain points and K + m <= 64, nslots <= 64 (lane = block point, and
 // lane = slot in the walk).
 __global__ __launch_bounds__(kWave) void k_resolve_blk(ResolveArgs a) {
+  if (!pipe_gate(a)) return;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63;
   RState st;
@@ -2314,7 +2326,8 @@ __global__ __launch_bounds__(1024) void k_finish_sweep(int* counts, int* sol, in
 // Cluster parameter upload (UploadLayout) from the staging buffer.
 __global__ void k_scatter_clusters(const uint8_t* __restrict__ stage, int nent, int dp, int d, int bw, int full,
                                    uint8_t* codes, double* tab, uint64_t* bnd, int* counts, int* sol, int* los,
-                                   int* src) {
+                                   int* src, const int* gate) {
+  if (gate && *(volatile const int*)gate == 0) return;
   const UploadLayout L = upload_layout(nent, dp, d, bw);
   const int* slot = (const int*)(stage + L.off_slot);
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (int64_t)gridDim.x * blockDim.x;
@@ -2614,11 +2627,11 @@ hipError_t launch_finish_sweep(int* counts, int* sol, int* los, int* src, int ca
 
 hipError_t launch_scatter_clusters(const uint8_t* stage, int nent, int dp, int d, int bw, int full, uint8_t* codes,
                                    double* tab, uint64_t* bnd, int* counts, int* sol, int* los, int* src,
-                                   hipStream_t s) {
+                                   hipStream_t s, const int* gate) {
   const int64_t work = (int64_t)nent * std::max(2 * d, std::max(dp, bw));
   const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (work + 255) / 256));
   hipLaunchKernelGGL(k_scatter_clusters, dim3(nb), dim3(256), 0, s, stage, nent, dp, d, bw, full, codes, tab, bnd,
-                     counts, sol, los, src);
+                     counts, sol, los, src, gate);
   return hipGetLastError();
 }
 

@@ -129,7 +129,24 @@ struct PrepassArgs {
   int* zero;                 // k_cluster_summary clears this word first (the sweep's move count), or nullptr
   int exact_grid;            // cap on the exact-rows grid (0: none); workgroups loop over the list
   int nlb, lblock;           // list blocks of this launch and their points (k_exact_rows_wg's own list scan)
+  // pipelined iterations (engine.cpp iterations_pipelined): the kernels run only while *gate
+  // is set, and read the sweep's draws from *raw_ptr (a position found on the device)
+  const int* gate;
+  const uint32_t* const* raw_ptr;
 };
+
+// A sweep's kernels in a pipeline read `raw` from the device (pipe_gate); false: skip.
+template <class A>
+__device__ __forceinline__ bool pipe_gate(A& a) {
+  if (!a.gate) return true;
+  if (*(volatile const int*)a.gate == 0) return false;
+  a.raw = *a.raw_ptr;
+  return true;
+}
+
+// The resolver of a pipelined sweep (ResolveArgs::dry) stops with this status before its
+// first decision that would change the state; nothing has changed then.
+constexpr int kDryStop = 9;
 
 // The resolver runs in block mode (csrc/kernels.hip, k_resolve_blk) when in the previous
 // launch at least this many uncertain points needed a decision of their own (their
@@ -195,6 +212,9 @@ struct ResolveArgs {
   int fstride;               // d * mmax
   long long* prof;           // diagnostics: resolver phase times (s_memrealtime ticks) or nullptr
   int blocks;                // 1: block mode (k_resolve_blk; needs K + m <= 64, nslots <= 64)
+  const int* gate;           // as PrepassArgs
+  const uint32_t* const* raw_ptr;
+  int dry;                   // 1: stop (kDryStop) at the first decision that is not "stay"
 };
 
 // Cluster parameter upload: one staging buffer, scattered on the device.
@@ -264,6 +284,116 @@ struct SmArgs {
 }  // namespace hdpm
 
 namespace hdpm {
+
+// update_phi (code/common_functions.cpp:511-591) on the device (csrc/phi.hip).  T clusters
+// (ascending labels) each draw d centers, then d sigmas (rhig, hyperg.cpp:346-378), from one
+// slice of the R stream.  The sigma draws consume 2 uniforms per rbeta attempt, so where a
+// draw starts depends on every earlier rejection: item k (cluster t = k / d, attribute
+// j = k % d) starts at its nominal position t*3d + d + 2j plus a drift delta >= 0.
+// k_phi_masks evaluates every candidate's acceptance at every drift of a window around the
+// expected drift (bit masks, all items in parallel); k_phi_walk resolves the drifts in
+// stream order over the masks (one wave, fixed-point rounds of 64 items); k_phi_values
+// computes sigmas, dhamming tables, bound records and the regrouped log-likelihood terms.
+// Anything the device does not restate (Walker tables, the bisection path of rhig, an
+// ambiguous pbeta branch test, a drift outside its window, a short stream slice) sets a
+// status and nothing is committed: the host runs the update itself.
+struct PhiCand {             // rbeta setup of one (cluster, attribute, center level)
+  int kind;                  // 2 = BC, 3 = BB (RBeta::Kind); 0: inactive; 1: bisection path
+  int pad;
+  double aa, a, b, alpha, beta, gamma, k1, k2, thr, m;   // as PoolClass
+};
+
+struct PhiArgs {
+  int T, d, dp, mmax, sumatt, wb, Ws, bw;
+  const int* lab;            // [T] label of cluster t (ascending)
+  const int* cnt;            // [T] its size
+  const unsigned* freq;      // [label][d][mmax]
+  const double* sig_in;      // [T][d] current sigma (cf:498 uses it in the center probabilities)
+  const int32_t* att;        // [d] m_j
+  const int* aoff;           // [d + 1] prefix sums of m_j
+  const double* v;           // [d]
+  const double* w;           // [d]
+  const uint64_t* gtab;      // glibc exp table then log table (512 words)
+  const uint32_t* raw;       // the stream slice from the update's first draw
+  int64_t nraw;              // its length
+  // scratch
+  double* cum;               // [T][sumatt] cumulative probabilities in revsort order
+  uint8_t* perm;             // [T][sumatt] level (0-based) of each sorted position
+  uint8_t* det;              // [T][d] deterministic pick + 1, or 0 (depends on the uniform)
+  PhiCand* cand;             // [T][sumatt] per center level
+  int* act;                  // active candidates: [0] count, then (t * sumatt + aoff[j] + l) entries
+  int64_t nact_cap;
+  uint64_t* mask;            // [T * sumatt][nw] acceptance bits per drift (candidates of uniform-dependent picks)
+  uint64_t* maskd;           // [T * d][nw] the same for items whose pick does not depend on the uniform
+  uint8_t* ikind;            // [T][d] such an item's candidate kind (0: the pick depends on the uniform)
+  int wpb;                   // waves per workgroup of k_phi_cwalk / k_phi_values
+  int groups;                // k_phi_cwalk workgroups per cluster
+  // pipelined iterations: raw from *raw_ptr (k_phi_locate), skipped unless *gate; the
+  // chain writes the next sweep's start position *pos_out = *pos_in + sweep_len + draws
+  const uint32_t* const* raw_ptr;
+  const int* gate;
+  const int64_t* pos_in;
+  int64_t* pos_out;
+  int64_t sweep_len;
+  int nw;                    // words per candidate
+  double rate, sdev;         // expected drift per item and its sd per sqrt(item): window model
+  uint8_t* pick;             // [T][d] drawn center level (0-based)
+  int64_t* apos;             // [T][d] position of the accepted attempt (relative to raw)
+  int* status;               // [0] status (0 ok), [1] first failing item, [2..3] consumption (int64)
+  // outputs
+  uint8_t* stage;            // UploadLayout(T, dp, d, bw) staging (entry t -> slot `slot_of[t]`)
+  const int* slot_of;        // [T] slot of each entry, or nullptr (slot = label)
+  double* sig_out;           // [T][d] new sigmas
+  double* ll;                // [T][2] regrouped log-likelihood (hi, lo) of each cluster
+  // speculative cluster walks (k_phi_cwalk): cluster t's start drift is one of
+  // phi_clo(t) + c, c < Wc; F[t][c] = its end drift (-1: the walk left its windows)
+  double* lg;                // [span] log(u / (1 - u)) of each stream position
+  double* lzz;               // [span] log(u_p * u_p * u_(p+1))
+  int64_t span;
+  int* F;                    // [T][Wc]
+  int Wc;
+  int64_t* dts;              // [T] the start drift of each cluster (k_phi_chain)
+};
+
+// Drift windows of the device update_phi (phi.hip).  Extra uniforms per sigma draw: mean
+// rate, sd sdev; after k draws the drift is rate k +- kPhiSd sdev sqrt(k).
+constexpr double kPhiSd = 7.0;
+__host__ __device__ inline int64_t phi_lo(int64_t k, double rate, double sdev) {
+  const double c = rate * (double)k - kPhiSd * sdev * sqrt((double)k) - 16.0;
+  return c <= 0.0 ? 0 : (int64_t)c;
+}
+__host__ __device__ inline int64_t phi_hi(int64_t k, double rate, double sdev) {
+  return (int64_t)(rate * (double)k + kPhiSd * sdev * sqrt((double)k)) + 80;
+}
+
+// Windows of the device stream a pipelined iteration may read (engine.cpp RngWindow).
+struct PipeWin {
+  const uint32_t* raw;
+  int64_t start, count;
+};
+
+// k_phi_locate: the update's slice after the sweep from *pos_in; k_pipe_check: the commit
+// decision of an iteration and the next sweep's slice.
+struct PipeArgs {
+  int* gate;                 // the pipeline runs while set
+  int* commit_ok;            // this iteration's tables go to the slots (k_scatter_clusters gate)
+  const ResolveCtl* ctl;     // the sweep's resolver control block
+  int* phi_status;           // the update's status words [4] (status, -, consumption int64)
+  const double* ll;          // the update's log-likelihood pairs [T][2]
+  int T, n;
+  const int64_t* pos_in;     // the sweep's start position
+  const int64_t* pos_next;   // the next sweep's start position (the update's chain)
+  int64_t sweep_len;         // N (m + 1)
+  int64_t need;              // k_phi_locate: stream words the update may read
+  PipeWin win[2];
+  const uint32_t** raw_out;  // k_phi_locate: the update's slice; k_pipe_check: the next sweep's
+  int* act;                  // k_phi_locate clears the candidate count
+  int64_t* rec;              // k_pipe_check: [0] 1 committed / 2 not run / 3 stopped, [1] ctl status,
+                             // [2] log-likelihood bits, [3] next position, [4] phi status, [5] window stop
+};
+
+enum PhiStatus { kPhiOk = 0, kPhiWalker = 1, kPhiBisect = 2, kPhiAmbig = 3, kPhiWindow = 4, kPhiShort = 5,
+                 kPhiProb = 6, kPhiInactive = 7, kPhiCap = 8 };
 
 // R's Mersenne-Twister stream on the device (one workgroup, one twist per barrier).
 // Output r >= 0 continues the host state (X_0, mti0): the first 624 - mti0 outputs temper

@@ -1,0 +1,839 @@
+// phi.hip -- update_phi (code/common_functions.cpp:511-591) on the device.
+//
+// For every cluster t of the update (ascending labels, cf:535) the reference draws d
+// centers -- sample(1:m_j, 1, TRUE, prob) with prob from the cluster's frequency table
+// (cf:461-509, 560) -- then d sigmas -- rhig(1, v', w', m_j) (cf:572-589, hyperg.cpp:346-378)
+// with v' = v + matches, w' = w + mismatches of the drawn center.  A center draw takes one
+// uniform; a sigma draw on rhig's beta path takes 2 uniforms per rbeta attempt, repeated
+// while rejected or above (m_j - 1) / m_j.  Where each draw starts therefore depends on every
+// earlier rejection -- the serial part of the update.  Here:
+//
+//   k_phi_prep   one thread per (cluster, attribute): the center probabilities, Rcpp
+//                sample's FixupProb / revsort / cumulative sums, the levels the draw can
+//                pick and, per pickable level, the sigma's rbeta setup (rhig's branch test
+//                decided exactly as the host does, hg:359)
+//   k_phi_logits the two stream-only logarithms of an rbeta attempt at every position
+//   k_phi_masks  every candidate's acceptance at every drift of a window around the expected
+//                drift, as bit masks (one wave = 64 drifts; all items at once)
+//   k_phi_cwalk  every cluster walked from every start drift of its window at once (one wave
+//                each): the center picks, then the sigma draws 64 at a time by a fixed-point
+//                iteration over the masks (each round fixes every lane up to the next
+//                rejection) -> the cluster's end drift as a function of its start drift
+//   k_phi_chain  the clusters' actual start drifts: T lookups in those functions
+//   k_phi_values one wave per cluster: its walk from its actual drift, the accepted attempts'
+//                draws, sigma = -1/log(out), the dhamming tables, the bound record
+//                (UploadLayout staging for k_scatter_clusters) and the regrouped
+//                log-likelihood of the cluster (cf:379-401 as sum_j matches * tab0 +
+//                mismatches * tab1)
+//
+// Every value that decides a draw is the host's bit for bit: IEEE adds, multiplies and
+// divides (-ffp-contract=off), glibc's exp / log replicas (glibc_math.hpp), and the branch
+// test's Cantelli bounds; its continued-fraction pbeta runs in device libm and an outcome
+// within 1e-7 of the threshold is left to the host (kPhiAmbig), as are Walker tables
+// (> 200 levels), the bisection path (rare: a center most members do not share) and a drift
+// outside the masks' window.  On any status nothing is committed and the host's update
+// runs instead, from the same stream position.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "kernels.hpp"
+#include "pool_gen.hpp"
+
+namespace hdpm {
+
+namespace {
+
+__device__ __forceinline__ PoolClass as_pool(const PhiCand& c) {
+  PoolClass p;
+  p.kind = c.kind;
+  p.pad = 0;
+  p.aa = c.aa; p.a = c.a; p.b = c.b; p.alpha = c.alpha; p.beta = c.beta; p.gamma = c.gamma;
+  p.k1 = c.k1; p.k2 = c.k2; p.thr = c.thr; p.m = c.m;
+  return p;
+}
+
+__device__ __forceinline__ void set_status(int* st, int code) { atomicMax(st, code); }
+
+
+// Serial revsort (R sort.c) on one thread: a[0..n) descending with 1-based levels in ib.
+__device__ void phi_revsort(double* a0, uint8_t* ib0, int n) {
+  if (n <= 1) return;
+  double* a = a0 - 1;
+  uint8_t* ib = ib0 - 1;
+  int l = (n >> 1) + 1, ir = n, i, j;
+  uint8_t ii;
+  double ra;
+  for (;;) {
+    if (l > 1) {
+      l = l - 1;
+      ra = a[l];
+      ii = ib[l];
+    } else {
+      ra = a[ir];
+      ii = ib[ir];
+      a[ir] = a[1];
+      ib[ir] = ib[1];
+      if (--ir == 1) {
+        a[1] = ra;
+        ib[1] = ii;
+        return;
+      }
+    }
+    i = l;
+    j = l << 1;
+    while (j <= ir) {
+      if (j < ir && a[j] > a[j + 1]) ++j;
+      if (ra > a[j]) {
+        a[i] = a[j];
+        ib[i] = ib[j];
+        j += (i = j);
+      } else {
+        j = ir + 1;
+      }
+    }
+    a[i] = ra;
+    ib[i] = ii;
+  }
+}
+
+// The continued fraction of the incomplete beta (rmath.hpp detail::betacf) and pbeta, in
+// device libm: used only for the branch test, with a margin (phi_beta_path).
+__device__ double phi_betacf(double a, double b, double x) {
+  const double FPMIN = 1e-300, EPS = 1e-16;
+  double qab = a + b, qap = a + 1.0, qam = a - 1.0, c = 1.0, d = 1.0 - qab * x / qap;
+  if (fabs(d) < FPMIN) d = FPMIN;
+  d = 1.0 / d;
+  double h = d;
+  for (int m = 1; m <= 200000; m++) {
+    const int m2 = 2 * m;
+    double aa = m * (b - m) * x / ((qam + m2) * (a + m2));
+    d = 1.0 + aa * d; if (fabs(d) < FPMIN) d = FPMIN;
+    c = 1.0 + aa / c; if (fabs(c) < FPMIN) c = FPMIN;
+    d = 1.0 / d; h *= d * c;
+    aa = -(a + m) * (qab + m) * x / ((a + m2) * (qap + m2));
+    d = 1.0 + aa * d; if (fabs(d) < FPMIN) d = FPMIN;
+    c = 1.0 + aa / c; if (fabs(c) < FPMIN) c = FPMIN;
+    d = 1.0 / d;
+    const double del = d * c;
+    h *= del;
+    if (fabs(del - 1.0) < EPS) break;
+  }
+  return h;
+}
+
+__device__ double phi_pbeta(double x, double a, double b) {
+  if (x <= 0.0) return 0.0;
+  if (x >= 1.0) return 1.0;
+  const double lbt = lgamma(a + b) - lgamma(a) - lgamma(b) + a * log(x) + b * log1p(-x);
+  if (x < (a + 1.0) / (a + b + 2.0)) return exp(lbt) * phi_betacf(a, b, x) / a;
+  return 1.0 - exp(lbt) * phi_betacf(b, a, 1.0 - x) / b;
+}
+
+// rhig_beta_path (rmath.hpp: qbeta01_lt(w + 1, v - 1, (m - 1) / m) && (m - 1) / m > 4 / 5):
+// 1 beta path, 0 bisection, -1 undecided here (pbeta within 1e-7 of 0.1).
+__device__ int phi_beta_path(double v, double w, double m) {
+  const double x = (m - 1) / m;
+  if (!(x > 0)) return 0;                    // (m - 1) / m > 4 / 5 with 4 / 5 == 0 (hg:359)
+  const double a = w + 1, b = v - 1;
+  if (isnan(a) || isnan(b) || a < 0 || b < 0) return 0;
+  if (b == 0) return 0;
+  if (a == 0) return x > 0 ? 1 : 0;
+  const double mu = a / (a + b);
+  const double s2 = a * b / ((a + b) * (a + b) * (a + b + 1.0));
+  const double dlt = x - mu;
+  const double bound = s2 / (s2 + dlt * dlt);
+  if (dlt > 0 && bound < 0.85) return 1;
+  if (dlt < 0 && bound < 0.05) return 0;
+  const double p = phi_pbeta(x, a, b);
+  if (fabs(p - 0.1) < 1e-7) return -1;
+  return p > 0.1 ? 1 : 0;
+}
+
+// rbeta_setup (rmath.hpp; nmath rbeta's constants) for kinds BB and BC; false otherwise.
+__device__ bool phi_rbeta_setup(double aa, double bb, PhiCand* c) {
+  if (isnan(aa) || isnan(bb) || aa < 0. || bb < 0.) return false;
+  if (isinf(aa) || isinf(bb) || aa == 0. || bb == 0.) return false;
+  c->aa = aa;
+  c->a = fmin(aa, bb);
+  c->b = fmax(aa, bb);
+  c->alpha = c->a + c->b;
+  c->beta = 0; c->gamma = 0; c->k1 = 0; c->k2 = 0;
+  if (c->a <= 1.0) {
+    c->kind = 2;
+    c->beta = 1.0 / c->a;
+    const double delta = 1.0 + c->b - c->a;
+    c->k1 = delta * (0.0138889 + 0.0416667 * c->a) / (c->b * c->beta - 0.777778);
+    c->k2 = 0.25 + (0.5 + 0.25 / delta) * c->a;
+  } else {
+    c->kind = 3;
+    c->beta = sqrt((c->alpha - 2.0) / (2.0 * c->a * c->b - c->alpha));
+    c->gamma = c->a + 1.0 / c->beta;
+  }
+  return true;
+}
+
+__device__ __forceinline__ int wave_excl_scan(int v, int* total) {
+  const int lane = threadIdx.x & 63;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(x, o);
+    if (lane >= o) x += t;
+  }
+  *total = __shfl(x, 63);
+  return x - v;
+}
+
+}  // namespace
+
+// One rbeta attempt as pool_attempt (pool_gen.hpp), operation for operation, with the two
+// stream-only logarithms read from the per-position tables: lg1 = log(u1 / (1 - u1)) and
+// lzz = log(u1 * u1 * u2) (BB; BC's u1 >= 0.5 branch).  BC's other branch forms
+// z = u1 * (u1 * u2), which rounds differently, and takes its log here.
+__device__ __forceinline__ bool phi_attempt(const PoolClass& C, double u1, double u2, double lg1, double lzz,
+                                            const uint64_t* texp, const uint64_t* tlog, double* x) {
+  const double expmax = 1024 * 0.693147180559945309417232121458;   // DBL_MAX_EXP * M_LN2
+  const double v = C.beta * lg1;
+  if (C.kind == 3) {   // BB
+    const double a = C.a, b = C.b, alpha = C.alpha;
+    double w;
+    if (v <= expmax) {
+      w = a * glibc::exp_r(v, texp);
+      if (!(w <= 1.7976931348623157e308)) w = 1.7976931348623157e308;
+    } else {
+      w = 1.7976931348623157e308;
+    }
+    *x = (C.aa != C.a) ? b / (b + w) : w / (b + w);
+    const double z = u1 * u1 * u2;
+    const double r = C.gamma * v - 1.3862944;
+    const double s = a + r - w;
+    if (s + 2.609438 >= 5.0 * z) return true;
+    const double t = lzz;
+    if (s > t) return true;
+    return !(r + alpha * glibc::log_r(alpha / (b + w), tlog) < t);
+  }
+  // BC
+  const double a = C.a, b = C.b, alpha = C.alpha;
+  double z;
+  if (u1 < 0.5) {
+    const double y = u1 * u2;
+    z = u1 * y;
+    if (0.25 * u2 + z - y >= C.k1) return false;
+  } else {
+    z = u1 * u1 * u2;
+    if (z > 0.25 && z >= C.k2) return false;
+  }
+  double w;
+  if (v <= expmax) {
+    w = b * glibc::exp_r(v, texp);
+    if (!(w <= 1.7976931348623157e308)) w = 1.7976931348623157e308;
+  } else {
+    w = 1.7976931348623157e308;
+  }
+  *x = (C.aa == a) ? a / (a + w) : w / (a + w);
+  if (!(u1 < 0.5) && z <= 0.25) return true;
+  const double lz = u1 < 0.5 ? glibc::log_r(z, tlog) : lzz;
+  return alpha * (glibc::log_r(alpha / (a + w), tlog) + v) - 1.3862944 >= lz;
+}
+
+// ------------------------------------------------------------------ prep
+// Per-thread scratch for the levels of one attribute: LDS when m_j <= kPhiLdsLevels, else
+// the global cum / perm rows themselves.
+constexpr int kPhiLdsLevels = 16;
+
+__global__ __launch_bounds__(256) void k_phi_prep(PhiArgs a) {
+  if (a.gate && *(volatile const int*)a.gate == 0) return;
+  if (a.raw_ptr) a.raw = *a.raw_ptr;
+  __shared__ uint64_t tabs[256];
+  __shared__ double spr[256 * kPhiLdsLevels];
+  __shared__ uint8_t spm[256 * kPhiLdsLevels];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) tabs[i] = a.gtab[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool ok = idx < (int64_t)a.T * a.d;
+  int status = 0, nact = 0;
+  const int t = ok ? (int)(idx / a.d) : 0, j = ok ? (int)(idx - (int64_t)t * a.d) : 0;
+  const int mj = ok ? a.att[j] : 1, off = a.aoff[j];
+  const int nn = a.cnt[t];
+  const unsigned* f = a.freq + ((int64_t)a.lab[t] * a.d + j) * a.mmax;
+  double* gpr = a.cum + (int64_t)t * a.sumatt + off;
+  uint8_t* gpm = a.perm + (int64_t)t * a.sumatt + off;
+  const bool lds = mj <= kPhiLdsLevels;
+  double* pr = lds ? spr + threadIdx.x * kPhiLdsLevels : gpr;
+  uint8_t* pm = lds ? spm + threadIdx.x * kPhiLdsLevels : gpm;
+  PhiCand* cb = a.cand + (int64_t)t * a.sumatt + off;
+  bool det = false;
+  if (ok) {
+    const double sg = a.sig_in[(int64_t)t * a.d + j];
+    // cf:496-503 (as the host's pj_phaseA)
+    for (int l = 0; l < mj; ++l) pr[l] = (-((double)nn - (double)f[l])) / sg;
+    double mx = pr[0];
+    for (int l = 1; l < mj; ++l) if (pr[l] > mx) mx = pr[l];
+    for (int l = 0; l < mj; ++l) pr[l] = glibc::exp_r(pr[l] - mx, tabs);
+    double sum = 0.0;
+    for (int l = 0; l < mj; ++l) sum += pr[l];
+    for (int l = 0; l < mj; ++l) pr[l] = pr[l] / sum;
+    // sample_prob1_prep: FixupProb, Walker check, revsort, cumulative sums
+    double s2 = 0.0;
+    int npos = 0;
+    for (int l = 0; l < mj; ++l) {
+      const double x = pr[l];
+      if (!isfinite(x) || x < 0) status = kPhiProb;
+      if (x > 0) { npos++; s2 += x; }
+    }
+    if (npos == 0) status = kPhiProb;
+    if (!status) {
+      for (int l = 0; l < mj; ++l) pr[l] = pr[l] / s2;
+      int nc = 0;
+      for (int l = 0; l < mj; ++l) nc += (mj * pr[l] > 0.1);
+      if (nc > 200) status = kPhiWalker;
+    }
+    if (!status) {
+      for (int l = 0; l < mj; ++l) pm[l] = (uint8_t)(l + 1);
+      phi_revsort(pr, pm, mj);
+      for (int l = 1; l < mj; ++l) pr[l] += pr[l - 1];
+      if (lds)
+        for (int l = 0; l < mj; ++l) { gpr[l] = pr[l]; gpm[l] = pm[l]; }
+      // the pick is perm[0] whatever the uniform when cum[0] >= 1 (a uniform is < 1)
+      det = mj == 1 || pr[0] >= 1.0;
+      a.det[idx] = det ? pm[0] : 0;
+      // candidates: the levels the draw can pick (sorted position s: the last, or cum rising)
+      for (int s = 0; s < mj && !status; ++s) {
+        const int l = pm[s] - 1;
+        PhiCand c{};
+        c.kind = 0;
+        const bool pickable = det ? s == 0 : (s == mj - 1 || pr[s] > (s > 0 ? pr[s - 1] : 0.0));
+        if (pickable) {
+          const double sumdelta = (double)f[l];
+          const double nw_ = a.w[j] + nn - sumdelta, nv_ = a.v[j] + sumdelta;
+          const double m = (double)mj;
+          const int bp = phi_beta_path(nv_, nw_, m);
+          if (bp < 0) status = kPhiAmbig;
+          c.kind = 1;                                   // bisection path (or a degenerate rbeta)
+          if (bp == 1 && phi_rbeta_setup(nw_ + 1, nv_ - 1, &c)) {
+            c.thr = (m - 1) / m;
+            c.m = m;
+            nact++;
+          }
+        }
+        cb[l] = c;
+        if (det && s == 0) a.ikind[idx] = (uint8_t)c.kind;
+      }
+      if (!det) a.ikind[idx] = 0;
+    }
+  }
+  if (status) set_status(a.status, status);
+  // the wave's candidates to evaluate, appended with one atomic per wave
+  int tot = 0;
+  const int before = wave_excl_scan(ok && !status ? nact : 0, &tot);
+  int base = 0;
+  if (lane == 0 && tot) base = atomicAdd(a.act, tot);
+  base = __shfl(base, 0);
+  if (ok && !status && nact) {
+    int e = base + before;
+    for (int l = 0; l < mj; ++l) {
+      const int kd = cb[l].kind;
+      if (kd != 2 && kd != 3) continue;
+      if (e < a.nact_cap) {
+        a.act[1 + 2 * e] = (int)((int64_t)t * a.sumatt + off + l);
+        a.act[2 + 2 * e] = det ? -1 - (int)idx : (int)idx;     // negative: item-indexed mask row
+      } else {
+        set_status(a.status, kPhiCap);
+      }
+      ++e;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ stream logits
+// lg[p] = log(u_p / (1 - u_p)) and lzz[p] = log(u_p * u_p * u_(p+1)) over the positions any
+// draw of the update can take (the same expressions as rbeta's, rmath.hpp RngSrc / BB).
+__global__ __launch_bounds__(256) void k_phi_logits(PhiArgs a) {
+  if (a.gate && *(volatile const int*)a.gate == 0) return;
+  if (a.raw_ptr) a.raw = *a.raw_ptr;
+  __shared__ uint64_t tlog[256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) tlog[i] = a.gtab[256 + i];
+  __syncthreads();
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < a.span; p += (int64_t)gridDim.x * blockDim.x) {
+    const double u1 = pool_unif(a.raw[p]), u2 = pool_unif(a.raw[p + 1]);
+    a.lg[p] = glibc::log_r(u1 / (1.0 - u1), tlog);
+    a.lzz[p] = glibc::log_r(u1 * u1 * u2, tlog);
+  }
+}
+
+// ------------------------------------------------------------------ masks
+// mask[cand][q] bit i: the rbeta attempt at drift lo + 64 q + i of the candidate's item is
+// accepted with x <= (m - 1) / m (rhig's loop ends there).
+__global__ __launch_bounds__(256) void k_phi_masks(PhiArgs a) {
+  if (a.gate && *(volatile const int*)a.gate == 0) return;
+  if (a.raw_ptr) a.raw = *a.raw_ptr;
+  __shared__ uint64_t tabs[512];
+  for (int i = threadIdx.x; i < 512; i += blockDim.x) tabs[i] = a.gtab[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int nact = min(*a.act, (int)a.nact_cap);
+  const int64_t total = (int64_t)nact * a.nw;
+  const int64_t nwv = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t wv = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); wv < total; wv += nwv) {
+    const int e = (int)(wv / a.nw), q = (int)(wv - (int64_t)e * a.nw);
+    const int ci = a.act[1 + 2 * e];
+    const int kr = a.act[2 + 2 * e];
+    const bool det = kr < 0;
+    const int64_t k = det ? -1 - (int64_t)kr : kr;
+    const int t = (int)(k / a.d), j = (int)(k - (int64_t)t * a.d);
+    const PoolClass C = as_pool(a.cand[ci]);
+    const int64_t nominal = (int64_t)t * 3 * a.d + a.d + 2 * (int64_t)j;
+    const int64_t pos = nominal + phi_lo(k, a.rate, a.sdev) + 64 * (int64_t)q + lane;
+    bool acc = false;
+    if (pos < a.span) {
+      double x = 0.0;
+      acc = phi_attempt(C, pool_unif(a.raw[pos]), pool_unif(a.raw[pos + 1]), a.lg[pos], a.lzz[pos], tabs, tabs + 256,
+                        &x) &&
+            !(x > C.thr);
+    }
+    const uint64_t b = __ballot(acc);
+    if (lane == 0) (det ? a.maskd + k * a.nw : a.mask + (int64_t)ci * a.nw)[q] = b;
+  }
+}
+
+// ------------------------------------------------------------------ walks
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Start-drift window of cluster t for the speculative walks.
+__device__ __forceinline__ int64_t phi_clo(int t, const PhiArgs& a) { return phi_lo((int64_t)t * a.d, a.rate, a.sdev); }
+
+// LDS image of cluster t for its walks: the mask rows of the items whose pick does not
+// depend on the uniform ([d][nw] words), their picks + 1 (det) and kinds.
+struct PhiClusterLds {
+  const uint64_t* maskd;
+  const uint8_t* det;
+  const uint8_t* ikind;
+};
+
+__device__ __forceinline__ void phi_stage_cluster(const PhiArgs& a, int t, uint64_t* m, uint8_t* det, uint8_t* ik) {
+  const int64_t nwd = (int64_t)a.d * a.nw;
+  const uint64_t* src = a.maskd + (int64_t)t * nwd;
+  for (int64_t q = threadIdx.x; q < nwd; q += blockDim.x) m[q] = src[q];
+  for (int j = threadIdx.x; j < a.d; j += blockDim.x) {
+    det[j] = a.det[(int64_t)t * a.d + j];
+    ik[j] = a.ikind[(int64_t)t * a.d + j];
+  }
+}
+
+// Cluster t of the update from start drift `delta` (one wave): the d center picks, then
+// the d sigma draws 64 at a time.  Lane j's drift is the batch's drift plus the extra
+// uniforms of the lanes before it; each round recomputes every lane's extra from its mask
+// words at its current drift, and stops when no drift changes (each round fixes every lane
+// up to the next rejection).  Returns the end drift, or -1 (a pick outside the candidates
+// or a drift outside the masks' windows).  spick: LDS (d bytes); sapos: per attribute the
+// accepted attempt's position, or nullptr.
+__device__ int64_t phi_walk_cluster(const PhiArgs& a, const PhiClusterLds& C, int t, int64_t delta, uint8_t* spick,
+                                    int64_t* sapos, int* why) {
+  const int lane = threadIdx.x & 63;
+  const int d = a.d;
+  const int64_t base = (int64_t)t * 3 * d;
+  bool bad = false;
+  for (int j = lane; j < d; j += 64) {
+    const int dt = C.det[j];
+    int pk = 0;
+    if (dt) {
+      pk = dt - 1;
+      const int kd = C.ikind[j];
+      if (kd != 2 && kd != 3) { bad = true; *why = kd == 1 ? kPhiBisect : kPhiInactive; }
+    } else {
+      const int64_t pos = base + delta + j;
+      if (pos >= a.span) bad = true;
+      else {
+        const double rU = pool_unif(a.raw[pos]);
+        const int mj = a.att[j];
+        const double* cum = a.cum + (int64_t)t * a.sumatt + a.aoff[j];
+        int s;
+        for (s = 0; s < mj - 1; ++s)
+          if (rU <= cum[s]) break;
+        pk = a.perm[(int64_t)t * a.sumatt + a.aoff[j] + s] - 1;
+        const int kd = a.cand[(int64_t)t * a.sumatt + a.aoff[j] + pk].kind;
+        if (kd != 2 && kd != 3) { bad = true; *why = kd == 1 ? kPhiBisect : kPhiInactive; }
+      }
+    }
+    spick[j] = (uint8_t)pk;
+  }
+  wave_lds_sync();
+  if (__ballot(bad)) {
+    if (*why == 0) *why = kPhiShort;
+    return -1;
+  }
+  for (int j0 = 0; j0 < d; j0 += 64) {
+    const int j = j0 + lane;
+    const bool act = j < d;
+    const int64_t k = (int64_t)t * d + j;
+    // the lane's three mask words from the batch's start drift (a batch drifts < 128)
+    uint64_t w0 = 0, w1 = 0, w2 = 0;
+    int64_t wlo = 0;
+    if (act) {
+      const int64_t lo = phi_lo(k, a.rate, a.sdev);
+      const int64_t q = delta >= lo ? (delta - lo) >> 6 : -1;
+      if (q < 0 || q >= a.nw) bad = true;
+      else {
+        const uint64_t* m = C.det[j] ? C.maskd + (int64_t)j * a.nw
+                                     : a.mask + ((int64_t)t * a.sumatt + a.aoff[j] + spick[j]) * a.nw;
+        w0 = m[q];
+        w1 = q + 1 < a.nw ? m[q + 1] : 0ull;
+        w2 = q + 2 < a.nw ? m[q + 2] : 0ull;
+        wlo = lo + 64 * q;
+      }
+    }
+    if (__ballot(bad)) { *why = kPhiWindow; return -1; }
+    int64_t dl = delta;
+    int ex = 0, tot = 0;
+    for (;;) {
+      ex = 0;
+      if (act) {
+        int o = (int)(dl - wlo);
+        ex = -1;
+        for (int r = 0; o < 192; ++r, o += 2) {
+          const uint64_t wd = o < 64 ? w0 : o < 128 ? w1 : w2;
+          if ((wd >> (o & 63)) & 1ull) { ex = 2 * r; break; }
+        }
+        if (ex < 0) { bad = true; ex = 0; }
+      }
+      if (__ballot(bad)) { *why = kPhiWindow; return -1; }
+      const int before = wave_excl_scan(ex, &tot);
+      const int64_t nd = delta + before;
+      const bool changed = act && nd != dl;
+      dl = nd;
+      if (!__ballot(changed)) break;
+    }
+    if (act && sapos) sapos[j] = base + d + 2 * (int64_t)j + dl + ex;   // the accepted attempt
+    delta += tot;
+  }
+  return delta;
+}
+
+// LDS of the cluster image: d nw mask words, d det bytes, d kind bytes (16-B aligned)
+__host__ __device__ inline size_t phi_cluster_lds(int d, int nw) {
+  return ((size_t)d * nw * 8 + 2 * (size_t)d + 15) & ~(size_t)15;
+}
+
+// Every cluster from every start drift of its window: F[t][c] = end drift from
+// phi_clo(t) + c.  `groups` workgroups per cluster stage its image in LDS; each wave walks
+// start drifts c = (g * wpb + wave) + k * groups * wpb.
+__global__ __launch_bounds__(1024) void k_phi_cwalk(PhiArgs a) {
+  if (a.gate && *(volatile const int*)a.gate == 0) return;
+  if (a.raw_ptr) a.raw = *a.raw_ptr;
+  extern __shared__ __attribute__((aligned(16))) uint8_t wl[];
+  if (*a.status != 0) return;
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int t = blockIdx.x / a.groups, g = blockIdx.x - t * a.groups;
+  uint64_t* m = reinterpret_cast<uint64_t*>(wl);
+  uint8_t* det = wl + (size_t)a.d * a.nw * 8;
+  uint8_t* ik = det + a.d;
+  phi_stage_cluster(a, t, m, det, ik);
+  __syncthreads();
+  const PhiClusterLds C{m, det, ik};
+  uint8_t* spick = wl + phi_cluster_lds(a.d, a.nw) + (size_t)wid * a.d;
+  const int64_t clo = phi_clo(t, a);
+  const int step = a.groups * a.wpb;
+  for (int c = g * a.wpb + wid; c < a.Wc; c += step) {
+    int why = 0;
+    const int64_t e = phi_walk_cluster(a, C, t, clo + c, spick, nullptr, &why);
+    if (lane == 0) a.F[(int64_t)t * a.Wc + c] = e < 0 || e > 0x7fffffff ? -1 : (int)e;
+  }
+}
+
+// The clusters' actual start drifts: delta_0 = 0, delta_{t+1} = F[t][delta_t - clo(t)]
+// (the table staged in LDS when it fits).
+__global__ __launch_bounds__(1024) void k_phi_chain(PhiArgs a) {
+  if (a.gate && *(volatile const int*)a.gate == 0) return;
+  if (a.raw_ptr) a.raw = *a.raw_ptr;
+  extern __shared__ int sF[];
+  if (*a.status != 0) return;
+  const int64_t nF = (int64_t)a.T * a.Wc;
+  const bool lds = nF <= 16384;
+  if (lds)
+    for (int64_t q = threadIdx.x; q < nF; q += blockDim.x) sF[q] = a.F[q];
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const int* F = lds ? sF : a.F;
+  int64_t delta = 0;
+  for (int t = 0; t < a.T; ++t) {
+    a.dts[t] = delta;
+    const int64_t c = delta - phi_clo(t, a);
+    if (c < 0 || c >= a.Wc) { set_status(a.status, kPhiWindow); return; }
+    const int e = F[(int64_t)t * a.Wc + c];
+    if (e < 0) { set_status(a.status, kPhiWindow); return; }
+    delta = e;
+  }
+  const int64_t cons = (int64_t)a.T * 3 * a.d + delta;
+  if (cons + 1 > a.span) set_status(a.status, kPhiShort);
+  *(int64_t*)(a.status + 2) = cons;
+  if (a.pos_out) *a.pos_out = *a.pos_in + a.sweep_len + cons;
+}
+
+// ------------------------------------------------------------------ pipelined iterations
+// The update after a pipelined sweep: its slice starts sweep_len draws after the sweep's
+// start; the window holding `need` words from there (kPhiShort when none does).
+__global__ void k_phi_locate(PipeArgs a) {
+  if (threadIdx.x != 0) return;
+  a.phi_status[0] = 0; a.phi_status[1] = 0; a.phi_status[2] = 0; a.phi_status[3] = 0;
+  *a.act = 0;
+  if (*(volatile const int*)a.gate == 0) return;
+  const int64_t p = *a.pos_in + a.sweep_len;
+  for (int w = 0; w < 2; ++w) {
+    const PipeWin& W = a.win[w];
+    if (W.raw && p >= W.start && p + a.need <= W.start + W.count) {
+      *a.raw_out = W.raw + (p - W.start);
+      return;
+    }
+  }
+  a.phi_status[0] = kPhiShort;
+  *a.raw_out = a.win[0].raw;
+}
+
+// The commit decision of a pipelined iteration: its sweep moved nothing (the dry resolver
+// finished it) and its update ran on the device.  Then the update's tables go to the slots
+// (commit_ok gates k_scatter_clusters), the record takes the log-likelihood and the next
+// sweep's start, and the next sweep's slice is located (none: the pipeline stops after
+// this iteration).  Otherwise the pipeline stops here and nothing is committed.
+__global__ void k_pipe_check(PipeArgs a) {
+  if (threadIdx.x != 0) return;
+  for (int q = 0; q < 6; ++q) a.rec[q] = 0;
+  *a.commit_ok = 0;
+  if (*(volatile const int*)a.gate == 0) { a.rec[0] = 2; return; }
+  // the resolver wrote the block to host memory: read it uncached, field by field
+  const volatile int* cv = reinterpret_cast<const volatile int*>(a.ctl);
+  const int c_next = cv[0], c_status = cv[1], c_restart = cv[2], c_moves = cv[5];
+  const int ps = a.phi_status[0];
+  a.rec[1] = c_status;
+  a.rec[4] = ps;
+  if (!(c_status == 0 && c_next >= a.n && c_moves == 0 && c_restart == 0 && ps == 0)) {
+    *a.gate = 0;
+    a.rec[0] = 3;
+    return;
+  }
+  *a.commit_ok = 1;
+  double hi = 0.0, lo = 0.0;
+  for (int t = 0; t < a.T; ++t)
+    for (int q = 0; q < 2; ++q) {
+      const double x = a.ll[2 * t + q], s = hi + x;
+      lo += fabs(hi) >= fabs(x) ? (hi - s) + x : (x - s) + hi;
+      hi = s;
+    }
+  const double ll = hi + lo;
+  a.rec[2] = __double_as_longlong(ll);
+  const int64_t p = *a.pos_next;
+  a.rec[3] = p;
+  a.rec[0] = 1;
+  for (int w = 0; w < 2; ++w) {
+    const PipeWin& W = a.win[w];
+    if (W.raw && p >= W.start && p + a.sweep_len <= W.start + W.count) {
+      *a.raw_out = W.raw + (p - W.start);
+      return;
+    }
+  }
+  *a.gate = 0;
+  a.rec[5] = 1;
+}
+
+hipError_t launch_phi_locate(const PipeArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_phi_locate, dim3(1), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_pipe_check(const PipeArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_pipe_check, dim3(1), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ values
+// One workgroup per cluster: wave 0 walks it again from its actual drift (picks and accepted
+// positions into LDS); then every wave takes attributes: the accepted attempts' draws,
+// sigma = -1/log(out), the dhamming tables; then the bound record (wave w: plane word w) and
+// the regrouped log-likelihood terms.  LDS: the cluster image, picks, positions, per
+// attribute (sigma, match, mismatch), per thread the partial sums.
+__global__ __launch_bounds__(1024) void k_phi_values(PhiArgs a) {
+  if (a.gate && *(volatile const int*)a.gate == 0) return;
+  if (a.raw_ptr) a.raw = *a.raw_ptr;
+  extern __shared__ __attribute__((aligned(16))) uint8_t wl[];
+  __shared__ uint64_t tabs[512];
+  __shared__ double red[4 * 16];
+  __shared__ int sbad;
+  for (int i = threadIdx.x; i < 512; i += blockDim.x) tabs[i] = a.gtab[i];
+  if (threadIdx.x == 0) sbad = 0;
+  if (*a.status != 0) return;
+  const uint64_t* texp = tabs;
+  const uint64_t* tlog = tabs + 256;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nth = blockDim.x;
+  const int t = blockIdx.x;
+  const int d = a.d;
+  uint64_t* m = reinterpret_cast<uint64_t*>(wl);
+  uint8_t* det = wl + (size_t)d * a.nw * 8;
+  uint8_t* ik = det + d;
+  phi_stage_cluster(a, t, m, det, ik);
+  double* wtab = reinterpret_cast<double*>(wl + phi_cluster_lds(d, a.nw));   // [d][2]
+  int64_t* sapos = reinterpret_cast<int64_t*>(wtab + 2 * d);
+  uint8_t* spick = reinterpret_cast<uint8_t*>(sapos + d);
+  __syncthreads();
+  if (wid == 0) {
+    int why = 0;
+    const PhiClusterLds C{m, det, ik};
+    if (phi_walk_cluster(a, C, t, a.dts[t], spick, sapos, &why) < 0 && lane == 0) {
+      set_status(a.status, why ? why : kPhiWindow);
+      sbad = 1;
+    }
+  }
+  __syncthreads();
+  if (sbad) return;
+  const UploadLayout L = upload_layout(a.T, a.dp, d, a.bw);
+  uint8_t* codes = a.stage + L.off_codes + (size_t)t * a.dp;
+  double* tab = reinterpret_cast<double*>(a.stage + L.off_tab) + (size_t)t * 2 * d;
+  uint64_t* rec = reinterpret_cast<uint64_t*>(a.stage + L.off_bnd) + (size_t)t * a.bw;
+  const int nn = a.cnt[t];
+  const unsigned* fb = a.freq + (int64_t)a.lab[t] * d * a.mmax;
+  double hi = 0.0, lo = 0.0;                     // regrouped log-likelihood terms (Neumaier)
+  auto add = [&](double x) {
+    const double s = hi + x;
+    lo += fabs(hi) >= fabs(x) ? (hi - s) + x : (x - s) + hi;
+    hi = s;
+  };
+  double A = 0.0, sc = 0.0, dmx = 0.0, dmn = __builtin_inf();
+  bool bad = false;
+  for (int j = threadIdx.x; j < a.dp; j += nth) {
+    if (j >= d) { codes[j] = 0; continue; }
+    const int64_t k = (int64_t)t * d + j;
+    const int pk = spick[j];
+    const PoolClass C = as_pool(a.cand[(int64_t)t * a.sumatt + a.aoff[j] + pk]);
+    const int64_t p = sapos[j];
+    double x = 0.0;
+    if (!(p + 1 < a.span) ||
+        !phi_attempt(C, pool_unif(a.raw[p]), pool_unif(a.raw[p + 1]), a.lg[p], a.lzz[p], texp, tlog, &x) ||
+        x > C.thr)
+      bad = true;
+    double sg, m0, m1;
+    pool_sigma_tables(C, x, a.att[j], texp, tlog, &sg, &m0, &m1);
+    codes[j] = (uint8_t)(pk + 1);
+    a.pick[k] = (uint8_t)pk;
+    wtab[2 * j] = m0;
+    wtab[2 * j + 1] = m1;
+    tab[2 * j] = m0;
+    tab[2 * j + 1] = m1;
+    a.sig_out[k] = sg;
+    A += m0;
+    sc += fmax(fabs(m0), fabs(m1));
+    const double dj = m0 - m1;
+    dmx = fmax(dmx, dj);
+    dmn = fmin(dmn, dj);
+    const double fm = (double)fb[(int64_t)j * a.mmax + pk];
+    add(fm * m0);
+    add(((double)nn - fm) * m1);
+  }
+  if (bad) atomicOr(&sbad, 1);
+  // per wave: A and scale summed (any order: only the bound's slack sees their rounding),
+  // the log-likelihood pairs in lane order
+  {
+    double H = 0.0, Lo = 0.0;
+    for (int q = 0; q < 64; ++q) {
+      const double x = __shfl(hi, q), y = __shfl(lo, q);
+      const double s = H + x;
+      Lo += fabs(H) >= fabs(x) ? (H - s) + x : (x - s) + H;
+      H = s;
+      Lo += y;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      A += __shfl_xor(A, o);
+      sc += __shfl_xor(sc, o);
+    }
+    if (lane == 0) {
+      red[wid] = A;
+      red[16 + wid] = sc;
+      red[32 + wid] = H;
+      red[48 + wid] = Lo;
+    }
+  }
+  __syncthreads();
+  if (sbad) {
+    if (threadIdx.x == 0) set_status(a.status, kPhiWindow);
+    return;
+  }
+  // the block's sums: A, scale (any order: only the bound's slack sees their rounding),
+  // dmax, dmin; the log-likelihood pairs in thread order
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    dmx = fmax(dmx, __shfl_xor(dmx, o));
+    dmn = fmin(dmn, __shfl_xor(dmn, o));
+  }
+  __shared__ double wmx[16], wmn[16];
+  if (lane == 0) { wmx[wid] = dmx; wmn[wid] = dmn; }
+  __syncthreads();
+  dmx = 0.0;
+  dmn = __builtin_inf();
+  for (int q = 0; q < nth / 64; ++q) { dmx = fmax(dmx, wmx[q]); dmn = fmin(dmn, wmn[q]); }
+  const double delta = dmx > 0 ? dmx / ((1 << kQ) - 1) : 0.0;
+  // bound record (Ctx::bounds_for, kernels.hpp "Bound data per parameter entry"): wave w
+  // builds plane word w
+  for (int k = wid; k < a.Ws; k += nth / 64) {
+    const int j = 64 * k + lane;
+    const bool valid = j < d;
+    const unsigned code = valid ? spick[j] : 0u;
+    int q = 0;
+    if (valid) {
+      const double dj = wtab[2 * j] - wtab[2 * j + 1];
+      q = delta > 0 ? (int)floor(dj / delta) : 0;
+      q = min(max(q, 0), (1 << kQ) - 1);
+      while (q > 0 && delta * q > dj) --q;
+      while (q < (1 << kQ) - 1 && delta * (q + 1) <= dj) ++q;
+    }
+    for (int b = 0; b < a.wb; ++b) {
+      const uint64_t bits = __ballot(valid && ((code >> b) & 1u));
+      if (lane == 0) rec[b * a.Ws + k] = bits;
+    }
+    for (int b = 0; b < kQ; ++b) {
+      const uint64_t bits = __ballot(valid && ((q >> b) & 1));
+      if (lane == 0) rec[(a.wb + b) * a.Ws + k] = bits;
+    }
+  }
+  if (threadIdx.x == 0) {
+    double As = 0.0, scs = 0.0, H = 0.0, Lo = 0.0;
+    for (int q = 0; q < nth / 64; ++q) {
+      As += red[q];
+      scs += red[16 + q];
+      const double x = red[32 + q];
+      const double s = H + x;
+      Lo += fabs(H) >= fabs(x) ? (H - s) + x : (x - s) + H;
+      H = s;
+      Lo += red[48 + q];
+    }
+    double* sv = reinterpret_cast<double*>(rec + (a.wb + kQ) * a.Ws);
+    sv[0] = As;
+    sv[1] = delta;
+    sv[2] = dmn > 0 ? dmn : 0.0;
+    sv[3] = scs;
+    reinterpret_cast<int*>(a.stage + L.off_counts)[t] = nn;
+    reinterpret_cast<int*>(a.stage + L.off_slot)[t] = a.slot_of ? a.slot_of[t] : a.lab[t];
+    a.ll[2 * t] = H;
+    a.ll[2 * t + 1] = Lo;
+  }
+}
+
+// dynamic LDS of k_phi_cwalk (cluster image + a pick row per wave) and k_phi_values
+// (cluster image + tables, positions, picks)
+size_t phi_cwalk_lds(int d, int nw, int wpb) { return phi_cluster_lds(d, nw) + (size_t)wpb * d; }
+size_t phi_values_lds(int d, int nw) { return phi_cluster_lds(d, nw) + (size_t)d * (16 + 8 + 1); }
+
+hipError_t launch_phi(const PhiArgs& a, hipStream_t s) {
+  const int64_t items = (int64_t)a.T * a.d;
+  if (items <= 0) return hipSuccess;
+  if (a.nw < 1 || a.Wc < 1 || a.wpb < 1 || a.wpb > 16 || a.groups < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_phi_prep, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_phi_logits, dim3((unsigned)std::min<int64_t>(1024, (a.span + 255) / 256)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_phi_masks, dim3(1024), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_phi_cwalk, dim3((unsigned)(a.T * a.groups)), dim3(64 * a.wpb), phi_cwalk_lds(a.d, a.nw, a.wpb),
+                     s, a);
+  const int64_t nF = (int64_t)a.T * a.Wc;
+  hipLaunchKernelGGL(k_phi_chain, dim3(1), dim3(1024), nF <= 16384 ? (size_t)nF * 4 : 0, s, a);
+  hipLaunchKernelGGL(k_phi_values, dim3((unsigned)a.T), dim3(64 * a.wpb), phi_values_lds(a.d, a.nw), s, a);
+  return hipGetLastError();
+}
+
+}  // namespace hdpm

@@ -199,6 +199,10 @@ class Engine:
                                             int(ocml), _lib.ptr(out)))
         return out
 
+    def set_phi_device(self, on: bool = True):
+        """update_phi on the device (include/hdpm.h HDPM_OPT_PHI_DEVICE); same chain."""
+        self._check(self._L.hdpm_set_option(self._h, _lib.OPT_PHI_DEVICE, 1.0 if on else 0.0))
+
     def set_hig_logspace(self, on: bool = True):
         """Extension beyond the reference (include/hdpm.h HDPM_OPT_HIG_LOGSPACE): finite HIG
         log-densities for clusters whose 2F1 series overflows (the reference throws)."""

@@ -67,12 +67,14 @@ def test_loglik_matrix_bit_exact(hd, oracle, zoo, which):
 
 
 # ------------------------------------------------------------------ single sweep
-def sweep_case(hd, oracle, ds, c, cen, sig, P, seed, m=3, debug=0, sweeps=1, phi=False):
+def sweep_case(hd, oracle, ds, c, cen, sig, P, seed, m=3, debug=0, sweeps=1, phi=False, phi_device=False):
     st = oracle.seed_state(seed)
     pc, ps, s0 = oracle.pool_generate(ds.attrisize, ds.v, ds.w, P, st)
     assert s0 == 0
     eng = make_engine(hd, ds)
     eng.set_debug(debug)
+    if phi_device:
+        eng.set_phi_device(True)
     eng.set_state(c, cen, sig)
     eng.set_pool(pc, ps)
     eng.rng_state = st
@@ -123,11 +125,13 @@ def test_zoo_sweeps_with_update_phi_one_cluster(hd, oracle, zoo, debug):
 # 16: recount the frequency tables every update_phi; 128: no speculative update_phi;
 # 2048: exact rows one wave per point; 4096: no block mode in the resolver; 8192: block mode
 # for every launch
+@pytest.mark.parametrize("phi_device", [False, True])
 @pytest.mark.parametrize("debug", [0, 1, 8, 16, 128, 2048, 2048 | 1, 4096, 8192, 8192 | 8, 262144])
-def test_synthetic_sweeps_with_update_phi(hd, oracle, debug):
+def test_synthetic_sweeps_with_update_phi(hd, oracle, debug, phi_device):
     ds = synth(6000, 32, 8, 2, seed=3)
     cen, sig = random_params(ds, 8, 7)
-    sweep_case(hd, oracle, ds, ds.truth, cen, sig, ds.n * 3, seed=31, sweeps=3, phi=True, debug=debug)
+    sweep_case(hd, oracle, ds, ds.truth, cen, sig, ds.n * 3, seed=31, sweeps=3, phi=True, debug=debug,
+               phi_device=phi_device)
 
 
 def test_speculative_update_phi(hd, oracle):
@@ -136,9 +140,33 @@ def test_speculative_update_phi(hd, oracle):
     # ran during the sweep; every step is compared with the oracle.
     ds = synth(4000, 64, 6, 4, seed=9)
     cen, sig = random_params(ds, 6, 11)
-    stats = sweep_case(hd, oracle, ds, ds.truth, cen, sig, ds.n * 3, seed=41, sweeps=8, phi=True)
+    stats = sweep_case(hd, oracle, ds, ds.truth, cen, sig, ds.n * 3, seed=41, sweeps=8, phi=True, debug=524288)
     assert stats["phi_spec_runs"] >= 6
     assert stats["phi_spec_clusters"] > 0
+
+
+# update_phi on the device (csrc/phi.hip): centers, sigmas, tables and the stream position
+# after it against the oracle, on shapes with one and several attribute classes, binary and
+# many-level attributes, wide rows; and that the device path ran (no silent host fallback).
+@pytest.mark.parametrize("shape", ["c5_like", "mixed", "binary", "wide", "zoo"])
+def test_device_update_phi(hd, oracle, zoo, shape):
+    if shape == "zoo":
+        ds, K = zoo, 7
+    else:
+        ds, K = {"c5_like": (synth(8000, 128, 12, 4, seed=5), 12), "mixed": (synth(5000, 48, 9, (2, 6), seed=6), 9),
+                 "binary": (synth(6000, 32, 8, 2, seed=7), 8), "wide": (synth(2500, 784, 6, 6, seed=8), 6)}[shape]
+    cen, sig = random_params(ds, K, 13)
+    stats = sweep_case(hd, oracle, ds, ds.truth, cen, sig, ds.n * 3, seed=43, sweeps=4, phi=True, phi_device=True)
+    assert stats["phi_device_calls"] >= 2, stats
+
+
+def test_device_update_phi_small_clusters_fall_back_or_match(hd, oracle, zoo):
+    # all-singleton Zoo clusters: rhig's bisection path and center levels that depend on the
+    # uniform; whatever the device hands back, the chain is the oracle's
+    c = np.arange(zoo.n, dtype=np.int32)
+    cen, sig = random_params(zoo, zoo.n, 5)
+    stats = sweep_case(hd, oracle, zoo, c, cen, sig, zoo.n * 3, seed=23, sweeps=3, phi=True, phi_device=True)
+    assert stats["phi_device_calls"] + stats["phi_device_fallbacks"] == 3
 
 
 def test_synthetic_large_d_sweep(hd, oracle):
