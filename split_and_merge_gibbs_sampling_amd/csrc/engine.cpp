@@ -66,6 +66,7 @@ hipError_t launch_lmatrix(const uint8_t* codes_t, int n, int d, int nq, ParamTab
 hipError_t launch_phi(const PhiArgs& a, hipStream_t s);
 size_t phi_cwalk_lds(int d, int nw, int wpb);
 size_t phi_values_lds(int d, int nw);
+int phi_ilp();
 int sm_restricted_gibbs_device(struct Ctx* c, const int32_t* S, int32_t nS, int32_t i1, int32_t i2,
                                int32_t t);
 
@@ -2671,7 +2672,7 @@ struct Ctx {
   // candidate, start drifts walked per cluster, stream words read, walk workgroup shape.
   struct PhiPlan {
     bool ok = false;
-    int T = 0, nw = 0, Wc = 0, wpb = 0, groups = 0;
+    int T = 0, nw = 0, Wc = 0, wpb = 0, groups = 0, L = 0, S = 1;
     int64_t items = 0, need = 0;
     double rate = 0, sdev = 0;
   };
@@ -2683,9 +2684,9 @@ struct Ctx {
     pl.rate = 2 * p / (1 - p);
     pl.sdev = 2 * std::sqrt(p) / (1 - p);
     pl.items = (int64_t)T * d;
-    const int64_t klast = pl.items - 1, tl = (int64_t)(T - 1) * d;
+    const int64_t klast = pl.items - 1;
     pl.nw = (int)((phi_hi(klast, pl.rate, pl.sdev) - phi_lo(klast, pl.rate, pl.sdev) + 63) / 64) + 3;
-    pl.Wc = (int)(phi_hi(tl, pl.rate, pl.sdev) - phi_lo(tl, pl.rate, pl.sdev)) + 2;
+    pl.Wc = (int)(phi_hi(klast, pl.rate, pl.sdev) - phi_lo(klast, pl.rate, pl.sdev)) + 2;   // any segment start
     pl.need = 3 * pl.items + phi_hi(pl.items, pl.rate, pl.sdev) + 256;
     // LDS of the walks: the cluster image (d nw mask words) with the per-wave pick rows;
     // 16 waves per workgroup while that fits, fewer otherwise
@@ -2693,8 +2694,12 @@ struct Ctx {
     while (wpb > 1 && (phi_cwalk_lds(d, pl.nw, wpb) > 150 * 1024 || phi_values_lds(d, pl.nw) > 150 * 1024)) wpb /= 2;
     if (phi_cwalk_lds(d, pl.nw, wpb) > 150 * 1024 || phi_values_lds(d, pl.nw) > 150 * 1024) return pl;
     pl.wpb = wpb;
-    // workgroups per cluster: about two start drifts per wave, at least a workgroup per CU overall
-    pl.groups = std::max(1, std::min((pl.Wc + 2 * wpb - 1) / (2 * wpb), (256 + T - 1) / T * 2));
+    // k_phi_cwalk: walk segments of at most 128 draws; kPhiIlp start drifts per thread, at
+    // most 1024 threads per workgroup
+    if (phi_cwalk_lds(d, pl.nw, 16) > 150 * 1024) return pl;
+    pl.S = (d + 127) / 128;
+    pl.L = (d + pl.S - 1) / pl.S;
+    pl.groups = (pl.Wc + 1024 * phi_ilp() - 1) / (1024 * phi_ilp());
     pl.ok = true;
     return pl;
   }
@@ -2715,7 +2720,7 @@ struct Ctx {
     phd.ikind.ensure(items);
     phd.lg.ensure(pl.need);
     phd.lzz.ensure(pl.need);
-    phd.F.ensure((size_t)T * pl.Wc);
+    phd.F.ensure((size_t)T * pl.S * pl.Wc);
     phd.dts.ensure(T);
     PhiArgs a{};
     a.T = T; a.d = d; a.dp = dp; a.mmax = mmax; a.sumatt = phd.sumatt; a.wb = wb; a.Ws = Ws; a.bw = bw;
@@ -2724,7 +2729,7 @@ struct Ctx {
     a.act = phd.act.p; a.nact_cap = cap; a.mask = phd.mask.p; a.nw = pl.nw; a.rate = pl.rate; a.sdev = pl.sdev;
     a.apos = phd.apos.p;
     a.lg = phd.lg.p; a.lzz = phd.lzz.p; a.span = pl.need - 1; a.F = phd.F.p; a.Wc = pl.Wc; a.dts = phd.dts.p;
-    a.maskd = phd.maskd.p; a.ikind = phd.ikind.p; a.wpb = pl.wpb; a.groups = pl.groups;
+    a.maskd = phd.maskd.p; a.ikind = phd.ikind.p; a.wpb = pl.wpb; a.groups = pl.groups; a.L = pl.L; a.S = pl.S;
     a.raw_ptr = nullptr; a.gate = nullptr; a.pos_in = nullptr; a.pos_out = nullptr; a.sweep_len = 0;
     a.slot_of = nullptr;
     return a;
@@ -2799,6 +2804,26 @@ struct Ctx {
     std::memcpy(&cons, phd.h_out.p + 8, 8);
     phd.last_status = status;
     const uint64_t target = rng.pos + (uint64_t)cons;
+    if (debug & 2) {
+      std::vector<int64_t> dts(T);
+      HIPCHK(hipMemcpy(dts.data(), phd.dts.p, (size_t)T * 8, hipMemcpyDeviceToHost));
+      std::vector<int> F((size_t)T * pl.S * pl.Wc);
+      HIPCHK(hipMemcpy(F.data(), phd.F.p, F.size() * 4, hipMemcpyDeviceToHost));
+      int valid0 = 0;
+      for (int c = 0; c < pl.Wc; ++c) valid0 += F[c] >= 0;
+      std::string vs;
+      for (int t = 0; t < T; ++t) {
+        int v = 0, lo = -1, hi = -1;
+        for (int c = 0; c < pl.Wc; ++c)
+          if (F[(size_t)t * pl.S * pl.Wc + c] >= 0) { v++; if (lo < 0) lo = c; hi = c; }
+        vs += " t" + std::to_string(t) + ":" + std::to_string(v) + "[" + std::to_string(lo) + "," + std::to_string(hi) +
+              "] F0 " + std::to_string(F[(size_t)t * pl.S * pl.Wc]) + " Fmid " + std::to_string(F[(size_t)t * pl.S * pl.Wc + pl.Wc / 2]) +
+              "] dts " + std::to_string(dts[t]) + " clo " + std::to_string(phi_lo((int64_t)t * d, pl.rate, pl.sdev));
+      }
+      std::fprintf(stderr, "[phi] F%s\n", vs.c_str());
+      std::fprintf(stderr, "[phi] T %d nw %d Wc %d status %d cons %lld dts0 %lld F[0][0] %d valid(t=0) %d rate %.4f sdev %.4f\n",
+                   T, pl.nw, pl.Wc, status, (long long)cons, (long long)dts[0], F[0], valid0, pl.rate, pl.sdev);
+    }
     if (status != kPhiOk || cons <= 0 || !can_adopt(*W, target)) {
       phd.fallbacks++;
       stats.phi_device_fallbacks++;

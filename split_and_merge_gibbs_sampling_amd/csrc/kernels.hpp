@@ -350,8 +350,9 @@ struct PhiArgs {
   double* lg;                // [span] log(u / (1 - u)) of each stream position
   double* lzz;               // [span] log(u_p * u_p * u_(p+1))
   int64_t span;
-  int* F;                    // [T][Wc]
+  int* F;                    // [T * S][Wc]
   int Wc;
+  int L, S;                  // walk segments: items [s L, (s + 1) L) of a cluster, S per cluster
   int64_t* dts;              // [T] the start drift of each cluster (k_phi_chain)
 };
 

@@ -57,10 +57,11 @@ __device__ __forceinline__ void set_status(int* st, int code) { atomicMax(st, co
 
 
 // Serial revsort (R sort.c) on one thread: a[0..n) descending with 1-based levels in ib.
-__device__ void phi_revsort(double* a0, uint8_t* ib0, int n) {
+template <class PR, class PM>
+__device__ __forceinline__ void phi_revsort_t(PR a0, PM ib0, int n) {
   if (n <= 1) return;
-  double* a = a0 - 1;
-  uint8_t* ib = ib0 - 1;
+  PR a = a0 - 1;
+  PM ib = ib0 - 1;
   int l = (n >> 1) + 1, ir = n, i, j;
   uint8_t ii;
   double ra;
@@ -242,6 +243,72 @@ __device__ __forceinline__ bool phi_attempt(const PoolClass& C, double u1, doubl
 // the global cum / perm rows themselves.
 constexpr int kPhiLdsLevels = 16;
 
+// One (cluster, attribute): the center probabilities (as the host's pj_phaseA, cf:496-503),
+// sample_prob1_prep (FixupProb, Walker check, revsort, cumulative sums) in pr / pm, the
+// candidates per pickable level.  Returns a PhiStatus; *det_out, *nact_out.  Called with LDS
+// or global scratch (two copies, so the compiler keeps each address space).
+template <class PR, class PM>
+__device__ __forceinline__ int phi_prep_item(const PhiArgs& a, int t, int j, int64_t idx, PR pr, PM pm,
+                                             const uint64_t* tabs, bool* det_out, int* nact_out) {
+  const int mj = a.att[j], off = a.aoff[j];
+  const int nn = a.cnt[t];
+  const unsigned* f = a.freq + ((int64_t)a.lab[t] * a.d + j) * a.mmax;
+  const double sg = a.sig_in[(int64_t)t * a.d + j];
+  for (int l = 0; l < mj; ++l) pr[l] = (-((double)nn - (double)f[l])) / sg;
+  double mx = pr[0];
+  for (int l = 1; l < mj; ++l) if (pr[l] > mx) mx = pr[l];
+  for (int l = 0; l < mj; ++l) pr[l] = glibc::exp_r(pr[l] - mx, tabs);
+  double sum = 0.0;
+  for (int l = 0; l < mj; ++l) sum += pr[l];
+  for (int l = 0; l < mj; ++l) pr[l] = pr[l] / sum;
+  double s2 = 0.0;
+  int npos = 0;
+  for (int l = 0; l < mj; ++l) {
+    const double x = pr[l];
+    if (!isfinite(x) || x < 0) return kPhiProb;
+    if (x > 0) { npos++; s2 += x; }
+  }
+  if (npos == 0) return kPhiProb;
+  for (int l = 0; l < mj; ++l) pr[l] = pr[l] / s2;
+  int nc = 0;
+  for (int l = 0; l < mj; ++l) nc += (mj * pr[l] > 0.1);
+  if (nc > 200) return kPhiWalker;
+  for (int l = 0; l < mj; ++l) pm[l] = (uint8_t)(l + 1);
+  phi_revsort_t(pr, pm, mj);
+  for (int l = 1; l < mj; ++l) pr[l] += pr[l - 1];
+  // the pick is perm[0] whatever the uniform when cum[0] >= 1 (a uniform is < 1)
+  const bool det = mj == 1 || pr[0] >= 1.0;
+  *det_out = det;
+  a.det[idx] = det ? pm[0] : 0;
+  a.ikind[idx] = 0;
+  // candidates: the levels the draw can pick (sorted position s: the last, or cum rising)
+  PhiCand* cb = a.cand + (int64_t)t * a.sumatt + off;
+  int nact = 0;
+  for (int s = 0; s < mj; ++s) {
+    const int l = pm[s] - 1;
+    PhiCand c{};
+    c.kind = 0;
+    const bool pickable = det ? s == 0 : (s == mj - 1 || pr[s] > (s > 0 ? pr[s - 1] : 0.0));
+    if (pickable) {
+      const double sumdelta = (double)f[l];
+      const double nw_ = a.w[j] + nn - sumdelta, nv_ = a.v[j] + sumdelta;
+      const double m = (double)mj;
+      const int bp = phi_beta_path(nv_, nw_, m);
+      if (bp < 0) return kPhiAmbig;
+      c.kind = 1;                                   // bisection path (or a degenerate rbeta)
+      if (bp == 1 && phi_rbeta_setup(nw_ + 1, nv_ - 1, &c)) {
+        c.thr = (m - 1) / m;
+        c.m = m;
+        nact++;
+      }
+      if (det) a.ikind[idx] = (uint8_t)c.kind;
+    }
+    cb[l] = c;
+  }
+  *nact_out = nact;
+  return 0;
+}
+
 __global__ __launch_bounds__(256) void k_phi_prep(PhiArgs a) {
   if (a.gate && *(volatile const int*)a.gate == 0) return;
   if (a.raw_ptr) a.raw = *a.raw_ptr;
@@ -252,76 +319,24 @@ __global__ __launch_bounds__(256) void k_phi_prep(PhiArgs a) {
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool ok = idx < (int64_t)a.T * a.d;
-  int status = 0, nact = 0;
+  const bool ok = idx < (int64_t)a.T * a.d;
   const int t = ok ? (int)(idx / a.d) : 0, j = ok ? (int)(idx - (int64_t)t * a.d) : 0;
-  const int mj = ok ? a.att[j] : 1, off = a.aoff[j];
-  const int nn = a.cnt[t];
-  const unsigned* f = a.freq + ((int64_t)a.lab[t] * a.d + j) * a.mmax;
-  double* gpr = a.cum + (int64_t)t * a.sumatt + off;
-  uint8_t* gpm = a.perm + (int64_t)t * a.sumatt + off;
-  const bool lds = mj <= kPhiLdsLevels;
-  double* pr = lds ? spr + threadIdx.x * kPhiLdsLevels : gpr;
-  uint8_t* pm = lds ? spm + threadIdx.x * kPhiLdsLevels : gpm;
-  PhiCand* cb = a.cand + (int64_t)t * a.sumatt + off;
+  int status = 0, nact = 0;
   bool det = false;
   if (ok) {
-    const double sg = a.sig_in[(int64_t)t * a.d + j];
-    // cf:496-503 (as the host's pj_phaseA)
-    for (int l = 0; l < mj; ++l) pr[l] = (-((double)nn - (double)f[l])) / sg;
-    double mx = pr[0];
-    for (int l = 1; l < mj; ++l) if (pr[l] > mx) mx = pr[l];
-    for (int l = 0; l < mj; ++l) pr[l] = glibc::exp_r(pr[l] - mx, tabs);
-    double sum = 0.0;
-    for (int l = 0; l < mj; ++l) sum += pr[l];
-    for (int l = 0; l < mj; ++l) pr[l] = pr[l] / sum;
-    // sample_prob1_prep: FixupProb, Walker check, revsort, cumulative sums
-    double s2 = 0.0;
-    int npos = 0;
-    for (int l = 0; l < mj; ++l) {
-      const double x = pr[l];
-      if (!isfinite(x) || x < 0) status = kPhiProb;
-      if (x > 0) { npos++; s2 += x; }
-    }
-    if (npos == 0) status = kPhiProb;
-    if (!status) {
-      for (int l = 0; l < mj; ++l) pr[l] = pr[l] / s2;
-      int nc = 0;
-      for (int l = 0; l < mj; ++l) nc += (mj * pr[l] > 0.1);
-      if (nc > 200) status = kPhiWalker;
-    }
-    if (!status) {
-      for (int l = 0; l < mj; ++l) pm[l] = (uint8_t)(l + 1);
-      phi_revsort(pr, pm, mj);
-      for (int l = 1; l < mj; ++l) pr[l] += pr[l - 1];
-      if (lds)
+    const int mj = a.att[j], off = a.aoff[j];
+    if (mj <= kPhiLdsLevels) {
+      double* pr = spr + threadIdx.x * kPhiLdsLevels;
+      uint8_t* pm = spm + threadIdx.x * kPhiLdsLevels;
+      status = phi_prep_item(a, t, j, idx, pr, pm, tabs, &det, &nact);
+      if (!status) {
+        double* gpr = a.cum + (int64_t)t * a.sumatt + off;
+        uint8_t* gpm = a.perm + (int64_t)t * a.sumatt + off;
         for (int l = 0; l < mj; ++l) { gpr[l] = pr[l]; gpm[l] = pm[l]; }
-      // the pick is perm[0] whatever the uniform when cum[0] >= 1 (a uniform is < 1)
-      det = mj == 1 || pr[0] >= 1.0;
-      a.det[idx] = det ? pm[0] : 0;
-      // candidates: the levels the draw can pick (sorted position s: the last, or cum rising)
-      for (int s = 0; s < mj && !status; ++s) {
-        const int l = pm[s] - 1;
-        PhiCand c{};
-        c.kind = 0;
-        const bool pickable = det ? s == 0 : (s == mj - 1 || pr[s] > (s > 0 ? pr[s - 1] : 0.0));
-        if (pickable) {
-          const double sumdelta = (double)f[l];
-          const double nw_ = a.w[j] + nn - sumdelta, nv_ = a.v[j] + sumdelta;
-          const double m = (double)mj;
-          const int bp = phi_beta_path(nv_, nw_, m);
-          if (bp < 0) status = kPhiAmbig;
-          c.kind = 1;                                   // bisection path (or a degenerate rbeta)
-          if (bp == 1 && phi_rbeta_setup(nw_ + 1, nv_ - 1, &c)) {
-            c.thr = (m - 1) / m;
-            c.m = m;
-            nact++;
-          }
-        }
-        cb[l] = c;
-        if (det && s == 0) a.ikind[idx] = (uint8_t)c.kind;
       }
-      if (!det) a.ikind[idx] = 0;
+    } else {
+      status = phi_prep_item(a, t, j, idx, a.cum + (int64_t)t * a.sumatt + off, a.perm + (int64_t)t * a.sumatt + off,
+                             tabs, &det, &nact);
     }
   }
   if (status) set_status(a.status, status);
@@ -332,6 +347,8 @@ __global__ __launch_bounds__(256) void k_phi_prep(PhiArgs a) {
   if (lane == 0 && tot) base = atomicAdd(a.act, tot);
   base = __shfl(base, 0);
   if (ok && !status && nact) {
+    const int mj = a.att[j], off = a.aoff[j];
+    const PhiCand* cb = a.cand + (int64_t)t * a.sumatt + off;
     int e = base + before;
     for (int l = 0; l < mj; ++l) {
       const int kd = cb[l].kind;
@@ -429,7 +446,8 @@ __device__ __forceinline__ void phi_stage_cluster(const PhiArgs& a, int t, uint6
 // up to the next rejection).  Returns the end drift, or -1 (a pick outside the candidates
 // or a drift outside the masks' windows).  spick: LDS (d bytes); sapos: per attribute the
 // accepted attempt's position, or nullptr.
-__device__ int64_t phi_walk_cluster(const PhiArgs& a, const PhiClusterLds& C, int t, int64_t delta, uint8_t* spick,
+__device__ __forceinline__ int64_t phi_walk_cluster(const PhiArgs& a, const PhiClusterLds& C, int t, int64_t delta,
+                                                    uint8_t* spick,
                                     int64_t* sapos, int* why) {
   const int lane = threadIdx.x & 63;
   const int d = a.d;
@@ -476,11 +494,17 @@ __device__ int64_t phi_walk_cluster(const PhiArgs& a, const PhiClusterLds& C, in
       const int64_t q = delta >= lo ? (delta - lo) >> 6 : -1;
       if (q < 0 || q >= a.nw) bad = true;
       else {
-        const uint64_t* m = C.det[j] ? C.maskd + (int64_t)j * a.nw
-                                     : a.mask + ((int64_t)t * a.sumatt + a.aoff[j] + spick[j]) * a.nw;
-        w0 = m[q];
-        w1 = q + 1 < a.nw ? m[q + 1] : 0ull;
-        w2 = q + 2 < a.nw ? m[q + 2] : 0ull;
+        if (C.det[j]) {                        // LDS image
+          const uint64_t* m = C.maskd + (int64_t)j * a.nw;
+          w0 = m[q];
+          w1 = q + 1 < a.nw ? m[q + 1] : 0ull;
+          w2 = q + 2 < a.nw ? m[q + 2] : 0ull;
+        } else {                               // global candidate rows
+          const uint64_t* m = a.mask + ((int64_t)t * a.sumatt + a.aoff[j] + spick[j]) * a.nw;
+          w0 = m[q];
+          w1 = q + 1 < a.nw ? m[q + 1] : 0ull;
+          w2 = q + 2 < a.nw ? m[q + 2] : 0ull;
+        }
         wlo = lo + 64 * q;
       }
     }
@@ -516,133 +540,231 @@ __host__ __device__ inline size_t phi_cluster_lds(int d, int nw) {
   return ((size_t)d * nw * 8 + 2 * (size_t)d + 15) & ~(size_t)15;
 }
 
-// Every cluster from every start drift of its window: F[t][c] = end drift from
-// phi_clo(t) + c.  `groups` workgroups per cluster stage its image in LDS; each wave walks
-// start drifts c = (g * wpb + wave) + k * groups * wpb.
+// Every walk segment from every start drift of its window: F[t S + s][c] = the drift after
+// items [s L, (s + 1) L) of cluster t from phi_lo(t d + s L) + c.  The walks are independent:
+// a thread carries kPhiIlp start drifts through the segment's sigma draws at once (each draw
+// a lookup in the item's mask row; independent chains hide the LDS latency).  A workgroup
+// stages its cluster's image in LDS: the mask rows of the items whose pick does not depend on
+// the uniform, and each item's window start.  The others' picks depend on the cluster's
+// start drift: drawn per thread from the stream (segment 0 only -- a later segment's start
+// drift is not the cluster's; such a cluster sets kPhiWindow and the host updates).
+constexpr int kPhiIlp = 4;
+
+__host__ __device__ inline size_t phi_cwalk_image(int d, int nw) {
+  return phi_cluster_lds(d, nw) + (((size_t)d * 4 + 4 + 15) & ~(size_t)15);
+}
+
 __global__ __launch_bounds__(1024) void k_phi_cwalk(PhiArgs a) {
   if (a.gate && *(volatile const int*)a.gate == 0) return;
   if (a.raw_ptr) a.raw = *a.raw_ptr;
   extern __shared__ __attribute__((aligned(16))) uint8_t wl[];
   if (*a.status != 0) return;
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int t = blockIdx.x / a.groups, g = blockIdx.x - t * a.groups;
+  const int d = a.d, nw = a.nw;
+  const int ts = blockIdx.x / a.groups, g = blockIdx.x - ts * a.groups;
+  const int t = ts / a.S, sg = ts - t * a.S;
+  const int j0 = sg * a.L, j1 = min(d, j0 + a.L);
   uint64_t* m = reinterpret_cast<uint64_t*>(wl);
-  uint8_t* det = wl + (size_t)a.d * a.nw * 8;
-  uint8_t* ik = det + a.d;
+  uint8_t* det = wl + (size_t)d * nw * 8;
+  uint8_t* ik = det + d;
+  int* slo = reinterpret_cast<int*>(wl + phi_cluster_lds(d, nw));
+  int* nd = slo + d;                       // [0]: uniform-dependent picks in the segment, -1: none possible
   phi_stage_cluster(a, t, m, det, ik);
+  for (int j = threadIdx.x; j < d; j += blockDim.x) slo[j] = (int)phi_lo((int64_t)t * d + j, a.rate, a.sdev);
   __syncthreads();
-  const PhiClusterLds C{m, det, ik};
-  uint8_t* spick = wl + phi_cluster_lds(a.d, a.nw) + (size_t)wid * a.d;
-  const int64_t clo = phi_clo(t, a);
-  const int step = a.groups * a.wpb;
-  for (int c = g * a.wpb + wid; c < a.Wc; c += step) {
-    int why = 0;
-    const int64_t e = phi_walk_cluster(a, C, t, clo + c, spick, nullptr, &why);
-    if (lane == 0) a.F[(int64_t)t * a.Wc + c] = e < 0 || e > 0x7fffffff ? -1 : (int)e;
+  if (threadIdx.x == 0) {
+    int cnt = 0;                           // -1: a fixed pick whose sigma the device does not draw
+    for (int j = j0; j < j1 && cnt >= 0; ++j)
+      if (det[j] && ik[j] != 2 && ik[j] != 3) cnt = -1;
+      else if (!det[j]) cnt = sg == 0 ? cnt + 1 : -1;
+    nd[0] = cnt;
+  }
+  __syncthreads();
+  const int cstep = a.groups * blockDim.x;
+  const int c0 = g * blockDim.x + threadIdx.x;
+  if (c0 >= a.Wc) return;
+  const int64_t clo = phi_lo((int64_t)t * d + j0, a.rate, a.sdev);
+  int64_t dt0[kPhiIlp], delta[kPhiIlp];
+  int code[kPhiIlp];
+  const bool img = nd[0] >= 0;
+#pragma unroll
+  for (int u = 0; u < kPhiIlp; ++u) {
+    const int c = c0 + u * cstep;
+    dt0[u] = clo + c;
+    delta[u] = dt0[u];
+    code[u] = c < a.Wc ? (img ? 0 : -2) : -6;     // -2 image, -3 pick, -4 window, -5 rejections, -6 unused
+  }
+  const int64_t base = (int64_t)t * 3 * d;
+  if (img && nd[0] == 0) {
+    // every pick of the segment is fixed: a branch-free walk, the chains' LDS reads in flight
+    // together (a chain that leaves its window or runs out of attempts keeps walking a clamped
+    // row and is marked)
+    const unsigned lim = 64u * (unsigned)(nw - 1);
+    int dl[kPhiIlp];
+#pragma unroll
+    for (int u = 0; u < kPhiIlp; ++u) dl[u] = (int)delta[u];
+    for (int j = j0; j < j1; ++j) {
+      const int sl = slo[j];
+      const uint64_t* row = m + (size_t)j * nw;
+      uint64_t lo[kPhiIlp], hi[kPhiIlp];
+      int sh[kPhiIlp];
+      bool bad[kPhiIlp];
+#pragma unroll
+      for (int u = 0; u < kPhiIlp; ++u) {
+        const int off = dl[u] - sl;
+        bad[u] = (unsigned)off >= lim;
+        const int q = bad[u] ? 0 : off >> 6;
+        sh[u] = off & 63;
+        lo[u] = row[q];
+        hi[u] = row[q + 1];
+      }
+#pragma unroll
+      for (int u = 0; u < kPhiIlp; ++u) {
+        const uint64_t win = sh[u] ? (lo[u] >> sh[u]) | (hi[u] << (64 - sh[u])) : lo[u];
+        const uint64_t acc = win & 0x5555555555555555ull;
+        const int ncode = bad[u] ? -4 : (acc ? 0 : -5);
+        code[u] = code[u] ? code[u] : ncode;
+        dl[u] += acc ? __builtin_ctzll(acc) : 0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kPhiIlp; ++u) delta[u] = dl[u];
+  } else {
+  for (int j = j0; j < j1; ++j) {
+    const int sl = slo[j];
+    const bool dj = det[j] != 0;
+    uint64_t lo[kPhiIlp], hi[kPhiIlp];
+    int sh[kPhiIlp];
+    bool live = false;
+#pragma unroll
+    for (int u = 0; u < kPhiIlp; ++u) {
+      lo[u] = 0; hi[u] = 0; sh[u] = 0;
+      if (code[u] != 0) continue;
+      const int64_t off = delta[u] - sl;
+      if (off < 0 || off >= 64 * (nw - 1)) { code[u] = -4; continue; }
+      const int q = (int)(off >> 6);
+      sh[u] = (int)(off & 63);
+      if (dj) {
+        lo[u] = m[(int64_t)j * nw + q];        // LDS
+        hi[u] = m[(int64_t)j * nw + q + 1];
+      } else {
+        // a pick that depends on the uniform (cf:560 at this start drift): drawn here
+        const int64_t pos = base + dt0[u] + j;
+        if (pos >= a.span) { code[u] = -3; continue; }
+        const double rU = pool_unif(a.raw[pos]);
+        const int mj = a.att[j];
+        const double* cum = a.cum + (int64_t)t * a.sumatt + a.aoff[j];
+        int s;
+        for (s = 0; s < mj - 1; ++s)
+          if (rU <= cum[s]) break;
+        const int64_t ci = (int64_t)t * a.sumatt + a.aoff[j] + a.perm[(int64_t)t * a.sumatt + a.aoff[j] + s] - 1;
+        const int kd = a.cand[ci].kind;
+        if (kd != 2 && kd != 3) { code[u] = -3; continue; }
+        lo[u] = a.mask[ci * nw + q];
+        hi[u] = a.mask[ci * nw + q + 1];
+      }
+      live = true;
+    }
+    if (!live) break;
+#pragma unroll
+    for (int u = 0; u < kPhiIlp; ++u) {
+      if (code[u] != 0) continue;
+      const uint64_t win = sh[u] ? (lo[u] >> sh[u]) | (hi[u] << (64 - sh[u])) : lo[u];
+      const uint64_t acc = win & 0x5555555555555555ull;
+      if (!acc) { code[u] = -5; continue; }
+      delta[u] += __builtin_ctzll(acc);
+    }
+  }
+  }
+#pragma unroll
+  for (int u = 0; u < kPhiIlp; ++u) {
+    const int c = c0 + u * cstep;
+    if (c < a.Wc)
+      a.F[(int64_t)ts * a.Wc + c] = code[u] == 0 && delta[u] <= 0x7fffffff ? (int)delta[u] : (code[u] ? code[u] : -1);
   }
 }
 
-// The clusters' actual start drifts: delta_0 = 0, delta_{t+1} = F[t][delta_t - clo(t)]
-// (the table staged in LDS when it fits).
+// One walk segment of cluster t from drift `delta` by one thread, from global memory (a
+// segment after the first whose picks depend on the uniform, i.e. on the cluster's start
+// drift dt, which its table cannot index): the end drift, or < 0.
+__device__ int64_t phi_walk_serial(const PhiArgs& a, int t, int j0, int j1, int64_t dt, int64_t delta) {
+  const int d = a.d, nw = a.nw;
+  const int64_t base = (int64_t)t * 3 * d;
+  for (int j = j0; j < j1; ++j) {
+    const int64_t off = delta - phi_lo((int64_t)t * d + j, a.rate, a.sdev);
+    if (off < 0 || off >= 64 * (int64_t)(nw - 1)) return -4;
+    const int q = (int)(off >> 6), sh = (int)(off & 63);
+    const uint64_t* row;
+    if (a.det[(int64_t)t * d + j]) {
+      const int kd = a.ikind[(int64_t)t * d + j];
+      if (kd != 2 && kd != 3) return -3;
+      row = a.maskd + ((int64_t)t * d + j) * nw;
+    } else {
+      const int64_t pos = base + dt + j;
+      if (pos >= a.span) return -3;
+      const double rU = pool_unif(a.raw[pos]);
+      const int64_t cb = (int64_t)t * a.sumatt + a.aoff[j];
+      int s;
+      for (s = 0; s < a.att[j] - 1; ++s)
+        if (rU <= a.cum[cb + s]) break;
+      const int64_t ci = cb + a.perm[cb + s] - 1;
+      const int kd = a.cand[ci].kind;
+      if (kd != 2 && kd != 3) return -3;
+      row = a.mask + ci * nw;
+    }
+    const uint64_t lo = row[q], hi = row[q + 1];
+    const uint64_t win = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+    const uint64_t acc = win & 0x5555555555555555ull;
+    if (!acc) return -5;
+    delta += __builtin_ctzll(acc);
+  }
+  return delta;
+}
+
+// The segments' actual start drifts: delta_0 = 0, delta after segment (t, s) =
+// F[t S + s][delta - phi_lo(t d + s L)] (the table staged in LDS when it fits, many loads in
+// flight per thread); dts[t] = cluster t's start drift.
 __global__ __launch_bounds__(1024) void k_phi_chain(PhiArgs a) {
   if (a.gate && *(volatile const int*)a.gate == 0) return;
   if (a.raw_ptr) a.raw = *a.raw_ptr;
   extern __shared__ int sF[];
   if (*a.status != 0) return;
-  const int64_t nF = (int64_t)a.T * a.Wc;
+  const int64_t nF = (int64_t)a.T * a.S * a.Wc;
   const bool lds = nF <= 16384;
-  if (lds)
-    for (int64_t q = threadIdx.x; q < nF; q += blockDim.x) sF[q] = a.F[q];
+  if (lds) {
+    constexpr int U = 16;
+    for (int64_t q0 = (int64_t)threadIdx.x; q0 < nF; q0 += (int64_t)U * blockDim.x) {
+      int v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t q = q0 + (int64_t)u * blockDim.x;
+        v[u] = q < nF ? a.F[q] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t q = q0 + (int64_t)u * blockDim.x;
+        if (q < nF) sF[q] = v[u];
+      }
+    }
+  }
   __syncthreads();
   if (threadIdx.x != 0) return;
   const int* F = lds ? sF : a.F;
   int64_t delta = 0;
   for (int t = 0; t < a.T; ++t) {
     a.dts[t] = delta;
-    const int64_t c = delta - phi_clo(t, a);
-    if (c < 0 || c >= a.Wc) { set_status(a.status, kPhiWindow); return; }
-    const int e = F[(int64_t)t * a.Wc + c];
-    if (e < 0) { set_status(a.status, kPhiWindow); return; }
-    delta = e;
+    for (int sg = 0; sg < a.S; ++sg) {
+      const int64_t c = delta - phi_lo((int64_t)t * a.d + (int64_t)sg * a.L, a.rate, a.sdev);
+      if (c < 0 || c >= a.Wc) { set_status(a.status, kPhiWindow); return; }
+      int64_t e = F[((int64_t)t * a.S + sg) * a.Wc + c];
+      if (e == -2 && sg > 0) e = phi_walk_serial(a, t, sg * a.L, min(a.d, (sg + 1) * a.L), a.dts[t], delta);
+      if (e < 0) { set_status(a.status, kPhiWindow); return; }
+      delta = e;
+    }
   }
   const int64_t cons = (int64_t)a.T * 3 * a.d + delta;
   if (cons + 1 > a.span) set_status(a.status, kPhiShort);
   *(int64_t*)(a.status + 2) = cons;
   if (a.pos_out) *a.pos_out = *a.pos_in + a.sweep_len + cons;
-}
-
-// ------------------------------------------------------------------ pipelined iterations
-// The update after a pipelined sweep: its slice starts sweep_len draws after the sweep's
-// start; the window holding `need` words from there (kPhiShort when none does).
-__global__ void k_phi_locate(PipeArgs a) {
-  if (threadIdx.x != 0) return;
-  a.phi_status[0] = 0; a.phi_status[1] = 0; a.phi_status[2] = 0; a.phi_status[3] = 0;
-  *a.act = 0;
-  if (*(volatile const int*)a.gate == 0) return;
-  const int64_t p = *a.pos_in + a.sweep_len;
-  for (int w = 0; w < 2; ++w) {
-    const PipeWin& W = a.win[w];
-    if (W.raw && p >= W.start && p + a.need <= W.start + W.count) {
-      *a.raw_out = W.raw + (p - W.start);
-      return;
-    }
-  }
-  a.phi_status[0] = kPhiShort;
-  *a.raw_out = a.win[0].raw;
-}
-
-// The commit decision of a pipelined iteration: its sweep moved nothing (the dry resolver
-// finished it) and its update ran on the device.  Then the update's tables go to the slots
-// (commit_ok gates k_scatter_clusters), the record takes the log-likelihood and the next
-// sweep's start, and the next sweep's slice is located (none: the pipeline stops after
-// this iteration).  Otherwise the pipeline stops here and nothing is committed.
-__global__ void k_pipe_check(PipeArgs a) {
-  if (threadIdx.x != 0) return;
-  for (int q = 0; q < 6; ++q) a.rec[q] = 0;
-  *a.commit_ok = 0;
-  if (*(volatile const int*)a.gate == 0) { a.rec[0] = 2; return; }
-  // the resolver wrote the block to host memory: read it uncached, field by field
-  const volatile int* cv = reinterpret_cast<const volatile int*>(a.ctl);
-  const int c_next = cv[0], c_status = cv[1], c_restart = cv[2], c_moves = cv[5];
-  const int ps = a.phi_status[0];
-  a.rec[1] = c_status;
-  a.rec[4] = ps;
-  if (!(c_status == 0 && c_next >= a.n && c_moves == 0 && c_restart == 0 && ps == 0)) {
-    *a.gate = 0;
-    a.rec[0] = 3;
-    return;
-  }
-  *a.commit_ok = 1;
-  double hi = 0.0, lo = 0.0;
-  for (int t = 0; t < a.T; ++t)
-    for (int q = 0; q < 2; ++q) {
-      const double x = a.ll[2 * t + q], s = hi + x;
-      lo += fabs(hi) >= fabs(x) ? (hi - s) + x : (x - s) + hi;
-      hi = s;
-    }
-  const double ll = hi + lo;
-  a.rec[2] = __double_as_longlong(ll);
-  const int64_t p = *a.pos_next;
-  a.rec[3] = p;
-  a.rec[0] = 1;
-  for (int w = 0; w < 2; ++w) {
-    const PipeWin& W = a.win[w];
-    if (W.raw && p >= W.start && p + a.sweep_len <= W.start + W.count) {
-      *a.raw_out = W.raw + (p - W.start);
-      return;
-    }
-  }
-  *a.gate = 0;
-  a.rec[5] = 1;
-}
-
-hipError_t launch_phi_locate(const PipeArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_phi_locate, dim3(1), dim3(64), 0, s, a);
-  return hipGetLastError();
-}
-hipError_t launch_pipe_check(const PipeArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_pipe_check, dim3(1), dim3(64), 0, s, a);
-  return hipGetLastError();
 }
 
 // ------------------------------------------------------------------ values
@@ -818,7 +940,8 @@ __global__ __launch_bounds__(1024) void k_phi_values(PhiArgs a) {
 
 // dynamic LDS of k_phi_cwalk (cluster image + a pick row per wave) and k_phi_values
 // (cluster image + tables, positions, picks)
-size_t phi_cwalk_lds(int d, int nw, int wpb) { return phi_cluster_lds(d, nw) + (size_t)wpb * d; }
+size_t phi_cwalk_lds(int d, int nw, int wpb) { return phi_cwalk_image(d, nw) + 0 * (size_t)wpb; }
+int phi_ilp() { return kPhiIlp; }
 size_t phi_values_lds(int d, int nw) { return phi_cluster_lds(d, nw) + (size_t)d * (16 + 8 + 1); }
 
 hipError_t launch_phi(const PhiArgs& a, hipStream_t s) {
@@ -828,9 +951,10 @@ hipError_t launch_phi(const PhiArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_phi_prep, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_phi_logits, dim3((unsigned)std::min<int64_t>(1024, (a.span + 255) / 256)), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_phi_masks, dim3(1024), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(k_phi_cwalk, dim3((unsigned)(a.T * a.groups)), dim3(64 * a.wpb), phi_cwalk_lds(a.d, a.nw, a.wpb),
+  const int wthreads = std::min(1024, ((a.Wc + kPhiIlp * a.groups - 1) / (kPhiIlp * a.groups) + 63) / 64 * 64);
+  hipLaunchKernelGGL(k_phi_cwalk, dim3((unsigned)(a.T * a.S * a.groups)), dim3(wthreads), phi_cwalk_lds(a.d, a.nw, 16),
                      s, a);
-  const int64_t nF = (int64_t)a.T * a.Wc;
+  const int64_t nF = (int64_t)a.T * a.S * a.Wc;
   hipLaunchKernelGGL(k_phi_chain, dim3(1), dim3(1024), nF <= 16384 ? (size_t)nF * 4 : 0, s, a);
   hipLaunchKernelGGL(k_phi_values, dim3((unsigned)a.T), dim3(64 * a.wpb), phi_values_lds(a.d, a.nw), s, a);
   return hipGetLastError();
