@@ -320,6 +320,9 @@ def main():
     from split_and_merge_gibbs_sampling_amd.data import CONFIGS, config
 
     setup = rank_setup(rank, local)
+    # torch's device context now, not between the warmup and the timed iterations (creating
+    # it there idles the GPU and the host pool for a long stretch: a cold first timed window)
+    cuda_sync()
     t_setup = time.perf_counter()
     ds = config(args.config, n=args.n)
     eng = hd.Engine(setup["device"])
@@ -423,6 +426,10 @@ def main():
             "split_merge": bool(args.sm),
             "hig_logspace": hig_log,
             "rounds_per_step": st["rounds"] / args.steps,
+            # next sweeps enqueued while the update was drawn / run (engine pre_enqueue), and
+            # update stream slices found in a copy made an iteration ahead
+            "pipeline": {"enqueued": st["pipe_enqueued"], "ran": st["pipe_runs"],
+                         "slice_lookahead_hits": st["phi_lookahead_hits"]},
             "rng_windows": {"launched": st["rng_windows"], "fresh": st["rng_windows_fresh"]},
             "pool_generation": {"init": pool_report(st_init, ds.n * args.m),
                                 "regeneration": pool_report(stats_diff(st0, st_init), ds.n * args.m)},

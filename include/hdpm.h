@@ -71,6 +71,10 @@ typedef struct {
      * handed back to the host (a case it does not restate: Walker, rhig's bisection path, a
      * drift outside its window, ...); the status of the last one (PhiStatus, 0 = ok) */
     int64_t phi_device_calls, phi_device_fallbacks, phi_device_last_status;
+    /* update stream slices found in a copy made an iteration ahead, and such copies made */
+    int64_t phi_lookahead_hits, phi_lookahead_copies;
+    /* next sweeps enqueued before the iteration's update was joined, and those that ran */
+    int64_t pipe_enqueued, pipe_runs;
 } hdpm_stats;
 
 int         hdpm_device_count(void);
@@ -170,7 +174,12 @@ int hdpm_reset_stats(hdpm_ctx* ctx);
  * generator windows); bit 17: a sweep prepared at the end of hdpm_iterations does not start
  * its prepass on the device; bit 18: the prepass certifies "stay" by the margin only (not by
  * the draw's uniform, kernels.hip stay_by_uniform); bit 19: update_phi on the host (the job
- * speculated during the sweep) instead of the device (csrc/phi.hip; also HDPM_PHI=host). */
+ * speculated during the sweep) even when the device update is selected (HDPM_OPT_PHI_DEVICE
+ * or HDPM_PHI=device; csrc/phi.hip); bit 20: no lookahead copy of the next update's stream
+ * slice (it is copied when the next sweep's draws are reserved); bit 21: the iteration
+ * commits the new tables and computes the log-likelihood before it prepares the next sweep
+ * (by default the next speculative update_phi is started first); bit 22: no next sweep
+ * enqueued while the iteration's update is drawn (gated on the device, k_pipe_wait). */
 int hdpm_set_debug(hdpm_ctx* ctx, int32_t mode);
 /* The prepass's pool-entry heads, P entries of wb*Ws + 2 words padded to a power of two
  * (Ws <= 4) or to a multiple of 8 words (wide layouts) (csrc/kernels.hpp "Pool-entry heads",

@@ -61,7 +61,8 @@ class Stats(C.Structure):
         [(n, C.c_int64) for n in ("phi_spec_runs", "phi_spec_clusters", "prepass_timed", "prepass_timed_points",
                                   "rng_windows", "rng_windows_fresh", "listed_points", "sm_moves")] + \
         [(n, C.c_double) for n in ("t_sm_ms", "t_sm_scan_ms", "t_sm_phi_ms", "t_sm_terms_ms")] + \
-        [(n, C.c_int64) for n in ("phi_device_calls", "phi_device_fallbacks", "phi_device_last_status")]
+        [(n, C.c_int64) for n in ("phi_device_calls", "phi_device_fallbacks", "phi_device_last_status",
+                                  "phi_lookahead_hits", "phi_lookahead_copies", "pipe_enqueued", "pipe_runs")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

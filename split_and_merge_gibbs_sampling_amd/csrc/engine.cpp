@@ -16,6 +16,7 @@
 #include <mutex>
 #include <pthread.h>
 #include <sched.h>
+#include <dirent.h>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -49,6 +50,8 @@ hipError_t launch_scatter_clusters(const uint8_t* stage, int nent, int dp, int d
                                    double* tab, uint64_t* bnd, int* counts, int* sol, int* los, int* src,
                                    hipStream_t s, const int* gate = nullptr);
 hipError_t launch_phi_locate(const PipeArgs& a, hipStream_t s);
+hipError_t launch_pipe_wait(const PipeSlot* slot, const ResolveCtl* prev, ResolveCtl* own, int n, PipeGate* g,
+                            long long limit, hipStream_t s);
 hipError_t launch_pipe_check(const PipeArgs& a, hipStream_t s);
 hipError_t launch_pool_heads(const double* tab, const uint64_t* bnd, int64_t P, int d, int wb, int Ws, int bw, int ha,
                              int hb, uint64_t* head, hipStream_t s);
@@ -422,11 +425,47 @@ static std::vector<int> gpu_home_domain(int device) {
   const std::vector<int> mine = local_list(device);
   if (mine.empty()) return none;
   int slot = 0, share = 0;
-  for (int d2 = 0; d2 < cnt; ++d2)
-    if (local_list(d2) == mine) {
-      if (d2 < device) ++slot;
-      ++share;
+  // this GPU's rank among all the node's AMD accelerators with the same local CPUs (sysfs:
+  // also the ones this process cannot see, so processes on different GPUs of a node pick
+  // different domains even when each sees only its own), else among the visible ones
+  {
+    char bus[64] = {0};
+    std::vector<std::string> peers;
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) == hipSuccess) {
+      for (char* p = bus; *p; ++p) *p = (char)std::tolower((unsigned char)*p);
+      if (DIR* dir = opendir("/sys/bus/pci/devices")) {
+        while (dirent* e = readdir(dir)) {
+          if (e->d_name[0] == '.') continue;
+          const std::string dev = std::string("/sys/bus/pci/devices/") + e->d_name;
+          char vendor[16] = {0}, cls[16] = {0};
+          FILE* f = std::fopen((dev + "/vendor").c_str(), "r");
+          if (!f) continue;
+          const bool okv = std::fgets(vendor, sizeof(vendor), f) != nullptr;
+          std::fclose(f);
+          f = std::fopen((dev + "/class").c_str(), "r");
+          if (!f) continue;
+          const bool okc = std::fgets(cls, sizeof(cls), f) != nullptr;
+          std::fclose(f);
+          if (!okv || !okc || std::strncmp(vendor, "0x1002", 6) != 0) continue;
+          if (std::strncmp(cls, "0x1200", 6) != 0 && std::strncmp(cls, "0x0380", 6) != 0) continue;
+          if (read_cpu_list(dev + "/local_cpulist") == mine) peers.push_back(e->d_name);
+        }
+        closedir(dir);
+      }
     }
+    std::sort(peers.begin(), peers.end());
+    for (size_t q = 0; q < peers.size(); ++q)
+      if (peers[q] == bus) {
+        slot = (int)q;
+        share = (int)peers.size();
+      }
+  }
+  if (share == 0)
+    for (int d2 = 0; d2 < cnt; ++d2)
+      if (local_list(d2) == mine) {
+        if (d2 < device) ++slot;
+        ++share;
+      }
   cpu_set_t allowed;
   if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return none;
   std::vector<std::vector<int>> doms;
@@ -507,6 +546,7 @@ struct RngWindow {
   int64_t export_after = 0;
   hipEvent_t done = nullptr;
   bool valid = false;
+  uint64_t gen = 0;                     // launches of this window (a pipelined sweep waited on one)
 };
 
 struct Ctx {
@@ -520,9 +560,21 @@ struct Ctx {
     uint64_t pos = 0, epoch = 0;
     int mti = 0;
     int64_t N = 0;
-    hipEvent_t ev = nullptr;
-    PinBuf<uint32_t> raw;
+    hipEvent_t ev = nullptr;           // the copy of the slice holding it
+    const uint32_t* blk = nullptr;     // tempered words from the start of the state's block
   } phidev;
+  // Host copies of stretches of the device windows (a ring): the slice of the next update,
+  // or one fetched an iteration ahead (phi_lookahead) so that the next one needs no copy.
+  struct PhiSlice {
+    PinBuf<uint32_t> buf;
+    hipEvent_t ev = nullptr;
+    uint64_t s0 = 0, epoch = ~0ull, stamp = 0;
+    int64_t words = 0;
+    bool valid = false;
+  } phis[3];
+  uint64_t phis_clock = 0;
+  uint64_t look_from = 0;              // the stretch the next lookahead copies (0: none)
+  int64_t look_words = 0;
   RngWindow win[2];
   // MT jump-ahead for multi-workgroup windows (mtjump.hpp)
   int mt_G = 0, mt_bpg = 0;
@@ -643,15 +695,38 @@ struct Ctx {
   DevBuf<uint64_t> d_csum;            // per-label cluster summary for the prepass
   DevBuf<unsigned> d_hist_part;
   DevBuf<long long> d_rprof;          // resolver phase times (debug mode bit 1)
-  PinBuf<int> h_ctl;                  // [ResolveCtl | pad to kCtlInts][resolver summary: 3 scap]
+  PinBuf<int> h_ctl;                  // two blocks [ResolveCtl | pad to kCtlInts][resolver summary: 3 scap]
+  // Consecutive sweeps alternate between the two control blocks (and resolver events), so a
+  // sweep enqueued ahead (pre_enqueue) does not overwrite the one the host is reading.
+  int par = 0;
+  hipEvent_t ev_res[2] = {nullptr, nullptr};
+  size_t ctl_stride() const { return kCtlInts + 3 * (size_t)scap; }
+  ResolveCtl* ctl_at(int q) { return reinterpret_cast<ResolveCtl*>(h_ctl.p + (size_t)q * ctl_stride()); }
+  // The next sweep enqueued before this iteration's update is joined (pre_enqueue): its
+  // kernels wait on the device (k_pipe_wait) for the host's go (pipe_go) or abort
+  // (pre_release); slots in host-coherent memory, gates on the device.
+  PinBuf<PipeSlot> h_pipe;
+  DevBuf<PipeGate> d_pipe;
+  struct PreSweep {
+    bool active = false;
+    bool round_ok = false;             // round 0 was enqueued
+    int par = 0, buf = -1, m = 0;
+    bool track = false;
+    uint64_t gen[2] = {0, 0};          // window launches the kernels waited for
+  } pre;
+  bool deep_ok = false;                // set by iteration(): the next sweep may be enqueued ahead
   static constexpr size_t kCtlInts = 16;
   static_assert(sizeof(ResolveCtl) <= kCtlInts * sizeof(int), "control block");
   // cluster parameter upload staging (UploadLayout)
   // two pinned staging buffers: one can be filled (e.g. by the update_phi speculated for the
   // next sweep) while the last commit's copy from the other is still in flight
-  PinBuf<uint8_t> h_stage_buf[2];
-  hipEvent_t ev_stage_buf[2] = {nullptr, nullptr};
+  PinBuf<uint8_t> h_stage_buf[3];
+  hipEvent_t ev_stage_buf[3] = {nullptr, nullptr, nullptr};
   int stage_fill = 0, stage_last = 1;   // buffer being filled / last committed
+  int stage_hold = -1;                  // filled by the speculative update_phi, not yet committed
+  // the new tables of a full update_phi, committed after the next speculative update_phi is
+  // started (flush_commit): buffer, entries
+  struct { bool active = false; int buf = 0, nent = 0; } commit_later;
   DevBuf<uint8_t> d_stage;
 
   // statistics buffers.  d_freq holds freq[slot][j][level] and, while freq_dev_valid,
@@ -678,6 +753,9 @@ struct Ctx {
   int64_t launch_count = 0;           // resolver launches issued (prepass timing cadence)
   bool round_timed = false, round_fine = false;
   int64_t round_points = 0;
+  // prepass timing of a sweep enqueued ahead (per control block: read one iteration later)
+  bool pre_timed[2] = {false, false};
+  hipEvent_t ev_pp[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
   int debug = 0;
   // debug bit 1: per-iteration host timeline
   std::vector<std::pair<const char*, std::chrono::steady_clock::time_point>> trace;
@@ -687,6 +765,17 @@ struct Ctx {
   // debug bit 5: accumulate the per-iteration timeline (no extra synchronisation); printed
   // by the context's destructor
   std::vector<std::pair<std::string, double>> trace_sum;
+  std::vector<std::vector<float>> trace_smp;   // per trace_sum entry: the samples (median / p90)
+  void trace_add(const std::string& name, double us) {
+    size_t q = 0;
+    while (q < trace_sum.size() && trace_sum[q].first != name) ++q;
+    if (q == trace_sum.size()) {
+      trace_sum.emplace_back(name, 0.0);
+      trace_smp.emplace_back();
+    }
+    trace_sum[q].second += us;
+    trace_smp[q].push_back((float)us);
+  }
   int64_t trace_iters = 0, trace_alloc0 = -1;
   std::unordered_map<uint64_t, bool> beta_cache;
 
@@ -701,18 +790,32 @@ struct Ctx {
     } catch (...) {
     }
     if (trace_iters > 0) {
-      std::string line = "[timeline] mean us/iteration:";
-      for (auto& kv : trace_sum) {
-        char buf[96];
-        std::snprintf(buf, sizeof(buf), " %s %.1f", kv.first.c_str(), kv.second / trace_iters);
+      std::string line = "[timeline] us/iteration, mean [median p90]:";
+      for (size_t q = 0; q < trace_sum.size(); ++q) {
+        std::vector<float> v = trace_smp[q];
+        std::sort(v.begin(), v.end());
+        char buf[128];
+        std::snprintf(buf, sizeof(buf), " %s %.1f [%.1f %.1f]", trace_sum[q].first.c_str(),
+                      trace_sum[q].second / trace_iters, v.empty() ? 0.0 : v[v.size() / 2],
+                      v.empty() ? 0.0 : v[v.size() * 9 / 10]);
         line += buf;
       }
+      for (size_t q = 0; q < trace_sum.size(); ++q)
+        if (trace_sum[q].first == "total") {
+          line += "; totals in order:";
+          for (size_t k = 0; k < trace_smp[q].size() && k < 40; ++k) {
+            char buf[32];
+            std::snprintf(buf, sizeof(buf), " %.0f", trace_smp[q][k]);
+            line += buf;
+          }
+        }
       std::fprintf(stderr, "%s (%lld iterations, %lld device allocations after the first)\n", line.c_str(),
                    (long long)trace_iters, (long long)(g_dev_allocs.load() - trace_alloc0));
     }
     if (cstream) {
       (void)hipStreamSynchronize(cstream);
-      if (phidev.ev) (void)hipEventDestroy(phidev.ev);
+      for (auto& sl : phis)
+        if (sl.ev) (void)hipEventDestroy(sl.ev);
       (void)hipStreamDestroy(cstream);
     }
     if (gstream) {
@@ -727,6 +830,11 @@ struct Ctx {
       for (auto& e : ev) (void)hipEventDestroy(e);
       for (auto& e : ev_stage_buf)
         if (e) (void)hipEventDestroy(e);
+      for (auto& e : ev_res)
+        if (e) (void)hipEventDestroy(e);
+      for (auto& pe : ev_pp)
+        for (auto& e : pe)
+          if (e) (void)hipEventDestroy(e);
       (void)hipStreamDestroy(stream);
     }
   }
@@ -766,7 +874,8 @@ struct Ctx {
   // a generator launch may overwrite buffers the copy stream still reads
   void gstream_after_copies() {
     if (pend.ev) HIPCHK(hipStreamWaitEvent(gstream, pend.ev, 0));
-    if (phidev.ev) HIPCHK(hipStreamWaitEvent(gstream, phidev.ev, 0));
+    for (auto& sl : phis)
+      if (sl.ev) HIPCHK(hipStreamWaitEvent(gstream, sl.ev, 0));
   }
   void run_window(RngWindow& W) {
     ensure_jump(W.count);
@@ -775,6 +884,7 @@ struct Ctx {
                 multi ? d_jpoly.p : nullptr, d_jidx.p, d_joff.p, mt_bpg, multi ? mt_G : 1};
     HIPCHK(launch_mt_gen(a, gstream));
     HIPCHK(hipEventRecord(W.done, gstream));
+    W.gen++;
     stats.rng_windows++;
     W.valid = true;
   }
@@ -962,25 +1072,73 @@ struct Ctx {
     if (blk == 0 || mti < 1) return false;
     const uint64_t s_blk = target - (uint64_t)mti;              // first word of the state's block
     const int64_t words = 624 * ((mti + N - 1) / 624 + 1);       // through the block of word N - 1
-    if (s_blk < W.start_pos || s_blk + (uint64_t)words > W.start_pos + (uint64_t)W.count) return false;
-    // with headroom: a pinned reallocation (hipHostFree) would synchronise the device
-    if (phidev.raw.n < (size_t)words) phidev.raw.ensure(std::max<size_t>(2 * (size_t)words, 1 << 15));
-    if (!phidev.ev) HIPCHK(hipEventCreateWithFlags(&phidev.ev, hipEventDisableTiming));
-    HIPCHK(hipStreamWaitEvent(cstream, W.done, 0));
-    HIPCHK(hipMemcpyAsync(phidev.raw.p, W.raw.p + (s_blk - W.start_pos), (size_t)words * 4, hipMemcpyDeviceToHost,
-                          cstream));
-    HIPCHK(hipEventRecord(phidev.ev, cstream));
+    PhiSlice* hit = nullptr;
+    for (auto& sl : phis)
+      if (sl.valid && sl.epoch == rng.epoch && sl.s0 <= s_blk && s_blk + (uint64_t)words <= sl.s0 + (uint64_t)sl.words)
+        hit = &sl;
+    if (hit) {
+      stats.phi_lookahead_hits++;
+    } else {
+      if (s_blk < W.start_pos || s_blk + (uint64_t)words > W.start_pos + (uint64_t)W.count) return false;
+      hit = phi_slice_copy(W, s_blk, words, nullptr);
+    }
+    hit->stamp = ++phis_clock;
     phidev.valid = true;
     phidev.pos = target;
     phidev.epoch = rng.epoch;
     phidev.mti = mti;
     phidev.N = N;
+    phidev.ev = hit->ev;
+    phidev.blk = hit->buf.p + (s_blk - hit->s0);
     // the host stream continues at target: its state arrives with the copy
     pend.active = true;
-    pend.from_raw = phidev.raw.p;
+    pend.from_raw = phidev.blk;
     pend.mti = mti;
     rng.pos = target;
     return true;
+  }
+  // Words [s0, s0 + words) of window W into the least recently used ring slot other than
+  // `keep` (asynchronous, on the copy stream).
+  PhiSlice* phi_slice_copy(const RngWindow& W, uint64_t s0, int64_t words, const PhiSlice* keep) {
+    PhiSlice* sl = nullptr;
+    for (auto& c : phis)
+      if (&c != keep && (!sl || c.stamp < sl->stamp)) sl = &c;
+    // with headroom: a pinned reallocation (hipHostFree) would synchronise the device
+    if (sl->buf.n < (size_t)words) {
+      if (sl->ev) HIPCHK(hipEventSynchronize(sl->ev));
+      sl->buf.ensure(std::max<size_t>(2 * (size_t)words, 1 << 15));
+    }
+    if (!sl->ev) HIPCHK(hipEventCreateWithFlags(&sl->ev, hipEventDisableTiming));
+    HIPCHK(hipStreamWaitEvent(cstream, W.done, 0));
+    HIPCHK(hipMemcpyAsync(sl->buf.p, W.raw.p + (s0 - W.start_pos), (size_t)words * 4, hipMemcpyDeviceToHost, cstream));
+    HIPCHK(hipEventRecord(sl->ev, cstream));
+    sl->valid = true;
+    sl->s0 = s0;
+    sl->words = words;
+    sl->epoch = rng.epoch;
+    sl->stamp = ++phis_clock;
+    return sl;
+  }
+  // The stretch device_draws noted for the next update's slice (the draws of the next sweep
+  // after at most a slice's worth of this update's), copied now: off the iteration's
+  // critical path, and landed by the time the next sweep's draws are reserved.
+  void phi_lookahead() {
+    if (!look_from || (debug & 1048576)) return;
+    const uint64_t from = look_from;
+    look_from = 0;
+    for (auto& sl : phis)
+      if (sl.valid && sl.epoch == rng.epoch && sl.s0 <= from && from + (uint64_t)look_words <= sl.s0 + (uint64_t)sl.words)
+        return;
+    for (auto& W : win)
+      if (W.valid && W.epoch == rng.epoch && W.start_pos <= from &&
+          from + (uint64_t)look_words <= W.start_pos + (uint64_t)W.count) {
+        const PhiSlice* keep = nullptr;
+        for (auto& sl : phis)
+          if (phidev.valid && sl.valid && phidev.blk >= sl.buf.p && phidev.blk < sl.buf.p + sl.words) keep = &sl;
+        (void)phi_slice_copy(W, from, look_words, keep);
+        stats.phi_lookahead_copies++;
+        return;
+      }
   }
 
   // Device pointer to the next n raw draws of the stream; advances the host stream past
@@ -1011,6 +1169,10 @@ struct Ctx {
     const uint32_t* p = W->raw.p + (rng.pos - W->start_pos);
     const uint64_t target = rng.pos + n;
     if (!phi_device_prefetch(*W, target, phi_prefetch)) adopt_state_at(*W, target);
+    // the next sweep's update slice starts after this update's draws (at most about a
+    // slice) and the next sweep's n: fetched ahead by phi_lookahead
+    look_from = target + (uint64_t)n > 624 ? target + (uint64_t)n - 624 : 0;
+    look_words = 2 * phi_prefetch + 3 * 624;
     RngWindow* other = (W == &win[0]) ? &win[1] : &win[0];
     const bool ahead = other->valid && other->epoch == rng.epoch && other->start_pos > W->start_pos;
     const uint64_t wend = W->start_pos + (uint64_t)W->count;
@@ -1082,12 +1244,23 @@ struct Ctx {
   // stage_commit (copy + scatter).
   UploadLayout stage_begin(int nent) {
     const UploadLayout L = upload_layout(nent, dp, d, bw);
-    stage_fill = 1 - stage_last;
+    auto pick = [&] {
+      int f = 0;
+      while (f < 3 && (f == stage_last || f == stage_hold || (commit_later.active && f == commit_later.buf))) ++f;
+      return f;
+    };
+    int f = pick();
+    if (f >= 3) {                                   // a commit deferred and another update held
+      flush_commit();
+      f = pick();
+    }
+    stage_fill = f;
     hipEvent_t& ev = ev_stage_buf[stage_fill];
     if (!ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     HIPCHK(hipEventSynchronize(ev));                // the upload before last has left this buffer
     PinBuf<uint8_t>& hb = h_stage_buf[stage_fill];
-    if (hb.n < L.bytes) hb.ensure(L.bytes + L.bytes / 2 + 4096);
+    // coherent: a sweep enqueued ahead scatters from it in place (pre_enqueue)
+    if (hb.n < L.bytes) hb.ensure(L.bytes + L.bytes / 2 + 4096, hipHostMallocCoherent);
     d_stage.ensure(L.bytes);
     return L;
   }
@@ -1101,12 +1274,21 @@ struct Ctx {
     ((int*)(st + L.off_slot))[r] = k;
   }
   void stage_commit(const UploadLayout& L, int nent, bool full) {
+    if (stage_hold == stage_fill) stage_hold = -1;
     HIPCHK(hipMemcpyAsync(d_stage.p, stage_ptr(), L.bytes, hipMemcpyHostToDevice, stream));
     HIPCHK(hipEventRecord(ev_stage_buf[stage_fill], stream));
     stage_last = stage_fill;
     stage_full = full;
     HIPCHK(launch_scatter_clusters(d_stage.p, nent, dp, d, bw, full ? 1 : 0, d_slot_codes.p, d_slot_tab.p,
                                    d_slot_bnd.p, d_counts.p, d_sol.p, d_los.p, d_src.p, stream));
+  }
+
+  bool defer_commit = false;           // set by iteration() around its update_phi
+  void flush_commit() {
+    if (!commit_later.active) return;
+    commit_later.active = false;
+    stage_fill = commit_later.buf;
+    stage_commit(upload_layout(commit_later.nent, dp, d, bw), commit_later.nent, true);
   }
 
   void stage_upload(const std::vector<int>* which) {
@@ -1607,14 +1789,20 @@ struct Ctx {
   // a prepared sweep can start on the device and still be dropped), kRoundResolve (the rest,
   // after a prefix launched with the same arguments and no state change in between).
   enum { kRoundAll = 0, kRoundPrefix = 1, kRoundResolve = 2 };
-  int launch_round(int p, int nslots, int m, const uint32_t* d_sweep_raw, bool track, int part = kRoundAll) {
+  // pg: a sweep enqueued ahead (pre_enqueue) -- its kernels take the gate and the draws
+  // from pg, its control block is cpar; no timing events, no counters.
+  int launch_round(int p, int nslots, int m, const uint32_t* d_sweep_raw, bool track, int part = kRoundAll,
+                   PipeGate* pg = nullptr, int cpar = -1) {
     const double dmax = 0.25;
+    if (cpar < 0) cpar = par;
     ensure_slots(nslots + 2);
     // the resolver writes its control block and summary straight into host memory
-    if (h_ctl.n < kCtlInts + 3 * (size_t)scap) h_ctl.ensure(kCtlInts + 3 * (size_t)scap, hipHostMallocCoherent);
+    if (h_ctl.n < 2 * ctl_stride()) h_ctl.ensure(2 * ctl_stride(), hipHostMallocCoherent);
+    for (auto& e : ev_res)
+      if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     // HIP events between kernels cost a dispatch gap each: the prepass is timed on every
     // 8th launch (all launches, and the other kernels too, in the diagnostic modes)
-    if (part != kRoundResolve) {
+    if (part != kRoundResolve && !pg) {
       round_fine = (debug & (2 | 32 | 512)) != 0;
       round_timed = round_fine || (launch_count++ % 8 == 0);
     }
@@ -1626,8 +1814,8 @@ struct Ctx {
     const int E = K + m;
     const double T = 54.0 * M_LN2 + std::log((double)E) + 0.5;
     PrepassArgs pa;
-    pa.gate = nullptr;
-    pa.raw_ptr = nullptr;
+    pa.gate = pg ? &pg->gate : nullptr;
+    pa.raw_ptr = pg ? &pg->raw : nullptr;
     pa.codes_t = d_codes_t.p; pa.n = n; pa.d = d; pa.nq = nq;
     pa.c = d_c.p; pa.counts = d_counts.p; pa.slot_of_label = d_sol.p; pa.K = K; pa.S = S;
     pa.slots = ParamTables{d_slot_codes.p, d_slot_tab.p};
@@ -1661,20 +1849,30 @@ struct Ctx {
       mcount_clear = false;
     }
     const int nblocks = (n - p + kBlock - 1) / kBlock;
+    const bool timed = round_timed && !pg, fine = round_fine && !pg;
+    if (pg) {
+      pre_timed[cpar] = launch_count++ % 8 == 0;
+      for (auto& e : ev_pp[cpar])
+        if (!e) HIPCHK(hipEventCreate(&e));
+    }
     if (part != kRoundResolve) {
       HIPCHK(launch_cluster_summary(pa, stream));
-      if (round_timed) HIPCHK(hipEventRecord(ev[0], stream));
+      if (timed) HIPCHK(hipEventRecord(ev[0], stream));
+      if (pg && pre_timed[cpar]) HIPCHK(hipEventRecord(ev_pp[cpar][0], stream));
       HIPCHK(launch_prepass(pa, nblocks, stream));
-      stats.prepass_points += n - p;
-      round_points = n - p;
-      if (round_timed) HIPCHK(hipEventRecord(ev[1], stream));
+      if (!pg) {
+        stats.prepass_points += n - p;
+        round_points = n - p;
+      }
+      if (timed) HIPCHK(hipEventRecord(ev[1], stream));
+      if (pg && pre_timed[cpar]) HIPCHK(hipEventRecord(ev_pp[cpar][1], stream));
       HIPCHK(launch_exact_rows(pa, nblocks, stream));
-      if (round_fine) HIPCHK(hipEventRecord(ev[5], stream));
+      if (fine) HIPCHK(hipEventRecord(ev[5], stream));
     }
 
     ResolveArgs ra;
-    ra.gate = nullptr;
-    ra.raw_ptr = nullptr;
+    ra.gate = pa.gate;
+    ra.raw_ptr = pa.raw_ptr;
     ra.dry = 0;
     ra.n = n; ra.d = d; ra.dp = dp; ra.m = m; ra.P = P;
     ra.c = d_c.p; ra.counts = d_counts.p; ra.slot_of_label = d_sol.p; ra.label_of_slot = d_los.p;
@@ -1687,13 +1885,13 @@ struct Ctx {
     ra.rq = pa.rq;
     ra.nblocks = nblocks; ra.p0 = p; ra.T = T; ra.dmax = dmax; ra.scap = scap; ra.K = K;
     ra.lcap = std::min(scap, nslots + 2);
-    ra.nslots = nslots; ra.ctl = (ResolveCtl*)h_ctl.p; ra.summary = h_ctl.p + kCtlInts; ra.force_exact = (debug & 1);
+    ra.nslots = nslots; ra.ctl = ctl_at(cpar); ra.summary = (int*)ctl_at(cpar) + kCtlInts; ra.force_exact = (debug & 1);
     ra.prof = nullptr;
     ra.mlog = track ? d_mlog.p : nullptr;
     ra.mcount = track ? d_mcount.p : nullptr;
     ra.freq = track ? d_freq.p : nullptr;
     ra.fstride = d * mmax;
-    if (debug & 2) {
+    if ((debug & 2) && !pg) {
       d_rprof.ensure(16);
       ra.prof = d_rprof.p;
     }
@@ -1708,8 +1906,8 @@ struct Ctx {
     }
     if (part == kRoundPrefix) return kOk;
     HIPCHK(launch_resolve(ra, stream));
-    if (round_fine) HIPCHK(hipEventRecord(ev[2], stream));
-    HIPCHK(hipEventRecord(ev[6], stream));
+    if (fine) HIPCHK(hipEventRecord(ev[2], stream));
+    HIPCHK(hipEventRecord(ev_res[cpar], stream));
     return kOk;
   }
 
@@ -1718,7 +1916,7 @@ struct Ctx {
   // applied to the frequency tables and these re-indexed to labels (copied out behind),
   // identity slot maps.  The kernels read the final launch's control block in host memory.
   void launch_sweep_end(int nslots, bool track) {
-    const ResolveCtl* hctl = (const ResolveCtl*)h_ctl.p;
+    const ResolveCtl* hctl = ctl_at(par);
     HIPCHK(launch_relabel(d_c.p, d_los.p, n, hctl, stream));
     if (track) {
       HIPCHK(launch_apply_moves(d_mlog.p, d_mcount.p, (int)std::min<int64_t>(n, 4096), d_codes_t.p, d, nq, mmax,
@@ -1745,6 +1943,8 @@ struct Ctx {
     bool launched = false;             // round 0 of the sweep is already on the device
     bool prefix = false;               // round 0's prepass part is on the device (droppable)
     bool track = false;
+    int par = 0;                       // control block of the prepared sweep
+    bool piped = false;                // enqueued ahead (pre_enqueue / pipe_go)
   } ahead;
 
   // With `launch` (only when the caller runs the sweep next, no other call in between:
@@ -1762,6 +1962,7 @@ struct Ctx {
     ahead.lv = labels_version;
     ahead.launched = false;
     ahead.prefix = false;
+    ahead.piped = false;
     ahead.active = true;
     // the speculative update_phi first: its serial draws, not the device sweep, are the
     // longer path (timeline: launching the sweep first cost ~8% of the iteration rate);
@@ -1771,7 +1972,10 @@ struct Ctx {
       spec_launch();
       mark("ahead.spec");
     }
+    flush_commit();                       // this iteration's tables, before the sweep that reads them
     if (resolve_smem_bytes(std::min(scap, K + 2), m, K + m <= 64 ? 1 : 0) <= 160 * 1024) {
+      par ^= 1;                           // the prepared sweep's control block
+      ahead.par = par;
       ahead.track = freq_dev_valid;
       sweep_buffers(ahead.track);
       mark("ahead.buf");
@@ -1791,6 +1995,7 @@ struct Ctx {
     }
   }
   void cancel_ahead() {
+    pre_release();
     if (!ahead.active) return;
     ahead.active = false;
     if (ahead.launched) {
@@ -1806,6 +2011,95 @@ struct Ctx {
     phi_stream.n = 0;
     pend.active = false;
     rng = ahead.saved;
+  }
+
+  int last_sweep_rounds = 0, last_sweep_moves = -1;   // of the last sweep (pipe_go)
+
+  // The next sweep, enqueued while the speculative update_phi of this one runs (its tables
+  // are that update's, from the held staging buffer): a wait kernel, the tables' copy and
+  // scatter, round 0 -- all gated on the device by k_pipe_wait.  The host decides after this
+  // iteration's update_phi: pipe_go (the sweep completed in its one launch without a move
+  // and the update came whole from the speculation) or pre_release.
+  void pre_enqueue(int m, bool track) {
+    const int q = 1 - par;
+    // every buffer sized before the wait kernel is queued (a reallocation would synchronise)
+    if (h_pipe.n < 2) h_pipe.ensure(2, hipHostMallocCoherent);
+    d_pipe.ensure(2);
+    sweep_buffers(track);
+    __atomic_store_n(&h_pipe.p[q].flag, 0, __ATOMIC_RELEASE);
+    h_pipe.p[q].raw = nullptr;
+    for (int k = 0; k < 2; ++k) {
+      pre.gen[k] = ~0ull;
+      if (win[k].valid && win[k].epoch == rng.epoch) {
+        HIPCHK(hipStreamWaitEvent(stream, win[k].done, 0));
+        pre.gen[k] = win[k].gen;
+      }
+    }
+    HIPCHK(launch_pipe_wait(&h_pipe.p[q], ctl_at(par), ctl_at(q), n, &d_pipe.p[q], 200000000LL, stream));
+    pre.active = true;
+    pre.par = q;
+    pre.buf = spec.stage_buf;
+    pre.m = m;
+    pre.track = track;
+    pre.round_ok = false;
+    // the scatter reads the staging buffer in host memory directly (no copy-engine hops
+    // between the wait kernel and the sweep)
+    HIPCHK(launch_scatter_clusters(h_stage_buf[pre.buf].p, K, dp, d, bw, 1, d_slot_codes.p, d_slot_tab.p, d_slot_bnd.p,
+                                   d_counts.p, d_sol.p, d_los.p, d_src.p, stream, &d_pipe.p[q].gate));
+    HIPCHK(hipEventRecord(ev_stage_buf[pre.buf], stream));
+    pre.round_ok = launch_round(0, K, m, nullptr, track, kRoundAll, &d_pipe.p[q], q) == kOk;
+    stats.pipe_enqueued++;
+  }
+  void pre_release() {
+    if (!pre.active) return;
+    pre.active = false;
+    __atomic_store_n(&h_pipe.p[pre.par].flag, 2, __ATOMIC_RELEASE);
+  }
+  // Go for the sweep enqueued ahead: its draws reserved and handed over, its tables (the
+  // update's held staging buffer) become the committed ones, the next speculative update
+  // started.  False (nothing done) when it cannot run.
+  bool pipe_go(int m) {
+    if (!pre.active || !pre.round_ok || pre.m != m || !commit_later.active || commit_later.buf != pre.buf ||
+        last_sweep_rounds != 1 || last_sweep_moves != 0 || !host_spec() || tables_dirty)
+      return false;
+    if (!(freq_dev_valid && freq_version == labels_version)) return false;
+    rng_sync();
+    const Rng saved = rng;
+    const uint32_t* raw = device_draws((int64_t)n * (m + 1));
+    bool waited = false;
+    for (int k = 0; k < 2; ++k)
+      if (win[k].gen == pre.gen[k] && raw >= win[k].raw.p && raw < win[k].raw.p + win[k].count) waited = true;
+    if (!waited) {                       // a window the enqueued kernels did not wait for
+      pend.active = false;
+      phidev.valid = false;
+      rng = saved;
+      return false;
+    }
+    PipeSlot& sl = h_pipe.p[pre.par];
+    __atomic_store_n(&sl.raw, raw, __ATOMIC_RELAXED);
+    __atomic_store_n(&sl.flag, 1, __ATOMIC_RELEASE);
+    pre.active = false;
+    mark("go");
+    ahead.saved = saved;
+    ahead.raw = raw;
+    ahead.m = m;
+    ahead.lv = labels_version;
+    ahead.launched = true;
+    ahead.prefix = false;
+    ahead.track = pre.track;
+    ahead.par = pre.par;
+    ahead.piped = true;
+    ahead.active = true;
+    stats.prepass_points += n;
+    stats.pipe_runs++;
+    // the tables of this iteration: copied and scattered by the enqueued kernels
+    commit_later.active = false;
+    stage_last = pre.buf;
+    stage_full = true;
+    if (stage_hold == pre.buf) stage_hold = -1;
+    spec_launch();
+    mark("ahead.spec");
+    return true;
   }
 
   int neal8_sweep(int m) {
@@ -1851,6 +2145,9 @@ struct Ctx {
     const uint32_t* d_sweep_raw = use_ahead ? ahead.raw : device_draws((int64_t)nraw);
     const bool ahead_launched = use_ahead && ahead.launched;
     const bool ahead_prefix = use_ahead && ahead.prefix && !ahead.launched;
+    const bool ahead_piped = ahead_launched && ahead.piped;
+    if (ahead_launched || ahead_prefix) par = ahead.par;
+    else par ^= 1;
     ahead.active = false;
     mark("draws");
     // update_phi speculated on the pool while this thread launches the sweep
@@ -1882,20 +2179,26 @@ struct Ctx {
       }
       mark("launched");
       if (stats.rounds == rounds0) {   // hidden behind the device work
+        if (deep_ok && spec.ran && spec.K == K && track && !(debug & 4194304)) {
+          pre_enqueue(m, track);
+          mark("pre");
+        }
         if (spec.ran) spec_join();
         else prefill_phi_stream();
       }
       mark("prefill");
-      HIPCHK(hipEventSynchronize(ev[6]));
+      HIPCHK(hipEventSynchronize(ev_res[par]));
       mark("resolved");
-      if (round_timed) {
+      const bool piped_round = ahead_piped && stats.rounds == rounds0;
+      if (piped_round ? pre_timed[par] : round_timed) {
         float t1 = 0;
-        HIPCHK(hipEventElapsedTime(&t1, ev[0], ev[1]));
+        if (piped_round) round_points = n;
+        HIPCHK(hipEventElapsedTime(&t1, piped_round ? ev_pp[par][0] : ev[0], piped_round ? ev_pp[par][1] : ev[1]));
         stats.t_prepass_ms += t1;
         stats.prepass_timed++;
         stats.prepass_timed_points += round_points;
       }
-      if (round_fine) {
+      if (round_fine && !piped_round) {
         float t2 = 0, t3 = 0;
         HIPCHK(hipEventElapsedTime(&t3, ev[1], ev[5]));
         HIPCHK(hipEventElapsedTime(&t2, ev[5], ev[2]));
@@ -1903,7 +2206,10 @@ struct Ctx {
         stats.t_resolve_ms += t2;
       }
       stats.rounds++;
-      const ResolveCtl c = *(const ResolveCtl*)h_ctl.p;
+      const ResolveCtl c = *ctl_at(par);
+      // the sweep enqueued ahead runs only after a complete sweep without moves
+      if (pre.active && (c.status || c.next < n || c.moves)) pre_release();
+      last_sweep_rounds = (int)(stats.rounds - rounds0);
       if (debug & 2) {
         long long tp[16];
         HIPCHK(hipMemcpy(tp, d_rprof.p, sizeof(tp), hipMemcpyDeviceToHost));
@@ -1925,7 +2231,9 @@ struct Ctx {
         err = c.status == kValidate ? "State validation failed: inconsistent cluster count from Neal8 case 2"
               : c.status == kWalker ? "Walker alias table failure"
               : c.status == kProb   ? "Too few positive probabilities"
+              : c.status == kPipeOff ? "a sweep enqueued ahead was gated off on the device"
                                     : "resolver failure";
+        if (c.status == kPipeOff) return kArg;
         return c.status;
       }
       K = c.K;
@@ -1936,7 +2244,7 @@ struct Ctx {
 
     // slots -> labels; rebuild per-label parameters and counts from the resolver summary
     auto ts0 = std::chrono::steady_clock::now();
-    const int* sol = h_ctl.p + kCtlInts;
+    const int* sol = (const int*)ctl_at(par) + kCtlInts;
     const int* cnt = sol + scap;
     const int* src = cnt + scap;
     if (sweep_moves > 0) {
@@ -1981,6 +2289,7 @@ struct Ctx {
       while (pfx < std::min(K, spec.K) && sol[pfx] == pfx && h_counts[pfx] == spec.counts[pfx]) ++pfx;
       spec.pfx = pfx;
     }
+    last_sweep_moves = sweep_moves;
     mark("sweep_end");
     stats.t_stats_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
     stats.sweeps++;
@@ -2072,6 +2381,7 @@ struct Ctx {
     std::vector<double> sigma;
     std::vector<int> counts;
     std::vector<int64_t> off;          // stream offset at the start of cluster t's draws
+    int stage_buf = -1;                // staging buffer of its tables (stage_hold until used)
   } spec;
   Rng spec_live;                       // spill target of the speculative pass (never the chain's)
   PinBuf<unsigned> h_freq_next;        // the sweep's frequency copy-out (h_freq keeps the pre-sweep one)
@@ -2086,10 +2396,10 @@ struct Ctx {
     if (dev) {
       HIPCHK(hipEventSynchronize(phidev.ev));
       if (pj_open) pj.ns_f2.store(pj_ns());
-      for (int i = 0; i < 624 && dev; ++i) dev = mt_untemper(phidev.raw.p[i]) == rng.mt[i];
+      for (int i = 0; i < 624 && dev; ++i) dev = mt_untemper(phidev.blk[i]) == rng.mt[i];
     }
     if (dev) {
-      sa.fill_raw(rng, phidev.raw.p, phidev.N);
+      sa.fill_raw(rng, phidev.blk, phidev.N);
       return true;
     }
     return sa.fill(rng, N);
@@ -2104,10 +2414,10 @@ struct Ctx {
                phidev.N >= N;
     if (dev) {
       HIPCHK(hipEventSynchronize(phidev.ev));
-      for (int i = 0; i < 624 && dev; ++i) dev = mt_untemper(phidev.raw.p[i]) == rng.mt[i];
+      for (int i = 0; i < 624 && dev; ++i) dev = mt_untemper(phidev.blk[i]) == rng.mt[i];
     }
     if (dev) {
-      sa.fill_raw(rng, phidev.raw.p, N);
+      sa.fill_raw(rng, phidev.blk, N);
       return true;
     }
     return sa.fill(rng, N);
@@ -2128,7 +2438,7 @@ struct Ctx {
   }
 
   void stage_entry_from(const UploadLayout& L, int r, int k, const uint8_t* cen, const double* sig, int count) {
-    uint8_t* st = stage_ptr();
+    uint8_t* st = h_stage_buf[pj.stage_buf].p;
     double* tt = (double*)(st + L.off_tab) + (size_t)r * 2 * d;
     tables_for(cen, sig, st + L.off_codes + (size_t)r * dp, tt);
     bounds_for(cen, tt, (uint64_t*)(st + L.off_bnd) + (size_t)r * bw);
@@ -2164,7 +2474,15 @@ struct Ctx {
     int64_t* offs = nullptr;           // offs[t]: stream offset at the start of cluster t's draws
     bool spec = false;                 // speculative: the slice is generated by the job from rng
     int64_t fill_count = 0;
-    static constexpr int kLogitChunk = 1024;
+    // logit chunks: small first ones (B starts on the first as soon as it is done), then
+    // 1024 entries
+    static constexpr int kLogitChunk = 1024, kSmall = 128, kNSmall = 8;
+    static int64_t chunk_beg(int c) {
+      return c <= kNSmall ? (int64_t)c * kSmall : (int64_t)kNSmall * kSmall + (int64_t)(c - kNSmall) * kLogitChunk;
+    }
+    static int chunk_of(int64_t pos) {
+      return pos < kNSmall * kSmall ? (int)(pos / kSmall) : kNSmall + (int)((pos - kNSmall * kSmall) / kLogitChunk);
+    }
     std::atomic<int> fill{0};          // 0 open, 1 taken, 2 done
     std::atomic<int> nextL{0}, doneL{0};
     std::atomic<int> nL{0};
@@ -2176,6 +2494,7 @@ struct Ctx {
     std::atomic<int> nextC{0}, gsl{-1};
     int berr = 0, b_end = 0;
     bool failed = false;
+    int stage_buf = 0;                 // staging buffer phase C fills
     const double* sig_in = nullptr;    // current sigmas (phase A), indexed like Sig
     bool stage = true;                 // phase C stages the label tables into L
     // diagnostics (debug bit 5): ns after launch
@@ -2187,10 +2506,7 @@ struct Ctx {
     return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - pj.t_launch).count();
   }
   void tsum(const char* name, double us) {
-    size_t q = 0;
-    while (q < trace_sum.size() && trace_sum[q].first != name) ++q;
-    if (q == trace_sum.size()) trace_sum.emplace_back(name, 0.0);
-    trace_sum[q].second += us;
+    trace_add(name, us);
   }
 
   void pj_phaseA(int t, int j0, int j1) {
@@ -2380,6 +2696,7 @@ struct Ctx {
     pj.spec = spec;
     pj.sig_in = h_sigma.data();
     pj.stage = true;
+    pj.stage_buf = stage_fill;
     pj.fill_count = phi_prefetch;
     phi_off.resize(d + 1);
     phi_off[0] = 0;
@@ -2389,7 +2706,7 @@ struct Ctx {
     phi_cum.resize((size_t)pj.T * pj.sumatt);
     phi_perm.resize((size_t)pj.T * pj.sumatt);
     // A in chunks of attributes so the first cluster is ready early
-    pj.achunk = std::max(8, (d + 3) / 4);
+    pj.achunk = std::max(4, (d + 15) / 16);
     pj.nach = (d + pj.achunk - 1) / pj.achunk;
     pj.stA.reset(new std::atomic<int>[std::max(pj.T, 1)]);
     pj.stB.reset(new std::atomic<int>[std::max(pj.T, 1)]);
@@ -2425,7 +2742,7 @@ struct Ctx {
     }
     sa.used = 0;
     sa.live = &spec_live;
-    const int nl = (int)((sa.n + PhiJob::kLogitChunk - 1) / PhiJob::kLogitChunk);
+    const int nl = sa.n > 0 ? PhiJob::chunk_of(sa.n - 1) + 1 : 0;
     if (nl > pj.ldone_cap) {
       pj.ldone.reset(new std::atomic<uint8_t>[nl]);
       pj.ldone_cap = nl;
@@ -2439,12 +2756,14 @@ struct Ctx {
     pj.fill.store(2, std::memory_order_release);
     return true;
   }
-  bool pj_logit() {
+  // limit: only chunks below it (the first ones, before phase A's first clusters)
+  bool pj_logit(int limit = INT_MAX) {
     if (pj.fill.load(std::memory_order_acquire) != 2) return false;
+    if (pj.nextL.load(std::memory_order_relaxed) >= limit) return false;
     const int c = pj.nextL.fetch_add(1);
     if (c >= pj.nL.load(std::memory_order_relaxed)) return false;
     StreamAhead& sa = phi_stream;
-    sa.logits((int64_t)c * PhiJob::kLogitChunk, std::min<int64_t>(sa.n, (int64_t)(c + 1) * PhiJob::kLogitChunk));
+    sa.logits(PhiJob::chunk_beg(c), std::min<int64_t>(sa.n, PhiJob::chunk_beg(c + 1)));
     pj.ldone[c].store(1, std::memory_order_release);
     if (pj.doneL.fetch_add(1, std::memory_order_release) + 1 == pj.nL.load()) pj.ns_logits.store(pj_ns());
     return true;
@@ -2454,14 +2773,16 @@ struct Ctx {
   int64_t pj_wait_chunk(int64_t pos) {
     const StreamAhead& sa = phi_stream;
     const int nl = pj.nL.load(std::memory_order_relaxed);
-    int c = (int)(pos / PhiJob::kLogitChunk);
+    int c = PhiJob::chunk_of(pos);
     if (c >= nl) return INT64_MAX;
     while (!pj.ldone[c].load(std::memory_order_acquire))
       if (!pj_logit()) HostPool::spin_pause();
     while (c + 1 < nl && pj.ldone[c + 1].load(std::memory_order_acquire)) ++c;
-    return c + 1 >= nl ? INT64_MAX : std::min<int64_t>(sa.n, (int64_t)(c + 1) * PhiJob::kLogitChunk);
+    return c + 1 >= nl ? INT64_MAX : std::min<int64_t>(sa.n, PhiJob::chunk_beg(c + 1));
   }
-  bool pj_take_a() {
+  // limit: only tasks of clusters below it
+  bool pj_take_a(int limit = INT_MAX) {
+    if (limit < pj.T && pj.nextA.load(std::memory_order_relaxed) >= limit * pj.nach) return false;
     const int task = pj.nextA.fetch_add(1);
     if (task >= pj.T * pj.nach) return false;
     const int t = task / pj.nach, c = task - t * pj.nach;
@@ -2501,8 +2822,10 @@ struct Ctx {
   void pj_work() {
     for (;;) {
       if (pj_fill()) continue;                    // the stream slice first: B waits on it
-      if (pj_logit()) continue;
+      if (pj_logit(PhiJob::kNSmall)) continue;    // the small first chunks: B's first draws
+      if (pj_take_a(pj.t0 + 2)) continue;         // phase A of the first clusters
       if (pj_try_b()) continue;
+      if (pj_logit()) continue;
       if (pj_take_a()) continue;
       if (pj.bclaim.load(std::memory_order_acquire) != 0) break;
       HostPool::spin_pause();                   // stream fill / logits in progress elsewhere
@@ -2553,6 +2876,7 @@ struct Ctx {
     std::vector<int> touched(K);
     for (int k = 0; k < K; ++k) touched[k] = k;
     const UploadLayout L = stage_begin(K);
+    stage_hold = spec.stage_buf = stage_fill;
     pj_setup(std::move(touched), 0, spec.counts.data(), h_freq.p, spec.center.data(), spec.sigma.data(), L, true,
              spec.off.data(), true);
     spec.moves = -1;
@@ -2877,6 +3201,7 @@ struct Ctx {
                           spec.pos == rng.pos && spec.epoch == rng.epoch && sa.n > 0 && sa.start.pos == rng.pos &&
                           !(debug & 128);
     spec.ran = false;
+    if (pre.active && !(use_spec && spec.moves == 0 && K == spec.K && spec.nvalid == K)) pre_release();
     if (!use_spec) {
       // the update on the device (csrc/phi.hip); -1: not applicable here, the host runs it
       const int st = device_update_phi(mask, nidx);
@@ -2937,8 +3262,18 @@ struct Ctx {
     const bool full = tables_dirty || T == K;
     if (full) ensure_slots(K + 2);
     const int nent = full ? K : T;
-    const UploadLayout L = stage_begin(std::max(nent, 1));
-    if (t0 > 0 && !(full && K == spec.K)) {
+    // the speculation staged its clusters into spec.stage_buf (held since): same layout
+    // when every label is staged and K did not change
+    const bool spec_layout = use_spec && t0 > 0 && full && K == spec.K && spec.stage_buf == stage_hold;
+    UploadLayout L;
+    if (spec_layout) {
+      L = upload_layout(K, dp, d, bw);
+      stage_fill = spec.stage_buf;
+    } else {
+      stage_hold = -1;
+      L = stage_begin(std::max(nent, 1));
+    }
+    if (t0 > 0 && !spec_layout) {
       // the speculation staged its clusters for a different layout: stage them again
       pool_for(t0, [&](int t) { stage_entry(L, full ? touched[t] : t, touched[t]); });
     }
@@ -2961,7 +3296,15 @@ struct Ctx {
       for (int k : touched) done[k] = 1;
       for (int k = 0; k < K; ++k)
         if (!done[k]) stage_entry(L, k, k);
-      if (K) stage_commit(L, K, true);
+      if (K && defer_commit && spec_layout) {
+        // committed by flush_commit, after the next speculative update_phi is started
+        commit_later.active = true;
+        commit_later.buf = stage_fill;
+        commit_later.nent = K;
+        stage_hold = stage_fill;
+      } else if (K) {
+        stage_commit(L, K, true);
+      }
       tables_dirty = false;
     } else if (T) {
       stage_commit(L, T, false);
@@ -3114,14 +3457,44 @@ int Ctx::iteration(const hdpm_chain_params* p, int iter, int* idx_1_sm, int* acc
   *accepted = 0;
   trace.clear();
   mark("start");
-  if (!(p->neal8 && iter % p->n8_step_size == 0)) cancel_ahead();
-  if (p->neal8 && iter % p->n8_step_size == 0) {       // la:94-103
+  const bool n8 = p->neal8 && iter % p->n8_step_size == 0;
+  const bool sm_now = p->split_merge && iter % p->sam_step_size == 0;
+  const bool next_n8 = p->neal8 && (iter + 1) % p->n8_step_size == 0;
+  // the next iteration's speculative update_phi started before this one's tables are
+  // committed and its log-likelihood summed (both off the host's critical path, which is the
+  // chain of update_phi draws): when this iteration is a lone Neal-8 sweep whose update
+  // came from the speculation and whose log-likelihood needs no device work
+  const bool early = n8 && !sm_now && next_n8 && iter % 1000 != 0 && !labels_out && !(debug & 2097152);
+  if (!n8) cancel_ahead();
+  if (n8) {                                              // la:94-103
+    // the next sweep may be enqueued while this one's update is drawn (pre_enqueue)
+    deep_ok = early && launch_next && !(debug & 4194304);
     st = neal8_sweep(p->m);
-    if (st) return st;
+    deep_ok = false;
+    if (st) {
+      pre_release();
+      return st;
+    }
+    defer_commit = early;
     st = update_phi(nullptr, 0);
-    if (st) return st;
+    defer_commit = false;
+    if (st) {
+      pre_release();
+      flush_commit();
+      return st;
+    }
   }
-  if (p->split_merge && iter % p->sam_step_size == 0) {  // la:111-115
+  bool prepared = false;
+  if (pre.active) {
+    if (early && launch_next && pipe_go(p->m)) prepared = true;
+    else pre_release();
+  }
+  if (!prepared && early && commit_later.active && freq_version == labels_version && !(debug & 4) && !tables_dirty) {
+    prepare_next_sweep(p->m, launch_next);               // spec_launch, flush_commit, round 0
+    prepared = true;
+  }
+  flush_commit();
+  if (sm_now) {                                          // la:111-115
     const auto t0 = std::chrono::steady_clock::now();
     st = split_and_merge(p->t, p->r, *idx_1_sm, accepted);
     stats.t_sm_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -3141,17 +3514,19 @@ int Ctx::iteration(const hdpm_chain_params* p, int iter, int* idx_1_sm, int* acc
   }
   // the next iteration starts with a sweep: prepare it now (cancelled by any other call;
   // launched on the device too when the caller runs that iteration next, launch_next)
-  if (!st && p->neal8 && (iter + 1) % p->n8_step_size == 0) prepare_next_sweep(p->m, launch_next);
+  if (!st && next_n8 && !prepared) {
+    prepare_next_sweep(p->m, launch_next);
+    prepared = true;
+  }
+  if (prepared && ahead.active) phi_lookahead();
   mark("ahead");
   if ((debug & 32) && trace.size() > 1) {
     if (trace_alloc0 < 0) trace_alloc0 = g_dev_allocs.load();
     for (size_t k = 1; k < trace.size(); ++k) {
       const double us = std::chrono::duration<double, std::micro>(trace[k].second - trace[k - 1].second).count();
-      size_t q = 0;
-      while (q < trace_sum.size() && trace_sum[q].first != trace[k].first) ++q;
-      if (q == trace_sum.size()) trace_sum.emplace_back(trace[k].first, 0.0);
-      trace_sum[q].second += us;
+      trace_add(trace[k].first, us);
     }
+    trace_add("total", std::chrono::duration<double, std::micro>(trace.back().second - trace.front().second).count());
     trace_iters++;
   }
   if ((debug & 2) && trace.size() > 1) {

@@ -2625,6 +2625,43 @@ hipError_t launch_finish_sweep(int* counts, int* sol, int* los, int* src, int ca
   return hipGetLastError();
 }
 
+// One thread: waits for the host's decision on the enqueued sweep (PipeSlot), at most
+// `limit` ticks of the 100 MHz constant clock (every wave exits), then the gate of its
+// kernels: go, and the previous sweep's control block (written by its resolver before this
+// kernel in stream order) shows it complete without a move.
+__global__ void k_pipe_wait(const PipeSlot* slot, const ResolveCtl* prev, ResolveCtl* own, int n, PipeGate* g,
+                            long long limit) {
+  if (threadIdx.x != 0) return;
+  const long long t0 = wall_clock64();
+  int f = 0;
+  for (;;) {
+    f = __hip_atomic_load(&slot->flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (f != 0) break;
+    if (wall_clock64() - t0 > limit) {
+      f = 3;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(8);
+  }
+  const volatile ResolveCtl* c = prev;
+  const bool ok = f == 1 && c->status == 0 && c->next >= n && c->moves == 0;
+  const uint64_t rw =
+      __hip_atomic_load(reinterpret_cast<const uint64_t*>(&slot->raw), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+  g->raw = ok ? reinterpret_cast<const uint32_t*>(rw) : nullptr;
+  g->status = f;
+  g->gate = ok ? 1 : 0;
+  if (!ok) {              // the sweep's control block says it did not run
+    volatile ResolveCtl* o = own;
+    o->status = kPipeOff;
+    o->next = 0;
+  }
+}
+hipError_t launch_pipe_wait(const PipeSlot* slot, const ResolveCtl* prev, ResolveCtl* own, int n, PipeGate* g,
+                            long long limit, hipStream_t s) {
+  hipLaunchKernelGGL(k_pipe_wait, dim3(1), dim3(64), 0, s, slot, prev, own, n, g, limit);
+  return hipGetLastError();
+}
+
 hipError_t launch_scatter_clusters(const uint8_t* stage, int nent, int dp, int d, int bw, int full, uint8_t* codes,
                                    double* tab, uint64_t* bnd, int* counts, int* sol, int* los, int* src,
                                    hipStream_t s, const int* gate) {

@@ -144,6 +144,23 @@ __device__ __forceinline__ bool pipe_gate(A& a) {
   return true;
 }
 
+// A sweep enqueued before the host knows whether it may run (k_pipe_wait): the host writes
+// its slot (host-coherent memory) once the previous iteration is decided -- flag 1 go (with
+// the sweep's draws), 2 abort -- and the wait kernel turns it into the gate the sweep's
+// kernels read (pipe_gate): go, and the previous sweep completed in its one launch without
+// a move.  status: the flag seen (3: none within the time limit).
+constexpr int kPipeOff = 10;   // ResolveCtl::status of an enqueued sweep that was gated off
+struct PipeSlot {
+  int flag;
+  int pad;
+  const uint32_t* raw;
+};
+struct PipeGate {
+  int gate;
+  int status;
+  const uint32_t* raw;
+};
+
 // The resolver of a pipelined sweep (ResolveArgs::dry) stops with this status before its
 // first decision that would change the state; nothing has changed then.
 constexpr int kDryStop = 9;
