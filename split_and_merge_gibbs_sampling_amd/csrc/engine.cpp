@@ -776,7 +776,8 @@ struct Ctx {
     trace_sum[q].second += us;
     trace_smp[q].push_back((float)us);
   }
-  int64_t trace_iters = 0, trace_alloc0 = -1;
+  int64_t trace_iters = 0, trace_alloc0 = -1, trace_slow = 0;
+  char spec_line[192] = {0};          // the last joined speculative update's stamps (debug bit 5)
   std::unordered_map<uint64_t, bool> beta_cache;
 
   SmWork sm;
@@ -908,6 +909,14 @@ struct Ctx {
     W.start_pos = rng.pos;
     W.epoch = rng.epoch;
     size_window(W, count, export_after);
+    // the other window's buffers too, now: its first launch comes mid-chain, where an
+    // allocation would stall the iteration
+    RngWindow& O = (&W == &win[0]) ? win[1] : win[0];
+    if (O.raw.n < W.raw.n) O.raw.ensure(W.raw.n);
+    if (O.arrays.n < W.arrays.n) O.arrays.ensure(W.arrays.n);
+    O.init.ensure(624);
+    O.h_init.ensure(624);
+    if (!O.done) HIPCHK(hipEventCreateWithFlags(&O.done, hipEventDisableTiming));
     std::memcpy(W.h_init.p, rng.mt, sizeof(rng.mt));
     HIPCHK(hipMemcpyAsync(W.init.p, W.h_init.p, 624 * 4, hipMemcpyHostToDevice, gstream));
     W.init_src = W.init.p;
@@ -1066,10 +1075,19 @@ struct Ctx {
   // last word.  False when window W does not hold them (then adopt_state_at).
   bool phi_device_prefetch(const RngWindow& W, uint64_t target, int64_t N) {
     phidev.valid = false;
-    int64_t blk;
+    // the state's position in its block (one stream: the same block edges in every window)
     int mti;
-    locate(W, target, &blk, &mti);
-    if (blk == 0 || mti < 1) return false;
+    {
+      const uint64_t r = target - W.start_pos;
+      const uint64_t head = W.mti0 >= 624 ? 0 : 624 - W.mti0;
+      if (r < head) {
+        mti = W.mti0 + (int)r;
+      } else {
+        const uint64_t k = (r - head) % 624;
+        mti = k == 0 ? 624 : (int)k;
+      }
+    }
+    if (mti < 1) return false;
     const uint64_t s_blk = target - (uint64_t)mti;              // first word of the state's block
     const int64_t words = 624 * ((mti + N - 1) / 624 + 1);       // through the block of word N - 1
     PhiSlice* hit = nullptr;
@@ -1079,8 +1097,15 @@ struct Ctx {
     if (hit) {
       stats.phi_lookahead_hits++;
     } else {
-      if (s_blk < W.start_pos || s_blk + (uint64_t)words > W.start_pos + (uint64_t)W.count) return false;
-      hit = phi_slice_copy(W, s_blk, words, nullptr);
+      // from whichever window holds the whole slice (one that ends inside it is followed by
+      // the next, which starts earlier)
+      const RngWindow* X = nullptr;
+      for (const auto& w : win)
+        if (w.valid && w.epoch == rng.epoch && s_blk >= w.start_pos &&
+            s_blk + (uint64_t)words <= w.start_pos + (uint64_t)w.count && (!X || w.start_pos < X->start_pos))
+          X = &w;                         // the earlier window: generated first
+      if (!X) return false;
+      hit = phi_slice_copy(*X, s_blk, words, nullptr);
     }
     hit->stamp = ++phis_clock;
     phidev.valid = true;
@@ -1129,16 +1154,22 @@ struct Ctx {
     for (auto& sl : phis)
       if (sl.valid && sl.epoch == rng.epoch && sl.s0 <= from && from + (uint64_t)look_words <= sl.s0 + (uint64_t)sl.words)
         return;
+    const RngWindow* X = nullptr;
     for (auto& W : win)
       if (W.valid && W.epoch == rng.epoch && W.start_pos <= from &&
-          from + (uint64_t)look_words <= W.start_pos + (uint64_t)W.count) {
+          from + (uint64_t)look_words <= W.start_pos + (uint64_t)W.count && (!X || W.start_pos < X->start_pos))
+        X = &W;
+    // a window still being generated would hold the in-order copy stream behind it
+    if (X && hipEventQuery(X->done) == hipSuccess) {
+      const RngWindow& W = *X;
+      {
         const PhiSlice* keep = nullptr;
         for (auto& sl : phis)
           if (phidev.valid && sl.valid && phidev.blk >= sl.buf.p && phidev.blk < sl.buf.p + sl.words) keep = &sl;
         (void)phi_slice_copy(W, from, look_words, keep);
         stats.phi_lookahead_copies++;
-        return;
       }
+    }
   }
 
   // Device pointer to the next n raw draws of the stream; advances the host stream past
@@ -1148,7 +1179,9 @@ struct Ctx {
   // sweeps and the draws between them, instead of one launch (dominated by the jump) per
   // sweep.  The next window is launched from the end of the current sweep's draws when the
   // current one has fewer than `kLead` sweeps' worth left, so it is ready well before use.
-  static constexpr int kLead = 3;
+  // (a window takes ~0.5 ms to generate at C5, several sweeps' time: started 8 sweeps
+  // ahead, it is done before the first draw from it)
+  static constexpr int kLead = 8;
   int64_t window_span(int64_t n) const {
     // independent of cmax unless the draws between sweeps outgrow its allowance, so the
     // span (window buffers, jump tables) stays fixed
@@ -2028,11 +2061,23 @@ struct Ctx {
     sweep_buffers(track);
     __atomic_store_n(&h_pipe.p[q].flag, 0, __ATOMIC_RELEASE);
     h_pipe.p[q].raw = nullptr;
+    // the next sweep's draws start after this update's (about a slice): the windows that
+    // overlap that stretch (not a window generation started for later sweeps)
+    const uint64_t lo = spec.pos, hi = spec.pos + (uint64_t)(2 * phi_prefetch) + (uint64_t)n * (m + 1);
+    int whole = -1;                      // the earliest window holding all of it
+    for (int k = 0; k < 2; ++k) {
+      const RngWindow& w = win[k];
+      if (w.valid && w.epoch == rng.epoch && w.start_pos <= lo && hi <= w.start_pos + (uint64_t)w.count &&
+          (whole < 0 || w.start_pos < win[whole].start_pos))
+        whole = k;
+    }
     for (int k = 0; k < 2; ++k) {
       pre.gen[k] = ~0ull;
-      if (win[k].valid && win[k].epoch == rng.epoch) {
-        HIPCHK(hipStreamWaitEvent(stream, win[k].done, 0));
-        pre.gen[k] = win[k].gen;
+      const RngWindow& w = win[k];
+      if (whole >= 0 ? k == whole
+                     : (w.valid && w.epoch == rng.epoch && w.start_pos < hi && lo < w.start_pos + (uint64_t)w.count)) {
+        HIPCHK(hipStreamWaitEvent(stream, w.done, 0));
+        pre.gen[k] = w.gen;
       }
     }
     HIPCHK(launch_pipe_wait(&h_pipe.p[q], ctl_at(par), ctl_at(q), n, &d_pipe.p[q], 200000000LL, stream));
@@ -2906,6 +2951,9 @@ struct Ctx {
       tsum("spec.B_to", pj.ns_b1.load() * 1e-3);
       tsum("spec.joined_at", pj_ns() * 1e-3);
       tsum("spec.B_on_caller", pj.b_thread.load());
+      std::snprintf(spec_line, sizeof(spec_line), " | spec fill %.0f state %.0f slice %.0f logits %.0f B %.0f-%.0f joined %.0f",
+                    pj.ns_f0.load() * 1e-3, pj.ns_f1.load() * 1e-3, pj.ns_fill.load() * 1e-3,
+                    pj.ns_logits.load() * 1e-3, pj.ns_b0.load() * 1e-3, pj.ns_b1.load() * 1e-3, pj_ns() * 1e-3);
     }
     // rewind: update_phi continues from spec.off[t0] of the same prefetched stream
     sa.used = 0;
@@ -3526,7 +3574,18 @@ int Ctx::iteration(const hdpm_chain_params* p, int iter, int* idx_1_sm, int* acc
       const double us = std::chrono::duration<double, std::micro>(trace[k].second - trace[k - 1].second).count();
       trace_add(trace[k].first, us);
     }
-    trace_add("total", std::chrono::duration<double, std::micro>(trace.back().second - trace.front().second).count());
+    const double tot = std::chrono::duration<double, std::micro>(trace.back().second - trace.front().second).count();
+    trace_add("total", tot);
+    if (tot > 180.0 && trace_slow++ < 12) {              // the segments of a slow iteration
+      std::string line = "[slow iteration " + std::to_string(trace_iters) + "]";
+      for (size_t k = 1; k < trace.size(); ++k) {
+        char buf[64];
+        std::snprintf(buf, sizeof(buf), " %s %.0f", trace[k].first,
+                      std::chrono::duration<double, std::micro>(trace[k].second - trace[k - 1].second).count());
+        line += buf;
+      }
+      std::fprintf(stderr, "%s%s\n", line.c_str(), spec_line);
+    }
     trace_iters++;
   }
   if ((debug & 2) && trace.size() > 1) {
