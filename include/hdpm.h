@@ -221,8 +221,8 @@ int hdpm_debug_draw(hdpm_ctx* ctx, const double* logw, int32_t E, double rU, int
 /* Testing: exp (fn = 0) or log (fn = 1) of x[n] on the device, glibc's algorithm (ocml = 0)
  * or the device libm's (ocml = 1). */
 int hdpm_debug_math(hdpm_ctx* ctx, const double* x, int64_t n, int32_t fn, int32_t ocml, double* out);
-/* Block until the chain's device work is done (a prepared next sweep's prefix -- scratch
- * outputs only -- may still be running; hipDeviceSynchronize waits for it too). */
+/* Block until every kernel and copy the context has queued is done, a prepared next
+ * sweep's prefix (scratch outputs only) included; the prepared sweep stays prepared. */
 int hdpm_synchronize(hdpm_ctx* ctx);
 
 #ifdef __cplusplus

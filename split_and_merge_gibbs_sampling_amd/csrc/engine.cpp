@@ -17,6 +17,10 @@
 #include <pthread.h>
 #include <sched.h>
 #include <dirent.h>
+#include <dlfcn.h>
+#include <execinfo.h>
+#include <csignal>
+#include <unistd.h>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -86,7 +90,26 @@ struct HipError {
 #ifndef HDPM_PHI_SPEC
 #define HDPM_PHI_SPEC 4   // update_phi phase B: first rbeta attempts speculated per batch
 #endif
-static std::atomic<int64_t> g_dev_allocs{0};   // device allocations made (diagnostics)
+static std::atomic<int64_t> g_dev_allocs{0};
+
+// HDPM_SEGV_TRACE=1: a host fault prints the library's call stack (addresses for addr2line)
+static void segv_trace(int sig) {
+  void* fr[64];
+  const int nf = backtrace(fr, 64);
+  backtrace_symbols_fd(fr, nf, 2);
+  Dl_info di;
+  if (dladdr((void*)&segv_trace, &di)) {
+    char buf[128];
+    const int len = std::snprintf(buf, sizeof(buf), "libhdpm base %p\n", di.dli_fbase);
+    if (len > 0) (void)!write(2, buf, (size_t)len);
+  }
+  std::signal(sig, SIG_DFL);
+  std::raise(sig);
+}
+static const bool g_segv_trace = [] {
+  if (std::getenv("HDPM_SEGV_TRACE")) std::signal(SIGSEGV, segv_trace);
+  return true;
+}();   // device allocations made (diagnostics)
 
 template <class T>
 struct DevBuf {
@@ -213,12 +236,16 @@ class HostPool {
       ~Release() { p->busy_.store(false, std::memory_order_release); }
     } rel{this};
     quiesce();
+    // a worker that saw the last generation but registers only now finds nothing to take
+    // while the job's fields are rewritten (next_ past any total, launches closed)
+    next_.store(INT64_MAX / 2, std::memory_order_release);
+    bclaim_.store(kClosed, std::memory_order_release);
     range_ = [&f](int64_t a, int64_t b) { f(a, b); };
     bcast_ = nullptr;
     total_ = n;
     grain_ = grain;
-    next_.store(0, std::memory_order_relaxed);
     done_.store(0, std::memory_order_relaxed);
+    next_.store(0, std::memory_order_release);
     publish();
     work();
     while (done_.load(std::memory_order_acquire) < total_) spin_pause();
@@ -234,11 +261,13 @@ class HostPool {
   bool try_launch(F&& f) {
     if (!acquire()) return false;
     quiesce();
+    bclaim_.store(kClosed, std::memory_order_release);     // (see run)
+    next_.store(INT64_MAX / 2, std::memory_order_release);
     bjob_ = std::forward<F>(f);
     bcast_ = &bjob_;
     range_ = nullptr;
     bdone_.store(0, std::memory_order_relaxed);
-    bclaim_.store(0, std::memory_order_relaxed);
+    bclaim_.store(0, std::memory_order_release);
     publish();
     return true;
   }
@@ -335,7 +364,7 @@ class HostPool {
   }
   void work() {
     for (;;) {
-      const int64_t a = next_.fetch_add(grain_, std::memory_order_relaxed);
+      const int64_t a = next_.fetch_add(grain_, std::memory_order_acquire);
       if (a >= total_) break;
       const int64_t b = std::min(total_, a + grain_);
       range_(a, b);
@@ -348,6 +377,24 @@ class HostPool {
       auto t0 = std::chrono::steady_clock::now();
       int polls = 0;
       for (;;) {
+        // spin on the generation with plain loads (registering in active_ on every poll kept
+        // its cache line bouncing between the cores and stalled quiesce()); register, then
+        // look again, only when it changed
+        if (gen_.load(std::memory_order_acquire) == seen) {
+          if (stop_) return;
+          spin_pause();
+          if (++polls % 256 == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us_)) {
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_.wait(lk, [&] {
+              return stop_ || gen_.load(std::memory_order_acquire) != seen ||
+                     wake_seq_.load(std::memory_order_acquire) != woke;
+            });
+            woke = wake_seq_.load(std::memory_order_acquire);
+            if (stop_) return;
+            t0 = std::chrono::steady_clock::now();
+          }
+          continue;
+        }
         active_.fetch_add(1, std::memory_order_acq_rel);
         const uint64_t g = gen_.load(std::memory_order_acquire);
         if (g != seen) {
@@ -1087,12 +1134,13 @@ struct Ctx {
         mti = k == 0 ? 624 : (int)k;
       }
     }
-    if (mti < 1) return false;
+    // (a block that starts before the stream's first word: no window holds it)
+    if (mti < 1 || target < (uint64_t)mti) return false;
     const uint64_t s_blk = target - (uint64_t)mti;              // first word of the state's block
     const int64_t words = 624 * ((mti + N - 1) / 624 + 1);       // through the block of word N - 1
     PhiSlice* hit = nullptr;
     for (auto& sl : phis)
-      if (sl.valid && sl.epoch == rng.epoch && sl.s0 <= s_blk && s_blk + (uint64_t)words <= sl.s0 + (uint64_t)sl.words)
+      if (sl.valid && sl.epoch == rng.epoch && sl.s0 <= s_blk && s_blk - sl.s0 + (uint64_t)words <= (uint64_t)sl.words)
         hit = &sl;
     if (hit) {
       stats.phi_lookahead_hits++;
@@ -1102,7 +1150,7 @@ struct Ctx {
       const RngWindow* X = nullptr;
       for (const auto& w : win)
         if (w.valid && w.epoch == rng.epoch && s_blk >= w.start_pos &&
-            s_blk + (uint64_t)words <= w.start_pos + (uint64_t)w.count && (!X || w.start_pos < X->start_pos))
+            s_blk - w.start_pos + (uint64_t)words <= (uint64_t)w.count && (!X || w.start_pos < X->start_pos))
           X = &w;                         // the earlier window: generated first
       if (!X) return false;
       hit = phi_slice_copy(*X, s_blk, words, nullptr);
@@ -2224,7 +2272,8 @@ struct Ctx {
       }
       mark("launched");
       if (stats.rounds == rounds0) {   // hidden behind the device work
-        if (deep_ok && spec.ran && spec.K == K && track && !(debug & 4194304)) {
+        // (not while sweeps keep moving points: the enqueued sweep would be dropped)
+        if (deep_ok && spec.ran && spec.K == K && track && last_sweep_moves == 0 && !(debug & 4194304)) {
           pre_enqueue(m, track);
           mark("pre");
         }
@@ -2260,9 +2309,10 @@ struct Ctx {
         HIPCHK(hipMemcpy(tp, d_rprof.p, sizeof(tp), hipMemcpyDeviceToHost));
         std::fprintf(stderr,
                      "[resolve] init %.2f us, batches %.2f us, decided points %lld in %.2f us (exact decisions "
-                     "%.2f us; block mode: %lld blocks), total %.2f us\n",
-                     (tp[1] - tp[0]) / 100.0, tp[3] / 100.0, tp[6], tp[4] / 100.0, tp[12] / 100.0, tp[5],
-                     (tp[7] - tp[0]) / 100.0);
+                     "%.2f us, state updates %.2f us, re-tests %.2f us over %lld points; block mode: %lld blocks), "
+                     "total %.2f us\n",
+                     (tp[1] - tp[0]) / 100.0, tp[3] / 100.0, tp[6], tp[4] / 100.0, tp[12] / 100.0, tp[14] / 100.0,
+                     tp[13] / 100.0, tp[15], tp[5], (tp[7] - tp[0]) / 100.0);
       }
       stats.exact_points += c.exact;
       stats.listed_points += c.listed;
@@ -4018,9 +4068,8 @@ int hdpm_debug_math(hdpm_ctx* h, const double* x, int64_t n, int32_t fn, int32_t
 }
 int hdpm_synchronize(hdpm_ctx* h) {
   CTX_KEEP();
-  // the chain's committed work; a prepared sweep's prefix (scratch only) may still run
-  if (ctx->ahead.active && ctx->ahead.prefix && !ctx->ahead.launched)
-    return hipEventSynchronize(ctx->ev[7]) == hipSuccess ? HDPM_OK : HDPM_E_DEVICE;
+  // everything queued on the device, a prepared sweep's prefix included (a timed window
+  // that ends here ends drained); the prepared sweep stays
   return hipStreamSynchronize(ctx->stream) == hipSuccess ? HDPM_OK : HDPM_E_DEVICE;
 }
 

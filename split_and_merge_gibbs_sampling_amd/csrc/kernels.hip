@@ -884,15 +884,22 @@ struct RState {
   int4* brq;    // [kRqWin] window of the listed points' inputs {row, point, slot, draw}
 };
 
-__host__ __device__ inline size_t resolve_lds_bytes(int lcap, int m, int blocks) {
+// LIST mode stages the exact rows of each 64 listed points in LDS ahead of their decisions
+// (one load round trip per 64 points instead of one per exact decision) when a row has at
+// most kTileCols columns; row stride odd (no bank aliasing between the lanes' rows).
+constexpr int kTileCols = 95;
+__host__ __device__ inline int resolve_tile_stride(int ncol) { return ncol | 1; }
+__host__ __device__ inline size_t resolve_lds_bytes(int lcap, int m, int blocks, int ncol = 0) {
   const size_t emax = (size_t)lcap + (size_t)m;
   size_t b = kRSharedBytes + emax * 4 * sizeof(double) + (size_t)lcap * 2 * sizeof(double) + (size_t)lcap * 4 * sizeof(int) +
              emax * sizeof(int);
   b = (b + 15) & ~(size_t)15;
   b += 256 * sizeof(uint64_t);
+  b += (size_t)lcap * 2 * sizeof(double);      // the snapshot's log counts (sl1, sl0)
   if (blocks)
-    b += (size_t)lcap * 2 * sizeof(double) + 64 * kWave * (sizeof(double) + sizeof(int)) + kWave * sizeof(int) +
-         16 + kRqWin * sizeof(int4);
+    b += 64 * kWave * (sizeof(double) + sizeof(int)) + kWave * sizeof(int) + 16 + kRqWin * sizeof(int4);
+  else if (ncol > 0 && ncol <= kTileCols)
+    b += (size_t)kWave * resolve_tile_stride(ncol) * sizeof(double);
   return b;
 }
 
@@ -1640,13 +1647,15 @@ struct RCtx {
   int lane, ncol, scap;
   int nlog;    // running move-log length (uniform across the wave)
   bool prof;
-  __device__ bool process(int64_t i, int row, int own, uint32_t rawU, int spec, double srad, bool given = false);
+  __device__ bool process(int64_t i, int row, int own, uint32_t rawU, int spec, double srad, bool given = false,
+                          const double* rowp = nullptr);
   __device__ bool verify(int64_t lo, int64_t hi, double dn_over = -1.0, const int* cmin = nullptr);
 };
 
 // Decide point i (exact row in LDS at Lr) and apply n8:107-159.  Returns false to stop
 // the sweep here.
-__device__ __forceinline__ bool RCtx::process(int64_t i, int row, int own, uint32_t rawU, int spec, double srad, bool given) {
+__device__ __forceinline__ bool RCtx::process(int64_t i, int row, int own, uint32_t rawU, int spec, double srad, bool given,
+                                              const double* rowp) {
   const int K = S.K;
   const long long tq0 = prof ? wall_clock64() : 0;
   // The snapshot draw holds while nothing has moved in this launch, and after moves while
@@ -1656,18 +1665,22 @@ __device__ __forceinline__ bool RCtx::process(int64_t i, int row, int own, uint3
   bool use_spec = given || (spec >= 0 && S.moves == 0);
   if (spec >= 0 && !use_spec && S.nstruct == 0) {
     const int sa = st.snap[own], sb = st.cnt[own];
-    const double du = sa == sb ? 0.0 : (sa >= 2 && sb >= 2 ? fabs(a.logn[sb - 1] - a.logn[sa - 1]) : INFINITY);
+    const double du = sa == sb ? 0.0 : (sa >= 2 && sb >= 2 ? fabs(st.l0[own] - st.sl0[own]) : INFINITY);
     use_spec = fmax(S.dvmax, du) < srad;
   }
 
   int pick = spec;
-  if (!use_spec) {   // the point's exact row, on demand
-    const double* src = a.L + (int64_t)row * ncol;
-    for (int c = lane; c < ncol; c += kWave) st.row[c] = src[c];
-    wave_sync();
-    pick = exact_decision(a, st, K, st.row, own, raw_to_unif(rawU));
+  if (!use_spec) {   // the point's exact row: staged in LDS (LIST mode), else loaded now
+    if (!rowp) {
+      const double* src = a.L + (int64_t)row * ncol;
+      for (int c = lane; c < ncol; c += kWave) st.row[c] = src[c];
+      wave_sync();
+      rowp = st.row;
+    }
+    pick = exact_decision(a, st, K, rowp, own, raw_to_unif(rawU));
   }
-  if (prof && lane == 0) S.tsub[4] += wall_clock64() - tq0;
+  const long long tq1 = prof ? wall_clock64() : 0;
+  if (prof && lane == 0) S.tsub[4] += tq1 - tq0;
   if (lane == 0) {
     if (!use_spec) S.exact++;
     // a pipelined sweep stops before its first decision that is not "stay" (nothing changed)
@@ -1738,6 +1751,7 @@ __device__ __forceinline__ bool RCtx::process(int64_t i, int row, int own, uint3
     }
   }
   wave_sync();
+  if (prof && lane == 0) S.tsub[6] += wall_clock64() - tq1;
   if (S.restart && S.status == 0) {
     const int ns = S.nslots - 1;
     copy_pool_params(a, S.src, ns);
@@ -1757,18 +1771,34 @@ __device__ __forceinline__ bool RCtx::verify(int64_t lo, int64_t hi, double dn_o
   if (lane == 0) S.checked = 1;
   const double dn = dn_over >= 0.0 ? dn_over : S.dnow;
   const int* cn = cmin ? cmin : st.cnt;
-  for (int64_t base = lo; base < hi; base += kWave) {
-    const int64_t j = base + lane;
-    bool fail = false;
-    if (j < hi && a.rowpos[j] < 0) {
-      const double mg = a.margin[j] - 2.0 * dn;
-      fail = !((mg > a.T || stay_by_uniform(mg, a.raw[j * (a.m + 1) + a.m], a.K + a.m)) && cn[a.c[j]] >= 2);
+  constexpr int U = 4;     // chunks of 64 points whose inputs are loaded together
+  for (int64_t base0 = lo; base0 < hi; base0 += U * kWave) {
+    int rp[U], cj[U];
+    double mgv[U];
+    uint32_t rwv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t j = base0 + u * kWave + lane;
+      const bool in = j < hi;
+      rp[u] = in ? a.rowpos[j] : 0;
+      mgv[u] = in ? a.margin[j] : 0.0;
+      rwv[u] = in ? a.raw[j * (a.m + 1) + a.m] : 0u;
+      cj[u] = in ? a.c[j] : 0;
     }
-    const unsigned long long bal = __ballot(fail);
-    if (bal) {
-      if (lane == 0) { S.restart = 1; S.next = (int)(base + __ffsll((long long)bal) - 1); }
-      wave_sync();
-      return false;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t j = base0 + u * kWave + lane;
+      bool fail = false;
+      if (j < hi && rp[u] < 0) {
+        const double mg = mgv[u] - 2.0 * dn;
+        fail = !((mg > a.T || stay_by_uniform(mg, rwv[u], a.K + a.m)) && cn[cj[u]] >= 2);
+      }
+      const unsigned long long bal = __ballot(fail);
+      if (bal) {
+        if (lane == 0) { S.restart = 1; S.next = (int)(base0 + u * kWave + __ffsll((long long)bal) - 1); }
+        wave_sync();
+        return false;
+      }
     }
   }
   return true;
@@ -1789,14 +1819,14 @@ __device__ __forceinline__ void resolve_layout(const ResolveArgs& a, RState& st,
   st.los = st.sol + st.lcap;
   st.perm = st.los + st.lcap;
   st.ltab = (uint64_t*)(((uintptr_t)(st.perm + st.emax) + 15) & ~(uintptr_t)15);
-  st.sl1 = st.sl0 = nullptr;
   st.bp = nullptr;
   st.bperm = nullptr;
   st.bcmin = nullptr;
   st.brq = nullptr;
+  // the snapshot's log counts in LDS (drift tests without global loads on the serial path)
+  st.sl1 = (double*)(st.ltab + 256);
+  st.sl0 = st.sl1 + st.lcap;
   if (blocks) {
-    st.sl1 = (double*)(st.ltab + 256);
-    st.sl0 = st.sl1 + st.lcap;
     st.bp = st.sl0 + st.lcap;
     st.bperm = (int*)(st.bp + 64 * kWave);
     st.bcmin = st.bperm + 64 * kWave;
@@ -1873,7 +1903,9 @@ __global__ __launch_bounds__(kWave) void k_resolve(ResolveArgs a) {
   resolve_init(a, st);
   RCtx R{a, st, S, lane, a.S + a.m, a.scap, a.mcount ? *a.mcount : 0, prof};
   const int ncol = R.ncol;
-  (void)ncol;
+  const int tstride = resolve_tile_stride(ncol);
+  // LIST mode's row tile after the layout's last array (resolve_lds_bytes)
+  double* tile = (ncol <= kTileCols && !a.force_exact) ? st.sl0 + st.lcap : nullptr;
   bool go = true;
   int64_t start_checked = -1;
 if (!a.force_exact) {
@@ -1909,22 +1941,37 @@ if (!a.force_exact) {
     const uint32_t ru = (uint32_t)rqv[b].w;
     const int sp = spv[b];
     const double sr = srv[b];
+    if (tile) {        // every lane its point's exact row, all loads in flight together
+      const double* src = a.L + (int64_t)rw * ncol;
+      double* dst = tile + lane * tstride;
+      for (int c0 = 0; c0 < ncol; c0 += 16) {
+        double v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = (lane < lim && c0 + u < ncol) ? src[c0 + u] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (c0 + u < ncol) dst[c0 + u] = v[u];
+      }
+      wave_sync();
+    }
     int q = 0;
     while (q < lim && go) {
       long long t0 = prof ? wall_clock64() : 0;
       bool stays = false;
       if (lane >= q && lane < lim && sp >= 0 && sp < S.K && st.cnt[ci] != 1 && st.sol[sp] == ci) {
         const int sa = st.snap[ci], sb = st.cnt[ci];
-        const double du =
-            sa == sb ? 0.0 : (sa >= 2 && sb >= 2 ? fabs(a.logn[sb - 1] - a.logn[sa - 1]) : INFINITY);
+        const double du = sa == sb ? 0.0 : (sa >= 2 && sb >= 2 ? fabs(st.l0[ci] - st.sl0[ci]) : INFINITY);
         stays = S.moves == 0 || (S.nstruct == 0 && fmax(S.dvmax, du) < sr);
       }
       const unsigned long long todo = __ballot(lane >= q && lane < lim && !stays);
       if (!todo) break;
       q = __ffsll((long long)todo) - 1;
       const int64_t i = __shfl(li, q);
+      const long long tv = prof ? wall_clock64() : 0;
       if (S.dnow > a.dmax && !R.verify(vfrom, i)) { go = false; break; }
-      go = R.process(i, __shfl(rw, q), __shfl(ci, q), (uint32_t)__shfl((int)ru, q), __shfl(sp, q), __shfl(sr, q));
+      if (prof && lane == 0) { S.tsub[5] += wall_clock64() - tv; S.tsub[7] += i - vfrom; }
+      go = R.process(i, __shfl(rw, q), __shfl(ci, q), (uint32_t)__shfl((int)ru, q), __shfl(sp, q), __shfl(sr, q),
+                     false, tile ? tile + q * tstride : nullptr);
       vfrom = i + 1;
       ++q;
       if (prof) {
@@ -2589,13 +2636,16 @@ hipError_t launch_prepass(const PrepassArgs& a, int nblocks, hipStream_t s) {
   }
 }
 
-size_t resolve_smem_bytes(int lcap, int m, int blocks) { return resolve_lds_bytes(lcap, m, blocks); }
+size_t resolve_smem_bytes(int lcap, int m, int blocks) {
+  // LIST mode's row tile is sized for the widest row it stages
+  return resolve_lds_bytes(lcap, m, blocks, blocks ? 0 : kTileCols);
+}
 
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s) {
   if (a.blocks)
     hipLaunchKernelGGL(k_resolve_blk, dim3(1), dim3(kWave), resolve_lds_bytes(a.lcap, a.m, 1), s, a);
   else
-    hipLaunchKernelGGL(k_resolve, dim3(1), dim3(kWave), resolve_lds_bytes(a.lcap, a.m, 0), s, a);
+    hipLaunchKernelGGL(k_resolve, dim3(1), dim3(kWave), resolve_lds_bytes(a.lcap, a.m, 0, a.S + a.m), s, a);
   return hipGetLastError();
 }
 

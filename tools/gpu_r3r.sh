@@ -1,0 +1,12 @@
+# round 3: resolver with LDS snapshot log counts: parity + C2 internal timings + C2/C5-random benches
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/r3r
+mkdir -p $O
+step() { "$@"; rc=$?; if [ $rc -ge 124 ]; then echo "step rc $rc: $*" >> $O/steps.log; exit $rc; fi; echo "rc $rc: $*" >> $O/steps.log; }
+step timeout -k 10 600 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_tiny.py > $O/parity.log 2>&1
+HDPM_BENCH_DEBUG=2 step timeout -k 10 120 python -u bench.py --config c2 --no-cpu-baseline --steps 30 --warmup 10 > $O/c2_dbg.jsonl 2> $O/c2_dbg.err
+step timeout -k 10 120 python -u bench.py --config c2 --no-cpu-baseline > $O/c2.jsonl 2> $O/c2.err
+step timeout -k 10 200 python -u bench.py --init random20 --no-cpu-baseline --steps 3 --warmup 1 > $O/c5r.jsonl 2> $O/c5r.err
+exit 0
