@@ -1981,6 +1981,10 @@ struct Ctx {
     // and vanishing); LIST mode passes over the rest in one ballot per 64
     ra.blocks = (K + m <= 64 && nslots <= 64 && !(debug & 4096) && !(debug & 1) &&
                  ((debug & 8192) || last_exact >= kResolveBlkMin)) ? 1 : 0;
+    // the fixed-point resolver whenever the state fits it (debug bit 23: the one-wave LIST /
+    // block modes; bits 12 / 13 select those modes and keep them)
+    ra.fp = (K + m <= 64 && ra.lcap <= 64 && !(debug & (1 | 4096 | 8192 | 8388608))) ? 1 : 0;
+    if (ra.fp) ra.blocks = 0;
     if (resolve_smem_bytes(ra.lcap, m, ra.blocks) > 160 * 1024) {
       err = "too many clusters for the resolver (K > ~2300)";
       return kArg;

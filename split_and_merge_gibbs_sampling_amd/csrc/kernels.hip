@@ -2303,6 +2303,438 @@ __global__ __launch_bounds__(kWave) void k_resolve_blk(ResolveArgs a) {
   resolve_finish(a, st, R.nlog, tp, prof);
 }
 
+// ------------------------------------------------------------------ fixed-point resolver
+// k_resolve_fp (kFpThreads threads, one listed point per thread) walks the dense list in
+// chunks of kFpThreads positions.  A chunk's outcomes are a fixed point: every point draws in
+// the state left by the outcomes of the chunk's points before it (the launch's committed
+// state plus their case-1 moves), and the draws are repeated -- for the points after the
+// first outcome that changed -- until no outcome changes.  Point k's state depends only on
+// the points before it, so after round r the first r outcomes are final, and the fixed point
+// is the n8 walk's sequence of decisions (code/neal8.cpp:40-160, in index order).
+// A point's draw is its snapshot draw (k_exact_rows) while no log-weight of it has moved by
+// its radius (decide_values), else the n8:95-102 draw on its own lane (fp_draw).  Outcomes:
+// stay, case-1 move, or stop -- cases 2-4, an error, or a pick among equal probabilities
+// (revsort's order decides those): the chunk commits its points before the first stop and
+// the stop goes through the serial path (RCtx::process on wave 0), then the next chunk
+// starts behind it.  Unlisted points between listed ones are re-tested against the drift
+// after the moves before them, as in k_resolve.  Needs K + m <= 64 and lcap <= 64.
+constexpr int kFpThreads = 256;
+constexpr int kFpWaves = kFpThreads / kWave;
+constexpr int kFpFallback = -1000;
+
+struct FpShared {
+  int wc[kFpWaves][kWave];          // slot counts at each wave's first point
+  int wd[kFpWaves][kWave];          // each wave's net count change per slot
+  double wl1[kFpWaves][kWave];      // logn[wc]
+  double wl0[kFpWaves][kWave];      // logn[wc - 1]
+  double wdr[kFpWaves];             // max over slots of |logn[wc] - logn[snapshot count]|
+  double wsd[kFpWaves];
+  int wstop[kFpWaves], wchg[kFpWaves], wmov[kFpWaves], wfresh[kFpWaves];
+  int cmo[kWave];                   // moves out of each slot in the chunk
+  int cmin[kWave];                  // lower bounds on the counts during the chunk
+  int pi[kFpThreads];               // point of each chunk position
+  double dnl[kFpThreads];           // the walk's drift after each chunk position
+  int nlog, go, ufail, stop_pick, stop_fresh, iters, pad0, pad1;
+  int4 stop_rq;
+  signed char corr[kWave][kFpThreads];  // per position: count changes from its wave's earlier moves
+};
+
+__host__ __device__ inline size_t resolve_fp_lds_bytes(int lcap, int m) {
+  return ((resolve_lds_bytes(lcap, m, 0, 0) + 15) & ~(size_t)15) + sizeof(FpShared);
+}
+
+__device__ __forceinline__ double logn_call(const uint64_t* ltab, int c) {
+  return c <= 0 ? -INFINITY : glibc::log_r((double)c, ltab);
+}
+
+// slot_drift of slot s at count b (k_resolve's running drift after a move)
+__device__ __forceinline__ double slot_drift_at(const RState& st, int s, int b) {
+  const int a = st.snap[s];
+  if (a >= 2) return b < 2 ? INFINITY : fabs(logn_call(st.ltab, b - 1) - st.sl0[s]);
+  if (a == 1) return b == 0 ? 0.0 : logn_call(st.ltab, b);
+  return INFINITY;
+}
+
+// The n8:95-102 draw from the log-weights v[0..E) on this lane: the operations of
+// decide_values (max, glibc exp, index-order sum, normalisation, FixupProb), then revsort's
+// descending order walked group by group of equal values with the reference's cumulative
+// sums; a pick inside a group of more than one entry (whose order is heapsort's) returns
+// kFpFallback.  E <= EM <= 200 (no Walker tables).  Returns the index or -status.
+template <int EM>
+__device__ int fp_draw(double (&v)[EM], int E, double rU) {
+  double mx = -INFINITY;
+#pragma unroll
+  for (int e = 0; e < EM; ++e)
+    if (e < E) mx = fmax(mx, v[e]);
+#pragma unroll
+  for (int e = 0; e < EM; ++e) v[e] = e < E ? dexp(v[e] - mx) : 0.0;       // n8:95
+  double sum = 0.0;
+#pragma unroll
+  for (int e = 0; e < EM; ++e)
+    if (e < E) sum += v[e];
+#pragma unroll
+  for (int e = 0; e < EM; ++e) v[e] = v[e] / sum;                           // n8:96
+  double s2 = 0.0;                                                          // FixupProb
+#pragma unroll
+  for (int e = 0; e < EM; ++e)
+    if (e < E) s2 += v[e] > 0 ? v[e] : 0.0;
+  if (!(s2 > 0)) return -3;
+#pragma unroll
+  for (int e = 0; e < EM; ++e) v[e] = e < E ? v[e] / s2 : -1.0;
+  double prev = INFINITY, c = 0.0;
+  for (int j = 0; j < E;) {
+    double cur = -1.0;
+    int g = 0, idx = -1;
+#pragma unroll
+    for (int e = 0; e < EM; ++e) {
+      const double x = v[e];
+      if (x < prev) {
+        if (x > cur) { cur = x; g = 1; idx = e; }
+        else if (x == cur) ++g;
+      }
+    }
+    if (g == 0) return kFpFallback;
+    for (int k = 0; k < g; ++k, ++j) {
+      c += cur;
+      if (j == E - 1 || rU <= c) return g == 1 ? idx : kFpFallback;
+    }
+    prev = cur;
+  }
+  return kFpFallback;
+}
+
+// Unlisted points in [lo, hi) re-tested as RCtx::verify does, each against the drift after
+// the chunk positions before it (dnl[k] for the last position k < nk with pi[k] < j, dn0
+// before any) and the count bounds cmin.  All threads; returns the first failing point
+// (restart there) or hi.
+__device__ int64_t fp_verify(const ResolveArgs& a, const RState& st, FpShared* F, int nk, double dn0, int64_t lo,
+                             int64_t hi, const int* cmin) {
+  RShared& S = *st.sh;
+  if (threadIdx.x == 0) { F->ufail = INT_MAX; S.checked = 1; }
+  __syncthreads();
+  for (int64_t b = lo; b < hi; b += kFpThreads) {
+    const int64_t j = b + threadIdx.x;
+    if (j < hi && a.rowpos[j] < 0) {
+      int k0 = 0, k1 = nk;
+      while (k0 < k1) {
+        const int md = (k0 + k1) >> 1;
+        if (F->pi[md] < j) k0 = md + 1; else k1 = md;
+      }
+      const double dn = k0 > 0 ? F->dnl[k0 - 1] : dn0;
+      if (dn > a.dmax) {
+        const double mg = a.margin[j] - 2.0 * dn;
+        if (!((mg > a.T || stay_by_uniform(mg, a.raw[j * (a.m + 1) + a.m], a.K + a.m)) && cmin[a.c[j]] >= 2))
+          atomicMin(&F->ufail, (int)j);
+      }
+    }
+    __syncthreads();
+    if (F->ufail != INT_MAX) break;
+  }
+  const int u = F->ufail;
+  __syncthreads();
+  if (u == INT_MAX) return hi;
+  if (threadIdx.x == 0) { S.restart = 1; S.next = u; }
+  return u;
+}
+
+// wave 0: the chunk's stop (F->stop_*) decided and applied by the serial path.  Not inlined:
+// the serial decision's registers stay out of the fixed-point loop's allocation.
+__device__ __noinline__ void fp_stop(const ResolveArgs& a, const RState& st, FpShared* F) {
+  const int lane = threadIdx.x & 63;
+  RCtx R{a, st, *st.sh, lane, a.S + a.m, a.scap, F->nlog, false};
+  const int4 rs = F->stop_rq;
+  const int pk = F->stop_pick;
+  const bool given = pk != kFpFallback;
+  const bool ok = R.process(rs.y, rs.x, rs.z, (uint32_t)rs.w, given ? pk : -1, 0.0, given);
+  if (lane == 0) {
+    F->nlog = R.nlog;
+    F->go = ok ? 1 : 0;
+    if (given && F->stop_fresh) st.sh->exact++;
+  }
+}
+
+template <int EM>
+__global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
+  if (!pipe_gate(a)) return;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  RState st;
+  resolve_layout(a, st, smem, false);
+  RShared& S = *st.sh;
+  FpShared* F = (FpShared*)(smem + ((resolve_lds_bytes(a.lcap, a.m, 0, 0) + 15) & ~(size_t)15));
+  long long tp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const bool prof = a.prof != nullptr;
+  if (prof) tp[0] = wall_clock64();
+  for (int x = tid; x < kWave * kFpThreads / 4; x += kFpThreads) ((int*)F->corr)[x] = 0;
+  if (tid == 0) { F->nlog = a.mcount ? *a.mcount : 0; F->go = 1; F->iters = 0; }
+  resolve_init(a, st);
+  const int total = *a.dense_total;
+  const int ncol = a.S + a.m;
+  const int nsl = S.nslots;      // a launch that opens a slot ends with it
+  int64_t vfrom = a.p0;
+  bool go = true;
+  int chunks = 0;
+  if (prof) tp[1] = wall_clock64();
+  for (int q0 = 0; q0 < total && go;) {
+    ++chunks;
+    const int nc = min(kFpThreads, total - q0);
+    const bool in = tid < nc;
+    const int4 r = in ? a.rq[q0 + tid] : make_int4(0, 0, 0, 0);
+    const int own = r.z;
+    const int sp = (in && a.spec) ? a.spec[q0 + tid] : -1;
+    const double sr = (in && a.spec) ? a.spec_rad[q0 + tid] : 0.0;
+    const double rU = raw_to_unif((uint32_t)r.w);
+    F->pi[tid] = in ? r.y : INT_MAX;
+    const int K = S.K, E = K + a.m;
+    const bool struct0 = S.nstruct == 0;
+    int cls = 0, tgt = own, pick = -1, co = 0, ct = 0;   // cls: 0 stay, 1 case-1 move to tgt, 2 stop
+    bool fresh = false;
+    int chg = -1, fs = nc;
+    bool conv = false;
+    for (int it = 0; it <= kFpThreads + 1; ++it) {
+      // (1) the first stop of the current outcomes; each wave's net count changes before it
+      const unsigned long long sbal = __ballot(in && cls == 2);
+      if (lane == 0) F->wstop[wv] = sbal ? wv * kWave + __ffsll((long long)sbal) - 1 : kFpThreads;
+      F->wd[wv][lane] = 0;
+      __syncthreads();
+      fs = nc;
+      for (int w = 0; w < kFpWaves; ++w) fs = min(fs, F->wstop[w]);
+      const bool mover = in && cls == 1 && tid < fs;
+      if (mover) {
+        atomicAdd(&F->wd[wv][own], -1);
+        atomicAdd(&F->wd[wv][tgt], 1);
+      }
+      __syncthreads();
+      // (2) the counts at each wave's first point (lane = slot)
+      if (wv == 0) {
+        int c = lane < nsl ? st.cnt[lane] : 0;
+        for (int w = 0; w < kFpWaves; ++w) {
+          F->wc[w][lane] = c;
+          c += F->wd[w][lane];
+        }
+      }
+      __syncthreads();
+      // (3) every wave: the log counts at its first point and their largest drift
+      {
+        const int c = F->wc[wv][lane];
+        double l1 = -INFINITY, l0 = -INFINITY, dr = 0.0;
+        if (lane < nsl) {
+          l1 = logn_dev(st, c);
+          l0 = logn_dev(st, c - 1);
+          const int a0 = st.snap[lane];
+          dr = a0 == c ? 0.0 : ((a0 < 1 || c < 1) ? INFINITY : fabs(l1 - st.sl1[lane]));
+        }
+        F->wl1[wv][lane] = l1;
+        F->wl0[wv][lane] = l0;
+        dr = wave_max(dr);
+        if (lane == 0) F->wdr[wv] = dr;
+        wave_sync();
+      }
+      // (4) the points after the first changed outcome draw again (all of them in round 0)
+      const unsigned long long mm = __ballot(mover);
+      const unsigned long long mb = mm & below;
+      bool changed = false;
+      if (in && tid > chg && tid <= fs) {
+        int cown = 0;
+        if (mb) {
+          for (unsigned long long t = mm; t; t &= t - 1) {
+            const int j = __ffsll((long long)t) - 1;
+            const int oj = __builtin_amdgcn_readlane(own, j), tj = __builtin_amdgcn_readlane(tgt, j);
+            if (j < lane) {
+              F->corr[oj][tid] -= 1;
+              F->corr[tj][tid] += 1;
+              cown += (tj == own ? 1 : 0) - (oj == own ? 1 : 0);
+            }
+          }
+        }
+        const int cnow = F->wc[wv][own] + cown;
+        const bool single = cnow == 1;
+        double drift = F->wdr[wv];
+        const double lo_own = cown == 0 ? F->wl0[wv][own] : logn_call(st.ltab, cnow - 1);
+        {
+          const int sa = st.snap[own];
+          drift = fmax(drift, sa == cnow ? 0.0 : ((sa >= 2 && cnow >= 2) ? fabs(lo_own - st.sl0[own]) : INFINITY));
+        }
+        double v[EM];
+#pragma unroll
+        for (int e = 0; e < EM; ++e) {
+          double w = 0.0;
+          if (e < K) {
+            const int s = st.sol[e];
+            const int cr = mb ? (int)F->corr[s][tid] : 0;
+            if (s == own) w = lo_own;
+            else if (cr == 0) w = F->wl1[wv][s];
+            else {
+              const int c = F->wc[wv][s] + cr;
+              w = logn_call(st.ltab, c);
+              const int a0 = st.snap[s];
+              drift = fmax(drift, a0 == c ? 0.0 : ((a0 < 1 || c < 1) ? INFINITY : fabs(w - st.sl1[s])));
+            }
+          }
+          v[e] = w;
+        }
+        int np;
+        if (struct0 && sp >= 0 && (drift == 0.0 || drift < sr)) {
+          np = sp;
+          fresh = false;
+        } else {
+          const double* Lr = a.L + (int64_t)r.x * ncol;
+#pragma unroll
+          for (int e = 0; e < EM; ++e) {
+            if (e < K) v[e] = v[e] + Lr[st.sol[e]];
+            else if (e < E) {
+              const int l = e - K;
+              v[e] = a.logfac + ((l == 0 && single) ? Lr[own] : Lr[a.S + l]);
+            }
+          }
+          np = fp_draw<EM>(v, E, rU);
+          fresh = true;
+        }
+        int ncl = 2, nt = own;
+        if (np >= 0) {
+          if (np < K) {
+            const int s2 = st.sol[np];
+            if (!single) { ncl = s2 != own ? 1 : 0; nt = s2; }
+          } else if (single && np == K) {
+            ncl = 0;
+          }
+        }
+        const int ctn = F->wc[wv][nt] + (mb ? (int)F->corr[nt][tid] : 0);
+        if (mb) {
+          for (unsigned long long t = mm; t; t &= t - 1) {
+            const int j = __ffsll((long long)t) - 1;
+            const int oj = __builtin_amdgcn_readlane(own, j), tj = __builtin_amdgcn_readlane(tgt, j);
+            if (j < lane) { F->corr[oj][tid] = 0; F->corr[tj][tid] = 0; }
+          }
+        }
+        changed = ncl != cls || (ncl == 1 && nt != tgt);
+        cls = ncl;
+        tgt = nt;
+        pick = np;
+        co = cnow;
+        ct = ctn;
+      }
+      const unsigned long long cbal = __ballot(changed);
+      if (lane == 0) F->wchg[wv] = cbal ? wv * kWave + __ffsll((long long)cbal) - 1 : kFpThreads;
+      __syncthreads();
+      int c2 = kFpThreads;
+      for (int w = 0; w < kFpWaves; ++w) c2 = min(c2, F->wchg[w]);
+      if (tid == 0) F->iters++;
+      if (c2 >= kFpThreads) { conv = true; break; }
+      chg = c2;
+    }
+    if (!conv) {       // cannot happen (at most nc + 1 rounds); stop loudly
+      if (tid == 0) { S.status = 5; S.next = F->pi[0]; }   // HDPM_E_ARG
+      go = false;
+      break;
+    }
+    // ---- the walk's drift after each position (running maximum from S.dnow), count bounds
+    const bool mv = in && cls == 1 && tid < fs;
+    double sd = mv ? fmax(slot_drift_at(st, own, co - 1), slot_drift_at(st, tgt, ct + 1)) : 0.0;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const double x = __shfl_up(sd, o);
+      if (lane >= o) sd = fmax(sd, x);
+    }
+    if (lane == kWave - 1) F->wsd[wv] = sd;
+    if (wv == 0) F->cmo[lane] = 0;
+    __syncthreads();
+    if (mv) atomicAdd(&F->cmo[own], 1);
+    double dpre = S.dnow;
+    for (int w = 0; w < wv; ++w) dpre = fmax(dpre, F->wsd[w]);
+    F->dnl[tid] = fmax(sd, dpre);
+    __syncthreads();
+    if (wv == 0) {
+      int mn = F->wc[0][lane];
+      for (int w = 1; w < kFpWaves; ++w) mn = min(mn, F->wc[w][lane]);
+      F->cmin[lane] = mn - F->cmo[lane];
+    }
+    __syncthreads();
+    // ---- unlisted points before the first stop (or before the chunk's last point)
+    int kc = fs;
+    {
+      const int64_t hi = fs < nc ? F->pi[fs] : F->pi[nc - 1];
+      const double dtop = fs > 0 ? F->dnl[fs - 1] : S.dnow;
+      if (dtop > a.dmax && hi > vfrom) {
+        const int64_t u = fp_verify(a, st, F, fs, S.dnow, vfrom, hi, F->cmin);
+        if (u < hi) {
+          int k = 0;
+          while (k < fs && F->pi[k] < u) ++k;
+          kc = k;
+          go = false;
+        }
+      }
+    }
+    // ---- commit the positions before kc: labels, move log, counts, drifts
+    const bool cm = mv && tid < kc;
+    const unsigned long long mmc = __ballot(cm);
+    const unsigned long long fbal = __ballot(in && tid < kc && fresh);
+    if (lane == 0) { F->wmov[wv] = __popcll(mmc); F->wfresh[wv] = __popcll(fbal); }
+    if (wv == 0) F->wd[0][lane] = 0;
+    __syncthreads();
+    if (cm) {
+      a.c[r.y] = tgt;
+      if (a.mlog) {
+        int q = F->nlog + __popcll(mmc & below);
+        for (int w = 0; w < wv; ++w) q += F->wmov[w];
+        a.mlog[3 * q] = r.y;
+        a.mlog[3 * q + 1] = own;
+        a.mlog[3 * q + 2] = tgt;
+      }
+      atomicAdd(&F->wd[0][own], -1);
+      atomicAdd(&F->wd[0][tgt], 1);
+    }
+    __syncthreads();
+    if (wv == 0) {
+      double cd = 0.0;
+      if (lane < nsl) {
+        const int dl = F->wd[0][lane];
+        if (dl != 0) {
+          const int c = st.cnt[lane] + dl;
+          st.cnt[lane] = c;
+          st.l1[lane] = logn_dev(st, c);
+          st.l0[lane] = logn_dev(st, c - 1);
+        }
+        cd = count_drift(st, a.logn, lane);
+      }
+      cd = wave_max(cd);
+      if (lane == 0) {
+        int nm = 0, nf = 0;
+        for (int w = 0; w < kFpWaves; ++w) { nm += F->wmov[w]; nf += F->wfresh[w]; }
+        S.moves += nm;
+        S.exact += nf;
+        if (kc > 0) S.dnow = fmax(S.dnow, F->dnl[kc - 1]);
+        S.dvmax = fmax(S.dvmax, cd);
+        if (a.mlog) F->nlog += nm;
+      }
+    }
+    if (tid == fs) {
+      F->stop_rq = r;
+      F->stop_pick = pick;
+      F->stop_fresh = fresh ? 1 : 0;
+    }
+    __syncthreads();
+    if (!go) break;
+    if (fs < nc) {
+      // ---- the stop: the serial path in the committed state (that of its turn)
+      const int4 rs = F->stop_rq;
+      if (wv == 0) fp_stop(a, st, F);
+      __syncthreads();
+      go = F->go != 0;
+      vfrom = (int64_t)rs.y + 1;
+      q0 += fs + 1;
+    } else {
+      vfrom = (int64_t)F->pi[nc - 1] + 1;
+      q0 += nc;
+    }
+    __syncthreads();
+  }
+  if (go && S.status == 0 && !S.restart && S.dnow > a.dmax) (void)fp_verify(a, st, F, 0, S.dnow, vfrom, a.n, st.cnt);
+  if (prof) { tp[5] = F->iters; tp[6] = total; tp[2] = chunks; }
+  resolve_finish(a, st, F->nlog, tp, prof);
+}
+
 // ------------------------------------------------------------------ end of sweep
 // The sweep-end kernels are enqueued behind every resolver launch and read its control
 // block: they act only when that launch finished the sweep, so the host need not wait for
@@ -2642,7 +3074,11 @@ size_t resolve_smem_bytes(int lcap, int m, int blocks) {
 }
 
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s) {
-  if (a.blocks)
+  if (a.fp) {
+    const size_t lds = resolve_fp_lds_bytes(a.lcap, a.m);
+    if (a.K + a.m <= 32) hipLaunchKernelGGL(k_resolve_fp<32>, dim3(1), dim3(kFpThreads), lds, s, a);
+    else hipLaunchKernelGGL(k_resolve_fp<64>, dim3(1), dim3(kFpThreads), lds, s, a);
+  } else if (a.blocks)
     hipLaunchKernelGGL(k_resolve_blk, dim3(1), dim3(kWave), resolve_lds_bytes(a.lcap, a.m, 1), s, a);
   else
     hipLaunchKernelGGL(k_resolve, dim3(1), dim3(kWave), resolve_lds_bytes(a.lcap, a.m, 0, a.S + a.m), s, a);

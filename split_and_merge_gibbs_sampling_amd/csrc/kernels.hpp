@@ -232,6 +232,7 @@ struct ResolveArgs {
   const int* gate;           // as PrepassArgs
   const uint32_t* const* raw_ptr;
   int dry;                   // 1: stop (kDryStop) at the first decision that is not "stay"
+  int fp;                    // 1: fixed-point resolver (k_resolve_fp; needs K + m <= 64, lcap <= 64)
 };
 
 // Cluster parameter upload: one staging buffer, scattered on the device.

@@ -122,7 +122,9 @@ def test_c4_full_size_neal8_and_split_merge(hd, oracle):
 
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("L", [1, 20])
-@pytest.mark.parametrize("debug", [0, 4096])     # 4096: the resolver without block mode
+# 0: the fixed-point resolver (k_resolve_fp); 4096: the one-wave LIST resolver without block
+# mode; 8388608 (bit 23): the one-wave resolvers with block mode after many exact decisions
+@pytest.mark.parametrize("debug", [0, 4096, 8388608])
 def test_c2_full_size_unconverged_starts(hd, oracle, L, debug):
     """C2: N = 10,000, D = 32, binary, from one cluster (L = 1) or a random assignment to 20
     labels (la:31-43, the scripts' L = 20): far from the posterior, points move every sweep
