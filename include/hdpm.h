@@ -179,7 +179,11 @@ int hdpm_reset_stats(hdpm_ctx* ctx);
  * slice (it is copied when the next sweep's draws are reserved); bit 21: the iteration
  * commits the new tables and computes the log-likelihood before it prepares the next sweep
  * (by default the next speculative update_phi is started first); bit 22: no next sweep
- * enqueued while the iteration's update is drawn (gated on the device, k_pipe_wait). */
+ * enqueued while the iteration's update is drawn (gated on the device, k_pipe_wait); bit 23:
+ * the one-wave resolvers (LIST mode, block mode after many exact decisions) instead of the
+ * fixed-point resolver k_resolve_fp (which bits 0, 12 and 13 also turn off); bit 24: with the
+ * fixed-point resolver too, a launch after one that decided many points itself lists every
+ * point (no certification by the draw's uniform), as the one-wave resolvers always do. */
 int hdpm_set_debug(hdpm_ctx* ctx, int32_t mode);
 /* The prepass's pool-entry heads, P entries of wb*Ws + 2 words padded to a power of two
  * (Ws <= 4) or to a multiple of 8 words (wide layouts) (csrc/kernels.hpp "Pool-entry heads",

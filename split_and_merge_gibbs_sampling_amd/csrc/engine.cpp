@@ -684,6 +684,7 @@ struct Ctx {
   DevBuf<double> d_slot_tab;
   DevBuf<uint64_t> d_slot_bnd;
   int scap = 0;
+  bool last_fp = false;        // the last resolver launch was k_resolve_fp (diagnostics)
   int last_exact = 0;         // points the previous resolver launch decided one by one (block-mode choice)
   int last_listed = -1;       // points the previous launch's prepass listed (exact-rows grid), -1 unknown
   bool last_unsettled = false;  // the previous launch exceeded its drift budget or restarted
@@ -1870,6 +1871,9 @@ struct Ctx {
   // a prepared sweep can start on the device and still be dropped), kRoundResolve (the rest,
   // after a prefix launched with the same arguments and no state change in between).
   enum { kRoundAll = 0, kRoundPrefix = 1, kRoundResolve = 2 };
+  bool fp_eligible(int E, int lcap) const {
+    return E <= 64 && lcap <= 64 && !(debug & (1 | 4096 | 8192 | 8388608));
+  }
   // pg: a sweep enqueued ahead (pre_enqueue) -- its kernels take the gate and the draws
   // from pg, its control block is cpar; no timing events, no counters.
   int launch_round(int p, int nslots, int m, const uint32_t* d_sweep_raw, bool track, int part = kRoundAll,
@@ -1913,7 +1917,11 @@ struct Ctx {
     // certification by the draw's uniform only while the chain is settled: after a launch
     // that exceeded its drift budget, restarted or decided many points itself, uniform-
     // certified points (no exact rows) would fail re-verification and restart the launch
-    pa.dmax2 = ((debug & (1 | 262144)) || last_unsettled || last_exact >= kResolveBlkMin) ? INFINITY : 2.0 * dmax;
+    // (the fixed-point resolver re-tests and restarts cheaply enough to keep the uniform
+    // certification after many exact decisions; debug bit 24 lists every point there too)
+    const bool fp_next = fp_eligible(K + m, std::min(scap, nslots + 2));
+    const bool many_exact = last_exact >= kResolveBlkMin && (!fp_next || (debug & 16777216));
+    pa.dmax2 = ((debug & (1 | 262144)) || last_unsettled || many_exact) ? INFINITY : 2.0 * dmax;
     pa.L = d_L.p; pa.rowpos = d_rowpos.p; pa.margin = d_margin.p; pa.list = d_list.p; pa.cnt = d_cnt.p;
     pa.dense = d_dense.p; pa.dense_total = d_dense_total.p;
     pa.spec = (debug & 8) ? nullptr : d_spec.p;
@@ -1983,8 +1991,9 @@ struct Ctx {
                  ((debug & 8192) || last_exact >= kResolveBlkMin)) ? 1 : 0;
     // the fixed-point resolver whenever the state fits it (debug bit 23: the one-wave LIST /
     // block modes; bits 12 / 13 select those modes and keep them)
-    ra.fp = (K + m <= 64 && ra.lcap <= 64 && !(debug & (1 | 4096 | 8192 | 8388608))) ? 1 : 0;
+    ra.fp = fp_eligible(K + m, ra.lcap) ? 1 : 0;
     if (ra.fp) ra.blocks = 0;
+    if (part != kRoundPrefix && !pg) last_fp = ra.fp != 0;
     if (resolve_smem_bytes(ra.lcap, m, ra.blocks) > 160 * 1024) {
       err = "too many clusters for the resolver (K > ~2300)";
       return kArg;
@@ -2308,7 +2317,16 @@ struct Ctx {
       // the sweep enqueued ahead runs only after a complete sweep without moves
       if (pre.active && (c.status || c.next < n || c.moves)) pre_release();
       last_sweep_rounds = (int)(stats.rounds - rounds0);
-      if (debug & 2) {
+      if ((debug & 2) && last_fp) {
+        long long tp[16];
+        HIPCHK(hipMemcpy(tp, d_rprof.p, sizeof(tp), hipMemcpyDeviceToHost));
+        std::fprintf(stderr,
+                     "[resolve_fp] init %.2f us, %lld listed in %lld chunks: rounds %lld (%.2f us), drift / re-test / "
+                     "commit %.2f us, %lld stops (%.2f us), total %.2f us; in rounds: counts %.2f us, ballots %.2f us, "
+                     "evaluations (slowest wave) %.2f us, %lld evaluations, %lld own draws\n",
+                     (tp[1] - tp[0]) / 100.0, tp[9], tp[8], tp[5], tp[3] / 100.0, tp[4] / 100.0, tp[6], tp[2] / 100.0,
+                     (tp[7] - tp[0]) / 100.0, tp[10] / 100.0, tp[11] / 100.0, tp[12] / 100.0, tp[14], tp[15]);
+      } else if (debug & 2) {
         long long tp[16];
         HIPCHK(hipMemcpy(tp, d_rprof.p, sizeof(tp), hipMemcpyDeviceToHost));
         std::fprintf(stderr,

@@ -2330,28 +2330,30 @@ struct FpShared {
   double wdr[kFpWaves];             // max over slots of |logn[wc] - logn[snapshot count]|
   double wsd[kFpWaves];
   int wstop[kFpWaves], wchg[kFpWaves], wmov[kFpWaves], wfresh[kFpWaves];
+  long long wev[kFpWaves];          // diagnostics: each wave's evaluation ticks in a round
   int cmo[kWave];                   // moves out of each slot in the chunk
   int cmin[kWave];                  // lower bounds on the counts during the chunk
   int pi[kFpThreads];               // point of each chunk position
   double dnl[kFpThreads];           // the walk's drift after each chunk position
   int nlog, go, ufail, stop_pick, stop_fresh, iters, pad0, pad1;
   int4 stop_rq;
-  signed char corr[kWave][kFpThreads];  // per position: count changes from its wave's earlier moves
+  unsigned long long bin[kFpWaves][kWave];   // per wave and slot: the movers into the slot
+  unsigned long long bout[kFpWaves][kWave];  // ... and out of it
 };
 
 __host__ __device__ inline size_t resolve_fp_lds_bytes(int lcap, int m) {
   return ((resolve_lds_bytes(lcap, m, 0, 0) + 15) & ~(size_t)15) + sizeof(FpShared);
 }
 
-__device__ __forceinline__ double logn_call(const uint64_t* ltab, int c) {
-  return c <= 0 ? -INFINITY : glibc::log_r((double)c, ltab);
-}
+// logn[c] from the host's table (the same glibc values logn_dev computes): independent loads
+// the per-lane code issues together, instead of dependent log evaluations
+__device__ __forceinline__ double fp_logn(const ResolveArgs& a, int c) { return c <= 0 ? -INFINITY : a.logn[c]; }
 
 // slot_drift of slot s at count b (k_resolve's running drift after a move)
-__device__ __forceinline__ double slot_drift_at(const RState& st, int s, int b) {
-  const int a = st.snap[s];
-  if (a >= 2) return b < 2 ? INFINITY : fabs(logn_call(st.ltab, b - 1) - st.sl0[s]);
-  if (a == 1) return b == 0 ? 0.0 : logn_call(st.ltab, b);
+__device__ __forceinline__ double slot_drift_at(const ResolveArgs& a, const RState& st, int s, int b) {
+  const int a0 = st.snap[s];
+  if (a0 >= 2) return b < 2 ? INFINITY : fabs(fp_logn(a, b - 1) - st.sl0[s]);
+  if (a0 == 1) return b == 0 ? 0.0 : fp_logn(a, b);
   return INFINITY;
 }
 
@@ -2466,7 +2468,6 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
   long long tp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const bool prof = a.prof != nullptr;
   if (prof) tp[0] = wall_clock64();
-  for (int x = tid; x < kWave * kFpThreads / 4; x += kFpThreads) ((int*)F->corr)[x] = 0;
   if (tid == 0) { F->nlog = a.mcount ? *a.mcount : 0; F->go = 1; F->iters = 0; }
   resolve_init(a, st);
   const int total = *a.dense_total;
@@ -2475,9 +2476,11 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
   int64_t vfrom = a.p0;
   bool go = true;
   int chunks = 0;
+  long long t_a = 0;
   if (prof) tp[1] = wall_clock64();
   for (int q0 = 0; q0 < total && go;) {
     ++chunks;
+    if (prof) t_a = wall_clock64();
     const int nc = min(kFpThreads, total - q0);
     const bool in = tid < nc;
     const int4 r = in ? a.rq[q0 + tid] : make_int4(0, 0, 0, 0);
@@ -2493,6 +2496,7 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
     int chg = -1, fs = nc;
     bool conv = false;
     for (int it = 0; it <= kFpThreads + 1; ++it) {
+      const long long tr0 = prof ? wall_clock64() : 0;
       // (1) the first stop of the current outcomes; each wave's net count changes before it
       const unsigned long long sbal = __ballot(in && cls == 2);
       if (lane == 0) F->wstop[wv] = sbal ? wv * kWave + __ffsll((long long)sbal) - 1 : kFpThreads;
@@ -2520,8 +2524,8 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
         const int c = F->wc[wv][lane];
         double l1 = -INFINITY, l0 = -INFINITY, dr = 0.0;
         if (lane < nsl) {
-          l1 = logn_dev(st, c);
-          l0 = logn_dev(st, c - 1);
+          l1 = fp_logn(a, c);
+          l0 = fp_logn(a, c - 1);
           const int a0 = st.snap[lane];
           dr = a0 == c ? 0.0 : ((a0 < 1 || c < 1) ? INFINITY : fabs(l1 - st.sl1[lane]));
         }
@@ -2531,27 +2535,32 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
         if (lane == 0) F->wdr[wv] = dr;
         wave_sync();
       }
-      // (4) the points after the first changed outcome draw again (all of them in round 0)
-      const unsigned long long mm = __ballot(mover);
-      const unsigned long long mb = mm & below;
+      const long long tr1 = prof ? wall_clock64() : 0;
+      // (4) the wave's moves per slot it touches (ballot masks: a point's count change of slot
+      // s from the moves before it in its wave is popc(in & below) - popc(out & below))
+      unsigned long long touch = mover ? ((1ull << own) | (1ull << tgt)) : 0ull;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) touch |= __shfl_xor(touch, o);
+      for (unsigned long long t = touch; t; t &= t - 1) {
+        const int sl = __ffsll((long long)t) - 1;
+        const unsigned long long bi = __ballot(mover && tgt == sl), bo = __ballot(mover && own == sl);
+        if (lane == 0) { F->bin[wv][sl] = bi; F->bout[wv][sl] = bo; }
+      }
+      wave_sync();
+      auto corr = [&](int sl) -> int {
+        if (!((touch >> sl) & 1ull)) return 0;
+        return __popcll(F->bin[wv][sl] & below) - __popcll(F->bout[wv][sl] & below);
+      };
+      const long long tr2 = prof ? wall_clock64() : 0;
+      // (5) the points after the first changed outcome draw again (all of them in round 0)
       bool changed = false;
-      if (in && tid > chg && tid <= fs) {
-        int cown = 0;
-        if (mb) {
-          for (unsigned long long t = mm; t; t &= t - 1) {
-            const int j = __ffsll((long long)t) - 1;
-            const int oj = __builtin_amdgcn_readlane(own, j), tj = __builtin_amdgcn_readlane(tgt, j);
-            if (j < lane) {
-              F->corr[oj][tid] -= 1;
-              F->corr[tj][tid] += 1;
-              cown += (tj == own ? 1 : 0) - (oj == own ? 1 : 0);
-            }
-          }
-        }
+      const bool evl = in && tid > chg && tid <= fs;
+      if (evl) {
+        const int cown = corr(own);
         const int cnow = F->wc[wv][own] + cown;
         const bool single = cnow == 1;
         double drift = F->wdr[wv];
-        const double lo_own = cown == 0 ? F->wl0[wv][own] : logn_call(st.ltab, cnow - 1);
+        const double lo_own = cown == 0 ? F->wl0[wv][own] : fp_logn(a, cnow - 1);
         {
           const int sa = st.snap[own];
           drift = fmax(drift, sa == cnow ? 0.0 : ((sa >= 2 && cnow >= 2) ? fabs(lo_own - st.sl0[own]) : INFINITY));
@@ -2562,12 +2571,12 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
           double w = 0.0;
           if (e < K) {
             const int s = st.sol[e];
-            const int cr = mb ? (int)F->corr[s][tid] : 0;
+            const int cr = corr(s);
             if (s == own) w = lo_own;
             else if (cr == 0) w = F->wl1[wv][s];
             else {
               const int c = F->wc[wv][s] + cr;
-              w = logn_call(st.ltab, c);
+              w = fp_logn(a, c);
               const int a0 = st.snap[s];
               drift = fmax(drift, a0 == c ? 0.0 : ((a0 < 1 || c < 1) ? INFINITY : fabs(w - st.sl1[s])));
             }
@@ -2600,14 +2609,7 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
             ncl = 0;
           }
         }
-        const int ctn = F->wc[wv][nt] + (mb ? (int)F->corr[nt][tid] : 0);
-        if (mb) {
-          for (unsigned long long t = mm; t; t &= t - 1) {
-            const int j = __ffsll((long long)t) - 1;
-            const int oj = __builtin_amdgcn_readlane(own, j), tj = __builtin_amdgcn_readlane(tgt, j);
-            if (j < lane) { F->corr[oj][tid] = 0; F->corr[tj][tid] = 0; }
-          }
-        }
+        const int ctn = F->wc[wv][nt] + corr(nt);
         changed = ncl != cls || (ncl == 1 && nt != tgt);
         cls = ncl;
         tgt = nt;
@@ -2617,10 +2619,25 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
       }
       const unsigned long long cbal = __ballot(changed);
       if (lane == 0) F->wchg[wv] = cbal ? wv * kWave + __ffsll((long long)cbal) - 1 : kFpThreads;
+      if (prof) {
+        const long long tr3 = wall_clock64();
+        const int ne = __popcll(__ballot(evl)), nf = __popcll(__ballot(evl && fresh));
+        if (lane == 0) {
+          F->wev[wv] = tr3 - tr2;
+          atomicAdd((unsigned long long*)&S.tsub[6], (unsigned long long)ne);
+          atomicAdd((unsigned long long*)&S.tsub[7], (unsigned long long)nf);
+        }
+        if (tid == 0) { S.tsub[2] += tr1 - tr0; S.tsub[3] += tr2 - tr1; }
+      }
       __syncthreads();
       int c2 = kFpThreads;
       for (int w = 0; w < kFpWaves; ++w) c2 = min(c2, F->wchg[w]);
       if (tid == 0) F->iters++;
+      if (prof && tid == 0) {
+        long long mx = 0;
+        for (int w = 0; w < kFpWaves; ++w) mx = max(mx, F->wev[w]);
+        S.tsub[4] += mx;
+      }
       if (c2 >= kFpThreads) { conv = true; break; }
       chg = c2;
     }
@@ -2629,9 +2646,10 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
       go = false;
       break;
     }
+    if (prof) { const long long t = wall_clock64(); tp[3] += t - t_a; t_a = t; }
     // ---- the walk's drift after each position (running maximum from S.dnow), count bounds
     const bool mv = in && cls == 1 && tid < fs;
-    double sd = mv ? fmax(slot_drift_at(st, own, co - 1), slot_drift_at(st, tgt, ct + 1)) : 0.0;
+    double sd = mv ? fmax(slot_drift_at(a, st, own, co - 1), slot_drift_at(a, st, tgt, ct + 1)) : 0.0;
 #pragma unroll
     for (int o = 1; o < kWave; o <<= 1) {
       const double x = __shfl_up(sd, o);
@@ -2693,8 +2711,8 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
         if (dl != 0) {
           const int c = st.cnt[lane] + dl;
           st.cnt[lane] = c;
-          st.l1[lane] = logn_dev(st, c);
-          st.l0[lane] = logn_dev(st, c - 1);
+          st.l1[lane] = fp_logn(a, c);
+          st.l0[lane] = fp_logn(a, c - 1);
         }
         cd = count_drift(st, a.logn, lane);
       }
@@ -2715,6 +2733,7 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
       F->stop_fresh = fresh ? 1 : 0;
     }
     __syncthreads();
+    if (prof) { const long long t = wall_clock64(); tp[4] += t - t_a; t_a = t; }
     if (!go) break;
     if (fs < nc) {
       // ---- the stop: the serial path in the committed state (that of its turn)
@@ -2724,6 +2743,7 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
       go = F->go != 0;
       vfrom = (int64_t)rs.y + 1;
       q0 += fs + 1;
+      if (prof) { tp[2] += wall_clock64() - t_a; tp[6] += 1; }
     } else {
       vfrom = (int64_t)F->pi[nc - 1] + 1;
       q0 += nc;
@@ -2731,7 +2751,9 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
     __syncthreads();
   }
   if (go && S.status == 0 && !S.restart && S.dnow > a.dmax) (void)fp_verify(a, st, F, 0, S.dnow, vfrom, a.n, st.cnt);
-  if (prof) { tp[5] = F->iters; tp[6] = total; tp[2] = chunks; }
+  // prof: [1] start of the walk, [2] stop ticks, [3] fixed-point rounds ticks, [4] drift /
+  // re-test / commit ticks, [5] rounds, [6] stops; tsub[0] chunks, tsub[1] listed
+  if (prof && tid == 0) { tp[5] = F->iters; S.tsub[0] = chunks; S.tsub[1] = total; }
   resolve_finish(a, st, F->nlog, tp, prof);
 }
 
