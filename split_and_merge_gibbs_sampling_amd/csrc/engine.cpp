@@ -2323,9 +2323,9 @@ struct Ctx {
         std::fprintf(stderr,
                      "[resolve_fp] init %.2f us, %lld listed in %lld chunks: rounds %lld (%.2f us), drift / re-test / "
                      "commit %.2f us, %lld stops (%.2f us), total %.2f us; in rounds: counts %.2f us, ballots %.2f us, "
-                     "evaluations (slowest wave) %.2f us, %lld evaluations, %lld own draws\n",
+                     "evaluations (slowest wave) %.2f us, %lld evaluations, %lld own draws (row loads + draws: %.2f us, summed over waves)\n",
                      (tp[1] - tp[0]) / 100.0, tp[9], tp[8], tp[5], tp[3] / 100.0, tp[4] / 100.0, tp[6], tp[2] / 100.0,
-                     (tp[7] - tp[0]) / 100.0, tp[10] / 100.0, tp[11] / 100.0, tp[12] / 100.0, tp[14], tp[15]);
+                     (tp[7] - tp[0]) / 100.0, tp[10] / 100.0, tp[11] / 100.0, tp[12] / 100.0, tp[14], tp[15], tp[13] / 100.0);
       } else if (debug & 2) {
         long long tp[16];
         HIPCHK(hipMemcpy(tp, d_rprof.p, sizeof(tp), hipMemcpyDeviceToHost));

@@ -89,6 +89,54 @@ HDPM_HD inline double exp_r(double x, const uint64_t* T) {
   return __builtin_fma(scale, tmp, scale);
 }
 
+// exp_r without branches: every path of exp_r evaluated (the main path's table index is
+// masked, so any input is safe) and the result selected, with the same operations on the
+// selected path -- straight-line code, so unrolled callers issue their table loads together
+// (k_resolve_fp's per-lane draws).  Same bits as exp_r for every input.
+HDPM_HD inline double exp_bf(double x, const uint64_t* T) {
+  const uint64_t ix = asu(x);
+  const uint32_t abstop = (uint32_t)(ix >> 52) & 0x7ffu;
+  const bool out = abstop - 0x3c9u > 0x3eu;
+  const bool tiny = out && (int)(abstop - 0x3c9u) < 0;
+  const bool huge = out && !tiny && abstop >= 0x409u;
+  const bool special = out && !tiny && !huge;
+  const double kd0 = __builtin_fma(x, kExpInvLn2N, kExpShift);
+  const uint64_t ki = asu(kd0);
+  const double kd = kd0 - kExpShift;
+  double r = __builtin_fma(kd, kExpNegLn2hiN, x);
+  r = __builtin_fma(kd, kExpNegLn2loN, r);
+  const uint32_t i2 = 2u * (uint32_t)(ki & 127u);
+  const uint64_t sbits = T[i2 + 1] + (ki << 45);
+  const double p23 = __builtin_fma(r, kExpC3, kExpC2);
+  const double rt = r + asd(T[i2]);
+  const double r2 = r * r;
+  const double p45 = __builtin_fma(r, kExpC5, kExpC4);
+  const double t = __builtin_fma(p23, r2, rt);
+  const double r4 = r2 * r2;
+  const double tmp = __builtin_fma(r4, p45, t);
+  const double scale = asd(sbits);
+  const double r_main = __builtin_fma(scale, tmp, scale);
+  // exp_special, both branches
+  const double sc1 = asd(sbits - (1009ull << 52));
+  const double r_hi = __builtin_fma(sc1, tmp, sc1) * 0x1p1009;
+  const double sc2 = asd(sbits + (1022ull << 52));
+  const double st = tmp * sc2;
+  const double y = sc2 + st;
+  const double hi = y + 1.0;
+  double lo = sc2 - y;
+  lo = lo + st;
+  double y2 = (1.0 - hi) + y;
+  y2 = y2 + lo;
+  y2 = y2 + hi;
+  y2 = y2 - 1.0;
+  y2 = y2 == 0.0 ? 0.0 : y2;
+  const double r_lo = (1.0 > y ? y2 : y) * 0x1p-1022;
+  const double r_sp = (ki & 0x80000000u) == 0 ? r_hi : r_lo;
+  const double r_huge = ix == 0xfff0000000000000ull ? 0.0
+                        : (abstop >= 0x7ffu ? x + 1.0 : ((ix >> 63) ? 0.0 : __builtin_inf()));
+  return tiny ? x + 1.0 : (huge ? r_huge : (special ? r_sp : r_main));
+}
+
 // log(x); T = kGlibcLogTab ({invc, logc} x 128) or a copy of it
 HDPM_HD inline double log_r(double x, const uint64_t* T) {
   uint64_t ix = asu(x);

@@ -1818,7 +1818,10 @@ __device__ __forceinline__ void resolve_layout(const ResolveArgs& a, RState& st,
   st.sol = st.snap + st.lcap;
   st.los = st.sol + st.lcap;
   st.perm = st.los + st.lcap;
-  st.ltab = (uint64_t*)(((uintptr_t)(st.perm + st.emax) + 15) & ~(uintptr_t)15);
+  // offsets from smem (not integer casts of the pointers): the arrays stay LDS pointers for
+  // the compiler (ds_read, not flat loads that the LDS wait counter would also wait for)
+  auto up16 = [&](const void* q) { return smem + ((((const unsigned char*)q - smem) + 15) & ~(ptrdiff_t)15); };
+  st.ltab = (uint64_t*)up16(st.perm + st.emax);
   st.bp = nullptr;
   st.bperm = nullptr;
   st.bcmin = nullptr;
@@ -1830,7 +1833,7 @@ __device__ __forceinline__ void resolve_layout(const ResolveArgs& a, RState& st,
     st.bp = st.sl0 + st.lcap;
     st.bperm = (int*)(st.bp + 64 * kWave);
     st.bcmin = st.bperm + 64 * kWave;
-    st.brq = (int4*)(((uintptr_t)(st.bcmin + kWave) + 15) & ~(uintptr_t)15);
+    st.brq = (int4*)up16(st.bcmin + kWave);
   }
 }
 
@@ -2325,12 +2328,10 @@ constexpr int kFpFallback = -1000;
 struct FpShared {
   int wc[kFpWaves][kWave];          // slot counts at each wave's first point
   int wd[kFpWaves][kWave];          // each wave's net count change per slot
-  double wl1[kFpWaves][kWave];      // logn[wc]
-  double wl0[kFpWaves][kWave];      // logn[wc - 1]
-  double wdr[kFpWaves];             // max over slots of |logn[wc] - logn[snapshot count]|
   double wsd[kFpWaves];
   int wstop[kFpWaves], wchg[kFpWaves], wmov[kFpWaves], wfresh[kFpWaves];
   long long wev[kFpWaves];          // diagnostics: each wave's evaluation ticks in a round
+  uint64_t etab[256];               // glibc's exp table (fp_draw)
   int cmo[kWave];                   // moves out of each slot in the chunk
   int cmin[kWave];                  // lower bounds on the counts during the chunk
   int pi[kFpThreads];               // point of each chunk position
@@ -2347,7 +2348,18 @@ __host__ __device__ inline size_t resolve_fp_lds_bytes(int lcap, int m) {
 
 // logn[c] from the host's table (the same glibc values logn_dev computes): independent loads
 // the per-lane code issues together, instead of dependent log evaluations
-__device__ __forceinline__ double fp_logn(const ResolveArgs& a, int c) { return c <= 0 ? -INFINITY : a.logn[c]; }
+// A load from global memory as such (a global_load, not a flat one: flat loads count
+// against the LDS wait counter too, so every LDS wait would wait for them)
+template <class T>
+__device__ __forceinline__ T gld(const T* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return *(const __attribute__((address_space(1))) T*)p;
+#else
+  return *p;     // host pass: never called
+#endif
+}
+
+__device__ __forceinline__ double fp_logn(const ResolveArgs& a, int c) { return c <= 0 ? -INFINITY : gld(a.logn + c); }
 
 // slot_drift of slot s at count b (k_resolve's running drift after a move)
 __device__ __forceinline__ double slot_drift_at(const ResolveArgs& a, const RState& st, int s, int b) {
@@ -2362,24 +2374,60 @@ __device__ __forceinline__ double slot_drift_at(const ResolveArgs& a, const RSta
 // descending order walked group by group of equal values with the reference's cumulative
 // sums; a pick inside a group of more than one entry (whose order is heapsort's) returns
 // kFpFallback.  E <= EM <= 200 (no Walker tables).  Returns the index or -status.
+// exp(x) for x = v - max <= 0 as fp_draw needs it: glibc's main path (exp_r's value for
+// -512 < x <= 0, its |x| < 2^-54 path included), and 0 for x <= -512.  An entry with x <= -512
+// has p < e^-512 < 2^-738 against a sum >= 1 (the maximum's exp(0) = 1), so the sums round
+// the same whether it is added or not, every other probability keeps its bits, and it cannot
+// be drawn: it sorts behind every entry with x > -512, and the cumulative sum over those
+// reaches 1 - E 2^-52 before it, far above the largest uniform 1 - 2^-33 (raw_to_unif).  So
+// the draw is the reference's for every input, with a third of exp_bf's operations.
+__device__ __forceinline__ double fp_exp(double x, const uint64_t* T) {
+  using namespace glibc;
+  const uint64_t ix = asu(x);
+  const uint32_t abstop = (uint32_t)(ix >> 52) & 0x7ffu;
+  const bool tiny = (int)(abstop - 0x3c9u) < 0;
+  const double kd0 = __builtin_fma(x, kExpInvLn2N, kExpShift);
+  const uint64_t ki = asu(kd0);
+  const double kd = kd0 - kExpShift;
+  double r = __builtin_fma(kd, kExpNegLn2hiN, x);
+  r = __builtin_fma(kd, kExpNegLn2loN, r);
+  const uint32_t i2 = 2u * (uint32_t)(ki & 127u);
+  const uint64_t sbits = T[i2 + 1] + (ki << 45);
+  const double p23 = __builtin_fma(r, kExpC3, kExpC2);
+  const double rt = r + asd(T[i2]);
+  const double r2 = r * r;
+  const double p45 = __builtin_fma(r, kExpC5, kExpC4);
+  const double t = __builtin_fma(p23, r2, rt);
+  const double r4 = r2 * r2;
+  const double tmp = __builtin_fma(r4, p45, t);
+  const double scale = asd(sbits);
+  const double y = __builtin_fma(scale, tmp, scale);
+  return tiny ? x + 1.0 : (x > -512.0 ? y : 0.0);
+}
+
 template <int EM>
-__device__ int fp_draw(double (&v)[EM], int E, double rU) {
+__device__ int fp_draw(double (&v)[EM], int E, double rU, const uint64_t* etab) {
+  // branch-free over the EM slots (padding: exp(-inf) = 0 adds nothing to the sums), so
+  // the exps' table loads are issued together
   double mx = -INFINITY;
 #pragma unroll
-  for (int e = 0; e < EM; ++e)
-    if (e < E) mx = fmax(mx, v[e]);
+  for (int e = 0; e < EM; ++e) {
+    v[e] = e < E ? v[e] : -INFINITY;
+    mx = fmax(mx, v[e]);
+  }
 #pragma unroll
-  for (int e = 0; e < EM; ++e) v[e] = e < E ? dexp(v[e] - mx) : 0.0;       // n8:95
+  for (int e = 0; e < EM; ++e) {
+    const double p = fp_exp(v[e] - mx, etab);                                 // n8:95
+    v[e] = e < E ? p : 0.0;
+  }
   double sum = 0.0;
 #pragma unroll
-  for (int e = 0; e < EM; ++e)
-    if (e < E) sum += v[e];
+  for (int e = 0; e < EM; ++e) sum += v[e];
 #pragma unroll
   for (int e = 0; e < EM; ++e) v[e] = v[e] / sum;                           // n8:96
   double s2 = 0.0;                                                          // FixupProb
 #pragma unroll
-  for (int e = 0; e < EM; ++e)
-    if (e < E) s2 += v[e] > 0 ? v[e] : 0.0;
+  for (int e = 0; e < EM; ++e) s2 += v[e] > 0 ? v[e] : 0.0;
   if (!(s2 > 0)) return -3;
 #pragma unroll
   for (int e = 0; e < EM; ++e) v[e] = e < E ? v[e] / s2 : -1.0;
@@ -2390,10 +2438,11 @@ __device__ int fp_draw(double (&v)[EM], int E, double rU) {
 #pragma unroll
     for (int e = 0; e < EM; ++e) {
       const double x = v[e];
-      if (x < prev) {
-        if (x > cur) { cur = x; g = 1; idx = e; }
-        else if (x == cur) ++g;
-      }
+      const bool lt = x < prev;
+      const bool gt = lt && x > cur, eq = lt && x == cur;
+      cur = gt ? x : cur;
+      idx = gt ? e : idx;
+      g = gt ? 1 : (eq ? g + 1 : g);
     }
     if (g == 0) return kFpFallback;
     for (int k = 0; k < g; ++k, ++j) {
@@ -2416,7 +2465,7 @@ __device__ int64_t fp_verify(const ResolveArgs& a, const RState& st, FpShared* F
   __syncthreads();
   for (int64_t b = lo; b < hi; b += kFpThreads) {
     const int64_t j = b + threadIdx.x;
-    if (j < hi && a.rowpos[j] < 0) {
+    if (j < hi && gld(a.rowpos + j) < 0) {
       int k0 = 0, k1 = nk;
       while (k0 < k1) {
         const int md = (k0 + k1) >> 1;
@@ -2424,8 +2473,8 @@ __device__ int64_t fp_verify(const ResolveArgs& a, const RState& st, FpShared* F
       }
       const double dn = k0 > 0 ? F->dnl[k0 - 1] : dn0;
       if (dn > a.dmax) {
-        const double mg = a.margin[j] - 2.0 * dn;
-        if (!((mg > a.T || stay_by_uniform(mg, a.raw[j * (a.m + 1) + a.m], a.K + a.m)) && cmin[a.c[j]] >= 2))
+        const double mg = gld(a.margin + j) - 2.0 * dn;
+        if (!((mg > a.T || stay_by_uniform(mg, gld(a.raw + j * (a.m + 1) + a.m), a.K + a.m)) && cmin[gld(a.c + j)] >= 2))
           atomicMin(&F->ufail, (int)j);
       }
     }
@@ -2441,8 +2490,12 @@ __device__ int64_t fp_verify(const ResolveArgs& a, const RState& st, FpShared* F
 
 // wave 0: the chunk's stop (F->stop_*) decided and applied by the serial path.  Not inlined:
 // the serial decision's registers stay out of the fixed-point loop's allocation.
-__device__ __noinline__ void fp_stop(const ResolveArgs& a, const RState& st, FpShared* F) {
+__device__ __noinline__ void fp_stop(const ResolveArgs& a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63;
+  RState st;     // rebuilt here: passing the caller's would keep its arrays out of registers
+  resolve_layout(a, st, smem, false);
+  FpShared* F = (FpShared*)(smem + ((resolve_lds_bytes(a.lcap, a.m, 0, 0) + 15) & ~(size_t)15));
   RCtx R{a, st, *st.sh, lane, a.S + a.m, a.scap, F->nlog, false};
   const int4 rs = F->stop_rq;
   const int pk = F->stop_pick;
@@ -2469,6 +2522,7 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
   const bool prof = a.prof != nullptr;
   if (prof) tp[0] = wall_clock64();
   if (tid == 0) { F->nlog = a.mcount ? *a.mcount : 0; F->go = 1; F->iters = 0; }
+  for (int e = tid; e < 256; e += kFpThreads) F->etab[e] = devtab::kGlibcExpTab[e];
   resolve_init(a, st);
   const int total = *a.dense_total;
   const int ncol = a.S + a.m;
@@ -2483,10 +2537,10 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
     if (prof) t_a = wall_clock64();
     const int nc = min(kFpThreads, total - q0);
     const bool in = tid < nc;
-    const int4 r = in ? a.rq[q0 + tid] : make_int4(0, 0, 0, 0);
+    const int4 r = in ? gld(a.rq + q0 + tid) : make_int4(0, 0, 0, 0);
     const int own = r.z;
-    const int sp = (in && a.spec) ? a.spec[q0 + tid] : -1;
-    const double sr = (in && a.spec) ? a.spec_rad[q0 + tid] : 0.0;
+    const int sp = (in && a.spec) ? gld(a.spec + q0 + tid) : -1;
+    const double sr = (in && a.spec) ? gld(a.spec_rad + q0 + tid) : 0.0;
     const double rU = raw_to_unif((uint32_t)r.w);
     F->pi[tid] = in ? r.y : INT_MAX;
     const int K = S.K, E = K + a.m;
@@ -2519,25 +2573,12 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
         }
       }
       __syncthreads();
-      // (3) every wave: the log counts at its first point and their largest drift
-      {
-        const int c = F->wc[wv][lane];
-        double l1 = -INFINITY, l0 = -INFINITY, dr = 0.0;
-        if (lane < nsl) {
-          l1 = fp_logn(a, c);
-          l0 = fp_logn(a, c - 1);
-          const int a0 = st.snap[lane];
-          dr = a0 == c ? 0.0 : ((a0 < 1 || c < 1) ? INFINITY : fabs(l1 - st.sl1[lane]));
-        }
-        F->wl1[wv][lane] = l1;
-        F->wl0[wv][lane] = l0;
-        dr = wave_max(dr);
-        if (lane == 0) F->wdr[wv] = dr;
-        wave_sync();
-      }
       const long long tr1 = prof ? wall_clock64() : 0;
-      // (4) the wave's moves per slot it touches (ballot masks: a point's count change of slot
-      // s from the moves before it in its wave is popc(in & below) - popc(out & below))
+      // (3) the wave's moves per slot it touches (ballot masks, zero for the others): a point's
+      // count change of slot s from the moves before it in its wave is
+      // popc(in & below) - popc(out & below)
+      F->bin[wv][lane] = 0ull;
+      F->bout[wv][lane] = 0ull;
       unsigned long long touch = mover ? ((1ull << own) | (1ull << tgt)) : 0ull;
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) touch |= __shfl_xor(touch, o);
@@ -2548,58 +2589,64 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
       }
       wave_sync();
       auto corr = [&](int sl) -> int {
-        if (!((touch >> sl) & 1ull)) return 0;
         return __popcll(F->bin[wv][sl] & below) - __popcll(F->bout[wv][sl] & below);
       };
       const long long tr2 = prof ? wall_clock64() : 0;
-      // (5) the points after the first changed outcome draw again (all of them in round 0)
+      // (4) the points after the first changed outcome draw again (all of them in round 0).
+      // Branch-free entry loops: every LDS read and table / row load of a pass is issued
+      // before its values are used.
       bool changed = false;
+      long long tdraw = 0;
       const bool evl = in && tid > chg && tid <= fs;
       if (evl) {
-        const int cown = corr(own);
-        const int cnow = F->wc[wv][own] + cown;
+        const int cnow = F->wc[wv][own] + corr(own);
         const bool single = cnow == 1;
-        double drift = F->wdr[wv];
-        const double lo_own = cown == 0 ? F->wl0[wv][own] : fp_logn(a, cnow - 1);
-        {
-          const int sa = st.snap[own];
-          drift = fmax(drift, sa == cnow ? 0.0 : ((sa >= 2 && cnow >= 2) ? fabs(lo_own - st.sl0[own]) : INFINITY));
-        }
+        int sl[EM], cc[EM];
         double v[EM];
 #pragma unroll
         for (int e = 0; e < EM; ++e) {
-          double w = 0.0;
-          if (e < K) {
-            const int s = st.sol[e];
-            const int cr = corr(s);
-            if (s == own) w = lo_own;
-            else if (cr == 0) w = F->wl1[wv][s];
-            else {
-              const int c = F->wc[wv][s] + cr;
-              w = fp_logn(a, c);
-              const int a0 = st.snap[s];
-              drift = fmax(drift, a0 == c ? 0.0 : ((a0 < 1 || c < 1) ? INFINITY : fabs(w - st.sl1[s])));
-            }
+          const int s = st.sol[e < K ? e : 0];
+          sl[e] = s;
+          cc[e] = F->wc[wv][s] + corr(s) - (s == own ? 1 : 0);     // the count in logn[.] (n8:40-92)
+        }
+#pragma unroll
+        for (int e = 0; e < EM; ++e) v[e] = gld(a.logn + ((e < K && cc[e] > 0) ? cc[e] : 0));   // logn[0] = -inf
+        bool take_spec = false;
+        if (struct0 && sp >= 0) {
+          // drift of every log-weight from the snapshot's (the draw holds below its radius)
+          double drift = 0.0;
+#pragma unroll
+          for (int e = 0; e < EM; ++e) {
+            const int s = sl[e];
+            const int a0 = st.snap[s];
+            const double b1 = st.sl1[s], b0 = st.sl0[s];
+            const int c = cc[e];
+            const double d_own = a0 == cnow ? 0.0 : ((a0 >= 2 && cnow >= 2) ? fabs(v[e] - b0) : INFINITY);
+            const double d_oth = a0 == c ? 0.0 : ((a0 < 1 || c < 1) ? INFINITY : fabs(v[e] - b1));
+            drift = fmax(drift, e < K ? (s == own ? d_own : d_oth) : 0.0);
           }
-          v[e] = w;
+          take_spec = drift == 0.0 || drift < sr;
         }
         int np;
-        if (struct0 && sp >= 0 && (drift == 0.0 || drift < sr)) {
+        const long long td0 = prof ? wall_clock64() : 0;
+        if (take_spec) {
           np = sp;
           fresh = false;
         } else {
           const double* Lr = a.L + (int64_t)r.x * ncol;
+          double x[EM];
 #pragma unroll
           for (int e = 0; e < EM; ++e) {
-            if (e < K) v[e] = v[e] + Lr[st.sol[e]];
-            else if (e < E) {
-              const int l = e - K;
-              v[e] = a.logfac + ((l == 0 && single) ? Lr[own] : Lr[a.S + l]);
-            }
+            const int l = e - K;
+            const int col = e < K ? sl[e] : (e < E ? ((l == 0 && single) ? own : a.S + l) : 0);
+            x[e] = gld(Lr + col);
           }
-          np = fp_draw<EM>(v, E, rU);
+#pragma unroll
+          for (int e = 0; e < EM; ++e) v[e] = e < K ? v[e] + x[e] : a.logfac + x[e];
+          np = fp_draw<EM>(v, E, rU, F->etab);
           fresh = true;
         }
+        if (prof) tdraw = wall_clock64() - td0;
         int ncl = 2, nt = own;
         if (np >= 0) {
           if (np < K) {
@@ -2622,8 +2669,10 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
       if (prof) {
         const long long tr3 = wall_clock64();
         const int ne = __popcll(__ballot(evl)), nf = __popcll(__ballot(evl && fresh));
+        const long long tdm = (long long)wave_max((double)tdraw);
         if (lane == 0) {
           F->wev[wv] = tr3 - tr2;
+          atomicAdd((unsigned long long*)&S.tsub[5], (unsigned long long)tdm);
           atomicAdd((unsigned long long*)&S.tsub[6], (unsigned long long)ne);
           atomicAdd((unsigned long long*)&S.tsub[7], (unsigned long long)nf);
         }
@@ -2738,7 +2787,7 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
     if (fs < nc) {
       // ---- the stop: the serial path in the committed state (that of its turn)
       const int4 rs = F->stop_rq;
-      if (wv == 0) fp_stop(a, st, F);
+      if (wv == 0) fp_stop(a);
       __syncthreads();
       go = F->go != 0;
       vfrom = (int64_t)rs.y + 1;
@@ -3098,7 +3147,8 @@ size_t resolve_smem_bytes(int lcap, int m, int blocks) {
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s) {
   if (a.fp) {
     const size_t lds = resolve_fp_lds_bytes(a.lcap, a.m);
-    if (a.K + a.m <= 32) hipLaunchKernelGGL(k_resolve_fp<32>, dim3(1), dim3(kFpThreads), lds, s, a);
+    if (a.K + a.m <= 24) hipLaunchKernelGGL(k_resolve_fp<24>, dim3(1), dim3(kFpThreads), lds, s, a);
+    else if (a.K + a.m <= 32) hipLaunchKernelGGL(k_resolve_fp<32>, dim3(1), dim3(kFpThreads), lds, s, a);
     else hipLaunchKernelGGL(k_resolve_fp<64>, dim3(1), dim3(kFpThreads), lds, s, a);
   } else if (a.blocks)
     hipLaunchKernelGGL(k_resolve_blk, dim3(1), dim3(kWave), resolve_lds_bytes(a.lcap, a.m, 1), s, a);

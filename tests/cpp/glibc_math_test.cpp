@@ -23,6 +23,10 @@ int main(int argc, char** argv) {
     if (!same(e0, e1)) {
       if (bad_exp++ < 5) printf("exp(%a): libm %a replica %a\n", x, e0, e1);
     }
+    const double e2 = hdpm::glibc::exp_bf(x, hdpm::glibc::kGlibcExpTab);   // the branch-free variant
+    if (!same(e0, e2)) {
+      if (bad_exp++ < 5) printf("exp(%a): libm %a branch-free %a\n", x, e0, e2);
+    }
     const double l0 = std::log(x), l1 = hdpm::glibc::log_h(x);
     if (!same(l0, l1)) {
       if (bad_log++ < 5) printf("log(%a): libm %a replica %a\n", x, l0, l1);
@@ -47,6 +51,8 @@ int main(int argc, char** argv) {
     check(asd(b & 0x7fffffffffffffffull) < INFINITY ? asd(b & 0x7fffffffffffffffull) : 1.5);
     check(asd((b & 0x800fffffffffffffull) | ((uint64_t)(0x3c0 + (b >> 60) * 6) << 52)));   // |x| in 2^-63..2^26
     check(-700.0 + 1400.0 * U(g));     // exp's special-case band
+    check(-1100.0 + 1100.0 * U(g));    // fp_draw's arguments v - max <= 0, subnormal results
+    check(-(512.0 + 512.0 * U(g)));
   }
   printf("checked %ld inputs: %ld exp mismatches, %ld log mismatches\n", cnt, bad_exp, bad_log);
   return (bad_exp || bad_log) ? 1 : 0;
