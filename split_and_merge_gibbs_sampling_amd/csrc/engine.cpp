@@ -1871,6 +1871,7 @@ struct Ctx {
   // a prepared sweep can start on the device and still be dropped), kRoundResolve (the rest,
   // after a prefix launched with the same arguments and no state change in between).
   enum { kRoundAll = 0, kRoundPrefix = 1, kRoundResolve = 2 };
+  static constexpr int kFpMinListed = 64;
   bool fp_eligible(int E, int lcap) const {
     return E <= 64 && lcap <= 64 && !(debug & (1 | 4096 | 8192 | 8388608));
   }
@@ -1919,7 +1920,8 @@ struct Ctx {
     // certified points (no exact rows) would fail re-verification and restart the launch
     // (the fixed-point resolver re-tests and restarts cheaply enough to keep the uniform
     // certification after many exact decisions; debug bit 24 lists every point there too)
-    const bool fp_next = fp_eligible(K + m, std::min(scap, nslots + 2));
+    const bool fp_next = fp_eligible(K + m, std::min(scap, nslots + 2)) &&
+                         (last_listed < 0 || last_listed >= kFpMinListed || (debug & 33554432));
     const bool many_exact = last_exact >= kResolveBlkMin && (!fp_next || (debug & 16777216));
     pa.dmax2 = ((debug & (1 | 262144)) || last_unsettled || many_exact) ? INFINITY : 2.0 * dmax;
     pa.L = d_L.p; pa.rowpos = d_rowpos.p; pa.margin = d_margin.p; pa.list = d_list.p; pa.cnt = d_cnt.p;
@@ -1991,7 +1993,10 @@ struct Ctx {
                  ((debug & 8192) || last_exact >= kResolveBlkMin)) ? 1 : 0;
     // the fixed-point resolver whenever the state fits it (debug bit 23: the one-wave LIST /
     // block modes; bits 12 / 13 select those modes and keep them)
-    ra.fp = fp_eligible(K + m, ra.lcap) ? 1 : 0;
+    // (a launch whose predecessor listed only a few points -- a converged chain -- keeps the
+    // one-wave LIST resolver: its fixed cost is half the fixed-point kernel's, ~7 vs ~13 us at C5)
+    ra.fp = (fp_eligible(K + m, ra.lcap) && (last_listed < 0 || last_listed >= kFpMinListed || (debug & 33554432)))
+                ? 1 : 0;
     if (ra.fp) ra.blocks = 0;
     if (part != kRoundPrefix && !pg) last_fp = ra.fp != 0;
     if (resolve_smem_bytes(ra.lcap, m, ra.blocks) > 160 * 1024) {

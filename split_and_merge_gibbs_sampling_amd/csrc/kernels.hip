@@ -2321,7 +2321,10 @@ __global__ __launch_bounds__(kWave) void k_resolve_blk(ResolveArgs a) {
 // the stop goes through the serial path (RCtx::process on wave 0), then the next chunk
 // starts behind it.  Unlisted points between listed ones are re-tested against the drift
 // after the moves before them, as in k_resolve.  Needs K + m <= 64 and lcap <= 64.
-constexpr int kFpThreads = 256;
+#ifndef HDPM_FP_THREADS
+#define HDPM_FP_THREADS 256     // build parameter for A/B (4 waves: one per SIMD)
+#endif
+constexpr int kFpThreads = HDPM_FP_THREADS;
 constexpr int kFpWaves = kFpThreads / kWave;
 constexpr int kFpFallback = -1000;
 

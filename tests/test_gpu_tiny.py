@@ -77,10 +77,13 @@ def test_tiny_shapes_chain_matches_oracle(hd, oracle, shape, m, mode):
     assert np.array_equal(res["rng_state"], rng)
 
 
+# debug 33554432 (bit 25): the fixed-point resolver (k_resolve_fp) for every launch, not only
+# after a launch that listed >= 64 points
+@pytest.mark.parametrize("debug", [0, 33554432])
 @pytest.mark.parametrize("mode", ["n8", "both"])
 @pytest.mark.parametrize("shape", [(2, 1, 1, 2), (4, 3, 2, 3), (7, 5, 3, 4), (65, 1, 2, 3), (130, 3, 4, (2, 5))],
                          ids=_shape_id)
-def test_tiny_shapes_iteration_api(hd, oracle, shape, mode):
+def test_tiny_shapes_iteration_api(hd, oracle, shape, mode, debug):
     # hdpm_iterations (prepared next sweep launched ahead, speculative update_phi, carried
     # tables) in batches of uneven length; state and stream compared after every batch
     n8, sm = MODES[mode]
@@ -93,6 +96,7 @@ def test_tiny_shapes_iteration_api(hd, oracle, shape, mode):
     try:
         e.set_data(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w)
         e.set_seed(9)
+        e.set_debug(debug)
         e.init_chain(e.chain_params(m=m, iterations=iters, L=1, burnin=0, neal8=n8, split_merge=sm), c_i=ds.truth)
         it = 0
         for b in batches:
@@ -112,10 +116,11 @@ def test_tiny_shapes_iteration_api(hd, oracle, shape, mode):
         e.close()
 
 
-@pytest.mark.parametrize("debug", [0, 16])
+@pytest.mark.parametrize("debug", [0, 16, 33554432])
 def test_tiny_shape_random_init_chain(hd, oracle, debug):
     # random L = 5 initial labels on 40 points: clusters vanish (case 2) and appear (cases 3 /
-    # 4) within the same sweeps, at the last point too; carried tables (0) and recounts (16)
+    # 4) within the same sweeps, at the last point too; carried tables (0), recounts (16), the
+    # fixed-point resolver for every launch (33554432)
     ds = _data((40, 4, 3, 3))
     iters = 12
     for seed in range(1, 40):
