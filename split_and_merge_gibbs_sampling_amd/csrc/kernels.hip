@@ -2322,7 +2322,7 @@ __global__ __launch_bounds__(kWave) void k_resolve_blk(ResolveArgs a) {
 // starts behind it.  Unlisted points between listed ones are re-tested against the drift
 // after the moves before them, as in k_resolve.  Needs K + m <= 64 and lcap <= 64.
 #ifndef HDPM_FP_THREADS
-#define HDPM_FP_THREADS 256     // build parameter for A/B (4 waves: one per SIMD)
+#define HDPM_FP_THREADS 512     // build parameter for A/B (8 waves: two per SIMD; 256: C2 -10%, C5 random-20 -26%)
 #endif
 constexpr int kFpThreads = HDPM_FP_THREADS;
 constexpr int kFpWaves = kFpThreads / kWave;
