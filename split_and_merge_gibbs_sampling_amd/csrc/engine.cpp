@@ -1998,6 +1998,7 @@ struct Ctx {
     ra.fp = (fp_eligible(K + m, ra.lcap) && (last_listed < 0 || last_listed >= kFpMinListed || (debug & 33554432)))
                 ? 1 : 0;
     if (ra.fp) ra.blocks = 0;
+    ra.debug_fp = (debug & 67108864) ? 1 : 0;
     if (part != kRoundPrefix && !pg) last_fp = ra.fp != 0;
     if (resolve_smem_bytes(ra.lcap, m, ra.blocks) > 160 * 1024) {
       err = "too many clusters for the resolver (K > ~2300)";
