@@ -186,8 +186,8 @@ int hdpm_reset_stats(hdpm_ctx* ctx);
  * point (no certification by the draw's uniform), as the one-wave resolvers always do; bit 25:
  * the fixed-point resolver for every launch it fits (by default a launch after one that listed
  * fewer than 64 points -- a converged chain -- takes the one-wave LIST resolver); bit 26: the
- * fixed-point resolver's first round starts every point from its snapshot draw's outcome
- * instead of "stay" (experimental). */
+ * fixed-point resolver's first round starts every point from "stay" instead of its snapshot
+ * draw's outcome. */
 int hdpm_set_debug(hdpm_ctx* ctx, int32_t mode);
 /* The prepass's pool-entry heads, P entries of wb*Ws + 2 words padded to a power of two
  * (Ws <= 4) or to a multiple of 8 words (wide layouts) (csrc/kernels.hpp "Pool-entry heads",

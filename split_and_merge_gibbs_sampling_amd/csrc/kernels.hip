@@ -2549,10 +2549,10 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
     const int K = S.K, E = K + a.m;
     const bool struct0 = S.nstruct == 0;
     int cls = 0, tgt = own, pick = -1, co = 0, ct = 0;   // cls: 0 stay, 1 case-1 move to tgt, 2 stop
-    // Optionally (debug bit 26, not yet measured) the first round's guess: the snapshot draws'
-    // outcomes in the chunk-start state (any guess converges to the same fixed point; a right
-    // one does so in one round instead of two).  By default the first round starts from "stay".
-    if (in && struct0 && sp >= 0 && (a.debug_fp & 1)) {
+    // The first round's guess: the snapshot draws' outcomes in the chunk-start state (any guess
+    // converges to the same fixed point; a right one does so in one round instead of two;
+    // debug bit 26 starts from "stay")
+    if (in && struct0 && sp >= 0 && !(a.debug_fp & 1)) {
       const bool single0 = st.cnt[own] == 1;
       if (sp < K) {
         const int s2 = st.sol[sp];

@@ -233,7 +233,7 @@ struct ResolveArgs {
   const uint32_t* const* raw_ptr;
   int dry;                   // 1: stop (kDryStop) at the first decision that is not "stay"
   int fp;                    // 1: fixed-point resolver (k_resolve_fp; needs K + m <= 64, lcap <= 64)
-  int debug_fp;              // bit 0: its first round starts from the snapshot draws' outcomes (not "stay")
+  int debug_fp;              // bit 0: its first round starts from "stay" (not the snapshot draws' outcomes)
 };
 
 // Cluster parameter upload: one staging buffer, scattered on the device.
