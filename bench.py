@@ -28,6 +28,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PMC_ROUND = "r04"        # profiles/<round>/pmc_{fetch,write}_<config>.csv: this round's counter passes
 
 
 def packed_layout(d: int, mmax: int):
@@ -299,7 +300,8 @@ def main():
                     help="first iteration index (0: the warmup includes iteration 0's pool regeneration)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="threads of the optimised CPU baseline (0: the usable CPUs, at most 16)")
+                    help="threads of the optimised CPU baseline (0: every CPU this process may use, within the "
+                         "share OMP_NUM_THREADS allots it -- 16 per GPU on the GPU box)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-csv", action="append", default=None,
                     help="rocprofv3 --pmc counter_collection CSV(s) with FETCH_SIZE / WRITE_SIZE of this workload "
@@ -342,6 +344,10 @@ def main():
     it = args.start_iter                         # iteration 0 regenerates the pool (la:123-129)
     eng.iterations(it, args.warmup)             # hdpm_iterations: the la:85-154 loop in one call
     it += args.warmup
+    # the warmup's last iteration prepared the next sweep (its prepass on the device, its
+    # speculative update_phi on the host pool): dropped here, so the timed window holds exactly
+    # `steps` iterations of work, each started inside it (hdpm_drop_prepared)
+    eng.drop_prepared()
     eng.synchronize()
     st0 = eng.stats()                            # + iteration 0's regeneration
     eng.reset_stats()
@@ -372,7 +378,7 @@ def main():
     traffic, traffic_src = None, None
     csvs = args.traffic_csv
     if csvs is None:
-        csvs = [os.path.join(ROOT, "profiles", "r02", f"pmc_{c}_{args.config}.csv") for c in ("fetch", "write")]
+        csvs = [os.path.join(ROOT, "profiles", PMC_ROUND, f"pmc_{c}_{args.config}.csv") for c in ("fetch", "write")]
     csvs = [c for c in csvs if os.path.exists(c)]
     s_b, g_b, gshape = prepass_shape(ds.d, int(ds.attrisize.max()), args.m)
     if csvs and args.n is None:
@@ -466,7 +472,9 @@ def main():
         "note": "the sweep proves 'stay' from bounds for most points (DESIGN.md 4.3-4.4) and moves the prepass bytes; "
                 "SURVEY 8(d)'s N(D(2+9m)+8) is the direct design's traffic and is not the roofline of this path"}
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
-        thr = args.cpu_threads or min(16, host_cpu()[1])
+        usable = host_cpu()[1]
+        share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+        thr = args.cpu_threads or (min(usable, share) if share > 0 else usable)
         out["cpu_baseline"] = cpu_baseline(ds, eng, args.m, args.cpu_baseline_seconds, thr)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -73,8 +73,10 @@ typedef struct {
     int64_t phi_device_calls, phi_device_fallbacks, phi_device_last_status;
     /* update stream slices found in a copy made an iteration ahead, and such copies made */
     int64_t phi_lookahead_hits, phi_lookahead_copies;
-    /* next sweeps enqueued before the iteration's update was joined, and those that ran */
-    int64_t pipe_enqueued, pipe_runs;
+    /* next sweeps enqueued before the iteration's update was joined, and those that ran;
+     * go decisions refused because the wait kernel's limit was near (the sweep ran
+     * unpipelined), and enqueued sweeps gated off on the device and re-run from point 0 */
+    int64_t pipe_enqueued, pipe_runs, pipe_refused, pipe_recovered;
 } hdpm_stats;
 
 int         hdpm_device_count(void);
@@ -208,6 +210,12 @@ int hdpm_get_pool_heads(hdpm_ctx* ctx, uint64_t* out, int64_t P);
  * sweep; cases the device does not restate fall back to the host.  Same chain either way.
  * Default 0 (or HDPM_PHI=device in the environment). */
 #define HDPM_OPT_PHI_DEVICE 2
+/* HDPM_OPT_PIPE_WAIT_US (testing): the limit, in microseconds, after which the wait kernel of
+ * a sweep enqueued ahead gives up and gates the sweep off (default 2 s).  A positive value
+ * also makes the host refuse a go given after a quarter of the limit; a negative value sets
+ * the limit to -value without that check, so the device-side gate-off (and the engine's
+ * recovery from it: the sweep re-run ungated, same chain) can be exercised. */
+#define HDPM_OPT_PIPE_WAIT_US 3
 int hdpm_set_option(hdpm_ctx* ctx, int32_t option, double value);
 /* Posterior analysis (realdata_analysis/zoo_simulator.R:193-236, 339-344; mcclust /
  * mcclust.ext).  hdpm_psm_build: the posterior similarity matrix of M saved label vectors
@@ -232,6 +240,12 @@ int hdpm_debug_math(hdpm_ctx* ctx, const double* x, int64_t n, int32_t fn, int32
 /* Block until every kernel and copy the context has queued is done, a prepared next
  * sweep's prefix (scratch outputs only) included; the prepared sweep stays prepared. */
 int hdpm_synchronize(hdpm_ctx* ctx);
+/* Drop a prepared next sweep (the one the last hdpm_iterations / hdpm_iteration call set up:
+ * its prepass possibly queued on the device, its speculative update_phi on the host pool):
+ * the job is joined and the stream rewound, so the next iteration does all of its own work
+ * (bench.py calls it between the warmup and the timed window).  Any other state-changing
+ * call does the same implicitly. */
+int hdpm_drop_prepared(hdpm_ctx* ctx);
 
 #ifdef __cplusplus
 }

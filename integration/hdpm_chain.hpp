@@ -12,6 +12,7 @@
 #pragma once
 
 #include <chrono>
+#include <cmath>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -56,21 +57,41 @@ class Ctx {
 inline int run_markov_chain(const double* data, int n, int d, const int32_t* attrisize, double gamma, const double* v,
                             const double* w, const hdpm_chain_params& p, const int32_t* c_i_init,
                             int32_t* rng_state, ChainResult* out, std::string* err, int device = 0) {
+  // NumericMatrix -> row-major codes.  The reference compares the doubles themselves
+  // (n8:48 -> cf:355), so a value that is not one of the levels 1..m_j cannot be narrowed to
+  // a byte: it is rejected here, before any cast (1.5 or 257.0 would otherwise become a valid
+  // code silently).
+  if (n <= 0 || d <= 0 || !data || !attrisize) {
+    if (err) *err = "empty data matrix";
+    return HDPM_E_ARG;
+  }
+  std::vector<uint8_t> codes((size_t)n * d);
+  for (int j = 0; j < d; j++) {
+    const double hi = (double)attrisize[j];
+    for (int i = 0; i < n; i++) {
+      const double x = data[(size_t)j * n + i];
+      if (!(x >= 1.0 && x <= hi && x <= 255.0) || x != std::floor(x)) {
+        if (err)
+          *err = "data[" + std::to_string(i) + ", " + std::to_string(j) + "] = " + std::to_string(x) +
+                 " is not an integer level in 1..attrisize[j]";
+        return HDPM_E_ARG;
+      }
+      codes[(size_t)i * d + j] = (uint8_t)x;
+    }
+  }
   Ctx ctx(device);
   auto fail = [&](int st) {
     if (err) *err = ctx.get() ? hdpm_last_error(ctx.get()) : "no gfx950 device";
     return st;
   };
   if (ctx.status() != HDPM_OK) return fail(ctx.status());
-  std::vector<uint8_t> codes((size_t)n * d);            // NumericMatrix -> row-major codes
-  for (int i = 0; i < n; i++)
-    for (int j = 0; j < d; j++) codes[(size_t)i * d + j] = (uint8_t)data[(size_t)j * n + i];
   int st = hdpm_set_data(ctx.get(), codes.data(), n, d, attrisize, gamma, v, w);
   if (st) return fail(st);
   if ((st = hdpm_rng_set_state(ctx.get(), rng_state))) return fail(st);
 
-  const auto t0 = std::chrono::steady_clock::now();
   if ((st = hdpm_init_chain(ctx.get(), &p, c_i_init))) return fail(st);   // la:27-77
+  // la:79: the clock starts after the initial state and the latent pool are built
+  const auto t0 = std::chrono::steady_clock::now();
   const int saved = p.iterations;
   out->total_cls.assign(saved, 0);
   out->c_i.assign(saved, {});

@@ -25,13 +25,14 @@ EXPORTS = (
     "hdpm_set_pool", "hdpm_get_pool", "hdpm_generate_pool", "hdpm_neal8_sweep", "hdpm_update_phi",
     "hdpm_compute_loglikelihood", "hdpm_loglik_matrix", "hdpm_restricted_gibbs", "hdpm_logprobgs_c_i",
     "hdpm_split_and_merge", "hdpm_run_markov_chain", "hdpm_get_stats", "hdpm_reset_stats",
-    "hdpm_set_debug", "hdpm_synchronize", "hdpm_init_chain", "hdpm_iteration", "hdpm_iterations", "hdpm_rng_fill_device",
+    "hdpm_set_debug", "hdpm_synchronize", "hdpm_drop_prepared", "hdpm_init_chain", "hdpm_iteration", "hdpm_iterations", "hdpm_rng_fill_device",
     "hdpm_get_pool_heads", "hdpm_set_option", "hdpm_debug_draw", "hdpm_debug_math",
     "hdpm_psm_build", "hdpm_psm_rows", "hdpm_psm_vi_lb",
 )
 
 OPT_HIG_LOGSPACE = 1
 OPT_PHI_DEVICE = 2
+OPT_PIPE_WAIT_US = 3
 
 STATUS = {0: "OK", 1: "E_VALIDATE", 2: "E_GSL", 3: "E_PROB", 4: "E_WALKER", 5: "E_ARG",
           6: "E_DEVICE", 7: "E_NODEVICE"}
@@ -62,7 +63,8 @@ class Stats(C.Structure):
                                   "rng_windows", "rng_windows_fresh", "listed_points", "sm_moves")] + \
         [(n, C.c_double) for n in ("t_sm_ms", "t_sm_scan_ms", "t_sm_phi_ms", "t_sm_terms_ms")] + \
         [(n, C.c_int64) for n in ("phi_device_calls", "phi_device_fallbacks", "phi_device_last_status",
-                                  "phi_lookahead_hits", "phi_lookahead_copies", "pipe_enqueued", "pipe_runs")]
+                                  "phi_lookahead_hits", "phi_lookahead_copies", "pipe_enqueued", "pipe_runs",
+                                  "pipe_refused", "pipe_recovered")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -120,6 +122,7 @@ def lib():
         "hdpm_rng_fill_device": ([vp, i64, vp], C.c_int),
         "hdpm_set_debug": ([vp, i32], C.c_int),
         "hdpm_synchronize": ([vp], C.c_int),
+        "hdpm_drop_prepared": ([vp], C.c_int),
         "hdpm_get_pool_heads": ([vp, vp, i64], C.c_int),
         "hdpm_set_option": ([vp, i32, f64], C.c_int),
         "hdpm_debug_draw": ([vp, vp, i32, f64, i32, i32, P(i32)], C.c_int),

@@ -90,26 +90,62 @@ struct HipError {
 #ifndef HDPM_PHI_SPEC
 #define HDPM_PHI_SPEC 4   // update_phi phase B: first rbeta attempts speculated per batch
 #endif
-static std::atomic<int64_t> g_dev_allocs{0};
+static std::atomic<int64_t> g_dev_allocs{0};   // device allocations made (diagnostics)
 
-// HDPM_SEGV_TRACE=1: a host fault prints the library's call stack (addresses for addr2line)
-static void segv_trace(int sig) {
+// HDPM_SEGV_TRACE=1: a host fault prints the raw return addresses of the faulting stack and
+// the library's load address (for addr2line), then hands the signal to the handler that was
+// installed before (Python's faulthandler, a runtime's), or to the default action.  Only
+// async-signal-safe calls in the handler: the frames are walked by backtrace() and written
+// by backtrace_symbols_fd() (both preloaded at install time, so no allocation or dynamic
+// loading happens in the handler), the text by write().
+static struct sigaction g_segv_prev;
+static uintptr_t g_lib_base = 0;
+static void segv_put_hex(uintptr_t x) {
+  char buf[32];
+  int k = 0;
+  buf[k++] = '0';
+  buf[k++] = 'x';
+  char tmp[16];
+  int t = 0;
+  do { tmp[t++] = "0123456789abcdef"[x & 15]; x >>= 4; } while (x && t < 16);
+  while (t) buf[k++] = tmp[--t];
+  buf[k++] = '\n';
+  (void)!write(2, buf, (size_t)k);
+}
+static void segv_trace(int sig, siginfo_t* info, void* uctx) {
+  static const char hdr[] = "libhdpm: fault; library base ";
+  (void)!write(2, hdr, sizeof(hdr) - 1);
+  segv_put_hex(g_lib_base);
   void* fr[64];
   const int nf = backtrace(fr, 64);
   backtrace_symbols_fd(fr, nf, 2);
-  Dl_info di;
-  if (dladdr((void*)&segv_trace, &di)) {
-    char buf[128];
-    const int len = std::snprintf(buf, sizeof(buf), "libhdpm base %p\n", di.dli_fbase);
-    if (len > 0) (void)!write(2, buf, (size_t)len);
+  if (g_segv_prev.sa_flags & SA_SIGINFO) {
+    if (g_segv_prev.sa_sigaction) { g_segv_prev.sa_sigaction(sig, info, uctx); return; }
+  } else if (g_segv_prev.sa_handler != SIG_DFL && g_segv_prev.sa_handler != SIG_IGN && g_segv_prev.sa_handler) {
+    g_segv_prev.sa_handler(sig);
+    return;
   }
-  std::signal(sig, SIG_DFL);
-  std::raise(sig);
+  // default action: re-raised with the default disposition on return from the handler
+  struct sigaction dfl;
+  std::memset(&dfl, 0, sizeof(dfl));
+  dfl.sa_handler = SIG_DFL;
+  sigemptyset(&dfl.sa_mask);
+  sigaction(sig, &dfl, nullptr);
+  raise(sig);
 }
 static const bool g_segv_trace = [] {
-  if (std::getenv("HDPM_SEGV_TRACE")) std::signal(SIGSEGV, segv_trace);
-  return true;
-}();   // device allocations made (diagnostics)
+  if (!std::getenv("HDPM_SEGV_TRACE")) return false;
+  Dl_info di;
+  if (dladdr((void*)&segv_put_hex, &di)) g_lib_base = (uintptr_t)di.dli_fbase;
+  void* warm[2];
+  (void)backtrace(warm, 2);          // loads libgcc's unwinder now, not inside the handler
+  struct sigaction sa;
+  std::memset(&sa, 0, sizeof(sa));
+  sa.sa_sigaction = segv_trace;
+  sa.sa_flags = SA_SIGINFO;
+  sigemptyset(&sa.sa_mask);
+  return sigaction(SIGSEGV, &sa, &g_segv_prev) == 0;
+}();
 
 template <class T>
 struct DevBuf {
@@ -761,7 +797,13 @@ struct Ctx {
     int par = 0, buf = -1, m = 0;
     bool track = false;
     uint64_t gen[2] = {0, 0};          // window launches the kernels waited for
+    std::chrono::steady_clock::time_point t_enq;   // the wait kernel was queued (pipe_go's deadline)
   } pre;
+  // k_pipe_wait's limit in ticks of the 100 MHz clock (2 s), and whether pipe_go refuses a go
+  // given after a quarter of it (HDPM_OPT_PIPE_WAIT_US; a negative value turns the check off, to
+  // exercise the device-side gate-off and its recovery in neal8_sweep)
+  long long pipe_limit_ticks = 200000000LL;
+  bool pipe_host_check = true;
   bool deep_ok = false;                // set by iteration(): the next sweep may be enqueued ahead
   static constexpr size_t kCtlInts = 16;
   static_assert(sizeof(ResolveCtl) <= kCtlInts * sizeof(int), "control block");
@@ -2147,7 +2189,8 @@ struct Ctx {
         pre.gen[k] = w.gen;
       }
     }
-    HIPCHK(launch_pipe_wait(&h_pipe.p[q], ctl_at(par), ctl_at(q), n, &d_pipe.p[q], 200000000LL, stream));
+    HIPCHK(launch_pipe_wait(&h_pipe.p[q], ctl_at(par), ctl_at(q), n, &d_pipe.p[q], pipe_limit_ticks, stream));
+    pre.t_enq = std::chrono::steady_clock::now();   // the kernel's clock starts no earlier
     pre.active = true;
     pre.par = q;
     pre.buf = spec.stage_buf;
@@ -2175,6 +2218,15 @@ struct Ctx {
         last_sweep_rounds != 1 || last_sweep_moves != 0 || !host_spec() || tables_dirty)
       return false;
     if (!(freq_dev_valid && freq_version == labels_version)) return false;
+    // the wait kernel gives up after pipe_limit_ticks: a go late enough to race its limit
+    // is refused (the sweep is then released and prepared again); a go the kernel still
+    // misses is recovered in neal8_sweep (kPipeOff)
+    if (pipe_host_check &&
+        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - pre.t_enq).count() >
+            (double)pipe_limit_ticks * 0.01 * 0.25) {
+      stats.pipe_refused++;
+      return false;
+    }
     rng_sync();
     const Rng saved = rng;
     const uint32_t* raw = device_draws((int64_t)n * (m + 1));
@@ -2320,6 +2372,18 @@ struct Ctx {
       }
       stats.rounds++;
       const ResolveCtl c = *ctl_at(par);
+      if (c.status == kPipeOff && piped_round) {
+        // the sweep enqueued ahead was gated off on the device (its wait kernel's limit
+        // passed before the host's go reached it): none of its kernels ran, the tables of
+        // this iteration (the held staging buffer) were not scattered and round 0's
+        // k_cluster_summary did not clear the move count.  Commit the tables and run the
+        // sweep ungated from point 0 with the same draws.
+        stage_fill = stage_last;
+        stage_commit(upload_layout(K, dp, d, bw), K, true);
+        if (track) mcount_clear = true;
+        stats.pipe_recovered++;
+        continue;
+      }
       // the sweep enqueued ahead runs only after a complete sweep without moves
       if (pre.active && (c.status || c.next < n || c.moves)) pre_release();
       last_sweep_rounds = (int)(stats.rounds - rounds0);
@@ -3315,6 +3379,9 @@ struct Ctx {
 
   int update_phi(const int32_t* idx, int nidx) {
     if (!have_state) { err = "no state"; return kArg; }
+    // the log-likelihood a full device update summed belongs to the parameters before this
+    // update: only a full device commit below sets it again
+    dev_ll_version = 0;
     HostPool& pool = HostPool::get();
     pool.prewake();                                   // workers spin while the device counts
     auto t0c = std::chrono::steady_clock::now();
@@ -3991,6 +4058,12 @@ int hdpm_set_option(hdpm_ctx* h, int32_t option, double value) {
       GUARD(ctx->cancel_ahead();)
       ctx->phi_mode = value != 0.0 ? 1 : 0;
       return HDPM_OK;
+    case HDPM_OPT_PIPE_WAIT_US:
+      if (value == 0.0 || !std::isfinite(value)) { ctx->err = "pipe wait limit must be non-zero"; return HDPM_E_ARG; }
+      GUARD(ctx->cancel_ahead();)
+      ctx->pipe_limit_ticks = std::max(1LL, (long long)(std::fabs(value) * 100.0));
+      ctx->pipe_host_check = value > 0;
+      return HDPM_OK;
     default:
       ctx->err = "unknown option";
       return HDPM_E_ARG;
@@ -4093,6 +4166,10 @@ int hdpm_debug_math(hdpm_ctx* h, const double* x, int64_t n, int32_t fn, int32_t
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return HDPM_OK;
   })
+}
+int hdpm_drop_prepared(hdpm_ctx* h) {
+  CTX();
+  return HDPM_OK;
 }
 int hdpm_synchronize(hdpm_ctx* h) {
   CTX_KEEP();

@@ -182,6 +182,11 @@ class Engine:
     def synchronize(self):
         self._check(self._L.hdpm_synchronize(self._h))
 
+    def drop_prepared(self):
+        """Drop a prepared next sweep (include/hdpm.h hdpm_drop_prepared): the next iteration
+        does all of its own work."""
+        self._check(self._L.hdpm_drop_prepared(self._h))
+
     def debug_draw(self, logw, rU: float, two_way: bool = False, ocml: bool = False) -> int:
         """Testing: one device draw from log-weights (n8:95-102, or the sm:204-215 two-way
         draw) with the engine's glibc exp, or the device libm's (ocml)."""
@@ -202,6 +207,11 @@ class Engine:
     def set_phi_device(self, on: bool = True):
         """update_phi on the device (include/hdpm.h HDPM_OPT_PHI_DEVICE); same chain."""
         self._check(self._L.hdpm_set_option(self._h, _lib.OPT_PHI_DEVICE, 1.0 if on else 0.0))
+
+    def set_pipe_wait_us(self, us: float):
+        """Testing (include/hdpm.h HDPM_OPT_PIPE_WAIT_US): the wait limit of a sweep enqueued
+        ahead; negative: no host-side check (exercises the device gate-off recovery)."""
+        self._check(self._L.hdpm_set_option(self._h, _lib.OPT_PIPE_WAIT_US, float(us)))
 
     def set_hig_logspace(self, on: bool = True):
         """Extension beyond the reference (include/hdpm.h HDPM_OPT_HIG_LOGSPACE): finite HIG

@@ -9,10 +9,11 @@
 //   int32 n, d; f64 gamma; int32 attrisize[d]; f64 v[d], w[d]; f64 data[n * d] (column-major,
 //   the NumericMatrix); uint32 seed (set.seed); int32 ncalls; per call: int32 params[12]
 //   (hdpm_chain_params order), int32 has_init, int32 init[n] when has_init.
-// Output: one line per call; exit status 0 when every call matches.
+// Output: one line per poisoned input and per call; exit status 0 when every check passes.
 // Compared per call: the status, and on success total_cls, c_i, accepted and final_ass
 // bit for bit, log-likelihoods within 1e-10 relative (north_star), the 625-word stream
 // after the call.  On an error status both sides must stop with the same status.
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -56,10 +57,31 @@ int main(int argc, char** argv) {
   if (!rd(f, att.data(), d) || !rd(f, v.data(), d) || !rd(f, w.data(), d) || !rd(f, data.data(), data.size()) ||
       !rd(f, &seed, 1) || !rd(f, &ncalls, 1))
     return 2;
+  int bad = 0;
+  // the adapter rejects a data matrix whose doubles are not integer levels 1..m_j before any
+  // narrowing cast (hdpm_chain.hpp), with HDPM_E_ARG and the stream untouched
+  {
+    const double poison[] = {1.5, 257.0, 0.0, -1.0, NAN, (double)att[0] + 1.0};
+    for (double x : poison) {
+      std::vector<double> bad_data = data;
+      bad_data[(size_t)(n / 2)] = x;   // column 0, row n / 2
+      std::vector<int32_t> st(625);
+      orc_ffi_set_seed(seed, st.data());
+      const std::vector<int32_t> st0 = st;
+      hdpm_chain_params p0{};
+      p0.m = 3; p0.iterations = 1; p0.L = 2; p0.neal8 = 1; p0.n8_step_size = 1; p0.sam_step_size = 1; p0.thinning = 1;
+      hdpm_adapter::ChainResult res;
+      std::string err;
+      const int se = hdpm_adapter::run_markov_chain(bad_data.data(), n, d, att.data(), gamma, v.data(), w.data(), p0,
+                                                    nullptr, st.data(), &res, &err);
+      const bool ok = se == HDPM_E_ARG && st == st0 && !err.empty();
+      std::printf("poisoned data %g: status %d (%s), %s\n", x, se, err.c_str(), ok ? "rejected" : "MISMATCH");
+      bad += !ok;
+    }
+  }
   std::vector<int32_t> st_eng(625), st_orc(625);
   orc_ffi_set_seed(seed, st_eng.data());
   st_orc = st_eng;
-  int bad = 0;
   for (int call = 0; call < ncalls; ++call) {
     int32_t pr[12], has_init = 0;
     if (!rd(f, pr, 12) || !rd(f, &has_init, 1)) return 2;
@@ -79,8 +101,10 @@ int main(int argc, char** argv) {
                                         ll.data(), acc.data(), fin.data());
     hdpm_adapter::ChainResult res;
     std::string err;
+    const auto wall0 = std::chrono::steady_clock::now();
     const int se = hdpm_adapter::run_markov_chain(data.data(), n, d, att.data(), gamma, v.data(), w.data(), p,
                                                   has_init ? init.data() : nullptr, st_eng.data(), &res, &err);
+    const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - wall0).count();
     std::string why;
     if (so != se) {
       why = "status oracle " + std::to_string(so) + " engine " + std::to_string(se) + " (" + err + ")";
@@ -96,6 +120,8 @@ int main(int argc, char** argv) {
       }
       if (why.empty() && std::memcmp(res.final_ass.data(), fin.data(), (size_t)n * 4) != 0) why = "final_ass";
       if (why.empty() && st_eng != st_orc) why = "random stream after the call";
+      // la:79: `time` covers the iterations only (the clock starts after init_chain)
+      if (why.empty() && !(res.time_s >= 0.0 && res.time_s <= wall)) why = "time outside the call";
     }
     std::printf("call %d: status %d, %s\n", call, so, why.empty() ? "match" : ("MISMATCH " + why).c_str());
     bad += !why.empty();

@@ -7,7 +7,9 @@ integration/adapter_replay) runs it against the oracle's run_markov_chain (la:6-
 consecutive calls sharing one random stream: .Random.seed in (hdpm_rng_set_state) ->
 hdpm_init_chain -> hdpm_iteration loop with hdpm_get_state at every saved iteration ->
 hdpm_rng_get_state -> the next call.  Labels, K, acceptances, final_ass and the stream
-after each call bit for bit, log-likelihoods within 1e-10 relative.
+after each call bit for bit, log-likelihoods within 1e-10 relative; `time` inside the call's
+wall time (the clock starts after init_chain, la:79); non-integer or out-of-range doubles in
+the data matrix rejected with HDPM_E_ARG before any narrowing cast.
 """
 import os
 import struct
@@ -49,6 +51,8 @@ def run(tmp_path, ds, seed, calls):
     print(r.stdout, r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.count("match") == len(calls)
+    # poisoned NumericMatrix values (1.5, 257, 0, -1, NaN, m_j + 1) are rejected before the cast
+    assert r.stdout.count("rejected") == 6
 
 
 def test_adapter_zoo_consecutive_calls(tmp_path, zoo):

@@ -169,8 +169,14 @@ def test_c5_full_size_random20_start(hd, oracle):
 
 
 @pytest.mark.timeout(1200)
-@pytest.mark.parametrize("name,warm,timed", [("c5", 5, 25), ("c3", 5, 25), ("c4", 3, 25)])
-def test_bench_path_iterations_api(hd, oracle, name, warm, timed):
+# mode "": the default path; "nopipe": debug bit 22 (no sweep enqueued ahead of the update's
+# go -- the same chain without the device-gated pipeline); "gateoff": the enqueued sweep's wait
+# kernel gives up after 1 us with no host-side check, so nearly every enqueued sweep is gated
+# off on the device and re-run ungated by the engine (its recovery path)
+@pytest.mark.parametrize("name,warm,timed,mode", [("c5", 5, 25, ""), ("c5", 3, 12, "nopipe"),
+                                                  ("c5", 3, 12, "gateoff"), ("c3", 5, 25, ""),
+                                                  ("c4", 3, 25, "")])
+def test_bench_path_iterations_api(hd, oracle, name, warm, timed, mode):
     """The path bench.py times (bench.py main: hdpm_iterations for the warmup, synchronize,
     reset_stats, hdpm_iterations for the timed window) at the full BASELINE size, against
     the oracle's chain (la:94-132: sweep, update_phi, compute_loglikelihood per iteration,
@@ -184,6 +190,10 @@ def test_bench_path_iterations_api(hd, oracle, name, warm, timed):
     batch, and again after a short batch that follows a get_state (which drops the prepared
     sweep) -- as launcher.cpp:85-132 would leave them."""
     ds, eng, ost, rng, pc, ps = start(hd, oracle, name, seed=11)
+    if mode == "nopipe":
+        eng.set_debug(4194304)
+    elif mode == "gateoff":
+        eng.set_pipe_wait_us(-1.0)
     params = eng.chain_params(m=3, iterations=warm + timed + 3, L=0, burnin=0, neal8=True, split_merge=False)
     eng._params = params
 
@@ -198,6 +208,8 @@ def test_bench_path_iterations_api(hd, oracle, name, warm, timed):
     it = 1
     _, ll = eng.iterations(it, warm)
     it += warm
+    if mode == "nopipe":
+        eng.drop_prepared()                    # bench.py's window start (hdpm_drop_prepared)
     eng.synchronize()
     eng.reset_stats()
     np.testing.assert_allclose(ll, oracle_iters(it - warm, warm), rtol=RTOL, atol=0)
@@ -206,6 +218,12 @@ def test_bench_path_iterations_api(hd, oracle, name, warm, timed):
     eng.synchronize()
     st = eng.stats()
     assert st["sweeps"] == timed
+    if name == "c5" and mode == "":
+        assert st["pipe_runs"] > 0, st          # the device-gated pipeline ran (engine.cpp pipe_go)
+    if mode == "nopipe":
+        assert st["pipe_enqueued"] == 0 and st["pipe_runs"] == 0, st
+    if mode == "gateoff":
+        assert st["pipe_recovered"] > 0, st
     np.testing.assert_allclose(ll, oracle_iters(it - timed, timed), rtol=RTOL, atol=0)
     same(eng, ost, rng, "after the timed batch")
     _, ll = eng.iterations(it, 3)

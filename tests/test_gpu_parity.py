@@ -169,6 +169,41 @@ def test_device_update_phi_small_clusters_fall_back_or_match(hd, oracle, zoo):
     assert stats["phi_device_calls"] + stats["phi_device_fallbacks"] == 3
 
 
+def test_device_update_phi_subset_then_loglik(hd, oracle):
+    # a full device update_phi sums the regrouped log-likelihood and caches it; a following
+    # update_phi of a label subset (device or host) changes parameters without a label change,
+    # so compute_loglikelihood must not return the cached sum
+    ds = synth(8000, 64, 6, (2, 5), seed=12)
+    cen, sig = random_params(ds, 6, 14)
+    st = oracle.seed_state(47)
+    pc, ps, _ = oracle.pool_generate(ds.attrisize, ds.v, ds.w, ds.n * 3, st)
+    eng = make_engine(hd, ds)
+    eng.set_phi_device(True)
+    eng.set_state(ds.truth, cen, sig)
+    eng.set_pool(pc, ps)
+    eng.rng_state = st
+    ost = oracle_state(oracle, ds.truth, cen, sig)
+    rng = st.copy()
+    for it in range(2):
+        eng.neal8_sweep(3)
+        assert oracle.neal8_sweep(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w, ost, 3, pc, ps, rng, fast=1) == 0
+        eng.update_phi()
+        assert oracle.update_phi(ds.codes, ds.attrisize, ds.v, ds.w, ost, rng) == 0
+        ll = eng.compute_loglikelihood()
+        ref = oracle.compute_loglikelihood(ds.codes, ds.attrisize, ost)
+        assert abs(ll - ref) <= RTOL * abs(ref)
+        sub = [0, 2] if it == 0 else [1]
+        eng.update_phi(sub)
+        assert oracle.update_phi(ds.codes, ds.attrisize, ds.v, ds.w, ost, rng, idx=sub) == 0
+        assert_same_state(eng, ost)
+        assert np.array_equal(eng.rng_state, rng)
+        ll = eng.compute_loglikelihood()
+        ref = oracle.compute_loglikelihood(ds.codes, ds.attrisize, ost)
+        assert abs(ll - ref) <= RTOL * abs(ref), f"stale log-likelihood after a subset update ({it})"
+    assert eng.stats()["phi_device_calls"] >= 2
+    eng.close()
+
+
 def test_synthetic_large_d_sweep(hd, oracle):
     ds = synth(1500, 300, 4, (2, 6), seed=4)
     cen, sig = random_params(ds, 4, 8)
