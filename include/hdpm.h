@@ -77,6 +77,12 @@ typedef struct {
      * go decisions refused because the wait kernel's limit was near (the sweep ran
      * unpipelined), and enqueued sweeps gated off on the device and re-run from point 0 */
     int64_t pipe_enqueued, pipe_runs, pipe_refused, pipe_recovered;
+    /* device update_phi by composition trees (every pick fixed), and tree-mode updates re-run
+     * by the per-start-drift walks (a pick depended on the uniform) */
+    int64_t phi_tree_calls, phi_tree_retries;
+    /* device pool generations whose entry starts fell back to the sequential host walk (a
+     * chunk of the parallel walk did not meet its predecessor, or debug bit 28) */
+    int64_t pool_walk_fallbacks;
 } hdpm_stats;
 
 int         hdpm_device_count(void);
@@ -189,7 +195,9 @@ int hdpm_reset_stats(hdpm_ctx* ctx);
  * the fixed-point resolver for every launch it fits (by default a launch after one that listed
  * fewer than 64 points -- a converged chain -- takes the one-wave LIST resolver); bit 26: the
  * fixed-point resolver's first round starts every point from "stay" instead of its snapshot
- * draw's outcome. */
+ * draw's outcome; bit 27: the device update_phi resolves its drifts by the per-start-drift walks
+ * (k_phi_cwalk) instead of the composition trees (k_phi_tree); bit 28: the device pool generator's
+ * entry starts by the sequential host walk instead of the parallel chunk walks (k_pool_walk). */
 int hdpm_set_debug(hdpm_ctx* ctx, int32_t mode);
 /* The prepass's pool-entry heads, P entries of wb*Ws + 2 words padded to a power of two
  * (Ws <= 4) or to a multiple of 8 words (wide layouts) (csrc/kernels.hpp "Pool-entry heads",

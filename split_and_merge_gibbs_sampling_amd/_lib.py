@@ -64,7 +64,8 @@ class Stats(C.Structure):
         [(n, C.c_double) for n in ("t_sm_ms", "t_sm_scan_ms", "t_sm_phi_ms", "t_sm_terms_ms")] + \
         [(n, C.c_int64) for n in ("phi_device_calls", "phi_device_fallbacks", "phi_device_last_status",
                                   "phi_lookahead_hits", "phi_lookahead_copies", "pipe_enqueued", "pipe_runs",
-                                  "pipe_refused", "pipe_recovered")]
+                                  "pipe_refused", "pipe_recovered", "phi_tree_calls", "phi_tree_retries",
+                                  "pool_walk_fallbacks")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -73,6 +73,8 @@ hipError_t launch_lmatrix(const uint8_t* codes_t, int n, int d, int nq, ParamTab
 hipError_t launch_phi(const PhiArgs& a, hipStream_t s);
 size_t phi_cwalk_lds(int d, int nw, int wpb);
 size_t phi_values_lds(int d, int nw);
+size_t phi_tree_lds_bytes(int SB, int nw, int W);
+size_t phi_values2_lds_bytes(int d, int nb, int T, int W, int nw);
 int phi_ilp();
 int sm_restricted_gibbs_device(struct Ctx* c, const int32_t* S, int32_t nS, int32_t i1, int32_t i2,
                                int32_t t);
@@ -756,8 +758,9 @@ struct Ctx {
     PinBuf<uint32_t> h_init, h_tail;
     DevBuf<uint64_t> bm;
     PinBuf<uint64_t> h_bm;
-    DevBuf<int64_t> starts;
+    DevBuf<int64_t> starts, ext;
     PinBuf<int64_t> h_starts;
+    int64_t walk_fallbacks = 0;       // chunks that did not meet: serial host parse
     DevBuf<PoolClass> cls;
     DevBuf<int> runs;
     DevBuf<int32_t> att;
@@ -1783,31 +1786,55 @@ struct Ctx {
 
       const int64_t nwords = (count + 127) / 128;
       pg.bm.ensure((size_t)nc * 2 * nwords);
-      PoolAcceptArgs aa{pg.raw.p, count, nc, pg.cls.p, pg.bm.p, nwords, pg.gtab.p};
+      // d even: every entry and every run starts at an even position, so only the even tables
+      // are read (pool_gen.hpp)
+      const int par_mask = (d % 2 == 0) ? 1 : 3;
+      PoolAcceptArgs aa{pg.raw.p, count, nc, pg.cls.p, pg.bm.p, nwords, pg.gtab.p, par_mask};
       HIPCHK(launch_pool_accept(aa, stream));
       HIPCHK(hipStreamSynchronize(stream));
       auto t1 = clk::now();
-      pg.h_bm.ensure((size_t)nc * 2 * nwords);
-      HIPCHK(hipMemcpyAsync(pg.h_bm.p, pg.bm.p, (size_t)nc * 2 * nwords * 8, hipMemcpyDeviceToHost, stream));
-      HIPCHK(hipStreamSynchronize(stream));
-
+      // entry starts: chunks walked in parallel from guesses, joined where they meet
+      // (k_pool_walk / k_pool_merge); the serial host parse when a chunk does not meet
+      const int C = 512, M = 512;
+      const int64_t chunks = P_ / C + 1;
+      pg.starts.ensure(P_ + 1);
+      pg.ext.ensure((size_t)chunks * M);
       pg.h_starts.ensure(P_ + 1);
-      PoolRuns R{(int)pl.run_cls.size(), pl.run_cls.data(), pl.run_len.data()};
-      const int64_t end = pool_parse(pg.h_bm.p, nwords, d, R, 0, 0, P_, pg.h_starts.p);
+      HIPCHK(hipMemsetAsync(pg.err.p, 0, 4, stream));
+      PoolWalkArgs wa{pg.bm.p, nwords, d, (int)pl.run_cls.size(), pg.runs.p, pg.runs.p + pl.run_cls.size(), P_, C, M,
+                      pl.mean_len, count, pg.starts.p, pg.ext.p, pg.err.p};
+      HIPCHK(launch_pool_walk(wa, stream));
+      HIPCHK(hipMemcpyAsync(pg.h_err.p, pg.err.p, 4, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipMemcpyAsync(&pg.h_starts.p[P_], pg.starts.p + P_, 8, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+      int64_t end = pg.h_starts.p[P_];
+      const int werr = *pg.h_err.p;
+      if (werr & 8) end = -1;
+      if (!(werr & 8) && (werr & 4 || (debug & 268435456))) {
+        // a chunk did not meet its predecessor (or debug bit 28): the sequential walk
+        pg.walk_fallbacks++;
+        stats.pool_walk_fallbacks++;
+        pg.h_bm.ensure((size_t)nc * 2 * nwords);
+        HIPCHK(hipMemcpyAsync(pg.h_bm.p, pg.bm.p, (size_t)nc * 2 * nwords * 8, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+        PoolRuns R{(int)pl.run_cls.size(), pl.run_cls.data(), pl.run_len.data()};
+        end = pool_parse(pg.h_bm.p, nwords, d, R, 0, 0, P_, pg.h_starts.p);
+        if (end >= 0) {
+          pg.h_starts.p[P_] = end;
+          HIPCHK(hipMemcpyAsync(pg.starts.p, pg.h_starts.p, (size_t)(P_ + 1) * 8, hipMemcpyHostToDevice, stream));
+        }
+      }
       auto t2 = clk::now();
       stats.t_pool_mt_ms += ms(t0, tm);
       stats.t_pool_accept_ms += ms(tm, t1);
       stats.t_pool_parse_ms += ms(t1, t2);
       if (end < 0 || end + 624 > count) continue;      // slice too short: a longer one
-      pg.h_starts.p[P_] = end;
 
       P = P_;
       d_pool_codes.ensure((size_t)P * dp);
       d_pool_tab.ensure((size_t)P * 2 * d);
       d_pool_bnd.ensure((size_t)P * bw);
       d_pool_sig.ensure((size_t)P * d);
-      pg.starts.ensure(P + 1);
-      HIPCHK(hipMemcpyAsync(pg.starts.p, pg.h_starts.p, (size_t)(P + 1) * 8, hipMemcpyHostToDevice, stream));
       HIPCHK(hipMemsetAsync(pg.err.p, 0, 4, stream));
       PoolValueArgs va{pg.raw.p, count, pg.starts.p, P, d, dp, wb, Ws, bw, pg.att.p, (int)pl.run_cls.size(),
                        pg.runs.p, pg.runs.p + pl.run_cls.size(), pg.cls.p, pg.bm.p, nwords, pg.gtab.p,
@@ -3126,6 +3153,11 @@ struct Ctx {
     DevBuf<int64_t> apos, dts;
     DevBuf<double> lg, lzz;
     DevBuf<int> F;
+    DevBuf<uint16_t> tree;             // composition trees (tree mode)
+    DevBuf<int> tnd;                   // per cluster: a pick depends on the uniform
+    // tree mode when every updated cluster has at least this many members (a small cluster's
+    // center picks can depend on the uniform); raised past a cluster size that needed a retry
+    int tree_min_count = 16;
     PinBuf<uint8_t> h_in, h_out;
     double p_rej = 0.12;               // rbeta attempts rejected (window model), adapted per call
     int64_t calls = 0, fallbacks = 0;
@@ -3189,6 +3221,10 @@ struct Ctx {
     int T = 0, nw = 0, Wc = 0, wpb = 0, groups = 0, L = 0, S = 1;
     int64_t items = 0, need = 0;
     double rate = 0, sdev = 0;
+    // composition trees (phi.hip k_phi_tree): tables of tW drifts, tnb level-0 blocks per
+    // cluster, tSB blocks per workgroup, tS workgroups per cluster, tpc tables per cluster
+    bool tree_ok = false;
+    int tW = 0, tnb = 0, tSB = 0, tS = 0, tpc = 0, root_lds = 0;
   };
   PhiPlan phi_plan(int T) const {
     PhiPlan pl;
@@ -3215,6 +3251,16 @@ struct Ctx {
     pl.L = (d + pl.S - 1) / pl.S;
     pl.groups = (pl.Wc + 1024 * phi_ilp() - 1) / (1024 * phi_ilp());
     pl.ok = true;
+    // tree mode: the largest segment (<= 32 blocks of 4 items) whose tables fit the LDS
+    pl.tW = 64 * (pl.nw - 1);
+    pl.tnb = (d + 3) / 4;
+    pl.tSB = 32;
+    while (pl.tSB > 1 && phi_tree_lds_bytes(pl.tSB, pl.nw, pl.tW) > 150 * 1024) pl.tSB /= 2;
+    pl.tS = (pl.tnb + pl.tSB - 1) / pl.tSB;
+    pl.tpc = phi_loff(pl.tnb, phi_ltop(pl.tnb) + 1);
+    pl.root_lds = phi_values2_lds_bytes(d, pl.tnb, T, pl.tW, pl.nw) <= 150 * 1024 ? 1 : 0;
+    pl.tree_ok = pl.tW >= 64 && phi_tree_lds_bytes(pl.tSB, pl.nw, pl.tW) <= 150 * 1024 && pl.root_lds &&
+                 pl.tW < 65535;
     return pl;
   }
   // scratch of a plan, and the arguments every call shares (the caller sets raw, labels /
@@ -3246,6 +3292,13 @@ struct Ctx {
     a.maskd = phd.maskd.p; a.ikind = phd.ikind.p; a.wpb = pl.wpb; a.groups = pl.groups; a.L = pl.L; a.S = pl.S;
     a.raw_ptr = nullptr; a.gate = nullptr; a.pos_in = nullptr; a.pos_out = nullptr; a.sweep_len = 0;
     a.slot_of = nullptr;
+    a.tree = nullptr;
+    a.tW = pl.tW; a.tnb = pl.tnb; a.tSB = pl.tSB; a.tS = pl.tS; a.tpc = pl.tpc; a.tRootLds = pl.root_lds;
+    if (pl.tree_ok) {
+      phd.tree.ensure((size_t)T * pl.tpc * pl.tW);
+      phd.tnd.ensure(T);
+    }
+    a.tnd = phd.tnd.p;
     return a;
   }
 
@@ -3289,22 +3342,34 @@ struct Ctx {
     phd.stage.ensure(L.bytes);
     HIPCHK(hipMemcpyAsync(phd.lab_cnt.p, hl, (size_t)2 * T * 4, hipMemcpyHostToDevice, stream));
     HIPCHK(hipMemcpyAsync(phd.sig_in.p, hs, (size_t)items * 8, hipMemcpyHostToDevice, stream));
-    HIPCHK(hipMemsetAsync(phd.status.p, 0, 16, stream));
-    HIPCHK(hipMemsetAsync(phd.act.p, 0, 4, stream));
     HIPCHK(hipStreamWaitEvent(stream, W->done, 0));
     a.lab = phd.lab_cnt.p; a.cnt = phd.lab_cnt.p + T; a.freq = fsrc; a.sig_in = phd.sig_in.p;
     a.raw = W->raw.p + (rng.pos - W->start_pos);
     a.nraw = (int64_t)(W->start_pos + (uint64_t)W->count - rng.pos);
     a.pick = phd.pick.p; a.status = phd.status.p;
     a.stage = phd.stage.p; a.sig_out = phd.sig_out.p; a.ll = phd.ll.p;
-    HIPCHK(launch_phi(a, stream));
     // results: status + consumption, picks, sigmas, log-likelihood terms
     const size_t o_pick = 16, o_sig = align16(o_pick + (size_t)items), o_ll = o_sig + (size_t)items * 8;
     phd.h_out.ensure(o_ll + (size_t)2 * T * 8);
-    HIPCHK(hipMemcpyAsync(phd.h_out.p, phd.status.p, 16, hipMemcpyDeviceToHost, stream));
-    HIPCHK(hipMemcpyAsync(phd.h_out.p + o_pick, phd.pick.p, (size_t)items, hipMemcpyDeviceToHost, stream));
-    HIPCHK(hipMemcpyAsync(phd.h_out.p + o_sig, phd.sig_out.p, (size_t)items * 8, hipMemcpyDeviceToHost, stream));
-    HIPCHK(hipMemcpyAsync(phd.h_out.p + o_ll, phd.ll.p, (size_t)2 * T * 8, hipMemcpyDeviceToHost, stream));
+    auto run = [&](bool tree) {
+      a.tree = tree ? phd.tree.p : nullptr;
+      if (tree) HIPCHK(hipMemsetAsync(phd.tnd.p, 0, (size_t)T * 4, stream));
+      HIPCHK(hipMemsetAsync(phd.status.p, 0, 16, stream));
+      HIPCHK(hipMemsetAsync(phd.act.p, 0, 4, stream));
+      HIPCHK(launch_phi(a, stream));
+      HIPCHK(hipMemcpyAsync(phd.h_out.p, phd.status.p, 16, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipMemcpyAsync(phd.h_out.p + o_pick, phd.pick.p, (size_t)items, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipMemcpyAsync(phd.h_out.p + o_sig, phd.sig_out.p, (size_t)items * 8, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipMemcpyAsync(phd.h_out.p + o_ll, phd.ll.p, (size_t)2 * T * 8, hipMemcpyDeviceToHost, stream));
+    };
+    // the composition trees unless a cluster is small enough for a pick to depend on the
+    // uniform (debug bit 27: always the per-start-drift walks)
+    int min_count = INT_MAX;
+    for (int t = 0; t < T; ++t) min_count = std::min(min_count, hl[T + t]);
+    // (with one walk segment per cluster, d <= 128, such clusters are walked inside the tree-mode
+    // update itself)
+    const bool tree = pl.tree_ok && (pl.S == 1 || min_count >= phd.tree_min_count) && !(debug & 134217728);
+    run(tree);
     histogram_wait(nidx == 0 ? nullptr : &mask);
     if (freq_next_pending) {
       std::swap(h_freq.p, h_freq_next.p);
@@ -3312,6 +3377,15 @@ struct Ctx {
       freq_next_pending = false;
     }
     phd.calls++;
+    if (tree) stats.phi_tree_calls++;
+    if (tree && ((const int*)phd.h_out.p)[0] == kPhiNonDet) {
+      // a pick depends on the uniform: the same update by the walks (same inputs, nothing
+      // committed yet); updates with clusters this small take the walks directly from now on
+      phd.tree_min_count = std::max(phd.tree_min_count, std::min(1 << 20, 2 * min_count));
+      stats.phi_tree_retries++;
+      run(false);
+      HIPCHK(hipStreamSynchronize(stream));
+    }
     const int status = ((const int*)phd.h_out.p)[0];
     stats.phi_device_last_status = status;
     int64_t cons = 0;

@@ -373,7 +373,35 @@ struct PhiArgs {
   int Wc;
   int L, S;                  // walk segments: items [s L, (s + 1) L) of a cluster, S per cluster
   int64_t* dts;              // [T] the start drift of each cluster (k_phi_chain)
+  // composition trees (k_phi_tree, k_phi_tree_top, k_phi_values2; used when tree != nullptr):
+  // every item whose pick does not depend on the uniform is a function of the drift, f(delta) =
+  // delta + 2 (attempts rejected from delta on); a node of the tree is the composition of the
+  // functions of its items, tabulated over the tW start drifts phi_lo(first item) + c as the
+  // extra uniforms it consumes (uint16, kPhiBad: outside the windows).  Level 0 nodes are
+  // blocks of 4 items, a level-l node the composition of its two level-(l - 1) children;
+  // cluster t's tables start at tree + t * tpc * tW (level l at phi_loff(tnb, l)).
+  uint16_t* tree;
+  int tW;                    // start drifts per table (64 (nw - 1): a lookup reads two mask words)
+  int tnb;                   // level-0 blocks per cluster, ceil(d / 4)
+  int tSB, tS;               // blocks per k_phi_tree workgroup (power of two), workgroups per cluster
+  int tpc;                   // tables per cluster
+  int tRootLds;              // (unused: the roots are always staged in LDS)
+  int* tnd;                  // [T] cluster t has a pick that depends on the uniform: walked per start
+                             // drift (k_phi_cwalk) into its root table, then from its drift (one wave)
 };
+// Level sizes of a composition tree over nb >= 1 level-0 blocks.
+__host__ __device__ inline int phi_lcount(int nb, int l) { return ((nb - 1) >> l) + 1; }
+__host__ __device__ inline int phi_loff(int nb, int l) {
+  int o = 0;
+  for (int i = 0; i < l; ++i) o += phi_lcount(nb, i);
+  return o;
+}
+__host__ __device__ inline int phi_ltop(int nb) {
+  int l = 0;
+  while (phi_lcount(nb, l) > 1) ++l;
+  return l;
+}
+constexpr uint16_t kPhiBad = 0xFFFF;
 
 // Drift windows of the device update_phi (phi.hip).  Extra uniforms per sigma draw: mean
 // rate, sd sdev; after k draws the drift is rate k +- kPhiSd sdev sqrt(k).
@@ -412,8 +440,10 @@ struct PipeArgs {
                              // [2] log-likelihood bits, [3] next position, [4] phi status, [5] window stop
 };
 
+// kPhiNonDet: a center pick depends on the uniform (the composition trees need fixed picks);
+// the update is re-run with the per-start-drift walks (k_phi_cwalk)
 enum PhiStatus { kPhiOk = 0, kPhiWalker = 1, kPhiBisect = 2, kPhiAmbig = 3, kPhiWindow = 4, kPhiShort = 5,
-                 kPhiProb = 6, kPhiInactive = 7, kPhiCap = 8 };
+                 kPhiProb = 6, kPhiInactive = 7, kPhiCap = 8, kPhiNonDet = 9 };
 
 // R's Mersenne-Twister stream on the device (one workgroup, one twist per barrier).
 // Output r >= 0 continues the host state (X_0, mti0): the first 624 - mti0 outputs temper

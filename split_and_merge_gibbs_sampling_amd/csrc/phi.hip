@@ -309,16 +309,11 @@ __device__ __forceinline__ int phi_prep_item(const PhiArgs& a, int t, int j, int
   return 0;
 }
 
-__global__ __launch_bounds__(256) void k_phi_prep(PhiArgs a) {
-  if (a.gate && *(volatile const int*)a.gate == 0) return;
-  if (a.raw_ptr) a.raw = *a.raw_ptr;
-  __shared__ uint64_t tabs[256];
-  __shared__ double spr[256 * kPhiLdsLevels];
-  __shared__ uint8_t spm[256 * kPhiLdsLevels];
-  for (int i = threadIdx.x; i < 256; i += blockDim.x) tabs[i] = a.gtab[i];
-  __syncthreads();
+// Prep of the items of workgroup `blk` (tabs: the glibc exp table in LDS).
+__device__ __forceinline__ void phi_prep_block(const PhiArgs& a, int blk, const uint64_t* tabs, double* spr,
+                                               uint8_t* spm) {
   const int lane = threadIdx.x & 63;
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t idx = (int64_t)blk * blockDim.x + threadIdx.x;
   const bool ok = idx < (int64_t)a.T * a.d;
   const int t = ok ? (int)(idx / a.d) : 0, j = ok ? (int)(idx - (int64_t)t * a.d) : 0;
   int status = 0, nact = 0;
@@ -337,6 +332,18 @@ __global__ __launch_bounds__(256) void k_phi_prep(PhiArgs a) {
     } else {
       status = phi_prep_item(a, t, j, idx, a.cum + (int64_t)t * a.sumatt + off, a.perm + (int64_t)t * a.sumatt + off,
                              tabs, &det, &nact);
+    }
+  }
+  // the composition trees need every pick fixed and on rhig's beta path
+  // (a cluster with a pick that depends on the uniform is walked per start drift, k_phi_cwalk,
+  // when it fits one walk segment; otherwise the update is re-run by the walks, kPhiNonDet)
+  if (ok && !status && a.tree) {
+    const int kd = a.ikind[idx];
+    if (!det) {
+      if (a.S > 1) status = kPhiNonDet;
+      else atomicOr(&a.tnd[t], 1);
+    } else {
+      status = kd == 1 ? kPhiBisect : (kd != 2 && kd != 3) ? kPhiInactive : 0;
     }
   }
   if (status) set_status(a.status, status);
@@ -367,17 +374,26 @@ __global__ __launch_bounds__(256) void k_phi_prep(PhiArgs a) {
 // ------------------------------------------------------------------ stream logits
 // lg[p] = log(u_p / (1 - u_p)) and lzz[p] = log(u_p * u_p * u_(p+1)) over the positions any
 // draw of the update can take (the same expressions as rbeta's, rmath.hpp RngSrc / BB).
-__global__ __launch_bounds__(256) void k_phi_logits(PhiArgs a) {
-  if (a.gate && *(volatile const int*)a.gate == 0) return;
-  if (a.raw_ptr) a.raw = *a.raw_ptr;
-  __shared__ uint64_t tlog[256];
-  for (int i = threadIdx.x; i < 256; i += blockDim.x) tlog[i] = a.gtab[256 + i];
-  __syncthreads();
-  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < a.span; p += (int64_t)gridDim.x * blockDim.x) {
+__device__ __forceinline__ void phi_logits_block(const PhiArgs& a, int blk, int nblk, const uint64_t* tlog) {
+  for (int64_t p = (int64_t)blk * blockDim.x + threadIdx.x; p < a.span; p += (int64_t)nblk * blockDim.x) {
     const double u1 = pool_unif(a.raw[p]), u2 = pool_unif(a.raw[p + 1]);
     a.lg[p] = glibc::log_r(u1 / (1.0 - u1), tlog);
     a.lzz[p] = glibc::log_r(u1 * u1 * u2, tlog);
   }
+}
+
+// Both in one launch: workgroups [0, nprep) prepare the items, the others compute the logits
+// (independent work; one dispatch less on the update's dependency chain).
+__global__ __launch_bounds__(256) void k_phi_prep(PhiArgs a, int nprep) {
+  if (a.gate && *(volatile const int*)a.gate == 0) return;
+  if (a.raw_ptr) a.raw = *a.raw_ptr;
+  __shared__ uint64_t tabs[512];
+  __shared__ double spr[256 * kPhiLdsLevels];
+  __shared__ uint8_t spm[256 * kPhiLdsLevels];
+  for (int i = threadIdx.x; i < 512; i += blockDim.x) tabs[i] = a.gtab[i];
+  __syncthreads();
+  if ((int)blockIdx.x < nprep) phi_prep_block(a, blockIdx.x, tabs, spr, spm);
+  else phi_logits_block(a, blockIdx.x - nprep, gridDim.x - nprep, tabs + 256);
 }
 
 // ------------------------------------------------------------------ masks
@@ -562,6 +578,8 @@ __global__ __launch_bounds__(1024) void k_phi_cwalk(PhiArgs a) {
   const int d = a.d, nw = a.nw;
   const int ts = blockIdx.x / a.groups, g = blockIdx.x - ts * a.groups;
   const int t = ts / a.S, sg = ts - t * a.S;
+  // tree mode: only the clusters with a pick that depends on the uniform (one segment)
+  if (a.tree && !a.tnd[t]) return;
   const int j0 = sg * a.L, j1 = min(d, j0 + a.L);
   uint64_t* m = reinterpret_cast<uint64_t*>(wl);
   uint8_t* det = wl + (size_t)d * nw * 8;
@@ -581,6 +599,9 @@ __global__ __launch_bounds__(1024) void k_phi_cwalk(PhiArgs a) {
   __syncthreads();
   const int cstep = a.groups * blockDim.x;
   const int c0 = g * blockDim.x + threadIdx.x;
+  uint16_t* root = a.tree ? a.tree + ((int64_t)t * a.tpc + phi_loff(a.tnb, phi_ltop(a.tnb))) * a.tW : nullptr;
+  if (root && g == 0)                      // start drifts past the walks' window
+    for (int c = a.Wc + threadIdx.x; c < a.tW; c += blockDim.x) root[c] = kPhiBad;
   if (c0 >= a.Wc) return;
   const int64_t clo = phi_lo((int64_t)t * d + j0, a.rate, a.sdev);
   int64_t dt0[kPhiIlp], delta[kPhiIlp];
@@ -678,7 +699,10 @@ __global__ __launch_bounds__(1024) void k_phi_cwalk(PhiArgs a) {
 #pragma unroll
   for (int u = 0; u < kPhiIlp; ++u) {
     const int c = c0 + u * cstep;
-    if (c < a.Wc)
+    if (c >= a.Wc) continue;
+    if (root)                              // tree mode: the cluster's root table (extra uniforms)
+      root[c] = code[u] == 0 && delta[u] - dt0[u] < (int64_t)kPhiBad ? (uint16_t)(delta[u] - dt0[u]) : kPhiBad;
+    else
       a.F[(int64_t)ts * a.Wc + c] = code[u] == 0 && delta[u] <= 0x7fffffff ? (int)delta[u] : (code[u] ? code[u] : -1);
   }
 }
@@ -773,39 +797,16 @@ __global__ __launch_bounds__(1024) void k_phi_chain(PhiArgs a) {
 // sigma = -1/log(out), the dhamming tables; then the bound record (wave w: plane word w) and
 // the regrouped log-likelihood terms.  LDS: the cluster image, picks, positions, per
 // attribute (sigma, match, mismatch), per thread the partial sums.
-__global__ __launch_bounds__(1024) void k_phi_values(PhiArgs a) {
-  if (a.gate && *(volatile const int*)a.gate == 0) return;
-  if (a.raw_ptr) a.raw = *a.raw_ptr;
-  extern __shared__ __attribute__((aligned(16))) uint8_t wl[];
-  __shared__ uint64_t tabs[512];
-  __shared__ double red[4 * 16];
-  __shared__ int sbad;
-  for (int i = threadIdx.x; i < 512; i += blockDim.x) tabs[i] = a.gtab[i];
-  if (threadIdx.x == 0) sbad = 0;
-  if (*a.status != 0) return;
-  const uint64_t* texp = tabs;
-  const uint64_t* tlog = tabs + 256;
+// The values of cluster t once its picks (spick) and accepted attempts' positions (sapos)
+// are known: every wave takes attributes -- the accepted attempts' draws, sigma = -1/log(out),
+// the dhamming tables -- then the bound record (wave w: plane word w) and the regrouped
+// log-likelihood terms.  wtab: LDS [d][2]; red: LDS [64]; wmx, wmn: LDS [16]; sbad: LDS flag
+// (0 on entry).  Called by every thread of the workgroup.
+__device__ __forceinline__ void phi_values_body(const PhiArgs& a, int t, const uint8_t* spick, const int64_t* sapos, double* wtab,
+                                const uint64_t* texp, const uint64_t* tlog, double* red, double* wmx, double* wmn,
+                                int* sbad) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nth = blockDim.x;
-  const int t = blockIdx.x;
   const int d = a.d;
-  uint64_t* m = reinterpret_cast<uint64_t*>(wl);
-  uint8_t* det = wl + (size_t)d * a.nw * 8;
-  uint8_t* ik = det + d;
-  phi_stage_cluster(a, t, m, det, ik);
-  double* wtab = reinterpret_cast<double*>(wl + phi_cluster_lds(d, a.nw));   // [d][2]
-  int64_t* sapos = reinterpret_cast<int64_t*>(wtab + 2 * d);
-  uint8_t* spick = reinterpret_cast<uint8_t*>(sapos + d);
-  __syncthreads();
-  if (wid == 0) {
-    int why = 0;
-    const PhiClusterLds C{m, det, ik};
-    if (phi_walk_cluster(a, C, t, a.dts[t], spick, sapos, &why) < 0 && lane == 0) {
-      set_status(a.status, why ? why : kPhiWindow);
-      sbad = 1;
-    }
-  }
-  __syncthreads();
-  if (sbad) return;
   const UploadLayout L = upload_layout(a.T, a.dp, d, a.bw);
   uint8_t* codes = a.stage + L.off_codes + (size_t)t * a.dp;
   double* tab = reinterpret_cast<double*>(a.stage + L.off_tab) + (size_t)t * 2 * d;
@@ -849,7 +850,7 @@ __global__ __launch_bounds__(1024) void k_phi_values(PhiArgs a) {
     add(fm * m0);
     add(((double)nn - fm) * m1);
   }
-  if (bad) atomicOr(&sbad, 1);
+  if (bad) atomicOr(sbad, 1);
   // per wave: A and scale summed (any order: only the bound's slack sees their rounding),
   // the log-likelihood pairs in lane order
   {
@@ -874,7 +875,7 @@ __global__ __launch_bounds__(1024) void k_phi_values(PhiArgs a) {
     }
   }
   __syncthreads();
-  if (sbad) {
+  if (*sbad) {
     if (threadIdx.x == 0) set_status(a.status, kPhiWindow);
     return;
   }
@@ -885,7 +886,6 @@ __global__ __launch_bounds__(1024) void k_phi_values(PhiArgs a) {
     dmx = fmax(dmx, __shfl_xor(dmx, o));
     dmn = fmin(dmn, __shfl_xor(dmn, o));
   }
-  __shared__ double wmx[16], wmn[16];
   if (lane == 0) { wmx[wid] = dmx; wmn[wid] = dmn; }
   __syncthreads();
   dmx = 0.0;
@@ -938,19 +938,346 @@ __global__ __launch_bounds__(1024) void k_phi_values(PhiArgs a) {
   }
 }
 
+// One workgroup per cluster: wave 0 walks it again from its actual drift (picks and accepted
+// positions into LDS), then phi_values_body.  LDS: the cluster image, picks, positions, per
+// attribute (sigma, match, mismatch), per thread the partial sums.
+__global__ __launch_bounds__(1024) void k_phi_values(PhiArgs a) {
+  if (a.gate && *(volatile const int*)a.gate == 0) return;
+  if (a.raw_ptr) a.raw = *a.raw_ptr;
+  extern __shared__ __attribute__((aligned(16))) uint8_t wl[];
+  __shared__ uint64_t tabs[512];
+  __shared__ double red[4 * 16];
+  __shared__ double wmx[16], wmn[16];
+  __shared__ int sbad;
+  for (int i = threadIdx.x; i < 512; i += blockDim.x) tabs[i] = a.gtab[i];
+  if (threadIdx.x == 0) sbad = 0;
+  if (*a.status != 0) return;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int t = blockIdx.x;
+  const int d = a.d;
+  uint64_t* m = reinterpret_cast<uint64_t*>(wl);
+  uint8_t* det = wl + (size_t)d * a.nw * 8;
+  uint8_t* ik = det + d;
+  phi_stage_cluster(a, t, m, det, ik);
+  double* wtab = reinterpret_cast<double*>(wl + phi_cluster_lds(d, a.nw));   // [d][2]
+  int64_t* sapos = reinterpret_cast<int64_t*>(wtab + 2 * d);
+  uint8_t* spick = reinterpret_cast<uint8_t*>(sapos + d);
+  __syncthreads();
+  if (wid == 0) {
+    int why = 0;
+    const PhiClusterLds C{m, det, ik};
+    if (phi_walk_cluster(a, C, t, a.dts[t], spick, sapos, &why) < 0 && lane == 0) {
+      set_status(a.status, why ? why : kPhiWindow);
+      sbad = 1;
+    }
+  }
+  __syncthreads();
+  if (sbad) return;
+  phi_values_body(a, t, spick, sapos, wtab, tabs, tabs + 256, red, wmx, wmn, &sbad);
+}
+
+// ------------------------------------------------------------------ composition trees
+// When every pick of the update is fixed (k_phi_prep, tree mode), item k's sigma draw is a
+// function of the drift alone: f_k(delta) = delta + 2 r with r the attempts its mask rejects
+// from delta on.  The update's drift is f_{T d - 1} o ... o f_0 (0), T d dependent steps; a
+// tree of compositions has log2(d) levels of independent table lookups instead.  A table holds
+// the extra uniforms its node consumes from each of tW start drifts phi_lo(first item) + c.
+
+// One item's step from drift e (mask row in `row`, window start `lo`): false outside the
+// windows or with no acceptance in the 32 attempts the two mask words hold.
+__device__ __forceinline__ bool phi_tree_step(const uint64_t* row, int lo, int W, int* e) {
+  const int off = *e - lo;
+  if ((unsigned)off >= (unsigned)W) return false;
+  const int q = off >> 6, sh = off & 63;
+  const uint64_t w0 = row[q], w1 = row[q + 1];
+  const uint64_t win = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
+  const uint64_t acc = win & 0x5555555555555555ull;
+  if (!acc) return false;
+  *e += __builtin_ctzll(acc);
+  return true;
+}
+
+// (left then right) at start offset c of the left table: the composed extra, or kPhiBad
+__device__ __forceinline__ uint16_t phi_tree_compose(const uint16_t* L, const uint16_t* R, int lo_l, int lo_r, int W,
+                                                     int c) {
+  const uint16_t v = L[c];
+  if (v == kPhiBad) return kPhiBad;
+  const int cr = lo_l + c + v - lo_r;
+  if ((unsigned)cr >= (unsigned)W) return kPhiBad;
+  const uint16_t r = R[cr];
+  if (r == kPhiBad || (int)v + (int)r >= (int)kPhiBad) return kPhiBad;
+  return (uint16_t)(v + r);
+}
+
+__host__ __device__ inline size_t phi_tree_lds(int SB, int nw, int W) {
+  return align16((size_t)4 * SB * nw * 8) + align16((size_t)4 * SB * 4) + align16((size_t)2 * SB * W * 2);
+}
+
+// Workgroup (t, s): level-0 tables of blocks [s SB, s SB + SB) of cluster t (each from the
+// item masks staged in LDS: a 4-item walk per start drift), then levels 1 .. log2(SB) of that
+// segment (compositions in LDS); every table also goes to a.tree.
+__global__ __launch_bounds__(1024) void k_phi_tree(PhiArgs a) {
+  if (a.gate && *(volatile const int*)a.gate == 0) return;
+  extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+  if (*a.status != 0) return;
+  const int S = a.tS, SB = a.tSB, nb = a.tnb, W = a.tW, nw = a.nw, d = a.d;
+  const int t = blockIdx.x / S, s = blockIdx.x - t * S;
+  if (a.tnd[t]) return;                              // walked per start drift (k_phi_cwalk)
+  const int b0 = s * SB, nblk = min(nb - b0, SB);
+  const int j0 = 4 * b0, nit = min(d, 4 * (b0 + nblk)) - j0;
+  uint64_t* M = reinterpret_cast<uint64_t*>(sm);
+  int* slo = reinterpret_cast<int*>(sm + align16((size_t)4 * SB * nw * 8));
+  uint16_t* A = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(slo) + align16((size_t)4 * SB * 4));
+  {
+    const uint64_t* src = a.maskd + ((int64_t)t * d + j0) * nw;
+    for (int q = threadIdx.x; q < nit * nw; q += blockDim.x) M[q] = src[q];
+    for (int j = threadIdx.x; j < nit; j += blockDim.x) slo[j] = (int)phi_lo((int64_t)t * d + j0 + j, a.rate, a.sdev);
+  }
+  __syncthreads();
+  uint16_t* G = a.tree + (int64_t)t * a.tpc * W;
+  for (int idx = threadIdx.x; idx < nblk * W; idx += blockDim.x) {
+    const int b = idx / W, c = idx - b * W;
+    const int jb = 4 * b, je = min(nit, jb + 4);
+    const int start = slo[jb] + c;
+    int e = start;
+    bool ok = true;
+    for (int j = jb; j < je && ok; ++j) ok = phi_tree_step(M + (size_t)j * nw, slo[j], W, &e);
+    const uint16_t v = ok && e - start < (int)kPhiBad ? (uint16_t)(e - start) : kPhiBad;
+    A[idx] = v;
+    G[(int64_t)(b0 + b) * W + c] = v;
+  }
+  const int ltop = phi_ltop(nb);
+  int np = nblk;                                     // nodes of the segment at the level below
+  // level l's tables at A + (l & 1) SB W (offsets from one LDS base: no pointer swaps)
+  for (int l = 1; l <= ltop && (1 << l) <= SB; ++l) {
+    __syncthreads();
+    const uint16_t* cur = A + (size_t)((l - 1) & 1) * SB * W;
+    uint16_t* nxt = A + (size_t)(l & 1) * SB * W;
+    const int nl = (np + 1) / 2;
+    const int off = phi_loff(nb, l) + (b0 >> l);
+    for (int idx = threadIdx.x; idx < nl * W; idx += blockDim.x) {
+      const int li = idx / W, c = idx - li * W;
+      const uint16_t* Lt = cur + (size_t)(2 * li) * W;
+      uint16_t v;
+      if (2 * li + 1 < np) {
+        const int jl = 4 * ((2 * li) << (l - 1)), jr = 4 * ((2 * li + 1) << (l - 1));
+        v = phi_tree_compose(Lt, cur + (size_t)(2 * li + 1) * W, slo[jl], slo[jr], W, c);
+      } else {
+        v = Lt[c];
+      }
+      nxt[(size_t)li * W + c] = v;
+      G[(int64_t)(off + li) * W + c] = v;
+    }
+    np = nl;
+  }
+}
+
+// Levels above the segments (tS > 1): one workgroup per cluster composes them in a.tree.
+__global__ __launch_bounds__(1024) void k_phi_tree_top(PhiArgs a) {
+  if (a.gate && *(volatile const int*)a.gate == 0) return;
+  if (*a.status != 0) return;
+  const int nb = a.tnb, W = a.tW, d = a.d, t = blockIdx.x;
+  if (a.tnd[t]) return;
+  int lseg = 0;
+  while ((1 << lseg) < a.tSB) ++lseg;
+  const int ltop = phi_ltop(nb);
+  uint16_t* G = a.tree + (int64_t)t * a.tpc * W;
+  for (int l = lseg + 1; l <= ltop; ++l) {
+    const int np = phi_lcount(nb, l - 1), nl = phi_lcount(nb, l);
+    const uint16_t* P = G + (int64_t)phi_loff(nb, l - 1) * W;
+    uint16_t* Q = G + (int64_t)phi_loff(nb, l) * W;
+    for (int idx = threadIdx.x; idx < nl * W; idx += blockDim.x) {
+      const int i = idx / W, c = idx - i * W;
+      const uint16_t* Lt = P + (size_t)(2 * i) * W;
+      uint16_t v;
+      if (2 * i + 1 < np) {
+        const int jl = 4 * ((2 * i) << (l - 1)), jr = 4 * ((2 * i + 1) << (l - 1));
+        v = phi_tree_compose(Lt, P + (size_t)(2 * i + 1) * W, (int)phi_lo((int64_t)t * d + jl, a.rate, a.sdev),
+                             (int)phi_lo((int64_t)t * d + jr, a.rate, a.sdev), W, c);
+      } else {
+        v = Lt[c];
+      }
+      Q[(size_t)i * W + c] = v;
+    }
+    __syncthreads();
+  }
+}
+
+__host__ __device__ inline size_t phi_values2_lds(int d, int nb, int T, int W, int nw) {
+  // (the roots of the clusters before each are always staged in LDS; then the cluster image
+  // of a cluster walked per start drift)
+  return align16((size_t)2 * d * 8) + align16((size_t)d * 8) + align16((size_t)d) + align16((size_t)2 * nb * 4 + 8) +
+         align16((size_t)T * W * 2) + phi_cluster_lds(d, nw);
+}
+
+// One workgroup per cluster t of a tree-mode update: its start drift (the root tables of the
+// clusters before it, composed from drift 0), the start drift of every tree node down to the
+// level-0 blocks (one lookup per node and level), each block's 4 items walked from its start
+// (picks fixed: det), then phi_values_body.  The last cluster also writes the consumption.
+__global__ __launch_bounds__(1024) void k_phi_values2(PhiArgs a) {
+  if (a.gate && *(volatile const int*)a.gate == 0) return;
+  if (a.raw_ptr) a.raw = *a.raw_ptr;
+  extern __shared__ __attribute__((aligned(16))) uint8_t wl[];
+  __shared__ uint64_t tabs[512];
+  __shared__ double red[4 * 16];
+  __shared__ double wmx[16], wmn[16];
+  __shared__ int sbad;
+  __shared__ int sdt;
+  for (int i = threadIdx.x; i < 512; i += blockDim.x) tabs[i] = a.gtab[i];
+  if (threadIdx.x == 0) sbad = 0;
+  if (*a.status != 0) return;
+  const int t = blockIdx.x, d = a.d, W = a.tW, nb = a.tnb, nw = a.nw;
+  double* wtab = reinterpret_cast<double*>(wl);
+  int64_t* sapos = reinterpret_cast<int64_t*>(wl + align16((size_t)2 * d * 8));
+  uint8_t* spick = reinterpret_cast<uint8_t*>(sapos) + align16((size_t)d * 8);
+  int* st = reinterpret_cast<int*>(spick + align16((size_t)d));     // node starts: two levels
+  uint16_t* R = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(st) + align16((size_t)2 * nb * 4 + 8));
+  uint8_t* img = reinterpret_cast<uint8_t*>(R) + align16((size_t)a.T * W * 2);   // cluster image (non-det)
+  const int ltop = phi_ltop(nb);
+  const int64_t rootoff = (int64_t)phi_loff(nb, ltop) * W;
+  // the start drift of cluster t: the clusters before it from drift 0 (their roots in LDS)
+  for (int q = threadIdx.x; q < t * W; q += blockDim.x) {
+    const int u = q / W, c = q - u * W;
+    R[q] = a.tree[(int64_t)u * a.tpc * W + rootoff + c];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int e = 0;
+    bool ok = true;
+    for (int u = 0; u < t && ok; ++u) {
+      const int c = e - (int)phi_lo((int64_t)u * d, a.rate, a.sdev);
+      if ((unsigned)c >= (unsigned)W) { ok = false; break; }
+      const uint16_t v = R[(size_t)u * W + c];
+      if (v == kPhiBad) ok = false;
+      else e += v;
+    }
+    sdt = ok ? e : -1;
+    if (!ok) sbad = 1;
+    else a.dts[t] = e;
+  }
+  __syncthreads();
+  if (sbad) {
+    if (threadIdx.x == 0) set_status(a.status, kPhiWindow);
+    return;
+  }
+  const uint16_t* G = a.tree + (int64_t)a.tpc * W * t;
+  if (a.tnd[t]) {
+    // a pick depends on the uniform: one wave walks the cluster from its start drift
+    uint64_t* m = reinterpret_cast<uint64_t*>(img);
+    uint8_t* det = img + (size_t)d * nw * 8;
+    uint8_t* ik = det + d;
+    phi_stage_cluster(a, t, m, det, ik);
+    __syncthreads();
+    if ((threadIdx.x >> 6) == 0) {
+      int why = 0;
+      const PhiClusterLds C{m, det, ik};
+      if (phi_walk_cluster(a, C, t, sdt, spick, sapos, &why) < 0 && (threadIdx.x & 63) == 0) {
+        set_status(a.status, why ? why : kPhiWindow);
+        sbad = 1;
+      }
+    }
+    __syncthreads();
+    if (sbad) return;
+  } else {
+  // node starts, from the root down (ping-pong between the two halves of st)
+  // level l's node starts at st + ((ltop - l) & 1) nb (offsets from one LDS base)
+  if (threadIdx.x == 0) st[0] = sdt;
+  __syncthreads();
+  for (int l = ltop; l >= 1; --l) {
+    const int* cur = st + ((ltop - l) & 1) * nb;
+    int* nxt = st + ((ltop - l + 1) & 1) * nb;
+    const int nc = phi_lcount(nb, l - 1);
+    const uint16_t* Lv = G + (int64_t)phi_loff(nb, l - 1) * W;
+    for (int i = threadIdx.x; i < nc; i += blockDim.x) {
+      int sv = cur[i >> 1];
+      if ((i & 1) && sv >= 0) {
+        // right child: after its left sibling's items
+        const int jl = 4 * ((i - 1) << (l - 1));
+        const int c = sv - (int)phi_lo((int64_t)t * d + jl, a.rate, a.sdev);
+        const uint16_t v = (unsigned)c < (unsigned)W ? Lv[(size_t)(i - 1) * W + c] : kPhiBad;
+        sv = v == kPhiBad ? -1 : sv + v;
+      }
+      nxt[i] = sv;
+    }
+    __syncthreads();
+  }
+  const int* cur = st + (ltop & 1) * nb;              // level 0
+  // each block's items from its start: the accepted attempt's position and the fixed pick
+  const int64_t base = (int64_t)t * 3 * d;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+    int e = cur[b];
+    bool ok = e >= 0;
+    for (int j = 4 * b; j < min(d, 4 * b + 4); ++j) {
+      const int64_t k = (int64_t)t * d + j;
+      spick[j] = (uint8_t)(a.det[k] - 1);
+      if (!ok) continue;
+      ok = phi_tree_step(a.maskd + k * nw, (int)phi_lo(k, a.rate, a.sdev), W, &e);
+      // the accepted attempt: nominal position + drift before the item + the rejected attempts
+      sapos[j] = base + d + 2 * (int64_t)j + e;
+    }
+    if (!ok) atomicOr(&sbad, 1);
+  }
+  __syncthreads();
+  if (sbad) {
+    if (threadIdx.x == 0) set_status(a.status, kPhiWindow);
+    return;
+  }
+  }
+  if (t == a.T - 1 && threadIdx.x == 0) {
+    const uint16_t v = (unsigned)(sdt - (int)phi_lo((int64_t)t * d, a.rate, a.sdev)) < (unsigned)W
+                           ? G[rootoff + sdt - (int)phi_lo((int64_t)t * d, a.rate, a.sdev)]
+                           : kPhiBad;
+    if (v == kPhiBad) {
+      set_status(a.status, kPhiWindow);
+    } else {
+      const int64_t cons = (int64_t)a.T * 3 * d + sdt + v;
+      if (cons + 1 > a.span) set_status(a.status, kPhiShort);
+      *(int64_t*)(a.status + 2) = cons;
+      if (a.pos_out) *a.pos_out = *a.pos_in + a.sweep_len + cons;
+    }
+  }
+  phi_values_body(a, t, spick, sapos, wtab, tabs, tabs + 256, red, wmx, wmn, &sbad);
+}
+
 // dynamic LDS of k_phi_cwalk (cluster image + a pick row per wave) and k_phi_values
 // (cluster image + tables, positions, picks)
 size_t phi_cwalk_lds(int d, int nw, int wpb) { return phi_cwalk_image(d, nw) + 0 * (size_t)wpb; }
 int phi_ilp() { return kPhiIlp; }
 size_t phi_values_lds(int d, int nw) { return phi_cluster_lds(d, nw) + (size_t)d * (16 + 8 + 1); }
 
+size_t phi_tree_lds_bytes(int SB, int nw, int W) { return phi_tree_lds(SB, nw, W); }
+size_t phi_values2_lds_bytes(int d, int nb, int T, int W, int nw) { return phi_values2_lds(d, nb, T, W, nw); }
+
+// tree mode (a.tree != nullptr): k_phi_prep (+ logits) -> k_phi_masks -> k_phi_tree ->
+// k_phi_tree_top (segments above one workgroup) -> k_phi_values2; else the per-start-drift
+// walks: k_phi_prep -> k_phi_masks -> k_phi_cwalk -> k_phi_chain -> k_phi_values
 hipError_t launch_phi(const PhiArgs& a, hipStream_t s) {
   const int64_t items = (int64_t)a.T * a.d;
   if (items <= 0) return hipSuccess;
-  if (a.nw < 1 || a.Wc < 1 || a.wpb < 1 || a.wpb > 16 || a.groups < 1) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_phi_prep, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(k_phi_logits, dim3((unsigned)std::min<int64_t>(1024, (a.span + 255) / 256)), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(k_phi_masks, dim3(1024), dim3(256), 0, s, a);
+  if (a.nw < 1 || a.wpb < 1 || a.wpb > 16) return hipErrorInvalidValue;
+  const int nprep = (int)((items + 255) / 256);
+  const int nlog = (int)std::min<int64_t>(1024, (a.span + 255) / 256);
+  hipLaunchKernelGGL(k_phi_prep, dim3((unsigned)(nprep + nlog)), dim3(256), 0, s, a, nprep);
+  // one wave per (candidate, mask word): enough workgroups for every fixed pick's item in one
+  // pass (the loop covers the extra candidates of uniform-dependent picks)
+  const int64_t mwaves = items * a.nw;
+  hipLaunchKernelGGL(k_phi_masks, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(32768, (mwaves + 3) / 4))),
+                     dim3(256), 0, s, a);
+  if (a.tree) {
+    if (a.tW < 64 || a.tSB < 1 || a.tS < 1 || a.tnb < 1) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_phi_tree, dim3((unsigned)(a.T * a.tS)), dim3(1024), phi_tree_lds(a.tSB, a.nw, a.tW), s, a);
+    if (a.tS > 1) hipLaunchKernelGGL(k_phi_tree_top, dim3((unsigned)a.T), dim3(1024), 0, s, a);
+    if (a.S == 1 && a.Wc >= 1 && a.groups >= 1) {
+      // clusters with a pick that depends on the uniform: their root tables by the walks
+      const int wthreads = std::min(1024, ((a.Wc + kPhiIlp * a.groups - 1) / (kPhiIlp * a.groups) + 63) / 64 * 64);
+      hipLaunchKernelGGL(k_phi_cwalk, dim3((unsigned)(a.T * a.groups)), dim3(wthreads), phi_cwalk_lds(a.d, a.nw, 16),
+                         s, a);
+    }
+    hipLaunchKernelGGL(k_phi_values2, dim3((unsigned)a.T), dim3(64 * a.wpb), phi_values2_lds(a.d, a.tnb, a.T, a.tW, a.nw),
+                       s, a);
+    return hipGetLastError();
+  }
+  if (a.Wc < 1 || a.groups < 1) return hipErrorInvalidValue;
   const int wthreads = std::min(1024, ((a.Wc + kPhiIlp * a.groups - 1) / (kPhiIlp * a.groups) + 63) / 64 * 64);
   hipLaunchKernelGGL(k_phi_cwalk, dim3((unsigned)(a.T * a.S * a.groups)), dim3(wthreads), phi_cwalk_lds(a.d, a.nw, 16),
                      s, a);

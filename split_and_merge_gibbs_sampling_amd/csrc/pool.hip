@@ -52,16 +52,116 @@ __global__ __launch_bounds__(256) void k_pool_accept(PoolAcceptArgs a) {
     if (p0 + k < a.count) y[k] = a.raw[p0 + k];
   const bool v0 = p0 + 1 < a.count, v1 = p0 + 2 < a.count;
   const double u0 = pool_unif(y[0]), u1 = pool_unif(y[1]), u2 = pool_unif(y[2]);
+  const bool pe = a.par_mask & 1, po = (a.par_mask >> 1) & 1;
   for (int c = 0; c < a.nclass; ++c) {
     const PoolClass C = a.cls[c];
-    const bool acc0 = v0 && pool_accept(C, u0, u1, tabs, tabs + 256);
-    const bool acc1 = v1 && pool_accept(C, u1, u2, tabs, tabs + 256);
+    const bool acc0 = pe && v0 && pool_accept(C, u0, u1, tabs, tabs + 256);
+    const bool acc1 = po && v1 && pool_accept(C, u1, u2, tabs, tabs + 256);
     const uint64_t b0 = __ballot(acc0), b1 = __ballot(acc1);
     if (lane == 0) {
-      a.bm[((int64_t)c * 2 + 0) * a.nwords + wv] = b0;
-      a.bm[((int64_t)c * 2 + 1) * a.nwords + wv] = b1;
+      if (pe) a.bm[((int64_t)c * 2 + 0) * a.nwords + wv] = b0;
+      if (po) a.bm[((int64_t)c * 2 + 1) * a.nwords + wv] = b1;
     }
   }
+}
+
+// Position after the len-th accepted attempt at the parity of pos, from pos (B: that parity's
+// table), by one wave 64 words at a time; -1 past the tables (pool_select_run).
+__device__ __forceinline__ int64_t wave_select_run(const uint64_t* B, int64_t nwords, int64_t pos, int len) {
+  const int lane = threadIdx.x & 63;
+  const int par = (int)(pos & 1);
+  const int64_t slot = pos >> 1;
+  int64_t w = slot >> 6;
+  uint64_t fmask = ~0ull << (slot & 63);
+  int need = len;
+  for (;;) {
+    if (w >= nwords) return -1;
+    const int64_t wi = w + lane;
+    uint64_t word = wi < nwords ? B[wi] : 0ull;
+    if (lane == 0) word &= fmask;
+    const int cnt = __popcll(word);
+    const int incl = wave_incl_scan(cnt);
+    const int total = __shfl(incl, 63);
+    if (total >= need) {
+      const uint64_t reach = __ballot(incl >= need);
+      const int q = __ffsll((unsigned long long)reach) - 1;
+      const uint64_t wq = __shfl(word, q);
+      const int before = __shfl(incl - cnt, q);
+      return 2 * ((w + q) * 64 + pool_select64(wq, need - before - 1)) + par + 2;
+    }
+    need -= total;
+    w += 64;
+    fmask = ~0ull;
+  }
+}
+
+// One wave per chunk (pool_gen.hpp PoolWalkArgs): the starts of its C entries from a guess,
+// and of the next M entries into ext.
+__global__ __launch_bounds__(256) void k_pool_walk(PoolWalkArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t e0 = g * a.C;
+  if (e0 > a.P) return;
+  int64_t pos = 0;
+  if (g > 0) {
+    pos = (int64_t)((double)e0 * a.mu);
+    pos = (pos & ~(int64_t)1) | ((e0 * a.d) & 1);
+    if (pos >= a.count) pos = (a.count - 2) | ((e0 * a.d) & 1);
+    if (pos < 0) pos = (e0 * a.d) & 1;
+  }
+  for (int k = 0; k < a.C + a.M; ++k) {
+    const int64_t e = e0 + k;
+    if (e > a.P) break;
+    if (lane == 0) {
+      if (k < a.C) a.starts[e] = pos;
+      else a.ext[g * a.M + (k - a.C)] = pos;
+    }
+    if (e == a.P || k + 1 == a.C + a.M) break;
+    pos += a.d;
+    for (int r = 0; r < a.nruns; ++r) {
+      pos = wave_select_run(a.bm + ((int64_t)a.run_cls[r] * 2 + (pos & 1)) * a.nwords, a.nwords, pos, a.run_len[r]);
+      if (pos < 0) {
+        // a guess past the true chain may run off the tables (only chunk 0's walk must not):
+        // its remaining entries are marked, never taken for a meeting point
+        if (lane == 0) {
+          if (g == 0) atomicOr(a.err, 8);
+          for (int k2 = k + 1; k2 < a.C + a.M && e0 + k2 <= a.P; ++k2) {
+            if (k2 < a.C) a.starts[e0 + k2] = -1;
+            else a.ext[g * a.M + (k2 - a.C)] = -1;
+          }
+        }
+        return;
+      }
+    }
+  }
+}
+
+// One wave per chunk g >= 1: the first entry where its walk meets chunk g - 1's overlap; the
+// entries before it take the overlap's starts.
+__global__ __launch_bounds__(256) void k_pool_merge(PoolWalkArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t g = 1 + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t e0 = g * a.C;
+  if (e0 > a.P) return;
+  const int lim = (int)min((int64_t)a.M, a.P - e0 + 1);
+  const int64_t* prev = a.ext + (g - 1) * a.M;
+  int meet = -1;
+  for (int k0 = 0; k0 < lim && meet < 0; k0 += 64) {
+    const int k = k0 + lane;
+    const bool eq = k < lim && prev[k] >= 0 && prev[k] == a.starts[e0 + k];
+    const uint64_t b = __ballot(eq);
+    if (b) meet = k0 + __ffsll((unsigned long long)b) - 1;
+  }
+  if (meet < 0) {
+    // the overlap reaches entry P: it holds every start of this chunk
+    if (lim == a.P - e0 + 1) {
+      meet = lim;
+    } else {
+      if (lane == 0) atomicOr(a.err, 4);
+      return;
+    }
+  }
+  for (int k = lane; k < meet; k += 64) a.starts[e0 + k] = prev[k];
 }
 
 // dynamic LDS: 512 table words, then per wave d doubles of sigma and 2d of tables
@@ -314,6 +414,14 @@ hipError_t launch_pool_heads(const double* tab, const uint64_t* bnd, int64_t P, 
 hipError_t launch_pool_accept(const PoolAcceptArgs& a, hipStream_t s) {
   const int64_t blocks = (a.nwords + 3) / 4;
   hipLaunchKernelGGL(k_pool_accept, dim3((unsigned)blocks), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_pool_walk(const PoolWalkArgs& a, hipStream_t s) {
+  if (a.C < 1 || a.M < 1 || a.M > a.C) return hipErrorInvalidValue;
+  const int64_t chunks = a.P / a.C + 1;              // chunk g covers entries g C .. g C + C - 1 (and P)
+  hipLaunchKernelGGL(k_pool_walk, dim3((unsigned)((chunks + 3) / 4)), dim3(256), 0, s, a);
+  if (chunks > 1) hipLaunchKernelGGL(k_pool_merge, dim3((unsigned)((chunks - 1 + 3) / 4)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -187,6 +187,35 @@ struct PoolAcceptArgs {
   uint64_t* bm;            // [nclass][2][nwords]
   int64_t nwords;          // ceil(count / 128)
   const uint64_t* gtab;    // kGlibcExpTab then kGlibcLogTab (512 words)
+  int par_mask;            // bit p: the parity-p tables are read (d even: entries and runs all start even)
+};
+
+// The entry starts in parallel (k_pool_walk, k_pool_merge).  Entry e + 1 starts where the
+// walk of entry e from its start ends, a deterministic function of the start.  Chunk g of C
+// entries is walked by one wave from a guess of its start (e_g times the mean entry length,
+// at the parity every start of e_g has: (e_g d) mod 2) through the first M entries of chunk
+// g + 1.  Walks from different starts coalesce: the run starts of two walks map to the same
+// accepted attempt unless an accepted attempt lies between them, so about one in eight pairs
+// of neighbouring walks merges per entry and the walk from a guess meets the true one within
+// ~100 entries.  Once two walks share an entry start they agree from there on, so chunk g + 1
+// is right from the first entry where its positions equal chunk g's overlap -- by induction
+// from chunk 0, which starts at 0 -- and the entries before it take chunk g's.  A chunk whose
+// walk has not met its predecessor's within M entries is reported (err bit 2) and the host
+// parses serially.
+struct PoolWalkArgs {
+  const uint64_t* bm;
+  int64_t nwords;
+  int d;
+  int nruns;
+  const int* run_cls;
+  const int* run_len;
+  int64_t P;
+  int C, M;                // entries per chunk, overlap (M <= C)
+  double mu;               // mean entry length (the chunk starts' guesses)
+  int64_t count;
+  int64_t* starts;         // [P + 1]
+  int64_t* ext;            // [chunks][M] chunk g's walk through entries e_g + C .. e_g + C + M - 1
+  int* err;                // bit 2: a chunk did not meet its predecessor; bit 3: the tables ended
 };
 
 struct PoolValueArgs {
@@ -212,6 +241,7 @@ struct PoolValueArgs {
 
 hipError_t launch_pool_accept(const PoolAcceptArgs& a, hipStream_t s);
 hipError_t launch_pool_values(const PoolValueArgs& a, hipStream_t s);
+hipError_t launch_pool_walk(const PoolWalkArgs& a, hipStream_t s);
 #endif
 
 }  // namespace hdpm

@@ -148,16 +148,26 @@ def test_speculative_update_phi(hd, oracle):
 # update_phi on the device (csrc/phi.hip): centers, sigmas, tables and the stream position
 # after it against the oracle, on shapes with one and several attribute classes, binary and
 # many-level attributes, wide rows; and that the device path ran (no silent host fallback).
+# walks: debug bit 27 (the per-start-drift walks, k_phi_cwalk, instead of the composition trees)
+@pytest.mark.parametrize("walks", [False, True])
 @pytest.mark.parametrize("shape", ["c5_like", "mixed", "binary", "wide", "zoo"])
-def test_device_update_phi(hd, oracle, zoo, shape):
+def test_device_update_phi(hd, oracle, zoo, shape, walks):
     if shape == "zoo":
         ds, K = zoo, 7
     else:
         ds, K = {"c5_like": (synth(8000, 128, 12, 4, seed=5), 12), "mixed": (synth(5000, 48, 9, (2, 6), seed=6), 9),
                  "binary": (synth(6000, 32, 8, 2, seed=7), 8), "wide": (synth(2500, 784, 6, 6, seed=8), 6)}[shape]
     cen, sig = random_params(ds, K, 13)
-    stats = sweep_case(hd, oracle, ds, ds.truth, cen, sig, ds.n * 3, seed=43, sweeps=4, phi=True, phi_device=True)
+    stats = sweep_case(hd, oracle, ds, ds.truth, cen, sig, ds.n * 3, seed=43, sweeps=4, phi=True, phi_device=True,
+                       debug=134217728 if walks else 0)
     assert stats["phi_device_calls"] >= 2, stats
+    if walks:
+        assert stats["phi_tree_calls"] == 0, stats
+    elif shape != "wide":
+        # d <= 128: the composition trees resolve the drifts, a cluster with a pick that
+        # depends on the uniform by the walks inside the same update (no re-run)
+        assert stats["phi_tree_calls"] >= 2 and stats["phi_tree_retries"] == 0, \
+            {k: v for k, v in stats.items() if "phi" in k}
 
 
 def test_device_update_phi_small_clusters_fall_back_or_match(hd, oracle, zoo):
@@ -524,7 +534,9 @@ def test_device_pool_matches_oracle_zoo(hd, oracle, zoo, pre):
     assert st["pool_device_calls"] == 1
 
 
-@pytest.mark.parametrize("case", ["mixed_levels", "odd_d_bc", "c5_like", "host_forced"])
+# c5_large: 200k entries (391 chunks of the parallel walk, k_pool_walk); serial_parse: debug
+# bit 28, the entry starts by the sequential host walk over the device's acceptance tables
+@pytest.mark.parametrize("case", ["mixed_levels", "odd_d_bc", "c5_like", "c5_large", "serial_parse", "host_forced"])
 def test_device_pool_matches_oracle_synthetic(hd, oracle, case):
     if case == "mixed_levels":
         ds = synth(2000, 64, 5, (2, 6), seed=3)
@@ -537,8 +549,14 @@ def test_device_pool_matches_oracle_synthetic(hd, oracle, case):
     else:
         ds = synth(3000, 128, 6, 4, seed=5)
         v, w, P = np.full(128, 6.0), np.full(128, 0.25), 30000   # ~14M draws: multi-workgroup slice
-    st = _pool_case(hd, oracle, ds, v, w, P, 77, 9, debug=64 if case == "host_forced" else 0)
+        if case == "c5_large":
+            P = 200_000
+    debug = {"host_forced": 64, "serial_parse": 268435456}.get(case, 0)
+    st = _pool_case(hd, oracle, ds, v, w, P, 77, 9, debug=debug)
     assert st["pool_device_calls"] == (0 if case == "host_forced" else 1)
+    if case != "host_forced":
+        # the parallel walk's chunks met (no serial fallback) unless the serial walk was forced
+        assert st["pool_walk_fallbacks"] == (1 if case == "serial_parse" else 0), st
 
 
 def test_device_pool_then_sweeps_match_oracle(hd, oracle):
