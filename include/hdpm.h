@@ -83,6 +83,9 @@ typedef struct {
     /* device pool generations whose entry starts fell back to the sequential host walk (a
      * chunk of the parallel walk did not meet its predecessor, or debug bit 28) */
     int64_t pool_walk_fallbacks;
+    /* update_phi speculated on the device beside the sweep (phi_mode device): launched, and
+     * committed as the iteration's update (the sweep moved no point) */
+    int64_t phi_dspec_launched, phi_dspec_used;
 } hdpm_stats;
 
 int         hdpm_device_count(void);

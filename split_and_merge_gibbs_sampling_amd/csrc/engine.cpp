@@ -639,6 +639,7 @@ struct Ctx {
   hipStream_t stream = nullptr;
   hipStream_t gstream = nullptr;   // random-stream generator
   hipStream_t cstream = nullptr;   // copies of stream states to the host (never queued behind a generator launch)
+  hipStream_t pstream = nullptr;   // update_phi speculated on the device beside the sweep (dspec)
   // update_phi's slice of the stream copied from the window that holds it (StreamAhead::fill_raw)
   struct PhiDev {
     bool valid = false;
@@ -758,7 +759,8 @@ struct Ctx {
     PinBuf<uint32_t> h_init, h_tail;
     DevBuf<uint64_t> bm;
     PinBuf<uint64_t> h_bm;
-    DevBuf<int64_t> starts, ext;
+    DevBuf<int64_t> starts, walk, a, delta;
+    DevBuf<int> rel;
     PinBuf<int64_t> h_starts;
     int64_t walk_fallbacks = 0;       // chunks that did not meet: serial host parse
     DevBuf<PoolClass> cls;
@@ -799,6 +801,7 @@ struct Ctx {
     bool round_ok = false;             // round 0 was enqueued
     int par = 0, buf = -1, m = 0;
     bool track = false;
+    bool dev = false;                  // its tables come from the device speculation (phd.stage)
     uint64_t gen[2] = {0, 0};          // window launches the kernels waited for
     std::chrono::steady_clock::time_point t_enq;   // the wait kernel was queued (pipe_go's deadline)
   } pre;
@@ -819,7 +822,8 @@ struct Ctx {
   int stage_hold = -1;                  // filled by the speculative update_phi, not yet committed
   // the new tables of a full update_phi, committed after the next speculative update_phi is
   // started (flush_commit): buffer, entries
-  struct { bool active = false; int buf = 0, nent = 0; } commit_later;
+  // (dev: the speculative device update's tables, phd.stage)
+  struct { bool active = false, dev = false; int buf = 0, nent = 0; } commit_later;
   DevBuf<uint8_t> d_stage;
 
   // statistics buffers.  d_freq holds freq[slot][j][level] and, while freq_dev_valid,
@@ -905,6 +909,12 @@ struct Ctx {
         }
       std::fprintf(stderr, "%s (%lld iterations, %lld device allocations after the first)\n", line.c_str(),
                    (long long)trace_iters, (long long)(g_dev_allocs.load() - trace_alloc0));
+    }
+    if (pstream) {
+      (void)hipStreamSynchronize(pstream);
+      if (dspec.ev) (void)hipEventDestroy(dspec.ev);
+      if (ev_phd_free) (void)hipEventDestroy(ev_phd_free);
+      (void)hipStreamDestroy(pstream);
     }
     if (cstream) {
       (void)hipStreamSynchronize(cstream);
@@ -1414,6 +1424,11 @@ struct Ctx {
   void flush_commit() {
     if (!commit_later.active) return;
     commit_later.active = false;
+    if (commit_later.dev) {
+      commit_later.dev = false;
+      scatter_dev_stage(commit_later.nent);
+      return;
+    }
     stage_fill = commit_later.buf;
     stage_commit(upload_layout(commit_later.nent, dp, d, bw), commit_later.nent, true);
   }
@@ -1793,16 +1808,20 @@ struct Ctx {
       HIPCHK(launch_pool_accept(aa, stream));
       HIPCHK(hipStreamSynchronize(stream));
       auto t1 = clk::now();
-      // entry starts: chunks walked in parallel from guesses, joined where they meet
-      // (k_pool_walk / k_pool_merge); the serial host parse when a chunk does not meet
+      // entry starts: chunks walked in parallel from guesses, placed where they meet the walk
+      // before them (k_pool_walk / k_pool_meet / k_pool_scan / k_pool_place, pool_gen.hpp);
+      // the serial host parse when a chunk does not meet its predecessor
       const int C = 512, M = 512;
       const int64_t chunks = P_ / C + 1;
       pg.starts.ensure(P_ + 1);
-      pg.ext.ensure((size_t)chunks * M);
+      pg.walk.ensure((size_t)chunks * (C + M));
+      pg.rel.ensure(chunks);
+      pg.a.ensure(chunks + 1);
+      pg.delta.ensure(chunks);
       pg.h_starts.ensure(P_ + 1);
       HIPCHK(hipMemsetAsync(pg.err.p, 0, 4, stream));
       PoolWalkArgs wa{pg.bm.p, nwords, d, (int)pl.run_cls.size(), pg.runs.p, pg.runs.p + pl.run_cls.size(), P_, C, M,
-                      pl.mean_len, count, pg.starts.p, pg.ext.p, pg.err.p};
+                      pl.mean_len, count, chunks, pg.walk.p, pg.rel.p, pg.a.p, pg.delta.p, pg.starts.p, pg.err.p};
       HIPCHK(launch_pool_walk(wa, stream));
       HIPCHK(hipMemcpyAsync(pg.h_err.p, pg.err.p, 4, hipMemcpyDeviceToHost, stream));
       HIPCHK(hipMemcpyAsync(&pg.h_starts.p[P_], pg.starts.p + P_, 8, hipMemcpyDeviceToHost, stream));
@@ -2142,6 +2161,10 @@ struct Ctx {
       mark("ahead.spec");
     }
     flush_commit();                       // this iteration's tables, before the sweep that reads them
+    if (!host_spec()) {
+      dspec_launch();                     // after the scatter of this iteration's tables (ev_phd_free)
+      mark("ahead.dspec");
+    }
     if (resolve_smem_bytes(std::min(scap, K + 2), m, K + m <= 64 ? 1 : 0) <= 160 * 1024) {
       par ^= 1;                           // the prepared sweep's control block
       ahead.par = par;
@@ -2177,6 +2200,7 @@ struct Ctx {
       if (!spec.joined && pj_open) (void)pj_finish();
       spec.ran = false;
     }
+    dspec.ran = false;                   // (its device work completes unused)
     phi_stream.n = 0;
     pend.active = false;
     rng = ahead.saved;
@@ -2199,7 +2223,9 @@ struct Ctx {
     h_pipe.p[q].raw = nullptr;
     // the next sweep's draws start after this update's (about a slice): the windows that
     // overlap that stretch (not a window generation started for later sweeps)
-    const uint64_t lo = spec.pos, hi = spec.pos + (uint64_t)(2 * phi_prefetch) + (uint64_t)n * (m + 1);
+    const bool dev = !host_spec();
+    const uint64_t lo = dev ? dspec.pos : spec.pos;
+    const uint64_t hi = lo + (uint64_t)(dev ? dspec.pl.need : 2 * phi_prefetch) + (uint64_t)n * (m + 1);
     int whole = -1;                      // the earliest window holding all of it
     for (int k = 0; k < 2; ++k) {
       const RngWindow& w = win[k];
@@ -2220,15 +2246,24 @@ struct Ctx {
     pre.t_enq = std::chrono::steady_clock::now();   // the kernel's clock starts no earlier
     pre.active = true;
     pre.par = q;
-    pre.buf = spec.stage_buf;
+    pre.dev = dev;
+    pre.buf = dev ? -1 : spec.stage_buf;
     pre.m = m;
     pre.track = track;
     pre.round_ok = false;
-    // the scatter reads the staging buffer in host memory directly (no copy-engine hops
-    // between the wait kernel and the sweep)
-    HIPCHK(launch_scatter_clusters(h_stage_buf[pre.buf].p, K, dp, d, bw, 1, d_slot_codes.p, d_slot_tab.p, d_slot_bnd.p,
-                                   d_counts.p, d_sol.p, d_los.p, d_src.p, stream, &d_pipe.p[q].gate));
-    HIPCHK(hipEventRecord(ev_stage_buf[pre.buf], stream));
+    if (dev) {
+      // the speculative device update's tables (phd.stage), once it is done
+      HIPCHK(hipStreamWaitEvent(stream, dspec.ev, 0));
+      HIPCHK(launch_scatter_clusters(phd.stage.p, K, dp, d, bw, 1, d_slot_codes.p, d_slot_tab.p, d_slot_bnd.p,
+                                     d_counts.p, d_sol.p, d_los.p, d_src.p, stream, &d_pipe.p[q].gate));
+      phd_release(stream);
+    } else {
+      // the scatter reads the staging buffer in host memory directly (no copy-engine hops
+      // between the wait kernel and the sweep)
+      HIPCHK(launch_scatter_clusters(h_stage_buf[pre.buf].p, K, dp, d, bw, 1, d_slot_codes.p, d_slot_tab.p,
+                                     d_slot_bnd.p, d_counts.p, d_sol.p, d_los.p, d_src.p, stream, &d_pipe.p[q].gate));
+      HIPCHK(hipEventRecord(ev_stage_buf[pre.buf], stream));
+    }
     pre.round_ok = launch_round(0, K, m, nullptr, track, kRoundAll, &d_pipe.p[q], q) == kOk;
     stats.pipe_enqueued++;
   }
@@ -2241,8 +2276,10 @@ struct Ctx {
   // update's held staging buffer) become the committed ones, the next speculative update
   // started.  False (nothing done) when it cannot run.
   bool pipe_go(int m) {
-    if (!pre.active || !pre.round_ok || pre.m != m || !commit_later.active || commit_later.buf != pre.buf ||
-        last_sweep_rounds != 1 || last_sweep_moves != 0 || !host_spec() || tables_dirty)
+    if (!pre.active || !pre.round_ok || pre.m != m || !commit_later.active || last_sweep_rounds != 1 ||
+        last_sweep_moves != 0 || tables_dirty)
+      return false;
+    if (pre.dev ? (!commit_later.dev || !dspec_on()) : (commit_later.dev || commit_later.buf != pre.buf || !host_spec()))
       return false;
     if (!(freq_dev_valid && freq_version == labels_version)) return false;
     // the wait kernel gives up after pipe_limit_ticks: a go late enough to race its limit
@@ -2285,10 +2322,16 @@ struct Ctx {
     stats.pipe_runs++;
     // the tables of this iteration: copied and scattered by the enqueued kernels
     commit_later.active = false;
-    stage_last = pre.buf;
-    stage_full = true;
-    if (stage_hold == pre.buf) stage_hold = -1;
-    spec_launch();
+    if (pre.dev) {
+      commit_later.dev = false;
+      stage_full = false;
+      dspec_launch();                  // waits for the enqueued scatter (ev_phd_free)
+    } else {
+      stage_last = pre.buf;
+      stage_full = true;
+      if (stage_hold == pre.buf) stage_hold = -1;
+      spec_launch();
+    }
     mark("ahead.spec");
     return true;
   }
@@ -2321,7 +2364,12 @@ struct Ctx {
     const bool spec_go = freq_dev_valid && freq_version == labels_version && !(debug & 128) && !recount_only() &&
                          host_spec();
     const bool freq_before_ok = freq_version == labels_version && !recount_only();
-    if (!use_ahead) spec.ran = false;
+    // or on the device beside the sweep (phi_mode 1)
+    const bool dspec_go = freq_dev_valid && freq_version == labels_version && !recount_only() && dspec_on();
+    if (!use_ahead) {
+      spec.ran = false;
+      dspec.ran = false;
+    }
     spec.lv = 0;
     labels_version++;
     const int K0 = K;
@@ -2352,6 +2400,7 @@ struct Ctx {
       }
     } spec_guard{this};
     if (spec_go && !use_ahead) spec_launch();
+    else if (dspec_go && !use_ahead) dspec_launch();
     stats.t_rng_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count();
 
     int nslots = K;
@@ -2371,12 +2420,13 @@ struct Ctx {
       mark("launched");
       if (stats.rounds == rounds0) {   // hidden behind the device work
         // (not while sweeps keep moving points: the enqueued sweep would be dropped)
-        if (deep_ok && spec.ran && spec.K == K && track && last_sweep_moves == 0 && !(debug & 4194304)) {
+        if (deep_ok && (host_spec() ? (spec.ran && spec.K == K) : (dspec.ran && dspec.K == K)) && track &&
+            last_sweep_moves == 0 && !(debug & 4194304)) {
           pre_enqueue(m, track);
           mark("pre");
         }
         if (spec.ran) spec_join();
-        else prefill_phi_stream();
+        else if (host_spec()) prefill_phi_stream();
       }
       mark("prefill");
       HIPCHK(hipEventSynchronize(ev_res[par]));
@@ -2405,8 +2455,12 @@ struct Ctx {
         // this iteration (the held staging buffer) were not scattered and round 0's
         // k_cluster_summary did not clear the move count.  Commit the tables and run the
         // sweep ungated from point 0 with the same draws.
-        stage_fill = stage_last;
-        stage_commit(upload_layout(K, dp, d, bw), K, true);
+        if (pre.dev || stage_last < 0 || !stage_full) {
+          upload_clusters();               // from the host's parameters (the device update's)
+        } else {
+          stage_fill = stage_last;
+          stage_commit(upload_layout(K, dp, d, bw), K, true);
+        }
         if (track) mcount_clear = true;
         stats.pipe_recovered++;
         continue;
@@ -2495,6 +2549,10 @@ struct Ctx {
     if (fetched && pool_on_device) HIPCHK(hipStreamSynchronize(stream));
     host_c_valid = false;
     tables_dirty = true;
+    if (dspec.ran) {
+      dspec.lv = labels_version;
+      dspec.moves = sweep_moves;
+    }
     if (spec.ran) {
       // leading labels with the same slot (hence parameters) and count as at the speculation
       spec.lv = labels_version;
@@ -3316,6 +3374,7 @@ struct Ctx {
     const PhiPlan pl = phi_plan(T);
     if (!pl.ok) return -1;
     const int64_t items = pl.items, need = pl.need;
+    dspec_wait();                                         // a speculation's use of phd is over
     RngWindow* W = window_at(rng.pos, need);
     if (!W) return -1;
     PhiArgs a = phi_args(pl);
@@ -3413,6 +3472,7 @@ struct Ctx {
                    T, pl.nw, pl.Wc, status, (long long)cons, (long long)dts[0], F[0], valid0, pl.rate, pl.sdev);
     }
     if (status != kPhiOk || cons <= 0 || !can_adopt(*W, target)) {
+      phd_release(stream);
       phd.fallbacks++;
       stats.phi_device_fallbacks++;
       if (status == kPhiOk) stats.phi_device_last_status = -1;
@@ -3422,6 +3482,7 @@ struct Ctx {
     // commit: tables on the device, parameters on the host, the stream past the draws
     HIPCHK(launch_scatter_clusters(phd.stage.p, T, dp, d, bw, full ? 1 : 0, d_slot_codes.p, d_slot_tab.p, d_slot_bnd.p,
                                    d_counts.p, d_sol.p, d_los.p, d_src.p, stream));
+    phd_release(stream);
     const uint8_t* pk = phd.h_out.p + o_pick;
     const double* sg = (const double*)(phd.h_out.p + o_sig);
     const double* ll = (const double*)(phd.h_out.p + o_ll);
@@ -3451,6 +3512,185 @@ struct Ctx {
     return kOk;
   }
 
+  // ------------------------------------------------------------------ update_phi speculated on the device
+  // phi_mode 1: the update of the pre-sweep state (every label with its count, frequency
+  // table and sigmas) is launched on pstream beside the sweep, at the stream position after the
+  // sweep's draws (a sweep consumes exactly N (m + 1) uniforms) -- the device counterpart of
+  // spec_launch.  A sweep that moves no point leaves all of its inputs as they were, so the
+  // speculation is then update_phi itself (dspec_commit); after a sweep with moves it is dropped
+  // and update_phi runs on the sweep's result.  phd's buffers are shared with device_update_phi:
+  // every device use of them on the sweep's stream records ev_phd_free, which the next
+  // speculation waits for, and device_update_phi waits for the speculation (dspec.ev).
+  struct DevSpec {
+    bool ran = false;                  // launched for the sweep whose draws end at pos
+    bool inflight = false;             // launched and not yet waited for on the host
+    uint64_t pos = 0, epoch = 0, lv = 0;
+    int K = 0;
+    int moves = -1;                    // the sweep's moves (set at its end)
+    PhiPlan pl;
+    RngWindow* W = nullptr;
+    bool tree = false;
+    size_t o_pick = 0, o_sig = 0, o_ll = 0;
+    hipEvent_t ev = nullptr;           // its outputs are in phd.h_out
+  } dspec;
+  hipEvent_t ev_phd_free = nullptr;    // the last device use of phd's buffers on `stream` is done
+  bool dspec_on() const { return phi_mode == 1 && !(debug & (524288 | 64 | 128)); }
+  void phd_release(hipStream_t s) {
+    if (!ev_phd_free) HIPCHK(hipEventCreateWithFlags(&ev_phd_free, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(ev_phd_free, s));
+  }
+  void dspec_wait() {
+    if (!dspec.inflight) return;
+    HIPCHK(hipEventSynchronize(dspec.ev));
+    dspec.inflight = false;
+  }
+  // outputs of a device update of T clusters in phd.h_out: status + consumption, picks, sigmas,
+  // log-likelihood pairs
+  static void phi_out_layout(int T, int d_, size_t* o_pick, size_t* o_sig, size_t* o_ll, size_t* bytes) {
+    const size_t items = (size_t)T * d_;
+    *o_pick = 16;
+    *o_sig = align16(*o_pick + items);
+    *o_ll = *o_sig + items * 8;
+    *bytes = *o_ll + (size_t)2 * T * 8;
+  }
+
+  void dspec_launch() {
+    dspec.ran = false;
+    if (!dspec_on() || K <= 0 || d > 2048 || !glibc_selfcheck()) return;
+    int min_count = INT_MAX;
+    for (int k = 0; k < K; ++k) {
+      if (h_counts[k] <= 0) return;
+      min_count = std::min(min_count, h_counts[k]);
+    }
+    const PhiPlan pl = phi_plan(K);
+    if (!pl.ok) return;
+    RngWindow* W = window_at(rng.pos, pl.need);
+    if (!W) return;
+    dspec_wait();                      // phd.h_in / h_out are free on the host
+    PhiArgs a = phi_args(pl);
+    const int T = K;
+    const int64_t items = pl.items;
+    const size_t in_bytes = (size_t)2 * T * 4 + (size_t)items * 8;
+    phd.h_in.ensure(in_bytes + 64);
+    int* hl = (int*)phd.h_in.p;
+    double* hs = (double*)(phd.h_in.p + align16((size_t)2 * T * 4));
+    for (int t = 0; t < T; ++t) {
+      hl[t] = t;
+      hl[T + t] = h_counts[t];
+    }
+    std::memcpy(hs, h_sigma.data(), (size_t)items * 8);
+    phd.lab_cnt.ensure(2 * T);
+    phd.sig_in.ensure(items);
+    phd.sig_out.ensure(items);
+    phd.ll.ensure(2 * T);
+    phd.pick.ensure(items);
+    phd.status.ensure(4);
+    phd.stage.ensure(upload_layout(T, dp, d, bw).bytes);
+    size_t bytes;
+    phi_out_layout(T, d, &dspec.o_pick, &dspec.o_sig, &dspec.o_ll, &bytes);
+    phd.h_out.ensure(bytes);
+    if (!dspec.ev) HIPCHK(hipEventCreateWithFlags(&dspec.ev, hipEventDisableTiming));
+    HIPCHK(hipStreamWaitEvent(pstream, W->done, 0));
+    if (ev_phd_free) HIPCHK(hipStreamWaitEvent(pstream, ev_phd_free, 0));
+    HIPCHK(hipMemcpyAsync(phd.lab_cnt.p, hl, (size_t)2 * T * 4, hipMemcpyHostToDevice, pstream));
+    HIPCHK(hipMemcpyAsync(phd.sig_in.p, hs, (size_t)items * 8, hipMemcpyHostToDevice, pstream));
+    a.lab = phd.lab_cnt.p; a.cnt = phd.lab_cnt.p + T; a.freq = d_freq.p; a.sig_in = phd.sig_in.p;
+    a.raw = W->raw.p + (rng.pos - W->start_pos);
+    a.nraw = (int64_t)(W->start_pos + (uint64_t)W->count - rng.pos);
+    a.pick = phd.pick.p; a.status = phd.status.p;
+    a.stage = phd.stage.p; a.sig_out = phd.sig_out.p; a.ll = phd.ll.p;
+    const bool tree = pl.tree_ok && (pl.S == 1 || min_count >= phd.tree_min_count) && !(debug & 134217728);
+    a.tree = tree ? phd.tree.p : nullptr;
+    if (tree) HIPCHK(hipMemsetAsync(phd.tnd.p, 0, (size_t)T * 4, pstream));
+    HIPCHK(hipMemsetAsync(phd.status.p, 0, 16, pstream));
+    HIPCHK(hipMemsetAsync(phd.act.p, 0, 4, pstream));
+    HIPCHK(launch_phi(a, pstream));
+    HIPCHK(hipMemcpyAsync(phd.h_out.p, phd.status.p, 16, hipMemcpyDeviceToHost, pstream));
+    HIPCHK(hipMemcpyAsync(phd.h_out.p + dspec.o_pick, phd.pick.p, (size_t)items, hipMemcpyDeviceToHost, pstream));
+    HIPCHK(hipMemcpyAsync(phd.h_out.p + dspec.o_sig, phd.sig_out.p, (size_t)items * 8, hipMemcpyDeviceToHost, pstream));
+    HIPCHK(hipMemcpyAsync(phd.h_out.p + dspec.o_ll, phd.ll.p, (size_t)2 * T * 8, hipMemcpyDeviceToHost, pstream));
+    HIPCHK(hipEventRecord(dspec.ev, pstream));
+    dspec.ran = true;
+    dspec.inflight = true;
+    dspec.pos = rng.pos;
+    dspec.epoch = rng.epoch;
+    dspec.lv = 0;
+    dspec.K = K;
+    dspec.moves = -1;
+    dspec.pl = pl;
+    dspec.W = W;
+    dspec.tree = tree;
+    stats.phi_dspec_launched++;
+  }
+
+  // The tables of the committed speculation, from phd.stage into the slots (full upload).
+  void scatter_dev_stage(int T) {
+    HIPCHK(hipStreamWaitEvent(stream, dspec.ev, 0));
+    HIPCHK(launch_scatter_clusters(phd.stage.p, T, dp, d, bw, 1, d_slot_codes.p, d_slot_tab.p, d_slot_bnd.p, d_counts.p,
+                                   d_sol.p, d_los.p, d_src.p, stream));
+    phd_release(stream);
+  }
+
+  // update_phi from the speculation (after a sweep without moves): kOk, or -1 when it did not
+  // complete on the device (the caller runs the update; nothing was changed).
+  int dspec_commit() {
+    dspec_wait();
+    dspec.ran = false;
+    phd.calls++;
+    if (dspec.tree) stats.phi_tree_calls++;
+    const int T = dspec.K;
+    const int status = ((const int*)phd.h_out.p)[0];
+    stats.phi_device_last_status = status;
+    int64_t cons = 0;
+    std::memcpy(&cons, phd.h_out.p + 8, 8);
+    const uint64_t target = rng.pos + (uint64_t)cons;
+    if (status == kPhiNonDet) {
+      int mc = INT_MAX;
+      for (int k = 0; k < T; ++k) mc = std::min(mc, h_counts[k]);
+      phd.tree_min_count = std::max(phd.tree_min_count, std::min(1 << 20, 2 * mc));
+    }
+    if (status != kPhiOk || cons <= 0 || !dspec.W || !can_adopt(*dspec.W, target) ||
+        !covers(*dspec.W, rng.pos, dspec.pl.need)) {
+      phd.fallbacks++;
+      stats.phi_device_fallbacks++;
+      return -1;
+    }
+    stats.phi_device_calls++;
+    stats.phi_dspec_used++;
+    // tables: by the sweep enqueued ahead (its gated scatter, pipe_go), flush_commit, or now
+    if (defer_commit) {
+      commit_later.active = true;
+      commit_later.dev = true;
+      commit_later.nent = T;
+    } else {
+      scatter_dev_stage(T);
+    }
+    const uint8_t* pk = phd.h_out.p + dspec.o_pick;
+    const double* sg = (const double*)(phd.h_out.p + dspec.o_sig);
+    const double* ll = (const double*)(phd.h_out.p + dspec.o_ll);
+    double hi = 0.0, lo = 0.0;
+    for (int t = 0; t < T; ++t) {
+      for (int j = 0; j < d; ++j) h_center[(size_t)t * d + j] = (uint8_t)(pk[(size_t)t * d + j] + 1);
+      for (int q = 0; q < 2; ++q) {
+        const double x = ll[2 * t + q], s2 = hi + x;
+        lo += std::fabs(hi) >= std::fabs(x) ? (hi - s2) + x : (x - s2) + hi;
+        hi = s2;
+      }
+    }
+    std::memcpy(h_sigma.data(), sg, (size_t)T * d * 8);
+    dev_ll = hi + lo;
+    dev_ll_version = labels_version;
+    tables_dirty = false;
+    stage_full = false;                // the host staging no longer mirrors the device tables
+    freq_next_pending = false;
+    freq_version = labels_version;
+    adopt_state_at(*dspec.W, target);
+    const double drift = (double)(cons - 3 * dspec.pl.items);
+    const double ph = drift / (drift + 2.0 * (double)dspec.pl.items);
+    phd.p_rej = std::min(0.3, std::max(0.05, 0.7 * phd.p_rej + 0.3 * ph));
+    return kOk;
+  }
+
   int update_phi(const int32_t* idx, int nidx) {
     if (!have_state) { err = "no state"; return kArg; }
     // the log-likelihood a full device update summed belongs to the parameters before this
@@ -3468,7 +3708,20 @@ struct Ctx {
                           spec.pos == rng.pos && spec.epoch == rng.epoch && sa.n > 0 && sa.start.pos == rng.pos &&
                           !(debug & 128);
     spec.ran = false;
-    if (pre.active && !(use_spec && spec.moves == 0 && K == spec.K && spec.nvalid == K)) pre_release();
+    // the device speculation of the sweep just done (dspec_launch)
+    const bool use_dspec = nidx == 0 && dspec.ran && dspec.lv == labels_version && dspec.moves == 0 &&
+                           dspec.pos == rng.pos && dspec.epoch == rng.epoch && K == dspec.K && dspec_on();
+    if (pre.active && !(use_spec && spec.moves == 0 && K == spec.K && spec.nvalid == K) && !use_dspec) pre_release();
+    if (use_dspec) {
+      mark("dspec_wait");
+      if (dspec_commit() == kOk) {
+        stats.t_host_phi_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0c).count();
+        mark("dspec");
+        return kOk;
+      }
+      if (pre.active) pre_release();
+    }
+    dspec.ran = false;
     if (!use_spec) {
       // the update on the device (csrc/phi.hip); -1: not applicable here, the host runs it
       const int st = device_update_phi(mask, nidx);
@@ -3566,6 +3819,7 @@ struct Ctx {
       if (K && defer_commit && spec_layout) {
         // committed by flush_commit, after the next speculative update_phi is started
         commit_later.active = true;
+        commit_later.dev = false;
         commit_later.buf = stage_fill;
         commit_later.nent = K;
         stage_hold = stage_fill;
@@ -3785,7 +4039,7 @@ int Ctx::iteration(const hdpm_chain_params* p, int iter, int* idx_1_sm, int* acc
     prepare_next_sweep(p->m, launch_next);
     prepared = true;
   }
-  if (prepared && ahead.active) phi_lookahead();
+  if (prepared && ahead.active && host_spec()) phi_lookahead();
   mark("ahead");
   if ((debug & 32) && trace.size() > 1) {
     if (trace_alloc0 < 0) trace_alloc0 = g_dev_allocs.load();
@@ -3912,6 +4166,11 @@ int hdpm_ctx_create(int32_t device, hdpm_ctx** out) {
     return HDPM_E_DEVICE;
   }
   if (hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return HDPM_E_DEVICE;
+  }
+  // the speculative device update_phi at the sweep's priority (it runs beside the sweep)
+  if (hipStreamCreateWithPriority(&c->pstream, hipStreamNonBlocking, prio_hi) != hipSuccess) {
     delete c;
     return HDPM_E_DEVICE;
   }

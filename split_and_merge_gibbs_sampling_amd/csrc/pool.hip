@@ -95,73 +95,149 @@ __device__ __forceinline__ int64_t wave_select_run(const uint64_t* B, int64_t nw
   }
 }
 
-// One wave per chunk (pool_gen.hpp PoolWalkArgs): the starts of its C entries from a guess,
-// and of the next M entries into ext.
+// One wave per chunk (pool_gen.hpp PoolWalkArgs): C + M entry starts from a guess.
 __global__ __launch_bounds__(256) void k_pool_walk(PoolWalkArgs a) {
   const int lane = threadIdx.x & 63;
   const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= a.chunks) return;
   const int64_t e0 = g * a.C;
-  if (e0 > a.P) return;
+  const int L = a.C + a.M;
+  int64_t* out = a.walk + g * L;
   int64_t pos = 0;
   if (g > 0) {
+    const int par = (int)((e0 * a.d) & 1);
     pos = (int64_t)((double)e0 * a.mu);
-    pos = (pos & ~(int64_t)1) | ((e0 * a.d) & 1);
-    if (pos >= a.count) pos = (a.count - 2) | ((e0 * a.d) & 1);
-    if (pos < 0) pos = (e0 * a.d) & 1;
+    if (pos > a.count - 2) pos = a.count - 2;
+    if (pos < 0) pos = 0;
+    pos = (pos & ~(int64_t)1) | par;
   }
-  for (int k = 0; k < a.C + a.M; ++k) {
-    const int64_t e = e0 + k;
-    if (e > a.P) break;
-    if (lane == 0) {
-      if (k < a.C) a.starts[e] = pos;
-      else a.ext[g * a.M + (k - a.C)] = pos;
-    }
-    if (e == a.P || k + 1 == a.C + a.M) break;
+  for (int k = 0; k < L; ++k) {
+    if (lane == 0) out[k] = pos;
+    if (k + 1 == L) break;
     pos += a.d;
-    for (int r = 0; r < a.nruns; ++r) {
+    for (int r = 0; r < a.nruns && pos >= 0; ++r)
       pos = wave_select_run(a.bm + ((int64_t)a.run_cls[r] * 2 + (pos & 1)) * a.nwords, a.nwords, pos, a.run_len[r]);
-      if (pos < 0) {
-        // a guess past the true chain may run off the tables (only chunk 0's walk must not):
-        // its remaining entries are marked, never taken for a meeting point
-        if (lane == 0) {
-          if (g == 0) atomicOr(a.err, 8);
-          for (int k2 = k + 1; k2 < a.C + a.M && e0 + k2 <= a.P; ++k2) {
-            if (k2 < a.C) a.starts[e0 + k2] = -1;
-            else a.ext[g * a.M + (k2 - a.C)] = -1;
-          }
-        }
-        return;
-      }
+    if (pos < 0) {
+      if (lane == 0)
+        for (int k2 = k + 1; k2 < L; ++k2) out[k2] = -1;
+      return;
     }
   }
 }
 
-// One wave per chunk g >= 1: the first entry where its walk meets chunk g - 1's overlap; the
-// entries before it take the overlap's starts.
-__global__ __launch_bounds__(256) void k_pool_merge(PoolWalkArgs a) {
+// One wave per chunk g >= 1: the first position of its walk found in chunk g - 1's walk (a
+// binary search per lane: both walks increase), hence rel[g] = k1 - k2 - C and the index k1 in
+// chunk g - 1's walk where chunk g's valid part starts.
+__global__ __launch_bounds__(256) void k_pool_meet(PoolWalkArgs a) {
   const int lane = threadIdx.x & 63;
   const int64_t g = 1 + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int64_t e0 = g * a.C;
-  if (e0 > a.P) return;
-  const int lim = (int)min((int64_t)a.M, a.P - e0 + 1);
-  const int64_t* prev = a.ext + (g - 1) * a.M;
-  int meet = -1;
-  for (int k0 = 0; k0 < lim && meet < 0; k0 += 64) {
-    const int k = k0 + lane;
-    const bool eq = k < lim && prev[k] >= 0 && prev[k] == a.starts[e0 + k];
-    const uint64_t b = __ballot(eq);
-    if (b) meet = k0 + __ffsll((unsigned long long)b) - 1;
-  }
-  if (meet < 0) {
-    // the overlap reaches entry P: it holds every start of this chunk
-    if (lim == a.P - e0 + 1) {
-      meet = lim;
-    } else {
-      if (lane == 0) atomicOr(a.err, 4);
+  if (g >= a.chunks) return;
+  const int L = a.C + a.M;
+  const int64_t* prev = a.walk + (g - 1) * L;
+  const int64_t* own = a.walk + g * L;
+  int nprev = L;                       // prev's positions before its -1 marks (near the tables' end)
+  while (nprev > 0 && prev[nprev - 1] < 0) --nprev;
+  for (int k0 = 0; k0 < L; k0 += 64) {
+    const int k2 = k0 + lane;
+    int k1 = -1;
+    if (k2 < L) {
+      const int64_t x = own[k2];
+      if (x >= 0) {
+        int lo = 0, hi = nprev;        // first index with prev[idx] >= x
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (prev[mid] < x) lo = mid + 1;
+          else hi = mid;
+        }
+        if (lo < nprev && prev[lo] == x) k1 = lo;
+      }
+    }
+    const uint64_t b = __ballot(k1 >= 0);
+    if (b) {
+      const int q = __ffsll((unsigned long long)b) - 1;
+      const int K1 = __shfl(k1, q), K2 = k0 + q;
+      if (lane == 0) {
+        a.rel[g] = K1 - K2 - a.C;
+        a.a[g] = K1;                   // made an entry index by k_pool_scan
+      }
       return;
     }
   }
-  for (int k = lane; k < meet; k += 64) a.starts[e0 + k] = prev[k];
+  if (lane == 0) {
+    a.rel[g] = 0;
+    a.a[g] = -1;
+    atomicOr(a.err, 4);
+  }
+}
+
+// One workgroup: delta_g = sum of rel over chunks 1..g; a_g = e_{g-1} + delta_{g-1} + k1_g, then
+// a running maximum (a walk that met its predecessor before that one met the true chain is
+// true only from where its predecessor is); a_0 = 0, a_chunks = P + 1.
+template <bool kMax>
+__device__ __forceinline__ long long block_scan(long long x, long long* carry, long long* wsum) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const long long t = __shfl_up(x, o);
+    if (lane >= o) x = kMax ? (t > x ? t : x) : x + t;
+  }
+  if (lane == 63) wsum[wid] = x;
+  __syncthreads();
+  long long before = *carry;
+  for (int w2 = 0; w2 < wid; ++w2) before = kMax ? (wsum[w2] > before ? wsum[w2] : before) : before + wsum[w2];
+  const long long r = kMax ? (x > before ? x : before) : before + x;
+  __syncthreads();
+  if (threadIdx.x == blockDim.x - 1) *carry = r;
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(1024) void k_pool_scan(PoolWalkArgs a) {
+  __shared__ long long carry;
+  __shared__ long long wsum[16];
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < a.chunks; base += blockDim.x) {
+    const int64_t g = base + threadIdx.x;
+    const long long dl = block_scan<false>((g >= 1 && g < a.chunks) ? (long long)a.rel[g] : 0, &carry, wsum);
+    if (g < a.chunks) a.delta[g] = dl;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < a.chunks; base += blockDim.x) {
+    const int64_t g = base + threadIdx.x;
+    long long v = 0;
+    if (g >= 1 && g < a.chunks) {
+      const long long k1 = a.a[g];
+      v = k1 >= 0 ? (long long)((g - 1) * a.C) + a.delta[g - 1] + k1 : 0;
+    }
+    const long long r = block_scan<true>(v, &carry, wsum);
+    if (g >= 1 && g < a.chunks && a.a[g] >= 0) a.a[g] = r;
+  }
+  if (threadIdx.x == 0) {
+    a.a[0] = 0;
+    a.a[a.chunks] = a.P + 1;
+  }
+}
+
+// One wave per chunk g: entries [a_g, a_{g+1}) from its walk (walk index e - g C - delta_g).
+__global__ __launch_bounds__(256) void k_pool_place(PoolWalkArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= a.chunks || (*a.err & 4)) return;
+  const int L = a.C + a.M;
+  const int64_t lo = a.a[g], hi = min(a.a[g + 1], a.P + 1);
+  const int64_t off = g * a.C + a.delta[g];          // the entry of walk index 0
+  const int64_t* w = a.walk + g * L;
+  if (lane == 0 && (lo < 0 || hi < lo)) atomicOr(a.err, 4);
+  for (int64_t e = max(lo, (int64_t)0) + lane; e < hi; e += 64) {
+    const int64_t k = e - off;
+    int64_t v = -1;
+    if (k >= 0 && k < L) v = w[k];
+    if (v < 0) atomicOr(a.err, (e == a.P && k >= 0 && k < L) ? 8 : 4);
+    a.starts[e] = v;
+  }
 }
 
 // dynamic LDS: 512 table words, then per wave d doubles of sigma and 2d of tables
@@ -418,10 +494,12 @@ hipError_t launch_pool_accept(const PoolAcceptArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_pool_walk(const PoolWalkArgs& a, hipStream_t s) {
-  if (a.C < 1 || a.M < 1 || a.M > a.C) return hipErrorInvalidValue;
-  const int64_t chunks = a.P / a.C + 1;              // chunk g covers entries g C .. g C + C - 1 (and P)
-  hipLaunchKernelGGL(k_pool_walk, dim3((unsigned)((chunks + 3) / 4)), dim3(256), 0, s, a);
-  if (chunks > 1) hipLaunchKernelGGL(k_pool_merge, dim3((unsigned)((chunks - 1 + 3) / 4)), dim3(256), 0, s, a);
+  if (a.C < 1 || a.M < 1 || a.chunks < 1) return hipErrorInvalidValue;
+  const unsigned blocks = (unsigned)((a.chunks + 3) / 4);
+  hipLaunchKernelGGL(k_pool_walk, dim3(blocks), dim3(256), 0, s, a);
+  if (a.chunks > 1) hipLaunchKernelGGL(k_pool_meet, dim3((unsigned)((a.chunks - 1 + 3) / 4)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_pool_scan, dim3(1), dim3(1024), 0, s, a);
+  hipLaunchKernelGGL(k_pool_place, dim3(blocks), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -190,18 +190,21 @@ struct PoolAcceptArgs {
   int par_mask;            // bit p: the parity-p tables are read (d even: entries and runs all start even)
 };
 
-// The entry starts in parallel (k_pool_walk, k_pool_merge).  Entry e + 1 starts where the
-// walk of entry e from its start ends, a deterministic function of the start.  Chunk g of C
-// entries is walked by one wave from a guess of its start (e_g times the mean entry length,
-// at the parity every start of e_g has: (e_g d) mod 2) through the first M entries of chunk
-// g + 1.  Walks from different starts coalesce: the run starts of two walks map to the same
-// accepted attempt unless an accepted attempt lies between them, so about one in eight pairs
-// of neighbouring walks merges per entry and the walk from a guess meets the true one within
-// ~100 entries.  Once two walks share an entry start they agree from there on, so chunk g + 1
-// is right from the first entry where its positions equal chunk g's overlap -- by induction
-// from chunk 0, which starts at 0 -- and the entries before it take chunk g's.  A chunk whose
-// walk has not met its predecessor's within M entries is reported (err bit 2) and the host
-// parses serially.
+// The entry starts in parallel (k_pool_walk, k_pool_meet, k_pool_place).  Entry e + 1 starts
+// where the walk of entry e from its start ends: a deterministic function of the start.
+// Chunk g (nominal entries e_g = g C ..) is walked by one wave for C + M entries from a guess
+// of its start (e_g times the mean entry length, at the parity every start of e_g has:
+// (e_g d) mod 2).  Walks from different starts coalesce: at a run's start two walks go to
+// the same accepted attempt unless an accepted attempt of the run's class lies between them,
+// so the walks between a guess and the true start merge into one within ~100 entries (one in
+// eight neighbours merges per run at C5's acceptance rate).  A walk from a guess is the true
+// chain, shifted by an unknown number of entries delta_g, from the first position it shares
+// with the (true) walk before it: chunk g's walk meets chunk g - 1's at walk indices k2 / k1,
+// so delta_g = delta_{g-1} + k1 - k2 - C (delta_0 = 0, chunk 0 starts at 0) -- a prefix sum
+// over the chunks -- and chunk g's walk is valid for the entries from
+// a_g = e_{g-1} + delta_{g-1} + k1 on.  Entry e takes the walk of the last chunk with a_g <= e.
+// A chunk that does not meet its predecessor within its walk is reported (err bit 2) and the
+// host parses serially; a walk that runs off the tables marks its remaining positions -1.
 struct PoolWalkArgs {
   const uint64_t* bm;
   int64_t nwords;
@@ -210,12 +213,16 @@ struct PoolWalkArgs {
   const int* run_cls;
   const int* run_len;
   int64_t P;
-  int C, M;                // entries per chunk, overlap (M <= C)
+  int C, M;                // nominal entries per chunk, extra entries walked
   double mu;               // mean entry length (the chunk starts' guesses)
   int64_t count;
+  int64_t chunks;          // P / C + 1
+  int64_t* walk;           // [chunks][C + M] the walk of each chunk (positions, increasing; -1 past the tables)
+  int* rel;                // [chunks] delta_g - delta_{g-1}
+  int64_t* a;              // [chunks + 1] first entry of chunk g's valid part (a_0 = 0, a_chunks = P + 1)
+  int64_t* delta;          // [chunks]
   int64_t* starts;         // [P + 1]
-  int64_t* ext;            // [chunks][M] chunk g's walk through entries e_g + C .. e_g + C + M - 1
-  int* err;                // bit 2: a chunk did not meet its predecessor; bit 3: the tables ended
+  int* err;                // bit 2: a chunk did not meet its predecessor; bit 3: the tables ended before entry P
 };
 
 struct PoolValueArgs {

@@ -29,7 +29,7 @@ def hd():
     return hd
 
 
-def start(hd, oracle, name, seed, hig_log=False):
+def start(hd, oracle, name, seed, hig_log=False, phi_device=False):
     from split_and_merge_gibbs_sampling_amd.data import config
     ds = config(name)
     eng = hd.Engine(0)
@@ -37,6 +37,8 @@ def start(hd, oracle, name, seed, hig_log=False):
     eng.set_seed(seed)
     if hig_log:
         eng.set_hig_logspace(True)
+    if phi_device:
+        eng.set_phi_device(True)
     m = 3
     params = eng.chain_params(m=m, iterations=1, L=0, burnin=0, neal8=True, split_merge=hig_log, t=10, r=10)
     eng.init_chain(params, c_i=ds.truth)
@@ -92,14 +94,23 @@ def test_c5_full_size_sweeps(hd, oracle):
 
 
 @pytest.mark.timeout(900)
-def test_c3_full_size_neal8_and_split_merge(hd, oracle):
-    """C3: N = 100,000, D = 64, m_j ~ U{2..6}, K = 20: Neal-8 + split-merge."""
+@pytest.mark.parametrize("phi_device", [False, True])
+def test_c3_full_size_neal8_and_split_merge(hd, oracle, phi_device):
+    """C3: N = 100,000, D = 64, m_j ~ U{2..6}, K = 20: Neal-8 + split-merge; with phi_device,
+    update_phi on the device (BASELINE config C3: "hyperg phi-update on device")."""
     oracle.set_hig_logspace(True)
     try:
-        ds, eng, ost, rng, pc, ps = start(hd, oracle, "c3", seed=2, hig_log=True)
+        ds, eng, ost, rng, pc, ps = start(hd, oracle, "c3", seed=2, hig_log=True, phi_device=phi_device)
         assert ds.n == 100_000 and ds.d == 64
+        eng.reset_stats()
         neal8_steps(eng, oracle, ds, ost, rng, pc, ps, sweeps=2)
+        if phi_device:
+            st = eng.stats()
+            assert st["phi_device_calls"] == 2 and st["phi_device_fallbacks"] == 0, st
         sm_steps(eng, oracle, ds, ost, rng, moves=4)
+        if phi_device:
+            st = eng.stats()
+            assert st["phi_device_fallbacks"] == 0, st
         eng.close()
     finally:
         oracle.set_hig_logspace(False)
@@ -173,9 +184,12 @@ def test_c5_full_size_random20_start(hd, oracle):
 # go -- the same chain without the device-gated pipeline); "gateoff": the enqueued sweep's wait
 # kernel gives up after 1 us with no host-side check, so nearly every enqueued sweep is gated
 # off on the device and re-run ungated by the engine (its recovery path)
+# "phidev": update_phi on the device (HDPM_OPT_PHI_DEVICE), speculated beside each sweep and
+# committed when the sweep moved no point (engine.cpp dspec_launch / dspec_commit)
 @pytest.mark.parametrize("name,warm,timed,mode", [("c5", 5, 25, ""), ("c5", 3, 12, "nopipe"),
-                                                  ("c5", 3, 12, "gateoff"), ("c3", 5, 25, ""),
-                                                  ("c4", 3, 25, "")])
+                                                  ("c5", 3, 12, "gateoff"), ("c5", 5, 25, "phidev"),
+                                                  ("c3", 5, 25, ""), ("c3", 5, 25, "phidev"),
+                                                  ("c4", 3, 25, ""), ("c4", 3, 15, "phidev")])
 def test_bench_path_iterations_api(hd, oracle, name, warm, timed, mode):
     """The path bench.py times (bench.py main: hdpm_iterations for the warmup, synchronize,
     reset_stats, hdpm_iterations for the timed window) at the full BASELINE size, against
@@ -194,6 +208,8 @@ def test_bench_path_iterations_api(hd, oracle, name, warm, timed, mode):
         eng.set_debug(4194304)
     elif mode == "gateoff":
         eng.set_pipe_wait_us(-1.0)
+    elif mode == "phidev":
+        eng.set_phi_device(True)
     params = eng.chain_params(m=3, iterations=warm + timed + 3, L=0, burnin=0, neal8=True, split_merge=False)
     eng._params = params
 
@@ -224,6 +240,10 @@ def test_bench_path_iterations_api(hd, oracle, name, warm, timed, mode):
         assert st["pipe_enqueued"] == 0 and st["pipe_runs"] == 0, st
     if mode == "gateoff":
         assert st["pipe_recovered"] > 0, st
+    if mode == "phidev":
+        # every update on the device (none handed back to the host), from the speculation
+        assert st["phi_device_calls"] == timed and st["phi_device_fallbacks"] == 0, st
+        assert st["phi_dspec_used"] > 0, st
     np.testing.assert_allclose(ll, oracle_iters(it - timed, timed), rtol=RTOL, atol=0)
     same(eng, ost, rng, "after the timed batch")
     _, ll = eng.iterations(it, 3)
