@@ -86,6 +86,10 @@ typedef struct {
     /* update_phi speculated on the device beside the sweep (phi_mode device): launched, and
      * committed as the iteration's update (the sweep moved no point) */
     int64_t phi_dspec_launched, phi_dspec_used;
+    /* resolver launches by the device-wide fixed-point resolver (k_resolve_fpg) */
+    int64_t fpg_launches;
+    /* split-merge update_phi calls (sm:221, 387, 584) run on the device */
+    int64_t phi_sm_device_calls;
 } hdpm_stats;
 
 int         hdpm_device_count(void);
@@ -200,7 +204,10 @@ int hdpm_reset_stats(hdpm_ctx* ctx);
  * fixed-point resolver's first round starts every point from "stay" instead of its snapshot
  * draw's outcome; bit 27: the device update_phi resolves its drifts by the per-start-drift walks
  * (k_phi_cwalk) instead of the composition trees (k_phi_tree); bit 28: the device pool generator's
- * entry starts by the sequential host walk instead of the parallel chunk walks (k_pool_walk). */
+ * entry starts by the sequential host walk instead of the parallel chunk walks (k_pool_walk);
+ * bit 29: the fixed-point resolver on one workgroup (k_resolve_fp) even after a launch that
+ * listed many points (by default those take the device-wide k_resolve_fpg); bit 30: k_resolve_fpg
+ * for every fixed-point launch (testing: also the launches with few listed points). */
 int hdpm_set_debug(hdpm_ctx* ctx, int32_t mode);
 /* The prepass's pool-entry heads, P entries of wb*Ws + 2 words padded to a power of two
  * (Ws <= 4) or to a multiple of 8 words (wide layouts) (csrc/kernels.hpp "Pool-entry heads",

@@ -65,7 +65,8 @@ class Stats(C.Structure):
         [(n, C.c_int64) for n in ("phi_device_calls", "phi_device_fallbacks", "phi_device_last_status",
                                   "phi_lookahead_hits", "phi_lookahead_copies", "pipe_enqueued", "pipe_runs",
                                   "pipe_refused", "pipe_recovered", "phi_tree_calls", "phi_tree_retries",
-                                  "pool_walk_fallbacks", "phi_dspec_launched", "phi_dspec_used")]
+                                  "pool_walk_fallbacks", "phi_dspec_launched", "phi_dspec_used",
+                                  "fpg_launches", "phi_sm_device_calls")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

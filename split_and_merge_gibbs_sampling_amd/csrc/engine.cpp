@@ -43,6 +43,8 @@ hipError_t launch_cluster_summary(const PrepassArgs& a, hipStream_t s);
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s);
 hipError_t launch_exact_rows(const PrepassArgs& a, int nblocks, hipStream_t s);
 size_t resolve_smem_bytes(int scap, int m, int blocks);
+size_t resolve_fpg_smem_bytes(int lcap, int m);
+int resolve_fpg_max_grid(int lcap, int m);
 hipError_t launch_relabel(int* c, const int* los, int n, const ResolveCtl* ctl, hipStream_t s);
 hipError_t launch_finish_sweep(int* counts, int* sol, int* los, int* src, int cap, const ResolveCtl* ctl, int n,
                                hipStream_t s);
@@ -784,6 +786,8 @@ struct Ctx {
   DevBuf<uint64_t> d_csum;            // per-label cluster summary for the prepass
   DevBuf<unsigned> d_hist_part;
   DevBuf<long long> d_rprof;          // resolver phase times (debug mode bit 1)
+  DevBuf<int> d_fpg;                   // k_resolve_fpg's cross-workgroup scratch
+  int fpg_grid_cache[65] = {0};        // its resident grid per resolver slot capacity (0: unknown, -1: none)
   PinBuf<int> h_ctl;                  // two blocks [ResolveCtl | pad to kCtlInts][resolver summary: 3 scap]
   // Consecutive sweeps alternate between the two control blocks (and resolver events), so a
   // sweep enqueued ahead (pre_enqueue) does not overwrite the one the host is reading.
@@ -1960,6 +1964,7 @@ struct Ctx {
   // after a prefix launched with the same arguments and no state change in between).
   enum { kRoundAll = 0, kRoundPrefix = 1, kRoundResolve = 2 };
   static constexpr int kFpMinListed = 64;
+  static constexpr int kFpgMinListed = 8192;   // listed points of the previous launch for k_resolve_fpg
   bool fp_eligible(int E, int lcap) const {
     return E <= 64 && lcap <= 64 && !(debug & (1 | 4096 | 8192 | 8388608));
   }
@@ -2087,6 +2092,25 @@ struct Ctx {
                 ? 1 : 0;
     if (ra.fp) ra.blocks = 0;
     ra.debug_fp = (debug & 67108864) ? 1 : 0;
+    // the device-wide fixed-point resolver (k_resolve_fpg) after a launch that listed many
+    // points: one 512-point chunk per workgroup, a workgroup per CU (debug bit 29: one workgroup)
+    ra.fpg = 0;
+    ra.fpg_buf = nullptr;
+    if (ra.fp && (last_listed >= kFpgMinListed || (debug & 1073741824)) && !(debug & 536870912) && ra.lcap <= 64) {
+      int& mg = fpg_grid_cache[ra.lcap];
+      if (mg == 0) {
+        mg = resolve_fpg_max_grid(ra.lcap, m);
+        if (mg < 2) mg = -1;
+      }
+      if (mg > 0 && resolve_fpg_smem_bytes(ra.lcap, m) <= 160 * 1024) {
+        const int G = std::min(mg, std::max(2, (std::max(last_listed, 0) + 511) / 512));
+        d_fpg.ensure(fpg_words(G));
+        HIPCHK(hipMemsetAsync(d_fpg.p, 0, 16, stream));
+        ra.fpg = G;
+        ra.fpg_buf = d_fpg.p;
+        if (!pg) stats.fpg_launches++;
+      }
+    }
     if (part != kRoundPrefix && !pg) last_fp = ra.fp != 0;
     if (resolve_smem_bytes(ra.lcap, m, ra.blocks) > 160 * 1024) {
       err = "too many clusters for the resolver (K > ~2300)";
@@ -3687,6 +3711,103 @@ struct Ctx {
     adopt_state_at(*dspec.W, target);
     const double drift = (double)(cons - 3 * dspec.pl.items);
     const double ph = drift / (drift + 2.0 * (double)dspec.pl.items);
+    phd.p_rej = std::min(0.3, std::max(0.05, 0.7 * phd.p_rej + 0.3 * ph));
+    return kOk;
+  }
+
+  // update_phi (cf:511-591) of T clusters of a split-merge state on the device (sm:221, sm:387,
+  // sm:584): their sizes `cnt`, frequency tables `freq` ([T][d][mmax], the move's host tables) and
+  // current sigmas; the new centers (codes) and sigmas into cen / sig ([T][d]).  kOk, or -1
+  // when the device path does not apply or hands the update back (nothing changed: same
+  // stream position).  The host stream is synchronised to the position after the draws.
+  DevBuf<unsigned> d_sm_freq;
+  PinBuf<unsigned> h_sm_freq;
+  int device_update_phi_sm(int T, const int* cnt, const unsigned* freq, const double* sig_in, uint8_t* cen,
+                           double* sig) {
+    if (phi_mode == 0 || (debug & (524288 | 64)) || T <= 0 || d > 2048 || !glibc_selfcheck()) return -1;
+    rng_sync();
+    const PhiPlan pl = phi_plan(T);
+    if (!pl.ok) return -1;
+    RngWindow* W = window_at(rng.pos, pl.need);
+    if (!W) return -1;
+    dspec_wait();
+    PhiArgs a = phi_args(pl);
+    const int64_t items = pl.items;
+    const size_t fw = (size_t)T * d * mmax;
+    h_sm_freq.ensure(fw);
+    d_sm_freq.ensure(fw);
+    std::memcpy(h_sm_freq.p, freq, fw * 4);
+    const size_t in_bytes = (size_t)2 * T * 4 + (size_t)items * 8;
+    phd.h_in.ensure(in_bytes + 64);
+    int* hl = (int*)phd.h_in.p;
+    double* hs = (double*)(phd.h_in.p + align16((size_t)2 * T * 4));
+    int min_count = INT_MAX;
+    for (int t = 0; t < T; ++t) {
+      hl[t] = t;
+      hl[T + t] = cnt[t];
+      min_count = std::min(min_count, cnt[t]);
+    }
+    std::memcpy(hs, sig_in, (size_t)items * 8);
+    phd.lab_cnt.ensure(2 * T);
+    phd.sig_in.ensure(items);
+    phd.sig_out.ensure(items);
+    phd.ll.ensure(2 * T);
+    phd.pick.ensure(items);
+    phd.status.ensure(4);
+    phd.stage.ensure(upload_layout(T, dp, d, bw).bytes);
+    size_t o_pick, o_sig, o_ll, bytes;
+    phi_out_layout(T, d, &o_pick, &o_sig, &o_ll, &bytes);
+    phd.h_out.ensure(bytes);
+    HIPCHK(hipMemcpyAsync(d_sm_freq.p, h_sm_freq.p, fw * 4, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(phd.lab_cnt.p, hl, (size_t)2 * T * 4, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(phd.sig_in.p, hs, (size_t)items * 8, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipStreamWaitEvent(stream, W->done, 0));
+    a.lab = phd.lab_cnt.p; a.cnt = phd.lab_cnt.p + T; a.freq = d_sm_freq.p; a.sig_in = phd.sig_in.p;
+    a.raw = W->raw.p + (rng.pos - W->start_pos);
+    a.nraw = (int64_t)(W->start_pos + (uint64_t)W->count - rng.pos);
+    a.pick = phd.pick.p; a.status = phd.status.p;
+    a.stage = phd.stage.p; a.sig_out = phd.sig_out.p; a.ll = phd.ll.p;
+    auto run = [&](bool tree) {
+      a.tree = tree ? phd.tree.p : nullptr;
+      if (tree) HIPCHK(hipMemsetAsync(phd.tnd.p, 0, (size_t)T * 4, stream));
+      HIPCHK(hipMemsetAsync(phd.status.p, 0, 16, stream));
+      HIPCHK(hipMemsetAsync(phd.act.p, 0, 4, stream));
+      HIPCHK(launch_phi(a, stream));
+      HIPCHK(hipMemcpyAsync(phd.h_out.p, phd.status.p, 16, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipMemcpyAsync(phd.h_out.p + o_pick, phd.pick.p, (size_t)items, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipMemcpyAsync(phd.h_out.p + o_sig, phd.sig_out.p, (size_t)items * 8, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+    };
+    const bool tree = pl.tree_ok && (pl.S == 1 || min_count >= phd.tree_min_count) && !(debug & 134217728);
+    run(tree);
+    phd.calls++;
+    if (tree) stats.phi_tree_calls++;
+    if (tree && ((const int*)phd.h_out.p)[0] == kPhiNonDet) {
+      phd.tree_min_count = std::max(phd.tree_min_count, std::min(1 << 20, 2 * min_count));
+      stats.phi_tree_retries++;
+      run(false);
+    }
+    phd_release(stream);
+    const int status = ((const int*)phd.h_out.p)[0];
+    stats.phi_device_last_status = status;
+    int64_t cons = 0;
+    std::memcpy(&cons, phd.h_out.p + 8, 8);
+    const uint64_t target = rng.pos + (uint64_t)cons;
+    if (status != kPhiOk || cons <= 0 || !can_adopt(*W, target)) {
+      phd.fallbacks++;
+      stats.phi_device_fallbacks++;
+      if (status == kPhiOk) stats.phi_device_last_status = -1;
+      return -1;
+    }
+    stats.phi_device_calls++;
+    stats.phi_sm_device_calls++;
+    const uint8_t* pk = phd.h_out.p + o_pick;
+    for (int64_t q = 0; q < items; ++q) cen[q] = (uint8_t)(pk[q] + 1);
+    std::memcpy(sig, phd.h_out.p + o_sig, (size_t)items * 8);
+    adopt_state_at(*W, target);
+    rng_sync();                        // split-merge draws on the host next
+    const double drift = (double)(cons - 3 * items);
+    const double ph = drift / (drift + 2.0 * (double)items);
     phd.p_rej = std::min(0.3, std::max(0.05, 0.7 * phd.p_rej + 0.3 * ph));
     return kOk;
   }

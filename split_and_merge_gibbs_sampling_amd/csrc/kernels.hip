@@ -2822,6 +2822,8 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
   resolve_finish(a, st, F->nlog, tp, prof);
 }
 
+#include "resolve_fpg.inl"
+
 // ------------------------------------------------------------------ end of sweep
 // The sweep-end kernels are enqueued behind every resolver launch and read its control
 // block: they act only when that launch finished the sweep, so the host need not wait for
@@ -3160,8 +3162,31 @@ size_t resolve_smem_bytes(int lcap, int m, int blocks) {
   return resolve_lds_bytes(lcap, m, blocks, blocks ? 0 : kTileCols);
 }
 
+size_t resolve_fpg_smem_bytes(int lcap, int m) { return resolve_fpg_lds_bytes(lcap, m); }
+
+// workgroups of k_resolve_fpg that are resident together on this device (0: none)
+int resolve_fpg_max_grid(int lcap, int m) {
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  const size_t lds = resolve_fpg_lds_bytes(lcap, m);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&k_resolve_fpg<32>),
+                                                   kFpThreads, lds) != hipSuccess)
+    return 0;
+  int per64 = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per64, reinterpret_cast<const void*>(&k_resolve_fpg<64>),
+                                                   kFpThreads, lds) != hipSuccess)
+    return 0;
+  return cus * std::min(per, per64) >= cus ? cus : 0;   // one per CU
+}
+
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s) {
-  if (a.fp) {
+  if (a.fp && a.fpg > 1) {
+    const size_t lds = resolve_fpg_lds_bytes(a.lcap, a.m);
+    if (a.K + a.m <= 24) hipLaunchKernelGGL(k_resolve_fpg<24>, dim3(a.fpg), dim3(kFpThreads), lds, s, a);
+    else if (a.K + a.m <= 32) hipLaunchKernelGGL(k_resolve_fpg<32>, dim3(a.fpg), dim3(kFpThreads), lds, s, a);
+    else hipLaunchKernelGGL(k_resolve_fpg<64>, dim3(a.fpg), dim3(kFpThreads), lds, s, a);
+  } else if (a.fp) {
     const size_t lds = resolve_fp_lds_bytes(a.lcap, a.m);
     if (a.K + a.m <= 24) hipLaunchKernelGGL(k_resolve_fp<24>, dim3(1), dim3(kFpThreads), lds, s, a);
     else if (a.K + a.m <= 32) hipLaunchKernelGGL(k_resolve_fp<32>, dim3(1), dim3(kFpThreads), lds, s, a);

@@ -272,8 +272,44 @@ static int hupdate_phi_job(Ctx* c, HState& s, const int* ks, const Freq* const* 
   return kOk;
 }
 
+// update_phi (cf:511-591) of clusters ks[0..nk) (ascending labels) on the device
+// (Ctx::device_update_phi_sm, csrc/phi.hip): -1 when it does not apply (the host job runs).
+static int dupdate_phi_sm(Ctx* c, HState& s, const int* ks, const Freq* const* Fs, int nk) {
+  if (c->phi_mode == 0) return -1;
+  SmTimer tm(c->stats.t_sm_phi_ms);
+  const int d = c->d, mm = c->mmax;
+  std::vector<int> idx;
+  for (int t = 0; t < nk; ++t)
+    if (Fs[t]->nn > 0) idx.push_back(t);
+  const int T = (int)idx.size();
+  if (T == 0) return kOk;
+  std::vector<unsigned> fq((size_t)T * d * mm);
+  std::vector<int> cnt(T);
+  std::vector<double> sg((size_t)T * d), so((size_t)T * d);
+  std::vector<uint8_t> cen((size_t)T * d);
+  for (int q = 0; q < T; ++q) {
+    const Freq& F = *Fs[idx[q]];
+    cnt[q] = F.nn;
+    for (size_t e = 0; e < (size_t)d * mm; ++e) fq[(size_t)q * d * mm + e] = (unsigned)F.f[e];
+    std::memcpy(&sg[(size_t)q * d], &s.sigma[(size_t)ks[idx[q]] * d], (size_t)d * 8);
+  }
+  const int st = c->device_update_phi_sm(T, cnt.data(), fq.data(), sg.data(), cen.data(), so.data());
+  if (st != kOk) return -1;
+  for (int q = 0; q < T; ++q) {
+    std::memcpy(&s.center[(size_t)ks[idx[q]] * d], &cen[(size_t)q * d], d);
+    std::memcpy(&s.sigma[(size_t)ks[idx[q]] * d], &so[(size_t)q * d], (size_t)d * 8);
+  }
+  return kOk;
+}
+
 // update_phi of {ka, kb} in the reference's order (ascending label; a repeated label once)
 static int hupdate_phi_pair(Ctx* c, HState& s, int ka, const Freq& Fa, int kb, const Freq& Fb) {
+  {
+    // on the device when update_phi is placed there (HDPM_OPT_PHI_DEVICE)
+    const int ks[2] = {std::min(ka, kb), std::max(ka, kb)};
+    const Freq* fs[2] = {ka <= kb ? &Fa : &Fb, ka <= kb ? &Fb : &Fa};
+    if (dupdate_phi_sm(c, s, ks, fs, ka == kb ? 1 : 2) == kOk) return kOk;
+  }
   if (c->d < 128 || (c->debug & 128)) {
     int st = ka <= kb ? hupdate_phi_one(c, s, ka, Fa) : hupdate_phi_one(c, s, kb, Fb);
     if (st) return st;

@@ -109,8 +109,9 @@ def test_c3_full_size_neal8_and_split_merge(hd, oracle, phi_device):
             assert st["phi_device_calls"] == 2 and st["phi_device_fallbacks"] == 0, st
         sm_steps(eng, oracle, ds, ost, rng, moves=4)
         if phi_device:
+            # split-merge's update_phi({c1, c2}) (sm:221, 387, 584) on the device too
             st = eng.stats()
-            assert st["phi_device_fallbacks"] == 0, st
+            assert st["phi_device_fallbacks"] == 0 and st["phi_sm_device_calls"] > 0, st
         eng.close()
     finally:
         oracle.set_hig_logspace(False)
@@ -134,8 +135,9 @@ def test_c4_full_size_neal8_and_split_merge(hd, oracle):
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("L", [1, 20])
 # 0: the fixed-point resolver (k_resolve_fp); 4096: the one-wave LIST resolver without block
-# mode; 8388608 (bit 23): the one-wave resolvers with block mode after many exact decisions
-@pytest.mark.parametrize("debug", [0, 4096, 8388608])
+# mode; 8388608 (bit 23): the one-wave resolvers with block mode after many exact decisions;
+# 1073741824 (bit 30): the device-wide fixed-point resolver (k_resolve_fpg) for every launch
+@pytest.mark.parametrize("debug", [0, 4096, 8388608, 1073741824])
 def test_c2_full_size_unconverged_starts(hd, oracle, L, debug):
     """C2: N = 10,000, D = 32, binary, from one cluster (L = 1) or a random assignment to 20
     labels (la:31-43, the scripts' L = 20): far from the posterior, points move every sweep
@@ -175,7 +177,9 @@ def test_c5_full_size_random20_start(hd, oracle):
     ost = oracle.OracleState(c, cen.shape[0], cen, sig, cap=4096)
     rng = eng.rng_state.copy()
     neal8_steps(eng, oracle, ds, ost, rng, pc, ps, sweeps=2)
-    assert eng.stats()["moves"] > 100_000
+    st = eng.stats()
+    assert st["moves"] > 100_000
+    assert st["fpg_launches"] > 0, st     # the device-wide fixed-point resolver decided the second sweep
     eng.close()
 
 

@@ -79,7 +79,9 @@ def test_tiny_shapes_chain_matches_oracle(hd, oracle, shape, m, mode):
 
 # debug 33554432 (bit 25): the fixed-point resolver (k_resolve_fp) for every launch, not only
 # after a launch that listed >= 64 points
-@pytest.mark.parametrize("debug", [0, 33554432])
+# debug 33554432 | 1073741824 (bits 25, 30): the device-wide fixed-point resolver (k_resolve_fpg,
+# a workgroup per 512-point chunk, grid barriers) for every launch
+@pytest.mark.parametrize("debug", [0, 33554432, 33554432 | 1073741824])
 @pytest.mark.parametrize("mode", ["n8", "both"])
 @pytest.mark.parametrize("shape", [(2, 1, 1, 2), (4, 3, 2, 3), (7, 5, 3, 4), (65, 1, 2, 3), (130, 3, 4, (2, 5))],
                          ids=_shape_id)
@@ -116,7 +118,7 @@ def test_tiny_shapes_iteration_api(hd, oracle, shape, mode, debug):
         e.close()
 
 
-@pytest.mark.parametrize("debug", [0, 16, 33554432])
+@pytest.mark.parametrize("debug", [0, 16, 33554432, 33554432 | 1073741824])
 def test_tiny_shape_random_init_chain(hd, oracle, debug):
     # random L = 5 initial labels on 40 points: clusters vanish (case 2) and appear (cases 3 /
     # 4) within the same sweeps, at the last point too; carried tables (0), recounts (16), the
