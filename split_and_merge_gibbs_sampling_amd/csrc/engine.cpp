@@ -787,6 +787,7 @@ struct Ctx {
   DevBuf<unsigned> d_hist_part;
   DevBuf<long long> d_rprof;          // resolver phase times (debug mode bit 1)
   DevBuf<int> d_fpg;                   // k_resolve_fpg's cross-workgroup scratch
+  DevBuf<int> d_wide_ctr;              // k_prepass_wide's chunk counter
   int fpg_grid_cache[65] = {0};        // its resident grid per resolver slot capacity (0: unknown, -1: none)
   PinBuf<int> h_ctl;                  // two blocks [ResolveCtl | pad to kCtlInts][resolver summary: 3 scap]
   // Consecutive sweeps alternate between the two control blocks (and resolver events), so a
@@ -1964,7 +1965,7 @@ struct Ctx {
   // after a prefix launched with the same arguments and no state change in between).
   enum { kRoundAll = 0, kRoundPrefix = 1, kRoundResolve = 2 };
   static constexpr int kFpMinListed = 64;
-  static constexpr int kFpgMinListed = 8192;   // listed points of the previous launch for k_resolve_fpg
+  static constexpr int kFpgMinListed = 1024;   // listed points of the previous launch for k_resolve_fpg (two chunks)
   bool fp_eligible(int E, int lcap) const {
     return E <= 64 && lcap <= 64 && !(debug & (1 | 4096 | 8192 | 8388608));
   }
@@ -2027,6 +2028,9 @@ struct Ctx {
     pa.exact_grid = last_listed < 0 ? 0 : std::min(1024, std::max(64, 4 * last_listed + 64));
     pa.wide = (debug & 16384) ? 0 : 1;
     pa.zero = nullptr;
+    d_wide_ctr.ensure(1);
+    pa.wide_ctr = d_wide_ctr.p;      // cleared by k_cluster_summary (below: K > 0)
+    if (K == 0 && part != kRoundResolve) HIPCHK(hipMemsetAsync(d_wide_ctr.p, 0, 4, stream));
     if (mcount_clear && part != kRoundResolve) {
       if (K > 0) pa.zero = d_mcount.p;
       else HIPCHK(hipMemsetAsync(d_mcount.p, 0, 4, stream));

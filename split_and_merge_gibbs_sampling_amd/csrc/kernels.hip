@@ -272,7 +272,10 @@ __device__ __forceinline__ int penalty_r(const uint64_t (&M)[WS], const uint64_t
 // csum[l] = [record of slot_of_label[l] (bw words), logn[count], slot].
 __global__ void k_cluster_summary(PrepassArgs a) {
   if (!pipe_gate(a)) return;
-  if (a.zero && blockIdx.x == 0 && threadIdx.x == 0) *a.zero = 0;   // a memset dispatch less per sweep
+  if (blockIdx.x == 0 && threadIdx.x == 0) {     // memset dispatches less per sweep
+    if (a.zero) *a.zero = 0;
+    if (a.wide_ctr) *a.wide_ctr = 0;
+  }
   const int sw = a.bw + 2;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < a.K * sw; e += gridDim.x * blockDim.x) {
     const int l = e / sw, w = e - l * sw;
@@ -604,7 +607,16 @@ __global__ __launch_bounds__(kWideThreads) void k_prepass_wide(PrepassArgs a, in
         if (tid + 64 * r < kWideChunk * m1) s_raw[par][tid + 64 * r] = pf_raw[r];
     }
   };
-  int c = blockIdx.x;
+  // chunks are claimed from a counter (k_cluster_summary zeroes it), two ahead: a workgroup that
+  // starts late (its CU busy with another stream's kernel) leaves its share to the others
+  // instead of holding the launch's tail
+  __shared__ int s_cl[2];
+  if (tid == 0) {
+    s_cl[0] = atomicAdd(a.wide_ctr, 1);
+    s_cl[1] = atomicAdd(a.wide_ctr, 1);
+  }
+  __syncthreads();
+  int c = s_cl[0];
   if (c < nchunks) {
     fetch(c);
     stage(0);
@@ -634,11 +646,14 @@ __global__ __launch_bounds__(kWideThreads) void k_prepass_wide(PrepassArgs a, in
     if (tid == 0) a.cnt[cf] = __popcll(bal);
   };
   int cprev = -1;
+  int it = 0;
 #pragma unroll 1
-  for (; c < nchunks; c += gridDim.x, par ^= 1) {
+  for (; c < nchunks; par ^= 1, ++it) {
     __syncthreads();                          // the chunk is staged; the previous chunk's margins are in
     if (cprev >= 0 && tid < 64) finish(cprev, par ^ 1);
-    const int cn = c + gridDim.x;
+    // the next chunk (claimed an iteration ago); claim the one after it
+    const int cn = s_cl[(it + 1) & 1];
+    if (tid == 0) s_cl[it & 1] = cn < nchunks ? atomicAdd(a.wide_ctr, 1) : nchunks;
     if (cn < nchunks) fetch(cn);
     const int64_t i0 = (int64_t)a.p0 + (int64_t)c * kWideChunk;
     const int npts = (int)min((int64_t)kWideChunk, (int64_t)a.n - i0);
@@ -769,6 +784,7 @@ __global__ __launch_bounds__(kWideThreads) void k_prepass_wide(PrepassArgs a, in
     // finished the previous chunk from them, above)
     if (cn < nchunks) stage(par ^ 1);
     cprev = c;
+    c = cn;
   }
   __syncthreads();
   if (cprev >= 0 && tid < 64) finish(cprev, par ^ 1);

@@ -127,6 +127,7 @@ struct PrepassArgs {
   int exact_wave;            // 1: exact rows one wave per point (no workgroup staging)
   int wide;                  // 1: wide layouts take k_prepass_wide (0: the generic kernel)
   int* zero;                 // k_cluster_summary clears this word first (the sweep's move count), or nullptr
+  int* wide_ctr;             // k_prepass_wide's chunk counter (cleared by k_cluster_summary)
   int exact_grid;            // cap on the exact-rows grid (0: none); workgroups loop over the list
   int nlb, lblock;           // list blocks of this launch and their points (k_exact_rows_wg's own list scan)
   // pipelined iterations (engine.cpp iterations_pipelined): the kernels run only while *gate
