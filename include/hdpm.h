@@ -90,6 +90,9 @@ typedef struct {
     int64_t fpg_launches;
     /* split-merge update_phi calls (sm:221, 387, 584) run on the device */
     int64_t phi_sm_device_calls;
+    /* bit s set: a device update_phi was handed back with PhiStatus s (bit 15: the status was
+     * ok but the stream position could not be adopted) */
+    int64_t phi_fallback_status_mask;
 } hdpm_stats;
 
 int         hdpm_device_count(void);

@@ -1737,6 +1737,23 @@ struct Ctx {
     return ok;
   }
 
+  // HDPM_POOL_TRACE: the chunks of a parallel entry-start walk that fell back (stderr)
+  void pool_walk_trace(int64_t chunks, int L) {
+    std::vector<int64_t> av(chunks + 1), wv((size_t)chunks * L);
+    std::vector<int> rv(chunks);
+    HIPCHK(hipMemcpy(av.data(), pg.a.p, (chunks + 1) * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(rv.data(), pg.rel.p, chunks * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(wv.data(), pg.walk.p, (size_t)chunks * L * 8, hipMemcpyDeviceToHost));
+    for (int64_t g = 0; g < chunks; ++g) {
+      const int64_t* w = wv.data() + g * L;
+      int nv = 0;
+      while (nv < L && w[nv] >= 0) ++nv;
+      std::fprintf(stderr, "[pool walk] chunk %lld a %lld rel %d walk %lld..%lld (%d valid)%s\n", (long long)g,
+                   (long long)av[g], rv[g], (long long)w[0], nv ? (long long)w[nv - 1] : -1LL, nv,
+                   (g > 0 && av[g] < 0) ? " UNMET" : "");
+    }
+  }
+
   // Returns -1 when the device generator does not apply (the caller falls back).
   int generate_pool_device(int64_t P_) {
     using clk = std::chrono::steady_clock;
@@ -1838,6 +1855,7 @@ struct Ctx {
         // a chunk did not meet its predecessor (or debug bit 28): the sequential walk
         pg.walk_fallbacks++;
         stats.pool_walk_fallbacks++;
+        if (std::getenv("HDPM_POOL_TRACE") && !(debug & 268435456)) pool_walk_trace(chunks, C + M);
         pg.h_bm.ensure((size_t)nc * 2 * nwords);
         HIPCHK(hipMemcpyAsync(pg.h_bm.p, pg.bm.p, (size_t)nc * 2 * nwords * 8, hipMemcpyDeviceToHost, stream));
         HIPCHK(hipStreamSynchronize(stream));
@@ -3503,6 +3521,7 @@ struct Ctx {
       phd_release(stream);
       phd.fallbacks++;
       stats.phi_device_fallbacks++;
+      stats.phi_fallback_status_mask |= (int64_t)1 << (status != kPhiOk ? std::min(std::max(status, 0), 14) : 15);
       if (status == kPhiOk) stats.phi_device_last_status = -1;
       return -1;
     }
@@ -3681,6 +3700,7 @@ struct Ctx {
         !covers(*dspec.W, rng.pos, dspec.pl.need)) {
       phd.fallbacks++;
       stats.phi_device_fallbacks++;
+      stats.phi_fallback_status_mask |= (int64_t)1 << (status != kPhiOk ? std::min(std::max(status, 0), 14) : 15);
       return -1;
     }
     stats.phi_device_calls++;
@@ -3800,6 +3820,7 @@ struct Ctx {
     if (status != kPhiOk || cons <= 0 || !can_adopt(*W, target)) {
       phd.fallbacks++;
       stats.phi_device_fallbacks++;
+      stats.phi_fallback_status_mask |= (int64_t)1 << (status != kPhiOk ? std::min(std::max(status, 0), 14) : 15);
       if (status == kPhiOk) stats.phi_device_last_status = -1;
       return -1;
     }

@@ -111,7 +111,10 @@ def test_c3_full_size_neal8_and_split_merge(hd, oracle, phi_device):
         if phi_device:
             # split-merge's update_phi({c1, c2}) (sm:221, 387, 584) on the device too
             st = eng.stats()
-            assert st["phi_device_fallbacks"] == 0 and st["phi_sm_device_calls"] > 0, st
+            assert st["phi_device_fallbacks"] == 0 and st["phi_sm_device_calls"] > 0, \
+                {k: st[k] for k in ("phi_device_calls", "phi_device_fallbacks", "phi_sm_device_calls",
+                                    "phi_device_last_status", "phi_fallback_status_mask", "phi_tree_calls",
+                                    "phi_tree_retries", "sm_moves")}
         eng.close()
     finally:
         oracle.set_hig_logspace(False)

@@ -511,6 +511,7 @@ def test_device_mt_stream_jump_ahead_matches_r(hd, oracle, zoo, pre):
 
 # ------------------------------------------------------------------ latent pool generator
 def _pool_case(hd, oracle, ds, v, w, P, pre, seed, debug=0):
+    os.environ["HDPM_POOL_TRACE"] = "1"           # a walk fallback lists its chunks on stderr
     eng = hd.Engine(0)
     eng.set_data(ds.codes, ds.attrisize, ds.gamma, v, w)
     eng.set_debug(debug)
@@ -556,7 +557,8 @@ def test_device_pool_matches_oracle_synthetic(hd, oracle, case):
     assert st["pool_device_calls"] == (0 if case == "host_forced" else 1)
     if case != "host_forced":
         # the parallel walk's chunks met (no serial fallback) unless the serial walk was forced
-        assert st["pool_walk_fallbacks"] == (1 if case == "serial_parse" else 0), st
+        assert st["pool_walk_fallbacks"] == (1 if case == "serial_parse" else 0), \
+            {k: st[k] for k in ("pool_walk_fallbacks", "pool_device_calls", "t_pool_parse_ms")}
 
 
 def test_device_pool_then_sweeps_match_oracle(hd, oracle):
