@@ -80,8 +80,8 @@ typedef struct {
     /* device update_phi by composition trees (every pick fixed), and tree-mode updates re-run
      * by the per-start-drift walks (a pick depended on the uniform) */
     int64_t phi_tree_calls, phi_tree_retries;
-    /* device pool generations whose entry starts fell back to the sequential host walk (a
-     * chunk of the parallel walk did not meet its predecessor, or debug bit 28) */
+    /* device pool generations whose entry starts fell back to the sequential host walk (the
+     * segment parse's chain left a window: an entry longer than mean + 14 sd; or debug bit 28) */
     int64_t pool_walk_fallbacks;
     /* update_phi speculated on the device beside the sweep (phi_mode device): launched, and
      * committed as the iteration's update (the sweep moved no point) */
@@ -207,7 +207,7 @@ int hdpm_reset_stats(hdpm_ctx* ctx);
  * fixed-point resolver's first round starts every point from "stay" instead of its snapshot
  * draw's outcome; bit 27: the device update_phi resolves its drifts by the per-start-drift walks
  * (k_phi_cwalk) instead of the composition trees (k_phi_tree); bit 28: the device pool generator's
- * entry starts by the sequential host walk instead of the parallel chunk walks (k_pool_walk);
+ * entry starts by the sequential host walk instead of the segment parse (k_pool_seg*);
  * bit 29: the fixed-point resolver on one workgroup (k_resolve_fp) even after a launch that
  * listed many points (by default those take the device-wide k_resolve_fpg); bit 30: k_resolve_fpg
  * for every fixed-point launch (testing: also the launches with few listed points). */

@@ -49,7 +49,7 @@ hipError_t launch_relabel(int* c, const int* los, int n, const ResolveCtl* ctl, 
 hipError_t launch_finish_sweep(int* counts, int* sol, int* los, int* src, int cap, const ResolveCtl* ctl, int n,
                                hipStream_t s);
 hipError_t launch_apply_moves(const int* mlog, const int* mcount, int grid, const uint8_t* codes_t, int d, int nq,
-                              int mmax, unsigned int* freq, const ResolveCtl* ctl, int n, hipStream_t s);
+                              int mmax, unsigned int* freq, const ResolveCtl* ctl, int n, int nslots, hipStream_t s);
 hipError_t launch_freq_gather(const unsigned int* freq, const int* sol, int Kmax, int fs, unsigned int* out,
                               const ResolveCtl* ctl, int n, hipStream_t s);
 hipError_t launch_scatter_clusters(const uint8_t* stage, int nent, int dp, int d, int bw, int full, uint8_t* codes,
@@ -761,10 +761,11 @@ struct Ctx {
     PinBuf<uint32_t> h_init, h_tail;
     DevBuf<uint64_t> bm;
     PinBuf<uint64_t> h_bm;
-    DevBuf<int64_t> starts, walk, a, delta;
-    DevBuf<int> rel;
+    DevBuf<int64_t> starts, cE, aux;
+    DevBuf<uint32_t> T;
+    DevBuf<int32_t> gj, gn, cidx;
     PinBuf<int64_t> h_starts;
-    int64_t walk_fallbacks = 0;       // chunks that did not meet: serial host parse
+    int64_t walk_fallbacks = 0;       // segment parses that left a window: serial host parse
     DevBuf<PoolClass> cls;
     DevBuf<int> runs;
     DevBuf<int32_t> att;
@@ -1737,23 +1738,6 @@ struct Ctx {
     return ok;
   }
 
-  // HDPM_POOL_TRACE: the chunks of a parallel entry-start walk that fell back (stderr)
-  void pool_walk_trace(int64_t chunks, int L) {
-    std::vector<int64_t> av(chunks + 1), wv((size_t)chunks * L);
-    std::vector<int> rv(chunks);
-    HIPCHK(hipMemcpy(av.data(), pg.a.p, (chunks + 1) * 8, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(rv.data(), pg.rel.p, chunks * 4, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(wv.data(), pg.walk.p, (size_t)chunks * L * 8, hipMemcpyDeviceToHost));
-    for (int64_t g = 0; g < chunks; ++g) {
-      const int64_t* w = wv.data() + g * L;
-      int nv = 0;
-      while (nv < L && w[nv] >= 0) ++nv;
-      std::fprintf(stderr, "[pool walk] chunk %lld a %lld rel %d walk %lld..%lld (%d valid)%s\n", (long long)g,
-                   (long long)av[g], rv[g], (long long)w[0], nv ? (long long)w[nv - 1] : -1LL, nv,
-                   (g > 0 && av[g] < 0) ? " UNMET" : "");
-    }
-  }
-
   // Returns -1 when the device generator does not apply (the caller falls back).
   int generate_pool_device(int64_t P_) {
     using clk = std::chrono::steady_clock;
@@ -1830,21 +1814,24 @@ struct Ctx {
       HIPCHK(launch_pool_accept(aa, stream));
       HIPCHK(hipStreamSynchronize(stream));
       auto t1 = clk::now();
-      // entry starts: chunks walked in parallel from guesses, placed where they meet the walk
-      // before them (k_pool_walk / k_pool_meet / k_pool_scan / k_pool_place, pool_gen.hpp);
-      // the serial host parse when a chunk does not meet its predecessor
-      const int C = 512, M = 512;
-      const int64_t chunks = P_ / C + 1;
+      // entry starts by segments (k_pool_seg*, pool_gen.hpp PoolSegPlan); the serial host
+      // parse when the chain leaves a window (an entry longer than mean + 14 sd)
+      const PoolSegPlan sp = pool_seg_plan(pl, d, count);
+      const size_t cells = (size_t)sp.nchunks * sp.ncand;
+      pg.T.ensure(cells);
+      pg.gj.ensure((size_t)sp.ngroups * sp.ncand);
+      pg.gn.ensure((size_t)sp.ngroups * sp.ncand);
+      pg.cidx.ensure(sp.nchunks);
+      pg.cE.ensure(sp.nchunks);
+      pg.aux.ensure(1);
       pg.starts.ensure(P_ + 1);
-      pg.walk.ensure((size_t)chunks * (C + M));
-      pg.rel.ensure(chunks);
-      pg.a.ensure(chunks + 1);
-      pg.delta.ensure(chunks);
       pg.h_starts.ensure(P_ + 1);
       HIPCHK(hipMemsetAsync(pg.err.p, 0, 4, stream));
-      PoolWalkArgs wa{pg.bm.p, nwords, d, (int)pl.run_cls.size(), pg.runs.p, pg.runs.p + pl.run_cls.size(), P_, C, M,
-                      pl.mean_len, count, chunks, pg.walk.p, pg.rel.p, pg.a.p, pg.delta.p, pg.starts.p, pg.err.p};
-      HIPCHK(launch_pool_walk(wa, stream));
+      HIPCHK(hipMemsetAsync(pg.cidx.p, 0xFF, (size_t)sp.nchunks * 4, stream));
+      const int nr = (int)pl.run_cls.size();
+      PoolSegArgs sa{pg.bm.p, nwords, d, PoolRuns{nr, pg.runs.p, pg.runs.p + nr}, sp, P_, pg.T.p, pg.gj.p, pg.gn.p,
+                     pg.cidx.p, pg.cE.p, pg.aux.p, pg.starts.p, pg.err.p};
+      HIPCHK(launch_pool_seg(sa, stream));
       HIPCHK(hipMemcpyAsync(pg.h_err.p, pg.err.p, 4, hipMemcpyDeviceToHost, stream));
       HIPCHK(hipMemcpyAsync(&pg.h_starts.p[P_], pg.starts.p + P_, 8, hipMemcpyDeviceToHost, stream));
       HIPCHK(hipStreamSynchronize(stream));
@@ -1852,10 +1839,9 @@ struct Ctx {
       const int werr = *pg.h_err.p;
       if (werr & 8) end = -1;
       if (!(werr & 8) && (werr & 4 || (debug & 268435456))) {
-        // a chunk did not meet its predecessor (or debug bit 28): the sequential walk
+        // the chain left a window (or debug bit 28): the sequential walk
         pg.walk_fallbacks++;
         stats.pool_walk_fallbacks++;
-        if (std::getenv("HDPM_POOL_TRACE") && !(debug & 268435456)) pool_walk_trace(chunks, C + M);
         pg.h_bm.ensure((size_t)nc * 2 * nwords);
         HIPCHK(hipMemcpyAsync(pg.h_bm.p, pg.bm.p, (size_t)nc * 2 * nwords * 8, hipMemcpyDeviceToHost, stream));
         HIPCHK(hipStreamSynchronize(stream));
@@ -2154,7 +2140,7 @@ struct Ctx {
     HIPCHK(launch_relabel(d_c.p, d_los.p, n, hctl, stream));
     if (track) {
       HIPCHK(launch_apply_moves(d_mlog.p, d_mcount.p, (int)std::min<int64_t>(n, 4096), d_codes_t.p, d, nq, mmax,
-                                d_freq.p, hctl, n, stream));
+                                d_freq.p, hctl, n, scap, stream));
       HIPCHK(launch_freq_gather(d_freq.p, d_sol.p, std::min(scap, nslots + 2), d * mmax, d_freq2.p, hctl, n, stream));
       const size_t fwords = (size_t)std::min(scap, nslots + 2) * d * mmax;
       h_freq_next.ensure(fwords);
@@ -3264,6 +3250,14 @@ struct Ctx {
     int tree_min_count = 16;
     PinBuf<uint8_t> h_in, h_out;
     double p_rej = 0.12;               // rbeta attempts rejected (window model), adapted per call
+    double p_rej_sm = 0.12;            // the same for split-merge's one- or two-cluster updates
+    // the estimate after an update with `drift` extra uniforms over `items` draws; a window
+    // the drift left (kPhiShort / kPhiWindow) widens the next one
+    static void adapt(double& p, int64_t drift, int64_t items) {
+      const double ph = (double)drift / ((double)drift + 2.0 * (double)items);
+      p = std::min(0.9, std::max(0.02, 0.7 * p + 0.3 * ph));
+    }
+    static void widen(double& p) { p = std::min(0.9, 1.5 * p + 0.05); }
     int64_t calls = 0, fallbacks = 0;
     int last_status = 0;
   } phd;
@@ -3330,11 +3324,11 @@ struct Ctx {
     bool tree_ok = false;
     int tW = 0, tnb = 0, tSB = 0, tS = 0, tpc = 0, root_lds = 0;
   };
-  PhiPlan phi_plan(int T) const {
+  PhiPlan phi_plan(int T, bool sm = false) const {
     PhiPlan pl;
     if (T <= 0 || d > 2048) return pl;
     pl.T = T;
-    const double p = phd.p_rej;
+    const double p = sm ? phd.p_rej_sm : phd.p_rej;
     pl.rate = 2 * p / (1 - p);
     pl.sdev = 2 * std::sqrt(p) / (1 - p);
     pl.items = (int64_t)T * d;
@@ -3523,6 +3517,7 @@ struct Ctx {
       stats.phi_device_fallbacks++;
       stats.phi_fallback_status_mask |= (int64_t)1 << (status != kPhiOk ? std::min(std::max(status, 0), 14) : 15);
       if (status == kPhiOk) stats.phi_device_last_status = -1;
+      if (status == kPhiShort || status == kPhiWindow) PhiDevice::widen(phd.p_rej);
       return -1;
     }
     stats.phi_device_calls++;
@@ -3552,9 +3547,7 @@ struct Ctx {
     stage_full = false;                // the host staging no longer mirrors the device tables
     adopt_state_at(*W, target);
     // the drift model follows the chain: extra uniforms per sigma draw seen here
-    const double drift = (double)(cons - 3 * items);
-    const double ph = drift / (drift + 2.0 * (double)items);
-    phd.p_rej = std::min(0.3, std::max(0.05, 0.7 * phd.p_rej + 0.3 * ph));
+    PhiDevice::adapt(phd.p_rej, cons - 3 * items, items);
     stats.t_host_phi_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp0).count();
     return kOk;
   }
@@ -3701,6 +3694,7 @@ struct Ctx {
       phd.fallbacks++;
       stats.phi_device_fallbacks++;
       stats.phi_fallback_status_mask |= (int64_t)1 << (status != kPhiOk ? std::min(std::max(status, 0), 14) : 15);
+      if (status == kPhiShort || status == kPhiWindow) PhiDevice::widen(phd.p_rej);
       return -1;
     }
     stats.phi_device_calls++;
@@ -3733,9 +3727,7 @@ struct Ctx {
     freq_next_pending = false;
     freq_version = labels_version;
     adopt_state_at(*dspec.W, target);
-    const double drift = (double)(cons - 3 * dspec.pl.items);
-    const double ph = drift / (drift + 2.0 * (double)dspec.pl.items);
-    phd.p_rej = std::min(0.3, std::max(0.05, 0.7 * phd.p_rej + 0.3 * ph));
+    PhiDevice::adapt(phd.p_rej, cons - 3 * dspec.pl.items, dspec.pl.items);
     return kOk;
   }
 
@@ -3750,7 +3742,7 @@ struct Ctx {
                            double* sig) {
     if (phi_mode == 0 || (debug & (524288 | 64)) || T <= 0 || d > 2048 || !glibc_selfcheck()) return -1;
     rng_sync();
-    const PhiPlan pl = phi_plan(T);
+    const PhiPlan pl = phi_plan(T, true);
     if (!pl.ok) return -1;
     RngWindow* W = window_at(rng.pos, pl.need);
     if (!W) return -1;
@@ -3822,6 +3814,11 @@ struct Ctx {
       stats.phi_device_fallbacks++;
       stats.phi_fallback_status_mask |= (int64_t)1 << (status != kPhiOk ? std::min(std::max(status, 0), 14) : 15);
       if (status == kPhiOk) stats.phi_device_last_status = -1;
+      if (std::getenv("HDPM_PHI_TRACE"))
+        std::fprintf(stderr, "[phi sm] T %d items %lld need %lld nw %d p_rej %.4f status %d cons %lld counts %d %d\n", T,
+                     (long long)items, (long long)pl.need, pl.nw, phd.p_rej_sm, status, (long long)cons, cnt[0],
+                     T > 1 ? cnt[1] : -1);
+      if (status == kPhiShort || status == kPhiWindow) PhiDevice::widen(phd.p_rej_sm);
       return -1;
     }
     stats.phi_device_calls++;
@@ -3831,9 +3828,7 @@ struct Ctx {
     std::memcpy(sig, phd.h_out.p + o_sig, (size_t)items * 8);
     adopt_state_at(*W, target);
     rng_sync();                        // split-merge draws on the host next
-    const double drift = (double)(cons - 3 * items);
-    const double ph = drift / (drift + 2.0 * (double)items);
-    phd.p_rej = std::min(0.3, std::max(0.05, 0.7 * phd.p_rej + 0.3 * ph));
+    PhiDevice::adapt(phd.p_rej_sm, cons - 3 * items, items);
     return kOk;
   }
 

@@ -2876,6 +2876,42 @@ __global__ __launch_bounds__(kWave) void k_apply_moves(const int* __restrict__ m
   }
 }
 
+// The same with the deltas of the first ls slots accumulated in LDS per workgroup (a
+// contiguous share of the move log each) and added once per changed counter: from a random
+// start half the points move per sweep, and per-move global atomics on the few thousand
+// counters of the tables serialised (3-4.6 ms per C5 sweep).  Moves of slots >= ls (past
+// the LDS budget) update the global tables directly.
+__global__ __launch_bounds__(256) void k_apply_moves_lds(const int* __restrict__ mlog, const int* __restrict__ mcount,
+                                                        const uint8_t* __restrict__ codes_t, int d, int nq, int mmax,
+                                                        unsigned int* freq, const ResolveCtl* ctl, int n, int ls) {
+  if (!sweep_done(ctl, n)) return;
+  const int nm = *mcount;
+  const int per = (nm + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int q0 = (int)blockIdx.x * per, q1 = min(nm, q0 + per);
+  if (q0 >= q1) return;
+  extern __shared__ int dl[];          // [ls][d * mmax] count changes
+  const int fs = d * mmax;
+  for (int e = threadIdx.x; e < ls * fs; e += blockDim.x) dl[e] = 0;
+  __syncthreads();
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, nwv = blockDim.x >> 6;
+  for (int q = q0 + wv; q < q1; q += nwv) {
+    const int64_t i = mlog[3 * q];
+    const int from = mlog[3 * q + 1], to = mlog[3 * q + 2];
+    for (int j = lane; j < d; j += kWave) {
+      const int off = j * mmax + a_code(codes_t, i, j, nq) - 1;
+      if (from < ls) atomicSub(&dl[from * fs + off], 1);
+      else atomicSub(freq + (int64_t)from * fs + off, 1u);
+      if (to < ls) atomicAdd(&dl[to * fs + off], 1);
+      else atomicAdd(freq + (int64_t)to * fs + off, 1u);
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < ls * fs; e += blockDim.x) {
+    const int v = dl[e];
+    if (v) atomicAdd(freq + e, (unsigned)v);
+  }
+}
+
 // freq per label after the sweep: out[l] = freq[slot_of_label[l]].
 __global__ void k_freq_gather(const unsigned int* __restrict__ freq, const int* __restrict__ sol, int fs,
                               unsigned int* __restrict__ out, const ResolveCtl* ctl, int n) {
@@ -3220,7 +3256,14 @@ hipError_t launch_relabel(int* c, const int* los, int n, const ResolveCtl* ctl, 
 }
 
 hipError_t launch_apply_moves(const int* mlog, const int* mcount, int grid, const uint8_t* codes_t, int d, int nq,
-                              int mmax, unsigned int* freq, const ResolveCtl* ctl, int n, hipStream_t s) {
+                              int mmax, unsigned int* freq, const ResolveCtl* ctl, int n, int nslots, hipStream_t s) {
+  // LDS deltas for the slots that fit 64 KB (C5: 32 of them; the sweep's slots are < nslots)
+  const int ls = std::min(nslots, (int)(64 * 1024 / ((size_t)d * mmax * 4)));
+  if (ls >= 2) {
+    hipLaunchKernelGGL(k_apply_moves_lds, dim3(512), dim3(256), (size_t)ls * d * mmax * 4, s, mlog, mcount, codes_t, d,
+                       nq, mmax, freq, ctl, n, ls);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_apply_moves, dim3(std::max(1, std::min(grid, 4096))), dim3(kWave), 0, s, mlog, mcount, codes_t,
                      d, nq, mmax, freq, ctl, n);
   return hipGetLastError();

@@ -2,6 +2,9 @@
 //
 //   k_pool_accept  every possible rbeta attempt of the slice, per attribute class, packed
 //                  per position parity (one wave = 128 stream positions, ballots)
+//   k_pool_seg*    the entry starts: every window candidate of every chunk walked to the next
+//                  chunk, the tables composed per group and chained, each chunk's entries
+//                  walked from its first start on the chain (pool_gen.hpp PoolSegPlan)
 //   k_pool_values  one wave per pool entry: centers, the entry's accepted attempts (wave
 //                  popcount scan + select over the packed words, run by run), sigma and
 //                  dhamming tables, bound record (kernels.hpp layout)
@@ -65,179 +68,96 @@ __global__ __launch_bounds__(256) void k_pool_accept(PoolAcceptArgs a) {
   }
 }
 
-// Position after the len-th accepted attempt at the parity of pos, from pos (B: that parity's
-// table), by one wave 64 words at a time; -1 past the tables (pool_select_run).
-__device__ __forceinline__ int64_t wave_select_run(const uint64_t* B, int64_t nwords, int64_t pos, int len) {
-  const int lane = threadIdx.x & 63;
-  const int par = (int)(pos & 1);
-  const int64_t slot = pos >> 1;
-  int64_t w = slot >> 6;
-  uint64_t fmask = ~0ull << (slot & 63);
-  int need = len;
-  for (;;) {
-    if (w >= nwords) return -1;
-    const int64_t wi = w + lane;
-    uint64_t word = wi < nwords ? B[wi] : 0ull;
-    if (lane == 0) word &= fmask;
-    const int cnt = __popcll(word);
-    const int incl = wave_incl_scan(cnt);
-    const int total = __shfl(incl, 63);
-    if (total >= need) {
-      const uint64_t reach = __ballot(incl >= need);
-      const int q = __ffsll((unsigned long long)reach) - 1;
-      const uint64_t wq = __shfl(word, q);
-      const int before = __shfl(incl - cnt, q);
-      return 2 * ((w + q) * 64 + pool_select64(wq, need - before - 1)) + par + 2;
+// Entry starts by segments (pool_gen.hpp PoolSegPlan).  k_pool_seg: a workgroup per chunk, a
+// thread per window candidate, walked to its first start in the next chunk (the candidates of a
+// window read the same few table words: L1 / L2 hits).
+__global__ __launch_bounds__(256) void k_pool_seg(PoolSegArgs a) {
+  const int64_t c = blockIdx.x;
+  for (int i = threadIdx.x; i < a.sp.ncand; i += blockDim.x)
+    a.T[c * a.sp.ncand + i] = pool_seg_cell(a.bm, a.nwords, a.d, a.R, a.sp, c, i);
+}
+
+// The tables of a group's chunks composed, one thread per candidate of the group's first window.
+__global__ __launch_bounds__(256) void k_pool_seg_group(PoolSegArgs a) {
+  const int64_t g = blockIdx.x;
+  const int64_t c0 = g * a.sp.G, c1 = min(a.sp.nchunks, c0 + a.sp.G);
+  for (int i = threadIdx.x; i < a.sp.ncand; i += blockDim.x) {
+    int idx = i, n = 0;
+    bool bad = false;
+    for (int64_t c = c0; c < c1; ++c) {
+      const uint32_t t = a.T[c * a.sp.ncand + idx];
+      if ((t & 0xFFFFu) == kSegBad) { bad = true; break; }
+      idx = (int)(t & 0xFFFFu);
+      n += (int)(t >> 16);
     }
-    need -= total;
-    w += 64;
-    fmask = ~0ull;
+    a.gj[g * a.sp.ncand + i] = bad ? -1 : idx;
+    a.gn[g * a.sp.ncand + i] = n;
   }
 }
 
-// One wave per chunk (pool_gen.hpp PoolWalkArgs): C + M entry starts from a guess.
-__global__ __launch_bounds__(256) void k_pool_walk(PoolWalkArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (g >= a.chunks) return;
-  const int64_t e0 = g * a.C;
-  const int L = a.C + a.M;
-  int64_t* out = a.walk + g * L;
-  int64_t pos = 0;
-  if (g > 0) {
-    const int par = (int)((e0 * a.d) & 1);
-    pos = (int64_t)((double)e0 * a.mu);
-    if (pos > a.count - 2) pos = a.count - 2;
-    if (pos < 0) pos = 0;
-    pos = (pos & ~(int64_t)1) | par;
+// The chain over the groups (one thread, one dependent load per group), from candidate 0 of
+// chunk 0; the group that holds entry P (or a broken cell) is unrolled per chunk here.
+__global__ __launch_bounds__(64) void k_pool_seg_top(PoolSegArgs a) {
+  if (threadIdx.x != 0) return;
+  const PoolSegPlan& sp = a.sp;
+  int idx = 0;
+  int64_t E = 0, gfin = sp.ngroups;
+  for (int64_t g = 0; g < sp.ngroups; ++g) {
+    const int32_t j = a.gj[g * sp.ncand + idx], n = a.gn[g * sp.ncand + idx];
+    a.cidx[g * sp.G] = idx;
+    a.cE[g * sp.G] = E;
+    if (j < 0 || E + n > a.P) {
+      gfin = g;
+      for (int64_t c = g * sp.G; c < min(sp.nchunks, (g + 1) * sp.G) && E <= a.P; ++c) {
+        a.cidx[c] = idx;
+        a.cE[c] = E;
+        const uint32_t t = a.T[c * sp.ncand + idx];
+        if ((t & 0xFFFFu) == kSegBad) break;
+        idx = (int)(t & 0xFFFFu);
+        E += t >> 16;
+      }
+      break;
+    }
+    idx = j;
+    E += n;
   }
-  for (int k = 0; k < L; ++k) {
-    if (lane == 0) out[k] = pos;
-    if (k + 1 == L) break;
-    pos += a.d;
-    for (int r = 0; r < a.nruns && pos >= 0; ++r)
-      pos = wave_select_run(a.bm + ((int64_t)a.run_cls[r] * 2 + (pos & 1)) * a.nwords, a.nwords, pos, a.run_len[r]);
-    if (pos < 0) {
-      if (lane == 0)
-        for (int k2 = k + 1; k2 < L; ++k2) out[k2] = -1;
+  a.aux[0] = gfin;
+  if (gfin == sp.ngroups) atomicOr(a.err, 8);
+}
+
+// Every chunk of the groups before the unrolled one: its first start on the chain.
+__global__ __launch_bounds__(256) void k_pool_seg_fill(PoolSegArgs a) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= a.aux[0]) return;
+  int idx = a.cidx[g * a.sp.G];
+  int64_t E = a.cE[g * a.sp.G];
+  for (int64_t c = g * a.sp.G; c < min(a.sp.nchunks, (g + 1) * a.sp.G); ++c) {
+    a.cidx[c] = idx;
+    a.cE[c] = E;
+    const uint32_t t = a.T[c * a.sp.ncand + idx];
+    idx = (int)(t & 0xFFFFu);
+    E += t >> 16;
+  }
+}
+
+// A thread per chunk on the chain: its entries walked from its first start and written; the
+// walk must end at the next chunk's first start (else the chain left a window: bit 2).
+__global__ __launch_bounds__(256) void k_pool_seg_emit(PoolSegArgs a) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.sp.nchunks || a.cidx[c] < 0) return;
+  const int64_t Xn = (c + 1) * a.sp.B;
+  int64_t p = c * a.sp.B + (int64_t)a.cidx[c] * a.sp.step, e = a.cE[c];
+  while (p < Xn) {
+    a.starts[e] = p;
+    if (e == a.P) return;
+    p = pool_entry_end(a.bm, a.nwords, a.d, a.R, p);
+    if (p < 0) {
+      atomicOr(a.err, 8);
       return;
     }
+    ++e;
   }
-}
-
-// One wave per chunk g >= 1: the first position of its walk found in chunk g - 1's walk (a
-// binary search per lane: both walks increase), hence rel[g] = k1 - k2 - C and the index k1 in
-// chunk g - 1's walk where chunk g's valid part starts.
-__global__ __launch_bounds__(256) void k_pool_meet(PoolWalkArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int64_t g = 1 + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (g >= a.chunks) return;
-  const int L = a.C + a.M;
-  const int64_t* prev = a.walk + (g - 1) * L;
-  const int64_t* own = a.walk + g * L;
-  int nprev = L;                       // prev's positions before its -1 marks (near the tables' end)
-  while (nprev > 0 && prev[nprev - 1] < 0) --nprev;
-  for (int k0 = 0; k0 < L; k0 += 64) {
-    const int k2 = k0 + lane;
-    int k1 = -1;
-    if (k2 < L) {
-      const int64_t x = own[k2];
-      if (x >= 0) {
-        int lo = 0, hi = nprev;        // first index with prev[idx] >= x
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (prev[mid] < x) lo = mid + 1;
-          else hi = mid;
-        }
-        if (lo < nprev && prev[lo] == x) k1 = lo;
-      }
-    }
-    const uint64_t b = __ballot(k1 >= 0);
-    if (b) {
-      const int q = __ffsll((unsigned long long)b) - 1;
-      const int K1 = __shfl(k1, q), K2 = k0 + q;
-      if (lane == 0) {
-        a.rel[g] = K1 - K2 - a.C;
-        a.a[g] = K1;                   // made an entry index by k_pool_scan
-      }
-      return;
-    }
-  }
-  if (lane == 0) {
-    a.rel[g] = 0;
-    a.a[g] = -1;
-    atomicOr(a.err, 4);
-  }
-}
-
-// One workgroup: delta_g = sum of rel over chunks 1..g; a_g = e_{g-1} + delta_{g-1} + k1_g, then
-// a running maximum (a walk that met its predecessor before that one met the true chain is
-// true only from where its predecessor is); a_0 = 0, a_chunks = P + 1.
-template <bool kMax>
-__device__ __forceinline__ long long block_scan(long long x, long long* carry, long long* wsum) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const long long t = __shfl_up(x, o);
-    if (lane >= o) x = kMax ? (t > x ? t : x) : x + t;
-  }
-  if (lane == 63) wsum[wid] = x;
-  __syncthreads();
-  long long before = *carry;
-  for (int w2 = 0; w2 < wid; ++w2) before = kMax ? (wsum[w2] > before ? wsum[w2] : before) : before + wsum[w2];
-  const long long r = kMax ? (x > before ? x : before) : before + x;
-  __syncthreads();
-  if (threadIdx.x == blockDim.x - 1) *carry = r;
-  __syncthreads();
-  return r;
-}
-
-__global__ __launch_bounds__(1024) void k_pool_scan(PoolWalkArgs a) {
-  __shared__ long long carry;
-  __shared__ long long wsum[16];
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
-  for (int64_t base = 0; base < a.chunks; base += blockDim.x) {
-    const int64_t g = base + threadIdx.x;
-    const long long dl = block_scan<false>((g >= 1 && g < a.chunks) ? (long long)a.rel[g] : 0, &carry, wsum);
-    if (g < a.chunks) a.delta[g] = dl;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
-  for (int64_t base = 0; base < a.chunks; base += blockDim.x) {
-    const int64_t g = base + threadIdx.x;
-    long long v = 0;
-    if (g >= 1 && g < a.chunks) {
-      const long long k1 = a.a[g];
-      v = k1 >= 0 ? (long long)((g - 1) * a.C) + a.delta[g - 1] + k1 : 0;
-    }
-    const long long r = block_scan<true>(v, &carry, wsum);
-    if (g >= 1 && g < a.chunks && a.a[g] >= 0) a.a[g] = r;
-  }
-  if (threadIdx.x == 0) {
-    a.a[0] = 0;
-    a.a[a.chunks] = a.P + 1;
-  }
-}
-
-// One wave per chunk g: entries [a_g, a_{g+1}) from its walk (walk index e - g C - delta_g).
-__global__ __launch_bounds__(256) void k_pool_place(PoolWalkArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (g >= a.chunks || (*a.err & 4)) return;
-  const int L = a.C + a.M;
-  const int64_t lo = a.a[g], hi = min(a.a[g + 1], a.P + 1);
-  const int64_t off = g * a.C + a.delta[g];          // the entry of walk index 0
-  const int64_t* w = a.walk + g * L;
-  if (lane == 0 && (lo < 0 || hi < lo)) atomicOr(a.err, 4);
-  for (int64_t e = max(lo, (int64_t)0) + lane; e < hi; e += 64) {
-    const int64_t k = e - off;
-    int64_t v = -1;
-    if (k >= 0 && k < L) v = w[k];
-    if (v < 0) atomicOr(a.err, (e == a.P && k >= 0 && k < L) ? 8 : 4);
-    a.starts[e] = v;
-  }
+  if (!(c + 1 < a.sp.nchunks && a.cidx[c + 1] == (p - Xn) / a.sp.step && a.cE[c + 1] == e)) atomicOr(a.err, 4);
 }
 
 // dynamic LDS: 512 table words, then per wave d doubles of sigma and 2d of tables
@@ -493,13 +413,16 @@ hipError_t launch_pool_accept(const PoolAcceptArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_pool_walk(const PoolWalkArgs& a, hipStream_t s) {
-  if (a.C < 1 || a.M < 1 || a.chunks < 1) return hipErrorInvalidValue;
-  const unsigned blocks = (unsigned)((a.chunks + 3) / 4);
-  hipLaunchKernelGGL(k_pool_walk, dim3(blocks), dim3(256), 0, s, a);
-  if (a.chunks > 1) hipLaunchKernelGGL(k_pool_meet, dim3((unsigned)((a.chunks - 1 + 3) / 4)), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(k_pool_scan, dim3(1), dim3(1024), 0, s, a);
-  hipLaunchKernelGGL(k_pool_place, dim3(blocks), dim3(256), 0, s, a);
+hipError_t launch_pool_seg(const PoolSegArgs& a, hipStream_t s) {
+  const PoolSegPlan& sp = a.sp;
+  if (sp.nchunks < 1 || sp.ncand < 1 || sp.ncand >= 0xFFFF || sp.B < 2 || sp.G < 1 || sp.nchunks > 0x7fffffff ||
+      sp.ngroups != (sp.nchunks + sp.G - 1) / sp.G)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_pool_seg, dim3((unsigned)sp.nchunks), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_pool_seg_group, dim3((unsigned)sp.ngroups), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_pool_seg_top, dim3(1), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(k_pool_seg_fill, dim3((unsigned)((sp.ngroups + 255) / 256)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_pool_seg_emit, dim3((unsigned)((sp.nchunks + 255) / 256)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -145,7 +145,7 @@ struct PoolRuns {
 };
 
 // Position after the len-th accepted attempt at parity(pos), from pos; -1 past the tables.
-inline int64_t pool_select_run(const uint64_t* B, int64_t nwords, int64_t pos, int len) {
+HDPM_HD inline int64_t pool_select_run(const uint64_t* B, int64_t nwords, int64_t pos, int len) {
   const int par = (int)(pos & 1);
   const int64_t slot = pos >> 1;
   int64_t w = slot >> 6;
@@ -161,20 +161,62 @@ inline int64_t pool_select_run(const uint64_t* B, int64_t nwords, int64_t pos, i
   }
 }
 
+// F(pos): where the entry that starts at pos ends (the next entry's start): D center
+// uniforms, then per run the len-th accepted attempt of its class; -1 past the tables.
+HDPM_HD inline int64_t pool_entry_end(const uint64_t* bm, int64_t nwords, int d, const PoolRuns& R, int64_t pos) {
+  pos += d;
+  for (int r = 0; r < R.n; ++r) {
+    pos = pool_select_run(bm + ((int64_t)R.cls[r] * 2 + (pos & 1)) * nwords, nwords, pos, R.len[r]);
+    if (pos < 0) return -1;
+  }
+  return pos;
+}
+
 // Entry starts (relative to the slice) for entries [e0, e1) from `pos` (the start of e0);
 // returns the position after entry e1 - 1, or -1 when the tables end first.
 inline int64_t pool_parse(const uint64_t* bm, int64_t nwords, int d, const PoolRuns& R, int64_t pos, int64_t e0,
                           int64_t e1, int64_t* starts) {
   for (int64_t e = e0; e < e1; ++e) {
     starts[e] = pos;
-    pos += d;
-    for (int r = 0; r < R.n; ++r) {
-      const int c = R.cls[r];
-      pos = pool_select_run(bm + ((int64_t)c * 2 + (pos & 1)) * nwords, nwords, pos, R.len[r]);
-      if (pos < 0) return -1;
-    }
+    pos = pool_entry_end(bm, nwords, d, R, pos);
+    if (pos < 0) return -1;
   }
   return pos;
+}
+
+// ------------------------------------------------------------------ entry starts by segments
+// s_{e+1} = F(s_e), s_0 = 0: a chain through the whole slice.  The slice is cut into chunks of
+// B positions.  The first start of the chain at or after chunk c's first position X_c lies in
+// the window [X_c, X_c + Lw) whenever every entry is shorter than Lw, so every candidate of the
+// window (every position, or every even one when D is even: all starts are then even) is
+// walked to its first start >= X_{c+1}:  T_c[i] = that start's candidate index in chunk c + 1's
+// window | entries walked << 16.  The chain is the path through the tables from candidate 0 of
+// chunk 0: composed per group of G chunks (one thread per candidate), followed over the groups
+// serially, unrolled per chunk, and each chunk then walks its entries from its true first
+// start and writes them.  Exact for any slice; an entry longer than Lw on the chain (beyond
+// 14 standard deviations) is reported and the host parses serially.
+struct PoolSegPlan {
+  int64_t B = 0;        // positions per chunk (even)
+  int step = 2;         // candidate spacing: 2 when D is even, else 1
+  int ncand = 0;        // candidates per window, < 0xFFFF
+  int64_t nchunks = 0;  // ceil(count / B)
+  int G = 64;           // chunks per group
+  int64_t ngroups = 0;
+};
+constexpr uint32_t kSegBad = 0xFFFFu;   // low half of a table cell: the walk left the tables / window
+
+// T_c[i] (see above)
+HDPM_HD inline uint32_t pool_seg_cell(const uint64_t* bm, int64_t nwords, int d, const PoolRuns& R,
+                                      const PoolSegPlan& sp, int64_t c, int i) {
+  const int64_t X = c * sp.B, Xn = X + sp.B;
+  int64_t p = X + (int64_t)i * sp.step;
+  uint32_t n = 0;
+  while (p < Xn) {
+    p = pool_entry_end(bm, nwords, d, R, p);
+    if (p < 0 || ++n >= 0xFFFFu) return kSegBad;
+  }
+  const int64_t j = (p - Xn) / sp.step;
+  return j < sp.ncand ? (uint32_t)j | (n << 16) : kSegBad;
 }
 
 #ifdef __HIPCC__
@@ -190,39 +232,23 @@ struct PoolAcceptArgs {
   int par_mask;            // bit p: the parity-p tables are read (d even: entries and runs all start even)
 };
 
-// The entry starts in parallel (k_pool_walk, k_pool_meet, k_pool_place).  Entry e + 1 starts
-// where the walk of entry e from its start ends: a deterministic function of the start.
-// Chunk g (nominal entries e_g = g C ..) is walked by one wave for C + M entries from a guess
-// of its start (e_g times the mean entry length, at the parity every start of e_g has:
-// (e_g d) mod 2).  Walks from different starts coalesce: at a run's start two walks go to
-// the same accepted attempt unless an accepted attempt of the run's class lies between them,
-// so the walks between a guess and the true start merge into one within ~100 entries (one in
-// eight neighbours merges per run at C5's acceptance rate).  A walk from a guess is the true
-// chain, shifted by an unknown number of entries delta_g, from the first position it shares
-// with the (true) walk before it: chunk g's walk meets chunk g - 1's at walk indices k2 / k1,
-// so delta_g = delta_{g-1} + k1 - k2 - C (delta_0 = 0, chunk 0 starts at 0) -- a prefix sum
-// over the chunks -- and chunk g's walk is valid for the entries from
-// a_g = e_{g-1} + delta_{g-1} + k1 on.  Entry e takes the walk of the last chunk with a_g <= e.
-// A chunk that does not meet its predecessor within its walk is reported (err bit 2) and the
-// host parses serially; a walk that runs off the tables marks its remaining positions -1.
-struct PoolWalkArgs {
+// The entry starts by segments (k_pool_seg, k_pool_seg_group, k_pool_seg_top, k_pool_seg_fill,
+// k_pool_seg_emit; see PoolSegPlan above).
+struct PoolSegArgs {
   const uint64_t* bm;
   int64_t nwords;
   int d;
-  int nruns;
-  const int* run_cls;
-  const int* run_len;
+  PoolRuns R;              // device arrays
+  PoolSegPlan sp;
   int64_t P;
-  int C, M;                // nominal entries per chunk, extra entries walked
-  double mu;               // mean entry length (the chunk starts' guesses)
-  int64_t count;
-  int64_t chunks;          // P / C + 1
-  int64_t* walk;           // [chunks][C + M] the walk of each chunk (positions, increasing; -1 past the tables)
-  int* rel;                // [chunks] delta_g - delta_{g-1}
-  int64_t* a;              // [chunks + 1] first entry of chunk g's valid part (a_0 = 0, a_chunks = P + 1)
-  int64_t* delta;          // [chunks]
+  uint32_t* T;             // [nchunks][ncand]
+  int32_t* gj;             // [ngroups][ncand] the group's composed next index (-1: a broken cell)
+  int32_t* gn;             // [ngroups][ncand] entries over the group
+  int32_t* cidx;           // [nchunks] the chain's first start in chunk c (candidate index; -1: not on it)
+  int64_t* cE;             // [nchunks] its entry index
+  int64_t* aux;            // [1] the group unrolled by k_pool_seg_top (ngroups: none)
   int64_t* starts;         // [P + 1]
-  int* err;                // bit 2: a chunk did not meet its predecessor; bit 3: the tables ended before entry P
+  int* err;                // bit 2: the chain left a window (serial host parse); bit 3: the tables end before entry P
 };
 
 struct PoolValueArgs {
@@ -248,7 +274,7 @@ struct PoolValueArgs {
 
 hipError_t launch_pool_accept(const PoolAcceptArgs& a, hipStream_t s);
 hipError_t launch_pool_values(const PoolValueArgs& a, hipStream_t s);
-hipError_t launch_pool_walk(const PoolWalkArgs& a, hipStream_t s);
+hipError_t launch_pool_seg(const PoolSegArgs& a, hipStream_t s);
 #endif
 
 }  // namespace hdpm

@@ -83,6 +83,104 @@ inline int64_t pool_slice_len(const PoolPlan& pl, int64_t P, double extra = 1.0)
 
 // (mt_untemper: rmath.hpp)
 
+// Chunking of the segment parse (pool_gen.hpp PoolSegPlan): windows of Lw = mean + 14 sd +
+// 16 positions (one entry's length, with margin), ~128 entries per chunk, 64 chunks per group.
+inline PoolSegPlan pool_seg_plan(const PoolPlan& pl, int d, int64_t count) {
+  PoolSegPlan sp;
+  sp.step = (d % 2 == 0) ? 2 : 1;
+  int64_t Lw = (int64_t)std::ceil(pl.mean_len + 14.0 * std::sqrt(pl.var_len)) + 16;
+  Lw = (Lw + 1) & ~(int64_t)1;
+  sp.ncand = (int)(Lw / sp.step);
+  int64_t B = (int64_t)std::ceil(128.0 * pl.mean_len);
+  B = std::max(B, 2 * Lw);
+  sp.B = (B + 1) & ~(int64_t)1;
+  sp.nchunks = (count + sp.B - 1) / sp.B;
+  sp.G = 64;
+  sp.ngroups = (sp.nchunks + sp.G - 1) / sp.G;
+  return sp;
+}
+
+// Host model of the segment parse, step for step as the device kernels (pool.hip k_pool_seg*):
+// the entry starts [0, P] into starts; returns the position after entry P - 1, -1 when the
+// tables end before it, -2 when the chain leaves a window.
+inline int64_t pool_parse_segments(const uint64_t* bm, int64_t nwords, int d, const PoolRuns& R, const PoolSegPlan& sp,
+                                   int64_t P, int64_t* starts) {
+  const int64_t nc = sp.nchunks;
+  std::vector<uint32_t> T((size_t)nc * sp.ncand);
+  for (int64_t c = 0; c < nc; ++c)
+    for (int i = 0; i < sp.ncand; ++i) T[(size_t)c * sp.ncand + i] = pool_seg_cell(bm, nwords, d, R, sp, c, i);
+  std::vector<int32_t> gj((size_t)sp.ngroups * sp.ncand), gn(gj.size());
+  for (int64_t g = 0; g < sp.ngroups; ++g)          // k_pool_seg_group
+    for (int i = 0; i < sp.ncand; ++i) {
+      int idx = i, n = 0;
+      bool bad = false;
+      for (int64_t c = g * sp.G; c < std::min(nc, (g + 1) * sp.G); ++c) {
+        const uint32_t t = T[(size_t)c * sp.ncand + idx];
+        if ((t & 0xFFFFu) == kSegBad) { bad = true; break; }
+        idx = (int)(t & 0xFFFFu);
+        n += (int)(t >> 16);
+      }
+      gj[(size_t)g * sp.ncand + i] = bad ? -1 : idx;
+      gn[(size_t)g * sp.ncand + i] = n;
+    }
+  std::vector<int32_t> cidx(nc, -1);
+  std::vector<int64_t> cE(nc, 0);
+  int64_t gfin = sp.ngroups;                          // k_pool_seg_top
+  {
+    int idx = 0;
+    int64_t E = 0;
+    for (int64_t g = 0; g < sp.ngroups; ++g) {
+      const int32_t j = gj[(size_t)g * sp.ncand + idx], n = gn[(size_t)g * sp.ncand + idx];
+      cidx[g * sp.G] = idx;
+      cE[g * sp.G] = E;
+      if (j < 0 || E + n > P) {
+        gfin = g;
+        for (int64_t c = g * sp.G; c < std::min(nc, (g + 1) * sp.G) && E <= P; ++c) {
+          cidx[c] = idx;
+          cE[c] = E;
+          const uint32_t t = T[(size_t)c * sp.ncand + idx];
+          if ((t & 0xFFFFu) == kSegBad) break;
+          idx = (int)(t & 0xFFFFu);
+          E += t >> 16;
+        }
+        break;
+      }
+      idx = j;
+      E += n;
+    }
+    if (gfin == sp.ngroups) return -1;
+  }
+  for (int64_t g = 0; g < gfin; ++g) {                // k_pool_seg_fill
+    int idx = cidx[g * sp.G];
+    int64_t E = cE[g * sp.G];
+    for (int64_t c = g * sp.G; c < std::min(nc, (g + 1) * sp.G); ++c) {
+      cidx[c] = idx;
+      cE[c] = E;
+      const uint32_t t = T[(size_t)c * sp.ncand + idx];
+      idx = (int)(t & 0xFFFFu);
+      E += t >> 16;
+    }
+  }
+  int err = 0;
+  for (int64_t c = 0; c < nc; ++c) {                  // k_pool_seg_emit
+    if (cidx[c] < 0) continue;
+    const int64_t Xn = (c + 1) * sp.B;
+    int64_t p = c * sp.B + (int64_t)cidx[c] * sp.step, e = cE[c];
+    bool done = false;
+    while (p < Xn) {
+      starts[e] = p;
+      if (e == P) { done = true; break; }
+      p = pool_entry_end(bm, nwords, d, R, p);
+      if (p < 0) { err |= 8; done = true; break; }
+      ++e;
+    }
+    if (!done && !(c + 1 < nc && cidx[c + 1] == (p - Xn) / sp.step && cE[c + 1] == e)) err |= 4;
+  }
+  if (err & 8) return -1;
+  if (err & 4) return -2;
+  return starts[P];
+}
+
 // Host model of the device pipeline on `raw` (the slice): packed accept tables, parse,
 // values.  Returns the position after the P-th entry, or -1 on overrun.
 inline int64_t pool_model(const PoolPlan& pl, int d, const int32_t* att, const uint32_t* raw, int64_t count, int64_t P,

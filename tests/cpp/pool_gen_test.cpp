@@ -19,6 +19,29 @@ static int fails = 0;
     }                                                                   \
   } while (0)
 
+// the segment parse (pool_parse_segments, the device's k_pool_seg* step for step) against the
+// sequential walk, on the packed tables of the slice
+static void check_segments(const char* name, const PoolPlan& pl, int d, const std::vector<uint32_t>& raw, int64_t P) {
+  const int64_t count = (int64_t)raw.size();
+  const int nc = (int)pl.cls.size();
+  const int64_t nwords = (count + 127) / 128;
+  std::vector<uint64_t> bm((size_t)nc * 2 * nwords, 0);
+  for (int64_t p = 0; p + 1 < count; ++p)
+    for (int c = 0; c < nc; ++c)
+      if (pool_accept(pl.cls[c], pool_unif(raw[p]), pool_unif(raw[p + 1]), glibc::kGlibcExpTab, glibc::kGlibcLogTab))
+        bm[((size_t)c * 2 + (p & 1)) * nwords + ((p >> 1) >> 6)] |= 1ull << ((p >> 1) & 63);
+  PoolRuns R{(int)pl.run_cls.size(), pl.run_cls.data(), pl.run_len.data()};
+  std::vector<int64_t> s0(P + 1), s1(P + 1, -7);
+  const int64_t e0 = pool_parse(bm.data(), nwords, d, R, 0, 0, P, s0.data());
+  s0[P] = e0;
+  const PoolSegPlan sp = pool_seg_plan(pl, d, count);
+  const int64_t e1 = pool_parse_segments(bm.data(), nwords, d, R, sp, P, s1.data());
+  CHECK(e0 >= 0 && e1 == e0);
+  CHECK(s0 == s1);
+  std::printf("%s: segments B=%lld step=%d ncand=%d chunks=%lld groups=%lld %s\n", name, (long long)sp.B, sp.step,
+              sp.ncand, (long long)sp.nchunks, (long long)sp.ngroups, (e1 == e0 && s0 == s1) ? "ok" : "MISMATCH");
+}
+
 static void run_case(const char* name, const std::vector<int32_t>& att, const std::vector<double>& v,
                      const std::vector<double>& w, int64_t P, int pre, uint32_t seed) {
   const int d = (int)att.size();
@@ -52,6 +75,7 @@ static void run_case(const char* name, const std::vector<int32_t>& att, const st
   CHECK(end == (int64_t)used);
   CHECK(std::memcmp(c0.data(), c1.data(), c0.size()) == 0);
   CHECK(std::memcmp(s0.data(), s1.data(), s0.size() * 8) == 0);
+  check_segments(name, pl, d, raw, P);
   std::printf("%s: P=%lld d=%d classes=%zu runs=%zu draws=%llu (%.1f per entry, estimate %.1f) %s\n", name,
               (long long)P, d, pl.cls.size(), pl.run_cls.size(), (unsigned long long)used, (double)used / P,
               pl.mean_len, end == (int64_t)used ? "ok" : "MISMATCH");
@@ -97,6 +121,12 @@ int main() {
     std::vector<int32_t> att(784, 6);
     std::vector<double> v(784, 3.0), w(784, 0.5);
     run_case("c4-like", att, v, w, 200, 300, 13u);
+  }
+  // C5-like: one class, D = 128 (the bench pool's shape), enough entries for several groups
+  {
+    std::vector<int32_t> att(128, 4);
+    std::vector<double> v(128, 6.0), w(128, 0.25);
+    run_case("c5-like", att, v, w, 20000, 77, 9u);
   }
   if (fails) return 1;
   std::printf("pool pipeline ok\n");

@@ -14,6 +14,8 @@ HDPM_E_GSL for clusters of ~1.4k+ members), so both sides run with the log-space
 HDPM_OPT_HIG_LOGSPACE; that part is parity with the oracle's mirror of the
 extension, not with the reference.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -99,6 +101,8 @@ def test_c3_full_size_neal8_and_split_merge(hd, oracle, phi_device):
     """C3: N = 100,000, D = 64, m_j ~ U{2..6}, K = 20: Neal-8 + split-merge; with phi_device,
     update_phi on the device (BASELINE config C3: "hyperg phi-update on device")."""
     oracle.set_hig_logspace(True)
+    if phi_device:
+        os.environ["HDPM_PHI_TRACE"] = "1"        # a split-merge update handed back prints why
     try:
         ds, eng, ost, rng, pc, ps = start(hd, oracle, "c3", seed=2, hig_log=True, phi_device=phi_device)
         assert ds.n == 100_000 and ds.d == 64

@@ -511,7 +511,6 @@ def test_device_mt_stream_jump_ahead_matches_r(hd, oracle, zoo, pre):
 
 # ------------------------------------------------------------------ latent pool generator
 def _pool_case(hd, oracle, ds, v, w, P, pre, seed, debug=0):
-    os.environ["HDPM_POOL_TRACE"] = "1"           # a walk fallback lists its chunks on stderr
     eng = hd.Engine(0)
     eng.set_data(ds.codes, ds.attrisize, ds.gamma, v, w)
     eng.set_debug(debug)
@@ -535,7 +534,7 @@ def test_device_pool_matches_oracle_zoo(hd, oracle, zoo, pre):
     assert st["pool_device_calls"] == 1
 
 
-# c5_large: 200k entries (391 chunks of the parallel walk, k_pool_walk); serial_parse: debug
+# c5_large: 200k entries (~1,560 chunks / 25 groups of the segment parse, k_pool_seg*); serial_parse: debug
 # bit 28, the entry starts by the sequential host walk over the device's acceptance tables
 @pytest.mark.parametrize("case", ["mixed_levels", "odd_d_bc", "c5_like", "c5_large", "serial_parse", "host_forced"])
 def test_device_pool_matches_oracle_synthetic(hd, oracle, case):
@@ -556,7 +555,7 @@ def test_device_pool_matches_oracle_synthetic(hd, oracle, case):
     st = _pool_case(hd, oracle, ds, v, w, P, 77, 9, debug=debug)
     assert st["pool_device_calls"] == (0 if case == "host_forced" else 1)
     if case != "host_forced":
-        # the parallel walk's chunks met (no serial fallback) unless the serial walk was forced
+        # the segment parse's chain stayed in its windows (no serial fallback) unless forced
         assert st["pool_walk_fallbacks"] == (1 if case == "serial_parse" else 0), \
             {k: st[k] for k in ("pool_walk_fallbacks", "pool_device_calls", "t_pool_parse_ms")}
 
