@@ -93,6 +93,8 @@ typedef struct {
     /* bit s set: a device update_phi was handed back with PhiStatus s (bit 15: the status was
      * ok but the stream position could not be adopted) */
     int64_t phi_fallback_status_mask;
+    /* split-merge device updates re-run with a wider drift window (the drift left the first) */
+    int64_t phi_sm_window_retries;
 } hdpm_stats;
 
 int         hdpm_device_count(void);

@@ -66,7 +66,8 @@ class Stats(C.Structure):
                                   "phi_lookahead_hits", "phi_lookahead_copies", "pipe_enqueued", "pipe_runs",
                                   "pipe_refused", "pipe_recovered", "phi_tree_calls", "phi_tree_retries",
                                   "pool_walk_fallbacks", "phi_dspec_launched", "phi_dspec_used",
-                                  "fpg_launches", "phi_sm_device_calls", "phi_fallback_status_mask")]
+                                  "fpg_launches", "phi_sm_device_calls", "phi_fallback_status_mask",
+                                  "phi_sm_window_retries")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -728,6 +728,7 @@ struct Ctx {
   bool last_fp = false;        // the last resolver launch was k_resolve_fp (diagnostics)
   int last_exact = 0;         // points the previous resolver launch decided one by one (block-mode choice)
   int last_listed = -1;       // points the previous launch's prepass listed (exact-rows grid), -1 unknown
+  double last_density = -1;   // ... per point of the range it covered (a restart covers the sweep's rest)
   bool last_unsettled = false;  // the previous launch exceeded its drift budget or restarted
 
   // latent pool
@@ -788,7 +789,7 @@ struct Ctx {
   DevBuf<unsigned> d_hist_part;
   DevBuf<long long> d_rprof;          // resolver phase times (debug mode bit 1)
   DevBuf<int> d_fpg;                   // k_resolve_fpg's cross-workgroup scratch
-  DevBuf<int> d_wide_ctr;              // k_prepass_wide's chunk counter
+  DevBuf<int> d_wide_ctr;              // k_prepass_wide's chunk counter, k_exact_rows_mass's point counter
   int fpg_grid_cache[65] = {0};        // its resident grid per resolver slot capacity (0: unknown, -1: none)
   PinBuf<int> h_ctl;                  // two blocks [ResolveCtl | pad to kCtlInts][resolver summary: 3 scap]
   // Consecutive sweeps alternate between the two control blocks (and resolver events), so a
@@ -1980,6 +1981,9 @@ struct Ctx {
     const double dmax = 0.25;
     if (cpar < 0) cpar = par;
     ensure_slots(nslots + 2);
+    // points this launch will likely list: the previous launch's density over [p, n) (a
+    // restart late in a sweep lists few points; the next sweep's first launch lists many)
+    const int el = last_density < 0 ? -1 : (int)std::min<double>((double)n, last_density * (double)(n - p) + 0.5);
     // the resolver writes its control block and summary straight into host memory
     if (h_ctl.n < 2 * ctl_stride()) h_ctl.ensure(2 * ctl_stride(), hipHostMallocCoherent);
     for (auto& e : ev_res)
@@ -2019,7 +2023,7 @@ struct Ctx {
     // (the fixed-point resolver re-tests and restarts cheaply enough to keep the uniform
     // certification after many exact decisions; debug bit 24 lists every point there too)
     const bool fp_next = fp_eligible(K + m, std::min(scap, nslots + 2)) &&
-                         (last_listed < 0 || last_listed >= kFpMinListed || (debug & 33554432));
+                         (el < 0 || el >= kFpMinListed || (debug & 33554432));
     const bool many_exact = last_exact >= kResolveBlkMin && (!fp_next || (debug & 16777216));
     pa.dmax2 = ((debug & (1 | 262144)) || last_unsettled || many_exact) ? INFINITY : 2.0 * dmax;
     pa.L = d_L.p; pa.rowpos = d_rowpos.p; pa.margin = d_margin.p; pa.list = d_list.p; pa.cnt = d_cnt.p;
@@ -2029,12 +2033,13 @@ struct Ctx {
     pa.rq = d_rq.p;
     pa.p0 = p;
     pa.exact_wave = (debug & 2048) ? 1 : 0;
-    pa.exact_grid = last_listed < 0 ? 0 : std::min(1024, std::max(64, 4 * last_listed + 64));
+    pa.exact_grid = el < 0 ? 0 : std::min(1536, std::max(64, el + 64));
+    pa.exact_scan = el >= 4096 ? 1 : 0;
     pa.wide = (debug & 16384) ? 0 : 1;
     pa.zero = nullptr;
-    d_wide_ctr.ensure(1);
+    d_wide_ctr.ensure(2);
     pa.wide_ctr = d_wide_ctr.p;      // cleared by k_cluster_summary (below: K > 0)
-    if (K == 0 && part != kRoundResolve) HIPCHK(hipMemsetAsync(d_wide_ctr.p, 0, 4, stream));
+    if (K == 0 && part != kRoundResolve) HIPCHK(hipMemsetAsync(d_wide_ctr.p, 0, 8, stream));
     if (mcount_clear && part != kRoundResolve) {
       if (K > 0) pa.zero = d_mcount.p;
       else HIPCHK(hipMemsetAsync(d_mcount.p, 0, 4, stream));
@@ -2096,7 +2101,7 @@ struct Ctx {
     // block modes; bits 12 / 13 select those modes and keep them)
     // (a launch whose predecessor listed only a few points -- a converged chain -- keeps the
     // one-wave LIST resolver: its fixed cost is half the fixed-point kernel's, ~7 vs ~13 us at C5)
-    ra.fp = (fp_eligible(K + m, ra.lcap) && (last_listed < 0 || last_listed >= kFpMinListed || (debug & 33554432)))
+    ra.fp = (fp_eligible(K + m, ra.lcap) && (el < 0 || el >= kFpMinListed || (debug & 33554432)))
                 ? 1 : 0;
     if (ra.fp) ra.blocks = 0;
     ra.debug_fp = (debug & 67108864) ? 1 : 0;
@@ -2104,14 +2109,14 @@ struct Ctx {
     // points: one 512-point chunk per workgroup, a workgroup per CU (debug bit 29: one workgroup)
     ra.fpg = 0;
     ra.fpg_buf = nullptr;
-    if (ra.fp && (last_listed >= kFpgMinListed || (debug & 1073741824)) && !(debug & 536870912) && ra.lcap <= 64) {
+    if (ra.fp && (el >= kFpgMinListed || (debug & 1073741824)) && !(debug & 536870912) && ra.lcap <= 64) {
       int& mg = fpg_grid_cache[ra.lcap];
       if (mg == 0) {
         mg = resolve_fpg_max_grid(ra.lcap, m);
         if (mg < 2) mg = -1;
       }
       if (mg > 0 && resolve_fpg_smem_bytes(ra.lcap, m) <= 160 * 1024) {
-        const int G = std::min(mg, std::max(2, (std::max(last_listed, 0) + 511) / 512));
+        const int G = std::min(mg, std::max(2, (std::max(el, 0) + 511) / 512));
         d_fpg.ensure(fpg_words(G));
         HIPCHK(hipMemsetAsync(d_fpg.p, 0, 16, stream));
         ra.fpg = G;
@@ -2523,6 +2528,8 @@ struct Ctx {
       stats.listed_points += c.listed;
       last_exact = c.exact;
       last_listed = c.listed;
+      // a sweep's first launch sets the density (a restart's tail of the sweep is not typical)
+      if (p == 0 || last_density < 0) last_density = (double)c.listed / (double)std::max(1, n - p);
       stats.moves += c.moves;
       sweep_moves += c.moves;
       stats.checked_rounds += c.checked;
@@ -3742,6 +3749,22 @@ struct Ctx {
                            double* sig) {
     if (phi_mode == 0 || (debug & (524288 | 64)) || T <= 0 || d > 2048 || !glibc_selfcheck()) return -1;
     rng_sync();
+    // a drift past the window (a merged or freshly split cluster can reject far more attempts
+    // than the chain's updates; nothing was consumed) is retried with a wider window
+    for (int attempt = 0;; ++attempt) {
+      const int r = device_update_phi_sm_once(T, cnt, freq, sig_in, cen, sig);
+      if (r == 1 && attempt >= 2) {
+        phd.fallbacks++;
+        stats.phi_device_fallbacks++;
+        return -1;
+      }
+      if (r != 1) return r;
+      stats.phi_sm_window_retries++;
+    }
+  }
+  // kOk, -1 (handed back), or 1: the drift left the window (widened for the next attempt)
+  int device_update_phi_sm_once(int T, const int* cnt, const unsigned* freq, const double* sig_in, uint8_t* cen,
+                                double* sig) {
     const PhiPlan pl = phi_plan(T, true);
     if (!pl.ok) return -1;
     RngWindow* W = window_at(rng.pos, pl.need);
@@ -3810,15 +3833,23 @@ struct Ctx {
     std::memcpy(&cons, phd.h_out.p + 8, 8);
     const uint64_t target = rng.pos + (uint64_t)cons;
     if (status != kPhiOk || cons <= 0 || !can_adopt(*W, target)) {
-      phd.fallbacks++;
-      stats.phi_device_fallbacks++;
       stats.phi_fallback_status_mask |= (int64_t)1 << (status != kPhiOk ? std::min(std::max(status, 0), 14) : 15);
       if (status == kPhiOk) stats.phi_device_last_status = -1;
+      if (status != kPhiShort && status != kPhiWindow) {
+        phd.fallbacks++;
+        stats.phi_device_fallbacks++;
+      }
       if (std::getenv("HDPM_PHI_TRACE"))
         std::fprintf(stderr, "[phi sm] T %d items %lld need %lld nw %d p_rej %.4f status %d cons %lld counts %d %d\n", T,
                      (long long)items, (long long)pl.need, pl.nw, phd.p_rej_sm, status, (long long)cons, cnt[0],
                      T > 1 ? cnt[1] : -1);
-      if (status == kPhiShort || status == kPhiWindow) PhiDevice::widen(phd.p_rej_sm);
+      if (status == kPhiShort || status == kPhiWindow) {
+        const double p0 = phd.p_rej_sm;
+        PhiDevice::widen(phd.p_rej_sm);
+        if (phd.p_rej_sm > p0) return 1;   // a wider window is worth another try
+        phd.fallbacks++;
+        stats.phi_device_fallbacks++;
+      }
       return -1;
     }
     stats.phi_device_calls++;

@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 
 #include "glibc_math.hpp"
 #include "kernels.hpp"
@@ -274,7 +275,10 @@ __global__ void k_cluster_summary(PrepassArgs a) {
   if (!pipe_gate(a)) return;
   if (blockIdx.x == 0 && threadIdx.x == 0) {     // memset dispatches less per sweep
     if (a.zero) *a.zero = 0;
-    if (a.wide_ctr) *a.wide_ctr = 0;
+    if (a.wide_ctr) {
+      a.wide_ctr[0] = 0;
+      a.wide_ctr[1] = 0;
+    }
   }
   const int sw = a.bw + 2;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < a.K * sw; e += gridDim.x * blockDim.x) {
@@ -801,6 +805,13 @@ static int wide_grid(F kern, size_t lds) {
   }
   int per = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, kWideThreads, lds) != hipSuccess || per <= 0) per = 1;
+  // HDPM_WIDE_WGS: workgroups per CU (A/B of the persistent grid; chunks are claimed from a
+  // counter, so workgroups beyond the resident ones only find the work gone)
+  static const int ovr = [] {
+    const char* e = std::getenv("HDPM_WIDE_WGS");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (ovr > 0 && ovr <= 32) per = ovr;
   return cus * per;
 }
 
@@ -1587,7 +1598,7 @@ template <int RE>
 __global__ __launch_bounds__(kExactWgThreads) void k_exact_rows_wg(PrepassArgs a) {
   if (!pipe_gate(a)) return;
   __shared__ int s_off[kExactWgThreads + 1];
-  const int total = exact_dense_scan(a, s_off);
+  const int total = a.exact_scan ? *a.dense_total : exact_dense_scan(a, s_off);
   if ((int)blockIdx.x >= total) return;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ double lp[4 * kWave];
@@ -1602,7 +1613,7 @@ __global__ __launch_bounds__(kExactWgThreads) void k_exact_rows_wg(PrepassArgs a
   const int t = threadIdx.x, lane = t & 63;
   const int nj4 = (D + 3) >> 2;
   for (int q = blockIdx.x; q < total; q += gridDim.x) {
-    const int row = exact_dense_row(a, s_off, q);
+    const int row = a.exact_scan ? a.dense[q] : exact_dense_row(a, s_off, q);
     const int64_t i = a.list[row];
     const uint32_t* raw = a.raw + i * (a.m + 1);
     if (t == 0) a.rq[q] = make_int4(row, (int)i, a.c[i], (int)raw[a.m]);   // the resolver's inputs
@@ -3170,21 +3181,150 @@ static hipError_t launch_prepass_w(const PrepassArgs& a, int nblocks, hipStream_
   return hipGetLastError();
 }
 
+// Exact rows when nearly every point is listed (a chain from a random start: ~1M per C5 sweep;
+// the dense list comes from k_list_scan).  Persistent workgroups of 8 waves, a wave per point,
+// lane e per entry (E <= 64).  The K clusters' codes and tables are staged in LDS once per
+// workgroup; per point the wave gathers the m latent entries' selected table values (all
+// lanes, every load of a batch in flight) into LDS, then lane e adds its entry's D values in
+// attribute order (n8:47-49; bit-exact) from LDS and the wave draws the snapshot decision.
+constexpr int kMassWaves = 8;
+__host__ __device__ inline size_t exact_mass_lds_bytes(int K, int m, int d, int dp) {
+  return (size_t)K * 2 * d * 8 + (size_t)kMassWaves * m * d * 8 + (size_t)K * dp + (size_t)kMassWaves * dp;
+}
+
+__global__ __launch_bounds__(kWave * kMassWaves) void k_exact_rows_mass(PrepassArgs a) {
+  if (!pipe_gate(a)) return;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ double lp_w[kMassWaves][kWave];
+  __shared__ int lperm_w[kMassWaves][kWave];
+  __shared__ int lpick_w[kMassWaves];
+  const int K = a.K, m = a.m, E = K + m, D = a.d, dp = a.nq * 16;
+  double* ltab = (double*)smem;                                  // [K][2D]
+  double* lval0 = ltab + (size_t)K * 2 * D;                       // [waves][m][D]
+  uint8_t* lcode = (uint8_t*)(lval0 + (size_t)kMassWaves * m * D);  // [K][dp]
+  uint8_t* lx0 = lcode + (size_t)K * dp;                          // [waves][dp]
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  for (int q = tid; q < K * 2 * D; q += blockDim.x) {
+    const int e = q / (2 * D);
+    ltab[q] = a.slots.tab[(int64_t)a.slot_of_label[e] * 2 * D + (q - e * 2 * D)];
+  }
+  for (int q = tid; q < K * dp; q += blockDim.x) {
+    const int e = q / dp;
+    lcode[q] = a.slots.codes[(int64_t)a.slot_of_label[e] * dp + (q - e * dp)];
+  }
+  __syncthreads();
+  const int total = *a.dense_total;
+  double* lval = lval0 + (size_t)wv * m * D;
+  uint8_t* lx = lx0 + (size_t)wv * dp;
+  const bool clu = lane < K, on = lane < E;
+  const int col = clu ? a.slot_of_label[lane] : a.S + (lane - K);
+  // lane's row of values: a cluster's table (stride 2, the mismatch value selected by the code
+  // compare) or the wave's gathered latent values (stride 1)
+  const double* base = clu ? ltab + (size_t)lane * 2 * D : lval + (size_t)(on ? lane - K : 0) * D;
+  const int stride = clu ? 2 : 1;
+  const uint8_t* cl = lcode + (size_t)(clu ? lane : 0) * dp;
+  // points claimed one at a time from a counter (k_cluster_summary clears it): a workgroup
+  // that is not resident leaves its share to the others
+  int q = 0;
+  if (lane == 0) q = atomicAdd(a.wide_ctr + 1, 1);
+  q = __shfl(q, 0);
+  while (q < total) {
+    int qn = 0;
+    if (lane == 0) qn = atomicAdd(a.wide_ctr + 1, 1);
+    const int row = a.dense[q];
+    const int64_t i = a.list[row];
+    const uint32_t* raw = a.raw + i * (m + 1);
+    if (lane == 0) a.rq[q] = make_int4(row, (int)i, a.c[i], (int)raw[m]);   // the resolver's inputs
+    if (lane < a.nq) *(uint4*)(lx + lane * 16) = *(const uint4*)(a.codes_t + tiled_offset(i, lane * 16, a.nq));
+    wave_sync();
+    // latent values: (u, j) pairs over the lanes, a batch of 8 per lane with every load issued first
+    for (int b0 = 0; b0 < m * D; b0 += 8 * kWave) {
+      uint8_t cc[8];
+      double2 pr[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int idx = b0 + k * kWave + lane;
+        if (idx < m * D) {
+          const int u = idx / D, j = idx - u * D;
+          const int64_t pe = pick_entry(raw[u], a.P);
+          cc[k] = a.pool.codes[pe * dp + j];
+          pr[k] = *(const double2*)(a.pool.tab + (pe * D + j) * 2);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int idx = b0 + k * kWave + lane;
+        if (idx < m * D) {
+          const int u = idx / D, j = idx - u * D;
+          lval[u * D + j] = lx[j] != cc[k] ? pr[k].y : pr[k].x;
+        }
+      }
+    }
+    wave_sync();
+    // lane e's entry in attribute order (n8:47-49), 16 values loaded before they are added;
+    // padding past D adds +0.0, which leaves the sum unchanged
+    double acc = 0.0;
+    for (int j0 = 0; j0 < D; j0 += 16) {
+      const uint4 xw = *(const uint4*)(lx + j0);
+      const uint4 cw = clu ? *(const uint4*)(cl + j0) : xw;
+      const uint32_t dx[4] = {xw.x ^ cw.x, xw.y ^ cw.y, xw.z ^ cw.z, xw.w ^ cw.w};
+      double v[16];
+#pragma unroll
+      for (int b = 0; b < 16; ++b) {
+        const int j = j0 + b;
+        const int sel = ((dx[b >> 2] >> (8 * (b & 3))) & 0xffu) ? 1 : 0;
+        v[b] = j < D ? base[(size_t)j * stride + sel] : 0.0;
+      }
+#pragma unroll
+      for (int b = 0; b < 16; ++b) acc += v[b];
+    }
+    if (on) a.L[(int64_t)row * (a.S + m) + col] = acc;
+    double acc_r[1] = {acc};
+    exact_rows_decide<1>(a, q, i, raw, acc_r, lp_w[wv], lperm_w[wv], &lpick_w[wv]);
+    wave_sync();                       // lx / lval are rewritten by the next point
+    q = __shfl(qn, 0);
+  }
+}
+
+static int mass_grid(size_t lds) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  int per = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_exact_rows_mass, kWave * kMassWaves, lds) != hipSuccess ||
+      per <= 0)
+    per = 1;
+  // two per CU when their LDS fits the CU's 160 KB (points are claimed from a counter, so a
+  // workgroup that does not become resident only finds the list done)
+  const size_t tot = lds + sizeof(double) * kMassWaves * kWave + sizeof(int) * kMassWaves * (kWave + 1);
+  if (per < 2 && 2 * tot <= 160 * 1024) per = 2;
+  return cus * per;
+}
+
 hipError_t launch_exact_rows(const PrepassArgs& a0, int nblocks, hipStream_t s) {
   PrepassArgs a = a0;
   a.lblock = prepass_list_block(a);
   a.nlb = (a.n - a.p0 + a.lblock - 1) / a.lblock;
   const int E = a.K + a.m;
   const size_t lds = exact_wg_lds_bytes(E, a.d, a.nq * 16);
-  // the workgroup kernels scan the list themselves; the one-wave kernel needs k_list_scan
-  if (a.exact_wave || lds > kExactWgLdsMax || E > 4 * kWave)
+  // the workgroup kernels scan the list themselves unless it is long (exact_scan); the
+  // one-wave kernel needs k_list_scan
+  const bool wg = !a.exact_wave && lds <= kExactWgLdsMax && E <= 4 * kWave;
+  if (!wg) a.exact_scan = 1;
+  if (a.exact_scan)
     hipLaunchKernelGGL(k_list_scan, dim3(1), dim3(kScanThreads), 0, s, a.cnt, a.nlb, a.lblock, a.dense,
                        a.dense_total);
-  // grid: the previous launch's list size sets a cap (a converged chain lists ~13 points per
-  // C5 sweep, so 1024 mostly idle workgroups were launched); a longer list is looped over
-  const int gx = std::min(nblocks * 4, 1024);
-  const dim3 g(a.exact_grid > 0 ? std::min(gx, a.exact_grid) : gx), b(kExactWgThreads);
-  const bool wg = !a.exact_wave && lds <= kExactWgLdsMax;
+  // grid: from the previous launch's list size (a converged chain lists ~13 points per C5
+  // sweep; a random start ~1M, looped over by every resident workgroup)
+  const dim3 g(a.exact_grid > 0 ? a.exact_grid : std::min(nblocks * 4, 1024)), b(kExactWgThreads);
+  const size_t mlds = exact_mass_lds_bytes(a.K, a.m, a.d, a.nq * 16);
+  if (a.exact_scan && !a.exact_wave && E <= kWave && mlds <= 96 * 1024) {
+    hipLaunchKernelGGL(k_exact_rows_mass, dim3(mass_grid(mlds)), dim3(kWave * kMassWaves), mlds, s, a);
+    return hipGetLastError();
+  }
   if (wg && E <= kWave) hipLaunchKernelGGL(k_exact_rows_wg<1>, g, b, lds, s, a);
   else if (wg && E <= 4 * kWave) hipLaunchKernelGGL(k_exact_rows_wg<4>, g, b, lds, s, a);
   else hipLaunchKernelGGL(k_exact_rows, dim3(std::min(nblocks, 1024)), dim3(kWave * kExactWaves), 0, s, a);

