@@ -782,7 +782,7 @@ struct Ctx {
   int Ecap = 0;
   DevBuf<double> d_margin;
   DevBuf<int> d_rowpos;
-  DevBuf<int> d_list, d_cnt, d_dense, d_dense_total, d_spec;
+  DevBuf<int> d_list, d_cnt, d_dense, d_dense_total, d_spec, d_boff;
   DevBuf<double> d_spec_rad;
   DevBuf<int4> d_rq;
   DevBuf<uint64_t> d_csum;            // per-label cluster summary for the prepass
@@ -1950,6 +1950,7 @@ struct Ctx {
     d_rowpos.ensure(n);
     d_list.ensure((size_t)nb_max * kBlock);
     d_cnt.ensure((size_t)nb_max * (kBlock / 16));   // list blocks of 16 points (k_prepass_wide chunks)
+    d_boff.ensure((size_t)nb_max * (kBlock / 16));
     d_dense.ensure((size_t)nb_max * kBlock);
     d_dense_total.ensure(1);
     d_spec.ensure((size_t)nb_max * kBlock);
@@ -2027,7 +2028,7 @@ struct Ctx {
     const bool many_exact = last_exact >= kResolveBlkMin && (!fp_next || (debug & 16777216));
     pa.dmax2 = ((debug & (1 | 262144)) || last_unsettled || many_exact) ? INFINITY : 2.0 * dmax;
     pa.L = d_L.p; pa.rowpos = d_rowpos.p; pa.margin = d_margin.p; pa.list = d_list.p; pa.cnt = d_cnt.p;
-    pa.dense = d_dense.p; pa.dense_total = d_dense_total.p;
+    pa.dense = d_dense.p; pa.dense_total = d_dense_total.p; pa.boff = d_boff.p;
     pa.spec = (debug & 8) ? nullptr : d_spec.p;
     pa.spec_rad = d_spec_rad.p;
     pa.rq = d_rq.p;

@@ -638,9 +638,11 @@ __global__ __launch_bounds__(kWideThreads) void k_prepass_wide(PrepassArgs a, in
     const bool on = tid < fn;
     const double mgp = on ? s_mg[pf_][tid] : -INFINITY;
     const int ocp = on ? s_oc[pf_][tid] : 0;
+    // the categorical draw from the chunk's staged draws (still in buffer pf_: the next chunk
+    // is staged there only after this); a global load here held the other waves at the barrier
     const bool uncertain =
         on && !(ocp >= 2 && (mgp > a.thresh ||
-                             stay_by_uniform(mgp - a.dmax2, a.raw[(f0 + tid) * m1 + a.m], a.K + a.m)));
+                             stay_by_uniform(mgp - a.dmax2, s_raw[pf_][(on ? tid : 0) * m1 + a.m], a.K + a.m)));
     const int64_t i = f0 + tid;
     if (on) a.margin[i] = mgp;
     const unsigned long long bal = __ballot(uncertain);
@@ -854,6 +856,56 @@ __global__ __launch_bounds__(kScanThreads) void k_list_scan(const int* __restric
     off += c;
   }
   if (tid == 0) *total = all;
+}
+
+// Long lists (~1M rows from a random start): the block offsets by one workgroup, then the
+// dense list written by a wave per list block, coalesced (k_list_scan's per-thread runs of
+// scattered stores cost ~0.3 ms at 1M rows).
+__global__ __launch_bounds__(kScanThreads) void k_list_offsets(const int* __restrict__ cnt, int nblocks,
+                                                              int* __restrict__ boff, int* __restrict__ total) {
+  __shared__ int s_sum[kScanThreads / kWave];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int chunk = (nblocks + kScanThreads - 1) / kScanThreads;
+  const int b0 = min(nblocks, tid * chunk), b1 = min(nblocks, b0 + chunk);
+  int mine = 0;
+  for (int b = b0; b < b1; ++b) mine += cnt[b];
+  int inc = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(inc, o);
+    if (lane >= o) inc += t;
+  }
+  if (lane == 63) s_sum[wv] = inc;
+  __syncthreads();
+  int base = 0, all = 0;
+#pragma unroll
+  for (int w = 0; w < kScanThreads / kWave; ++w) {
+    base += w < wv ? s_sum[w] : 0;
+    all += s_sum[w];
+  }
+  int off = base + inc - mine;
+  for (int b = b0; b < b1; ++b) {
+    boff[b] = off;
+    off += cnt[b];
+  }
+  if (tid == 0) *total = all;
+}
+
+// (rq: also the resolver's per-point records (row, point, slot, categorical draw), which
+// k_exact_rows_mass reads instead of walking row -> point -> label itself)
+__global__ __launch_bounds__(256) void k_list_fill(PrepassArgs a, int want_rq) {
+  if (!pipe_gate(a)) return;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (b >= a.nlb) return;
+  const int n = a.cnt[b], o = a.boff[b], m1 = a.m + 1;
+  for (int q = lane; q < n; q += kWave) {
+    const int row = b * a.lblock + q;
+    a.dense[o + q] = row;
+    if (want_rq) {
+      const int i = a.list[row];
+      a.rq[o + q] = make_int4(row, i, a.c[i], (int)a.raw[(int64_t)i * m1 + m1 - 1]);
+    }
+  }
 }
 
 // ------------------------------------------------------------------ resolver
@@ -3192,13 +3244,39 @@ __host__ __device__ inline size_t exact_mass_lds_bytes(int K, int m, int d, int 
   return (size_t)K * 2 * d * 8 + (size_t)kMassWaves * m * d * 8 + (size_t)K * dp + (size_t)kMassWaves * dp;
 }
 
+// exact_rows_decide with the launch's snapshot per entry in LDS: slot, count, log-counts
+__device__ __forceinline__ void mass_decide(const PrepassArgs& a, int q, int own, double acc, uint32_t rawm,
+                                            const int* s_sl, const int* s_cnt, const double* s_l0, const double* s_l1,
+                                            double* lp, int* lperm, int* lpick) {
+  const int lane = threadIdx.x & 63;
+  const int K = a.K, E = K + a.m;
+  const bool clu = lane < K;
+  const int s = clu ? s_sl[lane] : -1;
+  const unsigned long long bo = __ballot(clu && s == own);
+  const int lo = bo ? __ffsll((long long)bo) - 1 : 0;
+  const double ll_own = readlane_f64(acc, lo);
+  const int own_cnt = __shfl(clu ? s_cnt[lane] : 0, lo);
+  double v = -INFINITY;
+  if (clu) v = (s == own ? s_l0[lane] : s_l1[lane]) + acc;                         // n8:40-92
+  else if (lane < E) v = a.logfac + ((lane == K && own_cnt == 1) ? ll_own : acc);
+  double pv[1] = {v};
+  double rad = 0.0;
+  const int pick = decide_values<1>(pv, E, raw_to_unif(rawm), lp, lperm, lpick, &rad);
+  if (lane == 0) {
+    a.spec[q] = pick >= 0 ? pick : -1;
+    a.spec_rad[q] = rad;
+  }
+}
+
 __global__ __launch_bounds__(kWave * kMassWaves) void k_exact_rows_mass(PrepassArgs a) {
   if (!pipe_gate(a)) return;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ double lp_w[kMassWaves][kWave];
   __shared__ int lperm_w[kMassWaves][kWave];
   __shared__ int lpick_w[kMassWaves];
-  const int K = a.K, m = a.m, E = K + m, D = a.d, dp = a.nq * 16;
+  __shared__ int s_sl[kWave], s_cnt[kWave];
+  __shared__ double s_l0[kWave], s_l1[kWave];
+  const int K = a.K, m = a.m, E = K + m, D = a.d, dp = a.nq * 16, m1 = m + 1;
   double* ltab = (double*)smem;                                  // [K][2D]
   double* lval0 = ltab + (size_t)K * 2 * D;                       // [waves][m][D]
   uint8_t* lcode = (uint8_t*)(lval0 + (size_t)kMassWaves * m * D);  // [K][dp]
@@ -3212,77 +3290,93 @@ __global__ __launch_bounds__(kWave * kMassWaves) void k_exact_rows_mass(PrepassA
     const int e = q / dp;
     lcode[q] = a.slots.codes[(int64_t)a.slot_of_label[e] * dp + (q - e * dp)];
   }
+  if (tid < K) {
+    const int sl = a.slot_of_label[tid], c = a.counts[sl];
+    s_sl[tid] = sl;
+    s_cnt[tid] = c;
+    s_l1[tid] = a.logn[c];
+    s_l0[tid] = a.logn[c - 1];
+  }
   __syncthreads();
   const int total = *a.dense_total;
   double* lval = lval0 + (size_t)wv * m * D;
   uint8_t* lx = lx0 + (size_t)wv * dp;
   const bool clu = lane < K, on = lane < E;
-  const int col = clu ? a.slot_of_label[lane] : a.S + (lane - K);
+  const int col = clu ? s_sl[lane] : a.S + (lane - K);
   // lane's row of values: a cluster's table (stride 2, the mismatch value selected by the code
   // compare) or the wave's gathered latent values (stride 1)
   const double* base = clu ? ltab + (size_t)lane * 2 * D : lval + (size_t)(on ? lane - K : 0) * D;
   const int stride = clu ? 2 : 1;
   const uint8_t* cl = lcode + (size_t)(clu ? lane : 0) * dp;
-  // points claimed one at a time from a counter (k_cluster_summary clears it): a workgroup
-  // that is not resident leaves its share to the others
-  int q = 0;
-  if (lane == 0) q = atomicAdd(a.wide_ctr + 1, 1);
-  q = __shfl(q, 0);
-  while (q < total) {
-    int qn = 0;
-    if (lane == 0) qn = atomicAdd(a.wide_ctr + 1, 1);
-    const int row = a.dense[q];
-    const int64_t i = a.list[row];
-    const uint32_t* raw = a.raw + i * (m + 1);
-    if (lane == 0) a.rq[q] = make_int4(row, (int)i, a.c[i], (int)raw[m]);   // the resolver's inputs
-    if (lane < a.nq) *(uint4*)(lx + lane * 16) = *(const uint4*)(a.codes_t + tiled_offset(i, lane * 16, a.nq));
-    wave_sync();
-    // latent values: (u, j) pairs over the lanes, a batch of 8 per lane with every load issued first
-    for (int b0 = 0; b0 < m * D; b0 += 8 * kWave) {
-      uint8_t cc[8];
-      double2 pr[8];
+  // batches of kMassBatch points claimed from a counter (k_cluster_summary clears it; a
+  // workgroup that is not resident leaves its share to the others); the batch's records
+  // (k_list_fill wrote them to rq) and stream draws are loaded together, one lane per word
+  constexpr int kMassBatch = 4;
+  for (;;) {
+    int q0 = 0;
+    if (lane == 0) q0 = atomicAdd(a.wide_ctr + 1, kMassBatch);
+    q0 = __shfl(q0, 0);
+    if (q0 >= total) break;
+    const int nb = min(kMassBatch, total - q0);
+    const int kq = lane >> 4, wq = lane & 15;                     // point of the batch, word
+    int4 rec = make_int4(0, 0, 0, 0);
+    if (kq < nb) rec = a.rq[q0 + kq];
+    uint32_t rw = 0;
+    if (kq < nb && wq < m1) rw = a.raw[(int64_t)rec.y * m1 + wq];
+    for (int k = 0; k < nb; ++k) {
+      const int q = q0 + k;
+      const int row = __shfl(rec.x, 16 * k), own = __shfl(rec.z, 16 * k);
+      const int64_t i = __shfl(rec.y, 16 * k);
+      const uint32_t rawm = (uint32_t)__shfl(rec.w, 16 * k);
+      if (lane < a.nq) *(uint4*)(lx + lane * 16) = *(const uint4*)(a.codes_t + tiled_offset(i, lane * 16, a.nq));
+      // latent values: (u, j) pairs over the lanes, a batch of 8 per lane with every load issued first
+      for (int b0 = 0; b0 < m * D; b0 += 8 * kWave) {
+        uint8_t cc[8];
+        double2 pr[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int idx = b0 + k * kWave + lane;
-        if (idx < m * D) {
-          const int u = idx / D, j = idx - u * D;
-          const int64_t pe = pick_entry(raw[u], a.P);
-          cc[k] = a.pool.codes[pe * dp + j];
-          pr[k] = *(const double2*)(a.pool.tab + (pe * D + j) * 2);
+        for (int t = 0; t < 8; ++t) {
+          const int idx = b0 + t * kWave + lane;
+          const int u = idx / D;
+          const uint32_t y = (uint32_t)__shfl((int)rw, 16 * k + min(u, m - 1));
+          if (idx < m * D) {
+            const int j = idx - u * D;
+            const int64_t pe = pick_entry(y, a.P);
+            cc[t] = a.pool.codes[pe * dp + j];
+            pr[t] = *(const double2*)(a.pool.tab + (pe * D + j) * 2);
+          }
+        }
+        wave_sync();                   // lx of this point is in
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const int idx = b0 + t * kWave + lane;
+          if (idx < m * D) {
+            const int u = idx / D, j = idx - u * D;
+            lval[u * D + j] = lx[j] != cc[t] ? pr[t].y : pr[t].x;
+          }
         }
       }
+      wave_sync();
+      // lane e's entry in attribute order (n8:47-49), 16 values loaded before they are added;
+      // padding past D adds +0.0, which leaves the sum unchanged
+      double acc = 0.0;
+      for (int j0 = 0; j0 < D; j0 += 16) {
+        const uint4 xw = *(const uint4*)(lx + j0);
+        const uint4 cw = clu ? *(const uint4*)(cl + j0) : xw;
+        const uint32_t dx[4] = {xw.x ^ cw.x, xw.y ^ cw.y, xw.z ^ cw.z, xw.w ^ cw.w};
+        double v[16];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int idx = b0 + k * kWave + lane;
-        if (idx < m * D) {
-          const int u = idx / D, j = idx - u * D;
-          lval[u * D + j] = lx[j] != cc[k] ? pr[k].y : pr[k].x;
+        for (int b = 0; b < 16; ++b) {
+          const int j = j0 + b;
+          const int sel = ((dx[b >> 2] >> (8 * (b & 3))) & 0xffu) ? 1 : 0;
+          v[b] = j < D ? base[(size_t)j * stride + sel] : 0.0;
         }
-      }
-    }
-    wave_sync();
-    // lane e's entry in attribute order (n8:47-49), 16 values loaded before they are added;
-    // padding past D adds +0.0, which leaves the sum unchanged
-    double acc = 0.0;
-    for (int j0 = 0; j0 < D; j0 += 16) {
-      const uint4 xw = *(const uint4*)(lx + j0);
-      const uint4 cw = clu ? *(const uint4*)(cl + j0) : xw;
-      const uint32_t dx[4] = {xw.x ^ cw.x, xw.y ^ cw.y, xw.z ^ cw.z, xw.w ^ cw.w};
-      double v[16];
 #pragma unroll
-      for (int b = 0; b < 16; ++b) {
-        const int j = j0 + b;
-        const int sel = ((dx[b >> 2] >> (8 * (b & 3))) & 0xffu) ? 1 : 0;
-        v[b] = j < D ? base[(size_t)j * stride + sel] : 0.0;
+        for (int b = 0; b < 16; ++b) acc += v[b];
       }
-#pragma unroll
-      for (int b = 0; b < 16; ++b) acc += v[b];
+      if (on) a.L[(int64_t)row * (a.S + m) + col] = acc;
+      if (a.spec) mass_decide(a, q, own, acc, rawm, s_sl, s_cnt, s_l0, s_l1, lp_w[wv], lperm_w[wv], &lpick_w[wv]);
+      wave_sync();                     // lx / lval are rewritten by the next point
     }
-    if (on) a.L[(int64_t)row * (a.S + m) + col] = acc;
-    double acc_r[1] = {acc};
-    exact_rows_decide<1>(a, q, i, raw, acc_r, lp_w[wv], lperm_w[wv], &lpick_w[wv]);
-    wave_sync();                       // lx / lval are rewritten by the next point
-    q = __shfl(qn, 0);
   }
 }
 
@@ -3313,10 +3407,16 @@ hipError_t launch_exact_rows(const PrepassArgs& a0, int nblocks, hipStream_t s) 
   // the workgroup kernels scan the list themselves unless it is long (exact_scan); the
   // one-wave kernel needs k_list_scan
   const bool wg = !a.exact_wave && lds <= kExactWgLdsMax && E <= 4 * kWave;
-  if (!wg) a.exact_scan = 1;
-  if (a.exact_scan)
+  if (a.exact_scan && a.boff) {
+    hipLaunchKernelGGL(k_list_offsets, dim3(1), dim3(kScanThreads), 0, s, a.cnt, a.nlb, a.boff, a.dense_total);
+    const size_t mlds0 = exact_mass_lds_bytes(a.K, a.m, a.d, a.nq * 16);
+    const bool mass = !a.exact_wave && E <= kWave && mlds0 <= 96 * 1024;
+    hipLaunchKernelGGL(k_list_fill, dim3((unsigned)((a.nlb + 3) / 4)), dim3(256), 0, s, a, mass ? 1 : 0);
+  } else if (a.exact_scan || !wg) {
     hipLaunchKernelGGL(k_list_scan, dim3(1), dim3(kScanThreads), 0, s, a.cnt, a.nlb, a.lblock, a.dense,
                        a.dense_total);
+  }
+  if (!wg) a.exact_scan = 1;
   // grid: from the previous launch's list size (a converged chain lists ~13 points per C5
   // sweep; a random start ~1M, looped over by every resident workgroup)
   const dim3 g(a.exact_grid > 0 ? a.exact_grid : std::min(nblocks * 4, 1024)), b(kExactWgThreads);

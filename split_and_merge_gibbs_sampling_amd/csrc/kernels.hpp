@@ -130,6 +130,7 @@ struct PrepassArgs {
   int* wide_ctr;             // [2] k_prepass_wide's chunk counter, k_exact_rows_mass's point counter
                              // (cleared by k_cluster_summary)
   int exact_grid;            // the exact-rows grid (0: from the launch size); workgroups loop over the list
+  int* boff;                 // [list blocks] offsets of the blocks' rows in the dense list (exact_scan)
   int exact_scan;            // 1: the dense list by k_list_scan before the exact rows (many listed
                              // points: every workgroup then reads its rows, no per-point block walk)
   int nlb, lblock;           // list blocks of this launch and their points (k_exact_rows_wg's own list scan)

@@ -345,6 +345,70 @@ __device__ __forceinline__ double sum_smallest(const double (&dv)[NV], const uin
   return s + (double)(h - below) * t;
 }
 
+// The same two sums by a bitonic sort of the wave's 64 NV values (element k * 64 + lane;
+// padding +inf sorts last): ~log2(64 NV)^2 / 2 compare-exchange steps instead of two 64-step
+// bisections.  The heads round both sums down to float and one ulp further, so the summation
+// order of the doubles does not matter (the bound stays below the exact sum).
+template <int NV>
+__device__ __forceinline__ void sum_smallest2(double (&dv)[NV], uint64_t (&key)[NV], int ha, int hb, double* sa,
+                                              double* sb) {
+  const int lane = threadIdx.x & 63;
+  constexpr int N = 64 * NV;
+#pragma unroll
+  for (int size = 2; size <= N; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      if (stride >= 64) {
+        const int ks = stride >> 6;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+          if (k & ks) continue;
+          const int idx = k * 64 + lane;
+          const bool up = (idx & size) == 0;
+          const int k2 = k | ks;
+          const bool sw = up ? key[k] > key[k2] : key[k] < key[k2];
+          if (sw) {
+            const uint64_t tk = key[k];
+            key[k] = key[k2];
+            key[k2] = tk;
+            const double tv = dv[k];
+            dv[k] = dv[k2];
+            dv[k2] = tv;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+          const int idx = k * 64 + lane;
+          const bool up = (idx & size) == 0, lower = (lane & stride) == 0;
+          const uint64_t ok = __shfl_xor(key[k], stride);
+          const double ov = __shfl_xor(dv[k], stride);
+          // the lower element of the pair keeps the smaller key when ascending
+          const bool take = (lower == up) ? ok < key[k] : ok > key[k];
+          if (take) {
+            key[k] = ok;
+            dv[k] = ov;
+          }
+        }
+      }
+    }
+  }
+  double a = 0.0, b = 0.0;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int r = k * 64 + lane;
+    a += r < ha ? dv[k] : 0.0;
+    b += r < hb ? dv[k] : 0.0;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o);
+    b += __shfl_xor(b, o);
+  }
+  *sa = a;
+  *sb = b;
+}
+
 // Pool-entry heads (kernels.hpp) from the dhamming tables and bound records: one wave per
 // entry, nv = Ws attributes per lane (d <= 64 nv, nv <= NV).  S_a / S_b are the sums of the
 // h_a / h_b smallest d_j (sum_smallest).  Host and device pools alike.
@@ -368,8 +432,8 @@ __global__ __launch_bounds__(256) void k_pool_heads(const double* __restrict__ t
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mn = fmin(mn, __shfl_xor(mn, o));
-  const double sa = sum_smallest<NV>(dv, key, ha < d ? ha : d);
-  const double sb = sum_smallest<NV>(dv, key, hb < d ? hb : d);
+  double sa, sb;
+  sum_smallest2<NV>(dv, key, ha < d ? ha : d, hb < d ? hb : d, &sa, &sb);
   const int HW = wb * nv + 2, HS = head_stride(wb, nv);
   const uint64_t* r = bnd + e * bw;
   for (int q = lane; q < HS; q += 64) {
