@@ -1972,6 +1972,7 @@ struct Ctx {
   enum { kRoundAll = 0, kRoundPrefix = 1, kRoundResolve = 2 };
   static constexpr int kFpMinListed = 64;
   static constexpr int kFpgMinListed = 1024;   // listed points of the previous launch for k_resolve_fpg (two chunks)
+  static constexpr int kMassNoSpec = 65536;    // expected listed points above which no snapshot draws are made
   bool fp_eligible(int E, int lcap) const {
     return E <= 64 && lcap <= 64 && !(debug & (1 | 4096 | 8192 | 8388608));
   }
@@ -2029,7 +2030,10 @@ struct Ctx {
     pa.dmax2 = ((debug & (1 | 262144)) || last_unsettled || many_exact) ? INFINITY : 2.0 * dmax;
     pa.L = d_L.p; pa.rowpos = d_rowpos.p; pa.margin = d_margin.p; pa.list = d_list.p; pa.cnt = d_cnt.p;
     pa.dense = d_dense.p; pa.dense_total = d_dense_total.p; pa.boff = d_boff.p;
-    pa.spec = (debug & 8) ? nullptr : d_spec.p;
+    // snapshot draws (k_exact_rows*: the resolver's first-round guesses and kept draws) except
+    // when nearly every point is listed: the device-wide resolver then draws all of them in
+    // its first round anyway, and the mass exact-rows kernel is ~20% faster without them
+    pa.spec = ((debug & 8) || el >= kMassNoSpec) ? nullptr : d_spec.p;
     pa.spec_rad = d_spec_rad.p;
     pa.rq = d_rq.p;
     pa.p0 = p;
@@ -2443,6 +2447,7 @@ struct Ctx {
 
     int nslots = K;
     int p = 0;
+    bool end_queued = false;             // the sweep end is on the stream behind the last launch
     const int64_t rounds0 = stats.rounds;
     // round 0 may already be on the device (prepare_next_sweep with launch)
     const bool launched_ahead = ahead_launched;
@@ -2454,6 +2459,13 @@ struct Ctx {
         const int part = (ahead_prefix && stats.rounds == rounds0) ? kRoundResolve : kRoundAll;
         const int lst = launch_round(p, nslots, m, d_sweep_raw, track, part);
         if (lst) return lst;
+        // while sweeps keep moving points, the sweep-end kernels go behind every launch at
+        // once (they act only after the launch that completes the sweep): no host round trip
+        // between the resolver and the sweep end
+        end_queued = last_sweep_moves > 0;
+        if (end_queued) launch_sweep_end(scap - 2, track);
+      } else {
+        end_queued = false;
       }
       mark("launched");
       if (stats.rounds == rounds0) {   // hidden behind the device work
@@ -2556,7 +2568,7 @@ struct Ctx {
     const int* cnt = sol + scap;
     const int* src = cnt + scap;
     if (sweep_moves > 0) {
-      launch_sweep_end(nslots, track);
+      if (!end_queued) launch_sweep_end(nslots, track);
       if (track) {   // the gather wrote freq2 (and its copy is on its way)
         std::swap(d_freq.p, d_freq2.p);
         std::swap(d_freq.n, d_freq2.n);

@@ -307,53 +307,19 @@ __device__ __forceinline__ float f32_up(double x) {
   return f;
 }
 
-// Order-preserving key of a double (unsigned compare of keys = numeric compare).
-__device__ __forceinline__ uint64_t dkey(double x) {
-  const uint64_t u = (uint64_t)__double_as_longlong(x);
-  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
-}
-
-// Sum of the h smallest of the wave's values dv (NV per lane, +inf padding): bisection on
-// the key for the h-th smallest value t (64 steps, each a wave-wide count of keys < mid),
-// then sum(values < t) + (h - count(values < t)) t.
+// S_a / S_b (the sums of the h_a / h_b smallest d_j), as lower bounds, by a bitonic sort of the wave's 64 NV values rounded
+// down to float (32-bit keys, no payload: non-negative floats order as their bits; padding
+// +inf sorts last).  The heads round both sums down to float and one ulp further, so the
+// sums need only stay below the exact ones: every key is <= its d_j, and the double sums of
+// at most 2048 floats round by far less than that float ulp.
 template <int NV>
-__device__ __forceinline__ double sum_smallest(const double (&dv)[NV], const uint64_t (&key)[NV], int h) {
-  if (h <= 0) return 0.0;
-  uint64_t lo = 0, hi = ~0ull;        // invariant: count(key <= lo) < h <= count(key <= hi)
-  while (hi - lo > 1) {
-    const uint64_t mid = lo + (hi - lo) / 2;
-    int c = 0;
-#pragma unroll
-    for (int k = 0; k < NV; ++k) c += __popcll(__ballot(key[k] <= mid));
-    if (c >= h) hi = mid;
-    else lo = mid;
-  }
-  // hi is the key of the h-th smallest value
-  double s = 0.0, t = -__builtin_inf();
-  int below = 0;
-#pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    if (key[k] < hi) s += dv[k];
-    if (key[k] == hi) t = dv[k];
-    below += __popcll(__ballot(key[k] < hi));
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    s += __shfl_xor(s, o);
-    t = fmax(t, __shfl_xor(t, o));     // every lane holding the key holds the same value
-  }
-  return s + (double)(h - below) * t;
-}
-
-// The same two sums by a bitonic sort of the wave's 64 NV values (element k * 64 + lane;
-// padding +inf sorts last): ~log2(64 NV)^2 / 2 compare-exchange steps instead of two 64-step
-// bisections.  The heads round both sums down to float and one ulp further, so the summation
-// order of the doubles does not matter (the bound stays below the exact sum).
-template <int NV>
-__device__ __forceinline__ void sum_smallest2(double (&dv)[NV], uint64_t (&key)[NV], int ha, int hb, double* sa,
-                                              double* sb) {
+__device__ __forceinline__ void sum_smallest2(const double (&dv)[NV], int ha, int hb, double* sa, double* sb) {
   const int lane = threadIdx.x & 63;
   constexpr int N = 64 * NV;
+  uint32_t key[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
+    key[k] = dv[k] == __builtin_inf() ? 0x7f800000u : __float_as_uint(f32_down(dv[k] > 0.0 ? dv[k] : 0.0));
 #pragma unroll
   for (int size = 2; size <= N; size <<= 1) {
 #pragma unroll
@@ -363,32 +329,17 @@ __device__ __forceinline__ void sum_smallest2(double (&dv)[NV], uint64_t (&key)[
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
           if (k & ks) continue;
-          const int idx = k * 64 + lane;
-          const bool up = (idx & size) == 0;
-          const int k2 = k | ks;
-          const bool sw = up ? key[k] > key[k2] : key[k] < key[k2];
-          if (sw) {
-            const uint64_t tk = key[k];
-            key[k] = key[k2];
-            key[k2] = tk;
-            const double tv = dv[k];
-            dv[k] = dv[k2];
-            dv[k2] = tv;
-          }
+          const bool up = ((k * 64 + lane) & size) == 0;
+          const uint32_t x = key[k], y = key[k | ks];
+          key[k] = up ? min(x, y) : max(x, y);
+          key[k | ks] = up ? max(x, y) : min(x, y);
         }
       } else {
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
-          const int idx = k * 64 + lane;
-          const bool up = (idx & size) == 0, lower = (lane & stride) == 0;
-          const uint64_t ok = __shfl_xor(key[k], stride);
-          const double ov = __shfl_xor(dv[k], stride);
-          // the lower element of the pair keeps the smaller key when ascending
-          const bool take = (lower == up) ? ok < key[k] : ok > key[k];
-          if (take) {
-            key[k] = ok;
-            dv[k] = ov;
-          }
+          const bool up = ((k * 64 + lane) & size) == 0, lower = (lane & stride) == 0;
+          const uint32_t o = (uint32_t)__shfl_xor((int)key[k], stride);
+          key[k] = (lower == up) ? min(key[k], o) : max(key[k], o);
         }
       }
     }
@@ -397,8 +348,9 @@ __device__ __forceinline__ void sum_smallest2(double (&dv)[NV], uint64_t (&key)[
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int r = k * 64 + lane;
-    a += r < ha ? dv[k] : 0.0;
-    b += r < hb ? dv[k] : 0.0;
+    const double x = (double)__uint_as_float(key[k]);
+    a += r < ha ? x : 0.0;
+    b += r < hb ? x : 0.0;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -411,7 +363,7 @@ __device__ __forceinline__ void sum_smallest2(double (&dv)[NV], uint64_t (&key)[
 
 // Pool-entry heads (kernels.hpp) from the dhamming tables and bound records: one wave per
 // entry, nv = Ws attributes per lane (d <= 64 nv, nv <= NV).  S_a / S_b are the sums of the
-// h_a / h_b smallest d_j (sum_smallest).  Host and device pools alike.
+// h_a / h_b smallest d_j, as lower bounds (sum_smallest2).  Host and device pools alike.
 template <int NV>
 __global__ __launch_bounds__(256) void k_pool_heads(const double* __restrict__ tab, const uint64_t* __restrict__ bnd,
                                                    int64_t P, int d, int wb, int nv, int bw, int ha, int hb,
@@ -421,19 +373,17 @@ __global__ __launch_bounds__(256) void k_pool_heads(const double* __restrict__ t
   if (e >= P) return;
   const double* t = tab + e * 2 * d;
   double dv[NV];
-  uint64_t key[NV];
   double mn = __builtin_inf();
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int j = 64 * k + lane;
     dv[k] = j < d ? t[2 * j] - t[2 * j + 1] : __builtin_inf();   // d_j as in Ctx::bounds_for
-    key[k] = dkey(dv[k]);
     mn = fmin(mn, dv[k]);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mn = fmin(mn, __shfl_xor(mn, o));
   double sa, sb;
-  sum_smallest2<NV>(dv, key, ha < d ? ha : d, hb < d ? hb : d, &sa, &sb);
+  sum_smallest2<NV>(dv, ha < d ? ha : d, hb < d ? hb : d, &sa, &sb);
   const int HW = wb * nv + 2, HS = head_stride(wb, nv);
   const uint64_t* r = bnd + e * bw;
   for (int q = lane; q < HS; q += 64) {

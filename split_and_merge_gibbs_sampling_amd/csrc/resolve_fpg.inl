@@ -108,8 +108,19 @@ __device__ __forceinline__ bool sync(const Lay& L, int G, int* flag) {
 // into out[64] (LDS); red: LDS [kFpWaves][64]
 __device__ __forceinline__ void prefix_slots(const int* v, int hi, int* red, int* out) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // eight loads in flight per lane before they are added (a loop of load-then-add waited for
+  // every L2 round trip: ~32 of them per round for the last workgroup of a 256-wide window)
   int acc = 0;
-  for (int h = wv; h < hi; h += kFpWaves) acc += ald(v + (size_t)h * kFpgSlots + lane);
+  for (int h0 = wv; h0 < hi; h0 += 8 * kFpWaves) {
+    int x[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int h = h0 + k * kFpWaves;
+      x[k] = h < hi ? ald(v + (size_t)h * kFpgSlots + lane) : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc += x[k];
+  }
   red[wv * kWave + lane] = acc;
   __syncthreads();
   if (wv == 0) {
@@ -125,8 +136,13 @@ __device__ __forceinline__ void prefix_slots(const int* v, int hi, int* red, int
 __device__ __forceinline__ double wave_max_over(const double* v, int n, double init) {
   const int lane = threadIdx.x & 63;
   double m = init;
-  for (int h0 = 0; h0 < n; h0 += kWave)
-    if (h0 + lane < n) m = fmax(m, aldd(v + h0 + lane));
+  for (int h0 = 0; h0 < n; h0 += 4 * kWave) {
+    double x[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = h0 + k * kWave + lane < n ? aldd(v + h0 + k * kWave + lane) : init;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) m = fmax(m, x[k]);
+  }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o));
   return m;
@@ -134,8 +150,13 @@ __device__ __forceinline__ double wave_max_over(const double* v, int n, double i
 __device__ __forceinline__ int wave_min_over(const int* v, int n, int init) {
   const int lane = threadIdx.x & 63;
   int m = init;
-  for (int h0 = 0; h0 < n; h0 += kWave)
-    if (h0 + lane < n) m = min(m, ald(v + h0 + lane));
+  for (int h0 = 0; h0 < n; h0 += 4 * kWave) {
+    int x[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = h0 + k * kWave + lane < n ? ald(v + h0 + k * kWave + lane) : init;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) m = min(m, x[k]);
+  }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = min(m, __shfl_xor(m, o));
   return m;
@@ -143,8 +164,13 @@ __device__ __forceinline__ int wave_min_over(const int* v, int n, int init) {
 __device__ __forceinline__ int wave_sum_over(const int* v, int n) {
   const int lane = threadIdx.x & 63;
   int m = 0;
-  for (int h0 = 0; h0 < n; h0 += kWave)
-    if (h0 + lane < n) m += ald(v + h0 + lane);
+  for (int h0 = 0; h0 < n; h0 += 4 * kWave) {
+    int x[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = h0 + k * kWave + lane < n ? ald(v + h0 + k * kWave + lane) : 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) m += x[k];
+  }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m += __shfl_xor(m, o);
   return m;
