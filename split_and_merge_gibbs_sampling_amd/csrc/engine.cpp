@@ -728,6 +728,7 @@ struct Ctx {
   bool last_fp = false;        // the last resolver launch was k_resolve_fp (diagnostics)
   int last_exact = 0;         // points the previous resolver launch decided one by one (block-mode choice)
   int last_listed = -1;       // points the previous launch's prepass listed (exact-rows grid), -1 unknown
+  int last_fpg = 0;           // the previous launch's k_resolve_fpg grid (0: another resolver)
   double last_density = -1;   // ... per point of the range it covered (a restart covers the sweep's rest)
   bool last_unsettled = false;  // the previous launch exceeded its drift budget or restarted
 
@@ -2129,7 +2130,10 @@ struct Ctx {
         if (!pg) stats.fpg_launches++;
       }
     }
-    if (part != kRoundPrefix && !pg) last_fp = ra.fp != 0;
+    if (part != kRoundPrefix && !pg) {
+      last_fp = ra.fp != 0;
+      last_fpg = ra.fpg;
+    }
     if (resolve_smem_bytes(ra.lcap, m, ra.blocks) > 160 * 1024) {
       err = "too many clusters for the resolver (K > ~2300)";
       return kArg;
@@ -2518,7 +2522,15 @@ struct Ctx {
       // the sweep enqueued ahead runs only after a complete sweep without moves
       if (pre.active && (c.status || c.next < n || c.moves)) pre_release();
       last_sweep_rounds = (int)(stats.rounds - rounds0);
-      if ((debug & 2) && last_fp) {
+      if ((debug & 2) && last_fp && last_fpg) {
+        long long tp[16];
+        HIPCHK(hipMemcpy(tp, d_rprof.p, sizeof(tp), hipMemcpyDeviceToHost));
+        std::fprintf(stderr,
+                     "[resolve_fpg] G %d: %lld listed in %lld windows, %lld rounds; init %.2f us, rounds %.2f us, drift / "
+                     "re-test / commit %.2f us, in grid barriers %.2f us, total %.2f us\n",
+                     last_fpg, tp[9], tp[8], tp[5], (tp[1] - tp[0]) / 100.0, tp[3] / 100.0, tp[4] / 100.0, tp[2] / 100.0,
+                     (tp[7] - tp[0]) / 100.0);
+      } else if ((debug & 2) && last_fp) {
         long long tp[16];
         HIPCHK(hipMemcpy(tp, d_rprof.p, sizeof(tp), hipMemcpyDeviceToHost));
         std::fprintf(stderr,

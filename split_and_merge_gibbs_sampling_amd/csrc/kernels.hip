@@ -3304,8 +3304,10 @@ __global__ __launch_bounds__(kWave * kMassWaves) void k_exact_rows_mass(PrepassA
   const bool clu = lane < K, on = lane < E;
   const int col = clu ? s_sl[lane] : a.S + (lane - K);
   // lane's row of values: a cluster's table (stride 2, the mismatch value selected by the code
-  // compare) or the wave's gathered latent values (stride 1)
-  const double* base = clu ? ltab + (size_t)lane * 2 * D : lval + (size_t)(on ? lane - K : 0) * D;
+  // compare) or the wave's gathered latent values (stride 1); 32-bit offsets in doubles from
+  // the start of the LDS block
+  const double* lds_d = (const double*)smem;
+  const int boff = clu ? lane * 2 * D : (int)(lval - lds_d) + (on ? lane - K : 0) * D;
   const int stride = clu ? 2 : 1;
   const uint8_t* cl = lcode + (size_t)(clu ? lane : 0) * dp;
   // batches of kMassBatch points claimed from a counter (k_cluster_summary clears it; a
@@ -3359,16 +3361,25 @@ __global__ __launch_bounds__(kWave * kMassWaves) void k_exact_rows_mass(PrepassA
       // lane e's entry in attribute order (n8:47-49), 16 values loaded before they are added;
       // padding past D adds +0.0, which leaves the sum unchanged
       double acc = 0.0;
-      for (int j0 = 0; j0 < D; j0 += 16) {
+      int off = boff;
+      for (int j0 = 0; j0 < D; j0 += 16, off += 16 * stride) {
         const uint4 xw = *(const uint4*)(lx + j0);
         const uint4 cw = clu ? *(const uint4*)(cl + j0) : xw;
-        const uint32_t dx[4] = {xw.x ^ cw.x, xw.y ^ cw.y, xw.z ^ cw.z, xw.w ^ cw.w};
+        // bit 0 of each byte: the codes differ (the mismatch value)
+        uint32_t nz[4] = {xw.x ^ cw.x, xw.y ^ cw.y, xw.z ^ cw.z, xw.w ^ cw.w};
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          uint32_t t = nz[w];
+          t |= t >> 4;
+          t |= t >> 2;
+          t |= t >> 1;
+          nz[w] = t & 0x01010101u;
+        }
         double v[16];
 #pragma unroll
         for (int b = 0; b < 16; ++b) {
-          const int j = j0 + b;
-          const int sel = ((dx[b >> 2] >> (8 * (b & 3))) & 0xffu) ? 1 : 0;
-          v[b] = j < D ? base[(size_t)j * stride + sel] : 0.0;
+          const int sel = (int)((nz[b >> 2] >> (8 * (b & 3))) & 1u);
+          v[b] = j0 + b < D ? lds_d[off + b * stride + sel] : 0.0;
         }
 #pragma unroll
         for (int b = 0; b < 16; ++b) acc += v[b];

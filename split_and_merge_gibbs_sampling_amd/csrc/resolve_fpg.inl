@@ -205,6 +205,17 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
   FpgShared* X = (FpgShared*)(smem + ((resolve_fp_lds_bytes(a.lcap, a.m) + 15) & ~(size_t)15));
   const fpg::Lay L = fpg::lay(a.fpg_buf, G);
   long long tp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // debug bit 1 profile (workgroup 0): [2] ticks in grid barriers, [3] in the rounds, [4] in
+  // the drift / re-test / commit phase; tsub[0] windows
+  const bool prof = a.prof != nullptr && g == 0;
+  if (prof) tp[0] = wall_clock64();
+  int nwin = 0;
+  auto bar = [&]() -> bool {
+    const long long t = prof ? wall_clock64() : 0;
+    const bool r = fpg::sync(L, G, &X->flag);
+    if (prof) tp[2] += wall_clock64() - t;
+    return r;
+  };
   if (tid == 0) { F->nlog = a.mcount ? *a.mcount : 0; F->go = 1; F->iters = 0; X->gs_prev = G; }
   for (int e = tid; e < 256; e += kFpThreads) F->etab[e] = devtab::kGlibcExpTab[e];
   resolve_init(a, st);
@@ -217,7 +228,10 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
   // the move log is written at atomically claimed positions (k_apply_moves is order-free)
   int* mcnt = a.mcount;
   int q0 = 0;
+  if (prof) tp[1] = wall_clock64();
   while (q0 < total && go && ok) {
+    ++nwin;
+    const long long tw0 = prof ? wall_clock64() : 0;
     const int cq = q0 + g * kFpThreads;
     const int nc = max(0, min(kFpThreads, total - cq));
     const bool in = tid < nc;
@@ -265,7 +279,7 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
         L.dr[(size_t)g * kFpgSlots + lane] = t;
         if (lane == 0) L.stop[g] = fsl < nc ? fsl : kFpThreads;
       }
-      if (!(ok = fpg::sync(L, G, &X->flag))) break;
+      if (!(ok = bar())) break;
       // (2) the window's first stopping chunk; this chunk's start counts
       if (wv == 0) {
         int f = G;
@@ -395,7 +409,7 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
         X->gs_prev = gs;
       }
       chg = c2 < kFpThreads ? c2 : nc;
-      if (!(ok = fpg::sync(L, G, &X->flag))) break;
+      if (!(ok = bar())) break;
       // converged when no outcome of the window changed in this round
       if (wv == 0) {
         bool any = false;
@@ -408,6 +422,8 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
       __syncthreads();
       if (X->conv) { conv = true; break; }
     }
+    const long long tw1 = prof ? wall_clock64() : 0;
+    if (prof) tp[3] += tw1 - tw0;
     if (!ok) break;
     if (!conv) {       // cannot happen (at most WIN + 1 rounds); stop loudly
       if (tid == 0) { S.status = 5; S.next = F->pi[0]; }
@@ -432,7 +448,7 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
       for (int w = 0; w < kFpWaves; ++w) m2 = fmax(m2, F->wsd[w]);
       L.sd[g] = m2;
     }
-    if (!(ok = fpg::sync(L, G, &X->flag))) break;
+    if (!(ok = bar())) break;
     // the drift at this chunk's start and over the window (every chunk up to the stop)
     if (wv == 0) {
       const double x = fpg::wave_max_over(L.sd, min(g, gs + 1), S.dnow);
@@ -465,7 +481,7 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
     }
     __syncthreads();
     if (tid == 0) L.fail[g] = X->u;
-    if (!(ok = fpg::sync(L, G, &X->flag))) break;
+    if (!(ok = bar())) break;
     if (wv == 0) {
       const int x = fpg::wave_min_over(L.fail, min(G, gs + 1), INT_MAX);
       if (lane == 0) X->ufirst = x;
@@ -516,7 +532,7 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
       F->stop_pick = pick;
       F->stop_fresh = fresh ? 1 : 0;
     }
-    if (!(ok = fpg::sync(L, G, &X->flag))) break;
+    if (!(ok = bar())) break;
     // ---- every workgroup applies the window's committed changes to its copy of the state
     fpg::prefix_slots(L.dc, min(G, gs + 1), X->red, X->add);
     if (wv == 0) {
@@ -571,7 +587,7 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
           }
         }
       }
-      if (!(ok = fpg::sync(L, G, &X->flag))) break;
+      if (!(ok = bar())) break;
       if (g != gs) {
         if (wv == 0) {
           const int c = fpg::ald(L.cnt + lane);
@@ -604,6 +620,7 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
       vfrom = (int64_t)gld(a.rq + qe - 1).y + 1;
       q0 = qe;
     }
+    if (prof) tp[4] += wall_clock64() - tw1;
     __syncthreads();
   }
   if (!ok) {
@@ -615,6 +632,6 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
   __syncthreads();
   // the unlisted points after the last listed one (one workgroup, as k_resolve_fp)
   if (ok && go && S.status == 0 && !S.restart && S.dnow > a.dmax) (void)fp_verify(a, st, F, 0, S.dnow, vfrom, a.n, st.cnt);
-  if (tid == 0) { tp[5] = F->iters; S.tsub[0] = 0; S.tsub[1] = total; }
+  if (tid == 0) { tp[5] = F->iters; S.tsub[0] = nwin; S.tsub[1] = total; }
   resolve_finish(a, st, F->nlog, tp, a.prof != nullptr);
 }
