@@ -2443,6 +2443,26 @@ __device__ __forceinline__ T gld(const T* p) {
 
 __device__ __forceinline__ double fp_logn(const ResolveArgs& a, int c) { return c <= 0 ? -INFINITY : gld(a.logn + c); }
 
+__device__ __forceinline__ double fp_wave_drift_bound(const ResolveArgs& a, const RState& st, const int* wc,
+                                                      const unsigned long long* bin, const unsigned long long* bout,
+                                                      int nsl) {
+  const int s = threadIdx.x & 63;
+  double b = 0.0;
+  if (s < nsl) {
+    const int lo = wc[s] - __popcll(bout[s]), hi = wc[s] + __popcll(bin[s]);
+    const int a0 = st.snap[s];
+    if (!(lo == a0 && hi == a0)) {
+      const double d_oth = (a0 < 1 || lo < 1) ? INFINITY
+                                               : fmax(fabs(fp_logn(a, hi) - st.sl1[s]), fabs(fp_logn(a, lo) - st.sl1[s]));
+      const double d_own = (a0 < 2 || lo < 2)
+                               ? INFINITY
+                               : fmax(fabs(fp_logn(a, hi - 1) - st.sl0[s]), fabs(fp_logn(a, lo - 1) - st.sl0[s]));
+      b = fmax(d_oth, d_own);
+    }
+  }
+  return wave_max(b);
+}
+
 // slot_drift of slot s at count b (k_resolve's running drift after a move)
 __device__ __forceinline__ double slot_drift_at(const ResolveArgs& a, const RState& st, int s, int b) {
   const int a0 = st.snap[s];
@@ -2486,6 +2506,17 @@ __device__ __forceinline__ double fp_exp(double x, const uint64_t* T) {
   const double y = __builtin_fma(scale, tmp, scale);
   return tiny ? x + 1.0 : (x > -512.0 ? y : 0.0);
 }
+
+// An upper bound, over the wave's lanes, of the drift the fixed-point evaluation computes per
+// lane (the largest |log-count term now - at the snapshot| over the entries, n8:40-92): the
+// count a lane sees for slot s lies in [wc - movers out of s, wc + movers into s] (the wave's
+// movers before it), its own slot's term uses that count less one, and logn is monotone, so
+// the extremes bound every lane.  Below a lane's radius the snapshot draw holds without the
+// per-entry terms.  Lane = slot; every lane of the wave calls it.
+struct FpShared;
+__device__ __forceinline__ double fp_wave_drift_bound(const ResolveArgs& a, const RState& st, const int* wc,
+                                                      const unsigned long long* bin, const unsigned long long* bout,
+                                                      int nsl);
 
 template <int EM>
 __device__ int fp_draw(double (&v)[EM], int E, double rU, const uint64_t* etab) {
@@ -2693,7 +2724,29 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
       bool changed = false;
       long long tdraw = 0;
       const bool evl = in && tid > chg && tid <= fs;
-      if (evl) {
+      const double wdb = (struct0 && a.spec) ? fp_wave_drift_bound(a, st, F->wc[wv], F->bin[wv], F->bout[wv], nsl)
+                                             : INFINITY;
+      if (evl && struct0 && sp >= 0 && wdb < sr) {
+        // every entry's drift is below this point's radius: its snapshot draw holds
+        const int cnow = F->wc[wv][own] + corr(own);
+        const bool single = cnow == 1;
+        const int np = sp;
+        fresh = false;
+        int ncl = 2, nt = own;
+        if (np < K) {
+          const int s2 = st.sol[np];
+          if (!single) { ncl = s2 != own ? 1 : 0; nt = s2; }
+        } else if (single && np == K) {
+          ncl = 0;
+        }
+        const int ctn = F->wc[wv][nt] + corr(nt);
+        changed = ncl != cls || (ncl == 1 && nt != tgt);
+        cls = ncl;
+        tgt = nt;
+        pick = np;
+        co = cnow;
+        ct = ctn;
+      } else if (evl) {
         const int cnow = F->wc[wv][own] + corr(own);
         const bool single = cnow == 1;
         int sl[EM], cc[EM];
@@ -3391,6 +3444,119 @@ __global__ __launch_bounds__(kWave * kMassWaves) void k_exact_rows_mass(PrepassA
   }
 }
 
+// Exact rows with a thread per listed point, for sweeps without snapshot draws (nearly every
+// point listed: the device-wide resolver draws them all) and D <= 128.  The K clusters' codes
+// and (match, mismatch) pairs are staged in LDS; every lane of a wave reads the same pair at
+// the same time (a broadcast) and selects by its own point's code, four clusters' sums
+// interleaved; the m latent entries are walked per lane, 16 attributes per step.  Each sum runs
+// in attribute order (n8:47-49), so every row is bit-exact; ~5 VALU per (entry, attribute) for
+// 64 points at once instead of a wave per point.  Dynamic LDS: K (2 D 8 + dp) bytes.
+constexpr int kLanesMaxNq = 8;
+__global__ __launch_bounds__(256) void k_exact_rows_lanes(PrepassArgs a) {
+  if (!pipe_gate(a)) return;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int K = a.K, m = a.m, D = a.d, nq = a.nq, dp = nq * 16;
+  double* ltab = (double*)smem;                                   // [K][D][2]
+  uint8_t* lcode = (uint8_t*)(ltab + (size_t)K * 2 * D);          // [K][dp]
+  __shared__ int s_col[kWave];
+  for (int q = threadIdx.x; q < K * 2 * D; q += blockDim.x) {
+    const int e = q / (2 * D);
+    ltab[q] = a.slots.tab[(int64_t)a.slot_of_label[e] * 2 * D + (q - e * 2 * D)];
+  }
+  for (int q = threadIdx.x; q < K * dp; q += blockDim.x) {
+    const int e = q / dp;
+    lcode[q] = a.slots.codes[(int64_t)a.slot_of_label[e] * dp + (q - e * dp)];
+  }
+  if (threadIdx.x < K) s_col[threadIdx.x] = a.slot_of_label[threadIdx.x];
+  __syncthreads();
+  const int total = *a.dense_total;
+  const int stride = gridDim.x * blockDim.x;
+  for (int q0 = blockIdx.x * blockDim.x; q0 < total; q0 += stride) {   // uniform trip count per block
+    const int q = q0 + threadIdx.x;
+    const bool on = q < total;
+    const int4 r = on ? a.rq[q] : make_int4(0, 0, 0, 0);
+    const int64_t i = r.y;
+    double* Lr = a.L + (int64_t)r.x * (a.S + m);
+    uint32_t xw[4 * kLanesMaxNq];
+#pragma unroll
+    for (int c = 0; c < kLanesMaxNq; ++c) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (c < nq) v = *(const uint4*)(a.codes_t + tiled_offset(i, c * 16, nq));
+      xw[4 * c] = v.x; xw[4 * c + 1] = v.y; xw[4 * c + 2] = v.z; xw[4 * c + 3] = v.w;
+    }
+    for (int k0 = 0; k0 < K; k0 += 4) {
+      double acc[4] = {0.0, 0.0, 0.0, 0.0};
+      const double* tb[4];
+      const uint8_t* cb[4];
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int k = min(k0 + kk, K - 1);
+        tb[kk] = ltab + (size_t)k * 2 * D;
+        cb[kk] = lcode + (size_t)k * dp;
+      }
+#pragma unroll
+      for (int c = 0; c < kLanesMaxNq; ++c) {
+        if (c >= nq) break;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const uint32_t x4 = xw[4 * c + w];
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) {
+            const uint32_t c4 = *(const uint32_t*)(cb[kk] + c * 16 + 4 * w);
+            const uint32_t dx = x4 ^ c4;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+              const int j = c * 16 + 4 * w + b;
+              if (j < D) {
+                const double2 pr = *(const double2*)(tb[kk] + 2 * j);
+                acc[kk] += ((dx >> (8 * b)) & 0xffu) ? pr.y : pr.x;
+              }
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+        if (on && k0 + kk < K) Lr[s_col[k0 + kk]] = acc[kk];
+    }
+    const uint32_t* raw = a.raw + i * (m + 1);
+    for (int u = 0; u < m; ++u) {
+      const int64_t pe = on ? pick_entry(raw[u], a.P) : 0;
+      const uint8_t* cc = a.pool.codes + pe * dp;
+      const double* tl = a.pool.tab + pe * 2 * D;
+      double acc = 0.0;
+#pragma unroll
+      for (int c = 0; c < kLanesMaxNq; ++c) {
+        if (c >= nq) break;
+        const uint4 cq = *(const uint4*)(cc + c * 16);
+        const uint32_t cw[4] = {cq.x, cq.y, cq.z, cq.w};
+        double v[16];
+#pragma unroll
+        for (int b = 0; b < 16; ++b) {
+          const int j = c * 16 + b;
+          const uint32_t dx = xw[4 * c + (b >> 2)] ^ cw[b >> 2];
+          v[b] = j < D ? tl[2 * j + (((dx >> (8 * (b & 3))) & 0xffu) ? 1 : 0)] : 0.0;
+        }
+#pragma unroll
+        for (int b = 0; b < 16; ++b) acc += v[b];
+      }
+      if (on) Lr[a.S + u] = acc;
+    }
+  }
+}
+
+static int lanes_grid(size_t lds) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  int per = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_exact_rows_lanes, 256, lds) != hipSuccess || per <= 0) per = 1;
+  return cus * per;
+}
+
 static int mass_grid(size_t lds) {
   static int cus = 0;
   if (cus == 0) {
@@ -3421,7 +3587,7 @@ hipError_t launch_exact_rows(const PrepassArgs& a0, int nblocks, hipStream_t s) 
   if (a.exact_scan && a.boff) {
     hipLaunchKernelGGL(k_list_offsets, dim3(1), dim3(kScanThreads), 0, s, a.cnt, a.nlb, a.boff, a.dense_total);
     const size_t mlds0 = exact_mass_lds_bytes(a.K, a.m, a.d, a.nq * 16);
-    const bool mass = !a.exact_wave && E <= kWave && mlds0 <= 96 * 1024;
+    const bool mass = !a.exact_wave && ((E <= kWave && mlds0 <= 96 * 1024) || !a.spec);
     hipLaunchKernelGGL(k_list_fill, dim3((unsigned)((a.nlb + 3) / 4)), dim3(256), 0, s, a, mass ? 1 : 0);
   } else if (a.exact_scan || !wg) {
     hipLaunchKernelGGL(k_list_scan, dim3(1), dim3(kScanThreads), 0, s, a.cnt, a.nlb, a.lblock, a.dense,
@@ -3432,6 +3598,17 @@ hipError_t launch_exact_rows(const PrepassArgs& a0, int nblocks, hipStream_t s) 
   // sweep; a random start ~1M, looped over by every resident workgroup)
   const dim3 g(a.exact_grid > 0 ? a.exact_grid : std::min(nblocks * 4, 1024)), b(kExactWgThreads);
   const size_t mlds = exact_mass_lds_bytes(a.K, a.m, a.d, a.nq * 16);
+  const size_t llds = (size_t)a.K * (2 * a.d * 8 + a.nq * 16);
+  // HDPM_EXACT_MASS=1: the wave-per-point kernel for these sweeps too (A/B)
+  static const bool force_mass = [] {
+    const char* e = std::getenv("HDPM_EXACT_MASS");
+    return e && std::atoi(e) == 1;
+  }();
+  if (a.exact_scan && !a.spec && !a.exact_wave && a.nq <= kLanesMaxNq && a.K <= kWave && llds <= 64 * 1024 &&
+      !force_mass) {
+    hipLaunchKernelGGL(k_exact_rows_lanes, dim3(lanes_grid(llds)), dim3(256), llds, s, a);
+    return hipGetLastError();
+  }
   if (a.exact_scan && !a.exact_wave && E <= kWave && mlds <= 96 * 1024) {
     hipLaunchKernelGGL(k_exact_rows_mass, dim3(mass_grid(mlds)), dim3(kWave * kMassWaves), mlds, s, a);
     return hipGetLastError();

@@ -335,7 +335,29 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
       // (4) redraw behind the first changed outcome (k_resolve_fp's evaluation)
       bool changed = false;
       const bool evl = active && in && tid > chg && tid <= fs;
-      if (evl) {
+      const double wdb = (struct0 && a.spec) ? fp_wave_drift_bound(a, st, F->wc[wv], F->bin[wv], F->bout[wv], nsl)
+                                             : INFINITY;
+      if (evl && struct0 && sp >= 0 && wdb < sr) {
+        // every entry's drift is below this point's radius: its snapshot draw holds
+        const int cnow = F->wc[wv][own] + corr(own);
+        const bool single = cnow == 1;
+        const int np = sp;
+        fresh = false;
+        int ncl = 2, nt = own;
+        if (np < K) {
+          const int s2 = st.sol[np];
+          if (!single) { ncl = s2 != own ? 1 : 0; nt = s2; }
+        } else if (single && np == K) {
+          ncl = 0;
+        }
+        const int ctn = F->wc[wv][nt] + corr(nt);
+        changed = ncl != cls || (ncl == 1 && nt != tgt);
+        cls = ncl;
+        tgt = nt;
+        pick = np;
+        co = cnow;
+        ct = ctn;
+      } else if (evl) {
         const int cnow = F->wc[wv][own] + corr(own);
         const bool single = cnow == 1;
         int sl[EM], cc[EM];
