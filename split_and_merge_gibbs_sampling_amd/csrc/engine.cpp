@@ -2124,7 +2124,7 @@ struct Ctx {
       if (mg > 0 && resolve_fpg_smem_bytes(ra.lcap, m) <= 160 * 1024) {
         const int G = std::min(mg, std::max(2, (std::max(el, 0) + 511) / 512));
         d_fpg.ensure(fpg_words(G));
-        HIPCHK(hipMemsetAsync(d_fpg.p, 0, 16, stream));
+        HIPCHK(hipMemsetAsync(d_fpg.p, 0, (size_t)kFpgBarWords * 4, stream));
         ra.fpg = G;
         ra.fpg_buf = d_fpg.p;
         if (!pg) stats.fpg_launches++;

@@ -240,19 +240,21 @@ struct ResolveArgs {
   int fp;                    // 1: fixed-point resolver (k_resolve_fp; needs K + m <= 64, lcap <= 64)
   int debug_fp;              // bit 0: its first round starts from "stay" (not the snapshot draws' outcomes)
   // device-wide fixed-point resolver (k_resolve_fpg, fpg > 1 workgroups, one resident per CU):
-  // fpg_buf = fpg_words(fpg) ints of cross-workgroup scratch, its first 4 words zeroed by the host
+  // fpg_buf = fpg_words(fpg) ints of cross-workgroup scratch, its kFpgBarWords barrier words zeroed by the host
   int fpg;
   int* fpg_buf;
 };
-// Cross-workgroup scratch of k_resolve_fpg (G workgroups), in ints: barrier [0, 8), state mirror
-// [8, 8 + 3 * 64 + 16), then per workgroup: stop, changed, fail, moves, fresh, and the
+// Cross-workgroup scratch of k_resolve_fpg (G workgroups), in ints: barrier [0, 96), state mirror
+// [96, 96 + 8 + 3 * 64 + 16), then per workgroup: stop, changed, fail, moves, fresh, and the
 // last point of its chunk; per workgroup and slot: round deltas, committed deltas; then per
 // workgroup (doubles): drift.
 constexpr int kFpgSlots = 64;
 constexpr int kFpgState = 8;
 constexpr int kFpgPerWg = 8;
+constexpr int kFpgBarWords = 96;   // barrier words (arrivals, generation, abort on separate lines)
 __host__ __device__ inline size_t fpg_words(int G) {
-  return (size_t)kFpgState + 3 * kFpgSlots + 16 + (size_t)G * kFpgPerWg + (size_t)2 * G * kFpgSlots + (size_t)2 * G + 16;
+  return (size_t)kFpgBarWords + kFpgState + 3 * kFpgSlots + 16 + (size_t)G * kFpgPerWg + (size_t)2 * G * kFpgSlots +
+         (size_t)2 * G + 16;
 }
 
 // Cluster parameter upload: one staging buffer, scattered on the device.

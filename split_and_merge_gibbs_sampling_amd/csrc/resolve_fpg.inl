@@ -25,7 +25,8 @@ namespace fpg {
 
 // scratch layout (kernels.hpp fpg_words)
 struct Lay {
-  int* bar;      // [0] arrivals, [1] generation, [2] abort
+  int* bar;      // [0] arrivals, [32] generation, [64] abort: separate 128-B lines, so the spinning
+                 // loads of the generation do not contend with the arrivals' atomics
   int* ms;       // state mirror: K, nslots, status, restart, next, nstruct, exact, moves, go, nlog, checked
   int* sol;
   int* los;
@@ -43,8 +44,8 @@ struct Lay {
 __device__ __forceinline__ Lay lay(int* b, int G) {
   Lay L;
   L.bar = b;
-  L.ms = b + 4;
-  L.sol = b + kFpgState + 16;
+  L.ms = b + kFpgBarWords;
+  L.sol = b + kFpgBarWords + kFpgState + 16;
   L.los = L.sol + kFpgSlots;
   L.cnt = L.los + kFpgSlots;
   int* q = L.cnt + kFpgSlots;
@@ -80,19 +81,23 @@ __device__ __forceinline__ bool sync(const Lay& L, int G, int* flag) {
   if (threadIdx.x == 0) {
     __threadfence();
     int ab = 0;
-    const int gen = __hip_atomic_load(&L.bar[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    int* const gen_p = L.bar + 32;
+    int* const abort_p = L.bar + 64;
+    const int gen = __hip_atomic_load(gen_p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
     const int arrived = __hip_atomic_fetch_add(&L.bar[0], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1;
     if (arrived == G) {
       __hip_atomic_store(&L.bar[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&L.bar[1], gen + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(gen_p, gen + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     } else {
       const long long t0 = wall_clock64();
-      while (__hip_atomic_load(&L.bar[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == gen) {
-        if (__hip_atomic_load(&L.bar[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { ab = 1; break; }
-        if (wall_clock64() - t0 > 200000000LL) {
-          __hip_atomic_store(&L.bar[2], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          ab = 1;
-          break;
+      for (int spin = 0; __hip_atomic_load(gen_p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == gen; ++spin) {
+        if ((spin & 31) == 31) {     // the abort flag and the time limit, now and then
+          if (__hip_atomic_load(abort_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { ab = 1; break; }
+          if (wall_clock64() - t0 > 200000000LL) {
+            __hip_atomic_store(abort_p, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ab = 1;
+            break;
+          }
         }
         __builtin_amdgcn_s_sleep(1);
       }
