@@ -1957,6 +1957,17 @@ struct Ctx {
     d_spec.ensure((size_t)nb_max * kBlock);
     d_spec_rad.ensure((size_t)nb_max * kBlock);
     d_rq.ensure((size_t)nb_max * kBlock);
+    // the device-wide resolver's scratch for a grid of every CU (allocated here, not at its
+    // first launch: a hipMalloc inside a timed sweep cost ~8 ms)
+    {
+      static int cus = 0;
+      if (cus == 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+      }
+      d_fpg.ensure(fpg_words(2 * cus));
+    }
     if (track) {
       d_mlog.ensure((size_t)3 * n);
       d_mcount.ensure(1);
@@ -2157,7 +2168,7 @@ struct Ctx {
                                 d_freq.p, hctl, n, scap, stream));
       HIPCHK(launch_freq_gather(d_freq.p, d_sol.p, std::min(scap, nslots + 2), d * mmax, d_freq2.p, hctl, n, stream));
       const size_t fwords = (size_t)std::min(scap, nslots + 2) * d * mmax;
-      h_freq_next.ensure(fwords);
+      h_freq_next.ensure((size_t)scap * d * mmax);   // every slot count at once: no reallocation later
       HIPCHK(hipMemcpyAsync(h_freq_next.p, d_freq2.p, fwords * 4, hipMemcpyDeviceToHost, stream));
     }
     HIPCHK(launch_finish_sweep(d_counts.p, d_sol.p, d_los.p, d_src.p, scap, hctl, n, stream));
