@@ -3296,11 +3296,13 @@ struct Ctx {
     double p_rej_sm = 0.12;            // the same for split-merge's one- or two-cluster updates
     // the estimate after an update with `drift` extra uniforms over `items` draws; a window
     // the drift left (kPhiShort / kPhiWindow) widens the next one
-    static void adapt(double& p, int64_t drift, int64_t items) {
+    // (the chain's estimate stays in [0.05, 0.3] as before: a wider window no longer fits the
+    // LDS of wide rows' updates; split-merge's goes up to 0.9)
+    static void adapt(double& p, int64_t drift, int64_t items, double hi = 0.3) {
       const double ph = (double)drift / ((double)drift + 2.0 * (double)items);
-      p = std::min(0.9, std::max(0.02, 0.7 * p + 0.3 * ph));
+      p = std::min(hi, std::max(hi > 0.3 ? 0.02 : 0.05, 0.7 * p + 0.3 * ph));
     }
-    static void widen(double& p) { p = std::min(0.9, 1.5 * p + 0.05); }
+    static void widen(double& p, double hi = 0.3) { p = std::min(hi, 1.5 * p + 0.05); }
     int64_t calls = 0, fallbacks = 0;
     int last_status = 0;
   } phd;
@@ -3881,7 +3883,7 @@ struct Ctx {
                      T > 1 ? cnt[1] : -1);
       if (status == kPhiShort || status == kPhiWindow) {
         const double p0 = phd.p_rej_sm;
-        PhiDevice::widen(phd.p_rej_sm);
+        PhiDevice::widen(phd.p_rej_sm, 0.9);
         if (phd.p_rej_sm > p0) return 1;   // a wider window is worth another try
         phd.fallbacks++;
         stats.phi_device_fallbacks++;
@@ -3895,7 +3897,7 @@ struct Ctx {
     std::memcpy(sig, phd.h_out.p + o_sig, (size_t)items * 8);
     adopt_state_at(*W, target);
     rng_sync();                        // split-merge draws on the host next
-    PhiDevice::adapt(phd.p_rej_sm, cons - 3 * items, items);
+    PhiDevice::adapt(phd.p_rej_sm, cons - 3 * items, items, 0.9);
     return kOk;
   }
 
