@@ -45,6 +45,8 @@ hipError_t launch_exact_rows(const PrepassArgs& a, int nblocks, hipStream_t s);
 size_t resolve_smem_bytes(int scap, int m, int blocks);
 size_t resolve_fpg_smem_bytes(int lcap, int m);
 int resolve_fpg_max_grid(int lcap, int m);
+int warm_sweep_kernels(int lcap, int m);
+hipError_t warm_launch_kernels(const int* zero, const ResolveCtl* ctl, int* scratch, hipStream_t s);
 hipError_t launch_relabel(int* c, const int* los, int n, const ResolveCtl* ctl, hipStream_t s);
 hipError_t launch_finish_sweep(int* counts, int* sol, int* los, int* src, int cap, const ResolveCtl* ctl, int n,
                                hipStream_t s);
@@ -790,6 +792,8 @@ struct Ctx {
   DevBuf<unsigned> d_hist_part;
   DevBuf<long long> d_rprof;          // resolver phase times (debug mode bit 1)
   DevBuf<int> d_fpg;                   // k_resolve_fpg's cross-workgroup scratch
+  DevBuf<int> d_warm;                  // zero word, zeroed control block and scratch of warm_launch_kernels
+  bool kernels_warm = false;
   DevBuf<int> d_wide_ctr;              // k_prepass_wide's chunk counter, k_exact_rows_mass's point counter
   int fpg_grid_cache[65] = {0};        // its resident grid per resolver slot capacity (0: unknown, -1: none)
   PinBuf<int> h_ctl;                  // two blocks [ResolveCtl | pad to kCtlInts][resolver summary: 3 scap]
@@ -1945,7 +1949,7 @@ struct Ctx {
   // ------------------------------------------------------------------ Neal-8 sweep
   bool mcount_clear = false;
   // Buffers of a sweep (sized for n).
-  void sweep_buffers(bool track) {
+  void sweep_buffers(bool track, int m) {
     const int nb_max = (n + kBlock - 1) / kBlock;
     d_margin.ensure(n);
     d_rowpos.ensure(n);
@@ -1967,6 +1971,19 @@ struct Ctx {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
       }
       d_fpg.ensure(fpg_words(2 * cus));
+      // and the occupancy of the kernels of the unconverged regime, at every resolver slot
+      // capacity this chain can take next
+      for (int lc = 2; lc <= std::min(scap, 64); ++lc)
+        if (fpg_grid_cache[lc] == 0) {
+          const int mg = warm_sweep_kernels(lc, m);
+          fpg_grid_cache[lc] = mg >= 2 ? mg : -1;
+        }
+      if (!kernels_warm) {
+        d_warm.ensure(64);
+        HIPCHK(hipMemsetAsync(d_warm.p, 0, 64 * 4, stream));
+        HIPCHK(warm_launch_kernels(d_warm.p, (const ResolveCtl*)(d_warm.p + 16), d_warm.p + 48, stream));
+        kernels_warm = true;
+      }
     }
     if (track) {
       d_mlog.ensure((size_t)3 * n);
@@ -2226,7 +2243,7 @@ struct Ctx {
       par ^= 1;                           // the prepared sweep's control block
       ahead.par = par;
       ahead.track = freq_dev_valid;
-      sweep_buffers(ahead.track);
+      sweep_buffers(ahead.track, m);
       mark("ahead.buf");
       // the whole round 0 when the caller runs the sweep next; otherwise its prepass part
       // only (scratch outputs: any other call can still drop the prepared sweep)
@@ -2275,7 +2292,7 @@ struct Ctx {
     // every buffer sized before the wait kernel is queued (a reallocation would synchronise)
     if (h_pipe.n < 2) h_pipe.ensure(2, hipHostMallocCoherent);
     d_pipe.ensure(2);
-    sweep_buffers(track);
+    sweep_buffers(track, m);
     __atomic_store_n(&h_pipe.p[q].flag, 0, __ATOMIC_RELEASE);
     h_pipe.p[q].raw = nullptr;
     // the next sweep's draws start after this update's (about a slice): the windows that
@@ -2467,7 +2484,7 @@ struct Ctx {
     // round 0 may already be on the device (prepare_next_sweep with launch)
     const bool launched_ahead = ahead_launched;
     const bool track = (launched_ahead || ahead_prefix) ? ahead.track : (freq_dev_valid && !recount_only());
-    if (!launched_ahead && !ahead_prefix) sweep_buffers(track);
+    if (!launched_ahead && !ahead_prefix) sweep_buffers(track, m);
     while (p < n) {
       if (!(launched_ahead && stats.rounds == rounds0)) {
         // round 0 after a prepared prefix: the resolver part only (same arguments)
@@ -3562,7 +3579,6 @@ struct Ctx {
       stats.phi_device_fallbacks++;
       stats.phi_fallback_status_mask |= (int64_t)1 << (status != kPhiOk ? std::min(std::max(status, 0), 14) : 15);
       if (status == kPhiOk) stats.phi_device_last_status = -1;
-      if (status == kPhiShort || status == kPhiWindow) PhiDevice::widen(phd.p_rej);
       return -1;
     }
     stats.phi_device_calls++;
@@ -3739,7 +3755,6 @@ struct Ctx {
       phd.fallbacks++;
       stats.phi_device_fallbacks++;
       stats.phi_fallback_status_mask |= (int64_t)1 << (status != kPhiOk ? std::min(std::max(status, 0), 14) : 15);
-      if (status == kPhiShort || status == kPhiWindow) PhiDevice::widen(phd.p_rej);
       return -1;
     }
     stats.phi_device_calls++;

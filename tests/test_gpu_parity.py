@@ -160,7 +160,7 @@ def test_device_update_phi(hd, oracle, zoo, shape, walks):
     cen, sig = random_params(ds, K, 13)
     stats = sweep_case(hd, oracle, ds, ds.truth, cen, sig, ds.n * 3, seed=43, sweeps=4, phi=True, phi_device=True,
                        debug=134217728 if walks else 0)
-    assert stats["phi_device_calls"] >= 2, stats
+    assert stats["phi_device_calls"] >= 2, {k: v for k, v in stats.items() if "phi" in k}
     if walks:
         assert stats["phi_tree_calls"] == 0, stats
     elif shape != "wide":
