@@ -46,7 +46,6 @@ size_t resolve_smem_bytes(int scap, int m, int blocks);
 size_t resolve_fpg_smem_bytes(int lcap, int m);
 int resolve_fpg_max_grid(int lcap, int m);
 int warm_sweep_kernels(int lcap, int m);
-hipError_t warm_launch_kernels(const int* zero, const ResolveCtl* ctl, int* scratch, hipStream_t s);
 hipError_t launch_relabel(int* c, const int* los, int n, const ResolveCtl* ctl, hipStream_t s);
 hipError_t launch_finish_sweep(int* counts, int* sol, int* los, int* src, int cap, const ResolveCtl* ctl, int n,
                                hipStream_t s);
@@ -792,8 +791,6 @@ struct Ctx {
   DevBuf<unsigned> d_hist_part;
   DevBuf<long long> d_rprof;          // resolver phase times (debug mode bit 1)
   DevBuf<int> d_fpg;                   // k_resolve_fpg's cross-workgroup scratch
-  DevBuf<int> d_warm;                  // zero word, zeroed control block and scratch of warm_launch_kernels
-  bool kernels_warm = false;
   DevBuf<int> d_wide_ctr;              // k_prepass_wide's chunk counter, k_exact_rows_mass's point counter
   int fpg_grid_cache[65] = {0};        // its resident grid per resolver slot capacity (0: unknown, -1: none)
   PinBuf<int> h_ctl;                  // two blocks [ResolveCtl | pad to kCtlInts][resolver summary: 3 scap]
@@ -1978,12 +1975,7 @@ struct Ctx {
           const int mg = warm_sweep_kernels(lc, m);
           fpg_grid_cache[lc] = mg >= 2 ? mg : -1;
         }
-      if (!kernels_warm) {
-        d_warm.ensure(64);
-        HIPCHK(hipMemsetAsync(d_warm.p, 0, 64 * 4, stream));
-        HIPCHK(warm_launch_kernels(d_warm.p, (const ResolveCtl*)(d_warm.p + 16), d_warm.p + 48, stream));
-        kernels_warm = true;
-      }
+
     }
     if (track) {
       d_mlog.ensure((size_t)3 * n);

@@ -3669,28 +3669,6 @@ int warm_sweep_kernels(int lcap, int m) {
   return resolve_fpg_max_grid(lcap, m);
 }
 
-// One gated-off launch (every workgroup returns at its gate) of each kernel a chain reaches
-// only later, at the chain's first sweep: the first launch of a kernel inside a sweep cost
-// ~2 ms each (k_list_offsets / k_list_fill / k_exact_rows_lanes / k_resolve_fpg: ~8 ms in the
-// first unconverged sweep of a timed window).  zero: a device int that is 0; ctl: a zeroed
-// control block (k_apply_moves_lds sees an unfinished sweep).
-hipError_t warm_launch_kernels(const int* zero, const ResolveCtl* ctl, int* scratch, hipStream_t s) {
-  PrepassArgs pa{};
-  pa.gate = zero;
-  ResolveArgs ra{};
-  ra.gate = zero;
-  hipLaunchKernelGGL(k_exact_rows_lanes, dim3(1), dim3(256), 0, s, pa);
-  hipLaunchKernelGGL(k_exact_rows_mass, dim3(1), dim3(kWave * kMassWaves), 0, s, pa);
-  hipLaunchKernelGGL(k_list_fill, dim3(1), dim3(256), 0, s, pa, 0);
-  hipLaunchKernelGGL(k_list_offsets, dim3(1), dim3(kScanThreads), 0, s, (const int*)zero, 0, scratch, scratch + 1);
-  hipLaunchKernelGGL(k_resolve_fpg<24>, dim3(1), dim3(kFpThreads), 0, s, ra);
-  hipLaunchKernelGGL(k_resolve_fpg<32>, dim3(1), dim3(kFpThreads), 0, s, ra);
-  hipLaunchKernelGGL(k_resolve_fpg<64>, dim3(1), dim3(kFpThreads), 0, s, ra);
-  hipLaunchKernelGGL(k_apply_moves_lds, dim3(1), dim3(256), 0, s, (const int*)zero, (const int*)zero,
-                     (const uint8_t*)nullptr, 1, 1, 1, (unsigned int*)nullptr, ctl, 1, 2);
-  return hipGetLastError();
-}
-
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s) {
   if (a.fp && a.fpg > 1) {
     const size_t lds = resolve_fpg_lds_bytes(a.lcap, a.m);
