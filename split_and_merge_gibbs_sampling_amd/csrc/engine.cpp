@@ -2083,6 +2083,7 @@ struct Ctx {
       if (timed) HIPCHK(hipEventRecord(ev[0], stream));
       if (pg && pre_timed[cpar]) HIPCHK(hipEventRecord(ev_pp[cpar][0], stream));
       HIPCHK(launch_prepass(pa, nblocks, stream));
+      mark("r.prepass");
       if (!pg) {
         stats.prepass_points += n - p;
         round_points = n - p;
@@ -2090,6 +2091,7 @@ struct Ctx {
       if (timed) HIPCHK(hipEventRecord(ev[1], stream));
       if (pg && pre_timed[cpar]) HIPCHK(hipEventRecord(ev_pp[cpar][1], stream));
       HIPCHK(launch_exact_rows(pa, nblocks, stream));
+      mark("r.exact");
       if (fine) HIPCHK(hipEventRecord(ev[5], stream));
     }
 
@@ -2159,7 +2161,9 @@ struct Ctx {
       return kArg;
     }
     if (part == kRoundPrefix) return kOk;
+    mark("r.args");
     HIPCHK(launch_resolve(ra, stream));
+    mark("r.resolve");
     if (fine) HIPCHK(hipEventRecord(ev[2], stream));
     HIPCHK(hipEventRecord(ev_res[cpar], stream));
     return kOk;
