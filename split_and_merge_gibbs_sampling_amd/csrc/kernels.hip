@@ -548,7 +548,7 @@ bool prepass_wide_offsets_fit(const PrepassArgs& a) {
 }
 
 template <int WB, int NW, bool CL>
-__global__ __launch_bounds__(kWideThreads) void k_prepass_wide(PrepassArgs a, int nchunks) {
+__global__ __launch_bounds__(kWideThreads) void k_prepass_wide(PrepassArgs a, int nchunks, int claim) {
   if (!pipe_gate(a)) return;
   extern __shared__ uint64_t s_dyn[];
   __shared__ double s_mg[2][kWideChunk];
@@ -611,13 +611,14 @@ __global__ __launch_bounds__(kWideThreads) void k_prepass_wide(PrepassArgs a, in
         if (tid + 64 * r < kWideChunk * m1) s_raw[par][tid + 64 * r] = pf_raw[r];
     }
   };
-  // chunks are claimed from a counter (k_cluster_summary zeroes it), two ahead: a workgroup that
-  // starts late (its CU busy with another stream's kernel) leaves its share to the others
-  // instead of holding the launch's tail
+  // chunks c = blockIdx.x + k gridDim.x, two ahead.  claim != 0: claimed from a counter
+  // (k_cluster_summary zeroes it) instead, so a workgroup that starts late leaves its share to
+  // the others -- but every claim is a same-address device atomic, and at C4 (4,400 chunks on
+  // 1,024 workgroups) they took the kernel from 50 to 80 us (profiles/r04/r5)
   __shared__ int s_cl[2];
   if (tid == 0) {
-    s_cl[0] = atomicAdd(a.wide_ctr, 1);
-    s_cl[1] = atomicAdd(a.wide_ctr, 1);
+    s_cl[0] = claim ? atomicAdd(a.wide_ctr, 1) : (int)blockIdx.x;
+    s_cl[1] = claim ? atomicAdd(a.wide_ctr, 1) : (int)(blockIdx.x + gridDim.x);
   }
   __syncthreads();
   int c = s_cl[0];
@@ -659,7 +660,7 @@ __global__ __launch_bounds__(kWideThreads) void k_prepass_wide(PrepassArgs a, in
     if (cprev >= 0 && tid < 64) finish(cprev, par ^ 1);
     // the next chunk (claimed an iteration ago); claim the one after it
     const int cn = s_cl[(it + 1) & 1];
-    if (tid == 0) s_cl[it & 1] = cn < nchunks ? atomicAdd(a.wide_ctr, 1) : nchunks;
+    if (tid == 0) s_cl[it & 1] = cn < nchunks ? (claim ? atomicAdd(a.wide_ctr, 1) : cn + (int)gridDim.x) : nchunks;
     if (cn < nchunks) fetch(cn);
     const int64_t i0 = (int64_t)a.p0 + (int64_t)c * kWideChunk;
     const int npts = (int)min((int64_t)kWideChunk, (int64_t)a.n - i0);
@@ -807,8 +808,7 @@ static int wide_grid(F kern, size_t lds) {
   }
   int per = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, kWideThreads, lds) != hipSuccess || per <= 0) per = 1;
-  // HDPM_WIDE_WGS: workgroups per CU (A/B of the persistent grid; chunks are claimed from a
-  // counter, so workgroups beyond the resident ones only find the work gone)
+  // HDPM_WIDE_WGS: workgroups per CU (A/B of the persistent grid)
   static const int ovr = [] {
     const char* e = std::getenv("HDPM_WIDE_WGS");
     return e ? std::atoi(e) : 0;
@@ -3274,7 +3274,12 @@ static hipError_t launch_prepass_w(const PrepassArgs& a, int nblocks, hipStream_
     const int nchunks = (a.n - a.p0 + kWideChunk - 1) / kWideChunk;
     auto go = [&](auto kern) {
       const int grid = std::min(nchunks, wide_grid(kern, lds));
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(kWideThreads), lds, s, a, nchunks);
+      // HDPM_WIDE_CLAIM=1: chunks claimed from a counter (A/B; see k_prepass_wide)
+      static const int claim = [] {
+        const char* e = std::getenv("HDPM_WIDE_CLAIM");
+        return e ? std::atoi(e) : 0;
+      }();
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(kWideThreads), lds, s, a, nchunks, claim);
       return hipGetLastError();
     };
     if constexpr (WB <= 2) {
