@@ -3326,7 +3326,7 @@ __device__ __forceinline__ void mass_decide(const PrepassArgs& a, int q, int own
   }
 }
 
-__global__ __launch_bounds__(kWave * kMassWaves) void k_exact_rows_mass(PrepassArgs a) {
+__global__ __launch_bounds__(kWave * kMassWaves) void k_exact_rows_mass(PrepassArgs a, int order_static) {
   if (!pipe_gate(a)) return;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ double lp_w[kMassWaves][kWave];
@@ -3371,11 +3371,16 @@ __global__ __launch_bounds__(kWave * kMassWaves) void k_exact_rows_mass(PrepassA
   // batches of kMassBatch points claimed from a counter (k_cluster_summary clears it; a
   // workgroup that is not resident leaves its share to the others); the batch's records
   // (k_list_fill wrote them to rq) and stream draws are loaded together, one lane per word
+  // (order_static: batch b = wave + k waves of the grid instead, no claims -- A/B, HDPM_MASS_STATIC)
   constexpr int kMassBatch = 4;
-  for (;;) {
+  for (int bi = 0;; ++bi) {
     int q0 = 0;
-    if (lane == 0) q0 = atomicAdd(a.wide_ctr + 1, kMassBatch);
-    q0 = __shfl(q0, 0);
+    if (order_static) {
+      q0 = (int)(((int64_t)blockIdx.x * kMassWaves + wv + (int64_t)bi * gridDim.x * kMassWaves) * kMassBatch);
+    } else {
+      if (lane == 0) q0 = atomicAdd(a.wide_ctr + 1, kMassBatch);
+      q0 = __shfl(q0, 0);
+    }
     if (q0 >= total) break;
     const int nb = min(kMassBatch, total - q0);
     const int kq = lane >> 4, wq = lane & 15;                     // point of the batch, word
@@ -3615,7 +3620,11 @@ hipError_t launch_exact_rows(const PrepassArgs& a0, int nblocks, hipStream_t s) 
     return hipGetLastError();
   }
   if (a.exact_scan && !a.exact_wave && E <= kWave && mlds <= 96 * 1024) {
-    hipLaunchKernelGGL(k_exact_rows_mass, dim3(mass_grid(mlds)), dim3(kWave * kMassWaves), mlds, s, a);
+    static const int mstatic = [] {
+      const char* e = std::getenv("HDPM_MASS_STATIC");
+      return e ? std::atoi(e) : 0;
+    }();
+    hipLaunchKernelGGL(k_exact_rows_mass, dim3(mass_grid(mlds)), dim3(kWave * kMassWaves), mlds, s, a, mstatic);
     return hipGetLastError();
   }
   if (wg && E <= kWave) hipLaunchKernelGGL(k_exact_rows_wg<1>, g, b, lds, s, a);
