@@ -210,7 +210,7 @@ def host_cpu():
     return model, len(os.sched_getaffinity(0)), os.cpu_count()
 
 
-def cpu_baseline(ds, eng, m: int, budget_s: float, opt_threads: int):
+def cpu_baseline(ds, eng, m: int, budget_s: float, opt_threads: int, threads_source: str = ""):
     """The CPU baselines of SURVEY 8(d), timed on this host on the current chain state with
     the engine's latent pool (oracle/ is the checker; these legs only time it):
       1. reference-faithful restatement (O(N) bookkeeping per point as in code/neal8.cpp,
@@ -270,6 +270,7 @@ def cpu_baseline(ds, eng, m: int, budget_s: float, opt_threads: int):
     t_rest = time.perf_counter() - t0
     faithful["optimised"] = {
         "value": 1.0 / (t + t_rest), "unit": "sweeps/s", "cores": opt_threads, "kind": "port",
+        "threads_source": threads_source,
         "sample": (f"one full step of the optimised oracle (oracle/src/fast.c, same trace): sweep {t:.2f} s "
                    f"(log-likelihoods on {opt_threads} threads, serial scan) + update_phi + compute_loglikelihood "
                    f"{t_rest:.2f} s; host {model}"),
@@ -472,10 +473,18 @@ def main():
         "note": "the sweep proves 'stay' from bounds for most points (DESIGN.md 4.3-4.4) and moves the prepass bytes; "
                 "SURVEY 8(d)'s N(D(2+9m)+8) is the direct design's traffic and is not the roofline of this path"}
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+        # the optimised oracle's threads: --cpu-threads, else this process's CPU share
+        # (OMP_NUM_THREADS: 16 per GPU on the GPU box, whose nproc counts the whole host),
+        # else every usable CPU -- the source is recorded in the line
         usable = host_cpu()[1]
         share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-        thr = args.cpu_threads or (min(usable, share) if share > 0 else usable)
-        out["cpu_baseline"] = cpu_baseline(ds, eng, args.m, args.cpu_baseline_seconds, thr)
+        if args.cpu_threads:
+            thr, src = args.cpu_threads, "--cpu-threads"
+        elif share > 0:
+            thr, src = min(usable, share), f"OMP_NUM_THREADS={share} (the GPU's CPU share), {usable} usable"
+        else:
+            thr, src = usable, "every usable CPU (OMP_NUM_THREADS unset)"
+        out["cpu_baseline"] = cpu_baseline(ds, eng, args.m, args.cpu_baseline_seconds, thr, src)
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()

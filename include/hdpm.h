@@ -95,6 +95,16 @@ typedef struct {
     int64_t phi_fallback_status_mask;
     /* split-merge device updates re-run with a wider drift window (the drift left the first) */
     int64_t phi_sm_window_retries;
+    /* k_resolve_fpg launches that gave up at a grid barrier (a workgroup not resident within the
+     * limit, HDPM_OPT_FPG_WAIT_US) and were continued from their first undecided point by the
+     * one-workgroup resolver */
+    int64_t fpg_aborts;
+    /* exact-row launches by the mass kernels: a wave per point (k_exact_rows_mass) and a thread
+     * per point (k_exact_rows_lanes) */
+    int64_t exact_mass_launches, exact_lanes_launches;
+    /* launches that listed every point (a context's first launch, or more than half the points
+     * expected uncertain: a chain far from convergence) */
+    int64_t dense_launches;
 } hdpm_stats;
 
 int         hdpm_device_count(void);
@@ -239,6 +249,14 @@ int hdpm_get_pool_heads(hdpm_ctx* ctx, uint64_t* out, int64_t P);
  * the limit to -value without that check, so the device-side gate-off (and the engine's
  * recovery from it: the sweep re-run ungated, same chain) can be exercised. */
 #define HDPM_OPT_PIPE_WAIT_US 3
+/* HDPM_OPT_FPG_WAIT_US: the limit, in microseconds, after which a grid barrier of the device-wide
+ * resolver (k_resolve_fpg) gives up (default 2 s).  A launch that gives up has committed
+ * exactly the windows before the barrier; it ends as a restart there and the engine continues
+ * with the one-workgroup resolver (same chain; hdpm_stats.fpg_aborts counts these). */
+#define HDPM_OPT_FPG_WAIT_US 4
+/* HDPM_OPT_FPG_FAIL_AT (testing): workgroup 0 of every k_resolve_fpg launch gives up at its
+ * value-th grid barrier (0: never), to exercise that recovery deterministically. */
+#define HDPM_OPT_FPG_FAIL_AT 5
 int hdpm_set_option(hdpm_ctx* ctx, int32_t option, double value);
 /* Posterior analysis (realdata_analysis/zoo_simulator.R:193-236, 339-344; mcclust /
  * mcclust.ext).  hdpm_psm_build: the posterior similarity matrix of M saved label vectors

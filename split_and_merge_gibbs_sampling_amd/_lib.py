@@ -33,6 +33,8 @@ EXPORTS = (
 OPT_HIG_LOGSPACE = 1
 OPT_PHI_DEVICE = 2
 OPT_PIPE_WAIT_US = 3
+OPT_FPG_WAIT_US = 4
+OPT_FPG_FAIL_AT = 5
 
 STATUS = {0: "OK", 1: "E_VALIDATE", 2: "E_GSL", 3: "E_PROB", 4: "E_WALKER", 5: "E_ARG",
           6: "E_DEVICE", 7: "E_NODEVICE"}
@@ -67,7 +69,8 @@ class Stats(C.Structure):
                                   "pipe_refused", "pipe_recovered", "phi_tree_calls", "phi_tree_retries",
                                   "pool_walk_fallbacks", "phi_dspec_launched", "phi_dspec_used",
                                   "fpg_launches", "phi_sm_device_calls", "phi_fallback_status_mask",
-                                  "phi_sm_window_retries")]
+                                  "phi_sm_window_retries", "fpg_aborts", "exact_mass_launches",
+                                  "exact_lanes_launches", "dense_launches")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

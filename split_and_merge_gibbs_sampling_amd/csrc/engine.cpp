@@ -41,11 +41,12 @@ namespace hdpm {
 hipError_t launch_prepass(const PrepassArgs& a, int nblocks, hipStream_t s);
 hipError_t launch_cluster_summary(const PrepassArgs& a, hipStream_t s);
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s);
-hipError_t launch_exact_rows(const PrepassArgs& a, int nblocks, hipStream_t s);
+hipError_t launch_exact_rows(const PrepassArgs& a, int nblocks, hipStream_t s, int* path = nullptr);
 size_t resolve_smem_bytes(int scap, int m, int blocks);
 size_t resolve_fpg_smem_bytes(int lcap, int m);
 int resolve_fpg_max_grid(int lcap, int m);
 int warm_sweep_kernels(int lcap, int m);
+int device_cus();
 hipError_t launch_relabel(int* c, const int* los, int n, const ResolveCtl* ctl, hipStream_t s);
 hipError_t launch_finish_sweep(int* counts, int* sol, int* los, int* src, int cap, const ResolveCtl* ctl, int n,
                                hipStream_t s);
@@ -793,6 +794,14 @@ struct Ctx {
   DevBuf<int> d_fpg;                   // k_resolve_fpg's cross-workgroup scratch
   DevBuf<int> d_wide_ctr;              // k_prepass_wide's chunk counter, k_exact_rows_mass's point counter
   int fpg_grid_cache[65] = {0};        // its resident grid per resolver slot capacity (0: unknown, -1: none)
+  int fpg_grid_m = -1;                 // ... for this m (the LDS of k_resolve_fpg depends on m)
+  int& fpg_grid(int lcap, int m) {
+    if (m != fpg_grid_m) {
+      std::fill(fpg_grid_cache, fpg_grid_cache + 65, 0);
+      fpg_grid_m = m;
+    }
+    return fpg_grid_cache[lcap];
+  }
   PinBuf<int> h_ctl;                  // two blocks [ResolveCtl | pad to kCtlInts][resolver summary: 3 scap]
   // Consecutive sweeps alternate between the two control blocks (and resolver events), so a
   // sweep enqueued ahead (pre_enqueue) does not overwrite the one the host is reading.
@@ -819,6 +828,12 @@ struct Ctx {
   // exercise the device-side gate-off and its recovery in neal8_sweep)
   long long pipe_limit_ticks = 200000000LL;
   bool pipe_host_check = true;
+  // k_resolve_fpg's grid-barrier limit (ticks, 2 s) and the barrier at which workgroup 0 gives up
+  // (testing, 0: none): HDPM_OPT_FPG_WAIT_US / HDPM_OPT_FPG_FAIL_AT.  A launch that gave up ends
+  // as a restart and the next launch takes the one-workgroup resolver (fpg_skip).
+  long long fpg_limit_ticks = 200000000LL;
+  int fpg_fail_at = 0;
+  bool fpg_skip = false;
   bool deep_ok = false;                // set by iteration(): the next sweep may be enqueued ahead
   static constexpr size_t kCtlInts = 16;
   static_assert(sizeof(ResolveCtl) <= kCtlInts * sizeof(int), "control block");
@@ -1961,19 +1976,14 @@ struct Ctx {
     // the device-wide resolver's scratch for a grid of every CU (allocated here, not at its
     // first launch: a hipMalloc inside a timed sweep cost ~8 ms)
     {
-      static int cus = 0;
-      if (cus == 0) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-      }
+      const int cus = device_cus();
       d_fpg.ensure(fpg_words(2 * cus));
       // and the occupancy of the kernels of the unconverged regime, at every resolver slot
       // capacity this chain can take next
       for (int lc = 2; lc <= std::min(scap, 64); ++lc)
-        if (fpg_grid_cache[lc] == 0) {
+        if (fpg_grid(lc, m) == 0) {
           const int mg = warm_sweep_kernels(lc, m);
-          fpg_grid_cache[lc] = mg >= 2 ? mg : -1;
+          fpg_grid(lc, m) = mg >= 2 ? mg : -1;
         }
 
     }
@@ -1994,6 +2004,25 @@ struct Ctx {
   static constexpr int kFpMinListed = 64;
   static constexpr int kFpgMinListed = 1024;   // listed points of the previous launch for k_resolve_fpg (two chunks)
   static constexpr int kMassNoSpec = 65536;    // expected listed points above which no snapshot draws are made
+  static constexpr int kDenseMinPoints = 4096;  // dense listing only for launches over at least this many points
+  // the state fits the dense path: the fixed-point resolvers and a mass exact-rows kernel
+  // (kernels.hip launch_exact_rows: the thread-per-point kernel's LDS tables, or the
+  // wave-per-point kernel's)
+  bool dense_list_fits(int m, int nslots) const {
+    const int lcap = std::min(scap, nslots + 2);
+    if (!fp_eligible(K + m, lcap) || (debug & (2048 | 8))) return false;
+    const size_t lanes_lds = (size_t)K * (2 * (size_t)d * 8 + (size_t)nq * 16);
+    const size_t mass_lds = (size_t)K * 2 * d * 8 + (size_t)8 * m * d * 8 + (size_t)K * nq * 16 + (size_t)8 * nq * 16;
+    return (nq <= 8 && K <= 64 && lanes_lds <= 64 * 1024) || mass_lds <= 96 * 1024;
+  }
+  // HDPM_DENSE_LIST=0: no dense listing (A/B)
+  static bool dense_list_on() {
+    static const bool on = [] {
+      const char* e = std::getenv("HDPM_DENSE_LIST");
+      return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+  }
   bool fp_eligible(int E, int lcap) const {
     return E <= 64 && lcap <= 64 && !(debug & (1 | 4096 | 8192 | 8388608));
   }
@@ -2006,7 +2035,20 @@ struct Ctx {
     ensure_slots(nslots + 2);
     // points this launch will likely list: the previous launch's density over [p, n) (a
     // restart late in a sweep lists few points; the next sweep's first launch lists many)
-    const int el = last_density < 0 ? -1 : (int)std::min<double>((double)n, last_density * (double)(n - p) + 0.5);
+    // A context's first launch has no previous density: it is taken as dense (every point listed)
+    // where the mass exact-rows kernels and the fixed-point resolvers fit -- from a random start
+    // (the scripts' L = 20) nearly every point is uncertain, and a first sweep sized for a
+    // converged chain ran on one workgroup (~220 ms at C5); a converged chain pays one dense
+    // sweep once.
+    const bool dense_fits = dense_list_fits(m, nslots);
+    const int el = last_density < 0 ? (dense_fits ? n - p : -1)
+                                    : (int)std::min<double>((double)n, last_density * (double)(n - p) + 0.5);
+    // Dense launches (more than half the points expected uncertain) list every point: the
+    // resolver then decides all of them and never re-tests an unlisted one against the count
+    // drift -- a re-test failure restarted the launch, and its prepass and exact rows, at that
+    // point (C5 from a random start: ~118 certified points per sweep restarted ~700k rows)
+    const bool dense_list = dense_fits && el >= kDenseMinPoints && 2 * (int64_t)el >= (int64_t)(n - p) &&
+                            !(debug & 1) && dense_list_on();
     // the resolver writes its control block and summary straight into host memory
     if (h_ctl.n < 2 * ctl_stride()) h_ctl.ensure(2 * ctl_stride(), hipHostMallocCoherent);
     for (auto& e : ev_res)
@@ -2039,7 +2081,7 @@ struct Ctx {
     d_csum.ensure((size_t)std::max(K, 1) * (bw + 2));
     pa.csum = d_csum.p;
 
-    pa.thresh = (debug & 1) ? INFINITY : T + 2.0 * dmax;
+    pa.thresh = ((debug & 1) || dense_list) ? INFINITY : T + 2.0 * dmax;
     // certification by the draw's uniform only while the chain is settled: after a launch
     // that exceeded its drift budget, restarted or decided many points itself, uniform-
     // certified points (no exact rows) would fail re-verification and restart the launch
@@ -2048,7 +2090,8 @@ struct Ctx {
     const bool fp_next = fp_eligible(K + m, std::min(scap, nslots + 2)) &&
                          (el < 0 || el >= kFpMinListed || (debug & 33554432));
     const bool many_exact = last_exact >= kResolveBlkMin && (!fp_next || (debug & 16777216));
-    pa.dmax2 = ((debug & (1 | 262144)) || last_unsettled || many_exact) ? INFINITY : 2.0 * dmax;
+    pa.dmax2 = ((debug & (1 | 262144)) || last_unsettled || many_exact || dense_list) ? INFINITY : 2.0 * dmax;
+    if (dense_list && !pg && part != kRoundResolve) stats.dense_launches++;
     pa.L = d_L.p; pa.rowpos = d_rowpos.p; pa.margin = d_margin.p; pa.list = d_list.p; pa.cnt = d_cnt.p;
     pa.dense = d_dense.p; pa.dense_total = d_dense_total.p; pa.boff = d_boff.p;
     // snapshot draws (k_exact_rows*: the resolver's first-round guesses and kept draws) except
@@ -2090,7 +2133,12 @@ struct Ctx {
       }
       if (timed) HIPCHK(hipEventRecord(ev[1], stream));
       if (pg && pre_timed[cpar]) HIPCHK(hipEventRecord(ev_pp[cpar][1], stream));
-      HIPCHK(launch_exact_rows(pa, nblocks, stream));
+      int xpath = 0;
+      HIPCHK(launch_exact_rows(pa, nblocks, stream, &xpath));
+      if (!pg) {
+        if (xpath == 1) stats.exact_mass_launches++;
+        if (xpath == 2) stats.exact_lanes_launches++;
+      }
       mark("r.exact");
       if (fine) HIPCHK(hipEventRecord(ev[5], stream));
     }
@@ -2137,8 +2185,13 @@ struct Ctx {
     // points: one 512-point chunk per workgroup, a workgroup per CU (debug bit 29: one workgroup)
     ra.fpg = 0;
     ra.fpg_buf = nullptr;
-    if (ra.fp && (el >= kFpgMinListed || (debug & 1073741824)) && !(debug & 536870912) && ra.lcap <= 64) {
-      int& mg = fpg_grid_cache[ra.lcap];
+    ra.fpg_limit = fpg_limit_ticks;
+    ra.fpg_fail = fpg_fail_at;
+    const bool fpg_skipped = fpg_skip && part != kRoundPrefix;
+    if (fpg_skipped) fpg_skip = false;
+    if (ra.fp && !fpg_skipped && (el >= kFpgMinListed || (debug & 1073741824)) && !(debug & 536870912) &&
+        ra.lcap <= 64) {
+      int& mg = fpg_grid(ra.lcap, m);
       if (mg == 0) {
         mg = resolve_fpg_max_grid(ra.lcap, m);
         if (mg < 2) mg = -1;
@@ -2146,7 +2199,7 @@ struct Ctx {
       if (mg > 0 && resolve_fpg_smem_bytes(ra.lcap, m) <= 160 * 1024) {
         const int G = std::min(mg, std::max(2, (std::max(el, 0) + 511) / 512));
         d_fpg.ensure(fpg_words(G));
-        HIPCHK(hipMemsetAsync(d_fpg.p, 0, (size_t)kFpgBarWords * 4, stream));
+        HIPCHK(hipMemsetAsync(d_fpg.p, 0, (size_t)kFpgZeroWords * 4, stream));
         ra.fpg = G;
         ra.fpg_buf = d_fpg.p;
         if (!pg) stats.fpg_launches++;
@@ -2583,6 +2636,12 @@ struct Ctx {
       sweep_moves += c.moves;
       stats.checked_rounds += c.checked;
       last_unsettled = c.checked || (c.restart && c.next < n);
+      if (c.aborted && !c.status) {
+        // k_resolve_fpg gave up at a grid barrier (a workgroup not resident within the limit):
+        // everything before c.next is committed; the restart runs on one workgroup
+        stats.fpg_aborts++;
+        fpg_skip = true;
+      }
       if (c.status) {
         err = c.status == kValidate ? "State validation failed: inconsistent cluster count from Neal8 case 2"
               : c.status == kWalker ? "Walker alias table failure"
@@ -4611,6 +4670,16 @@ int hdpm_set_option(hdpm_ctx* h, int32_t option, double value) {
     case HDPM_OPT_PHI_DEVICE:
       GUARD(ctx->cancel_ahead();)
       ctx->phi_mode = value != 0.0 ? 1 : 0;
+      return HDPM_OK;
+    case HDPM_OPT_FPG_WAIT_US:
+      if (!(value > 0.0) || !std::isfinite(value)) { ctx->err = "fpg wait limit must be positive"; return HDPM_E_ARG; }
+      GUARD(ctx->cancel_ahead();)
+      ctx->fpg_limit_ticks = std::max(1LL, (long long)(value * 100.0));
+      return HDPM_OK;
+    case HDPM_OPT_FPG_FAIL_AT:
+      if (value < 0.0 || value > 1e9) { ctx->err = "fpg fail ordinal out of range"; return HDPM_E_ARG; }
+      GUARD(ctx->cancel_ahead();)
+      ctx->fpg_fail_at = (int)value;
       return HDPM_OK;
     case HDPM_OPT_PIPE_WAIT_US:
       if (value == 0.0 || !std::isfinite(value)) { ctx->err = "pipe wait limit must be non-zero"; return HDPM_E_ARG; }

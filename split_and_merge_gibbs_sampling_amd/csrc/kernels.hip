@@ -24,6 +24,20 @@
 
 namespace hdpm {
 
+// Compute units of the current device, queried once per device (grids of persistent kernels;
+// several contexts of one process may sit on different devices)
+int device_cus() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  int c = __atomic_load_n(&cache[dev], __ATOMIC_RELAXED);
+  if (c <= 0) {
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+    __atomic_store_n(&cache[dev], c, __ATOMIC_RELAXED);
+  }
+  return c;
+}
+
 // Device copies of glibc's exp / log tables: every exp and log whose result decides a draw
 // (n8:95, sm:209-210, sm:150-158) runs glibc's algorithm (glibc_math.hpp), so the device's
 // probabilities are the host libm's bit for bit and the reference's cumulative compare
@@ -800,12 +814,7 @@ __global__ __launch_bounds__(kWideThreads) void k_prepass_wide(PrepassArgs a, in
 // Workgroups of k_prepass_wide in flight on the whole GPU (persistent grid).
 template <class F>
 static int wide_grid(F kern, size_t lds) {
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-  }
+  const int cus = device_cus();
   int per = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, kWideThreads, lds) != hipSuccess || per <= 0) per = 1;
   // HDPM_WIDE_WGS: workgroups per CU (A/B of the persistent grid)
@@ -919,7 +928,7 @@ __global__ __launch_bounds__(256) void k_list_fill(PrepassArgs a, int want_rq) {
 __device__ __forceinline__ void wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 struct RShared {
-  int K, nslots, status, next, restart, moves, exact, checked, pick, src, nstruct, pad0;
+  int K, nslots, status, next, restart, moves, exact, checked, pick, src, nstruct, aborted;
   double dnow, sum;
   double dvmax;        // max over slots of |logn[count] - logn[snapshot count]|
   double pad;
@@ -1932,7 +1941,7 @@ __device__ __forceinline__ void resolve_init(const ResolveArgs& a, const RState&
   }
   if (threadIdx.x == 0) {
     S.K = a.K; S.nslots = a.nslots; S.status = 0; S.next = a.n; S.restart = 0;
-    S.moves = 0; S.exact = 0; S.checked = 0; S.dnow = 0.0; S.dvmax = 0.0; S.nstruct = 0;
+    S.moves = 0; S.exact = 0; S.checked = 0; S.dnow = 0.0; S.dvmax = 0.0; S.nstruct = 0; S.aborted = 0;
     S.bgo = 1; S.bq = 0;
     for (int k = 0; k < 8; ++k) S.tsub[k] = 0;
   }
@@ -1968,6 +1977,7 @@ __device__ __forceinline__ void resolve_finish(const ResolveArgs& a, const RStat
     c.next = S.next; c.status = S.status; c.restart = S.restart; c.K = S.K; c.nslots = S.nslots;
     c.moves = S.moves; c.exact = S.exact; c.checked = S.checked;
     c.listed = *a.dense_total;
+    c.aborted = S.aborted;
     *a.ctl = c;
   }
 }
@@ -3387,7 +3397,7 @@ __global__ __launch_bounds__(kWave * kMassWaves) void k_exact_rows_mass(PrepassA
     int4 rec = make_int4(0, 0, 0, 0);
     if (kq < nb) rec = a.rq[q0 + kq];
     uint32_t rw = 0;
-    if (kq < nb && wq < m1) rw = a.raw[(int64_t)rec.y * m1 + wq];
+    if (kq < nb && wq < m1 && m1 <= 16) rw = a.raw[(int64_t)rec.y * m1 + wq];
     for (int k = 0; k < nb; ++k) {
       const int q = q0 + k;
       const int row = __shfl(rec.x, 16 * k), own = __shfl(rec.z, 16 * k);
@@ -3395,6 +3405,8 @@ __global__ __launch_bounds__(kWave * kMassWaves) void k_exact_rows_mass(PrepassA
       const uint32_t rawm = (uint32_t)__shfl(rec.w, 16 * k);
       if (lane < a.nq) *(uint4*)(lx + lane * 16) = *(const uint4*)(a.codes_t + tiled_offset(i, lane * 16, a.nq));
       // latent values: (u, j) pairs over the lanes, a batch of 8 per lane with every load issued first
+      // (the point's m latent draws come from the 16 words its lane group loaded; with m + 1 > 16
+      // words each lane reads its draw from the stream itself)
       for (int b0 = 0; b0 < m * D; b0 += 8 * kWave) {
         uint8_t cc[8];
         double2 pr[8];
@@ -3402,7 +3414,8 @@ __global__ __launch_bounds__(kWave * kMassWaves) void k_exact_rows_mass(PrepassA
         for (int t = 0; t < 8; ++t) {
           const int idx = b0 + t * kWave + lane;
           const int u = idx / D;
-          const uint32_t y = (uint32_t)__shfl((int)rw, 16 * k + min(u, m - 1));
+          const uint32_t y = m1 <= 16 ? (uint32_t)__shfl((int)rw, 16 * k + min(u, m - 1))
+                                      : a.raw[i * m1 + min(u, m - 1)];
           if (idx < m * D) {
             const int j = idx - u * D;
             const int64_t pe = pick_entry(y, a.P);
@@ -3556,24 +3569,14 @@ __global__ __launch_bounds__(256) void k_exact_rows_lanes(PrepassArgs a) {
 }
 
 static int lanes_grid(size_t lds) {
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-  }
+  const int cus = device_cus();
   int per = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_exact_rows_lanes, 256, lds) != hipSuccess || per <= 0) per = 1;
   return cus * per;
 }
 
 static int mass_grid(size_t lds) {
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-  }
+  const int cus = device_cus();
   int per = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_exact_rows_mass, kWave * kMassWaves, lds) != hipSuccess ||
       per <= 0)
@@ -3585,7 +3588,8 @@ static int mass_grid(size_t lds) {
   return cus * per;
 }
 
-hipError_t launch_exact_rows(const PrepassArgs& a0, int nblocks, hipStream_t s) {
+hipError_t launch_exact_rows(const PrepassArgs& a0, int nblocks, hipStream_t s, int* path) {
+  if (path) *path = 0;
   PrepassArgs a = a0;
   a.lblock = prepass_list_block(a);
   a.nlb = (a.n - a.p0 + a.lblock - 1) / a.lblock;
@@ -3617,6 +3621,7 @@ hipError_t launch_exact_rows(const PrepassArgs& a0, int nblocks, hipStream_t s) 
   if (a.exact_scan && !a.spec && !a.exact_wave && a.nq <= kLanesMaxNq && a.K <= kWave && llds <= 64 * 1024 &&
       !force_mass) {
     hipLaunchKernelGGL(k_exact_rows_lanes, dim3(lanes_grid(llds)), dim3(256), llds, s, a);
+    if (path) *path = 2;
     return hipGetLastError();
   }
   if (a.exact_scan && !a.exact_wave && E <= kWave && mlds <= 96 * 1024) {
@@ -3625,6 +3630,7 @@ hipError_t launch_exact_rows(const PrepassArgs& a0, int nblocks, hipStream_t s) 
       return e ? std::atoi(e) : 0;
     }();
     hipLaunchKernelGGL(k_exact_rows_mass, dim3(mass_grid(mlds)), dim3(kWave * kMassWaves), mlds, s, a, mstatic);
+    if (path) *path = 1;
     return hipGetLastError();
   }
   if (wg && E <= kWave) hipLaunchKernelGGL(k_exact_rows_wg<1>, g, b, lds, s, a);
@@ -3763,6 +3769,7 @@ __global__ void k_pipe_wait(const PipeSlot* slot, const ResolveCtl* prev, Resolv
     volatile ResolveCtl* o = own;
     o->status = kPipeOff;
     o->next = 0;
+    o->aborted = 0;
   }
 }
 hipError_t launch_pipe_wait(const PipeSlot* slot, const ResolveCtl* prev, ResolveCtl* own, int n, PipeGate* g,

@@ -186,6 +186,8 @@ struct ResolveCtl {
   int exact;      // decisions computed in the resolver (not taken from the snapshot draws)
   int checked;    // 1 if the drift budget was exceeded (checked mode)
   int listed;     // points the prepass left uncertain (exact rows built) in this launch
+  int aborted;    // 1: k_resolve_fpg gave up at a grid barrier (a workgroup not resident in time);
+                  // the state is consistent at `next` (restart there, with k_resolve_fp)
 };
 
 struct ResolveArgs {
@@ -243,6 +245,8 @@ struct ResolveArgs {
   // fpg_buf = fpg_words(fpg) ints of cross-workgroup scratch, its kFpgBarWords barrier words zeroed by the host
   int fpg;
   int* fpg_buf;
+  long long fpg_limit;       // a grid barrier gives up after this many wall_clock64 ticks (100 MHz)
+  int fpg_fail;              // testing: workgroup 0 gives up at its fpg_fail-th grid barrier (0: never)
 };
 // Cross-workgroup scratch of k_resolve_fpg (G workgroups), in ints: barrier [0, 96), state mirror
 // [96, 96 + 8 + 3 * 64 + 16), then per workgroup: stop, changed, fail, moves, fresh, and the
@@ -251,7 +255,8 @@ struct ResolveArgs {
 constexpr int kFpgSlots = 64;
 constexpr int kFpgState = 8;
 constexpr int kFpgPerWg = 8;
-constexpr int kFpgBarWords = 96;   // barrier words (arrivals, generation, abort on separate lines)
+constexpr int kFpgBarWords = 96;   // barrier words (the 64-bit barrier word at 0, then padding)
+constexpr int kFpgZeroWords = kFpgBarWords + kFpgState + 16;   // zeroed before every launch (barrier, state mirror)
 __host__ __device__ inline size_t fpg_words(int G) {
   return (size_t)kFpgBarWords + kFpgState + 3 * kFpgSlots + 16 + (size_t)G * kFpgPerWg + (size_t)2 * G * kFpgSlots +
          (size_t)2 * G + 16;

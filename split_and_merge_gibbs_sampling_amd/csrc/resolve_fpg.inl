@@ -75,31 +75,58 @@ __device__ __forceinline__ double aldd(const double* p) {
   return __longlong_as_double((long long)u);
 }
 
-// Grid barrier (sense by generation): false when it gave up (2 s) or another workgroup did.
-__device__ __forceinline__ bool sync(const Lay& L, int G, int* flag) {
+// Grid barrier, all or nothing: either every workgroup passes it or none does.  One 64-bit
+// word (zeroed by the host before the launch): generation in the high half, a poison bit and
+// the arrival count in the low half.  The last arrival advances the generation (count back to
+// 0); a workgroup that waited `limit` ticks (or is told to give up: `fail`, testing) poisons the
+// word, by compare-and-swap, only while the generation is unchanged and not every workgroup has
+// arrived, so no barrier is both passed and poisoned.  A poisoned word stays poisoned: every
+// later arrival sees it and gives up too.  False: this barrier (and the launch) gave up -- the
+// caller then knows that no workgroup got past it.
+constexpr unsigned long long kBarPoison = 1ull << 31;
+constexpr unsigned long long kBarCount = kBarPoison - 1;
+__device__ __forceinline__ bool sync(const Lay& L, int G, int* flag, long long limit, bool fail) {
   __syncthreads();
   if (threadIdx.x == 0) {
     __threadfence();
     int ab = 0;
-    int* const gen_p = L.bar + 32;
-    int* const abort_p = L.bar + 64;
-    const int gen = __hip_atomic_load(gen_p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-    const int arrived = __hip_atomic_fetch_add(&L.bar[0], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1;
-    if (arrived == G) {
-      __hip_atomic_store(&L.bar[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(gen_p, gen + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long* const w = reinterpret_cast<unsigned long long*>(L.bar);
+    auto give_up = [&](unsigned gen) -> int {   // 1: poisoned (or found poisoned), 0: the barrier passed
+      unsigned long long cur = __hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      for (;;) {
+        if ((unsigned)(cur >> 32) != gen) return 0;
+        if (cur & kBarPoison) return 1;
+        if ((cur & kBarCount) >= (unsigned long long)G) return -1;   // completing: wait for the generation
+        if (__hip_atomic_compare_exchange_strong(w, &cur, cur | kBarPoison, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
+                                                 __HIP_MEMORY_SCOPE_AGENT))
+          return 1;
+      }
+    };
+    if (fail) {
+      // this workgroup never arrives, so the barrier can neither pass nor be completing
+      const unsigned long long cur = __hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      (void)give_up((unsigned)(cur >> 32));
+      ab = 1;
     } else {
-      const long long t0 = wall_clock64();
-      for (int spin = 0; __hip_atomic_load(gen_p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == gen; ++spin) {
-        if ((spin & 31) == 31) {     // the abort flag and the time limit, now and then
-          if (__hip_atomic_load(abort_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { ab = 1; break; }
-          if (wall_clock64() - t0 > 200000000LL) {
-            __hip_atomic_store(abort_p, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            ab = 1;
-            break;
+      const unsigned long long old = __hip_atomic_fetch_add(w, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned gen = (unsigned)(old >> 32);
+      if (old & kBarPoison) {
+        ab = 1;
+      } else if ((old & kBarCount) + 1 == (unsigned long long)G) {
+        __hip_atomic_fetch_add(w, (1ull << 32) - (unsigned long long)G, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        const long long t0 = wall_clock64();
+        for (int spin = 0;; ++spin) {
+          const unsigned long long v = __hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+          if ((unsigned)(v >> 32) != gen) break;
+          if (v & kBarPoison) { ab = 1; break; }
+          if ((spin & 31) == 31 && wall_clock64() - t0 > limit) {
+            const int r = give_up(gen);
+            if (r > 0) { ab = 1; break; }
+            if (r == 0) break;
           }
+          __builtin_amdgcn_s_sleep(1);
         }
-        __builtin_amdgcn_s_sleep(1);
       }
     }
     __threadfence();
@@ -215,9 +242,11 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
   const bool prof = a.prof != nullptr && g == 0;
   if (prof) tp[0] = wall_clock64();
   int nwin = 0;
+  int nbar = 0;      // grid barriers so far (the same sequence on every workgroup)
   auto bar = [&]() -> bool {
     const long long t = prof ? wall_clock64() : 0;
-    const bool r = fpg::sync(L, G, &X->flag);
+    ++nbar;
+    const bool r = fpg::sync(L, G, &X->flag, a.fpg_limit, g == 0 && nbar == a.fpg_fail);
     if (prof) tp[2] += wall_clock64() - t;
     return r;
   };
@@ -230,9 +259,35 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
   const int WIN = G * kFpThreads;
   int64_t vfrom = a.p0;
   bool go = true, ok = true;
-  // the move log is written at atomically claimed positions (k_apply_moves is order-free)
-  int* mcnt = a.mcount;
   int q0 = 0;
+  int qs = 0;            // dense-list position of the last window's stop
+  bool stopped = false;  // the launch gave up at the barrier behind a stop (of workgroup gs_stop)
+  int gs_stop = -1;
+  // the state the stopping workgroup published (L.ms, L.sol / los / cnt, L.md), taken over
+  auto adopt = [&]() {
+    if (wv == 0) {
+      const int c = fpg::ald(L.cnt + lane);
+      if (lane < st.lcap) {
+        st.sol[lane] = fpg::ald(L.sol + lane);
+        st.los[lane] = fpg::ald(L.los + lane);
+        if (c != st.cnt[lane]) {
+          st.cnt[lane] = c;
+          st.l1[lane] = fp_logn(a, c);
+          st.l0[lane] = fp_logn(a, c - 1);
+        }
+      }
+      if (lane == 0) {
+        const int* m = L.ms;
+        S.K = fpg::ald(m + 0); S.nslots = fpg::ald(m + 1); S.status = fpg::ald(m + 2);
+        S.restart = fpg::ald(m + 3); S.next = fpg::ald(m + 4); S.nstruct = fpg::ald(m + 5);
+        S.exact = fpg::ald(m + 6); S.moves = fpg::ald(m + 7); F->go = fpg::ald(m + 8);
+        F->nlog = fpg::ald(m + 9); S.checked = fpg::ald(m + 10);
+        S.dnow = fpg::aldd(L.md + 0);
+        S.dvmax = fpg::aldd(L.md + 1);
+      }
+    }
+    __syncthreads();
+  };
   if (prof) tp[1] = wall_clock64();
   while (q0 < total && go && ok) {
     ++nwin;
@@ -516,7 +571,9 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
     __syncthreads();
     const int ufirst = X->ufirst;
     if (dwin > a.dmax && tid == 0) S.checked = 1;
-    // ---- commit the positions before the first stop and before the first failing point
+    // ---- commit the positions before the first stop and before the first failing point: the
+    // count changes are published first, the labels and the move log written only after the
+    // barrier, so a launch that gives up at that barrier has committed nothing of this window
     int kc = active ? fs : 0;
     if (ufirst != INT_MAX)
       while (kc > 0 && F->pi[kc - 1] >= ufirst) --kc;
@@ -526,21 +583,7 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
     if (lane == 0) { F->wmov[wv] = __popcll(mmc); F->wfresh[wv] = __popcll(fbal); }
     if (wv == 0) F->wd[0][lane] = 0;
     __syncthreads();
-    if (wv == 0 && lane == 0) {
-      int nm = 0;
-      for (int w = 0; w < kFpWaves; ++w) nm += F->wmov[w];
-      X->red[0] = (nm > 0 && mcnt) ? atomicAdd(mcnt, nm) : 0;
-    }
-    __syncthreads();
     if (cm) {
-      a.c[r.y] = tgt;
-      if (a.mlog) {
-        int q = X->red[0] + __popcll(mmc & below);
-        for (int w = 0; w < wv; ++w) q += F->wmov[w];
-        a.mlog[3 * q] = r.y;
-        a.mlog[3 * q + 1] = own;
-        a.mlog[3 * q + 2] = tgt;
-      }
       atomicAdd(&F->wd[0][own], -1);
       atomicAdd(&F->wd[0][tgt], 1);
     }
@@ -560,6 +603,25 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
       F->stop_fresh = fresh ? 1 : 0;
     }
     if (!(ok = bar())) break;
+    // labels and the move log (positions: the window's log starts at F->nlog, this chunk's
+    // after the moves of the chunks before it -- the order k_resolve_fp would log them in)
+    if (wv == 0) {
+      const int before = fpg::wave_sum_over(L.mov, g);
+      if (lane == 0) X->red[0] = F->nlog + before;
+    }
+    __syncthreads();
+    const int lbase = X->red[0];
+    __syncthreads();             // (prefix_slots below reuses red)
+    if (cm) {
+      a.c[r.y] = tgt;
+      if (a.mlog) {
+        int q = lbase + __popcll(mmc & below);
+        for (int w = 0; w < wv; ++w) q += F->wmov[w];
+        a.mlog[3 * q] = r.y;
+        a.mlog[3 * q + 1] = own;
+        a.mlog[3 * q + 2] = tgt;
+      }
+    }
     // ---- every workgroup applies the window's committed changes to its copy of the state
     fpg::prefix_slots(L.dc, min(G, gs + 1), X->red, X->add);
     if (wv == 0) {
@@ -582,6 +644,7 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
         S.exact += nf;
         S.dnow = fmax(S.dnow, dwin);
         S.dvmax = fmax(S.dvmax, cd);
+        if (a.mlog) F->nlog += nm;
       }
     }
     __syncthreads();
@@ -593,11 +656,10 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
     }
     if (gs < G) {
       // ---- the window's first stop: the serial path on the workgroup that holds it, in the
-      // committed state; it publishes the state for the others
-      const int qs = q0 + gs * kFpThreads + fpg::ald(L.stop + gs);
+      // committed state; it publishes the state for the others (tagged with the window, last)
+      qs = q0 + gs * kFpThreads + fpg::ald(L.stop + gs);
+      gs_stop = gs;
       if (g == gs) {
-        if (tid == 0) F->nlog = mcnt ? __hip_atomic_load(mcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-        __syncthreads();
         if (wv == 0) fp_stop(a);
         __syncthreads();
         if (wv == 0) {
@@ -610,35 +672,13 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
             m[6] = S.exact; m[7] = S.moves; m[8] = F->go; m[9] = F->nlog; m[10] = S.checked;
             L.md[0] = S.dnow;
             L.md[1] = S.dvmax;
-            if (mcnt) __hip_atomic_store(mcnt, F->nlog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
+          __threadfence();
+          if (lane == 0) __hip_atomic_store(L.ms + 11, nwin, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
-      if (!(ok = bar())) break;
-      if (g != gs) {
-        if (wv == 0) {
-          const int c = fpg::ald(L.cnt + lane);
-          if (lane < st.lcap) {
-            st.sol[lane] = fpg::ald(L.sol + lane);
-            st.los[lane] = fpg::ald(L.los + lane);
-            if (c != st.cnt[lane]) {
-              st.cnt[lane] = c;
-              st.l1[lane] = fp_logn(a, c);
-              st.l0[lane] = fp_logn(a, c - 1);
-            }
-          }
-          if (lane == 0) {
-            const int* m = L.ms;
-            S.K = fpg::ald(m + 0); S.nslots = fpg::ald(m + 1); S.status = fpg::ald(m + 2);
-            S.restart = fpg::ald(m + 3); S.next = fpg::ald(m + 4); S.nstruct = fpg::ald(m + 5);
-            S.exact = fpg::ald(m + 6); S.moves = fpg::ald(m + 7); F->go = fpg::ald(m + 8);
-            F->nlog = fpg::ald(m + 9); S.checked = fpg::ald(m + 10);
-            S.dnow = fpg::aldd(L.md + 0);
-            S.dvmax = fpg::aldd(L.md + 1);
-          }
-        }
-        __syncthreads();
-      }
+      if (!(ok = bar())) { stopped = true; break; }
+      if (g != gs) adopt();
       go = F->go != 0;
       vfrom = (int64_t)gld(a.rq + qs).y + 1;
       q0 = qs + 1;
@@ -650,13 +690,42 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
     if (prof) tp[4] += wall_clock64() - tw1;
     __syncthreads();
   }
-  if (!ok) {
-    // a barrier gave up: every workgroup leaves; workgroup 0 reports a resolver failure
-    if (g == 0 && tid == 0) { S.status = 5; S.next = (int)a.p0; }
-  }
   if (g != 0) return;
-  if (tid == 0 && mcnt) F->nlog = __hip_atomic_load(mcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
+  if (!ok) {
+    // A barrier gave up (a workgroup was not resident in time, or fpg_fail): no workgroup got past
+    // it, so the committed state is the one at a window boundary -- before this window's commit
+    // (workgroup 0's copy of the state is that state), or after its stop, which the stopping
+    // workgroup published before the barrier.  The launch ends as a restart at the first point
+    // not decided; the host runs that restart with the one-workgroup resolver.
+    bool known = true;
+    if (stopped && gs_stop != 0) {
+      if (wv == 0) {
+        const long long t0 = wall_clock64();
+        int tag = 0;
+        while ((tag = __hip_atomic_load(L.ms + 11, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) != nwin &&
+               wall_clock64() - t0 < a.fpg_limit)
+          __builtin_amdgcn_s_sleep(2);
+        if (lane == 0) X->flag = tag == nwin ? 1 : 0;
+      }
+      __syncthreads();
+      known = X->flag != 0;
+      if (known) adopt();
+    }
+    if (tid == 0) {
+      if (!known) {
+        S.status = 5;              // the stopping workgroup never published: a resolver failure
+        S.next = (int)a.p0;
+      } else {
+        S.aborted = 1;
+        if (!(stopped && !F->go)) {
+          // (a stop that ended the launch itself keeps its own restart / status)
+          S.restart = 1;
+          S.next = (int)(stopped ? (int64_t)gld(a.rq + qs).y + 1 : vfrom);
+        }
+      }
+    }
+    __syncthreads();
+  }
   // the unlisted points after the last listed one (one workgroup, as k_resolve_fp)
   if (ok && go && S.status == 0 && !S.restart && S.dnow > a.dmax) (void)fp_verify(a, st, F, 0, S.dnow, vfrom, a.n, st.cnt);
   if (tid == 0) { tp[5] = F->iters; S.tsub[0] = nwin; S.tsub[1] = total; }

@@ -213,6 +213,16 @@ class Engine:
         ahead; negative: no host-side check (exercises the device gate-off recovery)."""
         self._check(self._L.hdpm_set_option(self._h, _lib.OPT_PIPE_WAIT_US, float(us)))
 
+    def set_fpg_wait_us(self, us: float):
+        """The grid-barrier limit of the device-wide resolver (include/hdpm.h
+        HDPM_OPT_FPG_WAIT_US); a launch that gives up is continued on one workgroup."""
+        self._check(self._L.hdpm_set_option(self._h, _lib.OPT_FPG_WAIT_US, float(us)))
+
+    def set_fpg_fail_at(self, k: int):
+        """Testing (include/hdpm.h HDPM_OPT_FPG_FAIL_AT): every device-wide resolver launch gives
+        up at its k-th grid barrier (0: never)."""
+        self._check(self._L.hdpm_set_option(self._h, _lib.OPT_FPG_FAIL_AT, float(k)))
+
     def set_hig_logspace(self, on: bool = True):
         """Extension beyond the reference (include/hdpm.h HDPM_OPT_HIG_LOGSPACE): finite HIG
         log-densities for clusters whose 2F1 series overflows (the reference throws)."""

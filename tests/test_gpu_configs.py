@@ -264,3 +264,73 @@ def test_bench_path_iterations_api(hd, oracle, name, warm, timed, mode):
     np.testing.assert_allclose(ll, oracle_iters(it, 3), rtol=RTOL, atol=0)
     same(eng, ost, rng, "after a batch that follows get_state")
     eng.close()
+
+
+@pytest.mark.timeout(900)
+# fail_at k: workgroup 0 of every device-wide resolver launch gives up at its k-th grid barrier
+# (k = 1, 2: the first round; later ordinals land in the later rounds, the drift / re-test
+# barriers, the one before a window's commit and the one behind a stop); wait_us: a 1 us barrier
+# limit, so that any barrier of any launch may give up
+@pytest.mark.parametrize("fail_at,wait_us", [(1, 0.0), (2, 0.0), (3, 0.0), (4, 0.0), (5, 0.0), (6, 0.0), (7, 0.0),
+                                             (9, 0.0), (12, 0.0), (17, 0.0), (0, 1.0)])
+def test_c2_device_wide_resolver_gives_up_and_recovers(hd, oracle, fail_at, wait_us):
+    """k_resolve_fpg's grid barriers are all-or-nothing (resolve_fpg.inl fpg::sync): a launch
+    that gives up has committed exactly the windows before that barrier, reports a restart at
+    its first undecided point, and the engine continues there on one workgroup (k_resolve_fp).
+    Forced at every barrier ordinal of a launch, and by a 1 us limit, the chain (C2 from a
+    random L = 20 start, the device-wide resolver for every fixed-point launch) stays
+    bit-identical to the oracle (n8:10-160)."""
+    from split_and_merge_gibbs_sampling_amd.data import config
+    ds = config("c2")
+    eng = hd.Engine(0)
+    eng.set_data(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w)
+    eng.set_seed(4)
+    eng.set_debug(1073741824)
+    if fail_at:
+        eng.set_fpg_fail_at(fail_at)
+    if wait_us:
+        eng.set_fpg_wait_us(wait_us)
+    params = eng.chain_params(m=3, iterations=1, L=20, burnin=0, neal8=True, split_merge=False)
+    eng.init_chain(params, c_i=None)
+    c, cen, sig = eng.get_state()
+    pc, ps = eng.get_pool(ds.n * 3)
+    ost = oracle.OracleState(c, cen.shape[0], cen, sig, cap=8192)
+    rng = eng.rng_state.copy()
+    eng.reset_stats()
+    neal8_steps(eng, oracle, ds, ost, rng, pc, ps, sweeps=3)
+    st = eng.stats()
+    assert st["fpg_launches"] > 0, st
+    if fail_at:
+        assert st["fpg_aborts"] > 0, st
+    eng.close()
+
+
+@pytest.mark.timeout(900)
+def test_c2_unconverged_many_latents(hd, oracle):
+    """m = 20 latent entries (E = K + m = 40 <= 64): the wave-per-point exact rows
+    (k_exact_rows_mass) take a point's m + 1 > 16 draws from the stream per lane (ADVICE r4:
+    its 16-word batch load picked the next point's words for latent u >= 16).  C2 from a random
+    L = 20 start, with snapshot draws (under 65,536 listed points), against the oracle."""
+    from split_and_merge_gibbs_sampling_amd.data import config
+    ds = config("c2")
+    eng = hd.Engine(0)
+    eng.set_data(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w)
+    eng.set_seed(8)
+    m = 20
+    params = eng.chain_params(m=m, iterations=1, L=20, burnin=0, neal8=True, split_merge=False)
+    eng.init_chain(params, c_i=None)
+    c, cen, sig = eng.get_state()
+    pc, ps = eng.get_pool(ds.n * m)
+    ost = oracle.OracleState(c, cen.shape[0], cen, sig, cap=8192)
+    rng = eng.rng_state.copy()
+    eng.reset_stats()
+    for k in range(3):
+        eng.neal8_sweep(m)
+        assert oracle.neal8_sweep(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w, ost, m, pc, ps, rng, fast=2) == 0
+        same(eng, ost, rng, f"sweep {k}")
+        eng.update_phi()
+        assert oracle.update_phi(ds.codes, ds.attrisize, ds.v, ds.w, ost, rng) == 0
+        same(eng, ost, rng, f"update_phi {k}")
+    st = eng.stats()
+    assert st["exact_mass_launches"] > 0, st
+    eng.close()
