@@ -40,6 +40,7 @@ namespace hdpm {
 
 hipError_t launch_prepass(const PrepassArgs& a, int nblocks, hipStream_t s);
 hipError_t launch_cluster_summary(const PrepassArgs& a, hipStream_t s);
+hipError_t launch_dense_list(const PrepassArgs& a, hipStream_t s);
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s);
 hipError_t launch_exact_rows(const PrepassArgs& a, int nblocks, hipStream_t s, int* path = nullptr);
 size_t resolve_smem_bytes(int scap, int m, int blocks);
@@ -834,6 +835,7 @@ struct Ctx {
   long long fpg_limit_ticks = 200000000LL;
   int fpg_fail_at = 0;
   bool fpg_skip = false;
+  int last_xpath = 0;                  // the exact-rows kernel of the last launch (launch_exact_rows' path)
   bool deep_ok = false;                // set by iteration(): the next sweep may be enqueued ahead
   static constexpr size_t kCtlInts = 16;
   static_assert(sizeof(ResolveCtl) <= kCtlInts * sizeof(int), "control block");
@@ -2015,6 +2017,21 @@ struct Ctx {
     const size_t mass_lds = (size_t)K * 2 * d * 8 + (size_t)8 * m * d * 8 + (size_t)K * nq * 16 + (size_t)8 * nq * 16;
     return (nq <= 8 && K <= 64 && lanes_lds <= 64 * 1024) || mass_lds <= 96 * 1024;
   }
+  // HDPM_DENSE_DIRECT=0: dense launches still run the prepass (A/B)
+  static bool dense_direct_on() {
+    static const bool on = [] {
+      const char* e = std::getenv("HDPM_DENSE_DIRECT");
+      return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+  }
+  static bool lv_spec_on() {
+    static const bool on = [] {
+      const char* e = std::getenv("HDPM_LV_SPEC");
+      return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+  }
   // HDPM_DENSE_LIST=0: no dense listing (A/B)
   static bool dense_list_on() {
     static const bool on = [] {
@@ -2069,7 +2086,7 @@ struct Ctx {
     PrepassArgs pa;
     pa.gate = pg ? &pg->gate : nullptr;
     pa.raw_ptr = pg ? &pg->raw : nullptr;
-    pa.codes_t = d_codes_t.p; pa.n = n; pa.d = d; pa.nq = nq;
+    pa.codes_t = d_codes_t.p; pa.n = n; pa.d = d; pa.nq = nq; pa.mmax = mmax;
     pa.c = d_c.p; pa.counts = d_counts.p; pa.slot_of_label = d_sol.p; pa.K = K; pa.S = S;
     pa.slots = ParamTables{d_slot_codes.p, d_slot_tab.p};
     pa.pool = ParamTables{d_pool_codes.p, d_pool_tab.p};
@@ -2082,6 +2099,7 @@ struct Ctx {
     pa.csum = d_csum.p;
 
     pa.thresh = ((debug & 1) || dense_list) ? INFINITY : T + 2.0 * dmax;
+    pa.thresh_ref = T + 2.0 * dmax;
     // certification by the draw's uniform only while the chain is settled: after a launch
     // that exceeded its drift budget, restarted or decided many points itself, uniform-
     // certified points (no exact rows) would fail re-verification and restart the launch
@@ -2097,7 +2115,12 @@ struct Ctx {
     // snapshot draws (k_exact_rows*: the resolver's first-round guesses and kept draws) except
     // when nearly every point is listed: the device-wide resolver then draws all of them in
     // its first round anyway, and the mass exact-rows kernel is ~20% faster without them
-    pa.spec = ((debug & 8) || el >= kMassNoSpec) ? nullptr : d_spec.p;
+    // (with the level-table exact rows the snapshot draws are made behind the rows by
+    // k_snap_draws, a thread per point, also for dense launches; HDPM_LV_SPEC=0: not there)
+    pa.spec_lv = lv_spec_on() ? 1 : 0;
+    // a dense launch needs no bounds: its list is every point (k_dense_list)
+    pa.dense_direct = dense_list && dense_direct_on() ? 1 : 0;
+    pa.spec = ((debug & 8) || (el >= kMassNoSpec && !pa.spec_lv)) ? nullptr : d_spec.p;
     pa.spec_rad = d_spec_rad.p;
     pa.rq = d_rq.p;
     pa.p0 = p;
@@ -2106,9 +2129,9 @@ struct Ctx {
     pa.exact_scan = el >= 4096 ? 1 : 0;
     pa.wide = (debug & 16384) ? 0 : 1;
     pa.zero = nullptr;
-    d_wide_ctr.ensure(2);
+    d_wide_ctr.ensure(4);
     pa.wide_ctr = d_wide_ctr.p;      // cleared by k_cluster_summary (below: K > 0)
-    if (K == 0 && part != kRoundResolve) HIPCHK(hipMemsetAsync(d_wide_ctr.p, 0, 8, stream));
+    if (K == 0 && part != kRoundResolve) HIPCHK(hipMemsetAsync(d_wide_ctr.p, 0, 16, stream));
     if (mcount_clear && part != kRoundResolve) {
       if (K > 0) pa.zero = d_mcount.p;
       else HIPCHK(hipMemsetAsync(d_mcount.p, 0, 4, stream));
@@ -2125,7 +2148,8 @@ struct Ctx {
       HIPCHK(launch_cluster_summary(pa, stream));
       if (timed) HIPCHK(hipEventRecord(ev[0], stream));
       if (pg && pre_timed[cpar]) HIPCHK(hipEventRecord(ev_pp[cpar][0], stream));
-      HIPCHK(launch_prepass(pa, nblocks, stream));
+      if (pa.dense_direct) HIPCHK(launch_dense_list(pa, stream));
+      else HIPCHK(launch_prepass(pa, nblocks, stream));
       mark("r.prepass");
       if (!pg) {
         stats.prepass_points += n - p;
@@ -2135,9 +2159,10 @@ struct Ctx {
       if (pg && pre_timed[cpar]) HIPCHK(hipEventRecord(ev_pp[cpar][1], stream));
       int xpath = 0;
       HIPCHK(launch_exact_rows(pa, nblocks, stream, &xpath));
+      last_xpath = xpath;
       if (!pg) {
         if (xpath == 1) stats.exact_mass_launches++;
-        if (xpath == 2) stats.exact_lanes_launches++;
+        if (xpath == 2 || xpath == 3) stats.exact_lanes_launches++;
       }
       mark("r.exact");
       if (fine) HIPCHK(hipEventRecord(ev[5], stream));
@@ -2185,6 +2210,8 @@ struct Ctx {
     // points: one 512-point chunk per workgroup, a workgroup per CU (debug bit 29: one workgroup)
     ra.fpg = 0;
     ra.fpg_buf = nullptr;
+    // (k_snap_draws, behind the level-table exact rows, counted them)
+    ra.uncertain = (pa.dense_direct && pa.spec && last_xpath == 3) ? d_wide_ctr.p + 2 : nullptr;
     ra.fpg_limit = fpg_limit_ticks;
     ra.fpg_fail = fpg_fail_at;
     const bool fpg_skipped = fpg_skip && part != kRoundPrefix;
@@ -2631,7 +2658,10 @@ struct Ctx {
       last_exact = c.exact;
       last_listed = c.listed;
       // a sweep's first launch sets the density (a restart's tail of the sweep is not typical)
-      if (p == 0 || last_density < 0) last_density = (double)c.listed / (double)std::max(1, n - p);
+      // (a dense launch listed every point: its density is what the prepass's margin test
+      // would have listed, counted by k_snap_draws)
+      if (p == 0 || last_density < 0)
+        last_density = (double)(c.uncertain >= 0 ? c.uncertain : c.listed) / (double)std::max(1, n - p);
       stats.moves += c.moves;
       sweep_moves += c.moves;
       stats.checked_rounds += c.checked;

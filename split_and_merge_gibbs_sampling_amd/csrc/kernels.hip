@@ -292,6 +292,7 @@ __global__ void k_cluster_summary(PrepassArgs a) {
     if (a.wide_ctr) {
       a.wide_ctr[0] = 0;
       a.wide_ctr[1] = 0;
+      a.wide_ctr[2] = 0;
     }
   }
   const int sw = a.bw + 2;
@@ -1978,6 +1979,7 @@ __device__ __forceinline__ void resolve_finish(const ResolveArgs& a, const RStat
     c.moves = S.moves; c.exact = S.exact; c.checked = S.checked;
     c.listed = *a.dense_total;
     c.aborted = S.aborted;
+    c.uncertain = a.uncertain ? *a.uncertain : -1;
     *a.ctl = c;
   }
 }
@@ -2528,8 +2530,15 @@ __device__ __forceinline__ double fp_wave_drift_bound(const ResolveArgs& a, cons
                                                       const unsigned long long* bin, const unsigned long long* bout,
                                                       int nsl);
 
-template <int EM>
-__device__ int fp_draw(double (&v)[EM], int E, double rU, const uint64_t* etab) {
+//
+// With kRad, *rad receives a radius as decide_values' (0 when none is kept): the draw stands
+// while every log-weight moves by less than it -- normalised probabilities then move by
+// factors within exp(+-2 rad), so the picked entry keeps its rank (its ratios to the nearest
+// larger and smaller values) and the uniform stays inside its cumulative interval; 1e-9 covers
+// the reference's few ulps of rounding.
+template <int EM, bool kRad = false>
+__device__ int fp_draw(double (&v)[EM], int E, double rU, const uint64_t* etab, double* rad = nullptr) {
+  if constexpr (kRad) *rad = 0.0;
   // branch-free over the EM slots (padding: exp(-inf) = 0 adds nothing to the sums), so
   // the exps' table loads are issued together
   double mx = -INFINITY;
@@ -2568,9 +2577,25 @@ __device__ int fp_draw(double (&v)[EM], int E, double rU, const uint64_t* etab) 
       g = gt ? 1 : (eq ? g + 1 : g);
     }
     if (g == 0) return kFpFallback;
+    const double cb = c;      // cumulative before this group
     for (int k = 0; k < g; ++k, ++j) {
       c += cur;
-      if (j == E - 1 || rU <= c) return g == 1 ? idx : kFpFallback;
+      if (j == E - 1 || rU <= c) {
+        if (g != 1) return kFpFallback;
+        if constexpr (kRad) {
+          if (rU <= c && cur > 0.0) {
+            double nx = 0.0;   // the next smaller positive value
+#pragma unroll
+            for (int e = 0; e < EM; ++e) nx = (v[e] < cur && v[e] > nx) ? v[e] : nx;
+            double r = 0.5 * log(c / rU);
+            if (prev < INFINITY) r = fmin(r, 0.5 * log(prev / cur));
+            if (nx > 0.0) r = fmin(r, 0.5 * log(cur / nx));
+            if (cb > 0.0) r = fmin(r, 0.5 * log(rU / cb));
+            *rad = fmax(0.0, r - 1e-9);
+          }
+        }
+        return idx;
+      }
     }
     prev = cur;
   }
@@ -3568,10 +3593,188 @@ __global__ __launch_bounds__(256) void k_exact_rows_lanes(PrepassArgs a) {
   }
 }
 
+// The same with the clusters' values in a level-indexed LDS table: vt[j][l][k] = the value
+// cluster k contributes at attribute j for a point of level l + 1 -- dhamming's match value if
+// l + 1 is its center's level there, else its mismatch value (n8:47-49 -> cf:355-377) -- so a
+// lane reads its own point's value directly (one address per level: no bank conflicts, no
+// compare / select), two clusters per 16-B read.  Sums per cluster in attribute order as
+// before (bit-exact).  One workgroup of 16 waves per CU (the table: K D mmax 8 bytes, 80 KB at
+// C5), a thread per listed point; the latent entries as in k_exact_rows_lanes.
+constexpr int kLvThreads = 1024;
+constexpr int kLvGroup = 4;       // clusters summed together (accumulators per lane)
+__host__ __device__ inline int exact_lv_kp(int K) { return (K + kLvGroup - 1) / kLvGroup * kLvGroup; }
+// [dp][mmax][KP] doubles: clusters padded to whole groups, attributes to the 16-byte code
+// chunks (zeros: the padding adds +0.0 to every sum, so no lane or attribute branches)
+__host__ __device__ inline size_t exact_lv_lds_bytes(int K, int nq, int mmax) {
+  return (size_t)exact_lv_kp(K) * nq * 16 * mmax * 8;
+}
+__global__ __launch_bounds__(kLvThreads) void k_exact_rows_lv(PrepassArgs a) {
+  if (!pipe_gate(a)) return;
+  extern __shared__ __attribute__((aligned(16))) double vt[];
+  __shared__ int s_col[kWave];
+  const int K = a.K, m = a.m, D = a.d, nq = a.nq, dp = nq * 16, mm = a.mmax;
+  const int KP = exact_lv_kp(K);
+  const int per = mm * KP;                        // doubles per attribute
+  for (int q = threadIdx.x; q < dp * per; q += blockDim.x) {
+    const int j = q / per, r = q - j * per, l = r / KP, k = r - l * KP;
+    double v = 0.0;
+    if (k < K && j < D) {
+      const int64_t sl = a.slot_of_label[k];
+      const int c = a.slots.codes[sl * dp + j];
+      v = a.slots.tab[(sl * D + j) * 2 + (c == l + 1 ? 0 : 1)];
+    }
+    vt[q] = v;
+  }
+  if (threadIdx.x < K) s_col[threadIdx.x] = a.slot_of_label[threadIdx.x];
+  __syncthreads();
+  const int total = *a.dense_total;
+  const int stride = gridDim.x * blockDim.x;
+  for (int q0 = blockIdx.x * blockDim.x; q0 < total; q0 += stride) {
+    const int q = q0 + threadIdx.x;
+    const bool on = q < total;
+    const int4 r = on ? a.rq[q] : make_int4(0, 0, 0, 0);
+    const int64_t i = r.y;
+    double* Lr = a.L + (int64_t)r.x * (a.S + m);
+    uint32_t xw[4 * kLanesMaxNq];
+#pragma unroll
+    for (int c = 0; c < kLanesMaxNq; ++c) {
+      uint4 v = make_uint4(0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u);
+      if (c < nq && on) v = *(const uint4*)(a.codes_t + tiled_offset(i, c * 16, nq));
+      xw[4 * c] = v.x; xw[4 * c + 1] = v.y; xw[4 * c + 2] = v.z; xw[4 * c + 3] = v.w;
+    }
+    for (int k0 = 0; k0 < K; k0 += kLvGroup) {
+      double acc[kLvGroup];
+#pragma unroll
+      for (int kk = 0; kk < kLvGroup; ++kk) acc[kk] = 0.0;
+      const double* g = vt + k0;
+      // (KP laundered per group: the per-attribute offsets l KP would otherwise be hoisted out
+      // of the group loop, 128 live values, and spilled)
+      int kpl = KP;
+      asm volatile("" : "+s"(kpl));
+#pragma unroll
+      for (int c = 0; c < kLanesMaxNq; ++c) {
+        if (c >= nq) break;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const uint32_t x4 = xw[4 * c + w];
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const int j = c * 16 + 4 * w + b;
+            // a padding attribute's byte is 0: level 1's row of zeros
+            const int x = (int)((x4 >> (8 * b)) & 0xffu);
+            const int l = (x > 0 ? x : 1) - 1;
+            const double2* p = (const double2*)(g + j * per + l * kpl);
+#pragma unroll
+            for (int kk = 0; kk < kLvGroup; kk += 2) {
+              const double2 v = p[kk >> 1];
+              acc[kk] += v.x;
+              acc[kk + 1] += v.y;
+            }
+          }
+          // (the scheduler would issue every LDS read of the unrolled attributes first and spill)
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+#pragma unroll
+      for (int kk = 0; kk < kLvGroup; ++kk)
+        if (on && k0 + kk < K) Lr[s_col[k0 + kk]] = acc[kk];
+    }
+    const uint32_t* raw = a.raw + i * (m + 1);
+    for (int u = 0; u < m; ++u) {
+      const int64_t pe = on ? pick_entry(raw[u], a.P) : 0;
+      const uint8_t* cc = a.pool.codes + pe * dp;
+      const double* tl = a.pool.tab + pe * 2 * D;
+      double acc = 0.0;
+#pragma unroll
+      for (int c = 0; c < kLanesMaxNq; ++c) {
+        if (c >= nq) break;
+        const uint4 cq = *(const uint4*)(cc + c * 16);
+        const uint32_t cw[4] = {cq.x, cq.y, cq.z, cq.w};
+        double v[16];
+#pragma unroll
+        for (int b = 0; b < 16; ++b) {
+          const int j = c * 16 + b;
+          const uint32_t dx = xw[4 * c + (b >> 2)] ^ cw[b >> 2];
+          v[b] = j < D ? tl[2 * j + (((dx >> (8 * (b & 3))) & 0xffu) ? 1 : 0)] : 0.0;
+        }
+#pragma unroll
+        for (int b = 0; b < 16; ++b) acc += v[b];
+      }
+      if (on) Lr[a.S + u] = acc;
+    }
+  }
+}
+
+// Snapshot draws for the thread-per-point exact rows (k_exact_rows_lanes / _lv), which build
+// rows only: per listed point its n8:95-102 draw in the launch's state (the counts and slots
+// every row was built against) from its row, as k_exact_rows_mass's mass_decide does with
+// decide_values, on the point's own lane (fp_draw: the resolver's exact draw), with the
+// radius under which it holds.  A pick inside a group of equal values is left to the resolver
+// (spec -1).  The device-wide resolver starts its rounds from these outcomes and keeps every
+// draw whose radius the count drift stays within.
+template <int EM>
+__global__ __launch_bounds__(256) void k_snap_draws(PrepassArgs a) {
+  if (!pipe_gate(a)) return;
+  __shared__ uint64_t etab[256];
+  __shared__ int s_sl[kWave];
+  __shared__ double s_l0[kWave], s_l1[kWave];
+  const int K = a.K, m = a.m, E = K + m, ncol = a.S + m;
+  for (int e = threadIdx.x; e < 256; e += blockDim.x) etab[e] = devtab::kGlibcExpTab[e];
+  if (threadIdx.x < K) {
+    const int sl = a.slot_of_label[threadIdx.x], c = a.counts[sl];
+    s_sl[threadIdx.x] = sl;
+    s_l1[threadIdx.x] = a.logn[c];
+    s_l0[threadIdx.x] = c > 0 ? a.logn[c - 1] : -INFINITY;
+  }
+  __syncthreads();
+  const int total = *a.dense_total;
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < total; q += gridDim.x * blockDim.x) {
+    const int4 r = a.rq[q];
+    const int own = r.z;
+    const double* row = a.L + (int64_t)r.x * ncol;
+    const int own_cnt = a.counts[own];
+    const bool single = own_cnt == 1;
+    double v[EM];
+    double vo = -INFINITY, mo = -INFINITY;
+#pragma unroll
+    for (int e = 0; e < EM; ++e) {
+      if (e < K) {
+        const int s = s_sl[e];
+        v[e] = (s == own ? s_l0[e] : s_l1[e]) + row[s];                     // n8:40-92
+        if (s == own) vo = v[e];
+        else mo = fmax(mo, v[e]);
+      } else if (e < E) {
+        const int l = e - K;
+        v[e] = a.logfac + ((l == 0 && single) ? row[own] : row[a.S + l]);     // n8:65-75
+        mo = fmax(mo, v[e]);
+      } else {
+        v[e] = -INFINITY;
+      }
+    }
+    // the prepass's margin test (kernels.hip k_prepass: the own cluster ahead of every other
+    // entry by thresh), here on exact values: what a launch with the prepass would have listed
+    const bool unc = !(own_cnt >= 2 && vo - mo > a.thresh_ref);
+    const unsigned long long ub = __ballot(unc);
+    if ((threadIdx.x & 63) == 0 && ub && a.wide_ctr) atomicAdd(a.wide_ctr + 2, __popcll(ub));
+    double rad = 0.0;
+    const int pick = fp_draw<EM, true>(v, E, raw_to_unif((uint32_t)r.w), etab, &rad);
+    a.spec[q] = pick >= 0 ? pick : -1;
+    a.spec_rad[q] = pick >= 0 ? rad : 0.0;
+  }
+}
+
 static int lanes_grid(size_t lds) {
   const int cus = device_cus();
   int per = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_exact_rows_lanes, 256, lds) != hipSuccess || per <= 0) per = 1;
+  return cus * per;
+}
+
+static int lv_grid(size_t lds) {
+  const int cus = device_cus();
+  int per = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_exact_rows_lv, kLvThreads, lds) != hipSuccess || per <= 0)
+    per = 1;
   return cus * per;
 }
 
@@ -3588,6 +3791,17 @@ static int mass_grid(size_t lds) {
   return cus * per;
 }
 
+static hipError_t launch_snap_draws(const PrepassArgs& a, hipStream_t s) {
+  if (a.spec) {
+    const dim3 g((unsigned)(device_cus() * 4)), b(256);
+    const int E = a.K + a.m;
+    if (E <= 24) hipLaunchKernelGGL(k_snap_draws<24>, g, b, 0, s, a);
+    else if (E <= 32) hipLaunchKernelGGL(k_snap_draws<32>, g, b, 0, s, a);
+    else hipLaunchKernelGGL(k_snap_draws<64>, g, b, 0, s, a);
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_exact_rows(const PrepassArgs& a0, int nblocks, hipStream_t s, int* path) {
   if (path) *path = 0;
   PrepassArgs a = a0;
@@ -3598,10 +3812,12 @@ hipError_t launch_exact_rows(const PrepassArgs& a0, int nblocks, hipStream_t s, 
   // the workgroup kernels scan the list themselves unless it is long (exact_scan); the
   // one-wave kernel needs k_list_scan
   const bool wg = !a.exact_wave && lds <= kExactWgLdsMax && E <= 4 * kWave;
-  if (a.exact_scan && a.boff) {
+  if (a.dense_direct) {
+    // every point of [p0, n) listed, in order (k_dense_list wrote the list and the records)
+  } else if (a.exact_scan && a.boff) {
     hipLaunchKernelGGL(k_list_offsets, dim3(1), dim3(kScanThreads), 0, s, a.cnt, a.nlb, a.boff, a.dense_total);
     const size_t mlds0 = exact_mass_lds_bytes(a.K, a.m, a.d, a.nq * 16);
-    const bool mass = !a.exact_wave && ((E <= kWave && mlds0 <= 96 * 1024) || !a.spec);
+    const bool mass = !a.exact_wave && ((E <= kWave && mlds0 <= 96 * 1024) || !a.spec || a.spec_lv);
     hipLaunchKernelGGL(k_list_fill, dim3((unsigned)((a.nlb + 3) / 4)), dim3(256), 0, s, a, mass ? 1 : 0);
   } else if (a.exact_scan || !wg) {
     hipLaunchKernelGGL(k_list_scan, dim3(1), dim3(kScanThreads), 0, s, a.cnt, a.nlb, a.lblock, a.dense,
@@ -3618,6 +3834,19 @@ hipError_t launch_exact_rows(const PrepassArgs& a0, int nblocks, hipStream_t s, 
     const char* e = std::getenv("HDPM_EXACT_MASS");
     return e && std::atoi(e) == 1;
   }();
+  // HDPM_EXACT_LANES=1: the thread-per-point kernel with compare / select (A/B of the level tables)
+  static const bool force_lanes = [] {
+    const char* e = std::getenv("HDPM_EXACT_LANES");
+    return e && std::atoi(e) == 1;
+  }();
+  const size_t vlds = exact_lv_lds_bytes(a.K, a.nq, a.mmax);
+  // (with snapshot draws when spec is set: k_snap_draws behind the rows)
+  if (a.exact_scan && (!a.spec || a.spec_lv) && !a.exact_wave && a.nq <= kLanesMaxNq && a.K <= kWave && a.mmax >= 1 &&
+      vlds <= 120 * 1024 && !force_mass && !force_lanes) {
+    hipLaunchKernelGGL(k_exact_rows_lv, dim3(lv_grid(vlds)), dim3(kLvThreads), vlds, s, a);
+    if (path) *path = 3;
+    return launch_snap_draws(a, s);
+  }
   if (a.exact_scan && !a.spec && !a.exact_wave && a.nq <= kLanesMaxNq && a.K <= kWave && llds <= 64 * 1024 &&
       !force_mass) {
     hipLaunchKernelGGL(k_exact_rows_lanes, dim3(lanes_grid(llds)), dim3(256), llds, s, a);
@@ -3636,6 +3865,27 @@ hipError_t launch_exact_rows(const PrepassArgs& a0, int nblocks, hipStream_t s, 
   if (wg && E <= kWave) hipLaunchKernelGGL(k_exact_rows_wg<1>, g, b, lds, s, a);
   else if (wg && E <= 4 * kWave) hipLaunchKernelGGL(k_exact_rows_wg<4>, g, b, lds, s, a);
   else hipLaunchKernelGGL(k_exact_rows, dim3(std::min(nblocks, 1024)), dim3(kWave * kExactWaves), 0, s, a);
+  return hipGetLastError();
+}
+
+// A dense launch (every point of [p0, n) listed, engine launch_round): the list and the
+// resolver's records straight from the labels and draws, instead of the prepass's bounds and
+// the list scan -- row q is point p0 + q.
+__global__ __launch_bounds__(256) void k_dense_list(PrepassArgs a) {
+  if (!pipe_gate(a)) return;
+  const int cnt = a.n - a.p0, m1 = a.m + 1;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.dense_total = cnt;
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < cnt; q += gridDim.x * blockDim.x) {
+    const int i = a.p0 + q;
+    a.dense[q] = q;
+    a.rowpos[i] = q;
+    a.rq[q] = make_int4(q, i, a.c[i], (int)a.raw[(int64_t)i * m1 + m1 - 1]);
+  }
+}
+hipError_t launch_dense_list(const PrepassArgs& a, hipStream_t s) {
+  const int cnt = a.n - a.p0;
+  hipLaunchKernelGGL(k_dense_list, dim3((unsigned)std::min(4 * device_cus(), std::max(1, (cnt + 255) / 256))), dim3(256),
+                     0, s, a);
   return hipGetLastError();
 }
 
@@ -3685,6 +3935,7 @@ int resolve_fpg_max_grid(int lcap, int m) {
 // first query inside a sweep cost ~8 ms.  Returns the resolver's grid for lcap.
 int warm_sweep_kernels(int lcap, int m) {
   (void)lanes_grid(0);
+  (void)lv_grid(0);
   (void)mass_grid(0);
   return resolve_fpg_max_grid(lcap, m);
 }
@@ -3770,6 +4021,7 @@ __global__ void k_pipe_wait(const PipeSlot* slot, const ResolveCtl* prev, Resolv
     o->status = kPipeOff;
     o->next = 0;
     o->aborted = 0;
+    o->uncertain = -1;
   }
 }
 hipError_t launch_pipe_wait(const PipeSlot* slot, const ResolveCtl* prev, ResolveCtl* own, int n, PipeGate* g,

@@ -134,6 +134,10 @@ struct PrepassArgs {
   int exact_scan;            // 1: the dense list by k_list_scan before the exact rows (many listed
                              // points: every workgroup then reads its rows, no per-point block walk)
   int nlb, lblock;           // list blocks of this launch and their points (k_exact_rows_wg's own list scan)
+  int mmax;                  // levels of the widest attribute (k_exact_rows_lv's level-indexed tables)
+  int spec_lv;               // 1: snapshot draws may come from k_snap_draws behind k_exact_rows_lv
+  int dense_direct;          // 1: every point listed by k_dense_list (no prepass, no list scan)
+  double thresh_ref;         // the prepass's margin threshold (k_snap_draws counts the points it would list)
   // pipelined iterations (engine.cpp iterations_pipelined): the kernels run only while *gate
   // is set, and read the sweep's draws from *raw_ptr (a position found on the device)
   const int* gate;
@@ -188,6 +192,8 @@ struct ResolveCtl {
   int listed;     // points the prepass left uncertain (exact rows built) in this launch
   int aborted;    // 1: k_resolve_fpg gave up at a grid barrier (a workgroup not resident in time);
                   // the state is consistent at `next` (restart there, with k_resolve_fp)
+  int uncertain;  // dense launches: listed points the prepass's margin test would have listed
+                  // (k_snap_draws' count), or -1
 };
 
 struct ResolveArgs {
@@ -245,6 +251,7 @@ struct ResolveArgs {
   // fpg_buf = fpg_words(fpg) ints of cross-workgroup scratch, its kFpgBarWords barrier words zeroed by the host
   int fpg;
   int* fpg_buf;
+  const int* uncertain;      // dense launches: k_snap_draws' count of would-be-listed points (or nullptr)
   long long fpg_limit;       // a grid barrier gives up after this many wall_clock64 ticks (100 MHz)
   int fpg_fail;              // testing: workgroup 0 gives up at its fpg_fail-th grid barrier (0: never)
 };
