@@ -257,6 +257,11 @@ int hdpm_get_pool_heads(hdpm_ctx* ctx, uint64_t* out, int64_t P);
 /* HDPM_OPT_FPG_FAIL_AT (testing): workgroup 0 of every k_resolve_fpg launch gives up at its
  * value-th grid barrier (0: never), to exercise that recovery deterministically. */
 #define HDPM_OPT_FPG_FAIL_AT 5
+/* HDPM_OPT_EXACT_KERNEL (testing): the exact-rows kernel of launches with many listed points:
+ * 0 automatic (default), 1 a wave per point (k_exact_rows_mass), 2 a thread per point with
+ * compare / select (k_exact_rows_lanes), 3 a thread per point with level-indexed tables
+ * (k_exact_rows_lv) -- where the state fits it.  Same chain either way. */
+#define HDPM_OPT_EXACT_KERNEL 6
 int hdpm_set_option(hdpm_ctx* ctx, int32_t option, double value);
 /* Posterior analysis (realdata_analysis/zoo_simulator.R:193-236, 339-344; mcclust /
  * mcclust.ext).  hdpm_psm_build: the posterior similarity matrix of M saved label vectors

@@ -35,6 +35,7 @@ OPT_PHI_DEVICE = 2
 OPT_PIPE_WAIT_US = 3
 OPT_FPG_WAIT_US = 4
 OPT_FPG_FAIL_AT = 5
+OPT_EXACT_KERNEL = 6
 
 STATUS = {0: "OK", 1: "E_VALIDATE", 2: "E_GSL", 3: "E_PROB", 4: "E_WALKER", 5: "E_ARG",
           6: "E_DEVICE", 7: "E_NODEVICE"}

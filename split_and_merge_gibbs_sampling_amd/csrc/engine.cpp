@@ -47,6 +47,8 @@ size_t resolve_smem_bytes(int scap, int m, int blocks);
 size_t resolve_fpg_smem_bytes(int lcap, int m);
 int resolve_fpg_max_grid(int lcap, int m);
 int warm_sweep_kernels(int lcap, int m);
+hipError_t warm_launch_kernels(const PrepassArgs& pa, const ResolveArgs& ra, const int* zero, int* scratch,
+                               hipStream_t s);
 int device_cus();
 hipError_t launch_relabel(int* c, const int* los, int n, const ResolveCtl* ctl, hipStream_t s);
 hipError_t launch_finish_sweep(int* counts, int* sol, int* los, int* src, int cap, const ResolveCtl* ctl, int n,
@@ -794,6 +796,8 @@ struct Ctx {
   DevBuf<long long> d_rprof;          // resolver phase times (debug mode bit 1)
   DevBuf<int> d_fpg;                   // k_resolve_fpg's cross-workgroup scratch
   DevBuf<int> d_wide_ctr;              // k_prepass_wide's chunk counter, k_exact_rows_mass's point counter
+  DevBuf<int> d_warm;                  // zero gate word and scratch of warm_launch_kernels
+  bool kernels_warm = false;
   int fpg_grid_cache[65] = {0};        // its resident grid per resolver slot capacity (0: unknown, -1: none)
   int fpg_grid_m = -1;                 // ... for this m (the LDS of k_resolve_fpg depends on m)
   int& fpg_grid(int lcap, int m) {
@@ -836,6 +840,7 @@ struct Ctx {
   int fpg_fail_at = 0;
   bool fpg_skip = false;
   int last_xpath = 0;                  // the exact-rows kernel of the last launch (launch_exact_rows' path)
+  int exact_pref = 0;                  // HDPM_OPT_EXACT_KERNEL (testing)
   bool deep_ok = false;                // set by iteration(): the next sweep may be enqueued ahead
   static constexpr size_t kCtlInts = 16;
   static_assert(sizeof(ResolveCtl) <= kCtlInts * sizeof(int), "control block");
@@ -2006,6 +2011,14 @@ struct Ctx {
   static constexpr int kFpMinListed = 64;
   static constexpr int kFpgMinListed = 1024;   // listed points of the previous launch for k_resolve_fpg (two chunks)
   static constexpr int kMassNoSpec = 65536;    // expected listed points above which no snapshot draws are made
+  // HDPM_FPG_MIN: the listed points (expected) from which launches take k_resolve_fpg (A/B)
+  static int fpg_min_listed() {
+    static const int v = [] {
+      const char* e = std::getenv("HDPM_FPG_MIN");
+      return e ? std::max(1, std::atoi(e)) : (int)kFpgMinListed;
+    }();
+    return v;
+  }
   static constexpr int kDenseMinPoints = 4096;  // dense listing only for launches over at least this many points
   // the state fits the dense path: the fixed-point resolvers and a mass exact-rows kernel
   // (kernels.hip launch_exact_rows: the thread-per-point kernel's LDS tables, or the
@@ -2118,6 +2131,7 @@ struct Ctx {
     // (with the level-table exact rows the snapshot draws are made behind the rows by
     // k_snap_draws, a thread per point, also for dense launches; HDPM_LV_SPEC=0: not there)
     pa.spec_lv = lv_spec_on() ? 1 : 0;
+    pa.exact_pref = exact_pref;
     // a dense launch needs no bounds: its list is every point (k_dense_list)
     pa.dense_direct = dense_list && dense_direct_on() ? 1 : 0;
     pa.spec = ((debug & 8) || (el >= kMassNoSpec && !pa.spec_lv)) ? nullptr : d_spec.p;
@@ -2216,7 +2230,7 @@ struct Ctx {
     ra.fpg_fail = fpg_fail_at;
     const bool fpg_skipped = fpg_skip && part != kRoundPrefix;
     if (fpg_skipped) fpg_skip = false;
-    if (ra.fp && !fpg_skipped && (el >= kFpgMinListed || (debug & 1073741824)) && !(debug & 536870912) &&
+    if (ra.fp && !fpg_skipped && (el >= fpg_min_listed() || (debug & 1073741824)) && !(debug & 536870912) &&
         ra.lcap <= 64) {
       int& mg = fpg_grid(ra.lcap, m);
       if (mg == 0) {
@@ -2242,6 +2256,13 @@ struct Ctx {
     }
     if (part == kRoundPrefix) return kOk;
     mark("r.args");
+    if (!kernels_warm && !pg) {
+      // the kernels this chain may reach only later, each launched once behind a closed gate
+      d_warm.ensure(32);
+      HIPCHK(hipMemsetAsync(d_warm.p, 0, 32 * sizeof(int), stream));
+      HIPCHK(warm_launch_kernels(pa, ra, d_warm.p, d_warm.p + 16, stream));
+      kernels_warm = true;
+    }
     HIPCHK(launch_resolve(ra, stream));
     mark("r.resolve");
     if (fine) HIPCHK(hipEventRecord(ev[2], stream));
@@ -4710,6 +4731,11 @@ int hdpm_set_option(hdpm_ctx* h, int32_t option, double value) {
       if (value < 0.0 || value > 1e9) { ctx->err = "fpg fail ordinal out of range"; return HDPM_E_ARG; }
       GUARD(ctx->cancel_ahead();)
       ctx->fpg_fail_at = (int)value;
+      return HDPM_OK;
+    case HDPM_OPT_EXACT_KERNEL:
+      if (value < 0.0 || value > 3.0) { ctx->err = "exact kernel: 0 auto, 1 mass, 2 lanes, 3 level tables"; return HDPM_E_ARG; }
+      GUARD(ctx->cancel_ahead();)
+      ctx->exact_pref = (int)value;
       return HDPM_OK;
     case HDPM_OPT_PIPE_WAIT_US:
       if (value == 0.0 || !std::isfinite(value)) { ctx->err = "pipe wait limit must be non-zero"; return HDPM_E_ARG; }

@@ -2555,6 +2555,31 @@ __device__ int fp_draw(double (&v)[EM], int E, double rU, const uint64_t* etab, 
   double sum = 0.0;
 #pragma unroll
   for (int e = 0; e < EM; ++e) sum += v[e];
+  // The dominant entry drawn (most draws: a point that stays).  With one entry at the maximum
+  // (exp 0 = 1; revsort puts it first) the reference's probability of it is
+  // (1 / sum) / s2 with s2 = 1 to within E ulps, so it is at least (1 / sum)(1 - 1e-12), and
+  // a uniform below that picks it: no normalisation or walk needed.
+  {
+    int nmax = 0, am = 0;
+    double e2 = 0.0;
+#pragma unroll
+    for (int e = 0; e < EM; ++e) {
+      const bool is1 = v[e] == 1.0;
+      nmax += is1 ? 1 : 0;
+      am = is1 ? e : am;
+      e2 = (!is1 && v[e] > e2) ? v[e] : e2;
+    }
+    const double pl = (1.0 / sum) * (1.0 - 1e-12);
+    if (nmax == 1 && rU <= pl) {
+      if constexpr (kRad) {
+        double r = 0.5 * log(pl / rU);
+        const double p2u = (e2 / sum) * (1.0 + 1e-12);
+        if (p2u > 0.0) r = fmin(r, 0.5 * log(pl / p2u));
+        *rad = fmax(0.0, r - 1e-9);
+      }
+      return am;
+    }
+  }
 #pragma unroll
   for (int e = 0; e < EM; ++e) v[e] = v[e] / sum;                           // n8:96
   double s2 = 0.0;                                                          // FixupProb
@@ -3840,18 +3865,19 @@ hipError_t launch_exact_rows(const PrepassArgs& a0, int nblocks, hipStream_t s, 
     return e && std::atoi(e) == 1;
   }();
   const size_t vlds = exact_lv_lds_bytes(a.K, a.nq, a.mmax);
+  const bool want_mass = force_mass || a.exact_pref == 1, want_lanes = force_lanes || a.exact_pref == 2;
   // (with snapshot draws when spec is set: k_snap_draws behind the rows)
   if (a.exact_scan && (!a.spec || a.spec_lv) && !a.exact_wave && a.nq <= kLanesMaxNq && a.K <= kWave && a.mmax >= 1 &&
-      vlds <= 120 * 1024 && !force_mass && !force_lanes) {
+      vlds <= 120 * 1024 && !want_mass && !want_lanes) {
     hipLaunchKernelGGL(k_exact_rows_lv, dim3(lv_grid(vlds)), dim3(kLvThreads), vlds, s, a);
     if (path) *path = 3;
     return launch_snap_draws(a, s);
   }
-  if (a.exact_scan && !a.spec && !a.exact_wave && a.nq <= kLanesMaxNq && a.K <= kWave && llds <= 64 * 1024 &&
-      !force_mass) {
+  if (a.exact_scan && (!a.spec || want_lanes) && !a.exact_wave && a.nq <= kLanesMaxNq && a.K <= kWave &&
+      llds <= 64 * 1024 && !want_mass) {
     hipLaunchKernelGGL(k_exact_rows_lanes, dim3(lanes_grid(llds)), dim3(256), llds, s, a);
     if (path) *path = 2;
-    return hipGetLastError();
+    return launch_snap_draws(a, s);
   }
   if (a.exact_scan && !a.exact_wave && E <= kWave && mlds <= 96 * 1024) {
     static const int mstatic = [] {
@@ -3938,6 +3964,42 @@ int warm_sweep_kernels(int lcap, int m) {
   (void)lv_grid(0);
   (void)mass_grid(0);
   return resolve_fpg_max_grid(lcap, m);
+}
+
+// One gated-off launch (a grid of one workgroup that returns at its gate) of every kernel a
+// chain may reach only later -- the exact-rows, list, snapshot-draw and resolver variants of
+// the unconverged regime -- at a context's first launch: the first launch of a kernel costs
+// ~2 ms (its code object loaded), ~8 ms in the first unconverged sweep of a timed window.
+// The argument blocks are the launch's own (every pointer valid); only the gate is replaced by
+// `zero` (a device word that is 0; pipe_gate returns before any other access).  `scratch` is
+// 16 zeroed device ints: k_list_offsets (no gate) over zero blocks writes scratch[1], and
+// k_apply_moves_lds reads a zeroed control block at scratch + 4 (an unfinished sweep: it
+// returns).
+hipError_t warm_launch_kernels(const PrepassArgs& pa0, const ResolveArgs& ra0, const int* zero, int* scratch,
+                               hipStream_t s) {
+  PrepassArgs pa = pa0;
+  pa.gate = zero;
+  ResolveArgs ra = ra0;
+  ra.gate = zero;
+  const dim3 one(1);
+  hipLaunchKernelGGL(k_dense_list, one, dim3(256), 0, s, pa);
+  hipLaunchKernelGGL(k_list_fill, one, dim3(256), 0, s, pa, 1);
+  hipLaunchKernelGGL(k_list_offsets, one, dim3(kScanThreads), 0, s, (const int*)scratch, 0, scratch, scratch + 1);
+  hipLaunchKernelGGL(k_exact_rows_lv, one, dim3(kLvThreads), 0, s, pa);
+  hipLaunchKernelGGL(k_exact_rows_lanes, one, dim3(256), 0, s, pa);
+  hipLaunchKernelGGL(k_exact_rows_mass, one, dim3(kWave * kMassWaves), 0, s, pa, 0);
+  hipLaunchKernelGGL(k_snap_draws<24>, one, dim3(256), 0, s, pa);
+  hipLaunchKernelGGL(k_snap_draws<32>, one, dim3(256), 0, s, pa);
+  hipLaunchKernelGGL(k_snap_draws<64>, one, dim3(256), 0, s, pa);
+  hipLaunchKernelGGL(k_resolve_fp<24>, one, dim3(kFpThreads), 0, s, ra);
+  hipLaunchKernelGGL(k_resolve_fp<32>, one, dim3(kFpThreads), 0, s, ra);
+  hipLaunchKernelGGL(k_resolve_fp<64>, one, dim3(kFpThreads), 0, s, ra);
+  hipLaunchKernelGGL(k_resolve_fpg<24>, one, dim3(kFpThreads), 0, s, ra);
+  hipLaunchKernelGGL(k_resolve_fpg<32>, one, dim3(kFpThreads), 0, s, ra);
+  hipLaunchKernelGGL(k_resolve_fpg<64>, one, dim3(kFpThreads), 0, s, ra);
+  hipLaunchKernelGGL(k_apply_moves_lds, one, dim3(256), 0, s, (const int*)scratch, (const int*)scratch,
+                     pa.codes_t, pa.d, pa.nq, pa.mmax, (unsigned int*)nullptr, (const ResolveCtl*)(scratch + 4), pa.n, 2);
+  return hipGetLastError();
 }
 
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s) {

@@ -137,6 +137,7 @@ struct PrepassArgs {
   int mmax;                  // levels of the widest attribute (k_exact_rows_lv's level-indexed tables)
   int spec_lv;               // 1: snapshot draws may come from k_snap_draws behind k_exact_rows_lv
   int dense_direct;          // 1: every point listed by k_dense_list (no prepass, no list scan)
+  int exact_pref;            // testing (HDPM_OPT_EXACT_KERNEL): 0 auto, 1 k_exact_rows_mass, 2 _lanes, 3 _lv
   double thresh_ref;         // the prepass's margin threshold (k_snap_draws counts the points it would list)
   // pipelined iterations (engine.cpp iterations_pipelined): the kernels run only while *gate
   // is set, and read the sweep's draws from *raw_ptr (a position found on the device)

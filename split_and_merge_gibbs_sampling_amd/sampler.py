@@ -223,6 +223,11 @@ class Engine:
         up at its k-th grid barrier (0: never)."""
         self._check(self._L.hdpm_set_option(self._h, _lib.OPT_FPG_FAIL_AT, float(k)))
 
+    def set_exact_kernel(self, which: int):
+        """Testing (include/hdpm.h HDPM_OPT_EXACT_KERNEL): 0 automatic, 1 a wave per point, 2 a
+        thread per point, 3 level-indexed tables."""
+        self._check(self._L.hdpm_set_option(self._h, _lib.OPT_EXACT_KERNEL, float(which)))
+
     def set_hig_logspace(self, on: bool = True):
         """Extension beyond the reference (include/hdpm.h HDPM_OPT_HIG_LOGSPACE): finite HIG
         log-densities for clusters whose 2F1 series overflows (the reference throws)."""

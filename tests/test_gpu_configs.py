@@ -306,17 +306,20 @@ def test_c2_device_wide_resolver_gives_up_and_recovers(hd, oracle, fail_at, wait
 
 
 @pytest.mark.timeout(900)
-def test_c2_unconverged_many_latents(hd, oracle):
-    """m = 20 latent entries (E = K + m = 40 <= 64): the wave-per-point exact rows
-    (k_exact_rows_mass) take a point's m + 1 > 16 draws from the stream per lane (ADVICE r4:
-    its 16-word batch load picked the next point's words for latent u >= 16).  C2 from a random
-    L = 20 start, with snapshot draws (under 65,536 listed points), against the oracle."""
+@pytest.mark.parametrize("kernel", [1, 2, 3])
+def test_c2_unconverged_many_latents(hd, oracle, kernel):
+    """m = 20 latent entries (E = K + m = 40 <= 64), C2 from a random L = 20 start, with
+    snapshot draws, against the oracle, on each mass exact-rows kernel: the wave-per-point one
+    (k_exact_rows_mass) takes a point's m + 1 > 16 draws from the stream per lane (ADVICE r4:
+    its 16-word batch load picked the next point's words for latent u >= 16); the
+    thread-per-point ones (compare / select, level tables) with k_snap_draws behind them."""
     from split_and_merge_gibbs_sampling_amd.data import config
     ds = config("c2")
     eng = hd.Engine(0)
     eng.set_data(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w)
     eng.set_seed(8)
     m = 20
+    eng.set_exact_kernel(kernel)
     params = eng.chain_params(m=m, iterations=1, L=20, burnin=0, neal8=True, split_merge=False)
     eng.init_chain(params, c_i=None)
     c, cen, sig = eng.get_state()
@@ -332,5 +335,5 @@ def test_c2_unconverged_many_latents(hd, oracle):
         assert oracle.update_phi(ds.codes, ds.attrisize, ds.v, ds.w, ost, rng) == 0
         same(eng, ost, rng, f"update_phi {k}")
     st = eng.stats()
-    assert st["exact_mass_launches"] > 0, st
+    assert st["exact_mass_launches" if kernel == 1 else "exact_lanes_launches"] > 0, st
     eng.close()
