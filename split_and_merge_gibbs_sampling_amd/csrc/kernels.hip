@@ -18,6 +18,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 
 #include "glibc_math.hpp"
 #include "kernels.hpp"
@@ -3123,7 +3124,7 @@ __global__ __launch_bounds__(1024) void k_finish_sweep(int* counts, int* sol, in
 __global__ void k_scatter_clusters(const uint8_t* __restrict__ stage, int nent, int dp, int d, int bw, int full,
                                    uint8_t* codes, double* tab, uint64_t* bnd, int* counts, int* sol, int* los,
                                    int* src, const int* gate) {
-  if (gate && *(volatile const int*)gate == 0) return;
+  if (gate_closed(gate)) return;
   const UploadLayout L = upload_layout(nent, dp, d, bw);
   const int* slot = (const int*)(stage + L.off_slot);
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (int64_t)gridDim.x * blockDim.x;
@@ -3309,7 +3310,7 @@ __global__ __launch_bounds__(kBlock) void k_lmatrix(const uint8_t* codes_t, int 
 // ------------------------------------------------------------------ launchers
 template <int WB, int WS, bool HEAD>
 static hipError_t launch_prepass_t(const PrepassArgs& a, int nblocks, hipStream_t s) {
-  hipLaunchKernelGGL((k_prepass<WB, WS, HEAD>), dim3(nblocks), dim3(kBlock), 0, s, a);
+  HDPM_LAUNCH((k_prepass<WB, WS, HEAD>), dim3(nblocks), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 
@@ -3339,7 +3340,7 @@ static hipError_t launch_prepass_w(const PrepassArgs& a, int nblocks, hipStream_
         const char* e = std::getenv("HDPM_WIDE_CLAIM");
         return e ? std::atoi(e) : 0;
       }();
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(kWideThreads), lds, s, a, nchunks, claim);
+      HDPM_LAUNCH(kern, dim3(grid), dim3(kWideThreads), lds, s, a, nchunks, claim);
       return hipGetLastError();
     };
     if constexpr (WB <= 2) {
@@ -3347,7 +3348,7 @@ static hipError_t launch_prepass_w(const PrepassArgs& a, int nblocks, hipStream_
     }
     return cl ? go(k_prepass_wide<WB, 1, kClOk>) : go(k_prepass_wide<WB, 1, false>);
   }
-  hipLaunchKernelGGL(k_prepass_generic, dim3(nblocks), dim3(kBlock), 0, s, a);
+  HDPM_LAUNCH(k_prepass_generic, dim3(nblocks), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 
@@ -3820,9 +3821,9 @@ static hipError_t launch_snap_draws(const PrepassArgs& a, hipStream_t s) {
   if (a.spec) {
     const dim3 g((unsigned)(device_cus() * 4)), b(256);
     const int E = a.K + a.m;
-    if (E <= 24) hipLaunchKernelGGL(k_snap_draws<24>, g, b, 0, s, a);
-    else if (E <= 32) hipLaunchKernelGGL(k_snap_draws<32>, g, b, 0, s, a);
-    else hipLaunchKernelGGL(k_snap_draws<64>, g, b, 0, s, a);
+    if (E <= 24) HDPM_LAUNCH(k_snap_draws<24>, g, b, 0, s, a);
+    else if (E <= 32) HDPM_LAUNCH(k_snap_draws<32>, g, b, 0, s, a);
+    else HDPM_LAUNCH(k_snap_draws<64>, g, b, 0, s, a);
   }
   return hipGetLastError();
 }
@@ -3840,12 +3841,12 @@ hipError_t launch_exact_rows(const PrepassArgs& a0, int nblocks, hipStream_t s, 
   if (a.dense_direct) {
     // every point of [p0, n) listed, in order (k_dense_list wrote the list and the records)
   } else if (a.exact_scan && a.boff) {
-    hipLaunchKernelGGL(k_list_offsets, dim3(1), dim3(kScanThreads), 0, s, a.cnt, a.nlb, a.boff, a.dense_total);
+    HDPM_LAUNCH(k_list_offsets, dim3(1), dim3(kScanThreads), 0, s, a.cnt, a.nlb, a.boff, a.dense_total);
     const size_t mlds0 = exact_mass_lds_bytes(a.K, a.m, a.d, a.nq * 16);
     const bool mass = !a.exact_wave && ((E <= kWave && mlds0 <= 96 * 1024) || !a.spec || a.spec_lv);
-    hipLaunchKernelGGL(k_list_fill, dim3((unsigned)((a.nlb + 3) / 4)), dim3(256), 0, s, a, mass ? 1 : 0);
+    HDPM_LAUNCH(k_list_fill, dim3((unsigned)((a.nlb + 3) / 4)), dim3(256), 0, s, a, mass ? 1 : 0);
   } else if (a.exact_scan || !wg) {
-    hipLaunchKernelGGL(k_list_scan, dim3(1), dim3(kScanThreads), 0, s, a.cnt, a.nlb, a.lblock, a.dense,
+    HDPM_LAUNCH(k_list_scan, dim3(1), dim3(kScanThreads), 0, s, a.cnt, a.nlb, a.lblock, a.dense,
                        a.dense_total);
   }
   if (!wg) a.exact_scan = 1;
@@ -3869,13 +3870,13 @@ hipError_t launch_exact_rows(const PrepassArgs& a0, int nblocks, hipStream_t s, 
   // (with snapshot draws when spec is set: k_snap_draws behind the rows)
   if (a.exact_scan && (!a.spec || a.spec_lv) && !a.exact_wave && a.nq <= kLanesMaxNq && a.K <= kWave && a.mmax >= 1 &&
       vlds <= 120 * 1024 && !want_mass && !want_lanes) {
-    hipLaunchKernelGGL(k_exact_rows_lv, dim3(lv_grid(vlds)), dim3(kLvThreads), vlds, s, a);
+    HDPM_LAUNCH(k_exact_rows_lv, dim3(lv_grid(vlds)), dim3(kLvThreads), vlds, s, a);
     if (path) *path = 3;
     return launch_snap_draws(a, s);
   }
   if (a.exact_scan && (!a.spec || want_lanes) && !a.exact_wave && a.nq <= kLanesMaxNq && a.K <= kWave &&
       llds <= 64 * 1024 && !want_mass) {
-    hipLaunchKernelGGL(k_exact_rows_lanes, dim3(lanes_grid(llds)), dim3(256), llds, s, a);
+    HDPM_LAUNCH(k_exact_rows_lanes, dim3(lanes_grid(llds)), dim3(256), llds, s, a);
     if (path) *path = 2;
     return launch_snap_draws(a, s);
   }
@@ -3884,13 +3885,13 @@ hipError_t launch_exact_rows(const PrepassArgs& a0, int nblocks, hipStream_t s, 
       const char* e = std::getenv("HDPM_MASS_STATIC");
       return e ? std::atoi(e) : 0;
     }();
-    hipLaunchKernelGGL(k_exact_rows_mass, dim3(mass_grid(mlds)), dim3(kWave * kMassWaves), mlds, s, a, mstatic);
+    HDPM_LAUNCH(k_exact_rows_mass, dim3(mass_grid(mlds)), dim3(kWave * kMassWaves), mlds, s, a, mstatic);
     if (path) *path = 1;
     return hipGetLastError();
   }
-  if (wg && E <= kWave) hipLaunchKernelGGL(k_exact_rows_wg<1>, g, b, lds, s, a);
-  else if (wg && E <= 4 * kWave) hipLaunchKernelGGL(k_exact_rows_wg<4>, g, b, lds, s, a);
-  else hipLaunchKernelGGL(k_exact_rows, dim3(std::min(nblocks, 1024)), dim3(kWave * kExactWaves), 0, s, a);
+  if (wg && E <= kWave) HDPM_LAUNCH(k_exact_rows_wg<1>, g, b, lds, s, a);
+  else if (wg && E <= 4 * kWave) HDPM_LAUNCH(k_exact_rows_wg<4>, g, b, lds, s, a);
+  else HDPM_LAUNCH(k_exact_rows, dim3(std::min(nblocks, 1024)), dim3(kWave * kExactWaves), 0, s, a);
   return hipGetLastError();
 }
 
@@ -3910,7 +3911,7 @@ __global__ __launch_bounds__(256) void k_dense_list(PrepassArgs a) {
 }
 hipError_t launch_dense_list(const PrepassArgs& a, hipStream_t s) {
   const int cnt = a.n - a.p0;
-  hipLaunchKernelGGL(k_dense_list, dim3((unsigned)std::min(4 * device_cus(), std::max(1, (cnt + 255) / 256))), dim3(256),
+  HDPM_LAUNCH(k_dense_list, dim3((unsigned)std::min(4 * device_cus(), std::max(1, (cnt + 255) / 256))), dim3(256),
                      0, s, a);
   return hipGetLastError();
 }
@@ -3918,7 +3919,7 @@ hipError_t launch_dense_list(const PrepassArgs& a, hipStream_t s) {
 hipError_t launch_cluster_summary(const PrepassArgs& a, hipStream_t s) {
   if (a.K > 0) {
     const int work = a.K * (a.bw + 2);
-    hipLaunchKernelGGL(k_cluster_summary, dim3(std::min(64, (work + 255) / 256)), dim3(256), 0, s, a);
+    HDPM_LAUNCH(k_cluster_summary, dim3(std::min(64, (work + 255) / 256)), dim3(256), 0, s, a);
   }
   return hipGetLastError();
 }
@@ -3977,51 +3978,86 @@ int warm_sweep_kernels(int lcap, int m) {
 // returns).
 hipError_t warm_launch_kernels(const PrepassArgs& pa0, const ResolveArgs& ra0, const int* zero, int* scratch,
                                hipStream_t s) {
+  // (raw_ptr too: a valid word, never read behind a closed gate -- pipe_gate)
+  const uint32_t* const* zero_ptr = reinterpret_cast<const uint32_t* const*>(scratch + 8);
   PrepassArgs pa = pa0;
   pa.gate = zero;
+  pa.raw_ptr = zero_ptr;
   ResolveArgs ra = ra0;
   ra.gate = zero;
+  ra.raw_ptr = zero_ptr;
   const dim3 one(1);
-  hipLaunchKernelGGL(k_dense_list, one, dim3(256), 0, s, pa);
-  hipLaunchKernelGGL(k_list_fill, one, dim3(256), 0, s, pa, 1);
-  hipLaunchKernelGGL(k_list_offsets, one, dim3(kScanThreads), 0, s, (const int*)scratch, 0, scratch, scratch + 1);
-  hipLaunchKernelGGL(k_exact_rows_lv, one, dim3(kLvThreads), 0, s, pa);
-  hipLaunchKernelGGL(k_exact_rows_lanes, one, dim3(256), 0, s, pa);
-  hipLaunchKernelGGL(k_exact_rows_mass, one, dim3(kWave * kMassWaves), 0, s, pa, 0);
-  hipLaunchKernelGGL(k_snap_draws<24>, one, dim3(256), 0, s, pa);
-  hipLaunchKernelGGL(k_snap_draws<32>, one, dim3(256), 0, s, pa);
-  hipLaunchKernelGGL(k_snap_draws<64>, one, dim3(256), 0, s, pa);
-  hipLaunchKernelGGL(k_resolve_fp<24>, one, dim3(kFpThreads), 0, s, ra);
-  hipLaunchKernelGGL(k_resolve_fp<32>, one, dim3(kFpThreads), 0, s, ra);
-  hipLaunchKernelGGL(k_resolve_fp<64>, one, dim3(kFpThreads), 0, s, ra);
-  hipLaunchKernelGGL(k_resolve_fpg<24>, one, dim3(kFpThreads), 0, s, ra);
-  hipLaunchKernelGGL(k_resolve_fpg<32>, one, dim3(kFpThreads), 0, s, ra);
-  hipLaunchKernelGGL(k_resolve_fpg<64>, one, dim3(kFpThreads), 0, s, ra);
-  hipLaunchKernelGGL(k_apply_moves_lds, one, dim3(256), 0, s, (const int*)scratch, (const int*)scratch,
-                     pa.codes_t, pa.d, pa.nq, pa.mmax, (unsigned int*)nullptr, (const ResolveCtl*)(scratch + 4), pa.n, 2);
-  return hipGetLastError();
+  // HDPM_WARM_SYNC=1 (diagnosis): synchronise after every launch and name it on stderr
+  static const bool wsync = [] {
+    const char* e = std::getenv("HDPM_WARM_SYNC");
+    return e && std::atoi(e) == 1;
+  }();
+  static const int wmask = [] {
+    const char* e = std::getenv("HDPM_WARM_MASK");
+    return e ? (int)std::strtol(e, nullptr, 0) : -1;
+  }();
+  int k = 0;
+  auto step = [&](const char* name) -> hipError_t {
+    hipError_t e = hipGetLastError();
+    if (wsync) {
+      if (e == hipSuccess) e = hipStreamSynchronize(s);
+      std::fprintf(stderr, "[warm] %2d %s: %s\n", k, name, hipGetErrorString(e));
+    }
+    ++k;
+    return e;
+  };
+  auto on = [&]() { return (wmask >> k) & 1; };
+  hipError_t e = hipSuccess;
+#define HDPM_WARM(name, ...)                                 \
+  if (e == hipSuccess) {                                     \
+    if (on()) {                                              \
+      hipLaunchKernelGGL(__VA_ARGS__);                       \
+      e = step(name);                                        \
+    } else {                                                 \
+      ++k;                                                   \
+    }                                                        \
+  }
+  HDPM_WARM("k_dense_list", k_dense_list, one, dim3(256), 0, s, pa)
+  HDPM_WARM("k_list_fill", k_list_fill, one, dim3(256), 0, s, pa, 1)
+  HDPM_WARM("k_list_offsets", k_list_offsets, one, dim3(kScanThreads), 0, s, (const int*)scratch, 0, scratch, scratch + 1)
+  HDPM_WARM("k_exact_rows_lv", k_exact_rows_lv, one, dim3(kLvThreads), 0, s, pa)
+  HDPM_WARM("k_exact_rows_lanes", k_exact_rows_lanes, one, dim3(256), 0, s, pa)
+  HDPM_WARM("k_exact_rows_mass", k_exact_rows_mass, one, dim3(kWave * kMassWaves), 0, s, pa, 0)
+  HDPM_WARM("k_apply_moves_lds", k_apply_moves_lds, one, dim3(256), 0, s, (const int*)scratch, (const int*)scratch,
+            pa.codes_t, pa.d, pa.nq, pa.mmax, (unsigned int*)nullptr, (const ResolveCtl*)(scratch + 4), pa.n, 2)
+  HDPM_WARM("k_snap_draws<24>", k_snap_draws<24>, one, dim3(256), 0, s, pa)
+  HDPM_WARM("k_snap_draws<32>", k_snap_draws<32>, one, dim3(256), 0, s, pa)
+  HDPM_WARM("k_snap_draws<64>", k_snap_draws<64>, one, dim3(256), 0, s, pa)
+  HDPM_WARM("k_resolve_fp<24>", k_resolve_fp<24>, one, dim3(kFpThreads), 0, s, ra)
+  HDPM_WARM("k_resolve_fp<32>", k_resolve_fp<32>, one, dim3(kFpThreads), 0, s, ra)
+  HDPM_WARM("k_resolve_fp<64>", k_resolve_fp<64>, one, dim3(kFpThreads), 0, s, ra)
+  HDPM_WARM("k_resolve_fpg<24>", k_resolve_fpg<24>, one, dim3(kFpThreads), 0, s, ra)
+  HDPM_WARM("k_resolve_fpg<32>", k_resolve_fpg<32>, one, dim3(kFpThreads), 0, s, ra)
+  HDPM_WARM("k_resolve_fpg<64>", k_resolve_fpg<64>, one, dim3(kFpThreads), 0, s, ra)
+#undef HDPM_WARM
+  return e;
 }
 
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s) {
   if (a.fp && a.fpg > 1) {
     const size_t lds = resolve_fpg_lds_bytes(a.lcap, a.m);
-    if (a.K + a.m <= 24) hipLaunchKernelGGL(k_resolve_fpg<24>, dim3(a.fpg), dim3(kFpThreads), lds, s, a);
-    else if (a.K + a.m <= 32) hipLaunchKernelGGL(k_resolve_fpg<32>, dim3(a.fpg), dim3(kFpThreads), lds, s, a);
-    else hipLaunchKernelGGL(k_resolve_fpg<64>, dim3(a.fpg), dim3(kFpThreads), lds, s, a);
+    if (a.K + a.m <= 24) HDPM_LAUNCH(k_resolve_fpg<24>, dim3(a.fpg), dim3(kFpThreads), lds, s, a);
+    else if (a.K + a.m <= 32) HDPM_LAUNCH(k_resolve_fpg<32>, dim3(a.fpg), dim3(kFpThreads), lds, s, a);
+    else HDPM_LAUNCH(k_resolve_fpg<64>, dim3(a.fpg), dim3(kFpThreads), lds, s, a);
   } else if (a.fp) {
     const size_t lds = resolve_fp_lds_bytes(a.lcap, a.m);
-    if (a.K + a.m <= 24) hipLaunchKernelGGL(k_resolve_fp<24>, dim3(1), dim3(kFpThreads), lds, s, a);
-    else if (a.K + a.m <= 32) hipLaunchKernelGGL(k_resolve_fp<32>, dim3(1), dim3(kFpThreads), lds, s, a);
-    else hipLaunchKernelGGL(k_resolve_fp<64>, dim3(1), dim3(kFpThreads), lds, s, a);
+    if (a.K + a.m <= 24) HDPM_LAUNCH(k_resolve_fp<24>, dim3(1), dim3(kFpThreads), lds, s, a);
+    else if (a.K + a.m <= 32) HDPM_LAUNCH(k_resolve_fp<32>, dim3(1), dim3(kFpThreads), lds, s, a);
+    else HDPM_LAUNCH(k_resolve_fp<64>, dim3(1), dim3(kFpThreads), lds, s, a);
   } else if (a.blocks)
-    hipLaunchKernelGGL(k_resolve_blk, dim3(1), dim3(kWave), resolve_lds_bytes(a.lcap, a.m, 1), s, a);
+    HDPM_LAUNCH(k_resolve_blk, dim3(1), dim3(kWave), resolve_lds_bytes(a.lcap, a.m, 1), s, a);
   else
-    hipLaunchKernelGGL(k_resolve, dim3(1), dim3(kWave), resolve_lds_bytes(a.lcap, a.m, 0, a.S + a.m), s, a);
+    HDPM_LAUNCH(k_resolve, dim3(1), dim3(kWave), resolve_lds_bytes(a.lcap, a.m, 0, a.S + a.m), s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_relabel(int* c, const int* los, int n, const ResolveCtl* ctl, hipStream_t s) {
-  hipLaunchKernelGGL(k_relabel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, c, los, n, ctl);
+  HDPM_LAUNCH(k_relabel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, c, los, n, ctl);
   return hipGetLastError();
 }
 
@@ -4030,11 +4066,11 @@ hipError_t launch_apply_moves(const int* mlog, const int* mcount, int grid, cons
   // LDS deltas for the slots that fit 64 KB (C5: 32 of them; the sweep's slots are < nslots)
   const int ls = std::min(nslots, (int)(64 * 1024 / ((size_t)d * mmax * 4)));
   if (ls >= 2) {
-    hipLaunchKernelGGL(k_apply_moves_lds, dim3(512), dim3(256), (size_t)ls * d * mmax * 4, s, mlog, mcount, codes_t, d,
+    HDPM_LAUNCH(k_apply_moves_lds, dim3(512), dim3(256), (size_t)ls * d * mmax * 4, s, mlog, mcount, codes_t, d,
                        nq, mmax, freq, ctl, n, ls);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(k_apply_moves, dim3(std::max(1, std::min(grid, 4096))), dim3(kWave), 0, s, mlog, mcount, codes_t,
+  HDPM_LAUNCH(k_apply_moves, dim3(std::max(1, std::min(grid, 4096))), dim3(kWave), 0, s, mlog, mcount, codes_t,
                      d, nq, mmax, freq, ctl, n);
   return hipGetLastError();
 }
@@ -4042,14 +4078,14 @@ hipError_t launch_apply_moves(const int* mlog, const int* mcount, int grid, cons
 hipError_t launch_freq_gather(const unsigned int* freq, const int* sol, int Kmax, int fs, unsigned int* out,
                               const ResolveCtl* ctl, int n, hipStream_t s) {
   const int64_t work = (int64_t)std::max(Kmax, 1) * fs;
-  hipLaunchKernelGGL(k_freq_gather, dim3((unsigned)std::min<int64_t>(1024, (work + 255) / 256)), dim3(256), 0, s, freq,
+  HDPM_LAUNCH(k_freq_gather, dim3((unsigned)std::min<int64_t>(1024, (work + 255) / 256)), dim3(256), 0, s, freq,
                      sol, fs, out, ctl, n);
   return hipGetLastError();
 }
 
 hipError_t launch_finish_sweep(int* counts, int* sol, int* los, int* src, int cap, const ResolveCtl* ctl, int n,
                                hipStream_t s) {
-  hipLaunchKernelGGL(k_finish_sweep, dim3(1), dim3(1024), (size_t)(2 * cap) * 4, s, counts, sol, los, src, ctl, n);
+  HDPM_LAUNCH(k_finish_sweep, dim3(1), dim3(1024), (size_t)(2 * cap) * 4, s, counts, sol, los, src, ctl, n);
   return hipGetLastError();
 }
 
@@ -4088,7 +4124,7 @@ __global__ void k_pipe_wait(const PipeSlot* slot, const ResolveCtl* prev, Resolv
 }
 hipError_t launch_pipe_wait(const PipeSlot* slot, const ResolveCtl* prev, ResolveCtl* own, int n, PipeGate* g,
                             long long limit, hipStream_t s) {
-  hipLaunchKernelGGL(k_pipe_wait, dim3(1), dim3(64), 0, s, slot, prev, own, n, g, limit);
+  HDPM_LAUNCH(k_pipe_wait, dim3(1), dim3(64), 0, s, slot, prev, own, n, g, limit);
   return hipGetLastError();
 }
 
@@ -4097,7 +4133,7 @@ hipError_t launch_scatter_clusters(const uint8_t* stage, int nent, int dp, int d
                                    hipStream_t s, const int* gate) {
   const int64_t work = (int64_t)nent * std::max(2 * d, std::max(dp, bw));
   const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (work + 255) / 256));
-  hipLaunchKernelGGL(k_scatter_clusters, dim3(nb), dim3(256), 0, s, stage, nent, dp, d, bw, full, codes, tab, bnd,
+  HDPM_LAUNCH(k_scatter_clusters, dim3(nb), dim3(256), 0, s, stage, nent, dp, d, bw, full, codes, tab, bnd,
                      counts, sol, los, src, gate);
   return hipGetLastError();
 }
@@ -4129,24 +4165,24 @@ hipError_t launch_hist(const HistArgs& a0, hipStream_t s) {
     const int ny = (a.K + kc - 1) / kc;
     const size_t hbytes = (((size_t)(kc + 1) * a.mmax * a.d * 4 + 15) / 16) * 16;
     const size_t lds = hbytes + (size_t)(kHistBlock / kWave) * a.W * 64 * 8;
-    hipLaunchKernelGGL(k_hist_packed, dim3(nbx, ny), dim3(kHistBlock), lds, s, a);
+    HDPM_LAUNCH(k_hist_packed, dim3(nbx, ny), dim3(kHistBlock), lds, s, a);
     const int hsize = kc * a.mmax * a.d;
-    hipLaunchKernelGGL(k_hist_reduce, dim3((hsize + 255) / 256, ny, kHistReduceSplit), dim3(256), 0, s, a, nbx);
+    HDPM_LAUNCH(k_hist_reduce, dim3((hsize + 255) / 256, ny, kHistReduceSplit), dim3(256), 0, s, a, nbx);
   } else {
     const int64_t nt = (int64_t)a.n * a.nq;
-    hipLaunchKernelGGL(k_hist_global, dim3((nt + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
+    HDPM_LAUNCH(k_hist_global, dim3((nt + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
   }
   return hipGetLastError();
 }
 
 hipError_t launch_loglik(const LoglikArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_loglik, dim3((a.n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
+  HDPM_LAUNCH(k_loglik, dim3((a.n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_lmatrix(const uint8_t* codes_t, int n, int d, int nq, ParamTables cl, int K, double* L,
                           int* H, int64_t ldL, hipStream_t s) {
-  hipLaunchKernelGGL(k_lmatrix, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, codes_t, n, d, nq, cl,
+  HDPM_LAUNCH(k_lmatrix, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, codes_t, n, d, nq, cl,
                      K, L, H, ldL);
   return hipGetLastError();
 }
@@ -4454,15 +4490,15 @@ hipError_t launch_sm_ll(const SmArgs& a, hipStream_t s) {
   const size_t lds = (size_t)4 * a.d * 8 + (size_t)2 * a.nq * 16;
   if (lds <= 64 * 1024) {
     const int per = kSmLLBlock / 2;     // points per workgroup (two lanes each)
-    hipLaunchKernelGGL(k_sm_ll_lds, dim3((a.nS + per - 1) / per), dim3(kSmLLBlock), lds, s, a);
+    HDPM_LAUNCH(k_sm_ll_lds, dim3((a.nS + per - 1) / per), dim3(kSmLLBlock), lds, s, a);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(k_sm_ll, dim3((a.nS + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
+  HDPM_LAUNCH(k_sm_ll, dim3((a.nS + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_sm_scan(const SmArgs& a, hipStream_t s) {
-  if (a.nS > 0) hipLaunchKernelGGL(k_sm_cert, dim3((a.nS + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
-  hipLaunchKernelGGL(k_sm_scan, dim3(1), dim3(kSmScanThreads), 2 * sizeof(SmChunk), s, a);
+  if (a.nS > 0) HDPM_LAUNCH(k_sm_cert, dim3((a.nS + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
+  HDPM_LAUNCH(k_sm_scan, dim3(1), dim3(kSmScanThreads), 2 * sizeof(SmChunk), s, a);
   return hipGetLastError();
 }
 
@@ -4494,20 +4530,20 @@ __global__ void k_debug_math(const double* x, int64_t n, int fn, double* out) {
 }
 hipError_t launch_debug_draw(const double* logw, int E, double rU, int two_way, int ocml, int* out, hipStream_t s) {
   if (E < 1 || E > 4 * kWave || (two_way && E != 2)) return hipErrorInvalidValue;
-  if (ocml) hipLaunchKernelGGL(k_debug_draw<true>, dim3(1), dim3(kWave), 0, s, logw, E, rU, two_way, out);
-  else hipLaunchKernelGGL(k_debug_draw<false>, dim3(1), dim3(kWave), 0, s, logw, E, rU, two_way, out);
+  if (ocml) HDPM_LAUNCH(k_debug_draw<true>, dim3(1), dim3(kWave), 0, s, logw, E, rU, two_way, out);
+  else HDPM_LAUNCH(k_debug_draw<false>, dim3(1), dim3(kWave), 0, s, logw, E, rU, two_way, out);
   return hipGetLastError();
 }
 hipError_t launch_debug_math(const double* x, int64_t n, int fn, int ocml, double* out, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   const dim3 g((unsigned)((n + kBlock - 1) / kBlock));
-  if (ocml) hipLaunchKernelGGL(k_debug_math<true>, g, dim3(kBlock), 0, s, x, n, fn, out);
-  else hipLaunchKernelGGL(k_debug_math<false>, g, dim3(kBlock), 0, s, x, n, fn, out);
+  if (ocml) HDPM_LAUNCH(k_debug_math<true>, g, dim3(kBlock), 0, s, x, n, fn, out);
+  else HDPM_LAUNCH(k_debug_math<false>, g, dim3(kBlock), 0, s, x, n, fn, out);
   return hipGetLastError();
 }
 hipError_t launch_sm_lpgs(const SmArgs& a, hipStream_t s) {
   if (a.nS == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_sm_lpgs, dim3((a.nS + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
+  HDPM_LAUNCH(k_sm_lpgs, dim3((a.nS + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 
@@ -4642,9 +4678,9 @@ __global__ __launch_bounds__(640) void k_mt_gen_multi(MtGenArgs a) {
 hipError_t launch_mt_gen(const MtGenArgs& a, hipStream_t s) {
   if (a.G > 1 && a.jpoly) {
     const size_t lds = ((size_t)(33 + 2) * 624 + kJumpChunk) * 4;
-    hipLaunchKernelGGL(k_mt_gen_multi, dim3(a.G), dim3(640), lds, s, a);
+    HDPM_LAUNCH(k_mt_gen_multi, dim3(a.G), dim3(640), lds, s, a);
   } else {
-    hipLaunchKernelGGL(k_mt_gen, dim3(1), dim3(640), 0, s, a);
+    HDPM_LAUNCH(k_mt_gen, dim3(1), dim3(640), 0, s, a);
   }
   return hipGetLastError();
 }

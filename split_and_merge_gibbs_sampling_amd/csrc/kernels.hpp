@@ -4,7 +4,31 @@
 
 #include <cstdint>
 
+#include <cstdio>
+#include <cstdlib>
+
 namespace hdpm {
+
+// Diagnosis (HDPM_SYNC_EACH=1): every kernel launch of the engine is followed by a stream
+// synchronisation and its name and status on stderr, so a device fault is pinned on the
+// kernel that raised it (the next launch would otherwise report it).
+inline bool sync_each() {
+  static const bool on = [] {
+    const char* e = std::getenv("HDPM_SYNC_EACH");
+    return e && std::atoi(e) == 1;
+  }();
+  return on;
+}
+inline void sync_report(const char* name, hipStream_t s) {
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  std::fprintf(stderr, "[sync] %s: %s\n", name, hipGetErrorString(e));
+}
+#define HDPM_LAUNCH(kern, grid, block, lds, strm, ...)                       \
+  do {                                                                      \
+    hipLaunchKernelGGL(kern, grid, block, lds, strm, __VA_ARGS__);          \
+    if (::hdpm::sync_each()) ::hdpm::sync_report(#kern, strm);              \
+  } while (0)
 
 constexpr int kBlock = 256;        // prepass points per workgroup (4 waves)
 constexpr int kWave = 64;
@@ -146,10 +170,19 @@ struct PrepassArgs {
 };
 
 // A sweep's kernels in a pipeline read `raw` from the device (pipe_gate); false: skip.
+// The gate word is read with a vector load, so the compiler takes its value as divergent and
+// guards the rest by the exec mask alone -- without a branch around a block this short -- and
+// the scalar load of *raw_ptr then ran with every lane off: a closed gate with raw_ptr null
+// (the gated-off warm launches) faulted on address 0.  The gate is made
+// wave-uniform (readfirstlane), so a closed gate branches around the load.
+__device__ __forceinline__ bool gate_closed(const int* gate) {
+  return gate && __builtin_amdgcn_readfirstlane(*(volatile const int*)gate) == 0;
+}
 template <class A>
 __device__ __forceinline__ bool pipe_gate(A& a) {
   if (!a.gate) return true;
-  if (*(volatile const int*)a.gate == 0) return false;
+  const int g = __builtin_amdgcn_readfirstlane(*(volatile const int*)a.gate);
+  if (g == 0) return false;
   a.raw = *a.raw_ptr;
   return true;
 }

@@ -385,7 +385,7 @@ __device__ __forceinline__ void phi_logits_block(const PhiArgs& a, int blk, int 
 // Both in one launch: workgroups [0, nprep) prepare the items, the others compute the logits
 // (independent work; one dispatch less on the update's dependency chain).
 __global__ __launch_bounds__(256) void k_phi_prep(PhiArgs a, int nprep) {
-  if (a.gate && *(volatile const int*)a.gate == 0) return;
+  if (gate_closed(a.gate)) return;
   if (a.raw_ptr) a.raw = *a.raw_ptr;
   __shared__ uint64_t tabs[512];
   __shared__ double spr[256 * kPhiLdsLevels];
@@ -400,7 +400,7 @@ __global__ __launch_bounds__(256) void k_phi_prep(PhiArgs a, int nprep) {
 // mask[cand][q] bit i: the rbeta attempt at drift lo + 64 q + i of the candidate's item is
 // accepted with x <= (m - 1) / m (rhig's loop ends there).
 __global__ __launch_bounds__(256) void k_phi_masks(PhiArgs a) {
-  if (a.gate && *(volatile const int*)a.gate == 0) return;
+  if (gate_closed(a.gate)) return;
   if (a.raw_ptr) a.raw = *a.raw_ptr;
   __shared__ uint64_t tabs[512];
   for (int i = threadIdx.x; i < 512; i += blockDim.x) tabs[i] = a.gtab[i];
@@ -571,7 +571,7 @@ __host__ __device__ inline size_t phi_cwalk_image(int d, int nw) {
 }
 
 __global__ __launch_bounds__(1024) void k_phi_cwalk(PhiArgs a) {
-  if (a.gate && *(volatile const int*)a.gate == 0) return;
+  if (gate_closed(a.gate)) return;
   if (a.raw_ptr) a.raw = *a.raw_ptr;
   extern __shared__ __attribute__((aligned(16))) uint8_t wl[];
   if (*a.status != 0) return;
@@ -748,7 +748,7 @@ __device__ int64_t phi_walk_serial(const PhiArgs& a, int t, int j0, int j1, int6
 // F[t S + s][delta - phi_lo(t d + s L)] (the table staged in LDS when it fits, many loads in
 // flight per thread); dts[t] = cluster t's start drift.
 __global__ __launch_bounds__(1024) void k_phi_chain(PhiArgs a) {
-  if (a.gate && *(volatile const int*)a.gate == 0) return;
+  if (gate_closed(a.gate)) return;
   if (a.raw_ptr) a.raw = *a.raw_ptr;
   extern __shared__ int sF[];
   if (*a.status != 0) return;
@@ -942,7 +942,7 @@ __device__ __forceinline__ void phi_values_body(const PhiArgs& a, int t, const u
 // positions into LDS), then phi_values_body.  LDS: the cluster image, picks, positions, per
 // attribute (sigma, match, mismatch), per thread the partial sums.
 __global__ __launch_bounds__(1024) void k_phi_values(PhiArgs a) {
-  if (a.gate && *(volatile const int*)a.gate == 0) return;
+  if (gate_closed(a.gate)) return;
   if (a.raw_ptr) a.raw = *a.raw_ptr;
   extern __shared__ __attribute__((aligned(16))) uint8_t wl[];
   __shared__ uint64_t tabs[512];
@@ -1017,7 +1017,7 @@ __host__ __device__ inline size_t phi_tree_lds(int SB, int nw, int W) {
 // item masks staged in LDS: a 4-item walk per start drift), then levels 1 .. log2(SB) of that
 // segment (compositions in LDS); every table also goes to a.tree.
 __global__ __launch_bounds__(1024) void k_phi_tree(PhiArgs a) {
-  if (a.gate && *(volatile const int*)a.gate == 0) return;
+  if (gate_closed(a.gate)) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
   if (*a.status != 0) return;
   const int S = a.tS, SB = a.tSB, nb = a.tnb, W = a.tW, nw = a.nw, d = a.d;
@@ -1074,7 +1074,7 @@ __global__ __launch_bounds__(1024) void k_phi_tree(PhiArgs a) {
 
 // Levels above the segments (tS > 1): one workgroup per cluster composes them in a.tree.
 __global__ __launch_bounds__(1024) void k_phi_tree_top(PhiArgs a) {
-  if (a.gate && *(volatile const int*)a.gate == 0) return;
+  if (gate_closed(a.gate)) return;
   if (*a.status != 0) return;
   const int nb = a.tnb, W = a.tW, d = a.d, t = blockIdx.x;
   if (a.tnd[t]) return;
@@ -1115,7 +1115,7 @@ __host__ __device__ inline size_t phi_values2_lds(int d, int nb, int T, int W, i
 // level-0 blocks (one lookup per node and level), each block's 4 items walked from its start
 // (picks fixed: det), then phi_values_body.  The last cluster also writes the consumption.
 __global__ __launch_bounds__(1024) void k_phi_values2(PhiArgs a) {
-  if (a.gate && *(volatile const int*)a.gate == 0) return;
+  if (gate_closed(a.gate)) return;
   if (a.raw_ptr) a.raw = *a.raw_ptr;
   extern __shared__ __attribute__((aligned(16))) uint8_t wl[];
   __shared__ uint64_t tabs[512];
@@ -1257,33 +1257,33 @@ hipError_t launch_phi(const PhiArgs& a, hipStream_t s) {
   if (a.nw < 1 || a.wpb < 1 || a.wpb > 16) return hipErrorInvalidValue;
   const int nprep = (int)((items + 255) / 256);
   const int nlog = (int)std::min<int64_t>(1024, (a.span + 255) / 256);
-  hipLaunchKernelGGL(k_phi_prep, dim3((unsigned)(nprep + nlog)), dim3(256), 0, s, a, nprep);
+  HDPM_LAUNCH(k_phi_prep, dim3((unsigned)(nprep + nlog)), dim3(256), 0, s, a, nprep);
   // one wave per (candidate, mask word): enough workgroups for every fixed pick's item in one
   // pass (the loop covers the extra candidates of uniform-dependent picks)
   const int64_t mwaves = items * a.nw;
-  hipLaunchKernelGGL(k_phi_masks, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(32768, (mwaves + 3) / 4))),
+  HDPM_LAUNCH(k_phi_masks, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(32768, (mwaves + 3) / 4))),
                      dim3(256), 0, s, a);
   if (a.tree) {
     if (a.tW < 64 || a.tSB < 1 || a.tS < 1 || a.tnb < 1) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_phi_tree, dim3((unsigned)(a.T * a.tS)), dim3(1024), phi_tree_lds(a.tSB, a.nw, a.tW), s, a);
-    if (a.tS > 1) hipLaunchKernelGGL(k_phi_tree_top, dim3((unsigned)a.T), dim3(1024), 0, s, a);
+    HDPM_LAUNCH(k_phi_tree, dim3((unsigned)(a.T * a.tS)), dim3(1024), phi_tree_lds(a.tSB, a.nw, a.tW), s, a);
+    if (a.tS > 1) HDPM_LAUNCH(k_phi_tree_top, dim3((unsigned)a.T), dim3(1024), 0, s, a);
     if (a.S == 1 && a.Wc >= 1 && a.groups >= 1) {
       // clusters with a pick that depends on the uniform: their root tables by the walks
       const int wthreads = std::min(1024, ((a.Wc + kPhiIlp * a.groups - 1) / (kPhiIlp * a.groups) + 63) / 64 * 64);
-      hipLaunchKernelGGL(k_phi_cwalk, dim3((unsigned)(a.T * a.groups)), dim3(wthreads), phi_cwalk_lds(a.d, a.nw, 16),
+      HDPM_LAUNCH(k_phi_cwalk, dim3((unsigned)(a.T * a.groups)), dim3(wthreads), phi_cwalk_lds(a.d, a.nw, 16),
                          s, a);
     }
-    hipLaunchKernelGGL(k_phi_values2, dim3((unsigned)a.T), dim3(64 * a.wpb), phi_values2_lds(a.d, a.tnb, a.T, a.tW, a.nw),
+    HDPM_LAUNCH(k_phi_values2, dim3((unsigned)a.T), dim3(64 * a.wpb), phi_values2_lds(a.d, a.tnb, a.T, a.tW, a.nw),
                        s, a);
     return hipGetLastError();
   }
   if (a.Wc < 1 || a.groups < 1) return hipErrorInvalidValue;
   const int wthreads = std::min(1024, ((a.Wc + kPhiIlp * a.groups - 1) / (kPhiIlp * a.groups) + 63) / 64 * 64);
-  hipLaunchKernelGGL(k_phi_cwalk, dim3((unsigned)(a.T * a.S * a.groups)), dim3(wthreads), phi_cwalk_lds(a.d, a.nw, 16),
+  HDPM_LAUNCH(k_phi_cwalk, dim3((unsigned)(a.T * a.S * a.groups)), dim3(wthreads), phi_cwalk_lds(a.d, a.nw, 16),
                      s, a);
   const int64_t nF = (int64_t)a.T * a.S * a.Wc;
-  hipLaunchKernelGGL(k_phi_chain, dim3(1), dim3(1024), nF <= 16384 ? (size_t)nF * 4 : 0, s, a);
-  hipLaunchKernelGGL(k_phi_values, dim3((unsigned)a.T), dim3(64 * a.wpb), phi_values_lds(a.d, a.nw), s, a);
+  HDPM_LAUNCH(k_phi_chain, dim3(1), dim3(1024), nF <= 16384 ? (size_t)nF * 4 : 0, s, a);
+  HDPM_LAUNCH(k_phi_values, dim3((unsigned)a.T), dim3(64 * a.wpb), phi_values_lds(a.d, a.nw), s, a);
   return hipGetLastError();
 }
 

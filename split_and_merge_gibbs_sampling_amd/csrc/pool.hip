@@ -413,17 +413,17 @@ hipError_t launch_pool_heads(const double* tab, const uint64_t* bnd, int64_t P, 
   if (P <= 0) return hipSuccess;
   if (!head_fits(wb, Ws)) return hipErrorInvalidValue;
   const dim3 g((unsigned)((P + 3) / 4)), b(256);
-  if (Ws == 2) hipLaunchKernelGGL(k_pool_heads<2>, g, b, 0, s, tab, bnd, P, d, wb, Ws, bw, ha, hb, head);
-  else if (Ws == 4) hipLaunchKernelGGL(k_pool_heads<4>, g, b, 0, s, tab, bnd, P, d, wb, Ws, bw, ha, hb, head);
-  else if (Ws <= 8) hipLaunchKernelGGL(k_pool_heads<8>, g, b, 0, s, tab, bnd, P, d, wb, Ws, bw, ha, hb, head);
-  else if (Ws <= 16) hipLaunchKernelGGL(k_pool_heads<16>, g, b, 0, s, tab, bnd, P, d, wb, Ws, bw, ha, hb, head);
-  else hipLaunchKernelGGL(k_pool_heads<32>, g, b, 0, s, tab, bnd, P, d, wb, Ws, bw, ha, hb, head);
+  if (Ws == 2) HDPM_LAUNCH(k_pool_heads<2>, g, b, 0, s, tab, bnd, P, d, wb, Ws, bw, ha, hb, head);
+  else if (Ws == 4) HDPM_LAUNCH(k_pool_heads<4>, g, b, 0, s, tab, bnd, P, d, wb, Ws, bw, ha, hb, head);
+  else if (Ws <= 8) HDPM_LAUNCH(k_pool_heads<8>, g, b, 0, s, tab, bnd, P, d, wb, Ws, bw, ha, hb, head);
+  else if (Ws <= 16) HDPM_LAUNCH(k_pool_heads<16>, g, b, 0, s, tab, bnd, P, d, wb, Ws, bw, ha, hb, head);
+  else HDPM_LAUNCH(k_pool_heads<32>, g, b, 0, s, tab, bnd, P, d, wb, Ws, bw, ha, hb, head);
   return hipGetLastError();
 }
 
 hipError_t launch_pool_accept(const PoolAcceptArgs& a, hipStream_t s) {
   const int64_t blocks = (a.nwords + 3) / 4;
-  hipLaunchKernelGGL(k_pool_accept, dim3((unsigned)blocks), dim3(256), 0, s, a);
+  HDPM_LAUNCH(k_pool_accept, dim3((unsigned)blocks), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
@@ -432,18 +432,18 @@ hipError_t launch_pool_seg(const PoolSegArgs& a, hipStream_t s) {
   if (sp.nchunks < 1 || sp.ncand < 1 || sp.ncand >= 0xFFFF || sp.B < 2 || sp.G < 1 || sp.nchunks > 0x7fffffff ||
       sp.ngroups != (sp.nchunks + sp.G - 1) / sp.G)
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_pool_seg, dim3((unsigned)sp.nchunks), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(k_pool_seg_group, dim3((unsigned)sp.ngroups), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(k_pool_seg_top, dim3(1), dim3(64), 0, s, a);
-  hipLaunchKernelGGL(k_pool_seg_fill, dim3((unsigned)((sp.ngroups + 255) / 256)), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(k_pool_seg_emit, dim3((unsigned)((sp.nchunks + 255) / 256)), dim3(256), 0, s, a);
+  HDPM_LAUNCH(k_pool_seg, dim3((unsigned)sp.nchunks), dim3(256), 0, s, a);
+  HDPM_LAUNCH(k_pool_seg_group, dim3((unsigned)sp.ngroups), dim3(256), 0, s, a);
+  HDPM_LAUNCH(k_pool_seg_top, dim3(1), dim3(64), 0, s, a);
+  HDPM_LAUNCH(k_pool_seg_fill, dim3((unsigned)((sp.ngroups + 255) / 256)), dim3(256), 0, s, a);
+  HDPM_LAUNCH(k_pool_seg_emit, dim3((unsigned)((sp.nchunks + 255) / 256)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_pool_values(const PoolValueArgs& a, hipStream_t s) {
   const int64_t blocks = (a.P + 3) / 4;
   const size_t lds = 512 * 8 + (size_t)4 * 3 * a.d * 8;
-  hipLaunchKernelGGL(k_pool_values, dim3((unsigned)blocks), dim3(256), lds, s, a);
+  HDPM_LAUNCH(k_pool_values, dim3((unsigned)blocks), dim3(256), lds, s, a);
   return hipGetLastError();
 }
 
