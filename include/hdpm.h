@@ -262,6 +262,11 @@ int hdpm_get_pool_heads(hdpm_ctx* ctx, uint64_t* out, int64_t P);
  * compare / select (k_exact_rows_lanes), 3 a thread per point with level-indexed tables
  * (k_exact_rows_lv) -- where the state fits it.  Same chain either way. */
 #define HDPM_OPT_EXACT_KERNEL 6
+/* HDPM_OPT_LAT_NEGLIGIBLE (testing): the margin (>= 40, default 40) below the best cluster under
+ * which a latent entry kept as a head bound by the exact rows counts as probability 0 in a draw;
+ * above it the draw computes the latent's exact sum.  A large value sends every such latent to
+ * the exact sum (the fallback path).  Same chain either way. */
+#define HDPM_OPT_LAT_NEGLIGIBLE 7
 int hdpm_set_option(hdpm_ctx* ctx, int32_t option, double value);
 /* Posterior analysis (realdata_analysis/zoo_simulator.R:193-236, 339-344; mcclust /
  * mcclust.ext).  hdpm_psm_build: the posterior similarity matrix of M saved label vectors

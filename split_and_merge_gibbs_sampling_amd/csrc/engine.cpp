@@ -797,6 +797,7 @@ struct Ctx {
   DevBuf<int> d_fpg;                   // k_resolve_fpg's cross-workgroup scratch
   DevBuf<int> d_wide_ctr;              // k_prepass_wide's chunk counter, k_exact_rows_mass's point counter
   DevBuf<int> d_warm;                  // zero gate word and scratch of warm_launch_kernels
+  DevBuf<unsigned int> d_lmask;        // per exact row: latent columns holding head bounds
   bool kernels_warm = false;
   int fpg_grid_cache[65] = {0};        // its resident grid per resolver slot capacity (0: unknown, -1: none)
   int fpg_grid_m = -1;                 // ... for this m (the LDS of k_resolve_fpg depends on m)
@@ -841,6 +842,7 @@ struct Ctx {
   bool fpg_skip = false;
   int last_xpath = 0;                  // the exact-rows kernel of the last launch (launch_exact_rows' path)
   int exact_pref = 0;                  // HDPM_OPT_EXACT_KERNEL (testing)
+  double lat_negl = kLatNegligible;    // HDPM_OPT_LAT_NEGLIGIBLE (testing)
   bool deep_ok = false;                // set by iteration(): the next sweep may be enqueued ahead
   static constexpr size_t kCtlInts = 16;
   static_assert(sizeof(ResolveCtl) <= kCtlInts * sizeof(int), "control block");
@@ -2038,6 +2040,14 @@ struct Ctx {
     }();
     return on;
   }
+  // HDPM_LAT_BOUND=0: every latent column exact in the level-table rows (A/B)
+  static bool lat_bound_on() {
+    static const bool on = [] {
+      const char* e = std::getenv("HDPM_LAT_BOUND");
+      return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+  }
   static bool lv_spec_on() {
     static const bool on = [] {
       const char* e = std::getenv("HDPM_LV_SPEC");
@@ -2121,7 +2131,8 @@ struct Ctx {
     const bool fp_next = fp_eligible(K + m, std::min(scap, nslots + 2)) &&
                          (el < 0 || el >= kFpMinListed || (debug & 33554432));
     const bool many_exact = last_exact >= kResolveBlkMin && (!fp_next || (debug & 16777216));
-    pa.dmax2 = ((debug & (1 | 262144)) || last_unsettled || many_exact || dense_list) ? INFINITY : 2.0 * dmax;
+    pa.dmax2_ref = ((debug & (1 | 262144)) || last_unsettled || many_exact) ? INFINITY : 2.0 * dmax;
+    pa.dmax2 = dense_list ? INFINITY : pa.dmax2_ref;
     if (dense_list && !pg && part != kRoundResolve) stats.dense_launches++;
     pa.L = d_L.p; pa.rowpos = d_rowpos.p; pa.margin = d_margin.p; pa.list = d_list.p; pa.cnt = d_cnt.p;
     pa.dense = d_dense.p; pa.dense_total = d_dense_total.p; pa.boff = d_boff.p;
@@ -2131,6 +2142,13 @@ struct Ctx {
     // (with the level-table exact rows the snapshot draws are made behind the rows by
     // k_snap_draws, a thread per point, also for dense launches; HDPM_LV_SPEC=0: not there)
     pa.spec_lv = lv_spec_on() ? 1 : 0;
+    // latents far below the clusters kept as head bounds by the level-table exact rows; only
+    // for the fixed-point resolvers (their draws and the serial path take the bounds,
+    // kernels.hip latent_fix), with pool-entry heads
+    pa.lbound = (fp_next && pa.pool_head && m <= 32 && lat_bound_on()) ? 1 : 0;
+    d_lmask.ensure((size_t)((n + kBlock - 1) / kBlock) * kBlock);
+    pa.lmask = d_lmask.p;
+    pa.lat_negl = lat_negl;
     pa.exact_pref = exact_pref;
     // a dense launch needs no bounds: its list is every point (k_dense_list)
     pa.dense_direct = dense_list && dense_direct_on() ? 1 : 0;
@@ -2226,6 +2244,10 @@ struct Ctx {
     ra.fpg_buf = nullptr;
     // (k_snap_draws, behind the level-table exact rows, counted them)
     ra.uncertain = (pa.dense_direct && pa.spec && last_xpath == 3) ? d_wide_ctr.p + 2 : nullptr;
+    ra.lmask = (pa.lbound && last_xpath == 3) ? d_lmask.p : nullptr;
+    ra.codes_t = d_codes_t.p;
+    ra.lat_negl = lat_negl;
+    ra.nq = nq;
     ra.fpg_limit = fpg_limit_ticks;
     ra.fpg_fail = fpg_fail_at;
     const bool fpg_skipped = fpg_skip && part != kRoundPrefix;
@@ -4736,6 +4758,11 @@ int hdpm_set_option(hdpm_ctx* h, int32_t option, double value) {
       if (value < 0.0 || value > 3.0) { ctx->err = "exact kernel: 0 auto, 1 mass, 2 lanes, 3 level tables"; return HDPM_E_ARG; }
       GUARD(ctx->cancel_ahead();)
       ctx->exact_pref = (int)value;
+      return HDPM_OK;
+    case HDPM_OPT_LAT_NEGLIGIBLE:
+      if (!(value >= 40.0)) { ctx->err = "latent negligibility margin must be >= 40"; return HDPM_E_ARG; }
+      GUARD(ctx->cancel_ahead();)
+      ctx->lat_negl = value;
       return HDPM_OK;
     case HDPM_OPT_PIPE_WAIT_US:
       if (value == 0.0 || !std::isfinite(value)) { ctx->err = "pipe wait limit must be non-zero"; return HDPM_E_ARG; }

@@ -73,6 +73,29 @@ __device__ __forceinline__ int64_t pick_entry(uint32_t y, int64_t P) {
   return (int64_t)((int)((double)(int)P * raw_to_unif(y) + 1)) - 1;
 }
 
+// Latent entries far below the point's clusters (k_exact_rows_lv, lbound).  A latent whose
+// log-weight is at least 40 below the best cluster's changes no draw whatever its exact value:
+// its exp(v - max) < 2^-57 of the partial sum it is added to (the clusters come first in index
+// order, n8:95-96), so sum(probs), FixupProb's sum and every other probability keep their bits,
+// and it sorts behind entries whose cumulative sum reaches 1 - E 2^-52 > the largest uniform
+// (1 - 2^-33): it can be taken as -inf (probability 0).  The exact rows store such a latent's
+// head bound (kLatMargin below, which covers a snapshot draw's radius cap kSpecRadCap twice) and
+// flag it; a reader that finds it no longer 40 below computes the exact sum (latent_exact).
+constexpr double kLatMargin = 56.0;
+constexpr double kSpecRadCap = 8.0;
+// n8:47-49 for one latent entry, attribute order (bit-exact with the exact-rows sums); one lane
+__device__ __noinline__ double latent_exact(const uint8_t* codes_t, int nq, int D, const uint8_t* pcodes,
+                                            const double* ptab, int64_t i, int64_t pe) {
+  const uint8_t* cc = pcodes + pe * (int64_t)(nq * 16);
+  const double* tl = ptab + pe * 2 * (int64_t)D;
+  double acc = 0.0;
+  for (int j = 0; j < D; ++j) {
+    const uint8_t x = codes_t[tiled_offset(i, j, nq)];
+    acc += tl[2 * j + (x != cc[j] ? 1 : 0)];
+  }
+  return acc;
+}
+
 __device__ __forceinline__ int a_code(const uint8_t* codes_t, int64_t i, int j, int nq) {
   return codes_t[tiled_offset(i, j, nq)];
 }
@@ -219,6 +242,51 @@ __device__ __forceinline__ uint64_t ldw(const uint64_t* p) {
 }
 
 __device__ __forceinline__ double as_f64(uint64_t u) { return __longlong_as_double((long long)u); }
+
+// Upper bound on latent entry pe's ll for point i from its pool-entry head (kernels.hpp
+// "Pool-entry heads"; the prepass's latent bound), one lane
+__device__ __forceinline__ double latent_head_ub(const PrepassArgs& a, int64_t i, int64_t pe) {
+  const int W = a.wb * a.Ws, HS = head_stride(a.wb, a.Ws);
+  const uint64_t* h = a.pool_head + pe * HS;
+  int H = 0;
+  for (int w = 0; w < a.Ws; ++w) {
+    uint64_t m = 0;
+    for (int b = 0; b < a.wb; ++b) m |= a.xbs[packed_offset(i, b * a.Ws + w, W)] ^ h[b * a.Ws + w];
+    H += __popcll(m);
+  }
+  const uint64_t p0 = h[W], p1 = h[W + 1];
+  const double A = (double)__uint_as_float((uint32_t)p0), dmn = (double)__uint_as_float((uint32_t)(p0 >> 32));
+  const double sa = (double)__uint_as_float((uint32_t)p1), sb = (double)__uint_as_float((uint32_t)(p1 >> 32));
+  double low = dmn * (double)H;
+  if (H >= a.head_ha) low = fmax(low, sa + dmn * (double)(H - a.head_ha));
+  if (H >= a.head_hb) low = fmax(low, sb + dmn * (double)(H - a.head_hb));
+  return A - low + kBoundEps * (1.0 + fabs(A) + low);
+}
+
+// A draw's log-weights v[0..E) (clusters, then latents) whose latent columns flagged in lmv hold
+// head bounds: each such latent is -inf (probability 0) while its bound is kLatNegligible below
+// the best cluster, else its exact sum (latent_exact).  Latent 0 of a singleton is the point's
+// own cluster (n8:65-75), never flagged.
+template <int EM>
+__device__ __forceinline__ void latent_fix(const uint8_t* codes_t, int nq, int D, ParamTables pool,
+                                           const uint32_t* raw, int64_t P, double logfac, double (&v)[EM], int K,
+                                           int E, unsigned int lmv, bool single, int64_t i, int m, double negl) {
+  double mxc = -INFINITY;
+#pragma unroll
+  for (int e = 0; e < EM; ++e) mxc = e < K ? fmax(mxc, v[e]) : mxc;
+#pragma unroll
+  for (int e = 0; e < EM; ++e) {
+    const int l = e - K;
+    if (e >= K && e < E && ((lmv >> l) & 1u) && !(l == 0 && single)) {
+      if (v[e] <= mxc - negl) {
+        v[e] = -INFINITY;
+      } else {
+        const int64_t pe = pick_entry(raw[i * (m + 1) + l], P);
+        v[e] = logfac + latent_exact(codes_t, nq, D, pool.codes, pool.tab, i, pe);
+      }
+    }
+  }
+}
 
 // Mismatch mask M (one bit per attribute) of bit-sliced rows x and record codes, and H.
 template <int WB, int WS, bool U>
@@ -1764,6 +1832,12 @@ __device__ __forceinline__ bool RCtx::process(int64_t i, int row, int own, uint3
     if (!rowp) {
       const double* src = a.L + (int64_t)row * ncol;
       for (int c = lane; c < ncol; c += kWave) st.row[c] = src[c];
+      if (a.lmask) {       // latent columns holding head bounds: their exact sums (latent_exact)
+        const unsigned int lmv = a.lmask[row];
+        if (lane < a.m && ((lmv >> lane) & 1u))
+          st.row[a.S + lane] = latent_exact(a.codes_t, a.nq, a.d, a.pool.codes, a.pool.tab, i,
+                                            pick_entry(a.raw[i * (a.m + 1) + lane], a.P));
+      }
       wave_sync();
       rowp = st.row;
     }
@@ -2852,6 +2926,11 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
           }
 #pragma unroll
           for (int e = 0; e < EM; ++e) v[e] = e < K ? v[e] + x[e] : a.logfac + x[e];
+          if (a.lmask) {
+            const unsigned int lmv = gld(a.lmask + r.x);
+            if (lmv) latent_fix<EM>(a.codes_t, a.nq, a.d, a.pool, a.raw, a.P, a.logfac, v, K, E, lmv, single, r.y, a.m,
+                                    a.lat_negl);
+          }
           np = fp_draw<EM>(v, E, rU, F->etab);
           fresh = true;
         }
@@ -3651,16 +3730,25 @@ __global__ __launch_bounds__(kLvThreads) void k_exact_rows_lv(PrepassArgs a) {
     }
     vt[q] = v;
   }
-  if (threadIdx.x < K) s_col[threadIdx.x] = a.slot_of_label[threadIdx.x];
+  __shared__ double s_l0[kWave], s_l1[kWave];    // the launch's log-counts (latent bounds)
+  if (threadIdx.x < K) {
+    const int sl = a.slot_of_label[threadIdx.x], c = a.counts[sl];
+    s_col[threadIdx.x] = sl;
+    s_l1[threadIdx.x] = a.logn[c];
+    s_l0[threadIdx.x] = c > 0 ? a.logn[c - 1] : -INFINITY;
+  }
   __syncthreads();
   const int total = *a.dense_total;
   const int stride = gridDim.x * blockDim.x;
+  const bool lb = a.lbound && a.lmask && a.pool_head && m <= 32;
   for (int q0 = blockIdx.x * blockDim.x; q0 < total; q0 += stride) {
     const int q = q0 + threadIdx.x;
     const bool on = q < total;
     const int4 r = on ? a.rq[q] : make_int4(0, 0, 0, 0);
     const int64_t i = r.y;
+    const int own = r.z;
     double* Lr = a.L + (int64_t)r.x * (a.S + m);
+    double mxc = -INFINITY;         // the best cluster log-weight in the launch's state (n8:40-92)
     uint32_t xw[4 * kLanesMaxNq];
 #pragma unroll
     for (int c = 0; c < kLanesMaxNq; ++c) {
@@ -3702,12 +3790,28 @@ __global__ __launch_bounds__(kLvThreads) void k_exact_rows_lv(PrepassArgs a) {
         }
       }
 #pragma unroll
-      for (int kk = 0; kk < kLvGroup; ++kk)
-        if (on && k0 + kk < K) Lr[s_col[k0 + kk]] = acc[kk];
+      for (int kk = 0; kk < kLvGroup; ++kk) {
+        const int k = k0 + kk;
+        if (k < K) {
+          const int sl = s_col[k];
+          if (on) Lr[sl] = acc[kk];
+          mxc = fmax(mxc, (sl == own ? s_l0[k] : s_l1[k]) + acc[kk]);
+        }
+      }
     }
     const uint32_t* raw = a.raw + i * (m + 1);
+    unsigned int lm = 0;
     for (int u = 0; u < m; ++u) {
       const int64_t pe = on ? pick_entry(raw[u], a.P) : 0;
+      if (lb && on) {
+        // far below the clusters: its head bound stands for it (latent_exact's readers)
+        const double ub = latent_head_ub(a, i, pe);
+        if (a.logfac + ub <= mxc - kLatMargin) {
+          Lr[a.S + u] = ub;
+          lm |= 1u << u;
+          continue;
+        }
+      }
       const uint8_t* cc = a.pool.codes + pe * dp;
       const double* tl = a.pool.tab + pe * 2 * D;
       double acc = 0.0;
@@ -3728,6 +3832,7 @@ __global__ __launch_bounds__(kLvThreads) void k_exact_rows_lv(PrepassArgs a) {
       }
       if (on) Lr[a.S + u] = acc;
     }
+    if (lb && on) a.lmask[r.x] = lm;
   }
 }
 
@@ -3777,15 +3882,22 @@ __global__ __launch_bounds__(256) void k_snap_draws(PrepassArgs a) {
         v[e] = -INFINITY;
       }
     }
-    // the prepass's margin test (kernels.hip k_prepass: the own cluster ahead of every other
-    // entry by thresh), here on exact values: what a launch with the prepass would have listed
-    const bool unc = !(own_cnt >= 2 && vo - mo > a.thresh_ref);
+    // the prepass's tests (prepass_finish: the own cluster ahead of every other entry by
+    // thresh, or by a margin the draw's uniform certifies), here on exact values: what a
+    // launch with the prepass would have listed
+    const double mg = vo - mo;
+    const bool unc = !(own_cnt >= 2 && (mg > a.thresh_ref || stay_by_uniform(mg - a.dmax2_ref, (uint32_t)r.w, E)));
     const unsigned long long ub = __ballot(unc);
     if ((threadIdx.x & 63) == 0 && ub && a.wide_ctr) atomicAdd(a.wide_ctr + 2, __popcll(ub));
+    if (a.lmask) {
+      const unsigned int lmv = a.lmask[r.x];
+      if (lmv) latent_fix<EM>(a.codes_t, a.nq, a.d, a.pool, a.raw, a.P, a.logfac, v, K, E, lmv, single, r.y, m, a.lat_negl);
+    }
     double rad = 0.0;
     const int pick = fp_draw<EM, true>(v, E, raw_to_unif((uint32_t)r.w), etab, &rad);
     a.spec[q] = pick >= 0 ? pick : -1;
-    a.spec_rad[q] = pick >= 0 ? rad : 0.0;
+    // (capped: a kept draw's latents stay kLatNegligible below the clusters, kernels.hip kLatMargin)
+    a.spec_rad[q] = pick >= 0 ? fmin(rad, kSpecRadCap) : 0.0;
   }
 }
 
@@ -3831,6 +3943,13 @@ static hipError_t launch_snap_draws(const PrepassArgs& a, hipStream_t s) {
 hipError_t launch_exact_rows(const PrepassArgs& a0, int nblocks, hipStream_t s, int* path) {
   if (path) *path = 0;
   PrepassArgs a = a0;
+  // latent bounds only from the level-table kernel (below); every other kernel writes exact
+  // columns, and the snapshot draws then read no flags
+  if (!a.lbound || !a.pool_head || a.m > 32) a.lbound = 0;
+  PrepassArgs an = a;
+  an.lmask = nullptr;
+  an.lbound = 0;
+  if (!a.lbound) a.lmask = nullptr;
   a.lblock = prepass_list_block(a);
   a.nlb = (a.n - a.p0 + a.lblock - 1) / a.lblock;
   const int E = a.K + a.m;
@@ -3878,7 +3997,7 @@ hipError_t launch_exact_rows(const PrepassArgs& a0, int nblocks, hipStream_t s, 
       llds <= 64 * 1024 && !want_mass) {
     HDPM_LAUNCH(k_exact_rows_lanes, dim3(lanes_grid(llds)), dim3(256), llds, s, a);
     if (path) *path = 2;
-    return launch_snap_draws(a, s);
+    return launch_snap_draws(an, s);
   }
   if (a.exact_scan && !a.exact_wave && E <= kWave && mlds <= 96 * 1024) {
     static const int mstatic = [] {

@@ -163,11 +163,22 @@ struct PrepassArgs {
   int dense_direct;          // 1: every point listed by k_dense_list (no prepass, no list scan)
   int exact_pref;            // testing (HDPM_OPT_EXACT_KERNEL): 0 auto, 1 k_exact_rows_mass, 2 _lanes, 3 _lv
   double thresh_ref;         // the prepass's margin threshold (k_snap_draws counts the points it would list)
+  double dmax2_ref;          // ... and its drift allowance of the uniform test (+inf: margins only)
+  // latent bounds (k_exact_rows_lv with lbound): a latent entry whose head bound puts it at
+  // least kLatMargin below the point's best cluster gets that bound in its L column instead of
+  // the exact sum, and bit u of lmask[row] set (readers: kernels.hip latent_value_fix)
+  int lbound;
+  unsigned int* lmask;       // [row] bounded latent columns (nullptr: none)
+  double lat_negl;           // a bounded latent counts as -inf this far below the best cluster (kLatNegligible)
   // pipelined iterations (engine.cpp iterations_pipelined): the kernels run only while *gate
   // is set, and read the sweep's draws from *raw_ptr (a position found on the device)
   const int* gate;
   const uint32_t* const* raw_ptr;
 };
+
+// A latent entry kept as a head bound counts as probability 0 this far below the best
+// cluster (kernels.hip latent_fix; the default of PrepassArgs / ResolveArgs::lat_negl)
+constexpr double kLatNegligible = 40.0;
 
 // A sweep's kernels in a pipeline read `raw` from the device (pipe_gate); false: skip.
 // The gate word is read with a vector load, so the compiler takes its value as divergent and
@@ -286,6 +297,10 @@ struct ResolveArgs {
   int fpg;
   int* fpg_buf;
   const int* uncertain;      // dense launches: k_snap_draws' count of would-be-listed points (or nullptr)
+  const unsigned int* lmask; // [row] latent columns of L holding head bounds, not exact sums (or nullptr)
+  const uint8_t* codes_t;    // the data (tiled codes): exact latent sums for bounded columns
+  int nq;
+  double lat_negl;           // as PrepassArgs::lat_negl
   long long fpg_limit;       // a grid barrier gives up after this many wall_clock64 ticks (100 MHz)
   int fpg_fail;              // testing: workgroup 0 gives up at its fpg_fail-th grid barrier (0: never)
 };

@@ -460,6 +460,11 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
           }
 #pragma unroll
           for (int e = 0; e < EM; ++e) v[e] = e < K ? v[e] + x[e] : a.logfac + x[e];
+          if (a.lmask) {
+            const unsigned int lmv = gld(a.lmask + r.x);
+            if (lmv) latent_fix<EM>(a.codes_t, a.nq, a.d, a.pool, a.raw, a.P, a.logfac, v, K, E, lmv, single, r.y, a.m,
+                                    a.lat_negl);
+          }
           np = fp_draw<EM>(v, E, rU, F->etab);
           fresh = true;
         }

@@ -228,6 +228,11 @@ class Engine:
         thread per point, 3 level-indexed tables."""
         self._check(self._L.hdpm_set_option(self._h, _lib.OPT_EXACT_KERNEL, float(which)))
 
+    def set_lat_negligible(self, margin: float):
+        """Testing (include/hdpm.h HDPM_OPT_LAT_NEGLIGIBLE): the margin under which a latent
+        kept as a head bound counts as probability 0 (>= 40; larger: exact sums instead)."""
+        self._check(self._L.hdpm_set_option(self._h, _lib.OPT_LAT_NEGLIGIBLE, float(margin)))
+
     def set_hig_logspace(self, on: bool = True):
         """Extension beyond the reference (include/hdpm.h HDPM_OPT_HIG_LOGSPACE): finite HIG
         log-densities for clusters whose 2F1 series overflows (the reference throws)."""

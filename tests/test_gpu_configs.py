@@ -172,14 +172,20 @@ def test_c2_full_size_unconverged_starts(hd, oracle, L, debug):
 
 
 @pytest.mark.timeout(900)
-def test_c5_full_size_random20_start(hd, oracle):
+# lat: the margin under which a latent kept as a head bound by the level-table exact rows counts
+# as probability 0 (kernels.hip latent_fix); 1e9 sends every such latent to its exact sum
+@pytest.mark.parametrize("lat", [None, 1e9])
+def test_c5_full_size_random20_start(hd, oracle, lat):
     """C5 from a random assignment to 20 labels (la:31, the scripts' L = 20): every point is
-    uncertain in the first sweeps, the resolver's block mode decides them."""
+    uncertain in the first sweeps; dense launches list every point, the level-table exact rows
+    keep far-below latents as head bounds, the device-wide resolver decides them."""
     from split_and_merge_gibbs_sampling_amd.data import config
     ds = config("c5")
     eng = hd.Engine(0)
     eng.set_data(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w)
     eng.set_seed(6)
+    if lat:
+        eng.set_lat_negligible(lat)
     params = eng.chain_params(m=3, iterations=1, L=20, burnin=0, neal8=True, split_merge=False)
     eng.init_chain(params, c_i=None)
     c, cen, sig = eng.get_state()
@@ -189,7 +195,8 @@ def test_c5_full_size_random20_start(hd, oracle):
     neal8_steps(eng, oracle, ds, ost, rng, pc, ps, sweeps=2)
     st = eng.stats()
     assert st["moves"] > 100_000
-    assert st["fpg_launches"] > 0, st     # the device-wide fixed-point resolver decided the second sweep
+    assert st["fpg_launches"] > 0, st     # the device-wide fixed-point resolver decided the sweeps
+    assert st["dense_launches"] > 0, st
     eng.close()
 
 
@@ -336,4 +343,30 @@ def test_c2_unconverged_many_latents(hd, oracle, kernel):
         same(eng, ost, rng, f"update_phi {k}")
     st = eng.stats()
     assert st["exact_mass_launches" if kernel == 1 else "exact_lanes_launches"] > 0, st
+    eng.close()
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("lat", [40.0, 1e9])
+def test_c2_latent_bounds(hd, oracle, lat):
+    """C2 from a random L = 20 start with the level-table exact rows and latent head bounds:
+    at the default margin (40) a bounded latent counts as probability 0, at 1e9 every bounded
+    latent is summed exactly when a draw reads it (kernels.hip latent_fix / latent_exact, in the
+    snapshot draws, both fixed-point resolvers and the serial path)."""
+    from split_and_merge_gibbs_sampling_amd.data import config
+    ds = config("c2")
+    eng = hd.Engine(0)
+    eng.set_data(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w)
+    eng.set_seed(12)
+    eng.set_exact_kernel(3)
+    eng.set_lat_negligible(lat)
+    params = eng.chain_params(m=3, iterations=1, L=20, burnin=0, neal8=True, split_merge=False)
+    eng.init_chain(params, c_i=None)
+    c, cen, sig = eng.get_state()
+    pc, ps = eng.get_pool(ds.n * 3)
+    ost = oracle.OracleState(c, cen.shape[0], cen, sig, cap=8192)
+    rng = eng.rng_state.copy()
+    eng.reset_stats()
+    neal8_steps(eng, oracle, ds, ost, rng, pc, ps, sweeps=4)
+    assert eng.stats()["exact_lanes_launches"] > 0
     eng.close()
