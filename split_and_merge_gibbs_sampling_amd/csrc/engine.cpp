@@ -2032,6 +2032,13 @@ struct Ctx {
     const size_t mass_lds = (size_t)K * 2 * d * 8 + (size_t)8 * m * d * 8 + (size_t)K * nq * 16 + (size_t)8 * nq * 16;
     return (nq <= 8 && K <= 64 && lanes_lds <= 64 * 1024) || mass_lds <= 96 * 1024;
   }
+  static bool fp_unsettled_unif() {
+    static const bool on = [] {
+      const char* e = std::getenv("HDPM_FP_UNSETTLED_UNIF");
+      return e && std::atoi(e) == 1;
+    }();
+    return on;
+  }
   // HDPM_DENSE_DIRECT=0: dense launches still run the prepass (A/B)
   static bool dense_direct_on() {
     static const bool on = [] {
@@ -2131,7 +2138,10 @@ struct Ctx {
     const bool fp_next = fp_eligible(K + m, std::min(scap, nslots + 2)) &&
                          (el < 0 || el >= kFpMinListed || (debug & 33554432));
     const bool many_exact = last_exact >= kResolveBlkMin && (!fp_next || (debug & 16777216));
-    pa.dmax2_ref = ((debug & (1 | 262144)) || last_unsettled || many_exact) ? INFINITY : 2.0 * dmax;
+    // (HDPM_FP_UNSETTLED_UNIF=1: the fixed-point resolvers keep the uniform's certification after
+    // an unsettled launch too -- A/B)
+    const bool unsettled_margins = last_unsettled && !(fp_next && fp_unsettled_unif());
+    pa.dmax2_ref = ((debug & (1 | 262144)) || unsettled_margins || many_exact) ? INFINITY : 2.0 * dmax;
     pa.dmax2 = dense_list ? INFINITY : pa.dmax2_ref;
     if (dense_list && !pg && part != kRoundResolve) stats.dense_launches++;
     pa.L = d_L.p; pa.rowpos = d_rowpos.p; pa.margin = d_margin.p; pa.list = d_list.p; pa.cnt = d_cnt.p;

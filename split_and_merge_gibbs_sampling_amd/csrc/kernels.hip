@@ -2498,7 +2498,9 @@ struct FpShared {
   int wc[kFpWaves][kWave];          // slot counts at each wave's first point
   int wd[kFpWaves][kWave];          // each wave's net count change per slot
   double wsd[kFpWaves];
-  int wstop[kFpWaves], wchg[kFpWaves], wmov[kFpWaves], wfresh[kFpWaves];
+  int wstop[kFpWaves], wchg[kFpWaves], wmov[kFpWaves], wfresh[kFpWaves], wneed[kFpWaves];
+  int dlist[kFpThreads];            // chunk positions whose draw is made this round (compacted)
+  int dpick[kFpThreads];            // ... and their picks
   long long wev[kFpWaves];          // diagnostics: each wave's evaluation ticks in a round
   uint64_t etab[256];               // glibc's exp table (fp_draw)
   int cmo[kWave];                   // moves out of each slot in the chunk
@@ -2702,6 +2704,71 @@ __device__ int fp_draw(double (&v)[EM], int E, double rU, const uint64_t* etab, 
   return kFpFallback;
 }
 
+// The draw of chunk position t (a point whose snapshot draw does not hold) in the state the
+// round gives it -- the counts at its wave's first point plus the moves before it in its wave
+// (ballot masks), n8:40-102 -- made by whichever lane the round's compacted list assigns it:
+// the positions that draw are gathered into dense waves first, so a wave with one drawing lane
+// no longer runs fp_draw for all 64 (the fixed-point resolvers' rounds, k_resolve_fp / _fpg).
+template <int EM>
+__device__ __forceinline__ int fp_draw_at(const ResolveArgs& a, const RState& st, FpShared* F, int t, int4 r, int K,
+                                          int E, int ncol) {
+  const int w = t >> 6;
+  const unsigned long long bl = (1ull << (t & 63)) - 1ull;
+  const int own = r.z;
+  auto corr = [&](int sl) -> int { return __popcll(F->bin[w][sl] & bl) - __popcll(F->bout[w][sl] & bl); };
+  const int cnow = F->wc[w][own] + corr(own);
+  const bool single = cnow == 1;
+  int sl[EM];
+  double v[EM], x[EM];
+#pragma unroll
+  for (int e = 0; e < EM; ++e) {
+    const int s = st.sol[e < K ? e : 0];
+    sl[e] = s;
+    const int c = F->wc[w][s] + corr(s) - (s == own ? 1 : 0);                  // n8:40-92
+    v[e] = gld(a.logn + ((e < K && c > 0) ? c : 0));
+  }
+  const double* Lr = a.L + (int64_t)r.x * ncol;
+#pragma unroll
+  for (int e = 0; e < EM; ++e) {
+    const int l = e - K;
+    const int col = e < K ? sl[e] : (e < E ? ((l == 0 && single) ? own : a.S + l) : 0);
+    x[e] = gld(Lr + col);
+  }
+#pragma unroll
+  for (int e = 0; e < EM; ++e) v[e] = e < K ? v[e] + x[e] : a.logfac + x[e];
+  if (a.lmask) {
+    const unsigned int lmv = gld(a.lmask + r.x);
+    if (lmv) latent_fix<EM>(a.codes_t, a.nq, a.d, a.pool, a.raw, a.P, a.logfac, v, K, E, lmv, single, r.y, a.m,
+                            a.lat_negl);
+  }
+  return fp_draw<EM>(v, E, raw_to_unif((uint32_t)r.w), F->etab);
+}
+
+// Every thread of the workgroup: positions with `need` set get their draws made in dense waves
+// (fp_draw_at); returns this thread's pick (or -1 without need).
+template <int EM>
+__device__ __forceinline__ int fp_draws_compacted(const ResolveArgs& a, const RState& st, FpShared* F, bool need,
+                                                  int q0, int K, int E, int ncol) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const unsigned long long nb = __ballot(need);
+  if (lane == 0) F->wneed[wv] = __popcll(nb);
+  __syncthreads();
+  int base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kFpWaves; ++w) {
+    base += w < wv ? F->wneed[w] : 0;
+    tot += F->wneed[w];
+  }
+  if (need) F->dlist[base + __popcll(nb & ((1ull << lane) - 1ull))] = tid;
+  __syncthreads();
+  for (int k = tid; k < tot; k += kFpThreads) {
+    const int t = F->dlist[k];
+    F->dpick[t] = fp_draw_at<EM>(a, st, F, t, gld(a.rq + q0 + t), K, E, ncol);
+  }
+  __syncthreads();
+  return need ? F->dpick[tid] : -1;
+}
+
 // Unlisted points in [lo, hi) re-tested as RCtx::verify does, each against the drift after
 // the chunk positions before it (dnl[k] for the last position k < nk with pi[k] < j, dn0
 // before any) and the count bounds cmin.  All threads; returns the first failing point
@@ -2858,6 +2925,8 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
       // before its values are used.
       bool changed = false;
       long long tdraw = 0;
+      bool ev2 = false, need = false;   // evaluated in full this round; its draw is made this round
+      int cnow2 = 0;
       const bool evl = in && tid > chg && tid <= fs;
       const double wdb = (struct0 && a.spec) ? fp_wave_drift_bound(a, st, F->wc[wv], F->bin[wv], F->bout[wv], nsl)
                                              : INFINITY;
@@ -2882,8 +2951,8 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
         co = cnow;
         ct = ctn;
       } else if (evl) {
-        const int cnow = F->wc[wv][own] + corr(own);
-        const bool single = cnow == 1;
+        ev2 = true;
+        cnow2 = F->wc[wv][own] + corr(own);
         int sl[EM], cc[EM];
         double v[EM];
 #pragma unroll
@@ -2904,37 +2973,29 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
             const int a0 = st.snap[s];
             const double b1 = st.sl1[s], b0 = st.sl0[s];
             const int c = cc[e];
-            const double d_own = a0 == cnow ? 0.0 : ((a0 >= 2 && cnow >= 2) ? fabs(v[e] - b0) : INFINITY);
+            const double d_own = a0 == cnow2 ? 0.0 : ((a0 >= 2 && cnow2 >= 2) ? fabs(v[e] - b0) : INFINITY);
             const double d_oth = a0 == c ? 0.0 : ((a0 < 1 || c < 1) ? INFINITY : fabs(v[e] - b1));
             drift = fmax(drift, e < K ? (s == own ? d_own : d_oth) : 0.0);
           }
           take_spec = drift == 0.0 || drift < sr;
         }
+        need = !take_spec;
+      }
+      // the draws of this round, compacted into dense waves (fp_draws_compacted)
+      const long long td0 = prof ? wall_clock64() : 0;
+      const int dpk = fp_draws_compacted<EM>(a, st, F, need, q0, K, E, ncol);
+      if (ev2) {
+        const int cnow = cnow2;
+        const bool single = cnow == 1;
         int np;
-        const long long td0 = prof ? wall_clock64() : 0;
-        if (take_spec) {
+        if (!need) {
           np = sp;
           fresh = false;
         } else {
-          const double* Lr = a.L + (int64_t)r.x * ncol;
-          double x[EM];
-#pragma unroll
-          for (int e = 0; e < EM; ++e) {
-            const int l = e - K;
-            const int col = e < K ? sl[e] : (e < E ? ((l == 0 && single) ? own : a.S + l) : 0);
-            x[e] = gld(Lr + col);
-          }
-#pragma unroll
-          for (int e = 0; e < EM; ++e) v[e] = e < K ? v[e] + x[e] : a.logfac + x[e];
-          if (a.lmask) {
-            const unsigned int lmv = gld(a.lmask + r.x);
-            if (lmv) latent_fix<EM>(a.codes_t, a.nq, a.d, a.pool, a.raw, a.P, a.logfac, v, K, E, lmv, single, r.y, a.m,
-                                    a.lat_negl);
-          }
-          np = fp_draw<EM>(v, E, rU, F->etab);
+          np = dpk;
           fresh = true;
         }
-        if (prof) tdraw = wall_clock64() - td0;
+        if (prof && need) tdraw = wall_clock64() - td0;
         int ncl = 2, nt = own;
         if (np >= 0) {
           if (np < K) {

@@ -394,6 +394,8 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
       };
       // (4) redraw behind the first changed outcome (k_resolve_fp's evaluation)
       bool changed = false;
+      bool ev2 = false, need = false;
+      int cnow2 = 0;
       const bool evl = active && in && tid > chg && tid <= fs;
       const double wdb = (struct0 && a.spec) ? fp_wave_drift_bound(a, st, F->wc[wv], F->bin[wv], F->bout[wv], nsl)
                                              : INFINITY;
@@ -418,8 +420,8 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
         co = cnow;
         ct = ctn;
       } else if (evl) {
-        const int cnow = F->wc[wv][own] + corr(own);
-        const bool single = cnow == 1;
+        ev2 = true;
+        cnow2 = F->wc[wv][own] + corr(own);
         int sl[EM], cc[EM];
         double v[EM];
 #pragma unroll
@@ -439,35 +441,21 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
             const int a0 = st.snap[s];
             const double b1 = st.sl1[s], b0 = st.sl0[s];
             const int c = cc[e];
-            const double d_own = a0 == cnow ? 0.0 : ((a0 >= 2 && cnow >= 2) ? fabs(v[e] - b0) : INFINITY);
+            const double d_own = a0 == cnow2 ? 0.0 : ((a0 >= 2 && cnow2 >= 2) ? fabs(v[e] - b0) : INFINITY);
             const double d_oth = a0 == c ? 0.0 : ((a0 < 1 || c < 1) ? INFINITY : fabs(v[e] - b1));
             drift = fmax(drift, e < K ? (s == own ? d_own : d_oth) : 0.0);
           }
           take_spec = drift == 0.0 || drift < sr;
         }
-        int np;
-        if (take_spec) {
-          np = sp;
-          fresh = false;
-        } else {
-          const double* Lr = a.L + (int64_t)r.x * ncol;
-          double x[EM];
-#pragma unroll
-          for (int e = 0; e < EM; ++e) {
-            const int l = e - K;
-            const int col = e < K ? sl[e] : (e < E ? ((l == 0 && single) ? own : a.S + l) : 0);
-            x[e] = gld(Lr + col);
-          }
-#pragma unroll
-          for (int e = 0; e < EM; ++e) v[e] = e < K ? v[e] + x[e] : a.logfac + x[e];
-          if (a.lmask) {
-            const unsigned int lmv = gld(a.lmask + r.x);
-            if (lmv) latent_fix<EM>(a.codes_t, a.nq, a.d, a.pool, a.raw, a.P, a.logfac, v, K, E, lmv, single, r.y, a.m,
-                                    a.lat_negl);
-          }
-          np = fp_draw<EM>(v, E, rU, F->etab);
-          fresh = true;
-        }
+        need = !take_spec;
+      }
+      // the draws of this round, compacted into dense waves (kernels.hip fp_draws_compacted)
+      const int dpk = fp_draws_compacted<EM>(a, st, F, need, cq, K, E, ncol);
+      if (ev2) {
+        const int cnow = cnow2;
+        const bool single = cnow == 1;
+        const int np = need ? dpk : sp;
+        fresh = need;
         int ncl = 2, nt = own;
         if (np >= 0) {
           if (np < K) {
