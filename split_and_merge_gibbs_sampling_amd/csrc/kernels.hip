@@ -2856,7 +2856,7 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
     const int own = r.z;
     const int sp = (in && a.spec) ? gld(a.spec + q0 + tid) : -1;
     const double sr = (in && a.spec) ? gld(a.spec_rad + q0 + tid) : 0.0;
-    const double rU = raw_to_unif((uint32_t)r.w);
+    // (the categorical uniform: fp_draw_at reads it from the record)
     F->pi[tid] = in ? r.y : INT_MAX;
     const int K = S.K, E = K + a.m;
     const bool struct0 = S.nstruct == 0;
