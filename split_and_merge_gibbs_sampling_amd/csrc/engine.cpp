@@ -2035,7 +2035,7 @@ struct Ctx {
   static bool fp_unsettled_unif() {
     static const bool on = [] {
       const char* e = std::getenv("HDPM_FP_UNSETTLED_UNIF");
-      return e && std::atoi(e) == 1;
+      return !(e && std::atoi(e) == 0);
     }();
     return on;
   }
@@ -2138,8 +2138,12 @@ struct Ctx {
     const bool fp_next = fp_eligible(K + m, std::min(scap, nslots + 2)) &&
                          (el < 0 || el >= kFpMinListed || (debug & 33554432));
     const bool many_exact = last_exact >= kResolveBlkMin && (!fp_next || (debug & 16777216));
-    // (HDPM_FP_UNSETTLED_UNIF=1: the fixed-point resolvers keep the uniform's certification after
-    // an unsettled launch too -- A/B)
+    // The fixed-point resolvers keep the uniform's certification after an unsettled launch
+    // (a restart behind a new cluster, a drift past the budget): a point it certified that no
+    // longer holds is re-tested and restarts the launch, which these resolvers do cheaply,
+    // while listing every uncertain point by margin alone cost C2's restart launches ~5x the
+    // points (3,106 vs ~530) and ~300 us each (HDPM_FP_UNSETTLED_UNIF=0: margins only, as the
+    // one-wave resolvers need)
     const bool unsettled_margins = last_unsettled && !(fp_next && fp_unsettled_unif());
     pa.dmax2_ref = ((debug & (1 | 262144)) || unsettled_margins || many_exact) ? INFINITY : 2.0 * dmax;
     pa.dmax2 = dense_list ? INFINITY : pa.dmax2_ref;
