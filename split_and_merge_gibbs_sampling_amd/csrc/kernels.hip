@@ -2769,6 +2769,34 @@ __device__ __forceinline__ int fp_draws_compacted(const ResolveArgs& a, const RS
   return need ? F->dpick[tid] : -1;
 }
 
+// The drift of a point's log-count terms from the snapshot's (n8:40-92: logn[count] per
+// cluster, logn[count - 1] for its own) -- the quantity a snapshot draw's radius bounds -- as an
+// upper bound from float logarithms plus their error (counts < 2^24 are exact in float; each
+// log2 is within a few ulps, < 2e-6 at these magnitudes, so 3e-5 covers the difference).  The
+// radius test needs only a bound, and this spares the EM table loads of the exact terms (the
+// drawing lanes load them, fp_draw_at).
+__device__ __forceinline__ double fdrift(int now, int snap) {
+  if (now == snap) return 0.0;
+  if (now < 1 || snap < 1) return INFINITY;
+  return (double)fabsf(__log2f((float)now) - __log2f((float)snap)) * 0.6931471805599453 + 3e-5;
+}
+template <int EM, class CORR>
+__device__ __forceinline__ double fp_lane_drift(const RState& st, const int* wc, CORR corr, int own, int cnow, int K) {
+  double drift = 0.0;
+#pragma unroll
+  for (int e = 0; e < EM; ++e) {
+    if (e < K) {
+      const int s = st.sol[e];
+      const int a0 = st.snap[s];
+      double d;
+      if (s == own) d = a0 == cnow ? 0.0 : ((a0 >= 2 && cnow >= 2) ? fdrift(cnow - 1, a0 - 1) : INFINITY);
+      else d = fdrift(wc[s] + corr(s), a0);
+      drift = fmax(drift, d);
+    }
+  }
+  return drift;
+}
+
 // Unlisted points in [lo, hi) re-tested as RCtx::verify does, each against the drift after
 // the chunk positions before it (dnl[k] for the last position k < nk with pi[k] < j, dn0
 // before any) and the count bounds cmin.  All threads; returns the first failing point
@@ -2953,30 +2981,10 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fp(ResolveArgs a) {
       } else if (evl) {
         ev2 = true;
         cnow2 = F->wc[wv][own] + corr(own);
-        int sl[EM], cc[EM];
-        double v[EM];
-#pragma unroll
-        for (int e = 0; e < EM; ++e) {
-          const int s = st.sol[e < K ? e : 0];
-          sl[e] = s;
-          cc[e] = F->wc[wv][s] + corr(s) - (s == own ? 1 : 0);     // the count in logn[.] (n8:40-92)
-        }
-#pragma unroll
-        for (int e = 0; e < EM; ++e) v[e] = gld(a.logn + ((e < K && cc[e] > 0) ? cc[e] : 0));   // logn[0] = -inf
+        // the snapshot draw holds while every log-count term drifted less than its radius
         bool take_spec = false;
         if (struct0 && sp >= 0) {
-          // drift of every log-weight from the snapshot's (the draw holds below its radius)
-          double drift = 0.0;
-#pragma unroll
-          for (int e = 0; e < EM; ++e) {
-            const int s = sl[e];
-            const int a0 = st.snap[s];
-            const double b1 = st.sl1[s], b0 = st.sl0[s];
-            const int c = cc[e];
-            const double d_own = a0 == cnow2 ? 0.0 : ((a0 >= 2 && cnow2 >= 2) ? fabs(v[e] - b0) : INFINITY);
-            const double d_oth = a0 == c ? 0.0 : ((a0 < 1 || c < 1) ? INFINITY : fabs(v[e] - b1));
-            drift = fmax(drift, e < K ? (s == own ? d_own : d_oth) : 0.0);
-          }
+          const double drift = fp_lane_drift<EM>(st, F->wc[wv], corr, own, cnow2, K);
           take_spec = drift == 0.0 || drift < sr;
         }
         need = !take_spec;

@@ -422,29 +422,10 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
       } else if (evl) {
         ev2 = true;
         cnow2 = F->wc[wv][own] + corr(own);
-        int sl[EM], cc[EM];
-        double v[EM];
-#pragma unroll
-        for (int e = 0; e < EM; ++e) {
-          const int s = st.sol[e < K ? e : 0];
-          sl[e] = s;
-          cc[e] = F->wc[wv][s] + corr(s) - (s == own ? 1 : 0);
-        }
-#pragma unroll
-        for (int e = 0; e < EM; ++e) v[e] = gld(a.logn + ((e < K && cc[e] > 0) ? cc[e] : 0));
+        // the snapshot draw holds while every log-count term drifted less than its radius
         bool take_spec = false;
         if (struct0 && sp >= 0) {
-          double drift = 0.0;
-#pragma unroll
-          for (int e = 0; e < EM; ++e) {
-            const int s = sl[e];
-            const int a0 = st.snap[s];
-            const double b1 = st.sl1[s], b0 = st.sl0[s];
-            const int c = cc[e];
-            const double d_own = a0 == cnow2 ? 0.0 : ((a0 >= 2 && cnow2 >= 2) ? fabs(v[e] - b0) : INFINITY);
-            const double d_oth = a0 == c ? 0.0 : ((a0 < 1 || c < 1) ? INFINITY : fabs(v[e] - b1));
-            drift = fmax(drift, e < K ? (s == own ? d_own : d_oth) : 0.0);
-          }
+          const double drift = fp_lane_drift<EM>(st, F->wc[wv], corr, own, cnow2, K);
           take_spec = drift == 0.0 || drift < sr;
         }
         need = !take_spec;
@@ -507,7 +488,11 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
     }
     const bool active = g <= gs && nc > 0;
     // ---- the drift after each position: within the chunk, then across the chunks before it
+    // (a dense launch lists every point: nothing to re-test, so neither phase runs)
     const bool mv = active && in && cls == 1 && tid < fs;
+    double dwin = S.dnow;
+    int ufirst = INT_MAX;
+    if (!a.dense) {
     double sd = mv ? fmax(slot_drift_at(a, st, own, co - 1), slot_drift_at(a, st, tgt, ct + 1)) : 0.0;
 #pragma unroll
     for (int o = 1; o < kWave; o <<= 1) {
@@ -531,7 +516,8 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
       if (lane == 0) { X->dch = x; X->dwin = y; }
     }
     __syncthreads();
-    const double dch = X->dch, dwin = X->dwin;
+    const double dch = X->dch;
+    dwin = X->dwin;
     double dpre = dch;
     for (int w = 0; w < wv; ++w) dpre = fmax(dpre, F->wsd[w]);
     F->dnl[tid] = fmax(sd, dpre);
@@ -562,8 +548,9 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
       if (lane == 0) X->ufirst = x;
     }
     __syncthreads();
-    const int ufirst = X->ufirst;
+    ufirst = X->ufirst;
     if (dwin > a.dmax && tid == 0) S.checked = 1;
+    }
     // ---- commit the positions before the first stop and before the first failing point: the
     // count changes are published first, the labels and the move log written only after the
     // barrier, so a launch that gives up at that barrier has committed nothing of this window
