@@ -2261,7 +2261,7 @@ struct Ctx {
     ra.lmask = (pa.lbound && last_xpath == 3) ? d_lmask.p : nullptr;
     ra.codes_t = d_codes_t.p;
     ra.lat_negl = lat_negl;
-    ra.dense = pa.dense_direct;
+    ra.all_listed = pa.dense_direct;
     ra.nq = nq;
     ra.fpg_limit = fpg_limit_ticks;
     ra.fpg_fail = fpg_fail_at;

@@ -301,7 +301,7 @@ struct ResolveArgs {
   const uint8_t* codes_t;    // the data (tiled codes): exact latent sums for bounded columns
   int nq;
   double lat_negl;           // as PrepassArgs::lat_negl
-  int dense;                 // 1: every point of [p0, n) listed (k_dense_list): nothing to re-test
+  int all_listed;            // 1: every point of [p0, n) listed (k_dense_list): nothing to re-test
   long long fpg_limit;       // a grid barrier gives up after this many wall_clock64 ticks (100 MHz)
   int fpg_fail;              // testing: workgroup 0 gives up at its fpg_fail-th grid barrier (0: never)
 };

@@ -492,7 +492,7 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
     const bool mv = active && in && cls == 1 && tid < fs;
     double dwin = S.dnow;
     int ufirst = INT_MAX;
-    if (!a.dense) {
+    if (!a.all_listed) {
     double sd = mv ? fmax(slot_drift_at(a, st, own, co - 1), slot_drift_at(a, st, tgt, ct + 1)) : 0.0;
 #pragma unroll
     for (int o = 1; o < kWave; o <<= 1) {
