@@ -631,8 +631,14 @@ bool prepass_wide_offsets_fit(const PrepassArgs& a) {
   return a.m + 1 <= kWideMaxM1 && a.P * (int64_t)std::max<int64_t>(a.bw, hs) * 8 + 4096 < 0x7fffffff;
 }
 
+// Waves per SIMD the compiler must fit: 4 (128 VGPRs; a few loop-invariant values spill) for
+// C4's layout (wb 4, one word per lane), measured 46.5 against 48.5 us at its natural 3
+// (profiles/r05/wide_prepass); the other layouts keep the register allocation they need.
+template <int WB, int NW>
+constexpr int wide_min_waves() { return WB == 4 && NW == 1 ? 4 : 1; }
+
 template <int WB, int NW, bool CL>
-__global__ __launch_bounds__(kWideThreads) void k_prepass_wide(PrepassArgs a, int nchunks, int claim) {
+__global__ __launch_bounds__(kWideThreads, (wide_min_waves<WB, NW>())) void k_prepass_wide(PrepassArgs a, int nchunks, int claim) {
   if (!pipe_gate(a)) return;
   extern __shared__ uint64_t s_dyn[];
   __shared__ double s_mg[2][kWideChunk];
@@ -784,7 +790,30 @@ __global__ __launch_bounds__(kWideThreads) void k_prepass_wide(PrepassArgs a, in
         if (u < a.m) gather(u, u);
       uint64_t M[NW];
       double lo;
-      {
+      // the own cluster's record: its copy among the cluster summaries in LDS (CL; a lane per
+      // summary, 16 at a time), so no global-memory latency precedes the cluster loop; the
+      // slot's record otherwise
+      int lown = -1;
+      if constexpr (CL) {
+        for (int l0 = 0; l0 < a.K; l0 += 16) {
+          const int l = l0 + w;
+          const unsigned long long hb = __ballot(l < a.K && (int)s_cs[l * cw + bw + 1] == own);
+          const unsigned gb = (unsigned)(hb >> (16 * (g & 3))) & 0xFFFFu;
+          if (gb) {
+            lown = l0 + __ffs((int)gb) - 1;
+            break;
+          }
+        }
+      }
+      if (lown >= 0) {
+        const uint64_t* rec = s_cs + lown * cw;
+        auto ld = [&](int k, int q) { return rec[q + w + 16 * k]; };
+        const int H = xr.mismatch(ld, M);
+        const int Sq = xr.penalty(ld, M);
+        const double A = as_f64(rec[SC]), dl = as_f64(rec[SC + 1]);
+        const double pmax = dl * (double)(Sq + H);
+        lo = a.logn[own_cnt - 1] + (A - pmax - kBoundEps * (1.0 + fabs(A) + pmax));
+      } else {
         const int ob = own * bw * 8;
         auto ld = [&](int k, int q) { return bload(r_slot, ob + w8 + 128 * k, 8 * q); };
         const int H = xr.mismatch(ld, M);
@@ -3482,7 +3511,18 @@ static hipError_t launch_prepass_w(const PrepassArgs& a, int nblocks, hipStream_
     const size_t lds = prepass_wide_lds_bytes(WB, a.Ws, a.m, a.K, a.bw, cl);
     const int nchunks = (a.n - a.p0 + kWideChunk - 1) / kWideChunk;
     auto go = [&](auto kern) {
-      const int grid = std::min(nchunks, wide_grid(kern, lds));
+      int grid = std::min(nchunks, wide_grid(kern, lds));
+      // the same number of chunks for every workgroup (C4: 4,375 chunks on 875 workgroups, 5
+      // each, instead of 4 or 5 on 1,024: the last round then runs on fewer CUs' worth of
+      // waves).  HDPM_WIDE_BAL=0: the full persistent grid (A/B)
+      static const int bal = [] {
+        const char* e = std::getenv("HDPM_WIDE_BAL");
+        return e ? std::atoi(e) : 1;
+      }();
+      if (bal) {
+        const int rounds = (nchunks + grid - 1) / grid;
+        grid = (nchunks + rounds - 1) / rounds;
+      }
       // HDPM_WIDE_CLAIM=1: chunks claimed from a counter (A/B; see k_prepass_wide)
       static const int claim = [] {
         const char* e = std::getenv("HDPM_WIDE_CLAIM");

@@ -306,8 +306,8 @@ struct ResolveArgs {
   int fpg_fail;              // testing: workgroup 0 gives up at its fpg_fail-th grid barrier (0: never)
 };
 // Cross-workgroup scratch of k_resolve_fpg (G workgroups), in ints: barrier [0, 96), state mirror
-// [96, 96 + 8 + 3 * 64 + 16), then per workgroup: stop, changed, fail, moves, fresh, and the
-// last point of its chunk; per workgroup and slot: round deltas, committed deltas; then per
+// [96, 96 + 8 + 3 * 64 + 16), then per workgroup: stop and changed (two parities each), fail,
+// moves, fresh; per workgroup and slot: round deltas (two parities), committed deltas; then per
 // workgroup (doubles): drift.
 constexpr int kFpgSlots = 64;
 constexpr int kFpgState = 8;
@@ -315,7 +315,7 @@ constexpr int kFpgPerWg = 8;
 constexpr int kFpgBarWords = 96;   // barrier words (the 64-bit barrier word at 0, then padding)
 constexpr int kFpgZeroWords = kFpgBarWords + kFpgState + 16;   // zeroed before every launch (barrier, state mirror)
 __host__ __device__ inline size_t fpg_words(int G) {
-  return (size_t)kFpgBarWords + kFpgState + 3 * kFpgSlots + 16 + (size_t)G * kFpgPerWg + (size_t)2 * G * kFpgSlots +
+  return (size_t)kFpgBarWords + kFpgState + 3 * kFpgSlots + 16 + (size_t)G * kFpgPerWg + (size_t)3 * G * kFpgSlots +
          (size_t)2 * G + 16;
 }
 

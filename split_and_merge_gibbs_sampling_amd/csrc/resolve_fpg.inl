@@ -31,12 +31,12 @@ struct Lay {
   int* sol;
   int* los;
   int* cnt;
-  int* stop;     // [G] first stop (chunk position) or kFpThreads
-  int* chg;      // [G] an outcome changed in this round
+  int* stop;     // [2][G] first stop (chunk position) or kFpThreads, by round parity
+  int* chg;      // [2][G] an outcome changed in the round before
   int* fail;     // [G] first failing unlisted point or INT_MAX
   int* mov;      // [G] committed moves
   int* fresh;    // [G] committed own draws
-  int* dr;       // [G][64] round deltas per slot
+  int* dr;       // [2][G][64] round deltas per slot, by round parity
   int* dc;       // [G][64] committed deltas per slot
   double* sd;    // [G] drift maximum over the chunk's movers
   double* md;    // state mirror: dnow, dvmax
@@ -49,15 +49,15 @@ __device__ __forceinline__ Lay lay(int* b, int G) {
   L.los = L.sol + kFpgSlots;
   L.cnt = L.los + kFpgSlots;
   int* q = L.cnt + kFpgSlots;
-  L.stop = q;
-  L.chg = q + G;
-  L.fail = q + 2 * G;
-  L.mov = q + 3 * G;
-  L.fresh = q + 4 * G;
+  L.stop = q;                  // [0, 2G)
+  L.chg = q + 2 * G;           // [2G, 4G)
+  L.fail = q + 4 * G;
+  L.mov = q + 5 * G;
+  L.fresh = q + 6 * G;
   q += kFpgPerWg * G;
   L.dr = q;
-  L.dc = q + G * kFpgSlots;
-  q += 2 * G * kFpgSlots;
+  L.dc = q + 2 * G * kFpgSlots;
+  q += 3 * G * kFpgSlots;
   q += ((uintptr_t)q & 7) ? 1 : 0;
   L.sd = reinterpret_cast<double*>(q);
   L.md = L.sd + G;
@@ -215,7 +215,7 @@ __device__ __forceinline__ int wave_sum_over(const int* v, int n) {
 struct FpgShared {
   int sc[kWave], sc_prev[kWave], add[kWave];
   int red[kFpWaves * kWave];
-  int flag, gs, gs_prev, conv, u, ufirst, nm, nf;
+  int flag, gs, gs_prev, conv, u, ufirst, nm, nf, flag2, pad2;
   double dch, dwin;
 };
 
@@ -317,9 +317,18 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
     bool fresh = false;
     int chg = -1, fs = nc, gs = G;
     bool conv = false;
+    int lastchg = 1, pb = 0;
     if (tid == 0) X->gs_prev = G;
     if (wv == 0) X->sc_prev[lane] = INT_MIN;
-    for (int it = 0; it <= WIN + 1; ++it) {
+    // One grid barrier per round: a round publishes its outcomes' count changes and stops
+    // together with whether the evaluation before changed an outcome, into the buffers of its
+    // parity (a workgroup still reading the last round's reads the other parity); the window has
+    // converged when, after a barrier, no workgroup's last evaluation changed an outcome.
+    for (int it = 0; it <= WIN + 2; ++it) {
+      pb = it & 1;
+      int* const Lstop = L.stop + pb * G;
+      int* const Lchg = L.chg + pb * G;
+      int* const Ldr = L.dr + (size_t)pb * G * kFpgSlots;
       // (1) this chunk's first stop and its movers' net change per slot, published
       const unsigned long long sbal = __ballot(in && cls == 2);
       if (lane == 0) F->wstop[wv] = sbal ? wv * kWave + __ffsll((long long)sbal) - 1 : kFpThreads;
@@ -336,21 +345,37 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
       if (wv == 0) {
         int t = 0;
         for (int w = 0; w < kFpWaves; ++w) t += F->wd[w][lane];
-        L.dr[(size_t)g * kFpgSlots + lane] = t;
-        if (lane == 0) L.stop[g] = fsl < nc ? fsl : kFpThreads;
+        Ldr[(size_t)g * kFpgSlots + lane] = t;
+        if (lane == 0) {
+          Lstop[g] = fsl < nc ? fsl : kFpThreads;
+          Lchg[g] = lastchg;
+        }
       }
       if (!(ok = bar())) break;
+      // converged when no outcome of the window changed in the last evaluation
+      if (it > 0) {
+        if (wv == 0) {
+          bool any = false;
+          for (int h0 = 0; h0 < G && !any; h0 += kWave) {
+            const int h = h0 + lane;
+            any = __ballot(h < G && fpg::ald(Lchg + h) != 0) != 0ull;
+          }
+          if (lane == 0) X->flag2 = any ? 0 : 1;
+        }
+        __syncthreads();
+        if (X->flag2) { conv = true; break; }
+      }
       // (2) the window's first stopping chunk; this chunk's start counts
       if (wv == 0) {
         int f = G;
         for (int h0 = 0; h0 < G; h0 += kWave) {
           const int h = h0 + lane;
-          const unsigned long long b = __ballot(h < G && fpg::ald(L.stop + h) < kFpThreads);
+          const unsigned long long b = __ballot(h < G && fpg::ald(Lstop + h) < kFpThreads);
           if (b) { f = h0 + __ffsll((long long)b) - 1; break; }
         }
         if (lane == 0) X->gs = f;
       }
-      fpg::prefix_slots(L.dr, g, X->red, X->add);
+      fpg::prefix_slots(Ldr, g, X->red, X->add);
       gs = X->gs;
       const bool active = g <= gs && nc > 0;
       fs = g < gs ? nc : (g == gs ? fsl : 0);
@@ -461,22 +486,11 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
       for (int w = 0; w < kFpWaves; ++w) c2 = min(c2, F->wchg[w]);
       if (tid == 0) {
         F->iters++;
-        L.chg[g] = c2 < kFpThreads ? 1 : 0;
         X->gs_prev = gs;
       }
+      lastchg = c2 < kFpThreads ? 1 : 0;
       chg = c2 < kFpThreads ? c2 : nc;
-      if (!(ok = bar())) break;
-      // converged when no outcome of the window changed in this round
-      if (wv == 0) {
-        bool any = false;
-        for (int h0 = 0; h0 < G && !any; h0 += kWave) {
-          const int h = h0 + lane;
-          any = __ballot(h < G && fpg::ald(L.chg + h) != 0) != 0ull;
-        }
-        if (lane == 0) X->conv = any ? 0 : 1;
-      }
-      __syncthreads();
-      if (X->conv) { conv = true; break; }
+      __syncthreads();              // (X->gs_prev, F->wchg before the next round rewrites them)
     }
     const long long tw1 = prof ? wall_clock64() : 0;
     if (prof) tp[3] += tw1 - tw0;
@@ -637,7 +651,7 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
     if (gs < G) {
       // ---- the window's first stop: the serial path on the workgroup that holds it, in the
       // committed state; it publishes the state for the others (tagged with the window, last)
-      qs = q0 + gs * kFpThreads + fpg::ald(L.stop + gs);
+      qs = q0 + gs * kFpThreads + fpg::ald(L.stop + pb * G + gs);
       gs_stop = gs;
       if (g == gs) {
         if (wv == 0) fp_stop(a);

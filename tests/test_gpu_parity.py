@@ -705,7 +705,7 @@ def test_wide_mixed_levels_sweeps_heads_and_records(hd, oracle, debug):
 # chain starts from the ground truth with update_phi'd parameters (hdpm_init_chain), so
 # most points are certified by the bounds and the rest take exact rows.
 @pytest.mark.parametrize("debug", [0, 1024, 16384])
-@pytest.mark.parametrize("shape", ["c4", "c4_k80", "ws18_binary", "ws5_wb8", "ws5_wb2", "ws20_wb2"])
+@pytest.mark.parametrize("shape", ["c4", "c4_k80", "ws18_binary", "ws5_wb8", "ws5_wb2", "ws20_wb2", "ws16_wb4"])
 def test_wide_prepass_sweeps(hd, oracle, debug, shape):
     if shape == "c4":
         ds = synth(4000, 784, 6, 6, seed=31)           # Ws = 13, wb = 4 (C4's layout)
@@ -717,8 +717,10 @@ def test_wide_prepass_sweeps(hd, oracle, debug, shape):
         ds = synth(2000, 300, 5, 20, seed=33)          # Ws = 5, wb = 8
     elif shape == "ws5_wb2":
         ds = synth(2000, 300, 5, 4, seed=37)           # Ws = 5, wb = 2
-    else:
+    elif shape == "ws20_wb2":
         ds = synth(2000, 1250, 5, 4, seed=38)          # Ws = 20, wb = 2: two words per lane
+    else:
+        ds = synth(1500, 1024, 5, 6, seed=39)          # Ws = 16, wb = 4: wb Ws = 64, the widest heads (66 words)
     eng = make_engine(hd, ds)
     eng.set_seed(35)
     eng.set_debug(debug)
