@@ -3511,18 +3511,9 @@ static hipError_t launch_prepass_w(const PrepassArgs& a, int nblocks, hipStream_
     const size_t lds = prepass_wide_lds_bytes(WB, a.Ws, a.m, a.K, a.bw, cl);
     const int nchunks = (a.n - a.p0 + kWideChunk - 1) / kWideChunk;
     auto go = [&](auto kern) {
-      int grid = std::min(nchunks, wide_grid(kern, lds));
-      // the same number of chunks for every workgroup (C4: 4,375 chunks on 875 workgroups, 5
-      // each, instead of 4 or 5 on 1,024: the last round then runs on fewer CUs' worth of
-      // waves).  HDPM_WIDE_BAL=0: the full persistent grid (A/B)
-      static const int bal = [] {
-        const char* e = std::getenv("HDPM_WIDE_BAL");
-        return e ? std::atoi(e) : 1;
-      }();
-      if (bal) {
-        const int rounds = (nchunks + grid - 1) / grid;
-        grid = (nchunks + rounds - 1) / rounds;
-      }
+      // (the same number of chunks for every workgroup -- 875 workgroups x 5 chunks at C4 instead of
+      // 1,024 x 4-5 -- measured 54 against 47 us: the kernel wants every resident wave)
+      const int grid = std::min(nchunks, wide_grid(kern, lds));
       // HDPM_WIDE_CLAIM=1: chunks claimed from a counter (A/B; see k_prepass_wide)
       static const int claim = [] {
         const char* e = std::getenv("HDPM_WIDE_CLAIM");
