@@ -28,7 +28,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-PMC_ROUND = "r04"        # profiles/<round>/pmc_{fetch,write}_<config>.csv: this round's counter passes
+PMC_ROUND = "r05"        # profiles/<round>/pmc_{fetch,write}_<config>.csv: this round's counter passes
 
 
 def packed_layout(d: int, mmax: int):
@@ -46,6 +46,11 @@ def packed_layout(d: int, mmax: int):
 # prepass's access shapes
 FETCH_FACTOR = {"stream16": 0.5, "gather64": 1.0, "gather128": 0.584, "gather448g": 0.569}
 RATE_GBPS = {"stream16": 5650.0, "gather64": 3080.0, "gather128": 3830.0, "gather448g": 5757.0}
+# The prepass's whole access mix replayed without its arithmetic (tools/fetch_calib.hip k_mix64 /
+# k_mix448g, best of 3, profiles/r05/fetch_calib.log): (points, us) for the layouts it models --
+# C5 (rows of 4 words, three 64-B heads from a 192 MB pool: the pool sits in the Infinity Cache,
+# which the 1 GiB gathers above do not model) and C4 (52-word rows, three 448-B heads, 16-lane groups)
+MIX_US = {("gather64", 4, 3): (1048576, 72.4), ("gather448g", 52, 3): (70000, 29.9)}
 
 
 def head_layout(d: int, mmax: int):
@@ -391,11 +396,21 @@ def main():
             traffic = round(stream + (fetch - FETCH_FACTOR["stream16"] * stream) / FETCH_FACTOR[gshape] + write)
         traffic_src = [os.path.relpath(c, ROOT) for c in csvs] + ["profiles/r01/fetch_calib.log",
                                                                   "profiles/r02/pmc_fetch_calib.csv"]
-    # the measured ceiling of this access mix: its streamed and gathered bytes at the rates
-    # tools/fetch_calib.hip measured for those shapes on MI355X
-    wb_ = bpp - s_b - g_b
-    ceil_ns = s_b / RATE_GBPS["stream16"] + g_b / RATE_GBPS[gshape] + wb_ / RATE_GBPS["stream16"]
-    ceiling = bpp / ceil_ns
+    # the measured ceiling of this access mix: the replayed mix's time per point where
+    # tools/fetch_calib.hip models the layout, else its streamed and gathered bytes at the
+    # rates measured for those shapes on MI355X
+    mix = MIX_US.get((gshape, packed_layout(ds.d, int(ds.attrisize.max()))[1], args.m))
+    if mix:
+        ceiling = bpp * mix[0] / (mix[1] * 1e3)
+        ceiling_what = (f"the prepass's access mix ({s_b} B/point streamed, {g_b} B/point in {gshape[6:]}-B random "
+                        f"gathers) replayed without its arithmetic: {mix[0]} points in {mix[1]} us "
+                        f"(tools/fetch_calib.hip, profiles/r05/fetch_calib.log)")
+    else:
+        wb_ = bpp - s_b - g_b
+        ceil_ns = s_b / RATE_GBPS["stream16"] + g_b / RATE_GBPS[gshape] + wb_ / RATE_GBPS["stream16"]
+        ceiling = bpp / ceil_ns
+        ceiling_what = (f"{s_b} B/point streamed + {g_b} B/point in {gshape[6:]}-B random gathers at the rates "
+                        f"tools/fetch_calib.hip measured (profiles/r01/fetch_calib.log)")
     out = {
         "metric": "full Gibbs sweeps/sec (N-point reassign) at N=1M D=128; achieved HBM GB/s",
         "value": round(value, 4),
@@ -452,8 +467,7 @@ def main():
             "traffic_source": traffic_src,
             "measured_ceiling": {"GBps": round(ceiling, 1),
                                  "frac": None if achieved is None else round(achieved / ceiling, 4),
-                                 "what": f"{s_b} B/point streamed + {g_b} B/point in {gshape[6:]}-B random gathers "
-                                         f"at the rates tools/fetch_calib.hip measured (profiles/r01/fetch_calib.log)"},
+                                 "what": ceiling_what},
             "bytes_per_point": bpp,
             "avg_launch_ms": round(pre_ms / launches, 4),
         },

@@ -198,6 +198,13 @@ __device__ __forceinline__ bool stay_by_uniform(double mg, uint32_t raw_cat, int
   return raw_to_unif(raw_cat) <= pl * (1.0 - 1e-12);
 }
 
+// The same test out of line, for kernels at their register limit: inlined, the exp's
+// polynomial constants were hoisted out of k_prepass_wide's chunk loop into VGPRs and spilled
+// (29 MB of scratch writes per C4 launch at 4 waves/SIMD).
+__device__ __attribute__((noinline)) bool stay_by_uniform_call(double mg, uint32_t raw_cat, int E) {
+  return stay_by_uniform(mg, raw_cat, E);
+}
+
 // Margin, row position and the ordered compaction of the block's uncertain points (the
 // block's kBlock points are threads 0..kBlock-1 of its NT; the others pass active = false).
 template <int NT = kBlock>
@@ -631,9 +638,9 @@ bool prepass_wide_offsets_fit(const PrepassArgs& a) {
   return a.m + 1 <= kWideMaxM1 && a.P * (int64_t)std::max<int64_t>(a.bw, hs) * 8 + 4096 < 0x7fffffff;
 }
 
-// Waves per SIMD the compiler must fit: 4 (128 VGPRs; a few loop-invariant values spill) for
-// C4's layout (wb 4, one word per lane), measured 46.5 against 48.5 us at its natural 3
-// (profiles/r05/wide_prepass); the other layouts keep the register allocation they need.
+// Waves per SIMD the compiler must fit: 4 (128 VGPRs) for C4's layout (wb 4, one word per
+// lane; 121 VGPRs with two heads in flight, no spills), measured 46.5 against 48.5 us at its
+// natural 3 (profiles/r05/wide_prepass); the other layouts keep the allocation they need.
 template <int WB, int NW>
 constexpr int wide_min_waves() { return WB == 4 && NW == 1 ? 4 : 1; }
 
@@ -664,13 +671,13 @@ __global__ __launch_bounds__(kWideThreads, (wide_min_waves<WB, NW>())) void k_pr
   uint32_t pf_raw[4];
   auto fetch = [&](int c) {
     const int64_t i0 = (int64_t)a.p0 + (int64_t)c * kWideChunk;
+    // (32-bit point indices: n < 2^31; 64-bit forms of them were kept live across the loop)
+    const int ip = min((int)i0 + (tid & (kWideChunk - 1)), a.n - 1);
+    const uint64_t* rowp = a.xbs + ((int64_t)(ip >> 6) * WR) * 64 + (ip & 63);
 #pragma unroll
     for (int r = 0; r < kWidePf; ++r) {
       const int e = tid + r * kWideThreads;
-      if (e < kWideChunk * WR) {
-        const int64_t i = min(i0 + (e & (kWideChunk - 1)), (int64_t)a.n - 1);
-        pf[r] = a.xbs[packed_offset(i, e / kWideChunk, WR)];
-      }
+      if (e < kWideChunk * WR) pf[r] = rowp[(e / kWideChunk) * 64];
     }
     if (tid < kWideChunk) {
       pf_own = a.c[min(i0 + tid, (int64_t)a.n - 1)];
@@ -733,7 +740,7 @@ __global__ __launch_bounds__(kWideThreads, (wide_min_waves<WB, NW>())) void k_pr
     // is staged there only after this); a global load here held the other waves at the barrier
     const bool uncertain =
         on && !(ocp >= 2 && (mgp > a.thresh ||
-                             stay_by_uniform(mgp - a.dmax2, s_raw[pf_][(on ? tid : 0) * m1 + a.m], a.K + a.m)));
+                             stay_by_uniform_call(mgp - a.dmax2, s_raw[pf_][(on ? tid : 0) * m1 + a.m], a.K + a.m)));
     const int64_t i = f0 + tid;
     if (on) a.margin[i] = mgp;
     const unsigned long long bal = __ballot(uncertain);
@@ -768,7 +775,7 @@ __global__ __launch_bounds__(kWideThreads, (wide_min_waves<WB, NW>())) void k_pr
       // the first latent heads' gathers go out first (their latency overlaps the own-cluster
       // bound and the cluster loop)
       constexpr int LW = WB * NW;
-      constexpr int NPF = LW <= 4 ? 3 : LW <= 8 ? 2 : 1;   // heads in flight (register budget)
+      constexpr int NPF = LW <= 2 ? 3 : LW <= 8 ? 2 : 1;   // heads in flight (register budget: 4 waves at wb 4)
       uint64_t Hd[NPF][LW + 2];
       int pe[NPF];                            // entry of the pick
       const bool heads = a.pool_head != nullptr;

@@ -60,6 +60,50 @@ __global__ void k_stream(const uint4* __restrict__ buf, int64_t n16, uint4* out)
   if ((acc.x & 0xfffff) == 0x12345) out[threadIdx.x] = acc;
 }
 
+// The prepass's own access mix, as a practical ceiling (bench.py measured_ceiling): per point a
+// streamed row of W words (tiled [N/64][W][64] as the bit-sliced rows) and 16 B of draws, and
+// three 64-B records gathered at random from a pool of P records (C5: 1M points, W = 4, P = 3M:
+// the pool's 192 MB sit in the Infinity Cache, which the 1 GiB gathers above do not).
+__global__ void k_mix64(const uint64_t* __restrict__ rows, const uint4* __restrict__ raw, const uint4* __restrict__ pool,
+                        int64_t n, int W, int64_t P, uint64_t seed, uint4* out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  uint64_t acc = 0;
+  for (int w = 0; w < W; ++w) acc ^= rows[((t >> 6) * W + w) * 64 + (t & 63)];
+  const uint4 r = raw[t];
+  acc ^= r.x ^ r.y;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int64_t e = (int64_t)(mix(seed + t * 7 + k) % (uint64_t)P);
+    const uint4* p = pool + e * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc ^= p[q].x ^ p[q].w;
+  }
+  if ((acc & 0xfffff) == 0x12345) out[t & 1023] = make_uint4((uint32_t)acc, 0, 0, 0);
+}
+// C4's mix (k_prepass_wide): a 16-lane group per point streams its row of W words (lane w:
+// words w, w + 16, ...) and gathers three HW-word heads (448 B) from P of them (94 MB).
+__global__ void k_mix448g(const uint64_t* __restrict__ rows, const uint4* __restrict__ raw,
+                          const uint64_t* __restrict__ pool, int64_t n, int W, int HW, int64_t P, uint64_t seed,
+                          uint4* out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t g = t >> 4;
+  const int lane = (int)(t & 15);
+  if (g >= n) return;
+  uint64_t acc = 0;
+  for (int w = lane; w < W; w += 16) acc ^= rows[((g >> 6) * W + w) * 64 + (g & 63)];
+  if (lane == 0) {
+    const uint4 r = raw[g];
+    acc ^= r.x ^ r.y;
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int64_t e = (int64_t)(mix(seed + g * 7 + k) % (uint64_t)P);
+    for (int w = lane; w < HW; w += 16) acc ^= pool[e * HW + w];
+  }
+  if ((acc & 0xfffff) == 0x12345) out[t & 1023] = make_uint4((uint32_t)acc, 0, 0, 0);
+}
+
 int main() {
   const size_t bytes = (size_t)1 << 30;
   uint4 *buf, *out;
@@ -98,6 +142,34 @@ int main() {
     (void)hipEventElapsedTime(&ms, a, b);
     std::printf("gather448g %.0f records, %.1f MB, %.1f us\n", nthr * 4 / 16 * R, nthr * 4 / 16 * R * 448 / 1e6,
                 ms * 1e3);
+  }
+  // the prepass mixes (bytes per point: C5 32 + 16 + 3 x 64 = 240, C4 416 + 16 + 3 x 448 = 1,776)
+  for (int rep = 0; rep < 3; ++rep) {
+    float ms;
+    const int64_t n5 = 1 << 20, P5 = 3 * n5;
+    const uint64_t* rows5 = (const uint64_t*)buf;                       // 32 MB
+    const uint4* raw5 = (const uint4*)((const char*)buf + (64 << 20));  // 16 MB
+    const uint4* pool5 = (const uint4*)((const char*)buf + (128 << 20)); // 192 MB
+    (void)hipEventRecord(a);
+    hipLaunchKernelGGL(k_mix64, dim3((unsigned)(n5 / 256)), dim3(256), 0, 0, rows5, raw5, pool5, n5, 4, P5, 13 + rep, out);
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    (void)hipEventElapsedTime(&ms, a, b);
+    std::printf("mix64 (C5) %lld points, %.1f MB, %.1f us, %.1f GB/s\n", (long long)n5, n5 * 240 / 1e6, ms * 1e3,
+                n5 * 240 / 1e6 / ms);
+    const int64_t n4 = 70000, P4 = 3 * n4;
+    const int W4 = 52, HW4 = 56;
+    const uint64_t* rows4 = (const uint64_t*)buf;                                      // 29 MB
+    const uint4* raw4 = (const uint4*)((const char*)buf + (64 << 20));
+    const uint64_t* pool4 = (const uint64_t*)((const char*)buf + (128 << 20));         // 94 MB
+    (void)hipEventRecord(a);
+    hipLaunchKernelGGL(k_mix448g, dim3((unsigned)((n4 * 16 + 255) / 256)), dim3(256), 0, 0, rows4, raw4, pool4, n4, W4,
+                       HW4, P4, 29 + rep, out);
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    (void)hipEventElapsedTime(&ms, a, b);
+    std::printf("mix448g (C4) %lld points, %.1f MB, %.1f us, %.1f GB/s\n", (long long)n4, n4 * 1776 / 1e6, ms * 1e3,
+                n4 * 1776 / 1e6 / ms);
   }
   (void)hipFree(buf);
   (void)hipFree(out);

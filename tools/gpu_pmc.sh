@@ -15,5 +15,6 @@ for c in c5 c4; do
   done
 done
 if [ -x tools/bin/fetch_calib ]; then
+  timeout -k 10 60 ./tools/bin/fetch_calib > $O/fetch_calib.log 2>&1 || exit 1
   timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/calib -o run --output-format csv -- ./tools/bin/fetch_calib > $O/log_calib.txt 2>&1 || exit 1
 fi
