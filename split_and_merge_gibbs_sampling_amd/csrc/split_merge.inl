@@ -602,14 +602,37 @@ static double priors(Ctx* c, const HState& s, int k, int* err) {
 
 static double min0(double x) { return (x < 0.0) ? x : 0.0; }
 
-// cf:296-353 clean_var(updated, current (by value), unique(current.c_i))
-static int clean_var(Ctx* c, HState& upd, const HState cur) {
-  int maxl = 0;
-  for (int x : cur.c) maxl = std::max(maxl, x);
-  std::vector<char> seen(maxl + 1, 0);
-  for (int x : cur.c) seen[x] = 1;
+// validate_state (cf:146-172) on a state whose counts are exact (labels in [0, K), counts[k]
+// its members): the distinct labels are then the non-empty clusters -- O(K) instead of two
+// passes over N.  Every state of the move keeps its counts exact (recount_delta, the
+// restricted scans' table sizes, clean_var).
+static int hvalidate_counted(const HState& s) {
+  int u = 0;
+  for (int k = 0; k < s.K; ++k) u += s.counts[k] > 0;
+  return u == s.K ? kOk : kValidate;
+}
+
+// Counts of `to` from the exact counts of `from`, the two states differing only at the points
+// of M (the move's members): O(|M|) instead of a pass over N.
+static void recount_delta(const HState& from, HState& to, const std::vector<int>& M) {
+  to.counts = from.counts;
+  to.counts.resize(to.K, 0);
+  for (int q : M) {
+    to.counts[from.c[q]]--;
+    to.counts[to.c[q]]++;
+  }
+}
+
+// cf:296-353 clean_var(updated, current, unique(current.c_i)) for a `cur` with exact counts
+// (labels in [0, cur.K)): unique(c_i) is its non-empty clusters in ascending order, and the
+// labels are rewritten only when the reference's map moves one (a cluster at or above the new
+// K); otherwise `upd` takes them as they are.  `upd` may be `cur` (every read of cur precedes
+// the write that could change it).
+static int clean_var(Ctx* c, HState& upd, const HState& cur) {
   std::vector<int> existing;
-  for (int l = 0; l <= maxl; ++l) if (seen[l]) existing.push_back(l);
+  for (int l = 0; l < cur.K; ++l)
+    if (cur.counts[l] > 0) existing.push_back(l);
+  const int maxl = existing.empty() ? 0 : existing.back();
   const int num = (int)existing.size();
   std::vector<int> map(maxl + 1, -1);
   for (int i = 0; i < num; ++i) {
@@ -622,21 +645,26 @@ static int clean_var(Ctx* c, HState& upd, const HState cur) {
   }
   std::vector<uint8_t> nc((size_t)num * c->d, 0);
   std::vector<double> ns((size_t)num * c->d, 0.0);
+  std::vector<int32_t> cnt(num, 0);
+  bool ident = true;
   for (int i = 0; i < num; ++i) {
     const int dst = map[existing[i]];
+    ident = ident && dst == existing[i];
     std::memcpy(&nc[(size_t)dst * c->d], &cur.center[(size_t)existing[i] * c->d], c->d);
     std::memcpy(&ns[(size_t)dst * c->d], &cur.sigma[(size_t)existing[i] * c->d], (size_t)c->d * 8);
+    cnt[dst] = cur.counts[existing[i]];
   }
-  upd.center = nc;
-  upd.sigma = ns;
+  if (!ident) {
+    upd.c.resize(cur.c.size());
+    for (size_t i = 0; i < cur.c.size(); ++i) upd.c[i] = map[cur.c[i]];   // every label exists
+  } else if (&upd != &cur) {
+    upd.c = cur.c;
+  }
+  upd.center = std::move(nc);
+  upd.sigma = std::move(ns);
+  upd.counts = std::move(cnt);
   upd.K = num;
-  upd.c.resize(cur.c.size());
-  for (size_t i = 0; i < cur.c.size(); ++i) {
-    const int l = cur.c[i];
-    if (l >= 0 && l <= maxl && map[l] != -1) upd.c[i] = map[l];
-  }
-  hrecount(c, upd);
-  return hvalidate(upd);
+  return hvalidate_counted(upd);
 }
 
 static void push_cluster(Ctx* c, HState& s) {
@@ -657,6 +685,7 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
   for (int x : st.c)
     if (x < 0 || x >= st.K) { err = "State validation failed: label outside 0..K-1"; return kValidate; }
   if (n < 2) { err = "split_and_merge needs at least two observations"; return kArg; }
+  if ((int)st.counts.size() != st.K) hrecount(this, st);   // (the move keeps counts exact from here)
   // sm:263-301 select_observations_random: sample(0..n-1, 2, FALSE)
   int i1, i2;
   {
@@ -696,13 +725,13 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
     const int ref[2] = {sl.c[i1], sl.c[i2]};
     for (int q : S) sl.c[q] = ref[(int)(2 * rng.unif())];
   }
-  hrecount(this, sl);
+  recount_delta(st, sl, M);
   Freq F1, F2;                         // tables of sl.c[i1], sl.c[i2] (they split M)
   freq_split(this, sl, M, sl.c[i1], F1, F2);
   freq_plus(F1, F2, FM);
   e = restricted_gibbs(this, S, sl, i1, i2, t, F1, F2, true);
   if (e) { err = "split launch state failed"; return e; }
-  e = hvalidate(sl);
+  e = hvalidate_counted(sl);
   if (e) { err = "State validation failed: split_launch_state"; return e; }
   const int n1_sl = F1.nn, n2_sl = F2.nn;
   // sm:354-391 merge_launch_state
@@ -710,6 +739,7 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
   if (ml.c[i1] != ml.c[i2]) {
     ml.c[i1] = ml.c[i2];
     for (int q : S) ml.c[q] = ml.c[i2];
+    recount_delta(st, ml, M);
   }
   sample_center_uniform(&ml.center[(size_t)ml.c[i2] * d]);
   e = sample_sigma_wide(v.data(), w.data(),&ml.sigma[(size_t)ml.c[i2] * d]);
@@ -720,7 +750,7 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
     e = hupdate_phi_pair(this, ml, ml.c[i2], FM, ml.c[i2], FM);
     if (e) { err = "update_phi failed"; return e; }
   }
-  e = hvalidate(ml);
+  e = hvalidate_counted(ml);
   if (e) { err = "State validation failed: merge_launch_state"; return e; }
   // proposal
   HState ss;
@@ -776,7 +806,7 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
     acpt = min0(log_prior + log_likelihood + log_proposal);
   }
   if (gerr) { err = "norm_const2 - hypergeometric diverging with infinity"; return gerr; }
-  e = hvalidate(ss);
+  e = hvalidate_counted(ss);
   if (e) { err = "State validation failed: split_and_merge - state_star"; return e; }
   if (std::log(rng.unif()) < acpt) {   // sm:591
     HState ns = st;
