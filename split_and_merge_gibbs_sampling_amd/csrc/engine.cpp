@@ -621,6 +621,8 @@ struct SmWork {
   PinBuf<uint32_t> h_raw;
   PinBuf<uint8_t> h_two_codes;
   PinBuf<double> h_two_tab;
+  DevBuf<uint32_t> d_freq;    // k_sm_freq's table
+  PinBuf<uint32_t> h_freq;
   int64_t phi_prefetch = 0;   // stream slice generated ahead for the move's update_phi jobs
 };
 
@@ -981,9 +983,11 @@ struct Ctx {
     if (!pend.active) return;
     if (pend.from_raw) {
       HIPCHK(hipEventSynchronize(phidev.ev));
+      mark("rs.slice");
       for (int i = 0; i < 624; ++i) rng.mt[i] = mt_untemper(pend.from_raw[i]);
     } else {
       HIPCHK(hipEventSynchronize(pend.ev));
+      mark("rs.state");
       std::memcpy(rng.mt, pend.host_src ? pend.host_src : pend.arr.p, sizeof(rng.mt));
     }
     rng.mti = pend.mti;
@@ -1335,10 +1339,12 @@ struct Ctx {
       launch_window(*W, window_span(n), n);
       stats.rng_windows_fresh++;
     }
+    mark("dd.window");
     HIPCHK(hipStreamWaitEvent(stream, W->done, 0));
     const uint32_t* p = W->raw.p + (rng.pos - W->start_pos);
     const uint64_t target = rng.pos + n;
     if (!phi_device_prefetch(*W, target, phi_prefetch)) adopt_state_at(*W, target);
+    mark("dd.state");
     // the next sweep's update slice starts after this update's draws (at most about a
     // slice) and the next sweep's n: fetched ahead by phi_lookahead
     look_from = target + (uint64_t)n > 624 ? target + (uint64_t)n - 624 : 0;

@@ -4767,6 +4767,56 @@ hipError_t launch_debug_math(const double* x, int64_t n, int fn, int ocml, doubl
   else HDPM_LAUNCH(k_debug_math<false>, g, dim3(kBlock), 0, s, x, n, fn, out);
   return hipGetLastError();
 }
+// Frequency tables of the split-merge move on the device (split_merge.inl sm_freq_device):
+// workgroup (c, part) counts attribute chunk c (16 attributes, one 16-byte load of the tiled
+// codes per point) over its share of the list in LDS, then adds its nonzero counters to the
+// table.  Counts are integers, so the table equals the host's membership count exactly.
+constexpr int kSmFreqThreads = 256;
+__global__ __launch_bounds__(kSmFreqThreads) void k_sm_freq(SmFreqArgs a, int parts) {
+  extern __shared__ uint32_t s_bins[];            // [16][mmax]
+  const int c = blockIdx.x / parts, part = blockIdx.x - c * parts;
+  const int nb = 16 * a.mmax;
+  for (int e = threadIdx.x; e < nb; e += kSmFreqThreads) s_bins[e] = 0u;
+  __syncthreads();
+  const int per = (a.nlist + 2 + parts - 1) / parts;
+  const int q0 = part * per, q1 = min(a.nlist + 2, q0 + per);
+  for (int q = q0 + (int)threadIdx.x; q < q1; q += kSmFreqThreads) {
+    int i;
+    if (q < a.nlist) {
+      if (a.side && a.side[q] != a.want) continue;
+      i = a.list[q];
+    } else {
+      i = a.extra[q - a.nlist];
+      if (i < 0) continue;
+    }
+    const uint4 v = *(const uint4*)(a.codes_t + tiled_offset(i, c * 16, a.nq));
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      const int x = (int)((w[b >> 2] >> (8 * (b & 3))) & 0xffu);
+      if (x > 0 && c * 16 + b < a.d) atomicAdd(&s_bins[b * a.mmax + x - 1], 1u);
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < nb; e += kSmFreqThreads) {
+    const int j = c * 16 + e / a.mmax;
+    if (j < a.d && s_bins[e]) atomicAdd(&a.out[(size_t)j * a.mmax + e % a.mmax], s_bins[e]);
+  }
+}
+
+hipError_t launch_sm_freq(const SmFreqArgs& a, hipStream_t s) {
+  {
+    const hipError_t e = hipMemsetAsync(a.out, 0, (size_t)a.d * a.mmax * 4, s);
+    if (e != hipSuccess) return e;
+  }
+  const size_t lds = (size_t)16 * a.mmax * 4;
+  if (lds > 64 * 1024) return hipErrorInvalidValue;
+  // about 512 workgroups, every point list split into `parts` shares per attribute chunk
+  const int parts = std::max(1, std::min((a.nlist + 2 + 255) / 256, 512 / std::max(a.nq, 1)));
+  HDPM_LAUNCH(k_sm_freq, dim3((unsigned)(a.nq * parts)), dim3(kSmFreqThreads), lds, s, a, parts);
+  return hipGetLastError();
+}
+
 hipError_t launch_sm_lpgs(const SmArgs& a, hipStream_t s) {
   if (a.nS == 0) return hipSuccess;
   HDPM_LAUNCH(k_sm_lpgs, dim3((a.nS + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);

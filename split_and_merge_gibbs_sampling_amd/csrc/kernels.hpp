@@ -366,6 +366,19 @@ struct LoglikArgs {
 namespace hdpm {
 
 // Restricted Gibbs scan over S (code/split_merge.cpp:163-225) and logprobgs_c_i (96-161).
+// Frequency table of a point list (k_sm_freq): out[j * mmax + x_ij - 1] += 1 over the points
+// list[q] with side[q] == want (side == nullptr: every point), and the extra points (>= 0).
+struct SmFreqArgs {
+  const uint8_t* codes_t;
+  int n, d, nq, mmax;
+  const int* list;
+  int nlist;
+  const int* side;
+  int want;
+  int extra[2];
+  uint32_t* out;             // [d][mmax], zeroed by the launcher
+};
+
 struct SmArgs {
   const uint8_t* codes_t;
   int n, d, nq;

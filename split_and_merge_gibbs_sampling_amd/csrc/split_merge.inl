@@ -9,6 +9,7 @@ namespace hdpm {
 hipError_t launch_sm_ll(const SmArgs& a, hipStream_t s);
 hipError_t launch_sm_scan(const SmArgs& a, hipStream_t s);
 hipError_t launch_sm_lpgs(const SmArgs& a, hipStream_t s);
+hipError_t launch_sm_freq(const SmFreqArgs& a, hipStream_t s);
 
 // A host copy of internal_state (cfh:32-63): labels, parameters, sizes.
 struct HState {
@@ -384,12 +385,37 @@ static void sm_upload_S(Ctx* c, SmWork& W, const std::vector<int>& S) {
   if (nS) HIPCHK(hipMemcpyAsync(W.d_S.p, S.data(), nS * 4, hipMemcpyHostToDevice, c->stream));
 }
 
+// Table of the points of S (uploaded, W.d_S) on side `want` of the device sides (or all of
+// them: side = nullptr) plus the points e0, e1 (>= 0), counted on the device (k_sm_freq): one
+// launch and one table download instead of a host pass over |S| D codes.
+static void sm_freq_device(Ctx* c, SmWork& W, int nS, const int* side, int want, int e0, int e1, Freq& F) {
+  const size_t nt = (size_t)c->d * c->mmax;
+  W.d_freq.ensure(nt);
+  W.h_freq.ensure(nt);
+  SmFreqArgs a;
+  a.codes_t = c->d_codes_t.p; a.n = c->n; a.d = c->d; a.nq = c->nq; a.mmax = c->mmax;
+  a.list = W.d_S.p; a.nlist = nS; a.side = side; a.want = want;
+  a.extra[0] = e0; a.extra[1] = e1;
+  a.out = W.d_freq.p;
+  HIPCHK(launch_sm_freq(a, c->stream));
+  HIPCHK(hipMemcpyAsync(W.h_freq.p, W.d_freq.p, nt * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  F.f.resize(nt);
+  int nn = 0;
+  for (size_t e = 0; e < nt; ++e) F.f[e] = (double)W.h_freq.p[e];
+  for (int l = 0; l < c->mmax; ++l) nn += (int)W.h_freq.p[l];    // every point has a code at attribute 0
+  F.nn = nn;
+}
+
 // sm:163-225 on host state s with the scan on the device.  F1 / F2: the tables of s.c[i1]
 // and s.c[i2] on entry, kept current (points the scan moves change sides).  The members of
 // both clusters are S + {i1, i2}, so their sizes come from the tables, neither can empty
 // (i1, i2 never move) and validate_state (sm:222) cannot fail.
 // members_are_S: the two clusters hold exactly S + {i1, i2} (the split-merge move; the C ABI
-// entry point takes any S).
+// entry point takes any S).  Then the tables come from the device (sm_freq_device): F1 / F2
+// empty on entry are counted there (the split launch state), and after every scan F1 is
+// recounted from the device sides and F2 = (F1 + F2 on entry) - F1; the sides come down once,
+// after the last scan.
 static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1, int i2, int t, Freq& F1,
                             Freq& F2, bool members_are_S) {
   SmWork& W = smwork(c);
@@ -403,6 +429,26 @@ static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1
   int* hs = W.h_side.p;
   uint32_t* raw = W.h_raw.p;
   for (int q = 0; q < nS; ++q) side[q] = (s.c[S[q]] == c1) ? 0 : 1;
+  const bool dev_tables = members_are_S && c1 != c2 && c->mmax * 16 * 4 <= 64 * 1024;
+  if (!dev_tables && F1.f.empty()) {
+    std::vector<int> M(S);
+    M.push_back(i1);
+    M.push_back(i2);
+    std::sort(M.begin(), M.end());
+    freq_split(c, s, M, c1, F1, F2);
+  }
+  Freq FM;                                      // the table of S + {i1, i2} (dev_tables)
+  if (dev_tables) {
+    std::memcpy(hs, side.data(), (size_t)nS * 4);
+    if (nS) HIPCHK(hipMemcpyAsync(W.d_side.p, hs, (size_t)nS * 4, hipMemcpyHostToDevice, c->stream));
+    if (F1.f.empty()) {
+      sm_freq_device(c, W, nS, nullptr, 0, i1, i2, FM);
+      sm_freq_device(c, W, nS, W.d_side.p, 0, i1, -1, F1);
+      freq_minus(FM, F1, F2);
+    } else {
+      freq_plus(F1, F2, FM);
+    }
+  }
   // large scans take their |S| draws from the device windows (no host generation and copy;
   // the host stream adopts the state after them); debug bit 16 draws them on the host
   const bool dev_draws = nS >= 4096 && !(c->debug & 65536);
@@ -410,6 +456,7 @@ static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1
     const uint32_t* d_raw = nullptr;
     if (dev_draws) {
       c->rng_sync();
+      c->mark("sm.sync");
       d_raw = c->device_draws(nS);
     } else {
       c->rng.raw_block(raw, nS);
@@ -422,7 +469,7 @@ static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1
       sm_upload_two(c, W, s, c1, c2);
       c->mark("sm.upload");
       // later scans start from the sides the previous scan left on the device
-      if (iter == 0) {
+      if (iter == 0 && !dev_tables) {
         std::memcpy(hs, side.data(), (size_t)nS * 4);
         HIPCHK(hipMemcpyAsync(W.d_side.p, hs, (size_t)nS * 4, hipMemcpyHostToDevice, c->stream));
       }
@@ -432,6 +479,24 @@ static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1
       a.n1 = F1.nn; a.n2 = F2.nn;
       HIPCHK(launch_sm_ll(a, c->stream));
       HIPCHK(launch_sm_scan(a, c->stream));
+      if (dev_tables) {
+        sm_freq_device(c, W, nS, W.d_side.p, 0, i1, -1, F1);
+        freq_minus(FM, F1, F2);
+        c->mark("sm.device");
+        if (iter + 1 == t) {
+          // the state's labels after the last scan
+          HIPCHK(hipMemcpyAsync(hs, W.d_side.p, (size_t)nS * 4, hipMemcpyDeviceToHost, c->stream));
+          HIPCHK(hipStreamSynchronize(c->stream));
+          for (int q = 0; q < nS; ++q) s.c[S[q]] = hs[q] == 0 ? c1 : c2;
+        }
+        c->mark("sm.sides");
+        s.counts[c1] = F1.nn;
+        s.counts[c2] = F2.nn;
+        const int st = hupdate_phi_pair(c, s, c1, F1, c2, F2);
+        c->mark("sm.phi");
+        if (st) return st;
+        continue;
+      }
       HIPCHK(hipMemcpyAsync(hs, W.d_side.p, (size_t)nS * 4, hipMemcpyDeviceToHost, c->stream));
       HIPCHK(hipStreamSynchronize(c->stream));
       c->mark("sm.device");
@@ -727,9 +792,9 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
   }
   recount_delta(st, sl, M);
   Freq F1, F2;                         // tables of sl.c[i1], sl.c[i2] (they split M)
-  freq_split(this, sl, M, sl.c[i1], F1, F2);
-  freq_plus(F1, F2, FM);
+  // (counted by restricted_gibbs: on the device from the launch sides)
   e = restricted_gibbs(this, S, sl, i1, i2, t, F1, F2, true);
+  freq_plus(F1, F2, FM);
   if (e) { err = "split launch state failed"; return e; }
   e = hvalidate_counted(sl);
   if (e) { err = "State validation failed: split_launch_state"; return e; }
