@@ -610,7 +610,7 @@ static void pool_for(int64_t n, F f, int64_t grain = 0) {
 
 // Device scratch of the split-merge move (split_merge.inl).
 struct SmWork {
-  DevBuf<int> d_S, d_side, d_side_ref, d_counts2, d_cert;
+  DevBuf<int> d_S, d_side, d_side_ref, d_counts2, d_cert, d_side_prev;
   DevBuf<double> d_ll, d_out;
   DevBuf<uint8_t> d_two_codes;
   DevBuf<double> d_two_tab;
@@ -623,6 +623,11 @@ struct SmWork {
   PinBuf<double> h_two_tab;
   DevBuf<uint32_t> d_freq;    // k_sm_freq's table
   PinBuf<uint32_t> h_freq;
+  // norm_const2(w_j, v_j, m_j) of the prior density (sm:419-436 priors): a function of the
+  // hyperparameters alone, computed once per (v, w, log-space mode)
+  std::vector<double> prior_nc, prior_v, prior_w;
+  std::vector<int> prior_err;
+  int prior_log = -1;
   int64_t phi_prefetch = 0;   // stream slice generated ahead for the move's update_phi jobs
 };
 

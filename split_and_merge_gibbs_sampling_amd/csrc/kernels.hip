@@ -4437,8 +4437,27 @@ __global__ __launch_bounds__(kSmLLBlock) void k_sm_ll_lds(SmArgs a) {
   const int d = a.d, dp = a.nq * 16;
   double* tab = sm_lds;                                    // [2][d][2]
   uint8_t* cc = (uint8_t*)(sm_lds + 4 * d);                // [2][dp]
-  for (int t = threadIdx.x; t < 4 * d; t += kSmLLBlock) tab[t] = a.two.tab[t];
-  for (int t = threadIdx.x; t < 2 * dp / 16; t += kSmLLBlock) ((uint4*)cc)[t] = ((const uint4*)a.two.codes)[t];
+  {
+    // staged with 8 loads in flight per lane (a load-store loop paid an L2 latency per
+    // 8 bytes: 49 of them per lane at C4, most of the kernel's 36 us)
+    const int nt = 2 * d, nc = 2 * dp / 16;           // uint4s of the tables, of the codes
+    const uint4* st = (const uint4*)a.two.tab;
+    const uint4* sc = (const uint4*)a.two.codes;
+    for (int t0 = 0; t0 < nt + nc; t0 += 8 * kSmLLBlock) {
+      uint4 r[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int t = t0 + k * kSmLLBlock + (int)threadIdx.x;
+        r[k] = t < nt ? st[t] : (t < nt + nc ? sc[t - nt] : make_uint4(0, 0, 0, 0));
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int t = t0 + k * kSmLLBlock + (int)threadIdx.x;
+        if (t < nt) ((uint4*)tab)[t] = r[k];
+        else if (t < nt + nc) ((uint4*)cc)[t - nt] = r[k];
+      }
+    }
+  }
   __syncthreads();
   // lane pair (2p, 2p + 1): point p of the block against cluster 0 and cluster 1, so a scan
   // of |S| points runs 2|S| lanes (the chains are sequential; more waves per SIMD is what
@@ -4451,24 +4470,35 @@ __global__ __launch_bounds__(kSmLLBlock) void k_sm_ll_lds(SmArgs a) {
   const uint4* cz = (const uint4*)(cc + dp * cl);
   double l = 0.0;
   const int nfull = d / 16;
-  uint4 xn = *(const uint4*)(a.codes_t + tiled_offset(i, 0, a.nq));
-  for (int qq = 0; qq < a.nq; ++qq) {
-    const uint4 xq = xn;
-    if (qq + 1 < a.nq) xn = *(const uint4*)(a.codes_t + tiled_offset(i, (qq + 1) * 16, a.nq));
-    const uint4 c = cz[qq];
-    const uint4 dx = make_uint4(xq.x ^ c.x, xq.y ^ c.y, xq.z ^ c.z, xq.w ^ c.w);
-    if (qq < nfull) {
-      // all 16 terms read before their ordered adds (LDS reads in flight)
-      double v[16];
+  // the point's 16-byte code chunks lie 1 KB apart (tiled rows): kAhead loads in flight per
+  // lane (one at a time left every chunk a memory latency: 38 us per C4 scan)
+  constexpr int kAhead = 8;
+  const uint8_t* xp = a.codes_t + tiled_offset(i, 0, a.nq);
+  uint4 buf[kAhead];
 #pragma unroll
-      for (int b = 0; b < 16; ++b) v[b] = t[2 * (qq * 16 + b) + (byte_differs(dx, b) ? 1 : 0)];
+  for (int k = 0; k < kAhead; ++k) buf[k] = k < a.nq ? *(const uint4*)(xp + (size_t)k * 1024) : make_uint4(0, 0, 0, 0);
+  for (int q0 = 0; q0 < a.nq; q0 += kAhead) {
 #pragma unroll
-      for (int b = 0; b < 16; ++b) l += v[b];
-    } else {
+    for (int k = 0; k < kAhead; ++k) {
+      const int qq = q0 + k;
+      if (qq >= a.nq) break;
+      const uint4 xq = buf[k];
+      if (qq + kAhead < a.nq) buf[k] = *(const uint4*)(xp + (size_t)(qq + kAhead) * 1024);
+      const uint4 c = cz[qq];
+      const uint4 dx = make_uint4(xq.x ^ c.x, xq.y ^ c.y, xq.z ^ c.z, xq.w ^ c.w);
+      if (qq < nfull) {
+        // all 16 terms read before their ordered adds (LDS reads in flight)
+        double v[16];
 #pragma unroll
-      for (int b = 0; b < 16; ++b) {
-        const int j = qq * 16 + b;
-        if (j < d) l += t[2 * j + (byte_differs(dx, b) ? 1 : 0)];
+        for (int b = 0; b < 16; ++b) v[b] = t[2 * (qq * 16 + b) + (byte_differs(dx, b) ? 1 : 0)];
+#pragma unroll
+        for (int b = 0; b < 16; ++b) l += v[b];
+      } else {
+#pragma unroll
+        for (int b = 0; b < 16; ++b) {
+          const int j = qq * 16 + b;
+          if (j < d) l += t[2 * j + (byte_differs(dx, b) ? 1 : 0)];
+        }
       }
     }
   }
@@ -4538,6 +4568,7 @@ __global__ __launch_bounds__(kBlock) void k_sm_cert(SmArgs a) {
   const int q = blockIdx.x * kBlock + threadIdx.x;
   if (q >= a.nS) return;
   const int cur = a.side[q];
+  if (a.side_prev) a.side_prev[q] = cur;
   const double dl = a.ll[q] - a.ll[a.nS + q];
   const double rU = raw_to_unif(a.raw[q]);
   const int tot = a.n1 + a.n2;
@@ -4780,21 +4811,43 @@ __global__ __launch_bounds__(kSmFreqThreads) void k_sm_freq(SmFreqArgs a, int pa
   __syncthreads();
   const int per = (a.nlist + 2 + parts - 1) / parts;
   const int q0 = part * per, q1 = min(a.nlist + 2, q0 + per);
-  for (int q = q0 + (int)threadIdx.x; q < q1; q += kSmFreqThreads) {
-    int i;
-    if (q < a.nlist) {
-      if (a.side && a.side[q] != a.want) continue;
-      i = a.list[q];
-    } else {
-      i = a.extra[q - a.nlist];
-      if (i < 0) continue;
-    }
-    const uint4 v = *(const uint4*)(a.codes_t + tiled_offset(i, c * 16, a.nq));
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  // 4 points per lane at a time: their indices, then their code chunks, in flight together
+  constexpr int kB = 4;
+  for (int qb = q0; qb < q1; qb += kB * kSmFreqThreads) {
+    int pi[kB];
 #pragma unroll
-    for (int b = 0; b < 16; ++b) {
-      const int x = (int)((w[b >> 2] >> (8 * (b & 3))) & 0xffu);
-      if (x > 0 && c * 16 + b < a.d) atomicAdd(&s_bins[b * a.mmax + x - 1], 1u);
+    for (int k = 0; k < kB; ++k) {
+      const int q = qb + k * kSmFreqThreads + (int)threadIdx.x;
+      int i = -1;
+      if (q < q1) {
+        if (a.side_prev) {
+          // delta mode: only the points that changed sides, +1 onto `want`, -1 off it
+          if (q < a.nlist && a.side[q] != a.side_prev[q]) i = a.side[q] == a.want ? a.list[q] : ~a.list[q];
+          else i = INT_MIN;
+        } else if (q < a.nlist) {
+          i = (a.side && a.side[q] != a.want) ? INT_MIN : a.list[q];
+        } else {
+          i = a.extra[q - a.nlist] >= 0 ? a.extra[q - a.nlist] : INT_MIN;
+        }
+      }
+      pi[k] = q < q1 ? i : INT_MIN;
+    }
+    uint4 v[kB];
+#pragma unroll
+    for (int k = 0; k < kB; ++k) {
+      const int i = pi[k] == INT_MIN ? -1 : (pi[k] < 0 ? ~pi[k] : pi[k]);
+      v[k] = i >= 0 ? *(const uint4*)(a.codes_t + tiled_offset(i, c * 16, a.nq)) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < kB; ++k) {
+      if (pi[k] == INT_MIN) continue;
+      const uint32_t inc = pi[k] < 0 ? 0xffffffffu : 1u;
+      const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+      for (int b = 0; b < 16; ++b) {
+        const int x = (int)((w[b >> 2] >> (8 * (b & 3))) & 0xffu);
+        if (x > 0 && c * 16 + b < a.d) atomicAdd(&s_bins[b * a.mmax + x - 1], inc);
+      }
     }
   }
   __syncthreads();

@@ -376,6 +376,9 @@ struct SmFreqArgs {
   const int* side;
   int want;
   int extra[2];
+  // side_prev != nullptr: the change of the want-side table since side_prev (points now on
+  // `want` count +1, points that left it -1, two's complement in the u32 counters; no extras)
+  const int* side_prev;
   uint32_t* out;             // [d][mmax], zeroed by the launcher
 };
 
@@ -394,6 +397,7 @@ struct SmArgs {
   int* out_counts;           // [2] final sizes after the scan
   double* out;               // logprobgs partial (hi, lo) per block
   int* cert;                 // scan: per S position, [3][2] certified count bands (k_sm_cert)
+  int* side_prev;            // k_sm_cert copies the sides before the scan here (nullptr: no copy)
 };
 
 }  // namespace hdpm

@@ -369,6 +369,7 @@ static SmArgs sm_args(Ctx* c, SmWork& W, int nS) {
   a.ll = W.d_ll.p; a.side = W.d_side.p; a.side_ref = W.d_side_ref.p; a.raw = W.d_raw.p;
   a.logn = c->d_logn.p; a.n1 = 0; a.n2 = 0; a.out_counts = W.d_counts2.p; a.out = W.d_out.p;
   a.cert = W.d_cert.p;
+  a.side_prev = nullptr;
   return a;
 }
 
@@ -387,8 +388,11 @@ static void sm_upload_S(Ctx* c, SmWork& W, const std::vector<int>& S) {
 
 // Table of the points of S (uploaded, W.d_S) on side `want` of the device sides (or all of
 // them: side = nullptr) plus the points e0, e1 (>= 0), counted on the device (k_sm_freq): one
-// launch and one table download instead of a host pass over |S| D codes.
-static void sm_freq_device(Ctx* c, SmWork& W, int nS, const int* side, int want, int e0, int e1, Freq& F) {
+// launch and one table download instead of a host pass over |S| D codes.  With side_prev,
+// F is updated instead by the points whose side differs from side_prev (+1 onto `want`, -1
+// off it): after a scan only the points it moved are counted.
+static void sm_freq_device(Ctx* c, SmWork& W, int nS, const int* side, int want, int e0, int e1, Freq& F,
+                           const int* side_prev = nullptr) {
   const size_t nt = (size_t)c->d * c->mmax;
   W.d_freq.ensure(nt);
   W.h_freq.ensure(nt);
@@ -396,15 +400,22 @@ static void sm_freq_device(Ctx* c, SmWork& W, int nS, const int* side, int want,
   a.codes_t = c->d_codes_t.p; a.n = c->n; a.d = c->d; a.nq = c->nq; a.mmax = c->mmax;
   a.list = W.d_S.p; a.nlist = nS; a.side = side; a.want = want;
   a.extra[0] = e0; a.extra[1] = e1;
+  a.side_prev = side_prev;
   a.out = W.d_freq.p;
   HIPCHK(launch_sm_freq(a, c->stream));
   HIPCHK(hipMemcpyAsync(W.h_freq.p, W.d_freq.p, nt * 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
-  F.f.resize(nt);
+  const int32_t* h = (const int32_t*)W.h_freq.p;
   int nn = 0;
-  for (size_t e = 0; e < nt; ++e) F.f[e] = (double)W.h_freq.p[e];
-  for (int l = 0; l < c->mmax; ++l) nn += (int)W.h_freq.p[l];    // every point has a code at attribute 0
-  F.nn = nn;
+  for (int l = 0; l < c->mmax; ++l) nn += h[l];    // every point has a code at attribute 0
+  if (side_prev) {
+    for (size_t e = 0; e < nt; ++e) F.f[e] += (double)h[e];
+    F.nn += nn;
+  } else {
+    F.f.resize(nt);
+    for (size_t e = 0; e < nt; ++e) F.f[e] = (double)h[e];
+    F.nn = nn;
+  }
 }
 
 // sm:163-225 on host state s with the scan on the device.  F1 / F2: the tables of s.c[i1]
@@ -477,10 +488,14 @@ static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1
       SmArgs a = sm_args(c, W, nS);
       if (d_raw) a.raw = d_raw;
       a.n1 = F1.nn; a.n2 = F2.nn;
+      if (dev_tables) {
+        W.d_side_prev.ensure(std::max(nS, 1));
+        a.side_prev = W.d_side_prev.p;
+      }
       HIPCHK(launch_sm_ll(a, c->stream));
       HIPCHK(launch_sm_scan(a, c->stream));
       if (dev_tables) {
-        sm_freq_device(c, W, nS, W.d_side.p, 0, i1, -1, F1);
+        sm_freq_device(c, W, nS, W.d_side.p, 0, -1, -1, F1, W.d_side_prev.p);
         freq_minus(FM, F1, F2);
         c->mark("sm.device");
         if (iter + 1 == t) {
@@ -574,9 +589,12 @@ static double logprobgs_c_i(Ctx* c, const HState& gs, const HState& g, const std
 }
 
 // sm:6-18
+static double logdensity_hig_k(double K, double sigmaj, double vv, double ww, double m) {
+  return K - (vv + ww) * std::log(1 + std::exp(-1 / sigmaj) * (m - 1)) - (ww + 1) / sigmaj - 2 * std::log(sigmaj);
+}
 static double logdensity_hig(double sigmaj, double vv, double ww, double m, int* err, bool logspace) {
   double K = norm_const2(ww, vv, m, err, logspace);
-  return K - (vv + ww) * std::log(1 + std::exp(-1 / sigmaj) * (m - 1)) - (ww + 1) / sigmaj - 2 * std::log(sigmaj);
+  return logdensity_hig_k(K, sigmaj, vv, ww, m);
 }
 
 // sm:20-94
@@ -646,21 +664,31 @@ static double loglikelihood_hamming(Ctx* c, const HState& s, int k, const Freq& 
   return hi + lo;
 }
 
-// sm:419-436
+// sm:419-436.  Its normalising constants norm_const2(w_j, v_j, m_j) depend on the
+// hyperparameters only: computed once (SmWork::prior_nc) and reused by every move.
 static double priors(Ctx* c, const HState& s, int k, int* err) {
-  const double* sig = &s.sigma[(size_t)k * c->d];
-  std::vector<double> ld(c->d);
-  std::vector<int> er(c->d, 0);
-  per_attribute(c, [&](int j) {
-    int e = 0;
-    ld[j] = logdensity_hig(sig[j], c->v[j], c->w[j], c->att[j], &e, c->hig_log);
-    er[j] = e;
-  });
+  SmWork& W = smwork(c);
+  const int d = c->d;
+  if (W.prior_log != (int)c->hig_log || W.prior_v != c->v || W.prior_w != c->w || (int)W.prior_nc.size() != d) {
+    W.prior_nc.assign(d, 0.0);
+    W.prior_err.assign(d, 0);
+    per_attribute(c, [&](int j) {
+      int e = 0;
+      W.prior_nc[j] = norm_const2(c->w[j], c->v[j], c->att[j], &e, c->hig_log);
+      W.prior_err[j] = e;
+    });
+    W.prior_v = c->v;
+    W.prior_w = c->w;
+    W.prior_log = (int)c->hig_log;
+  }
+  const double* sig = &s.sigma[(size_t)k * d];
+  std::vector<double> ld(d);
+  per_attribute(c, [&](int j) { ld[j] = logdensity_hig_k(W.prior_nc[j], sig[j], c->v[j], c->w[j], c->att[j]); });
   double priorg = 0;
-  for (int j = 0; j < c->d; ++j) {
+  for (int j = 0; j < d; ++j) {
     priorg -= std::log((double)c->att[j]);
     priorg += ld[j];
-    if (er[j]) *err = er[j];
+    if (W.prior_err[j]) *err = W.prior_err[j];
   }
   return priorg;
 }
