@@ -4432,6 +4432,7 @@ __global__ __launch_bounds__(kBlock) void k_sm_ll(SmArgs a) {
 // k_sm_ll with both clusters' tables and codes staged in LDS; one lane per (point, cluster)
 // attribute-order sum and 64-lane workgroups, so a scan of ~10^4 points spreads over the CUs.
 constexpr int kSmLLBlock = 64;
+__device__ __forceinline__ void sm_cert_point(const SmArgs& a, int q, double dl);
 __global__ __launch_bounds__(kSmLLBlock) void k_sm_ll_lds(SmArgs a) {
   extern __shared__ double sm_lds[];
   const int d = a.d, dp = a.nq * 16;
@@ -4459,6 +4460,8 @@ __global__ __launch_bounds__(kSmLLBlock) void k_sm_ll_lds(SmArgs a) {
     }
   }
   __syncthreads();
+  if (a.zero)
+    for (int e = blockIdx.x * kSmLLBlock + (int)threadIdx.x; e < a.zero_n; e += gridDim.x * kSmLLBlock) a.zero[e] = 0u;
   // lane pair (2p, 2p + 1): point p of the block against cluster 0 and cluster 1, so a scan
   // of |S| points runs 2|S| lanes (the chains are sequential; more waves per SIMD is what
   // hides their issue and LDS latency)
@@ -4503,6 +4506,11 @@ __global__ __launch_bounds__(kSmLLBlock) void k_sm_ll_lds(SmArgs a) {
     }
   }
   a.ll[cl * a.nS + q] = l;
+  if (a.cert_in_ll) {
+    // the pair's other sum; lane 0 of the pair certifies the point (k_sm_cert's work)
+    const double lo = __shfl_xor(l, 1);
+    if (cl == 0) sm_cert_point(a, q, l - lo);
+  }
 }
 
 // Exact sm:204-215 two-way draw.  probs[k] = log(n_k) + H_k; normalise; FixupProb;
@@ -4564,12 +4572,9 @@ constexpr double kSmScanMargin = 1e-4;
 // s0 + L sigmoid(D_t -/+ margin - (l0 - l1)); every integer n1 below the band
 // [floor(x-) - 1, ceil(x+) + 1] has D < D_t - margin + 1e-9, every one above it D > D_t +
 // margin - 1e-9.  The walk then certifies a lane by integer compares against 3 bands.
-__global__ __launch_bounds__(kBlock) void k_sm_cert(SmArgs a) {
-  const int q = blockIdx.x * kBlock + threadIdx.x;
-  if (q >= a.nS) return;
+__device__ __forceinline__ void sm_cert_point(const SmArgs& a, int q, double dl) {
   const int cur = a.side[q];
   if (a.side_prev) a.side_prev[q] = cur;
-  const double dl = a.ll[q] - a.ll[a.nS + q];
   const double rU = raw_to_unif(a.raw[q]);
   const int tot = a.n1 + a.n2;
   const int s0 = cur == 0, s1 = cur == 1;
@@ -4583,6 +4588,11 @@ __global__ __launch_bounds__(kBlock) void k_sm_cert(SmArgs a) {
     a.cert[(2 * t) * a.nS + q] = (int)floor(xm) - 1;
     a.cert[(2 * t + 1) * a.nS + q] = (int)ceil(xp) + 1;
   }
+}
+__global__ __launch_bounds__(kBlock) void k_sm_cert(SmArgs a) {
+  const int q = blockIdx.x * kBlock + threadIdx.x;
+  if (q >= a.nS) return;
+  sm_cert_point(a, q, a.ll[q] - a.ll[a.nS + q]);
 }
 
 // The walk: wave 0 goes through S in batches of 64 in order; waves 1..15 stage the next chunk
@@ -4742,6 +4752,8 @@ __global__ __launch_bounds__(kBlock) void k_sm_lpgs(SmArgs a) {
   }
 }
 
+// k_sm_ll_lds runs (and carries the fused cert / zeroing, which the callers set only then)
+bool sm_ll_lds_fits(int d, int nq) { return (size_t)4 * d * 8 + (size_t)2 * nq * 16 <= 64 * 1024; }
 hipError_t launch_sm_ll(const SmArgs& a, hipStream_t s) {
   if (a.nS == 0) return hipSuccess;
   const size_t lds = (size_t)4 * a.d * 8 + (size_t)2 * a.nq * 16;
@@ -4754,7 +4766,7 @@ hipError_t launch_sm_ll(const SmArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 hipError_t launch_sm_scan(const SmArgs& a, hipStream_t s) {
-  if (a.nS > 0) HDPM_LAUNCH(k_sm_cert, dim3((a.nS + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
+  if (a.nS > 0 && !a.cert_in_ll) HDPM_LAUNCH(k_sm_cert, dim3((a.nS + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
   HDPM_LAUNCH(k_sm_scan, dim3(1), dim3(kSmScanThreads), 2 * sizeof(SmChunk), s, a);
   return hipGetLastError();
 }
@@ -4858,7 +4870,7 @@ __global__ __launch_bounds__(kSmFreqThreads) void k_sm_freq(SmFreqArgs a, int pa
 }
 
 hipError_t launch_sm_freq(const SmFreqArgs& a, hipStream_t s) {
-  {
+  if (!a.prezeroed) {
     const hipError_t e = hipMemsetAsync(a.out, 0, (size_t)a.d * a.mmax * 4, s);
     if (e != hipSuccess) return e;
   }

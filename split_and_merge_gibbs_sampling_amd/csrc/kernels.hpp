@@ -379,7 +379,8 @@ struct SmFreqArgs {
   // side_prev != nullptr: the change of the want-side table since side_prev (points now on
   // `want` count +1, points that left it -1, two's complement in the u32 counters; no extras)
   const int* side_prev;
-  uint32_t* out;             // [d][mmax], zeroed by the launcher
+  uint32_t* out;             // [d][mmax], zeroed by the launcher (unless prezeroed)
+  int prezeroed;
 };
 
 struct SmArgs {
@@ -398,6 +399,9 @@ struct SmArgs {
   double* out;               // logprobgs partial (hi, lo) per block
   int* cert;                 // scan: per S position, [3][2] certified count bands (k_sm_cert)
   int* side_prev;            // k_sm_cert copies the sides before the scan here (nullptr: no copy)
+  int cert_in_ll;            // k_sm_ll_lds computes the certified bands too (no k_sm_cert launch)
+  uint32_t* zero;            // zeroed by k_sm_ll_lds (zero_n words): the table k_sm_freq fills next
+  int zero_n;
 };
 
 }  // namespace hdpm

@@ -10,6 +10,7 @@ hipError_t launch_sm_ll(const SmArgs& a, hipStream_t s);
 hipError_t launch_sm_scan(const SmArgs& a, hipStream_t s);
 hipError_t launch_sm_lpgs(const SmArgs& a, hipStream_t s);
 hipError_t launch_sm_freq(const SmFreqArgs& a, hipStream_t s);
+bool sm_ll_lds_fits(int d, int nq);
 
 // A host copy of internal_state (cfh:32-63): labels, parameters, sizes.
 struct HState {
@@ -370,6 +371,9 @@ static SmArgs sm_args(Ctx* c, SmWork& W, int nS) {
   a.logn = c->d_logn.p; a.n1 = 0; a.n2 = 0; a.out_counts = W.d_counts2.p; a.out = W.d_out.p;
   a.cert = W.d_cert.p;
   a.side_prev = nullptr;
+  a.cert_in_ll = 0;
+  a.zero = nullptr;
+  a.zero_n = 0;
   return a;
 }
 
@@ -392,7 +396,7 @@ static void sm_upload_S(Ctx* c, SmWork& W, const std::vector<int>& S) {
 // F is updated instead by the points whose side differs from side_prev (+1 onto `want`, -1
 // off it): after a scan only the points it moved are counted.
 static void sm_freq_device(Ctx* c, SmWork& W, int nS, const int* side, int want, int e0, int e1, Freq& F,
-                           const int* side_prev = nullptr) {
+                           const int* side_prev = nullptr, bool prezeroed = false) {
   const size_t nt = (size_t)c->d * c->mmax;
   W.d_freq.ensure(nt);
   W.h_freq.ensure(nt);
@@ -402,6 +406,7 @@ static void sm_freq_device(Ctx* c, SmWork& W, int nS, const int* side, int want,
   a.extra[0] = e0; a.extra[1] = e1;
   a.side_prev = side_prev;
   a.out = W.d_freq.p;
+  a.prezeroed = prezeroed ? 1 : 0;
   HIPCHK(launch_sm_freq(a, c->stream));
   HIPCHK(hipMemcpyAsync(W.h_freq.p, W.d_freq.p, nt * 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
@@ -488,14 +493,22 @@ static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1
       SmArgs a = sm_args(c, W, nS);
       if (d_raw) a.raw = d_raw;
       a.n1 = F1.nn; a.n2 = F2.nn;
+      // one launch fewer: the certified bands and the delta table's zeroing in k_sm_ll_lds
+      const bool fused = dev_tables && sm_ll_lds_fits(c->d, c->nq);
       if (dev_tables) {
         W.d_side_prev.ensure(std::max(nS, 1));
+        W.d_freq.ensure((size_t)c->d * c->mmax);
         a.side_prev = W.d_side_prev.p;
+        if (fused) {
+          a.cert_in_ll = 1;
+          a.zero = W.d_freq.p;
+          a.zero_n = c->d * c->mmax;
+        }
       }
       HIPCHK(launch_sm_ll(a, c->stream));
       HIPCHK(launch_sm_scan(a, c->stream));
       if (dev_tables) {
-        sm_freq_device(c, W, nS, W.d_side.p, 0, -1, -1, F1, W.d_side_prev.p);
+        sm_freq_device(c, W, nS, W.d_side.p, 0, -1, -1, F1, W.d_side_prev.p, fused);
         freq_minus(FM, F1, F2);
         c->mark("sm.device");
         if (iter + 1 == t) {
