@@ -3018,6 +3018,7 @@ struct Ctx {
     // diagnostics (debug bit 5): ns after launch
     std::chrono::steady_clock::time_point t_launch;
     std::atomic<int64_t> ns_fill{0}, ns_logits{0}, ns_b0{0}, ns_b1{0}, ns_f0{0}, ns_f1{0}, ns_f2{0};
+    int64_t ns_wait_a = 0, ns_wait_l = 0;   // (debug bit 5) B's waits for phase A / logit chunks
     std::atomic<int> b_thread{0};
   } pj;
   int64_t pj_ns() const {
@@ -3293,8 +3294,12 @@ struct Ctx {
     const int nl = pj.nL.load(std::memory_order_relaxed);
     int c = PhiJob::chunk_of(pos);
     if (c >= nl) return INT64_MAX;
-    while (!pj.ldone[c].load(std::memory_order_acquire))
-      if (!pj_logit()) HostPool::spin_pause();
+    if (!pj.ldone[c].load(std::memory_order_acquire)) {
+      const int64_t w0 = (debug & 32) ? pj_ns() : 0;
+      while (!pj.ldone[c].load(std::memory_order_acquire))
+        if (!pj_logit()) HostPool::spin_pause();
+      if (debug & 32) pj.ns_wait_l += pj_ns() - w0;
+    }
     while (c + 1 < nl && pj.ldone[c + 1].load(std::memory_order_acquire)) ++c;
     return c + 1 >= nl ? INT64_MAX : std::min<int64_t>(sa.n, PhiJob::chunk_beg(c + 1));
   }
@@ -3323,9 +3328,14 @@ struct Ctx {
     pj.ns_b0.store(pj_ns());
     pj.b_thread.store(sched_getcpu() == HostPool::get().main_cpu() ? 1 : 0);
     int tb = pj.t0;
+    pj.ns_wait_a = pj.ns_wait_l = 0;
     for (; tb < pj.T; ++tb) {
-      while (pj.stA[tb].load(std::memory_order_acquire) < pj.nach)
-        if (!pj_take_a()) HostPool::spin_pause();
+      if (pj.stA[tb].load(std::memory_order_acquire) < pj.nach) {
+        const int64_t w0 = (debug & 32) ? pj_ns() : 0;
+        while (pj.stA[tb].load(std::memory_order_acquire) < pj.nach)
+          if (!pj_take_a()) HostPool::spin_pause();
+        if (debug & 32) pj.ns_wait_a += pj_ns() - w0;
+      }
       if (pj.offs) pj.offs[tb] = sa.used;
       pj.berr = pj_phaseB(tb);
       if (pj.berr) break;
@@ -3422,6 +3432,8 @@ struct Ctx {
       tsum("spec.logits_at", pj.ns_logits.load() * 1e-3);
       tsum("spec.B_from", pj.ns_b0.load() * 1e-3);
       tsum("spec.B_to", pj.ns_b1.load() * 1e-3);
+      tsum("spec.B_waitA", pj.ns_wait_a * 1e-3);
+      tsum("spec.B_waitL", pj.ns_wait_l * 1e-3);
       tsum("spec.joined_at", pj_ns() * 1e-3);
       tsum("spec.B_on_caller", pj.b_thread.load());
       std::snprintf(spec_line, sizeof(spec_line), " | spec fill %.0f state %.0f slice %.0f logits %.0f B %.0f-%.0f joined %.0f",
