@@ -2481,9 +2481,11 @@ struct Ctx {
       // between the wait kernel and the sweep)
       HIPCHK(launch_scatter_clusters(h_stage_buf[pre.buf].p, K, dp, d, bw, 1, d_slot_codes.p, d_slot_tab.p,
                                      d_slot_bnd.p, d_counts.p, d_sol.p, d_los.p, d_src.p, stream, &d_pipe.p[q].gate));
-      HIPCHK(hipEventRecord(ev_stage_buf[pre.buf], stream));
     }
     pre.round_ok = launch_round(0, K, m, nullptr, track, kRoundAll, &d_pipe.p[q], q) == kOk;
+    // the staging buffer's release marker after the round, not between the scatter and the
+    // round's first kernel: an event record there cost the sweep a ~6 us gap
+    if (!dev) HIPCHK(hipEventRecord(ev_stage_buf[pre.buf], stream));
     stats.pipe_enqueued++;
   }
   void pre_release() {
