@@ -59,7 +59,8 @@ hipError_t launch_freq_gather(const unsigned int* freq, const int* sol, int Kmax
                               const ResolveCtl* ctl, int n, hipStream_t s);
 hipError_t launch_scatter_clusters(const uint8_t* stage, int nent, int dp, int d, int bw, int full, uint8_t* codes,
                                    double* tab, uint64_t* bnd, int* counts, int* sol, int* los, int* src,
-                                   hipStream_t s, const int* gate = nullptr);
+                                   hipStream_t s, const int* gate = nullptr, uint64_t* csum = nullptr,
+                                   const double* logn = nullptr, int* zero = nullptr, int* wide_ctr = nullptr);
 hipError_t launch_phi_locate(const PipeArgs& a, hipStream_t s);
 hipError_t launch_pipe_wait(const PipeSlot* slot, const ResolveCtl* prev, ResolveCtl* own, int n, PipeGate* g,
                             long long limit, hipStream_t s);
@@ -1980,6 +1981,7 @@ struct Ctx {
 
   // ------------------------------------------------------------------ Neal-8 sweep
   bool mcount_clear = false;
+  bool summary_by_scatter = false;     // the pipelined scatter wrote this round's summaries (pre_enqueue)
   // Buffers of a sweep (sized for n).
   void sweep_buffers(bool track, int m) {
     const int nb_max = (n + kBlock - 1) / kBlock;
@@ -2202,7 +2204,7 @@ struct Ctx {
         if (!e) HIPCHK(hipEventCreate(&e));
     }
     if (part != kRoundResolve) {
-      HIPCHK(launch_cluster_summary(pa, stream));
+      if (!summary_by_scatter) HIPCHK(launch_cluster_summary(pa, stream));
       if (timed) HIPCHK(hipEventRecord(ev[0], stream));
       if (pg && pre_timed[cpar]) HIPCHK(hipEventRecord(ev_pp[cpar][0], stream));
       if (pa.dense_direct) HIPCHK(launch_dense_list(pa, stream));
@@ -2470,19 +2472,32 @@ struct Ctx {
     pre.m = m;
     pre.track = track;
     pre.round_ok = false;
+    // the scatter also writes the round's cluster summaries (k_cluster_summary's work) from the
+    // staged records: one launch fewer between the wait kernel and the prepass
+    d_csum.ensure((size_t)K * (bw + 2));
+    d_wide_ctr.ensure(4);
+    int* zero = nullptr;
+    if (mcount_clear && K > 0) {
+      zero = d_mcount.p;
+      mcount_clear = false;
+    }
     if (dev) {
       // the speculative device update's tables (phd.stage), once it is done
       HIPCHK(hipStreamWaitEvent(stream, dspec.ev, 0));
       HIPCHK(launch_scatter_clusters(phd.stage.p, K, dp, d, bw, 1, d_slot_codes.p, d_slot_tab.p, d_slot_bnd.p,
-                                     d_counts.p, d_sol.p, d_los.p, d_src.p, stream, &d_pipe.p[q].gate));
+                                     d_counts.p, d_sol.p, d_los.p, d_src.p, stream, &d_pipe.p[q].gate, d_csum.p,
+                                     d_logn.p, zero, d_wide_ctr.p));
       phd_release(stream);
     } else {
       // the scatter reads the staging buffer in host memory directly (no copy-engine hops
       // between the wait kernel and the sweep)
       HIPCHK(launch_scatter_clusters(h_stage_buf[pre.buf].p, K, dp, d, bw, 1, d_slot_codes.p, d_slot_tab.p,
-                                     d_slot_bnd.p, d_counts.p, d_sol.p, d_los.p, d_src.p, stream, &d_pipe.p[q].gate));
+                                     d_slot_bnd.p, d_counts.p, d_sol.p, d_los.p, d_src.p, stream, &d_pipe.p[q].gate,
+                                     d_csum.p, d_logn.p, zero, d_wide_ctr.p));
     }
+    summary_by_scatter = true;
     pre.round_ok = launch_round(0, K, m, nullptr, track, kRoundAll, &d_pipe.p[q], q) == kOk;
+    summary_by_scatter = false;
     // the staging buffer's release marker after the round, not between the scatter and the
     // round's first kernel: an event record there cost the sweep a ~6 us gap
     if (!dev) HIPCHK(hipEventRecord(ev_stage_buf[pre.buf], stream));

@@ -3304,14 +3304,41 @@ __global__ __launch_bounds__(1024) void k_finish_sweep(int* counts, int* sol, in
   }
 }
 
-// Cluster parameter upload (UploadLayout) from the staging buffer.
+// Cluster parameter upload (UploadLayout) from the staging buffer.  With `sum` (full uploads
+// of entry r = label r = slot r, the pipelined sweep's), also k_cluster_summary's work for the
+// round that follows: the per-label summaries straight from the staged records and counts,
+// and its counter clears -- one launch fewer on the sweep's path.
+struct ScatterSummary {
+  uint64_t* csum;           // [nent][bw + 2]: record, logn[count], slot
+  const double* logn;
+  int* zero;                // cleared (nullable)
+  int* wide_ctr;            // [3] cleared
+};
 __global__ void k_scatter_clusters(const uint8_t* __restrict__ stage, int nent, int dp, int d, int bw, int full,
                                    uint8_t* codes, double* tab, uint64_t* bnd, int* counts, int* sol, int* los,
-                                   int* src, const int* gate) {
+                                   int* src, const int* gate, ScatterSummary sum) {
   if (gate_closed(gate)) return;
   const UploadLayout L = upload_layout(nent, dp, d, bw);
   const int* slot = (const int*)(stage + L.off_slot);
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (int64_t)gridDim.x * blockDim.x;
+  if (sum.csum) {
+    if (tid == 0) {
+      if (sum.zero) *sum.zero = 0;
+      sum.wide_ctr[0] = 0;
+      sum.wide_ctr[1] = 0;
+      sum.wide_ctr[2] = 0;
+    }
+    const int sw = bw + 2;
+    const int* scount = (const int*)(stage + L.off_counts);
+    for (int64_t q = tid; q < (int64_t)nent * sw; q += nth) {
+      const int l = (int)(q / sw), w = (int)(q - (int64_t)l * sw);
+      uint64_t v;
+      if (w < bw) v = ((const uint64_t*)(stage + L.off_bnd))[(int64_t)l * bw + w];
+      else if (w == bw) v = (uint64_t)__double_as_longlong(sum.logn[scount[l]]);
+      else v = (uint64_t)l;
+      sum.csum[q] = v;
+    }
+  }
   const int tw = 2 * d;
   for (int64_t q = tid; q < (int64_t)nent * tw; q += nth) {
     const int r = (int)(q / tw), o = (int)(q - (int64_t)r * tw);
@@ -4356,11 +4383,14 @@ hipError_t launch_pipe_wait(const PipeSlot* slot, const ResolveCtl* prev, Resolv
 
 hipError_t launch_scatter_clusters(const uint8_t* stage, int nent, int dp, int d, int bw, int full, uint8_t* codes,
                                    double* tab, uint64_t* bnd, int* counts, int* sol, int* los, int* src,
-                                   hipStream_t s, const int* gate) {
-  const int64_t work = (int64_t)nent * std::max(2 * d, std::max(dp, bw));
+                                   hipStream_t s, const int* gate, uint64_t* csum, const double* logn, int* zero,
+                                   int* wide_ctr) {
+  if (csum && !full) return hipErrorInvalidValue;     // the summaries assume entry r = label r = slot r
+  const int64_t work = (int64_t)nent * std::max(2 * d, std::max(dp, bw + 2));
   const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (work + 255) / 256));
+  const ScatterSummary sum{csum, logn, zero, wide_ctr};
   HDPM_LAUNCH(k_scatter_clusters, dim3(nb), dim3(256), 0, s, stage, nent, dp, d, bw, full, codes, tab, bnd,
-                     counts, sol, los, src, gate);
+                     counts, sol, los, src, gate, sum);
   return hipGetLastError();
 }
 
