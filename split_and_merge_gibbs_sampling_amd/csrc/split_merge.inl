@@ -836,6 +836,7 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
   // (counted by restricted_gibbs: on the device from the launch sides)
   e = restricted_gibbs(this, S, sl, i1, i2, t, F1, F2, true);
   freq_plus(F1, F2, FM);
+  mark("sm.split_state");
   if (e) { err = "split launch state failed"; return e; }
   e = hvalidate_counted(sl);
   if (e) { err = "State validation failed: split_launch_state"; return e; }
@@ -858,6 +859,7 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
   }
   e = hvalidate_counted(ml);
   if (e) { err = "State validation failed: merge_launch_state"; return e; }
+  mark("sm.merge_state");
   // proposal
   HState ss;
   double acpt;
@@ -869,6 +871,7 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
     if (e) { err = "restricted gibbs failed"; return e; }
     // sm:438-487 (st.c[i1]'s members are all of M)
     SmTimer tm(stats.t_sm_terms_ms);
+    mark("sm.t0");
     double log_prior = 0.0, log_likelihood = 0.0, log_proposal = 0.0;
     log_prior += std::log(alpha);
     log_prior += std::lgamma((double)F1.nn);
@@ -877,13 +880,17 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
     log_prior += priors(this, ss, ss.c[i2], &gerr);
     log_prior -= std::lgamma((double)FM.nn);
     log_prior -= priors(this, st, st.c[i1], &gerr);
+    mark("sm.t.priors");
     log_likelihood += loglikelihood_hamming(this, ss, ss.c[i1], F1);
     log_likelihood += loglikelihood_hamming(this, ss, ss.c[i2], F2);
     log_likelihood -= loglikelihood_hamming(this, st, st.c[i1], FM);
+    mark("sm.t.ll");
     log_proposal += logprobgs_phi(this, st, ml, i1, FM, &gerr);
     log_proposal -= logprobgs_phi(this, ss, sl, i1, F1, &gerr);
     log_proposal -= logprobgs_phi(this, ss, sl, i2, F2, &gerr);
+    mark("sm.t.lpphi");
     log_proposal -= logprobgs_c_i(this, ss, sl, S, i1, i2, n1_sl, n2_sl);
+    mark("sm.t.lpci");
     acpt = min0(log_prior + log_likelihood + log_proposal);
   } else {
     ss = ml;
@@ -891,9 +898,24 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
     if (e) { err = "update_phi failed"; return e; }
     // sm:489-540 (ss's merged cluster is M; st's two clusters split M)
     SmTimer tm(stats.t_sm_terms_ms);
+    mark("sm.t0");
     Freq S1, S2;
-    freq_over(this, st, M, st.c[i1], S1);
+    if (!S.empty() && mmax * 16 * 4 <= 64 * 1024) {
+      // st's c(i1) within M counted on the device from st's sides of S (a host pass over
+      // |M| D codes took ~0.6 ms at C4)
+      SmWork& W = smwork(this);
+      const int nS = (int)S.size();
+      sm_upload_S(this, W, S);
+      W.h_side.ensure(nS);
+      W.d_side_prev.ensure(nS);
+      for (int q = 0; q < nS; ++q) W.h_side.p[q] = st.c[S[q]] == st.c[i1] ? 0 : 1;
+      HIPCHK(hipMemcpyAsync(W.d_side_prev.p, W.h_side.p, (size_t)nS * 4, hipMemcpyHostToDevice, stream));
+      sm_freq_device(this, W, nS, W.d_side_prev.p, 0, i1, st.c[i2] == st.c[i1] ? i2 : -1, S1);
+    } else {
+      freq_over(this, st, M, st.c[i1], S1);
+    }
     freq_minus(FM, S1, S2);
+    mark("sm.t.freq");
     double log_prior = 0.0, log_likelihood = 0.0, log_proposal = 0.0;
     log_prior += std::lgamma((double)FM.nn);
     log_prior += priors(this, ss, ss.c[i1], &gerr);
@@ -902,13 +924,16 @@ int Ctx::split_and_merge(int t, int r, int idx_1_sm, int* accepted) {
     log_prior -= std::lgamma((double)S2.nn);
     log_prior -= priors(this, st, st.c[i1], &gerr);
     log_prior -= priors(this, st, st.c[i2], &gerr);
+    mark("sm.t.priors");
     log_likelihood += loglikelihood_hamming(this, ss, ss.c[i2], FM);
     log_likelihood -= loglikelihood_hamming(this, st, st.c[i1], S1);
     log_likelihood -= loglikelihood_hamming(this, st, st.c[i2], S2);
+    mark("sm.t.ll");
     log_proposal += logprobgs_phi(this, st, sl, i1, S1, &gerr);
     log_proposal += logprobgs_phi(this, st, sl, i2, S2, &gerr);
     log_proposal += logprobgs_c_i(this, st, sl, S, i1, i2, n1_sl, n2_sl);
     log_proposal -= logprobgs_phi(this, ss, ml, i2, FM, &gerr);
+    mark("sm.t.lp");
     acpt = min0(log_prior + log_likelihood + log_proposal);
   }
   if (gerr) { err = "norm_const2 - hypergeometric diverging with infinity"; return gerr; }
