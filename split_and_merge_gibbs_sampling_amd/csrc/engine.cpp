@@ -3036,6 +3036,7 @@ struct Ctx {
     std::chrono::steady_clock::time_point t_launch;
     std::atomic<int64_t> ns_fill{0}, ns_logits{0}, ns_b0{0}, ns_b1{0}, ns_f0{0}, ns_f1{0}, ns_f2{0};
     int64_t ns_wait_a = 0, ns_wait_l = 0;   // (debug bit 5) B's waits for phase A / logit chunks
+    int64_t b_draws = 0, b_clusters_extra = 0;   // (debug bit 5) B's draws, clusters with an extra draw
     std::atomic<int> b_thread{0};
   } pj;
   int64_t pj_ns() const {
@@ -3346,7 +3347,11 @@ struct Ctx {
     pj.b_thread.store(sched_getcpu() == HostPool::get().main_cpu() ? 1 : 0);
     int tb = pj.t0;
     pj.ns_wait_a = pj.ns_wait_l = 0;
+    pj.b_draws = 0;
+    pj.b_clusters_extra = 0;
+    const int64_t used0 = sa.used;
     for (; tb < pj.T; ++tb) {
+      const int64_t u0 = sa.used;
       if (pj.stA[tb].load(std::memory_order_acquire) < pj.nach) {
         const int64_t w0 = (debug & 32) ? pj_ns() : 0;
         while (pj.stA[tb].load(std::memory_order_acquire) < pj.nach)
@@ -3356,9 +3361,11 @@ struct Ctx {
       if (pj.offs) pj.offs[tb] = sa.used;
       pj.berr = pj_phaseB(tb);
       if (pj.berr) break;
+      if (debug & 32) pj.b_clusters_extra += (sa.used - u0) != 3 * (int64_t)d;
       pj.stB[tb].store(1, std::memory_order_release);
     }
     if (pj.offs && !pj.berr) pj.offs[pj.T] = sa.used;
+    pj.b_draws = sa.used - used0;
     pj.b_end = tb;
     pj.ns_b1.store(pj_ns());
     for (int t = tb; t < pj.T; ++t) pj.stB[t].store(-1, std::memory_order_release);
@@ -3450,6 +3457,8 @@ struct Ctx {
       tsum("spec.B_from", pj.ns_b0.load() * 1e-3);
       tsum("spec.B_to", pj.ns_b1.load() * 1e-3);
       tsum("spec.B_waitA", pj.ns_wait_a * 1e-3);
+      tsum("spec.B_extra_draws", (double)(pj.b_draws - 3 * (int64_t)(pj.T - pj.t0) * d));
+      tsum("spec.B_clusters_extra", (double)pj.b_clusters_extra);
       tsum("spec.B_waitL", pj.ns_wait_l * 1e-3);
       tsum("spec.joined_at", pj_ns() * 1e-3);
       tsum("spec.B_on_caller", pj.b_thread.load());
