@@ -105,6 +105,9 @@ typedef struct {
     /* launches that listed every point (a context's first launch, or more than half the points
      * expected uncertain: a chain far from convergence) */
     int64_t dense_launches;
+    /* split-merge restricted scans walked on many CUs (k_sm_scan_wide), and those that gave up
+     * (grid not resident) and ran on one workgroup */
+    int64_t sm_wide_scans, sm_wide_fallbacks;
 } hdpm_stats;
 
 int         hdpm_device_count(void);

@@ -72,7 +72,8 @@ class Stats(C.Structure):
                                   "pool_walk_fallbacks", "phi_dspec_launched", "phi_dspec_used",
                                   "fpg_launches", "phi_sm_device_calls", "phi_fallback_status_mask",
                                   "phi_sm_window_retries", "fpg_aborts", "exact_mass_launches",
-                                  "exact_lanes_launches", "dense_launches")]
+                                  "exact_lanes_launches", "dense_launches", "sm_wide_scans",
+                                  "sm_wide_fallbacks")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -622,6 +622,8 @@ struct SmWork {
   PinBuf<uint32_t> h_raw;
   PinBuf<uint8_t> h_two_codes;
   PinBuf<double> h_two_tab;
+  DevBuf<int> d_wide;         // k_sm_scan_wide's barrier, flags and chunk deltas
+  PinBuf<int> h_wide;
   DevBuf<uint32_t> d_freq;    // k_sm_freq's table
   PinBuf<uint32_t> h_freq;
   // norm_const2(w_j, v_j, m_j) of the prior density (sm:419-436 priors): a function of the

@@ -4739,6 +4739,166 @@ __global__ __launch_bounds__(kSmScanThreads) void k_sm_scan(SmArgs a) {
   if (tid == 0) { a.out_counts[0] = n1; a.out_counts[1] = tot - n1; }
 }
 
+// The restricted scan on many CUs (k_sm_scan_wide).  Workgroup c walks chunk c of S (256
+// consecutive points) with wave 0 exactly as k_sm_scan walks its batches (certified compares,
+// the fixed-point draws of the uncertain lanes), from the chunk's start count: the committed
+// n1 plus the net moves of the chunks before it in the last round.  After each round (one grid
+// barrier) every workgroup reads the round's chunk deltas; the scan has converged when they
+// equal the previous round's (the start counts, and so every outcome, would repeat).  Chunk
+// c's start depends only on chunks < c, so after round r the first r chunks are final: the
+// fixed point is the sequential walk, reached in at most G + 1 rounds.  A barrier that waits
+// longer than wide_limit (a workgroup not resident) sets wide_buf[1]; nothing is written then
+// and the host runs k_sm_scan instead.
+constexpr int kSmWideChunk = 256;
+constexpr int kSmWideMaxG = 1024;
+__global__ __launch_bounds__(kSmWideChunk) void k_sm_scan_wide(SmArgs a) {
+  __shared__ double s_l0[kSmWideChunk], s_l1[kSmWideChunk];
+  __shared__ uint32_t s_raw[kSmWideChunk];
+  __shared__ int s_cur[kSmWideChunk], s_choice[kSmWideChunk];
+  __shared__ int s_band[6][kSmWideChunk];
+  __shared__ int s_prev[kSmWideMaxG];
+  __shared__ int s_start, s_state;
+  const int c = blockIdx.x, G = gridDim.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int q0 = c * kSmWideChunk, nq = min(kSmWideChunk, a.nS - q0);
+  if (tid < nq) {
+    s_l0[tid] = a.ll[q0 + tid];
+    s_l1[tid] = a.ll[a.nS + q0 + tid];
+    s_raw[tid] = a.raw[q0 + tid];
+    s_cur[tid] = a.side[q0 + tid];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) s_band[k][tid] = a.cert[k * a.nS + q0 + tid];
+  }
+  for (int h = tid; h < G; h += kSmWideChunk) s_prev[h] = 0;
+  if (tid == 0) {
+    s_start = a.n1;
+    s_state = 0;
+  }
+  __syncthreads();
+  const int tot = a.n1 + a.n2;
+  int* bar = a.wide_buf;
+  int* gave_up = a.wide_buf + 1;
+  int* dl = a.wide_buf + 4;
+  int r = 0;
+  for (; r <= G; ++r) {
+    if (wv == 0) {
+      int n1 = s_start;
+      const int nstart = n1;
+      for (int base = 0; base < nq; base += kWave) {
+        const int e = base + lane;
+        const bool act = e < nq;
+        const int cur = act ? s_cur[e] : 0;
+        bool certain = false;
+        int choice = cur;
+        if (act) {
+          const int lo = max(n1 - lane, 1 + (cur == 0)), hi = min(n1 + lane, tot - 1 - (cur == 1));
+          bool above[3];
+          certain = true;
+#pragma unroll
+          for (int t = 0; t < 3; ++t) {
+            const int blo = s_band[2 * t][e], bhi = s_band[2 * t + 1][e];
+            certain = certain && (hi < blo || lo > bhi);
+            above[t] = lo > bhi;
+          }
+          if (certain) choice = ((above[0] && above[1]) || (!above[0] && above[2])) ? 0 : 1;
+        }
+        const bool unc = act && !certain;
+        if (__ballot(unc)) {
+          const double l0 = unc ? s_l0[e] : 0.0, l1 = unc ? s_l1[e] : 0.0;
+          const double rU = unc ? raw_to_unif(s_raw[e]) : 0.5;
+          int gprev = -1;
+          const unsigned long long below = (1ull << lane) - 1ull;
+          for (;;) {
+            const unsigned long long up = __ballot(act && choice == 0 && cur == 1);
+            const unsigned long long dn = __ballot(act && choice == 1 && cur == 0);
+            const int pre = __popcll(up & below) - __popcll(dn & below);
+            bool changed = false;
+            if (unc) {
+              const int g = min(max(n1 + pre, 1 + (cur == 0)), tot - 1 - (cur == 1));
+              if (g != gprev) {
+                gprev = g;
+                const int nz1 = g - (cur == 0), nz2 = tot - g - (cur == 1);
+                const int pk = two_way_draw(dlog((double)nz1) + l0, dlog((double)nz2) + l1, rU);
+                changed = pk != choice;
+                choice = pk;
+              }
+            }
+            if (!__ballot(changed)) break;
+          }
+        }
+        n1 += __popcll(__ballot(act && choice == 0 && cur == 1)) - __popcll(__ballot(act && choice == 1 && cur == 0));
+        if (act) s_choice[e] = choice;
+      }
+      if (lane == 0) __hip_atomic_store(dl + (r & 1) * G + c, n1 - nstart, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      // grid barrier r: arrivals counted, agent-scope release / acquire
+      __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      const long long t0 = wall_clock64();
+      for (;;) {
+        if (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= G * (r + 1)) break;
+        if (__hip_atomic_load(gave_up, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
+            wall_clock64() - t0 > a.wide_limit) {
+          __hip_atomic_store(gave_up, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          s_state = -1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __syncthreads();
+    if (s_state < 0) break;
+    // the round's deltas: this chunk's next start, and whether any delta changed
+    if (wv == 0) {
+      int pre = 0;
+      bool diff = false;
+      for (int h0 = 0; h0 < G; h0 += kWave) {
+        const int h = h0 + lane;
+        const int v = h < G ? __hip_atomic_load(dl + (r & 1) * G + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        diff = diff || (h < G && v != s_prev[h]);
+        if (h < G) s_prev[h] = v;
+        int x = h < c ? v : 0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+        pre += x;
+      }
+      const bool any = __ballot(diff) != 0ull;
+      if (lane == 0) {
+        s_start = a.n1 + pre;
+        s_state = any ? 0 : 1;
+      }
+    }
+    __syncthreads();
+    if (s_state == 1) break;
+  }
+  if (s_state == 1) {
+    for (int e = tid; e < nq; e += kSmWideChunk) a.side[q0 + e] = s_choice[e];
+    if (c == 0 && tid == 0) {
+      int tot_d = 0;
+      for (int h = 0; h < G; ++h) tot_d += s_prev[h];
+      a.out_counts[0] = a.n1 + tot_d;
+      a.out_counts[1] = tot - (a.n1 + tot_d);
+      a.wide_buf[2] = r + 1;
+    }
+  } else if (tid == 0) {
+    __hip_atomic_store(gave_up, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// G workgroups for k_sm_scan_wide, or 0 when the scan is too large for one resident grid.
+int sm_scan_wide_grid(int nS) {
+  const int G = (nS + kSmWideChunk - 1) / kSmWideChunk;
+  return (G >= 2 && G <= kSmWideMaxG && G <= device_cus()) ? G : 0;
+}
+hipError_t launch_sm_scan_wide(const SmArgs& a, int G, hipStream_t s) {
+  {
+    const hipError_t e = hipMemsetAsync(a.wide_buf, 0, 16, s);
+    if (e != hipSuccess) return e;
+  }
+  HDPM_LAUNCH(k_sm_scan_wide, dim3(G), dim3(kSmWideChunk), 0, s, a);
+  return hipGetLastError();
+}
+
 // logprobgs_c_i terms: log(probs[current side]) with fixed launch sizes; compensated
 // per-block sums (hi, lo).
 __global__ __launch_bounds__(kBlock) void k_sm_lpgs(SmArgs a) {

@@ -400,6 +400,8 @@ struct SmArgs {
   int* cert;                 // scan: per S position, [3][2] certified count bands (k_sm_cert)
   int* side_prev;            // k_sm_cert copies the sides before the scan here (nullptr: no copy)
   int cert_in_ll;            // k_sm_ll_lds computes the certified bands too (no k_sm_cert launch)
+  int* wide_buf;             // k_sm_scan_wide: [0] arrivals, [1] gave up, [2] rounds, [3] pad, [4, 4 + 2G) deltas
+  long long wide_limit;      // its barrier waits give up after this many wall_clock64 ticks
   uint32_t* zero;            // zeroed by k_sm_ll_lds (zero_n words): the table k_sm_freq fills next
   int zero_n;
 };

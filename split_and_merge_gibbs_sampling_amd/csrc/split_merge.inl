@@ -11,6 +11,18 @@ hipError_t launch_sm_scan(const SmArgs& a, hipStream_t s);
 hipError_t launch_sm_lpgs(const SmArgs& a, hipStream_t s);
 hipError_t launch_sm_freq(const SmFreqArgs& a, hipStream_t s);
 bool sm_ll_lds_fits(int d, int nq);
+int sm_scan_wide_grid(int nS);
+hipError_t launch_sm_scan_wide(const SmArgs& a, int G, hipStream_t s);
+
+// HDPM_SM_WIDE=1: the restricted scans of the move on many CUs (k_sm_scan_wide); default: the
+// one-workgroup k_sm_scan
+static bool sm_wide_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("HDPM_SM_WIDE");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
 
 // A host copy of internal_state (cfh:32-63): labels, parameters, sizes.
 struct HState {
@@ -374,6 +386,8 @@ static SmArgs sm_args(Ctx* c, SmWork& W, int nS) {
   a.cert_in_ll = 0;
   a.zero = nullptr;
   a.zero_n = 0;
+  a.wide_buf = nullptr;
+  a.wide_limit = 0;
   return a;
 }
 
@@ -506,9 +520,30 @@ static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1
         }
       }
       HIPCHK(launch_sm_ll(a, c->stream));
-      HIPCHK(launch_sm_scan(a, c->stream));
+      // the walk on many CUs when the move's tables come from the device (k_sm_scan_wide; it
+      // gives up, writing nothing, if its grid is not resident -- then k_sm_scan runs)
+      const int Gw = (dev_tables && fused && sm_wide_on()) ? sm_scan_wide_grid(nS) : 0;
+      if (Gw) {
+        W.d_wide.ensure(4 + 2 * (size_t)Gw);
+        W.h_wide.ensure(4);
+        a.wide_buf = W.d_wide.p;
+        a.wide_limit = 5000000;                   // 50 ms of the 100 MHz clock
+        HIPCHK(launch_sm_scan_wide(a, Gw, c->stream));
+        HIPCHK(hipMemcpyAsync(W.h_wide.p, W.d_wide.p, 16, hipMemcpyDeviceToHost, c->stream));
+      } else {
+        HIPCHK(launch_sm_scan(a, c->stream));
+      }
       if (dev_tables) {
         sm_freq_device(c, W, nS, W.d_side.p, 0, -1, -1, F1, W.d_side_prev.p, fused);
+        if (Gw) {
+          c->stats.sm_wide_scans++;
+          if (W.h_wide.p[1] != 0) {
+            // (the sides are unchanged, so F1's delta above was zero) the one-workgroup walk
+            c->stats.sm_wide_fallbacks++;
+            HIPCHK(launch_sm_scan(a, c->stream));
+            sm_freq_device(c, W, nS, W.d_side.p, 0, -1, -1, F1, W.d_side_prev.p, false);
+          }
+        }
         freq_minus(FM, F1, F2);
         c->mark("sm.device");
         if (iter + 1 == t) {

@@ -136,7 +136,12 @@ def test_c4_full_size_neal8_and_split_merge(hd, oracle):
         ds, eng, ost, rng, pc, ps = start(hd, oracle, "c4", seed=3, hig_log=True)
         assert ds.n == 70_000 and ds.d == 784
         neal8_steps(eng, oracle, ds, ost, rng, pc, ps, sweeps=2)
+        eng.reset_stats()
         sm_steps(eng, oracle, ds, ost, rng, moves=3)
+        # with HDPM_SM_WIDE=1 the restricted scans walked on many CUs (k_sm_scan_wide)
+        st = eng.stats()
+        if os.environ.get("HDPM_SM_WIDE") == "1":
+            assert st["sm_wide_scans"] > 0 and st["sm_wide_fallbacks"] == 0, st
         eng.close()
     finally:
         oracle.set_hig_logspace(False)
