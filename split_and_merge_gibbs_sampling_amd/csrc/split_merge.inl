@@ -14,12 +14,12 @@ bool sm_ll_lds_fits(int d, int nq);
 int sm_scan_wide_grid(int nS);
 hipError_t launch_sm_scan_wide(const SmArgs& a, int G, hipStream_t s);
 
-// HDPM_SM_WIDE=1: the restricted scans of the move on many CUs (k_sm_scan_wide); default: the
-// one-workgroup k_sm_scan
+// HDPM_SM_WIDE=0: the one-workgroup restricted scan only (A/B of k_sm_scan_wide, the default:
+// 13.5 against 80 us per C4 scan, profiles/r05/split_merge/wide/)
 static bool sm_wide_on() {
   static const bool on = [] {
     const char* e = std::getenv("HDPM_SM_WIDE");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   return on;
 }
