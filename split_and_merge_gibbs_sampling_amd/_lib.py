@@ -37,6 +37,7 @@ OPT_FPG_WAIT_US = 4
 OPT_FPG_FAIL_AT = 5
 OPT_EXACT_KERNEL = 6
 OPT_LAT_NEGLIGIBLE = 7
+OPT_SM_WIDE_WAIT_US = 8
 
 STATUS = {0: "OK", 1: "E_VALIDATE", 2: "E_GSL", 3: "E_PROB", 4: "E_WALKER", 5: "E_ARG",
           6: "E_DEVICE", 7: "E_NODEVICE"}

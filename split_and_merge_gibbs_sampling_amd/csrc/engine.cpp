@@ -853,6 +853,7 @@ struct Ctx {
   int last_xpath = 0;                  // the exact-rows kernel of the last launch (launch_exact_rows' path)
   int exact_pref = 0;                  // HDPM_OPT_EXACT_KERNEL (testing)
   double lat_negl = kLatNegligible;    // HDPM_OPT_LAT_NEGLIGIBLE (testing)
+  long long sm_wide_ticks = 5000000;   // k_sm_scan_wide's barrier limit (100 MHz ticks; HDPM_OPT_SM_WIDE_WAIT_US)
   bool deep_ok = false;                // set by iteration(): the next sweep may be enqueued ahead
   static constexpr size_t kCtlInts = 16;
   static_assert(sizeof(ResolveCtl) <= kCtlInts * sizeof(int), "control block");
@@ -4829,6 +4830,10 @@ int hdpm_set_option(hdpm_ctx* h, int32_t option, double value) {
       if (!(value >= 40.0)) { ctx->err = "latent negligibility margin must be >= 40"; return HDPM_E_ARG; }
       GUARD(ctx->cancel_ahead();)
       ctx->lat_negl = value;
+      return HDPM_OK;
+    case HDPM_OPT_SM_WIDE_WAIT_US:
+      if (!(value >= 0.0) || !std::isfinite(value)) { ctx->err = "wide scan wait must be >= 0 us"; return HDPM_E_ARG; }
+      ctx->sm_wide_ticks = (long long)(value * 100.0);
       return HDPM_OK;
     case HDPM_OPT_PIPE_WAIT_US:
       if (value == 0.0 || !std::isfinite(value)) { ctx->err = "pipe wait limit must be non-zero"; return HDPM_E_ARG; }

@@ -4655,6 +4655,14 @@ __global__ __launch_bounds__(kSmScanThreads) void k_sm_scan(SmArgs a) {
   extern __shared__ unsigned char sm_scan_lds[];
   SmChunk* buf = (SmChunk*)sm_scan_lds;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (a.wide_buf) {
+    // behind k_sm_scan_wide: nothing to do when it finished; when it gave up (some of its
+    // chunks may have written their sides) the walk starts from the sides before the scan
+    if (__hip_atomic_load(a.wide_buf + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+    for (int q = tid; q < a.nS; q += kSmScanThreads) a.side[q] = a.side_prev[q];
+    __threadfence_block();
+    __syncthreads();
+  }
   int n1 = a.n1;
   const int tot = a.n1 + a.n2;
   const int nch = (a.nS + kSmChunk - 1) / kSmChunk;

@@ -527,22 +527,18 @@ static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1
         W.d_wide.ensure(4 + 2 * (size_t)Gw);
         W.h_wide.ensure(4);
         a.wide_buf = W.d_wide.p;
-        a.wide_limit = 5000000;                   // 50 ms of the 100 MHz clock
+        a.wide_limit = c->sm_wide_ticks;          // 50 ms of the 100 MHz clock by default
         HIPCHK(launch_sm_scan_wide(a, Gw, c->stream));
         HIPCHK(hipMemcpyAsync(W.h_wide.p, W.d_wide.p, 16, hipMemcpyDeviceToHost, c->stream));
-      } else {
-        HIPCHK(launch_sm_scan(a, c->stream));
       }
+      // (behind the wide scan, k_sm_scan returns at once unless it gave up: then it restores
+      // the pre-scan sides and walks -- no host round trip either way)
+      HIPCHK(launch_sm_scan(a, c->stream));
       if (dev_tables) {
         sm_freq_device(c, W, nS, W.d_side.p, 0, -1, -1, F1, W.d_side_prev.p, fused);
         if (Gw) {
           c->stats.sm_wide_scans++;
-          if (W.h_wide.p[1] != 0) {
-            // (the sides are unchanged, so F1's delta above was zero) the one-workgroup walk
-            c->stats.sm_wide_fallbacks++;
-            HIPCHK(launch_sm_scan(a, c->stream));
-            sm_freq_device(c, W, nS, W.d_side.p, 0, -1, -1, F1, W.d_side_prev.p, false);
-          }
+          if (W.h_wide.p[1] != 0) c->stats.sm_wide_fallbacks++;
         }
         freq_minus(FM, F1, F2);
         c->mark("sm.device");

@@ -233,6 +233,11 @@ class Engine:
         kept as a head bound counts as probability 0 (>= 40; larger: exact sums instead)."""
         self._check(self._L.hdpm_set_option(self._h, _lib.OPT_LAT_NEGLIGIBLE, float(margin)))
 
+    def set_sm_wide_wait_us(self, us: float):
+        """Testing (include/hdpm.h HDPM_OPT_SM_WIDE_WAIT_US): the grid-barrier limit of the
+        split-merge scan on many CUs; 0 gives up at once (the one-workgroup scan runs)."""
+        self._check(self._L.hdpm_set_option(self._h, _lib.OPT_SM_WIDE_WAIT_US, float(us)))
+
     def set_hig_logspace(self, on: bool = True):
         """Extension beyond the reference (include/hdpm.h HDPM_OPT_HIG_LOGSPACE): finite HIG
         log-densities for clusters whose 2F1 series overflows (the reference throws)."""

@@ -794,6 +794,40 @@ def test_split_merge_chain_large_moves(hd, oracle, debug):
     np.testing.assert_allclose(res["loglikelihood"], ref["loglikelihood"], rtol=RTOL, atol=0)
 
 
+@pytest.mark.parametrize("wait_us", [None, 0])
+def test_split_merge_chain_wide_scan_and_give_up(hd, oracle, wait_us):
+    """Split-merge moves whose restricted scans (|S| >= 512) walk on many CUs
+    (k_sm_scan_wide), and with a zero barrier limit give up at once and walk on one workgroup:
+    the same chain as the oracle either way."""
+    ds = synth(6000, 64, 2, 3, seed=44)
+    kw = dict(m=3, iterations=4, L=1, c_i=ds.truth, burnin=0, t=3, r=3, neal8=True, split_merge=True)
+    try:
+        oracle.set_hig_logspace(True)
+        st, ref = oracle.run_markov_chain(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w, seed=8, fast=2, **kw)
+    finally:
+        oracle.set_hig_logspace(False)
+    assert st == 0
+    eng = make_engine(hd, ds)
+    try:
+        eng.set_hig_logspace(True)
+        eng.set_seed(8)
+        if wait_us is not None:
+            eng.set_sm_wide_wait_us(wait_us)
+        res = eng.run_markov_chain(**kw)
+        stats = eng.stats()
+    finally:
+        eng.close()
+    assert np.array_equal(res["c_i"], ref["c_i"])
+    assert np.array_equal(res["total_cls"], ref["total_cls"])
+    assert np.array_equal(res["accepted"], ref["accepted"])
+    np.testing.assert_allclose(res["loglikelihood"], ref["loglikelihood"], rtol=RTOL, atol=0)
+    assert stats["sm_wide_scans"] > 0, stats
+    if wait_us == 0:
+        assert stats["sm_wide_fallbacks"] == stats["sm_wide_scans"], stats
+    else:
+        assert stats["sm_wide_fallbacks"] == 0, stats
+
+
 def test_restricted_gibbs_random_split_of_one_cluster(hd, oracle):
     # The split proposal's launch state: one true cluster's members dealt at random to two
     # labels with fresh parameters, so most scan draws are close calls whose pick depends
