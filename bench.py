@@ -304,6 +304,8 @@ def main():
                          "random assignment to 20 labels (la:31, the scripts' L = 20): the unconverged regime")
     ap.add_argument("--start-iter", type=int, default=0,
                     help="first iteration index (0: the warmup includes iteration 0's pool regeneration)")
+    ap.add_argument("--phi", choices=("auto", "host", "device"), default="auto",
+                    help="update_phi on the host job or the device (HDPM_OPT_PHI_DEVICE); auto = the engine's default")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads of the optimised CPU baseline (0: every CPU this process may use, within the "
@@ -341,6 +343,9 @@ def main():
         eng.set_hig_logspace(True)
     if os.environ.get("HDPM_BENCH_HOST_POOL"):
         eng.set_debug(64)                        # sequential host pool generator (A/B runs)
+    if args.phi != "auto":
+        eng.set_phi_device(args.phi == "device")
+    phi_dev = eng.phi_device
     L, ci = {"truth": (0, ds.truth), "one": (1, np.zeros(ds.n, np.int32)), "random20": (20, None)}[args.init]
     params = eng.chain_params(m=args.m, iterations=args.steps + args.warmup, L=L, burnin=0, neal8=True,
                               split_merge=args.sm, t=10, r=10)
@@ -453,6 +458,13 @@ def main():
             "pipeline": {"enqueued": st["pipe_enqueued"], "ran": st["pipe_runs"],
                          "slice_lookahead_hits": st["phi_lookahead_hits"]},
             "rng_windows": {"launched": st["rng_windows"], "fresh": st["rng_windows_fresh"]},
+            # recoveries inside the timed window (each keeps the chain; a non-zero count means a
+            # slow path ran): device-wide resolver give-ups, restricted scans that gave up on many
+            # CUs, sweeps enqueued ahead and re-run ungated, device update_phi handed to the host
+            "fallbacks": {k: int(st[k]) for k in ("fpg_aborts", "sm_wide_fallbacks", "pipe_recovered",
+                                                  "phi_device_fallbacks", "phi_fallback_status_mask")},
+            "update_phi": {"mode": "device" if phi_dev else "host",
+                           "device_calls": int(st["phi_device_calls"]), "spec_used": int(st["phi_dspec_used"])},
             "pool_generation": {"init": pool_report(st_init, ds.n * args.m),
                                 "regeneration": pool_report(stats_diff(st0, st_init), ds.n * args.m)},
         },

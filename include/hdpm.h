@@ -272,9 +272,13 @@ int hdpm_get_pool_heads(hdpm_ctx* ctx, uint64_t* out, int64_t P);
 #define HDPM_OPT_LAT_NEGLIGIBLE 7
 /* HDPM_OPT_SM_WIDE_WAIT_US (testing): the grid-barrier limit of the split-merge scan on many CUs
  * (default 50000 us); a scan that gives up writes nothing and is walked on one workgroup
- * (hdpm_stats.sm_wide_fallbacks).  0 gives up at the first barrier.  Same chain either way. */
+ * (hdpm_stats.sm_wide_fallbacks).  0 gives up at the first barrier, unconditionally; values above
+ * 1e9 us are an argument error.  Same chain either way. */
 #define HDPM_OPT_SM_WIDE_WAIT_US 8
 int hdpm_set_option(hdpm_ctx* ctx, int32_t option, double value);
+/* The current value of an option (the same units as hdpm_set_option; HDPM_OPT_PHI_DEVICE
+ * reads 1 when update_phi runs on the device, which may be the default). */
+int hdpm_get_option(hdpm_ctx* ctx, int32_t option, double* value);
 /* Posterior analysis (realdata_analysis/zoo_simulator.R:193-236, 339-344; mcclust /
  * mcclust.ext).  hdpm_psm_build: the posterior similarity matrix of M saved label vectors
  * c_trace[M x N] (results$c_i, labels 0..254) -- comp.psm(C) -- kept on the device as

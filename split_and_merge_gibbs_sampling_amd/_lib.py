@@ -26,7 +26,7 @@ EXPORTS = (
     "hdpm_compute_loglikelihood", "hdpm_loglik_matrix", "hdpm_restricted_gibbs", "hdpm_logprobgs_c_i",
     "hdpm_split_and_merge", "hdpm_run_markov_chain", "hdpm_get_stats", "hdpm_reset_stats",
     "hdpm_set_debug", "hdpm_synchronize", "hdpm_drop_prepared", "hdpm_init_chain", "hdpm_iteration", "hdpm_iterations", "hdpm_rng_fill_device",
-    "hdpm_get_pool_heads", "hdpm_set_option", "hdpm_debug_draw", "hdpm_debug_math",
+    "hdpm_get_pool_heads", "hdpm_set_option", "hdpm_get_option", "hdpm_debug_draw", "hdpm_debug_math",
     "hdpm_psm_build", "hdpm_psm_rows", "hdpm_psm_vi_lb",
 )
 
@@ -135,6 +135,7 @@ def lib():
         "hdpm_drop_prepared": ([vp], C.c_int),
         "hdpm_get_pool_heads": ([vp, vp, i64], C.c_int),
         "hdpm_set_option": ([vp, i32, f64], C.c_int),
+        "hdpm_get_option": ([vp, i32, P(f64)], C.c_int),
         "hdpm_debug_draw": ([vp, vp, i32, f64, i32, i32, P(i32)], C.c_int),
         "hdpm_debug_math": ([vp, vp, i64, i32, i32, vp], C.c_int),
         "hdpm_psm_build": ([vp, vp, i32, i32], C.c_int),

@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "../../include/hdpm.h"
+#include "host_topology.hpp"
 #include "kernels.hpp"
 #include "mtjump.hpp"
 #include "pool_host.hpp"
@@ -256,8 +257,25 @@ static std::vector<int> read_cpu_list(const std::string& path) {
 // HDPM_SPIN_US the spin window.
 class HostPool {
  public:
+  // The pool of the calling engine call's context (PoolScope), else, on a pool worker, its
+  // own pool, else the process's default pool (the creating thread's L3 domain).
   static HostPool& get() {
-    static HostPool p;
+    if (HostPool* p = current()) return *p;
+    return for_home(std::vector<int>{});
+  }
+  // One pool per home L3 domain (created on first use, alive for the process): contexts
+  // whose GPUs have different homes get different pools (gpu_home_domain).
+  static HostPool& for_home(const std::vector<int>& dom) {
+    static std::mutex mu;
+    static std::vector<std::pair<std::vector<int>, std::unique_ptr<HostPool>>> pools;
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto& e : pools)
+      if (e.first == dom) return *e.second;
+    pools.emplace_back(dom, std::unique_ptr<HostPool>(new HostPool(dom)));
+    return *pools.back().second;
+  }
+  static HostPool*& current() {
+    static thread_local HostPool* p = nullptr;
     return p;
   }
   int threads() const { return (int)th_.size() + 1; }
@@ -343,7 +361,7 @@ class HostPool {
   }
 
  private:
-  HostPool() {
+  explicit HostPool(const std::vector<int>& home) : home_(home) {
     if (const char* e = std::getenv("HDPM_SPIN_US")) spin_us_ = std::max(0, std::atoi(e));
     int T = 0;
     if (const char* e = std::getenv("HDPM_HOST_THREADS")) T = std::atoi(e);
@@ -351,20 +369,23 @@ class HostPool {
       unsigned h = std::thread::hardware_concurrency();
       T = (int)std::min<unsigned>(h ? h : 4, 8);
     }
-    for (int t = 1; t < T; ++t) th_.emplace_back([this] { loop(); });
+    for (int t = 1; t < T; ++t)
+      th_.emplace_back([this] {
+        current() = this;        // jobs running on a worker see their own pool
+        loop();
+      });
     pin_workers();
   }
   // Workers on distinct physical cores of one L3 domain (the host phases hand data between
-  // cores every iteration): the home domain set before the pool's creation (the GPU's,
-  // hdpm_ctx_create), else the creating thread's; HDPM_PIN_THREADS=0 leaves placement to
-  // the OS.
+  // cores every iteration): the pool's home domain (the GPU's, hdpm_ctx_create), else the
+  // creating thread's; HDPM_PIN_THREADS=0 leaves placement to the OS.
   void pin_workers() {
     if (const char* e = std::getenv("HDPM_PIN_THREADS"))
       if (std::atoi(e) == 0) return;
     cpu_set_t allowed;
     if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return;
     const std::string base = "/sys/devices/system/cpu/cpu";
-    std::vector<int> dom = home();
+    std::vector<int> dom = home_;
     int me = dom.empty() ? sched_getcpu() : dom.front();
     if (me < 0) return;
     main_cpu_ = me;
@@ -488,14 +509,20 @@ class HostPool {
   std::atomic<bool> stop_{false};
   int spin_us_ = 2000;   // an iteration's host phases are ~1 ms apart: stay awake between them
   int main_cpu_ = -1;    // the calling thread's core (kept free of workers)
+  std::vector<int> home_;   // CPUs of the L3 domain the pool lives on (empty: the creator's)
 
  public:
   int main_cpu() const { return main_cpu_; }
-  // CPUs of the L3 domain the pool is to live on (set before the first get())
-  static std::vector<int>& home() {
-    static std::vector<int> h;
-    return h;
+  const std::vector<int>& home() const { return home_; }
+};
+
+// The context's pool for the duration of an engine call (C ABI entry points).
+struct PoolScope {
+  HostPool* prev;
+  explicit PoolScope(HostPool* p) : prev(HostPool::current()) {
+    if (p) HostPool::current() = p;
   }
+  ~PoolScope() { HostPool::current() = prev; }
 };
 
 // The host pool's home for a process driving `device`: an L3 domain among the CPUs local to
@@ -561,24 +588,14 @@ static std::vector<int> gpu_home_domain(int device) {
       }
   cpu_set_t allowed;
   if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return none;
-  std::vector<std::vector<int>> doms;
-  std::vector<int> keys;
-  for (int c : mine) {
-    if (c < 0 || c >= CPU_SETSIZE || !CPU_ISSET(c, &allowed)) continue;
-    const std::vector<int> l3 =
-        read_cpu_list("/sys/devices/system/cpu/cpu" + std::to_string(c) + "/cache/index3/shared_cpu_list");
-    const int key = l3.empty() ? c : l3.front();
-    size_t q = 0;
-    while (q < keys.size() && keys[q] != key) ++q;
-    if (q == keys.size()) {
-      keys.push_back(key);
-      doms.emplace_back();
-    }
-    doms[q].push_back(c);
-  }
-  if (doms.empty() || share <= 0) return none;
-  // spread over the domains, keeping off the first (CPU 0's: interrupts and daemons)
-  return doms[std::min(doms.size() - 1, (size_t)(slot + 1) * doms.size() / (size_t)(share + 1))];
+  return choose_home_domain(
+      mine, slot, share,
+      [](int c) {
+        const std::vector<int> l3 =
+            read_cpu_list("/sys/devices/system/cpu/cpu" + std::to_string(c) + "/cache/index3/shared_cpu_list");
+        return l3.empty() ? c : l3.front();
+      },
+      [&](int c) { return c >= 0 && c < CPU_SETSIZE && CPU_ISSET(c, &allowed); });
 }
 
 // The calling thread on the core kept free of pool workers for the duration of an engine
@@ -629,6 +646,7 @@ struct SmWork {
   // norm_const2(w_j, v_j, m_j) of the prior density (sm:419-436 priors): a function of the
   // hyperparameters alone, computed once per (v, w, log-space mode)
   std::vector<double> prior_nc, prior_v, prior_w;
+  std::vector<int32_t> prior_att;
   std::vector<int> prior_err;
   int prior_log = -1;
   int64_t phi_prefetch = 0;   // stream slice generated ahead for the move's update_phi jobs
@@ -653,6 +671,7 @@ struct RngWindow {
 
 struct Ctx {
   int device = 0;
+  HostPool* hpool = nullptr;       // the host worker pool homed next to this GPU (HostPool::for_home)
   hipStream_t stream = nullptr;
   hipStream_t gstream = nullptr;   // random-stream generator
   hipStream_t cstream = nullptr;   // copies of stream states to the host (never queued behind a generator launch)
@@ -927,6 +946,7 @@ struct Ctx {
   std::vector<int> sperm;
 
   ~Ctx() {
+    PoolScope scope(hpool);          // a speculative job still open is joined on this context's pool
     try {
       cancel_ahead();
     } catch (...) {
@@ -4561,14 +4581,17 @@ int hdpm_ctx_create(int32_t device, hdpm_ctx** out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) return HDPM_E_NODEVICE;
   if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return HDPM_E_NODEVICE;
-  {
-    // the host pool's home next to this GPU, before the pool exists (one process per GPU)
-    static std::once_flag once;
-    std::call_once(once, [device] { hdpm::HostPool::home() = hdpm::gpu_home_domain(device); });
-  }
   auto* c = new (std::nothrow) Ctx();
   if (!c) return HDPM_E_ARG;
   c->device = device;
+  // the host pool homed next to this GPU: one pool per home domain, so contexts on GPUs with
+  // different homes in one process (an R session with replicas on two GPUs) do not share one
+  try {
+    c->hpool = &hdpm::HostPool::for_home(hdpm::gpu_home_domain(device));
+  } catch (...) {
+    delete c;
+    return HDPM_E_ARG;
+  }
   // the sweep's stream at the highest priority, the generator windows' side stream at the
   // lowest: a window's generation (~1 ms per 16 sweeps of draws) then takes the CUs the
   // sweep leaves (HDPM_STREAM_PRIO=0: default priorities)
@@ -4614,6 +4637,7 @@ const char* hdpm_last_error(const hdpm_ctx* h) {
 #define CTX_KEEP()                              \
   auto* ctx = reinterpret_cast<Ctx*>(h);        \
   if (!ctx) return HDPM_E_ARG;                  \
+  hdpm::PoolScope pool_scope_(ctx->hpool);      \
   (void)hipSetDevice(ctx->device);              \
   ctx->err.clear();
 // every entry point but the sweep and the iteration drops a prepared sweep first
@@ -4645,6 +4669,7 @@ int hdpm_rng_get_state(const hdpm_ctx* h, int32_t* s) {
   // the state is logically const; an adoption still in flight lands first
   auto* ctx = const_cast<Ctx*>(reinterpret_cast<const Ctx*>(h));
   if (!ctx || !s) return HDPM_E_ARG;
+  hdpm::PoolScope pool_scope_(ctx->hpool);
   GUARD({
     ctx->cancel_ahead();
     ctx->rng_sync();
@@ -4801,6 +4826,23 @@ int hdpm_get_pool_heads(hdpm_ctx* h, uint64_t* out, int64_t P) {
     return HDPM_OK;
   })
 }
+int hdpm_get_option(hdpm_ctx* h, int32_t option, double* value) {
+  CTX();
+  if (!value) return HDPM_E_ARG;
+  switch (option) {
+    case HDPM_OPT_HIG_LOGSPACE: *value = ctx->hig_log ? 1.0 : 0.0; return HDPM_OK;
+    case HDPM_OPT_PHI_DEVICE: *value = (double)ctx->phi_mode; return HDPM_OK;
+    case HDPM_OPT_PIPE_WAIT_US: *value = (double)ctx->pipe_limit_ticks * 0.01 * (ctx->pipe_host_check ? 1 : -1); return HDPM_OK;
+    case HDPM_OPT_FPG_WAIT_US: *value = (double)ctx->fpg_limit_ticks * 0.01; return HDPM_OK;
+    case HDPM_OPT_FPG_FAIL_AT: *value = (double)ctx->fpg_fail_at; return HDPM_OK;
+    case HDPM_OPT_EXACT_KERNEL: *value = (double)ctx->exact_pref; return HDPM_OK;
+    case HDPM_OPT_LAT_NEGLIGIBLE: *value = ctx->lat_negl; return HDPM_OK;
+    case HDPM_OPT_SM_WIDE_WAIT_US: *value = (double)ctx->sm_wide_ticks * 0.01; return HDPM_OK;
+    default:
+      ctx->err = "unknown option";
+      return HDPM_E_ARG;
+  }
+}
 int hdpm_set_option(hdpm_ctx* h, int32_t option, double value) {
   CTX();
   switch (option) {
@@ -4832,8 +4874,9 @@ int hdpm_set_option(hdpm_ctx* h, int32_t option, double value) {
       ctx->lat_negl = value;
       return HDPM_OK;
     case HDPM_OPT_SM_WIDE_WAIT_US:
-      if (!(value >= 0.0) || !std::isfinite(value)) { ctx->err = "wide scan wait must be >= 0 us"; return HDPM_E_ARG; }
-      ctx->sm_wide_ticks = (long long)(value * 100.0);
+      if (!(value >= 0.0) || !(value <= 1e9)) { ctx->err = "wide scan wait must be in [0, 1e9] us"; return HDPM_E_ARG; }
+      GUARD(ctx->cancel_ahead();)
+      ctx->sm_wide_ticks = (long long)(value * 100.0);   // 0: every wide scan gives up at its first barrier
       return HDPM_OK;
     case HDPM_OPT_PIPE_WAIT_US:
       if (value == 0.0 || !std::isfinite(value)) { ctx->err = "pipe wait limit must be non-zero"; return HDPM_E_ARG; }

@@ -4839,7 +4839,12 @@ __global__ __launch_bounds__(kSmWideChunk) void k_sm_scan_wide(SmArgs a) {
       if (lane == 0) __hip_atomic_store(dl + (r & 1) * G + c, n1 - nstart, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
-    if (tid == 0) {
+    if (tid == 0 && a.wide_limit <= 0) {
+      // a zero limit gives up at the first barrier unconditionally (deterministic: the
+      // give-up test must not depend on how fast the workgroups arrive)
+      __hip_atomic_store(gave_up, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_state = -1;
+    } else if (tid == 0) {
       // grid barrier r: arrivals counted, agent-scope release / acquire
       __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       const long long t0 = wall_clock64();

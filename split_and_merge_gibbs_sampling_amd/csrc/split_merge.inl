@@ -426,7 +426,10 @@ static void sm_freq_device(Ctx* c, SmWork& W, int nS, const int* side, int want,
   HIPCHK(hipStreamSynchronize(c->stream));
   const int32_t* h = (const int32_t*)W.h_freq.p;
   int nn = 0;
-  for (int l = 0; l < c->mmax; ++l) nn += h[l];    // every point has a code at attribute 0
+  // every counted point has a code in 1..m_0 at attribute 0, so row 0 sums to the point count:
+  // this relies on Ctx::set_data rejecting code 0 ("codes must lie in 1..attrisize[j]") and on
+  // k_sm_freq counting every code >= 1.  If codes ever admit 0 (NA), count the points here.
+  for (int l = 0; l < c->mmax; ++l) nn += h[l];
   if (side_prev) {
     for (size_t e = 0; e < nt; ++e) F.f[e] += (double)h[e];
     F.nn += nn;
@@ -709,11 +712,15 @@ static double loglikelihood_hamming(Ctx* c, const HState& s, int k, const Freq& 
 }
 
 // sm:419-436.  Its normalising constants norm_const2(w_j, v_j, m_j) depend on the
-// hyperparameters only: computed once (SmWork::prior_nc) and reused by every move.
+// hyperparameters and attribute sizes only: computed once (SmWork::prior_nc) and reused by
+// every move.
 static double priors(Ctx* c, const HState& s, int k, int* err) {
   SmWork& W = smwork(c);
   const int d = c->d;
-  if (W.prior_log != (int)c->hig_log || W.prior_v != c->v || W.prior_w != c->w || (int)W.prior_nc.size() != d) {
+  // keyed on every input of norm_const2: v, w, the attribute sizes m_j and the 2F1 mode (a
+  // second set_data with the same v / w but other m_j must not reuse the constants)
+  if (W.prior_log != (int)c->hig_log || W.prior_v != c->v || W.prior_w != c->w || W.prior_att != c->att ||
+      (int)W.prior_nc.size() != d) {
     W.prior_nc.assign(d, 0.0);
     W.prior_err.assign(d, 0);
     per_attribute(c, [&](int j) {
@@ -723,6 +730,7 @@ static double priors(Ctx* c, const HState& s, int k, int* err) {
     });
     W.prior_v = c->v;
     W.prior_w = c->w;
+    W.prior_att = c->att;
     W.prior_log = (int)c->hig_log;
   }
   const double* sig = &s.sigma[(size_t)k * d];

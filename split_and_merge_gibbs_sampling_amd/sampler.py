@@ -208,6 +208,17 @@ class Engine:
         """update_phi on the device (include/hdpm.h HDPM_OPT_PHI_DEVICE); same chain."""
         self._check(self._L.hdpm_set_option(self._h, _lib.OPT_PHI_DEVICE, 1.0 if on else 0.0))
 
+    def get_option(self, option: int) -> float:
+        """The current value of an include/hdpm.h HDPM_OPT_* option (hdpm_get_option)."""
+        v = C.c_double()
+        self._check(self._L.hdpm_get_option(self._h, int(option), C.byref(v)))
+        return float(v.value)
+
+    @property
+    def phi_device(self) -> bool:
+        """True when update_phi runs on the device (HDPM_OPT_PHI_DEVICE, default or set)."""
+        return self.get_option(_lib.OPT_PHI_DEVICE) != 0.0
+
     def set_pipe_wait_us(self, us: float):
         """Testing (include/hdpm.h HDPM_OPT_PIPE_WAIT_US): the wait limit of a sweep enqueued
         ahead; negative: no host-side check (exercises the device gate-off recovery)."""

@@ -828,6 +828,32 @@ def test_split_merge_chain_wide_scan_and_give_up(hd, oracle, wait_us):
         assert stats["sm_wide_fallbacks"] == 0, stats
 
 
+def test_split_merge_second_dataset_other_attrisize(hd, oracle):
+    """One engine, two data sets with the same d, v and w but other attribute sizes m_j: the
+    split-merge priors' normalising constants norm_const2(w_j, v_j, m_j) (sm:419-436) must
+    follow the new m_j (the cache was keyed on v / w only)."""
+    kw = dict(m=3, iterations=4, L=1, burnin=0, t=3, r=3, neal8=True, split_merge=True)
+    da = synth(900, 16, 3, 2, seed=61)
+    db = synth(900, 16, 3, 5, seed=62)
+    assert np.array_equal(da.v, db.v) and np.array_equal(da.w, db.w)
+    eng = make_engine(hd, da)
+    try:
+        eng.set_seed(9)
+        eng.run_markov_chain(c_i=da.truth, **kw)
+        assert eng.stats()["sm_moves"] > 0
+        eng.set_data(db.codes, db.attrisize, db.gamma, db.v, db.w)
+        eng.set_seed(10)
+        res = eng.run_markov_chain(c_i=db.truth, **kw)
+    finally:
+        eng.close()
+    st, ref = oracle.run_markov_chain(db.codes, db.attrisize, db.gamma, db.v, db.w, seed=10, c_i=db.truth,
+                                      fast=1, **kw)
+    assert st == 0
+    assert np.array_equal(res["c_i"], ref["c_i"])
+    assert np.array_equal(res["accepted"], ref["accepted"])
+    np.testing.assert_allclose(res["loglikelihood"], ref["loglikelihood"], rtol=RTOL, atol=0)
+
+
 def test_restricted_gibbs_random_split_of_one_cluster(hd, oracle):
     # The split proposal's launch state: one true cluster's members dealt at random to two
     # labels with fresh parameters, so most scan draws are close calls whose pick depends

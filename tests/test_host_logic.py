@@ -49,3 +49,16 @@ def test_pool_pipeline_model_matches_sequential_generator(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "pool pipeline ok" in r.stdout
+
+
+def test_host_pool_home_domain_choice(tmp_path):
+    """csrc/host_topology.hpp: the L3 domain a context's host pool is homed on (one pool per
+    home, engine.cpp HostPool::for_home), on synthetic node topologies."""
+    exe = tmp_path / "host_topology_test"
+    src = os.path.join(HERE, "cpp", "host_topology_test.cpp")
+    r = subprocess.run(["g++", "-O2", "-std=c++17", "-o", str(exe), src], capture_output=True, text=True)
+    if r.returncode != 0:
+        pytest.fail(r.stderr)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "host topology ok" in r.stdout
