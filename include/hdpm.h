@@ -108,6 +108,9 @@ typedef struct {
     /* split-merge restricted scans walked on many CUs (k_sm_scan_wide), and those that gave up
      * (grid not resident) and ran on one workgroup */
     int64_t sm_wide_scans, sm_wide_fallbacks;
+    /* device update_phi calls enqueued on the fast path (csrc/phi.hip launch_phi2: every pick
+     * fixed, no copies), and those of them handed to the general kernels or the host */
+    int64_t phi_fast_calls, phi_fast_handbacks;
 } hdpm_stats;
 
 int         hdpm_device_count(void);

@@ -74,7 +74,7 @@ class Stats(C.Structure):
                                   "fpg_launches", "phi_sm_device_calls", "phi_fallback_status_mask",
                                   "phi_sm_window_retries", "fpg_aborts", "exact_mass_launches",
                                   "exact_lanes_launches", "dense_launches", "sm_wide_scans",
-                                  "sm_wide_fallbacks")]
+                                  "sm_wide_fallbacks", "phi_fast_calls", "phi_fast_handbacks")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -80,6 +80,10 @@ hipError_t launch_debug_math(const double* x, int64_t n, int fn, int ocml, doubl
 hipError_t launch_lmatrix(const uint8_t* codes_t, int n, int d, int nq, ParamTables cl, int K, double* L,
                           int* H, int64_t ldL, hipStream_t s);
 hipError_t launch_phi(const PhiArgs& a, hipStream_t s);
+hipError_t launch_phi2(const PhiArgs& a, hipStream_t s);
+size_t phi2_group_lds_bytes(int gs, int nw, double rate);
+size_t phi2_tree_lds_bytes(int T, int G, int tW);
+size_t phi2_values_lds_bytes(int d, int G, int tW);
 size_t phi_cwalk_lds(int d, int nw, int wpb);
 size_t phi_values_lds(int d, int nw);
 size_t phi_tree_lds_bytes(int SB, int nw, int W);
@@ -3520,6 +3524,14 @@ struct Ctx {
     DevBuf<int> F;
     DevBuf<uint16_t> tree;             // composition trees (tree mode)
     DevBuf<int> tnd;                   // per cluster: a pick depends on the uniform
+    // fast path (launch_phi2): group and cluster tables, last-workgroup counters, the status
+    // generation, and the inputs / outputs in coherent host memory (the kernels read and write
+    // them directly: no copy commands on the update's path)
+    DevBuf<uint16_t> gtab2, roots;
+    DevBuf<int> ctr;
+    int gen = 0;
+    PinBuf<uint8_t> h_in2, h_out2;
+    int64_t fast_calls = 0;
     // tree mode when every updated cluster has at least this many members (a small cluster's
     // center picks can depend on the uniform); raised past a cluster size that needed a retry
     int tree_min_count = 16;
@@ -3543,7 +3555,9 @@ struct Ctx {
   // debug bit 19 (value 524288) forces the host.
   int phi_mode = [] {
     const char* e = std::getenv("HDPM_PHI");
-    return e && std::strcmp(e, "device") == 0 ? 1 : 0;
+    if (e && std::strcmp(e, "device") == 0) return 1;
+    if (e && std::strcmp(e, "device-general") == 0) return 2;
+    return 0;
   }();
   bool host_spec() const { return phi_mode == 0 || (debug & 524288); }
   double dev_ll = 0.0;                 // compute_loglikelihood from the last full device update
@@ -3600,6 +3614,9 @@ struct Ctx {
     // cluster, tSB blocks per workgroup, tS workgroups per cluster, tpc tables per cluster
     bool tree_ok = false;
     int tW = 0, tnb = 0, tSB = 0, tS = 0, tpc = 0, root_lds = 0;
+    // fast path (launch_phi2): groups of gs items, G per cluster
+    bool fast_ok = false;
+    int gs = 0, G = 0;
   };
   PhiPlan phi_plan(int T, bool sm = false) const {
     PhiPlan pl;
@@ -3636,6 +3653,19 @@ struct Ctx {
     pl.root_lds = phi_values2_lds_bytes(d, pl.tnb, T, pl.tW, pl.nw) <= 150 * 1024 ? 1 : 0;
     pl.tree_ok = pl.tW >= 64 && phi_tree_lds_bytes(pl.tSB, pl.nw, pl.tW) <= 150 * 1024 && pl.root_lds &&
                  pl.tW < 65535;
+    // fast path: the smallest group (most workgroups for the masks) whose cluster of group
+    // tables fits one workgroup's LDS
+    if (pl.tW >= 64 && pl.tW < 65535)
+      for (int gs = 8; gs <= 64; gs *= 2) {
+        const int G = (d + gs - 1) / gs;
+        if (phi2_tree_lds_bytes(T, G, pl.tW) <= 150 * 1024 && phi2_values_lds_bytes(d, G, pl.tW) <= 140 * 1024 &&
+            phi2_group_lds_bytes(gs, pl.nw, pl.rate) <= 150 * 1024) {
+          pl.fast_ok = true;
+          pl.gs = gs;
+          pl.G = G;
+          break;
+        }
+      }
     return pl;
   }
   // scratch of a plan, and the arguments every call shares (the caller sets raw, labels /
@@ -3674,7 +3704,90 @@ struct Ctx {
       phd.tnd.ensure(T);
     }
     a.tnd = phd.tnd.p;
+    a.gs = 0; a.G = 0; a.gtab2 = nullptr; a.roots = nullptr; a.ctr = nullptr; a.gen = 0; a.status_host = nullptr;
     return a;
+  }
+
+  // phi_mode 1: the fast path first where the plan allows it; 2: the general kernels only
+  bool phi_fast(const PhiPlan& pl) const { return pl.fast_ok && phi_mode == 1; }
+
+  // Enqueue one device update of T clusters on stream s: labels / counts / current sigmas in,
+  // status + consumption, picks, sigmas and log-likelihood pairs out (phi_out_layout) in the
+  // returned host buffer, complete once s reaches this point.  mode 2: the fast path
+  // (launch_phi2: inputs and outputs in coherent host memory, no copy or fill commands);
+  // 1: the general kernels with composition trees; 0: with the per-start-drift walks (both
+  // with copies and fills around launch_phi).
+  const uint8_t* enqueue_phi(PhiArgs& a, const PhiPlan& pl, int mode, const int* lab, const int* cnt,
+                             const double* sig_in, hipStream_t s) {
+    const int T = pl.T;
+    const int64_t items = pl.items;
+    size_t o_pick, o_sig, o_ll, bytes;
+    phi_out_layout(T, d, &o_pick, &o_sig, &o_ll, &bytes);
+    phd.status.ensure(4);
+    phd.stage.ensure(upload_layout(T, dp, d, bw).bytes);
+    a.status = phd.status.p;
+    a.stage = phd.stage.p;
+    const size_t o_sigin = align16((size_t)2 * T * 4), in_bytes = o_sigin + (size_t)items * 8;
+    if (mode == 2) {
+      phd.h_in2.ensure(in_bytes + 64, hipHostMallocCoherent);
+      phd.h_out2.ensure(bytes + 64, hipHostMallocCoherent);
+      if (!phd.ctr.p) {
+        phd.ctr.ensure(2);
+        HIPCHK(hipMemset(phd.ctr.p, 0, 2 * sizeof(int)));
+      }
+      phd.gtab2.ensure((size_t)T * pl.G * pl.tW);
+      phd.roots.ensure((size_t)T * pl.tW);
+      if (++phd.gen >= (1 << 26)) {                      // generations only grow: restart from 1
+        HIPCHK(hipStreamSynchronize(s));
+        HIPCHK(hipMemset(phd.status.p, 0, 16));
+        phd.gen = 1;
+      }
+      int* hl = (int*)phd.h_in2.p;
+      std::memcpy(hl, lab, (size_t)T * 4);
+      std::memcpy(hl + T, cnt, (size_t)T * 4);
+      std::memcpy(phd.h_in2.p + o_sigin, sig_in, (size_t)items * 8);
+      ((volatile int*)phd.h_out2.p)[0] = -1;           // (written by the last k_phi2_values workgroup)
+      a.lab = hl; a.cnt = hl + T; a.sig_in = (const double*)(phd.h_in2.p + o_sigin);
+      a.pick = phd.h_out2.p + o_pick;
+      a.sig_out = (double*)(phd.h_out2.p + o_sig);
+      a.ll = (double*)(phd.h_out2.p + o_ll);
+      a.status_host = (int*)phd.h_out2.p;
+      a.gs = pl.gs; a.G = pl.G; a.gtab2 = phd.gtab2.p; a.roots = phd.roots.p; a.ctr = phd.ctr.p; a.gen = phd.gen;
+      a.tree = nullptr;
+      a.lg = nullptr; a.lzz = nullptr;                   // the fast path computes its logits itself
+      HIPCHK(launch_phi2(a, s));
+      phd.fast_calls++;
+      stats.phi_fast_calls++;
+      return phd.h_out2.p;
+    }
+    phd.h_in.ensure(in_bytes + 64);
+    phd.h_out.ensure(bytes);
+    int* hl = (int*)phd.h_in.p;
+    std::memcpy(hl, lab, (size_t)T * 4);
+    std::memcpy(hl + T, cnt, (size_t)T * 4);
+    std::memcpy(phd.h_in.p + o_sigin, sig_in, (size_t)items * 8);
+    phd.lab_cnt.ensure(2 * T);
+    phd.sig_in.ensure(items);
+    phd.sig_out.ensure(items);
+    phd.ll.ensure(2 * T);
+    phd.pick.ensure(items);
+    HIPCHK(hipMemcpyAsync(phd.lab_cnt.p, hl, (size_t)2 * T * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(phd.sig_in.p, phd.h_in.p + o_sigin, (size_t)items * 8, hipMemcpyHostToDevice, s));
+    a.lab = phd.lab_cnt.p; a.cnt = phd.lab_cnt.p + T; a.sig_in = phd.sig_in.p;
+    a.pick = phd.pick.p; a.sig_out = phd.sig_out.p; a.ll = phd.ll.p;
+    a.status_host = nullptr;
+    a.gen = 0;
+    a.lg = phd.lg.p; a.lzz = phd.lzz.p;
+    a.tree = mode == 1 ? phd.tree.p : nullptr;
+    if (mode == 1) HIPCHK(hipMemsetAsync(phd.tnd.p, 0, (size_t)T * 4, s));
+    HIPCHK(hipMemsetAsync(phd.status.p, 0, 16, s));
+    HIPCHK(hipMemsetAsync(phd.act.p, 0, 4, s));
+    HIPCHK(launch_phi(a, s));
+    HIPCHK(hipMemcpyAsync(phd.h_out.p, phd.status.p, 16, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(phd.h_out.p + o_pick, phd.pick.p, (size_t)items, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(phd.h_out.p + o_sig, phd.sig_out.p, (size_t)items * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(phd.h_out.p + o_ll, phd.ll.p, (size_t)2 * T * 8, hipMemcpyDeviceToHost, s));
+    return phd.h_out.p;
   }
 
   int device_update_phi(const std::vector<unsigned char>& mask, int nidx) {
@@ -3699,76 +3812,64 @@ struct Ctx {
     histogram_launch(nidx == 0 ? nullptr : &mask);
     const unsigned* fsrc = nidx == 0 ? d_freq.p : d_freq_m.p;
     // inputs: labels, counts, current sigmas
-    const size_t in_bytes = (size_t)2 * T * 4 + (size_t)items * 8;
-    phd.h_in.ensure(in_bytes + 64);
-    int* hl = (int*)phd.h_in.p;
-    double* hs = (double*)(phd.h_in.p + align16((size_t)2 * T * 4));
+    std::vector<int> labs(T), cnts(T);
+    std::vector<double> sigs((size_t)items);
     for (int t = 0; t < T; ++t) {
-      hl[t] = touched[t];
-      hl[T + t] = h_counts[touched[t]];
-      std::memcpy(hs + (size_t)t * d, &h_sigma[(size_t)touched[t] * d], (size_t)d * 8);
+      labs[t] = touched[t];
+      cnts[t] = h_counts[touched[t]];
+      std::memcpy(&sigs[(size_t)t * d], &h_sigma[(size_t)touched[t] * d], (size_t)d * 8);
     }
-    phd.lab_cnt.ensure(2 * T);
-    phd.sig_in.ensure(items);
-    phd.sig_out.ensure(items);
-    phd.ll.ensure(2 * T);
-    phd.pick.ensure(items);
-    phd.status.ensure(4);
-    const UploadLayout L = upload_layout(T, dp, d, bw);
-    phd.stage.ensure(L.bytes);
-    HIPCHK(hipMemcpyAsync(phd.lab_cnt.p, hl, (size_t)2 * T * 4, hipMemcpyHostToDevice, stream));
-    HIPCHK(hipMemcpyAsync(phd.sig_in.p, hs, (size_t)items * 8, hipMemcpyHostToDevice, stream));
     HIPCHK(hipStreamWaitEvent(stream, W->done, 0));
-    a.lab = phd.lab_cnt.p; a.cnt = phd.lab_cnt.p + T; a.freq = fsrc; a.sig_in = phd.sig_in.p;
+    a.freq = fsrc;
     a.raw = W->raw.p + (rng.pos - W->start_pos);
     a.nraw = (int64_t)(W->start_pos + (uint64_t)W->count - rng.pos);
-    a.pick = phd.pick.p; a.status = phd.status.p;
-    a.stage = phd.stage.p; a.sig_out = phd.sig_out.p; a.ll = phd.ll.p;
-    // results: status + consumption, picks, sigmas, log-likelihood terms
-    const size_t o_pick = 16, o_sig = align16(o_pick + (size_t)items), o_ll = o_sig + (size_t)items * 8;
-    phd.h_out.ensure(o_ll + (size_t)2 * T * 8);
-    auto run = [&](bool tree) {
-      a.tree = tree ? phd.tree.p : nullptr;
-      if (tree) HIPCHK(hipMemsetAsync(phd.tnd.p, 0, (size_t)T * 4, stream));
-      HIPCHK(hipMemsetAsync(phd.status.p, 0, 16, stream));
-      HIPCHK(hipMemsetAsync(phd.act.p, 0, 4, stream));
-      HIPCHK(launch_phi(a, stream));
-      HIPCHK(hipMemcpyAsync(phd.h_out.p, phd.status.p, 16, hipMemcpyDeviceToHost, stream));
-      HIPCHK(hipMemcpyAsync(phd.h_out.p + o_pick, phd.pick.p, (size_t)items, hipMemcpyDeviceToHost, stream));
-      HIPCHK(hipMemcpyAsync(phd.h_out.p + o_sig, phd.sig_out.p, (size_t)items * 8, hipMemcpyDeviceToHost, stream));
-      HIPCHK(hipMemcpyAsync(phd.h_out.p + o_ll, phd.ll.p, (size_t)2 * T * 8, hipMemcpyDeviceToHost, stream));
-    };
-    // the composition trees unless a cluster is small enough for a pick to depend on the
-    // uniform (debug bit 27: always the per-start-drift walks)
+    size_t o_pick, o_sig, o_ll, obytes;
+    phi_out_layout(T, d, &o_pick, &o_sig, &o_ll, &obytes);
+    const uint8_t* out = nullptr;
+    auto run = [&](int mode) { out = enqueue_phi(a, pl, mode, labs.data(), cnts.data(), sigs.data(), stream); };
+    // the fast path, else the composition trees unless a cluster is small enough for a pick to
+    // depend on the uniform (debug bit 27: always the per-start-drift walks)
     int min_count = INT_MAX;
-    for (int t = 0; t < T; ++t) min_count = std::min(min_count, hl[T + t]);
+    for (int t = 0; t < T; ++t) min_count = std::min(min_count, cnts[t]);
     // (with one walk segment per cluster, d <= 128, such clusters are walked inside the tree-mode
     // update itself)
     const bool tree = pl.tree_ok && (pl.S == 1 || min_count >= phd.tree_min_count) && !(debug & 134217728);
-    run(tree);
+    const bool fast = phi_fast(pl) && min_count >= phd.tree_min_count && !(debug & 134217728);
+    run(fast ? 2 : tree ? 1 : 0);
     histogram_wait(nidx == 0 ? nullptr : &mask);
     if (freq_next_pending) {
       std::swap(h_freq.p, h_freq_next.p);
       std::swap(h_freq.n, h_freq_next.n);
       freq_next_pending = false;
     }
+    HIPCHK(hipStreamSynchronize(stream));
     phd.calls++;
-    if (tree) stats.phi_tree_calls++;
-    if (tree && ((const int*)phd.h_out.p)[0] == kPhiNonDet) {
+    if (tree && !fast) stats.phi_tree_calls++;
+    if (std::getenv("HDPM_PHI_TRACE"))
+      std::fprintf(stderr, "[phi] T %d nw %d tW %d fast_ok %d gs %d G %d min_count %d tree_min %d fast %d tree %d status %d\n",
+                   T, pl.nw, pl.tW, (int)pl.fast_ok, pl.gs, pl.G, min_count, phd.tree_min_count, (int)fast, (int)tree,
+                   ((const int*)out)[0]);
+    if (fast && ((const int*)out)[0] != kPhiOk) stats.phi_fast_handbacks++;
+    if ((fast || tree) && ((const int*)out)[0] == kPhiNonDet) {
       // a pick depends on the uniform: the same update by the walks (same inputs, nothing
       // committed yet); updates with clusters this small take the walks directly from now on
       phd.tree_min_count = std::max(phd.tree_min_count, std::min(1 << 20, 2 * min_count));
       stats.phi_tree_retries++;
-      run(false);
+      run(0);
+      HIPCHK(hipStreamSynchronize(stream));
+    } else if (fast && ((const int*)out)[0] != kPhiOk && ((const int*)out)[0] != kPhiWindow &&
+               ((const int*)out)[0] != kPhiShort) {
+      // a case the fast path leaves to the general kernels (the bisection path, ...)
+      run(tree ? 1 : 0);
       HIPCHK(hipStreamSynchronize(stream));
     }
-    const int status = ((const int*)phd.h_out.p)[0];
+    const int status = ((const int*)out)[0];
     stats.phi_device_last_status = status;
     int64_t cons = 0;
-    std::memcpy(&cons, phd.h_out.p + 8, 8);
+    std::memcpy(&cons, out + 8, 8);
     phd.last_status = status;
     const uint64_t target = rng.pos + (uint64_t)cons;
-    if (debug & 2) {
+    if ((debug & 2) && !fast) {
       std::vector<int64_t> dts(T);
       HIPCHK(hipMemcpy(dts.data(), phd.dts.p, (size_t)T * 8, hipMemcpyDeviceToHost));
       std::vector<int> F((size_t)T * pl.S * pl.Wc);
@@ -3801,9 +3902,9 @@ struct Ctx {
     HIPCHK(launch_scatter_clusters(phd.stage.p, T, dp, d, bw, full ? 1 : 0, d_slot_codes.p, d_slot_tab.p, d_slot_bnd.p,
                                    d_counts.p, d_sol.p, d_los.p, d_src.p, stream));
     phd_release(stream);
-    const uint8_t* pk = phd.h_out.p + o_pick;
-    const double* sg = (const double*)(phd.h_out.p + o_sig);
-    const double* ll = (const double*)(phd.h_out.p + o_ll);
+    const uint8_t* pk = out + o_pick;
+    const double* sg = (const double*)(out + o_sig);
+    const double* ll = (const double*)(out + o_ll);
     double hi = 0.0, lo = 0.0;
     for (int t = 0; t < T; ++t) {
       const int k = touched[t];
@@ -3847,10 +3948,12 @@ struct Ctx {
     RngWindow* W = nullptr;
     bool tree = false;
     size_t o_pick = 0, o_sig = 0, o_ll = 0;
-    hipEvent_t ev = nullptr;           // its outputs are in phd.h_out
+    const uint8_t* out = nullptr;      // its outputs (phd.h_out, or phd.h_out2 on the fast path)
+    bool fast = false;
+    hipEvent_t ev = nullptr;           // they are complete
   } dspec;
   hipEvent_t ev_phd_free = nullptr;    // the last device use of phd's buffers on `stream` is done
-  bool dspec_on() const { return phi_mode == 1 && !(debug & (524288 | 64 | 128)); }
+  bool dspec_on() const { return phi_mode != 0 && !(debug & (524288 | 64 | 128)); }
   void phd_release(hipStream_t s) {
     if (!ev_phd_free) HIPCHK(hipEventCreateWithFlags(&ev_phd_free, hipEventDisableTiming));
     HIPCHK(hipEventRecord(ev_phd_free, s));
@@ -3885,46 +3988,19 @@ struct Ctx {
     dspec_wait();                      // phd.h_in / h_out are free on the host
     PhiArgs a = phi_args(pl);
     const int T = K;
-    const int64_t items = pl.items;
-    const size_t in_bytes = (size_t)2 * T * 4 + (size_t)items * 8;
-    phd.h_in.ensure(in_bytes + 64);
-    int* hl = (int*)phd.h_in.p;
-    double* hs = (double*)(phd.h_in.p + align16((size_t)2 * T * 4));
-    for (int t = 0; t < T; ++t) {
-      hl[t] = t;
-      hl[T + t] = h_counts[t];
-    }
-    std::memcpy(hs, h_sigma.data(), (size_t)items * 8);
-    phd.lab_cnt.ensure(2 * T);
-    phd.sig_in.ensure(items);
-    phd.sig_out.ensure(items);
-    phd.ll.ensure(2 * T);
-    phd.pick.ensure(items);
-    phd.status.ensure(4);
-    phd.stage.ensure(upload_layout(T, dp, d, bw).bytes);
     size_t bytes;
     phi_out_layout(T, d, &dspec.o_pick, &dspec.o_sig, &dspec.o_ll, &bytes);
-    phd.h_out.ensure(bytes);
+    std::vector<int> labs(T);
+    for (int t = 0; t < T; ++t) labs[t] = t;
     if (!dspec.ev) HIPCHK(hipEventCreateWithFlags(&dspec.ev, hipEventDisableTiming));
     HIPCHK(hipStreamWaitEvent(pstream, W->done, 0));
     if (ev_phd_free) HIPCHK(hipStreamWaitEvent(pstream, ev_phd_free, 0));
-    HIPCHK(hipMemcpyAsync(phd.lab_cnt.p, hl, (size_t)2 * T * 4, hipMemcpyHostToDevice, pstream));
-    HIPCHK(hipMemcpyAsync(phd.sig_in.p, hs, (size_t)items * 8, hipMemcpyHostToDevice, pstream));
-    a.lab = phd.lab_cnt.p; a.cnt = phd.lab_cnt.p + T; a.freq = d_freq.p; a.sig_in = phd.sig_in.p;
+    a.freq = d_freq.p;
     a.raw = W->raw.p + (rng.pos - W->start_pos);
     a.nraw = (int64_t)(W->start_pos + (uint64_t)W->count - rng.pos);
-    a.pick = phd.pick.p; a.status = phd.status.p;
-    a.stage = phd.stage.p; a.sig_out = phd.sig_out.p; a.ll = phd.ll.p;
     const bool tree = pl.tree_ok && (pl.S == 1 || min_count >= phd.tree_min_count) && !(debug & 134217728);
-    a.tree = tree ? phd.tree.p : nullptr;
-    if (tree) HIPCHK(hipMemsetAsync(phd.tnd.p, 0, (size_t)T * 4, pstream));
-    HIPCHK(hipMemsetAsync(phd.status.p, 0, 16, pstream));
-    HIPCHK(hipMemsetAsync(phd.act.p, 0, 4, pstream));
-    HIPCHK(launch_phi(a, pstream));
-    HIPCHK(hipMemcpyAsync(phd.h_out.p, phd.status.p, 16, hipMemcpyDeviceToHost, pstream));
-    HIPCHK(hipMemcpyAsync(phd.h_out.p + dspec.o_pick, phd.pick.p, (size_t)items, hipMemcpyDeviceToHost, pstream));
-    HIPCHK(hipMemcpyAsync(phd.h_out.p + dspec.o_sig, phd.sig_out.p, (size_t)items * 8, hipMemcpyDeviceToHost, pstream));
-    HIPCHK(hipMemcpyAsync(phd.h_out.p + dspec.o_ll, phd.ll.p, (size_t)2 * T * 8, hipMemcpyDeviceToHost, pstream));
+    const bool fast = phi_fast(pl) && min_count >= phd.tree_min_count && !(debug & 134217728);
+    dspec.out = enqueue_phi(a, pl, fast ? 2 : tree ? 1 : 0, labs.data(), h_counts.data(), h_sigma.data(), pstream);
     HIPCHK(hipEventRecord(dspec.ev, pstream));
     dspec.ran = true;
     dspec.inflight = true;
@@ -3935,7 +4011,8 @@ struct Ctx {
     dspec.moves = -1;
     dspec.pl = pl;
     dspec.W = W;
-    dspec.tree = tree;
+    dspec.tree = tree && !fast;
+    dspec.fast = fast;
     stats.phi_dspec_launched++;
   }
 
@@ -3955,10 +4032,13 @@ struct Ctx {
     phd.calls++;
     if (dspec.tree) stats.phi_tree_calls++;
     const int T = dspec.K;
-    const int status = ((const int*)phd.h_out.p)[0];
+    const int status = ((const int*)dspec.out)[0];
+    if (dspec.fast && status != kPhiOk) stats.phi_fast_handbacks++;
+    if (std::getenv("HDPM_PHI_TRACE"))
+      std::fprintf(stderr, "[phi dspec] T %d fast %d status %d\n", T, (int)dspec.fast, status);
     stats.phi_device_last_status = status;
     int64_t cons = 0;
-    std::memcpy(&cons, phd.h_out.p + 8, 8);
+    std::memcpy(&cons, dspec.out + 8, 8);
     const uint64_t target = rng.pos + (uint64_t)cons;
     if (status == kPhiNonDet) {
       int mc = INT_MAX;
@@ -3982,9 +4062,9 @@ struct Ctx {
     } else {
       scatter_dev_stage(T);
     }
-    const uint8_t* pk = phd.h_out.p + dspec.o_pick;
-    const double* sg = (const double*)(phd.h_out.p + dspec.o_sig);
-    const double* ll = (const double*)(phd.h_out.p + dspec.o_ll);
+    const uint8_t* pk = dspec.out + dspec.o_pick;
+    const double* sg = (const double*)(dspec.out + dspec.o_sig);
+    const double* ll = (const double*)(dspec.out + dspec.o_ll);
     double hi = 0.0, lo = 0.0;
     for (int t = 0; t < T; ++t) {
       for (int j = 0; j < d; ++j) h_center[(size_t)t * d + j] = (uint8_t)(pk[(size_t)t * d + j] + 1);
@@ -4044,61 +4124,43 @@ struct Ctx {
     h_sm_freq.ensure(fw);
     d_sm_freq.ensure(fw);
     std::memcpy(h_sm_freq.p, freq, fw * 4);
-    const size_t in_bytes = (size_t)2 * T * 4 + (size_t)items * 8;
-    phd.h_in.ensure(in_bytes + 64);
-    int* hl = (int*)phd.h_in.p;
-    double* hs = (double*)(phd.h_in.p + align16((size_t)2 * T * 4));
+    std::vector<int> labs(T);
     int min_count = INT_MAX;
     for (int t = 0; t < T; ++t) {
-      hl[t] = t;
-      hl[T + t] = cnt[t];
+      labs[t] = t;
       min_count = std::min(min_count, cnt[t]);
     }
-    std::memcpy(hs, sig_in, (size_t)items * 8);
-    phd.lab_cnt.ensure(2 * T);
-    phd.sig_in.ensure(items);
-    phd.sig_out.ensure(items);
-    phd.ll.ensure(2 * T);
-    phd.pick.ensure(items);
-    phd.status.ensure(4);
-    phd.stage.ensure(upload_layout(T, dp, d, bw).bytes);
     size_t o_pick, o_sig, o_ll, bytes;
     phi_out_layout(T, d, &o_pick, &o_sig, &o_ll, &bytes);
-    phd.h_out.ensure(bytes);
     HIPCHK(hipMemcpyAsync(d_sm_freq.p, h_sm_freq.p, fw * 4, hipMemcpyHostToDevice, stream));
-    HIPCHK(hipMemcpyAsync(phd.lab_cnt.p, hl, (size_t)2 * T * 4, hipMemcpyHostToDevice, stream));
-    HIPCHK(hipMemcpyAsync(phd.sig_in.p, hs, (size_t)items * 8, hipMemcpyHostToDevice, stream));
     HIPCHK(hipStreamWaitEvent(stream, W->done, 0));
-    a.lab = phd.lab_cnt.p; a.cnt = phd.lab_cnt.p + T; a.freq = d_sm_freq.p; a.sig_in = phd.sig_in.p;
+    a.freq = d_sm_freq.p;
     a.raw = W->raw.p + (rng.pos - W->start_pos);
     a.nraw = (int64_t)(W->start_pos + (uint64_t)W->count - rng.pos);
-    a.pick = phd.pick.p; a.status = phd.status.p;
-    a.stage = phd.stage.p; a.sig_out = phd.sig_out.p; a.ll = phd.ll.p;
-    auto run = [&](bool tree) {
-      a.tree = tree ? phd.tree.p : nullptr;
-      if (tree) HIPCHK(hipMemsetAsync(phd.tnd.p, 0, (size_t)T * 4, stream));
-      HIPCHK(hipMemsetAsync(phd.status.p, 0, 16, stream));
-      HIPCHK(hipMemsetAsync(phd.act.p, 0, 4, stream));
-      HIPCHK(launch_phi(a, stream));
-      HIPCHK(hipMemcpyAsync(phd.h_out.p, phd.status.p, 16, hipMemcpyDeviceToHost, stream));
-      HIPCHK(hipMemcpyAsync(phd.h_out.p + o_pick, phd.pick.p, (size_t)items, hipMemcpyDeviceToHost, stream));
-      HIPCHK(hipMemcpyAsync(phd.h_out.p + o_sig, phd.sig_out.p, (size_t)items * 8, hipMemcpyDeviceToHost, stream));
+    const uint8_t* out = nullptr;
+    auto run = [&](int mode) {
+      out = enqueue_phi(a, pl, mode, labs.data(), cnt, sig_in, stream);
       HIPCHK(hipStreamSynchronize(stream));
     };
     const bool tree = pl.tree_ok && (pl.S == 1 || min_count >= phd.tree_min_count) && !(debug & 134217728);
-    run(tree);
+    const bool fast = phi_fast(pl) && min_count >= phd.tree_min_count && !(debug & 134217728);
+    run(fast ? 2 : tree ? 1 : 0);
     phd.calls++;
-    if (tree) stats.phi_tree_calls++;
-    if (tree && ((const int*)phd.h_out.p)[0] == kPhiNonDet) {
+    if (tree && !fast) stats.phi_tree_calls++;
+    if (fast && ((const int*)out)[0] != kPhiOk) stats.phi_fast_handbacks++;
+    if ((fast || tree) && ((const int*)out)[0] == kPhiNonDet) {
       phd.tree_min_count = std::max(phd.tree_min_count, std::min(1 << 20, 2 * min_count));
       stats.phi_tree_retries++;
-      run(false);
+      run(0);
+    } else if (fast && ((const int*)out)[0] != kPhiOk && ((const int*)out)[0] != kPhiWindow &&
+               ((const int*)out)[0] != kPhiShort) {
+      run(tree ? 1 : 0);
     }
     phd_release(stream);
-    const int status = ((const int*)phd.h_out.p)[0];
+    const int status = ((const int*)out)[0];
     stats.phi_device_last_status = status;
     int64_t cons = 0;
-    std::memcpy(&cons, phd.h_out.p + 8, 8);
+    std::memcpy(&cons, out + 8, 8);
     const uint64_t target = rng.pos + (uint64_t)cons;
     if (status != kPhiOk || cons <= 0 || !can_adopt(*W, target)) {
       stats.phi_fallback_status_mask |= (int64_t)1 << (status != kPhiOk ? std::min(std::max(status, 0), 14) : 15);
@@ -4122,9 +4184,9 @@ struct Ctx {
     }
     stats.phi_device_calls++;
     stats.phi_sm_device_calls++;
-    const uint8_t* pk = phd.h_out.p + o_pick;
+    const uint8_t* pk = out + o_pick;
     for (int64_t q = 0; q < items; ++q) cen[q] = (uint8_t)(pk[q] + 1);
-    std::memcpy(sig, phd.h_out.p + o_sig, (size_t)items * 8);
+    std::memcpy(sig, out + o_sig, (size_t)items * 8);
     adopt_state_at(*W, target);
     rng_sync();                        // split-merge draws on the host next
     PhiDevice::adapt(phd.p_rej_sm, cons - 3 * items, items, 0.9);
@@ -4850,8 +4912,9 @@ int hdpm_set_option(hdpm_ctx* h, int32_t option, double value) {
       ctx->hig_log = value != 0.0;
       return HDPM_OK;
     case HDPM_OPT_PHI_DEVICE:
+      if (!(value == 0.0 || value == 1.0 || value == 2.0)) { ctx->err = "phi device: 0 host, 1 device, 2 device (general kernels)"; return HDPM_E_ARG; }
       GUARD(ctx->cancel_ahead();)
-      ctx->phi_mode = value != 0.0 ? 1 : 0;
+      ctx->phi_mode = (int)value;
       return HDPM_OK;
     case HDPM_OPT_FPG_WAIT_US:
       if (!(value > 0.0) || !std::isfinite(value)) { ctx->err = "fpg wait limit must be positive"; return HDPM_E_ARG; }

@@ -494,6 +494,16 @@ struct PhiArgs {
   int tRootLds;              // (unused: the roots are always staged in LDS)
   int* tnd;                  // [T] cluster t has a pick that depends on the uniform: walked per start
                              // drift (k_phi_cwalk) into its root table, then from its drift (one wave)
+  // fast path (launch_phi2: k_phi2_group -> k_phi2_tree -> k_phi2_values), every pick fixed:
+  // groups of gs consecutive items of a cluster (G per cluster), each tabulated over tW start
+  // drifts by the workgroup that computes its masks; inputs and outputs may live in coherent
+  // host memory (no copies); status words tagged with the call's generation (no memset)
+  int gs, G;
+  uint16_t* gtab2;           // [T * G][tW] group tables
+  uint16_t* roots;           // [T][tW] cluster tables
+  int* ctr;                  // [2] last-workgroup counters of k_phi2_tree / k_phi2_values (self-resetting)
+  int gen;                   // status generation: status[0] = gen << 4 | code belongs to this call
+  int* status_host;          // [4] status (code, -, consumption int64) written by the last k_phi2_values workgroup
 };
 // Level sizes of a composition tree over nb >= 1 level-0 blocks.
 __host__ __device__ inline int phi_lcount(int nb, int l) { return ((nb - 1) >> l) + 1; }

@@ -55,6 +55,18 @@ __device__ __forceinline__ PoolClass as_pool(const PhiCand& c) {
 
 __device__ __forceinline__ void set_status(int* st, int code) { atomicMax(st, code); }
 
+// The update's status: plain codes (launch_phi: the status words are zeroed before the call),
+// or tagged with the call's generation (launch_phi2: gen << 4 | code, no zeroing; a word of an
+// earlier call reads as 0 -- generations only grow, so atomicMax keeps the current call's).
+__device__ __forceinline__ void phi_set_status(const PhiArgs& a, int code) {
+  atomicMax(a.status, a.gen > 0 ? (a.gen << 4) | code : code);
+}
+__device__ __forceinline__ int phi_get_status(const PhiArgs& a) {
+  const int v = __hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (a.gen <= 0) return v;
+  return (v >> 4) == a.gen ? (v & 15) : 0;
+}
+
 
 // Serial revsort (R sort.c) on one thread: a[0..n) descending with 1-based levels in ib.
 template <class PR, class PM>
@@ -828,10 +840,15 @@ __device__ __forceinline__ void phi_values_body(const PhiArgs& a, int t, const u
     const PoolClass C = as_pool(a.cand[(int64_t)t * a.sumatt + a.aoff[j] + pk]);
     const int64_t p = sapos[j];
     double x = 0.0;
-    if (!(p + 1 < a.span) ||
-        !phi_attempt(C, pool_unif(a.raw[p]), pool_unif(a.raw[p + 1]), a.lg[p], a.lzz[p], texp, tlog, &x) ||
-        x > C.thr)
+    if (!(p + 1 < a.span)) {
       bad = true;
+    } else {
+      const double u1 = pool_unif(a.raw[p]), u2 = pool_unif(a.raw[p + 1]);
+      // the stream logits from the tables, or (launch_phi2: no tables) the same expressions here
+      const double lg1 = a.lg ? a.lg[p] : glibc::log_r(u1 / (1.0 - u1), tlog);
+      const double lzz = a.lzz ? a.lzz[p] : glibc::log_r(u1 * u1 * u2, tlog);
+      if (!phi_attempt(C, u1, u2, lg1, lzz, texp, tlog, &x) || x > C.thr) bad = true;
+    }
     double sg, m0, m1;
     pool_sigma_tables(C, x, a.att[j], texp, tlog, &sg, &m0, &m1);
     codes[j] = (uint8_t)(pk + 1);
@@ -876,7 +893,7 @@ __device__ __forceinline__ void phi_values_body(const PhiArgs& a, int t, const u
   }
   __syncthreads();
   if (*sbad) {
-    if (threadIdx.x == 0) set_status(a.status, kPhiWindow);
+    if (threadIdx.x == 0) phi_set_status(a, kPhiWindow);
     return;
   }
   // the block's sums: A, scale (any order: only the bound's slack sees their rounding),
@@ -1237,6 +1254,383 @@ __global__ __launch_bounds__(1024) void k_phi_values2(PhiArgs a) {
     }
   }
   phi_values_body(a, t, spick, sapos, wtab, tabs, tabs + 256, red, wmx, wmn, &sbad);
+}
+
+// ------------------------------------------------------------------ fast path (launch_phi2)
+// The common case of a converged chain: every center pick of the update is fixed (its
+// cumulative probability reaches 1 at the first sorted level) and on rhig's beta path, so
+// item k's sigma draw is a function of the drift alone, f_k(delta) = delta + 2 (attempts its
+// mask rejects from delta on) -- the composition trees of k_phi_tree, laid out for latency:
+//
+//   k_phi2_group   one workgroup per group of gs consecutive items of a cluster: the items'
+//                  preparation (phi_prep_item), the stream logits of the positions the group
+//                  can read (in LDS), the items' masks over the window (LDS and maskd), and the
+//                  group's table: the extra uniforms of its gs items from each of tW start drifts
+//   k_phi2_tree    one workgroup per cluster: its group tables composed in LDS into the
+//                  cluster's table; the last workgroup to finish chains the cluster tables from
+//                  drift 0 (the clusters' start drifts, the consumption)
+//   k_phi2_values  one workgroup per cluster: its groups' start drifts (the group tables from
+//                  the cluster's start), each group walked by one wave (a lane per item,
+//                  fixed-point rounds over the prefetched mask words), then phi_values_body; the
+//                  last workgroup writes the status and the consumption for the host
+//
+// No copies: the labels, counts and sigmas can be read from (coherent) host memory and the
+// picks, sigmas and log-likelihood pairs written there; the status words carry the call's
+// generation instead of being zeroed.  Any case the fast path does not take (a pick that
+// depends on the uniform, the bisection path, an ambiguous branch test, a drift outside the
+// windows) is a status, and the caller runs launch_phi or the host job from the same stream
+// position; nothing else is committed.
+
+__host__ __device__ inline int phi2_npos(int gs, int nw, double rate) {
+  // positions a group can read: 2 (gs - 1) nominal steps, the growth of the window start over
+  // the group (<= rate (gs - 1) + 1), 64 nw drifts, the attempt's second uniform
+  return 2 * (gs - 1) + (int)(rate * (gs - 1)) + 2 + 64 * nw + 2;
+}
+__host__ __device__ inline size_t phi2_group_lds(int gs, int nw, double rate) {
+  return align16((size_t)gs * sizeof(PoolClass)) + align16((size_t)gs * 4) + align16((size_t)gs * nw * 8) +
+         align16((size_t)gs * kPhiLdsLevels * 8) + align16((size_t)gs * kPhiLdsLevels) +
+         3 * align16((size_t)phi2_npos(gs, nw, rate) * 8);
+}
+__host__ __device__ inline size_t phi2_tree_lds(int T, int G, int tW) {
+  const size_t a = (size_t)(G + (G + 1) / 2) * tW * 2, b = (size_t)T * tW * 2;
+  return align16(a > b ? a : b);
+}
+__host__ __device__ inline size_t phi2_values_lds(int d, int G, int tW) {
+  return align16((size_t)G * tW * 2) + align16((size_t)(G + 1) * 8) + align16((size_t)2 * d * 8) + align16((size_t)d * 8) +
+         align16((size_t)d);
+}
+
+__global__ __launch_bounds__(512) void k_phi2_group(PhiArgs a) {
+  if (gate_closed(a.gate)) return;
+  if (a.raw_ptr) a.raw = *a.raw_ptr;
+  extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+  __shared__ uint64_t tabs[512];
+  __shared__ int sbad;
+  const int gs = a.gs, G = a.G, d = a.d, nw = a.nw, tW = a.tW;
+  const int t = blockIdx.x / G, g = blockIdx.x - t * G;
+  const int j0 = g * gs, ni = min(gs, d - j0);
+  const int64_t k0 = (int64_t)t * d + j0;
+  PoolClass* sp = reinterpret_cast<PoolClass*>(sm);
+  int* slo = reinterpret_cast<int*>(sm + align16((size_t)gs * sizeof(PoolClass)));
+  uint64_t* smk = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(slo) + align16((size_t)gs * 4));
+  double* spr = reinterpret_cast<double*>(reinterpret_cast<uint8_t*>(smk) + align16((size_t)gs * nw * 8));
+  uint8_t* spm = reinterpret_cast<uint8_t*>(spr) + align16((size_t)gs * kPhiLdsLevels * 8);
+  const int npos = phi2_npos(gs, nw, a.rate);
+  double* su = reinterpret_cast<double*>(spm + align16((size_t)gs * kPhiLdsLevels));
+  double* slg = su + (align16((size_t)npos * 8) >> 3);
+  double* slz = slg + (align16((size_t)npos * 8) >> 3);
+  for (int i = threadIdx.x; i < 512; i += blockDim.x) tabs[i] = a.gtab[i];
+  if (threadIdx.x == 0) sbad = 0;
+  __syncthreads();
+  // 1. the items: center probabilities, fixed pick, rbeta setup (as k_phi_prep)
+  if ((int)threadIdx.x < ni) {
+    const int i = threadIdx.x, j = j0 + i;
+    const int64_t k = k0 + i;
+    const int mj = a.att[j], off = a.aoff[j];
+    bool det = false;
+    int nact = 0, status;
+    if (mj <= kPhiLdsLevels) {
+      status = phi_prep_item(a, t, j, k, spr + i * kPhiLdsLevels, spm + i * kPhiLdsLevels, tabs, &det, &nact);
+    } else {
+      status = phi_prep_item(a, t, j, k, a.cum + (int64_t)t * a.sumatt + off, a.perm + (int64_t)t * a.sumatt + off, tabs,
+                             &det, &nact);
+    }
+    if (!status && !det) status = kPhiNonDet;
+    if (!status) {
+      const int kd = a.ikind[k];
+      if (kd == 1) status = kPhiBisect;
+      else if (kd != 2 && kd != 3) status = kPhiInactive;
+    }
+    if (status) {
+      phi_set_status(a, status);
+      sbad = 1;
+    } else {
+      // the candidate of the fixed pick, written by this thread (phi_prep_item)
+      sp[i] = as_pool(a.cand[(int64_t)t * a.sumatt + off + a.det[k] - 1]);
+    }
+    slo[i] = (int)phi_lo(k, a.rate, a.sdev);
+  }
+  __syncthreads();
+  if (sbad) return;
+  // 2. the stream logits of every position the group's masks read
+  const int64_t nom0 = (int64_t)t * 3 * d + d + 2 * (int64_t)j0;
+  const int64_t p0 = nom0 + slo[0];
+  const int64_t plast = nom0 + 2 * (int64_t)(ni - 1) + slo[ni - 1] + 64 * (int64_t)nw;   // last attempt's first uniform
+  if (plast - p0 + 2 > npos) {                                // (window model: never)
+    if (threadIdx.x == 0) phi_set_status(a, kPhiWindow);
+    return;
+  }
+  const int np = (int)(plast - p0 + 2);
+  const uint64_t* tlog = tabs + 256;
+  for (int q = threadIdx.x; q < np; q += blockDim.x) {
+    const int64_t p = p0 + q;
+    double u = 0.5, lg = 0.0, lz = 0.0;
+    if (p < a.span + 1) u = pool_unif(a.raw[p]);
+    if (p < a.span) {
+      const double u2 = pool_unif(a.raw[p + 1]);
+      lg = glibc::log_r(u / (1.0 - u), tlog);
+      lz = glibc::log_r(u * u * u2, tlog);
+    }
+    su[q] = u;
+    slg[q] = lg;
+    slz[q] = lz;
+  }
+  __syncthreads();
+  // 3. masks: bit i of word q of item j is the attempt at drift lo_j + 64 q + i (as k_phi_masks)
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  for (int task = wid; task < ni * nw; task += nwv) {
+    const int i = task / nw, q = task - i * nw;
+    const int64_t k = k0 + i;
+    const int64_t pos = nom0 + 2 * (int64_t)i + slo[i] + 64 * (int64_t)q + lane;
+    const int li = (int)(pos - p0);
+    bool acc = false;
+    if (pos < a.span) {
+      double x = 0.0;
+      acc = phi_attempt(sp[i], su[li], su[li + 1], slg[li], slz[li], tabs, tlog, &x) && !(x > sp[i].thr);
+    }
+    const uint64_t b = __ballot(acc);
+    if (lane == 0) {
+      smk[i * nw + q] = b;
+      a.maskd[k * nw + q] = b;
+    }
+  }
+  __syncthreads();
+  // 4. the group's table: the extra uniforms of its items from start drift lo_0 + c
+  uint16_t* out = a.gtab2 + ((int64_t)t * G + g) * tW;
+  for (int c = threadIdx.x; c < tW; c += blockDim.x) {
+    const int start = slo[0] + c;
+    int e = start;
+    bool ok = true;
+    for (int i = 0; i < ni && ok; ++i) ok = phi_tree_step(smk + i * nw, slo[i], tW, &e);
+    out[c] = ok && e - start < (int)kPhiBad ? (uint16_t)(e - start) : kPhiBad;
+  }
+}
+
+// Cluster t's group tables composed into its table (a.roots); the last workgroup chains the
+// cluster tables from drift 0.
+__global__ __launch_bounds__(1024) void k_phi2_tree(PhiArgs a) {
+  if (gate_closed(a.gate)) return;
+  extern __shared__ __attribute__((aligned(16))) uint16_t st[];
+  __shared__ int slast;
+  const int G = a.G, tW = a.tW, d = a.d, gs = a.gs;
+  const int t = blockIdx.x;
+  if (phi_get_status(a) == 0) {
+    uint16_t* A = st;                                   // G tables, then the levels above in B
+    uint16_t* B = st + (size_t)G * tW;
+    const uint16_t* src = a.gtab2 + (int64_t)t * G * tW;
+    for (int q = threadIdx.x; q < G * tW; q += blockDim.x) A[q] = src[q];
+    __syncthreads();
+    uint16_t* cur = A;
+    uint16_t* nxt = B;
+    int np = G, span = 1;                               // nodes, groups per node
+    while (np > 1) {
+      const int nl = (np + 1) / 2;
+      for (int li = 0; li < nl; ++li) {
+        const uint16_t* L = cur + (size_t)(2 * li) * tW;
+        uint16_t* O = nxt + (size_t)li * tW;
+        if (2 * li + 1 < np) {
+          const int lol = (int)phi_lo((int64_t)t * d + (int64_t)(2 * li) * span * gs, a.rate, a.sdev);
+          const int lor = (int)phi_lo((int64_t)t * d + (int64_t)(2 * li + 1) * span * gs, a.rate, a.sdev);
+          const uint16_t* R = cur + (size_t)(2 * li + 1) * tW;
+          for (int c = threadIdx.x; c < tW; c += blockDim.x) O[c] = phi_tree_compose(L, R, lol, lor, tW, c);
+        } else {
+          for (int c = threadIdx.x; c < tW; c += blockDim.x) O[c] = L[c];
+        }
+      }
+      __syncthreads();
+      // ping-pong: the level just written becomes the source; the next goes where the old source was
+      uint16_t* tmp = cur;
+      cur = nxt;
+      nxt = (cur == B) ? A : B;
+      (void)tmp;
+      np = nl;
+      span *= 2;
+    }
+    for (int c = threadIdx.x; c < tW; c += blockDim.x) a.roots[(int64_t)t * tW + c] = cur[c];
+  }
+  // the last workgroup: every cluster's start drift from drift 0
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0)
+    slast = __hip_atomic_fetch_add(&a.ctr[0], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (!slast) return;
+  __threadfence();
+  if (threadIdx.x == 0) __hip_atomic_store(&a.ctr[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (phi_get_status(a) != 0) return;
+  for (int q = threadIdx.x; q < a.T * tW; q += blockDim.x)
+    st[q] = __hip_atomic_load(a.roots + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  int64_t e = 0;
+  for (int u = 0; u < a.T; ++u) {
+    const int64_t c = e - phi_lo((int64_t)u * d, a.rate, a.sdev);
+    const uint16_t v = (c >= 0 && c < tW) ? st[(size_t)u * tW + c] : kPhiBad;
+    if (v == kPhiBad) {
+      phi_set_status(a, kPhiWindow);
+      return;
+    }
+    a.dts[u] = e;
+    e += v;
+  }
+  const int64_t cons = (int64_t)a.T * 3 * d + e;
+  if (cons + 1 > a.span) phi_set_status(a, kPhiShort);
+  *(int64_t*)(a.status + 2) = cons;
+  if (a.pos_out) *a.pos_out = *a.pos_in + a.sweep_len + cons;
+}
+
+// One wave: group g's items from start drift e0 (lane i = item j0 + i), the drift of each
+// lane the group start plus the extra uniforms of the lanes before it, in fixed-point rounds
+// (each round fixes every lane up to the next rejection); the mask words around the group's
+// drifts prefetched in registers.  Writes sapos; false when a lane leaves its window.
+__device__ __forceinline__ bool phi2_walk_group(const PhiArgs& a, int t, int j0, int ni, int64_t e0, int64_t* sapos,
+                                                int64_t* total) {
+  const int lane = threadIdx.x & 63;
+  const int nw = a.nw, tW = a.tW;
+  const bool act = lane < ni;
+  const int64_t k = (int64_t)t * a.d + j0 + lane;
+  const int64_t lo = act ? phi_lo(k, a.rate, a.sdev) : 0;
+  const uint64_t* row = a.maskd + k * nw;
+  const int q0 = act ? (int)max((int64_t)0, (e0 - lo) >> 6) : 0;
+  uint64_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+  if (act) {
+    w0 = q0 < nw ? row[q0] : 0ull;
+    w1 = q0 + 1 < nw ? row[q0 + 1] : 0ull;
+    w2 = q0 + 2 < nw ? row[q0 + 2] : 0ull;
+    w3 = q0 + 3 < nw ? row[q0 + 3] : 0ull;
+  }
+  int64_t dl = e0;
+  int ex = 0, tot = 0;
+  for (;;) {
+    bool bad = false;
+    ex = 0;
+    if (act) {
+      const int64_t off = dl - lo;
+      if (off < 0 || off >= tW) {
+        bad = true;
+      } else {
+        const int q = (int)(off >> 6), sh = (int)(off & 63);
+        uint64_t lw, hw;
+        const int r = q - q0;
+        if (r >= 0 && r + 1 <= 3) {
+          lw = r == 0 ? w0 : r == 1 ? w1 : w2;
+          hw = r == 0 ? w1 : r == 1 ? w2 : w3;
+        } else {
+          lw = row[q];
+          hw = row[q + 1];
+        }
+        const uint64_t win = sh ? (lw >> sh) | (hw << (64 - sh)) : lw;
+        const uint64_t acc = win & 0x5555555555555555ull;
+        if (!acc) bad = true;
+        else ex = __builtin_ctzll(acc);
+      }
+    }
+    if (__ballot(bad)) return false;
+    const int before = wave_excl_scan(ex, &tot);
+    const int64_t nd = e0 + before;
+    const bool changed = act && nd != dl;
+    dl = nd;
+    if (!__ballot(changed)) break;
+  }
+  if (act) sapos[j0 + lane] = (int64_t)t * 3 * a.d + a.d + 2 * (int64_t)(j0 + lane) + dl + ex;
+  *total = tot;
+  return true;
+}
+
+__global__ __launch_bounds__(1024) void k_phi2_values(PhiArgs a) {
+  if (gate_closed(a.gate)) return;
+  if (a.raw_ptr) a.raw = *a.raw_ptr;
+  extern __shared__ __attribute__((aligned(16))) uint8_t wl[];
+  __shared__ uint64_t tabs[512];
+  __shared__ double red[4 * 16];
+  __shared__ double wmx[16], wmn[16];
+  __shared__ int sbad, slast;
+  const int t = blockIdx.x, d = a.d, G = a.G, gs = a.gs, tW = a.tW;
+  uint16_t* stb = reinterpret_cast<uint16_t*>(wl);
+  int64_t* sgs = reinterpret_cast<int64_t*>(wl + align16((size_t)G * tW * 2));            // [G + 1] group starts
+  double* wtab = reinterpret_cast<double*>(reinterpret_cast<uint8_t*>(sgs) + align16((size_t)(G + 1) * 8));
+  int64_t* sapos = reinterpret_cast<int64_t*>(reinterpret_cast<uint8_t*>(wtab) + align16((size_t)2 * d * 8));
+  uint8_t* spick = reinterpret_cast<uint8_t*>(sapos) + align16((size_t)d * 8);
+  for (int i = threadIdx.x; i < 512; i += blockDim.x) tabs[i] = a.gtab[i];
+  if (threadIdx.x == 0) sbad = phi_get_status(a) != 0;
+  __syncthreads();
+  if (!sbad) {
+    const uint16_t* src = a.gtab2 + (int64_t)t * G * tW;
+    for (int q = threadIdx.x; q < G * tW; q += blockDim.x) stb[q] = src[q];
+    for (int j = threadIdx.x; j < d; j += blockDim.x) spick[j] = (uint8_t)(a.det[(int64_t)t * d + j] - 1);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      // the groups' start drifts from the cluster's (k_phi2_tree's chain)
+      int64_t e = a.dts[t];
+      for (int g = 0; g <= G; ++g) {
+        sgs[g] = e;
+        if (g == G) break;
+        const int64_t c = e - phi_lo((int64_t)t * d + (int64_t)g * gs, a.rate, a.sdev);
+        const uint16_t v = (c >= 0 && c < tW) ? stb[(size_t)g * tW + c] : kPhiBad;
+        if (v == kPhiBad) {
+          sbad = 1;
+          break;
+        }
+        e += v;
+      }
+    }
+    __syncthreads();
+    if (!sbad) {
+      const int wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+      for (int g = wid; g < G; g += nwv) {
+        const int j0 = g * gs, ni = min(gs, d - j0);
+        int64_t tot = 0;
+        const bool ok = phi2_walk_group(a, t, j0, ni, sgs[g], sapos, &tot);
+        // the walk must end where the group's table says it does
+        if ((!ok || sgs[g] + tot != sgs[g + 1]) && (threadIdx.x & 63) == 0) atomicOr(&sbad, 1);
+      }
+    }
+    __syncthreads();
+    if (sbad) {
+      if (threadIdx.x == 0) phi_set_status(a, kPhiWindow);
+    } else {
+      phi_values_body(a, t, spick, sapos, wtab, tabs, tabs + 256, red, wmx, wmn, &sbad);
+    }
+  }
+  // the last workgroup hands the status and the consumption to the host
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0)
+    slast = __hip_atomic_fetch_add(&a.ctr[1], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (!slast || threadIdx.x != 0) return;
+  __threadfence();
+  __hip_atomic_store(&a.ctr[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (a.status_host) {
+    const int code = phi_get_status(a);
+    const int lo32 = __hip_atomic_load(a.status + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int hi32 = __hip_atomic_load(a.status + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    a.status_host[1] = 0;
+    a.status_host[2] = code ? 0 : lo32;
+    a.status_host[3] = code ? 0 : hi32;
+    __threadfence_system();
+    __hip_atomic_store(a.status_host, code, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+size_t phi2_group_lds_bytes(int gs, int nw, double rate) { return phi2_group_lds(gs, nw, rate); }
+size_t phi2_tree_lds_bytes(int T, int G, int tW) { return phi2_tree_lds(T, G, tW); }
+size_t phi2_values_lds_bytes(int d, int G, int tW) { return phi2_values_lds(d, G, tW); }
+
+hipError_t launch_phi2(const PhiArgs& a, hipStream_t s) {
+  const int64_t items = (int64_t)a.T * a.d;
+  if (items <= 0) return hipSuccess;
+  if (a.gs < 1 || a.gs > 64 || a.G != (a.d + a.gs - 1) / a.gs || a.tW < 64 || a.tW != 64 * (a.nw - 1) ||
+      a.tW >= 65535 || a.gen <= 0 || !a.gtab2 || !a.roots || !a.ctr || !a.dts || !a.maskd)
+    return hipErrorInvalidValue;
+  const size_t l1 = phi2_group_lds(a.gs, a.nw, a.rate), l2 = phi2_tree_lds(a.T, a.G, a.tW),
+               l3 = phi2_values_lds(a.d, a.G, a.tW);
+  if (l1 > 150 * 1024 || l2 > 150 * 1024 || l3 > 140 * 1024) return hipErrorInvalidValue;
+  const int th1 = 512;
+  HDPM_LAUNCH(k_phi2_group, dim3((unsigned)(a.T * a.G)), dim3(th1), l1, s, a);
+  HDPM_LAUNCH(k_phi2_tree, dim3((unsigned)a.T), dim3(1024), l2, s, a);
+  HDPM_LAUNCH(k_phi2_values, dim3((unsigned)a.T), dim3(64 * a.wpb), l3, s, a);
+  return hipGetLastError();
 }
 
 // dynamic LDS of k_phi_cwalk (cluster image + a pick row per wave) and k_phi_values

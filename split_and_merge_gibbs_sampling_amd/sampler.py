@@ -204,9 +204,10 @@ class Engine:
                                             int(ocml), _lib.ptr(out)))
         return out
 
-    def set_phi_device(self, on: bool = True):
-        """update_phi on the device (include/hdpm.h HDPM_OPT_PHI_DEVICE); same chain."""
-        self._check(self._L.hdpm_set_option(self._h, _lib.OPT_PHI_DEVICE, 1.0 if on else 0.0))
+    def set_phi_device(self, on: bool = True, general: bool = False):
+        """update_phi on the device (include/hdpm.h HDPM_OPT_PHI_DEVICE); same chain.  general:
+        the general kernels only (launch_phi), not the fast path (launch_phi2) first."""
+        self._check(self._L.hdpm_set_option(self._h, _lib.OPT_PHI_DEVICE, (2.0 if general else 1.0) if on else 0.0))
 
     def get_option(self, option: int) -> float:
         """The current value of an include/hdpm.h HDPM_OPT_* option (hdpm_get_option)."""

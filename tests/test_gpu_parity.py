@@ -74,7 +74,7 @@ def sweep_case(hd, oracle, ds, c, cen, sig, P, seed, m=3, debug=0, sweeps=1, phi
     eng = make_engine(hd, ds)
     eng.set_debug(debug)
     if phi_device:
-        eng.set_phi_device(True)
+        eng.set_phi_device(True, general=phi_device == "general")
     eng.set_state(c, cen, sig)
     eng.set_pool(pc, ps)
     eng.rng_state = st
@@ -148,26 +148,58 @@ def test_speculative_update_phi(hd, oracle):
 # update_phi on the device (csrc/phi.hip): centers, sigmas, tables and the stream position
 # after it against the oracle, on shapes with one and several attribute classes, binary and
 # many-level attributes, wide rows; and that the device path ran (no silent host fallback).
-# walks: debug bit 27 (the per-start-drift walks, k_phi_cwalk, instead of the composition trees)
-@pytest.mark.parametrize("walks", [False, True])
+# path: "fast" (launch_phi2, the default where every pick is fixed), "trees" (the general
+# kernels' composition trees), "walks" (debug bit 27: the per-start-drift walks, k_phi_cwalk)
+@pytest.mark.parametrize("path", ["fast", "trees", "walks"])
 @pytest.mark.parametrize("shape", ["c5_like", "mixed", "binary", "wide", "zoo"])
-def test_device_update_phi(hd, oracle, zoo, shape, walks):
+def test_device_update_phi(hd, oracle, zoo, shape, path):
     if shape == "zoo":
         ds, K = zoo, 7
     else:
         ds, K = {"c5_like": (synth(8000, 128, 12, 4, seed=5), 12), "mixed": (synth(5000, 48, 9, (2, 6), seed=6), 9),
                  "binary": (synth(6000, 32, 8, 2, seed=7), 8), "wide": (synth(2500, 784, 6, 6, seed=8), 6)}[shape]
     cen, sig = random_params(ds, K, 13)
-    stats = sweep_case(hd, oracle, ds, ds.truth, cen, sig, ds.n * 3, seed=43, sweeps=4, phi=True, phi_device=True,
-                       debug=134217728 if walks else 0)
-    assert stats["phi_device_calls"] >= 2, {k: v for k, v in stats.items() if "phi" in k}
-    if walks:
-        assert stats["phi_tree_calls"] == 0, stats
+    stats = sweep_case(hd, oracle, ds, ds.truth, cen, sig, ds.n * 3, seed=43, sweeps=4, phi=True,
+                       phi_device=True if path == "fast" else "general", debug=134217728 if path == "walks" else 0)
+    phis = {k: v for k, v in stats.items() if "phi" in k}
+    assert stats["phi_device_calls"] >= 2, phis
+    if path == "fast":
+        # (random parameters: some picks depend on the uniform, and such updates are handed to
+        # the general kernels; test_device_update_phi_fast_path_converged covers commits)
+        if shape in ("c5_like", "mixed", "wide"):
+            assert stats["phi_fast_calls"] >= 1, phis
+    elif path == "walks":
+        assert stats["phi_tree_calls"] == 0 and stats["phi_fast_calls"] == 0, stats
     elif shape != "wide":
         # d <= 128: the composition trees resolve the drifts, a cluster with a pick that
         # depends on the uniform by the walks inside the same update (no re-run)
         assert stats["phi_tree_calls"] >= 2 and stats["phi_tree_retries"] == 0, \
             {k: v for k, v in stats.items() if "phi" in k}
+
+
+def converged_params(ds, c, K, sigma=0.5):
+    """Centers at each cluster's per-attribute mode, sigmas `sigma`: the state of a converged
+    chain (every update_phi center pick fixed by its cluster's frequency table)."""
+    cen = np.zeros((K, ds.d))
+    for k in range(K):
+        rows = ds.codes[c == k]
+        for j in range(ds.d):
+            cen[k, j] = np.bincount(rows[:, j], minlength=int(ds.attrisize[j]) + 1)[1:].argmax() + 1
+    return cen, np.full((K, ds.d), sigma)
+
+
+# The fast path (launch_phi2) from a converged state: every update commits there (no hand-back
+# to the general kernels), C5-, C3- and C4-like shapes, the chain bit-identical to the oracle.
+@pytest.mark.parametrize("shape", ["c5_like", "c3_like", "c4_like", "binary"])
+def test_device_update_phi_fast_path_converged(hd, oracle, shape):
+    ds, K = {"c5_like": (synth(20000, 128, 10, 4, seed=15), 10), "c3_like": (synth(12000, 64, 8, (2, 6), seed=16), 8),
+             "c4_like": (synth(6000, 784, 5, 6, seed=17), 5), "binary": (synth(8000, 32, 6, 2, seed=18), 6)}[shape]
+    cen, sig = converged_params(ds, ds.truth, K)
+    stats = sweep_case(hd, oracle, ds, ds.truth, cen, sig, ds.n * 3, seed=44, sweeps=5, phi=True, phi_device=True)
+    phis = {k: v for k, v in stats.items() if "phi" in k}
+    # (a speculation beside a sweep that then moved points is dropped and the update re-run)
+    assert stats["phi_fast_calls"] >= 5 and stats["phi_fast_handbacks"] == 0, phis
+    assert stats["phi_device_calls"] == 5, phis
 
 
 def test_device_update_phi_small_clusters_fall_back_or_match(hd, oracle, zoo):
