@@ -464,7 +464,8 @@ def main():
             "fallbacks": {k: int(st[k]) for k in ("fpg_aborts", "sm_wide_fallbacks", "pipe_recovered",
                                                   "phi_device_fallbacks", "phi_fallback_status_mask")},
             "update_phi": {"mode": "device" if phi_dev else "host",
-                           "device_calls": int(st["phi_device_calls"]), "spec_used": int(st["phi_dspec_used"])},
+                           "device_calls": int(st["phi_device_calls"]), "spec_used": int(st["phi_dspec_used"]),
+                           "fast_calls": int(st["phi_fast_calls"]), "fast_handbacks": int(st["phi_fast_handbacks"])},
             "pool_generation": {"init": pool_report(st_init, ds.n * args.m),
                                 "regeneration": pool_report(stats_diff(st0, st_init), ds.n * args.m)},
         },

@@ -83,7 +83,7 @@ hipError_t launch_phi(const PhiArgs& a, hipStream_t s);
 hipError_t launch_phi2(const PhiArgs& a, hipStream_t s);
 size_t phi2_group_lds_bytes(int gs, int nw, double rate);
 size_t phi2_tree_lds_bytes(int T, int G, int tW);
-size_t phi2_values_lds_bytes(int d, int G, int tW);
+size_t phi2_values_lds_bytes(int d, int G, int tW, int T);
 size_t phi_cwalk_lds(int d, int nw, int wpb);
 size_t phi_values_lds(int d, int nw);
 size_t phi_tree_lds_bytes(int SB, int nw, int W);
@@ -3529,12 +3529,18 @@ struct Ctx {
     // them directly: no copy commands on the update's path)
     DevBuf<uint16_t> gtab2, roots;
     DevBuf<int> ctr;
+    DevBuf<unsigned long long> tdbg;
     int gen = 0;
     PinBuf<uint8_t> h_in2, h_out2;
+    DevBuf<uint8_t> d_in2;
     int64_t fast_calls = 0;
     // tree mode when every updated cluster has at least this many members (a small cluster's
     // center picks can depend on the uniform); raised past a cluster size that needed a retry
     int tree_min_count = 16;
+    // fast path: a hand-back because a pick depended on the uniform (an unsettled chain) skips
+    // the fast path for the next fast_backoff updates, then it is tried again
+    int fast_backoff = 0;
+    static constexpr int kFastBackoff = 16;
     PinBuf<uint8_t> h_in, h_out;
     double p_rej = 0.12;               // rbeta attempts rejected (window model), adapted per call
     double p_rej_sm = 0.12;            // the same for split-merge's one- or two-cluster updates
@@ -3618,13 +3624,15 @@ struct Ctx {
     bool fast_ok = false;
     int gs = 0, G = 0;
   };
-  PhiPlan phi_plan(int T, bool sm = false) const {
+  // sd_scale < 1 narrows the drift windows (the fast path: kPhiFastSd standard deviations
+  // instead of kPhiSd; a drift outside them is a window status and the update goes to the host)
+  PhiPlan phi_plan(int T, bool sm = false, double sd_scale = 1.0) const {
     PhiPlan pl;
     if (T <= 0 || d > 2048) return pl;
     pl.T = T;
     const double p = sm ? phd.p_rej_sm : phd.p_rej;
     pl.rate = 2 * p / (1 - p);
-    pl.sdev = 2 * std::sqrt(p) / (1 - p);
+    pl.sdev = sd_scale * 2 * std::sqrt(p) / (1 - p);
     pl.items = (int64_t)T * d;
     const int64_t klast = pl.items - 1;
     pl.nw = (int)((phi_hi(klast, pl.rate, pl.sdev) - phi_lo(klast, pl.rate, pl.sdev) + 63) / 64) + 3;
@@ -3658,7 +3666,7 @@ struct Ctx {
     if (pl.tW >= 64 && pl.tW < 65535)
       for (int gs = 8; gs <= 64; gs *= 2) {
         const int G = (d + gs - 1) / gs;
-        if (phi2_tree_lds_bytes(T, G, pl.tW) <= 150 * 1024 && phi2_values_lds_bytes(d, G, pl.tW) <= 140 * 1024 &&
+        if (phi2_tree_lds_bytes(T, G, pl.tW) <= 150 * 1024 && phi2_values_lds_bytes(d, G, pl.tW, T) <= 150 * 1024 &&
             phi2_group_lds_bytes(gs, pl.nw, pl.rate) <= 150 * 1024) {
           pl.fast_ok = true;
           pl.gs = gs;
@@ -3705,11 +3713,25 @@ struct Ctx {
     }
     a.tnd = phd.tnd.p;
     a.gs = 0; a.G = 0; a.gtab2 = nullptr; a.roots = nullptr; a.ctr = nullptr; a.gen = 0; a.status_host = nullptr;
+    a.tdbg = nullptr;
+    a.lab_dev = nullptr;
     return a;
   }
 
   // phi_mode 1: the fast path first where the plan allows it; 2: the general kernels only
   bool phi_fast(const PhiPlan& pl) const { return pl.fast_ok && phi_mode == 1; }
+  // the fast path's plan (narrower windows), and whether it is taken for an update whose
+  // smallest cluster has min_count members
+  static constexpr double kPhiFastSd = 4.75;
+  PhiPlan fast_plan(int T, bool sm, int min_count, bool* fast) {
+    const PhiPlan pf = phi_plan(T, sm, kPhiFastSd / kPhiSd);
+    *fast = phi_fast(pf) && min_count >= 16 && !(debug & 134217728);
+    if (*fast && phd.fast_backoff > 0) {
+      --phd.fast_backoff;
+      *fast = false;
+    }
+    return pf;
+  }
 
   // Enqueue one device update of T clusters on stream s: labels / counts / current sigmas in,
   // status + consumption, picks, sigmas and log-likelihood pairs out (phi_out_layout) in the
@@ -3718,7 +3740,7 @@ struct Ctx {
   // 1: the general kernels with composition trees; 0: with the per-start-drift walks (both
   // with copies and fills around launch_phi).
   const uint8_t* enqueue_phi(PhiArgs& a, const PhiPlan& pl, int mode, const int* lab, const int* cnt,
-                             const double* sig_in, hipStream_t s) {
+                             const double* sig_in, hipStream_t s, hipEvent_t w1 = nullptr, hipEvent_t w2 = nullptr) {
     const int T = pl.T;
     const int64_t items = pl.items;
     size_t o_pick, o_sig, o_ll, bytes;
@@ -3747,19 +3769,37 @@ struct Ctx {
       std::memcpy(hl + T, cnt, (size_t)T * 4);
       std::memcpy(phd.h_in2.p + o_sigin, sig_in, (size_t)items * 8);
       ((volatile int*)phd.h_out2.p)[0] = -1;           // (written by the last k_phi2_values workgroup)
-      a.lab = hl; a.cnt = hl + T; a.sig_in = (const double*)(phd.h_in2.p + o_sigin);
+      // the inputs to the device in one copy, queued before the update's waits (the sweep's
+      // scatter, the stream window) so it overlaps them: the kernels then read device memory
+      // (a kernel's reads of host memory cost it a PCIe round trip each)
+      phd.d_in2.ensure(in_bytes + 64);
+      HIPCHK(hipMemcpyAsync(phd.d_in2.p, phd.h_in2.p, in_bytes, hipMemcpyHostToDevice, s));
+      if (w1) HIPCHK(hipStreamWaitEvent(s, w1, 0));
+      if (w2) HIPCHK(hipStreamWaitEvent(s, w2, 0));
+      const int* dl = (const int*)phd.d_in2.p;
+      a.lab = dl; a.cnt = dl + T; a.sig_in = (const double*)(phd.d_in2.p + o_sigin);
       a.pick = phd.h_out2.p + o_pick;
       a.sig_out = (double*)(phd.h_out2.p + o_sig);
       a.ll = (double*)(phd.h_out2.p + o_ll);
       a.status_host = (int*)phd.h_out2.p;
       a.gs = pl.gs; a.G = pl.G; a.gtab2 = phd.gtab2.p; a.roots = phd.roots.p; a.ctr = phd.ctr.p; a.gen = phd.gen;
+      phd.lab_cnt.ensure(2 * T);
+      a.lab_dev = phd.lab_cnt.p;   // (k_phi2_group's copy of the labels and counts for k_phi2_values)
       a.tree = nullptr;
       a.lg = nullptr; a.lzz = nullptr;                   // the fast path computes its logits itself
+      if (std::getenv("HDPM_PHI_TIMING")) {
+        // testing: phase marks of the fast path (printed after a synchronous device update)
+        if (!phd.tdbg.p) phd.tdbg.ensure(24);
+        HIPCHK(hipMemsetAsync(phd.tdbg.p, 0, 24 * 8, s));
+        a.tdbg = phd.tdbg.p;
+      }
       HIPCHK(launch_phi2(a, s));
       phd.fast_calls++;
       stats.phi_fast_calls++;
       return phd.h_out2.p;
     }
+    if (w1) HIPCHK(hipStreamWaitEvent(s, w1, 0));
+    if (w2) HIPCHK(hipStreamWaitEvent(s, w2, 0));
     phd.h_in.ensure(in_bytes + 64);
     phd.h_out.ensure(bytes);
     int* hl = (int*)phd.h_in.p;
@@ -3801,13 +3841,16 @@ struct Ctx {
     const bool full = tables_dirty || T == K;
     if (full && T != K) return -1;                        // untouched labels need the host's tables
     rng_sync();
+    int min_count = INT_MAX;
+    for (int t = 0; t < T; ++t) min_count = std::min(min_count, h_counts[touched[t]]);
     const PhiPlan pl = phi_plan(T);
+    bool fast = false;
+    const PhiPlan pf = fast_plan(T, false, min_count, &fast);
     if (!pl.ok) return -1;
     const int64_t items = pl.items, need = pl.need;
     dspec_wait();                                         // a speculation's use of phd is over
     RngWindow* W = window_at(rng.pos, need);
     if (!W) return -1;
-    PhiArgs a = phi_args(pl);
     auto tp0 = std::chrono::steady_clock::now();
     histogram_launch(nidx == 0 ? nullptr : &mask);
     const unsigned* fsrc = nidx == 0 ? d_freq.p : d_freq_m.p;
@@ -3819,22 +3862,22 @@ struct Ctx {
       cnts[t] = h_counts[touched[t]];
       std::memcpy(&sigs[(size_t)t * d], &h_sigma[(size_t)touched[t] * d], (size_t)d * 8);
     }
-    HIPCHK(hipStreamWaitEvent(stream, W->done, 0));
-    a.freq = fsrc;
-    a.raw = W->raw.p + (rng.pos - W->start_pos);
-    a.nraw = (int64_t)(W->start_pos + (uint64_t)W->count - rng.pos);
     size_t o_pick, o_sig, o_ll, obytes;
     phi_out_layout(T, d, &o_pick, &o_sig, &o_ll, &obytes);
     const uint8_t* out = nullptr;
-    auto run = [&](int mode) { out = enqueue_phi(a, pl, mode, labs.data(), cnts.data(), sigs.data(), stream); };
+    auto run = [&](int mode) {
+      const PhiPlan& pm = mode == 2 ? pf : pl;
+      PhiArgs a = phi_args(pm);
+      a.freq = fsrc;
+      a.raw = W->raw.p + (rng.pos - W->start_pos);
+      a.nraw = (int64_t)(W->start_pos + (uint64_t)W->count - rng.pos);
+      out = enqueue_phi(a, pm, mode, labs.data(), cnts.data(), sigs.data(), stream, W->done);
+    };
     // the fast path, else the composition trees unless a cluster is small enough for a pick to
     // depend on the uniform (debug bit 27: always the per-start-drift walks)
-    int min_count = INT_MAX;
-    for (int t = 0; t < T; ++t) min_count = std::min(min_count, cnts[t]);
     // (with one walk segment per cluster, d <= 128, such clusters are walked inside the tree-mode
     // update itself)
     const bool tree = pl.tree_ok && (pl.S == 1 || min_count >= phd.tree_min_count) && !(debug & 134217728);
-    const bool fast = phi_fast(pl) && min_count >= phd.tree_min_count && !(debug & 134217728);
     run(fast ? 2 : tree ? 1 : 0);
     histogram_wait(nidx == 0 ? nullptr : &mask);
     if (freq_next_pending) {
@@ -3845,6 +3888,17 @@ struct Ctx {
     HIPCHK(hipStreamSynchronize(stream));
     phd.calls++;
     if (tree && !fast) stats.phi_tree_calls++;
+    if (fast && phd.tdbg.p && std::getenv("HDPM_PHI_TIMING")) {
+      unsigned long long m[24];
+      HIPCHK(hipMemcpy(m, phd.tdbg.p, sizeof(m), hipMemcpyDeviceToHost));
+      std::string line = "[phi2 us]";
+      for (int q = 1; q < 19; ++q) {
+        char b[32];
+        std::snprintf(b, sizeof(b), " %d:%.2f", q, m[q] && m[0] ? (double)(long long)(m[q] - m[0]) * 0.01 : -1.0);
+        line += b;
+      }
+      std::fprintf(stderr, "%s\n", line.c_str());
+    }
     if (std::getenv("HDPM_PHI_TRACE"))
       std::fprintf(stderr, "[phi] T %d nw %d tW %d fast_ok %d gs %d G %d min_count %d tree_min %d fast %d tree %d status %d\n",
                    T, pl.nw, pl.tW, (int)pl.fast_ok, pl.gs, pl.G, min_count, phd.tree_min_count, (int)fast, (int)tree,
@@ -3853,7 +3907,8 @@ struct Ctx {
     if ((fast || tree) && ((const int*)out)[0] == kPhiNonDet) {
       // a pick depends on the uniform: the same update by the walks (same inputs, nothing
       // committed yet); updates with clusters this small take the walks directly from now on
-      phd.tree_min_count = std::max(phd.tree_min_count, std::min(1 << 20, 2 * min_count));
+      if (fast) phd.fast_backoff = PhiDevice::kFastBackoff;
+      else phd.tree_min_count = std::max(phd.tree_min_count, std::min(1 << 20, 2 * min_count));
       stats.phi_tree_retries++;
       run(0);
       HIPCHK(hipStreamSynchronize(stream));
@@ -3960,7 +4015,23 @@ struct Ctx {
   }
   void dspec_wait() {
     if (!dspec.inflight) return;
-    HIPCHK(hipEventSynchronize(dspec.ev));
+    if (dspec.fast) {
+      // the fast path's last workgroup writes the status word last (system-scope release, after
+      // every other output and after every other workgroup finished): spin on it instead of a
+      // blocking event wait (whose wake-up alone costs tens of microseconds); 2 s, then the event
+      const auto t0 = std::chrono::steady_clock::now();
+      for (int polls = 0;; ++polls) {
+        if (__atomic_load_n((const int*)dspec.out, __ATOMIC_ACQUIRE) != -1) break;
+        HostPool::spin_pause();
+        if ((polls & 1023) == 1023 &&
+            std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+          HIPCHK(hipEventSynchronize(dspec.ev));
+          break;
+        }
+      }
+    } else {
+      HIPCHK(hipEventSynchronize(dspec.ev));
+    }
     dspec.inflight = false;
   }
   // outputs of a device update of T clusters in phd.h_out: status + consumption, picks, sigmas,
@@ -3981,7 +4052,12 @@ struct Ctx {
       if (h_counts[k] <= 0) return;
       min_count = std::min(min_count, h_counts[k]);
     }
-    const PhiPlan pl = phi_plan(K);
+    bool fast = false;
+    const PhiPlan pf = fast_plan(K, false, min_count, &fast);
+    const PhiPlan pl = fast ? pf : phi_plan(K);
+    if (std::getenv("HDPM_PHI_TRACE"))
+      std::fprintf(stderr, "[phi dspec launch] T %d p_rej %.4f nw %d tW %d fast_ok %d gs %d G %d min_count %d tree_min %d fast %d\n",
+                   K, phd.p_rej, pf.nw, pf.tW, (int)pf.fast_ok, pf.gs, pf.G, min_count, phd.tree_min_count, (int)fast);
     if (!pl.ok) return;
     RngWindow* W = window_at(rng.pos, pl.need);
     if (!W) return;
@@ -3993,14 +4069,13 @@ struct Ctx {
     std::vector<int> labs(T);
     for (int t = 0; t < T; ++t) labs[t] = t;
     if (!dspec.ev) HIPCHK(hipEventCreateWithFlags(&dspec.ev, hipEventDisableTiming));
-    HIPCHK(hipStreamWaitEvent(pstream, W->done, 0));
-    if (ev_phd_free) HIPCHK(hipStreamWaitEvent(pstream, ev_phd_free, 0));
+
     a.freq = d_freq.p;
     a.raw = W->raw.p + (rng.pos - W->start_pos);
     a.nraw = (int64_t)(W->start_pos + (uint64_t)W->count - rng.pos);
     const bool tree = pl.tree_ok && (pl.S == 1 || min_count >= phd.tree_min_count) && !(debug & 134217728);
-    const bool fast = phi_fast(pl) && min_count >= phd.tree_min_count && !(debug & 134217728);
-    dspec.out = enqueue_phi(a, pl, fast ? 2 : tree ? 1 : 0, labs.data(), h_counts.data(), h_sigma.data(), pstream);
+    dspec.out = enqueue_phi(a, pl, fast ? 2 : tree ? 1 : 0, labs.data(), h_counts.data(), h_sigma.data(), pstream,
+                            W->done, ev_phd_free);
     HIPCHK(hipEventRecord(dspec.ev, pstream));
     dspec.ran = true;
     dspec.inflight = true;
@@ -4041,9 +4116,13 @@ struct Ctx {
     std::memcpy(&cons, dspec.out + 8, 8);
     const uint64_t target = rng.pos + (uint64_t)cons;
     if (status == kPhiNonDet) {
-      int mc = INT_MAX;
-      for (int k = 0; k < T; ++k) mc = std::min(mc, h_counts[k]);
-      phd.tree_min_count = std::max(phd.tree_min_count, std::min(1 << 20, 2 * mc));
+      if (dspec.fast) {
+        phd.fast_backoff = PhiDevice::kFastBackoff;
+      } else {
+        int mc = INT_MAX;
+        for (int k = 0; k < T; ++k) mc = std::min(mc, h_counts[k]);
+        phd.tree_min_count = std::max(phd.tree_min_count, std::min(1 << 20, 2 * mc));
+      }
     }
     if (status != kPhiOk || cons <= 0 || !dspec.W || !can_adopt(*dspec.W, target) ||
         !covers(*dspec.W, rng.pos, dspec.pl.need)) {
@@ -4113,43 +4192,43 @@ struct Ctx {
   // kOk, -1 (handed back), or 1: the drift left the window (widened for the next attempt)
   int device_update_phi_sm_once(int T, const int* cnt, const unsigned* freq, const double* sig_in, uint8_t* cen,
                                 double* sig) {
+    int min_count = INT_MAX;
+    for (int t = 0; t < T; ++t) min_count = std::min(min_count, cnt[t]);
     const PhiPlan pl = phi_plan(T, true);
+    bool fast = false;
+    const PhiPlan pf = fast_plan(T, true, min_count, &fast);
     if (!pl.ok) return -1;
     RngWindow* W = window_at(rng.pos, pl.need);
     if (!W) return -1;
     dspec_wait();
-    PhiArgs a = phi_args(pl);
     const int64_t items = pl.items;
     const size_t fw = (size_t)T * d * mmax;
     h_sm_freq.ensure(fw);
     d_sm_freq.ensure(fw);
     std::memcpy(h_sm_freq.p, freq, fw * 4);
     std::vector<int> labs(T);
-    int min_count = INT_MAX;
-    for (int t = 0; t < T; ++t) {
-      labs[t] = t;
-      min_count = std::min(min_count, cnt[t]);
-    }
+    for (int t = 0; t < T; ++t) labs[t] = t;
     size_t o_pick, o_sig, o_ll, bytes;
     phi_out_layout(T, d, &o_pick, &o_sig, &o_ll, &bytes);
     HIPCHK(hipMemcpyAsync(d_sm_freq.p, h_sm_freq.p, fw * 4, hipMemcpyHostToDevice, stream));
-    HIPCHK(hipStreamWaitEvent(stream, W->done, 0));
-    a.freq = d_sm_freq.p;
-    a.raw = W->raw.p + (rng.pos - W->start_pos);
-    a.nraw = (int64_t)(W->start_pos + (uint64_t)W->count - rng.pos);
     const uint8_t* out = nullptr;
     auto run = [&](int mode) {
-      out = enqueue_phi(a, pl, mode, labs.data(), cnt, sig_in, stream);
+      const PhiPlan& pm = mode == 2 ? pf : pl;
+      PhiArgs a = phi_args(pm);
+      a.freq = d_sm_freq.p;
+      a.raw = W->raw.p + (rng.pos - W->start_pos);
+      a.nraw = (int64_t)(W->start_pos + (uint64_t)W->count - rng.pos);
+      out = enqueue_phi(a, pm, mode, labs.data(), cnt, sig_in, stream, W->done);
       HIPCHK(hipStreamSynchronize(stream));
     };
     const bool tree = pl.tree_ok && (pl.S == 1 || min_count >= phd.tree_min_count) && !(debug & 134217728);
-    const bool fast = phi_fast(pl) && min_count >= phd.tree_min_count && !(debug & 134217728);
     run(fast ? 2 : tree ? 1 : 0);
     phd.calls++;
     if (tree && !fast) stats.phi_tree_calls++;
     if (fast && ((const int*)out)[0] != kPhiOk) stats.phi_fast_handbacks++;
     if ((fast || tree) && ((const int*)out)[0] == kPhiNonDet) {
-      phd.tree_min_count = std::max(phd.tree_min_count, std::min(1 << 20, 2 * min_count));
+      if (fast) phd.fast_backoff = PhiDevice::kFastBackoff;
+      else phd.tree_min_count = std::max(phd.tree_min_count, std::min(1 << 20, 2 * min_count));
       stats.phi_tree_retries++;
       run(0);
     } else if (fast && ((const int*)out)[0] != kPhiOk && ((const int*)out)[0] != kPhiWindow &&

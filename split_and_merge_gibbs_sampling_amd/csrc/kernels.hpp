@@ -504,6 +504,8 @@ struct PhiArgs {
   int* ctr;                  // [2] last-workgroup counters of k_phi2_tree / k_phi2_values (self-resetting)
   int gen;                   // status generation: status[0] = gen << 4 | code belongs to this call
   int* status_host;          // [4] status (code, -, consumption int64) written by the last k_phi2_values workgroup
+  unsigned long long* tdbg;  // testing (HDPM_PHI_TIMING): wall-clock marks of the fast path's phases, or nullptr
+  int* lab_dev;              // [2T] device copy of lab then cnt, written by k_phi2_group for k_phi2_values
 };
 // Level sizes of a composition tree over nb >= 1 level-0 blocks.
 __host__ __device__ inline int phi_lcount(int nb, int l) { return ((nb - 1) >> l) + 1; }

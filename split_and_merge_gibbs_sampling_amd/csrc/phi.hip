@@ -112,7 +112,7 @@ __device__ __forceinline__ void phi_revsort_t(PR a0, PM ib0, int n) {
 
 // The continued fraction of the incomplete beta (rmath.hpp detail::betacf) and pbeta, in
 // device libm: used only for the branch test, with a margin (phi_beta_path).
-__device__ double phi_betacf(double a, double b, double x) {
+__device__ __noinline__ double phi_betacf(double a, double b, double x) {
   const double FPMIN = 1e-300, EPS = 1e-16;
   double qab = a + b, qap = a + 1.0, qam = a - 1.0, c = 1.0, d = 1.0 - qab * x / qap;
   if (fabs(d) < FPMIN) d = FPMIN;
@@ -135,7 +135,7 @@ __device__ double phi_betacf(double a, double b, double x) {
   return h;
 }
 
-__device__ double phi_pbeta(double x, double a, double b) {
+__device__ __noinline__ double phi_pbeta(double x, double a, double b) {
   if (x <= 0.0) return 0.0;
   if (x >= 1.0) return 1.0;
   const double lbt = lgamma(a + b) - lgamma(a) - lgamma(b) + a * log(x) + b * log1p(-x);
@@ -184,6 +184,11 @@ __device__ bool phi_rbeta_setup(double aa, double bb, PhiCand* c) {
     c->gamma = c->a + 1.0 / c->beta;
   }
   return true;
+}
+
+// phase marks (HDPM_PHI_TIMING): thread 0 of workgroup `blk` stamps slot q
+__device__ __forceinline__ void phi2_mark(const PhiArgs& a, int blk, int q) {
+  if (a.tdbg && (int)blockIdx.x == blk && threadIdx.x == 0) a.tdbg[q] = wall_clock64();
 }
 
 __device__ __forceinline__ int wave_excl_scan(int v, int* total) {
@@ -259,13 +264,13 @@ constexpr int kPhiLdsLevels = 16;
 // sample_prob1_prep (FixupProb, Walker check, revsort, cumulative sums) in pr / pm, the
 // candidates per pickable level.  Returns a PhiStatus; *det_out, *nact_out.  Called with LDS
 // or global scratch (two copies, so the compiler keeps each address space).
+// (nn, lab, sg: the cluster's size and label and the item's current sigma, loaded by the caller)
 template <class PR, class PM>
-__device__ __forceinline__ int phi_prep_item(const PhiArgs& a, int t, int j, int64_t idx, PR pr, PM pm,
-                                             const uint64_t* tabs, bool* det_out, int* nact_out) {
+__device__ __forceinline__ int phi_prep_item_in(const PhiArgs& a, int t, int j, int64_t idx, int nn, int lab, double sg,
+                                                PR pr, PM pm, const uint64_t* tabs, bool* det_out, int* nact_out,
+                                                PhiCand* cpick = nullptr) {
   const int mj = a.att[j], off = a.aoff[j];
-  const int nn = a.cnt[t];
-  const unsigned* f = a.freq + ((int64_t)a.lab[t] * a.d + j) * a.mmax;
-  const double sg = a.sig_in[(int64_t)t * a.d + j];
+  const unsigned* f = a.freq + ((int64_t)lab * a.d + j) * a.mmax;
   for (int l = 0; l < mj; ++l) pr[l] = (-((double)nn - (double)f[l])) / sg;
   double mx = pr[0];
   for (int l = 1; l < mj; ++l) if (pr[l] > mx) mx = pr[l];
@@ -315,10 +320,17 @@ __device__ __forceinline__ int phi_prep_item(const PhiArgs& a, int t, int j, int
       }
       if (det) a.ikind[idx] = (uint8_t)c.kind;
     }
+    if (cpick && det && s == 0) *cpick = c;         // (the fixed pick's candidate, for the caller)
     cb[l] = c;
   }
   *nact_out = nact;
   return 0;
+}
+template <class PR, class PM>
+__device__ __forceinline__ int phi_prep_item(const PhiArgs& a, int t, int j, int64_t idx, PR pr, PM pm,
+                                             const uint64_t* tabs, bool* det_out, int* nact_out) {
+  return phi_prep_item_in(a, t, j, idx, a.cnt[t], a.lab[t], a.sig_in[(int64_t)t * a.d + j], pr, pm, tabs, det_out,
+                          nact_out);
 }
 
 // Prep of the items of workgroup `blk` (tabs: the glibc exp table in LDS).
@@ -816,15 +828,18 @@ __global__ __launch_bounds__(1024) void k_phi_chain(PhiArgs a) {
 // (0 on entry).  Called by every thread of the workgroup.
 __device__ __forceinline__ void phi_values_body(const PhiArgs& a, int t, const uint8_t* spick, const int64_t* sapos, double* wtab,
                                 const uint64_t* texp, const uint64_t* tlog, double* red, double* wmx, double* wmn,
-                                int* sbad) {
+                                int* sbad, const int* lab_cnt = nullptr) {
+  // (lab_cnt: a device copy of the labels then the counts, else a.lab / a.cnt)
+  const int* labs = lab_cnt ? lab_cnt : a.lab;
+  const int* cnts = lab_cnt ? lab_cnt + a.T : a.cnt;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nth = blockDim.x;
   const int d = a.d;
   const UploadLayout L = upload_layout(a.T, a.dp, d, a.bw);
   uint8_t* codes = a.stage + L.off_codes + (size_t)t * a.dp;
   double* tab = reinterpret_cast<double*>(a.stage + L.off_tab) + (size_t)t * 2 * d;
   uint64_t* rec = reinterpret_cast<uint64_t*>(a.stage + L.off_bnd) + (size_t)t * a.bw;
-  const int nn = a.cnt[t];
-  const unsigned* fb = a.freq + (int64_t)a.lab[t] * d * a.mmax;
+  const int nn = cnts[t];
+  const unsigned* fb = a.freq + (int64_t)labs[t] * d * a.mmax;
   double hi = 0.0, lo = 0.0;                     // regrouped log-likelihood terms (Neumaier)
   auto add = [&](double x) {
     const double s = hi + x;
@@ -868,19 +883,20 @@ __device__ __forceinline__ void phi_values_body(const PhiArgs& a, int t, const u
     add(((double)nn - fm) * m1);
   }
   if (bad) atomicOr(sbad, 1);
+  phi2_mark(a, 0, 16);
   // per wave: A and scale summed (any order: only the bound's slack sees their rounding),
   // the log-likelihood pairs in lane order
   {
-    double H = 0.0, Lo = 0.0;
-    for (int q = 0; q < 64; ++q) {
-      const double x = __shfl(hi, q), y = __shfl(lo, q);
-      const double s = H + x;
-      Lo += fabs(H) >= fabs(x) ? (H - s) + x : (x - s) + H;
-      H = s;
-      Lo += y;
-    }
+    // the lanes' (hi, lo) pairs by a butterfly of error-free sums (TwoSum: the exact rounding
+    // error whatever the order, so every lane ends with the same pair)
+    double H = hi, Lo = lo;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
+      const double x = __shfl_xor(H, o), y = __shfl_xor(Lo, o);
+      const double s = H + x, bb = s - H;
+      const double err = (H - (s - bb)) + (x - bb);
+      H = s;
+      Lo = (Lo + y) + err;
       A += __shfl_xor(A, o);
       sc += __shfl_xor(sc, o);
     }
@@ -909,6 +925,7 @@ __device__ __forceinline__ void phi_values_body(const PhiArgs& a, int t, const u
   dmn = __builtin_inf();
   for (int q = 0; q < nth / 64; ++q) { dmx = fmax(dmx, wmx[q]); dmn = fmin(dmn, wmn[q]); }
   const double delta = dmx > 0 ? dmx / ((1 << kQ) - 1) : 0.0;
+  phi2_mark(a, 0, 17);
   // bound record (Ctx::bounds_for, kernels.hpp "Bound data per parameter entry"): wave w
   // builds plane word w
   for (int k = wid; k < a.Ws; k += nth / 64) {
@@ -932,6 +949,7 @@ __device__ __forceinline__ void phi_values_body(const PhiArgs& a, int t, const u
       if (lane == 0) rec[(a.wb + b) * a.Ws + k] = bits;
     }
   }
+  phi2_mark(a, 0, 18);
   if (threadIdx.x == 0) {
     double As = 0.0, scs = 0.0, H = 0.0, Lo = 0.0;
     for (int q = 0; q < nth / 64; ++q) {
@@ -949,7 +967,7 @@ __device__ __forceinline__ void phi_values_body(const PhiArgs& a, int t, const u
     sv[2] = dmn > 0 ? dmn : 0.0;
     sv[3] = scs;
     reinterpret_cast<int*>(a.stage + L.off_counts)[t] = nn;
-    reinterpret_cast<int*>(a.stage + L.off_slot)[t] = a.slot_of ? a.slot_of[t] : a.lab[t];
+    reinterpret_cast<int*>(a.stage + L.off_slot)[t] = a.slot_of ? a.slot_of[t] : labs[t];
     a.ll[2 * t] = H;
     a.ll[2 * t + 1] = Lo;
   }
@@ -1281,6 +1299,27 @@ __global__ __launch_bounds__(1024) void k_phi_values2(PhiArgs a) {
 // windows) is a status, and the caller runs launch_phi or the host job from the same stream
 // position; nothing else is committed.
 
+// n uint16 words (a multiple of 8, 16-B aligned at both ends) from global memory into LDS,
+// 16 B per load and 4 loads in flight per thread
+__device__ __forceinline__ void phi2_stage_u16(uint16_t* dst, const uint16_t* src, int n) {
+  const uint4* s4 = reinterpret_cast<const uint4*>(src);
+  uint4* d4 = reinterpret_cast<uint4*>(dst);
+  const int n4 = n >> 3, step = blockDim.x;
+  for (int q0 = threadIdx.x; q0 < n4; q0 += 4 * step) {
+    const int q1 = min(q0 + step, n4 - 1), q2 = min(q0 + 2 * step, n4 - 1), q3 = min(q0 + 3 * step, n4 - 1);
+    // (clamped indices: a lane past the end reloads and rewrites the last vector, same value)
+    const uint4 v0 = s4[q0], v1 = s4[q1], v2 = s4[q2], v3 = s4[q3];
+    d4[q0] = v0;
+    d4[q1] = v1;
+    d4[q2] = v2;
+    d4[q3] = v3;
+  }
+}
+
+
+constexpr int kPhi2MaxG = 512;        // groups per cluster (d <= 4096 at gs = 8)
+constexpr int kPhi2MaxT = 1024;       // clusters of one fast-path update
+
 __host__ __device__ inline int phi2_npos(int gs, int nw, double rate) {
   // positions a group can read: 2 (gs - 1) nominal steps, the growth of the window start over
   // the group (<= rate (gs - 1) + 1), 64 nw drifts, the attempt's second uniform
@@ -1292,12 +1331,12 @@ __host__ __device__ inline size_t phi2_group_lds(int gs, int nw, double rate) {
          3 * align16((size_t)phi2_npos(gs, nw, rate) * 8);
 }
 __host__ __device__ inline size_t phi2_tree_lds(int T, int G, int tW) {
-  const size_t a = (size_t)(G + (G + 1) / 2) * tW * 2, b = (size_t)T * tW * 2;
-  return align16(a > b ? a : b);
+  (void)T;
+  return align16((size_t)(G + (G + 1) / 2) * tW * 2);
 }
-__host__ __device__ inline size_t phi2_values_lds(int d, int G, int tW) {
+__host__ __device__ inline size_t phi2_values_lds(int d, int G, int tW, int T) {
   return align16((size_t)G * tW * 2) + align16((size_t)(G + 1) * 8) + align16((size_t)2 * d * 8) + align16((size_t)d * 8) +
-         align16((size_t)d);
+         align16((size_t)d) + align16((size_t)T * tW * 2);
 }
 
 __global__ __launch_bounds__(512) void k_phi2_group(PhiArgs a) {
@@ -1312,6 +1351,7 @@ __global__ __launch_bounds__(512) void k_phi2_group(PhiArgs a) {
   const int64_t k0 = (int64_t)t * d + j0;
   PoolClass* sp = reinterpret_cast<PoolClass*>(sm);
   int* slo = reinterpret_cast<int*>(sm + align16((size_t)gs * sizeof(PoolClass)));
+  __shared__ int snw[64];
   uint64_t* smk = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(slo) + align16((size_t)gs * 4));
   double* spr = reinterpret_cast<double*>(reinterpret_cast<uint8_t*>(smk) + align16((size_t)gs * nw * 8));
   uint8_t* spm = reinterpret_cast<uint8_t*>(spr) + align16((size_t)gs * kPhiLdsLevels * 8);
@@ -1319,40 +1359,28 @@ __global__ __launch_bounds__(512) void k_phi2_group(PhiArgs a) {
   double* su = reinterpret_cast<double*>(spm + align16((size_t)gs * kPhiLdsLevels));
   double* slg = su + (align16((size_t)npos * 8) >> 3);
   double* slz = slg + (align16((size_t)npos * 8) >> 3);
+  phi2_mark(a, 0, 0);
+  // the inputs first (possibly in host memory: one round trip, all loads in flight together,
+  // beside the glibc tables'); the label and count copied to the device for k_phi2_values
+  int in_lab = 0, in_cnt = 0;
+  double in_sig = 0.0;
+  if ((int)threadIdx.x < ni) {
+    in_lab = a.lab[t];
+    in_cnt = a.cnt[t];
+    in_sig = a.sig_in[k0 + threadIdx.x];
+  }
   for (int i = threadIdx.x; i < 512; i += blockDim.x) tabs[i] = a.gtab[i];
   if (threadIdx.x == 0) sbad = 0;
   __syncthreads();
-  // 1. the items: center probabilities, fixed pick, rbeta setup (as k_phi_prep)
+  // 1. the items' windows: start lo and the mask words worth evaluating, [lo, hi) (later words
+  // stay 0: a drift past phi_hi fails the walk, as it would the window model)
   if ((int)threadIdx.x < ni) {
-    const int i = threadIdx.x, j = j0 + i;
-    const int64_t k = k0 + i;
-    const int mj = a.att[j], off = a.aoff[j];
-    bool det = false;
-    int nact = 0, status;
-    if (mj <= kPhiLdsLevels) {
-      status = phi_prep_item(a, t, j, k, spr + i * kPhiLdsLevels, spm + i * kPhiLdsLevels, tabs, &det, &nact);
-    } else {
-      status = phi_prep_item(a, t, j, k, a.cum + (int64_t)t * a.sumatt + off, a.perm + (int64_t)t * a.sumatt + off, tabs,
-                             &det, &nact);
-    }
-    if (!status && !det) status = kPhiNonDet;
-    if (!status) {
-      const int kd = a.ikind[k];
-      if (kd == 1) status = kPhiBisect;
-      else if (kd != 2 && kd != 3) status = kPhiInactive;
-    }
-    if (status) {
-      phi_set_status(a, status);
-      sbad = 1;
-    } else {
-      // the candidate of the fixed pick, written by this thread (phi_prep_item)
-      sp[i] = as_pool(a.cand[(int64_t)t * a.sumatt + off + a.det[k] - 1]);
-    }
-    slo[i] = (int)phi_lo(k, a.rate, a.sdev);
+    const int64_t k = k0 + threadIdx.x;
+    slo[threadIdx.x] = (int)phi_lo(k, a.rate, a.sdev);
+    snw[threadIdx.x] = (int)min((int64_t)nw, ((phi_hi(k, a.rate, a.sdev) - slo[threadIdx.x]) >> 6) + 2);
   }
   __syncthreads();
-  if (sbad) return;
-  // 2. the stream logits of every position the group's masks read
+  // 2. the stream logits (while the inputs, possibly in host memory, are on their way) of every position the group's masks read
   const int64_t nom0 = (int64_t)t * 3 * d + d + 2 * (int64_t)j0;
   const int64_t p0 = nom0 + slo[0];
   const int64_t plast = nom0 + 2 * (int64_t)(ni - 1) + slo[ni - 1] + 64 * (int64_t)nw;   // last attempt's first uniform
@@ -1362,7 +1390,10 @@ __global__ __launch_bounds__(512) void k_phi2_group(PhiArgs a) {
   }
   const int np = (int)(plast - p0 + 2);
   const uint64_t* tlog = tabs + 256;
-  for (int q = threadIdx.x; q < np; q += blockDim.x) {
+  // (waves 1.. compute the logits while wave 0's lanes prepare the items: the preparation is a
+  // long dependent chain per item, the logits are independent work)
+  for (int q = (int)threadIdx.x - 64; q < np; q += (int)blockDim.x - 64) {
+    if (q < 0) break;
     const int64_t p = p0 + q;
     double u = 0.5, lg = 0.0, lz = 0.0;
     if (p < a.span + 1) u = pool_unif(a.raw[p]);
@@ -1375,26 +1406,70 @@ __global__ __launch_bounds__(512) void k_phi2_group(PhiArgs a) {
     slg[q] = lg;
     slz[q] = lz;
   }
-  __syncthreads();
-  // 3. masks: bit i of word q of item j is the attempt at drift lo_j + 64 q + i (as k_phi_masks)
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
-  for (int task = wid; task < ni * nw; task += nwv) {
-    const int i = task / nw, q = task - i * nw;
+  phi2_mark(a, 0, 1);
+  // 3. the items: center probabilities, fixed pick, rbeta setup (as k_phi_prep)
+  if (threadIdx.x == 0 && g == 0) {
+    a.lab_dev[t] = in_lab;
+    a.lab_dev[a.T + t] = in_cnt;
+  }
+  if ((int)threadIdx.x < ni) {
+    const int i = threadIdx.x, j = j0 + i;
     const int64_t k = k0 + i;
-    const int64_t pos = nom0 + 2 * (int64_t)i + slo[i] + 64 * (int64_t)q + lane;
-    const int li = (int)(pos - p0);
-    bool acc = false;
-    if (pos < a.span) {
-      double x = 0.0;
-      acc = phi_attempt(sp[i], su[li], su[li + 1], slg[li], slz[li], tabs, tlog, &x) && !(x > sp[i].thr);
+    const int mj = a.att[j], off = a.aoff[j];
+    bool det = false;
+    int nact = 0, status;
+    PhiCand cp{};
+    if (mj <= kPhiLdsLevels) {
+      status = phi_prep_item_in(a, t, j, k, in_cnt, in_lab, in_sig, spr + i * kPhiLdsLevels, spm + i * kPhiLdsLevels,
+                                tabs, &det, &nact, &cp);
+    } else {
+      status = phi_prep_item_in(a, t, j, k, in_cnt, in_lab, in_sig, a.cum + (int64_t)t * a.sumatt + off,
+                                a.perm + (int64_t)t * a.sumatt + off, tabs, &det, &nact, &cp);
     }
-    const uint64_t b = __ballot(acc);
-    if (lane == 0) {
-      smk[i * nw + q] = b;
-      a.maskd[k * nw + q] = b;
+    if (!status && !det) status = kPhiNonDet;
+    if (!status) {
+      if (cp.kind == 1) status = kPhiBisect;
+      else if (cp.kind != 2 && cp.kind != 3) status = kPhiInactive;
+    }
+    if (status) {
+      phi_set_status(a, status);
+      sbad = 1;
+    } else {
+      sp[i] = as_pool(cp);
     }
   }
   __syncthreads();
+  phi2_mark(a, 0, 2);
+  if (sbad) return;
+  // 4. masks: bit i of word q of item j is the attempt at drift lo_j + 64 q + i (as k_phi_masks)
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  // a wave per item (its rbeta setup in registers), two attempts per lane in flight
+  for (int i = wid; i < ni; i += nwv) {
+    const PoolClass C = sp[i];
+    const int cnw = snw[i];
+    const int64_t cpos = nom0 + 2 * (int64_t)i + slo[i];
+    for (int q = 0; q < nw; q += 2) {
+      const int64_t pa = cpos + 64 * (int64_t)q + lane, pb = pa + 64;
+      const int la = (int)(pa - p0), lb = la + 64;
+      bool acc0 = false, acc1 = false;
+      double x0 = 0.0, x1 = 0.0;
+      if (q < cnw && pa < a.span)
+        acc0 = phi_attempt(C, su[la], su[la + 1], slg[la], slz[la], tabs, tlog, &x0) && !(x0 > C.thr);
+      if (q + 1 < cnw && pb < a.span)
+        acc1 = phi_attempt(C, su[lb], su[lb + 1], slg[lb], slz[lb], tabs, tlog, &x1) && !(x1 > C.thr);
+      const uint64_t b0 = __ballot(acc0), b1 = __ballot(acc1);
+      if (lane == 0) {
+        smk[i * nw + q] = b0;
+        a.maskd[(k0 + i) * nw + q] = b0;
+        if (q + 1 < nw) {
+          smk[i * nw + q + 1] = b1;
+          a.maskd[(k0 + i) * nw + q + 1] = b1;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  phi2_mark(a, 0, 3);
   // 4. the group's table: the extra uniforms of its items from start drift lo_0 + c
   uint16_t* out = a.gtab2 + ((int64_t)t * G + g) * tW;
   for (int c = threadIdx.x; c < tW; c += blockDim.x) {
@@ -1404,6 +1479,8 @@ __global__ __launch_bounds__(512) void k_phi2_group(PhiArgs a) {
     for (int i = 0; i < ni && ok; ++i) ok = phi_tree_step(smk + i * nw, slo[i], tW, &e);
     out[c] = ok && e - start < (int)kPhiBad ? (uint16_t)(e - start) : kPhiBad;
   }
+  __syncthreads();
+  phi2_mark(a, 0, 4);
 }
 
 // Cluster t's group tables composed into its table (a.roots); the last workgroup chains the
@@ -1411,30 +1488,35 @@ __global__ __launch_bounds__(512) void k_phi2_group(PhiArgs a) {
 __global__ __launch_bounds__(1024) void k_phi2_tree(PhiArgs a) {
   if (gate_closed(a.gate)) return;
   extern __shared__ __attribute__((aligned(16))) uint16_t st[];
-  __shared__ int slast;
+  __shared__ int sglo[kPhi2MaxG];                     // window start of each group's first item (of cluster)
   const int G = a.G, tW = a.tW, d = a.d, gs = a.gs;
   const int t = blockIdx.x;
-  if (phi_get_status(a) == 0) {
+  phi2_mark(a, 0, 5);
+  __shared__ int sok;
+  if (threadIdx.x == 0) sok = phi_get_status(a) == 0;   // (one atomic load per workgroup, not per thread)
+  __syncthreads();
+  if (sok) {
     uint16_t* A = st;                                   // G tables, then the levels above in B
     uint16_t* B = st + (size_t)G * tW;
-    const uint16_t* src = a.gtab2 + (int64_t)t * G * tW;
-    for (int q = threadIdx.x; q < G * tW; q += blockDim.x) A[q] = src[q];
+    for (int g = threadIdx.x; g < G; g += blockDim.x) sglo[g] = (int)phi_lo((int64_t)t * d + (int64_t)g * gs, a.rate, a.sdev);
+    phi2_stage_u16(A, a.gtab2 + (int64_t)t * G * tW, G * tW);
     __syncthreads();
+    phi2_mark(a, 0, 6);
     uint16_t* cur = A;
     uint16_t* nxt = B;
     int np = G, span = 1;                               // nodes, groups per node
     while (np > 1) {
       const int nl = (np + 1) / 2;
-      for (int li = 0; li < nl; ++li) {
-        const uint16_t* L = cur + (size_t)(2 * li) * tW;
-        uint16_t* O = nxt + (size_t)li * tW;
-        if (2 * li + 1 < np) {
-          const int lol = (int)phi_lo((int64_t)t * d + (int64_t)(2 * li) * span * gs, a.rate, a.sdev);
-          const int lor = (int)phi_lo((int64_t)t * d + (int64_t)(2 * li + 1) * span * gs, a.rate, a.sdev);
-          const uint16_t* R = cur + (size_t)(2 * li + 1) * tW;
-          for (int c = threadIdx.x; c < tW; c += blockDim.x) O[c] = phi_tree_compose(L, R, lol, lor, tW, c);
-        } else {
-          for (int c = threadIdx.x; c < tW; c += blockDim.x) O[c] = L[c];
+      // every node of the level at once (the lookups of different nodes are independent)
+      for (int c = threadIdx.x; c < tW; c += blockDim.x) {
+        for (int li = 0; li < nl; ++li) {
+          const uint16_t* L = cur + (size_t)(2 * li) * tW;
+          uint16_t v;
+          if (2 * li + 1 < np)
+            v = phi_tree_compose(L, cur + (size_t)(2 * li + 1) * tW, sglo[2 * li * span], sglo[(2 * li + 1) * span], tW, c);
+          else
+            v = L[c];
+          nxt[(size_t)li * tW + c] = v;
         }
       }
       __syncthreads();
@@ -1447,36 +1529,8 @@ __global__ __launch_bounds__(1024) void k_phi2_tree(PhiArgs a) {
       span *= 2;
     }
     for (int c = threadIdx.x; c < tW; c += blockDim.x) a.roots[(int64_t)t * tW + c] = cur[c];
+    phi2_mark(a, 0, 7);
   }
-  // the last workgroup: every cluster's start drift from drift 0
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0)
-    slast = __hip_atomic_fetch_add(&a.ctr[0], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
-  __syncthreads();
-  if (!slast) return;
-  __threadfence();
-  if (threadIdx.x == 0) __hip_atomic_store(&a.ctr[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (phi_get_status(a) != 0) return;
-  for (int q = threadIdx.x; q < a.T * tW; q += blockDim.x)
-    st[q] = __hip_atomic_load(a.roots + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  int64_t e = 0;
-  for (int u = 0; u < a.T; ++u) {
-    const int64_t c = e - phi_lo((int64_t)u * d, a.rate, a.sdev);
-    const uint16_t v = (c >= 0 && c < tW) ? st[(size_t)u * tW + c] : kPhiBad;
-    if (v == kPhiBad) {
-      phi_set_status(a, kPhiWindow);
-      return;
-    }
-    a.dts[u] = e;
-    e += v;
-  }
-  const int64_t cons = (int64_t)a.T * 3 * d + e;
-  if (cons + 1 > a.span) phi_set_status(a, kPhiShort);
-  *(int64_t*)(a.status + 2) = cons;
-  if (a.pos_out) *a.pos_out = *a.pos_in + a.sweep_len + cons;
 }
 
 // One wave: group g's items from start drift e0 (lane i = item j0 + i), the drift of each
@@ -1551,18 +1605,39 @@ __global__ __launch_bounds__(1024) void k_phi2_values(PhiArgs a) {
   double* wtab = reinterpret_cast<double*>(reinterpret_cast<uint8_t*>(sgs) + align16((size_t)(G + 1) * 8));
   int64_t* sapos = reinterpret_cast<int64_t*>(reinterpret_cast<uint8_t*>(wtab) + align16((size_t)2 * d * 8));
   uint8_t* spick = reinterpret_cast<uint8_t*>(sapos) + align16((size_t)d * 8);
+  uint16_t* sroot = reinterpret_cast<uint16_t*>(spick + align16((size_t)d));   // [t + 1][tW] cluster tables
+  __shared__ int64_t sclo[kPhi2MaxT];                  // window start of each cluster up to t
+  phi2_mark(a, 0, 11);
   for (int i = threadIdx.x; i < 512; i += blockDim.x) tabs[i] = a.gtab[i];
   if (threadIdx.x == 0) sbad = phi_get_status(a) != 0;
   __syncthreads();
   if (!sbad) {
-    const uint16_t* src = a.gtab2 + (int64_t)t * G * tW;
-    for (int q = threadIdx.x; q < G * tW; q += blockDim.x) stb[q] = src[q];
+    phi2_stage_u16(stb, a.gtab2 + (int64_t)t * G * tW, G * tW);
+    phi2_stage_u16(sroot, a.roots, (t + 1) * tW);
+    for (int u = threadIdx.x; u <= t; u += blockDim.x) sclo[u] = phi_lo((int64_t)u * d, a.rate, a.sdev);
     for (int j = threadIdx.x; j < d; j += blockDim.x) spick[j] = (uint8_t)(a.det[(int64_t)t * d + j] - 1);
     __syncthreads();
     if (threadIdx.x == 0) {
-      // the groups' start drifts from the cluster's (k_phi2_tree's chain)
-      int64_t e = a.dts[t];
-      for (int g = 0; g <= G; ++g) {
+      // the cluster's start drift: the clusters before it from drift 0 (their tables, k_phi2_tree);
+      // the last cluster's end is the update's consumption
+      int64_t e = 0;
+      for (int u = 0; u <= t && !sbad; ++u) {
+        if (u == t) a.dts[t] = e;
+        if (u == t && t != a.T - 1) break;
+        const int64_t c = e - sclo[u];
+        const uint16_t v = (c >= 0 && c < tW) ? sroot[(size_t)u * tW + c] : kPhiBad;
+        if (v == kPhiBad) sbad = 1;
+        else e += v;
+      }
+      if (!sbad && t == a.T - 1) {
+        const int64_t cons = (int64_t)a.T * 3 * d + e;
+        if (cons + 1 > a.span) phi_set_status(a, kPhiShort);
+        *(int64_t*)(a.status + 2) = cons;
+        if (a.pos_out) *a.pos_out = *a.pos_in + a.sweep_len + cons;
+      }
+      // the groups' start drifts from the cluster's
+      e = a.dts[t];
+      for (int g = 0; g <= G && !sbad; ++g) {
         sgs[g] = e;
         if (g == G) break;
         const int64_t c = e - phi_lo((int64_t)t * d + (int64_t)g * gs, a.rate, a.sdev);
@@ -1575,6 +1650,7 @@ __global__ __launch_bounds__(1024) void k_phi2_values(PhiArgs a) {
       }
     }
     __syncthreads();
+    phi2_mark(a, 0, 12);
     if (!sbad) {
       const int wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
       for (int g = wid; g < G; g += nwv) {
@@ -1586,11 +1662,14 @@ __global__ __launch_bounds__(1024) void k_phi2_values(PhiArgs a) {
       }
     }
     __syncthreads();
+    phi2_mark(a, 0, 13);
     if (sbad) {
       if (threadIdx.x == 0) phi_set_status(a, kPhiWindow);
     } else {
-      phi_values_body(a, t, spick, sapos, wtab, tabs, tabs + 256, red, wmx, wmn, &sbad);
+      // (the labels / counts k_phi2_group copied to the device)
+      phi_values_body(a, t, spick, sapos, wtab, tabs, tabs + 256, red, wmx, wmn, &sbad, a.lab_dev);
     }
+    phi2_mark(a, 0, 14);
   }
   // the last workgroup hands the status and the consumption to the host
   __threadfence();
@@ -1600,6 +1679,7 @@ __global__ __launch_bounds__(1024) void k_phi2_values(PhiArgs a) {
   __syncthreads();
   if (!slast || threadIdx.x != 0) return;
   __threadfence();
+  if (a.tdbg) a.tdbg[15] = wall_clock64();
   __hip_atomic_store(&a.ctr[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (a.status_host) {
     const int code = phi_get_status(a);
@@ -1615,17 +1695,18 @@ __global__ __launch_bounds__(1024) void k_phi2_values(PhiArgs a) {
 
 size_t phi2_group_lds_bytes(int gs, int nw, double rate) { return phi2_group_lds(gs, nw, rate); }
 size_t phi2_tree_lds_bytes(int T, int G, int tW) { return phi2_tree_lds(T, G, tW); }
-size_t phi2_values_lds_bytes(int d, int G, int tW) { return phi2_values_lds(d, G, tW); }
+size_t phi2_values_lds_bytes(int d, int G, int tW, int T) { return phi2_values_lds(d, G, tW, T); }
 
 hipError_t launch_phi2(const PhiArgs& a, hipStream_t s) {
   const int64_t items = (int64_t)a.T * a.d;
   if (items <= 0) return hipSuccess;
-  if (a.gs < 1 || a.gs > 64 || a.G != (a.d + a.gs - 1) / a.gs || a.tW < 64 || a.tW != 64 * (a.nw - 1) ||
-      a.tW >= 65535 || a.gen <= 0 || !a.gtab2 || !a.roots || !a.ctr || !a.dts || !a.maskd)
+  if (a.gs < 1 || a.gs > 64 || a.G != (a.d + a.gs - 1) / a.gs || a.G > kPhi2MaxG || a.T > kPhi2MaxT || a.tW < 64 ||
+      a.tW != 64 * (a.nw - 1) || a.tW >= 65535 || a.gen <= 0 || !a.gtab2 || !a.roots || !a.ctr || !a.dts || !a.maskd ||
+      !a.lab_dev)
     return hipErrorInvalidValue;
   const size_t l1 = phi2_group_lds(a.gs, a.nw, a.rate), l2 = phi2_tree_lds(a.T, a.G, a.tW),
-               l3 = phi2_values_lds(a.d, a.G, a.tW);
-  if (l1 > 150 * 1024 || l2 > 150 * 1024 || l3 > 140 * 1024) return hipErrorInvalidValue;
+               l3 = phi2_values_lds(a.d, a.G, a.tW, a.T);
+  if (l1 > 150 * 1024 || l2 > 150 * 1024 || l3 > 150 * 1024) return hipErrorInvalidValue;
   const int th1 = 512;
   HDPM_LAUNCH(k_phi2_group, dim3((unsigned)(a.T * a.G)), dim3(th1), l1, s, a);
   HDPM_LAUNCH(k_phi2_tree, dim3((unsigned)a.T), dim3(1024), l2, s, a);
