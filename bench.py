@@ -304,8 +304,12 @@ def main():
                          "random assignment to 20 labels (la:31, the scripts' L = 20): the unconverged regime")
     ap.add_argument("--start-iter", type=int, default=0,
                     help="first iteration index (0: the warmup includes iteration 0's pool regeneration)")
-    ap.add_argument("--phi", choices=("auto", "host", "device"), default="auto",
-                    help="update_phi on the host job or the device (HDPM_OPT_PHI_DEVICE); auto = the engine's default")
+    ap.add_argument("--phi", choices=("default", "auto", "host", "device"), default="default",
+                    help="update_phi on the host job or the device (HDPM_OPT_PHI_DEVICE); auto = device for updates of "
+                         ">= 4096 (cluster, attribute) items; default = the engine's (auto unless HDPM_PHI says otherwise)")
+    ap.add_argument("--record", action="store_true",
+                    help="the R driver's sampling phase: every iteration saved (thinning 1, la:139-153) -- K, labels, "
+                         "centers and sigmas recorded through hdpm_iterations_record (batches of 16, buffers reused)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads of the optimised CPU baseline (0: every CPU this process may use, within the "
@@ -343,9 +347,9 @@ def main():
         eng.set_hig_logspace(True)
     if os.environ.get("HDPM_BENCH_HOST_POOL"):
         eng.set_debug(64)                        # sequential host pool generator (A/B runs)
-    if args.phi != "auto":
-        eng.set_phi_device(args.phi == "device")
-    phi_dev = eng.phi_device
+    if args.phi != "default":
+        eng.set_phi_device("auto" if args.phi == "auto" else args.phi == "device")
+    phi_mode = eng.phi_mode
     L, ci = {"truth": (0, ds.truth), "one": (1, np.zeros(ds.n, np.int32)), "random20": (20, None)}[args.init]
     params = eng.chain_params(m=args.m, iterations=args.steps + args.warmup, L=L, burnin=0, neal8=True,
                               split_merge=args.sm, t=10, r=10)
@@ -368,8 +372,14 @@ def main():
         eng.set_debug(32 | (64 if os.environ.get("HDPM_BENCH_HOST_POOL") else 0))                        # host timeline of the timed iterations (stderr)
     D.barrier()
     cuda_sync()
+    rec_buf = np.zeros((16, ds.n), np.int32) if args.record else None
     t0 = time.perf_counter()
-    eng.iterations(it, args.steps)
+    if args.record:
+        # every iteration saved (burnin 0, thinning 1): its K, labels, centers, sigmas, loglik
+        for k0 in range(0, args.steps, 16):
+            eng.iterations_record(it + k0, min(16, args.steps - k0), out=rec_buf)
+    else:
+        eng.iterations(it, args.steps)
     it += args.steps
     eng.synchronize()
     cuda_sync()
@@ -433,6 +443,7 @@ def main():
             "workload": (f"{args.config}: {CONFIGS.get(args.config, {}).get('name', args.config)}, N={ds.n} D={ds.d} "
                          f"m={args.m}; one step = Neal-8 sweep + update_phi"
                          f"{' + split-merge (t=r=10)' if args.sm else ''} + compute_loglikelihood "
+                         f"{'+ recording K / labels / centers / sigmas (thinning 1) ' if args.record else ''}"
                          f"(code/launcher.cpp:94-132), "
                          f"{ {'truth': 'ground-truth init', 'one': 'one-cluster init (L=1)', 'random20': 'random init, L=20'}[args.init]}"),
             "n": ds.n, "d": ds.d, "m": args.m, "K_final": K, "parallelism": f"replicas{ws}",
@@ -451,6 +462,8 @@ def main():
             "listed_points_per_step": st["listed_points"] / args.steps,
             "moves_per_step": st["moves"] / args.steps,
             "split_merge": bool(args.sm),
+            "record": ({"labels_mirrored": int(st["labels_mirrored"]), "labels_downloaded": int(st["labels_downloaded"])}
+                       if args.record else None),
             "hig_logspace": hig_log,
             "rounds_per_step": st["rounds"] / args.steps,
             # next sweeps enqueued while the update was drawn / run (engine pre_enqueue), and
@@ -463,7 +476,7 @@ def main():
             # CUs, sweeps enqueued ahead and re-run ungated, device update_phi handed to the host
             "fallbacks": {k: int(st[k]) for k in ("fpg_aborts", "sm_wide_fallbacks", "pipe_recovered",
                                                   "phi_device_fallbacks", "phi_fallback_status_mask")},
-            "update_phi": {"mode": "device" if phi_dev else "host",
+            "update_phi": {"mode": phi_mode, "where": "device" if st["phi_device_calls"] > 0 else "host",
                            "device_calls": int(st["phi_device_calls"]), "spec_used": int(st["phi_dspec_used"]),
                            "fast_calls": int(st["phi_fast_calls"]), "fast_handbacks": int(st["phi_fast_handbacks"])},
             "pool_generation": {"init": pool_report(st_init, ds.n * args.m),

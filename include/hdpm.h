@@ -111,6 +111,9 @@ typedef struct {
     /* device update_phi calls enqueued on the fast path (csrc/phi.hip launch_phi2: every pick
      * fixed, no copies), and those of them handed to the general kernels or the host */
     int64_t phi_fast_calls, phi_fast_handbacks;
+    /* recorded iterations' labels (hdpm_iterations_record, la:145): taken from the host mirror
+     * with the sweep's move log applied (12 B per moved point), and downloaded whole (N words) */
+    int64_t labels_mirrored, labels_downloaded;
 } hdpm_stats;
 
 int         hdpm_device_count(void);
@@ -185,6 +188,21 @@ int hdpm_iteration(hdpm_ctx* ctx, const hdpm_chain_params* p, int32_t iter, int3
 int hdpm_iterations(hdpm_ctx* ctx, const hdpm_chain_params* p, int32_t iter0, int32_t count, int32_t* idx_1_sm,
                     int32_t* accepted, double* loglik);
 
+/* hdpm_iterations with the saved iterations recorded (la:139-153, the R driver's sampling phase):
+ * iteration iter is saved when iter >= thinning * burnin and iter % thinning == 0; the s-th saved
+ * iteration of this call writes total_cls[s] (K), c_i[s * n .. s * n + n) (its labels; may be
+ * NULL), and appends its K x d centers and sigmas (doubles, as hdpm_get_state) to the context's
+ * record, taken with hdpm_record_take.  *nsaved: saved iterations of this call.  Unlike
+ * hdpm_get_state between hdpm_iteration calls, nothing is dropped: the next sweep stays
+ * pipelined, and a label vector comes from the host's mirror of the labels (kept across sweeps
+ * without moves, updated from the sweep's move log otherwise) instead of an N-word download. */
+int hdpm_iterations_record(hdpm_ctx* ctx, const hdpm_chain_params* p, int32_t iter0, int32_t count, int32_t* idx_1_sm,
+                           int32_t* accepted, double* loglik, int32_t* total_cls, int32_t* c_i, int32_t* nsaved);
+/* The recorded centers / sigmas (rows of d doubles, in saved-iteration order) appended since the
+ * last take: *nrows is their number; with centers and sigmas non-NULL (nrows rows each) they are
+ * copied out and the record is cleared. */
+int hdpm_record_take(hdpm_ctx* ctx, double* centers, double* sigmas, int64_t* nrows);
+
 /* Diagnostics / testing. */
 /* Draw `count` raw 32-bit MT outputs (MT_genrand before scaling) on the device and advance
  * the context stream past them (same values as `count` host draws). */
@@ -243,11 +261,15 @@ int hdpm_get_pool_heads(hdpm_ctx* ctx, uint64_t* out, int64_t P);
  * finite within 30000 terms the values are bit-identical.  Default 0 (reference
  * semantics). */
 #define HDPM_OPT_HIG_LOGSPACE 1
-/* HDPM_OPT_PHI_DEVICE (value != 0): update_phi runs on the device (csrc/phi.hip: center
- * draws, rhig's beta-path sigma draws resolved by speculative parallel walks over
- * acceptance masks, tables and bound records) instead of the host job speculated during the
- * sweep; cases the device does not restate fall back to the host.  Same chain either way.
- * Default 0 (or HDPM_PHI=device in the environment). */
+/* HDPM_OPT_PHI_DEVICE: where update_phi runs.  0: the host job speculated during the sweep;
+ * 1: the device (csrc/phi.hip: center draws, rhig's beta-path sigma draws resolved over
+ * acceptance masks by composition tables, tables and bound records; the fast path launch_phi2
+ * first when every pick is fixed, else the general kernels); 2: the device's general kernels
+ * only; 3 (default): automatic -- the device for the chain's update_phi of at least 4096
+ * (cluster, attribute) items, where the host job's serial draws outlast the sweep, the host job
+ * otherwise and for split-merge's updates.  Cases the device does not restate fall back to the
+ * host.  Same chain either way.  HDPM_PHI=host|device|device-general|auto in the environment
+ * sets the default. */
 #define HDPM_OPT_PHI_DEVICE 2
 /* HDPM_OPT_PIPE_WAIT_US (testing): the limit, in microseconds, after which the wait kernel of
  * a sweep enqueued ahead gives up and gates the sweep off (default 2 s).  A positive value

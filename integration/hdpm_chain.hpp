@@ -6,11 +6,14 @@
 // Call sequence (one call of the R function):
 //   hdpm_ctx_create -> hdpm_set_data (NumericMatrix -> codes) -> hdpm_rng_set_state
 //   (.Random.seed words 1..625, la: RNGScope entry) -> hdpm_init_chain (la:27-77) ->
-//   hdpm_iteration x (iterations + burnin) * thinning (la:85-154), hdpm_get_state at every
-//   saved iteration (la:140-153) -> hdpm_get_state (final_ass, la:170) -> hdpm_rng_get_state
-//   (the advanced stream back to R) -> hdpm_ctx_destroy.
+//   hdpm_iterations_record over the (iterations + burnin) * thinning iterations in batches
+//   (la:85-154; every saved iteration's K, labels, centers and sigmas recorded, la:140-153,
+//   with the next sweep kept pipelined) + hdpm_record_take after each batch ->
+//   hdpm_get_state (final_ass, la:170) -> hdpm_rng_get_state (the advanced stream back to R)
+//   -> hdpm_ctx_destroy.
 #pragma once
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdint>
@@ -102,22 +105,37 @@ inline int run_markov_chain(const double* data, int n, int d, const int32_t* att
   std::vector<int32_t> lab(n);
   int32_t idx_1_sm = 0;
   const int total = (p.iterations + p.burnin) * p.thinning;
-  for (int iter = 0; iter < total; ++iter) {                                  // la:85-154
-    int32_t a = 0;
-    double lik = 0.0;
-    if ((st = hdpm_iteration(ctx.get(), &p, iter, &idx_1_sm, &a, &lik))) return fail(st);
-    if (iter >= p.thinning * p.burnin && iter % p.thinning == 0) {          // la:140-153
+  // batches of iterations (la:85-154) with the saved ones recorded (la:140-153)
+  const int kBatch = 256;
+  std::vector<int32_t> acc(kBatch), kk(kBatch), labs;
+  std::vector<double> lik(kBatch), cen, sig;
+  for (int it0 = 0; it0 < total; it0 += kBatch) {
+    const int cnt = std::min(kBatch, total - it0);
+    labs.resize((size_t)cnt * n);
+    int32_t ns = 0;
+    if ((st = hdpm_iterations_record(ctx.get(), &p, it0, cnt, &idx_1_sm, acc.data(), lik.data(), kk.data(),
+                                     labs.data(), &ns)))
+      return fail(st);
+    int64_t rows = 0;
+    if ((st = hdpm_record_take(ctx.get(), nullptr, nullptr, &rows))) return fail(st);
+    cen.resize((size_t)rows * d);
+    sig.resize((size_t)rows * d);
+    if ((st = hdpm_record_take(ctx.get(), cen.data(), sig.data(), &rows))) return fail(st);
+    size_t row = 0;
+    int q = 0;
+    for (int k = 0; k < cnt; ++k) {
+      const int iter = it0 + k;
+      if (!(iter >= p.thinning * p.burnin && iter % p.thinning == 0)) continue;
       const int at = iter / p.thinning - p.burnin;
-      int32_t K = 0;
-      if ((st = hdpm_get_state(ctx.get(), lab.data(), &K, nullptr, nullptr, 0))) return fail(st);
-      out->centers[at].resize((size_t)K * d);
-      out->sigmas[at].resize((size_t)K * d);
-      if ((st = hdpm_get_state(ctx.get(), lab.data(), &K, out->centers[at].data(), out->sigmas[at].data(), K)))
-        return fail(st);
+      const int K = kk[q];
       out->total_cls[at] = K;
-      out->c_i[at] = lab;
-      out->loglikelihood[at] = lik;
-      out->accepted[at] = a;
+      out->c_i[at].assign(labs.begin() + (size_t)q * n, labs.begin() + (size_t)(q + 1) * n);
+      out->centers[at].assign(cen.begin() + row * d, cen.begin() + (row + K) * d);
+      out->sigmas[at].assign(sig.begin() + row * d, sig.begin() + (row + K) * d);
+      out->loglikelihood[at] = lik[k];
+      out->accepted[at] = acc[k];
+      row += (size_t)K;
+      ++q;
     }
   }
   out->time_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

@@ -25,7 +25,7 @@ EXPORTS = (
     "hdpm_set_pool", "hdpm_get_pool", "hdpm_generate_pool", "hdpm_neal8_sweep", "hdpm_update_phi",
     "hdpm_compute_loglikelihood", "hdpm_loglik_matrix", "hdpm_restricted_gibbs", "hdpm_logprobgs_c_i",
     "hdpm_split_and_merge", "hdpm_run_markov_chain", "hdpm_get_stats", "hdpm_reset_stats",
-    "hdpm_set_debug", "hdpm_synchronize", "hdpm_drop_prepared", "hdpm_init_chain", "hdpm_iteration", "hdpm_iterations", "hdpm_rng_fill_device",
+    "hdpm_set_debug", "hdpm_synchronize", "hdpm_drop_prepared", "hdpm_init_chain", "hdpm_iteration", "hdpm_iterations", "hdpm_iterations_record", "hdpm_record_take", "hdpm_rng_fill_device",
     "hdpm_get_pool_heads", "hdpm_set_option", "hdpm_get_option", "hdpm_debug_draw", "hdpm_debug_math",
     "hdpm_psm_build", "hdpm_psm_rows", "hdpm_psm_vi_lb",
 )
@@ -74,7 +74,8 @@ class Stats(C.Structure):
                                   "fpg_launches", "phi_sm_device_calls", "phi_fallback_status_mask",
                                   "phi_sm_window_retries", "fpg_aborts", "exact_mass_launches",
                                   "exact_lanes_launches", "dense_launches", "sm_wide_scans",
-                                  "sm_wide_fallbacks", "phi_fast_calls", "phi_fast_handbacks")]
+                                  "sm_wide_fallbacks", "phi_fast_calls", "phi_fast_handbacks",
+                                  "labels_mirrored", "labels_downloaded")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -128,6 +129,8 @@ def lib():
         "hdpm_init_chain": ([vp, P(ChainParams), vp], C.c_int),
         "hdpm_iteration": ([vp, P(ChainParams), i32, P(i32), P(i32), P(f64)], C.c_int),
         "hdpm_iterations": ([vp, P(ChainParams), i32, i32, P(i32), vp, vp], C.c_int),
+        "hdpm_iterations_record": ([vp, P(ChainParams), i32, i32, P(i32), vp, vp, vp, vp, P(i32)], C.c_int),
+        "hdpm_record_take": ([vp, vp, vp, P(i64)], C.c_int),
         "hdpm_reset_stats": ([vp], C.c_int),
         "hdpm_rng_fill_device": ([vp, i64, vp], C.c_int),
         "hdpm_set_debug": ([vp, i32], C.c_int),

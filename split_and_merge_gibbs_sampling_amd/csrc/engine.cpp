@@ -1523,6 +1523,40 @@ struct Ctx {
   // Upload tables of the labels in `which` only (after update_phi on a subset).
   void upload_some(const std::vector<int>& which) { stage_upload(&which); }
 
+  // moves of the last sweep to apply to the host mirror from the move log (see neal8_sweep)
+  int mirror_moves = 0;
+  // hdpm_iterations_record's centers / sigmas of the saved iterations (K x d rows each)
+  std::vector<uint8_t> rec_cen;
+  std::vector<double> rec_sig;
+  void record_params() {
+    rec_cen.insert(rec_cen.end(), h_center.begin(), h_center.begin() + (size_t)K * d);
+    rec_sig.insert(rec_sig.end(), h_sigma.begin(), h_sigma.begin() + (size_t)K * d);
+  }
+  // The labels on the host before the device can change them again (the recording path, right
+  // after a sweep): the mirror, the move log applied to it, or a download (on cstream: the
+  // sweep stream may hold a sweep enqueued ahead behind its wait kernel).
+  void capture_labels() {
+    if (host_c_valid) return;
+    if (mirror_moves > 0) {
+      mlog_h.resize((size_t)3 * mirror_moves);
+      HIPCHK(hipMemcpyAsync(mlog_h.data(), d_mlog.p, mlog_h.size() * 4, hipMemcpyDeviceToHost, cstream));
+      HIPCHK(hipStreamSynchronize(cstream));
+      for (int q = 0; q < mirror_moves; ++q) h_c[mlog_h[3 * q]] = mlog_h[3 * q + 2];
+      mirror_moves = 0;
+      host_c_valid = true;
+      host_c_device = true;
+      stats.labels_mirrored++;
+      return;
+    }
+    h_c.resize(n);
+    HIPCHK(hipMemcpyAsync(h_c.data(), d_c.p, (size_t)n * 4, hipMemcpyDeviceToHost, cstream));
+    HIPCHK(hipStreamSynchronize(cstream));
+    host_c_valid = true;
+    host_c_device = true;
+    stats.labels_downloaded++;
+  }
+  std::vector<int> mlog_h;
+
   void download_labels() {
     if (host_c_valid) return;
     h_c.resize(n);
@@ -2637,6 +2671,7 @@ struct Ctx {
     labels_version++;
     const int K0 = K;
     int sweep_moves = 0;
+    const bool hc_before = host_c_valid;     // the host label mirror before the sweep
     std::vector<uint8_t> old_center = h_center;
     std::vector<double> old_sigma = h_sigma;
 
@@ -2837,7 +2872,20 @@ struct Ctx {
       }
     }
     if (fetched && pool_on_device) HIPCHK(hipStreamSynchronize(stream));
-    host_c_valid = false;
+    // the host's label mirror: a sweep without moves changes no label; with moves, and the
+    // labels still in slot order (same K, every label on its own slot), the move log gives the
+    // new labels of the moved points (12 B each: the recording path's labels without an N-word
+    // download, mirror_moves); anything else invalidates the mirror
+    mirror_moves = 0;
+    if (!hc_before || sweep_moves > 0) host_c_valid = false;
+    // (a mirror kept across the sweep now mirrors device labels: consistent with K by
+    // construction, so the next sweep does not re-validate it over N points)
+    if (host_c_valid) host_c_device = true;
+    if (hc_before && sweep_moves > 0 && track && K == K0 && sweep_moves <= n / 16) {
+      bool ident = true;
+      for (int l = 0; l < K && ident; ++l) ident = sol[l] == l;
+      if (ident) mirror_moves = sweep_moves;
+    }
     tables_dirty = true;
     if (dspec.ran) {
       dspec.lv = labels_version;
@@ -3559,13 +3607,23 @@ struct Ctx {
   // update_phi placement: the host job speculated during the sweep (default), or the device
   // (phi.hip, after the sweep): HDPM_OPT_PHI_DEVICE, or HDPM_PHI=device in the environment;
   // debug bit 19 (value 524288) forces the host.
+  // phi_mode: 0 the host job, 1 the device (fast path first), 2 the device's general kernels
+  // only, 3 automatic (default): the device for the chain's update_phi when it has at least
+  // kPhiAutoItems (cluster, attribute) items -- where the host job's serial draws outlast the
+  // sweep (C4: 7,840 items, device 4.5k vs host 3.3k it/s) -- and the host job below that and for
+  // split-merge's one- and two-cluster updates (C5 / C3: host 7.7k / 12.8k vs device 5.2k / 8.3k,
+  // profiles/r06/ab_phi_auto/).  HDPM_PHI=host|device|device-general|auto overrides the default.
+  static constexpr int64_t kPhiAutoItems = 4096;
   int phi_mode = [] {
     const char* e = std::getenv("HDPM_PHI");
+    if (e && std::strcmp(e, "host") == 0) return 0;
     if (e && std::strcmp(e, "device") == 0) return 1;
     if (e && std::strcmp(e, "device-general") == 0) return 2;
-    return 0;
+    return 3;
   }();
-  bool host_spec() const { return phi_mode == 0 || (debug & 524288); }
+  // update_phi of `items` (cluster, attribute) pairs of the chain on the device?
+  bool phi_dev_for(int64_t items) const { return phi_mode == 1 || phi_mode == 2 || (phi_mode == 3 && items >= kPhiAutoItems); }
+  bool host_spec() const { return !phi_dev_for((int64_t)K * d) || (debug & 524288); }
   double dev_ll = 0.0;                 // compute_loglikelihood from the last full device update
   uint64_t dev_ll_version = 0;         // labels_version it belongs to (0: none)
 
@@ -3719,7 +3777,7 @@ struct Ctx {
   }
 
   // phi_mode 1: the fast path first where the plan allows it; 2: the general kernels only
-  bool phi_fast(const PhiPlan& pl) const { return pl.fast_ok && phi_mode == 1; }
+  bool phi_fast(const PhiPlan& pl) const { return pl.fast_ok && phi_mode != 2; }
   // the fast path's plan (narrower windows), and whether it is taken for an update whose
   // smallest cluster has min_count members
   static constexpr double kPhiFastSd = 4.75;
@@ -3832,6 +3890,11 @@ struct Ctx {
 
   int device_update_phi(const std::vector<unsigned char>& mask, int nidx) {
     if (phi_mode == 0 || (debug & (524288 | 64))) return -1;   // bit 19: host update_phi; bit 6: host pools
+    if (phi_mode == 3) {                                  // automatic: by the update's size
+      int64_t T0 = 0;
+      for (int k = 0; k < K; ++k) T0 += mask[k] && h_counts[k] != 0;
+      if (!phi_dev_for(T0 * d)) return -1;
+    }
     if (!glibc_selfcheck() || d > 2048) return -1;
     std::vector<int> touched;
     for (int k = 0; k < K; ++k)
@@ -4008,7 +4071,7 @@ struct Ctx {
     hipEvent_t ev = nullptr;           // they are complete
   } dspec;
   hipEvent_t ev_phd_free = nullptr;    // the last device use of phd's buffers on `stream` is done
-  bool dspec_on() const { return phi_mode != 0 && !(debug & (524288 | 64 | 128)); }
+  bool dspec_on() const { return phi_dev_for((int64_t)K * d) && !(debug & (524288 | 64 | 128)); }
   void phd_release(hipStream_t s) {
     if (!ev_phd_free) HIPCHK(hipEventCreateWithFlags(&ev_phd_free, hipEventDisableTiming));
     HIPCHK(hipEventRecord(ev_phd_free, s));
@@ -4174,7 +4237,8 @@ struct Ctx {
   PinBuf<unsigned> h_sm_freq;
   int device_update_phi_sm(int T, const int* cnt, const unsigned* freq, const double* sig_in, uint8_t* cen,
                            double* sig) {
-    if (phi_mode == 0 || (debug & (524288 | 64)) || T <= 0 || d > 2048 || !glibc_selfcheck()) return -1;
+    // (automatic mode: split-merge's updates stay on the host job)
+    if (phi_mode == 0 || phi_mode == 3 || (debug & (524288 | 64)) || T <= 0 || d > 2048 || !glibc_selfcheck()) return -1;
     rng_sync();
     // a drift past the window (a merged or freshly split cluster can reject far more attempts
     // than the chain's updates; nothing was consumed) is retried with a wider window
@@ -4566,7 +4630,7 @@ int Ctx::iteration(const hdpm_chain_params* p, int iter, int* idx_1_sm, int* acc
   // committed and its log-likelihood summed (both off the host's critical path, which is the
   // chain of update_phi draws): when this iteration is a lone Neal-8 sweep whose update
   // came from the speculation and whose log-likelihood needs no device work
-  const bool early = n8 && !sm_now && next_n8 && iter % 1000 != 0 && !labels_out && !(debug & 2097152);
+  const bool early = n8 && !sm_now && next_n8 && iter % 1000 != 0 && !(debug & 2097152);
   if (!n8) cancel_ahead();
   if (n8) {                                              // la:94-103
     // the next sweep may be enqueued while this one's update is drawn (pre_enqueue)
@@ -4577,6 +4641,8 @@ int Ctx::iteration(const hdpm_chain_params* p, int iter, int* idx_1_sm, int* acc
       pre_release();
       return st;
     }
+    // a recorded iteration's labels, before a sweep enqueued ahead can be given the go
+    if (labels_out) capture_labels();
     defer_commit = early;
     st = update_phi(nullptr, 0);
     defer_commit = false;
@@ -4611,7 +4677,7 @@ int Ctx::iteration(const hdpm_chain_params* p, int iter, int* idx_1_sm, int* acc
   st = compute_loglikelihood(ll);                        // la:132
   mark("loglik");
   if (!st && labels_out) {                               // la:145 (before the next sweep is launched)
-    download_labels();
+    if (sm_now || !n8) capture_labels();                 // (split-merge may have relabelled)
     std::memcpy(labels_out, h_c.data(), (size_t)n * 4);
   }
   // the next iteration starts with a sweep: prepare it now (cancelled by any other call;
@@ -4926,6 +4992,45 @@ int hdpm_iterations(hdpm_ctx* h, const hdpm_chain_params* p, int32_t iter0, int3
   })
   return st;
 }
+int hdpm_iterations_record(hdpm_ctx* h, const hdpm_chain_params* p, int32_t iter0, int32_t count, int32_t* idx_1_sm,
+                           int32_t* accepted, double* loglik, int32_t* total_cls, int32_t* c_i, int32_t* nsaved) {
+  CTX_KEEP();
+  if (!p || !idx_1_sm || count < 0 || p->thinning < 1) return HDPM_E_ARG;
+  ScopedPin pin;
+  int st = HDPM_OK;
+  int saved = 0;
+  GUARD({
+    for (int k = 0; k < count && st == HDPM_OK; ++k) {
+      const int iter = iter0 + k;
+      const bool rec = iter >= p->thinning * p->burnin && iter % p->thinning == 0;   // la:140
+      int acc = 0;
+      double ll = 0.0;
+      st = ctx->iteration(p, iter, idx_1_sm, &acc, &ll, k + 1 < count,
+                          rec && c_i ? c_i + (size_t)saved * ctx->n : nullptr);
+      if (accepted) accepted[k] = acc;
+      if (loglik) loglik[k] = ll;
+      if (st == HDPM_OK && rec) {                                            // la:141-153
+        if (total_cls) total_cls[saved] = ctx->K;
+        ctx->record_params();
+        saved++;
+      }
+    }
+  })
+  if (nsaved) *nsaved = saved;
+  return st;
+}
+int hdpm_record_take(hdpm_ctx* h, double* centers, double* sigmas, int64_t* nrows) {
+  CTX_KEEP();
+  if (!nrows) return HDPM_E_ARG;
+  const int64_t rows = ctx->d ? (int64_t)(ctx->rec_cen.size() / (size_t)ctx->d) : 0;
+  *nrows = rows;
+  if (!centers || !sigmas) return HDPM_OK;
+  for (size_t q = 0; q < ctx->rec_cen.size(); ++q) centers[q] = (double)ctx->rec_cen[q];
+  std::memcpy(sigmas, ctx->rec_sig.data(), ctx->rec_sig.size() * 8);
+  ctx->rec_cen.clear();
+  ctx->rec_sig.clear();
+  return HDPM_OK;
+}
 int hdpm_rng_fill_device(hdpm_ctx* h, int64_t count, uint32_t* out) {
   CTX();
   if (count <= 0 || !out) return HDPM_E_ARG;
@@ -4991,7 +5096,10 @@ int hdpm_set_option(hdpm_ctx* h, int32_t option, double value) {
       ctx->hig_log = value != 0.0;
       return HDPM_OK;
     case HDPM_OPT_PHI_DEVICE:
-      if (!(value == 0.0 || value == 1.0 || value == 2.0)) { ctx->err = "phi device: 0 host, 1 device, 2 device (general kernels)"; return HDPM_E_ARG; }
+      if (!(value == 0.0 || value == 1.0 || value == 2.0 || value == 3.0)) {
+        ctx->err = "phi device: 0 host, 1 device, 2 device (general kernels), 3 automatic";
+        return HDPM_E_ARG;
+      }
       GUARD(ctx->cancel_ahead();)
       ctx->phi_mode = (int)value;
       return HDPM_OK;

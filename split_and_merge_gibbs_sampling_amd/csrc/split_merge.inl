@@ -289,7 +289,7 @@ static int hupdate_phi_job(Ctx* c, HState& s, const int* ks, const Freq* const* 
 // update_phi (cf:511-591) of clusters ks[0..nk) (ascending labels) on the device
 // (Ctx::device_update_phi_sm, csrc/phi.hip): -1 when it does not apply (the host job runs).
 static int dupdate_phi_sm(Ctx* c, HState& s, const int* ks, const Freq* const* Fs, int nk) {
-  if (c->phi_mode == 0) return -1;
+  if (c->phi_mode == 0 || c->phi_mode == 3) return -1;    // (automatic mode: the host job)
   SmTimer tm(c->stats.t_sm_phi_ms);
   const int d = c->d, mm = c->mmax;
   std::vector<int> idx;

@@ -204,10 +204,12 @@ class Engine:
                                             int(ocml), _lib.ptr(out)))
         return out
 
-    def set_phi_device(self, on: bool = True, general: bool = False):
-        """update_phi on the device (include/hdpm.h HDPM_OPT_PHI_DEVICE); same chain.  general:
-        the general kernels only (launch_phi), not the fast path (launch_phi2) first."""
-        self._check(self._L.hdpm_set_option(self._h, _lib.OPT_PHI_DEVICE, (2.0 if general else 1.0) if on else 0.0))
+    def set_phi_device(self, on=True, general: bool = False):
+        """update_phi on the device (include/hdpm.h HDPM_OPT_PHI_DEVICE); same chain.  on: True
+        (device), False (host job), or "auto" (the default: device for updates of >= 4096 items);
+        general: the device's general kernels only (launch_phi), not the fast path (launch_phi2)."""
+        v = 3.0 if on == "auto" else (2.0 if general else 1.0) if on else 0.0
+        self._check(self._L.hdpm_set_option(self._h, _lib.OPT_PHI_DEVICE, v))
 
     def get_option(self, option: int) -> float:
         """The current value of an include/hdpm.h HDPM_OPT_* option (hdpm_get_option)."""
@@ -216,9 +218,9 @@ class Engine:
         return float(v.value)
 
     @property
-    def phi_device(self) -> bool:
-        """True when update_phi runs on the device (HDPM_OPT_PHI_DEVICE, default or set)."""
-        return self.get_option(_lib.OPT_PHI_DEVICE) != 0.0
+    def phi_mode(self) -> str:
+        """Where update_phi runs (HDPM_OPT_PHI_DEVICE): "host", "device", "device-general" or "auto"."""
+        return {0: "host", 1: "device", 2: "device-general", 3: "auto"}[int(self.get_option(_lib.OPT_PHI_DEVICE))]
 
     def set_pipe_wait_us(self, us: float):
         """Testing (include/hdpm.h HDPM_OPT_PIPE_WAIT_US): the wait limit of a sweep enqueued
@@ -286,6 +288,34 @@ class Engine:
                                             C.byref(self._idx_1_sm), ptr(acc), ptr(ll)))
         return acc, ll
 
+    def iterations_record(self, it0: int, count: int, labels: bool = True, out=None):
+        """Iterations it0 .. it0+count-1 with the saved ones recorded (hdpm_iterations_record,
+        la:139-153): (accepted[count], loglik[count], total_cls[saved], c_i[saved, n] or None,
+        centers / sigmas: lists of K x D arrays per saved iteration).  out: a preallocated
+        int32 (>= count) x n array for the labels (reused by bench.py --record)."""
+        acc = np.zeros(count, np.int32)
+        ll = np.zeros(count, np.float64)
+        tot = np.zeros(count, np.int32)
+        if out is not None:
+            assert out.dtype == np.int32 and out.shape[0] >= count and out.shape[1] == self.n and out.flags.c_contiguous
+            cis = out
+        else:
+            cis = np.zeros((count, self.n), np.int32) if labels else None
+        ns = C.c_int32(0)
+        self._check(self._L.hdpm_iterations_record(self._h, C.byref(self._params), int(it0), int(count),
+                                                   C.byref(self._idx_1_sm), ptr(acc), ptr(ll), ptr(tot), ptr(cis),
+                                                   C.byref(ns)))
+        s = ns.value
+        rows = C.c_int64(0)
+        self._check(self._L.hdpm_record_take(self._h, None, None, C.byref(rows)))
+        cen = np.zeros((rows.value, self.d), np.float64)
+        sig = np.zeros((rows.value, self.d), np.float64)
+        self._check(self._L.hdpm_record_take(self._h, ptr(cen), ptr(sig), C.byref(rows)))
+        off = np.concatenate([[0], np.cumsum(tot[:s])])
+        cens = [cen[off[q]:off[q + 1]] for q in range(s)]
+        sigs = [sig[off[q]:off[q + 1]] for q in range(s)]
+        return acc, ll, tot[:s], (cis[:s] if labels else None), cens, sigs
+
     def run_markov_chain(self, *, verbose=0, m=5, iterations=1000, L=1, c_i=None, burnin=5000, t=10, r=10,
                          neal8=False, split_merge=True, n8_step_size=1, sam_step_size=1, thinning=1,
                          keep_params=False):
@@ -305,10 +335,11 @@ class Engine:
         return {"total_cls": tot, "c_i": cis, "loglikelihood": ll, "final_ass": fin,
                 "time": float(tm[0]), "accepted": acc}
 
-    def _run_recording(self, p, c_i):
-        """The la:85-154 loop iteration by iteration (hdpm_init_chain + hdpm_iteration), also
-        recording the cluster parameters of every saved iteration as the reference does
-        (centers / sigmas, la:144-147: K x D arrays)."""
+    def _run_recording(self, p, c_i, chunk: int = 256):
+        """The la:85-154 loop with the cluster parameters of every saved iteration recorded as
+        the reference does (centers / sigmas, la:144-147: K x D arrays): hdpm_init_chain, then
+        hdpm_iterations_record in batches (the pipelined sweeps keep running across saved
+        iterations)."""
         import time
         iterations, burnin, thinning = p.iterations, p.burnin, p.thinning
         tot = np.zeros(iterations, np.int32)
@@ -318,13 +349,20 @@ class Engine:
         cens, sigs = [None] * iterations, [None] * iterations
         t0 = time.perf_counter()
         self.init_chain(p, c_i)
-        for it in range((iterations + burnin) * thinning):
-            a, lik = self.iteration(it)
-            if it >= thinning * burnin and it % thinning == 0:
-                at = it // thinning - burnin
-                c, cen, sig = self.get_state()
-                tot[at], cis[at], ll[at], acc[at] = cen.shape[0], c, lik, a
-                cens[at], sigs[at] = cen, sig
+        total = (iterations + burnin) * thinning
+        it = 0
+        while it < total:
+            cnt = min(chunk, total - it)
+            a, lik, kk, cc, cen, sig = self.iterations_record(it, cnt)
+            q = 0
+            for k in range(cnt):
+                i = it + k
+                if i >= thinning * burnin and i % thinning == 0:
+                    at = i // thinning - burnin
+                    tot[at], cis[at], ll[at], acc[at] = kk[q], cc[q], lik[k], a[k]
+                    cens[at], sigs[at] = cen[q], sig[q]
+                    q += 1
+            it += cnt
         fin = self.get_state()[0]
         return {"total_cls": tot, "c_i": cis, "centers": cens, "sigmas": sigs, "loglikelihood": ll,
                 "final_ass": fin, "time": time.perf_counter() - t0, "accepted": acc}

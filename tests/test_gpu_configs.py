@@ -211,11 +211,15 @@ def test_c5_full_size_random20_start(hd, oracle, lat):
 # kernel gives up after 1 us with no host-side check, so nearly every enqueued sweep is gated
 # off on the device and re-run ungated by the engine (its recovery path)
 # "phidev": update_phi on the device (HDPM_OPT_PHI_DEVICE), speculated beside each sweep and
-# committed when the sweep moved no point (engine.cpp dspec_launch / dspec_commit)
+# committed when the sweep moved no point (engine.cpp dspec_launch / dspec_commit); "phigen": the
+# same with the device's general kernels only (launch_phi, not the fast path launch_phi2);
+# "host": the host job (the default -- automatic -- places C4's update on the device, C5's and
+# C3's on the host)
 @pytest.mark.parametrize("name,warm,timed,mode", [("c5", 5, 25, ""), ("c5", 3, 12, "nopipe"),
                                                   ("c5", 3, 12, "gateoff"), ("c5", 5, 25, "phidev"),
                                                   ("c3", 5, 25, ""), ("c3", 5, 25, "phidev"),
-                                                  ("c4", 3, 25, ""), ("c4", 3, 15, "phidev")])
+                                                  ("c4", 3, 25, ""), ("c4", 3, 15, "host"),
+                                                  ("c4", 3, 10, "phigen")])
 def test_bench_path_iterations_api(hd, oracle, name, warm, timed, mode):
     """The path bench.py times (bench.py main: hdpm_iterations for the warmup, synchronize,
     reset_stats, hdpm_iterations for the timed window) at the full BASELINE size, against
@@ -236,6 +240,10 @@ def test_bench_path_iterations_api(hd, oracle, name, warm, timed, mode):
         eng.set_pipe_wait_us(-1.0)
     elif mode == "phidev":
         eng.set_phi_device(True)
+    elif mode == "phigen":
+        eng.set_phi_device(True, general=True)
+    elif mode == "host":
+        eng.set_phi_device(False)
     params = eng.chain_params(m=3, iterations=warm + timed + 3, L=0, burnin=0, neal8=True, split_merge=False)
     eng._params = params
 
@@ -266,10 +274,17 @@ def test_bench_path_iterations_api(hd, oracle, name, warm, timed, mode):
         assert st["pipe_enqueued"] == 0 and st["pipe_runs"] == 0, st
     if mode == "gateoff":
         assert st["pipe_recovered"] > 0, st
-    if mode == "phidev":
+    dev = mode in ("phidev", "phigen") or (mode == "" and name == "c4")
+    if dev:
         # every update on the device (none handed back to the host), from the speculation
         assert st["phi_device_calls"] == timed and st["phi_device_fallbacks"] == 0, st
         assert st["phi_dspec_used"] > 0, st
+        if mode == "phigen":
+            assert st["phi_fast_calls"] == 0, st
+        else:
+            assert st["phi_fast_calls"] >= timed and st["phi_fast_handbacks"] == 0, st
+    else:
+        assert st["phi_device_calls"] == 0, st
     np.testing.assert_allclose(ll, oracle_iters(it - timed, timed), rtol=RTOL, atol=0)
     same(eng, ost, rng, "after the timed batch")
     _, ll = eng.iterations(it, 3)

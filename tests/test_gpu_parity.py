@@ -417,6 +417,48 @@ def test_run_markov_chain_keep_params_and_stream_handback(hd, oracle, zoo):
     assert ost == 0 and np.array_equal(ref2["c_i"], c["c_i"]) and np.array_equal(c["rng_state"], st)
 
 
+@pytest.mark.parametrize("shape", ["settled", "moving"])
+def test_iterations_record_matches_stepwise(hd, oracle, shape):
+    """hdpm_iterations_record (the adapter's sampling loop, la:139-153, thinning 1 and 2): every
+    saved iteration's K, labels, centers and sigmas equal what hdpm_iteration + hdpm_get_state
+    give step by step, the labels equal the oracle's chain; the labels come from the host mirror
+    (the sweep's move log applied) rather than N-word downloads once the chain settles."""
+    ds = synth(20000, 64, 8, 4, seed=71) if shape == "settled" else synth(6000, 32, 6, 2, seed=72)
+    for thinning in (1, 2):
+        iters, burnin = 12, 2
+        kw = dict(m=3, iterations=iters, L=1, c_i=ds.truth, burnin=burnin, neal8=True, split_merge=False,
+                  thinning=thinning)
+        st, ref = oracle.run_markov_chain(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w, seed=8, fast=1, **kw)
+        assert st == 0
+        a = make_engine(hd, ds)
+        a.set_seed(8)
+        p = a.chain_params(m=3, iterations=iters, L=1, burnin=burnin, neal8=True, split_merge=False, thinning=thinning)
+        a.init_chain(p, c_i=ds.truth)
+        total = (iters + burnin) * thinning
+        acc, ll, kk, cis, cens, sigs = a.iterations_record(0, 5)
+        acc2, ll2, kk2, cis2, cens2, sigs2 = a.iterations_record(5, total - 5)
+        kk, cis = np.concatenate([kk, kk2]), np.concatenate([cis, cis2])
+        cens, sigs, ll = cens + cens2, sigs + sigs2, np.concatenate([ll, ll2])
+        stats = a.stats()
+        a.close()
+        assert len(kk) == iters and np.array_equal(cis, ref["c_i"]) and np.array_equal(kk, ref["total_cls"])
+        b = make_engine(hd, ds)
+        b.set_seed(8)
+        b.init_chain(p, c_i=ds.truth)
+        q = 0
+        for it in range(total):
+            _, lik = b.iteration(it)
+            assert lik == ll[it]
+            if it >= thinning * burnin and it % thinning == 0:
+                c, cen, sig = b.get_state()
+                assert np.array_equal(c, cis[q]) and np.array_equal(cen, cens[q]) and np.array_equal(sig, sigs[q])
+                q += 1
+        b.close()
+        assert q == iters
+        if shape == "settled":
+            assert stats["labels_downloaded"] <= 2, stats
+
+
 def test_run_markov_chain_random_init_matches_oracle(hd, oracle, zoo):
     # L = 20 random labels, a seed whose initial draw uses all 20 labels
     seed = next(s for s in range(1, 100)
