@@ -114,6 +114,9 @@ typedef struct {
     /* recorded iterations' labels (hdpm_iterations_record, la:145): taken from the host mirror
      * with the sweep's move log applied (12 B per moved point), and downloaded whole (N words) */
     int64_t labels_mirrored, labels_downloaded;
+    /* device updates whose stream state came back with their outputs (k_phi2_values copies the
+     * block of the position after the draws; no state copy to wait for) */
+    int64_t phi_state_direct;
 } hdpm_stats;
 
 int         hdpm_device_count(void);

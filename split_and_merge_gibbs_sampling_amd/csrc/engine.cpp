@@ -80,7 +80,7 @@ hipError_t launch_debug_math(const double* x, int64_t n, int fn, int ocml, doubl
 hipError_t launch_lmatrix(const uint8_t* codes_t, int n, int d, int nq, ParamTables cl, int K, double* L,
                           int* H, int64_t ldL, hipStream_t s);
 hipError_t launch_phi(const PhiArgs& a, hipStream_t s);
-hipError_t launch_phi2(const PhiArgs& a, hipStream_t s);
+hipError_t launch_phi2(const PhiArgs& a, hipStream_t s, hipEvent_t before_values = nullptr);
 size_t phi2_group_lds_bytes(int gs, int nw, double rate);
 size_t phi2_tree_lds_bytes(int T, int G, int tW);
 size_t phi2_values_lds_bytes(int d, int G, int tW, int T);
@@ -1219,6 +1219,40 @@ struct Ctx {
            p + n >= W.start_pos + (uint64_t)W.export_after;
   }
 
+  // The index (1..624; 0: none) of position p in its block of the stream (the same block edges
+  // in every window)
+  static int mti_at(const RngWindow& W, uint64_t p) {
+    if (p < W.start_pos) return 0;
+    const uint64_t r = p - W.start_pos;
+    const uint64_t head = W.mti0 >= 624 ? 0 : 624 - W.mti0;
+    if (r < head) return W.mti0 + (int)r;
+    const uint64_t k = (r - head) % 624;
+    return k == 0 ? 624 : (int)k;
+  }
+  // an update's stream slice: from position rng.pos in window W
+  void phi_raw(PhiArgs& a, const RngWindow& W) const {
+    a.raw = W.raw.p + (rng.pos - W.start_pos);
+    a.nraw = (int64_t)(W.start_pos + (uint64_t)W.count - rng.pos);
+    a.raw_back = (int64_t)(rng.pos - W.start_pos);
+    a.mti_pos = mti_at(W, rng.pos);
+  }
+  // After a device update that consumed up to `target`: the state the fast path copied out
+  // (`state`: the block's 624 words, then its index; k_phi2_values), else adopt_state_at.
+  void adopt_after_phi(RngWindow& W, uint64_t target, const uint32_t* state) {
+    if (state) {
+      const int mt = (int)state[624];
+      if (mt >= 1 && mt <= 624 && mt == mti_at(W, target)) {
+        for (int i = 0; i < 624; ++i) rng.mt[i] = mt_untemper(state[i]);
+        rng.mti = mt;
+        pend.active = false;
+        rng.pos = target;
+        stats.phi_state_direct++;
+        return;
+      }
+    }
+    adopt_state_at(W, target);
+  }
+
   // Make the host stream continue at position `target` inside window W: rng.pos now, the
   // state array asynchronously (rng_sync()).
   void adopt_state_at(RngWindow& W, uint64_t target) {
@@ -1249,17 +1283,7 @@ struct Ctx {
   bool phi_device_prefetch(const RngWindow& W, uint64_t target, int64_t N) {
     phidev.valid = false;
     // the state's position in its block (one stream: the same block edges in every window)
-    int mti;
-    {
-      const uint64_t r = target - W.start_pos;
-      const uint64_t head = W.mti0 >= 624 ? 0 : 624 - W.mti0;
-      if (r < head) {
-        mti = W.mti0 + (int)r;
-      } else {
-        const uint64_t k = (r - head) % 624;
-        mti = k == 0 ? 624 : (int)k;
-      }
-    }
+    const int mti = mti_at(W, target);
     // (a block that starts before the stream's first word: no window holds it)
     if (mti < 1 || target < (uint64_t)mti) return false;
     const uint64_t s_blk = target - (uint64_t)mti;              // first word of the state's block
@@ -3809,8 +3833,9 @@ struct Ctx {
     a.stage = phd.stage.p;
     const size_t o_sigin = align16((size_t)2 * T * 4), in_bytes = o_sigin + (size_t)items * 8;
     if (mode == 2) {
+      const size_t o_state = align16(bytes);             // the stream state after the update
       phd.h_in2.ensure(in_bytes + 64, hipHostMallocCoherent);
-      phd.h_out2.ensure(bytes + 64, hipHostMallocCoherent);
+      phd.h_out2.ensure(o_state + 625 * 4 + 64, hipHostMallocCoherent);
       if (!phd.ctr.p) {
         phd.ctr.ensure(2);
         HIPCHK(hipMemset(phd.ctr.p, 0, 2 * sizeof(int)));
@@ -3833,13 +3858,16 @@ struct Ctx {
       phd.d_in2.ensure(in_bytes + 64);
       HIPCHK(hipMemcpyAsync(phd.d_in2.p, phd.h_in2.p, in_bytes, hipMemcpyHostToDevice, s));
       if (w1) HIPCHK(hipStreamWaitEvent(s, w1, 0));
-      if (w2) HIPCHK(hipStreamWaitEvent(s, w2, 0));
+      // (w2, the release of phd's buffers by the sweep's stream, guards the staging buffer:
+      // only k_phi2_values writes it, so only it waits)
       const int* dl = (const int*)phd.d_in2.p;
       a.lab = dl; a.cnt = dl + T; a.sig_in = (const double*)(phd.d_in2.p + o_sigin);
       a.pick = phd.h_out2.p + o_pick;
       a.sig_out = (double*)(phd.h_out2.p + o_sig);
       a.ll = (double*)(phd.h_out2.p + o_ll);
       a.status_host = (int*)phd.h_out2.p;
+      a.state_host = a.raw_ptr == nullptr && a.mti_pos >= 1 ? (uint32_t*)(phd.h_out2.p + o_state) : nullptr;
+      if (a.state_host) a.state_host[624] = 0;
       a.gs = pl.gs; a.G = pl.G; a.gtab2 = phd.gtab2.p; a.roots = phd.roots.p; a.ctr = phd.ctr.p; a.gen = phd.gen;
       phd.lab_cnt.ensure(2 * T);
       a.lab_dev = phd.lab_cnt.p;   // (k_phi2_group's copy of the labels and counts for k_phi2_values)
@@ -3851,7 +3879,7 @@ struct Ctx {
         HIPCHK(hipMemsetAsync(phd.tdbg.p, 0, 24 * 8, s));
         a.tdbg = phd.tdbg.p;
       }
-      HIPCHK(launch_phi2(a, s));
+      HIPCHK(launch_phi2(a, s, w2));
       phd.fast_calls++;
       stats.phi_fast_calls++;
       return phd.h_out2.p;
@@ -3932,8 +3960,7 @@ struct Ctx {
       const PhiPlan& pm = mode == 2 ? pf : pl;
       PhiArgs a = phi_args(pm);
       a.freq = fsrc;
-      a.raw = W->raw.p + (rng.pos - W->start_pos);
-      a.nraw = (int64_t)(W->start_pos + (uint64_t)W->count - rng.pos);
+      phi_raw(a, *W);
       out = enqueue_phi(a, pm, mode, labs.data(), cnts.data(), sigs.data(), stream, W->done);
     };
     // the fast path, else the composition trees unless a cluster is small enough for a pick to
@@ -4040,7 +4067,7 @@ struct Ctx {
       tables_dirty = false;
     }
     stage_full = false;                // the host staging no longer mirrors the device tables
-    adopt_state_at(*W, target);
+    adopt_after_phi(*W, target, out == phd.h_out2.p ? (const uint32_t*)(out + phi_state_off(T, d)) : nullptr);
     // the drift model follows the chain: extra uniforms per sigma draw seen here
     PhiDevice::adapt(phd.p_rej, cons - 3 * items, items);
     stats.t_host_phi_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp0).count();
@@ -4106,6 +4133,12 @@ struct Ctx {
     *o_ll = *o_sig + items * 8;
     *bytes = *o_ll + (size_t)2 * T * 8;
   }
+  // (the fast path's copy of the stream state follows them)
+  static size_t phi_state_off(int T, int d_) {
+    size_t o_pick, o_sig, o_ll, bytes;
+    phi_out_layout(T, d_, &o_pick, &o_sig, &o_ll, &bytes);
+    return align16(bytes);
+  }
 
   void dspec_launch() {
     dspec.ran = false;
@@ -4134,8 +4167,7 @@ struct Ctx {
     if (!dspec.ev) HIPCHK(hipEventCreateWithFlags(&dspec.ev, hipEventDisableTiming));
 
     a.freq = d_freq.p;
-    a.raw = W->raw.p + (rng.pos - W->start_pos);
-    a.nraw = (int64_t)(W->start_pos + (uint64_t)W->count - rng.pos);
+    phi_raw(a, *W);
     const bool tree = pl.tree_ok && (pl.S == 1 || min_count >= phd.tree_min_count) && !(debug & 134217728);
     dspec.out = enqueue_phi(a, pl, fast ? 2 : tree ? 1 : 0, labs.data(), h_counts.data(), h_sigma.data(), pstream,
                             W->done, ev_phd_free);
@@ -4196,6 +4228,7 @@ struct Ctx {
     }
     stats.phi_device_calls++;
     stats.phi_dspec_used++;
+    const uint32_t* st_words = dspec.fast ? (const uint32_t*)(dspec.out + phi_state_off(T, d)) : nullptr;
     // tables: by the sweep enqueued ahead (its gated scatter, pipe_go), flush_commit, or now
     if (defer_commit) {
       commit_later.active = true;
@@ -4223,7 +4256,7 @@ struct Ctx {
     stage_full = false;                // the host staging no longer mirrors the device tables
     freq_next_pending = false;
     freq_version = labels_version;
-    adopt_state_at(*dspec.W, target);
+    adopt_after_phi(*dspec.W, target, st_words);
     PhiDevice::adapt(phd.p_rej, cons - 3 * dspec.pl.items, dspec.pl.items);
     return kOk;
   }
@@ -4280,8 +4313,7 @@ struct Ctx {
       const PhiPlan& pm = mode == 2 ? pf : pl;
       PhiArgs a = phi_args(pm);
       a.freq = d_sm_freq.p;
-      a.raw = W->raw.p + (rng.pos - W->start_pos);
-      a.nraw = (int64_t)(W->start_pos + (uint64_t)W->count - rng.pos);
+      phi_raw(a, *W);
       out = enqueue_phi(a, pm, mode, labs.data(), cnt, sig_in, stream, W->done);
       HIPCHK(hipStreamSynchronize(stream));
     };
@@ -4330,7 +4362,7 @@ struct Ctx {
     const uint8_t* pk = out + o_pick;
     for (int64_t q = 0; q < items; ++q) cen[q] = (uint8_t)(pk[q] + 1);
     std::memcpy(sig, out + o_sig, (size_t)items * 8);
-    adopt_state_at(*W, target);
+    adopt_after_phi(*W, target, out == phd.h_out2.p ? (const uint32_t*)(out + phi_state_off(T, d)) : nullptr);
     rng_sync();                        // split-merge draws on the host next
     PhiDevice::adapt(phd.p_rej_sm, cons - 3 * items, items, 0.9);
     return kOk;
@@ -4805,8 +4837,12 @@ int hdpm_ctx_create(int32_t device, hdpm_ctx** out) {
   int prio_lo = 0, prio_hi = 0;
   const char* sp = std::getenv("HDPM_STREAM_PRIO");
   if (!(sp && sp[0] == '0') && hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
+  // (testing, HDPM_STREAM_PRIO=2: the sweep's stream at the generator's priority, the device
+  // update_phi's above it)
+  const int prio_sweep = (sp && sp[0] == '2') ? prio_lo : prio_hi;
+  if (std::getenv("HDPM_PHI_TRACE")) std::fprintf(stderr, "[streams] priorities %d..%d sweep %d\n", prio_lo, prio_hi, prio_sweep);
   if (hipSetDevice(device) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi) != hipSuccess) {
+      hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_sweep) != hipSuccess) {
     delete c;
     return HDPM_E_DEVICE;
   }

@@ -506,6 +506,12 @@ struct PhiArgs {
   int* status_host;          // [4] status (code, -, consumption int64) written by the last k_phi2_values workgroup
   unsigned long long* tdbg;  // testing (HDPM_PHI_TIMING): wall-clock marks of the fast path's phases, or nullptr
   int* lab_dev;              // [2T] device copy of lab then cnt, written by k_phi2_group for k_phi2_values
+  // the stream state after the update (fast path): the 624 words of the block that holds the
+  // position after its draws, then that position's index in the block (0: not copied -- the
+  // block is not inside [raw - raw_back, raw + nraw)); written before status_host, or nullptr
+  uint32_t* state_host;
+  int mti_pos;               // the index in its block (1..624) of the update's first position
+  int64_t raw_back;          // words of the stream window before `raw`
 };
 // Level sizes of a composition tree over nb >= 1 level-0 blocks.
 __host__ __device__ inline int phi_lcount(int nb, int l) { return ((nb - 1) >> l) + 1; }

@@ -1677,12 +1677,38 @@ __global__ __launch_bounds__(1024) void k_phi2_values(PhiArgs a) {
   if (threadIdx.x == 0)
     slast = __hip_atomic_fetch_add(&a.ctr[1], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
   __syncthreads();
-  if (!slast || threadIdx.x != 0) return;
+  if (!slast) return;
   __threadfence();
+  __shared__ int scode, smti;
+  __shared__ int64_t soff;
+  if (threadIdx.x == 0) {
+    scode = phi_get_status(a);
+    smti = 0;
+    if (scode == 0 && a.state_host) {
+      // the block of the position after the update's draws, relative to `raw`
+      const uint32_t lo = (uint32_t)__hip_atomic_load(a.status + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t hi = (uint32_t)__hip_atomic_load(a.status + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int64_t cons = (int64_t)(((uint64_t)hi << 32) | lo);
+      const int mt = (int)((a.mti_pos - 1 + cons) % 624) + 1;
+      const int64_t off = cons - mt;
+      if (a.mti_pos >= 1 && a.mti_pos <= 624 && cons > 0 && off >= -a.raw_back && off + 624 <= a.nraw) {
+        smti = mt;
+        soff = off;
+      }
+    }
+  }
+  __syncthreads();
+  if (smti) {
+    for (int i = threadIdx.x; i < 624; i += blockDim.x) a.state_host[i] = a.raw[soff + i];
+  }
+  if (a.state_host && threadIdx.x == 0) a.state_host[624] = smti;
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x != 0) return;
   if (a.tdbg) a.tdbg[15] = wall_clock64();
   __hip_atomic_store(&a.ctr[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (a.status_host) {
-    const int code = phi_get_status(a);
+    const int code = scode;
     const int lo32 = __hip_atomic_load(a.status + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int hi32 = __hip_atomic_load(a.status + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     a.status_host[1] = 0;
@@ -1697,7 +1723,7 @@ size_t phi2_group_lds_bytes(int gs, int nw, double rate) { return phi2_group_lds
 size_t phi2_tree_lds_bytes(int T, int G, int tW) { return phi2_tree_lds(T, G, tW); }
 size_t phi2_values_lds_bytes(int d, int G, int tW, int T) { return phi2_values_lds(d, G, tW, T); }
 
-hipError_t launch_phi2(const PhiArgs& a, hipStream_t s) {
+hipError_t launch_phi2(const PhiArgs& a, hipStream_t s, hipEvent_t before_values) {
   const int64_t items = (int64_t)a.T * a.d;
   if (items <= 0) return hipSuccess;
   if (a.gs < 1 || a.gs > 64 || a.G != (a.d + a.gs - 1) / a.gs || a.G > kPhi2MaxG || a.T > kPhi2MaxT || a.tW < 64 ||
@@ -1710,6 +1736,10 @@ hipError_t launch_phi2(const PhiArgs& a, hipStream_t s) {
   const int th1 = 512;
   HDPM_LAUNCH(k_phi2_group, dim3((unsigned)(a.T * a.G)), dim3(th1), l1, s, a);
   HDPM_LAUNCH(k_phi2_tree, dim3((unsigned)a.T), dim3(1024), l2, s, a);
+  if (before_values) {
+    const hipError_t e = hipStreamWaitEvent(s, before_values, 0);
+    if (e != hipSuccess) return e;
+  }
   HDPM_LAUNCH(k_phi2_values, dim3((unsigned)a.T), dim3(64 * a.wpb), l3, s, a);
   return hipGetLastError();
 }
