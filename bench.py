@@ -478,7 +478,9 @@ def main():
                                                   "phi_device_fallbacks", "phi_fallback_status_mask")},
             "update_phi": {"mode": phi_mode, "where": "device" if st["phi_device_calls"] > 0 else "host",
                            "device_calls": int(st["phi_device_calls"]), "spec_used": int(st["phi_dspec_used"]),
-                           "fast_calls": int(st["phi_fast_calls"]), "fast_handbacks": int(st["phi_fast_handbacks"])},
+                           "fast_calls": int(st["phi_fast_calls"]), "fast_handbacks": int(st["phi_fast_handbacks"]),
+                           "chained": int(st["phi_chain_used"]), "chain_dropped": int(st["phi_chain_dropped"]),
+                           "state_direct": int(st["phi_state_direct"])},
             "pool_generation": {"init": pool_report(st_init, ds.n * args.m),
                                 "regeneration": pool_report(stats_diff(st0, st_init), ds.n * args.m)},
         },

@@ -117,6 +117,10 @@ typedef struct {
     /* device updates whose stream state came back with their outputs (k_phi2_values copies the
      * block of the position after the draws; no state copy to wait for) */
     int64_t phi_state_direct;
+    /* chained device updates (the next iteration's, enqueued behind the current speculation
+     * before it ran): launched, committed, and dropped at the go (the update before them was not
+     * the one committed) */
+    int64_t phi_chain_launched, phi_chain_used, phi_chain_dropped;
 } hdpm_stats;
 
 int         hdpm_device_count(void);

@@ -981,6 +981,7 @@ struct Ctx {
     if (pstream) {
       (void)hipStreamSynchronize(pstream);
       if (dspec.ev) (void)hipEventDestroy(dspec.ev);
+      if (dnext.ev) (void)hipEventDestroy(dnext.ev);
       if (ev_phd_free) (void)hipEventDestroy(ev_phd_free);
       (void)hipStreamDestroy(pstream);
     }
@@ -1235,6 +1236,7 @@ struct Ctx {
     a.nraw = (int64_t)(W.start_pos + (uint64_t)W.count - rng.pos);
     a.raw_back = (int64_t)(rng.pos - W.start_pos);
     a.mti_pos = mti_at(W, rng.pos);
+    a.pos0 = (int64_t)rng.pos;
   }
   // After a device update that consumed up to `target`: the state the fast path copied out
   // (`state`: the block's 624 words, then its index; k_phi2_values), else adopt_state_at.
@@ -2507,6 +2509,7 @@ struct Ctx {
       spec.ran = false;
     }
     dspec.ran = false;                   // (its device work completes unused)
+    dnext.ran = false;
     phi_stream.n = 0;
     pend.active = false;
     rng = ahead.saved;
@@ -2567,9 +2570,9 @@ struct Ctx {
       mcount_clear = false;
     }
     if (dev) {
-      // the speculative device update's tables (phd.stage), once it is done
+      // the speculative device update's tables (its staging buffer), once it is done
       HIPCHK(hipStreamWaitEvent(stream, dspec.ev, 0));
-      HIPCHK(launch_scatter_clusters(phd.stage.p, K, dp, d, bw, 1, d_slot_codes.p, d_slot_tab.p, d_slot_bnd.p,
+      HIPCHK(launch_scatter_clusters(dspec.stage, K, dp, d, bw, 1, d_slot_codes.p, d_slot_tab.p, d_slot_bnd.p,
                                      d_counts.p, d_sol.p, d_los.p, d_src.p, stream, &d_pipe.p[q].gate, d_csum.p,
                                      d_logn.p, zero, d_wide_ctr.p));
       phd_release(stream);
@@ -2646,7 +2649,10 @@ struct Ctx {
     if (pre.dev) {
       commit_later.dev = false;
       stage_full = false;
-      dspec_launch();                  // waits for the enqueued scatter (ev_phd_free)
+      // the chained update enqueued behind the one just committed, else a new one; then the
+      // next iteration's, chained behind it (both wait for the enqueued scatter, ev_phd_free)
+      if (!dspec_promote(m)) dspec_launch();
+      dnext_launch(m);
     } else {
       stage_last = pre.buf;
       stage_full = true;
@@ -3603,8 +3609,19 @@ struct Ctx {
     DevBuf<int> ctr;
     DevBuf<unsigned long long> tdbg;
     int gen = 0;
-    PinBuf<uint8_t> h_in2, h_out2;
+    PinBuf<uint8_t> h_in2;
     DevBuf<uint8_t> d_in2;
+    // by slot (consecutive fast updates alternate, so a chained update reads its predecessor's
+    // labels, counts and sigmas on the device and writes its own tables and outputs beside
+    // them): outputs + status + stream state in coherent host memory, staged tables, labels and
+    // counts, sigmas, chain words
+    PinBuf<uint8_t> out2[2];
+    DevBuf<uint8_t> stage2[2];
+    DevBuf<int> labc2[2];
+    DevBuf<double> sigd2[2];
+    DevBuf<PhiChain> chain2;
+    int slot = 0;                      // the slot of the next fast update
+    bool fast_out(const uint8_t* o) const { return o && (o == out2[0].p || o == out2[1].p); }
     int64_t fast_calls = 0;
     // tree mode when every updated cluster has at least this many members (a small cluster's
     // center picks can depend on the uniform); raised past a cluster size that needed a retry
@@ -3821,8 +3838,12 @@ struct Ctx {
   // (launch_phi2: inputs and outputs in coherent host memory, no copy or fill commands);
   // 1: the general kernels with composition trees; 0: with the per-start-drift walks (both
   // with copies and fills around launch_phi).
+  // chainW (mode 2 only): a chained update (PhiArgs::chain_in) behind the previous fast update
+  // on s, its slice in window chainW after the previous update's end and sweep_len draws; lab,
+  // cnt and sig_in are then unused (the previous update's, on the device).
   const uint8_t* enqueue_phi(PhiArgs& a, const PhiPlan& pl, int mode, const int* lab, const int* cnt,
-                             const double* sig_in, hipStream_t s, hipEvent_t w1 = nullptr, hipEvent_t w2 = nullptr) {
+                             const double* sig_in, hipStream_t s, hipEvent_t w1 = nullptr, hipEvent_t w2 = nullptr,
+                             const RngWindow* chainW = nullptr, int64_t sweep_len = 0) {
     const int T = pl.T;
     const int64_t items = pl.items;
     size_t o_pick, o_sig, o_ll, bytes;
@@ -3834,8 +3855,21 @@ struct Ctx {
     const size_t o_sigin = align16((size_t)2 * T * 4), in_bytes = o_sigin + (size_t)items * 8;
     if (mode == 2) {
       const size_t o_state = align16(bytes);             // the stream state after the update
-      phd.h_in2.ensure(in_bytes + 64, hipHostMallocCoherent);
-      phd.h_out2.ensure(o_state + 625 * 4 + 64, hipHostMallocCoherent);
+      const int sl = phd.slot;
+      phd.slot ^= 1;
+      PinBuf<uint8_t>& hout = phd.out2[sl];
+      hout.ensure(o_state + 625 * 4 + 64, hipHostMallocCoherent);
+      phd.stage2[sl].ensure(upload_layout(T, dp, d, bw).bytes);
+      a.stage = phd.stage2[sl].p;
+      phd.labc2[sl].ensure(2 * T);
+      phd.sigd2[sl].ensure(items);
+      if (!phd.chain2.p) {
+        phd.chain2.ensure(2);
+        HIPCHK(hipMemset(phd.chain2.p, 0, 2 * sizeof(PhiChain)));
+      }
+      a.chain_out = phd.chain2.p + sl;
+      a.sig_dev = phd.sigd2[sl].p;
+      a.lab_dev = phd.labc2[sl].p;   // (k_phi2_group's copy of the labels and counts for k_phi2_values)
       if (!phd.ctr.p) {
         phd.ctr.ensure(2);
         HIPCHK(hipMemset(phd.ctr.p, 0, 2 * sizeof(int)));
@@ -3847,30 +3881,42 @@ struct Ctx {
         HIPCHK(hipMemset(phd.status.p, 0, 16));
         phd.gen = 1;
       }
-      int* hl = (int*)phd.h_in2.p;
-      std::memcpy(hl, lab, (size_t)T * 4);
-      std::memcpy(hl + T, cnt, (size_t)T * 4);
-      std::memcpy(phd.h_in2.p + o_sigin, sig_in, (size_t)items * 8);
-      ((volatile int*)phd.h_out2.p)[0] = -1;           // (written by the last k_phi2_values workgroup)
-      // the inputs to the device in one copy, queued before the update's waits (the sweep's
-      // scatter, the stream window) so it overlaps them: the kernels then read device memory
-      // (a kernel's reads of host memory cost it a PCIe round trip each)
-      phd.d_in2.ensure(in_bytes + 64);
-      HIPCHK(hipMemcpyAsync(phd.d_in2.p, phd.h_in2.p, in_bytes, hipMemcpyHostToDevice, s));
-      if (w1) HIPCHK(hipStreamWaitEvent(s, w1, 0));
+      ((volatile int*)hout.p)[0] = -1;                 // (written by the last k_phi2_values workgroup)
+      if (chainW) {
+        // the previous fast update's labels, counts and sigmas, its end position (device words)
+        const int pv = sl ^ 1;
+        a.lab = phd.labc2[pv].p; a.cnt = phd.labc2[pv].p + T; a.sig_in = phd.sigd2[pv].p;
+        a.chain_in = phd.chain2.p + pv;
+        a.win_raw = chainW->raw.p; a.win_start = (int64_t)chainW->start_pos; a.win_count = chainW->count;
+        a.win_mti0 = chainW->mti0;
+        a.sweep_len = sweep_len;
+        a.raw = nullptr; a.nraw = 0; a.raw_back = 0; a.mti_pos = 0; a.pos0 = 0;
+        if (w1) HIPCHK(hipStreamWaitEvent(s, w1, 0));
+      } else {
+        phd.h_in2.ensure(in_bytes + 64, hipHostMallocCoherent);
+        int* hl = (int*)phd.h_in2.p;
+        std::memcpy(hl, lab, (size_t)T * 4);
+        std::memcpy(hl + T, cnt, (size_t)T * 4);
+        std::memcpy(phd.h_in2.p + o_sigin, sig_in, (size_t)items * 8);
+        // the inputs to the device in one copy, queued before the update's waits (the sweep's
+        // scatter, the stream window) so it overlaps them: the kernels then read device memory
+        // (a kernel's reads of host memory cost it a PCIe round trip each)
+        phd.d_in2.ensure(in_bytes + 64);
+        HIPCHK(hipMemcpyAsync(phd.d_in2.p, phd.h_in2.p, in_bytes, hipMemcpyHostToDevice, s));
+        if (w1) HIPCHK(hipStreamWaitEvent(s, w1, 0));
+        const int* dl = (const int*)phd.d_in2.p;
+        a.lab = dl; a.cnt = dl + T; a.sig_in = (const double*)(phd.d_in2.p + o_sigin);
+        a.chain_in = nullptr;
+      }
       // (w2, the release of phd's buffers by the sweep's stream, guards the staging buffer:
       // only k_phi2_values writes it, so only it waits)
-      const int* dl = (const int*)phd.d_in2.p;
-      a.lab = dl; a.cnt = dl + T; a.sig_in = (const double*)(phd.d_in2.p + o_sigin);
-      a.pick = phd.h_out2.p + o_pick;
-      a.sig_out = (double*)(phd.h_out2.p + o_sig);
-      a.ll = (double*)(phd.h_out2.p + o_ll);
-      a.status_host = (int*)phd.h_out2.p;
-      a.state_host = a.raw_ptr == nullptr && a.mti_pos >= 1 ? (uint32_t*)(phd.h_out2.p + o_state) : nullptr;
+      a.pick = hout.p + o_pick;
+      a.sig_out = (double*)(hout.p + o_sig);
+      a.ll = (double*)(hout.p + o_ll);
+      a.status_host = (int*)hout.p;
+      a.state_host = a.raw_ptr == nullptr && (chainW || a.mti_pos >= 1) ? (uint32_t*)(hout.p + o_state) : nullptr;
       if (a.state_host) a.state_host[624] = 0;
       a.gs = pl.gs; a.G = pl.G; a.gtab2 = phd.gtab2.p; a.roots = phd.roots.p; a.ctr = phd.ctr.p; a.gen = phd.gen;
-      phd.lab_cnt.ensure(2 * T);
-      a.lab_dev = phd.lab_cnt.p;   // (k_phi2_group's copy of the labels and counts for k_phi2_values)
       a.tree = nullptr;
       a.lg = nullptr; a.lzz = nullptr;                   // the fast path computes its logits itself
       if (std::getenv("HDPM_PHI_TIMING")) {
@@ -3882,10 +3928,12 @@ struct Ctx {
       HIPCHK(launch_phi2(a, s, w2));
       phd.fast_calls++;
       stats.phi_fast_calls++;
-      return phd.h_out2.p;
+      return hout.p;
     }
     if (w1) HIPCHK(hipStreamWaitEvent(s, w1, 0));
     if (w2) HIPCHK(hipStreamWaitEvent(s, w2, 0));
+    a.stage = phd.stage.p;
+    a.chain_in = nullptr; a.chain_out = nullptr; a.sig_dev = nullptr;
     phd.h_in.ensure(in_bytes + 64);
     phd.h_out.ensure(bytes);
     int* hl = (int*)phd.h_in.p;
@@ -3939,7 +3987,7 @@ struct Ctx {
     const PhiPlan pf = fast_plan(T, false, min_count, &fast);
     if (!pl.ok) return -1;
     const int64_t items = pl.items, need = pl.need;
-    dspec_wait();                                         // a speculation's use of phd is over
+    dspec_drain();                                        // a speculation's use of phd is over
     RngWindow* W = window_at(rng.pos, need);
     if (!W) return -1;
     auto tp0 = std::chrono::steady_clock::now();
@@ -3956,12 +4004,14 @@ struct Ctx {
     size_t o_pick, o_sig, o_ll, obytes;
     phi_out_layout(T, d, &o_pick, &o_sig, &o_ll, &obytes);
     const uint8_t* out = nullptr;
+    uint8_t* out_stage = nullptr;      // the staged tables of the update that produced `out`
     auto run = [&](int mode) {
       const PhiPlan& pm = mode == 2 ? pf : pl;
       PhiArgs a = phi_args(pm);
       a.freq = fsrc;
       phi_raw(a, *W);
       out = enqueue_phi(a, pm, mode, labs.data(), cnts.data(), sigs.data(), stream, W->done);
+      out_stage = a.stage;
     };
     // the fast path, else the composition trees unless a cluster is small enough for a pick to
     // depend on the uniform (debug bit 27: always the per-start-drift walks)
@@ -4044,7 +4094,7 @@ struct Ctx {
     }
     stats.phi_device_calls++;
     // commit: tables on the device, parameters on the host, the stream past the draws
-    HIPCHK(launch_scatter_clusters(phd.stage.p, T, dp, d, bw, full ? 1 : 0, d_slot_codes.p, d_slot_tab.p, d_slot_bnd.p,
+    HIPCHK(launch_scatter_clusters(out_stage, T, dp, d, bw, full ? 1 : 0, d_slot_codes.p, d_slot_tab.p, d_slot_bnd.p,
                                    d_counts.p, d_sol.p, d_los.p, d_src.p, stream));
     phd_release(stream);
     const uint8_t* pk = out + o_pick;
@@ -4067,7 +4117,7 @@ struct Ctx {
       tables_dirty = false;
     }
     stage_full = false;                // the host staging no longer mirrors the device tables
-    adopt_after_phi(*W, target, out == phd.h_out2.p ? (const uint32_t*)(out + phi_state_off(T, d)) : nullptr);
+    adopt_after_phi(*W, target, phd.fast_out(out) ? (const uint32_t*)(out + phi_state_off(T, d)) : nullptr);
     // the drift model follows the chain: extra uniforms per sigma draw seen here
     PhiDevice::adapt(phd.p_rej, cons - 3 * items, items);
     stats.t_host_phi_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp0).count();
@@ -4093,10 +4143,21 @@ struct Ctx {
     RngWindow* W = nullptr;
     bool tree = false;
     size_t o_pick = 0, o_sig = 0, o_ll = 0;
-    const uint8_t* out = nullptr;      // its outputs (phd.h_out, or phd.h_out2 on the fast path)
+    const uint8_t* out = nullptr;      // its outputs (phd.h_out, or phd.out2[slot] on the fast path)
     bool fast = false;
     hipEvent_t ev = nullptr;           // they are complete
-  } dspec;
+    uint8_t* stage = nullptr;          // its staged tables
+    int gen = 0;                       // fast path: its status generation
+    int prev_gen = 0;                  // chained: the update it follows
+    uint64_t est_pos = 0;              // chained: its nominal first position (when launched)
+    uint64_t wgen = 0;                 // W's generation when launched
+    int64_t sweep_len = 0;             // chained: the sweep's draws before it
+  } dspec, dnext;
+  // dnext: the fast update after dspec's, enqueued behind it on pstream before dspec ran
+  // (chained, PhiArgs::chain_in): the update of the iteration after next, valid when the sweep
+  // between them moves nothing and dspec's update is the one committed (pipe_go promotes it)
+  int committed_gen = 0;               // the fast update update_phi committed last (0: another)
+  bool phi_chain = true;               // HDPM_PHI_CHAIN=0: no chained updates
   hipEvent_t ev_phd_free = nullptr;    // the last device use of phd's buffers on `stream` is done
   bool dspec_on() const { return phi_dev_for((int64_t)K * d) && !(debug & (524288 | 64 | 128)); }
   void phd_release(hipStream_t s) {
@@ -4169,9 +4230,14 @@ struct Ctx {
     a.freq = d_freq.p;
     phi_raw(a, *W);
     const bool tree = pl.tree_ok && (pl.S == 1 || min_count >= phd.tree_min_count) && !(debug & 134217728);
+    dnext.ran = false;                 // (a chained update still queued completes unused)
     dspec.out = enqueue_phi(a, pl, fast ? 2 : tree ? 1 : 0, labs.data(), h_counts.data(), h_sigma.data(), pstream,
                             W->done, ev_phd_free);
     HIPCHK(hipEventRecord(dspec.ev, pstream));
+    dspec.stage = a.stage;
+    dspec.gen = fast ? a.gen : 0;
+    dspec.prev_gen = 0;
+    dspec.wgen = W->gen;
     dspec.ran = true;
     dspec.inflight = true;
     dspec.pos = rng.pos;
@@ -4186,10 +4252,92 @@ struct Ctx {
     stats.phi_dspec_launched++;
   }
 
+  // Every speculation's use of phd's buffers is over (dspec and a chained dnext).
+  void dspec_drain() {
+    dspec_wait();
+    if (dnext.inflight) {
+      HIPCHK(hipEventSynchronize(dnext.ev));
+      dnext.inflight = false;
+    }
+    dnext.ran = false;
+  }
+
+  // The chained update after dspec's (fast path): enqueued now, behind dspec on pstream, before
+  // dspec ran.  Its first draw follows dspec's end and the next sweep's N (m + 1) draws (found on
+  // the device: k_phi2_* read dspec's chain word), its inputs are dspec's outputs (labels,
+  // counts, sigmas on the device), in the window that holds the nominal stretch; it runs only if
+  // dspec completed.  pipe_go makes it the next iteration's speculation (dspec_promote).
+  void dnext_launch(int m) {
+    dnext.ran = false;
+    static const bool env_off = [] {
+      const char* e = std::getenv("HDPM_PHI_CHAIN");
+      return e && e[0] == '0';
+    }();
+    if (!phi_chain || env_off || !dspec.ran || !dspec.fast || !dspec.inflight || dspec.gen != phd.gen ||
+        phd.fast_backoff > 0 || K <= 0)
+      return;
+    const PhiPlan pl = phi_plan(K, false, kPhiFastSd / kPhiSd);
+    if (!pl.ok || !phi_fast(pl)) return;
+    const int64_t sweep_len = (int64_t)n * (m + 1);
+    const uint64_t lo = dspec.pos + 3 * (uint64_t)dspec.pl.items + (uint64_t)sweep_len;   // >= 3 draws per item
+    const uint64_t hi = dspec.pos + (uint64_t)dspec.pl.need + (uint64_t)sweep_len + (uint64_t)pl.need;
+    RngWindow* W = window_at(lo, (int64_t)(hi - lo));
+    if (!W) return;
+    PhiArgs a = phi_args(pl);
+    a.freq = d_freq.p;
+    if (!dnext.ev) HIPCHK(hipEventCreateWithFlags(&dnext.ev, hipEventDisableTiming));
+    dnext.out = enqueue_phi(a, pl, 2, nullptr, nullptr, nullptr, pstream, W->done, ev_phd_free, W, sweep_len);
+    HIPCHK(hipEventRecord(dnext.ev, pstream));
+    dnext.ran = true;
+    dnext.inflight = true;
+    dnext.pos = 0;                     // (known when dspec's update is committed)
+    dnext.epoch = rng.epoch;
+    dnext.lv = 0;
+    dnext.K = K;
+    dnext.moves = -1;
+    dnext.pl = pl;
+    dnext.W = W;
+    dnext.wgen = W->gen;
+    dnext.tree = false;
+    dnext.fast = true;
+    dnext.stage = a.stage;
+    dnext.gen = a.gen;
+    dnext.prev_gen = dspec.gen;
+    dnext.est_pos = lo;
+    dnext.sweep_len = sweep_len;
+    dnext.o_pick = dspec.o_pick;
+    dnext.o_sig = dspec.o_sig;
+    dnext.o_ll = dspec.o_ll;
+    stats.phi_chain_launched++;
+  }
+  // pipe_go (the sweep enqueued ahead goes, dspec's update committed): the chained update
+  // becomes the speculation of the sweep now going when it follows the committed update
+  bool dspec_promote(int m) {
+    if (!dnext.ran) return false;
+    dnext.ran = false;
+    const bool ok = committed_gen != 0 && dnext.prev_gen == committed_gen && dnext.K == K &&
+                    dnext.epoch == rng.epoch && dnext.sweep_len == (int64_t)n * (m + 1) && dnext.W &&
+                    dnext.W->gen == dnext.wgen && covers(*dnext.W, rng.pos, dnext.pl.need) && dspec_on() &&
+                    !dspec.inflight;
+    if (!ok) {
+      stats.phi_chain_dropped++;
+      return false;
+    }
+    std::swap(dspec, dnext);
+    dspec.ran = true;
+    dspec.pos = rng.pos;
+    dspec.lv = 0;
+    dspec.moves = -1;
+    dnext.ran = false;
+    dnext.inflight = false;
+    stats.phi_dspec_launched++;
+    return true;
+  }
+
   // The tables of the committed speculation, from phd.stage into the slots (full upload).
   void scatter_dev_stage(int T) {
     HIPCHK(hipStreamWaitEvent(stream, dspec.ev, 0));
-    HIPCHK(launch_scatter_clusters(phd.stage.p, T, dp, d, bw, 1, d_slot_codes.p, d_slot_tab.p, d_slot_bnd.p, d_counts.p,
+    HIPCHK(launch_scatter_clusters(dspec.stage, T, dp, d, bw, 1, d_slot_codes.p, d_slot_tab.p, d_slot_bnd.p, d_counts.p,
                                    d_sol.p, d_los.p, d_src.p, stream));
     phd_release(stream);
   }
@@ -4219,7 +4367,7 @@ struct Ctx {
         phd.tree_min_count = std::max(phd.tree_min_count, std::min(1 << 20, 2 * mc));
       }
     }
-    if (status != kPhiOk || cons <= 0 || !dspec.W || !can_adopt(*dspec.W, target) ||
+    if (status != kPhiOk || cons <= 0 || !dspec.W || dspec.W->gen != dspec.wgen || !can_adopt(*dspec.W, target) ||
         !covers(*dspec.W, rng.pos, dspec.pl.need)) {
       phd.fallbacks++;
       stats.phi_device_fallbacks++;
@@ -4228,6 +4376,8 @@ struct Ctx {
     }
     stats.phi_device_calls++;
     stats.phi_dspec_used++;
+    if (dspec.prev_gen) stats.phi_chain_used++;
+    committed_gen = dspec.fast ? dspec.gen : 0;
     const uint32_t* st_words = dspec.fast ? (const uint32_t*)(dspec.out + phi_state_off(T, d)) : nullptr;
     // tables: by the sweep enqueued ahead (its gated scatter, pipe_go), flush_commit, or now
     if (defer_commit) {
@@ -4297,7 +4447,7 @@ struct Ctx {
     if (!pl.ok) return -1;
     RngWindow* W = window_at(rng.pos, pl.need);
     if (!W) return -1;
-    dspec_wait();
+    dspec_drain();
     const int64_t items = pl.items;
     const size_t fw = (size_t)T * d * mmax;
     h_sm_freq.ensure(fw);
@@ -4362,7 +4512,7 @@ struct Ctx {
     const uint8_t* pk = out + o_pick;
     for (int64_t q = 0; q < items; ++q) cen[q] = (uint8_t)(pk[q] + 1);
     std::memcpy(sig, out + o_sig, (size_t)items * 8);
-    adopt_after_phi(*W, target, out == phd.h_out2.p ? (const uint32_t*)(out + phi_state_off(T, d)) : nullptr);
+    adopt_after_phi(*W, target, phd.fast_out(out) ? (const uint32_t*)(out + phi_state_off(T, d)) : nullptr);
     rng_sync();                        // split-merge draws on the host next
     PhiDevice::adapt(phd.p_rej_sm, cons - 3 * items, items, 0.9);
     return kOk;
@@ -4371,8 +4521,10 @@ struct Ctx {
   int update_phi(const int32_t* idx, int nidx) {
     if (!have_state) { err = "no state"; return kArg; }
     // the log-likelihood a full device update summed belongs to the parameters before this
-    // update: only a full device commit below sets it again
+    // update: only a full device commit below sets it again (and the chained update follows
+    // only a committed speculation)
     dev_ll_version = 0;
+    committed_gen = 0;
     HostPool& pool = HostPool::get();
     pool.prewake();                                   // workers spin while the device counts
     auto t0c = std::chrono::steady_clock::now();

@@ -512,6 +512,25 @@ struct PhiArgs {
   uint32_t* state_host;
   int mti_pos;               // the index in its block (1..624) of the update's first position
   int64_t raw_back;          // words of the stream window before `raw`
+  // chained updates (fast path): an update enqueued behind the previous one before that one
+  // ran.  With chain_in set, its first draw is at chain_in->end + sweep_len (the previous
+  // update's end, then the sweep between them) inside the window (win_raw, win_start, win_count,
+  // win_mti0: raw, nraw, raw_back and mti_pos are derived on the device), its labels, counts and
+  // sigmas are the previous update's (lab / cnt / sig_in point at its lab_dev and sig_dev), and
+  // it runs only if the previous update completed (else status kPhiOff, nothing computed).
+  const struct PhiChain* chain_in;
+  struct PhiChain* chain_out;  // this update's end position and completion, or nullptr
+  int64_t pos0;              // absolute stream position of the first draw (chain_in: set on the device)
+  const uint32_t* win_raw;
+  int64_t win_start, win_count;
+  int win_mti0;
+  double* sig_dev;           // [T][d] device copy of sig_out (a chained successor's sig_in), or nullptr
+};
+// Written by the last k_phi2_values workgroup of an update with chain_out.
+struct PhiChain {
+  int64_t end;               // absolute stream position after the update's draws
+  int ok;                    // 1: completed (status 0), 0: not
+  int pad;
 };
 // Level sizes of a composition tree over nb >= 1 level-0 blocks.
 __host__ __device__ inline int phi_lcount(int nb, int l) { return ((nb - 1) >> l) + 1; }
@@ -567,7 +586,8 @@ struct PipeArgs {
 // kPhiNonDet: a center pick depends on the uniform (the composition trees need fixed picks);
 // the update is re-run with the per-start-drift walks (k_phi_cwalk)
 enum PhiStatus { kPhiOk = 0, kPhiWalker = 1, kPhiBisect = 2, kPhiAmbig = 3, kPhiWindow = 4, kPhiShort = 5,
-                 kPhiProb = 6, kPhiInactive = 7, kPhiCap = 8, kPhiNonDet = 9 };
+                 kPhiProb = 6, kPhiInactive = 7, kPhiCap = 8, kPhiNonDet = 9,
+                 kPhiOff = 10 /* chained update whose predecessor did not complete: not run */ };
 
 // R's Mersenne-Twister stream on the device (one workgroup, one twist per barrier).
 // Output r >= 0 continues the host state (X_0, mti0): the first 624 - mti0 outputs temper

@@ -873,6 +873,7 @@ __device__ __forceinline__ void phi_values_body(const PhiArgs& a, int t, const u
     tab[2 * j] = m0;
     tab[2 * j + 1] = m1;
     a.sig_out[k] = sg;
+    if (a.sig_dev) a.sig_dev[k] = sg;
     A += m0;
     sc += fmax(fabs(m0), fabs(m1));
     const double dj = m0 - m1;
@@ -1317,6 +1318,34 @@ __device__ __forceinline__ void phi2_stage_u16(uint16_t* dst, const uint16_t* sr
 }
 
 
+// A chained update's stream slice from its predecessor's end (PhiArgs::chain_in); false: the
+// predecessor did not complete or the slice is not inside the window (the update is off).
+// Wave-uniform (readfirstlane): the branches on it are scalar.
+__device__ __forceinline__ bool phi2_chain(PhiArgs& a) {
+  if (!a.chain_in) return true;
+  const int ok = __builtin_amdgcn_readfirstlane(
+      __hip_atomic_load(&a.chain_in->ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  if (!ok) return false;
+  const uint64_t e = __hip_atomic_load((const uint64_t*)&a.chain_in->end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t elo = __builtin_amdgcn_readfirstlane((uint32_t)e), ehi = __builtin_amdgcn_readfirstlane((uint32_t)(e >> 32));
+  const int64_t p = (int64_t)(((uint64_t)ehi << 32) | elo) + a.sweep_len;
+  const int64_t r = p - a.win_start;
+  if (r < 0 || r + a.span + 1 > a.win_count) return false;
+  a.pos0 = p;
+  a.raw = a.win_raw + r;
+  a.nraw = a.win_count - r;
+  a.raw_back = r;
+  // the index of p in its block (engine.cpp mti_at)
+  const int64_t head = a.win_mti0 >= 624 ? 0 : 624 - a.win_mti0;
+  if (r < head) {
+    a.mti_pos = a.win_mti0 + (int)r;
+  } else {
+    const int k = (int)((r - head) % 624);
+    a.mti_pos = k == 0 ? 624 : k;
+  }
+  return true;
+}
+
 constexpr int kPhi2MaxG = 512;        // groups per cluster (d <= 4096 at gs = 8)
 constexpr int kPhi2MaxT = 1024;       // clusters of one fast-path update
 
@@ -1342,6 +1371,7 @@ __host__ __device__ inline size_t phi2_values_lds(int d, int G, int tW, int T) {
 __global__ __launch_bounds__(512) void k_phi2_group(PhiArgs a) {
   if (gate_closed(a.gate)) return;
   if (a.raw_ptr) a.raw = *a.raw_ptr;
+  if (!phi2_chain(a)) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
   __shared__ uint64_t tabs[512];
   __shared__ int sbad;
@@ -1487,6 +1517,7 @@ __global__ __launch_bounds__(512) void k_phi2_group(PhiArgs a) {
 // cluster tables from drift 0.
 __global__ __launch_bounds__(1024) void k_phi2_tree(PhiArgs a) {
   if (gate_closed(a.gate)) return;
+  if (!phi2_chain(a)) return;
   extern __shared__ __attribute__((aligned(16))) uint16_t st[];
   __shared__ int sglo[kPhi2MaxG];                     // window start of each group's first item (of cluster)
   const int G = a.G, tW = a.tW, d = a.d, gs = a.gs;
@@ -1608,8 +1639,12 @@ __global__ __launch_bounds__(1024) void k_phi2_values(PhiArgs a) {
   uint16_t* sroot = reinterpret_cast<uint16_t*>(spick + align16((size_t)d));   // [t + 1][tW] cluster tables
   __shared__ int64_t sclo[kPhi2MaxT];                  // window start of each cluster up to t
   phi2_mark(a, 0, 11);
+  const bool on = phi2_chain(a);
   for (int i = threadIdx.x; i < 512; i += blockDim.x) tabs[i] = a.gtab[i];
-  if (threadIdx.x == 0) sbad = phi_get_status(a) != 0;
+  if (threadIdx.x == 0) {
+    if (!on) phi_set_status(a, kPhiOff);
+    sbad = !on || phi_get_status(a) != 0;
+  }
   __syncthreads();
   if (!sbad) {
     phi2_stage_u16(stb, a.gtab2 + (int64_t)t * G * tW, G * tW);
@@ -1702,6 +1737,12 @@ __global__ __launch_bounds__(1024) void k_phi2_values(PhiArgs a) {
     for (int i = threadIdx.x; i < 624; i += blockDim.x) a.state_host[i] = a.raw[soff + i];
   }
   if (a.state_host && threadIdx.x == 0) a.state_host[624] = smti;
+  if (a.chain_out && threadIdx.x == 0) {
+    const uint32_t lo = (uint32_t)__hip_atomic_load(a.status + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t hi = (uint32_t)__hip_atomic_load(a.status + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    a.chain_out->end = a.pos0 + (int64_t)(((uint64_t)hi << 32) | lo);
+    a.chain_out->ok = scode == 0 ? 1 : 0;
+  }
   __threadfence_system();
   __syncthreads();
   if (threadIdx.x != 0) return;
