@@ -919,10 +919,11 @@ __global__ __launch_bounds__(kWideThreads, (wide_min_waves<WB, NW>())) void k_pr
 
 // Workgroups of k_prepass_wide in flight on the whole GPU (persistent grid).
 template <class F>
-static int wide_grid(F kern, size_t lds) {
+static int wide_grid(F kern, size_t lds, int want) {
   const int cus = device_cus();
   int per = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, kWideThreads, lds) != hipSuccess || per <= 0) per = 1;
+  if (want > 0) per = std::min(per, want);
   // HDPM_WIDE_WGS: workgroups per CU (A/B of the persistent grid)
   static const int ovr = [] {
     const char* e = std::getenv("HDPM_WIDE_WGS");
@@ -3547,7 +3548,7 @@ static hipError_t launch_prepass_w(const PrepassArgs& a, int nblocks, hipStream_
     auto go = [&](auto kern) {
       // (the same number of chunks for every workgroup -- 875 workgroups x 5 chunks at C4 instead of
       // 1,024 x 4-5 -- measured 54 against 47 us: the kernel wants every resident wave)
-      const int grid = std::min(nchunks, wide_grid(kern, lds));
+      const int grid = std::min(nchunks, wide_grid(kern, lds, a.wide_per_cu));
       // HDPM_WIDE_CLAIM=1: chunks claimed from a counter (A/B; see k_prepass_wide)
       static const int claim = [] {
         const char* e = std::getenv("HDPM_WIDE_CLAIM");

@@ -174,6 +174,9 @@ struct PrepassArgs {
   // is set, and read the sweep's draws from *raw_ptr (a position found on the device)
   const int* gate;
   const uint32_t* const* raw_ptr;
+  // k_prepass_wide's persistent grid: workgroups per CU (0: as many as fit).  Fewer leave room
+  // on every CU for the device update_phi beside the sweep (engine.cpp wide_per_cu).
+  int wide_per_cu = 0;
 };
 
 // A latent entry kept as a head bound counts as probability 0 this far below the best
@@ -501,7 +504,7 @@ struct PhiArgs {
   int gs, G;
   uint16_t* gtab2;           // [T * G][tW] group tables
   uint16_t* roots;           // [T][tW] cluster tables
-  int* ctr;                  // [2] last-workgroup counters of k_phi2_tree / k_phi2_values (self-resetting)
+  int* ctr;                  // [2] last-workgroup counters ([1]: k_phi2_values; self-resetting)
   int gen;                   // status generation: status[0] = gen << 4 | code belongs to this call
   int* status_host;          // [4] status (code, -, consumption int64) written by the last k_phi2_values workgroup
   unsigned long long* tdbg;  // testing (HDPM_PHI_TIMING): wall-clock marks of the fast path's phases, or nullptr

@@ -190,6 +190,10 @@ __device__ bool phi_rbeta_setup(double aa, double bb, PhiCand* c) {
 __device__ __forceinline__ void phi2_mark(const PhiArgs& a, int blk, int q) {
   if (a.tdbg && (int)blockIdx.x == blk && threadIdx.x == 0) a.tdbg[q] = wall_clock64();
 }
+// (the latest workgroup to reach the mark)
+__device__ __forceinline__ void phi2_mark_last(const PhiArgs& a, int q) {
+  if (a.tdbg && threadIdx.x == 0) atomicMax(&a.tdbg[q], (unsigned long long)wall_clock64());
+}
 
 __device__ __forceinline__ int wave_excl_scan(int v, int* total) {
   const int lane = threadIdx.x & 63;
@@ -1286,8 +1290,9 @@ __global__ __launch_bounds__(1024) void k_phi_values2(PhiArgs a) {
 //                  can read (in LDS), the items' masks over the window (LDS and maskd), and the
 //                  group's table: the extra uniforms of its gs items from each of tW start drifts
 //   k_phi2_tree    one workgroup per cluster: its group tables composed in LDS into the
-//                  cluster's table; the last workgroup to finish chains the cluster tables from
-//                  drift 0 (the clusters' start drifts, the consumption)
+//                  cluster's table (phi2_tree_body).  (Run by the last group workgroup of each
+//                  cluster instead, behind a per-cluster arrival counter, it cost ~80 us at C4:
+//                  every workgroup's agent-scope release writes back its XCD's L2.)
 //   k_phi2_values  one workgroup per cluster: its groups' start drifts (the group tables from
 //                  the cluster's start), each group walked by one wave (a lane per item,
 //                  fixed-point rounds over the prefetched mask words), then phi_values_body; the
@@ -1379,6 +1384,7 @@ __global__ __launch_bounds__(512) void k_phi2_group(PhiArgs a) {
   const int t = blockIdx.x / G, g = blockIdx.x - t * G;
   const int j0 = g * gs, ni = min(gs, d - j0);
   const int64_t k0 = (int64_t)t * d + j0;
+  phi2_mark_last(a, 19);
   PoolClass* sp = reinterpret_cast<PoolClass*>(sm);
   int* slo = reinterpret_cast<int*>(sm + align16((size_t)gs * sizeof(PoolClass)));
   __shared__ int snw[64];
@@ -1470,6 +1476,7 @@ __global__ __launch_bounds__(512) void k_phi2_group(PhiArgs a) {
   }
   __syncthreads();
   phi2_mark(a, 0, 2);
+  phi2_mark_last(a, 20);
   if (sbad) return;
   // 4. masks: bit i of word q of item j is the attempt at drift lo_j + 64 q + i (as k_phi_masks)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
@@ -1500,6 +1507,7 @@ __global__ __launch_bounds__(512) void k_phi2_group(PhiArgs a) {
   }
   __syncthreads();
   phi2_mark(a, 0, 3);
+  phi2_mark_last(a, 21);
   // 4. the group's table: the extra uniforms of its items from start drift lo_0 + c
   uint16_t* out = a.gtab2 + ((int64_t)t * G + g) * tW;
   for (int c = threadIdx.x; c < tW; c += blockDim.x) {
@@ -1511,57 +1519,57 @@ __global__ __launch_bounds__(512) void k_phi2_group(PhiArgs a) {
   }
   __syncthreads();
   phi2_mark(a, 0, 4);
+  phi2_mark_last(a, 22);
 }
 
-// Cluster t's group tables composed into its table (a.roots); the last workgroup chains the
-// cluster tables from drift 0.
+// Cluster t's group tables composed into its table (a.roots) in LDS `st` (phi2_tree_lds);
+// sglo: [G] LDS scratch.
+__device__ __forceinline__ void phi2_tree_body(const PhiArgs& a, int t, uint16_t* st, int* sglo) {
+  const int G = a.G, tW = a.tW, d = a.d, gs = a.gs;
+  phi2_mark(a, 0, 5);
+  __shared__ int sok;
+  if (threadIdx.x == 0) sok = phi_get_status(a) == 0;   // (one atomic load per workgroup, not per thread)
+  __syncthreads();
+  if (!sok) return;
+  uint16_t* A = st;                                     // G tables, then the levels above in B
+  uint16_t* B = st + (size_t)G * tW;
+  for (int g = threadIdx.x; g < G; g += blockDim.x) sglo[g] = (int)phi_lo((int64_t)t * d + (int64_t)g * gs, a.rate, a.sdev);
+  phi2_stage_u16(A, a.gtab2 + (int64_t)t * G * tW, G * tW);
+  __syncthreads();
+  phi2_mark(a, 0, 6);
+  uint16_t* cur = A;
+  uint16_t* nxt = B;
+  int np = G, span = 1;                                 // nodes, groups per node
+  while (np > 1) {
+    const int nl = (np + 1) / 2;
+    // every node of the level at once (the lookups of different nodes are independent)
+    for (int c = threadIdx.x; c < tW; c += blockDim.x) {
+      for (int li = 0; li < nl; ++li) {
+        const uint16_t* L = cur + (size_t)(2 * li) * tW;
+        uint16_t v;
+        if (2 * li + 1 < np)
+          v = phi_tree_compose(L, cur + (size_t)(2 * li + 1) * tW, sglo[2 * li * span], sglo[(2 * li + 1) * span], tW, c);
+        else
+          v = L[c];
+        nxt[(size_t)li * tW + c] = v;
+      }
+    }
+    __syncthreads();
+    // ping-pong: the level just written becomes the source; the next goes where the old source was
+    cur = nxt;
+    nxt = (cur == B) ? A : B;
+    np = nl;
+    span *= 2;
+  }
+  for (int c = threadIdx.x; c < tW; c += blockDim.x) a.roots[(int64_t)t * tW + c] = cur[c];
+  phi2_mark(a, 0, 7);
+}
 __global__ __launch_bounds__(1024) void k_phi2_tree(PhiArgs a) {
   if (gate_closed(a.gate)) return;
   if (!phi2_chain(a)) return;
   extern __shared__ __attribute__((aligned(16))) uint16_t st[];
   __shared__ int sglo[kPhi2MaxG];                     // window start of each group's first item (of cluster)
-  const int G = a.G, tW = a.tW, d = a.d, gs = a.gs;
-  const int t = blockIdx.x;
-  phi2_mark(a, 0, 5);
-  __shared__ int sok;
-  if (threadIdx.x == 0) sok = phi_get_status(a) == 0;   // (one atomic load per workgroup, not per thread)
-  __syncthreads();
-  if (sok) {
-    uint16_t* A = st;                                   // G tables, then the levels above in B
-    uint16_t* B = st + (size_t)G * tW;
-    for (int g = threadIdx.x; g < G; g += blockDim.x) sglo[g] = (int)phi_lo((int64_t)t * d + (int64_t)g * gs, a.rate, a.sdev);
-    phi2_stage_u16(A, a.gtab2 + (int64_t)t * G * tW, G * tW);
-    __syncthreads();
-    phi2_mark(a, 0, 6);
-    uint16_t* cur = A;
-    uint16_t* nxt = B;
-    int np = G, span = 1;                               // nodes, groups per node
-    while (np > 1) {
-      const int nl = (np + 1) / 2;
-      // every node of the level at once (the lookups of different nodes are independent)
-      for (int c = threadIdx.x; c < tW; c += blockDim.x) {
-        for (int li = 0; li < nl; ++li) {
-          const uint16_t* L = cur + (size_t)(2 * li) * tW;
-          uint16_t v;
-          if (2 * li + 1 < np)
-            v = phi_tree_compose(L, cur + (size_t)(2 * li + 1) * tW, sglo[2 * li * span], sglo[(2 * li + 1) * span], tW, c);
-          else
-            v = L[c];
-          nxt[(size_t)li * tW + c] = v;
-        }
-      }
-      __syncthreads();
-      // ping-pong: the level just written becomes the source; the next goes where the old source was
-      uint16_t* tmp = cur;
-      cur = nxt;
-      nxt = (cur == B) ? A : B;
-      (void)tmp;
-      np = nl;
-      span *= 2;
-    }
-    for (int c = threadIdx.x; c < tW; c += blockDim.x) a.roots[(int64_t)t * tW + c] = cur[c];
-    phi2_mark(a, 0, 7);
-  }
+  phi2_tree_body(a, blockIdx.x, st, sglo);
 }
 
 // One wave: group g's items from start drift e0 (lane i = item j0 + i), the drift of each
@@ -1638,6 +1646,7 @@ __global__ __launch_bounds__(1024) void k_phi2_values(PhiArgs a) {
   uint8_t* spick = reinterpret_cast<uint8_t*>(sapos) + align16((size_t)d * 8);
   uint16_t* sroot = reinterpret_cast<uint16_t*>(spick + align16((size_t)d));   // [t + 1][tW] cluster tables
   __shared__ int64_t sclo[kPhi2MaxT];                  // window start of each cluster up to t
+  __shared__ int sglo3[kPhi2MaxG];                     // window start of each of its groups
   phi2_mark(a, 0, 11);
   const bool on = phi2_chain(a);
   for (int i = threadIdx.x; i < 512; i += blockDim.x) tabs[i] = a.gtab[i];
@@ -1650,6 +1659,7 @@ __global__ __launch_bounds__(1024) void k_phi2_values(PhiArgs a) {
     phi2_stage_u16(stb, a.gtab2 + (int64_t)t * G * tW, G * tW);
     phi2_stage_u16(sroot, a.roots, (t + 1) * tW);
     for (int u = threadIdx.x; u <= t; u += blockDim.x) sclo[u] = phi_lo((int64_t)u * d, a.rate, a.sdev);
+    for (int g = threadIdx.x; g < G; g += blockDim.x) sglo3[g] = (int)phi_lo((int64_t)t * d + (int64_t)g * gs, a.rate, a.sdev);
     for (int j = threadIdx.x; j < d; j += blockDim.x) spick[j] = (uint8_t)(a.det[(int64_t)t * d + j] - 1);
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1675,7 +1685,7 @@ __global__ __launch_bounds__(1024) void k_phi2_values(PhiArgs a) {
       for (int g = 0; g <= G && !sbad; ++g) {
         sgs[g] = e;
         if (g == G) break;
-        const int64_t c = e - phi_lo((int64_t)t * d + (int64_t)g * gs, a.rate, a.sdev);
+        const int64_t c = e - sglo3[g];
         const uint16_t v = (c >= 0 && c < tW) ? stb[(size_t)g * tW + c] : kPhiBad;
         if (v == kPhiBad) {
           sbad = 1;
