@@ -475,12 +475,13 @@ def main():
             # slow path ran): device-wide resolver give-ups, restricted scans that gave up on many
             # CUs, sweeps enqueued ahead and re-run ungated, device update_phi handed to the host
             "fallbacks": {k: int(st[k]) for k in ("fpg_aborts", "sm_wide_fallbacks", "pipe_recovered",
-                                                  "phi_device_fallbacks", "phi_fallback_status_mask")},
+                                                  "phi_device_fallbacks", "phi_fallback_status_mask",
+                                                  "pipe_desync")},
             "update_phi": {"mode": phi_mode, "where": "device" if st["phi_device_calls"] > 0 else "host",
                            "device_calls": int(st["phi_device_calls"]), "spec_used": int(st["phi_dspec_used"]),
                            "fast_calls": int(st["phi_fast_calls"]), "fast_handbacks": int(st["phi_fast_handbacks"]),
                            "chained": int(st["phi_chain_used"]), "chain_dropped": int(st["phi_chain_dropped"]),
-                           "state_direct": int(st["phi_state_direct"])},
+                           "state_direct": int(st["phi_state_direct"]), "device_go": int(st["pipe_auto"])},
             "pool_generation": {"init": pool_report(st_init, ds.n * args.m),
                                 "regeneration": pool_report(stats_diff(st0, st_init), ds.n * args.m)},
         },

@@ -121,6 +121,10 @@ typedef struct {
      * before it ran): launched, committed, and dropped at the go (the update before them was not
      * the one committed) */
     int64_t phi_chain_launched, phi_chain_used, phi_chain_dropped;
+    /* sweeps enqueued ahead that the device started itself (k_pipe_wait's own go behind a
+     * completed device update, no host round trip), and goes the host could not follow (the
+     * chain state is then undefined and the context reports an error; never expected) */
+    int64_t pipe_auto, pipe_desync;
 } hdpm_stats;
 
 int         hdpm_device_count(void);

@@ -76,7 +76,8 @@ class Stats(C.Structure):
                                   "exact_lanes_launches", "dense_launches", "sm_wide_scans",
                                   "sm_wide_fallbacks", "phi_fast_calls", "phi_fast_handbacks",
                                   "labels_mirrored", "labels_downloaded", "phi_state_direct",
-                                  "phi_chain_launched", "phi_chain_used", "phi_chain_dropped")]
+                                  "phi_chain_launched", "phi_chain_used", "phi_chain_dropped",
+                                  "pipe_auto", "pipe_desync")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -63,8 +63,8 @@ hipError_t launch_scatter_clusters(const uint8_t* stage, int nent, int dp, int d
                                    hipStream_t s, const int* gate = nullptr, uint64_t* csum = nullptr,
                                    const double* logn = nullptr, int* zero = nullptr, int* wide_ctr = nullptr);
 hipError_t launch_phi_locate(const PipeArgs& a, hipStream_t s);
-hipError_t launch_pipe_wait(const PipeSlot* slot, const ResolveCtl* prev, ResolveCtl* own, int n, PipeGate* g,
-                            long long limit, hipStream_t s);
+hipError_t launch_pipe_wait(PipeSlot* slot, const ResolveCtl* prev, ResolveCtl* own, int n, PipeGate* g,
+                            long long limit, hipStream_t s, const PipeAuto& au);
 hipError_t launch_pipe_check(const PipeArgs& a, hipStream_t s);
 hipError_t launch_pool_heads(const double* tab, const uint64_t* bnd, int64_t P, int d, int wb, int Ws, int bw, int ha,
                              int hb, uint64_t* head, hipStream_t s);
@@ -861,7 +861,25 @@ struct Ctx {
     bool dev = false;                  // its tables come from the device speculation (phd.stage)
     uint64_t gen[2] = {0, 0};          // window launches the kernels waited for
     std::chrono::steady_clock::time_point t_enq;   // the wait kernel was queued (pipe_go's deadline)
+    bool au = false;                   // the wait kernel may give the go itself (PipeAuto)
   } pre;
+  bool pipe_auto = true;               // device-side go for the device update's pipeline (HDPM_PIPE_AUTO=0: off)
+  // PipeAuto: the wait kernel's decision (1: it gave the go, 2: it waits for the host), once it
+  // has run (it runs once the previous sweep and the speculated update are done: microseconds)
+  int pre_dev_decision() {
+    if (!pre.active || !pre.au) return 0;
+    const int* w = &h_pipe.p[pre.par].dev;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int polls = 0;; ++polls) {
+      const int v = __atomic_load_n(w, __ATOMIC_ACQUIRE);
+      if (v != 0) return v;
+      HostPool::spin_pause();
+      if ((polls & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+        // (the kernel behind the stream's work never ran: treat it as waiting for the flag)
+        return 2;
+      }
+    }
+  }
   // k_pipe_wait's limit in ticks of the 100 MHz clock (2 s), and whether pipe_go refuses a go
   // given after a quarter of it (HDPM_OPT_PIPE_WAIT_US; a negative value turns the check off, to
   // exercise the device-side gate-off and its recovery in neal8_sweep)
@@ -2533,7 +2551,9 @@ struct Ctx {
     d_pipe.ensure(2);
     sweep_buffers(track, m);
     __atomic_store_n(&h_pipe.p[q].flag, 0, __ATOMIC_RELEASE);
+    __atomic_store_n(&h_pipe.p[q].dev, 0, __ATOMIC_RELEASE);
     h_pipe.p[q].raw = nullptr;
+    h_pipe.p[q].raw_dev = nullptr;
     // the next sweep's draws start after this update's (about a slice): the windows that
     // overlap that stretch (not a window generation started for later sweeps)
     const bool dev = !host_spec();
@@ -2555,7 +2575,20 @@ struct Ctx {
         pre.gen[k] = w.gen;
       }
     }
-    HIPCHK(launch_pipe_wait(&h_pipe.p[q], ctl_at(par), ctl_at(q), n, &d_pipe.p[q], pipe_limit_ticks, stream));
+    // the device's own go (PipeAuto) when the speculated update is the fast path's: the wait
+    // kernel goes behind the update's completion and reads its chain word
+    static const bool auto_env_off = [] {
+      const char* e = std::getenv("HDPM_PIPE_AUTO");
+      return e && e[0] == '0';
+    }();
+    PipeAuto au{};
+    if (dev && pipe_auto && !auto_env_off && dspec.ran && dspec.fast && dspec.chain && whole >= 0) {
+      const RngWindow& w = win[whole];
+      au = PipeAuto{dspec.chain, w.raw.p, (int64_t)w.start_pos, w.count, (int64_t)n * (m + 1), 1};
+    }
+    if (dev) HIPCHK(hipStreamWaitEvent(stream, dspec.ev, 0));   // (the update's tables, below)
+    HIPCHK(launch_pipe_wait(&h_pipe.p[q], ctl_at(par), ctl_at(q), n, &d_pipe.p[q], pipe_limit_ticks, stream, au));
+    pre.au = au.on != 0;
     pre.t_enq = std::chrono::steady_clock::now();   // the kernel's clock starts no earlier
     pre.active = true;
     pre.par = q;
@@ -2574,8 +2607,7 @@ struct Ctx {
       mcount_clear = false;
     }
     if (dev) {
-      // the speculative device update's tables (its staging buffer), once it is done
-      HIPCHK(hipStreamWaitEvent(stream, dspec.ev, 0));
+      // the speculative device update's tables (its staging buffer; the stream waited for it)
       HIPCHK(launch_scatter_clusters(dspec.stage, K, dp, d, bw, 1, d_slot_codes.p, d_slot_tab.p, d_slot_bnd.p,
                                      d_counts.p, d_sol.p, d_los.p, d_src.p, stream, &d_pipe.p[q].gate, d_csum.p,
                                      d_logn.p, zero, d_wide_ctr.p));
@@ -2597,6 +2629,14 @@ struct Ctx {
   }
   void pre_release() {
     if (!pre.active) return;
+    if (pre_dev_decision() == 1) {
+      // the device gave the go for a sweep the host now drops: the chain state is no longer
+      // defined (never expected: the device goes only where the host would)
+      (void)hipStreamSynchronize(stream);
+      have_state = false;
+      err = "a sweep went ahead on the device after the host released it";
+      stats.pipe_desync++;
+    }
     pre.active = false;
     __atomic_store_n(&h_pipe.p[pre.par].flag, 2, __ATOMIC_RELEASE);
   }
@@ -2604,36 +2644,54 @@ struct Ctx {
   // update's held staging buffer) become the committed ones, the next speculative update
   // started.  False (nothing done) when it cannot run.
   bool pipe_go(int m) {
-    if (!pre.active || !pre.round_ok || pre.m != m || !commit_later.active || last_sweep_rounds != 1 ||
-        last_sweep_moves != 0 || tables_dirty)
+    // (PipeAuto: the wait kernel may have given the go itself; the host then follows it)
+    const bool went = pre_dev_decision() == 1;
+    const bool agree = pre.active && pre.round_ok && pre.m == m && commit_later.active && last_sweep_rounds == 1 &&
+                       last_sweep_moves == 0 && !tables_dirty;
+    if (went && !(agree && pre.dev && commit_later.dev && freq_dev_valid && freq_version == labels_version)) {
+      (void)hipStreamSynchronize(stream);
+      have_state = false;
+      err = "a sweep went ahead on the device where the host would not have";
+      stats.pipe_desync++;
+      pre.active = false;
       return false;
-    if (pre.dev ? (!commit_later.dev || !dspec_on()) : (commit_later.dev || commit_later.buf != pre.buf || !host_spec()))
-      return false;
-    if (!(freq_dev_valid && freq_version == labels_version)) return false;
-    // the wait kernel gives up after pipe_limit_ticks: a go late enough to race its limit
-    // is refused (the sweep is then released and prepared again); a go the kernel still
-    // misses is recovered in neal8_sweep (kPipeOff)
-    if (pipe_host_check &&
-        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - pre.t_enq).count() >
-            (double)pipe_limit_ticks * 0.01 * 0.25) {
-      stats.pipe_refused++;
-      return false;
+    }
+    if (!went) {
+      if (!agree) return false;
+      if (pre.dev ? (!commit_later.dev || !dspec_on()) : (commit_later.dev || commit_later.buf != pre.buf || !host_spec()))
+        return false;
+      if (!(freq_dev_valid && freq_version == labels_version)) return false;
+      // the wait kernel gives up after pipe_limit_ticks: a go late enough to race its limit
+      // is refused (the sweep is then released and prepared again); a go the kernel still
+      // misses is recovered in neal8_sweep (kPipeOff)
+      if (pipe_host_check &&
+          std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - pre.t_enq).count() >
+              (double)pipe_limit_ticks * 0.01 * 0.25) {
+        stats.pipe_refused++;
+        return false;
+      }
     }
     rng_sync();
     const Rng saved = rng;
     const uint32_t* raw = device_draws((int64_t)n * (m + 1));
-    bool waited = false;
-    for (int k = 0; k < 2; ++k)
-      if (win[k].gen == pre.gen[k] && raw >= win[k].raw.p && raw < win[k].raw.p + win[k].count) waited = true;
-    if (!waited) {                       // a window the enqueued kernels did not wait for
-      pend.active = false;
-      phidev.valid = false;
-      rng = saved;
-      return false;
-    }
     PipeSlot& sl = h_pipe.p[pre.par];
-    __atomic_store_n(&sl.raw, raw, __ATOMIC_RELAXED);
-    __atomic_store_n(&sl.flag, 1, __ATOMIC_RELEASE);
+    if (went) {
+      // the draws the device chose (the same stretch of the stream, in a window it waited for)
+      raw = __atomic_load_n(&sl.raw_dev, __ATOMIC_ACQUIRE);
+      stats.pipe_auto++;
+    } else {
+      bool waited = false;
+      for (int k = 0; k < 2; ++k)
+        if (win[k].gen == pre.gen[k] && raw >= win[k].raw.p && raw < win[k].raw.p + win[k].count) waited = true;
+      if (!waited) {                       // a window the enqueued kernels did not wait for
+        pend.active = false;
+        phidev.valid = false;
+        rng = saved;
+        return false;
+      }
+      __atomic_store_n(&sl.raw, raw, __ATOMIC_RELAXED);
+      __atomic_store_n(&sl.flag, 1, __ATOMIC_RELEASE);
+    }
     pre.active = false;
     mark("go");
     ahead.saved = saved;
@@ -4156,6 +4214,7 @@ struct Ctx {
     uint64_t est_pos = 0;              // chained: its nominal first position (when launched)
     uint64_t wgen = 0;                 // W's generation when launched
     int64_t sweep_len = 0;             // chained: the sweep's draws before it
+    PhiChain* chain = nullptr;         // fast path: its chain word (end position, completion)
   } dspec, dnext;
   // dnext: the fast update after dspec's, enqueued behind it on pstream before dspec ran
   // (chained, PhiArgs::chain_in): the update of the iteration after next, valid when the sweep
@@ -4242,6 +4301,7 @@ struct Ctx {
     dspec.gen = fast ? a.gen : 0;
     dspec.prev_gen = 0;
     dspec.wgen = W->gen;
+    dspec.chain = fast ? a.chain_out : nullptr;
     dspec.ran = true;
     dspec.inflight = true;
     dspec.pos = rng.pos;
@@ -4305,6 +4365,7 @@ struct Ctx {
     dnext.tree = false;
     dnext.fast = true;
     dnext.stage = a.stage;
+    dnext.chain = a.chain_out;
     dnext.gen = a.gen;
     dnext.prev_gen = dspec.gen;
     dnext.est_pos = lo;
@@ -4371,8 +4432,18 @@ struct Ctx {
         phd.tree_min_count = std::max(phd.tree_min_count, std::min(1 << 20, 2 * mc));
       }
     }
-    if (status != kPhiOk || cons <= 0 || !dspec.W || dspec.W->gen != dspec.wgen || !can_adopt(*dspec.W, target) ||
-        !covers(*dspec.W, rng.pos, dspec.pl.need)) {
+    // a sweep the device already started behind this update (PipeAuto) is followed: the update
+    // completed with its stream state (the chain word), so the host takes it as it is
+    const bool followed = pre_dev_decision() == 1;
+    if (followed && (status != kPhiOk || cons <= 0 || !dspec.W)) {
+      (void)hipStreamSynchronize(stream);
+      have_state = false;
+      err = "a sweep went ahead on the device behind an update the host cannot take";
+      stats.pipe_desync++;
+      return -1;
+    }
+    if (!followed && (status != kPhiOk || cons <= 0 || !dspec.W || dspec.W->gen != dspec.wgen ||
+                      !can_adopt(*dspec.W, target) || !covers(*dspec.W, rng.pos, dspec.pl.need))) {
       phd.fallbacks++;
       stats.phi_device_fallbacks++;
       stats.phi_fallback_status_mask |= (int64_t)1 << (status != kPhiOk ? std::min(std::max(status, 0), 14) : 15);

@@ -4347,9 +4347,29 @@ hipError_t launch_finish_sweep(int* counts, int* sol, int* los, int* src, int ca
 // `limit` ticks of the 100 MHz constant clock (every wave exits), then the gate of its
 // kernels: go, and the previous sweep's control block (written by its resolver before this
 // kernel in stream order) shows it complete without a move.
-__global__ void k_pipe_wait(const PipeSlot* slot, const ResolveCtl* prev, ResolveCtl* own, int n, PipeGate* g,
-                            long long limit) {
+__global__ void k_pipe_wait(PipeSlot* slot, const ResolveCtl* prev, ResolveCtl* own, int n, PipeGate* g,
+                            long long limit, PipeAuto au) {
   if (threadIdx.x != 0) return;
+  if (au.on) {
+    // the device's own go (PipeAuto): the update's chain word, the previous sweep's control block
+    const volatile ResolveCtl* c = prev;
+    const int cok = __hip_atomic_load(&au.chain->ok, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const int64_t end =
+        (int64_t)__hip_atomic_load(reinterpret_cast<const uint64_t*>(&au.chain->end), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int64_t r = end - au.win_start;
+    const bool ok = cok == 1 && c->status == 0 && c->next >= n && c->moves == 0 && r >= 0 && r + au.sweep_len <= au.win_count;
+    if (ok) {
+      const uint32_t* raw = au.win_raw + r;
+      g->raw = raw;
+      g->status = 4;
+      g->gate = 1;
+      __hip_atomic_store(reinterpret_cast<uint64_t*>(&slot->raw_dev), reinterpret_cast<uint64_t>(raw), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&slot->dev, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    __hip_atomic_store(&slot->dev, 2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   const long long t0 = wall_clock64();
   int f = 0;
   for (;;) {
@@ -4376,9 +4396,9 @@ __global__ void k_pipe_wait(const PipeSlot* slot, const ResolveCtl* prev, Resolv
     o->uncertain = -1;
   }
 }
-hipError_t launch_pipe_wait(const PipeSlot* slot, const ResolveCtl* prev, ResolveCtl* own, int n, PipeGate* g,
-                            long long limit, hipStream_t s) {
-  HDPM_LAUNCH(k_pipe_wait, dim3(1), dim3(64), 0, s, slot, prev, own, n, g, limit);
+hipError_t launch_pipe_wait(PipeSlot* slot, const ResolveCtl* prev, ResolveCtl* own, int n, PipeGate* g,
+                            long long limit, hipStream_t s, const PipeAuto& au) {
+  HDPM_LAUNCH(k_pipe_wait, dim3(1), dim3(64), 0, s, slot, prev, own, n, g, limit, au);
   return hipGetLastError();
 }
 

@@ -205,12 +205,29 @@ __device__ __forceinline__ bool pipe_gate(A& a) {
 // its slot (host-coherent memory) once the previous iteration is decided -- flag 1 go (with
 // the sweep's draws), 2 abort -- and the wait kernel turns it into the gate the sweep's
 // kernels read (pipe_gate): go, and the previous sweep completed in its one launch without
-// a move.  status: the flag seen (3: none within the time limit).
+// a move.  status: the flag seen (3: none within the time limit; 4: the device's own go).
+//
+// Device-side go (PipeAuto, the device update_phi's chained pipeline): the host authorises it
+// when it enqueues the sweep (the iteration after this one runs a Neal-8 sweep with the
+// speculated update); the wait kernel -- behind the speculated update's completion in stream
+// order -- then gives the go itself when the previous sweep completed in one launch without a
+// move and the update completed (its chain word), its draws in the window `win_*` after the
+// update's end, and tells the host (dev 1, raw_dev); otherwise it writes dev 2 and waits for
+// the host's flag as before.  The host follows a device go (pipe_go) and never releases it.
 constexpr int kPipeOff = 10;   // ResolveCtl::status of an enqueued sweep that was gated off
 struct PipeSlot {
   int flag;
-  int pad;
+  int dev;                     // written by k_pipe_wait with PipeAuto: 1 went, 2 waits for flag
   const uint32_t* raw;
+  const uint32_t* raw_dev;     // the sweep's draws, when dev == 1
+};
+struct PhiChain;
+struct PipeAuto {
+  const PhiChain* chain;       // the update whose tables the sweep scatters
+  const uint32_t* win_raw;
+  int64_t win_start, win_count;
+  int64_t sweep_len;           // N (m + 1)
+  int on;
 };
 struct PipeGate {
   int gate;

@@ -1751,7 +1751,8 @@ __global__ __launch_bounds__(1024) void k_phi2_values(PhiArgs a) {
     const uint32_t lo = (uint32_t)__hip_atomic_load(a.status + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t hi = (uint32_t)__hip_atomic_load(a.status + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     a.chain_out->end = a.pos0 + (int64_t)(((uint64_t)hi << 32) | lo);
-    a.chain_out->ok = scode == 0 ? 1 : 0;
+    // (complete with its stream state: a device-side go needs no host adoption, PipeAuto)
+    a.chain_out->ok = scode == 0 && smti != 0 ? 1 : 0;
   }
   __threadfence_system();
   __syncthreads();
@@ -1785,13 +1786,25 @@ hipError_t launch_phi2(const PhiArgs& a, hipStream_t s, hipEvent_t before_values
                l3 = phi2_values_lds(a.d, a.G, a.tW, a.T);
   if (l1 > 150 * 1024 || l2 > 150 * 1024 || l3 > 150 * 1024) return hipErrorInvalidValue;
   const int th1 = 512;
+  // (testing: HDPM_PHI2_TREE_THREADS / HDPM_PHI2_VALUES_WAVES, the workgroup sizes of the two
+  // per-cluster kernels)
+  static const int th2 = [] {
+    const char* e = std::getenv("HDPM_PHI2_TREE_THREADS");
+    const int v = e ? std::atoi(e) : 1024;
+    return v >= 64 && v <= 1024 && v % 64 == 0 ? v : 1024;
+  }();
+  static const int w3 = [] {
+    const char* e = std::getenv("HDPM_PHI2_VALUES_WAVES");
+    const int v = e ? std::atoi(e) : 0;
+    return v >= 1 && v <= 16 ? v : 0;
+  }();
   HDPM_LAUNCH(k_phi2_group, dim3((unsigned)(a.T * a.G)), dim3(th1), l1, s, a);
-  HDPM_LAUNCH(k_phi2_tree, dim3((unsigned)a.T), dim3(1024), l2, s, a);
+  HDPM_LAUNCH(k_phi2_tree, dim3((unsigned)a.T), dim3(th2), l2, s, a);
   if (before_values) {
     const hipError_t e = hipStreamWaitEvent(s, before_values, 0);
     if (e != hipSuccess) return e;
   }
-  HDPM_LAUNCH(k_phi2_values, dim3((unsigned)a.T), dim3(64 * a.wpb), l3, s, a);
+  HDPM_LAUNCH(k_phi2_values, dim3((unsigned)a.T), dim3(64 * (w3 ? w3 : a.wpb)), l3, s, a);
   return hipGetLastError();
 }
 
