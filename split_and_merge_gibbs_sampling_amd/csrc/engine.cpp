@@ -1001,6 +1001,7 @@ struct Ctx {
       if (dspec.ev) (void)hipEventDestroy(dspec.ev);
       if (dnext.ev) (void)hipEventDestroy(dnext.ev);
       if (ev_phd_free) (void)hipEventDestroy(ev_phd_free);
+      if (phd.ev_last) (void)hipEventDestroy(phd.ev_last);
       (void)hipStreamDestroy(pstream);
     }
     if (cstream) {
@@ -3683,6 +3684,10 @@ struct Ctx {
     DevBuf<double> sigd2[2];
     DevBuf<PhiChain> chain2;
     int slot = 0;                      // the slot of the next fast update
+    // the scratch (masks, tables, status) is shared by every update: one enqueued on another
+    // stream than the last one waits for it (ev_last, recorded after each update's launch)
+    hipEvent_t ev_last = nullptr;
+    hipStream_t last_s = nullptr;
     bool fast_out(const uint8_t* o) const { return o && (o == out2[0].p || o == out2[1].p); }
     int64_t fast_calls = 0;
     // tree mode when every updated cluster has at least this many members (a small cluster's
@@ -3910,7 +3915,15 @@ struct Ctx {
     const int64_t items = pl.items;
     size_t o_pick, o_sig, o_ll, bytes;
     phi_out_layout(T, d, &o_pick, &o_sig, &o_ll, &bytes);
-    phd.status.ensure(4);
+    if (phd.last_s && phd.last_s != s) HIPCHK(hipStreamWaitEvent(s, phd.ev_last, 0));
+    if (!phd.ev_last) HIPCHK(hipEventCreateWithFlags(&phd.ev_last, hipEventDisableTiming));
+    phd.last_s = s;
+    if (!phd.status.p) {
+      // (zeroed in stream order: the fast path's generation-tagged words are never cleared, and
+      // a hipMemset on the null stream is not ordered with these non-blocking streams)
+      phd.status.ensure(4);
+      HIPCHK(hipMemsetAsync(phd.status.p, 0, 16, s));
+    }
     phd.stage.ensure(upload_layout(T, dp, d, bw).bytes);
     a.status = phd.status.p;
     a.stage = phd.stage.p;
@@ -3927,20 +3940,20 @@ struct Ctx {
       phd.sigd2[sl].ensure(items);
       if (!phd.chain2.p) {
         phd.chain2.ensure(2);
-        HIPCHK(hipMemset(phd.chain2.p, 0, 2 * sizeof(PhiChain)));
+        HIPCHK(hipMemsetAsync(phd.chain2.p, 0, 2 * sizeof(PhiChain), s));
       }
       a.chain_out = phd.chain2.p + sl;
       a.sig_dev = phd.sigd2[sl].p;
       a.lab_dev = phd.labc2[sl].p;   // (k_phi2_group's copy of the labels and counts for k_phi2_values)
       if (!phd.ctr.p) {
         phd.ctr.ensure(2);
-        HIPCHK(hipMemset(phd.ctr.p, 0, 2 * sizeof(int)));
+        HIPCHK(hipMemsetAsync(phd.ctr.p, 0, 2 * sizeof(int), s));
       }
       phd.gtab2.ensure((size_t)T * pl.G * pl.tW);
       phd.roots.ensure((size_t)T * pl.tW);
       if (++phd.gen >= (1 << 26)) {                      // generations only grow: restart from 1
         HIPCHK(hipStreamSynchronize(s));
-        HIPCHK(hipMemset(phd.status.p, 0, 16));
+        HIPCHK(hipMemsetAsync(phd.status.p, 0, 16, s));
         phd.gen = 1;
       }
       ((volatile int*)hout.p)[0] = -1;                 // (written by the last k_phi2_values workgroup)
@@ -3988,6 +4001,7 @@ struct Ctx {
         a.tdbg = phd.tdbg.p;
       }
       HIPCHK(launch_phi2(a, s, w2));
+      HIPCHK(hipEventRecord(phd.ev_last, s));
       phd.fast_calls++;
       stats.phi_fast_calls++;
       return hout.p;
@@ -4023,6 +4037,7 @@ struct Ctx {
     HIPCHK(hipMemcpyAsync(phd.h_out.p + o_pick, phd.pick.p, (size_t)items, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(phd.h_out.p + o_sig, phd.sig_out.p, (size_t)items * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(phd.h_out.p + o_ll, phd.ll.p, (size_t)2 * T * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipEventRecord(phd.ev_last, s));
     return phd.h_out.p;
   }
 

@@ -4372,9 +4372,14 @@ __global__ void k_pipe_wait(PipeSlot* slot, const ResolveCtl* prev, ResolveCtl* 
   }
   const long long t0 = wall_clock64();
   int f = 0;
+  // (relaxed polls of host memory, one acquire fence after: an acquire load invalidates the
+  // XCD's L2 on every poll, under the kernels beside this one)
   for (;;) {
-    f = __hip_atomic_load(&slot->flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (f != 0) break;
+    f = __hip_atomic_load(&slot->flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (f != 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      break;
+    }
     if (wall_clock64() - t0 > limit) {
       f = 3;
       break;
@@ -4869,8 +4874,13 @@ __global__ __launch_bounds__(kSmWideChunk) void k_sm_scan_wide(SmArgs a) {
       // grid barrier r: arrivals counted, agent-scope release / acquire
       __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       const long long t0 = wall_clock64();
+      // (relaxed polls, one acquire fence after the barrier: an agent-scope acquire load
+      // invalidates the XCD's L2 on every poll)
       for (;;) {
-        if (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= G * (r + 1)) break;
+        if (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= G * (r + 1)) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          break;
+        }
         if (__hip_atomic_load(gave_up, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
             wall_clock64() - t0 > a.wide_limit) {
           __hip_atomic_store(gave_up, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -1785,26 +1785,37 @@ hipError_t launch_phi2(const PhiArgs& a, hipStream_t s, hipEvent_t before_values
   const size_t l1 = phi2_group_lds(a.gs, a.nw, a.rate), l2 = phi2_tree_lds(a.T, a.G, a.tW),
                l3 = phi2_values_lds(a.d, a.G, a.tW, a.T);
   if (l1 > 150 * 1024 || l2 > 150 * 1024 || l3 > 150 * 1024) return hipErrorInvalidValue;
-  const int th1 = 512;
-  // (testing: HDPM_PHI2_TREE_THREADS / HDPM_PHI2_VALUES_WAVES, the workgroup sizes of the two
-  // per-cluster kernels)
-  static const int th2 = [] {
-    const char* e = std::getenv("HDPM_PHI2_TREE_THREADS");
-    const int v = e ? std::atoi(e) : 1024;
-    return v >= 64 && v <= 1024 && v % 64 == 0 ? v : 1024;
+  static const int th1 = [] {
+    const char* e = std::getenv("HDPM_PHI2_GROUP_THREADS");
+    const int v = e ? std::atoi(e) : 512;
+    return v >= 128 && v <= 512 && v % 64 == 0 ? v : 512;   // (wave 0 prepares, the others compute logits)
   }();
-  static const int w3 = [] {
+  // The per-cluster kernels beside the sweep's prepass: a workgroup starts only where a CU has
+  // room for all of its waves, and the prepass's small workgroups take every slot that frees,
+  // so short rows (d <= 256: the tree's and the values' work fits few waves) run in 4-wave
+  // workgroups (C5 6,522 -> 7,559 it/s, C3 10,847 -> 11,891 with the device update); wide
+  // rows keep 16 waves (C4 6,753 against 5,314 at 4).  HDPM_PHI2_TREE_THREADS /
+  // HDPM_PHI2_VALUES_WAVES / HDPM_PHI2_GROUP_THREADS override (testing).
+  static const int th2e = [] {
+    const char* e = std::getenv("HDPM_PHI2_TREE_THREADS");
+    const int v = e ? std::atoi(e) : 0;
+    return v >= 64 && v <= 1024 && v % 64 == 0 ? v : 0;
+  }();
+  static const int w3e = [] {
     const char* e = std::getenv("HDPM_PHI2_VALUES_WAVES");
     const int v = e ? std::atoi(e) : 0;
     return v >= 1 && v <= 16 ? v : 0;
   }();
+  const bool narrow = a.d <= 256;
+  const int th2 = th2e ? th2e : narrow ? 256 : 1024;
+  const int w3 = w3e ? w3e : narrow ? std::min(4, a.wpb) : a.wpb;
   HDPM_LAUNCH(k_phi2_group, dim3((unsigned)(a.T * a.G)), dim3(th1), l1, s, a);
   HDPM_LAUNCH(k_phi2_tree, dim3((unsigned)a.T), dim3(th2), l2, s, a);
   if (before_values) {
     const hipError_t e = hipStreamWaitEvent(s, before_values, 0);
     if (e != hipSuccess) return e;
   }
-  HDPM_LAUNCH(k_phi2_values, dim3((unsigned)a.T), dim3(64 * (w3 ? w3 : a.wpb)), l3, s, a);
+  HDPM_LAUNCH(k_phi2_values, dim3((unsigned)a.T), dim3(64 * w3), l3, s, a);
   return hipGetLastError();
 }
 

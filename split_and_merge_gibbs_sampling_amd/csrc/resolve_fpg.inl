@@ -116,8 +116,10 @@ __device__ __forceinline__ bool sync(const Lay& L, int G, int* flag, long long l
         __hip_atomic_fetch_add(w, (1ull << 32) - (unsigned long long)G, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       } else {
         const long long t0 = wall_clock64();
+        // (relaxed polls, one acquire fence after: an agent-scope acquire load invalidates the
+        // XCD's L2 -- per poll, it cost every workgroup of the XCD its cached data)
         for (int spin = 0;; ++spin) {
-          const unsigned long long v = __hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+          const unsigned long long v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if ((unsigned)(v >> 32) != gen) break;
           if (v & kBarPoison) { ab = 1; break; }
           if ((spin & 31) == 31 && wall_clock64() - t0 > limit) {
@@ -127,6 +129,7 @@ __device__ __forceinline__ bool sync(const Lay& L, int G, int* flag, long long l
           }
           __builtin_amdgcn_s_sleep(1);
         }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       }
     }
     __threadfence();
@@ -696,9 +699,10 @@ __global__ __launch_bounds__(kFpThreads) void k_resolve_fpg(ResolveArgs a) {
       if (wv == 0) {
         const long long t0 = wall_clock64();
         int tag = 0;
-        while ((tag = __hip_atomic_load(L.ms + 11, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) != nwin &&
+        while ((tag = __hip_atomic_load(L.ms + 11, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != nwin &&
                wall_clock64() - t0 < a.fpg_limit)
           __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         if (lane == 0) X->flag = tag == nwin ? 1 : 0;
       }
       __syncthreads();
