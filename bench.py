@@ -462,6 +462,10 @@ def main():
             "listed_points_per_step": st["listed_points"] / args.steps,
             "moves_per_step": st["moves"] / args.steps,
             "split_merge": bool(args.sm),
+            # restricted Gibbs samplers run as one device chain (split_merge.inl sm_chain), their
+            # scans, and chains the host continued from their first unfinished step
+            "sm_chain": ({k[9:]: int(st[k]) for k in ("sm_chain_runs", "sm_chain_scans", "sm_chain_resumes")}
+                         if args.sm else None),
             "record": ({"labels_mirrored": int(st["labels_mirrored"]), "labels_downloaded": int(st["labels_downloaded"])}
                        if args.record else None),
             "hig_logspace": hig_log,

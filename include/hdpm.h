@@ -125,6 +125,11 @@ typedef struct {
      * completed device update, no host round trip), and goes the host could not follow (the
      * chain state is then undefined and the context reports an error; never expected) */
     int64_t pipe_auto, pipe_desync;
+    /* restricted Gibbs samplers run as one device chain (every scan, its table update and its
+     * update_phi({c1, c2}) enqueued together, sm:163-225): chains, scans run in them, and chains
+     * the host continued from their first unfinished scan or update (an update the device handed
+     * back, a draw outside the stream window) */
+    int64_t sm_chain_runs, sm_chain_scans, sm_chain_resumes;
 } hdpm_stats;
 
 int         hdpm_device_count(void);
@@ -311,6 +316,12 @@ int hdpm_get_pool_heads(hdpm_ctx* ctx, uint64_t* out, int64_t P);
  * (hdpm_stats.sm_wide_fallbacks).  0 gives up at the first barrier, unconditionally; values above
  * 1e9 us are an argument error.  Same chain either way. */
 #define HDPM_OPT_SM_WIDE_WAIT_US 8
+/* HDPM_OPT_SM_CHAIN: the restricted Gibbs sampler of a split-merge move (sm:163-225, its t scans
+ * and update_phi({c1, c2}) calls) as one device chain where it applies (1, the default; also
+ * HDPM_SM_CHAIN=0 in the environment) or scan by scan with the host between them (0).  Testing:
+ * 2 + 2k turns the chain off at scan k (the host continues from there), 3 + 2k hands update k
+ * back after its scan ran.  Same chain either way (hdpm_stats.sm_chain_*). */
+#define HDPM_OPT_SM_CHAIN 9
 int hdpm_set_option(hdpm_ctx* ctx, int32_t option, double value);
 /* The current value of an option (the same units as hdpm_set_option; HDPM_OPT_PHI_DEVICE
  * reads 1 when update_phi runs on the device, which may be the default). */

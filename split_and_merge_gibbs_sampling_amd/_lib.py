@@ -38,6 +38,7 @@ OPT_FPG_FAIL_AT = 5
 OPT_EXACT_KERNEL = 6
 OPT_LAT_NEGLIGIBLE = 7
 OPT_SM_WIDE_WAIT_US = 8
+OPT_SM_CHAIN = 9
 
 STATUS = {0: "OK", 1: "E_VALIDATE", 2: "E_GSL", 3: "E_PROB", 4: "E_WALKER", 5: "E_ARG",
           6: "E_DEVICE", 7: "E_NODEVICE"}
@@ -77,7 +78,8 @@ class Stats(C.Structure):
                                   "sm_wide_fallbacks", "phi_fast_calls", "phi_fast_handbacks",
                                   "labels_mirrored", "labels_downloaded", "phi_state_direct",
                                   "phi_chain_launched", "phi_chain_used", "phi_chain_dropped",
-                                  "pipe_auto", "pipe_desync")]
+                                  "pipe_auto", "pipe_desync", "sm_chain_runs", "sm_chain_scans",
+                                  "sm_chain_resumes")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -654,6 +654,16 @@ struct SmWork {
   std::vector<int> prior_err;
   int prior_log = -1;
   int64_t phi_prefetch = 0;   // stream slice generated ahead for the move's update_phi jobs
+  // the restricted Gibbs sampler's device chain (split_merge.inl sm_chain), by scan k
+  DevBuf<SmLink> d_links;
+  DevBuf<PhiChain> d_chain;   // [0] the seed (the chain's first position), then per scan the link's (1 + 2k) and the update's (2 + 2k)
+  DevBuf<uint32_t> d_F, d_FM; // both tables (ascending label order); the table of S + {i1, i2}
+  DevBuf<int> d_labcnt, d_labdev;   // [k][4] each update's labels and sizes (k_sm_tabs), their copy (k_phi2_group)
+  DevBuf<uint8_t> d_stage;    // [k] each update's staged tables
+  DevBuf<double> d_sig;       // [k + 1][2 d] sigmas: the chain's first, then each update's
+  PinBuf<uint8_t> h_cout;     // [k] each update's outputs, status and stream state (coherent)
+  PinBuf<uint8_t> h_cin, h_cback;   // the chain's inputs; its results (tables, chain words, scan flags)
+  hipEvent_t ev_chain = nullptr;
 };
 
 // A window of the R random stream generated on the device (k_mt_gen), starting at the
@@ -895,6 +905,12 @@ struct Ctx {
   int exact_pref = 0;                  // HDPM_OPT_EXACT_KERNEL (testing)
   double lat_negl = kLatNegligible;    // HDPM_OPT_LAT_NEGLIGIBLE (testing)
   long long sm_wide_ticks = 5000000;   // k_sm_scan_wide's barrier limit (100 MHz ticks; HDPM_OPT_SM_WIDE_WAIT_US)
+  // restricted Gibbs samplers as one device chain (HDPM_OPT_SM_CHAIN: 0 off, 1 on; >= 2 testing:
+  // the chain stops at step sm_chain_fail - 2, split_merge.inl sm_chain)
+  int sm_chain_mode = [] {
+    const char* e = std::getenv("HDPM_SM_CHAIN");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
   bool deep_ok = false;                // set by iteration(): the next sweep may be enqueued ahead
   static constexpr size_t kCtlInts = 16;
   static_assert(sizeof(ResolveCtl) <= kCtlInts * sizeof(int), "control block");
@@ -1024,6 +1040,7 @@ struct Ctx {
         if (e) (void)hipEventDestroy(e);
       for (auto& e : ev_res)
         if (e) (void)hipEventDestroy(e);
+      if (sm.ev_chain) (void)hipEventDestroy(sm.ev_chain);
       for (auto& pe : ev_pp)
         for (auto& e : pe)
           if (e) (void)hipEventDestroy(e);
@@ -5362,6 +5379,7 @@ int hdpm_get_option(hdpm_ctx* h, int32_t option, double* value) {
     case HDPM_OPT_EXACT_KERNEL: *value = (double)ctx->exact_pref; return HDPM_OK;
     case HDPM_OPT_LAT_NEGLIGIBLE: *value = ctx->lat_negl; return HDPM_OK;
     case HDPM_OPT_SM_WIDE_WAIT_US: *value = (double)ctx->sm_wide_ticks * 0.01; return HDPM_OK;
+    case HDPM_OPT_SM_CHAIN: *value = (double)ctx->sm_chain_mode; return HDPM_OK;
     default:
       ctx->err = "unknown option";
       return HDPM_E_ARG;
@@ -5405,6 +5423,14 @@ int hdpm_set_option(hdpm_ctx* h, int32_t option, double value) {
       if (!(value >= 0.0) || !(value <= 1e9)) { ctx->err = "wide scan wait must be in [0, 1e9] us"; return HDPM_E_ARG; }
       GUARD(ctx->cancel_ahead();)
       ctx->sm_wide_ticks = (long long)(value * 100.0);   // 0: every wide scan gives up at its first barrier
+      return HDPM_OK;
+    case HDPM_OPT_SM_CHAIN:
+      if (!(value >= 0.0) || !(value <= 1000.0) || value != std::floor(value)) {
+        ctx->err = "sm chain: 0 off, 1 on, 2 + 2k / 3 + 2k stop at scan / update k (testing)";
+        return HDPM_E_ARG;
+      }
+      GUARD(ctx->cancel_ahead();)
+      ctx->sm_chain_mode = (int)value;
       return HDPM_OK;
     case HDPM_OPT_PIPE_WAIT_US:
       if (value == 0.0 || !std::isfinite(value)) { ctx->err = "pipe wait limit must be non-zero"; return HDPM_E_ARG; }

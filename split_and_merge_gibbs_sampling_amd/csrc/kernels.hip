@@ -4474,7 +4474,22 @@ hipError_t launch_lmatrix(const uint8_t* codes_t, int n, int d, int nq, ParamTab
 namespace hdpm {
 
 // ------------------------------------------------------------------ split-merge
+// A scan of the device chain (SmArgs::link): false when it does not run, else its draws and
+// sizes into a.  Read at the kernel's start by every lane and made wave-uniform, so the
+// branches on it are scalar.
+__device__ __forceinline__ bool sm_link_in(SmArgs& a) {
+  if (!a.link) return true;
+  if (__builtin_amdgcn_readfirstlane(a.link->ok) == 0) return false;
+  const uint64_t r = (uint64_t)a.link->raw;
+  a.raw = (const uint32_t*)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(r >> 32)) << 32) |
+                            (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)r));
+  a.n1 = __builtin_amdgcn_readfirstlane(a.link->n1);
+  a.n2 = __builtin_amdgcn_readfirstlane(a.link->n2);
+  return true;
+}
+
 __global__ __launch_bounds__(kBlock) void k_sm_ll(SmArgs a) {
+  if (!sm_link_in(a)) return;
   const int q = blockIdx.x * kBlock + threadIdx.x;
   if (q >= a.nS) return;
   const int64_t i = a.S[q];
@@ -4490,6 +4505,7 @@ __global__ __launch_bounds__(kBlock) void k_sm_ll(SmArgs a) {
 constexpr int kSmLLBlock = 64;
 __device__ __forceinline__ void sm_cert_point(const SmArgs& a, int q, double dl);
 __global__ __launch_bounds__(kSmLLBlock) void k_sm_ll_lds(SmArgs a) {
+  if (!sm_link_in(a)) return;
   extern __shared__ double sm_lds[];
   const int d = a.d, dp = a.nq * 16;
   double* tab = sm_lds;                                    // [2][d][2]
@@ -4646,6 +4662,7 @@ __device__ __forceinline__ void sm_cert_point(const SmArgs& a, int q, double dl)
   }
 }
 __global__ __launch_bounds__(kBlock) void k_sm_cert(SmArgs a) {
+  if (!sm_link_in(a)) return;
   const int q = blockIdx.x * kBlock + threadIdx.x;
   if (q >= a.nS) return;
   sm_cert_point(a, q, a.ll[q] - a.ll[a.nS + q]);
@@ -4681,6 +4698,7 @@ __global__ __launch_bounds__(kSmScanThreads) void k_sm_scan(SmArgs a) {
   extern __shared__ unsigned char sm_scan_lds[];
   SmChunk* buf = (SmChunk*)sm_scan_lds;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (!sm_link_in(a)) return;
   if (a.wide_buf) {
     // behind k_sm_scan_wide: nothing to do when it finished; when it gave up (some of its
     // chunks may have written their sides) the walk starts from the sides before the scan
@@ -4786,6 +4804,7 @@ __global__ __launch_bounds__(kSmScanThreads) void k_sm_scan(SmArgs a) {
 constexpr int kSmWideChunk = 256;
 constexpr int kSmWideMaxG = 1024;
 __global__ __launch_bounds__(kSmWideChunk) void k_sm_scan_wide(SmArgs a) {
+  if (!sm_link_in(a)) return;     // (every workgroup alike: no barrier is left waiting)
   __shared__ double s_l0[kSmWideChunk], s_l1[kSmWideChunk];
   __shared__ uint32_t s_raw[kSmWideChunk];
   __shared__ int s_cur[kSmWideChunk], s_choice[kSmWideChunk];
@@ -5050,6 +5069,7 @@ hipError_t launch_debug_math(const double* x, int64_t n, int fn, int ocml, doubl
 // table.  Counts are integers, so the table equals the host's membership count exactly.
 constexpr int kSmFreqThreads = 256;
 __global__ __launch_bounds__(kSmFreqThreads) void k_sm_freq(SmFreqArgs a, int parts) {
+  if (a.link && __builtin_amdgcn_readfirstlane(a.link->ok) == 0) return;
   extern __shared__ uint32_t s_bins[];            // [16][mmax]
   const int c = blockIdx.x / parts, part = blockIdx.x - c * parts;
   const int nb = 16 * a.mmax;
@@ -5113,6 +5133,70 @@ hipError_t launch_sm_freq(const SmFreqArgs& a, hipStream_t s) {
   // about 512 workgroups, every point list split into `parts` shares per attribute chunk
   const int parts = std::max(1, std::min((a.nlist + 2 + 255) / 256, 512 / std::max(a.nq, 1)));
   HDPM_LAUNCH(k_sm_freq, dim3((unsigned)(a.nq * parts)), dim3(kSmFreqThreads), lds, s, a, parts);
+  return hipGetLastError();
+}
+
+// The device chain's link before scan k (SmLinkArgs): one workgroup.
+__global__ __launch_bounds__(256) void k_sm_link(SmLinkArgs a) {
+  __shared__ int s_ok;
+  __shared__ int64_t s_r, s_end;
+  if (threadIdx.x == 0) {
+    int ok = __hip_atomic_load(&a.prev->ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int64_t end = (int64_t)__hip_atomic_load((const uint64_t*)&a.prev->end, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+    const int64_t r = end - a.win_start;
+    if (r < 0 || r + a.nS > a.win_count) ok = 0;
+    s_ok = ok;
+    s_r = r;
+    s_end = end;
+  }
+  __syncthreads();
+  const int ok = s_ok;
+  if (ok && a.stage) {
+    const UploadLayout L = upload_layout(2, a.dp, a.d, a.bw);
+    for (int e = 0; e < 2; ++e) {
+      const int src = e ^ a.swap;
+      const uint8_t* sc = a.stage + L.off_codes + (size_t)src * a.dp;
+      const double* st = reinterpret_cast<const double*>(a.stage + L.off_tab) + (size_t)src * 2 * a.d;
+      for (int j = threadIdx.x; j < a.dp; j += blockDim.x) a.two_codes[(size_t)e * a.dp + j] = sc[j];
+      for (int j = threadIdx.x; j < 2 * a.d; j += blockDim.x) a.two_tab[(size_t)e * 2 * a.d + j] = st[j];
+    }
+  }
+  if (threadIdx.x == 0) {
+    a.link->raw = ok ? a.win_raw + s_r : nullptr;
+    a.link->n1 = a.counts_in ? a.counts_in[0] : a.n1;
+    a.link->n2 = a.counts_in ? a.counts_in[1] : a.n2;
+    a.link->ok = ok;
+    a.chain->end = s_end;
+    a.chain->ok = ok;
+  }
+}
+hipError_t launch_sm_link(const SmLinkArgs& a, hipStream_t s) {
+  HDPM_LAUNCH(k_sm_link, dim3(1), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+// Both tables of the device chain after scan k (SmTabsArgs).
+__global__ __launch_bounds__(256) void k_sm_tabs(SmTabsArgs a) {
+  if (__builtin_amdgcn_readfirstlane(a.link->ok) == 0) return;
+  uint32_t* f1 = a.F + (size_t)a.a1 * a.nt;
+  uint32_t* f2 = a.F + (size_t)(1 - a.a1) * a.nt;
+  for (int e = blockIdx.x * 256 + (int)threadIdx.x; e < a.nt; e += gridDim.x * 256) {
+    const uint32_t x = f1[e] + a.delta[e];
+    f1[e] = x;
+    f2[e] = a.fm[e] - x;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const int c0 = a.counts[0], c1 = a.counts[1];
+    a.lab_cnt[0] = 0;
+    a.lab_cnt[1] = 1;
+    a.lab_cnt[2] = a.a1 == 0 ? c0 : c1;
+    a.lab_cnt[3] = a.a1 == 0 ? c1 : c0;
+  }
+}
+hipError_t launch_sm_tabs(const SmTabsArgs& a, hipStream_t s) {
+  const int g = std::max(1, std::min(64, (a.nt + 255) / 256));
+  HDPM_LAUNCH(k_sm_tabs, dim3((unsigned)g), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

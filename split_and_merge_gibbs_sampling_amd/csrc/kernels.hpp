@@ -386,6 +386,15 @@ struct LoglikArgs {
 namespace hdpm {
 
 // Restricted Gibbs scan over S (code/split_merge.cpp:163-225) and logprobgs_c_i (96-161).
+// The device chain of a restricted Gibbs sampler (split_merge.inl sm_chain): scan k's gate,
+// draws and cluster sizes, written by k_sm_link from the update before it (kernels with a
+// link read them there instead of their arguments and do nothing when ok == 0).
+struct SmLink {
+  const uint32_t* raw;       // the scan's nS draws (inside the stream window)
+  int ok;                    // 1: the scan runs (the update before it completed, its draws in the window)
+  int n1, n2;                // sizes of c_i_1, c_i_2 before the scan
+};
+
 // Frequency table of a point list (k_sm_freq): out[j * mmax + x_ij - 1] += 1 over the points
 // list[q] with side[q] == want (side == nullptr: every point), and the extra points (>= 0).
 struct SmFreqArgs {
@@ -401,6 +410,7 @@ struct SmFreqArgs {
   const int* side_prev;
   uint32_t* out;             // [d][mmax], zeroed by the launcher (unless prezeroed)
   int prezeroed;
+  const SmLink* link;        // device chain: nothing counted unless link->ok (nullptr: always)
 };
 
 struct SmArgs {
@@ -424,6 +434,7 @@ struct SmArgs {
   long long wide_limit;      // its barrier waits give up after this many wall_clock64 ticks
   uint32_t* zero;            // zeroed by k_sm_ll_lds (zero_n words): the table k_sm_freq fills next
   int zero_n;
+  const SmLink* link;        // device chain: raw, n1, n2 from the link; nothing runs unless link->ok
 };
 
 }  // namespace hdpm
@@ -552,6 +563,37 @@ struct PhiChain {
   int ok;                    // 1: completed (status 0), 0: not
   int pad;
 };
+// Device chain of a restricted Gibbs sampler (split_merge.inl sm_chain), per scan k:
+// k_sm_link: scan k's link from the update before it (`prev`: its end position and completion,
+// or the chain's seed word), the link's own chain word for the update after the scan (same
+// end, ok = the link's: that update's first draw follows the scan's nS), and the two
+// clusters' tables of the previous update's staging in side order (entry 0 = c_i_1).
+struct SmLinkArgs {
+  const PhiChain* prev;
+  const int* counts_in;      // sizes after the previous scan, or nullptr: n1, n2
+  int n1, n2, nS;
+  const uint32_t* win_raw;   // the stream window holding the chain's draws
+  int64_t win_start, win_count;
+  SmLink* link;
+  PhiChain* chain;
+  const uint8_t* stage;      // the previous update's UploadLayout(2, dp, d, bw) staging, or nullptr
+  int dp, d, bw, swap;       // swap: c_i_1 is staging entry 1 (its label is the larger)
+  uint8_t* two_codes;        // [2][dp]
+  double* two_tab;           // [2][2 d]
+};
+// k_sm_tabs: after scan k's k_sm_freq (delta: the change of c_i_1's table), both tables in
+// ascending label order (F[a1] = c_i_1's += delta, F[1 - a1] = fm - F[a1]) and the update's
+// labels and sizes (lab_cnt = {0, 1, size of F[0], size of F[1]}).
+struct SmTabsArgs {
+  const SmLink* link;
+  const uint32_t* delta;
+  const uint32_t* fm;        // [d][mmax] the table of S + {i1, i2}
+  uint32_t* F;               // [2][d][mmax]
+  int a1, nt;                // index of c_i_1's table, d * mmax
+  const int* counts;         // [2] sizes after the scan (c_i_1, c_i_2)
+  int* lab_cnt;              // [4]
+};
+
 // Level sizes of a composition tree over nb >= 1 level-0 blocks.
 __host__ __device__ inline int phi_lcount(int nb, int l) { return ((nb - 1) >> l) + 1; }
 __host__ __device__ inline int phi_loff(int nb, int l) {

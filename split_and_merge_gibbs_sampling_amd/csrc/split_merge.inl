@@ -13,6 +13,9 @@ hipError_t launch_sm_freq(const SmFreqArgs& a, hipStream_t s);
 bool sm_ll_lds_fits(int d, int nq);
 int sm_scan_wide_grid(int nS);
 hipError_t launch_sm_scan_wide(const SmArgs& a, int G, hipStream_t s);
+hipError_t launch_sm_link(const SmLinkArgs& a, hipStream_t s);
+hipError_t launch_sm_tabs(const SmTabsArgs& a, hipStream_t s);
+hipError_t launch_phi2(const PhiArgs& a, hipStream_t s, hipEvent_t before_values);
 
 // HDPM_SM_WIDE=0: the one-workgroup restricted scan only (A/B of k_sm_scan_wide, the default:
 // 13.5 against 80 us per C4 scan, profiles/r05/split_merge/wide/)
@@ -388,6 +391,7 @@ static SmArgs sm_args(Ctx* c, SmWork& W, int nS) {
   a.zero_n = 0;
   a.wide_buf = nullptr;
   a.wide_limit = 0;
+  a.link = nullptr;
   return a;
 }
 
@@ -421,6 +425,7 @@ static void sm_freq_device(Ctx* c, SmWork& W, int nS, const int* side, int want,
   a.side_prev = side_prev;
   a.out = W.d_freq.p;
   a.prezeroed = prezeroed ? 1 : 0;
+  a.link = nullptr;
   HIPCHK(launch_sm_freq(a, c->stream));
   HIPCHK(hipMemcpyAsync(W.h_freq.p, W.d_freq.p, nt * 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
@@ -438,6 +443,292 @@ static void sm_freq_device(Ctx* c, SmWork& W, int nS, const int* side, int want,
     for (size_t e = 0; e < nt; ++e) F.f[e] = (double)h[e];
     F.nn = nn;
   }
+}
+
+
+// sm:163-225's t scans, each followed by update_phi({c1, c2}) (sm:221), as one device chain
+// when the move's tables live on the device.  Per scan k: k_sm_link (the scan's draws after the
+// previous update's end, its sizes, the previous update's tables in side order) -> k_sm_ll_lds
+// -> k_sm_scan_wide / k_sm_scan -> k_sm_freq (the points the scan moved) -> k_sm_tabs (both
+// tables, the update's sizes) -> the fast device update_phi (launch_phi2, chained: its first
+// draw after the scan's nS, its labels, sizes, tables and sigmas on the device).  No host step
+// between scans: the sides, tables, chain words and the last update's outputs come down once.
+// An update the device hands back (or a scan whose draws would leave the stream window) turns
+// every later link off, so the device holds the state after the last complete step and the
+// host continues from there: *next_iter, and *at_phi when that iteration's scan already ran.
+// -1: not applicable (nothing changed, nothing enqueued).
+static int sm_chain(Ctx* c, SmWork& W, const std::vector<int>& S, HState& s, int i1, int i2, int t, Freq& F1,
+                    Freq& F2, const Freq& FM, int* next_iter, bool* at_phi) {
+  *next_iter = 0;
+  *at_phi = false;
+  const int c1 = s.c[i1], c2 = s.c[i2];
+  const int nS = (int)S.size(), d = c->d, mm = c->mmax;
+  if (c->sm_chain_mode == 0 || t < 1 || t > 64 || nS < 1 || c1 == c2) return -1;
+  if (c->phi_mode == 0 || (c->debug & (524288 | 64 | 65536)) || d > 2048 || !Ctx::glibc_selfcheck()) return -1;
+  if (!sm_ll_lds_fits(d, c->nq)) return -1;
+  bool fast = false;
+  const Ctx::PhiPlan pf = c->fast_plan(2, true, std::min(F1.nn, F2.nn), &fast);
+  if (!fast) return -1;
+  c->rng_sync();
+  const uint64_t P0 = c->rng.pos;
+  RngWindow* Wn = c->window_at(P0, (int64_t)t * (nS + pf.need));
+  if (!Wn || !c->can_adopt(*Wn, P0)) return -1;
+  SmTimer tm(c->stats.t_sm_scan_ms);
+  c->dspec_drain();                                 // phd's scratch is the chain's now
+  hipStream_t st = c->stream;
+  auto& phd = c->phd;
+  const size_t nt = (size_t)d * mm;
+  const int a1 = c1 < c2 ? 0 : 1;                   // c_i_1's place in ascending label order
+  const int Gw = sm_wide_on() ? sm_scan_wide_grid(nS) : 0;
+  const size_t wstride = 4 + 2 * (size_t)std::max(Gw, 1);
+  const UploadLayout L2 = upload_layout(2, c->dp, d, c->bw);
+  const size_t stage_b = align16(L2.bytes);
+  size_t o_pick, o_sig, o_ll, obytes;
+  Ctx::phi_out_layout(2, d, &o_pick, &o_sig, &o_ll, &obytes);
+  const size_t o_state = align16(obytes), out_b = align16(o_state + 625 * 4 + 64);
+  const int tc = std::max(t, 16);                   // (sized once for the usual t: no reallocation)
+  W.d_links.ensure(tc);
+  W.d_chain.ensure(1 + 2 * (size_t)tc);
+  W.d_F.ensure(2 * nt);
+  W.d_FM.ensure(nt);
+  W.d_labcnt.ensure(4 * (size_t)tc);
+  W.d_labdev.ensure(4 * (size_t)tc);
+  W.d_stage.ensure(stage_b * tc);
+  W.d_sig.ensure((size_t)(tc + 1) * 2 * d);
+  W.h_cout.ensure(out_b * tc, hipHostMallocCoherent);
+  W.d_wide.ensure(wstride * tc);
+  W.d_side_prev.ensure(std::max(nS, 1));
+  W.d_freq.ensure(nt);
+  W.h_side.ensure(std::max(nS, 1));
+  // inputs: both tables and the table of S + {i1, i2} (counts, exact in u32), both sigma rows,
+  // the seed chain word (the first scan's draws start at P0)
+  const size_t o_fm = align16(2 * nt * 4), o_sg = align16(o_fm + nt * 4), o_seed = align16(o_sg + 2 * (size_t)d * 8),
+               in_b = o_seed + sizeof(PhiChain);
+  W.h_cin.ensure(in_b + 64);
+  {
+    uint32_t* hf = (uint32_t*)W.h_cin.p;
+    for (size_t e = 0; e < nt; ++e) {
+      hf[a1 * nt + e] = (uint32_t)F1.f[e];
+      hf[(1 - a1) * nt + e] = (uint32_t)F2.f[e];
+      ((uint32_t*)(W.h_cin.p + o_fm))[e] = (uint32_t)FM.f[e];
+    }
+    double* hs = (double*)(W.h_cin.p + o_sg);
+    std::memcpy(hs + (size_t)a1 * d, &s.sigma[(size_t)c1 * d], (size_t)d * 8);
+    std::memcpy(hs + (size_t)(1 - a1) * d, &s.sigma[(size_t)c2 * d], (size_t)d * 8);
+    PhiChain seed{(int64_t)P0, 1, 0};
+    std::memcpy(W.h_cin.p + o_seed, &seed, sizeof(seed));
+  }
+  HIPCHK(hipMemcpyAsync(W.d_F.p, W.h_cin.p, 2 * nt * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(W.d_FM.p, W.h_cin.p + o_fm, nt * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(W.d_sig.p, W.h_cin.p + o_sg, 2 * (size_t)d * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(W.d_chain.p, W.h_cin.p + o_seed, sizeof(PhiChain), hipMemcpyHostToDevice, st));
+  sm_upload_two(c, W, s, c1, c2);                   // the first scan's tables (later ones: k_sm_link)
+  HIPCHK(hipStreamWaitEvent(st, Wn->done, 0));
+  if (phd.last_s && phd.last_s != st) HIPCHK(hipStreamWaitEvent(st, phd.ev_last, 0));
+  if (!phd.ev_last) HIPCHK(hipEventCreateWithFlags(&phd.ev_last, hipEventDisableTiming));
+  if (!phd.status.p) {
+    phd.status.ensure(4);
+    HIPCHK(hipMemsetAsync(phd.status.p, 0, 16, st));
+  }
+  if (!phd.ctr.p) {
+    phd.ctr.ensure(2);
+    HIPCHK(hipMemsetAsync(phd.ctr.p, 0, 2 * sizeof(int), st));
+  }
+  phd.gtab2.ensure((size_t)2 * pf.G * pf.tW);
+  phd.roots.ensure((size_t)2 * pf.tW);
+  c->mark("sm.chain_in");
+  for (int k = 0; k < t; ++k) {
+    SmLink* lk = W.d_links.p + k;
+    SmLinkArgs la{};
+    la.prev = W.d_chain.p + 2 * k;                  // the seed, then update k - 1's word
+    la.counts_in = k == 0 ? nullptr : W.d_counts2.p;
+    la.n1 = F1.nn;
+    la.n2 = F2.nn;
+    la.nS = nS;
+    la.win_raw = Wn->raw.p;
+    la.win_start = (int64_t)Wn->start_pos;
+    la.win_count = c->sm_chain_mode == 2 + 2 * k ? 0 : Wn->count;   // (testing: this scan off)
+    la.link = lk;
+    la.chain = W.d_chain.p + 1 + 2 * k;
+    la.stage = k == 0 ? nullptr : W.d_stage.p + stage_b * (k - 1);
+    la.dp = c->dp;
+    la.d = d;
+    la.bw = c->bw;
+    la.swap = a1;
+    la.two_codes = W.d_two_codes.p;
+    la.two_tab = W.d_two_tab.p;
+    HIPCHK(launch_sm_link(la, st));
+    SmArgs a = sm_args(c, W, nS);
+    a.raw = nullptr;
+    a.link = lk;
+    a.side_prev = W.d_side_prev.p;
+    a.cert_in_ll = 1;
+    a.zero = W.d_freq.p;
+    a.zero_n = (int)nt;
+    HIPCHK(launch_sm_ll(a, st));
+    if (Gw) {
+      a.wide_buf = W.d_wide.p + wstride * k;
+      a.wide_limit = c->sm_wide_ticks;
+      HIPCHK(launch_sm_scan_wide(a, Gw, st));
+    }
+    HIPCHK(launch_sm_scan(a, st));
+    SmFreqArgs fa{};
+    fa.codes_t = c->d_codes_t.p; fa.n = c->n; fa.d = d; fa.nq = c->nq; fa.mmax = mm;
+    fa.list = W.d_S.p; fa.nlist = nS; fa.side = W.d_side.p; fa.want = 0;
+    fa.extra[0] = -1; fa.extra[1] = -1;
+    fa.side_prev = W.d_side_prev.p;
+    fa.out = W.d_freq.p;
+    fa.prezeroed = 1;
+    fa.link = lk;
+    HIPCHK(launch_sm_freq(fa, st));
+    SmTabsArgs ta{lk, W.d_freq.p, W.d_FM.p, W.d_F.p, a1, (int)nt, W.d_counts2.p, W.d_labcnt.p + 4 * k};
+    HIPCHK(launch_sm_tabs(ta, st));
+    // update k (fast path, chained behind the link: its first draw after the scan's nS)
+    PhiArgs pa = c->phi_args(pf);
+    pa.freq = W.d_F.p;
+    pa.lab = W.d_labcnt.p + 4 * k;
+    pa.cnt = pa.lab + 2;
+    pa.sig_in = W.d_sig.p + (size_t)k * 2 * d;
+    pa.chain_in = W.d_chain.p + 1 + 2 * k;
+    pa.chain_out = W.d_chain.p + 2 + 2 * k;
+    pa.win_raw = Wn->raw.p;
+    pa.win_start = (int64_t)Wn->start_pos;
+    pa.win_count = c->sm_chain_mode == 3 + 2 * k ? 0 : Wn->count;   // (testing: this update off)
+    pa.win_mti0 = Wn->mti0;
+    pa.sweep_len = nS;
+    pa.raw = nullptr; pa.nraw = 0; pa.raw_back = 0; pa.mti_pos = 0; pa.pos0 = 0;
+    pa.status = phd.status.p;
+    pa.stage = W.d_stage.p + stage_b * k;
+    pa.lab_dev = W.d_labdev.p + 4 * k;
+    pa.sig_dev = W.d_sig.p + (size_t)(k + 1) * 2 * d;
+    uint8_t* ho = W.h_cout.p + out_b * k;
+    ((volatile int*)ho)[0] = -1;
+    pa.pick = ho + o_pick;
+    pa.sig_out = (double*)(ho + o_sig);
+    pa.ll = (double*)(ho + o_ll);
+    pa.status_host = (int*)ho;
+    pa.state_host = (uint32_t*)(ho + o_state);
+    pa.state_host[624] = 0;
+    if (++phd.gen >= (1 << 26)) {                   // generations only grow: restart from 1
+      HIPCHK(hipStreamSynchronize(st));
+      HIPCHK(hipMemsetAsync(phd.status.p, 0, 16, st));
+      phd.gen = 1;
+    }
+    pa.gs = pf.gs; pa.G = pf.G; pa.gtab2 = phd.gtab2.p; pa.roots = phd.roots.p; pa.ctr = phd.ctr.p; pa.gen = phd.gen;
+    pa.tree = nullptr;
+    pa.lg = nullptr;
+    pa.lzz = nullptr;
+    pa.tdbg = nullptr;
+    HIPCHK(launch_phi2(pa, st, nullptr));
+    phd.fast_calls++;
+    c->stats.phi_fast_calls++;
+  }
+  HIPCHK(hipEventRecord(phd.ev_last, st));
+  phd.last_s = st;
+  c->phd_release(st);
+  // the results down once: the sides, both tables, the chain words, the wide scans' flags
+  const size_t o_cw = align16(2 * nt * 4), o_wd = align16(o_cw + (1 + 2 * (size_t)t) * sizeof(PhiChain)),
+               back_b = o_wd + wstride * t * 4;
+  W.h_cback.ensure(back_b + 64);
+  HIPCHK(hipMemcpyAsync(W.h_side.p, W.d_side.p, (size_t)nS * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(W.h_cback.p, W.d_F.p, 2 * nt * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(W.h_cback.p + o_cw, W.d_chain.p, (1 + 2 * (size_t)t) * sizeof(PhiChain), hipMemcpyDeviceToHost, st));
+  if (Gw) HIPCHK(hipMemcpyAsync(W.h_cback.p + o_wd, W.d_wide.p, wstride * t * 4, hipMemcpyDeviceToHost, st));
+  if (!W.ev_chain) HIPCHK(hipEventCreateWithFlags(&W.ev_chain, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(W.ev_chain, st));
+  c->mark("sm.chain_enqueued");
+  {
+    // (a blocking wait's wake-up costs tens of microseconds: poll, then block after 2 s)
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int polls = 0;; ++polls) {
+      const hipError_t q = hipEventQuery(W.ev_chain);
+      if (q == hipSuccess) break;
+      if (q != hipErrorNotReady) HIPCHK(q);
+      HostPool::spin_pause();
+      if ((polls & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+        HIPCHK(hipEventSynchronize(W.ev_chain));
+        break;
+      }
+    }
+  }
+  c->mark("sm.chain_done");
+  const PhiChain* cw = (const PhiChain*)(W.h_cback.p + o_cw);
+  const uint32_t* hF = (const uint32_t*)W.h_cback.p;
+  // the first update that did not complete (t: none)
+  int kf = t;
+  for (int k = 0; k < t; ++k)
+    if (((const int*)(W.h_cout.p + out_b * k))[0] != kPhiOk || cw[2 + 2 * k].ok != 1) {
+      kf = k;
+      break;
+    }
+  const bool scan_kf = kf < t && cw[1 + 2 * kf].ok == 1;   // scan kf ran (its update did not complete)
+  const int ran = kf + (scan_kf ? 1 : 0);                   // scans run
+  if (Gw)
+    for (int k = 0; k < ran; ++k) {
+      c->stats.sm_wide_scans++;
+      if (((const int*)(W.h_cback.p + o_wd))[wstride * k + 1] != 0) c->stats.sm_wide_fallbacks++;
+    }
+  // the state after the last complete step: sides, tables, sizes
+  if (ran > 0) {
+    const int* hs = W.h_side.p;
+    for (int q = 0; q < nS; ++q) s.c[S[q]] = hs[q] == 0 ? c1 : c2;
+    for (int e2 = 0; e2 < 2; ++e2) {
+      Freq& F = (e2 == 0) ? F1 : F2;
+      const uint32_t* src = hF + (size_t)(e2 == 0 ? a1 : 1 - a1) * nt;
+      for (size_t e = 0; e < nt; ++e) F.f[e] = (double)src[e];
+      int nn = 0;
+      for (int l = 0; l < mm; ++l) nn += (int)src[l];
+      F.nn = nn;
+    }
+    s.counts[c1] = F1.nn;
+    s.counts[c2] = F2.nn;
+  }
+  // the parameters of the last update that completed
+  const int64_t items = 2 * (int64_t)d;
+  for (int k = 0; k < kf; ++k) {
+    int64_t cons = 0;
+    std::memcpy(&cons, W.h_cout.p + out_b * k + 8, 8);
+    Ctx::PhiDevice::adapt(phd.p_rej_sm, cons - 3 * items, items, 0.9);
+  }
+  if (kf > 0) {
+    const uint8_t* ho = W.h_cout.p + out_b * (kf - 1);
+    const uint8_t* pk = ho + o_pick;
+    const double* sg = (const double*)(ho + o_sig);
+    for (int e2 = 0; e2 < 2; ++e2) {
+      const int k = e2 == 0 ? c1 : c2, src = e2 == 0 ? a1 : 1 - a1;
+      for (int j = 0; j < d; ++j) s.center[(size_t)k * d + j] = (uint8_t)(pk[(size_t)src * d + j] + 1);
+      std::memcpy(&s.sigma[(size_t)k * d], sg + (size_t)src * d, (size_t)d * 8);
+    }
+    c->stats.phi_device_calls += kf;
+    c->stats.phi_sm_device_calls += kf;
+  }
+  c->stats.sm_chain_runs++;
+  c->stats.sm_chain_scans += ran;
+  if (kf == t) {
+    // the host stream after the last update's draws (its state came back with its outputs)
+    const uint8_t* ho = W.h_cout.p + out_b * (t - 1);
+    c->adopt_after_phi(*Wn, (uint64_t)cw[2 * t].end, (const uint32_t*)(ho + o_state));
+    *next_iter = t;
+    return kOk;
+  }
+  // continue on the host from the first unfinished step
+  c->stats.sm_chain_resumes++;
+  const int stk = ((const int*)(W.h_cout.p + out_b * kf))[0];
+  if (scan_kf && stk != kPhiOff) {
+    c->stats.phi_fallback_status_mask |= (int64_t)1 << std::min(std::max(stk, 0), 14);
+    c->stats.phi_fast_handbacks++;
+    if (stk == kPhiNonDet) phd.fast_backoff = Ctx::PhiDevice::kFastBackoff;
+    if (stk == kPhiShort || stk == kPhiWindow) Ctx::PhiDevice::widen(phd.p_rej_sm, 0.9);
+  }
+  if (std::getenv("HDPM_PHI_TRACE"))
+    std::fprintf(stderr, "[sm chain] t %d nS %d: step %d %s (update status %d)\n", t, nS, kf,
+                 scan_kf ? "update handed back" : "scan off", stk);
+  const uint64_t pos = scan_kf ? (uint64_t)cw[1 + 2 * kf].end + (uint64_t)nS : (uint64_t)cw[2 * kf].end;
+  c->adopt_state_at(*Wn, pos);
+  c->rng_sync();
+  *next_iter = kf;
+  *at_phi = scan_kf;
+  return kOk;
 }
 
 // sm:163-225 on host state s with the scan on the device.  F1 / F2: the tables of s.c[i1]
@@ -485,7 +776,22 @@ static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1
   // large scans take their |S| draws from the device windows (no host generation and copy;
   // the host stream adopts the state after them); debug bit 16 draws them on the host
   const bool dev_draws = nS >= 4096 && !(c->debug & 65536);
-  for (int iter = 0; iter < t; ++iter) {
+  // the whole sampler as one device chain where it applies (sm_chain); the host continues
+  // from the first step the chain did not finish
+  int iter0 = 0;
+  bool at_phi = false;
+  if (dev_tables && sm_chain(c, W, S, s, i1, i2, t, F1, F2, FM, &iter0, &at_phi) == kOk) {
+    c->mark("sm.chain");
+    if (iter0 == t) return kOk;
+  }
+  for (int iter = iter0; iter < t; ++iter) {
+    if (at_phi && iter == iter0) {
+      // the chain's scan ran, its update did not: update_phi({c1, c2}) here
+      const int st = hupdate_phi_pair(c, s, c1, F1, c2, F2);
+      c->mark("sm.phi");
+      if (st) return st;
+      continue;
+    }
     const uint32_t* d_raw = nullptr;
     if (dev_draws) {
       c->rng_sync();

@@ -252,6 +252,11 @@ class Engine:
         split-merge scan on many CUs; 0 gives up at once (the one-workgroup scan runs)."""
         self._check(self._L.hdpm_set_option(self._h, _lib.OPT_SM_WIDE_WAIT_US, float(us)))
 
+    def set_sm_chain(self, mode: int):
+        """include/hdpm.h HDPM_OPT_SM_CHAIN: the restricted Gibbs sampler as one device chain (1,
+        default) or scan by scan (0); testing: 2 + 2k / 3 + 2k stop the chain at scan / update k."""
+        self._check(self._L.hdpm_set_option(self._h, _lib.OPT_SM_CHAIN, float(mode)))
+
     def set_hig_logspace(self, on: bool = True):
         """Extension beyond the reference (include/hdpm.h HDPM_OPT_HIG_LOGSPACE): finite HIG
         log-densities for clusters whose 2F1 series overflows (the reference throws)."""

@@ -902,6 +902,41 @@ def test_split_merge_chain_wide_scan_and_give_up(hd, oracle, wait_us):
         assert stats["sm_wide_fallbacks"] == 0, stats
 
 
+@pytest.mark.parametrize("mode", [0, 1, 2, 3, 6, 7])
+def test_split_merge_device_chain(hd, oracle, mode):
+    """The restricted Gibbs samplers of split-merge moves as one device chain (sm_chain: the t
+    scans and their update_phi({c1, c2}) enqueued together, sm:163-225), scan by scan (mode 0),
+    and chains stopped at scan 0 / update 0 / scan 2 / update 2 (modes 2, 3, 6, 7: the host
+    continues from there): the same chain as the oracle every time."""
+    ds = synth(6000, 64, 2, 3, seed=44)
+    kw = dict(m=3, iterations=4, L=1, c_i=ds.truth, burnin=0, t=4, r=4, neal8=True, split_merge=True)
+    try:
+        oracle.set_hig_logspace(True)
+        st, ref = oracle.run_markov_chain(ds.codes, ds.attrisize, ds.gamma, ds.v, ds.w, seed=8, fast=2, **kw)
+    finally:
+        oracle.set_hig_logspace(False)
+    assert st == 0
+    eng = make_engine(hd, ds)
+    try:
+        eng.set_hig_logspace(True)
+        eng.set_seed(8)
+        eng.set_sm_chain(mode)
+        res = eng.run_markov_chain(**kw)
+        stats = eng.stats()
+    finally:
+        eng.close()
+    assert np.array_equal(res["c_i"], ref["c_i"])
+    assert np.array_equal(res["total_cls"], ref["total_cls"])
+    assert np.array_equal(res["accepted"], ref["accepted"])
+    np.testing.assert_allclose(res["loglikelihood"], ref["loglikelihood"], rtol=RTOL, atol=0)
+    if mode == 0:
+        assert stats["sm_chain_runs"] == 0, stats
+    else:
+        assert stats["sm_chain_runs"] > 0, stats
+        if mode >= 2:
+            assert stats["sm_chain_resumes"] == stats["sm_chain_runs"], stats
+
+
 def test_split_merge_second_dataset_other_attrisize(hd, oracle):
     """One engine, two data sets with the same d, v and w but other attribute sizes m_j: the
     split-merge priors' normalising constants norm_const2(w_j, v_j, m_j) (sm:419-436) must
