@@ -317,10 +317,11 @@ int hdpm_get_pool_heads(hdpm_ctx* ctx, uint64_t* out, int64_t P);
  * 1e9 us are an argument error.  Same chain either way. */
 #define HDPM_OPT_SM_WIDE_WAIT_US 8
 /* HDPM_OPT_SM_CHAIN: the restricted Gibbs sampler of a split-merge move (sm:163-225, its t scans
- * and update_phi({c1, c2}) calls) as one device chain where it applies (1, the default; also
- * HDPM_SM_CHAIN=0 in the environment) or scan by scan with the host between them (0).  Testing:
- * 2 + 2k turns the chain off at scan k (the host continues from there), 3 + 2k hands update k
- * back after its scan ran.  Same chain either way (hdpm_stats.sm_chain_*). */
+ * and update_phi({c1, c2}) calls) as one device chain where it applies (1; also HDPM_SM_CHAIN=1
+ * in the environment) or scan by scan with the host between them (0, the default: measured
+ * faster at C3 and C4).  Testing:
+ * 2 + 3k turns the chain off at scan k (the host continues from there), 3 + 3k / 4 + 3k hand the
+ * scan's update of the lower / larger label back.  Same chain either way (hdpm_stats.sm_chain_*). */
 #define HDPM_OPT_SM_CHAIN 9
 int hdpm_set_option(hdpm_ctx* ctx, int32_t option, double value);
 /* The current value of an option (the same units as hdpm_set_option; HDPM_OPT_PHI_DEVICE

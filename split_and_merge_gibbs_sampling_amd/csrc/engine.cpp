@@ -905,11 +905,13 @@ struct Ctx {
   int exact_pref = 0;                  // HDPM_OPT_EXACT_KERNEL (testing)
   double lat_negl = kLatNegligible;    // HDPM_OPT_LAT_NEGLIGIBLE (testing)
   long long sm_wide_ticks = 5000000;   // k_sm_scan_wide's barrier limit (100 MHz ticks; HDPM_OPT_SM_WIDE_WAIT_US)
-  // restricted Gibbs samplers as one device chain (HDPM_OPT_SM_CHAIN: 0 off, 1 on; >= 2 testing:
-  // the chain stops at step sm_chain_fail - 2, split_merge.inl sm_chain)
+  // restricted Gibbs samplers as one device chain (HDPM_OPT_SM_CHAIN: 0 off, the default -- the
+  // chain's one-cluster device updates cost ~100 us each at C4 against ~45 us per cluster on the
+  // host job, profiles/r06/sm_chain/ -- 1 on; >= 2 testing: the chain stops at step
+  // sm_chain_mode - 2, split_merge.inl sm_chain; HDPM_SM_CHAIN=1 in the environment turns it on)
   int sm_chain_mode = [] {
     const char* e = std::getenv("HDPM_SM_CHAIN");
-    return (e && e[0] == '0') ? 0 : 1;
+    return (e && e[0] == '1') ? 1 : 0;
   }();
   bool deep_ok = false;                // set by iteration(): the next sweep may be enqueued ahead
   static constexpr size_t kCtlInts = 16;
@@ -5426,7 +5428,7 @@ int hdpm_set_option(hdpm_ctx* h, int32_t option, double value) {
       return HDPM_OK;
     case HDPM_OPT_SM_CHAIN:
       if (!(value >= 0.0) || !(value <= 1000.0) || value != std::floor(value)) {
-        ctx->err = "sm chain: 0 off, 1 on, 2 + 2k / 3 + 2k stop at scan / update k (testing)";
+        ctx->err = "sm chain: 0 off, 1 on, 2 + 3k / 3 + 3k / 4 + 3k stop at scan k / its updates (testing)";
         return HDPM_E_ARG;
       }
       GUARD(ctx->cancel_ahead();)

@@ -5152,12 +5152,12 @@ __global__ __launch_bounds__(256) void k_sm_link(SmLinkArgs a) {
   }
   __syncthreads();
   const int ok = s_ok;
-  if (ok && a.stage) {
-    const UploadLayout L = upload_layout(2, a.dp, a.d, a.bw);
+  if (ok && a.stage[0]) {
+    const UploadLayout L = upload_layout(1, a.dp, a.d, a.bw);
     for (int e = 0; e < 2; ++e) {
-      const int src = e ^ a.swap;
-      const uint8_t* sc = a.stage + L.off_codes + (size_t)src * a.dp;
-      const double* st = reinterpret_cast<const double*>(a.stage + L.off_tab) + (size_t)src * 2 * a.d;
+      const uint8_t* sb = a.stage[e ^ a.swap];
+      const uint8_t* sc = sb + L.off_codes;
+      const double* st = reinterpret_cast<const double*>(sb + L.off_tab);
       for (int j = threadIdx.x; j < a.dp; j += blockDim.x) a.two_codes[(size_t)e * a.dp + j] = sc[j];
       for (int j = threadIdx.x; j < 2 * a.d; j += blockDim.x) a.two_tab[(size_t)e * 2 * a.d + j] = st[j];
     }

@@ -567,7 +567,10 @@ struct PhiChain {
 // k_sm_link: scan k's link from the update before it (`prev`: its end position and completion,
 // or the chain's seed word), the link's own chain word for the update after the scan (same
 // end, ok = the link's: that update's first draw follows the scan's nS), and the two
-// clusters' tables of the previous update's staging in side order (entry 0 = c_i_1).
+// clusters' tables from the previous scan's updates' staging in side order (entry 0 = c_i_1).
+// (update_phi({c1, c2}) runs as two one-cluster updates in ascending label order, the second
+// chained behind the first: each starts at drift 0, so its center picks are fixed by its
+// first d uniforms and the fast path never hands back for a pick that depends on them)
 struct SmLinkArgs {
   const PhiChain* prev;
   const int* counts_in;      // sizes after the previous scan, or nullptr: n1, n2
@@ -576,14 +579,16 @@ struct SmLinkArgs {
   int64_t win_start, win_count;
   SmLink* link;
   PhiChain* chain;
-  const uint8_t* stage;      // the previous update's UploadLayout(2, dp, d, bw) staging, or nullptr
-  int dp, d, bw, swap;       // swap: c_i_1 is staging entry 1 (its label is the larger)
+  const uint8_t* stage[2];   // the previous scan's updates' UploadLayout(1, dp, d, bw) staging by
+                             // ascending label, or nullptr (the tables stay)
+  int dp, d, bw, swap;       // swap: c_i_1 has the larger label
   uint8_t* two_codes;        // [2][dp]
   double* two_tab;           // [2][2 d]
 };
 // k_sm_tabs: after scan k's k_sm_freq (delta: the change of c_i_1's table), both tables in
 // ascending label order (F[a1] = c_i_1's += delta, F[1 - a1] = fm - F[a1]) and the update's
-// labels and sizes (lab_cnt = {0, 1, size of F[0], size of F[1]}).
+// labels and sizes (lab_cnt = {0, 1, size of F[0], size of F[1]}: the first update reads label
+// lab_cnt[0] and size lab_cnt[2], the second lab_cnt[1] and lab_cnt[3]).
 struct SmTabsArgs {
   const SmLink* link;
   const uint32_t* delta;

@@ -272,7 +272,7 @@ constexpr int kPhiLdsLevels = 16;
 template <class PR, class PM>
 __device__ __forceinline__ int phi_prep_item_in(const PhiArgs& a, int t, int j, int64_t idx, int nn, int lab, double sg,
                                                 PR pr, PM pm, const uint64_t* tabs, bool* det_out, int* nact_out,
-                                                PhiCand* cpick = nullptr) {
+                                                PhiCand* cpick = nullptr, double ucen = -1.0) {
   const int mj = a.att[j], off = a.aoff[j];
   const unsigned* f = a.freq + ((int64_t)lab * a.d + j) * a.mmax;
   for (int l = 0; l < mj; ++l) pr[l] = (-((double)nn - (double)f[l])) / sg;
@@ -297,10 +297,18 @@ __device__ __forceinline__ int phi_prep_item_in(const PhiArgs& a, int t, int j, 
   for (int l = 0; l < mj; ++l) pm[l] = (uint8_t)(l + 1);
   phi_revsort_t(pr, pm, mj);
   for (int l = 1; l < mj; ++l) pr[l] += pr[l - 1];
-  // the pick is perm[0] whatever the uniform when cum[0] >= 1 (a uniform is < 1)
-  const bool det = mj == 1 || pr[0] >= 1.0;
+  // the pick is perm[0] whatever the uniform when cum[0] >= 1 (a uniform is < 1); when the
+  // center's uniform is known (ucen >= 0: the update's first cluster, whose draws start at
+  // drift 0) it is the level that uniform takes (sample_prob1_pick: the first sorted position
+  // with u <= cum, the last one otherwise)
+  bool det = mj == 1 || pr[0] >= 1.0;
+  int sp = 0;
+  if (!det && ucen >= 0.0) {
+    while (sp < mj - 1 && !(ucen <= pr[sp])) ++sp;
+    det = true;
+  }
   *det_out = det;
-  a.det[idx] = det ? pm[0] : 0;
+  a.det[idx] = det ? pm[sp] : 0;
   a.ikind[idx] = 0;
   // candidates: the levels the draw can pick (sorted position s: the last, or cum rising)
   PhiCand* cb = a.cand + (int64_t)t * a.sumatt + off;
@@ -309,7 +317,7 @@ __device__ __forceinline__ int phi_prep_item_in(const PhiArgs& a, int t, int j, 
     const int l = pm[s] - 1;
     PhiCand c{};
     c.kind = 0;
-    const bool pickable = det ? s == 0 : (s == mj - 1 || pr[s] > (s > 0 ? pr[s - 1] : 0.0));
+    const bool pickable = det ? s == sp : (s == mj - 1 || pr[s] > (s > 0 ? pr[s - 1] : 0.0));
     if (pickable) {
       const double sumdelta = (double)f[l];
       const double nw_ = a.w[j] + nn - sumdelta, nv_ = a.v[j] + sumdelta;
@@ -324,7 +332,7 @@ __device__ __forceinline__ int phi_prep_item_in(const PhiArgs& a, int t, int j, 
       }
       if (det) a.ikind[idx] = (uint8_t)c.kind;
     }
-    if (cpick && det && s == 0) *cpick = c;         // (the fixed pick's candidate, for the caller)
+    if (cpick && det && s == sp) *cpick = c;        // (the fixed pick's candidate, for the caller)
     cb[l] = c;
   }
   *nact_out = nact;
@@ -1455,12 +1463,15 @@ __global__ __launch_bounds__(512) void k_phi2_group(PhiArgs a) {
     bool det = false;
     int nact = 0, status;
     PhiCand cp{};
+    // the first cluster's center draws take the slice's first d uniforms whatever the drifts:
+    // its picks are fixed by them (later clusters start after the drifts before them)
+    const double ucen = t == 0 ? pool_unif(a.raw[j]) : -1.0;
     if (mj <= kPhiLdsLevels) {
       status = phi_prep_item_in(a, t, j, k, in_cnt, in_lab, in_sig, spr + i * kPhiLdsLevels, spm + i * kPhiLdsLevels,
-                                tabs, &det, &nact, &cp);
+                                tabs, &det, &nact, &cp, ucen);
     } else {
       status = phi_prep_item_in(a, t, j, k, in_cnt, in_lab, in_sig, a.cum + (int64_t)t * a.sumatt + off,
-                                a.perm + (int64_t)t * a.sumatt + off, tabs, &det, &nact, &cp);
+                                a.perm + (int64_t)t * a.sumatt + off, tabs, &det, &nact, &cp, ucen);
     }
     if (!status && !det) status = kPhiNonDet;
     if (!status) {

@@ -448,30 +448,34 @@ static void sm_freq_device(Ctx* c, SmWork& W, int nS, const int* side, int want,
 
 // sm:163-225's t scans, each followed by update_phi({c1, c2}) (sm:221), as one device chain
 // when the move's tables live on the device.  Per scan k: k_sm_link (the scan's draws after the
-// previous update's end, its sizes, the previous update's tables in side order) -> k_sm_ll_lds
+// previous update's end, its sizes, the previous updates' tables in side order) -> k_sm_ll_lds
 // -> k_sm_scan_wide / k_sm_scan -> k_sm_freq (the points the scan moved) -> k_sm_tabs (both
-// tables, the update's sizes) -> the fast device update_phi (launch_phi2, chained: its first
-// draw after the scan's nS, its labels, sizes, tables and sigmas on the device).  No host step
-// between scans: the sides, tables, chain words and the last update's outputs come down once.
-// An update the device hands back (or a scan whose draws would leave the stream window) turns
-// every later link off, so the device holds the state after the last complete step and the
-// host continues from there: *next_iter, and *at_phi when that iteration's scan already ran.
+// tables, the updates' sizes) -> update_phi({c1, c2}) as two fast one-cluster device updates in
+// ascending label order (launch_phi2, chained: the first draws after the scan's nS, the second
+// after the first; inputs on the device).  Each one-cluster update starts at drift 0, so its
+// center picks are fixed by its first d uniforms (k_phi2_group) -- a two-cluster update's second
+// cluster starts at an unknown drift, and a freshly split cluster's picks depend on it.  No host
+// step between scans: the sides, tables, chain words and the last updates' outputs come down
+// once.  An update the device hands back (or a scan whose draws would leave the stream window)
+// turns every later step off, so the device holds the state after the last complete step and
+// the host continues from there: *next_iter, and *at_phi = 1 when that iteration's scan ran (both
+// updates to do), 2 when its first update completed too (the larger label's update to do).
 // -1: not applicable (nothing changed, nothing enqueued).
 static int sm_chain(Ctx* c, SmWork& W, const std::vector<int>& S, HState& s, int i1, int i2, int t, Freq& F1,
-                    Freq& F2, const Freq& FM, int* next_iter, bool* at_phi) {
+                    Freq& F2, const Freq& FM, int* next_iter, int* at_phi) {
   *next_iter = 0;
-  *at_phi = false;
+  *at_phi = 0;
   const int c1 = s.c[i1], c2 = s.c[i2];
   const int nS = (int)S.size(), d = c->d, mm = c->mmax;
   if (c->sm_chain_mode == 0 || t < 1 || t > 64 || nS < 1 || c1 == c2) return -1;
   if (c->phi_mode == 0 || (c->debug & (524288 | 64 | 65536)) || d > 2048 || !Ctx::glibc_selfcheck()) return -1;
   if (!sm_ll_lds_fits(d, c->nq)) return -1;
   bool fast = false;
-  const Ctx::PhiPlan pf = c->fast_plan(2, true, std::min(F1.nn, F2.nn), &fast);
+  const Ctx::PhiPlan pf = c->fast_plan(1, true, 16, &fast);
   if (!fast) return -1;
   c->rng_sync();
   const uint64_t P0 = c->rng.pos;
-  RngWindow* Wn = c->window_at(P0, (int64_t)t * (nS + pf.need));
+  RngWindow* Wn = c->window_at(P0, (int64_t)t * (nS + 2 * pf.need));
   if (!Wn || !c->can_adopt(*Wn, P0)) return -1;
   SmTimer tm(c->stats.t_sm_scan_ms);
   c->dspec_drain();                                 // phd's scratch is the chain's now
@@ -479,23 +483,24 @@ static int sm_chain(Ctx* c, SmWork& W, const std::vector<int>& S, HState& s, int
   auto& phd = c->phd;
   const size_t nt = (size_t)d * mm;
   const int a1 = c1 < c2 ? 0 : 1;                   // c_i_1's place in ascending label order
+  const int klab[2] = {std::min(c1, c2), std::max(c1, c2)};
   const int Gw = sm_wide_on() ? sm_scan_wide_grid(nS) : 0;
   const size_t wstride = 4 + 2 * (size_t)std::max(Gw, 1);
-  const UploadLayout L2 = upload_layout(2, c->dp, d, c->bw);
-  const size_t stage_b = align16(L2.bytes);
+  const size_t stage_b = align16(upload_layout(1, c->dp, d, c->bw).bytes);
   size_t o_pick, o_sig, o_ll, obytes;
-  Ctx::phi_out_layout(2, d, &o_pick, &o_sig, &o_ll, &obytes);
+  Ctx::phi_out_layout(1, d, &o_pick, &o_sig, &o_ll, &obytes);
   const size_t o_state = align16(obytes), out_b = align16(o_state + 625 * 4 + 64);
+  const int nu = 2 * t;                             // updates: scan k's are 2k (lower label), 2k + 1
   const int tc = std::max(t, 16);                   // (sized once for the usual t: no reallocation)
   W.d_links.ensure(tc);
-  W.d_chain.ensure(1 + 2 * (size_t)tc);
+  W.d_chain.ensure(1 + 3 * (size_t)tc);
   W.d_F.ensure(2 * nt);
   W.d_FM.ensure(nt);
   W.d_labcnt.ensure(4 * (size_t)tc);
   W.d_labdev.ensure(4 * (size_t)tc);
-  W.d_stage.ensure(stage_b * tc);
+  W.d_stage.ensure(stage_b * 2 * tc);
   W.d_sig.ensure((size_t)(tc + 1) * 2 * d);
-  W.h_cout.ensure(out_b * tc, hipHostMallocCoherent);
+  W.h_cout.ensure(out_b * 2 * tc, hipHostMallocCoherent);
   W.d_wide.ensure(wstride * tc);
   W.d_side_prev.ensure(std::max(nS, 1));
   W.d_freq.ensure(nt);
@@ -534,23 +539,26 @@ static int sm_chain(Ctx* c, SmWork& W, const std::vector<int>& S, HState& s, int
     phd.ctr.ensure(2);
     HIPCHK(hipMemsetAsync(phd.ctr.p, 0, 2 * sizeof(int), st));
   }
-  phd.gtab2.ensure((size_t)2 * pf.G * pf.tW);
-  phd.roots.ensure((size_t)2 * pf.tW);
+  phd.gtab2.ensure((size_t)pf.G * pf.tW);
+  phd.roots.ensure((size_t)pf.tW);
+  // chain words: [0] the seed, then per scan k the link's (1 + 3k) and its updates' (2 + 3k, 3 + 3k)
+  auto link_w = [](int k) { return 1 + 3 * k; };
+  auto upd_w = [](int u) { return 2 + 3 * (u >> 1) + (u & 1); };
   c->mark("sm.chain_in");
   for (int k = 0; k < t; ++k) {
     SmLink* lk = W.d_links.p + k;
     SmLinkArgs la{};
-    la.prev = W.d_chain.p + 2 * k;                  // the seed, then update k - 1's word
+    la.prev = W.d_chain.p + (k == 0 ? 0 : upd_w(2 * k - 1));
     la.counts_in = k == 0 ? nullptr : W.d_counts2.p;
     la.n1 = F1.nn;
     la.n2 = F2.nn;
     la.nS = nS;
     la.win_raw = Wn->raw.p;
     la.win_start = (int64_t)Wn->start_pos;
-    la.win_count = c->sm_chain_mode == 2 + 2 * k ? 0 : Wn->count;   // (testing: this scan off)
+    la.win_count = c->sm_chain_mode == 2 + 3 * k ? 0 : Wn->count;   // (testing: this scan off)
     la.link = lk;
-    la.chain = W.d_chain.p + 1 + 2 * k;
-    la.stage = k == 0 ? nullptr : W.d_stage.p + stage_b * (k - 1);
+    la.chain = W.d_chain.p + link_w(k);
+    for (int e = 0; e < 2; ++e) la.stage[e] = k == 0 ? nullptr : W.d_stage.p + stage_b * (2 * (k - 1) + e);
     la.dp = c->dp;
     la.d = d;
     la.bw = c->bw;
@@ -583,56 +591,62 @@ static int sm_chain(Ctx* c, SmWork& W, const std::vector<int>& S, HState& s, int
     HIPCHK(launch_sm_freq(fa, st));
     SmTabsArgs ta{lk, W.d_freq.p, W.d_FM.p, W.d_F.p, a1, (int)nt, W.d_counts2.p, W.d_labcnt.p + 4 * k};
     HIPCHK(launch_sm_tabs(ta, st));
-    // update k (fast path, chained behind the link: its first draw after the scan's nS)
-    PhiArgs pa = c->phi_args(pf);
-    pa.freq = W.d_F.p;
-    pa.lab = W.d_labcnt.p + 4 * k;
-    pa.cnt = pa.lab + 2;
-    pa.sig_in = W.d_sig.p + (size_t)k * 2 * d;
-    pa.chain_in = W.d_chain.p + 1 + 2 * k;
-    pa.chain_out = W.d_chain.p + 2 + 2 * k;
-    pa.win_raw = Wn->raw.p;
-    pa.win_start = (int64_t)Wn->start_pos;
-    pa.win_count = c->sm_chain_mode == 3 + 2 * k ? 0 : Wn->count;   // (testing: this update off)
-    pa.win_mti0 = Wn->mti0;
-    pa.sweep_len = nS;
-    pa.raw = nullptr; pa.nraw = 0; pa.raw_back = 0; pa.mti_pos = 0; pa.pos0 = 0;
-    pa.status = phd.status.p;
-    pa.stage = W.d_stage.p + stage_b * k;
-    pa.lab_dev = W.d_labdev.p + 4 * k;
-    pa.sig_dev = W.d_sig.p + (size_t)(k + 1) * 2 * d;
-    uint8_t* ho = W.h_cout.p + out_b * k;
-    ((volatile int*)ho)[0] = -1;
-    pa.pick = ho + o_pick;
-    pa.sig_out = (double*)(ho + o_sig);
-    pa.ll = (double*)(ho + o_ll);
-    pa.status_host = (int*)ho;
-    pa.state_host = (uint32_t*)(ho + o_state);
-    pa.state_host[624] = 0;
-    if (++phd.gen >= (1 << 26)) {                   // generations only grow: restart from 1
-      HIPCHK(hipStreamSynchronize(st));
-      HIPCHK(hipMemsetAsync(phd.status.p, 0, 16, st));
-      phd.gen = 1;
+    // the scan's update_phi({c1, c2}): the lower label's update behind the link (its first draw
+    // after the scan's nS), the larger label's behind it
+    for (int e = 0; e < 2; ++e) {
+      const int u = 2 * k + e;
+      PhiArgs pa = c->phi_args(pf);
+      pa.freq = W.d_F.p;
+      pa.lab = W.d_labcnt.p + 4 * k + e;
+      pa.cnt = W.d_labcnt.p + 4 * k + 2 + e;
+      pa.sig_in = W.d_sig.p + ((size_t)k * 2 + e) * d;
+      pa.chain_in = W.d_chain.p + (e == 0 ? link_w(k) : upd_w(u - 1));
+      pa.chain_out = W.d_chain.p + upd_w(u);
+      pa.win_raw = Wn->raw.p;
+      pa.win_start = (int64_t)Wn->start_pos;
+      pa.win_count = c->sm_chain_mode == 3 + 3 * k + e ? 0 : Wn->count;   // (testing: this update off)
+      pa.win_mti0 = Wn->mti0;
+      pa.sweep_len = e == 0 ? nS : 0;
+      pa.raw = nullptr; pa.nraw = 0; pa.raw_back = 0; pa.mti_pos = 0; pa.pos0 = 0;
+      pa.status = phd.status.p;
+      pa.stage = W.d_stage.p + stage_b * u;
+      pa.lab_dev = W.d_labdev.p + 4 * k + 2 * e;
+      pa.sig_dev = W.d_sig.p + ((size_t)(k + 1) * 2 + e) * d;
+      uint8_t* ho = W.h_cout.p + out_b * u;
+      ((volatile int*)ho)[0] = -1;
+      pa.pick = ho + o_pick;
+      pa.sig_out = (double*)(ho + o_sig);
+      pa.ll = (double*)(ho + o_ll);
+      pa.status_host = (int*)ho;
+      pa.state_host = (uint32_t*)(ho + o_state);
+      pa.state_host[624] = 0;
+      if (++phd.gen >= (1 << 26)) {                 // generations only grow: restart from 1
+        HIPCHK(hipStreamSynchronize(st));
+        HIPCHK(hipMemsetAsync(phd.status.p, 0, 16, st));
+        phd.gen = 1;
+      }
+      pa.gs = pf.gs; pa.G = pf.G; pa.gtab2 = phd.gtab2.p; pa.roots = phd.roots.p; pa.ctr = phd.ctr.p;
+      pa.gen = phd.gen;
+      pa.tree = nullptr;
+      pa.lg = nullptr;
+      pa.lzz = nullptr;
+      pa.tdbg = nullptr;
+      HIPCHK(launch_phi2(pa, st, nullptr));
+      phd.fast_calls++;
+      c->stats.phi_fast_calls++;
     }
-    pa.gs = pf.gs; pa.G = pf.G; pa.gtab2 = phd.gtab2.p; pa.roots = phd.roots.p; pa.ctr = phd.ctr.p; pa.gen = phd.gen;
-    pa.tree = nullptr;
-    pa.lg = nullptr;
-    pa.lzz = nullptr;
-    pa.tdbg = nullptr;
-    HIPCHK(launch_phi2(pa, st, nullptr));
-    phd.fast_calls++;
-    c->stats.phi_fast_calls++;
   }
   HIPCHK(hipEventRecord(phd.ev_last, st));
   phd.last_s = st;
   c->phd_release(st);
   // the results down once: the sides, both tables, the chain words, the wide scans' flags
-  const size_t o_cw = align16(2 * nt * 4), o_wd = align16(o_cw + (1 + 2 * (size_t)t) * sizeof(PhiChain)),
+  const int ncw = 1 + 3 * t;
+  const size_t o_cw = align16(2 * nt * 4), o_wd = align16(o_cw + (size_t)ncw * sizeof(PhiChain)),
                back_b = o_wd + wstride * t * 4;
   W.h_cback.ensure(back_b + 64);
   HIPCHK(hipMemcpyAsync(W.h_side.p, W.d_side.p, (size_t)nS * 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(W.h_cback.p, W.d_F.p, 2 * nt * 4, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(W.h_cback.p + o_cw, W.d_chain.p, (1 + 2 * (size_t)t) * sizeof(PhiChain), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(W.h_cback.p + o_cw, W.d_chain.p, (size_t)ncw * sizeof(PhiChain), hipMemcpyDeviceToHost, st));
   if (Gw) HIPCHK(hipMemcpyAsync(W.h_cback.p + o_wd, W.d_wide.p, wstride * t * 4, hipMemcpyDeviceToHost, st));
   if (!W.ev_chain) HIPCHK(hipEventCreateWithFlags(&W.ev_chain, hipEventDisableTiming));
   HIPCHK(hipEventRecord(W.ev_chain, st));
@@ -654,14 +668,16 @@ static int sm_chain(Ctx* c, SmWork& W, const std::vector<int>& S, HState& s, int
   c->mark("sm.chain_done");
   const PhiChain* cw = (const PhiChain*)(W.h_cback.p + o_cw);
   const uint32_t* hF = (const uint32_t*)W.h_cback.p;
-  // the first update that did not complete (t: none)
-  int kf = t;
-  for (int k = 0; k < t; ++k)
-    if (((const int*)(W.h_cout.p + out_b * k))[0] != kPhiOk || cw[2 + 2 * k].ok != 1) {
-      kf = k;
+  auto ustat = [&](int u) { return ((const int*)(W.h_cout.p + out_b * u))[0]; };
+  // the first update that did not complete (nu: none)
+  int uf = nu;
+  for (int u = 0; u < nu; ++u)
+    if (ustat(u) != kPhiOk || cw[upd_w(u)].ok != 1) {
+      uf = u;
       break;
     }
-  const bool scan_kf = kf < t && cw[1 + 2 * kf].ok == 1;   // scan kf ran (its update did not complete)
+  const int kf = uf >> 1;                                   // its scan
+  const bool scan_kf = uf < nu && cw[link_w(kf)].ok == 1;   // that scan ran
   const int ran = kf + (scan_kf ? 1 : 0);                   // scans run
   if (Gw)
     for (int k = 0; k < ran; ++k) {
@@ -683,51 +699,52 @@ static int sm_chain(Ctx* c, SmWork& W, const std::vector<int>& S, HState& s, int
     s.counts[c1] = F1.nn;
     s.counts[c2] = F2.nn;
   }
-  // the parameters of the last update that completed
-  const int64_t items = 2 * (int64_t)d;
-  for (int k = 0; k < kf; ++k) {
+  // the parameters of the updates that completed (each cluster's last)
+  for (int u = 0; u < uf; ++u) {
     int64_t cons = 0;
-    std::memcpy(&cons, W.h_cout.p + out_b * k + 8, 8);
-    Ctx::PhiDevice::adapt(phd.p_rej_sm, cons - 3 * items, items, 0.9);
+    std::memcpy(&cons, W.h_cout.p + out_b * u + 8, 8);
+    Ctx::PhiDevice::adapt(phd.p_rej_sm, cons - 3 * (int64_t)d, d, 0.9);
   }
-  if (kf > 0) {
-    const uint8_t* ho = W.h_cout.p + out_b * (kf - 1);
+  for (int e = 0; e < 2; ++e) {
+    int u = uf - 1;
+    while (u >= 0 && (u & 1) != e) --u;
+    if (u < 0) continue;
+    const uint8_t* ho = W.h_cout.p + out_b * u;
     const uint8_t* pk = ho + o_pick;
-    const double* sg = (const double*)(ho + o_sig);
-    for (int e2 = 0; e2 < 2; ++e2) {
-      const int k = e2 == 0 ? c1 : c2, src = e2 == 0 ? a1 : 1 - a1;
-      for (int j = 0; j < d; ++j) s.center[(size_t)k * d + j] = (uint8_t)(pk[(size_t)src * d + j] + 1);
-      std::memcpy(&s.sigma[(size_t)k * d], sg + (size_t)src * d, (size_t)d * 8);
-    }
-    c->stats.phi_device_calls += kf;
-    c->stats.phi_sm_device_calls += kf;
+    const int k = klab[e];
+    for (int j = 0; j < d; ++j) s.center[(size_t)k * d + j] = (uint8_t)(pk[j] + 1);
+    std::memcpy(&s.sigma[(size_t)k * d], ho + o_sig, (size_t)d * 8);
   }
+  c->stats.phi_device_calls += uf;
+  c->stats.phi_sm_device_calls += uf;
   c->stats.sm_chain_runs++;
   c->stats.sm_chain_scans += ran;
-  if (kf == t) {
+  if (uf == nu) {
     // the host stream after the last update's draws (its state came back with its outputs)
-    const uint8_t* ho = W.h_cout.p + out_b * (t - 1);
-    c->adopt_after_phi(*Wn, (uint64_t)cw[2 * t].end, (const uint32_t*)(ho + o_state));
+    const uint8_t* ho = W.h_cout.p + out_b * (nu - 1);
+    c->adopt_after_phi(*Wn, (uint64_t)cw[upd_w(nu - 1)].end, (const uint32_t*)(ho + o_state));
     *next_iter = t;
     return kOk;
   }
   // continue on the host from the first unfinished step
   c->stats.sm_chain_resumes++;
-  const int stk = ((const int*)(W.h_cout.p + out_b * kf))[0];
-  if (scan_kf && stk != kPhiOff) {
+  const int stk = ustat(uf);
+  if (scan_kf && stk != kPhiOff && stk != kPhiOk) {
     c->stats.phi_fallback_status_mask |= (int64_t)1 << std::min(std::max(stk, 0), 14);
     c->stats.phi_fast_handbacks++;
-    if (stk == kPhiNonDet) phd.fast_backoff = Ctx::PhiDevice::kFastBackoff;
     if (stk == kPhiShort || stk == kPhiWindow) Ctx::PhiDevice::widen(phd.p_rej_sm, 0.9);
   }
   if (std::getenv("HDPM_PHI_TRACE"))
-    std::fprintf(stderr, "[sm chain] t %d nS %d: step %d %s (update status %d)\n", t, nS, kf,
-                 scan_kf ? "update handed back" : "scan off", stk);
-  const uint64_t pos = scan_kf ? (uint64_t)cw[1 + 2 * kf].end + (uint64_t)nS : (uint64_t)cw[2 * kf].end;
+    std::fprintf(stderr, "[sm chain] t %d nS %d: scan %d %s (update status %d)\n", t, nS, kf,
+                 !scan_kf ? "off" : (uf & 1) ? "ran, second update handed back" : "ran, update handed back", stk);
+  uint64_t pos;
+  if (!scan_kf) pos = (uint64_t)cw[kf == 0 ? 0 : upd_w(2 * kf - 1)].end;
+  else if ((uf & 1) == 0) pos = (uint64_t)cw[link_w(kf)].end + (uint64_t)nS;
+  else pos = (uint64_t)cw[upd_w(uf - 1)].end;
   c->adopt_state_at(*Wn, pos);
   c->rng_sync();
   *next_iter = kf;
-  *at_phi = scan_kf;
+  *at_phi = !scan_kf ? 0 : (uf & 1) ? 2 : 1;
   return kOk;
 }
 
@@ -778,16 +795,23 @@ static int restricted_gibbs(Ctx* c, const std::vector<int>& S, HState& s, int i1
   const bool dev_draws = nS >= 4096 && !(c->debug & 65536);
   // the whole sampler as one device chain where it applies (sm_chain); the host continues
   // from the first step the chain did not finish
-  int iter0 = 0;
-  bool at_phi = false;
+  int iter0 = 0, at_phi = 0;
   if (dev_tables && sm_chain(c, W, S, s, i1, i2, t, F1, F2, FM, &iter0, &at_phi) == kOk) {
     c->mark("sm.chain");
     if (iter0 == t) return kOk;
   }
   for (int iter = iter0; iter < t; ++iter) {
     if (at_phi && iter == iter0) {
-      // the chain's scan ran, its update did not: update_phi({c1, c2}) here
-      const int st = hupdate_phi_pair(c, s, c1, F1, c2, F2);
+      // the chain's scan ran, its update_phi({c1, c2}) did not (1) or only the lower label's
+      // did (2): the rest here
+      int st;
+      if (at_phi == 2) {
+        const int kh = std::max(c1, c2);
+        const Freq& Fh = kh == c1 ? F1 : F2;
+        st = hupdate_phi_pair(c, s, kh, Fh, kh, Fh);
+      } else {
+        st = hupdate_phi_pair(c, s, c1, F1, c2, F2);
+      }
       c->mark("sm.phi");
       if (st) return st;
       continue;

@@ -253,8 +253,9 @@ class Engine:
         self._check(self._L.hdpm_set_option(self._h, _lib.OPT_SM_WIDE_WAIT_US, float(us)))
 
     def set_sm_chain(self, mode: int):
-        """include/hdpm.h HDPM_OPT_SM_CHAIN: the restricted Gibbs sampler as one device chain (1,
-        default) or scan by scan (0); testing: 2 + 2k / 3 + 2k stop the chain at scan / update k."""
+        """include/hdpm.h HDPM_OPT_SM_CHAIN: the restricted Gibbs sampler as one device chain (1)
+        or scan by scan (0, default); testing: 2 + 3k / 3 + 3k / 4 + 3k stop the chain at scan k / its
+        lower / larger label's update."""
         self._check(self._L.hdpm_set_option(self._h, _lib.OPT_SM_CHAIN, float(mode)))
 
     def set_hig_logspace(self, on: bool = True):

@@ -902,12 +902,12 @@ def test_split_merge_chain_wide_scan_and_give_up(hd, oracle, wait_us):
         assert stats["sm_wide_fallbacks"] == 0, stats
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2, 3, 6, 7])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4, 8, 9, 10])
 def test_split_merge_device_chain(hd, oracle, mode):
     """The restricted Gibbs samplers of split-merge moves as one device chain (sm_chain: the t
     scans and their update_phi({c1, c2}) enqueued together, sm:163-225), scan by scan (mode 0),
-    and chains stopped at scan 0 / update 0 / scan 2 / update 2 (modes 2, 3, 6, 7: the host
-    continues from there): the same chain as the oracle every time."""
+    and chains stopped at scan k / its first / its second one-cluster update for k = 0, 2 (modes
+    2-4, 8-10: the host continues from there): the same chain as the oracle every time."""
     ds = synth(6000, 64, 2, 3, seed=44)
     kw = dict(m=3, iterations=4, L=1, c_i=ds.truth, burnin=0, t=4, r=4, neal8=True, split_merge=True)
     try:

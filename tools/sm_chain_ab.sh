@@ -12,3 +12,13 @@ for r in 1 2; do
     HDPM_SM_CHAIN=$v timeout -k 10 200 python -u bench.py --config c3 --sm --no-cpu-baseline --steps 60 --warmup 5 > $O/c3sm_${v}_$r.jsonl 2> $O/c3sm_${v}_$r.err || exit 1
   done
 done
+# stream windows started at the end of the current one (default) or at the current position
+for r in 1 2 3; do
+  for v in new old; do
+    if [ $v = old ]; then export HDPM_WINDOW_FROM_NOW=1; else unset HDPM_WINDOW_FROM_NOW; fi
+    timeout -k 10 120 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/c5w_${v}_$r.jsonl 2> $O/c5w_${v}_$r.err || exit 1
+  done
+done
+unset HDPM_WINDOW_FROM_NOW
+timeout -k 10 120 python -u bench.py --no-cpu-baseline > $O/c5_300.jsonl 2> $O/c5_300.err || exit 1
+timeout -k 10 120 python -u bench.py --config c4 --no-cpu-baseline > $O/c4_300.jsonl 2> $O/c4_300.err || exit 1
