@@ -309,7 +309,8 @@ def main():
                          ">= 4096 (cluster, attribute) items; default = the engine's (auto unless HDPM_PHI says otherwise)")
     ap.add_argument("--record", action="store_true",
                     help="the R driver's sampling phase: every iteration saved (thinning 1, la:139-153) -- K, labels, "
-                         "centers and sigmas recorded through hdpm_iterations_record (batches of 16, buffers reused)")
+                         "centers and sigmas recorded through hdpm_iterations_record (the adapter's batches of 64, "
+                         "buffers reused)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads of the optimised CPU baseline (0: every CPU this process may use, within the "
@@ -372,12 +373,19 @@ def main():
         eng.set_debug(32 | (64 if os.environ.get("HDPM_BENCH_HOST_POOL") else 0))                        # host timeline of the timed iterations (stderr)
     D.barrier()
     cuda_sync()
-    rec_buf = np.zeros((16, ds.n), np.int32) if args.record else None
+    # the adapter's batches (integration/hdpm_chain.hpp: 64 iterations per hdpm_iterations_record
+    # call; a call boundary restarts the pipeline; HDPM_BENCH_RECORD_BATCH for A/B: 16 / 64 / 256
+    # at C5 7,790 / 7,766 / 5,254 against 7,674 unrecorded, C4 5,904 / 6,063 / 5,818 against
+    # 6,372, profiles/r06/record6c/)
+    rec_batch = min(int(os.environ.get("HDPM_BENCH_RECORD_BATCH", "64")), args.steps)
+    # (written through once here: the adapter's result buffers are reused, so their pages are
+    # resident; a fresh calloc'd buffer would fault a page at a time inside the timed window)
+    rec_buf = np.full((rec_batch, ds.n), -1, np.int32) if args.record else None
     t0 = time.perf_counter()
     if args.record:
         # every iteration saved (burnin 0, thinning 1): its K, labels, centers, sigmas, loglik
-        for k0 in range(0, args.steps, 16):
-            eng.iterations_record(it + k0, min(16, args.steps - k0), out=rec_buf)
+        for k0 in range(0, args.steps, rec_batch):
+            eng.iterations_record(it + k0, min(rec_batch, args.steps - k0), out=rec_buf)
     else:
         eng.iterations(it, args.steps)
     it += args.steps
