@@ -3846,19 +3846,38 @@ struct Ctx {
     pl.root_lds = phi_values2_lds_bytes(d, pl.tnb, T, pl.tW, pl.nw) <= 150 * 1024 ? 1 : 0;
     pl.tree_ok = pl.tW >= 64 && phi_tree_lds_bytes(pl.tSB, pl.nw, pl.tW) <= 150 * 1024 && pl.root_lds &&
                  pl.tW < 65535;
-    // fast path: the smallest group (most workgroups for the masks) whose cluster of group
-    // tables fits one workgroup's LDS
-    if (pl.tW >= 64 && pl.tW < 65535)
-      for (int gs = 8; gs <= 64; gs *= 2) {
+    // fast path: groups of gs items, k_phi2_group a workgroup per group.  The largest gs that
+    // still gives >= 160 workgroups (their prep and masks run beside each other: more, smaller
+    // groups contend for the CUs; fewer leave them idle), else the smallest that fits the LDS
+    // (measured, one box, profiles/r06/phi2gs/: C4 T = 10, D = 784 -- gs 8 / 16 / 32 / 64: 6,512 /
+    // 6,518 / 6,792 / 5,301 it/s; C5 with the device update, T = 20, D = 128 -- 8 / 16 / 32: 7,244 /
+    // 7,566 / 7,163; C3, D = 64 -- 11,308 / 11,164 / 10,044).  HDPM_PHI2_GS forces one (testing).
+    static const int gs_force = [] {
+      const char* e = std::getenv("HDPM_PHI2_GS");
+      const int v = e ? std::atoi(e) : 0;
+      return (v == 8 || v == 16 || v == 32 || v == 64) ? v : 0;
+    }();
+    if (pl.tW >= 64 && pl.tW < 65535) {
+      auto fits = [&](int gs) {
         const int G = (d + gs - 1) / gs;
-        if (phi2_tree_lds_bytes(T, G, pl.tW) <= 150 * 1024 && phi2_values_lds_bytes(d, G, pl.tW, T) <= 150 * 1024 &&
-            phi2_group_lds_bytes(gs, pl.nw, pl.rate) <= 150 * 1024) {
-          pl.fast_ok = true;
-          pl.gs = gs;
-          pl.G = G;
-          break;
-        }
+        return phi2_tree_lds_bytes(T, G, pl.tW) <= 150 * 1024 && phi2_values_lds_bytes(d, G, pl.tW, T) <= 150 * 1024 &&
+               phi2_group_lds_bytes(gs, pl.nw, pl.rate) <= 150 * 1024;
+      };
+      int pick = 0;
+      if (gs_force) {
+        if (fits(gs_force)) pick = gs_force;
+      } else {
+        for (int gs = 64; gs >= 8 && !pick; gs /= 2)
+          if (fits(gs) && (int64_t)T * ((d + gs - 1) / gs) >= 160) pick = gs;
+        for (int gs = 8; gs <= 64 && !pick; gs *= 2)
+          if (fits(gs)) pick = gs;
       }
+      if (pick) {
+        pl.fast_ok = true;
+        pl.gs = pick;
+        pl.G = (d + pick - 1) / pick;
+      }
+    }
     return pl;
   }
   // scratch of a plan, and the arguments every call shares (the caller sets raw, labels /
