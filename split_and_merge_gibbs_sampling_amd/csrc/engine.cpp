@@ -1043,6 +1043,7 @@ struct Ctx {
       for (auto& e : ev_res)
         if (e) (void)hipEventDestroy(e);
       if (sm.ev_chain) (void)hipEventDestroy(sm.ev_chain);
+      if (ev_labels) (void)hipEventDestroy(ev_labels);
       for (auto& pe : ev_pp)
         for (auto& e : pe)
           if (e) (void)hipEventDestroy(e);
@@ -1601,6 +1602,9 @@ struct Ctx {
   // sweep stream may hold a sweep enqueued ahead behind its wait kernel).
   void capture_labels() {
     if (host_c_valid) return;
+    // behind the last sweep end (slot ids -> labels, the move log complete); a sweep enqueued
+    // ahead sits behind it on `stream`, so the wait cannot reach that sweep's gate
+    if (ev_labels) HIPCHK(hipStreamWaitEvent(cstream, ev_labels, 0));
     if (mirror_moves > 0) {
       mlog_h.resize((size_t)3 * mirror_moves);
       HIPCHK(hipMemcpyAsync(mlog_h.data(), d_mlog.p, mlog_h.size() * 4, hipMemcpyDeviceToHost, cstream));
@@ -2465,7 +2469,12 @@ struct Ctx {
       HIPCHK(hipMemcpyAsync(h_freq_next.p, d_freq2.p, fwords * 4, hipMemcpyDeviceToHost, stream));
     }
     HIPCHK(launch_finish_sweep(d_counts.p, d_sol.p, d_los.p, d_src.p, scap, hctl, n, stream));
+    // (the labels' copies on cstream wait for this: the resolver's end tells the host the sweep
+    // is done, not that k_relabel has turned its slot ids into labels)
+    if (!ev_labels) HIPCHK(hipEventCreateWithFlags(&ev_labels, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(ev_labels, stream));
   }
+  hipEvent_t ev_labels = nullptr;      // the last sweep end (launch_sweep_end) on `stream`
 
   // The next sweep prepared at the end of an iteration (prepare_next_sweep): its draws
   // reserved (their stream slice and update_phi's are copied out) and update_phi speculated

@@ -2,7 +2,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out/final6
+O=gpurun_out/final6b
 mkdir -p $O
 timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests > $O/tests_gpu.log 2>&1 &&
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1
