@@ -3,7 +3,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out/final6
+O=gpurun_out/final6b
 mkdir -p $O
 timeout -k 10 300 python -u bench.py > $O/bench_c5.jsonl 2> $O/bench_c5.err &&
 timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_c5_driver.jsonl 2> $O/bench_c5_driver.err &&
