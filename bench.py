@@ -28,7 +28,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-PMC_ROUND = "r05"        # profiles/<round>/pmc_{fetch,write}_<config>.csv: this round's counter passes
+PMC_ROUND = "r06"        # profiles/<round>/pmc_{fetch,write}_<config>.csv: this round's counter passes
 
 
 def packed_layout(d: int, mmax: int):
